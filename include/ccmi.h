@@ -1,0 +1,278 @@
+/*
+ * ccmi.h — C ABI of the MI355X proposal engine (libccmi.so).
+ *
+ * Drop-in boundary for Cruise Control's goal-optimizer hot path. Every entry point replaces a
+ * reference interface (paths relative to cruise-control/src/main/java/com/linkedin/kafka/cruisecontrol/):
+ *
+ *   ccmi_session_create        <- the ClusterModel a caller hands to GoalOptimizer.optimizations
+ *                                 (model/ClusterModel.java:135-139 createRack/createBroker/createReplica/
+ *                                 setReplicaLoad, :395-446); the desc is the flattened model.
+ *   ccmi_optimizations         <- GoalOptimizer.optimizations(ClusterModel, List<Goal>, OperationProgress,
+ *                                 Map, OptimizationOptions)  analyzer/GoalOptimizer.java:435-524
+ *   ccmi_goal_optimize         <- Goal.optimize(ClusterModel, Set<Goal>, OptimizationOptions)
+ *                                 analyzer/goals/Goal.java:60-66, AbstractGoal.java:81-135
+ *   ccmi_action_acceptance     <- Goal.actionAcceptance(BalancingAction, ClusterModel)
+ *                                 analyzer/goals/Goal.java:68-80
+ *   ccmi_compute_cluster_stats <- ClusterModel.getClusterStats(BalancingConstraint, OptimizationOptions)
+ *                                 model/ClusterModel.java:137-139 -> ClusterModelStats.populate :84-102
+ *   ccmi_action_log_*          <- the ordered relocateReplica/relocateLeadership calls a goal makes
+ *                                 (model/ClusterModel.java:380-441); a Java shim replays them so the
+ *                                 caller's ClusterModel ends in the identical state.
+ *   ccmi_replica_distribution / ccmi_leader_distribution
+ *                              <- ClusterModel.getReplicaDistribution / getLeaderDistribution :167-198
+ *   ccmi_proposals             <- AnalyzerUtils.getDiff -> Set<ExecutionProposal>  analyzer/AnalyzerUtils.java:55-93
+ *   ccmi_random_cluster        <- test fixture RandomCluster.generate+populate
+ *                                 (src/test/java/.../model/RandomCluster.java:53-455)
+ *
+ * Plain C: pointers + sizes only. All arrays are caller-owned for inputs and copied in.
+ * Errors: every call returns ccmi_status; the last error text is available from ccmi_last_error().
+ * Threading: a session is single-threaded; the library is thread-safe across sessions.
+ */
+#ifndef CCMI_H_
+#define CCMI_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define CCMI_ABI_VERSION 1
+
+typedef enum ccmi_status {
+  CCMI_OK = 0,
+  CCMI_E_INVALID = 1,     /* IllegalArgumentException */
+  CCMI_E_DEVICE = 2,      /* HIP runtime / device failure, or no gfx950 device */
+  CCMI_E_OPT_FAILURE = 3, /* OptimizationFailureException */
+  CCMI_E_STATE = 4,       /* IllegalStateException (e.g. stats regression check, AbstractGoal.java:114-117) */
+  CCMI_E_UNSUPPORTED = 5  /* goal kind / option outside the implemented scope */
+} ccmi_status;
+
+/* common/Resource.java:17-25 ids */
+typedef enum ccmi_resource { CCMI_CPU = 0, CCMI_NW_IN = 1, CCMI_NW_OUT = 2, CCMI_DISK = 3, CCMI_NUM_RESOURCES = 4 } ccmi_resource;
+
+/* KafkaMetricDef COMMON metrics that carry a resource group (monitor/metricdefinition/KafkaMetricDef.java:43-53) */
+typedef enum ccmi_metric {
+  CCMI_M_CPU_USAGE = 0,
+  CCMI_M_DISK_USAGE = 1,
+  CCMI_M_LEADER_BYTES_IN = 2,
+  CCMI_M_LEADER_BYTES_OUT = 3,
+  CCMI_M_REPLICATION_BYTES_IN = 4,
+  CCMI_M_REPLICATION_BYTES_OUT = 5,
+  CCMI_NUM_METRICS = 6
+} ccmi_metric;
+
+/* model/Broker.java State */
+typedef enum ccmi_broker_state {
+  CCMI_BROKER_ALIVE = 0,
+  CCMI_BROKER_DEAD = 1,
+  CCMI_BROKER_NEW = 2,
+  CCMI_BROKER_DEMOTED = 3,
+  CCMI_BROKER_BAD_DISKS = 4
+} ccmi_broker_state;
+
+/* analyzer/ActionType.java */
+typedef enum ccmi_action_type {
+  CCMI_INTER_BROKER_REPLICA_MOVEMENT = 0,
+  CCMI_LEADERSHIP_MOVEMENT = 1,
+  CCMI_INTER_BROKER_REPLICA_SWAP = 2,
+  CCMI_INTRA_BROKER_REPLICA_MOVEMENT = 3,
+  CCMI_INTRA_BROKER_REPLICA_SWAP = 4
+} ccmi_action_type;
+
+/* analyzer/ActionAcceptance.java */
+typedef enum ccmi_acceptance { CCMI_ACCEPT = 0, CCMI_REPLICA_REJECT = 1, CCMI_BROKER_REJECT = 2 } ccmi_acceptance;
+
+/* Goal plugins by reference simple class name (Goal.name(), AbstractGoal.java:141-144); numbering follows
+ * the default.goals priority order (config/constants/AnalyzerConfig.java:352-367). */
+typedef enum ccmi_goal_kind {
+  CCMI_GOAL_RACK_AWARE = 0,                        /* RackAwareGoal */
+  CCMI_GOAL_MIN_TOPIC_LEADERS_PER_BROKER = 1,      /* MinTopicLeadersPerBrokerGoal */
+  CCMI_GOAL_REPLICA_CAPACITY = 2,                  /* ReplicaCapacityGoal */
+  CCMI_GOAL_DISK_CAPACITY = 3,                     /* DiskCapacityGoal */
+  CCMI_GOAL_NW_IN_CAPACITY = 4,                    /* NetworkInboundCapacityGoal */
+  CCMI_GOAL_NW_OUT_CAPACITY = 5,                   /* NetworkOutboundCapacityGoal */
+  CCMI_GOAL_CPU_CAPACITY = 6,                      /* CpuCapacityGoal */
+  CCMI_GOAL_REPLICA_DISTRIBUTION = 7,              /* ReplicaDistributionGoal */
+  CCMI_GOAL_POTENTIAL_NW_OUT = 8,                  /* PotentialNwOutGoal */
+  CCMI_GOAL_DISK_USAGE_DISTRIBUTION = 9,           /* DiskUsageDistributionGoal */
+  CCMI_GOAL_NW_IN_USAGE_DISTRIBUTION = 10,         /* NetworkInboundUsageDistributionGoal */
+  CCMI_GOAL_NW_OUT_USAGE_DISTRIBUTION = 11,        /* NetworkOutboundUsageDistributionGoal */
+  CCMI_GOAL_CPU_USAGE_DISTRIBUTION = 12,           /* CpuUsageDistributionGoal */
+  CCMI_GOAL_TOPIC_REPLICA_DISTRIBUTION = 13,       /* TopicReplicaDistributionGoal */
+  CCMI_GOAL_LEADER_REPLICA_DISTRIBUTION = 14,      /* LeaderReplicaDistributionGoal */
+  CCMI_GOAL_LEADER_BYTES_IN_DISTRIBUTION = 15,     /* LeaderBytesInDistributionGoal */
+  CCMI_GOAL_INTRA_BROKER_DISK_CAPACITY = 16,       /* IntraBrokerDiskCapacityGoal */
+  CCMI_GOAL_INTRA_BROKER_DISK_USAGE_DISTRIBUTION = 17 /* IntraBrokerDiskUsageDistributionGoal */
+} ccmi_goal_kind;
+
+/*
+ * Flattened ClusterModel. Semantics of construction (mirrors the reference's model building):
+ *   brokers are created in index order (broker_id[b] == b in ABI v1), then for r = 0..R-1 in index order
+ *   replica r is created on replica_broker[r] (ClusterModel.createReplica) and its load is set
+ *   (ClusterModel.setReplicaLoad) — so broker/host/cluster/potential-leadership aggregates accumulate in
+ *   replica index order exactly as the Java model does; finally each partition's replica list is put in
+ *   partition_offset CSR order and broker states other than ALIVE are applied in broker index order
+ *   (ClusterModel.setBrokerState).
+ */
+typedef struct ccmi_cluster_desc {
+  int32_t num_windows;               /* W, 1..5 (num.partition.metrics.windows) */
+  int32_t num_racks;
+  int32_t num_brokers;               /* B */
+  const int32_t* broker_id;          /* [B] */
+  const int32_t* broker_rack;        /* [B] rack index */
+  const int32_t* broker_state;       /* [B] ccmi_broker_state */
+  const double* broker_capacity;     /* [B*4] ccmi_resource order */
+  int32_t num_topics;                /* T */
+  const char* const* topic_names;    /* [T] ASCII topic names (Replica.compareTo tie-break) */
+  int32_t num_partitions;            /* P */
+  const int32_t* partition_topic;    /* [P] */
+  const int32_t* partition_number;   /* [P] */
+  const int32_t* partition_offset;   /* [P+1] CSR into a permutation of replicas (Partition._replicas order) */
+  const int32_t* partition_replicas; /* [R] replica indices, grouped by partition via partition_offset */
+  int32_t num_replicas;              /* R */
+  const int32_t* replica_partition;  /* [R] */
+  const int32_t* replica_broker;     /* [R] */
+  const uint8_t* replica_is_leader;  /* [R] */
+  const uint8_t* replica_offline;    /* [R] isOriginalOffline flag (replica on a broken disk) */
+  const float* replica_load;         /* [R * 6 * W] float window values, ccmi_metric order, newest first */
+} ccmi_cluster_desc;
+
+/* analyzer/BalancingConstraint.java; defaults AnalyzerConfig.java:58-464 via ccmi_default_constraint */
+typedef struct ccmi_balancing_constraint {
+  double resource_balance_percentage[4];
+  double capacity_threshold[4];
+  double low_utilization_threshold[4];
+  double replica_balance_percentage;
+  double leader_replica_balance_percentage;
+  double topic_replica_balance_percentage;
+  int32_t topic_replica_balance_min_gap;
+  int32_t topic_replica_balance_max_gap;
+  double goal_violation_distribution_threshold_multiplier;
+  int64_t max_replicas_per_broker;
+  int64_t overprovisioned_max_replicas_per_broker;
+  int32_t overprovisioned_min_brokers;
+} ccmi_balancing_constraint;
+
+/* analyzer/OptimizationOptions.java (7-field form) */
+typedef struct ccmi_opt_options {
+  const int32_t* excluded_topics;
+  int32_t num_excluded_topics;
+  const int32_t* excluded_brokers_for_leadership;
+  int32_t num_excluded_brokers_for_leadership;
+  const int32_t* excluded_brokers_for_replica_move;
+  int32_t num_excluded_brokers_for_replica_move;
+  int32_t triggered_by_goal_violation;
+  const int32_t* requested_destination_broker_ids;
+  int32_t num_requested_destination_broker_ids;
+  int32_t only_move_immigrant_replicas;
+  int32_t fast_mode; /* accepted for API parity; the engine never applies wall-clock cut-offs */
+} ccmi_opt_options;
+
+typedef struct ccmi_action {
+  int32_t type;                  /* ccmi_action_type */
+  int32_t partition;             /* partition index (desc order) */
+  int32_t source_broker;
+  int32_t destination_broker;
+  int32_t destination_partition; /* swaps only, else -1 */
+} ccmi_action;
+
+/* model/ClusterModelStats.java fields */
+typedef struct ccmi_cluster_stats {
+  double resource_avg[4], resource_max[4], resource_min[4], resource_std[4];
+  int32_t num_balanced_brokers_by_resource[4];
+  double potential_nw_out_avg, potential_nw_out_max, potential_nw_out_min, potential_nw_out_std;
+  int32_t num_brokers_under_potential_nw_out;
+  double replica_avg, replica_std;
+  int32_t replica_max, replica_min;
+  double leader_avg, leader_std;
+  int32_t leader_max, leader_min;
+  double topic_replica_avg, topic_replica_std;
+  int32_t topic_replica_max, topic_replica_min;
+  int32_t num_brokers, num_replicas_in_cluster, num_partitions_with_offline_replicas, num_topics;
+  int32_t num_unbalanced_disks;
+  double disk_utilization_std;
+} ccmi_cluster_stats;
+
+typedef struct ccmi_goal_result {
+  int32_t goal_kind;
+  int32_t succeeded;            /* Goal.optimize return value */
+  int32_t has_diff;             /* AnalyzerUtils.hasDiff after this goal */
+  double seconds;               /* wall time of the goal */
+  int64_t candidates;           /* reference-equivalent candidate evaluations (BASELINE.md unit) */
+  int64_t device_candidates;    /* candidates evaluated on the device, speculation included */
+  int64_t device_launches;      /* scan-kernel launches */
+  int64_t actions;              /* relocate* calls recorded in the action log */
+  ccmi_cluster_stats stats;     /* ClusterModelStats after the goal (GoalOptimizer.statsByGoalPriority) */
+} ccmi_goal_result;
+
+/* Test fixture generator: RandomCluster properties (common/ClusterProperty.java + populate() flags) */
+typedef struct ccmi_random_cluster_props {
+  int32_t num_racks, num_brokers, num_dead_brokers, num_brokers_with_bad_disk;
+  int32_t num_replicas, num_topics, min_replication, max_replication;
+  double mean_cpu, mean_disk, mean_nw_in, mean_nw_out;
+  int32_t distribution;          /* 0 UNIFORM, 1 LINEAR, 2 EXPONENTIAL */
+  int32_t rack_aware;
+  int32_t leader_in_first_position;
+} ccmi_random_cluster_props;
+
+typedef struct ccmi_session ccmi_session;
+typedef struct ccmi_cluster_buffers ccmi_cluster_buffers; /* owns the arrays behind a generated desc */
+
+const char* ccmi_last_error(void);
+int32_t ccmi_abi_version(void);
+void ccmi_default_constraint(ccmi_balancing_constraint* out);
+void ccmi_default_random_cluster_props(ccmi_random_cluster_props* out); /* TestConstants.BASE_PROPERTIES */
+
+ccmi_status ccmi_random_cluster(const ccmi_random_cluster_props* props, ccmi_cluster_buffers** out);
+const ccmi_cluster_desc* ccmi_cluster_buffers_desc(const ccmi_cluster_buffers* buf);
+void ccmi_cluster_buffers_free(ccmi_cluster_buffers* buf);
+
+/* device_ordinal: HIP device; num_devices > 1 shards the candidate space by destination broker across
+ * device_ordinal .. device_ordinal+num_devices-1 inside one process (multi-process sharding uses RCCL
+ * from the host harness instead). */
+ccmi_status ccmi_session_create(int32_t device_ordinal, const ccmi_cluster_desc* desc, ccmi_session** out);
+ccmi_status ccmi_session_destroy(ccmi_session* s);
+
+/* Run a whole goal chain (GoalOptimizer.optimizations). results: caller array of n_goals entries. */
+ccmi_status ccmi_optimizations(ccmi_session* s, const int32_t* goal_kinds, int32_t n_goals,
+                               const ccmi_balancing_constraint* constraint, const ccmi_opt_options* options,
+                               ccmi_goal_result* results);
+/* Optimize one goal; the session remembers it (with its frozen state) as an optimized goal for later calls. */
+ccmi_status ccmi_goal_optimize(ccmi_session* s, int32_t goal_kind, const ccmi_balancing_constraint* constraint,
+                               const ccmi_opt_options* options, ccmi_goal_result* result);
+/* Acceptance of an action by the i-th goal this session has optimized. */
+ccmi_status ccmi_action_acceptance(ccmi_session* s, int32_t optimized_goal_index, const ccmi_action* action,
+                                   int32_t* acceptance);
+ccmi_status ccmi_compute_cluster_stats(ccmi_session* s, const ccmi_balancing_constraint* constraint,
+                               const ccmi_opt_options* options, ccmi_cluster_stats* out);
+
+int64_t ccmi_action_log_count(const ccmi_session* s);
+ccmi_status ccmi_action_log_copy(const ccmi_session* s, int64_t first, int64_t count, ccmi_action* out);
+/* [R] current broker of each replica slot in partition CSR order / [P] leader broker per partition */
+ccmi_status ccmi_replica_distribution(const ccmi_session* s, int32_t* out);
+ccmi_status ccmi_leader_distribution(const ccmi_session* s, int32_t* out);
+/* ExecutionProposals: count, then per proposal: partition, size, old leader, RF; old and new broker lists
+ * (new list leader-first) packed into old_out/new_out with stride max_rf. */
+int64_t ccmi_proposal_count(const ccmi_session* s);
+ccmi_status ccmi_proposals(const ccmi_session* s, int32_t max_rf, int32_t* partition, int32_t* size,
+                           int32_t* old_leader, int32_t* old_out, int32_t* new_out);
+
+/* Measurement hooks used by bench.py: device time of the last optimization's scan kernels (HIP events
+ * on the engine stream) and their algorithmic bytes. */
+typedef struct ccmi_perf_counters {
+  int64_t scan_launches;
+  double scan_kernel_ms;       /* sum of HIP-event durations of the scan kernel */
+  int64_t scan_bytes;          /* algorithmic bytes (DESIGN.md per-candidate figure x candidates) */
+  int64_t stats_launches;
+  double stats_kernel_ms;
+  int64_t stats_bytes;
+  int64_t host_syncs;
+} ccmi_perf_counters;
+ccmi_status ccmi_perf(const ccmi_session* s, ccmi_perf_counters* out);
+void ccmi_perf_reset(ccmi_session* s);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* CCMI_H_ */

@@ -1,0 +1,163 @@
+// ORACLE — test infrastructure only (see jsem.h header).
+// Goal plugin restatement:
+//   Goal interface          analyzer/goals/Goal.java:39-164
+//   AbstractGoal            analyzer/goals/AbstractGoal.java:81-430
+//   GoalUtils               analyzer/goals/GoalUtils.java:122-602
+//   AnalyzerUtils.isProposalAcceptableForOptimizedGoals  analyzer/AnalyzerUtils.java:169-179
+//   ReplicaDistributionAbstractGoal / ReplicaDistributionGoal
+//                           analyzer/goals/ReplicaDistributionAbstractGoal.java, ReplicaDistributionGoal.java
+//   ResourceDistributionGoal (+ Cpu/Disk/NetworkInbound/NetworkOutbound UsageDistributionGoal)
+//                           analyzer/goals/ResourceDistributionGoal.java:55-1078
+// Wall-clock fast-mode timeouts are treated as infinite (parity mode).
+#pragma once
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "model.h"
+#include "stats.h"
+
+namespace oracle {
+
+struct OptimizationFailure : std::runtime_error {
+  using std::runtime_error::runtime_error;
+};
+
+class Goal;
+using GoalList = std::vector<Goal*>;
+
+class Goal {
+ public:
+  virtual ~Goal() = default;
+  virtual std::string name() const = 0;
+  virtual bool isHardGoal() const = 0;
+  virtual bool optimize(ClusterModel& cm, const GoalList& optimizedGoals, const OptimizationOptions& o) = 0;
+  virtual Acceptance actionAcceptance(const BalancingAction& a, ClusterModel& cm) = 0;
+  // ClusterModelStatsComparator.compare(after, before): < 0 means "before" is preferred.
+  virtual int compareStats(const ClusterModelStats& s1, const ClusterModelStats& s2) const = 0;
+};
+
+class AbstractGoal : public Goal {
+ public:
+  explicit AbstractGoal(const BalancingConstraint& bc) : bc_(bc) {}
+  bool optimize(ClusterModel& cm, const GoalList& optimizedGoals, const OptimizationOptions& o) override;
+
+ protected:
+  virtual void initGoalState(ClusterModel& cm, const OptimizationOptions& o) = 0;
+  virtual void updateGoalState(ClusterModel& cm, const OptimizationOptions& o) = 0;
+  virtual void rebalanceForBroker(int broker, ClusterModel& cm, const GoalList& g, const OptimizationOptions& o) = 0;
+  virtual bool selfSatisfied(ClusterModel& cm, const BalancingAction& a) = 0;
+  virtual std::vector<int> brokersToBalance(ClusterModel& cm);
+
+  int maybeApplyBalancingAction(ClusterModel& cm, int replica, const std::vector<int>& candidates, ActionType action,
+                                const GoalList& g, const OptimizationOptions& o);
+  // candidates: in-order snapshot of the candidate broker's tracked sorted set (live view at call time)
+  int maybeApplySwapAction(ClusterModel& cm, int srcReplica, const std::vector<int>& candidateReplicas,
+                           const GoalList& g, const OptimizationOptions& o);
+  std::string replicaSortName(bool reverse, bool leaderOnly) const {
+    return name() + (reverse ? "-REVERSE" : "") + (leaderOnly ? "-LEADER" : "");
+  }
+
+  BalancingConstraint bc_;
+  bool finished_ = false;
+  bool succeeded_ = true;
+};
+
+// GoalUtils helpers
+std::vector<int> eligibleBrokers(ClusterModel& cm, int replica, const std::vector<int>& candidates, ActionType a,
+                                 const OptimizationOptions& o);
+bool legitMove(ClusterModel& cm, int replica, int destBroker, ActionType a);
+Acceptance isProposalAcceptableForOptimizedGoals(const GoalList& g, const BalancingAction& a, ClusterModel& cm);
+void ensureNoOfflineReplicas(ClusterModel& cm, const std::string& goal);
+std::vector<int> javaHashSetOrderIntKeys(const std::vector<int>& insertionOrder);
+
+class ReplicaDistributionGoal : public AbstractGoal {
+ public:
+  using AbstractGoal::AbstractGoal;
+  std::string name() const override { return "ReplicaDistributionGoal"; }
+  bool isHardGoal() const override { return false; }
+  Acceptance actionAcceptance(const BalancingAction& a, ClusterModel& cm) override;
+  int compareStats(const ClusterModelStats& s1, const ClusterModelStats& s2) const override;
+
+  int balanceUpperLimit() const { return upper_; }
+  int balanceLowerLimit() const { return lower_; }
+
+ protected:
+  void initGoalState(ClusterModel& cm, const OptimizationOptions& o) override;
+  void updateGoalState(ClusterModel& cm, const OptimizationOptions& o) override;
+  void rebalanceForBroker(int broker, ClusterModel& cm, const GoalList& g, const OptimizationOptions& o) override;
+  bool selfSatisfied(ClusterModel& cm, const BalancingAction& a) override;
+
+ private:
+  bool rebalanceByMovingReplicasOut(int broker, ClusterModel& cm, const GoalList& g, const OptimizationOptions& o);
+  bool rebalanceByMovingReplicasIn(int broker, ClusterModel& cm, const GoalList& g, const OptimizationOptions& o);
+  bool isExcludedForReplicaMove(const ClusterModel& cm, int b) const { return !allowed_[b]; }
+  bool underUpperAfter(const ClusterModel& cm, int b, int count, bool add) const;
+  bool aboveLowerAfter(const ClusterModel& cm, int b, int count, bool add) const;
+
+  bool fixOfflineReplicasOnly_ = false;
+  std::set<int> aboveUpper_, underLower_;
+  double avgReplicasOnAliveBroker_ = 0;
+  int upper_ = 0, lower_ = 0;
+  std::vector<char> allowed_;
+  int numAllowed_ = 0;
+};
+
+class ResourceDistributionGoal : public AbstractGoal {
+ public:
+  ResourceDistributionGoal(const BalancingConstraint& bc, int resource) : AbstractGoal(bc), resource_(resource) {}
+  std::string name() const override;
+  bool isHardGoal() const override { return false; }
+  Acceptance actionAcceptance(const BalancingAction& a, ClusterModel& cm) override;
+  int compareStats(const ClusterModelStats& s1, const ClusterModelStats& s2) const override;
+  double balanceUpperThreshold() const { return upperThr_; }
+  double balanceLowerThreshold() const { return lowerThr_; }
+
+ protected:
+  void initGoalState(ClusterModel& cm, const OptimizationOptions& o) override;
+  void updateGoalState(ClusterModel& cm, const OptimizationOptions& o) override;
+  void rebalanceForBroker(int broker, ClusterModel& cm, const GoalList& g, const OptimizationOptions& o) override;
+  bool selfSatisfied(ClusterModel& cm, const BalancingAction& a) override;
+  std::vector<int> brokersToBalance(ClusterModel& cm) override;
+
+ private:
+  Acceptance baseAcceptance(const BalancingAction& a, ClusterModel& cm);
+  bool rebalanceByMovingLoadOut(int broker, ClusterModel& cm, const GoalList& g, ActionType at,
+                                const OptimizationOptions& o);
+  bool rebalanceByMovingLoadIn(int broker, ClusterModel& cm, const GoalList& g, ActionType at,
+                               const OptimizationOptions& o, bool moveImmigrantsOnly);
+  bool rebalanceBySwappingLoadOut(int broker, ClusterModel& cm, const GoalList& g, const OptimizationOptions& o,
+                                  bool moveImmigrantsOnly);
+  bool rebalanceBySwappingLoadIn(int broker, ClusterModel& cm, const GoalList& g, const OptimizationOptions& o,
+                                 bool moveImmigrantsOnly);
+  std::string sortedCandidateReplicas(int broker, ClusterModel& cm, const OptimizationOptions& o, double loadLimit,
+                                      bool isAscending, bool followersOnly, bool leadersOnly, bool immigrantsOnly);
+  double getMaxReplicaLoad(ClusterModel& cm, const std::vector<int>& sorted) const;
+  double getMinReplicaLoad(ClusterModel& cm, const std::vector<int>& sorted) const;
+
+  bool isExcludedForReplicaMove(int b) const { return !allowed_[b]; }
+  bool aboveLowerLimit(ClusterModel& cm, int b) { return aboveLowerAfterChange(cm, -1, b, true); }
+  bool underUpperLimit(ClusterModel& cm, int b) { return underUpperAfterChange(cm, -1, b, false, upperThr_); }
+  bool aboveLowerAfterChange(ClusterModel& cm, int replicaLoadOf, int b, bool add);
+  bool underUpperAfterChange(ClusterModel& cm, int replicaLoadOf, int b, bool add, double thr);
+  bool underUpperAfterChange(ClusterModel& cm, int replicaLoadOf, int b, bool add) {
+    return underUpperAfterChange(cm, replicaLoadOf, b, add, upperThr_);
+  }
+  bool isAcceptableAfterReplicaMove(ClusterModel& cm, int srcReplica, int destBroker);
+  bool isSelfSatisfiedAfterSwap(ClusterModel& cm, int srcReplica, int destReplica);
+  bool isGettingMoreBalanced(ClusterModel& cm, int srcBroker, double delta, int destBroker);
+  bool isSwapViolatingLimit(ClusterModel& cm, int srcReplica, int destReplica);
+  bool isSwapViolatingContainerLimit(ClusterModel& cm, double delta, int srcReplica, int destReplica);
+  int cmpBroker(ClusterModel& cm, int a, int b) const {
+    int c = dcompare(cm.utilizationPct(a, resource_), cm.utilizationPct(b, resource_));
+    return c != 0 ? c : icompare(cm.brokers[a].id, cm.brokers[b].id);
+  }
+
+  int resource_;
+  bool fixOfflineReplicasOnly_ = false;
+  double upperThr_ = 0, lowerThr_ = 0;
+  std::vector<char> allowed_;
+  bool isLowUtilization_ = false;
+};
+
+}  // namespace oracle

@@ -1,0 +1,492 @@
+// ORACLE — test infrastructure only (see jsem.h header). Restates the reference model mutations:
+//   ClusterModel.createBroker/createReplica/setReplicaLoad  ClusterModel.java (createReplica :395-446)
+//   ClusterModel.relocateReplica/removeReplica              ClusterModel.java:380-396,546-564
+//   ClusterModel.relocateLeadership                         ClusterModel.java:409-441
+//   Broker.addReplica/removeReplica/makeFollower/makeLeader Broker.java:336-510
+//   Replica.makeFollower/computeCpuLoadAsFollower/makeLeader Replica.java:210-310
+//   ModelUtils.getFollowerCpuUtilFromLeaderLoad             ModelUtils.java:64-80 (weights 0.7/0.15/0.15)
+#include "model.h"
+
+#include <algorithm>
+#include <stdexcept>
+
+namespace oracle {
+
+const char* resourceName(int r) {
+  static const char* n[] = {"CPU", "NW_IN", "NW_OUT", "DISK"};
+  return n[r];
+}
+
+// ------------------------------------------------------------------ sorted replicas
+SortedReplicas::SortedReplicas(const ClusterModel* cm, SortSpec s, int broker)
+    : spec(std::move(s)), set(ReplicaCmp{cm, nullptr}), owner(broker) {
+  // rebind comparator to our own (stable) spec storage
+  set = std::set<int, ReplicaCmp>(ReplicaCmp{cm, &spec});
+}
+
+int ReplicaCmp::compare(int a, int b) const {
+  for (PrioFn p : spec->priority) {
+    int p1, p2;
+    if (p == PrioFn::IMMIGRANTS) {
+      p1 = cm->isImmigrant(a) ? 0 : 1;
+      p2 = cm->isImmigrant(b) ? 0 : 1;
+    } else {
+      p1 = cm->isCurrentOffline(a) ? 0 : 1;
+      p2 = cm->isCurrentOffline(b) ? 0 : 1;
+    }
+    if (p1 != p2) return p1 < p2 ? -1 : 1;
+  }
+  if (spec->score != ScoreFn::NONE) {
+    double s1 = (double)groupAvg(cm->replicas[a].load, spec->scoreResource, cm->W);
+    double s2 = (double)groupAvg(cm->replicas[b].load, spec->scoreResource, cm->W);
+    if (spec->score == ScoreFn::REVERSE_BY_GROUP) {
+      s1 = -s1;
+      s2 = -s2;
+    }
+    int c = dcompare(s1, s2);
+    if (c != 0) return c;
+  }
+  // Replica.compareTo (Replica.java:350-376)
+  bool o1 = cm->isCurrentOffline(a), o2 = cm->isCurrentOffline(b);
+  if (o1 && !o2) return -1;
+  if (!o1 && o2) return 1;
+  const Replica& ra = cm->replicas[a];
+  const Replica& rb = cm->replicas[b];
+  const Partition& pa = cm->partitions[ra.partition];
+  const Partition& pb = cm->partitions[rb.partition];
+  if (pa.number != pb.number) return pa.number > pb.number ? 1 : -1;
+  int ida = cm->brokers[ra.origBroker].id, idb = cm->brokers[rb.origBroker].id;
+  if (ida != idb) return ida > idb ? 1 : -1;
+  int ta = cm->topicRank[pa.topic], tb = cm->topicRank[pb.topic];
+  return ta == tb ? 0 : (ta < tb ? -1 : 1);
+}
+bool ReplicaCmp::operator()(int a, int b) const { return compare(a, b) < 0; }
+
+bool ClusterModel::passesSelection(const SortSpec& spec, int r) const {
+  const Replica& rep = replicas[r];
+  for (const Selection& s : spec.selection) {
+    bool ok = true;
+    switch (s.fn) {
+      case SelFn::LEADERS: ok = rep.isLeader; break;
+      case SelFn::FOLLOWERS: ok = !rep.isLeader; break;
+      case SelFn::ONLINE: ok = !isCurrentOffline(r); break;
+      case SelFn::OFFLINE: ok = isCurrentOffline(r); break;
+      case SelFn::IMMIGRANTS: ok = isImmigrant(r); break;
+      case SelFn::IMMIGRANT_OR_OFFLINE: ok = isImmigrant(r) || isCurrentOffline(r); break;
+      case SelFn::EXCLUDED_TOPICS: ok = true; break;  // resolved by caller-provided excluded set (empty in scope)
+      case SelFn::ABOVE_LIMIT: ok = replicaUtil(r, s.resource) > s.limit; break;
+      case SelFn::BELOW_LIMIT: ok = replicaUtil(r, s.resource) < s.limit; break;
+    }
+    if (!ok) return false;
+  }
+  return true;
+}
+
+void ClusterModel::trackSortedReplicas(int b, const std::string& name, const SortSpec& spec) {
+  auto& m = brokers[b].sorted;
+  if (m.find(name) == m.end()) m.emplace(name, std::make_unique<SortedReplicas>(this, spec, b));  // putIfAbsent
+}
+void ClusterModel::untrackSortedReplicas(const std::string& name) {
+  for (auto& br : brokers) br.sorted.erase(name);
+}
+void ClusterModel::brokerUntrackSortedReplicas(int b, const std::string& name) { brokers[b].sorted.erase(name); }
+void ClusterModel::clearSortedReplicas() {
+  for (auto& br : brokers) br.sorted.clear();
+}
+void ClusterModel::brokerClearSortedReplicas(int b) { brokers[b].sorted.clear(); }
+
+SortedReplicas& ClusterModel::trackedSortedReplicas(int b, const std::string& name) {
+  auto it = brokers[b].sorted.find(name);
+  if (it == brokers[b].sorted.end()) throw std::runtime_error("The sort name " + name + " is not found.");
+  SortedReplicas& sr = *it->second;
+  if (!sr.initialized) {  // SortedReplicas.ensureInitialize
+    sr.initialized = true;
+    for (int r : brokers[b].replicas)
+      if (passesSelection(sr.spec, r)) sr.set.insert(r);
+  }
+  return sr;
+}
+const std::set<int, ReplicaCmp>& ClusterModel::sortedReplicasView(int b, const std::string& name) {
+  return trackedSortedReplicas(b, name).set;
+}
+std::vector<int> ClusterModel::sortedReplicasClone(int b, const std::string& name) {
+  const auto& s = trackedSortedReplicas(b, name).set;
+  return std::vector<int>(s.begin(), s.end());
+}
+void ClusterModel::sortedAdd(int b, int r) {
+  for (auto& kv : brokers[b].sorted) {
+    SortedReplicas& sr = *kv.second;
+    if (sr.initialized && passesSelection(sr.spec, r)) sr.set.insert(r);
+  }
+}
+void ClusterModel::sortedRemove(int b, int r) {
+  for (auto& kv : brokers[b].sorted) {
+    SortedReplicas& sr = *kv.second;
+    if (sr.initialized) sr.set.erase(r);
+  }
+}
+
+// ------------------------------------------------------------------ construction
+int ClusterModel::createRack(const std::string& id) {
+  for (size_t i = 0; i < racks.size(); ++i)
+    if (racks[i].id == id) return (int)i;
+  racks.push_back({id, {}});
+  return (int)racks.size() - 1;
+}
+int ClusterModel::createBroker(int rackIdx, int brokerId, const double cap[NUM_RESOURCES]) {
+  if (brokerId != (int)brokers.size()) throw std::runtime_error("oracle requires dense broker ids 0..B-1");
+  Broker b;
+  b.id = brokerId;
+  b.rack = rackIdx;
+  for (int r = 0; r < NUM_RESOURCES; ++r) b.capacity[r] = cap[r];
+  brokers.push_back(std::move(b));
+  potentialLeadershipLoad.emplace_back();
+  racks[rackIdx].brokers.push_back(brokerId);
+  refreshCapacity();
+  return brokerId;
+}
+int ClusterModel::ensureTopic(const std::string& name) {
+  for (int i = (int)topicNames.size() - 1; i >= 0; --i)
+    if (topicNames[i] == name) return i;
+  topicNames.push_back(name);
+  numReplicasByTopic.push_back(0);
+  replicationFactorByTopic.push_back(0);
+  return (int)topicNames.size() - 1;
+}
+void ClusterModel::finalizeTopics() {
+  std::vector<int> idx(topicNames.size());
+  for (size_t i = 0; i < idx.size(); ++i) idx[i] = (int)i;
+  std::sort(idx.begin(), idx.end(), [&](int a, int b) { return topicNames[a] < topicNames[b]; });
+  topicRank.assign(topicNames.size(), 0);
+  for (size_t i = 0; i < idx.size(); ++i) topicRank[idx[i]] = (int)i;
+}
+
+int ClusterModel::createPartition(int topic, int number) {
+  Partition part;
+  part.topic = topic;
+  part.number = number;
+  partitions.push_back(std::move(part));
+  if (replicationFactorByTopic[topic] == 0) replicationFactorByTopic[topic] = 1;  // putIfAbsent(topic, 1)
+  return (int)partitions.size() - 1;
+}
+
+int ClusterModel::createReplica(int brokerIdx, int p, int index, bool isLeader, bool isOffline) {
+  int topic = partitions[p].topic;
+  Replica rep;
+  rep.broker = brokerIdx;
+  rep.origBroker = brokerIdx;
+  rep.isLeader = isLeader;
+  rep.origOfflineFlag = isOffline;
+  int r = (int)replicas.size();
+  rep.partition = p;
+  replicas.push_back(std::move(rep));
+  brokerAddReplica(brokerIdx, r);  // rack.addReplica -> host.addReplica -> broker.addReplica
+  numReplicasByTopic[topic] += 1;
+  Partition& part = partitions[p];
+  if (isLeader) {
+    if (part.leader >= 0) throw std::runtime_error("Partition already has a leader");
+    part.leader = r;
+    part.replicas.insert(part.replicas.begin() + index, r);
+    return r;
+  }
+  part.replicas.insert(part.replicas.begin() + index, r);
+  if (part.leader >= 0) loadAddLoad(potentialLeadershipLoad[brokerIdx], replicas[part.leader].load, W);
+  int followers = 0;
+  for (int x : part.replicas)
+    if (!replicas[x].isLeader) followers++;
+  int rf = std::max(replicationFactorByTopic[topic], followers + 1);
+  replicationFactorByTopic[topic] = rf;
+  maxReplicationFactor = std::max(maxReplicationFactor, rf);
+  return r;
+}
+
+void ClusterModel::setReplicaLoad(int r, const Load& amv) {
+  Replica& rep = replicas[r];
+  if (!rep.load.empty()) throw std::runtime_error("load already set");
+  int b = rep.broker;
+  // Broker.setReplicaLoad
+  amvAdd(rep.load, amv, W);  // Load.initializeMetricValues
+  if (rep.isLeader) amvAdd(brokers[b].leadershipLoadForNwResources, amv, W);
+  amvAdd(brokers[b].load, amv, W);
+  // (host and rack loads receive identical operations; host == broker here, rack load unused)
+  amvAdd(load, amv, W);  // cluster
+  const Partition& part = partitions[rep.partition];
+  if (part.leader >= 0 && replicas[part.leader].broker == b) {
+    for (int x : part.replicas) amvAdd(potentialLeadershipLoad[replicas[x].broker], amv, W);
+  }
+}
+
+void ClusterModel::refreshCapacity() {
+  for (int r = 0; r < NUM_RESOURCES; ++r) {
+    double c = 0;
+    for (const Broker& b : brokers)
+      if (b.isAlive()) c += b.capacity[r];
+    clusterCapacity[r] = c;
+  }
+}
+
+void ClusterModel::setBrokerState(int b, BrokerState s) {
+  Broker& br = brokers[b];
+  br.state = s;
+  if (!br.isAlive()) {  // Broker.setState
+    for (int r : br.replicas) {
+      if (!replicas[r].inBrokerOffline) {
+        replicas[r].inBrokerOffline = true;
+        br.numOffline++;
+      }
+    }
+    for (int k = 0; k < NUM_RESOURCES; ++k) br.capacity[k] = -1.0;
+  }
+  for (int r : br.replicas)
+    if (replicas[r].inBrokerOffline) selfHealingEligibleReplicas.insert(r);
+  refreshCapacity();
+  switch (s) {
+    case BrokerState::DEAD:
+      deadBrokers.insert(b);
+      brokersWithBadDisks.erase(b);
+      break;
+    case BrokerState::NEW:
+      newBrokers.insert(b);
+      deadBrokers.erase(b);
+      brokersWithBadDisks.erase(b);
+      break;
+    case BrokerState::DEMOTED:
+    case BrokerState::ALIVE:
+      deadBrokers.erase(b);
+      brokersWithBadDisks.erase(b);
+      break;
+    case BrokerState::BAD_DISKS:
+      deadBrokers.erase(b);
+      brokersWithBadDisks.insert(b);
+      for (int r : br.replicas)
+        if (replicas[r].inBrokerOffline) partitions[replicas[r].partition].ineligibleBrokers.insert(b);
+      break;
+  }
+}
+
+// ------------------------------------------------------------------ queries
+int ClusterModel::replicaOnBroker(int partition, int b) const {
+  for (int r : partitions[partition].replicas)
+    if (replicas[r].broker == b) return r;
+  return -1;
+}
+std::vector<int> ClusterModel::aliveBrokers() const {
+  std::vector<int> out;
+  out.reserve(brokers.size());
+  for (size_t i = 0; i < brokers.size(); ++i)
+    if (brokers[i].isAlive()) out.push_back((int)i);
+  return out;
+}
+std::vector<int> ClusterModel::aliveBrokersUnderThreshold(int res, double thr) const {
+  std::vector<int> out;
+  for (size_t i = 0; i < brokers.size(); ++i) {
+    const Broker& b = brokers[i];
+    if (!b.isAlive()) continue;
+    if (isBrokerResource(res)) {
+      double lim = b.capacity[res] * thr;
+      if (brokerUtil((int)i, res) >= lim) continue;
+    }
+    if (isHostResource(res)) {
+      double lim = hostCapacity((int)i, res) * thr;
+      if (hostUtil((int)i, res) >= lim) continue;
+    }
+    out.push_back((int)i);
+  }
+  return out;
+}
+std::vector<int> ClusterModel::aliveBrokersOverThreshold(int res, double thr) const {
+  std::vector<int> out;
+  for (size_t i = 0; i < brokers.size(); ++i) {
+    const Broker& b = brokers[i];
+    if (!b.isAlive()) continue;
+    if (isBrokerResource(res)) {
+      double lim = b.capacity[res] * thr;
+      if (brokerUtil((int)i, res) <= lim) continue;
+    }
+    if (isHostResource(res)) {
+      double lim = hostCapacity((int)i, res) * thr;
+      if (hostUtil((int)i, res) <= lim) continue;
+    }
+    out.push_back((int)i);
+  }
+  return out;
+}
+double ClusterModel::capacityWithAllowedReplicaMovesFor(int res, const OptimizationOptions& o) const {
+  double drop = 0.0;  // DoubleStream.sum over alive excluded brokers
+  JDoubleSum s;
+  for (size_t i = 0; i < brokers.size(); ++i)
+    if (brokers[i].isAlive() && o.excludedBrokersForReplicaMove.count(brokers[i].id)) s.add(brokers[i].capacity[res]);
+  drop = s.result();
+  return clusterCapacity[res] - drop;
+}
+std::vector<int> ClusterModel::onlineFollowerBrokers(int p) const {
+  std::vector<int> out;
+  for (int r : partitions[p].replicas)
+    if (!replicas[r].isLeader && !isCurrentOffline(r)) out.push_back(replicas[r].broker);
+  return out;
+}
+
+std::vector<int> ClusterModel::replicaDistributionFlat() const {
+  std::vector<int> out;
+  for (const Partition& p : partitions)
+    for (int r : p.replicas) out.push_back(replicas[r].broker);
+  return out;
+}
+std::vector<int> ClusterModel::leaderDistribution() const {
+  std::vector<int> out;
+  out.reserve(partitions.size());
+  for (const Partition& p : partitions) out.push_back(replicas[p.leader].broker);
+  return out;
+}
+
+// ------------------------------------------------------------------ broker mutations
+void ClusterModel::brokerAddReplica(int b, int r) {
+  Broker& br = brokers[b];
+  Replica& rep = replicas[r];
+  rep.posInBroker = (int)br.replicas.size();
+  br.replicas.push_back(r);
+  rep.inBrokerImmigrants = rep.inBrokerOffline = rep.inBrokerLeaders = false;
+  if (brokers[rep.origBroker].id != br.id) {
+    rep.inBrokerImmigrants = true;
+    br.numImmigrants++;
+  } else if (isOriginalOffline(r)) {
+    rep.inBrokerOffline = true;
+    br.numOffline++;
+  }
+  br.topicReplicaCount[partitions[rep.partition].topic] += 1;
+  if (rep.isLeader) {
+    loadAddLoad(br.leadershipLoadForNwResources, rep.load, W);
+    rep.inBrokerLeaders = true;
+    br.numLeaders++;
+  }
+  loadAddLoad(br.load, rep.load, W);
+  sortedAdd(b, r);
+}
+
+int ClusterModel::brokerRemoveReplica(int b, int partition) {
+  int r = replicaOnBroker(partition, b);
+  if (r < 0) return -1;
+  Broker& br = brokers[b];
+  Replica& rep = replicas[r];
+  // _replicas.remove (swap-remove keeps O(1); HashSet order is not semantically used)
+  int pos = rep.posInBroker;
+  int last = br.replicas.back();
+  br.replicas[pos] = last;
+  replicas[last].posInBroker = pos;
+  br.replicas.pop_back();
+  rep.posInBroker = -1;
+  loadSubLoad(br.load, rep.load, W);
+  br.topicReplicaCount[partitions[partition].topic] -= 1;
+  if (rep.isLeader) {
+    loadSubLoad(br.leadershipLoadForNwResources, rep.load, W);
+    if (rep.inBrokerLeaders) br.numLeaders--;
+  }
+  rep.inBrokerLeaders = false;
+  if (rep.inBrokerImmigrants) br.numImmigrants--;
+  if (rep.inBrokerOffline) br.numOffline--;
+  rep.inBrokerImmigrants = rep.inBrokerOffline = false;
+  sortedRemove(b, r);
+  return r;
+}
+
+Load ClusterModel::replicaMakeFollower(int r) {
+  Replica& rep = replicas[r];
+  if (!rep.isLeader) throw std::runtime_error("makeFollower on non-leader");
+  Load& L = rep.load;
+  Load delta;
+  // computeCpuLoadAsFollower
+  MV chg;
+  mvZero(chg, W);
+  MV totOut, totIn;
+  mvZero(totOut, W);
+  mvAdd(totOut, L.m[M_LBO], W);
+  mvAdd(totOut, L.m[M_RBO], W);
+  mvZero(totIn, W);
+  mvAdd(totIn, L.m[M_LBI], W);
+  mvAdd(totIn, L.m[M_RBI], W);
+  MV& cpu = L.m[M_CPU];
+  for (int i = 0; i < W; ++i) {
+    double in = (double)totIn.v[i], out = (double)totOut.v[i], c = (double)cpu.v[i];
+    double newCpu;
+    if (in == 0.0 && out == 0.0) newCpu = 0.0;
+    else newCpu = c * (0.15 * in) / (0.7 * in + 0.15 * out);
+    mvSet(chg, i, (double)cpu.v[i] - newCpu);
+    mvSet(cpu, i, newCpu);
+  }
+  // leadershipLoadDelta.add(cpuMetricId, cpuLoadChange); leadershipLoadDelta.add(nwOutLoad)
+  delta.mask = (uint8_t)((1u << M_CPU) | (1u << M_LBO) | (1u << M_RBO));
+  mvZero(delta.m[M_CPU], W);
+  mvAdd(delta.m[M_CPU], chg, W);
+  mvZero(delta.m[M_LBO], W);
+  mvAdd(delta.m[M_LBO], L.m[M_LBO], W);
+  mvZero(delta.m[M_RBO], W);
+  mvAdd(delta.m[M_RBO], L.m[M_RBO], W);
+  // clearLoadFor(NW_OUT)
+  mvZero(L.m[M_LBO], W);
+  mvZero(L.m[M_RBO], W);
+  rep.isLeader = false;
+  return delta;
+}
+
+Load ClusterModel::brokerMakeFollower(int b, int partition) {
+  int r = replicaOnBroker(partition, b);
+  Broker& br = brokers[b];
+  loadSubLoad(br.leadershipLoadForNwResources, replicas[r].load, W);
+  sortedRemove(b, r);
+  Load delta = replicaMakeFollower(r);
+  loadSubDelta(br.load, delta, W);
+  if (replicas[r].inBrokerLeaders) {
+    replicas[r].inBrokerLeaders = false;
+    br.numLeaders--;
+  }
+  sortedAdd(b, r);
+  return delta;
+}
+
+void ClusterModel::brokerMakeLeader(int b, int partition, const Load& delta) {
+  int r = replicaOnBroker(partition, b);
+  Broker& br = brokers[b];
+  sortedRemove(b, r);
+  replicas[r].isLeader = true;
+  loadAddDelta(replicas[r].load, delta, W);
+  loadAddLoad(br.leadershipLoadForNwResources, replicas[r].load, W);
+  loadAddDelta(br.load, delta, W);
+  if (!replicas[r].inBrokerLeaders) {
+    replicas[r].inBrokerLeaders = true;
+    br.numLeaders++;
+  }
+  sortedAdd(b, r);
+}
+
+// ------------------------------------------------------------------ cluster mutations
+void ClusterModel::relocateReplica(int p, int src, int dst) {
+  int r = brokerRemoveReplica(src, p);
+  if (r < 0) throw std::runtime_error("Replica is not in the cluster.");
+  int topic = partitions[p].topic;
+  numReplicasByTopic[topic] -= 1;
+  loadSubLoad(load, replicas[r].load, W);
+  loadSubLoad(potentialLeadershipLoad[src], replicas[partitions[p].leader].load, W);
+  replicas[r].broker = dst;
+  brokerAddReplica(dst, r);
+  numReplicasByTopic[topic] += 1;
+  loadAddLoad(load, replicas[r].load, W);
+  loadAddLoad(potentialLeadershipLoad[dst], replicas[partitions[p].leader].load, W);
+  if (recordActions) actionLog.push_back({(int)ActionType::INTER_BROKER_REPLICA_MOVEMENT, p, src, dst, -1});
+}
+
+bool ClusterModel::relocateLeadership(int p, int src, int dst) {
+  int sr = replicaOnBroker(p, src);
+  if (!replicas[sr].isLeader) return false;
+  int dr = replicaOnBroker(p, dst);
+  if (replicas[dr].isLeader) throw std::runtime_error("destination replica is a leader");
+  Load delta = brokerMakeFollower(src, p);
+  brokerMakeLeader(dst, p, delta);
+  Partition& part = partitions[p];
+  int pos = (int)(std::find(part.replicas.begin(), part.replicas.end(), dr) - part.replicas.begin());
+  std::swap(part.replicas[0], part.replicas[pos]);
+  part.leader = dr;
+  if (recordActions) actionLog.push_back({(int)ActionType::LEADERSHIP_MOVEMENT, p, src, dst, -1});
+  return true;
+}
+
+}  // namespace oracle

@@ -1,0 +1,43 @@
+// ORACLE — test infrastructure only (see jsem.h header).
+// GoalOptimizer.optimizations restatement (analyzer/GoalOptimizer.java:435-524) and
+// AnalyzerUtils.getDiff/hasDiff (analyzer/AnalyzerUtils.java:55-158).
+#pragma once
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "goals.h"
+
+namespace oracle {
+
+struct GoalResult {
+  std::string name;
+  bool succeeded;
+  bool hasDiff;
+  double seconds;
+  ClusterModelStats stats;  // GoalOptimizer.statsByGoalPriority entry
+  int64_t candidates;
+  int64_t actions;
+};
+
+struct Proposal {  // ExecutionProposal (executor/ExecutionProposal.java:58-)
+  int partition;
+  int partitionSize;  // (int) leader DISK util
+  int oldLeader;
+  std::vector<int> oldReplicas, newReplicas;  // broker ids, new list has the leader first
+};
+
+struct OptimizerResult {
+  ClusterModelStats initStats;
+  std::vector<GoalResult> goals;
+  std::vector<Proposal> proposals;
+  double seconds = 0;
+  int64_t candidates = 0;
+};
+
+std::unique_ptr<Goal> makeGoal(int kind, const BalancingConstraint& bc);  // kinds: include/ccmi.h ccmi_goal_kind
+
+OptimizerResult optimizations(ClusterModel& cm, const std::vector<int>& goalKinds, const BalancingConstraint& bc,
+                              const OptimizationOptions& o);
+
+}  // namespace oracle

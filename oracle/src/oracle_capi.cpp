@@ -1,0 +1,300 @@
+// ORACLE — test infrastructure only (see jsem.h header). C entry points (liboracle_cc.so) used by
+// tests/ (ctypes) and bench.py's cpu_baseline leg. Shares only the data layout of include/ccmi.h.
+#include <chrono>
+#include <cstring>
+#include <memory>
+#include <string>
+
+#include "../../include/ccmi.h"
+#include "optimizer.h"
+#include "random_cluster.h"
+
+using namespace oracle;
+
+namespace {
+struct Handle {
+  ClusterModel cm;
+  OptimizerResult last;
+  std::string err;
+};
+
+BalancingConstraint toBc(const ccmi_balancing_constraint* c) {
+  BalancingConstraint bc;
+  if (!c) return bc;
+  for (int r = 0; r < 4; ++r) {
+    bc.resourceBalancePercentage[r] = c->resource_balance_percentage[r];
+    bc.capacityThreshold[r] = c->capacity_threshold[r];
+    bc.lowUtilizationThreshold[r] = c->low_utilization_threshold[r];
+  }
+  bc.replicaBalancePercentage = c->replica_balance_percentage;
+  bc.leaderReplicaBalancePercentage = c->leader_replica_balance_percentage;
+  bc.topicReplicaBalancePercentage = c->topic_replica_balance_percentage;
+  bc.topicReplicaBalanceMinGap = c->topic_replica_balance_min_gap;
+  bc.topicReplicaBalanceMaxGap = c->topic_replica_balance_max_gap;
+  bc.goalViolationDistributionThresholdMultiplier = c->goal_violation_distribution_threshold_multiplier;
+  bc.maxReplicasPerBroker = c->max_replicas_per_broker;
+  bc.overprovisionedMaxReplicasPerBroker = c->overprovisioned_max_replicas_per_broker;
+  bc.overprovisionedMinBrokers = c->overprovisioned_min_brokers;
+  return bc;
+}
+
+OptimizationOptions toOpts(const ccmi_opt_options* o) {
+  OptimizationOptions oo;
+  if (!o) return oo;
+  for (int i = 0; i < o->num_excluded_topics; ++i) oo.excludedTopics.insert(o->excluded_topics[i]);
+  for (int i = 0; i < o->num_excluded_brokers_for_leadership; ++i)
+    oo.excludedBrokersForLeadership.insert(o->excluded_brokers_for_leadership[i]);
+  for (int i = 0; i < o->num_excluded_brokers_for_replica_move; ++i)
+    oo.excludedBrokersForReplicaMove.insert(o->excluded_brokers_for_replica_move[i]);
+  oo.triggeredByGoalViolation = o->triggered_by_goal_violation != 0;
+  for (int i = 0; i < o->num_requested_destination_broker_ids; ++i)
+    oo.requestedDestinationBrokerIds.insert(o->requested_destination_broker_ids[i]);
+  oo.onlyMoveImmigrantReplicas = o->only_move_immigrant_replicas != 0;
+  oo.fastMode = o->fast_mode != 0;
+  return oo;
+}
+
+void toCStats(const ClusterModelStats& s, ccmi_cluster_stats* o) {
+  for (int r = 0; r < 4; ++r) {
+    o->resource_avg[r] = s.resAvg[r];
+    o->resource_max[r] = s.resMax[r];
+    o->resource_min[r] = s.resMin[r];
+    o->resource_std[r] = s.resStd[r];
+    o->num_balanced_brokers_by_resource[r] = s.numBalancedBrokersByResource[r];
+  }
+  o->potential_nw_out_avg = s.pnwAvg;
+  o->potential_nw_out_max = s.pnwMax;
+  o->potential_nw_out_min = s.pnwMin;
+  o->potential_nw_out_std = s.pnwStd;
+  o->num_brokers_under_potential_nw_out = s.numBrokersUnderPotentialNwOut;
+  o->replica_avg = s.repAvg;
+  o->replica_std = s.repStd;
+  o->replica_max = s.repMax;
+  o->replica_min = s.repMin;
+  o->leader_avg = s.leadAvg;
+  o->leader_std = s.leadStd;
+  o->leader_max = s.leadMax;
+  o->leader_min = s.leadMin;
+  o->topic_replica_avg = s.topicAvg;
+  o->topic_replica_std = s.topicStd;
+  o->topic_replica_max = s.topicMax;
+  o->topic_replica_min = s.topicMin;
+  o->num_brokers = s.numBrokers;
+  o->num_replicas_in_cluster = s.numReplicasInCluster;
+  o->num_partitions_with_offline_replicas = s.numPartitionsWithOfflineReplicas;
+  o->num_topics = s.numTopics;
+  o->num_unbalanced_disks = s.numUnbalancedDisks;
+  o->disk_utilization_std = s.diskUtilizationStDev;
+}
+}  // namespace
+
+extern "C" {
+
+void* oc_random_cluster(const ccmi_random_cluster_props* p) {
+  auto* h = new Handle();
+  ClusterProperties cp;
+  cp.numRacks = p->num_racks;
+  cp.numBrokers = p->num_brokers;
+  cp.numDeadBrokers = p->num_dead_brokers;
+  cp.numBrokersWithBadDisk = p->num_brokers_with_bad_disk;
+  cp.numReplicas = p->num_replicas;
+  cp.numTopics = p->num_topics;
+  cp.minReplication = p->min_replication;
+  cp.maxReplication = p->max_replication;
+  cp.meanCpu = p->mean_cpu;
+  cp.meanDisk = p->mean_disk;
+  cp.meanNwIn = p->mean_nw_in;
+  cp.meanNwOut = p->mean_nw_out;
+  cp.distribution = p->distribution;
+  cp.rackAware = p->rack_aware != 0;
+  cp.leaderInFirstPosition = p->leader_in_first_position != 0;
+  try {
+    randomCluster(h->cm, cp);
+  } catch (std::exception& e) {
+    delete h;
+    return nullptr;
+  }
+  return h;
+}
+
+// Build the model from a flattened desc exactly as ccmi.h documents (replica index order replay).
+void* oc_from_desc(const ccmi_cluster_desc* d) {
+  auto* h = new Handle();
+  ClusterModel& cm = h->cm;
+  try {
+    cm.W = d->num_windows;
+    for (int i = 0; i < d->num_racks; ++i) cm.createRack(std::to_string(i));
+    for (int b = 0; b < d->num_brokers; ++b) cm.createBroker(d->broker_rack[b], d->broker_id[b], &d->broker_capacity[4 * b]);
+    for (int t = 0; t < d->num_topics; ++t) {
+      cm.topicNames.push_back(d->topic_names[t]);
+      cm.numReplicasByTopic.push_back(0);
+      cm.replicationFactorByTopic.push_back(0);
+    }
+    std::vector<char> created(d->num_partitions, 0);
+    const int W = d->num_windows;
+    for (int r = 0; r < d->num_replicas; ++r) {
+      int p = d->replica_partition[r];
+      if (!created[p]) {
+        while ((int)cm.partitions.size() <= p) cm.createPartition(d->partition_topic[cm.partitions.size()],
+                                                                   d->partition_number[cm.partitions.size()]);
+        created[p] = 1;
+      }
+      int b = d->replica_broker[r];
+      int idx = (int)cm.partitions[p].replicas.size();
+      int rr = cm.createReplica(b, p, idx, d->replica_is_leader[r] != 0, d->replica_offline[r] != 0);
+      Load amv;
+      amv.mask = 0x3F;
+      for (int k = 0; k < NUM_METRICS; ++k) {
+        amv.m[k].sum = 0.0;
+        for (int w = 0; w < W; ++w) {
+          amv.m[k].v[w] = d->replica_load[((size_t)r * NUM_METRICS + k) * W + w];
+          amv.m[k].sum += (double)amv.m[k].v[w];
+        }
+      }
+      cm.setReplicaLoad(rr, amv);
+    }
+    for (int p = 0; p < d->num_partitions; ++p) {
+      auto& lst = cm.partitions[p].replicas;
+      lst.assign(d->partition_replicas + d->partition_offset[p], d->partition_replicas + d->partition_offset[p + 1]);
+    }
+    cm.finalizeTopics();
+    for (int b = 0; b < d->num_brokers; ++b)
+      if (d->broker_state[b] != CCMI_BROKER_ALIVE) cm.setBrokerState(b, (BrokerState)d->broker_state[b]);
+  } catch (std::exception& e) {
+    delete h;
+    return nullptr;
+  }
+  return h;
+}
+
+void oc_free(void* h) { delete (Handle*)h; }
+
+void oc_sizes(void* hv, int32_t* out) {
+  auto* h = (Handle*)hv;
+  out[0] = (int32_t)h->cm.brokers.size();
+  out[1] = (int32_t)h->cm.topicNames.size();
+  out[2] = (int32_t)h->cm.partitions.size();
+  out[3] = (int32_t)h->cm.replicas.size();
+  out[4] = (int32_t)h->cm.racks.size();
+  out[5] = h->cm.W;
+}
+const char* oc_topic_name(void* hv, int t) { return ((Handle*)hv)->cm.topicNames[t].c_str(); }
+
+// Export the *initial* model in desc layout (valid before any optimization).
+void oc_export(void* hv, int32_t* broker_rack, int32_t* broker_state, double* cap, int32_t* partition_topic,
+               int32_t* partition_number, int32_t* partition_offset, int32_t* partition_replicas,
+               int32_t* replica_partition, int32_t* replica_broker, uint8_t* is_leader, uint8_t* offline, float* load) {
+  auto* h = (Handle*)hv;
+  ClusterModel& cm = h->cm;
+  for (size_t b = 0; b < cm.brokers.size(); ++b) {
+    broker_rack[b] = cm.brokers[b].rack;
+    broker_state[b] = (int32_t)cm.brokers[b].state;
+    for (int r = 0; r < 4; ++r) cap[4 * b + r] = cm.brokers[b].state == BrokerState::DEAD ? -1.0 : cm.brokers[b].capacity[r];
+  }
+  int off = 0;
+  for (size_t p = 0; p < cm.partitions.size(); ++p) {
+    partition_topic[p] = cm.partitions[p].topic;
+    partition_number[p] = cm.partitions[p].number;
+    partition_offset[p] = off;
+    for (int r : cm.partitions[p].replicas) partition_replicas[off++] = r;
+  }
+  partition_offset[cm.partitions.size()] = off;
+  const int W = cm.W;
+  for (size_t r = 0; r < cm.replicas.size(); ++r) {
+    const Replica& rep = cm.replicas[r];
+    replica_partition[r] = rep.partition;
+    replica_broker[r] = rep.broker;
+    is_leader[r] = rep.isLeader;
+    offline[r] = rep.origOfflineFlag;
+    for (int k = 0; k < NUM_METRICS; ++k)
+      for (int w = 0; w < W; ++w) load[((size_t)r * NUM_METRICS + k) * W + w] = rep.load.m[k].v[w];
+  }
+}
+
+int oc_optimize(void* hv, const int32_t* goals, int n, const ccmi_balancing_constraint* c, const ccmi_opt_options* o,
+                ccmi_goal_result* results) {
+  auto* h = (Handle*)hv;
+  try {
+    std::vector<int> kinds(goals, goals + n);
+    h->last = optimizations(h->cm, kinds, toBc(c), toOpts(o));
+    for (int i = 0; i < n; ++i) {
+      const GoalResult& g = h->last.goals[i];
+      ccmi_goal_result& r = results[i];
+      std::memset(&r, 0, sizeof(r));
+      r.goal_kind = goals[i];
+      r.succeeded = g.succeeded;
+      r.has_diff = g.hasDiff;
+      r.seconds = g.seconds;
+      r.candidates = g.candidates;
+      r.actions = g.actions;
+      toCStats(g.stats, &r.stats);
+    }
+    return 0;
+  } catch (OptimizationFailure& e) {
+    h->err = e.what();
+    return CCMI_E_OPT_FAILURE;
+  } catch (std::logic_error& e) {
+    h->err = e.what();
+    return CCMI_E_STATE;
+  } catch (std::exception& e) {
+    h->err = e.what();
+    return CCMI_E_INVALID;
+  }
+}
+const char* oc_error(void* hv) { return ((Handle*)hv)->err.c_str(); }
+double oc_last_seconds(void* hv) { return ((Handle*)hv)->last.seconds; }
+int64_t oc_candidates(void* hv) { return ((Handle*)hv)->cm.candidatesEvaluated; }
+
+int64_t oc_action_count(void* hv) { return (int64_t)((Handle*)hv)->cm.actionLog.size(); }
+void oc_actions(void* hv, ccmi_action* out) {
+  auto* h = (Handle*)hv;
+  for (size_t i = 0; i < h->cm.actionLog.size(); ++i) {
+    const ActionRecord& a = h->cm.actionLog[i];
+    out[i] = {a.type, a.partition, a.src, a.dst, a.destPartition};
+  }
+}
+void oc_replica_distribution(void* hv, int32_t* out) {
+  auto v = ((Handle*)hv)->cm.replicaDistributionFlat();
+  std::memcpy(out, v.data(), v.size() * sizeof(int32_t));
+}
+void oc_leader_distribution(void* hv, int32_t* out) {
+  auto v = ((Handle*)hv)->cm.leaderDistribution();
+  std::memcpy(out, v.data(), v.size() * sizeof(int32_t));
+}
+void oc_stats(void* hv, const ccmi_balancing_constraint* c, const ccmi_opt_options* o, ccmi_cluster_stats* out) {
+  auto* h = (Handle*)hv;
+  toCStats(computeStats(h->cm, toBc(c), toOpts(o)), out);
+}
+int64_t oc_proposal_count(void* hv) { return (int64_t)((Handle*)hv)->last.proposals.size(); }
+void oc_proposals(void* hv, int max_rf, int32_t* partition, int32_t* size, int32_t* old_leader, int32_t* old_out,
+                  int32_t* new_out) {
+  auto* h = (Handle*)hv;
+  for (size_t i = 0; i < h->last.proposals.size(); ++i) {
+    const Proposal& p = h->last.proposals[i];
+    partition[i] = p.partition;
+    size[i] = p.partitionSize;
+    old_leader[i] = p.oldLeader;
+    for (int k = 0; k < max_rf; ++k) {
+      old_out[i * max_rf + k] = k < (int)p.oldReplicas.size() ? p.oldReplicas[k] : -1;
+      new_out[i * max_rf + k] = k < (int)p.newReplicas.size() ? p.newReplicas[k] : -1;
+    }
+  }
+}
+// Replica utilization of broker b / resource (for host-side checks in tests).
+double oc_broker_util(void* hv, int b, int res) { return ((Handle*)hv)->cm.brokerUtil(b, res); }
+// Exact RB-tree / PQ / Random probes for the known-answer tests.
+int64_t oc_java_random_probe(int64_t seed, int bound, int n, int32_t* ints, double* doubles) {
+  JRandom r(seed), r2(seed);
+  for (int i = 0; i < n; ++i) ints[i] = r.nextInt(bound);
+  for (int i = 0; i < n; ++i) doubles[i] = r2.nextDouble();
+  return r.seed;
+}
+double oc_balance_threshold(double avg, int res, double balancePct, double lowUtil, double multiplier, int triggered,
+                            double margin, int isLower) {
+  BalancingConstraint bc;
+  bc.resourceBalancePercentage[res] = balancePct;
+  bc.lowUtilizationThreshold[res] = lowUtil;
+  bc.goalViolationDistributionThresholdMultiplier = multiplier;
+  return computeResourceUtilizationBalanceThreshold(avg, res, bc, triggered != 0, margin, isLower != 0);
+}
+}

@@ -1,0 +1,170 @@
+// ORACLE — test infrastructure only (see jsem.h header).
+// RandomCluster.java:53-92 (generate), :119-336 (populate), :352-391 (dead broker marking),
+// :465-478 (uniformlyRandom / exponentialRandom). Math.log is glibc log (HotSpot's intrinsic is
+// within 1 ulp; a rare last-bit difference is a documented residual generator risk).
+#include "random_cluster.h"
+
+#include <cmath>
+#include <stdexcept>
+#include <string>
+
+namespace oracle {
+
+static const int64_t SEED_BASE = 3140, REPLICATION_SEED = 5234, LEADER_SEED = 72033, REPLICA_ASSIGNMENT_SEED = 1240,
+                     TOPIC_POPULARITY_SEED = 7234;
+
+static int uniformlyRandom(int min, int max, int64_t seed) { return JRandom(seed).nextInt((max - min) + 1) + min; }
+static double exponentialRandom(double mean, JRandom& r) { return std::log(1.0 - r.nextDouble()) * (-mean); }
+
+struct TopicMeta {
+  std::string name;
+  int rf, leaders;
+  int total() const { return rf * leaders; }
+};
+
+static int totalReplicas(const std::vector<TopicMeta>& m) {
+  int t = 0;
+  for (const auto& x : m) t += x.total();
+  return t;
+}
+
+void randomCluster(ClusterModel& cm, const ClusterProperties& p) {
+  if (p.numRacks > p.numBrokers || p.numBrokers <= 0 || p.numRacks <= 0) throw std::invalid_argument("bad input");
+  cm.W = 1;
+  for (int i = 0; i < p.numRacks; ++i) cm.createRack(std::to_string(i));
+  const double defCap[NUM_RESOURCES] = {100.0, 300000.0, 200000.0, 300000.0};  // CPU, NW_IN, NW_OUT, DISK
+  const double b1Cap[NUM_RESOURCES] = {100.0, 150000.0, 150000.0, 150000.0};
+  for (int i = 0; i < p.numRacks; ++i) cm.createBroker(i, i, i == 1 ? b1Cap : defCap);
+  for (int i = p.numRacks; i < p.numBrokers; ++i) {
+    int rack = uniformlyRandom(0, p.numRacks - 1, SEED_BASE + i);
+    cm.createBroker(rack, i, i == 1 ? b1Cap : defCap);
+  }
+  // populate
+  const int numBrokers = p.numBrokers;
+  if (p.numDeadBrokers < 0 || p.numBrokersWithBadDisk < 0 || numBrokers < p.numDeadBrokers + p.numBrokersWithBadDisk ||
+      p.numTopics <= 0 || p.minReplication > p.maxReplication || (p.leaderInFirstPosition && p.minReplication < 2) ||
+      p.maxReplication > numBrokers || p.numTopics > p.numReplicas ||
+      (p.minReplication == p.maxReplication && p.numReplicas % p.minReplication != 0))
+    throw std::invalid_argument("Random cluster population failed due to bad input.");
+  std::vector<TopicMeta> meta;
+  for (int i = 0; i < p.numTopics; ++i) meta.push_back({"T" + std::to_string(i), 1, 1});
+  for (int i = 0; i < p.numTopics; ++i) {
+    meta[i].rf = uniformlyRandom(p.minReplication, p.maxReplication, REPLICATION_SEED + i);
+    if (totalReplicas(meta) > p.numReplicas) meta[i].rf = p.minReplication;
+  }
+  int maxRandomLeaders = p.numReplicas / p.numTopics;
+  for (int i = 0; i < p.numTopics; ++i) {
+    int old = meta[i].leaders;
+    meta[i].leaders = uniformlyRandom(2, maxRandomLeaders, LEADER_SEED + i);
+    if (totalReplicas(meta) > p.numReplicas) meta[i].leaders = old;
+  }
+  int total = totalReplicas(meta);
+  while (total < p.numReplicas) {
+    for (int i = 0; i < p.numTopics; ++i) {
+      meta[i].leaders++;
+      total += meta[i].rf;
+      if (total > p.numReplicas) {
+        meta[i].leaders--;
+        total -= meta[i].rf;
+      }
+      if (total == p.numReplicas) break;
+    }
+  }
+  JRandom rCpu(100000), rDisk(300000), rNwIn(500000), rNwOut(700000);
+  JRandom rPop(TOPIC_POPULARITY_SEED);
+  meta.push_back({"TopicWithOneLeaderPerBroker", 2, numBrokers});
+  for (const auto& m : meta) cm.ensureTopic(m.name);
+  int replicaIndex = 0;
+  for (size_t ti = 0; ti < meta.size(); ++ti) {
+    const TopicMeta& datum = meta[ti];
+    double pop = exponentialRandom(1.0, rPop);
+    for (int i = 1; i <= datum.leaders; ++i) {
+      std::vector<int> usedBrokers, usedRacks;
+      int resolver = 0;
+      auto used = [&](int b) {
+        for (int x : usedBrokers)
+          if (x == b) return true;
+        if (p.rackAware)
+          for (int rk : usedRacks)
+            if (rk == cm.brokers[b].rack) return true;
+        return false;
+      };
+      auto binOf = [&](int v, bool linear) {
+        for (int bin = 1; bin <= numBrokers; ++bin) {
+          if (linear) {
+            int bv = 2 * v;
+            if (bv <= bin * (bin + 1) && bv > (bin - 1) * bin) return bin - 1;
+          } else if (v <= bin * bin) {
+            return bin - 1;
+          }
+        }
+        return 0;
+      };
+      int partitionIdx = -1;
+      for (int j = 1; j <= datum.rf; ++j) {
+        int b;
+        if (p.distribution == 0) {
+          b = uniformlyRandom(0, numBrokers - 1, REPLICA_ASSIGNMENT_SEED + replicaIndex);
+          while (used(b)) {
+            resolver++;
+            b = uniformlyRandom(0, numBrokers - 1, REPLICA_ASSIGNMENT_SEED + replicaIndex + resolver);
+          }
+        } else {
+          bool linear = p.distribution == 1;
+          int range = linear ? (numBrokers * (numBrokers + 1)) / 2 : numBrokers * numBrokers;
+          int v = uniformlyRandom(1, range, REPLICA_ASSIGNMENT_SEED + replicaIndex);
+          b = binOf(v, linear);
+          while (used(b)) {
+            resolver++;
+            v = uniformlyRandom(1, range, REPLICA_ASSIGNMENT_SEED + replicaIndex + resolver);
+            b = binOf(v, linear);
+          }
+        }
+        Load amv;
+        amv.mask = 0x3F;
+        for (int k = 0; k < NUM_METRICS; ++k) mvZero(amv.m[k], 1);
+        double cpu = exponentialRandom(p.meanCpu * pop, rCpu);
+        mvSet(amv.m[M_CPU], 0, cpu);
+        double nwIn = exponentialRandom(p.meanNwIn * pop, rNwIn);
+        mvSet(amv.m[M_LBI], 0, nwIn);
+        double disk = exponentialRandom(p.meanDisk * pop, rDisk);
+        mvSet(amv.m[M_DISK], 0, disk);
+        bool leader = (j == 1);
+        if (leader) {
+          double nwOut = exponentialRandom(p.meanNwOut * pop, rNwOut);
+          mvSet(amv.m[M_LBO], 0, nwOut);
+        } else {
+          mvSet(amv.m[M_LBO], 0, 0.0);
+        }
+        // AggregatedMetricValues.add(id, metricValues) copies through MetricValues.add (float values only)
+        Load staged;
+        amvAdd(staged, amv, 1);
+        if (j == 1) partitionIdx = cm.createPartition((int)ti, i - 1);
+        int r = cm.createReplica(b, partitionIdx, j - 1, leader, !cm.brokers[b].isAlive());
+        cm.setReplicaLoad(r, staged);
+        usedBrokers.push_back(b);
+        usedRacks.push_back(cm.brokers[b].rack);
+        replicaIndex++;
+      }
+      if (!p.leaderInFirstPosition) {
+        Partition& part = cm.partitions[partitionIdx];
+        int lpos = 0;
+        for (size_t k = 0; k < part.replicas.size(); ++k)
+          if (part.replicas[k] == part.leader) lpos = (int)k;
+        std::swap(part.replicas[1], part.replicas[lpos]);
+      }
+    }
+  }
+  cm.finalizeTopics();
+  // markBrokenBrokers: dead brokers (no excluded topics in scope)
+  if (p.numDeadBrokers > 0) {
+    int idx = 0;
+    while (p.numDeadBrokers - idx > 0) {
+      if (cm.brokers[idx].isAlive()) cm.setBrokerState(idx, BrokerState::DEAD);
+      idx++;
+    }
+  }
+  if (p.numBrokersWithBadDisk > 0) throw std::runtime_error("bad-disk marking not in round-1 scope");
+}
+
+}  // namespace oracle

@@ -1,0 +1,48 @@
+// ORACLE — test infrastructure only (see jsem.h header).
+// ClusterModelStats.populate restatement: cruise-control/src/main/java/.../model/ClusterModelStats.java:84-511
+// plus the BalancingConstraint analyzer knobs it reads (analyzer/BalancingConstraint.java:54-105,
+// defaults config/constants/AnalyzerConfig.java:58-464).
+#pragma once
+#include "model.h"
+
+namespace oracle {
+
+struct BalancingConstraint {
+  double resourceBalancePercentage[NUM_RESOURCES] = {1.10, 1.10, 1.10, 1.10};
+  double capacityThreshold[NUM_RESOURCES] = {0.7, 0.8, 0.8, 0.8};  // CPU, NW_IN, NW_OUT, DISK
+  double lowUtilizationThreshold[NUM_RESOURCES] = {0.0, 0.0, 0.0, 0.0};
+  double replicaBalancePercentage = 1.10;
+  double leaderReplicaBalancePercentage = 1.10;
+  double topicReplicaBalancePercentage = 3.00;
+  int topicReplicaBalanceMinGap = 2;
+  int topicReplicaBalanceMaxGap = 40;
+  double goalViolationDistributionThresholdMultiplier = 1.0;
+  int64_t maxReplicasPerBroker = 10000;
+  int64_t overprovisionedMaxReplicasPerBroker = 1500;
+  int overprovisionedMinBrokers = 3;
+};
+
+struct ClusterModelStats {
+  double resAvg[NUM_RESOURCES], resMax[NUM_RESOURCES], resMin[NUM_RESOURCES], resStd[NUM_RESOURCES];
+  int numBalancedBrokersByResource[NUM_RESOURCES];
+  double pnwAvg, pnwMax, pnwMin, pnwStd;
+  int numBrokersUnderPotentialNwOut;
+  double repAvg, repStd;
+  int repMax, repMin;
+  double leadAvg, leadStd;
+  int leadMax, leadMin;
+  double topicAvg, topicStd;
+  int topicMax, topicMin;
+  int numBrokers, numReplicasInCluster, numPartitionsWithOfflineReplicas, numTopics;
+  int numUnbalancedDisks;
+  double diskUtilizationStDev;
+};
+
+// GoalUtils.computeResourceUtilizationBalanceThreshold (GoalUtils.java:550-602)
+double computeResourceUtilizationBalanceThreshold(double avgUtilizationPercentage, int resource,
+                                                  const BalancingConstraint& bc, bool triggeredByGoalViolation,
+                                                  double balanceMargin, bool isLowerThreshold);
+
+ClusterModelStats computeStats(const ClusterModel& cm, const BalancingConstraint& bc, const OptimizationOptions& o);
+
+}  // namespace oracle
