@@ -1,0 +1,531 @@
+"""Python binding of libccmi.so (include/ccmi.h) mirroring the reference's optimizer interface.
+
+Names follow the reference so parity tests read like the reference's own tests:
+
+  ClusterModel            <- com.linkedin.kafka.cruisecontrol.model.ClusterModel (a device session)
+  GoalOptimizer           <- analyzer/GoalOptimizer.java  (optimizations(), GoalOptimizer.java:435-524)
+  <Goal>                  <- analyzer/goals/*Goal.java     (name(), optimize(), actionAcceptance())
+  OptimizationOptions     <- analyzer/OptimizationOptions.java
+  BalancingConstraint     <- analyzer/BalancingConstraint.java (AnalyzerConfig.java defaults)
+  OptimizerResult         <- analyzer/OptimizerResult.java  (proposals, per-goal stats)
+  ExecutionProposal       <- executor/ExecutionProposal.java
+  RandomCluster           <- src/test/.../model/RandomCluster.java (fixture generator)
+
+Errors map to the reference's exceptions: OptimizationFailureException, IllegalStateException,
+IllegalArgumentException; a missing/unsupported device raises DeviceError (no CPU fallback exists).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional, Sequence
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+DEFAULT_LIB = os.path.join(_HERE, "libccmi.so")
+
+RESOURCES = ("CPU", "NW_IN", "NW_OUT", "DISK")
+CPU, NW_IN, NW_OUT, DISK = range(4)
+
+GOAL_KINDS: Dict[str, int] = {
+    "RackAwareGoal": 0,
+    "MinTopicLeadersPerBrokerGoal": 1,
+    "ReplicaCapacityGoal": 2,
+    "DiskCapacityGoal": 3,
+    "NetworkInboundCapacityGoal": 4,
+    "NetworkOutboundCapacityGoal": 5,
+    "CpuCapacityGoal": 6,
+    "ReplicaDistributionGoal": 7,
+    "PotentialNwOutGoal": 8,
+    "DiskUsageDistributionGoal": 9,
+    "NetworkInboundUsageDistributionGoal": 10,
+    "NetworkOutboundUsageDistributionGoal": 11,
+    "CpuUsageDistributionGoal": 12,
+    "TopicReplicaDistributionGoal": 13,
+    "LeaderReplicaDistributionGoal": 14,
+    "LeaderBytesInDistributionGoal": 15,
+    "IntraBrokerDiskCapacityGoal": 16,
+    "IntraBrokerDiskUsageDistributionGoal": 17,
+}
+GOAL_NAMES = {v: k for k, v in GOAL_KINDS.items()}
+# Goals whose drivers are implemented in this build (config C1's chain).
+IMPLEMENTED = ("ReplicaDistributionGoal", "DiskUsageDistributionGoal", "NetworkInboundUsageDistributionGoal",
+               "NetworkOutboundUsageDistributionGoal", "CpuUsageDistributionGoal")
+
+ACTION_TYPES = ("INTER_BROKER_REPLICA_MOVEMENT", "LEADERSHIP_MOVEMENT", "INTER_BROKER_REPLICA_SWAP",
+                "INTRA_BROKER_REPLICA_MOVEMENT", "INTRA_BROKER_REPLICA_SWAP")
+ACCEPTANCE = ("ACCEPT", "REPLICA_REJECT", "BROKER_REJECT")
+
+
+# ----------------------------------------------------------------------------------------------- ctypes layouts
+class ClusterDesc(C.Structure):
+    _fields_ = [("num_windows", C.c_int32), ("num_racks", C.c_int32), ("num_brokers", C.c_int32),
+                ("broker_id", C.POINTER(C.c_int32)), ("broker_rack", C.POINTER(C.c_int32)),
+                ("broker_state", C.POINTER(C.c_int32)), ("broker_capacity", C.POINTER(C.c_double)),
+                ("num_topics", C.c_int32), ("topic_names", C.POINTER(C.c_char_p)),
+                ("num_partitions", C.c_int32), ("partition_topic", C.POINTER(C.c_int32)),
+                ("partition_number", C.POINTER(C.c_int32)), ("partition_offset", C.POINTER(C.c_int32)),
+                ("partition_replicas", C.POINTER(C.c_int32)), ("num_replicas", C.c_int32),
+                ("replica_partition", C.POINTER(C.c_int32)), ("replica_broker", C.POINTER(C.c_int32)),
+                ("replica_is_leader", C.POINTER(C.c_uint8)), ("replica_offline", C.POINTER(C.c_uint8)),
+                ("replica_load", C.POINTER(C.c_float))]
+
+
+class ConstraintStruct(C.Structure):
+    _fields_ = [("resource_balance_percentage", C.c_double * 4), ("capacity_threshold", C.c_double * 4),
+                ("low_utilization_threshold", C.c_double * 4), ("replica_balance_percentage", C.c_double),
+                ("leader_replica_balance_percentage", C.c_double), ("topic_replica_balance_percentage", C.c_double),
+                ("topic_replica_balance_min_gap", C.c_int32), ("topic_replica_balance_max_gap", C.c_int32),
+                ("goal_violation_distribution_threshold_multiplier", C.c_double),
+                ("max_replicas_per_broker", C.c_int64), ("overprovisioned_max_replicas_per_broker", C.c_int64),
+                ("overprovisioned_min_brokers", C.c_int32)]
+
+
+class OptionsStruct(C.Structure):
+    _fields_ = [("excluded_topics", C.POINTER(C.c_int32)), ("num_excluded_topics", C.c_int32),
+                ("excluded_brokers_for_leadership", C.POINTER(C.c_int32)),
+                ("num_excluded_brokers_for_leadership", C.c_int32),
+                ("excluded_brokers_for_replica_move", C.POINTER(C.c_int32)),
+                ("num_excluded_brokers_for_replica_move", C.c_int32), ("triggered_by_goal_violation", C.c_int32),
+                ("requested_destination_broker_ids", C.POINTER(C.c_int32)),
+                ("num_requested_destination_broker_ids", C.c_int32), ("only_move_immigrant_replicas", C.c_int32),
+                ("fast_mode", C.c_int32)]
+
+
+class ActionStruct(C.Structure):
+    _fields_ = [("type", C.c_int32), ("partition", C.c_int32), ("source_broker", C.c_int32),
+                ("destination_broker", C.c_int32), ("destination_partition", C.c_int32)]
+
+
+class StatsStruct(C.Structure):
+    _fields_ = [("resource_avg", C.c_double * 4), ("resource_max", C.c_double * 4),
+                ("resource_min", C.c_double * 4), ("resource_std", C.c_double * 4),
+                ("num_balanced_brokers_by_resource", C.c_int32 * 4), ("potential_nw_out_avg", C.c_double),
+                ("potential_nw_out_max", C.c_double), ("potential_nw_out_min", C.c_double),
+                ("potential_nw_out_std", C.c_double), ("num_brokers_under_potential_nw_out", C.c_int32),
+                ("replica_avg", C.c_double), ("replica_std", C.c_double), ("replica_max", C.c_int32),
+                ("replica_min", C.c_int32), ("leader_avg", C.c_double), ("leader_std", C.c_double),
+                ("leader_max", C.c_int32), ("leader_min", C.c_int32), ("topic_replica_avg", C.c_double),
+                ("topic_replica_std", C.c_double), ("topic_replica_max", C.c_int32), ("topic_replica_min", C.c_int32),
+                ("num_brokers", C.c_int32), ("num_replicas_in_cluster", C.c_int32),
+                ("num_partitions_with_offline_replicas", C.c_int32), ("num_topics", C.c_int32),
+                ("num_unbalanced_disks", C.c_int32), ("disk_utilization_std", C.c_double)]
+
+
+class GoalResultStruct(C.Structure):
+    _fields_ = [("goal_kind", C.c_int32), ("succeeded", C.c_int32), ("has_diff", C.c_int32), ("seconds", C.c_double),
+                ("candidates", C.c_int64), ("device_candidates", C.c_int64), ("device_launches", C.c_int64),
+                ("actions", C.c_int64), ("stats", StatsStruct)]
+
+
+class RandomClusterProps(C.Structure):
+    _fields_ = [("num_racks", C.c_int32), ("num_brokers", C.c_int32), ("num_dead_brokers", C.c_int32),
+                ("num_brokers_with_bad_disk", C.c_int32), ("num_replicas", C.c_int32), ("num_topics", C.c_int32),
+                ("min_replication", C.c_int32), ("max_replication", C.c_int32), ("mean_cpu", C.c_double),
+                ("mean_disk", C.c_double), ("mean_nw_in", C.c_double), ("mean_nw_out", C.c_double),
+                ("distribution", C.c_int32), ("rack_aware", C.c_int32), ("leader_in_first_position", C.c_int32)]
+
+
+class PerfStruct(C.Structure):
+    _fields_ = [("scan_launches", C.c_int64), ("scan_kernel_ms", C.c_double), ("scan_bytes", C.c_int64),
+                ("stats_launches", C.c_int64), ("stats_kernel_ms", C.c_double), ("stats_bytes", C.c_int64),
+                ("host_syncs", C.c_int64)]
+
+
+# ----------------------------------------------------------------------------------------------- errors
+class CruiseControlError(RuntimeError):
+    pass
+
+
+class OptimizationFailureException(CruiseControlError):
+    pass
+
+
+class IllegalStateException(CruiseControlError):
+    pass
+
+
+class IllegalArgumentException(CruiseControlError):
+    pass
+
+
+class UnsupportedOperationException(CruiseControlError):
+    pass
+
+
+class DeviceError(CruiseControlError):
+    pass
+
+
+_STATUS = {1: IllegalArgumentException, 2: DeviceError, 3: OptimizationFailureException, 4: IllegalStateException,
+           5: UnsupportedOperationException}
+
+EXPORTED_SYMBOLS = (
+    "ccmi_last_error", "ccmi_abi_version", "ccmi_default_constraint", "ccmi_default_random_cluster_props",
+    "ccmi_random_cluster", "ccmi_cluster_buffers_desc", "ccmi_cluster_buffers_free", "ccmi_session_create",
+    "ccmi_session_destroy", "ccmi_optimizations", "ccmi_goal_optimize", "ccmi_action_acceptance",
+    "ccmi_compute_cluster_stats", "ccmi_action_log_count", "ccmi_action_log_copy", "ccmi_replica_distribution",
+    "ccmi_leader_distribution", "ccmi_proposal_count", "ccmi_proposals", "ccmi_perf", "ccmi_perf_reset",
+    "ccmi_set_kernel_timing")
+
+
+class Library:
+    """Loaded libccmi.so (or, in CPU tests only, the emulation build from tests/emu)."""
+
+    _cache: Dict[str, "Library"] = {}
+
+    def __init__(self, path: str = DEFAULT_LIB):
+        if not os.path.exists(path):
+            raise DeviceError(f"{path} not found: build it with __graft_entry__.build() (no CPU fallback exists)")
+        self.path = path
+        self.lib = C.CDLL(path)
+        L = self.lib
+        L.ccmi_last_error.restype = C.c_char_p
+        L.ccmi_random_cluster.argtypes = [C.POINTER(RandomClusterProps), C.POINTER(C.c_void_p)]
+        L.ccmi_cluster_buffers_desc.restype = C.POINTER(ClusterDesc)
+        L.ccmi_cluster_buffers_desc.argtypes = [C.c_void_p]
+        L.ccmi_cluster_buffers_free.argtypes = [C.c_void_p]
+        L.ccmi_session_create.argtypes = [C.c_int32, C.POINTER(ClusterDesc), C.POINTER(C.c_void_p)]
+        L.ccmi_session_destroy.argtypes = [C.c_void_p]
+        L.ccmi_optimizations.argtypes = [C.c_void_p, C.POINTER(C.c_int32), C.c_int32, C.POINTER(ConstraintStruct),
+                                         C.POINTER(OptionsStruct), C.POINTER(GoalResultStruct)]
+        L.ccmi_goal_optimize.argtypes = [C.c_void_p, C.c_int32, C.POINTER(ConstraintStruct), C.POINTER(OptionsStruct),
+                                         C.POINTER(GoalResultStruct)]
+        L.ccmi_action_acceptance.argtypes = [C.c_void_p, C.c_int32, C.POINTER(ActionStruct), C.POINTER(C.c_int32)]
+        L.ccmi_compute_cluster_stats.argtypes = [C.c_void_p, C.POINTER(ConstraintStruct), C.POINTER(OptionsStruct),
+                                                 C.POINTER(StatsStruct)]
+        L.ccmi_action_log_count.restype = C.c_int64
+        L.ccmi_action_log_count.argtypes = [C.c_void_p]
+        L.ccmi_action_log_copy.argtypes = [C.c_void_p, C.c_int64, C.c_int64, C.POINTER(ActionStruct)]
+        L.ccmi_replica_distribution.argtypes = [C.c_void_p, C.POINTER(C.c_int32)]
+        L.ccmi_leader_distribution.argtypes = [C.c_void_p, C.POINTER(C.c_int32)]
+        L.ccmi_proposal_count.restype = C.c_int64
+        L.ccmi_proposal_count.argtypes = [C.c_void_p]
+        L.ccmi_proposals.argtypes = [C.c_void_p, C.c_int32] + [C.POINTER(C.c_int32)] * 5
+        L.ccmi_perf.argtypes = [C.c_void_p, C.POINTER(PerfStruct)]
+        L.ccmi_perf_reset.argtypes = [C.c_void_p]
+        L.ccmi_set_kernel_timing.argtypes = [C.c_void_p, C.c_int32]
+        L.ccmi_default_constraint.argtypes = [C.POINTER(ConstraintStruct)]
+        L.ccmi_default_random_cluster_props.argtypes = [C.POINTER(RandomClusterProps)]
+
+    @classmethod
+    def get(cls, path: str = DEFAULT_LIB) -> "Library":
+        if path not in cls._cache:
+            cls._cache[path] = Library(path)
+        return cls._cache[path]
+
+    def check(self, status: int) -> None:
+        if status != 0:
+            msg = self.lib.ccmi_last_error().decode(errors="replace")
+            raise _STATUS.get(status, CruiseControlError)(msg)
+
+
+# ----------------------------------------------------------------------------------------------- options / constraint
+@dataclass
+class BalancingConstraint:
+    resource_balance_percentage: Sequence[float] = (1.10, 1.10, 1.10, 1.10)
+    capacity_threshold: Sequence[float] = (0.7, 0.8, 0.8, 0.8)
+    low_utilization_threshold: Sequence[float] = (0.0, 0.0, 0.0, 0.0)
+    replica_balance_percentage: float = 1.10
+    goal_violation_distribution_threshold_multiplier: float = 1.0
+    max_replicas_per_broker: int = 10000
+
+    def set_resource_balance_percentage(self, p: float) -> None:  # BalancingConstraint.setResourceBalancePercentage
+        self.resource_balance_percentage = (p, p, p, p)
+
+    def set_capacity_threshold(self, t: float) -> None:
+        self.capacity_threshold = (t, t, t, t)
+
+    def to_struct(self) -> ConstraintStruct:
+        s = ConstraintStruct()
+        s.resource_balance_percentage[:] = list(self.resource_balance_percentage)
+        s.capacity_threshold[:] = list(self.capacity_threshold)
+        s.low_utilization_threshold[:] = list(self.low_utilization_threshold)
+        s.replica_balance_percentage = self.replica_balance_percentage
+        s.leader_replica_balance_percentage = 1.10
+        s.topic_replica_balance_percentage = 3.00
+        s.topic_replica_balance_min_gap = 2
+        s.topic_replica_balance_max_gap = 40
+        s.goal_violation_distribution_threshold_multiplier = self.goal_violation_distribution_threshold_multiplier
+        s.max_replicas_per_broker = self.max_replicas_per_broker
+        s.overprovisioned_max_replicas_per_broker = 1500
+        s.overprovisioned_min_brokers = 3
+        return s
+
+
+@dataclass
+class OptimizationOptions:
+    excluded_topics: Sequence[int] = ()
+    excluded_brokers_for_leadership: Sequence[int] = ()
+    excluded_brokers_for_replica_move: Sequence[int] = ()
+    is_triggered_by_goal_violation: bool = False
+    requested_destination_broker_ids: Sequence[int] = ()
+    only_move_immigrant_replicas: bool = False
+    fast_mode: bool = True
+
+    def to_struct(self):
+        keep = []
+
+        def arr(xs):
+            a = (C.c_int32 * max(1, len(xs)))(*xs)
+            keep.append(a)
+            return C.cast(a, C.POINTER(C.c_int32)), len(xs)
+
+        s = OptionsStruct()
+        s.excluded_topics, s.num_excluded_topics = arr(list(self.excluded_topics))
+        s.excluded_brokers_for_leadership, s.num_excluded_brokers_for_leadership = arr(
+            list(self.excluded_brokers_for_leadership))
+        s.excluded_brokers_for_replica_move, s.num_excluded_brokers_for_replica_move = arr(
+            list(self.excluded_brokers_for_replica_move))
+        s.triggered_by_goal_violation = int(self.is_triggered_by_goal_violation)
+        s.requested_destination_broker_ids, s.num_requested_destination_broker_ids = arr(
+            list(self.requested_destination_broker_ids))
+        s.only_move_immigrant_replicas = int(self.only_move_immigrant_replicas)
+        s.fast_mode = int(self.fast_mode)
+        return s, keep
+
+
+# ----------------------------------------------------------------------------------------------- goals
+class Goal:
+    """A goal plugin by reference simple class name (Goal.name(), AbstractGoal.java:141-144)."""
+
+    def __init__(self, name: Optional[str] = None, constraint: Optional[BalancingConstraint] = None):
+        self._name = name or type(self).__name__
+        if self._name not in GOAL_KINDS:
+            raise IllegalArgumentException(f"unknown goal {self._name}")
+        self.constraint = constraint
+
+    def name(self) -> str:
+        return self._name
+
+    @property
+    def kind(self) -> int:
+        return GOAL_KINDS[self._name]
+
+    def is_hard_goal(self) -> bool:
+        return self._name in ("RackAwareGoal", "MinTopicLeadersPerBrokerGoal", "ReplicaCapacityGoal",
+                              "DiskCapacityGoal", "NetworkInboundCapacityGoal", "NetworkOutboundCapacityGoal",
+                              "CpuCapacityGoal")
+
+    def optimize(self, cluster: "ClusterModel", options: Optional[OptimizationOptions] = None) -> bool:
+        """Goal.optimize: the session remembers this goal as optimized afterwards."""
+        res = cluster._goal_optimize(self, options)
+        return bool(res.succeeded)
+
+    def __repr__(self) -> str:
+        return self._name
+
+
+for _n in GOAL_KINDS:
+    globals()[_n] = type(_n, (Goal,), {})
+
+
+# ----------------------------------------------------------------------------------------------- results
+@dataclass
+class ExecutionProposal:
+    partition: int
+    partition_size: int
+    old_leader: int
+    old_replicas: List[int]
+    new_replicas: List[int]
+
+
+@dataclass
+class GoalResult:
+    name: str
+    succeeded: bool
+    has_diff: bool
+    seconds: float
+    candidates: int
+    device_candidates: int
+    device_launches: int
+    actions: int
+    stats: Dict[str, object]
+
+
+@dataclass
+class OptimizerResult:
+    goal_results: List[GoalResult]
+    proposals: List[ExecutionProposal]
+    actions: List[tuple]
+    seconds: float
+    violated_goals_after: List[str] = field(default_factory=list)
+
+    @property
+    def candidates(self) -> int:
+        return sum(g.candidates for g in self.goal_results)
+
+
+def stats_to_dict(s: StatsStruct) -> Dict[str, object]:
+    out = {}
+    for name, typ in StatsStruct._fields_:
+        v = getattr(s, name)
+        out[name] = list(v) if hasattr(v, "__len__") else v
+    return out
+
+
+# ----------------------------------------------------------------------------------------------- cluster / session
+class ClusterBuffers:
+    """Owns a generated flattened cluster (RandomCluster fixture)."""
+
+    def __init__(self, lib: Library, handle: int):
+        self.lib = lib
+        self.handle = C.c_void_p(handle)
+        self.desc = lib.lib.ccmi_cluster_buffers_desc(self.handle).contents
+
+    def __del__(self):
+        try:
+            self.lib.lib.ccmi_cluster_buffers_free(self.handle)
+        except Exception:
+            pass
+
+
+class RandomCluster:
+    """RandomCluster.generate + populate (RandomCluster.java:53-336) with TestConstants.BASE_PROPERTIES defaults."""
+
+    BASE = dict(num_racks=10, num_brokers=40, num_dead_brokers=0, num_brokers_with_bad_disk=0, num_replicas=50001,
+                num_topics=3000, min_replication=3, max_replication=3, mean_cpu=0.01, mean_disk=100.0,
+                mean_nw_in=100.0, mean_nw_out=100.0, distribution=0, rack_aware=0, leader_in_first_position=1)
+
+    @staticmethod
+    def props(**overrides) -> RandomClusterProps:
+        d = dict(RandomCluster.BASE)
+        d.update(overrides)
+        p = RandomClusterProps()
+        for k, v in d.items():
+            setattr(p, k, v)
+        return p
+
+    @staticmethod
+    def generate(lib: Optional[Library] = None, **overrides) -> ClusterBuffers:
+        lib = lib or Library.get()
+        h = C.c_void_p()
+        lib.check(lib.lib.ccmi_random_cluster(C.byref(RandomCluster.props(**overrides)), C.byref(h)))
+        return ClusterBuffers(lib, h.value)
+
+
+class ClusterModel:
+    """A device-resident model session (ccmi_session)."""
+
+    def __init__(self, desc: ClusterDesc, device: int = 0, lib: Optional[Library] = None, keepalive=None):
+        self.lib = lib or Library.get()
+        self._keep = keepalive
+        self.desc = desc
+        h = C.c_void_p()
+        self.lib.check(self.lib.lib.ccmi_session_create(device, C.byref(desc), C.byref(h)))
+        self.handle = h
+        self.num_partitions = desc.num_partitions
+        self.num_replicas = desc.num_replicas
+
+    @staticmethod
+    def from_buffers(buf: ClusterBuffers, device: int = 0) -> "ClusterModel":
+        return ClusterModel(buf.desc, device=device, lib=buf.lib, keepalive=buf)
+
+    def close(self) -> None:
+        if self.handle:
+            self.lib.lib.ccmi_session_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _goal_optimize(self, goal: Goal, options: Optional[OptimizationOptions]) -> GoalResultStruct:
+        res = GoalResultStruct()
+        o, keep = (options or OptimizationOptions()).to_struct()
+        c = (goal.constraint or BalancingConstraint()).to_struct()
+        self.lib.check(self.lib.lib.ccmi_goal_optimize(self.handle, goal.kind, C.byref(c), C.byref(o), C.byref(res)))
+        return res
+
+    def action_acceptance(self, optimized_goal_index: int, action_type: int, partition: int, source: int,
+                          destination: int, destination_partition: int = -1) -> str:
+        a = ActionStruct(action_type, partition, source, destination, destination_partition)
+        out = C.c_int32()
+        self.lib.check(self.lib.lib.ccmi_action_acceptance(self.handle, optimized_goal_index, C.byref(a),
+                                                           C.byref(out)))
+        return ACCEPTANCE[out.value]
+
+    def cluster_stats(self, constraint: Optional[BalancingConstraint] = None,
+                      options: Optional[OptimizationOptions] = None) -> Dict[str, object]:
+        s = StatsStruct()
+        o, keep = (options or OptimizationOptions()).to_struct()
+        c = (constraint or BalancingConstraint()).to_struct()
+        self.lib.check(self.lib.lib.ccmi_compute_cluster_stats(self.handle, C.byref(c), C.byref(o), C.byref(s)))
+        return stats_to_dict(s)
+
+    def actions(self) -> List[tuple]:
+        n = self.lib.lib.ccmi_action_log_count(self.handle)
+        buf = (ActionStruct * max(1, n))()
+        if n:
+            self.lib.check(self.lib.lib.ccmi_action_log_copy(self.handle, 0, n, buf))
+        return [(a.type, a.partition, a.source_broker, a.destination_broker, a.destination_partition)
+                for a in buf[:n]]
+
+    def replica_distribution(self) -> List[int]:
+        out = (C.c_int32 * self.num_replicas)()
+        self.lib.check(self.lib.lib.ccmi_replica_distribution(self.handle, out))
+        return list(out)
+
+    def leader_distribution(self) -> List[int]:
+        out = (C.c_int32 * self.num_partitions)()
+        self.lib.check(self.lib.lib.ccmi_leader_distribution(self.handle, out))
+        return list(out)
+
+    def proposals(self, max_rf: int = 8) -> List[ExecutionProposal]:
+        n = self.lib.lib.ccmi_proposal_count(self.handle)
+        if n == 0:
+            return []
+        part = (C.c_int32 * n)()
+        size = (C.c_int32 * n)()
+        old_leader = (C.c_int32 * n)()
+        old_r = (C.c_int32 * (n * max_rf))()
+        new_r = (C.c_int32 * (n * max_rf))()
+        self.lib.check(self.lib.lib.ccmi_proposals(self.handle, max_rf, part, size, old_leader, old_r, new_r))
+        out = []
+        for i in range(n):
+            o = [x for x in old_r[i * max_rf:(i + 1) * max_rf] if x >= 0]
+            nw = [x for x in new_r[i * max_rf:(i + 1) * max_rf] if x >= 0]
+            out.append(ExecutionProposal(part[i], size[i], old_leader[i], o, nw))
+        return out
+
+    def perf(self) -> PerfStruct:
+        p = PerfStruct()
+        self.lib.check(self.lib.lib.ccmi_perf(self.handle, C.byref(p)))
+        return p
+
+    def reset_perf(self) -> None:
+        self.lib.lib.ccmi_perf_reset(self.handle)
+
+    def set_kernel_timing(self, enabled: bool) -> None:
+        self.lib.lib.ccmi_set_kernel_timing(self.handle, int(enabled))
+
+
+class GoalOptimizer:
+    """GoalOptimizer.optimizations (GoalOptimizer.java:435-524) on a device session."""
+
+    def __init__(self, constraint: Optional[BalancingConstraint] = None):
+        self.constraint = constraint or BalancingConstraint()
+
+    def optimizations(self, cluster: ClusterModel, goals_by_priority: Sequence[Goal],
+                      options: Optional[OptimizationOptions] = None) -> OptimizerResult:
+        if not goals_by_priority:
+            raise IllegalArgumentException("At least one goal must be provided to get an optimization result.")
+        kinds = (C.c_int32 * len(goals_by_priority))(*[g.kind for g in goals_by_priority])
+        results = (GoalResultStruct * len(goals_by_priority))()
+        o, keep = (options or OptimizationOptions()).to_struct()
+        c = self.constraint.to_struct()
+        import time
+        t0 = time.perf_counter()
+        cluster.lib.check(cluster.lib.lib.ccmi_optimizations(cluster.handle, kinds, len(goals_by_priority),
+                                                             C.byref(c), C.byref(o), results))
+        dt = time.perf_counter() - t0
+        grs = [GoalResult(GOAL_NAMES[r.goal_kind], bool(r.succeeded), bool(r.has_diff), r.seconds, r.candidates,
+                          r.device_candidates, r.device_launches, r.actions, stats_to_dict(r.stats)) for r in results]
+        return OptimizerResult(grs, cluster.proposals(), cluster.actions(), dt,
+                               [g.name for g in grs if not g.succeeded])
+
+
+def goals_from_names(names: Sequence[str], constraint: Optional[BalancingConstraint] = None) -> List[Goal]:
+    return [globals()[n](constraint=constraint) for n in names]

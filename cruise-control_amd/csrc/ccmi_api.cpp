@@ -1,0 +1,355 @@
+// C ABI of libccmi.so (include/ccmi.h). Exceptions never cross the boundary: every entry point maps them to a
+// ccmi_status and keeps the message for ccmi_last_error() (thread-local).
+#include <cstring>
+#include <memory>
+#include <mutex>
+#include <string>
+
+#include "ccmi.h"
+#include "engine/buffers.h"
+#include "engine/device.h"
+#include "engine/engine.h"
+#include "engine/model.h"
+
+namespace ccmi {
+ccmi_cluster_buffers* generateRandomCluster(const ccmi_random_cluster_props& p);
+}
+
+struct ccmi_session {
+  ccmi::Model model;
+  std::unique_ptr<ccmi::Device> device;
+  std::unique_ptr<ccmi::Engine> engine;
+  std::vector<int32_t> initDist, initLeaders;  // for ExecutionProposal diffs
+  struct Prop {
+    int32_t partition, size, oldLeader;
+    std::vector<int32_t> oldR, newR;
+  };
+  std::vector<Prop> proposals;
+};
+
+namespace {
+thread_local std::string g_err;
+
+ccmi_status fail(ccmi_status s, const std::string& msg) {
+  g_err = msg;
+  return s;
+}
+
+template <class F>
+ccmi_status guarded(F&& f) {
+  try {
+    return f();
+  } catch (ccmi::OptimizationFailure& e) {
+    return fail(CCMI_E_OPT_FAILURE, e.what());
+  } catch (ccmi::StateError& e) {
+    return fail(CCMI_E_STATE, e.what());
+  } catch (ccmi::Unsupported& e) {
+    return fail(CCMI_E_UNSUPPORTED, e.what());
+  } catch (std::invalid_argument& e) {
+    return fail(CCMI_E_INVALID, e.what());
+  } catch (std::exception& e) {
+    const std::string w = e.what();
+    return fail(w.rfind("HIP", 0) == 0 || w.find("gfx950") != std::string::npos || w.find("device") != std::string::npos
+                    ? CCMI_E_DEVICE
+                    : CCMI_E_INVALID,
+                w);
+  }
+}
+
+void setOptions(ccmi_session* s, const ccmi_balancing_constraint* c, const ccmi_opt_options* o) {
+  ccmi::Engine& e = *s->engine;
+  ccmi_balancing_constraint def;
+  ccmi_default_constraint(&def);
+  if (!c) c = &def;
+  for (int r = 0; r < 4; ++r) {
+    e.bc.resBalance[r] = c->resource_balance_percentage[r];
+    e.bc.capThreshold[r] = c->capacity_threshold[r];
+    e.bc.lowUtil[r] = c->low_utilization_threshold[r];
+  }
+  e.bc.replicaBalance = c->replica_balance_percentage;
+  e.bc.goalViolationMultiplier = c->goal_violation_distribution_threshold_multiplier;
+  const int B = s->model.B;
+  ccmi::Options opt;
+  opt.exclMove.assign(B, 0);
+  opt.exclLead.assign(B, 0);
+  opt.requested.assign(B, 0);
+  if (o) {
+    if (o->num_excluded_topics > 0) throw ccmi::Unsupported("excluded topics are outside ABI v1 scope");
+    if (o->num_excluded_brokers_for_leadership > 0)
+      throw ccmi::Unsupported("excluded brokers for leadership are outside ABI v1 scope");
+    if (o->num_excluded_brokers_for_replica_move > 0)
+      throw ccmi::Unsupported("excluded brokers for replica move are outside ABI v1 scope");
+    if (o->only_move_immigrant_replicas) throw ccmi::Unsupported("only_move_immigrant_replicas is outside ABI v1 scope");
+    for (int i = 0; i < o->num_requested_destination_broker_ids; ++i) {
+      const int b = o->requested_destination_broker_ids[i];
+      if (b < 0 || b >= B) throw std::invalid_argument("requested destination broker out of range");
+      opt.requested[b] = 1;
+      opt.anyRequested = true;
+    }
+    opt.triggered = o->triggered_by_goal_violation != 0;
+  }
+  if (s->model.numNew > 0) throw ccmi::Unsupported("NEW brokers are outside ABI v1 scope");
+  e.opt = std::move(opt);
+}
+
+std::vector<int32_t> replicaDist(const ccmi::Model& m) {
+  std::vector<int32_t> v(m.R);
+  for (int i = 0; i < m.R; ++i) v[i] = m.rBroker[m.pSlots[i]];
+  return v;
+}
+std::vector<int32_t> leaderDist(const ccmi::Model& m) {
+  std::vector<int32_t> v(m.P);
+  for (int p = 0; p < m.P; ++p) v[p] = m.rBroker[m.pLeader[p]];
+  return v;
+}
+
+void buildProposals(ccmi_session* s) {
+  const ccmi::Model& m = s->model;
+  s->proposals.clear();
+  const std::vector<int32_t> fin = replicaDist(m);
+  for (int p = 0; p < m.P; ++p) {
+    const int a = m.pOff[p], n = m.pOff[p + 1] - a;
+    std::vector<int32_t> oldR(s->initDist.begin() + a, s->initDist.begin() + a + n);
+    std::vector<int32_t> newR(fin.begin() + a, fin.begin() + a + n);
+    const int finalLeader = m.rBroker[m.pLeader[p]];
+    if (oldR == newR && s->initLeaders[p] == finalLeader) continue;
+    if (newR[0] != finalLeader) {
+      int pos = 0;
+      for (int k = 0; k < n; ++k)
+        if (newR[k] == finalLeader) pos = k;
+      newR[pos] = newR[0];
+      newR[0] = finalLeader;
+    }
+    s->proposals.push_back({p, (int32_t)m.ru(m.pLeader[p], ccmi::R_DISK), s->initLeaders[p], oldR, newR});
+  }
+}
+}  // namespace
+
+extern "C" {
+
+const char* ccmi_last_error(void) { return g_err.c_str(); }
+int32_t ccmi_abi_version(void) { return CCMI_ABI_VERSION; }
+
+void ccmi_default_constraint(ccmi_balancing_constraint* c) {
+  std::memset(c, 0, sizeof(*c));
+  for (int r = 0; r < 4; ++r) {
+    c->resource_balance_percentage[r] = 1.10;
+    c->capacity_threshold[r] = r == CCMI_CPU ? 0.7 : 0.8;
+    c->low_utilization_threshold[r] = 0.0;
+  }
+  c->replica_balance_percentage = 1.10;
+  c->leader_replica_balance_percentage = 1.10;
+  c->topic_replica_balance_percentage = 3.00;
+  c->topic_replica_balance_min_gap = 2;
+  c->topic_replica_balance_max_gap = 40;
+  c->goal_violation_distribution_threshold_multiplier = 1.0;
+  c->max_replicas_per_broker = 10000;
+  c->overprovisioned_max_replicas_per_broker = 1500;
+  c->overprovisioned_min_brokers = 3;
+}
+
+void ccmi_default_random_cluster_props(ccmi_random_cluster_props* p) {
+  std::memset(p, 0, sizeof(*p));
+  p->num_racks = 10;
+  p->num_brokers = 40;
+  p->num_replicas = 50001;
+  p->num_topics = 3000;
+  p->min_replication = 3;
+  p->max_replication = 3;
+  p->mean_cpu = 0.01;
+  p->mean_disk = 100.0;
+  p->mean_nw_in = 100.0;
+  p->mean_nw_out = 100.0;
+  p->distribution = 0;
+  p->rack_aware = 0;
+  p->leader_in_first_position = 1;
+}
+
+ccmi_status ccmi_random_cluster(const ccmi_random_cluster_props* props, ccmi_cluster_buffers** out) {
+  return guarded([&] {
+    if (!props || !out) throw std::invalid_argument("null argument");
+    *out = ccmi::generateRandomCluster(*props);
+    return CCMI_OK;
+  });
+}
+const ccmi_cluster_desc* ccmi_cluster_buffers_desc(const ccmi_cluster_buffers* buf) { return buf ? &buf->desc : nullptr; }
+void ccmi_cluster_buffers_free(ccmi_cluster_buffers* buf) { delete buf; }
+
+ccmi_status ccmi_session_create(int32_t device_ordinal, const ccmi_cluster_desc* desc, ccmi_session** out) {
+  return guarded([&] {
+    if (!desc || !out) throw std::invalid_argument("null argument");
+    auto s = std::make_unique<ccmi_session>();
+    s->model.build(*desc);
+    ccmi::Model& m = s->model;
+    s->device = std::make_unique<ccmi::Device>(device_ordinal, m.B, m.R, m.P, m.T, ccmi::kMaxGoals);
+    // device layout: resource-major broker/replica columns
+    std::vector<double> capRM((size_t)4 * m.B), utilRM((size_t)4 * m.B), rutilRM((size_t)4 * m.R), pot(m.B);
+    std::vector<int32_t> nrep(m.B), pBrokers(m.R);
+    std::vector<uint8_t> alive(m.B), flags(m.R);
+    for (int b = 0; b < m.B; ++b) {
+      for (int k = 0; k < 4; ++k) {
+        capRM[(size_t)k * m.B + b] = m.cap(b, k);
+        utilRM[(size_t)k * m.B + b] = m.bu(b, k);
+      }
+      nrep[b] = m.nrep(b);
+      alive[b] = m.alive(b);
+      pot[b] = m.ops.util(m.bPot[b], ccmi::R_NW_OUT);
+    }
+    for (int r = 0; r < m.R; ++r) {
+      for (int k = 0; k < 4; ++k) rutilRM[(size_t)k * m.R + r] = m.ru(r, k);
+      flags[r] = (m.rLeader[r] ? ccmi::RF_LEADER : 0) | (m.rOrigOff[r] ? ccmi::RF_ORIG_OFFLINE : 0);
+    }
+    for (int i = 0; i < m.R; ++i) pBrokers[i] = m.rBroker[m.pSlots[i]];
+    s->device->uploadStatic(capRM.data(), m.rPart.data(), m.rOrig.data(), m.pOff.data(), m.topicNrep.data());
+    s->device->uploadDynamic(utilRM.data(), nrep.data(), m.bNlead.data(), pot.data(), alive.data(), rutilRM.data(),
+                             m.rBroker.data(), flags.data(), pBrokers.data(), m.topicCountDense.data());
+    m.topicCountDense.clear();
+    m.topicCountDense.shrink_to_fit();
+    m.dev = s->device.get();
+    s->engine = std::make_unique<ccmi::Engine>(m, s->device.get());
+    s->initDist = replicaDist(m);
+    s->initLeaders = leaderDist(m);
+    *out = s.release();
+    return CCMI_OK;
+  });
+}
+
+ccmi_status ccmi_session_destroy(ccmi_session* s) {
+  return guarded([&] {
+    delete s;
+    return CCMI_OK;
+  });
+}
+
+ccmi_status ccmi_goal_optimize(ccmi_session* s, int32_t goal_kind, const ccmi_balancing_constraint* c,
+                               const ccmi_opt_options* o, ccmi_goal_result* result) {
+  return guarded([&] {
+    if (!s) throw std::invalid_argument("null session");
+    setOptions(s, c, o);
+    auto g = ccmi::makeGoal(goal_kind);
+    ccmi_goal_result tmp;
+    std::memset(&tmp, 0, sizeof(tmp));
+    const std::vector<int32_t> pre = replicaDist(s->model), preL = leaderDist(s->model);
+    s->engine->optimizeGoal(std::move(g), &tmp);
+    tmp.has_diff = (replicaDist(s->model) != pre || leaderDist(s->model) != preL) ? 1 : 0;
+    if (result) *result = tmp;
+    buildProposals(s);
+    return CCMI_OK;
+  });
+}
+
+ccmi_status ccmi_optimizations(ccmi_session* s, const int32_t* goal_kinds, int32_t n_goals,
+                               const ccmi_balancing_constraint* c, const ccmi_opt_options* o, ccmi_goal_result* results) {
+  return guarded([&] {
+    if (!s || (!goal_kinds && n_goals > 0)) throw std::invalid_argument("null argument");
+    if (n_goals <= 0) throw std::invalid_argument("At least one goal must be provided to get an optimization result.");
+    setOptions(s, c, o);
+    for (int i = 0; i < n_goals; ++i) (void)ccmi::makeGoal(goal_kinds[i]);  // fail fast on unsupported kinds
+    for (int i = 0; i < n_goals; ++i) {
+      ccmi_goal_result tmp;
+      std::memset(&tmp, 0, sizeof(tmp));
+      const std::vector<int32_t> pre = replicaDist(s->model), preL = leaderDist(s->model);
+      s->engine->optimizeGoal(ccmi::makeGoal(goal_kinds[i]), &tmp);
+      tmp.has_diff = (replicaDist(s->model) != pre || leaderDist(s->model) != preL) ? 1 : 0;
+      if (results) results[i] = tmp;
+    }
+    buildProposals(s);
+    return CCMI_OK;
+  });
+}
+
+ccmi_status ccmi_action_acceptance(ccmi_session* s, int32_t idx, const ccmi_action* a, int32_t* acceptance) {
+  return guarded([&] {
+    if (!s || !a || !acceptance) throw std::invalid_argument("null argument");
+    if (idx < 0 || idx >= (int)s->engine->optimized.size()) throw std::invalid_argument("optimized goal index out of range");
+    *acceptance = s->engine->acceptance(idx, *a);
+    return CCMI_OK;
+  });
+}
+
+ccmi_status ccmi_compute_cluster_stats(ccmi_session* s, const ccmi_balancing_constraint* c, const ccmi_opt_options* o,
+                                       ccmi_cluster_stats* out) {
+  return guarded([&] {
+    if (!s || !out) throw std::invalid_argument("null argument");
+    setOptions(s, c, o);
+    *out = s->engine->stats();
+    return CCMI_OK;
+  });
+}
+
+int64_t ccmi_action_log_count(const ccmi_session* s) { return s ? (int64_t)s->model.log.size() : 0; }
+
+ccmi_status ccmi_action_log_copy(const ccmi_session* s, int64_t first, int64_t count, ccmi_action* out) {
+  return guarded([&] {
+    if (!s || !out) throw std::invalid_argument("null argument");
+    if (first < 0 || count < 0 || first + count > (int64_t)s->model.log.size()) throw std::invalid_argument("range");
+    for (int64_t i = 0; i < count; ++i) {
+      const ccmi::ActionRec& a = s->model.log[first + i];
+      out[i] = {a.type, a.partition, a.src, a.dst, a.destPartition};
+    }
+    return CCMI_OK;
+  });
+}
+
+ccmi_status ccmi_replica_distribution(const ccmi_session* s, int32_t* out) {
+  return guarded([&] {
+    if (!s || !out) throw std::invalid_argument("null argument");
+    const auto v = replicaDist(s->model);
+    std::memcpy(out, v.data(), v.size() * sizeof(int32_t));
+    return CCMI_OK;
+  });
+}
+
+ccmi_status ccmi_leader_distribution(const ccmi_session* s, int32_t* out) {
+  return guarded([&] {
+    if (!s || !out) throw std::invalid_argument("null argument");
+    const auto v = leaderDist(s->model);
+    std::memcpy(out, v.data(), v.size() * sizeof(int32_t));
+    return CCMI_OK;
+  });
+}
+
+int64_t ccmi_proposal_count(const ccmi_session* s) { return s ? (int64_t)s->proposals.size() : 0; }
+
+ccmi_status ccmi_proposals(const ccmi_session* s, int32_t max_rf, int32_t* partition, int32_t* size,
+                           int32_t* old_leader, int32_t* old_out, int32_t* new_out) {
+  return guarded([&] {
+    if (!s) throw std::invalid_argument("null session");
+    for (size_t i = 0; i < s->proposals.size(); ++i) {
+      const auto& p = s->proposals[i];
+      partition[i] = p.partition;
+      size[i] = p.size;
+      old_leader[i] = p.oldLeader;
+      for (int k = 0; k < max_rf; ++k) {
+        old_out[i * max_rf + k] = k < (int)p.oldR.size() ? p.oldR[k] : -1;
+        new_out[i * max_rf + k] = k < (int)p.newR.size() ? p.newR[k] : -1;
+      }
+    }
+    return CCMI_OK;
+  });
+}
+
+ccmi_status ccmi_perf(const ccmi_session* s, ccmi_perf_counters* out) {
+  return guarded([&] {
+    if (!s || !out) throw std::invalid_argument("null argument");
+    const auto& p = s->device->perf;
+    out->scan_launches = p.scanLaunches;
+    out->scan_kernel_ms = p.scanKernelMs;
+    out->scan_bytes = p.scanBytes;
+    out->stats_launches = p.statsLaunches;
+    out->stats_kernel_ms = p.statsKernelMs;
+    out->stats_bytes = p.statsBytes;
+    out->host_syncs = p.syncs;
+    return CCMI_OK;
+  });
+}
+
+void ccmi_perf_reset(ccmi_session* s) {
+  if (s) s->device->perf = ccmi::DevicePerf();
+}
+
+void ccmi_set_kernel_timing(ccmi_session* s, int32_t enabled) {
+  if (s) s->device->timing = enabled != 0;
+}
+
+}  // extern "C"

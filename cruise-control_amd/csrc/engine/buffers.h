@@ -1,0 +1,18 @@
+// Owner of the arrays behind a generated ccmi_cluster_desc (ccmi_random_cluster / ccmi_cluster_buffers_free).
+#pragma once
+#include <string>
+#include <vector>
+
+#include "ccmi.h"
+
+struct ccmi_cluster_buffers {
+  ccmi_cluster_desc desc;
+  std::vector<int32_t> brokerId, brokerRack, brokerState;
+  std::vector<double> brokerCap;
+  std::vector<std::string> topicStr;
+  std::vector<const char*> topicPtr;
+  std::vector<int32_t> partTopic, partNumber, partOff, partReplicas;
+  std::vector<int32_t> repPart, repBroker;
+  std::vector<uint8_t> repLeader, repOffline;
+  std::vector<float> repLoad;
+};

@@ -1,0 +1,118 @@
+// Device-resident structure-of-arrays mirror of the cluster model, and the scan request formats.
+// Shared by host engine code and gfx950 kernels (plain POD, no HIP types).
+//
+// Layout in HBM (one session, B brokers, R replicas, P partitions, T topics):
+//   broker rows   bUtil[4][B] f64 (expected utilization, ModelUtils.expectedUtilizationFor),
+//                 bCap[4][B] f64, bNrep[B] i32, bNlead[B] i32, bPotNwOut[B] f64, bAlive[B] u8
+//   replica rows  rUtil[4][R] f64, rPart/rBroker/rOrig[R] i32, rFlags[R] u8 (bit0 leader, bit1 orig-offline)
+//   partitions    pOff[P+1] i32, pBrokers[R] i32 (current broker of every replica slot, Partition._replicas order)
+//   topics        topicCount[T][B] i32 (dense Broker._topicReplicas sizes, for ClusterModelStats topic stats)
+//   goal state    allowed[G][B] u8 (per optimized goal: _brokersAllowedReplicaMove, frozen at initGoalState)
+// Resource-major broker columns make a candidate row (consecutive destination brokers) a coalesced read.
+#pragma once
+#include <stdint.h>
+
+namespace ccmi {
+
+constexpr int kMaxGoals = 20;
+constexpr int kMaxRf = 8;
+
+enum DevGoalKind : int32_t { DG_REPLICA_DISTRIBUTION = 0, DG_RESOURCE_DISTRIBUTION = 1 };
+enum DevAction : int32_t { DA_MOVE = 0, DA_LEADERSHIP = 1, DA_SWAP = 2 };
+enum RFlag : uint8_t { RF_LEADER = 1, RF_ORIG_OFFLINE = 2 };
+
+// Frozen per-goal state needed by selfSatisfied/actionAcceptance (a goal's initGoalState output).
+struct DevGoal {
+  int32_t kind;
+  int32_t resource;
+  int32_t upper, lower;        // ReplicaDistributionAbstractGoal._balanceUpperLimit/_balanceLowerLimit
+  double upperThr, lowerThr;   // ResourceDistributionGoal._balanceUpperThreshold/_balanceLowerThreshold
+  int32_t fixOffline;          // _fixOfflineReplicasOnly
+  int32_t allowedSlot;         // row of DevTables.allowed
+};
+
+// goals[0] is the goal being optimized (selfSatisfied); goals[1..n) are the optimized goals in the order
+// AnalyzerUtils.isProposalAcceptableForOptimizedGoals visits them.
+struct DevProgram {
+  int32_t nGoals;
+  int32_t action;
+  DevGoal goals[kMaxGoals];
+};
+
+struct DevTables {
+  const double* bUtil;
+  const double* bCap;
+  const int32_t* bNrep;
+  const uint8_t* bAlive;
+  const uint8_t* allowed;
+  const double* rUtil;
+  const int32_t* rPart;
+  const int32_t* rBroker;
+  const int32_t* rOrig;
+  const uint8_t* rFlags;
+  const int32_t* pOff;
+  const int32_t* pBrokers;
+  int32_t B, R, P;
+};
+
+// Row updates the host flushes to the device before a scan (only rows touched since the last flush).
+struct BrokerRow {
+  int32_t b, nrep, nlead, alive;
+  double util[4];
+  double potNwOut;
+  double pad;
+};
+struct ReplicaRow {
+  int32_t r, broker, flags, pad;
+  double util[4];
+};
+struct PartitionRow {
+  int32_t p, n;
+  int32_t brokers[kMaxRf];
+};
+struct TopicCountDelta {
+  int32_t topic, broker, delta, pad;
+};
+
+// Scan request modes.
+//   CROSS : pairs (replicas[k], cands[j]) in k-major order; key = k * N + j
+//   SWAP  : rows (m, s) = (candidate broker segment m, source replica s); a row's candidates are
+//           cbRep[cbOff[m] .. cbOff[m+1]); key = ((m * S + s) << 24) | j of the row's FIRST terminal j,
+//           kept only when that terminal is an ACCEPT (AbstractGoal.maybeApplySwapAction semantics).
+enum ScanMode : int32_t { SM_CROSS = 0, SM_SWAP = 1 };
+
+struct ScanHeader {
+  int32_t mode;
+  int32_t K;     // CROSS: number of replicas; SWAP: number of source replicas S
+  int32_t N;     // CROSS: number of candidates; SWAP: number of segments M
+  int32_t nCand; // SWAP: total candidate replicas
+};
+
+// ClusterModelStats reduction (kernels/stats.hip)
+struct TopicPartial {
+  double avg, sd;
+  int32_t mx, mn;
+};
+struct StatsParams {
+  int32_t B, T;
+  int32_t numAllowed;
+  double clusterUtil[4];
+  double avgPct[4];
+  double upperThr[4], lowerThr[4];
+  double potCapacity;  // capacityWithAllowedReplicaMovesFor(NW_OUT)
+  double nwOutCapThreshold;
+};
+struct StatsOut {
+  double resAvg[4], resMax[4], resMin[4], resStd[4];
+  int32_t numBalanced[4];
+  double pnwAvg, pnwMax, pnwMin, pnwStd;
+  int32_t numUnderPot;
+  double repAvg, repStd;
+  int32_t repMax, repMin;
+  double leadAvg, leadStd;
+  int32_t leadMax, leadMin;
+  double topicAvg, topicStd;
+  int32_t topicMax, topicMin;
+};
+
+}  // namespace ccmi

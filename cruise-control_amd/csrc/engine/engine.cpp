@@ -1,0 +1,861 @@
+// Engine: goal drivers with device-batched candidate scans (see engine.h for the reference map).
+#include "engine.h"
+
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstring>
+
+#include "device.h"
+#include "predicates.h"
+
+namespace ccmi {
+
+namespace {
+
+constexpr double kBalanceMargin = 0.9;  // ResourceDistributionGoal.BALANCE_MARGIN / ReplicaDistributionAbstractGoal
+
+// Host view of the model for predicates.h (same expressions the kernels evaluate).
+struct HostView {
+  const Model& m;
+  const std::vector<const std::vector<uint8_t>*>& allowedBySlot;
+  double bu(int b, int res) const { return m.bu(b, res); }
+  double bcap(int b, int res) const { return m.cap(b, res); }
+  int nrep(int b) const { return m.nrep(b); }
+  bool alive(int b) const { return m.alive(b); }
+  bool allowed(int slot, int b) const { return (*allowedBySlot[slot])[b] != 0; }
+  double ru(int r, int res) const { return m.ru(r, res); }
+  int flags(int r) const { return (m.rLeader[r] ? RF_LEADER : 0) | (m.rOrigOff[r] ? RF_ORIG_OFFLINE : 0); }
+  int rbroker(int r) const { return m.rBroker[r]; }
+  int rorig(int r) const { return m.rOrig[r]; }
+  int rpart(int r) const { return m.rPart[r]; }
+  int pbegin(int p) const { return m.pOff[p]; }
+  int pend(int p) const { return m.pOff[p + 1]; }
+  int pbroker(int i) const { return m.rBroker[m.pSlots[i]]; }
+};
+
+Model::Spec makeSpec() { return Model::Spec(); }
+
+}  // namespace
+
+std::vector<int> GoalImpl::brokersToBalance(Engine& e) {
+  std::vector<int> v(e.m.B);
+  for (int b = 0; b < e.m.B; ++b) v[b] = b;
+  return v;
+}
+
+// GoalUtils.computeResourceUtilizationBalanceThreshold (GoalUtils.java:550-602)
+double Engine::threshold(double avgPct, int res, bool lower) const {
+  const bool low = avgPct <= bc.lowUtil[res];
+  double bp = bc.resBalance[res];
+  if (opt.triggered) bp *= bc.goalViolationMultiplier;
+  const double margin = (bp - 1) * kBalanceMargin;
+  if (lower) return low ? 0.0 : avgPct * jmax(0, (1 - margin));
+  const double t = avgPct * (1 + margin);
+  return low ? jmax(t, bc.lowUtil[res] * kBalanceMargin) : t;
+}
+
+DevProgram Engine::program(const GoalImpl& self, int action) const {
+  DevProgram p;
+  std::memset(&p, 0, sizeof(p));
+  p.action = action;
+  p.nGoals = 1 + (int)optimized.size();
+  if (p.nGoals > kMaxGoals) throw Unsupported("too many goals in one chain");
+  p.goals[0] = self.dg;
+  for (size_t i = 0; i < optimized.size(); ++i) p.goals[i + 1] = optimized[i]->dg;
+  return p;
+}
+
+// GoalUtils.eligibleBrokers for the replica-independent option subset of ABI v1.
+void Engine::eligible(const std::vector<int32_t>& in, int action, std::vector<int32_t>& out) const {
+  out.clear();
+  for (int b : in) {
+    if (opt.anyRequested) {
+      if (action != DA_LEADERSHIP && !opt.requested[b]) continue;
+    } else if (opt.anyExclMove && action == DA_MOVE && opt.exclMove[b]) {
+      continue;
+    }
+    out.push_back(b);
+  }
+}
+
+int64_t Engine::crossScan(GoalImpl& self, int action, const std::vector<int32_t>& reps, size_t r0,
+                          const std::vector<int32_t>& cands) {
+  const int K = (int)(reps.size() - r0), N = (int)cands.size();
+  if (K <= 0) return -1;
+  if (N == 0) return -1;  // every replica visits an empty eligible list
+  m.flushToDevice();
+  const int64_t key = dev->scanCross(program(self, action), reps.data() + r0, K, cands.data(), N);
+  candidates += key >= 0 ? key + 1 : (int64_t)K * N;
+  return key;
+}
+
+int64_t Engine::pairScan(GoalImpl& self, const std::vector<int32_t>& pr, const std::vector<int32_t>& pb) {
+  if (pr.empty()) return -1;
+  m.flushToDevice();
+  const int64_t key = dev->scanPairs(program(self, DA_LEADERSHIP), pr.data(), pb.data(), (int)pr.size());
+  candidates += key >= 0 ? key + 1 : (int64_t)pr.size();
+  return key;
+}
+
+int64_t Engine::swapScan(GoalImpl& self, const std::vector<int32_t>& srcs, const std::vector<int32_t>& cbOff,
+                         const std::vector<int32_t>& cbRep) {
+  if (srcs.empty() || cbRep.empty()) return -1;
+  m.flushToDevice();
+  int64_t visited = 0;
+  const int64_t key = dev->scanSwap(program(self, DA_SWAP), srcs.data(), (int)srcs.size(), cbOff.data(),
+                                    (int)cbOff.size() - 1, cbRep.data(), (int)cbRep.size(), &visited);
+  candidates += visited;
+  return key;
+}
+
+int Engine::acceptance(int gi, const ccmi_action& a) {
+  std::vector<const std::vector<uint8_t>*> allowedBySlot;
+  for (auto& g : optimized) allowedBySlot.push_back(&g->allowed);
+  HostView v{m, allowedBySlot};
+  const GoalImpl& g = *optimized.at(gi);
+  const int sr = m.replicaOn(a.partition, a.source_broker);
+  if (sr < 0) throw std::invalid_argument("no replica of the partition on the source broker");
+  if (a.type == CCMI_INTER_BROKER_REPLICA_SWAP) {
+    const int dr = m.replicaOn(a.destination_partition, a.destination_broker);
+    if (dr < 0) throw std::invalid_argument("no replica of the destination partition on the destination broker");
+    return goalAcceptSwap(g.dg, v, sr, a.source_broker, dr, a.destination_broker);
+  }
+  const int action = a.type == CCMI_LEADERSHIP_MOVEMENT ? DA_LEADERSHIP : DA_MOVE;
+  if (a.type != CCMI_INTER_BROKER_REPLICA_MOVEMENT && a.type != CCMI_LEADERSHIP_MOVEMENT)
+    throw std::invalid_argument("Unsupported balancing action");
+  return goalAcceptMove(g.dg, v, action, sr, a.source_broker, a.destination_broker) ? CCMI_ACCEPT : CCMI_REPLICA_REJECT;
+}
+
+ccmi_cluster_stats Engine::stats() {
+  m.flushToDevice();
+  const int ldB = dev->ldB();
+  std::vector<uint8_t> aa(ldB, 0);
+  int na = 0;
+  for (int b = 0; b < m.B; ++b)
+    if (m.alive(b) && !(opt.anyExclMove && opt.exclMove[b])) {
+      aa[b] = 1;
+      na++;
+    }
+  StatsParams P;
+  std::memset(&P, 0, sizeof(P));
+  P.B = m.B;
+  P.T = m.T;
+  P.numAllowed = na;
+  for (int res = 0; res < 4; ++res) {
+    P.clusterUtil[res] = m.clusterUtil(res);
+    P.avgPct[res] = P.clusterUtil[res] / m.capacityWithAllowedReplicaMoves(res, opt.exclMove);
+    P.upperThr[res] = threshold(P.avgPct[res], res, false);
+    P.lowerThr[res] = threshold(P.avgPct[res], res, true);
+  }
+  P.potCapacity = m.capacityWithAllowedReplicaMoves(R_NW_OUT, opt.exclMove);
+  P.nwOutCapThreshold = bc.capThreshold[R_NW_OUT];
+  StatsOut o;
+  dev->stats(P, aa.data(), &o);
+  ccmi_cluster_stats s;
+  std::memset(&s, 0, sizeof(s));
+  for (int r = 0; r < 4; ++r) {
+    s.resource_avg[r] = o.resAvg[r];
+    s.resource_max[r] = o.resMax[r];
+    s.resource_min[r] = o.resMin[r];
+    s.resource_std[r] = o.resStd[r];
+    s.num_balanced_brokers_by_resource[r] = o.numBalanced[r];
+  }
+  s.potential_nw_out_avg = o.pnwAvg;
+  s.potential_nw_out_max = o.pnwMax;
+  s.potential_nw_out_min = o.pnwMin;
+  s.potential_nw_out_std = o.pnwStd;
+  s.num_brokers_under_potential_nw_out = o.numUnderPot;
+  s.replica_avg = o.repAvg;
+  s.replica_std = o.repStd;
+  s.replica_max = o.repMax;
+  s.replica_min = o.repMin;
+  s.leader_avg = o.leadAvg;
+  s.leader_std = o.leadStd;
+  s.leader_max = o.leadMax;
+  s.leader_min = o.leadMin;
+  s.topic_replica_avg = o.topicAvg;
+  s.topic_replica_std = o.topicStd;
+  s.topic_replica_max = o.topicMax;
+  s.topic_replica_min = o.topicMin;
+  s.num_brokers = m.B;
+  s.num_replicas_in_cluster = m.R;
+  s.num_topics = m.T;
+  {
+    std::vector<uint8_t> seen(m.P, 0);
+    int n = 0;
+    for (int r = 0; r < m.R; ++r)
+      if (m.selfHealing[r] && !seen[m.rPart[r]]) {
+        seen[m.rPart[r]] = 1;
+        n++;
+      }
+    s.num_partitions_with_offline_replicas = n;
+  }
+  return s;
+}
+
+// AbstractGoal.optimize (AbstractGoal.java:81-135) + the per-goal bookkeeping of GoalOptimizer.optimizations
+bool Engine::optimizeGoal(std::unique_ptr<GoalImpl> g, ccmi_goal_result* res) {
+  using clk = std::chrono::steady_clock;
+  const auto t0 = clk::now();
+  const int64_t c0 = candidates;
+  const size_t a0 = m.log.size();
+  const int64_t l0 = dev->perf.scanLaunches, p0 = dev->perf.scanPairs;
+  struct Clear {
+    Model& m;
+    ~Clear() { m.clearTracked(); }
+  } guard{m};
+  g->succeeded = true;
+  const ccmi_cluster_stats before = stats();
+  g->finished = false;
+  g->dg.allowedSlot = (int)optimized.size();
+  g->init(*this);
+  dev->setAllowed(g->dg.allowedSlot, g->allowed.data());
+  const bool brokenEmpty = m.numDead == 0 && m.numBadDisk == 0;
+  bool exclWithReplicas = false;
+  for (int b = 0; b < m.B; ++b)
+    if (m.alive(b) && opt.anyExclMove && opt.exclMove[b] && m.nrep(b) > 0) exclWithReplicas = true;
+  while (!g->finished) {
+    for (int b : g->brokersToBalance(*this)) g->rebalance(*this, b);
+    g->update(*this);
+  }
+  const ccmi_cluster_stats after = stats();
+  if (brokenEmpty && !exclWithReplicas && g->compareStats(after, before) < 0)
+    throw StateError("Optimization for goal " + g->name + " failed because the optimized result is worse than before.");
+  const bool ok = g->succeeded;
+  if (res) {
+    res->goal_kind = g->kind;
+    res->succeeded = ok ? 1 : 0;
+    res->candidates = candidates - c0;
+    res->actions = (int64_t)(m.log.size() - a0);
+    res->device_launches = dev->perf.scanLaunches - l0;
+    res->device_candidates = dev->perf.scanPairs - p0;
+  }
+  m.clearTracked();
+  optimized.push_back(std::move(g));
+  if (res) {
+    res->stats = stats();  // GoalOptimizer.statsByGoalPriority
+    res->seconds = std::chrono::duration<double>(clk::now() - t0).count();
+  }
+  return ok;
+}
+
+// ======================================================================================= ReplicaDistributionGoal
+namespace {
+
+class ReplicaDistribution : public GoalImpl {
+ public:
+  ReplicaDistribution() {
+    kind = CCMI_GOAL_REPLICA_DISTRIBUTION;
+    name = "ReplicaDistributionGoal";
+  }
+  static constexpr int kName = 4 * CCMI_GOAL_REPLICA_DISTRIBUTION;
+  int upper = 0, lower = 0;
+  bool anyAbove = false, anyUnder = false;
+
+  bool excluded(int b) const { return !allowed[b]; }
+
+  // ReplicaDistributionAbstractGoal.initGoalState + ReplicaDistributionGoal.initGoalState
+  void init(Engine& e) override {
+    Model& m = e.m;
+    allowed.assign(m.B, 0);
+    int n = 0;
+    for (int b = 0; b < m.B; ++b)
+      if (m.alive(b) && !(e.opt.anyExclMove && e.opt.exclMove[b])) {
+        allowed[b] = 1;
+        n++;
+      }
+    if (n == 0) throw OptimizationFailure("[" + name + "] All alive brokers are excluded from replica moves.");
+    const double avg = m.R / (double)n;
+    const double adj = (e.bc.replicaBalance - 1) * kBalanceMargin;
+    upper = (int)std::ceil(avg * (1 + adj));
+    lower = (int)std::floor(avg * jmax(0, (1 - adj)));
+    dg = DevGoal{};
+    dg.kind = DG_REPLICA_DISTRIBUTION;
+    dg.upper = upper;
+    dg.lower = lower;
+    dg.fixOffline = 0;
+    dg.allowedSlot = (int)e.optimized.size();
+    const bool selfHealing = m.numSelfHealing > 0;
+    for (int b = 0; b < m.B; ++b) {
+      Model::Spec s;
+      s.selImmigrants = e.opt.onlyImmigrants;
+      s.selImmOrOffline = selfHealing && m.alive(b);
+      s.prioOffline = selfHealing;
+      s.prioImmigrants = !e.opt.onlyImmigrants;
+      s.scoreRes = R_DISK;
+      s.scoreReverse = false;
+      m.track(b, kName, s);
+    }
+  }
+
+  void update(Engine& e) override {
+    if (anyAbove) succeeded = false;
+    if (anyUnder) succeeded = false;
+    anyAbove = anyUnder = false;
+    Model& m = e.m;
+    for (int r = 0; r < m.R; ++r)
+      if (m.selfHealing[r] && m.curOffline(r)) {
+        if (dg.fixOffline) throw OptimizationFailure("[" + name + "] Cannot remove offline replicas.");
+        dg.fixOffline = 1;
+        return;
+      }
+    finished = true;
+  }
+
+  int compareStats(const ccmi_cluster_stats& after, const ccmi_cluster_stats& before) const override {
+    const double d1 = after.replica_std, d2 = before.replica_std;
+    if (d1 - d2 > 1e-5) return -1;
+    if (d2 - d1 > 1e-5) return 1;
+    return 0;
+  }
+
+  // ReplicaDistributionGoal.rebalanceForBroker (:181-224)
+  void rebalance(Engine& e, int b) override {
+    Model& m = e.m;
+    const int n = m.nrep(b), off = m.bNoff[b];
+    const bool excl = excluded(b);
+    const bool less = off > 0 || n > upper || excl;
+    const bool more = !excl && m.alive(b) && n - off < lower;
+    if (m.alive(b) && !more && !less) return;
+    if (m.numNew > 0 && !m.isNew(b) && !less) return;
+    if (((m.numSelfHealing > 0 && m.bNoff[b] == 0) || e.opt.onlyImmigrants) && less && m.bNimm[b] == 0) return;
+    if (less && moveOut(e, b)) anyAbove = true;
+    if (more && moveIn(e, b)) anyUnder = true;
+  }
+
+  // rebalanceByMovingReplicasOut (:226-276): batches = runs of equal offline status
+  bool moveOut(Engine& e, int b) {
+    Model& m = e.m;
+    const bool fix = dg.fixOffline != 0;
+    auto cmp = [&m](int x, int y) {
+      const int c = jcmpInt(m.nrep(x), m.nrep(y));
+      return c ? c : jcmpInt(m.bId[x], m.bId[y]);
+    };
+    RbTreeSet<decltype(cmp)> cand(cmp);
+    {
+      std::vector<int> ins, order;
+      for (int x = 0; x < m.B; ++x)
+        if (m.alive(x) && (fix || m.nrep(x) < upper)) ins.push_back(x);
+      if (fix) order = ins;
+      else javaHashSetOrder(ins, order);  // Collectors.toSet()
+      for (int x : order) cand.add(x);
+    }
+    const int upperSrc = excluded(b) ? 0 : upper;
+    bool wasUnable = false;
+    const std::vector<int32_t> list = m.sorted(b, kName);  // sortedReplicas(true): a clone
+    std::vector<int32_t> inorder, cands, batch;
+    size_t i = 0;
+    while (i < list.size()) {
+      if (!m.curOffline(list[i]) && wasUnable && m.nrep(b) <= upperSrc) return false;
+      const bool runOffline = m.curOffline(list[i]);
+      size_t e2 = i;
+      while (e2 < list.size() && m.curOffline(list[e2]) == runOffline) ++e2;
+      batch.assign(list.begin() + i, list.begin() + e2);
+      cand.inorder(inorder);
+      e.eligible(inorder, DA_MOVE, cands);
+      const int64_t key = e.crossScan(*this, DA_MOVE, batch, 0, cands);
+      if (key < 0) {
+        if (runOffline) wasUnable = true;
+        i = e2;
+        continue;
+      }
+      const int N = (int)cands.size();
+      const int k = (int)(key / N), j = (int)(key % N);
+      if (runOffline && k > 0) wasUnable = true;
+      const int r = batch[k], dst = cands[j];
+      m.relocateReplica(m.rPart[r], b, dst);
+      if (m.nrep(b) <= (m.bNoff[b] == 0 ? upperSrc : 0)) return false;
+      cand.remove(dst);
+      if (m.nrep(dst) < upper || fix) cand.add(dst);
+      i = i + k + 1;
+    }
+    return m.nrep(b) != 0;
+  }
+
+  // rebalanceByMovingReplicasIn (:278-340): speculative multi-source batches over the source queue
+  bool moveIn(Engine& e, int dest) {
+    Model& m = e.m;
+    auto cmp = [&m](int b1, int b2) {
+      const int r = jcmpInt(m.bNoff[b2], m.bNoff[b1]);
+      if (r == 0) {
+        const int r2 = jcmpInt(m.nrep(b2), m.nrep(b1));
+        return r2 == 0 ? jcmpInt(m.bId[b1], m.bId[b2]) : r2;
+      }
+      return r;
+    };
+    JavaPQ<decltype(cmp)> pq(cmp);
+    if (dg.fixOffline) {
+      for (int s = 0; s < m.B; ++s)
+        if (s != dest) pq.add(s);
+    } else {
+      for (int s = 0; s < m.B; ++s)
+        if (m.nrep(s) > lower || m.bNoff[s] > 0 || excluded(s)) pq.add(s);
+    }
+    std::vector<int32_t> single{dest}, cands;
+    e.eligible(single, DA_MOVE, cands);
+    if (cands.empty()) return true;  // every replica visits an empty candidate list
+    struct Seg {
+      int src;
+      std::vector<int32_t> list;  // clone of the source's sorted replicas
+      size_t start;
+    };
+    std::vector<Seg> segs;
+    std::vector<int32_t> flat;
+    size_t target = 256;
+    bool haveCur = false;
+    Seg cur;
+    while (haveCur || !pq.empty()) {
+      segs.clear();
+      flat.clear();
+      if (haveCur) {  // the source being iterated continues first (its clone, after the winner)
+        segs.push_back(std::move(cur));
+        haveCur = false;
+        flat.insert(flat.end(), segs.back().list.begin() + segs.back().start, segs.back().list.end());
+      }
+      while (!pq.empty() && (segs.empty() || flat.size() < target)) {
+        const int s = pq.poll();
+        segs.push_back({s, m.sorted(s, kName), 0});
+        flat.insert(flat.end(), segs.back().list.begin(), segs.back().list.end());
+      }
+      const int64_t key = e.crossScan(*this, DA_MOVE, flat, 0, cands);
+      if (key < 0) {
+        target = std::min<size_t>(target * 2, 1 << 16);
+        continue;  // all segments exhausted; sources are not re-enqueued
+      }
+      target = 256;
+      size_t q = (size_t)key, mIdx = 0;
+      while (q >= segs[mIdx].list.size() - segs[mIdx].start) {
+        q -= segs[mIdx].list.size() - segs[mIdx].start;
+        ++mIdx;
+      }
+      Seg& hit = segs[mIdx];
+      const size_t idx = hit.start + q;
+      const int r = hit.list[idx];
+      m.relocateReplica(m.rPart[r], hit.src, dest);
+      if (m.nrep(dest) >= lower) return false;
+      for (size_t t = mIdx + 1; t < segs.size(); ++t) pq.add(segs[t].src);  // un-poll speculative sources
+      bool requeued = false;
+      if (!pq.empty()) {
+        const int top = pq.peek();
+        const int res = jcmpInt(m.bNoff[hit.src], m.bNoff[top]);
+        if (res == -1 || (res == 0 && m.nrep(hit.src) < m.nrep(top))) {
+          pq.add(hit.src);
+          requeued = true;
+        }
+      }
+      if (!requeued && idx + 1 < hit.list.size()) {
+        cur = std::move(hit);
+        cur.start = idx + 1;
+        haveCur = true;
+      }
+    }
+    return true;
+  }
+};
+
+// ======================================================================================= ResourceDistributionGoal
+class ResourceDistribution : public GoalImpl {
+ public:
+  explicit ResourceDistribution(int kindIn) {
+    kind = kindIn;
+    switch (kindIn) {
+      case CCMI_GOAL_CPU_USAGE_DISTRIBUTION: res = R_CPU; name = "CpuUsageDistributionGoal"; break;
+      case CCMI_GOAL_NW_IN_USAGE_DISTRIBUTION: res = R_NW_IN; name = "NetworkInboundUsageDistributionGoal"; break;
+      case CCMI_GOAL_NW_OUT_USAGE_DISTRIBUTION: res = R_NW_OUT; name = "NetworkOutboundUsageDistributionGoal"; break;
+      default: res = R_DISK; name = "DiskUsageDistributionGoal"; break;
+    }
+  }
+  int res = 0;
+  double upperThr = 0, lowerThr = 0;
+  bool fix = false;
+  int nameBase() const { return 4 * kind; }
+  int nameId(bool reverse, bool leader) const { return nameBase() + (reverse ? 1 : 0) + (leader ? 2 : 0); }
+  bool excluded(int b) const { return !allowed[b]; }
+
+  // isLoadAboveBalanceLowerLimit / isLoadUnderBalanceUpperLimit with a null load
+  bool aboveLower(const Model& m, int b) const { return m.bu(b, res) + 0 >= m.cap(b, res) * lowerThr; }
+  bool underUpper(const Model& m, int b, double thr) const { return m.bu(b, res) - 0 <= m.cap(b, res) * thr; }
+  int cmpBroker(const Model& m, int x, int y) const {
+    const int c = jcmpDouble(m.pct(x, res), m.pct(y, res));
+    return c ? c : jcmpInt(m.bId[x], m.bId[y]);
+  }
+
+  std::vector<int> brokersToBalance(Engine& e) override {
+    if (e.m.numNew == 0) return GoalImpl::brokersToBalance(e);
+    std::vector<int> v;
+    for (int b = 0; b < e.m.B; ++b)
+      if (e.m.isNew(b)) v.push_back(b);
+    return v;
+  }
+
+  // initGoalState (:234-278)
+  void init(Engine& e) override {
+    Model& m = e.m;
+    allowed.assign(m.B, 0);
+    int n = 0;
+    for (int b = 0; b < m.B; ++b)
+      if (m.alive(b) && !(e.opt.anyExclMove && e.opt.exclMove[b])) {
+        allowed[b] = 1;
+        n++;
+      }
+    if (n == 0) throw OptimizationFailure("[" + name + "] All alive brokers are excluded from replica moves.");
+    fix = false;
+    const double util = m.clusterUtil(res);
+    const double capacity = m.capacityWithAllowedReplicaMoves(res, e.opt.exclMove);
+    const double avgPct = util / capacity;
+    upperThr = e.threshold(avgPct, res, false);
+    lowerThr = e.threshold(avgPct, res, true);
+    dg = DevGoal{};
+    dg.kind = DG_RESOURCE_DISTRIBUTION;
+    dg.resource = res;
+    dg.upperThr = upperThr;
+    dg.lowerThr = lowerThr;
+    dg.fixOffline = 0;
+    dg.allowedSlot = (int)e.optimized.size();
+  }
+
+  // updateGoalState (:301-349)
+  void update(Engine& e) override {
+    Model& m = e.m;
+    for (int b = 0; b < m.B; ++b) {
+      if (!m.alive(b)) continue;
+      if (!underUpper(m, b, upperThr)) succeeded = false;
+      if (!excluded(b) && !aboveLower(m, b)) succeeded = false;
+    }
+    for (int r = 0; r < m.R; ++r)
+      if (m.selfHealing[r] && m.curOffline(r)) {
+        if (fix) throw OptimizationFailure("[" + name + "] Cannot remove offline replicas.");
+        fix = true;
+        dg.fixOffline = 1;
+        return;
+      }
+    finished = true;
+  }
+
+  int compareStats(const ccmi_cluster_stats& after, const ccmi_cluster_stats& before) const override {
+    const int n1 = after.num_balanced_brokers_by_resource[res], n2 = before.num_balanced_brokers_by_resource[res];
+    if (n2 > n1 && jcmpDouble(before.resource_std[res], after.resource_std[res]) < 0) return -1;
+    return 1;
+  }
+
+  // rebalanceForBroker (:379-435)
+  void rebalance(Engine& e, int b) override {
+    Model& m = e.m;
+    const int off = m.bNoff[b];
+    const bool excl = excluded(b);
+    bool less = off > 0 || excl || !underUpper(m, b, upperThr);
+    bool more = !excl && !aboveLower(m, b);
+    bool immOnly = false;
+    if (m.bNoff[b] == 0) {
+      if (!more && !less) return;
+      immOnly = m.numSelfHealing > 0 || e.opt.onlyImmigrants;
+      if (immOnly && less && m.bNimm[b] == 0) return;
+    }
+    if ((res == R_NW_OUT || res == R_CPU) && !(fix && m.bNoff[b] > 0)) {
+      if (less && !moveOut(e, b, DA_LEADERSHIP)) less = false;
+      if (more && !moveIn(e, b, DA_LEADERSHIP, false)) more = false;
+    }
+    bool unbalanced = false;
+    if (less && moveOut(e, b, DA_MOVE)) unbalanced = swapOut(e, b, immOnly);
+    if (more && moveIn(e, b, DA_MOVE, immOnly)) unbalanced = unbalanced || swapIn(e, b, immOnly);
+  }
+
+  // sortedCandidateReplicas (:543-569)
+  int trackCandidates(Engine& e, int b, double limit, bool asc, bool followersOnly, bool leadersOnly, bool immOnly) {
+    Model& m = e.m;
+    Model::Spec s;
+    s.selFollowers = followersOnly;
+    s.selLeaders = leadersOnly;
+    s.selImmigrants = immOnly;
+    s.prioOffline = m.numSelfHealing > 0;
+    if (asc) {
+      if (limit < 1.7976931348623157e308) {
+        s.selBelowRes = res;
+        s.belowLimit = limit;
+      }
+      s.scoreReverse = false;
+    } else {
+      s.selAboveRes = res;
+      s.aboveLimit = limit;
+      s.scoreReverse = true;
+    }
+    s.scoreRes = res;
+    const int id = nameId(!asc, leadersOnly);
+    m.track(b, id, s);
+    return id;
+  }
+
+  double firstOnlineLoad(const Model& m, const std::vector<int32_t>& v, bool wantMax) const {
+    double x = m.ru(v.front(), res);
+    for (int r : v) {
+      if (m.curOffline(r)) continue;
+      if (wantMax ? m.ru(r, res) > x : m.ru(r, res) < x) x = m.ru(r, res);
+      break;
+    }
+    return x;
+  }
+
+  // rebalanceByMovingLoadOut (:779-863)
+  bool moveOut(Engine& e, int b, int action) {
+    Model& m = e.m;
+    auto cmp = [this, &m](int x, int y) { return cmpBroker(m, x, y); };
+    RbTreeSet<decltype(cmp)> cand(cmp);
+    for (int x = 0; x < m.B; ++x) {
+      if (!m.alive(x)) continue;
+      if (!fix) {  // aliveBrokersUnderThreshold(resource, upper)
+        if ((res == R_CPU || res == R_DISK) && m.bu(x, res) >= m.cap(x, res) * upperThr) continue;
+        if (res != R_DISK && m.bu(x, res) >= m.cap(x, res) * upperThr) continue;
+      }
+      cand.add(x);
+    }
+    const bool lead = action == DA_LEADERSHIP;
+    const bool selfHealing = m.numSelfHealing > 0;
+    Model::Spec s;
+    s.selLeaders = lead;
+    s.selImmigrants = e.opt.onlyImmigrants;
+    s.selImmOrOffline = selfHealing && m.alive(b);
+    s.prioOffline = selfHealing;
+    s.prioImmigrants = !e.opt.onlyImmigrants;
+    s.scoreRes = res;
+    s.scoreReverse = true;
+    const int id = nameId(true, lead);
+    m.track(b, id, s);
+    std::vector<int32_t> list = m.sorted(b, id);  // clone
+    // the loop breaks at the first online replica with zero utilization (static during the loop)
+    size_t z = 0;
+    while (z < list.size() && (m.curOffline(list[z]) || m.ru(list[z], res) != 0.0)) ++z;
+    list.resize(z);
+    const double upperSrc = excluded(b) ? 0 : upperThr;
+    std::vector<int32_t> inorder, cands, pr, pb, fol, elig;
+    std::vector<int32_t> pairOwner;
+    size_t i = 0;
+    while (i < list.size()) {
+      int dst = -1;
+      size_t hitIdx = 0;
+      if (!lead) {
+        cand.inorder(inorder);
+        e.eligible(inorder, DA_MOVE, cands);
+        const int64_t key = e.crossScan(*this, DA_MOVE, list, i, cands);
+        if (key < 0) break;
+        const int N = (int)cands.size();
+        hitIdx = i + (size_t)(key / N);
+        dst = cands[key % N];
+        m.relocateReplica(m.rPart[list[hitIdx]], b, dst);
+      } else {
+        pr.clear();
+        pb.clear();
+        pairOwner.clear();
+        for (size_t q = i; q < list.size(); ++q) {
+          const int r = list[q];
+          m.onlineFollowerBrokers(m.rPart[r], fol);
+          inorder.clear();
+          for (int fb : fol)
+            if (cand.contains(fb)) inorder.push_back(fb);
+          std::sort(inorder.begin(), inorder.end(), [&](int x, int y) { return cmpBroker(m, x, y) < 0; });
+          inorder.erase(std::unique(inorder.begin(), inorder.end()), inorder.end());
+          e.eligible(inorder, DA_LEADERSHIP, elig);
+          for (int fb : elig) {
+            pr.push_back(r);
+            pb.push_back(fb);
+            pairOwner.push_back((int)q);
+          }
+        }
+        const int64_t key = e.pairScan(*this, pr, pb);
+        if (key < 0) break;
+        hitIdx = (size_t)pairOwner[key];
+        dst = pb[key];
+        m.relocateLeadership(m.rPart[list[hitIdx]], b, dst);
+      }
+      if (underUpper(m, b, upperSrc) && !(fix && m.bNoff[b] > 0)) {
+        m.clearTracked(b);
+        return false;
+      }
+      cand.remove(dst);
+      if (m.pct(dst, res) < upperThr) cand.add(dst);
+      i = hitIdx + 1;
+    }
+    m.clearTracked(b);
+    return m.nrep(b) != 0;
+  }
+
+  // rebalanceByMovingLoadIn (:437-526): speculative multi-candidate-broker batches over the live views
+  bool moveIn(Engine& e, int b, int action, bool immOnly) {
+    Model& m = e.m;
+    if (m.numNew > 0 && !m.isNew(b)) return true;
+    const bool followersOnly = e.opt.anyExclLead && e.opt.exclLead[b];
+    auto rcmp = [this, &m](int x, int y) { return cmpBroker(m, y, x); };
+    JavaPQ<decltype(rcmp)> pq(rcmp);
+    int id = -1;
+    for (int c = 0; c < m.B; ++c) {
+      if (!m.alive(c)) continue;
+      if (m.pct(c, res) > (excluded(c) ? 0.0 : lowerThr)) {
+        id = trackCandidates(e, c, 0.0, false, followersOnly, res == R_NW_OUT, immOnly);
+        pq.add(c);
+      }
+    }
+    std::vector<int32_t> single{b}, cands;
+    e.eligible(single, action, cands);
+    struct Seg {
+      int cb;
+      size_t skip;
+      size_t len;
+    };
+    std::vector<Seg> segs;
+    std::vector<int32_t> flat;
+    size_t target = 256;
+    bool haveCur = false;
+    Seg cur{0, 0, 0};
+    auto cond = [&]() { return action == DA_MOVE || m.bNlead[b] != m.nrep(b); };
+    while (haveCur || (!pq.empty() && cond())) {
+      segs.clear();
+      flat.clear();
+      if (haveCur) {
+        const auto& v = m.sorted(cur.cb, id);
+        cur.len = v.size() > cur.skip ? v.size() - cur.skip : 0;
+        segs.push_back(cur);
+        for (size_t q = cur.skip; q < v.size(); ++q) flat.push_back(v[q]);
+        haveCur = false;
+      }
+      while (!pq.empty() && (segs.empty() || flat.size() < target) && cond()) {
+        const int cb = pq.poll();
+        const auto& v = m.sorted(cb, id);
+        segs.push_back({cb, 0, v.size()});
+        flat.insert(flat.end(), v.begin(), v.end());
+      }
+      if (segs.empty()) break;
+      const int64_t key = cands.empty() ? -1 : e.crossScan(*this, action, flat, 0, cands);
+      if (key < 0) {
+        target = std::min<size_t>(target * 2, 1 << 16);
+        continue;
+      }
+      target = 256;
+      size_t q = (size_t)key, mi = 0;
+      while (q >= segs[mi].len) {
+        q -= segs[mi].len;
+        ++mi;
+      }
+      const Seg hit = segs[mi];
+      const size_t idx = hit.skip + q;  // index in cb's live view == iteratedIndices at the hit
+      const int r = m.sorted(hit.cb, id)[idx];
+      if (action == DA_MOVE) m.relocateReplica(m.rPart[r], hit.cb, b);
+      else m.relocateLeadership(m.rPart[r], hit.cb, b);
+      if (aboveLower(m, b)) {
+        m.untrackAll(id);
+        return false;
+      }
+      for (size_t t = mi + 1; t < segs.size(); ++t) pq.add(segs[t].cb);  // un-poll speculative brokers
+      if (!pq.empty() && m.pct(hit.cb, res) < m.pct(pq.peek(), res)) {
+        pq.add(hit.cb);
+      } else {
+        cur = {hit.cb, idx, 0};
+        haveCur = true;
+      }
+    }
+    if (id >= 0) m.untrackAll(id);
+    return true;
+  }
+
+  bool swapCommon(Engine& e, int b, bool out, bool immOnly) {
+    Model& m = e.m;
+    if (!m.alive(b) || (e.opt.anyExclMove && e.opt.exclMove[b])) return true;
+    const int srcId = out ? trackCandidates(e, b, 0.0, false, false, res == R_NW_OUT, immOnly)
+                          : trackCandidates(e, b, 1.7976931348623157e308, true, false, false, immOnly);
+    if (m.sorted(b, srcId).empty()) {
+      m.untrack(b, srcId);
+      return true;
+    }
+    const double limit = firstOnlineLoad(m, m.sorted(b, srcId), out);
+    const bool followersOnly = e.opt.anyExclLead && e.opt.exclLead[b];
+    auto cmpUp = [this, &m](int x, int y) { return cmpBroker(m, x, y); };
+    auto cmpDown = [this, &m](int x, int y) { return cmpBroker(m, y, x); };
+    JavaPQ<decltype(cmpUp)> pqUp(cmpUp);
+    JavaPQ<decltype(cmpDown)> pqDown(cmpDown);
+    auto pqEmpty = [&]() { return out ? pqUp.empty() : pqDown.empty(); };
+    auto pqPoll = [&]() { return out ? pqUp.poll() : pqDown.poll(); };
+    auto pqAdd = [&](int x) {
+      if (out) pqUp.add(x);
+      else pqDown.add(x);
+    };
+    int candId = -1;
+    if (out) {
+      std::vector<int> under, order;
+      for (int x = 0; x < m.B; ++x) {
+        if (!m.alive(x)) continue;
+        if ((res == R_CPU || res == R_DISK) && m.bu(x, res) >= m.cap(x, res) * upperThr) continue;
+        if (res != R_DISK && m.bu(x, res) >= m.cap(x, res) * upperThr) continue;
+        if (m.nrep(x) > 0) under.push_back(x);
+      }
+      javaHashSetOrder(under, order);  // Collectors.toSet()
+      for (int c : order) {
+        candId = trackCandidates(e, c, limit, true, followersOnly, false, immOnly);
+        pqAdd(c);
+      }
+    } else {
+      for (int x = 0; x < m.B; ++x) {
+        if (!m.alive(x)) continue;
+        if ((res == R_CPU || res == R_DISK) && m.bu(x, res) <= m.cap(x, res) * lowerThr) continue;
+        if (res != R_DISK && m.bu(x, res) <= m.cap(x, res) * lowerThr) continue;
+        candId = trackCandidates(e, x, limit, false, followersOnly, res == R_NW_OUT, immOnly);
+        pqAdd(x);
+      }
+    }
+    std::vector<int32_t> srcs, cbOff, cbRep, polled;
+    size_t target = 4;
+    while (!pqEmpty()) {
+      polled.clear();
+      cbOff.assign(1, 0);
+      cbRep.clear();
+      while (!pqEmpty() && (polled.empty() || polled.size() < target)) {
+        const int cb = pqPoll();
+        polled.push_back(cb);
+        const auto& v = m.sorted(cb, candId);
+        cbRep.insert(cbRep.end(), v.begin(), v.end());
+        cbOff.push_back((int32_t)cbRep.size());
+      }
+      srcs = m.sorted(b, srcId);
+      const int64_t key = e.swapScan(*this, srcs, cbOff, cbRep);
+      if (key < 0) {
+        target = std::min<size_t>(target * 2, 1024);
+        continue;  // every polled broker exhausted without a swap
+      }
+      target = 4;
+      const int64_t row = key >> 24;
+      const int j = (int)(key & 0xFFFFFF);
+      const int mi = (int)(row / (int64_t)srcs.size());
+      const int si = (int)(row % (int64_t)srcs.size());
+      const int cb = polled[mi];
+      const int sr = srcs[si];
+      const int dr = cbRep[cbOff[mi] + j];
+      const int dp = m.rPart[dr];
+      m.relocateReplica(m.rPart[sr], b, cb);
+      m.relocateReplica(dp, cb, b);
+      const bool done = out ? underUpper(m, b, upperThr) : aboveLower(m, b);
+      if (done) {
+        m.clearTracked();
+        return false;
+      }
+      for (size_t t = mi + 1; t < polled.size(); ++t) pqAdd(polled[t]);  // un-poll speculative brokers
+      pqAdd(cb);
+    }
+    m.clearTracked();
+    return true;
+  }
+  bool swapOut(Engine& e, int b, bool immOnly) { return swapCommon(e, b, true, immOnly); }
+  bool swapIn(Engine& e, int b, bool immOnly) { return swapCommon(e, b, false, immOnly); }
+};
+
+}  // namespace
+
+std::unique_ptr<GoalImpl> makeGoal(int kind) {
+  switch (kind) {
+    case CCMI_GOAL_REPLICA_DISTRIBUTION: return std::make_unique<ReplicaDistribution>();
+    case CCMI_GOAL_DISK_USAGE_DISTRIBUTION:
+    case CCMI_GOAL_NW_IN_USAGE_DISTRIBUTION:
+    case CCMI_GOAL_NW_OUT_USAGE_DISTRIBUTION:
+    case CCMI_GOAL_CPU_USAGE_DISTRIBUTION: return std::make_unique<ResourceDistribution>(kind);
+    default: throw Unsupported("goal kind " + std::to_string(kind) + " is not implemented in this build");
+  }
+}
+
+}  // namespace ccmi

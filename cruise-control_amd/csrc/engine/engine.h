@@ -1,0 +1,98 @@
+// Engine: the session-level goal optimizer. Goal drivers keep the reference's sequential control flow
+// on the host (they decide WHICH candidate lists are scanned and in what order, with the JDK collection
+// semantics the decisions depend on); every candidate-predicate evaluation runs on the device as a
+// batched first-fit scan, speculating over whole replica lists, popped candidate brokers and source-
+// replica x candidate-replica swap grids. After a winning (replica, destination) the host applies the
+// move to its model, marks the touched rows dirty, and resumes the reference loop right after the winner.
+//
+// Reference control flow restated here:
+//   GoalOptimizer.optimizations               analyzer/GoalOptimizer.java:435-524
+//   AbstractGoal.optimize                     analyzer/goals/AbstractGoal.java:81-135
+//   ReplicaDistributionGoal                   analyzer/goals/ReplicaDistributionGoal.java:151-340
+//   ReplicaDistributionAbstractGoal           analyzer/goals/ReplicaDistributionAbstractGoal.java:79-229
+//   ResourceDistributionGoal                  analyzer/goals/ResourceDistributionGoal.java:234-863
+#pragma once
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "ccmi.h"
+#include "devtypes.h"
+#include "model.h"
+
+namespace ccmi {
+
+class Device;
+
+struct Options {  // OptimizationOptions
+  std::vector<uint8_t> exclMove, exclLead, requested;  // [B] flags
+  bool anyExclMove = false, anyExclLead = false, anyRequested = false;
+  bool triggered = false, onlyImmigrants = false;
+};
+
+struct Constraint {  // BalancingConstraint
+  double resBalance[4], capThreshold[4], lowUtil[4];
+  double replicaBalance, goalViolationMultiplier;
+};
+
+class Engine;
+
+class GoalImpl {
+ public:
+  virtual ~GoalImpl() = default;
+  int kind = 0;
+  std::string name;
+  DevGoal dg{};  // frozen acceptance state
+  std::vector<uint8_t> allowed;
+  bool succeeded = true;
+  bool finished = false;
+  virtual void init(Engine& e) = 0;
+  virtual void rebalance(Engine& e, int b) = 0;
+  virtual void update(Engine& e) = 0;
+  virtual std::vector<int> brokersToBalance(Engine& e);
+  virtual int compareStats(const ccmi_cluster_stats& after, const ccmi_cluster_stats& before) const = 0;
+};
+
+class Engine {
+ public:
+  Engine(Model& m, Device* dev) : m(m), dev(dev) {}
+  Model& m;
+  Device* dev;
+  Options opt;
+  Constraint bc{};
+  std::vector<std::unique_ptr<GoalImpl>> optimized;  // optimized goals, priority order
+  int64_t candidates = 0;
+
+  // one Goal.optimize; throws OptimizationFailure / StateError
+  bool optimizeGoal(std::unique_ptr<GoalImpl> g, ccmi_goal_result* res);
+  ccmi_cluster_stats stats();
+  int acceptance(int goalIndex, const ccmi_action& a);
+
+  // device scans: return winning index or -1; add reference-equivalent candidate counts
+  int64_t crossScan(GoalImpl& self, int action, const std::vector<int32_t>& reps, size_t r0,
+                    const std::vector<int32_t>& cands);
+  int64_t pairScan(GoalImpl& self, const std::vector<int32_t>& pr, const std::vector<int32_t>& pb);
+  int64_t swapScan(GoalImpl& self, const std::vector<int32_t>& srcs, const std::vector<int32_t>& cbOff,
+                   const std::vector<int32_t>& cbRep);
+  void eligible(const std::vector<int32_t>& in, int action, std::vector<int32_t>& out) const;
+
+  double threshold(double avgPct, int res, bool lower) const;  // GoalUtils.computeResourceUtilizationBalanceThreshold
+
+ private:
+  DevProgram program(const GoalImpl& self, int action) const;
+  void refreshAllowed(GoalImpl& g);
+};
+
+std::unique_ptr<GoalImpl> makeGoal(int kind);
+
+struct OptimizationFailure : std::runtime_error {
+  using std::runtime_error::runtime_error;
+};
+struct StateError : std::runtime_error {
+  using std::runtime_error::runtime_error;
+};
+struct Unsupported : std::runtime_error {
+  using std::runtime_error::runtime_error;
+};
+
+}  // namespace ccmi

@@ -1,0 +1,429 @@
+// Host model: build from the flattened desc, exact mutations, sorted-replica tracking, dirty rows.
+#include "model.h"
+
+#include <algorithm>
+#include <stdexcept>
+
+#include "device.h"
+
+namespace ccmi {
+
+void Model::build(const ccmi_cluster_desc& d) {
+  if (d.num_windows < 1 || d.num_windows > kMaxW) throw std::invalid_argument("num_windows must be in [1,5]");
+  W = d.num_windows;
+  ops = LoadOps(W);
+  B = d.num_brokers;
+  R = d.num_replicas;
+  P = d.num_partitions;
+  T = d.num_topics;
+  bState.assign(B, BState::ALIVE);
+  bRack.assign(d.broker_rack, d.broker_rack + B);
+  bId.assign(B, 0);
+  for (int b = 0; b < B; ++b) {
+    bId[b] = d.broker_id[b];
+    if (bId[b] != b) throw std::invalid_argument("ABI v1 requires broker_id[b] == b");
+  }
+  bCap.assign(d.broker_capacity, d.broker_capacity + 4 * (size_t)B);
+  bRepl.assign(B, {});
+  bNlead.assign(B, 0);
+  bNimm.assign(B, 0);
+  bNoff.assign(B, 0);
+  bLoad.assign(B, LoadVec());
+  bLnw.assign(B, LoadVec());
+  bPot.assign(B, LoadVec());
+  rPart.assign(d.replica_partition, d.replica_partition + R);
+  rBroker.assign(d.replica_broker, d.replica_broker + R);
+  rOrig = rBroker;
+  rPos.assign(R, -1);
+  rLeader.assign(d.replica_is_leader, d.replica_is_leader + R);
+  rOrigOff.assign(d.replica_offline, d.replica_offline + R);
+  rInImm.assign(R, 0);
+  rInOff.assign(R, 0);
+  rLoad.assign(R, LoadVec());
+  pTopic.assign(d.partition_topic, d.partition_topic + P);
+  pNumber.assign(d.partition_number, d.partition_number + P);
+  pOff.assign(d.partition_offset, d.partition_offset + P + 1);
+  pSlots.assign(d.partition_replicas, d.partition_replicas + R);
+  pLeader.assign(P, -1);
+  topicNames.clear();
+  for (int t = 0; t < T; ++t) topicNames.emplace_back(d.topic_names[t]);
+  {
+    std::vector<int> idx(T);
+    for (int t = 0; t < T; ++t) idx[t] = t;
+    std::sort(idx.begin(), idx.end(), [&](int a, int b) { return topicNames[a] < topicNames[b]; });
+    topicRank.assign(T, 0);
+    for (int i = 0; i < T; ++i) topicRank[idx[i]] = i;
+  }
+  topicNrep.assign(T, 0);
+  selfHealing.assign(R, 0);
+  tracked.assign(B, {});
+  for (int p = 0; p < P; ++p)
+    for (int i = pOff[p]; i < pOff[p + 1]; ++i) {
+      const int r = pSlots[i];
+      if (r < 0 || r >= R || rPart[r] != p) throw std::invalid_argument("partition CSR inconsistent with replica_partition");
+    }
+  // Replay createReplica + setReplicaLoad in replica index order.
+  std::vector<std::vector<int32_t>> created(P);
+  for (int r = 0; r < R; ++r) {
+    const int p = rPart[r], b = rBroker[r];
+    if (b < 0 || b >= B) throw std::invalid_argument("replica broker out of range");
+    brokerAdd(b, r);  // load still empty: only sets/counters change
+    topicNrep[pTopic[p]]++;
+    if (rLeader[r]) {
+      if (pLeader[p] >= 0) throw std::invalid_argument("partition has two leaders");
+      pLeader[p] = r;
+    } else if (pLeader[p] >= 0) {
+      ops.addAll(bPot[b], rLoad[pLeader[p]]);
+    }
+    created[p].push_back(r);
+    if ((int)created[p].size() > maxRf) maxRf = (int)created[p].size();
+    // setReplicaLoad
+    LoadVec amv;
+    amv.mask = 0x3F;
+    for (int k = 0; k < 6; ++k) {
+      ops.zero(amv.m[k]);
+      for (int w = 0; w < W; ++w) {
+        amv.m[k].v[w] = d.replica_load[((size_t)r * 6 + k) * W + w];
+        amv.m[k].sum += (double)amv.m[k].v[w];
+      }
+    }
+    ops.addAll(rLoad[r], amv);
+    if (rLeader[r]) ops.addAll(bLnw[b], amv);
+    ops.addAll(bLoad[b], amv);
+    ops.addAll(cLoad, amv);
+    if (pLeader[p] >= 0 && rBroker[pLeader[p]] == b)
+      for (int x : created[p]) ops.addAll(bPot[rBroker[x]], amv);
+  }
+  if (maxRf > kMaxRf) throw std::invalid_argument("replication factor above 8 is not supported");
+  for (int p = 0; p < P; ++p)
+    if (pLeader[p] < 0) throw std::invalid_argument("partition without leader");
+  // broker states (ClusterModel.setBrokerState)
+  for (int b = 0; b < B; ++b) {
+    const BState s = (BState)d.broker_state[b];
+    if (s == BState::ALIVE) continue;
+    if (s == BState::BAD_DISKS) throw std::invalid_argument("BAD_DISKS brokers are outside ABI v1 scope");
+    bState[b] = s;
+    if (s == BState::DEAD) {
+      numDead++;
+      for (int r : bRepl[b])
+        if (!rInOff[r]) {
+          rInOff[r] = 1;
+          bNoff[b]++;
+        }
+      for (int k = 0; k < 4; ++k) bCap[4 * b + k] = -1.0;
+    }
+    if (s == BState::NEW) numNew++;
+    for (int r : bRepl[b])
+      if (rInOff[r] && !selfHealing[r]) {
+        selfHealing[r] = 1;
+        numSelfHealing++;
+      }
+  }
+  for (int k = 0; k < 4; ++k) {
+    double c = 0;
+    for (int b = 0; b < B; ++b)
+      if (alive(b)) c += bCap[4 * b + k];
+    clusterCap[k] = c;
+  }
+  bUtilC.assign((size_t)4 * B, 0.0);
+  rUtilC.assign((size_t)4 * R, 0.0);
+  rScoreC.assign((size_t)4 * R, 0.f);
+  for (int b = 0; b < B; ++b) refreshBroker(b);
+  for (int r = 0; r < R; ++r) refreshReplica(r);
+  const int ldB = (B + 3) & ~3;
+  topicCountDense.assign((size_t)T * ldB, 0);
+  for (int r = 0; r < R; ++r) topicCountDense[(size_t)pTopic[rPart[r]] * ldB + rBroker[r]]++;
+  bDirty.assign(B, 0);
+  rDirty.assign(R, 0);
+  pDirty.assign(P, 0);
+}
+
+void Model::refreshBroker(int b) {
+  for (int k = 0; k < 4; ++k) bUtilC[4 * b + k] = ops.util(bLoad[b], k);
+}
+void Model::refreshReplica(int r) {
+  for (int k = 0; k < 4; ++k) {
+    rUtilC[4 * r + k] = ops.util(rLoad[r], k);
+    rScoreC[4 * r + k] = rLoad[r].mask ? ops.groupAvg(rLoad[r], k) : 0.f;
+  }
+}
+
+double Model::capacityWithAllowedReplicaMoves(int res, const std::vector<uint8_t>& excluded) const {
+  // _clusterCapacity[res] - DoubleStream.sum(capacity of alive excluded brokers)
+  double s0 = 0, s1 = 0, simple = 0;
+  bool any = false;
+  for (int b = 0; b < B; ++b)
+    if (alive(b) && !excluded.empty() && excluded[b]) {
+      const double v = cap(b, res);
+      const double t = v - s1, vv = s0 + t;
+      s1 = (vv - s0) - t;
+      s0 = vv;
+      simple += v;
+      any = true;
+    }
+  double drop = any ? s0 + s1 : 0.0;
+  if (std::isnan(drop) && std::isinf(simple)) drop = simple;
+  return clusterCap[res] - drop;
+}
+
+// ------------------------------------------------------------------------------- broker membership
+void Model::brokerAdd(int b, int r) {
+  rPos[r] = (int)bRepl[b].size();
+  bRepl[b].push_back(r);
+  rInImm[r] = rInOff[r] = 0;
+  if (rOrig[r] != b) {
+    rInImm[r] = 1;
+    bNimm[b]++;
+  } else if (origOffline(r)) {
+    rInOff[r] = 1;
+    bNoff[b]++;
+  }
+  if (rLeader[r]) {
+    ops.addAll(bLnw[b], rLoad[r]);
+    bNlead[b]++;
+  }
+  ops.addAll(bLoad[b], rLoad[r]);
+  sortedInsert(b, r);
+}
+
+int Model::brokerRemove(int b, int p) {
+  const int r = replicaOn(p, b);
+  if (r < 0) return -1;
+  auto& v = bRepl[b];
+  const int pos = rPos[r];
+  v[pos] = v.back();
+  rPos[v[pos]] = pos;
+  v.pop_back();
+  rPos[r] = -1;
+  ops.subAll(bLoad[b], rLoad[r]);
+  if (rLeader[r]) {
+    ops.subAll(bLnw[b], rLoad[r]);
+    bNlead[b]--;
+  }
+  if (rInImm[r]) bNimm[b]--;
+  if (rInOff[r]) bNoff[b]--;
+  rInImm[r] = rInOff[r] = 0;
+  sortedErase(b, r);
+  return r;
+}
+
+void Model::relocateReplica(int p, int src, int dst) {
+  const int r = brokerRemove(src, p);
+  if (r < 0) throw std::runtime_error("Replica is not in the cluster.");
+  ops.subAll(cLoad, rLoad[r]);
+  ops.subAll(bPot[src], rLoad[pLeader[p]]);
+  rBroker[r] = dst;
+  brokerAdd(dst, r);
+  ops.addAll(cLoad, rLoad[r]);
+  ops.addAll(bPot[dst], rLoad[pLeader[p]]);
+  refreshBroker(src);
+  refreshBroker(dst);
+  log.push_back({CCMI_INTER_BROKER_REPLICA_MOVEMENT, p, src, dst, -1});
+  if (dev) {
+    markB(src);
+    markB(dst);
+    markR(r);
+    markP(p);
+    dev->tdeltas.push_back({pTopic[p], src, -1, 0});
+    dev->tdeltas.push_back({pTopic[p], dst, +1, 0});
+  }
+}
+
+bool Model::relocateLeadership(int p, int src, int dst) {
+  const int sr = replicaOn(p, src);
+  if (sr < 0 || !rLeader[sr]) return false;
+  const int dr = replicaOn(p, dst);
+  if (dr < 0 || rLeader[dr]) throw std::runtime_error("destination replica is a leader");
+  // Broker.makeFollower(src)
+  ops.subAll(bLnw[src], rLoad[sr]);
+  sortedErase(src, sr);
+  LoadVec& L = rLoad[sr];
+  Window totOut, totIn, chg;
+  ops.zero(totOut);
+  ops.add(totOut, L.m[M_LBO]);
+  ops.add(totOut, L.m[M_RBO]);
+  ops.zero(totIn);
+  ops.add(totIn, L.m[M_LBI]);
+  ops.add(totIn, L.m[M_RBI]);
+  ops.zero(chg);
+  for (int i = 0; i < W; ++i) {
+    const double in = (double)totIn.v[i], out = (double)totOut.v[i], c = (double)L.m[M_CPU].v[i];
+    const double follower = (in == 0.0 && out == 0.0) ? 0.0 : c * (0.15 * in) / (0.7 * in + 0.15 * out);
+    ops.set(chg, i, (double)L.m[M_CPU].v[i] - follower);
+    ops.set(L.m[M_CPU], i, follower);
+  }
+  LoadVec delta;
+  delta.mask = (1 << M_CPU) | (1 << M_LBO) | (1 << M_RBO);
+  ops.zero(delta.m[M_CPU]);
+  ops.add(delta.m[M_CPU], chg);
+  ops.zero(delta.m[M_LBO]);
+  ops.add(delta.m[M_LBO], L.m[M_LBO]);
+  ops.zero(delta.m[M_RBO]);
+  ops.add(delta.m[M_RBO], L.m[M_RBO]);
+  ops.zero(L.m[M_LBO]);
+  ops.zero(L.m[M_RBO]);
+  rLeader[sr] = 0;
+  refreshReplica(sr);
+  if (bLoad[src].mask) ops.subAll(bLoad[src], delta);
+  bNlead[src]--;
+  sortedInsert(src, sr);
+  // Broker.makeLeader(dst)
+  sortedErase(dst, dr);
+  rLeader[dr] = 1;
+  if (rLoad[dr].mask) ops.addAll(rLoad[dr], delta);
+  refreshReplica(dr);
+  ops.addAll(bLnw[dst], rLoad[dr]);
+  if (bLoad[dst].mask) ops.addAll(bLoad[dst], delta);
+  bNlead[dst]++;
+  sortedInsert(dst, dr);
+  // Partition.relocateLeadership: swap positions 0 and indexOf(dr)
+  int pos = pOff[p];
+  while (pSlots[pos] != dr) ++pos;
+  std::swap(pSlots[pOff[p]], pSlots[pos]);
+  pLeader[p] = dr;
+  refreshBroker(src);
+  refreshBroker(dst);
+  log.push_back({CCMI_LEADERSHIP_MOVEMENT, p, src, dst, -1});
+  if (dev) {
+    markB(src);
+    markB(dst);
+    markR(sr);
+    markR(dr);
+    markP(p);
+  }
+  return true;
+}
+
+void Model::flushToDevice() {
+  if (!dev) return;
+  for (int b : bDirtyList) {
+    BrokerRow row;
+    row.b = b;
+    row.nrep = nrep(b);
+    row.nlead = bNlead[b];
+    row.alive = alive(b) ? 1 : 0;
+    for (int k = 0; k < 4; ++k) row.util[k] = bUtilC[4 * b + k];
+    row.potNwOut = ops.util(bPot[b], R_NW_OUT);
+    row.pad = 0;
+    dev->brows.push_back(row);
+    bDirty[b] = 0;
+  }
+  bDirtyList.clear();
+  for (int r : rDirtyList) {
+    ReplicaRow row;
+    row.r = r;
+    row.broker = rBroker[r];
+    row.flags = (rLeader[r] ? RF_LEADER : 0) | (rOrigOff[r] ? RF_ORIG_OFFLINE : 0);
+    row.pad = 0;
+    for (int k = 0; k < 4; ++k) row.util[k] = rUtilC[4 * r + k];
+    dev->rrows.push_back(row);
+    rDirty[r] = 0;
+  }
+  rDirtyList.clear();
+  for (int p : pDirtyList) {
+    PartitionRow row;
+    row.p = p;
+    row.n = pOff[p + 1] - pOff[p];
+    for (int k = 0; k < row.n; ++k) row.brokers[k] = rBroker[pSlots[pOff[p] + k]];
+    dev->prows.push_back(row);
+    pDirty[p] = 0;
+  }
+  pDirtyList.clear();
+}
+
+// ------------------------------------------------------------------------------- sorted replicas
+bool Model::selects(const Spec& s, int r) const {
+  if (s.selLeaders && !rLeader[r]) return false;
+  if (s.selFollowers && rLeader[r]) return false;
+  if (s.selImmigrants && !immigrant(r)) return false;
+  if (s.selImmOrOffline && !(immigrant(r) || curOffline(r))) return false;
+  if (s.selAboveRes >= 0 && !(ru(r, s.selAboveRes) > s.aboveLimit)) return false;
+  if (s.selBelowRes >= 0 && !(ru(r, s.selBelowRes) < s.belowLimit)) return false;
+  return true;
+}
+
+// SortedReplicas comparator: priority functions, score (Double.compare), Replica.compareTo
+int Model::cmpReplica(const Spec& s, int a, int b) const {
+  if (s.prioOffline) {
+    const int pa = curOffline(a) ? 0 : 1, pb = curOffline(b) ? 0 : 1;
+    if (pa != pb) return pa < pb ? -1 : 1;
+  }
+  if (s.prioImmigrants) {
+    const int pa = immigrant(a) ? 0 : 1, pb = immigrant(b) ? 0 : 1;
+    if (pa != pb) return pa < pb ? -1 : 1;
+  }
+  if (s.scoreRes >= 0) {
+    double sa = (double)rScoreC[4 * a + s.scoreRes], sb = (double)rScoreC[4 * b + s.scoreRes];
+    if (s.scoreReverse) {
+      sa = -sa;
+      sb = -sb;
+    }
+    const int c = jcmpDouble(sa, sb);
+    if (c) return c;
+  }
+  const bool oa = curOffline(a), ob = curOffline(b);
+  if (oa != ob) return oa ? -1 : 1;
+  const int na = pNumber[rPart[a]], nb = pNumber[rPart[b]];
+  if (na != nb) return na > nb ? 1 : -1;
+  const int ia = bId[rOrig[a]], ib = bId[rOrig[b]];
+  if (ia != ib) return ia > ib ? 1 : -1;
+  const int ta = topicRank[pTopic[rPart[a]]], tb = topicRank[pTopic[rPart[b]]];
+  return ta == tb ? 0 : (ta < tb ? -1 : 1);
+}
+
+void Model::track(int b, int nameId, const Spec& s) {
+  for (auto& t : tracked[b])
+    if (t.nameId == nameId) return;  // putIfAbsent
+  tracked[b].push_back({nameId, s, false, {}});
+}
+void Model::untrackAll(int nameId) {
+  for (int b = 0; b < B; ++b) untrack(b, nameId);
+}
+void Model::untrack(int b, int nameId) {
+  auto& v = tracked[b];
+  for (size_t i = 0; i < v.size(); ++i)
+    if (v[i].nameId == nameId) {
+      v.erase(v.begin() + i);
+      return;
+    }
+}
+void Model::clearTracked() {
+  for (int b = 0; b < B; ++b) tracked[b].clear();
+}
+void Model::clearTracked(int b) { tracked[b].clear(); }
+
+const std::vector<int32_t>& Model::sorted(int b, int nameId) {
+  for (auto& t : tracked[b])
+    if (t.nameId == nameId) {
+      if (!t.init) {
+        t.init = true;
+        t.v.clear();
+        for (int r : bRepl[b])
+          if (selects(t.spec, r)) t.v.push_back(r);
+        const Spec& s = t.spec;
+        std::sort(t.v.begin(), t.v.end(), [&](int x, int y) { return cmpReplica(s, x, y) < 0; });
+      }
+      return t.v;
+    }
+  throw std::runtime_error("sorted replicas not tracked");
+}
+
+void Model::sortedInsert(int b, int r) {
+  for (auto& t : tracked[b]) {
+    if (!t.init || !selects(t.spec, r)) continue;
+    const Spec& s = t.spec;
+    auto it = std::lower_bound(t.v.begin(), t.v.end(), r, [&](int x, int y) { return cmpReplica(s, x, y) < 0; });
+    if (it != t.v.end() && cmpReplica(s, *it, r) == 0) continue;  // TreeSet.add of an equal element
+    t.v.insert(it, r);
+  }
+}
+void Model::sortedErase(int b, int r) {
+  for (auto& t : tracked[b]) {
+    if (!t.init) continue;
+    const Spec& s = t.spec;
+    auto it = std::lower_bound(t.v.begin(), t.v.end(), r, [&](int x, int y) { return cmpReplica(s, x, y) < 0; });
+    if (it != t.v.end() && *it == r) t.v.erase(it);
+  }
+}
+
+}  // namespace ccmi

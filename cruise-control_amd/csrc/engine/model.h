@@ -1,0 +1,240 @@
+// Host half of the engine's cluster model: structure-of-arrays state with the reference's exact load
+// arithmetic, plus dirty-row tracking that feeds the device mirror (device.h).
+//
+// Numeric representation follows MetricValues (float window values + double running sum;
+// cruise-control-core/.../aggregator/MetricValues.java:17-221) and ModelUtils.expectedUtilizationFor
+// (model/ModelUtils.java:162-176). Mutations follow ClusterModel.relocateReplica / relocateLeadership
+// (model/ClusterModel.java:380-441,546-564), Broker.add/removeReplica/makeFollower/makeLeader
+// (model/Broker.java:336-510) and Replica.makeFollower/makeLeader (model/Replica.java:210-310), in the
+// reference's operation order so every float/double rounding is reproduced.
+#pragma once
+#include <cstdint>
+#include <memory>
+#include <string>
+#include <unordered_set>
+#include <vector>
+
+#include "ccmi.h"
+#include "devtypes.h"
+#include "jsem.h"
+
+namespace ccmi {
+
+enum Res { R_CPU = 0, R_NW_IN = 1, R_NW_OUT = 2, R_DISK = 3 };
+enum Met { M_CPU = 0, M_DISK = 1, M_LBI = 2, M_LBO = 3, M_RBI = 4, M_RBO = 5 };
+constexpr int kMaxW = 5;
+
+struct Window {  // one MetricValues
+  float v[kMaxW];
+  double sum;
+};
+struct LoadVec {  // AggregatedMetricValues over the 6 resource metrics
+  uint8_t mask = 0;
+  Window m[6];
+};
+
+class LoadOps {
+ public:
+  explicit LoadOps(int W) : W(W) {}
+  int W;
+  void zero(Window& x) const {
+    for (int i = 0; i < W; ++i) x.v[i] = 0.f;
+    x.sum = 0.0;
+  }
+  void add(Window& a, const Window& b) const {
+    for (int i = 0; i < W; ++i) {
+      const double d = (double)b.v[i];
+      a.v[i] = (float)((double)a.v[i] + d);
+      a.sum += d;
+    }
+  }
+  void sub(Window& a, const Window& b) const {
+    for (int i = 0; i < W; ++i) {
+      const double d = (double)b.v[i];
+      a.v[i] = (float)((double)a.v[i] - d);
+      a.sum -= d;
+    }
+  }
+  void set(Window& a, int i, double x) const {
+    a.sum += x - (double)a.v[i];
+    a.v[i] = (float)x;
+  }
+  float avg(const Window& a) const { return (float)(a.sum / W); }
+  void addAll(LoadVec& d, const LoadVec& s) const {  // AggregatedMetricValues.add
+    for (int k = 0; k < 6; ++k)
+      if (s.mask >> k & 1) {
+        if (!(d.mask >> k & 1)) {
+          zero(d.m[k]);
+          d.mask |= (uint8_t)(1 << k);
+        }
+        add(d.m[k], s.m[k]);
+      }
+  }
+  void subAll(LoadVec& d, const LoadVec& s) const {
+    for (int k = 0; k < 6; ++k)
+      if (s.mask >> k & 1) {
+        if (!(d.mask >> k & 1)) throw std::runtime_error("subtract from a missing metric");
+        sub(d.m[k], s.m[k]);
+      }
+  }
+  double util(const LoadVec& l, int res) const {  // ModelUtils.expectedUtilizationFor
+    if (!l.mask) return 0.0;
+    double r = 0;
+    switch (res) {
+      case R_CPU: r += (double)avg(l.m[M_CPU]); break;
+      case R_DISK: r += (double)l.m[M_DISK].v[0]; break;
+      case R_NW_IN: r += (double)avg(l.m[M_LBI]); r += (double)avg(l.m[M_RBI]); break;
+      default: r += (double)avg(l.m[M_LBO]); r += (double)avg(l.m[M_RBO]); break;
+    }
+    return jmax(r, 0.0);
+  }
+  float groupAvg(const LoadVec& l, int res) const {  // valuesForGroup(group, def, shareValueArray=true).avg()
+    if (res == R_CPU) return avg(l.m[M_CPU]);
+    if (res == R_DISK) return avg(l.m[M_DISK]);
+    Window acc;
+    zero(acc);
+    add(acc, l.m[res == R_NW_IN ? M_LBI : M_LBO]);
+    add(acc, l.m[res == R_NW_IN ? M_RBI : M_RBO]);
+    return avg(acc);
+  }
+};
+
+enum class BState : int32_t { ALIVE = 0, DEAD = 1, NEW = 2, DEMOTED = 3, BAD_DISKS = 4 };
+
+struct ActionRec {
+  int32_t type, partition, src, dst, destPartition;
+};
+
+class Device;
+
+class Model {
+ public:
+  int W = 1, B = 0, R = 0, P = 0, T = 0;
+  LoadOps ops{1};
+  // brokers
+  std::vector<BState> bState;
+  std::vector<int32_t> bRack, bId;
+  std::vector<double> bCap;                 // [B][4]
+  std::vector<std::vector<int32_t>> bRepl;  // replica ids hosted (HashSet contents; order unused)
+  std::vector<int32_t> bNlead, bNimm, bNoff;
+  std::vector<LoadVec> bLoad, bLnw, bPot;
+  std::vector<double> bUtilC;               // cache [B][4] of ops.util(bLoad[b], res)
+  // replicas
+  std::vector<int32_t> rPart, rBroker, rOrig, rPos;
+  std::vector<uint8_t> rLeader, rOrigOff, rInImm, rInOff;
+  std::vector<LoadVec> rLoad;
+  std::vector<double> rUtilC;               // [R][4]
+  std::vector<float> rScoreC;               // [R][4] groupAvg per resource (sorted-replica score)
+  // partitions
+  std::vector<int32_t> pTopic, pNumber, pOff, pSlots, pLeader;  // pSlots: replica ids, Partition._replicas order
+  // topics
+  std::vector<std::string> topicNames;
+  std::vector<int32_t> topicRank, topicNrep;
+  std::vector<int32_t> topicCountDense;     // [T][ldB] (host copy only at build time)
+  // cluster
+  LoadVec cLoad;
+  double clusterCap[4] = {0, 0, 0, 0};
+  std::vector<uint8_t> selfHealing;         // per replica: in _selfHealingEligibleReplicas
+  int64_t numSelfHealing = 0;
+  int numDead = 0, numNew = 0, numBadDisk = 0;
+  int maxRf = 1;
+  // action log + counters
+  std::vector<ActionRec> log;
+  int64_t candidates = 0;
+
+  // device mirror
+  Device* dev = nullptr;
+  std::vector<uint8_t> bDirty, rDirty, pDirty;
+  std::vector<int32_t> bDirtyList, rDirtyList, pDirtyList;
+  void markB(int b) {
+    if (!bDirty[b]) {
+      bDirty[b] = 1;
+      bDirtyList.push_back(b);
+    }
+  }
+  void markR(int r) {
+    if (!rDirty[r]) {
+      rDirty[r] = 1;
+      rDirtyList.push_back(r);
+    }
+  }
+  void markP(int p) {
+    if (!pDirty[p]) {
+      pDirty[p] = 1;
+      pDirtyList.push_back(p);
+    }
+  }
+  void flushToDevice();  // turn dirty rows into Device::brows/rrows/prows
+
+  // ---- queries
+  bool alive(int b) const { return bState[b] != BState::DEAD; }
+  bool isNew(int b) const { return bState[b] == BState::NEW; }
+  double cap(int b, int res) const { return bCap[4 * b + res]; }
+  double bu(int b, int res) const { return bUtilC[4 * b + res]; }
+  double ru(int r, int res) const { return rUtilC[4 * r + res]; }
+  double pct(int b, int res) const {  // GoalUtils.utilization
+    const double c = cap(b, res);
+    return c > 0 ? bu(b, res) / c : 1.0;
+  }
+  int nrep(int b) const { return (int)bRepl[b].size(); }
+  bool origOffline(int r) const { return rOrigOff[r] || !alive(rOrig[r]); }
+  bool curOffline(int r) const { return (origOffline(r) && rBroker[r] == rOrig[r]) || !alive(rBroker[r]); }
+  bool immigrant(int r) const { return rOrig[r] != rBroker[r]; }
+  int replicaOn(int p, int b) const {
+    for (int i = pOff[p]; i < pOff[p + 1]; ++i)
+      if (rBroker[pSlots[i]] == b) return pSlots[i];
+    return -1;
+  }
+  void onlineFollowerBrokers(int p, std::vector<int>& out) const {
+    out.clear();
+    for (int i = pOff[p]; i < pOff[p + 1]; ++i) {
+      const int r = pSlots[i];
+      if (!rLeader[r] && !curOffline(r)) out.push_back(rBroker[r]);
+    }
+  }
+  double capacityWithAllowedReplicaMoves(int res, const std::vector<uint8_t>& excludedReplicaMove) const;
+  double clusterUtil(int res) const { return ops.util(cLoad, res); }
+
+  // ---- mutations (record into the action log, mark dirty rows)
+  void relocateReplica(int p, int src, int dst);
+  bool relocateLeadership(int p, int src, int dst);
+
+  // ---- sorted replica tracking (sorted-vector implementation of SortedReplicas)
+  struct Spec {
+    bool selLeaders = false, selFollowers = false, selImmigrants = false, selImmOrOffline = false;
+    int selAboveRes = -1, selBelowRes = -1;
+    double aboveLimit = 0, belowLimit = 0;
+    bool prioOffline = false, prioImmigrants = false;
+    int scoreRes = -1;  // -1 none
+    bool scoreReverse = false;
+  };
+  struct Tracked {
+    int nameId;
+    Spec spec;
+    bool init = false;
+    std::vector<int32_t> v;
+  };
+  std::vector<std::vector<Tracked>> tracked;  // per broker
+  void track(int b, int nameId, const Spec& s);
+  void untrackAll(int nameId);
+  void untrack(int b, int nameId);
+  void clearTracked();
+  void clearTracked(int b);
+  const std::vector<int32_t>& sorted(int b, int nameId);  // lazily initialized live view
+  bool selects(const Spec& s, int r) const;
+  int cmpReplica(const Spec& s, int a, int b) const;
+
+  // Replays the desc construction order documented in include/ccmi.h (ClusterModel.createReplica +
+  // setReplicaLoad per replica, then partition list order, then broker states).
+  void build(const ccmi_cluster_desc& d);
+
+ private:
+  void brokerAdd(int b, int r);
+  int brokerRemove(int b, int p);
+  void refreshBroker(int b);
+  void refreshReplica(int r);
+  void sortedInsert(int b, int r);
+  void sortedErase(int b, int r);
+};
+
+}  // namespace ccmi

@@ -271,6 +271,8 @@ typedef struct ccmi_perf_counters {
 } ccmi_perf_counters;
 ccmi_status ccmi_perf(const ccmi_session* s, ccmi_perf_counters* out);
 void ccmi_perf_reset(ccmi_session* s);
+/* Record HIP events around every scan/stats kernel (adds a little host overhead; off by default). */
+void ccmi_set_kernel_timing(ccmi_session* s, int32_t enabled);
 
 #ifdef __cplusplus
 }

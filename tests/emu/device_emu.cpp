@@ -1,0 +1,257 @@
+// TEST INFRASTRUCTURE ONLY — never linked into libccmi.so.
+//
+// A sequential host implementation of ccmi::Device (cruise-control_amd/csrc/engine/device.h) used to build
+// tests/emu/libccmi_emu.so, so the engine's host driver logic (batching, speculation/un-polling, winner
+// decoding, resumption) can be parity-checked against the CPU oracle on machines without a GPU. It
+// evaluates the same predicates.h conjunctions as the gfx950 kernels, pair by pair in reference order.
+// The product library always uses the HIP implementation (device.cpp) and fails loudly without a gfx950.
+#include <cmath>
+#include <cstring>
+#include <stdexcept>
+#include <vector>
+
+#include "device.h"
+#include "predicates.h"
+
+namespace ccmi {
+
+namespace {
+struct Emu {
+  int B, R, P, T, ldB, G;
+  std::vector<double> bUtil, bCap, bPot, rUtil;
+  std::vector<int32_t> bNrep, bNlead, rPart, rBroker, rOrig, pOff, pBrokers, topicCount, topicNrep;
+  std::vector<uint8_t> bAlive, allowed, rFlags;
+};
+struct View {
+  const Emu& e;
+  double bu(int b, int res) const { return e.bUtil[(size_t)res * e.B + b]; }
+  double bcap(int b, int res) const { return e.bCap[(size_t)res * e.B + b]; }
+  int nrep(int b) const { return e.bNrep[b]; }
+  bool alive(int b) const { return e.bAlive[b] != 0; }
+  bool allowed(int slot, int b) const { return e.allowed[(size_t)slot * e.B + b] != 0; }
+  double ru(int r, int res) const { return e.rUtil[(size_t)res * e.R + r]; }
+  int flags(int r) const { return e.rFlags[r]; }
+  int rbroker(int r) const { return e.rBroker[r]; }
+  int rorig(int r) const { return e.rOrig[r]; }
+  int rpart(int r) const { return e.rPart[r]; }
+  int pbegin(int p) const { return e.pOff[p]; }
+  int pend(int p) const { return e.pOff[p + 1]; }
+  int pbroker(int i) const { return e.pBrokers[i]; }
+};
+Emu& E(void* st) { return *static_cast<Emu*>(st); }
+}  // namespace
+
+Device::Device(int ordinal, int B, int R, int P, int T, int maxGoalSlots)
+    : ordinal_(ordinal), B_(B), R_(R), P_(P), T_(T), ldB_((B + 3) & ~3), G_(maxGoalSlots) {
+  auto* e = new Emu();
+  e->B = B;
+  e->R = R;
+  e->P = P;
+  e->T = T;
+  e->ldB = ldB_;
+  e->G = maxGoalSlots;
+  e->allowed.assign((size_t)maxGoalSlots * B, 0);
+  st_ = e;
+}
+Device::~Device() { delete static_cast<Emu*>(st_); }
+
+void Device::uploadStatic(const double* bCapRM, const int32_t* rPart, const int32_t* rOrig, const int32_t* pOff,
+                          const int32_t* topicNrep) {
+  Emu& e = E(st_);
+  e.bCap.assign(bCapRM, bCapRM + 4 * (size_t)B_);
+  e.rPart.assign(rPart, rPart + R_);
+  e.rOrig.assign(rOrig, rOrig + R_);
+  e.pOff.assign(pOff, pOff + P_ + 1);
+  e.topicNrep.assign(topicNrep, topicNrep + T_);
+}
+void Device::uploadDynamic(const double* bUtilRM, const int32_t* bNrep, const int32_t* bNlead, const double* bPot,
+                           const uint8_t* bAlive, const double* rUtilRM, const int32_t* rBroker, const uint8_t* rFlags,
+                           const int32_t* pBrokers, const int32_t* tc) {
+  Emu& e = E(st_);
+  e.bUtil.assign(bUtilRM, bUtilRM + 4 * (size_t)B_);
+  e.bNrep.assign(bNrep, bNrep + B_);
+  e.bNlead.assign(bNlead, bNlead + B_);
+  e.bPot.assign(bPot, bPot + B_);
+  e.bAlive.assign(bAlive, bAlive + B_);
+  e.rUtil.assign(rUtilRM, rUtilRM + 4 * (size_t)R_);
+  e.rBroker.assign(rBroker, rBroker + R_);
+  e.rFlags.assign(rFlags, rFlags + R_);
+  e.pBrokers.assign(pBrokers, pBrokers + R_);
+  e.topicCount.assign(tc, tc + (size_t)T_ * ldB_);
+}
+void Device::setAllowed(int slot, const uint8_t* a) {
+  std::memcpy(E(st_).allowed.data() + (size_t)slot * B_, a, B_);
+}
+
+void Device::flushOnly() {
+  Emu& e = E(st_);
+  for (const BrokerRow& x : brows) {
+    for (int k = 0; k < 4; ++k) e.bUtil[(size_t)k * B_ + x.b] = x.util[k];
+    e.bNrep[x.b] = x.nrep;
+    e.bNlead[x.b] = x.nlead;
+    e.bPot[x.b] = x.potNwOut;
+    e.bAlive[x.b] = (uint8_t)x.alive;
+  }
+  for (const ReplicaRow& x : rrows) {
+    for (int k = 0; k < 4; ++k) e.rUtil[(size_t)k * R_ + x.r] = x.util[k];
+    e.rBroker[x.r] = x.broker;
+    e.rFlags[x.r] = (uint8_t)x.flags;
+  }
+  for (const PartitionRow& x : prows)
+    for (int k = 0; k < x.n; ++k) e.pBrokers[e.pOff[x.p] + k] = x.brokers[k];
+  for (const TopicCountDelta& d : tdeltas) e.topicCount[(size_t)d.topic * ldB_ + d.broker] += d.delta;
+  brows.clear();
+  rrows.clear();
+  prows.clear();
+  tdeltas.clear();
+}
+
+int64_t Device::scanCross(const DevProgram& prog, const int32_t* reps, int K, const int32_t* cands, int N) {
+  flushOnly();
+  View v{E(st_)};
+  perf.scanLaunches++;
+  perf.scanPairs += (int64_t)K * N;
+  for (int k = 0; k < K; ++k)
+    for (int j = 0; j < N; ++j)
+      if (moveCandidateAccepted(prog, v, reps[k], cands[j])) return (int64_t)k * N + j;
+  return -1;
+}
+
+int64_t Device::scanPairs(const DevProgram& prog, const int32_t* pr, const int32_t* pb, int n) {
+  flushOnly();
+  View v{E(st_)};
+  perf.scanLaunches++;
+  perf.scanPairs += n;
+  for (int q = 0; q < n; ++q)
+    if (moveCandidateAccepted(prog, v, pr[q], pb[q])) return q;
+  return -1;
+}
+
+int64_t Device::scanSwap(const DevProgram& prog, const int32_t* srcs, int S, const int32_t* cbOff, int M,
+                         const int32_t* cbRep, int nCand, int64_t* visited) {
+  flushOnly();
+  View v{E(st_)};
+  perf.scanLaunches++;
+  perf.scanPairs += (int64_t)S * nCand;
+  *visited = 0;
+  for (int m = 0; m < M; ++m)
+    for (int s = 0; s < S; ++s) {
+      const int c0 = cbOff[m], c1 = cbOff[m + 1];
+      if (c0 == c1) continue;
+      const int db = E(st_).rBroker[cbRep[c0]];
+      for (int j = c0; j < c1; ++j) {
+        const int o = swapCandidateOutcome(prog, v, srcs[s], cbRep[j], db);
+        (*visited)++;
+        if (o == 1) return ((int64_t)((int64_t)m * S + s) << 24) | (j - c0);
+        if (o == 2) break;
+      }
+    }
+  return -1;
+}
+
+void Device::stats(const StatsParams& P, const uint8_t* aa, StatsOut* out) {
+  flushOnly();
+  Emu& e = E(st_);
+  perf.statsLaunches++;
+  const int B = P.B, na = P.numAllowed;
+  std::memset(out, 0, sizeof(*out));
+  for (int res = 0; res < 4; ++res) {
+    double hot = 0, cold = 1.7976931348623157e308, var = 0;
+    int bal = 0;
+    for (int b = 0; b < B; ++b) {
+      if (!e.bAlive[b]) continue;
+      const double u = e.bUtil[(size_t)res * B + b];
+      hot = u > hot ? u : hot;
+      cold = u < cold ? u : cold;
+      if (aa[b]) {
+        const double cap = e.bCap[(size_t)res * B + b];
+        const double pct = u / cap;
+        if (pct >= P.lowerThr[res] && pct <= P.upperThr[res]) bal++;
+        const double d = u - P.avgPct[res] * cap;
+        var += d * d;
+      }
+    }
+    out->numBalanced[res] = bal;
+    out->resAvg[res] = P.clusterUtil[res] / na;
+    out->resMax[res] = hot;
+    out->resMin[res] = cold;
+    out->resStd[res] = std::sqrt(var / na);
+  }
+  {
+    double s = 0;
+    for (int b = 0; b < B; ++b)
+      if (e.bAlive[b] && aa[b]) s += e.bPot[b];
+    const double avgPct = s / P.potCapacity;
+    double hot = 0, cold = 1.7976931348623157e308, var = 0;
+    int under = 0;
+    for (int b = 0; b < B; ++b) {
+      if (!e.bAlive[b]) continue;
+      const double u = e.bPot[b], cap = e.bCap[(size_t)2 * B + b];
+      hot = u > hot ? u : hot;
+      cold = u < cold ? u : cold;
+      if (aa[b]) {
+        if (u / cap <= P.nwOutCapThreshold) under++;
+        const double d = u - avgPct * cap;
+        var += d * d;
+      }
+    }
+    out->pnwAvg = s / na;
+    out->pnwMax = hot;
+    out->pnwMin = cold;
+    out->pnwStd = std::sqrt(var / na);
+    out->numUnderPot = under;
+  }
+  for (int which = 0; which < 2; ++which) {
+    const std::vector<int32_t>& cnt = which == 0 ? e.bNrep : e.bNlead;
+    int total = 0, mx = 0, mn = 0x7fffffff;
+    for (int b = 0; b < B; ++b) {
+      total += cnt[b];
+      mx = cnt[b] > mx ? cnt[b] : mx;
+      mn = cnt[b] < mn ? cnt[b] : mn;
+    }
+    const double avg = (double)total / na;
+    double var = 0;
+    for (int b = 0; b < B; ++b)
+      if (e.bAlive[b] && aa[b]) {
+        const double d = (double)cnt[b] - avg;
+        var += (d * d) / na;
+      }
+    if (which == 0) {
+      out->repAvg = avg;
+      out->repStd = std::sqrt(var);
+      out->repMax = mx;
+      out->repMin = mn;
+    } else {
+      out->leadAvg = avg;
+      out->leadStd = std::sqrt(var);
+      out->leadMax = mx;
+      out->leadMin = mn;
+    }
+  }
+  double avgSum = 0, sdSum = 0;
+  int tmx = 0, tmn = 0x7fffffff;
+  for (int t = 0; t < P.T; ++t) {
+    const double avg = (double)e.topicNrep[t] / na;
+    double var = 0;
+    int mx = 0, mn = 0x7fffffff;
+    for (int b = 0; b < B; ++b) {
+      const int n = e.topicCount[(size_t)t * ldB_ + b];
+      mx = n > mx ? n : mx;
+      mn = n < mn ? n : mn;
+      if (aa[b]) {
+        const double d = n - avg;
+        var += (d * d) / na;
+      }
+    }
+    avgSum += avg;
+    sdSum += std::sqrt(var);
+    tmx = mx > tmx ? mx : tmx;
+    tmn = mn < tmn ? mn : tmn;
+  }
+  out->topicAvg = avgSum / P.T;
+  out->topicStd = sdSum / P.T;
+  out->topicMax = tmx;
+  out->topicMin = tmn;
+}
+
+}  // namespace ccmi

@@ -1,0 +1,179 @@
+"""ctypes binding of the CPU oracle (oracle/build/liboracle_cc.so) — TEST INFRASTRUCTURE ONLY.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg use this module, and only as the
+checker / CPU baseline. The product path (cruise-control_amd/) never imports it.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+import sys
+from typing import List, Optional
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "cruise-control_amd"))
+import ccmi  # noqa: E402
+
+ORACLE_DIR = os.path.join(REPO, "oracle")
+ORACLE_LIB = os.path.join(ORACLE_DIR, "build", "liboracle_cc.so")
+
+
+def build_oracle() -> str:
+    if not os.path.exists(ORACLE_LIB) or any(
+            os.path.getmtime(os.path.join(ORACLE_DIR, "src", f)) > os.path.getmtime(ORACLE_LIB)
+            for f in os.listdir(os.path.join(ORACLE_DIR, "src"))):
+        subprocess.run(["make", "-C", ORACLE_DIR, "-j8"], check=True, capture_output=True)
+    return ORACLE_LIB
+
+
+class Oracle:
+    _lib = None
+
+    @classmethod
+    def lib(cls):
+        if cls._lib is None:
+            L = C.CDLL(build_oracle())
+            L.oc_random_cluster.restype = C.c_void_p
+            L.oc_random_cluster.argtypes = [C.POINTER(ccmi.RandomClusterProps)]
+            L.oc_from_desc.restype = C.c_void_p
+            L.oc_from_desc.argtypes = [C.POINTER(ccmi.ClusterDesc)]
+            L.oc_free.argtypes = [C.c_void_p]
+            L.oc_sizes.argtypes = [C.c_void_p, C.POINTER(C.c_int32)]
+            L.oc_topic_name.restype = C.c_char_p
+            L.oc_topic_name.argtypes = [C.c_void_p, C.c_int]
+            L.oc_export.argtypes = [C.c_void_p] + [C.POINTER(C.c_int32)] * 2 + [C.POINTER(C.c_double)] + \
+                [C.POINTER(C.c_int32)] * 6 + [C.POINTER(C.c_uint8)] * 2 + [C.POINTER(C.c_float)]
+            L.oc_optimize.restype = C.c_int
+            L.oc_optimize.argtypes = [C.c_void_p, C.POINTER(C.c_int32), C.c_int, C.POINTER(ccmi.ConstraintStruct),
+                                      C.POINTER(ccmi.OptionsStruct), C.POINTER(ccmi.GoalResultStruct)]
+            L.oc_error.restype = C.c_char_p
+            L.oc_error.argtypes = [C.c_void_p]
+            L.oc_last_seconds.restype = C.c_double
+            L.oc_last_seconds.argtypes = [C.c_void_p]
+            L.oc_candidates.restype = C.c_int64
+            L.oc_candidates.argtypes = [C.c_void_p]
+            L.oc_action_count.restype = C.c_int64
+            L.oc_action_count.argtypes = [C.c_void_p]
+            L.oc_actions.argtypes = [C.c_void_p, C.POINTER(ccmi.ActionStruct)]
+            L.oc_replica_distribution.argtypes = [C.c_void_p, C.POINTER(C.c_int32)]
+            L.oc_leader_distribution.argtypes = [C.c_void_p, C.POINTER(C.c_int32)]
+            L.oc_stats.argtypes = [C.c_void_p, C.POINTER(ccmi.ConstraintStruct), C.POINTER(ccmi.OptionsStruct),
+                                   C.POINTER(ccmi.StatsStruct)]
+            L.oc_proposal_count.restype = C.c_int64
+            L.oc_proposal_count.argtypes = [C.c_void_p]
+            L.oc_proposals.argtypes = [C.c_void_p, C.c_int] + [C.POINTER(C.c_int32)] * 5
+            L.oc_java_random_probe.restype = C.c_int64
+            L.oc_java_random_probe.argtypes = [C.c_int64, C.c_int, C.c_int, C.POINTER(C.c_int32),
+                                               C.POINTER(C.c_double)]
+            L.oc_balance_threshold.restype = C.c_double
+            L.oc_balance_threshold.argtypes = [C.c_double, C.c_int, C.c_double, C.c_double, C.c_double, C.c_int,
+                                               C.c_double, C.c_int]
+            cls._lib = L
+        return cls._lib
+
+
+class OracleCluster:
+    """A CPU-oracle ClusterModel."""
+
+    def __init__(self, handle: int):
+        if not handle:
+            raise RuntimeError("oracle failed to build the cluster")
+        self.h = C.c_void_p(handle)
+        self.L = Oracle.lib()
+        sz = (C.c_int32 * 6)()
+        self.L.oc_sizes(self.h, sz)
+        self.B, self.T, self.P, self.R, self.racks, self.W = list(sz)
+        self.last_results = None
+
+    @staticmethod
+    def random(**overrides) -> "OracleCluster":
+        return OracleCluster(Oracle.lib().oc_random_cluster(C.byref(ccmi.RandomCluster.props(**overrides))))
+
+    @staticmethod
+    def from_desc(desc: ccmi.ClusterDesc) -> "OracleCluster":
+        return OracleCluster(Oracle.lib().oc_from_desc(C.byref(desc)))
+
+    def __del__(self):
+        try:
+            self.L.oc_free(self.h)
+        except Exception:
+            pass
+
+    def export(self) -> dict:
+        B, T, P, R, W = self.B, self.T, self.P, self.R, self.W
+        a = dict(broker_rack=(C.c_int32 * B)(), broker_state=(C.c_int32 * B)(), cap=(C.c_double * (4 * B))(),
+                 partition_topic=(C.c_int32 * P)(), partition_number=(C.c_int32 * P)(),
+                 partition_offset=(C.c_int32 * (P + 1))(), partition_replicas=(C.c_int32 * R)(),
+                 replica_partition=(C.c_int32 * R)(), replica_broker=(C.c_int32 * R)(),
+                 is_leader=(C.c_uint8 * R)(), offline=(C.c_uint8 * R)(), load=(C.c_float * (R * 6 * W))())
+        self.L.oc_export(self.h, a["broker_rack"], a["broker_state"], a["cap"], a["partition_topic"],
+                         a["partition_number"], a["partition_offset"], a["partition_replicas"], a["replica_partition"],
+                         a["replica_broker"], a["is_leader"], a["offline"], a["load"])
+        out = {k: list(v) for k, v in a.items()}
+        out["topics"] = [self.L.oc_topic_name(self.h, t).decode() for t in range(T)]
+        return out
+
+    def optimize(self, goal_names: List[str], constraint: Optional[ccmi.BalancingConstraint] = None,
+                 options: Optional[ccmi.OptimizationOptions] = None):
+        kinds = (C.c_int32 * len(goal_names))(*[ccmi.GOAL_KINDS[n] for n in goal_names])
+        res = (ccmi.GoalResultStruct * len(goal_names))()
+        o, keep = (options or ccmi.OptimizationOptions()).to_struct()
+        c = (constraint or ccmi.BalancingConstraint()).to_struct()
+        st = self.L.oc_optimize(self.h, kinds, len(goal_names), C.byref(c), C.byref(o), res)
+        if st != 0:
+            raise ccmi._STATUS.get(st, RuntimeError)(self.L.oc_error(self.h).decode())
+        self.last_results = [ccmi.GoalResult(ccmi.GOAL_NAMES[r.goal_kind], bool(r.succeeded), bool(r.has_diff),
+                                             r.seconds, r.candidates, 0, 0, r.actions, ccmi.stats_to_dict(r.stats))
+                             for r in res]
+        return self.last_results
+
+    def seconds(self) -> float:
+        return self.L.oc_last_seconds(self.h)
+
+    def actions(self) -> List[tuple]:
+        n = self.L.oc_action_count(self.h)
+        buf = (ccmi.ActionStruct * max(1, n))()
+        self.L.oc_actions(self.h, buf)
+        return [(a.type, a.partition, a.source_broker, a.destination_broker, a.destination_partition)
+                for a in buf[:n]]
+
+    def replica_distribution(self) -> List[int]:
+        out = (C.c_int32 * self.R)()
+        self.L.oc_replica_distribution(self.h, out)
+        return list(out)
+
+    def leader_distribution(self) -> List[int]:
+        out = (C.c_int32 * self.P)()
+        self.L.oc_leader_distribution(self.h, out)
+        return list(out)
+
+    def stats(self, constraint=None, options=None) -> dict:
+        s = ccmi.StatsStruct()
+        o, keep = (options or ccmi.OptimizationOptions()).to_struct()
+        c = (constraint or ccmi.BalancingConstraint()).to_struct()
+        self.L.oc_stats(self.h, C.byref(c), C.byref(o), C.byref(s))
+        return ccmi.stats_to_dict(s)
+
+    def proposals(self, max_rf: int = 8) -> List[ccmi.ExecutionProposal]:
+        n = self.L.oc_proposal_count(self.h)
+        if n == 0:
+            return []
+        part, size, old_leader = (C.c_int32 * n)(), (C.c_int32 * n)(), (C.c_int32 * n)()
+        old_r, new_r = (C.c_int32 * (n * max_rf))(), (C.c_int32 * (n * max_rf))()
+        self.L.oc_proposals(self.h, max_rf, part, size, old_leader, old_r, new_r)
+        return [ccmi.ExecutionProposal(part[i], size[i], old_leader[i],
+                                       [x for x in old_r[i * max_rf:(i + 1) * max_rf] if x >= 0],
+                                       [x for x in new_r[i * max_rf:(i + 1) * max_rf] if x >= 0]) for i in range(n)]
+
+
+def desc_arrays(desc: ccmi.ClusterDesc) -> dict:
+    """Flattened desc as python lists (same keys as OracleCluster.export)."""
+    B, P, R, W, T = desc.num_brokers, desc.num_partitions, desc.num_replicas, desc.num_windows, desc.num_topics
+    return dict(broker_rack=desc.broker_rack[:B], broker_state=desc.broker_state[:B],
+                cap=desc.broker_capacity[:4 * B], partition_topic=desc.partition_topic[:P],
+                partition_number=desc.partition_number[:P], partition_offset=desc.partition_offset[:P + 1],
+                partition_replicas=desc.partition_replicas[:R], replica_partition=desc.replica_partition[:R],
+                replica_broker=desc.replica_broker[:R], is_leader=desc.replica_is_leader[:R],
+                offline=desc.replica_offline[:R], load=desc.replica_load[:R * 6 * W],
+                topics=[desc.topic_names[t].decode() for t in range(T)])
