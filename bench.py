@@ -1,0 +1,164 @@
+"""Headline benchmark: candidate moves evaluated/s + proposal wall time (BASELINE.json `metric`).
+
+Workload (BASELINE.json configs[1], the largest single-GPU config): RandomCluster with 20 racks, 1 000 brokers,
+99 999 + 2 000 replicas (R = 101 999), 3 001 topics, W = 1; goals ReplicaDistributionGoal,
+DiskUsageDistributionGoal, NetworkInboundUsageDistributionGoal, NetworkOutboundUsageDistributionGoal,
+CpuUsageDistributionGoal (default priority order), default BalancingConstraint.
+
+A "step" is one full GoalOptimizer.optimizations over that cluster (all five goals, stats after every goal,
+final ExecutionProposals). Each step works on its own device session, uploaded to HBM before the timed region
+starts; the step count K therefore means K independent proposal computations per GPU.
+
+value = reference-equivalent candidate moves evaluated/s summed over all ranks (the candidates the reference's
+first-fit loops would visit), ms_per_step = proposal wall time.
+
+Multi-GPU (torchrun, one process per GPU): every rank runs its own independent what-if proposal request
+(weak scaling, no data-path collective); timing is max over ranks.
+
+Roofline: the dominant kernel is the candidate scan. Its HIP-event duration is measured in a separate
+instrumented pass after the timed region (events on the engine stream); algorithmic bytes = 96 B per
+reference-equivalent candidate. cpu_baseline = the single-threaded C++ restatement
+(oracle/, "port") on one full optimization of the same workload, rank 0 / N = 1 only.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "cruise-control_amd"))
+
+import ccmi  # noqa: E402
+
+C1_PROPS = dict(num_racks=20, num_brokers=1000, num_replicas=99999, num_topics=3000)
+C1_GOALS = ["ReplicaDistributionGoal", "DiskUsageDistributionGoal", "NetworkInboundUsageDistributionGoal",
+            "NetworkOutboundUsageDistributionGoal", "CpuUsageDistributionGoal"]
+BYTES_PER_CANDIDATE = 96
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E (MI355X_MICROARCH.md)
+
+
+def cpu_baseline(buf) -> dict:
+    """The oracle restatement, single thread, one full optimization of the same cluster (rank 0, N=1 only)."""
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    from oracle_binding import OracleCluster
+
+    oc = OracleCluster.from_desc(buf.desc)
+    t0 = time.perf_counter()
+    res = oc.optimize(C1_GOALS, ccmi.BalancingConstraint())
+    dt = time.perf_counter() - t0
+    cands = sum(r.candidates for r in res)
+    return {"value": cands / dt, "unit": "candidate moves evaluated/s", "cores": 1, "kind": "port",
+            "sample": f"one full optimizations() of the C1 workload ({cands} candidates, {len(oc.actions())} actions) "
+                      f"in {dt:.2f} s by the single-threaded C++ restatement (oracle/)",
+            "proposal_wall_s": dt}
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl", init_method="env://")
+    device = local_rank if world > 1 else 0
+    torch.cuda.set_device(device)
+
+    lib = ccmi.Library.get()
+    buf = ccmi.RandomCluster.generate(lib, **C1_PROPS)
+    goals = ccmi.goals_from_names(C1_GOALS)
+    opt = ccmi.GoalOptimizer(ccmi.BalancingConstraint())
+
+    def session():
+        return ccmi.ClusterModel.from_buffers(buf, device=device)
+
+    for _ in range(args.warmup):
+        opt.optimizations(session(), goals)
+
+    sessions = [session() for _ in range(args.steps)]  # cluster resident in HBM before timing starts
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    results = [opt.optimizations(s, goals) for s in sessions]
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+
+    cands = sum(r.candidates for r in results)
+    if world > 1:
+        t = torch.tensor([elapsed, float(cands)], dtype=torch.float64, device=f"cuda:{device}")
+        tmax = t.clone()
+        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+        elapsed, cands = float(tmax[0]), float(t[1])
+
+    # Instrumented pass (outside the timed region): HIP events around every scan kernel on the engine stream.
+    inst = session()
+    inst.set_kernel_timing(True)
+    inst.reset_perf()
+    r_inst = opt.optimizations(inst, goals)
+    perf = inst.perf()
+    scan_avg_ms = perf.scan_kernel_ms / max(1, perf.scan_launches)
+    ref_bytes_per_launch = r_inst.candidates * BYTES_PER_CANDIDATE / max(1, perf.scan_launches)
+    achieved = ref_bytes_per_launch / (scan_avg_ms * 1e-3) / 1e9 if scan_avg_ms > 0 else 0.0
+
+    if rank != 0:
+        dist.destroy_process_group()
+        return
+    first = results[0]
+    line = {
+        "metric": "candidate moves evaluated/s + proposal wall time, 10K brokers/1M replicas",
+        "value": cands / elapsed,
+        "unit": "candidate moves evaluated/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": elapsed * 1e3 / args.steps,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic (RandomCluster restatement, TestConstants seeds)",
+        "config": {"workload": "C1: 1K brokers x 100K replicas, 5 distribution goals (BASELINE configs[1])",
+                   "brokers": buf.desc.num_brokers, "replicas": buf.desc.num_replicas,
+                   "partitions": buf.desc.num_partitions, "topics": buf.desc.num_topics,
+                   "goals": C1_GOALS, "parallelism": f"independent what-if per GPU x{world}"},
+        "proposal_wall_s": elapsed / args.steps,
+        "candidates_per_step": first.candidates,
+        "actions_per_step": len(first.actions),
+        "proposals_per_step": len(first.proposals),
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                     "kernel": "scan (scan_cross/scan_pairs/scan_swap)", "avg_launch_us": scan_avg_ms * 1e3,
+                     "launches_per_step": perf.scan_launches,
+                     "algorithmic_bytes_per_launch": ref_bytes_per_launch,
+                     "stats_avg_launch_us": perf.stats_kernel_ms * 1e3 / max(1, perf.stats_launches),
+                     "stats_bytes_per_launch": perf.stats_bytes / max(1, perf.stats_launches),
+                     "host_syncs_per_step": perf.host_syncs},
+        "cpu_baseline": None,
+    }
+    if world == 1 and not args.no_cpu_baseline:
+        line["cpu_baseline"] = cpu_baseline(buf)
+    print(json.dumps(line))
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -165,7 +165,11 @@ ccmi_cluster_buffers* generateRandomCluster(const ccmi_random_cluster_props& p) 
   }
   o.repOffline.assign(o.repPart.size(), 0);
   // markBrokenBrokers: brokers 0..numDead-1 become DEAD
-  for (int b = 0; b < p.num_dead_brokers; ++b) o.brokerState[b] = CCMI_BROKER_DEAD;
+  // (Broker.setState(DEAD) also overwrites the capacity with DEAD_BROKER_CAPACITY, Broker.java:322-329)
+  for (int b = 0; b < p.num_dead_brokers; ++b) {
+    o.brokerState[b] = CCMI_BROKER_DEAD;
+    for (int k = 0; k < 4; ++k) o.brokerCap[4 * (size_t)b + k] = -1.0;
+  }
   for (auto& s : o.topicStr) o.topicPtr.push_back(s.c_str());
   ccmi_cluster_desc& d = o.desc;
   std::memset(&d, 0, sizeof(d));

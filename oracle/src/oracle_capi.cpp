@@ -189,7 +189,7 @@ void oc_export(void* hv, int32_t* broker_rack, int32_t* broker_state, double* ca
   for (size_t b = 0; b < cm.brokers.size(); ++b) {
     broker_rack[b] = cm.brokers[b].rack;
     broker_state[b] = (int32_t)cm.brokers[b].state;
-    for (int r = 0; r < 4; ++r) cap[4 * b + r] = cm.brokers[b].state == BrokerState::DEAD ? -1.0 : cm.brokers[b].capacity[r];
+    for (int r = 0; r < 4; ++r) cap[4 * b + r] = cm.brokers[b].capacity[r];  // as given at creation (the desc form)
   }
   int off = 0;
   for (size_t p = 0; p < cm.partitions.size(); ++p) {

@@ -1,0 +1,71 @@
+"""Shared parity helpers: run the product library (HIP build, or the test-only emulation) on a golden case and
+compare with the committed fixture and/or a live oracle run on the identical flattened input."""
+import json
+import os
+
+import pytest
+
+import ccmi
+from oracle_binding import OracleCluster
+from test_oracle_kat import check_against_golden
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def golden(name):
+    with open(os.path.join(GOLDEN, f"{name}.json")) as f:
+        return json.load(f)
+
+
+def constraint(balance):
+    bc = ccmi.BalancingConstraint()
+    if balance is not None:
+        bc.set_resource_balance_percentage(balance)
+        bc.set_capacity_threshold(0.8)
+    return bc
+
+
+def run_product(lib, props, goals, balance, device=0):
+    buf = ccmi.RandomCluster.generate(lib, **props)
+    cm = ccmi.ClusterModel.from_buffers(buf, device=device)
+    res = ccmi.GoalOptimizer(constraint(balance)).optimizations(cm, ccmi.goals_from_names(goals))
+    return buf, cm, res
+
+
+def check_product_against_golden(lib, name):
+    g = golden(name)
+    buf, cm, res = run_product(lib, g["props"], g["goals"], g["resource_balance_percentage"])
+    check_against_golden(g, cm.actions(), cm.replica_distribution(), cm.leader_distribution(), res.goal_results,
+                         res.goal_results[-1].stats)
+    return cm, res
+
+
+def compare_stats(a, b, rel=1e-9):
+    for k, v in b.items():
+        got = a[k]
+        for x, y in zip(got if isinstance(got, list) else [got], v if isinstance(v, list) else [v]):
+            assert x == pytest.approx(y, rel=rel, abs=1e-12), k
+
+
+def _key(p):
+    return p.partition, p.partition_size, p.old_leader, tuple(p.old_replicas), tuple(p.new_replicas)
+
+
+def check_product_against_oracle(lib, props, goals, balance=None, device=0):
+    """Live parity: same flattened input into both; action log, final assignment/leaders, per-goal results and
+    every goal's post-optimization ClusterModelStats."""
+    buf, cm, res = run_product(lib, props, goals, balance, device)
+    oc = OracleCluster.from_desc(buf.desc)
+    ores = oc.optimize(goals, constraint(balance))
+    pa, oa = cm.actions(), oc.actions()
+    for i, (x, y) in enumerate(zip(pa, oa)):
+        assert x == y, f"first action mismatch at {i}: {x} vs {y}"
+    assert len(pa) == len(oa)
+    assert cm.replica_distribution() == oc.replica_distribution()
+    assert cm.leader_distribution() == oc.leader_distribution()
+    for r, o in zip(res.goal_results, ores):
+        assert (r.name, r.succeeded, r.candidates, r.actions) == (o.name, o.succeeded, o.candidates, o.actions)
+        compare_stats(r.stats, o.stats)
+    # Set<ExecutionProposal>: order-free
+    assert sorted(map(_key, res.proposals)) == sorted(map(_key, oc.proposals()))
+    return cm, res, oc
