@@ -34,6 +34,10 @@ sys.path.insert(0, os.path.join(REPO, "cruise-control_amd"))
 import ccmi  # noqa: E402
 
 C1_PROPS = dict(num_racks=20, num_brokers=1000, num_replicas=99999, num_topics=3000)
+C2_PROPS = dict(num_racks=100, num_brokers=10000, num_replicas=999999, num_topics=10000)
+WORKLOADS = {"c1": (C1_PROPS, "C1: 1K brokers x 100K replicas, 5 distribution goals (BASELINE configs[1])"),
+             "c2": (C2_PROPS, "C2 sizes: 10K brokers x 1M replicas, the 5 distribution goals (BASELINE configs[2] "
+                              "cluster, C1 goal list)")}
 C1_GOALS = ["ReplicaDistributionGoal", "DiskUsageDistributionGoal", "NetworkInboundUsageDistributionGoal",
             "NetworkOutboundUsageDistributionGoal", "CpuUsageDistributionGoal"]
 BYTES_PER_CANDIDATE = 96
@@ -41,7 +45,8 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E (MI355X_MICROARCH.md)
 
 
 def cpu_baseline(buf) -> dict:
-    """The oracle restatement, single thread, one full optimization of the same cluster (rank 0, N=1 only)."""
+    """The oracle restatement, single thread, one full optimization of the same cluster (rank 0, N=1 only).
+    At C1 this is ~4-9 s of CPU work; at C2 sizes it takes ~20 min, so it is only run for the C1 workload."""
     sys.path.insert(0, os.path.join(REPO, "tests"))
     from oracle_binding import OracleCluster
 
@@ -62,6 +67,7 @@ def main() -> None:
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--workload", choices=sorted(WORKLOADS), default="c1")
     args = ap.parse_args()
 
     import torch
@@ -77,7 +83,8 @@ def main() -> None:
     torch.cuda.set_device(device)
 
     lib = ccmi.Library.get()
-    buf = ccmi.RandomCluster.generate(lib, **C1_PROPS)
+    props, workload_name = WORKLOADS[args.workload]
+    buf = ccmi.RandomCluster.generate(lib, **props)
     goals = ccmi.goals_from_names(C1_GOALS)
     opt = ccmi.GoalOptimizer(ccmi.BalancingConstraint())
 
@@ -135,7 +142,7 @@ def main() -> None:
         "vs_baseline": None,
         "dtype": "f64",
         "data": "synthetic (RandomCluster restatement, TestConstants seeds)",
-        "config": {"workload": "C1: 1K brokers x 100K replicas, 5 distribution goals (BASELINE configs[1])",
+        "config": {"workload": workload_name,
                    "brokers": buf.desc.num_brokers, "replicas": buf.desc.num_replicas,
                    "partitions": buf.desc.num_partitions, "topics": buf.desc.num_topics,
                    "goals": C1_GOALS, "parallelism": f"independent what-if per GPU x{world}"},
@@ -153,7 +160,7 @@ def main() -> None:
                      "host_syncs_per_step": perf.host_syncs},
         "cpu_baseline": None,
     }
-    if world == 1 and not args.no_cpu_baseline:
+    if world == 1 and not args.no_cpu_baseline and args.workload == "c1":
         line["cpu_baseline"] = cpu_baseline(buf)
     print(json.dumps(line))
     if world > 1:

@@ -10,6 +10,7 @@
 #include "engine/device.h"
 #include "engine/engine.h"
 #include "engine/model.h"
+#include "engine/prof.h"
 
 namespace ccmi {
 ccmi_cluster_buffers* generateRandomCluster(const ccmi_random_cluster_props& p);
@@ -216,6 +217,8 @@ ccmi_status ccmi_session_create(int32_t device_ordinal, const ccmi_cluster_desc*
 
 ccmi_status ccmi_session_destroy(ccmi_session* s) {
   return guarded([&] {
+    ccmi::prof().print("session");
+    ccmi::prof() = ccmi::PhaseProf();
     delete s;
     return CCMI_OK;
   });

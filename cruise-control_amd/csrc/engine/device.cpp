@@ -22,8 +22,8 @@ hipError_t launchScanPairs(const DevTables& T, const DevProgram& prog, const int
 hipError_t launchApplyRows(double* bUtil, int32_t* bNrep, int32_t* bNlead, double* bPot, uint8_t* bAlive, int B,
                            const BrokerRow* brows, int nb, double* rUtil, int32_t* rBroker, uint8_t* rFlags, int R,
                            const ReplicaRow* rrows, int nr, const int32_t* pOff, int32_t* pBrokers,
-                           const PartitionRow* prows, int np, int32_t* topicCount, const TopicCountDelta* tdel, int nt,
-                           hipStream_t st);
+                           const PartitionRow* prows, int np, int32_t* topicCount, int ldB, const TopicCountDelta* tdel,
+                           int nt, hipStream_t st);
 hipError_t launchStats(const StatsParams& P, const int32_t* tc, const int32_t* topicNrep, const double* bUtil,
                        const double* bCap, const int32_t* bNrep, const int32_t* bNlead, const double* bPot,
                        const uint8_t* bAlive, const uint8_t* allowedAlive, TopicPartial* scratch, StatsOut* out,
@@ -189,7 +189,7 @@ void Device::launchApply(int nb, int nr, int np, int nt, size_t obr, size_t orr,
   if (nb + nr + np + nt == 0) return;
   hipCheck(launchApplyRows(bUtil_, bNrep_, bNlead_, bPot_, bAlive_, B_, (const BrokerRow*)(dStage_ + obr), nb, rUtil_,
                            rBroker_, rFlags_, R_, (const ReplicaRow*)(dStage_ + orr), nr, pOff_, pBrokers_,
-                           (const PartitionRow*)(dStage_ + opr), np, topicCount_,
+                           (const PartitionRow*)(dStage_ + opr), np, topicCount_, ldB_,
                            (const TopicCountDelta*)(dStage_ + otd), nt, ST),
            "apply_rows");
 }

@@ -8,6 +8,7 @@
 
 #include "device.h"
 #include "predicates.h"
+#include "prof.h"
 
 namespace ccmi {
 
@@ -84,14 +85,17 @@ int64_t Engine::crossScan(GoalImpl& self, int action, const std::vector<int32_t>
   const int K = (int)(reps.size() - r0), N = (int)cands.size();
   if (K <= 0) return -1;
   if (N == 0) return -1;  // every replica visits an empty eligible list
+  PhaseScope ps(PH_DEV_SCAN);
   m.flushToDevice();
   const int64_t key = dev->scanCross(program(self, action), reps.data() + r0, K, cands.data(), N);
+
   candidates += key >= 0 ? key + 1 : (int64_t)K * N;
   return key;
 }
 
 int64_t Engine::pairScan(GoalImpl& self, const std::vector<int32_t>& pr, const std::vector<int32_t>& pb) {
   if (pr.empty()) return -1;
+  PhaseScope ps(PH_DEV_SCAN);
   m.flushToDevice();
   const int64_t key = dev->scanPairs(program(self, DA_LEADERSHIP), pr.data(), pb.data(), (int)pr.size());
   candidates += key >= 0 ? key + 1 : (int64_t)pr.size();
@@ -101,6 +105,7 @@ int64_t Engine::pairScan(GoalImpl& self, const std::vector<int32_t>& pr, const s
 int64_t Engine::swapScan(GoalImpl& self, const std::vector<int32_t>& srcs, const std::vector<int32_t>& cbOff,
                          const std::vector<int32_t>& cbRep) {
   if (srcs.empty() || cbRep.empty()) return -1;
+  PhaseScope ps(PH_DEV_SCAN);
   m.flushToDevice();
   int64_t visited = 0;
   const int64_t key = dev->scanSwap(program(self, DA_SWAP), srcs.data(), (int)srcs.size(), cbOff.data(),
@@ -128,6 +133,7 @@ int Engine::acceptance(int gi, const ccmi_action& a) {
 }
 
 ccmi_cluster_stats Engine::stats() {
+  PhaseScope ps(PH_DEV_STATS);
   m.flushToDevice();
   const int ldB = dev->ldB();
   std::vector<uint8_t> aa(ldB, 0);
@@ -217,6 +223,7 @@ bool Engine::optimizeGoal(std::unique_ptr<GoalImpl> g, ccmi_goal_result* res) {
     if (m.alive(b) && opt.anyExclMove && opt.exclMove[b] && m.nrep(b) > 0) exclWithReplicas = true;
   while (!g->finished) {
     for (int b : g->brokersToBalance(*this)) g->rebalance(*this, b);
+    PhaseScope ps(PH_UPDATE);
     g->update(*this);
   }
   const ccmi_cluster_stats after = stats();
@@ -242,6 +249,29 @@ bool Engine::optimizeGoal(std::unique_ptr<GoalImpl> g, ccmi_goal_result* res) {
 
 // ======================================================================================= ReplicaDistributionGoal
 namespace {
+
+// The drivers' broker PriorityQueues: an OrderedQueue (O(n) build from a maintained order) when no queued
+// broker can change key while queued, otherwise the exact java.util.PriorityQueue emulation.
+template <class Cmp>
+class LiveQueue {
+ public:
+  explicit LiveQueue(Cmp c) : oq_(c), pq_(c) {}
+  void init(int /*capacity*/, bool ordered) { ordered_ = ordered; }
+  bool ordered() const { return ordered_; }
+  void push_sorted(int x) { oq_.sorted().push_back(x); }
+  bool empty() const { return ordered_ ? oq_.empty() : pq_.empty(); }
+  int peek() const { return ordered_ ? oq_.peek() : pq_.peek(); }
+  int poll() { return ordered_ ? oq_.poll() : pq_.poll(); }
+  void add(int x) {
+    if (ordered_) oq_.add(x);
+    else pq_.add(x);
+  }
+
+ private:
+  bool ordered_ = false;
+  OrderedQueue<Cmp> oq_;
+  JavaPQ<Cmp> pq_;
+};
 
 class ReplicaDistribution : public GoalImpl {
  public:
@@ -326,6 +356,7 @@ class ReplicaDistribution : public GoalImpl {
 
   // rebalanceByMovingReplicasOut (:226-276): batches = runs of equal offline status
   bool moveOut(Engine& e, int b) {
+    PhaseScope ps(PH_RDG_OUT);
     Model& m = e.m;
     const bool fix = dg.fixOffline != 0;
     auto cmp = [&m](int x, int y) {
@@ -375,6 +406,7 @@ class ReplicaDistribution : public GoalImpl {
 
   // rebalanceByMovingReplicasIn (:278-340): speculative multi-source batches over the source queue
   bool moveIn(Engine& e, int dest) {
+    PhaseScope ps(PH_RDG_IN);
     Model& m = e.m;
     auto cmp = [&m](int b1, int b2) {
       const int r = jcmpInt(m.bNoff[b2], m.bNoff[b1]);
@@ -597,18 +629,43 @@ class ResourceDistribution : public GoalImpl {
   }
 
   // rebalanceByMovingLoadOut (:779-863)
+  //
+  // The candidate TreeSet (sortedAliveBrokersUnderThreshold, keyed on live utilization) is only materialised
+  // when a second iteration needs it: the first scan's candidate order is the maintained (pct, id) order
+  // filtered by membership, which is exactly the in-order walk of a freshly built tree. The tree is then
+  // built with the entry keys of the two brokers the first move changed, so its structure — and therefore
+  // the stale-key remove/add that follows — is identical to the reference's.
   bool moveOut(Engine& e, int b, int action) {
+    PhaseScope ps(PH_RES_OUT);
     Model& m = e.m;
-    auto cmp = [this, &m](int x, int y) { return cmpBroker(m, x, y); };
+    int ovB[2] = {-1, -1};
+    double ovP[2] = {0, 0};
+    auto key = [&](int x) { return x == ovB[0] ? ovP[0] : (x == ovB[1] ? ovP[1] : m.pct(x, res)); };
+    auto cmp = [&](int x, int y) {
+      const int c = jcmpDouble(key(x), key(y));
+      return c ? c : jcmpInt(m.bId[x], m.bId[y]);
+    };
     RbTreeSet<decltype(cmp)> cand(cmp);
-    for (int x = 0; x < m.B; ++x) {
-      if (!m.alive(x)) continue;
-      if (!fix) {  // aliveBrokersUnderThreshold(resource, upper)
-        if ((res == R_CPU || res == R_DISK) && m.bu(x, res) >= m.cap(x, res) * upperThr) continue;
-        if (res != R_DISK && m.bu(x, res) >= m.cap(x, res) * upperThr) continue;
+    bool built = false;
+    std::vector<uint8_t>& inSet = e.scratchB;
+    inSet.assign(m.B, 0);
+    std::vector<int32_t> inorder;
+    {
+      PhaseScope pi(PH_PQ_INIT);
+      for (int x : m.brokersByPct(res)) {
+        if (!m.alive(x)) continue;
+        if (!fix && m.bu(x, res) >= m.cap(x, res) * upperThr) continue;  // aliveBrokersUnderThreshold
+        inSet[x] = 1;
+        inorder.push_back(x);
       }
-      cand.add(x);
     }
+    auto build = [&]() {
+      PhaseScope pi(PH_PQ_INIT);
+      for (int x = 0; x < m.B; ++x)
+        if (inSet[x]) cand.add(x);
+      ovB[0] = ovB[1] = -1;
+      built = true;
+    };
     const bool lead = action == DA_LEADERSHIP;
     const bool selfHealing = m.numSelfHealing > 0;
     Model::Spec s;
@@ -627,22 +684,26 @@ class ResourceDistribution : public GoalImpl {
     while (z < list.size() && (m.curOffline(list[z]) || m.ru(list[z], res) != 0.0)) ++z;
     list.resize(z);
     const double upperSrc = excluded(b) ? 0 : upperThr;
-    std::vector<int32_t> inorder, cands, pr, pb, fol, elig;
+    std::vector<int32_t> cands, pr, pb, fol, elig;
     std::vector<int32_t> pairOwner;
     size_t i = 0;
+    bool first = true;
     while (i < list.size()) {
       int dst = -1;
       size_t hitIdx = 0;
       if (!lead) {
-        cand.inorder(inorder);
-        e.eligible(inorder, DA_MOVE, cands);
+        {
+          PhaseScope pc(PH_CAND_BUILD);
+          if (!first) cand.inorder(inorder);
+          e.eligible(inorder, DA_MOVE, cands);
+        }
         const int64_t key = e.crossScan(*this, DA_MOVE, list, i, cands);
         if (key < 0) break;
         const int N = (int)cands.size();
         hitIdx = i + (size_t)(key / N);
         dst = cands[key % N];
-        m.relocateReplica(m.rPart[list[hitIdx]], b, dst);
       } else {
+        PhaseScope pc(PH_CAND_BUILD);
         pr.clear();
         pb.clear();
         pairOwner.clear();
@@ -651,7 +712,7 @@ class ResourceDistribution : public GoalImpl {
           m.onlineFollowerBrokers(m.rPart[r], fol);
           inorder.clear();
           for (int fb : fol)
-            if (cand.contains(fb)) inorder.push_back(fb);
+            if (built ? cand.contains(fb) : inSet[fb] != 0) inorder.push_back(fb);
           std::sort(inorder.begin(), inorder.end(), [&](int x, int y) { return cmpBroker(m, x, y) < 0; });
           inorder.erase(std::unique(inorder.begin(), inorder.end()), inorder.end());
           e.eligible(inorder, DA_LEADERSHIP, elig);
@@ -665,12 +726,21 @@ class ResourceDistribution : public GoalImpl {
         if (key < 0) break;
         hitIdx = (size_t)pairOwner[key];
         dst = pb[key];
-        m.relocateLeadership(m.rPart[list[hitIdx]], b, dst);
       }
+      if (!built) {  // entry keys of the two brokers this move changes, for a lazy build of the tree
+        ovB[0] = b;
+        ovP[0] = m.pct(b, res);
+        ovB[1] = dst;
+        ovP[1] = m.pct(dst, res);
+      }
+      if (!lead) m.relocateReplica(m.rPart[list[hitIdx]], b, dst);
+      else m.relocateLeadership(m.rPart[list[hitIdx]], b, dst);
+      first = false;
       if (underUpper(m, b, upperSrc) && !(fix && m.bNoff[b] > 0)) {
         m.clearTracked(b);
         return false;
       }
+      if (!built) build();
       cand.remove(dst);
       if (m.pct(dst, res) < upperThr) cand.add(dst);
       i = hitIdx + 1;
@@ -681,18 +751,31 @@ class ResourceDistribution : public GoalImpl {
 
   // rebalanceByMovingLoadIn (:437-526): speculative multi-candidate-broker batches over the live views
   bool moveIn(Engine& e, int b, int action, bool immOnly) {
+    PhaseScope ps(PH_RES_IN);
     Model& m = e.m;
     if (m.numNew > 0 && !m.isNew(b)) return true;
     const bool followersOnly = e.opt.anyExclLead && e.opt.exclLead[b];
     auto rcmp = [this, &m](int x, int y) { return cmpBroker(m, y, x); };
-    JavaPQ<decltype(rcmp)> pq(rcmp);
+    // SortedReplicas are lazily initialised (SortedReplicas.java:47-193), so registering a candidate broker's
+    // set when it is first polled is equivalent to trackSortedReplicas over all candidates up front.
     int id = -1;
-    for (int c = 0; c < m.B; ++c) {
-      if (!m.alive(c)) continue;
-      if (m.pct(c, res) > (excluded(c) ? 0.0 : lowerThr)) {
-        id = trackCandidates(e, c, 0.0, false, followersOnly, res == R_NW_OUT, immOnly);
-        pq.add(c);
-      }
+    std::vector<int> trackedCb;
+    auto trackCb = [&](int c) {
+      id = trackCandidates(e, c, 0.0, false, followersOnly, res == R_NW_OUT, immOnly);
+      trackedCb.push_back(c);
+    };
+    LiveQueue<decltype(rcmp)> pq(rcmp);
+    {
+      PhaseScope pi(PH_PQ_INIT);
+      const auto& ord = m.brokersByPct(res);
+      auto member = [&](int c) { return m.alive(c) && m.pct(c, res) > (excluded(c) ? 0.0 : lowerThr); };
+      // only b's key changes while brokers are queued (moves go cb -> b, cb polled): exact unless b is queued
+      pq.init(m.B, !member(b));
+      for (auto it = ord.rbegin(); it != ord.rend(); ++it)
+        if (member(*it)) pq.push_sorted(*it);
+      if (!pq.ordered())
+        for (int c = 0; c < m.B; ++c)
+          if (member(c)) pq.add(c);
     }
     std::vector<int32_t> single{b}, cands;
     e.eligible(single, action, cands);
@@ -719,6 +802,7 @@ class ResourceDistribution : public GoalImpl {
       }
       while (!pq.empty() && (segs.empty() || flat.size() < target) && cond()) {
         const int cb = pq.poll();
+        trackCb(cb);
         const auto& v = m.sorted(cb, id);
         segs.push_back({cb, 0, v.size()});
         flat.insert(flat.end(), v.begin(), v.end());
@@ -741,7 +825,7 @@ class ResourceDistribution : public GoalImpl {
       if (action == DA_MOVE) m.relocateReplica(m.rPart[r], hit.cb, b);
       else m.relocateLeadership(m.rPart[r], hit.cb, b);
       if (aboveLower(m, b)) {
-        m.untrackAll(id);
+        for (int c : trackedCb) m.untrack(c, id);
         return false;
       }
       for (size_t t = mi + 1; t < segs.size(); ++t) pq.add(segs[t].cb);  // un-poll speculative brokers
@@ -752,11 +836,12 @@ class ResourceDistribution : public GoalImpl {
         haveCur = true;
       }
     }
-    if (id >= 0) m.untrackAll(id);
+    for (int c : trackedCb) m.untrack(c, id);
     return true;
   }
 
   bool swapCommon(Engine& e, int b, bool out, bool immOnly) {
+    PhaseScope ps(PH_SWAP);
     Model& m = e.m;
     if (!m.alive(b) || (e.opt.anyExclMove && e.opt.exclMove[b])) return true;
     const int srcId = out ? trackCandidates(e, b, 0.0, false, false, res == R_NW_OUT, immOnly)
@@ -769,8 +854,8 @@ class ResourceDistribution : public GoalImpl {
     const bool followersOnly = e.opt.anyExclLead && e.opt.exclLead[b];
     auto cmpUp = [this, &m](int x, int y) { return cmpBroker(m, x, y); };
     auto cmpDown = [this, &m](int x, int y) { return cmpBroker(m, y, x); };
-    JavaPQ<decltype(cmpUp)> pqUp(cmpUp);
-    JavaPQ<decltype(cmpDown)> pqDown(cmpDown);
+    LiveQueue<decltype(cmpUp)> pqUp(cmpUp);
+    LiveQueue<decltype(cmpDown)> pqDown(cmpDown);
     auto pqEmpty = [&]() { return out ? pqUp.empty() : pqDown.empty(); };
     auto pqPoll = [&]() { return out ? pqUp.poll() : pqDown.poll(); };
     auto pqAdd = [&](int x) {
@@ -778,28 +863,46 @@ class ResourceDistribution : public GoalImpl {
       else pqDown.add(x);
     };
     int candId = -1;
-    if (out) {
-      std::vector<int> under, order;
-      for (int x = 0; x < m.B; ++x) {
-        if (!m.alive(x)) continue;
-        if ((res == R_CPU || res == R_DISK) && m.bu(x, res) >= m.cap(x, res) * upperThr) continue;
-        if (res != R_DISK && m.bu(x, res) >= m.cap(x, res) * upperThr) continue;
-        if (m.nrep(x) > 0) under.push_back(x);
-      }
-      javaHashSetOrder(under, order);  // Collectors.toSet()
-      for (int c : order) {
-        candId = trackCandidates(e, c, limit, true, followersOnly, false, immOnly);
-        pqAdd(c);
-      }
-    } else {
-      for (int x = 0; x < m.B; ++x) {
-        if (!m.alive(x)) continue;
-        if ((res == R_CPU || res == R_DISK) && m.bu(x, res) <= m.cap(x, res) * lowerThr) continue;
-        if (res != R_DISK && m.bu(x, res) <= m.cap(x, res) * lowerThr) continue;
-        candId = trackCandidates(e, x, limit, false, followersOnly, res == R_NW_OUT, immOnly);
-        pqAdd(x);
+    {
+      PhaseScope pi(PH_PQ_INIT);
+      // candidates: out = alive brokers under the upper limit hosting replicas (a Collectors.toSet() whose
+      // insertion order does not matter to a PriorityQueue); in = alive brokers above the lower limit
+      auto member = [&](int x) {
+        if (!m.alive(x)) return false;
+        if (out) return !(m.bu(x, res) >= m.cap(x, res) * upperThr) && m.nrep(x) > 0;
+        return !(m.bu(x, res) <= m.cap(x, res) * lowerThr);
+      };
+      // swaps change only b and the polled broker; the ordered form is exact unless b itself is queued
+      const bool ordered = !member(b);
+      const auto& ord = m.brokersByPct(res);
+      if (out) {
+        pqUp.init(m.B, ordered);
+        if (ordered) {
+          for (int x : ord)
+            if (member(x)) pqUp.push_sorted(x);
+        } else {
+          std::vector<int> under, order;
+          for (int x = 0; x < m.B; ++x)
+            if (member(x)) under.push_back(x);
+          javaHashSetOrder(under, order);
+          for (int c : order) pqUp.add(c);
+        }
+      } else {
+        pqDown.init(m.B, ordered);
+        if (ordered) {
+          for (auto it = ord.rbegin(); it != ord.rend(); ++it)
+            if (member(*it)) pqDown.push_sorted(*it);
+        } else {
+          for (int x = 0; x < m.B; ++x)
+            if (member(x)) pqDown.add(x);
+        }
       }
     }
+    // candidate brokers' SortedReplicas are registered when first polled (lazy init, as in moveIn)
+    auto trackCb = [&](int c) {
+      candId = out ? trackCandidates(e, c, limit, true, followersOnly, false, immOnly)
+                   : trackCandidates(e, c, limit, false, followersOnly, res == R_NW_OUT, immOnly);
+    };
     std::vector<int32_t> srcs, cbOff, cbRep, polled;
     size_t target = 4;
     while (!pqEmpty()) {
@@ -809,6 +912,7 @@ class ResourceDistribution : public GoalImpl {
       while (!pqEmpty() && (polled.empty() || polled.size() < target)) {
         const int cb = pqPoll();
         polled.push_back(cb);
+        trackCb(cb);
         const auto& v = m.sorted(cb, candId);
         cbRep.insert(cbRep.end(), v.begin(), v.end());
         cbOff.push_back((int32_t)cbRep.size());

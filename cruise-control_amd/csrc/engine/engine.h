@@ -62,6 +62,7 @@ class Engine {
   Constraint bc{};
   std::vector<std::unique_ptr<GoalImpl>> optimized;  // optimized goals, priority order
   int64_t candidates = 0;
+  std::vector<uint8_t> scratchB;  // per-broker scratch flags for the goal drivers
 
   // one Goal.optimize; throws OptimizationFailure / StateError
   bool optimizeGoal(std::unique_ptr<GoalImpl> g, ccmi_goal_result* res);

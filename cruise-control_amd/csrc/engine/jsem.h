@@ -357,6 +357,36 @@ class JavaPQ {
   std::vector<int> h_;
 };
 
+// A java.util.PriorityQueue whose elements never change key while they are queued polls in ascending
+// comparator order (the heap invariant always holds and the comparator is a total order). OrderedQueue is that
+// queue built in O(n): a cursor over the members presorted by the caller plus a JavaPQ for elements added later.
+// Callers must fall back to JavaPQ when a queued element's key can change (stale-key heap semantics).
+template <class Cmp>
+class OrderedQueue {
+ public:
+  explicit OrderedQueue(Cmp c) : cmp_(c), heap_(c) {}
+  std::vector<int>& sorted() { return s_; }  // members in ascending comparator order, filled before use
+  bool empty() const { return pos_ >= s_.size() && heap_.empty(); }
+  int peek() const {
+    if (heap_.empty()) return s_[pos_];
+    if (pos_ >= s_.size()) return heap_.peek();
+    return cmp_(heap_.peek(), s_[pos_]) < 0 ? heap_.peek() : s_[pos_];
+  }
+  int poll() {
+    if (heap_.empty()) return s_[pos_++];
+    if (pos_ >= s_.size()) return heap_.poll();
+    if (cmp_(heap_.peek(), s_[pos_]) < 0) return heap_.poll();
+    return s_[pos_++];
+  }
+  void add(int x) { heap_.add(x); }
+
+ private:
+  Cmp cmp_;
+  JavaPQ<Cmp> heap_;
+  std::vector<int> s_;
+  size_t pos_ = 0;
+};
+
 // Iteration order of a HashSet<Broker> filled by add() in `ins` order (Broker.hashCode() == id).
 inline void javaHashSetOrder(const std::vector<int>& ins, std::vector<int>& out) {
   unsigned cap = 16;

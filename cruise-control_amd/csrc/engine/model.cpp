@@ -5,6 +5,7 @@
 #include <stdexcept>
 
 #include "device.h"
+#include "prof.h"
 
 namespace ccmi {
 
@@ -125,7 +126,10 @@ void Model::build(const ccmi_cluster_desc& d) {
       if (alive(b)) c += bCap[4 * b + k];
     clusterCap[k] = c;
   }
+  bVer.assign(B, 0);
+  sortedCache.assign(B, {});
   bUtilC.assign((size_t)4 * B, 0.0);
+  bPctC.assign((size_t)4 * B, 0.0);
   rUtilC.assign((size_t)4 * R, 0.0);
   rScoreC.assign((size_t)4 * R, 0.f);
   for (int b = 0; b < B; ++b) refreshBroker(b);
@@ -139,7 +143,44 @@ void Model::build(const ccmi_cluster_desc& d) {
 }
 
 void Model::refreshBroker(int b) {
-  for (int k = 0; k < 4; ++k) bUtilC[4 * b + k] = ops.util(bLoad[b], k);
+  for (int k = 0; k < 4; ++k) {
+    const double u = ops.util(bLoad[b], k), c = cap(b, k);
+    bUtilC[4 * b + k] = u;
+    bPctC[4 * b + k] = c > 0 ? u / c : 1.0;
+    if (ordBuilt_[k] && !ordDirty_[k][b]) {
+      ordDirty_[k][b] = 1;
+      ordDirtyList_[k].push_back(b);
+    }
+  }
+}
+
+const std::vector<int32_t>& Model::brokersByPct(int res) {
+  auto less = [this, res](int x, int y) { return cmpBrokerPct(res, x, y) < 0; };
+  std::vector<int32_t>& ord = ordPct_[res];
+  std::vector<int32_t>& dl = ordDirtyList_[res];
+  std::vector<uint8_t>& df = ordDirty_[res];
+  if (!ordBuilt_[res] || dl.size() * 16 > (size_t)B) {
+    ord.resize(B);
+    for (int b = 0; b < B; ++b) ord[b] = b;
+    std::sort(ord.begin(), ord.end(), less);
+    df.assign(B, 0);
+    dl.clear();
+    ordBuilt_[res] = true;
+    return ord;
+  }
+  if (dl.empty()) return ord;
+  // drop the moved brokers, then merge them back at their new keys: O(B + d log d)
+  size_t w = 0;
+  for (size_t i = 0; i < ord.size(); ++i)
+    if (!df[ord[i]]) ord[w++] = ord[i];
+  ord.resize(w);
+  std::sort(dl.begin(), dl.end(), less);
+  ordScratch_.resize((size_t)B);
+  std::merge(ord.begin(), ord.end(), dl.begin(), dl.end(), ordScratch_.begin(), less);
+  ord.swap(ordScratch_);
+  for (int b : dl) df[b] = 0;
+  dl.clear();
+  return ord;
 }
 void Model::refreshReplica(int r) {
   for (int k = 0; k < 4; ++k) {
@@ -208,6 +249,9 @@ int Model::brokerRemove(int b, int p) {
 }
 
 void Model::relocateReplica(int p, int src, int dst) {
+  PhaseScope ps(PH_RELOCATE);
+  bVer[src]++;
+  bVer[dst]++;
   const int r = brokerRemove(src, p);
   if (r < 0) throw std::runtime_error("Replica is not in the cluster.");
   ops.subAll(cLoad, rLoad[r]);
@@ -230,6 +274,9 @@ void Model::relocateReplica(int p, int src, int dst) {
 }
 
 bool Model::relocateLeadership(int p, int src, int dst) {
+  PhaseScope ps(PH_RELOCATE);
+  bVer[src]++;
+  bVer[dst]++;
   const int sr = replicaOn(p, src);
   if (sr < 0 || !rLeader[sr]) return false;
   const int dr = replicaOn(p, dst);
@@ -396,12 +443,36 @@ const std::vector<int32_t>& Model::sorted(int b, int nameId) {
   for (auto& t : tracked[b])
     if (t.nameId == nameId) {
       if (!t.init) {
+        PhaseScope ps(PH_SORTED_INIT);
         t.init = true;
+        auto& cache = sortedCache[b];
+        for (auto& c : cache)
+          if (c.ver == bVer[b] && c.spec == t.spec) {
+            t.v = c.v;
+            return t.v;
+          }
         t.v.clear();
         for (int r : bRepl[b])
           if (selects(t.spec, r)) t.v.push_back(r);
         const Spec& s = t.spec;
         std::sort(t.v.begin(), t.v.end(), [&](int x, int y) { return cmpReplica(s, x, y) < 0; });
+        SortedCacheEntry* slot = nullptr;
+        for (auto& c : cache)
+          if (c.spec == t.spec || c.ver != bVer[b]) {
+            slot = &c;
+            break;
+          }
+        if (!slot) {
+          if (cache.size() < 4) {
+            cache.emplace_back();
+            slot = &cache.back();
+          } else {
+            slot = &cache[bVer[b] & 3];
+          }
+        }
+        slot->spec = t.spec;
+        slot->ver = bVer[b];
+        slot->v = t.v;
       }
       return t.v;
     }

@@ -119,6 +119,14 @@ class Model {
   std::vector<int32_t> bNlead, bNimm, bNoff;
   std::vector<LoadVec> bLoad, bLnw, bPot;
   std::vector<double> bUtilC;               // cache [B][4] of ops.util(bLoad[b], res)
+  std::vector<double> bPctC;                // cache [B][4] of GoalUtils.utilization: util / cap, 1.0 if cap <= 0
+  // All brokers ordered by (utilization %, id) per resource — the order every utilization-keyed TreeSet /
+  // PriorityQueue of the ResourceDistribution drivers iterates in. Repaired lazily from a dirty list.
+  const std::vector<int32_t>& brokersByPct(int res);
+  int cmpBrokerPct(int res, int x, int y) const {
+    const int c = jcmpDouble(pct(x, res), pct(y, res));
+    return c ? c : jcmpInt(bId[x], bId[y]);
+  }
   // replicas
   std::vector<int32_t> rPart, rBroker, rOrig, rPos;
   std::vector<uint8_t> rLeader, rOrigOff, rInImm, rInOff;
@@ -172,10 +180,7 @@ class Model {
   double cap(int b, int res) const { return bCap[4 * b + res]; }
   double bu(int b, int res) const { return bUtilC[4 * b + res]; }
   double ru(int r, int res) const { return rUtilC[4 * r + res]; }
-  double pct(int b, int res) const {  // GoalUtils.utilization
-    const double c = cap(b, res);
-    return c > 0 ? bu(b, res) / c : 1.0;
-  }
+  double pct(int b, int res) const { return bPctC[4 * b + res]; }  // GoalUtils.utilization (cached)
   int nrep(int b) const { return (int)bRepl[b].size(); }
   bool origOffline(int r) const { return rOrigOff[r] || !alive(rOrig[r]); }
   bool curOffline(int r) const { return (origOffline(r) && rBroker[r] == rOrig[r]) || !alive(rBroker[r]); }
@@ -207,6 +212,12 @@ class Model {
     bool prioOffline = false, prioImmigrants = false;
     int scoreRes = -1;  // -1 none
     bool scoreReverse = false;
+    bool operator==(const Spec& o) const {
+      return selLeaders == o.selLeaders && selFollowers == o.selFollowers && selImmigrants == o.selImmigrants &&
+             selImmOrOffline == o.selImmOrOffline && selAboveRes == o.selAboveRes && selBelowRes == o.selBelowRes &&
+             aboveLimit == o.aboveLimit && belowLimit == o.belowLimit && prioOffline == o.prioOffline &&
+             prioImmigrants == o.prioImmigrants && scoreRes == o.scoreRes && scoreReverse == o.scoreReverse;
+    }
   };
   struct Tracked {
     int nameId;
@@ -215,6 +226,16 @@ class Model {
     std::vector<int32_t> v;
   };
   std::vector<std::vector<Tracked>> tracked;  // per broker
+  // Initial contents of a SortedReplicas depend only on the broker's replicas (set, loads, leadership,
+  // origin) and the Spec; bVer[b] changes whenever any of those change, so an initialisation can be reused
+  // from a cache entry with the same Spec and version instead of re-sorting.
+  struct SortedCacheEntry {
+    Spec spec;
+    uint32_t ver = 0;
+    std::vector<int32_t> v;
+  };
+  std::vector<uint32_t> bVer;
+  std::vector<std::vector<SortedCacheEntry>> sortedCache;  // per broker, a few Specs
   void track(int b, int nameId, const Spec& s);
   void untrackAll(int nameId);
   void untrack(int b, int nameId);
@@ -232,6 +253,9 @@ class Model {
   void brokerAdd(int b, int r);
   int brokerRemove(int b, int p);
   void refreshBroker(int b);
+  std::vector<int32_t> ordPct_[4], ordDirtyList_[4], ordScratch_;
+  std::vector<uint8_t> ordDirty_[4];
+  bool ordBuilt_[4] = {false, false, false, false};
   void refreshReplica(int r);
   void sortedInsert(int b, int r);
   void sortedErase(int b, int r);

@@ -187,7 +187,7 @@ __global__ void apply_rows(double* bUtil, int32_t* bNrep, int32_t* bNlead, doubl
                            const BrokerRow* __restrict__ brows, int nb, double* rUtil, int32_t* rBroker, uint8_t* rFlags,
                            int R, const ReplicaRow* __restrict__ rrows, int nr, const int32_t* __restrict__ pOff,
                            int32_t* pBrokers, const PartitionRow* __restrict__ prows, int np, int32_t* topicCount,
-                           const TopicCountDelta* __restrict__ tdel, int nt) {
+                           int ldB, const TopicCountDelta* __restrict__ tdel, int nt) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i < nb) {
     const BrokerRow& x = brows[i];
@@ -212,7 +212,7 @@ __global__ void apply_rows(double* bUtil, int32_t* bNrep, int32_t* bNlead, doubl
   }
   if (i < nt) {
     const TopicCountDelta& d = tdel[i];
-    atomicAdd(&topicCount[(size_t)d.topic * B + d.broker], d.delta);
+    atomicAdd(&topicCount[(size_t)d.topic * ldB + d.broker], d.delta);
   }
 }
 
@@ -256,8 +256,8 @@ hipError_t launchScanPairs(const DevTables& T, const DevProgram& prog, const int
 hipError_t launchApplyRows(double* bUtil, int32_t* bNrep, int32_t* bNlead, double* bPot, uint8_t* bAlive, int B,
                            const BrokerRow* brows, int nb, double* rUtil, int32_t* rBroker, uint8_t* rFlags, int R,
                            const ReplicaRow* rrows, int nr, const int32_t* pOff, int32_t* pBrokers,
-                           const PartitionRow* prows, int np, int32_t* topicCount, const TopicCountDelta* tdel, int nt,
-                           hipStream_t st) {
+                           const PartitionRow* prows, int np, int32_t* topicCount, int ldB, const TopicCountDelta* tdel,
+                           int nt, hipStream_t st) {
   int n = nb;
   if (nr > n) n = nr;
   if (np > n) n = np;
@@ -266,7 +266,7 @@ hipError_t launchApplyRows(double* bUtil, int32_t* bNrep, int32_t* bNlead, doubl
   const int threads = 256;
   const int blocks = (n + threads - 1) / threads;
   hipLaunchKernelGGL(apply_rows, dim3(blocks), dim3(threads), 0, st, bUtil, bNrep, bNlead, bPot, bAlive, B, brows, nb,
-                     rUtil, rBroker, rFlags, R, rrows, nr, pOff, pBrokers, prows, np, topicCount, tdel, nt);
+                     rUtil, rBroker, rFlags, R, rrows, nr, pOff, pBrokers, prows, np, topicCount, ldB, tdel, nt);
   return hipGetLastError();
 }
 

@@ -67,13 +67,16 @@ def test_gpu_sessions_are_independent(gpu_lib, oracle_lib):
 
 
 def test_gpu_acceptance_after_optimization(gpu_lib):
-    """Goal.actionAcceptance through the C ABI: a move onto a broker already hosting the partition is not a
-    legit move, but acceptance is only the goal predicate; index out of range is IllegalArgument."""
+    """Goal.actionAcceptance through the C ABI on the optimized goals of a session; an out-of-range goal index
+    is an IllegalArgumentException."""
     buf = ccmi.RandomCluster.generate(gpu_lib, num_racks=5, num_brokers=20, num_replicas=6000, num_topics=300)
     cm = ccmi.ClusterModel.from_buffers(buf, device=0)
-    ccmi.GoalOptimizer(constraint(1.05)).optimizations(cm, ccmi.goals_from_names(["ReplicaDistributionGoal"]))
+    ccmi.GoalOptimizer(constraint(1.05)).optimizations(cm, ccmi.goals_from_names(C1_GOALS))
     with pytest.raises(ccmi.IllegalArgumentException):
-        cm.action_acceptance(3, 0, 0, 0, 1)
-    # applying the reverse of the last accepted move is always judged by the (frozen) goal bounds
-    last = cm.actions()[-1]
-    assert cm.action_acceptance(0, last[0], last[1], last[3], last[2]) in ccmi.ACCEPTANCE
+        cm.action_acceptance(len(C1_GOALS), 0, 0, 0, 1)
+    acts = cm.actions()
+    assert acts
+    for gi in range(len(C1_GOALS)):
+        for a in acts[-5:]:
+            # the reverse of an applied action is a legal question to ask every optimized goal
+            assert cm.action_acceptance(gi, a[0], a[1], a[3], a[2]) in ccmi.ACCEPTANCE

@@ -1,6 +1,7 @@
 #!/bin/bash
-# One GPU-box pass: smoke, GPU parity tests, bench, rocprofv3 kernel-trace summary.
+# One GPU-box pass: smoke, GPU parity tests, bench, optional rocprofv3 kernel-trace summary and PMC passes.
 # Every GPU step has its own time limit; a crash/abort/timeout (anything but pass/fail) stops the script.
+#   env: PYTEST_ARGS, BENCH_ARGS, PROFILE=1, PMC=1, C2=1, SKIP_TESTS=1
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out
 step() {  # step <name> <seconds> <cmd...>
@@ -9,15 +10,27 @@ step() {  # step <name> <seconds> <cmd...>
   timeout -k 10 "$secs" "$@" > "gpurun_out/$name.log" 2>&1
   local rc=$?
   echo "== $name rc=$rc"
-  tail -5 "gpurun_out/$name.log"
+  tail -4 "gpurun_out/$name.log"
   if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stopping: $name exited $rc"; exit $rc; fi
   return $rc
 }
 make -C cruise-control_amd -j16 > gpurun_out/make.log 2>&1 && make -C oracle -j16 >> gpurun_out/make.log 2>&1 || exit 1
-step smoke 400 python -c "import __graft_entry__ as g; g.smoke()"
-step pytest_gpu 900 python -m pytest tests -m gpu -x -q ${PYTEST_ARGS:-}
+if [ -z "${SKIP_TESTS:-}" ]; then
+  step smoke 400 python -c "import __graft_entry__ as g; g.smoke()"
+  step pytest_gpu 900 python -m pytest tests -m gpu -x -q ${PYTEST_ARGS:-}
+fi
 step bench 600 python bench.py ${BENCH_ARGS:-}
 if [ -n "${PROFILE:-}" ]; then
-  step rocprof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o bench -- python3 bench.py --no-cpu-baseline --steps 2 --warmup 1
+  step rocprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o bench -- \
+    python3 bench.py --no-cpu-baseline --steps 2 --warmup 1
+fi
+if [ -n "${PMC:-}" ]; then
+  step pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc_fetch -o bench -- \
+    python3 bench.py --no-cpu-baseline --steps 1 --warmup 0
+  step pmc_write 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc_write -o bench -- \
+    python3 bench.py --no-cpu-baseline --steps 1 --warmup 0
+fi
+if [ -n "${C2:-}" ]; then
+  step bench_c2 900 python bench.py --workload c2 --steps 1 --warmup 0
 fi
 exit 0
