@@ -630,17 +630,22 @@ class ResourceDistribution : public GoalImpl {
 
   // rebalanceByMovingLoadOut (:779-863)
   //
-  // The candidate TreeSet (sortedAliveBrokersUnderThreshold, keyed on live utilization) is only materialised
-  // when a second iteration needs it: the first scan's candidate order is the maintained (pct, id) order
-  // filtered by membership, which is exactly the in-order walk of a freshly built tree. The tree is then
-  // built with the entry keys of the two brokers the first move changed, so its structure — and therefore
-  // the stale-key remove/add that follows — is identical to the reference's.
+  // The candidate TreeSet (sortedAliveBrokersUnderThreshold, keyed on LIVE utilization) is emulated without
+  // materialising it while that is provably exact: its in-order walk is the maintained (pct, id) order
+  // filtered by membership, and TreeMap.remove(dst) after dst's key moved from k to k' finds dst's node
+  // whenever no other member's key lies strictly between k and k' (every ancestor then sends the search for
+  // k' the same way it sent k). When that does not hold, the exact tree is built by replaying the entry
+  // state and every remove/add so far with the keys each broker had at that time, and the reference's
+  // stale-key behaviour follows from the real structure.
   bool moveOut(Engine& e, int b, int action) {
     PhaseScope ps(PH_RES_OUT);
     Model& m = e.m;
-    int ovB[2] = {-1, -1};
-    double ovP[2] = {0, 0};
-    auto key = [&](int x) { return x == ovB[0] ? ovP[0] : (x == ovB[1] ? ovP[1] : m.pct(x, res)); };
+    std::vector<std::pair<int, double>> ovr;  // brokers whose key differs from the live one during a replay
+    auto key = [&](int x) {
+      for (const auto& o : ovr)
+        if (o.first == x) return o.second;
+      return m.pct(x, res);
+    };
     auto cmp = [&](int x, int y) {
       const int c = jcmpDouble(key(x), key(y));
       return c ? c : jcmpInt(m.bId[x], m.bId[y]);
@@ -659,12 +664,53 @@ class ResourceDistribution : public GoalImpl {
         inorder.push_back(x);
       }
     }
-    auto build = [&]() {
-      PhaseScope pi(PH_PQ_INIT);
+    struct Step {
+      int dst;
+      double keyAfter;
+      bool add;
+    };
+    std::vector<Step> hist;
+    std::vector<std::pair<int, double>> entryKey;  // pct at entry of every broker a move changed
+    std::vector<uint8_t> entryIn;
+    auto noteEntry = [&](int x) {
+      for (const auto& o : entryKey)
+        if (o.first == x) return;
+      entryKey.push_back({x, m.pct(x, res)});
+    };
+    auto materialise = [&]() {
+      PhaseScope pi(PH_TREE_BUILD);
+      ovr = entryKey;
       for (int x = 0; x < m.B; ++x)
-        if (inSet[x]) cand.add(x);
-      ovB[0] = ovB[1] = -1;
+        if (entryIn[x]) cand.add(x);
+      for (const Step& h : hist) {
+        for (auto& o : ovr)
+          if (o.first == h.dst) o.second = h.keyAfter;
+        cand.remove(h.dst);
+        if (h.add) cand.add(h.dst);
+      }
+      ovr.clear();
       built = true;
+    };
+    // b's own key changes with every move: if b is a member the lazy form does not apply
+    if (inSet[b]) {
+      entryIn = inSet;
+      materialise();
+    } else {
+      entryIn = inSet;
+    }
+    auto memberBetween = [&](int dst, double k0, double k1) {
+      // is a member other than dst strictly between (k0, id(dst)) and (k1, id(dst)) in (pct, id) order?
+      const double lo = jcmpDouble(k0, k1) <= 0 ? k0 : k1, hi = jcmpDouble(k0, k1) <= 0 ? k1 : k0;
+      const int id = m.bId[dst];
+      auto cmpKey = [&](int x, double k) {
+        const int c = jcmpDouble(m.pct(x, res), k);
+        return c ? c : jcmpInt(m.bId[x], id);
+      };
+      const auto& ord = m.brokersByPct(res);
+      auto it = std::partition_point(ord.begin(), ord.end(), [&](int x) { return cmpKey(x, lo) <= 0; });
+      for (; it != ord.end() && cmpKey(*it, hi) < 0; ++it)
+        if (*it != dst && inSet[*it]) return true;
+      return false;
     };
     const bool lead = action == DA_LEADERSHIP;
     const bool selfHealing = m.numSelfHealing > 0;
@@ -694,7 +740,13 @@ class ResourceDistribution : public GoalImpl {
       if (!lead) {
         {
           PhaseScope pc(PH_CAND_BUILD);
-          if (!first) cand.inorder(inorder);
+          if (built) {
+            cand.inorder(inorder);
+          } else if (!first) {
+            inorder.clear();
+            for (int x : m.brokersByPct(res))
+              if (inSet[x]) inorder.push_back(x);
+          }
           e.eligible(inorder, DA_MOVE, cands);
         }
         const int64_t key = e.crossScan(*this, DA_MOVE, list, i, cands);
@@ -727,11 +779,10 @@ class ResourceDistribution : public GoalImpl {
         hitIdx = (size_t)pairOwner[key];
         dst = pb[key];
       }
-      if (!built) {  // entry keys of the two brokers this move changes, for a lazy build of the tree
-        ovB[0] = b;
-        ovP[0] = m.pct(b, res);
-        ovB[1] = dst;
-        ovP[1] = m.pct(dst, res);
+      const double dstBefore = m.pct(dst, res);
+      if (!built) {
+        noteEntry(b);
+        noteEntry(dst);
       }
       if (!lead) m.relocateReplica(m.rPart[list[hitIdx]], b, dst);
       else m.relocateLeadership(m.rPart[list[hitIdx]], b, dst);
@@ -740,9 +791,19 @@ class ResourceDistribution : public GoalImpl {
         m.clearTracked(b);
         return false;
       }
-      if (!built) build();
+      const bool add = m.pct(dst, res) < upperThr;
+      if (!built) {
+        if (memberBetween(dst, dstBefore, m.pct(dst, res))) {
+          materialise();
+        } else {  // the removal finds dst's node: the set stays clean
+          hist.push_back({dst, m.pct(dst, res), add});
+          inSet[dst] = add ? 1 : 0;
+          i = hitIdx + 1;
+          continue;
+        }
+      }
       cand.remove(dst);
-      if (m.pct(dst, res) < upperThr) cand.add(dst);
+      if (add) cand.add(dst);
       i = hitIdx + 1;
     }
     m.clearTracked(b);

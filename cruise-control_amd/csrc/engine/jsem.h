@@ -94,6 +94,38 @@ class RbTreeSet {
     ++size_;
     return true;
   }
+  // Insert `ids` in order into an EMPTY tree whose comparator agrees with `rank` (distinct ranks) on these
+  // elements: the same sequence of TreeMap.put calls and therefore the same structure, with integer compares.
+  void buildByRank(const std::vector<int>& ids, const std::vector<int32_t>& rank) {
+    const size_t n = ids.size();
+    key_.reserve(n);
+    left_.reserve(n);
+    right_.reserve(n);
+    parent_.reserve(n);
+    red_.reserve(n);
+    nodeRank_.resize(n);
+    for (int k : ids) {
+      const int32_t rk = rank[k];
+      if (root_ < 0) {
+        root_ = alloc(k, -1);
+        nodeRank_[root_] = rk;
+        size_ = 1;
+        continue;
+      }
+      int t = root_, parent = -1;
+      bool goLeft = false;
+      while (t >= 0) {
+        parent = t;
+        goLeft = rk < nodeRank_[t];
+        t = goLeft ? left_[t] : right_[t];
+      }
+      const int e = alloc(k, parent);
+      nodeRank_[e] = rk;
+      (goLeft ? left_[parent] : right_[parent]) = e;
+      insertFix(e);
+      ++size_;
+    }
+  }
   bool remove(int k) {
     int p = find(k);
     if (p < 0) return false;
@@ -112,6 +144,7 @@ class RbTreeSet {
  private:
   Cmp cmp_;
   std::vector<int> key_, left_, right_, parent_;
+  std::vector<int32_t> nodeRank_;  // buildByRank only
   std::vector<uint8_t> red_;
   std::vector<int> free_;
   int root_ = -1, size_ = 0;

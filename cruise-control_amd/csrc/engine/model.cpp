@@ -155,11 +155,12 @@ void Model::refreshBroker(int b) {
 }
 
 const std::vector<int32_t>& Model::brokersByPct(int res) {
+  PhaseScope ps(PH_ORDER);
   auto less = [this, res](int x, int y) { return cmpBrokerPct(res, x, y) < 0; };
   std::vector<int32_t>& ord = ordPct_[res];
   std::vector<int32_t>& dl = ordDirtyList_[res];
   std::vector<uint8_t>& df = ordDirty_[res];
-  if (!ordBuilt_[res] || dl.size() * 16 > (size_t)B) {
+  if (!ordBuilt_[res]) {
     ord.resize(B);
     for (int b = 0; b < B; ++b) ord[b] = b;
     std::sort(ord.begin(), ord.end(), less);
@@ -169,15 +170,20 @@ const std::vector<int32_t>& Model::brokersByPct(int res) {
     return ord;
   }
   if (dl.empty()) return ord;
-  // drop the moved brokers, then merge them back at their new keys: O(B + d log d)
+  // drop the moved brokers (one compaction pass), then put them back at their new keys: binary-search
+  // insertion for a few, a merge for many
   size_t w = 0;
   for (size_t i = 0; i < ord.size(); ++i)
     if (!df[ord[i]]) ord[w++] = ord[i];
   ord.resize(w);
-  std::sort(dl.begin(), dl.end(), less);
-  ordScratch_.resize((size_t)B);
-  std::merge(ord.begin(), ord.end(), dl.begin(), dl.end(), ordScratch_.begin(), less);
-  ord.swap(ordScratch_);
+  if (dl.size() <= 16) {
+    for (int b : dl) ord.insert(std::lower_bound(ord.begin(), ord.end(), b, less), b);
+  } else {
+    std::sort(dl.begin(), dl.end(), less);
+    ordScratch_.resize((size_t)B);
+    std::merge(ord.begin(), ord.end(), dl.begin(), dl.end(), ordScratch_.begin(), less);
+    ord.swap(ordScratch_);
+  }
   for (int b : dl) df[b] = 0;
   dl.clear();
   return ord;
@@ -445,17 +451,19 @@ const std::vector<int32_t>& Model::sorted(int b, int nameId) {
       if (!t.init) {
         PhaseScope ps(PH_SORTED_INIT);
         t.init = true;
+        t.owned = false;
         auto& cache = sortedCache[b];
         for (auto& c : cache)
           if (c.ver == bVer[b] && c.spec == t.spec) {
-            t.v = c.v;
-            return t.v;
+            t.shared = c.v;
+            return t.view();
           }
-        t.v.clear();
+        auto v = std::make_shared<std::vector<int32_t>>();
         for (int r : bRepl[b])
-          if (selects(t.spec, r)) t.v.push_back(r);
+          if (selects(t.spec, r)) v->push_back(r);
         const Spec& s = t.spec;
-        std::sort(t.v.begin(), t.v.end(), [&](int x, int y) { return cmpReplica(s, x, y) < 0; });
+        std::sort(v->begin(), v->end(), [&](int x, int y) { return cmpReplica(s, x, y) < 0; });
+        t.shared = v;
         SortedCacheEntry* slot = nullptr;
         for (auto& c : cache)
           if (c.spec == t.spec || c.ver != bVer[b]) {
@@ -472,9 +480,9 @@ const std::vector<int32_t>& Model::sorted(int b, int nameId) {
         }
         slot->spec = t.spec;
         slot->ver = bVer[b];
-        slot->v = t.v;
+        slot->v = t.shared;
       }
-      return t.v;
+      return t.view();
     }
   throw std::runtime_error("sorted replicas not tracked");
 }
@@ -483,17 +491,27 @@ void Model::sortedInsert(int b, int r) {
   for (auto& t : tracked[b]) {
     if (!t.init || !selects(t.spec, r)) continue;
     const Spec& s = t.spec;
-    auto it = std::lower_bound(t.v.begin(), t.v.end(), r, [&](int x, int y) { return cmpReplica(s, x, y) < 0; });
-    if (it != t.v.end() && cmpReplica(s, *it, r) == 0) continue;  // TreeSet.add of an equal element
-    t.v.insert(it, r);
+    auto less = [&](int x, int y) { return cmpReplica(s, x, y) < 0; };
+    const auto& cv = t.view();
+    auto cit = std::lower_bound(cv.begin(), cv.end(), r, less);
+    if (cit != cv.end() && cmpReplica(s, *cit, r) == 0) continue;  // TreeSet.add of an equal element
+    const size_t pos = (size_t)(cit - cv.begin());
+    auto& v = t.mut();
+    v.insert(v.begin() + pos, r);
   }
 }
 void Model::sortedErase(int b, int r) {
   for (auto& t : tracked[b]) {
     if (!t.init) continue;
     const Spec& s = t.spec;
-    auto it = std::lower_bound(t.v.begin(), t.v.end(), r, [&](int x, int y) { return cmpReplica(s, x, y) < 0; });
-    if (it != t.v.end() && *it == r) t.v.erase(it);
+    auto less = [&](int x, int y) { return cmpReplica(s, x, y) < 0; };
+    const auto& cv = t.view();
+    auto cit = std::lower_bound(cv.begin(), cv.end(), r, less);
+    if (cit != cv.end() && *cit == r) {
+      const size_t pos = (size_t)(cit - cv.begin());
+      auto& v = t.mut();
+      v.erase(v.begin() + pos);
+    }
   }
 }
 

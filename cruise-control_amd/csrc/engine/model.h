@@ -223,7 +223,18 @@ class Model {
     int nameId;
     Spec spec;
     bool init = false;
-    std::vector<int32_t> v;
+    std::shared_ptr<const std::vector<int32_t>> shared;  // initial contents shared with the cache
+    std::vector<int32_t> own;                            // private copy once the live view diverges
+    bool owned = false;
+    const std::vector<int32_t>& view() const { return owned ? own : *shared; }
+    std::vector<int32_t>& mut() {
+      if (!owned) {
+        own = *shared;
+        owned = true;
+        shared.reset();
+      }
+      return own;
+    }
   };
   std::vector<std::vector<Tracked>> tracked;  // per broker
   // Initial contents of a SortedReplicas depend only on the broker's replicas (set, loads, leadership,
@@ -232,7 +243,7 @@ class Model {
   struct SortedCacheEntry {
     Spec spec;
     uint32_t ver = 0;
-    std::vector<int32_t> v;
+    std::shared_ptr<const std::vector<int32_t>> v;
   };
   std::vector<uint32_t> bVer;
   std::vector<std::vector<SortedCacheEntry>> sortedCache;  // per broker, a few Specs

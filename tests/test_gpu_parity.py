@@ -76,7 +76,7 @@ def test_gpu_acceptance_after_optimization(gpu_lib):
         cm.action_acceptance(len(C1_GOALS), 0, 0, 0, 1)
     acts = cm.actions()
     assert acts
+    a = acts[-1]
     for gi in range(len(C1_GOALS)):
-        for a in acts[-5:]:
-            # the reverse of an applied action is a legal question to ask every optimized goal
-            assert cm.action_acceptance(gi, a[0], a[1], a[3], a[2]) in ccmi.ACCEPTANCE
+        # the reverse of the last applied action is a legal question to ask every optimized goal
+        assert cm.action_acceptance(gi, a[0], a[1], a[3], a[2]) in ccmi.ACCEPTANCE
