@@ -12,18 +12,22 @@ namespace ccmi {
 #define EV0 ((hipEvent_t)ev0_)
 #define EV1 ((hipEvent_t)ev1_)
 
-hipError_t launchScanCross(const DevTables& T, const DevProgram& prog, const int32_t* reps, const int32_t* cands, int K,
-                           int N, unsigned long long* result, hipStream_t st);
+hipError_t launchScanCross(const DevTables& T, const MutTables& M, const UpdateList& U, const DevProgram& prog,
+                           const int32_t* reps, const int32_t* cands, int K, int N, unsigned long long* result,
+                           unsigned int* done, unsigned long long* mail, unsigned long long seq, hipStream_t st);
 hipError_t launchScanSwap(const DevTables& T, const DevProgram& prog, const int32_t* srcs, int S, const int32_t* cbOff,
-                          const int32_t* cbRep, int M, unsigned long long* result, int32_t* rowVisited, hipStream_t st,
-                          hipEvent_t ev0, hipEvent_t ev1);
-hipError_t launchScanPairs(const DevTables& T, const DevProgram& prog, const int32_t* pr, const int32_t* pb, int n,
-                           unsigned long long* result, hipStream_t st);
-hipError_t launchApplyRows(double* bUtil, int32_t* bNrep, int32_t* bNlead, double* bPot, uint8_t* bAlive, int B,
-                           const BrokerRow* brows, int nb, double* rUtil, int32_t* rBroker, uint8_t* rFlags, int R,
-                           const ReplicaRow* rrows, int nr, const int32_t* pOff, int32_t* pBrokers,
-                           const PartitionRow* prows, int np, int32_t* topicCount, int ldB, const TopicCountDelta* tdel,
-                           int nt, hipStream_t st);
+                          const int32_t* cbRep, int M, unsigned long long* result, int32_t* rowVisited,
+                          unsigned long long* mail, unsigned long long seq, hipStream_t st, hipEvent_t ev0,
+                          hipEvent_t ev1);
+hipError_t launchScanPairs(const DevTables& T, const MutTables& M, const UpdateList& U, const DevProgram& prog,
+                           const int32_t* pr, const int32_t* pb, int n, unsigned long long* result, unsigned int* done,
+                           unsigned long long* mail, unsigned long long seq, hipStream_t st);
+hipError_t launchPrep(double* bUtil, int32_t* bNrep, int32_t* bNlead, double* bPot, uint8_t* bAlive, int B,
+                      const BrokerRow* brows, int nb, double* rUtil, int32_t* rBroker, uint8_t* rFlags, int R,
+                      const ReplicaRow* rrows, int nr, const int32_t* pOff, int32_t* pBrokers,
+                      const PartitionRow* prows, int np, int32_t* topicCount, int ldB, const TopicCountDelta* tdel,
+                      int nt, const int4* req, int4* dReq, int nReq4, unsigned long long* result, unsigned int* done,
+                      hipStream_t st);
 hipError_t launchStats(const StatsParams& P, const int32_t* tc, const int32_t* topicNrep, const double* bUtil,
                        const double* bCap, const int32_t* bNrep, const int32_t* bNlead, const double* bPot,
                        const uint8_t* bAlive, const uint8_t* allowedAlive, TopicPartial* scratch, StatsOut* out,
@@ -68,11 +72,19 @@ Device::Device(int ordinal, int B, int R, int P, int T, int maxGoalSlots)
   dalloc(&pBrokers_, R);
   dalloc(&topicCount_, (size_t)T * ldB_);
   dalloc(&topicNrep_, T);
+  dalloc(&dResult_, 4);
+  dalloc(&dDone_, 4);
   hipCheck(hipMalloc(&topicScratch_, (size_t)(T ? T : 1) * sizeof(TopicPartial)), "hipMalloc");
   hipCheck(hipMalloc(&statsOut_, 1024), "hipMalloc");
   hipCheck(hipMemset(allowed_, 0, (size_t)G_ * B), "hipMemset");
-  hipCheck(hipHostMalloc((void**)&hResult_, 1024, hipHostMallocDefault), "hipHostMalloc");
+  hipCheck(hipMemset(dDone_, 0, 4 * sizeof(unsigned int)), "hipMemset");
+  hipCheck(hipMemset(dResult_, 0xff, 2 * sizeof(unsigned long long)), "hipMemset");
+  // host-coherent (fine-grained) mapped memory: kernels read the staging area and write the mailbox directly
+  hipCheck(hipHostMalloc((void**)&hResult_, 1024, hipHostMallocMapped | hipHostMallocCoherent), "hipHostMalloc");
+  hipCheck(hipHostGetDevicePointer((void**)&hResultDev_, hResult_, 0), "hipHostGetDevicePointer");
+  std::memset(hResult_, 0, 1024);
   ensureStage(1 << 20);
+  ensureReq(1 << 20);
   hipCheck(hipEventCreate((hipEvent_t*)&ev0_), "hipEventCreate");
   hipCheck(hipEventCreate((hipEvent_t*)&ev1_), "hipEventCreate");
 }
@@ -81,8 +93,8 @@ Device::~Device() {
   (void)hipSetDevice(ordinal_);
   if (ST) (void)hipStreamSynchronize(ST);
   void* ps[] = {bUtil_, bCap_, bPot_, bNrep_, bNlead_, bAlive_, allowed_, allowedAlive_, rUtil_, rPart_, rBroker_,
-                rOrig_, rFlags_, pOff_, pBrokers_, topicCount_, topicNrep_, topicScratch_, statsOut_, dStage_,
-                rowVisited_};
+                rOrig_, rFlags_, pOff_, pBrokers_, topicCount_, topicNrep_, topicScratch_, statsOut_, dReq_,
+                rowVisited_, dResult_, dDone_};
   for (void* p : ps)
     if (p) (void)hipFree(p);
   if (hStage_) (void)hipHostFree(hStage_);
@@ -92,15 +104,30 @@ Device::~Device() {
   if (ST) (void)hipStreamDestroy(ST);
 }
 
+// Staging is only rewritten after the previous request completed (every request waits for its mailbox), so
+// growing it in place is safe.
 void Device::ensureStage(size_t bytes) {
   if (bytes <= stageCap_) return;
   size_t cap = stageCap_ ? stageCap_ : (1 << 20);
   while (cap < bytes) cap <<= 1;
-  if (hStage_) (void)hipHostFree(hStage_);
-  if (dStage_) (void)hipFree(dStage_);
-  hipCheck(hipHostMalloc((void**)&hStage_, cap, hipHostMallocDefault), "hipHostMalloc stage");
-  hipCheck(hipMalloc((void**)&dStage_, cap), "hipMalloc stage");
+  char* fresh = nullptr;
+  hipCheck(hipHostMalloc((void**)&fresh, cap, hipHostMallocMapped | hipHostMallocCoherent), "hipHostMalloc stage");
+  if (hStage_) {
+    std::memcpy(fresh, hStage_, stageUsed_);
+    (void)hipHostFree(hStage_);
+  }
+  hStage_ = fresh;
+  hipCheck(hipHostGetDevicePointer((void**)&hStageDev_, hStage_, 0), "hipHostGetDevicePointer");
   stageCap_ = cap;
+}
+
+void Device::ensureReq(size_t bytes) {
+  if (bytes <= reqCap_) return;
+  size_t cap = reqCap_ ? reqCap_ : (1 << 20);
+  while (cap < bytes) cap <<= 1;
+  if (dReq_) (void)hipFree(dReq_);
+  hipCheck(hipMalloc((void**)&dReq_, cap), "hipMalloc request");
+  reqCap_ = cap;
 }
 
 DevTables Device::tables() const {
@@ -161,88 +188,142 @@ size_t Device::updatesBytes() const {
          align16(prows.size() * sizeof(PartitionRow)) + align16(tdeltas.size() * sizeof(TopicCountDelta));
 }
 
-size_t Device::packUpdates(size_t off, int& nb, int& nr, int& np, int& nt, size_t& obr, size_t& orr, size_t& opr,
-                           size_t& otd) {
-  nb = (int)brows.size();
-  nr = (int)rrows.size();
-  np = (int)prows.size();
-  nt = (int)tdeltas.size();
-  size_t need = off + align16(nb * sizeof(BrokerRow)) + align16(nr * sizeof(ReplicaRow)) +
-                align16(np * sizeof(PartitionRow)) + align16(nt * sizeof(TopicCountDelta));
-  ensureStage(need + (1 << 16));
-  obr = off;
-  std::memcpy(hStage_ + obr, brows.data(), nb * sizeof(BrokerRow));
-  orr = obr + align16(nb * sizeof(BrokerRow));
-  std::memcpy(hStage_ + orr, rrows.data(), nr * sizeof(ReplicaRow));
-  opr = orr + align16(nr * sizeof(ReplicaRow));
-  std::memcpy(hStage_ + opr, prows.data(), np * sizeof(PartitionRow));
-  otd = opr + align16(np * sizeof(PartitionRow));
-  std::memcpy(hStage_ + otd, tdeltas.data(), nt * sizeof(TopicCountDelta));
+// [broker rows | replica rows | partition rows | topic deltas] at the start of the staging area
+Device::Staged Device::packUpdates(size_t extra) {
+  Staged g;
+  g.nb = (int)brows.size();
+  g.nr = (int)rrows.size();
+  g.np = (int)prows.size();
+  g.nt = (int)tdeltas.size();
+  stageUsed_ = 0;
+  ensureStage(updatesBytes() + extra + 64);
+  g.obr = 0;
+  std::memcpy(hStage_ + g.obr, brows.data(), g.nb * sizeof(BrokerRow));
+  g.orr = g.obr + align16(g.nb * sizeof(BrokerRow));
+  std::memcpy(hStage_ + g.orr, rrows.data(), g.nr * sizeof(ReplicaRow));
+  g.opr = g.orr + align16(g.nr * sizeof(ReplicaRow));
+  std::memcpy(hStage_ + g.opr, prows.data(), g.np * sizeof(PartitionRow));
+  g.otd = g.opr + align16(g.np * sizeof(PartitionRow));
+  std::memcpy(hStage_ + g.otd, tdeltas.data(), g.nt * sizeof(TopicCountDelta));
+  g.end = g.otd + align16(g.nt * sizeof(TopicCountDelta));
   brows.clear();
   rrows.clear();
   prows.clear();
   tdeltas.clear();
-  return otd + align16(nt * sizeof(TopicCountDelta));
+  stageUsed_ = g.end;
+  return g;
 }
 
-void Device::launchApply(int nb, int nr, int np, int nt, size_t obr, size_t orr, size_t opr, size_t otd) {
-  if (nb + nr + np + nt == 0) return;
-  hipCheck(launchApplyRows(bUtil_, bNrep_, bNlead_, bPot_, bAlive_, B_, (const BrokerRow*)(dStage_ + obr), nb, rUtil_,
-                           rBroker_, rFlags_, R_, (const ReplicaRow*)(dStage_ + orr), nr, pOff_, pBrokers_,
-                           (const PartitionRow*)(dStage_ + opr), np, topicCount_, ldB_,
-                           (const TopicCountDelta*)(dStage_ + otd), nt, ST),
-           "apply_rows");
+// One `prep` launch: apply the staged rows, copy `reqBytes` of request (staged at g.end) into HBM, and (for a
+// scan) reset the result words and the arrival counter.
+void Device::launchPrepFor(const Staged& g, size_t reqBytes, bool scan) {
+  const int nReq4 = (int)(align16(reqBytes) / 16);
+  if (nReq4) ensureReq((size_t)nReq4 * 16);
+  hipCheck(launchPrep(bUtil_, bNrep_, bNlead_, bPot_, bAlive_, B_, (const BrokerRow*)(hStageDev_ + g.obr), g.nb,
+                      rUtil_, rBroker_, rFlags_, R_, (const ReplicaRow*)(hStageDev_ + g.orr), g.nr, pOff_, pBrokers_,
+                      (const PartitionRow*)(hStageDev_ + g.opr), g.np, topicCount_, ldB_,
+                      (const TopicCountDelta*)(hStageDev_ + g.otd), g.nt, (const int4*)(hStageDev_ + g.end),
+                      (int4*)dReq_, nReq4, scan ? dResult_ : nullptr, scan ? dDone_ : nullptr, ST),
+           "prep");
+}
+
+// Spin on the host-mapped mailbox for `seq`; a stream error (or a stream that drained without publishing)
+// is reported instead of spinning forever.
+void Device::waitMail(unsigned long long seq) {
+  volatile unsigned long long* mail = hResult_;
+  const unsigned long long want = seq & 0xffffffffull;
+  uint64_t spins = 0;
+  while ((__atomic_load_n(&mail[0], __ATOMIC_ACQUIRE) >> 32) != want) {
+    if ((++spins & 1023) == 0) {
+      const hipError_t q = hipStreamQuery(ST);
+      if (q == hipSuccess) {
+        if ((__atomic_load_n(&mail[0], __ATOMIC_ACQUIRE) >> 32) == want) break;
+        throw std::runtime_error("scan finished without publishing its result");
+      }
+      if (q != hipErrorNotReady) hipCheck(q, "scan");
+    }
+    __builtin_ia32_pause();
+  }
+  perf.syncs++;
 }
 
 void Device::flushOnly() {
-  int nb, nr, np, nt;
-  size_t obr, orr, opr, otd;
-  size_t used = packUpdates(0, nb, nr, np, nt, obr, orr, opr, otd);
-  if (nb + nr + np + nt == 0) return;
-  hipCheck(hipMemcpyAsync(dStage_, hStage_, used, hipMemcpyHostToDevice, ST), "H2D stage");
-  launchApply(nb, nr, np, nt, obr, orr, opr, otd);
+  if (brows.empty() && rrows.empty() && prows.empty() && tdeltas.empty()) return;
+  const Staged g = packUpdates(0);
+  launchPrepFor(g, 0, false);
   hipCheck(hipStreamSynchronize(ST), "sync");
   perf.syncs++;
 }
 
-int64_t Device::finishScan(size_t resultOff, size_t bytes) {
-  hipCheck(hipMemcpyAsync(hResult_, dStage_ + resultOff, bytes, hipMemcpyDeviceToHost, ST), "D2H result");
-  hipCheck(hipStreamSynchronize(ST), "sync");
-  perf.syncs++;
+int64_t Device::finishScan() {
+  waitMail(seq_);
   if (timing) {
+    hipCheck(hipEventSynchronize(EV1), "hipEventSynchronize");
     float ms = 0.f;
     hipCheck(hipEventElapsedTime(&ms, EV0, EV1), "hipEventElapsedTime");
     perf.scanKernelMs += ms;
   }
-  const unsigned long long v = *hResult_;
-  return v == ~0ull ? -1 : (int64_t)v;
+  const unsigned long long lo = hResult_[0] & 0xffffffffull;  // key + 1, 0 = no winner
+  return lo == 0 ? -1 : (int64_t)(lo - 1);
+}
+
+// A cross/pair scan is one launch when its update list fits the kernel's LDS overlay and its request is
+// small enough to read straight from host memory; otherwise `prep` applies the rows and copies the request
+// into HBM first.
+constexpr int kOverlayRows = 32;
+constexpr size_t kDirectRequestBytes = 16 << 10;
+
+UpdateList Device::overlayFor(const Staged& g) const {
+  UpdateList u;
+  u.brows = (const BrokerRow*)(hStageDev_ + g.obr);
+  u.rrows = (const ReplicaRow*)(hStageDev_ + g.orr);
+  u.prows = (const PartitionRow*)(hStageDev_ + g.opr);
+  u.tdel = (const TopicCountDelta*)(hStageDev_ + g.otd);
+  u.nb = g.nb;
+  u.nr = g.nr;
+  u.np = g.np;
+  u.nt = g.nt;
+  return u;
+}
+
+MutTables Device::mutTables() const {
+  return MutTables{bUtil_, bNrep_, bNlead_, bPot_, bAlive_, rUtil_, rBroker_, rFlags_, pBrokers_, topicCount_, ldB_};
+}
+
+// Returns the request base the scan reads (host-mapped staging or the HBM copy) and the update list it
+// applies itself (empty when prep ran).
+const char* Device::stageScan(const Staged& g, size_t req, UpdateList& u) {
+  const bool fits = g.nb <= kOverlayRows && g.nr <= kOverlayRows && g.np <= kOverlayRows;
+  if (fits && req <= kDirectRequestBytes) {
+    u = overlayFor(g);
+    perf.singleLaunch++;
+    return hStageDev_ + g.end;
+  }
+  launchPrepFor(g, req, false);
+  u = UpdateList{nullptr, nullptr, nullptr, nullptr, 0, 0, 0, 0};
+  return dReq_;
 }
 
 int64_t Device::scanCross(const DevProgram& prog, const int32_t* reps, int K, const int32_t* cands, int N) {
   if (K <= 0 || N <= 0) return -1;
   if ((uint64_t)K * (uint64_t)N >= (1ull << 31)) throw std::runtime_error("scan too large");
-  ensureStage(updatesBytes() + align16((size_t)K * 4) + align16((size_t)N * 4) + 64);
-  int nb, nr, np, nt;
-  size_t obr, orr, opr, otd;
-  size_t off = packUpdates(0, nb, nr, np, nt, obr, orr, opr, otd);
-  const size_t oRep = off;
-  const size_t oCand = oRep + align16((size_t)K * 4);
-  const size_t oRes = oCand + align16((size_t)N * 4);
-  const size_t used = oRes + 16;
-  std::memcpy(hStage_ + oRep, reps, (size_t)K * 4);
-  std::memcpy(hStage_ + oCand, cands, (size_t)N * 4);
-  *(unsigned long long*)(hStage_ + oRes) = ~0ull;
-  hipCheck(hipMemcpyAsync(dStage_, hStage_, used, hipMemcpyHostToDevice, ST), "H2D stage");
-  launchApply(nb, nr, np, nt, obr, orr, opr, otd);
+  const size_t oCand = align16((size_t)K * 4);
+  const size_t req = oCand + align16((size_t)N * 4);
+  const Staged g = packUpdates(req);
+  std::memcpy(hStage_ + g.end, reps, (size_t)K * 4);
+  std::memcpy(hStage_ + g.end + oCand, cands, (size_t)N * 4);
+  UpdateList u;
+  const char* base = stageScan(g, req, u);
+  ++seq_;
   if (timing) (void)hipEventRecord(EV0, ST);
-  hipCheck(launchScanCross(tables(), prog, (const int32_t*)(dStage_ + oRep), (const int32_t*)(dStage_ + oCand), K, N,
-                           (unsigned long long*)(dStage_ + oRes), ST),
+  hipCheck(launchScanCross(tables(), mutTables(), u, prog, (const int32_t*)base, (const int32_t*)(base + oCand), K, N,
+                           dResult_, dDone_, hResultDev_, seq_, ST),
            "scan_cross");
   if (timing) (void)hipEventRecord(EV1, ST);
   perf.scanLaunches++;
   perf.scanPairs += (int64_t)K * N;
   perf.scanBytes += (int64_t)K * N * kBytesPerCandidate;
-  return finishScan(oRes, 8);
+  return finishScan();
 }
 
 int64_t Device::scanSwap(const DevProgram& prog, const int32_t* srcs, int S, const int32_t* cbOff, int M,
@@ -255,72 +336,60 @@ int64_t Device::scanSwap(const DevProgram& prog, const int32_t* srcs, int S, con
     rowVisitedCap_ = rows * 2;
     hipCheck(hipMalloc((void**)&rowVisited_, rowVisitedCap_ * sizeof(int32_t)), "hipMalloc rowVisited");
   }
-  ensureStage(updatesBytes() + align16((size_t)S * 4) + align16((size_t)(M + 1) * 4) + align16((size_t)nCand * 4) + 64);
-  int nb, nr, np, nt;
-  size_t obr, orr, opr, otd;
-  size_t off = packUpdates(0, nb, nr, np, nt, obr, orr, opr, otd);
-  const size_t oSrc = off;
-  const size_t oOff = oSrc + align16((size_t)S * 4);
+  const size_t oOff = align16((size_t)S * 4);
   const size_t oRep = oOff + align16((size_t)(M + 1) * 4);
-  const size_t oRes = oRep + align16((size_t)nCand * 4);
-  const size_t used = oRes + 16;
-  std::memcpy(hStage_ + oSrc, srcs, (size_t)S * 4);
-  std::memcpy(hStage_ + oOff, cbOff, (size_t)(M + 1) * 4);
-  std::memcpy(hStage_ + oRep, cbRep, (size_t)nCand * 4);
-  *(unsigned long long*)(hStage_ + oRes) = ~0ull;
-  *(unsigned long long*)(hStage_ + oRes + 8) = 0ull;
-  hipCheck(hipMemcpyAsync(dStage_, hStage_, used, hipMemcpyHostToDevice, ST), "H2D stage");
-  launchApply(nb, nr, np, nt, obr, orr, opr, otd);
-  hipCheck(launchScanSwap(tables(), prog, (const int32_t*)(dStage_ + oSrc), S, (const int32_t*)(dStage_ + oOff),
-                          (const int32_t*)(dStage_ + oRep), M, (unsigned long long*)(dStage_ + oRes), rowVisited_, ST,
+  const size_t req = oRep + align16((size_t)nCand * 4);
+  const Staged g = packUpdates(req);
+  std::memcpy(hStage_ + g.end, srcs, (size_t)S * 4);
+  std::memcpy(hStage_ + g.end + oOff, cbOff, (size_t)(M + 1) * 4);
+  std::memcpy(hStage_ + g.end + oRep, cbRep, (size_t)nCand * 4);
+  launchPrepFor(g, req, true);
+  ++seq_;
+  hipCheck(launchScanSwap(tables(), prog, (const int32_t*)dReq_, S, (const int32_t*)(dReq_ + oOff),
+                          (const int32_t*)(dReq_ + oRep), M, dResult_, rowVisited_, hResultDev_, seq_, ST,
                           timing ? EV0 : nullptr, timing ? EV1 : nullptr),
            "scan_swap");
   perf.scanLaunches++;
   perf.scanPairs += (int64_t)S * nCand;
   perf.scanBytes += (int64_t)S * nCand * kBytesPerCandidate;
-  const int64_t key = finishScan(oRes, 16);
-  *visited = (int64_t)hResult_[1];
-  return key;
+  (void)finishScan();
+  const unsigned long long best = hResult_[1];
+  *visited = (int64_t)hResult_[2];
+  return best == ~0ull ? -1 : (int64_t)best;
 }
 
 int64_t Device::scanPairs(const DevProgram& prog, const int32_t* pr, const int32_t* pb, int n) {
   if (n <= 0) return -1;
-  ensureStage(updatesBytes() + 2 * align16((size_t)n * 4) + 64);
-  int nb, nr, np, nt;
-  size_t obr, orr, opr, otd;
-  size_t off = packUpdates(0, nb, nr, np, nt, obr, orr, opr, otd);
-  const size_t oR = off;
-  const size_t oB = oR + align16((size_t)n * 4);
-  const size_t oRes = oB + align16((size_t)n * 4);
-  const size_t used = oRes + 16;
-  std::memcpy(hStage_ + oR, pr, (size_t)n * 4);
-  std::memcpy(hStage_ + oB, pb, (size_t)n * 4);
-  *(unsigned long long*)(hStage_ + oRes) = ~0ull;
-  hipCheck(hipMemcpyAsync(dStage_, hStage_, used, hipMemcpyHostToDevice, ST), "H2D stage");
-  launchApply(nb, nr, np, nt, obr, orr, opr, otd);
+  const size_t oB = align16((size_t)n * 4);
+  const size_t req = oB + align16((size_t)n * 4);
+  const Staged g = packUpdates(req);
+  std::memcpy(hStage_ + g.end, pr, (size_t)n * 4);
+  std::memcpy(hStage_ + g.end + oB, pb, (size_t)n * 4);
+  UpdateList u;
+  const char* base = stageScan(g, req, u);
+  ++seq_;
   if (timing) (void)hipEventRecord(EV0, ST);
-  hipCheck(launchScanPairs(tables(), prog, (const int32_t*)(dStage_ + oR), (const int32_t*)(dStage_ + oB), n,
-                           (unsigned long long*)(dStage_ + oRes), ST),
+  hipCheck(launchScanPairs(tables(), mutTables(), u, prog, (const int32_t*)base, (const int32_t*)(base + oB), n,
+                           dResult_, dDone_, hResultDev_, seq_, ST),
            "scan_pairs");
   if (timing) (void)hipEventRecord(EV1, ST);
   perf.scanLaunches++;
   perf.scanPairs += n;
   perf.scanBytes += (int64_t)n * kBytesPerCandidate;
-  return finishScan(oRes, 8);
+  return finishScan();
 }
 
 void Device::stats(const StatsParams& P, const uint8_t* allowedAliveHost, StatsOut* out) {
-  int nb, nr, np, nt;
-  size_t obr, orr, opr, otd;
-  size_t used = packUpdates(0, nb, nr, np, nt, obr, orr, opr, otd);
-  if (used) hipCheck(hipMemcpyAsync(dStage_, hStage_, used, hipMemcpyHostToDevice, ST), "H2D stage");
-  launchApply(nb, nr, np, nt, obr, orr, opr, otd);
-  hipCheck(hipMemcpyAsync(allowedAlive_, allowedAliveHost, ldB_, hipMemcpyHostToDevice, ST), "H2D allowedAlive");
+  const size_t req = align16((size_t)ldB_);
+  const Staged g = packUpdates(req);
+  std::memcpy(hStage_ + g.end, allowedAliveHost, (size_t)ldB_);
+  launchPrepFor(g, req, false);
+  hipCheck(hipMemcpyAsync(allowedAlive_, dReq_, (size_t)ldB_, hipMemcpyDeviceToDevice, ST), "allowedAlive");
   hipCheck(launchStats(P, topicCount_, topicNrep_, bUtil_, bCap_, bNrep_, bNlead_, bPot_, bAlive_, allowedAlive_,
                        (TopicPartial*)topicScratch_, (StatsOut*)statsOut_, ldB_, ST, timing ? EV0 : nullptr,
                        timing ? EV1 : nullptr),
            "stats");
-  hipCheck(hipMemcpyAsync(hResult_, statsOut_, sizeof(StatsOut), hipMemcpyDeviceToHost, ST), "D2H stats");
+  hipCheck(hipMemcpyAsync(statsHost_, statsOut_, sizeof(StatsOut), hipMemcpyDeviceToHost, ST), "D2H stats");
   hipCheck(hipStreamSynchronize(ST), "sync");
   perf.syncs++;
   perf.statsLaunches++;
@@ -330,7 +399,7 @@ void Device::stats(const StatsParams& P, const uint8_t* allowedAliveHost, StatsO
     hipCheck(hipEventElapsedTime(&ms, EV0, EV1), "hipEventElapsedTime");
     perf.statsKernelMs += ms;
   }
-  std::memcpy((void*)out, hResult_, sizeof(StatsOut));
+  std::memcpy((void*)out, statsHost_, sizeof(StatsOut));
 }
 
 }  // namespace ccmi

@@ -1,9 +1,11 @@
-// Device side of a session: HBM tables, a pinned staging ring for row updates and scan requests, and
-// the launch/readback protocol of one scan:
-//   H2D  one hipMemcpyAsync of [row updates | request arrays | result word = ~0]
-//   K4   apply_rows     (only if rows are dirty)
-//   K1/5 scan_cross or scan_swap
-//   D2H  8-byte result, hipStreamSynchronize
+// Device side of a session: HBM tables, a host-coherent mapped staging area for row updates and scan
+// requests, and the launch/readback protocol of one scan (no DMA copies, no stream synchronisation):
+//   host  packs [row updates | request arrays] into the mapped staging area
+//   K1/2  scan_cross / scan_pairs: when the update list fits the LDS overlay and the request is small, the
+//         scan applies the rows itself and reads the request from the staging area (one launch);
+//         otherwise K4 prep applies the rows and copies the request into HBM first
+//   K5    scan_swap (+ visited sum) always after prep
+//   the last workgroup writes one {seq, key} word into a host-mapped mailbox; the host spins on it
 // Everything runs on one HIP stream per session, so HIP events on that stream time the kernels.
 #pragma once
 #include <cstdint>
@@ -28,6 +30,7 @@ struct DevicePerf {
   double statsKernelMs = 0;
   int64_t statsBytes = 0;
   int64_t syncs = 0;
+  int64_t singleLaunch = 0;  // scans that applied their rows in-kernel and read the request from host memory
 };
 
 class Device {
@@ -72,18 +75,35 @@ class Device {
   int32_t *pOff_ = nullptr, *pBrokers_ = nullptr, *topicCount_ = nullptr, *topicNrep_ = nullptr;
   uint8_t *bAlive_ = nullptr, *allowed_ = nullptr, *rFlags_ = nullptr, *allowedAlive_ = nullptr;
   void *topicScratch_ = nullptr, *statsOut_ = nullptr;
-  // staging
+  // staging (host-coherent, mapped) and the request copy in HBM
   char* hStage_ = nullptr;
-  char* dStage_ = nullptr;
-  size_t stageCap_ = 0;
+  char* hStageDev_ = nullptr;
+  size_t stageCap_ = 0, stageUsed_ = 0;
+  char* dReq_ = nullptr;
+  size_t reqCap_ = 0;
+  // result words in HBM, arrival counter, host mailbox {seq, value, extra}
+  unsigned long long* dResult_ = nullptr;
+  unsigned int* dDone_ = nullptr;
   unsigned long long* hResult_ = nullptr;
+  unsigned long long* hResultDev_ = nullptr;
+  unsigned long long seq_ = 0;
+  alignas(16) unsigned char statsHost_[sizeof(StatsOut)];
   void *ev0_ = nullptr, *ev1_ = nullptr;  // hipEvent_t
+  struct Staged {
+    int nb = 0, nr = 0, np = 0, nt = 0;
+    size_t obr = 0, orr = 0, opr = 0, otd = 0, end = 0;
+  };
   DevTables tables() const;
   size_t updatesBytes() const;
-  size_t packUpdates(size_t off, int& nb, int& nr, int& np, int& nt, size_t& obr, size_t& orr, size_t& opr, size_t& otd);
+  Staged packUpdates(size_t extra);
   void ensureStage(size_t bytes);
-  void launchApply(int nb, int nr, int np, int nt, size_t obr, size_t orr, size_t opr, size_t otd);
-  int64_t finishScan(size_t resultOff, size_t bytes);
+  void ensureReq(size_t bytes);
+  void launchPrepFor(const Staged& g, size_t reqBytes, bool scan);
+  UpdateList overlayFor(const Staged& g) const;
+  MutTables mutTables() const;
+  const char* stageScan(const Staged& g, size_t req, UpdateList& u);
+  void waitMail(unsigned long long seq);
+  int64_t finishScan();
   int32_t* rowVisited_ = nullptr;
   size_t rowVisitedCap_ = 0;
 };

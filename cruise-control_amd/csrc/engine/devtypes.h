@@ -74,6 +74,28 @@ struct TopicCountDelta {
   int32_t topic, broker, delta, pad;
 };
 
+// Writable views of the dynamic tables (row application inside a scan) and a staged update list.
+struct MutTables {
+  double* bUtil;
+  int32_t* bNrep;
+  int32_t* bNlead;
+  double* bPot;
+  uint8_t* bAlive;
+  double* rUtil;
+  int32_t* rBroker;
+  uint8_t* rFlags;
+  int32_t* pBrokers;
+  int32_t* topicCount;
+  int32_t ldB;
+};
+struct UpdateList {
+  const BrokerRow* brows;
+  const ReplicaRow* rrows;
+  const PartitionRow* prows;
+  const TopicCountDelta* tdel;
+  int32_t nb, nr, np, nt;
+};
+
 // Scan request modes.
 //   CROSS : pairs (replicas[k], cands[j]) in k-major order; key = k * N + j
 //   SWAP  : rows (m, s) = (candidate broker segment m, source replica s); a row's candidates are

@@ -33,6 +33,11 @@ struct HostView {
   int pbegin(int p) const { return m.pOff[p]; }
   int pend(int p) const { return m.pOff[p + 1]; }
   int pbroker(int i) const { return m.rBroker[m.pSlots[i]]; }
+  bool hosts(int p, int b) const {
+    bool has = false;
+    for (int i = pbegin(p); i < pend(p); ++i) has |= (pbroker(i) == b);
+    return has;
+  }
 };
 
 Model::Spec makeSpec() { return Model::Spec(); }

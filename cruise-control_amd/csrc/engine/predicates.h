@@ -27,7 +27,8 @@
 namespace ccmi {
 
 // V must provide: bu(b,res) bcap(b,res) nrep(b) alive(b) allowed(slot,b) ru(r,res) flags(r) rbroker(r)
-// rorig(r) rpart(r) pbegin(p) pend(p) pbroker(i)
+// rorig(r) rpart(r) and, for partition membership, hosts(p,b) — or pbegin(p) pend(p) pbroker(i) through
+// hostsPartition's generic form.
 template <class V>
 CCMI_HD bool currentOffline(const V& v, int r) {
   const int orig = v.rorig(r), br = v.rbroker(r);
@@ -37,9 +38,7 @@ CCMI_HD bool currentOffline(const V& v, int r) {
 
 template <class V>
 CCMI_HD bool hostsPartition(const V& v, int p, int b) {
-  bool has = false;
-  for (int i = v.pbegin(p); i < v.pend(p); ++i) has |= (v.pbroker(i) == b);
-  return has;
+  return v.hosts(p, b);
 }
 
 template <class V>

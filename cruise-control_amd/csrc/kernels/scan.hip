@@ -10,8 +10,13 @@
 //                     candidate replicas (AbstractGoal.maybeApplySwapAction, AbstractGoal.java:287-338);
 //                     the row's FIRST terminal outcome decides it, and the smallest row whose terminal is
 //                     an ACCEPT wins.
-// K4     apply_rows : scatters the host's dirty broker/replica/partition rows and topic-count deltas into
-//                     the device tables before a scan or a stats pass.
+// K4     prep       : scatters the host's dirty broker/replica/partition rows and topic-count deltas into
+//                     the device tables, copies the scan request from the host-mapped staging area into HBM
+//                     and resets the result words — one launch, no DMA copy.
+// Cross/pair scans apply small update lists themselves (LDS overlay, see OverlayLds) and read small requests
+// straight from the host-mapped staging area, so a scan is ONE launch. Results go back without a copy or a
+// stream sync: the last workgroup to finish (arrival counter) writes one {seq, key} word into a host-mapped
+// mailbox, and the host spins on it.
 // Built with -ffp-contract=off: every predicate is the reference's IEEE double expression.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -36,10 +41,238 @@ struct DevView {
   __device__ __forceinline__ int pbegin(int p) const { return t.pOff[p]; }
   __device__ __forceinline__ int pend(int p) const { return t.pOff[p + 1]; }
   __device__ __forceinline__ int pbroker(int i) const { return t.pBrokers[i]; }
+  __device__ __forceinline__ bool hosts(int p, int b) const {
+    bool has = false;
+    for (int i = pbegin(p); i < pend(p); ++i) has |= (pbroker(i) == b);
+    return has;
+  }
+};
+
+// Row updates a cross/pair scan applies itself (instead of a separate launch): every workgroup stages the
+// host's dirty rows from the host-mapped staging area into LDS and reads a dirty entity from there, while
+// workgroup 0 writes the rows into the HBM tables for the next launch. Only dirty rows are written and no
+// workgroup reads a dirty row from HBM during the launch, so there is no read/write race.
+constexpr int kOvB = 32, kOvR = 32, kOvP = 32;
+
+struct OverlayLds {
+  BrokerRow b[kOvB];
+  ReplicaRow r[kOvR];
+  PartitionRow p[kOvP];
+  int nb, nr, np;
+  __device__ __forceinline__ int broker(int x) const {
+    for (int i = 0; i < nb; ++i)
+      if (b[i].b == x) return i;
+    return -1;
+  }
+  __device__ __forceinline__ int replica(int x) const {
+    for (int i = 0; i < nr; ++i)
+      if (r[i].r == x) return i;
+    return -1;
+  }
+  __device__ __forceinline__ int partition(int x) const {
+    for (int i = 0; i < np; ++i)
+      if (p[i].p == x) return i;
+    return -1;
+  }
+};
+
+template <class Row, int Cap>
+__device__ __forceinline__ void stageRows(Row* dst, const Row* __restrict__ src, int n) {
+  const int words = n * (int)(sizeof(Row) / 4);
+  for (int w = threadIdx.x; w < words; w += blockDim.x)
+    reinterpret_cast<int32_t*>(dst)[w] = reinterpret_cast<const int32_t*>(src)[w];
+}
+
+__device__ __forceinline__ void applyRowsBlock(const MutTables& M, int B, int R, const BrokerRow* brows, int nb,
+                                               const ReplicaRow* rrows, int nr, const int32_t* __restrict__ pOff,
+                                               const PartitionRow* prows, int np, const TopicCountDelta* tdel,
+                                               int nt, int first, int stride) {
+  for (int i = first; i < nb; i += stride) {
+    const BrokerRow& x = brows[i];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) M.bUtil[(size_t)k * B + x.b] = x.util[k];
+    M.bNrep[x.b] = x.nrep;
+    M.bNlead[x.b] = x.nlead;
+    M.bPot[x.b] = x.potNwOut;
+    M.bAlive[x.b] = (uint8_t)x.alive;
+  }
+  for (int i = first; i < nr; i += stride) {
+    const ReplicaRow& x = rrows[i];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) M.rUtil[(size_t)k * R + x.r] = x.util[k];
+    M.rBroker[x.r] = x.broker;
+    M.rFlags[x.r] = (uint8_t)x.flags;
+  }
+  for (int i = first; i < np; i += stride) {
+    const PartitionRow& x = prows[i];
+    const int o = pOff[x.p];
+    for (int k = 0; k < x.n; ++k) M.pBrokers[o + k] = x.brokers[k];
+  }
+  for (int i = first; i < nt; i += stride) {
+    const TopicCountDelta d = tdel[i];
+    atomicAdd(&M.topicCount[(size_t)d.topic * M.ldB + d.broker], d.delta);
+  }
+}
+
+// Stage the update list into LDS (all workgroups) and apply it to HBM (workgroup 0).
+__device__ __forceinline__ void overlayBegin(OverlayLds& ov, const UpdateList& U, const MutTables& M,
+                                             const DevTables& T) {
+  if (threadIdx.x == 0) {
+    ov.nb = U.nb;
+    ov.nr = U.nr;
+    ov.np = U.np;
+  }
+  if (U.nb | U.nr | U.np) {
+    stageRows<BrokerRow, kOvB>(ov.b, U.brows, U.nb);
+    stageRows<ReplicaRow, kOvR>(ov.r, U.rrows, U.nr);
+    stageRows<PartitionRow, kOvP>(ov.p, U.prows, U.np);
+  }
+  __syncthreads();
+  if (blockIdx.x == 0 && (U.nb | U.nr | U.np | U.nt))
+    applyRowsBlock(M, T.B, T.R, ov.b, ov.nb, ov.r, ov.nr, T.pOff, ov.p, ov.np, U.tdel, U.nt, threadIdx.x,
+                   blockDim.x);
+}
+
+// A move candidate's operands gathered up front with independent loads (row side: the replica, its broker,
+// its partition's brokers; destination side: one broker record), so the predicate conjunction runs on
+// registers instead of a chain of control-dependent loads. Accessors answer only for the ids a move
+// predicate asks about (the replica r, its source/original broker, the destination, r's partition).
+struct PreView {
+  int r, src, orig, p, rflags, dst, snrep, dnrep;
+  uint32_t aliveBits;   // bit 0 src, bit 1 orig, bit 2 dst (values, never addressed: keeps the view in VGPRs)
+  uint32_t srcAllowed;  // bit `slot` = allowed(slot, src)
+  int pb0, pb1, pb2, pb3, pb4, pb5, pb6, pb7;
+  double ru0, ru1, ru2, ru3, sbu0, sbu1, sbu2, sbu3, scap0, scap1, scap2, scap3;
+  double dbu0, dbu1, dbu2, dbu3, dcap0, dcap1, dcap2, dcap3;
+
+  static __device__ __forceinline__ double sel(int k, double a, double b, double c, double d) {
+    return k == 0 ? a : (k == 1 ? b : (k == 2 ? c : d));
+  }
+  __device__ __forceinline__ void loadRow(const DevTables& t, const DevProgram& prog, int rr, const OverlayLds& ov) {
+    r = rr;
+    orig = t.rOrig[r];
+    p = t.rPart[r];
+    const int ri = ov.replica(r);
+    if (ri >= 0) {
+      const ReplicaRow& x = ov.r[ri];
+      src = x.broker;
+      rflags = x.flags;
+      ru0 = x.util[0];
+      ru1 = x.util[1];
+      ru2 = x.util[2];
+      ru3 = x.util[3];
+    } else {
+      src = t.rBroker[r];
+      rflags = t.rFlags[r];
+      ru0 = t.rUtil[r];
+      ru1 = t.rUtil[(size_t)t.R + r];
+      ru2 = t.rUtil[(size_t)2 * t.R + r];
+      ru3 = t.rUtil[(size_t)3 * t.R + r];
+    }
+    const int pi = ov.partition(p);
+    if (pi >= 0) {
+      const PartitionRow& x = ov.p[pi];
+      const int pn = x.n;
+      pb0 = pn > 0 ? x.brokers[0] : -1;
+      pb1 = pn > 1 ? x.brokers[1] : -1;
+      pb2 = pn > 2 ? x.brokers[2] : -1;
+      pb3 = pn > 3 ? x.brokers[3] : -1;
+      pb4 = pn > 4 ? x.brokers[4] : -1;
+      pb5 = pn > 5 ? x.brokers[5] : -1;
+      pb6 = pn > 6 ? x.brokers[6] : -1;
+      pb7 = pn > 7 ? x.brokers[7] : -1;
+    } else {
+      const int o0 = t.pOff[p], pn = t.pOff[p + 1] - o0;
+      const int32_t* q = t.pBrokers + o0;
+      pb0 = pn > 0 ? q[0] : -1;
+      pb1 = pn > 1 ? q[1] : -1;
+      pb2 = pn > 2 ? q[2] : -1;
+      pb3 = pn > 3 ? q[3] : -1;
+      pb4 = pn > 4 ? q[4] : -1;
+      pb5 = pn > 5 ? q[5] : -1;
+      pb6 = pn > 6 ? q[6] : -1;
+      pb7 = pn > 7 ? q[7] : -1;
+    }
+    const int oi = ov.broker(orig);
+    const bool aOrig = oi >= 0 ? ov.b[oi].alive != 0 : t.bAlive[orig] != 0;
+    const int si = ov.broker(src);
+    bool aSrc;
+    if (si >= 0) {
+      const BrokerRow& x = ov.b[si];
+      aSrc = x.alive != 0;
+      snrep = x.nrep;
+      sbu0 = x.util[0];
+      sbu1 = x.util[1];
+      sbu2 = x.util[2];
+      sbu3 = x.util[3];
+    } else {
+      aSrc = t.bAlive[src] != 0;
+      snrep = t.bNrep[src];
+      sbu0 = t.bUtil[src];
+      sbu1 = t.bUtil[(size_t)t.B + src];
+      sbu2 = t.bUtil[(size_t)2 * t.B + src];
+      sbu3 = t.bUtil[(size_t)3 * t.B + src];
+    }
+    aliveBits = (aSrc ? 1u : 0u) | (aOrig ? 2u : 0u);
+    scap0 = t.bCap[src];
+    scap1 = t.bCap[(size_t)t.B + src];
+    scap2 = t.bCap[(size_t)2 * t.B + src];
+    scap3 = t.bCap[(size_t)3 * t.B + src];
+    srcAllowed = 0;
+    for (int i = 0; i < prog.nGoals; ++i) {
+      const int slot = prog.goals[i].allowedSlot;
+      srcAllowed |= (t.allowed[(size_t)slot * t.B + src] ? 1u : 0u) << slot;
+    }
+  }
+  __device__ __forceinline__ void loadDst(const DevTables& t, int d, const OverlayLds& ov) {
+    dst = d;
+    const int di = ov.broker(d);
+    bool aDst;
+    if (di >= 0) {
+      const BrokerRow& x = ov.b[di];
+      aDst = x.alive != 0;
+      dnrep = x.nrep;
+      dbu0 = x.util[0];
+      dbu1 = x.util[1];
+      dbu2 = x.util[2];
+      dbu3 = x.util[3];
+    } else {
+      aDst = t.bAlive[d] != 0;
+      dnrep = t.bNrep[d];
+      dbu0 = t.bUtil[d];
+      dbu1 = t.bUtil[(size_t)t.B + d];
+      dbu2 = t.bUtil[(size_t)2 * t.B + d];
+      dbu3 = t.bUtil[(size_t)3 * t.B + d];
+    }
+    aliveBits = (aliveBits & 3u) | (aDst ? 4u : 0u);
+    dcap0 = t.bCap[d];
+    dcap1 = t.bCap[(size_t)t.B + d];
+    dcap2 = t.bCap[(size_t)2 * t.B + d];
+    dcap3 = t.bCap[(size_t)3 * t.B + d];
+  }
+  __device__ __forceinline__ double bu(int b, int k) const {
+    return b == dst ? sel(k, dbu0, dbu1, dbu2, dbu3) : sel(k, sbu0, sbu1, sbu2, sbu3);
+  }
+  __device__ __forceinline__ double bcap(int b, int k) const {
+    return b == dst ? sel(k, dcap0, dcap1, dcap2, dcap3) : sel(k, scap0, scap1, scap2, scap3);
+  }
+  __device__ __forceinline__ int nrep(int b) const { return b == dst ? dnrep : snrep; }
+  __device__ __forceinline__ bool alive(int b) const {
+    const uint32_t bit = b == dst ? 4u : (b == src ? 1u : 2u);
+    return (aliveBits & bit) != 0;
+  }
+  __device__ __forceinline__ bool allowed(int slot, int /*b == src*/) const { return (srcAllowed >> slot) & 1u; }
+  __device__ __forceinline__ double ru(int /*r*/, int k) const { return sel(k, ru0, ru1, ru2, ru3); }
+  __device__ __forceinline__ int flags(int) const { return rflags; }
+  __device__ __forceinline__ int rbroker(int) const { return src; }
+  __device__ __forceinline__ int rorig(int) const { return orig; }
+  __device__ __forceinline__ int rpart(int) const { return p; }
+  __device__ __forceinline__ bool hosts(int /*p*/, int b) const {
+    return (pb0 == b) | (pb1 == b) | (pb2 == b) | (pb3 == b) | (pb4 == b) | (pb5 == b) | (pb6 == b) | (pb7 == b);
+  }
 };
 
 constexpr int kBlock = 256;
-constexpr int kItems = 4;
 constexpr unsigned long long kNone = ~0ull;
 
 __device__ __forceinline__ unsigned long long waveMin(unsigned long long v) {
@@ -74,30 +307,55 @@ __device__ __forceinline__ unsigned long long blockBest(const unsigned long long
   return b;
 }
 
-__global__ __launch_bounds__(kBlock) void scan_cross(DevTables T, DevProgram prog, const int32_t* __restrict__ reps,
+// Last-arriver publish: every workgroup arrives once (after its final atomicMin); the last one reads the
+// winning key and writes ONE 64-bit word {seq:32 | key+1:32} (0 in the low half = no winner) to the host
+// mailbox — a single aligned 8-byte store, so the host never sees a sequence number without its key and
+// no system-scope fence (an L2 writeback) is needed. Keys of cross/pair scans are < 2^31 (host-checked).
+__device__ __forceinline__ void publishLast(unsigned long long* __restrict__ result, unsigned int* __restrict__ done,
+                                            unsigned long long* __restrict__ mail, unsigned long long seq) {
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");  // this workgroup's atomicMin before its arrival
+    const unsigned int prev = __hip_atomic_fetch_add(done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (prev == gridDim.x - 1) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      const unsigned long long v = __hip_atomic_load(&result[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const unsigned long long lo = v == kNone ? 0ull : (v + 1) & 0xffffffffull;
+      result[0] = kNone;  // self-cleaning: the next scan starts from a reset result and counter
+      *done = 0;
+      __hip_atomic_store(&mail[0], ((seq & 0xffffffffull) << 32) | lo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void scan_cross(DevTables T, MutTables Mt, UpdateList U, DevProgram prog,
+                                                     const int32_t* __restrict__ reps,
                                                      const int32_t* __restrict__ cands, int K, int N,
-                                                     unsigned long long* __restrict__ result) {
-  const DevView v{T};
+                                                     unsigned long long* __restrict__ result,
+                                                     unsigned int* __restrict__ done,
+                                                     unsigned long long* __restrict__ mail, unsigned long long seq) {
+  __shared__ OverlayLds ov;
+  overlayBegin(ov, U, Mt, T);
   const uint32_t total = (uint32_t)K * (uint32_t)N;
-  const uint32_t chunk = kBlock * kItems;
-  for (uint32_t base = blockIdx.x * chunk; base < total; base += gridDim.x * chunk) {
-    if (blockBest(result) <= base) return;  // an earlier pair already won: nothing later can (block-uniform)
+  for (uint32_t base = blockIdx.x * kBlock; base < total; base += gridDim.x * kBlock) {
+    if (blockBest(result) <= base) break;  // an earlier pair already won: nothing later can (block-uniform)
     unsigned long long local = kNone;
-#pragma unroll
-    for (int it = 0; it < kItems; ++it) {
-      const uint32_t q = base + it * kBlock + threadIdx.x;
-      if (q < total && local == kNone) {
-        const uint32_t k = q / (uint32_t)N;
-        const uint32_t j = q - k * (uint32_t)N;
-        if (moveCandidateAccepted(prog, v, reps[k], cands[j])) local = q;
-      }
+    const uint32_t q = base + threadIdx.x;
+    if (q < total) {
+      const uint32_t k = q / (uint32_t)N;
+      const uint32_t j = q - k * (uint32_t)N;
+      PreView v;
+      v.loadRow(T, prog, reps[k], ov);
+      v.loadDst(T, cands[j], ov);
+      if (moveCandidateAccepted(prog, v, v.r, v.dst)) local = q;
     }
     const unsigned long long m = blockMin(local);
     if (m != kNone) {
       if (threadIdx.x == 0) atomicMin(result, m);
-      return;
+      break;
     }
   }
+  publishLast(result, done, mail, seq);
 }
 
 // One wavefront per row (m, s). rowsPerBlock = kBlock / 64.
@@ -144,7 +402,8 @@ __global__ __launch_bounds__(kBlock) void scan_swap(DevTables T, DevProgram prog
 // Reference-equivalent candidate count of a swap scan: every row before the winning row ran to its first
 // terminal (or its end), plus the winning row up to its accepted candidate.
 __global__ __launch_bounds__(1024) void swap_visited_sum(const int32_t* __restrict__ rowVisited, long long rows,
-                                                         unsigned long long* __restrict__ result) {
+                                                         unsigned long long* __restrict__ result,
+                                                         unsigned long long* __restrict__ mail, unsigned long long seq) {
   __shared__ long long part[16];
   const unsigned long long best = result[0];
   const long long lim = best == kNone ? rows : (long long)(best >> 24) + 1;
@@ -158,115 +417,144 @@ __global__ __launch_bounds__(1024) void swap_visited_sum(const int32_t* __restri
     long long t = 0;
     for (int w = 0; w < (int)(blockDim.x >> 6); ++w) t += part[w];
     result[1] = (unsigned long long)t;
+    // rare path (swap scans): values first, then the sequence word behind a system-scope release
+    __hip_atomic_store(&mail[1], best, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(&mail[2], (unsigned long long)t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    result[0] = kNone;
+    result[1] = 0;
+    __hip_atomic_store(&mail[0], (seq & 0xffffffffull) << 32, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
   }
 }
 
 // PAIRS: explicit (replica, broker) list in iteration order (leadership moves: per-replica follower lists).
-__global__ __launch_bounds__(kBlock) void scan_pairs(DevTables T, DevProgram prog, const int32_t* __restrict__ pr,
+__global__ __launch_bounds__(kBlock) void scan_pairs(DevTables T, MutTables Mt, UpdateList U, DevProgram prog,
+                                                     const int32_t* __restrict__ pr,
                                                      const int32_t* __restrict__ pb, int n,
-                                                     unsigned long long* __restrict__ result) {
-  const DevView v{T};
-  const int chunk = kBlock * kItems;
-  for (int base = blockIdx.x * chunk; base < n; base += gridDim.x * chunk) {
-    if (blockBest(result) <= (unsigned long long)base) return;
+                                                     unsigned long long* __restrict__ result,
+                                                     unsigned int* __restrict__ done,
+                                                     unsigned long long* __restrict__ mail, unsigned long long seq) {
+  __shared__ OverlayLds ov;
+  overlayBegin(ov, U, Mt, T);
+  for (int base = blockIdx.x * kBlock; base < n; base += gridDim.x * kBlock) {
+    if (blockBest(result) <= (unsigned long long)base) break;
     unsigned long long local = kNone;
-#pragma unroll
-    for (int it = 0; it < kItems; ++it) {
-      const int q = base + it * kBlock + threadIdx.x;
-      if (q < n && local == kNone && moveCandidateAccepted(prog, v, pr[q], pb[q])) local = (unsigned long long)q;
+    const int q = base + threadIdx.x;
+    if (q < n) {
+      PreView v;
+      v.loadRow(T, prog, pr[q], ov);
+      v.loadDst(T, pb[q], ov);
+      if (moveCandidateAccepted(prog, v, v.r, v.dst)) local = (unsigned long long)q;
     }
     const unsigned long long m = blockMin(local);
     if (m != kNone) {
       if (threadIdx.x == 0) atomicMin(result, m);
-      return;
+      break;
     }
   }
+  publishLast(result, done, mail, seq);
 }
 
-__global__ void apply_rows(double* bUtil, int32_t* bNrep, int32_t* bNlead, double* bPot, uint8_t* bAlive, int B,
-                           const BrokerRow* __restrict__ brows, int nb, double* rUtil, int32_t* rBroker, uint8_t* rFlags,
-                           int R, const ReplicaRow* __restrict__ rrows, int nr, const int32_t* __restrict__ pOff,
-                           int32_t* pBrokers, const PartitionRow* __restrict__ prows, int np, int32_t* topicCount,
-                           int ldB, const TopicCountDelta* __restrict__ tdel, int nt) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < nb) {
-    const BrokerRow& x = brows[i];
+__global__ __launch_bounds__(256) void prep(double* bUtil, int32_t* bNrep, int32_t* bNlead, double* bPot,
+                                            uint8_t* bAlive, int B, const BrokerRow* __restrict__ brows, int nb,
+                                            double* rUtil, int32_t* rBroker, uint8_t* rFlags, int R,
+                                            const ReplicaRow* __restrict__ rrows, int nr,
+                                            const int32_t* __restrict__ pOff, int32_t* pBrokers,
+                                            const PartitionRow* __restrict__ prows, int np, int32_t* topicCount,
+                                            int ldB, const TopicCountDelta* __restrict__ tdel, int nt,
+                                            const int4* __restrict__ req, int4* __restrict__ dReq, int nReq4,
+                                            unsigned long long* __restrict__ result, unsigned int* __restrict__ done) {
+  const int stride = gridDim.x * blockDim.x;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x;; i += stride) {
+    if (i >= nb && i >= nr && i >= np && i >= nt && i >= nReq4) break;
+    if (i < nb) {
+      const BrokerRow x = brows[i];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) bUtil[(size_t)k * B + x.b] = x.util[k];
-    bNrep[x.b] = x.nrep;
-    bNlead[x.b] = x.nlead;
-    bPot[x.b] = x.potNwOut;
-    bAlive[x.b] = (uint8_t)x.alive;
-  }
-  if (i < nr) {
-    const ReplicaRow& x = rrows[i];
+      for (int k = 0; k < 4; ++k) bUtil[(size_t)k * B + x.b] = x.util[k];
+      bNrep[x.b] = x.nrep;
+      bNlead[x.b] = x.nlead;
+      bPot[x.b] = x.potNwOut;
+      bAlive[x.b] = (uint8_t)x.alive;
+    }
+    if (i < nr) {
+      const ReplicaRow x = rrows[i];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) rUtil[(size_t)k * R + x.r] = x.util[k];
-    rBroker[x.r] = x.broker;
-    rFlags[x.r] = (uint8_t)x.flags;
+      for (int k = 0; k < 4; ++k) rUtil[(size_t)k * R + x.r] = x.util[k];
+      rBroker[x.r] = x.broker;
+      rFlags[x.r] = (uint8_t)x.flags;
+    }
+    if (i < np) {
+      const PartitionRow x = prows[i];
+      const int o = pOff[x.p];
+      for (int k = 0; k < x.n; ++k) pBrokers[o + k] = x.brokers[k];
+    }
+    if (i < nt) {
+      const TopicCountDelta d = tdel[i];
+      atomicAdd(&topicCount[(size_t)d.topic * ldB + d.broker], d.delta);
+    }
+    if (i < nReq4) dReq[i] = req[i];
   }
-  if (i < np) {
-    const PartitionRow& x = prows[i];
-    const int o = pOff[x.p];
-    for (int k = 0; k < x.n; ++k) pBrokers[o + k] = x.brokers[k];
-  }
-  if (i < nt) {
-    const TopicCountDelta& d = tdel[i];
-    atomicAdd(&topicCount[(size_t)d.topic * ldB + d.broker], d.delta);
+  if (blockIdx.x == 0 && threadIdx.x == 0 && result) {
+    result[0] = kNone;
+    result[1] = 0;
+    *done = 0;
   }
 }
 
 // ------------------------------------------------------------------------------------------------ launchers
-hipError_t launchScanCross(const DevTables& T, const DevProgram& prog, const int32_t* reps, const int32_t* cands, int K,
-                           int N, unsigned long long* result, hipStream_t st) {
-  const uint64_t total = (uint64_t)K * (uint64_t)N;
-  const uint64_t chunk = kBlock * kItems;
-  uint64_t blocks = (total + chunk - 1) / chunk;
+static unsigned gridFor(uint64_t work, uint64_t perBlock) {
+  uint64_t blocks = (work + perBlock - 1) / perBlock;
   if (blocks > 4096) blocks = 4096;
   if (blocks == 0) blocks = 1;
-  hipLaunchKernelGGL(scan_cross, dim3((unsigned)blocks), dim3(kBlock), 0, st, T, prog, reps, cands, K, N, result);
+  return (unsigned)blocks;
+}
+
+hipError_t launchScanCross(const DevTables& T, const MutTables& M, const UpdateList& U, const DevProgram& prog,
+                           const int32_t* reps, const int32_t* cands, int K, int N, unsigned long long* result,
+                           unsigned int* done, unsigned long long* mail, unsigned long long seq, hipStream_t st) {
+  const unsigned blocks = gridFor((uint64_t)K * (uint64_t)N, (uint64_t)kBlock);
+  hipLaunchKernelGGL(scan_cross, dim3(blocks), dim3(kBlock), 0, st, T, M, U, prog, reps, cands, K, N, result, done,
+                     mail, seq);
   return hipGetLastError();
 }
 
 hipError_t launchScanSwap(const DevTables& T, const DevProgram& prog, const int32_t* srcs, int S, const int32_t* cbOff,
-                          const int32_t* cbRep, int M, unsigned long long* result, int32_t* rowVisited, hipStream_t st,
-                          hipEvent_t ev0, hipEvent_t ev1) {
+                          const int32_t* cbRep, int M, unsigned long long* result, int32_t* rowVisited,
+                          unsigned long long* mail, unsigned long long seq, hipStream_t st, hipEvent_t ev0,
+                          hipEvent_t ev1) {
   const uint64_t rows = (uint64_t)M * (uint64_t)S;
-  uint64_t blocks = (rows + (kBlock / 64) - 1) / (kBlock / 64);
-  if (blocks > 4096) blocks = 4096;
-  if (blocks == 0) blocks = 1;
+  const unsigned blocks = gridFor(rows, kBlock / 64);
   if (ev0) (void)hipEventRecord(ev0, st);
-  hipLaunchKernelGGL(scan_swap, dim3((unsigned)blocks), dim3(kBlock), 0, st, T, prog, srcs, S, cbOff, cbRep, M, result,
+  hipLaunchKernelGGL(scan_swap, dim3(blocks), dim3(kBlock), 0, st, T, prog, srcs, S, cbOff, cbRep, M, result,
                      rowVisited);
   if (ev1) (void)hipEventRecord(ev1, st);
-  hipLaunchKernelGGL(swap_visited_sum, dim3(1), dim3(1024), 0, st, rowVisited, (long long)rows, result);
+  hipLaunchKernelGGL(swap_visited_sum, dim3(1), dim3(1024), 0, st, rowVisited, (long long)rows, result, mail, seq);
   return hipGetLastError();
 }
 
-hipError_t launchScanPairs(const DevTables& T, const DevProgram& prog, const int32_t* pr, const int32_t* pb, int n,
-                           unsigned long long* result, hipStream_t st) {
-  const int chunk = kBlock * kItems;
-  int blocks = (n + chunk - 1) / chunk;
-  if (blocks > 4096) blocks = 4096;
-  if (blocks < 1) blocks = 1;
-  hipLaunchKernelGGL(scan_pairs, dim3(blocks), dim3(kBlock), 0, st, T, prog, pr, pb, n, result);
+hipError_t launchScanPairs(const DevTables& T, const MutTables& M, const UpdateList& U, const DevProgram& prog,
+                           const int32_t* pr, const int32_t* pb, int n, unsigned long long* result, unsigned int* done,
+                           unsigned long long* mail, unsigned long long seq, hipStream_t st) {
+  const unsigned blocks = gridFor((uint64_t)n, (uint64_t)kBlock);
+  hipLaunchKernelGGL(scan_pairs, dim3(blocks), dim3(kBlock), 0, st, T, M, U, prog, pr, pb, n, result, done, mail, seq);
   return hipGetLastError();
 }
 
-hipError_t launchApplyRows(double* bUtil, int32_t* bNrep, int32_t* bNlead, double* bPot, uint8_t* bAlive, int B,
-                           const BrokerRow* brows, int nb, double* rUtil, int32_t* rBroker, uint8_t* rFlags, int R,
-                           const ReplicaRow* rrows, int nr, const int32_t* pOff, int32_t* pBrokers,
-                           const PartitionRow* prows, int np, int32_t* topicCount, int ldB, const TopicCountDelta* tdel,
-                           int nt, hipStream_t st) {
+hipError_t launchPrep(double* bUtil, int32_t* bNrep, int32_t* bNlead, double* bPot, uint8_t* bAlive, int B,
+                      const BrokerRow* brows, int nb, double* rUtil, int32_t* rBroker, uint8_t* rFlags, int R,
+                      const ReplicaRow* rrows, int nr, const int32_t* pOff, int32_t* pBrokers,
+                      const PartitionRow* prows, int np, int32_t* topicCount, int ldB, const TopicCountDelta* tdel,
+                      int nt, const int4* req, int4* dReq, int nReq4, unsigned long long* result, unsigned int* done,
+                      hipStream_t st) {
   int n = nb;
   if (nr > n) n = nr;
   if (np > n) n = np;
   if (nt > n) n = nt;
-  if (n == 0) return hipSuccess;
-  const int threads = 256;
-  const int blocks = (n + threads - 1) / threads;
-  hipLaunchKernelGGL(apply_rows, dim3(blocks), dim3(threads), 0, st, bUtil, bNrep, bNlead, bPot, bAlive, B, brows, nb,
-                     rUtil, rBroker, rFlags, R, rrows, nr, pOff, pBrokers, prows, np, topicCount, ldB, tdel, nt);
+  if (nReq4 > n) n = nReq4;
+  if (n == 0 && !result) return hipSuccess;
+  const unsigned blocks = gridFor((uint64_t)(n ? n : 1), 256);
+  hipLaunchKernelGGL(prep, dim3(blocks), dim3(256), 0, st, bUtil, bNrep, bNlead, bPot, bAlive, B, brows, nb, rUtil,
+                     rBroker, rFlags, R, rrows, nr, pOff, pBrokers, prows, np, topicCount, ldB, tdel, nt, req, dReq,
+                     nReq4, result, done);
   return hipGetLastError();
 }
 

@@ -37,6 +37,11 @@ struct View {
   int pbegin(int p) const { return e.pOff[p]; }
   int pend(int p) const { return e.pOff[p + 1]; }
   int pbroker(int i) const { return e.pBrokers[i]; }
+  bool hosts(int p, int b) const {
+    bool has = false;
+    for (int i = pbegin(p); i < pend(p); ++i) has |= (pbroker(i) == b);
+    return has;
+  }
 };
 Emu& E(void* st) { return *static_cast<Emu*>(st); }
 }  // namespace
