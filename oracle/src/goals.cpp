@@ -62,7 +62,7 @@ void ensureNoOfflineReplicas(ClusterModel& cm, const std::string& goal) {
       throw OptimizationFailure("[" + goal + "] Cannot remove replica from broker " +
                                 std::to_string(cm.brokers[cm.replicas[r].broker].id));
 }
-static void ensureReplicasMoveOffBrokersWithBadDisks(ClusterModel& cm, const std::string& goal) {
+void ensureReplicasMoveOffBrokersWithBadDisks(ClusterModel& cm, const std::string& goal) {
   for (int b : cm.brokersWithBadDisks)
     for (int r : cm.brokers[b].replicas)
       if (cm.partitions[cm.replicas[r].partition].ineligibleBrokers.count(b))

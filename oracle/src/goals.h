@@ -10,6 +10,8 @@
 //                           analyzer/goals/ResourceDistributionGoal.java:55-1078
 // Wall-clock fast-mode timeouts are treated as infinite (parity mode).
 #pragma once
+#include <functional>
+#include <set>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -69,6 +71,7 @@ std::vector<int> eligibleBrokers(ClusterModel& cm, int replica, const std::vecto
 bool legitMove(ClusterModel& cm, int replica, int destBroker, ActionType a);
 Acceptance isProposalAcceptableForOptimizedGoals(const GoalList& g, const BalancingAction& a, ClusterModel& cm);
 void ensureNoOfflineReplicas(ClusterModel& cm, const std::string& goal);
+void ensureReplicasMoveOffBrokersWithBadDisks(ClusterModel& cm, const std::string& goal);
 std::vector<int> javaHashSetOrderIntKeys(const std::vector<int>& insertionOrder);
 
 class ReplicaDistributionGoal : public AbstractGoal {
@@ -158,6 +161,203 @@ class ResourceDistributionGoal : public AbstractGoal {
   double upperThr_ = 0, lowerThr_ = 0;
   std::vector<char> allowed_;
   bool isLowUtilization_ = false;
+};
+
+// ===================================================================== remaining default goals
+//   RackAwareGoal / AbstractRackAwareGoal  analyzer/goals/RackAwareGoal.java, AbstractRackAwareGoal.java
+//   MinTopicLeadersPerBrokerGoal           analyzer/goals/MinTopicLeadersPerBrokerGoal.java (default config:
+//                                          no topic matches, so only moveAwayOfflineReplicas acts)
+//   ReplicaCapacityGoal                    analyzer/goals/ReplicaCapacityGoal.java
+//   CapacityGoal (Disk/NwIn/NwOut/Cpu)     analyzer/goals/CapacityGoal.java
+//   PotentialNwOutGoal                     analyzer/goals/PotentialNwOutGoal.java
+//   TopicReplicaDistributionGoal           analyzer/goals/TopicReplicaDistributionGoal.java
+//   LeaderReplicaDistributionGoal          analyzer/goals/LeaderReplicaDistributionGoal.java (+ ReplicaDistributionAbstractGoal)
+//   LeaderBytesInDistributionGoal          analyzer/goals/LeaderBytesInDistributionGoal.java
+
+class RackAwareGoal : public AbstractGoal {
+ public:
+  using AbstractGoal::AbstractGoal;
+  std::string name() const override { return "RackAwareGoal"; }
+  bool isHardGoal() const override { return true; }
+  Acceptance actionAcceptance(const BalancingAction& a, ClusterModel& cm) override;
+  int compareStats(const ClusterModelStats&, const ClusterModelStats&) const override { return 0; }
+
+ protected:
+  void initGoalState(ClusterModel& cm, const OptimizationOptions& o) override;
+  void updateGoalState(ClusterModel& cm, const OptimizationOptions& o) override;
+  void rebalanceForBroker(int broker, ClusterModel& cm, const GoalList& g, const OptimizationOptions& o) override;
+  bool selfSatisfied(ClusterModel&, const BalancingAction&) override { return true; }
+
+ private:
+  bool violates(ClusterModel& cm, int replica, int destBroker) const;
+  bool shouldKeepInTheCurrentBroker(ClusterModel& cm, int replica) const;
+  std::vector<int> rackAwareEligibleBrokers(ClusterModel& cm, int replica) const;
+};
+
+class MinTopicLeadersPerBrokerGoal : public AbstractGoal {
+ public:
+  using AbstractGoal::AbstractGoal;
+  std::string name() const override { return "MinTopicLeadersPerBrokerGoal"; }
+  bool isHardGoal() const override { return false; }
+  Acceptance actionAcceptance(const BalancingAction& a, ClusterModel& cm) override;
+  int compareStats(const ClusterModelStats&, const ClusterModelStats&) const override { return 0; }
+
+ protected:
+  void initGoalState(ClusterModel& cm, const OptimizationOptions& o) override;
+  void updateGoalState(ClusterModel& cm, const OptimizationOptions& o) override;
+  void rebalanceForBroker(int broker, ClusterModel& cm, const GoalList& g, const OptimizationOptions& o) override;
+  bool selfSatisfied(ClusterModel& cm, const BalancingAction& a) override;
+};
+
+class ReplicaCapacityGoal : public AbstractGoal {
+ public:
+  using AbstractGoal::AbstractGoal;
+  std::string name() const override { return "ReplicaCapacityGoal"; }
+  bool isHardGoal() const override { return true; }
+  Acceptance actionAcceptance(const BalancingAction& a, ClusterModel& cm) override;
+  int compareStats(const ClusterModelStats&, const ClusterModelStats&) const override { return 0; }
+
+ protected:
+  void initGoalState(ClusterModel& cm, const OptimizationOptions& o) override;
+  void updateGoalState(ClusterModel& cm, const OptimizationOptions& o) override;
+  void rebalanceForBroker(int broker, ClusterModel& cm, const GoalList& g, const OptimizationOptions& o) override;
+  bool selfSatisfied(ClusterModel& cm, const BalancingAction& a) override;
+
+ private:
+  bool selfHealingMode_ = false;
+};
+
+class CapacityGoal : public AbstractGoal {
+ public:
+  CapacityGoal(const BalancingConstraint& bc, int resource) : AbstractGoal(bc), resource_(resource) {}
+  std::string name() const override;
+  bool isHardGoal() const override { return true; }
+  Acceptance actionAcceptance(const BalancingAction& a, ClusterModel& cm) override;
+  int compareStats(const ClusterModelStats&, const ClusterModelStats&) const override { return 0; }
+
+ protected:
+  void initGoalState(ClusterModel& cm, const OptimizationOptions& o) override;
+  void updateGoalState(ClusterModel& cm, const OptimizationOptions& o) override;
+  void rebalanceForBroker(int broker, ClusterModel& cm, const GoalList& g, const OptimizationOptions& o) override;
+  bool selfSatisfied(ClusterModel& cm, const BalancingAction& a) override;
+
+ private:
+  bool utilizationOverLimit(ClusterModel& cm, int b, double brokerLimit, double hostLimit) const;
+  bool underLimitAfterAdding(ClusterModel& cm, int b, double util) const;
+  bool movementAcceptable(ClusterModel& cm, int srcReplica, int destBroker) const;
+  bool swapAcceptable(ClusterModel& cm, int srcReplica, int destReplica) const;
+  int resource_;
+};
+
+class PotentialNwOutGoal : public AbstractGoal {
+ public:
+  using AbstractGoal::AbstractGoal;
+  std::string name() const override { return "PotentialNwOutGoal"; }
+  bool isHardGoal() const override { return false; }
+  Acceptance actionAcceptance(const BalancingAction& a, ClusterModel& cm) override;
+  int compareStats(const ClusterModelStats& s1, const ClusterModelStats& s2) const override {
+    return icompare(s1.numBrokersUnderPotentialNwOut, s2.numBrokersUnderPotentialNwOut);
+  }
+
+ protected:
+  void initGoalState(ClusterModel& cm, const OptimizationOptions& o) override;
+  void updateGoalState(ClusterModel& cm, const OptimizationOptions& o) override;
+  void rebalanceForBroker(int broker, ClusterModel& cm, const GoalList& g, const OptimizationOptions& o) override;
+  bool selfSatisfied(ClusterModel& cm, const BalancingAction& a) override;
+  std::vector<int> brokersToBalance(ClusterModel& cm) override;
+
+ private:
+  double leaderNwOutOf(ClusterModel& cm, int partition) const {
+    return cm.replicaUtil(cm.partitions[partition].leader, NW_OUT);
+  }
+  bool fixOfflineReplicasOnly_ = false;
+};
+
+class TopicReplicaDistributionGoal : public AbstractGoal {
+ public:
+  using AbstractGoal::AbstractGoal;
+  std::string name() const override { return "TopicReplicaDistributionGoal"; }
+  bool isHardGoal() const override { return false; }
+  Acceptance actionAcceptance(const BalancingAction& a, ClusterModel& cm) override;
+  int compareStats(const ClusterModelStats& s1, const ClusterModelStats& s2) const override;
+  int upperLimit(int topic) const { return upper_[topic]; }
+  int lowerLimit(int topic) const { return lower_[topic]; }
+
+ protected:
+  void initGoalState(ClusterModel& cm, const OptimizationOptions& o) override;
+  void updateGoalState(ClusterModel& cm, const OptimizationOptions& o) override;
+  void rebalanceForBroker(int broker, ClusterModel& cm, const GoalList& g, const OptimizationOptions& o) override;
+  bool selfSatisfied(ClusterModel& cm, const BalancingAction& a) override;
+
+ private:
+  int count(const ClusterModel& cm, int b, int topic) const {
+    auto it = cm.brokers[b].topicReplicaCount.find(topic);
+    return it == cm.brokers[b].topicReplicaCount.end() ? 0 : it->second;
+  }
+  bool underUpperAfter(const ClusterModel& cm, int topic, int b, bool add) const;
+  bool aboveLowerAfter(const ClusterModel& cm, int topic, int b, bool add) const;
+  std::vector<int> replicasToMoveOut(ClusterModel& cm, int b, int topic);
+  bool moveOut(int b, int topic, ClusterModel& cm, const GoalList& g, const OptimizationOptions& o);
+  bool moveIn(int b, int topic, ClusterModel& cm, const GoalList& g, const OptimizationOptions& o);
+  bool isExcluded(int b) const { return !allowed_[b]; }
+  bool fixOfflineReplicasOnly_ = false;
+  std::vector<int> upper_, lower_;
+  std::vector<char> rebalanceTopic_;
+  std::vector<char> allowed_;
+  bool anyAbove_ = false, anyUnder_ = false;
+};
+
+class LeaderReplicaDistributionGoal : public AbstractGoal {
+ public:
+  using AbstractGoal::AbstractGoal;
+  std::string name() const override { return "LeaderReplicaDistributionGoal"; }
+  bool isHardGoal() const override { return false; }
+  Acceptance actionAcceptance(const BalancingAction& a, ClusterModel& cm) override;
+  int compareStats(const ClusterModelStats& s1, const ClusterModelStats& s2) const override;
+  int balanceUpperLimit() const { return upper_; }
+  int balanceLowerLimit() const { return lower_; }
+
+ protected:
+  void initGoalState(ClusterModel& cm, const OptimizationOptions& o) override;
+  void updateGoalState(ClusterModel& cm, const OptimizationOptions& o) override;
+  void rebalanceForBroker(int broker, ClusterModel& cm, const GoalList& g, const OptimizationOptions& o) override;
+  bool selfSatisfied(ClusterModel& cm, const BalancingAction& a) override;
+
+ private:
+  Acceptance leaderMovementSatisfiable(ClusterModel& cm, int src, int dst) const;
+  bool moveLeadershipOut(int b, ClusterModel& cm, const GoalList& g, const OptimizationOptions& o);
+  bool moveLeadershipIn(int b, ClusterModel& cm, const GoalList& g, const OptimizationOptions& o);
+  bool moveReplicasOut(int b, ClusterModel& cm, const GoalList& g, const OptimizationOptions& o);
+  bool moveLeaderReplicasIn(int b, ClusterModel& cm, const GoalList& g, const OptimizationOptions& o);
+  bool isExcluded(int b) const { return !allowed_[b]; }
+  bool fixOfflineReplicasOnly_ = false;
+  int upper_ = 0, lower_ = 0;
+  std::vector<char> allowed_;
+  bool anyAbove_ = false, anyUnder_ = false;
+};
+
+class LeaderBytesInDistributionGoal : public AbstractGoal {
+ public:
+  using AbstractGoal::AbstractGoal;
+  std::string name() const override { return "LeaderBytesInDistributionGoal"; }
+  bool isHardGoal() const override { return false; }
+  Acceptance actionAcceptance(const BalancingAction& a, ClusterModel& cm) override;
+  int compareStats(const ClusterModelStats& s1, const ClusterModelStats& s2) const override;
+  double meanLeaderBytesIn() const { return mean_; }
+
+ protected:
+  void initGoalState(ClusterModel& cm, const OptimizationOptions& o) override;
+  void updateGoalState(ClusterModel& cm, const OptimizationOptions& o) override;
+  void rebalanceForBroker(int broker, ClusterModel& cm, const GoalList& g, const OptimizationOptions& o) override;
+  bool selfSatisfied(ClusterModel& cm, const BalancingAction& a) override;
+  std::vector<int> brokersToBalance(ClusterModel& cm) override;
+
+ private:
+  void initMean(ClusterModel& cm);
+  double threshold(ClusterModel& cm, int b);
+  double mean_ = 0.0;
+  int numAllowed_ = 0;
+  bool overLimit_ = false;
 };
 
 }  // namespace oracle

@@ -46,18 +46,24 @@ int ReplicaCmp::compare(int a, int b) const {
     int c = dcompare(s1, s2);
     if (c != 0) return c;
   }
-  // Replica.compareTo (Replica.java:350-376)
-  bool o1 = cm->isCurrentOffline(a), o2 = cm->isCurrentOffline(b);
+  return cm->replicaCompareTo(a, b);
+}
+int ClusterModel::replicaCompareTo(int a, int b) const {
+  bool o1 = isCurrentOffline(a), o2 = isCurrentOffline(b);
   if (o1 && !o2) return -1;
   if (!o1 && o2) return 1;
-  const Replica& ra = cm->replicas[a];
-  const Replica& rb = cm->replicas[b];
-  const Partition& pa = cm->partitions[ra.partition];
-  const Partition& pb = cm->partitions[rb.partition];
+  const Replica& ra = replicas[a];
+  const Replica& rb = replicas[b];
+  const Partition& pa = partitions[ra.partition];
+  const Partition& pb = partitions[rb.partition];
   if (pa.number != pb.number) return pa.number > pb.number ? 1 : -1;
-  int ida = cm->brokers[ra.origBroker].id, idb = cm->brokers[rb.origBroker].id;
+  int ida = brokers[ra.origBroker].id, idb = brokers[rb.origBroker].id;
   if (ida != idb) return ida > idb ? 1 : -1;
-  int ta = cm->topicRank[pa.topic], tb = cm->topicRank[pb.topic];
+  if ((int)topicRank.size() != numTopics()) {  // before finalizeTopics: String.compareTo on the names
+    const int c = topicNames[pa.topic].compare(topicNames[pb.topic]);
+    return c == 0 ? 0 : (c < 0 ? -1 : 1);
+  }
+  int ta = topicRank[pa.topic], tb = topicRank[pb.topic];
   return ta == tb ? 0 : (ta < tb ? -1 : 1);
 }
 bool ReplicaCmp::operator()(int a, int b) const { return compare(a, b) < 0; }
@@ -138,6 +144,10 @@ int ClusterModel::createBroker(int rackIdx, int brokerId, const double cap[NUM_R
   Broker b;
   b.id = brokerId;
   b.rack = rackIdx;
+  b.replicaSet.setComparator([this](int x, int y) { return replicaCompareTo(x, y); });
+  b.leaderSet.setComparator([this](int x, int y) { return replicaCompareTo(x, y); });
+  b.offlineSet.setComparator([this](int x, int y) { return replicaCompareTo(x, y); });
+  b.topicKeys.setComparator([this](int x, int y) { return topicNames[x].compare(topicNames[y]); });
   for (int r = 0; r < NUM_RESOURCES; ++r) b.capacity[r] = cap[r];
   brokers.push_back(std::move(b));
   potentialLeadershipLoad.emplace_back();
@@ -149,6 +159,7 @@ int ClusterModel::ensureTopic(const std::string& name) {
   for (int i = (int)topicNames.size() - 1; i >= 0; --i)
     if (topicNames[i] == name) return i;
   topicNames.push_back(name);
+  topicHash.push_back(jStringHash(name));
   numReplicasByTopic.push_back(0);
   replicationFactorByTopic.push_back(0);
   return (int)topicNames.size() - 1;
@@ -228,7 +239,8 @@ void ClusterModel::refreshCapacity() {
 void ClusterModel::setBrokerState(int b, BrokerState s) {
   Broker& br = brokers[b];
   br.state = s;
-  if (!br.isAlive()) {  // Broker.setState
+  if (!br.isAlive()) {  // Broker.setState: _currentOfflineReplicas.addAll(replicas())
+    for (int r : br.replicaSet.order()) br.offlineSet.add(r, replicaHash(r));
     for (int r : br.replicas) {
       if (!replicas[r].inBrokerOffline) {
         replicas[r].inBrokerOffline = true;
@@ -345,6 +357,8 @@ void ClusterModel::brokerAddReplica(int b, int r) {
   Replica& rep = replicas[r];
   rep.posInBroker = (int)br.replicas.size();
   br.replicas.push_back(r);
+  br.replicaSet.add(r, replicaHash(r));
+  br.topicKeys.add(partitions[rep.partition].topic, topicHash[partitions[rep.partition].topic]);
   rep.inBrokerImmigrants = rep.inBrokerOffline = rep.inBrokerLeaders = false;
   if (brokers[rep.origBroker].id != br.id) {
     rep.inBrokerImmigrants = true;
@@ -352,12 +366,14 @@ void ClusterModel::brokerAddReplica(int b, int r) {
   } else if (isOriginalOffline(r)) {
     rep.inBrokerOffline = true;
     br.numOffline++;
+    br.offlineSet.add(r, replicaHash(r));
   }
   br.topicReplicaCount[partitions[rep.partition].topic] += 1;
   if (rep.isLeader) {
     loadAddLoad(br.leadershipLoadForNwResources, rep.load, W);
     rep.inBrokerLeaders = true;
     br.numLeaders++;
+    br.leaderSet.add(r, replicaHash(r));
   }
   loadAddLoad(br.load, rep.load, W);
   sortedAdd(b, r);
@@ -375,11 +391,14 @@ int ClusterModel::brokerRemoveReplica(int b, int partition) {
   replicas[last].posInBroker = pos;
   br.replicas.pop_back();
   rep.posInBroker = -1;
+  br.replicaSet.remove(r, replicaHash(r));
+  br.offlineSet.remove(r, replicaHash(r));
   loadSubLoad(br.load, rep.load, W);
   br.topicReplicaCount[partitions[partition].topic] -= 1;
   if (rep.isLeader) {
     loadSubLoad(br.leadershipLoadForNwResources, rep.load, W);
     if (rep.inBrokerLeaders) br.numLeaders--;
+    br.leaderSet.remove(r, replicaHash(r));
   }
   rep.inBrokerLeaders = false;
   if (rep.inBrokerImmigrants) br.numImmigrants--;
@@ -439,6 +458,7 @@ Load ClusterModel::brokerMakeFollower(int b, int partition) {
     replicas[r].inBrokerLeaders = false;
     br.numLeaders--;
   }
+  br.leaderSet.remove(r, replicaHash(r));
   sortedAdd(b, r);
   return delta;
 }
@@ -455,7 +475,14 @@ void ClusterModel::brokerMakeLeader(int b, int partition, const Load& delta) {
     replicas[r].inBrokerLeaders = true;
     br.numLeaders++;
   }
+  br.leaderSet.add(r, replicaHash(r));
   sortedAdd(b, r);
+}
+
+std::vector<int> ClusterModel::partitionBrokersSet(int p) const {
+  JHashSet set;
+  for (int r : partitions[p].replicas) set.add(replicas[r].broker, brokers[replicas[r].broker].id);
+  return set.order();
 }
 
 // ------------------------------------------------------------------ cluster mutations

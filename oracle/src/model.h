@@ -202,6 +202,10 @@ struct Broker {
   Load load;
   Load leadershipLoadForNwResources;
   std::map<std::string, std::unique_ptr<SortedReplicas>> sorted;
+  // Java iteration order of Broker._replicas / _leaderReplicas (HashSet<Replica>) and of the
+  // Broker._topicReplicas key set (HashMap<String, ...>, keys never removed)
+  JHashSet replicaSet, leaderSet, topicKeys;
+  JHashSet offlineSet;  // Broker._currentOfflineReplicas
   bool isAlive() const { return state != BrokerState::DEAD; }
   bool isNew() const { return state == BrokerState::NEW; }
   bool hasBadDisks() const { return state == BrokerState::BAD_DISKS; }
@@ -244,6 +248,7 @@ class ClusterModel {
   std::vector<Broker> brokers;  // index == broker id
   std::vector<Rack> racks;
   std::vector<std::string> topicNames;
+  std::vector<int32_t> topicHash;  // String.hashCode of each topic name
   std::vector<int> topicRank;  // rank of topic name in String.compareTo order
   std::vector<Partition> partitions;
   std::vector<Replica> replicas;
@@ -294,6 +299,18 @@ class ClusterModel {
     return c > 0 ? brokerUtil(b, res) / c : 1.0;
   }
   int numReplicas() const { return (int)replicas.size(); }
+  // TopicPartition.hashCode (kafka-clients: 31 * (31 + partition) + topic.hashCode()) and
+  // Replica.hashCode (Replica.java:392-394: Objects.hash(tp, originalBroker.id()))
+  int32_t tpHash(int p) const { return jHashMix(jHashMix(1, partitions[p].number), topicHash[partitions[p].topic]); }
+  int32_t replicaHash(int r) const {
+    return jHashMix(jHashMix(1, tpHash(replicas[r].partition)), brokers[replicas[r].origBroker].id);
+  }
+  // Replica.compareTo (Replica.java:349-377): offline first, partition number, original broker id, topic name
+  int replicaCompareTo(int a, int b) const;
+  // Partition.partitionBrokers(): HashSet<Broker> filled in partition replica order (Broker.hashCode == id)
+  std::vector<int> partitionBrokersSet(int p) const;
+  double leadershipNwIn(int b) const { return expectedUtil(brokers[b].leadershipLoadForNwResources, NW_IN, W); }
+  double potentialNwOut(int b) const { return expectedUtil(potentialLeadershipLoad[b], NW_OUT, W); }
   int numTopics() const { return (int)topicNames.size(); }
   std::vector<int> aliveBrokers() const;  // HashSet<Broker> iteration order == ascending id here
   std::vector<int> aliveBrokersUnderThreshold(int res, double thr) const;

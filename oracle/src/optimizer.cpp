@@ -9,6 +9,17 @@ namespace oracle {
 
 std::unique_ptr<Goal> makeGoal(int kind, const BalancingConstraint& bc) {
   switch (kind) {
+    case CCMI_GOAL_RACK_AWARE: return std::make_unique<RackAwareGoal>(bc);
+    case CCMI_GOAL_MIN_TOPIC_LEADERS_PER_BROKER: return std::make_unique<MinTopicLeadersPerBrokerGoal>(bc);
+    case CCMI_GOAL_REPLICA_CAPACITY: return std::make_unique<ReplicaCapacityGoal>(bc);
+    case CCMI_GOAL_DISK_CAPACITY: return std::make_unique<CapacityGoal>(bc, DISK);
+    case CCMI_GOAL_NW_IN_CAPACITY: return std::make_unique<CapacityGoal>(bc, NW_IN);
+    case CCMI_GOAL_NW_OUT_CAPACITY: return std::make_unique<CapacityGoal>(bc, NW_OUT);
+    case CCMI_GOAL_CPU_CAPACITY: return std::make_unique<CapacityGoal>(bc, CPU);
+    case CCMI_GOAL_POTENTIAL_NW_OUT: return std::make_unique<PotentialNwOutGoal>(bc);
+    case CCMI_GOAL_TOPIC_REPLICA_DISTRIBUTION: return std::make_unique<TopicReplicaDistributionGoal>(bc);
+    case CCMI_GOAL_LEADER_REPLICA_DISTRIBUTION: return std::make_unique<LeaderReplicaDistributionGoal>(bc);
+    case CCMI_GOAL_LEADER_BYTES_IN_DISTRIBUTION: return std::make_unique<LeaderBytesInDistributionGoal>(bc);
     case CCMI_GOAL_REPLICA_DISTRIBUTION: return std::make_unique<ReplicaDistributionGoal>(bc);
     case CCMI_GOAL_DISK_USAGE_DISTRIBUTION: return std::make_unique<ResourceDistributionGoal>(bc, DISK);
     case CCMI_GOAL_NW_IN_USAGE_DISTRIBUTION: return std::make_unique<ResourceDistributionGoal>(bc, NW_IN);
