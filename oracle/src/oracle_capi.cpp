@@ -127,6 +127,7 @@ void* oc_from_desc(const ccmi_cluster_desc* d) {
     for (int b = 0; b < d->num_brokers; ++b) cm.createBroker(d->broker_rack[b], d->broker_id[b], &d->broker_capacity[4 * b]);
     for (int t = 0; t < d->num_topics; ++t) {
       cm.topicNames.push_back(d->topic_names[t]);
+      cm.topicHash.push_back(jStringHash(cm.topicNames.back()));
       cm.numReplicasByTopic.push_back(0);
       cm.replicationFactorByTopic.push_back(0);
     }
