@@ -61,6 +61,24 @@ def cpu_baseline(buf) -> dict:
             "proposal_wall_s": dt}
 
 
+SCAN_KERNELS = ("scan_cross", "scan_pairs", "scan_swap")
+
+
+def pmc_traffic(workload: str):
+    """HBM bytes per scan launch from the newest committed PMC summary of this workload (profiles/rNN/
+    <workload>_pmc_summary.json, written by tools/pmc_summary.py from separate rocprofv3 --pmc FETCH_SIZE /
+    WRITE_SIZE passes of this same bench command). PMC counters cannot be read inside the timed process."""
+    import glob
+    paths = sorted(glob.glob(os.path.join(REPO, "profiles", "r*", f"{workload}_pmc_summary.json")))
+    if not paths:
+        return None, None
+    with open(paths[-1]) as f:
+        ks = json.load(f)["kernels"]
+    n = sum(ks[k]["launches"] for k in SCAN_KERNELS if k in ks)
+    b = sum(ks[k]["launches"] * ks[k]["hbm_bytes_per_launch"] for k in SCAN_KERNELS if k in ks)
+    return (b / n if n else None), os.path.relpath(paths[-1], REPO)
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -129,6 +147,7 @@ def main() -> None:
         dist.destroy_process_group()
         return
     first = results[0]
+    traffic, traffic_src = pmc_traffic(args.workload)
     line = {
         "metric": "candidate moves evaluated/s + proposal wall time, 10K brokers/1M replicas",
         "value": cands / elapsed,
@@ -151,7 +170,8 @@ def main() -> None:
         "actions_per_step": len(first.actions),
         "proposals_per_step": len(first.proposals),
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_unit": "HBM bytes per scan launch",
+                     "traffic_source": traffic_src,
                      "kernel": "scan (scan_cross/scan_pairs/scan_swap)", "avg_launch_us": scan_avg_ms * 1e3,
                      "launches_per_step": perf.scan_launches,
                      "algorithmic_bytes_per_launch": ref_bytes_per_launch,
