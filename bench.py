@@ -35,11 +35,12 @@ import ccmi  # noqa: E402
 
 C1_PROPS = dict(num_racks=20, num_brokers=1000, num_replicas=99999, num_topics=3000)
 C2_PROPS = dict(num_racks=100, num_brokers=10000, num_replicas=999999, num_topics=10000)
-WORKLOADS = {"c1": (C1_PROPS, "C1: 1K brokers x 100K replicas, 5 distribution goals (BASELINE configs[1])"),
-             "c2": (C2_PROPS, "C2 sizes: 10K brokers x 1M replicas, the 5 distribution goals (BASELINE configs[2] "
-                              "cluster, C1 goal list)")}
-C1_GOALS = ["ReplicaDistributionGoal", "DiskUsageDistributionGoal", "NetworkInboundUsageDistributionGoal",
-            "NetworkOutboundUsageDistributionGoal", "CpuUsageDistributionGoal"]
+C1_GOALS = list(ccmi.C1_GOALS)
+DEFAULT_GOALS = list(ccmi.DEFAULT_GOALS)
+WORKLOADS = {"c1": (C1_PROPS, C1_GOALS, "C1: 1K brokers x 100K replicas, 5 distribution goals (BASELINE configs[1])"),
+             "c2": (C2_PROPS, DEFAULT_GOALS, "C2: 10K brokers x 1M replicas, the 16 default goals (BASELINE configs[2])"),
+             "c2_c1goals": (C2_PROPS, C1_GOALS, "C2 cluster with the C1 goal list"),
+             "c0": ({}, DEFAULT_GOALS, "C0: TestConstants.BASE_PROPERTIES, the 16 default goals (BASELINE configs[0])")}
 BYTES_PER_CANDIDATE = 96
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E (MI355X_MICROARCH.md)
 
@@ -101,9 +102,9 @@ def main() -> None:
     torch.cuda.set_device(device)
 
     lib = ccmi.Library.get()
-    props, workload_name = WORKLOADS[args.workload]
+    props, goal_names, workload_name = WORKLOADS[args.workload]
     buf = ccmi.RandomCluster.generate(lib, **props)
-    goals = ccmi.goals_from_names(C1_GOALS)
+    goals = ccmi.goals_from_names(goal_names)
     opt = ccmi.GoalOptimizer(ccmi.BalancingConstraint())
 
     def session():
@@ -164,7 +165,7 @@ def main() -> None:
         "config": {"workload": workload_name,
                    "brokers": buf.desc.num_brokers, "replicas": buf.desc.num_replicas,
                    "partitions": buf.desc.num_partitions, "topics": buf.desc.num_topics,
-                   "goals": C1_GOALS, "parallelism": f"independent what-if per GPU x{world}"},
+                   "goals": goal_names, "parallelism": f"independent what-if per GPU x{world}"},
         "proposal_wall_s": elapsed / args.steps,
         "candidates_per_step": first.candidates,
         "actions_per_step": len(first.actions),

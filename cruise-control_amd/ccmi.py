@@ -48,9 +48,18 @@ GOAL_KINDS: Dict[str, int] = {
     "IntraBrokerDiskUsageDistributionGoal": 17,
 }
 GOAL_NAMES = {v: k for k, v in GOAL_KINDS.items()}
-# Goals whose drivers are implemented in this build (config C1's chain).
-IMPLEMENTED = ("ReplicaDistributionGoal", "DiskUsageDistributionGoal", "NetworkInboundUsageDistributionGoal",
-               "NetworkOutboundUsageDistributionGoal", "CpuUsageDistributionGoal")
+# default.goals in priority order (config/constants/AnalyzerConfig.java:352-367, TestConstants.DEFAULT_GOALS_VALUES)
+DEFAULT_GOALS = ("RackAwareGoal", "MinTopicLeadersPerBrokerGoal", "ReplicaCapacityGoal", "DiskCapacityGoal",
+                 "NetworkInboundCapacityGoal", "NetworkOutboundCapacityGoal", "CpuCapacityGoal",
+                 "ReplicaDistributionGoal", "PotentialNwOutGoal", "DiskUsageDistributionGoal",
+                 "NetworkInboundUsageDistributionGoal", "NetworkOutboundUsageDistributionGoal",
+                 "CpuUsageDistributionGoal", "TopicReplicaDistributionGoal", "LeaderReplicaDistributionGoal",
+                 "LeaderBytesInDistributionGoal")
+# config C1's chain
+C1_GOALS = ("ReplicaDistributionGoal", "DiskUsageDistributionGoal", "NetworkInboundUsageDistributionGoal",
+            "NetworkOutboundUsageDistributionGoal", "CpuUsageDistributionGoal")
+# Goals whose drivers are implemented in this build.
+IMPLEMENTED = DEFAULT_GOALS
 
 ACTION_TYPES = ("INTER_BROKER_REPLICA_MOVEMENT", "LEADERSHIP_MOVEMENT", "INTER_BROKER_REPLICA_SWAP",
                 "INTRA_BROKER_REPLICA_MOVEMENT", "INTRA_BROKER_REPLICA_SWAP")
@@ -229,6 +238,10 @@ class BalancingConstraint:
     replica_balance_percentage: float = 1.10
     goal_violation_distribution_threshold_multiplier: float = 1.0
     max_replicas_per_broker: int = 10000
+    leader_replica_balance_percentage: float = 1.10
+    topic_replica_balance_percentage: float = 3.00
+    topic_replica_balance_min_gap: int = 2
+    topic_replica_balance_max_gap: int = 40
 
     def set_resource_balance_percentage(self, p: float) -> None:  # BalancingConstraint.setResourceBalancePercentage
         self.resource_balance_percentage = (p, p, p, p)
@@ -242,10 +255,10 @@ class BalancingConstraint:
         s.capacity_threshold[:] = list(self.capacity_threshold)
         s.low_utilization_threshold[:] = list(self.low_utilization_threshold)
         s.replica_balance_percentage = self.replica_balance_percentage
-        s.leader_replica_balance_percentage = 1.10
-        s.topic_replica_balance_percentage = 3.00
-        s.topic_replica_balance_min_gap = 2
-        s.topic_replica_balance_max_gap = 40
+        s.leader_replica_balance_percentage = self.leader_replica_balance_percentage
+        s.topic_replica_balance_percentage = self.topic_replica_balance_percentage
+        s.topic_replica_balance_min_gap = self.topic_replica_balance_min_gap
+        s.topic_replica_balance_max_gap = self.topic_replica_balance_max_gap
         s.goal_violation_distribution_threshold_multiplier = self.goal_violation_distribution_threshold_multiplier
         s.max_replicas_per_broker = self.max_replicas_per_broker
         s.overprovisioned_max_replicas_per_broker = 1500
@@ -303,8 +316,7 @@ class Goal:
         return GOAL_KINDS[self._name]
 
     def is_hard_goal(self) -> bool:
-        return self._name in ("RackAwareGoal", "MinTopicLeadersPerBrokerGoal", "ReplicaCapacityGoal",
-                              "DiskCapacityGoal", "NetworkInboundCapacityGoal", "NetworkOutboundCapacityGoal",
+        return self._name in ("RackAwareGoal", "ReplicaCapacityGoal", "DiskCapacityGoal", "NetworkInboundCapacityGoal", "NetworkOutboundCapacityGoal",
                               "CpuCapacityGoal")
 
     def optimize(self, cluster: "ClusterModel", options: Optional[OptimizationOptions] = None) -> bool:

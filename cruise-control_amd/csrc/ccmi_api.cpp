@@ -69,6 +69,11 @@ void setOptions(ccmi_session* s, const ccmi_balancing_constraint* c, const ccmi_
   }
   e.bc.replicaBalance = c->replica_balance_percentage;
   e.bc.goalViolationMultiplier = c->goal_violation_distribution_threshold_multiplier;
+  e.bc.leaderReplicaBalance = c->leader_replica_balance_percentage;
+  e.bc.topicReplicaBalance = c->topic_replica_balance_percentage;
+  e.bc.topicMinGap = c->topic_replica_balance_min_gap;
+  e.bc.topicMaxGap = c->topic_replica_balance_max_gap;
+  e.bc.maxReplicasPerBroker = c->max_replicas_per_broker;
   const int B = s->model.B;
   ccmi::Options opt;
   opt.exclMove.assign(B, 0);
@@ -185,6 +190,7 @@ ccmi_status ccmi_session_create(int32_t device_ordinal, const ccmi_cluster_desc*
     s->device = std::make_unique<ccmi::Device>(device_ordinal, m.B, m.R, m.P, m.T, ccmi::kMaxGoals);
     // device layout: resource-major broker/replica columns
     std::vector<double> capRM((size_t)4 * m.B), utilRM((size_t)4 * m.B), rutilRM((size_t)4 * m.R), pot(m.B);
+    std::vector<double> lbi(m.B), plno(m.P);
     std::vector<int32_t> nrep(m.B), pBrokers(m.R);
     std::vector<uint8_t> alive(m.B), flags(m.R);
     for (int b = 0; b < m.B; ++b) {
@@ -194,18 +200,20 @@ ccmi_status ccmi_session_create(int32_t device_ordinal, const ccmi_cluster_desc*
       }
       nrep[b] = m.nrep(b);
       alive[b] = m.alive(b);
-      pot[b] = m.ops.util(m.bPot[b], ccmi::R_NW_OUT);
+      pot[b] = m.potNwOut(b);
+      lbi[b] = m.leadNwIn(b);
     }
+    for (int p = 0; p < m.P; ++p) plno[p] = m.pLeadNwOut(p);
     for (int r = 0; r < m.R; ++r) {
       for (int k = 0; k < 4; ++k) rutilRM[(size_t)k * m.R + r] = m.ru(r, k);
       flags[r] = (m.rLeader[r] ? ccmi::RF_LEADER : 0) | (m.rOrigOff[r] ? ccmi::RF_ORIG_OFFLINE : 0);
     }
     for (int i = 0; i < m.R; ++i) pBrokers[i] = m.rBroker[m.pSlots[i]];
-    s->device->uploadStatic(capRM.data(), m.rPart.data(), m.rOrig.data(), m.pOff.data(), m.topicNrep.data());
-    s->device->uploadDynamic(utilRM.data(), nrep.data(), m.bNlead.data(), pot.data(), alive.data(), rutilRM.data(),
-                             m.rBroker.data(), flags.data(), pBrokers.data(), m.topicCountDense.data());
-    m.topicCountDense.clear();
-    m.topicCountDense.shrink_to_fit();
+    s->device->uploadStatic(capRM.data(), m.rPart.data(), m.rOrig.data(), m.pOff.data(), m.topicNrep.data(),
+                            m.bRack.data(), m.pTopic.data());
+    s->device->uploadDynamic(utilRM.data(), nrep.data(), m.bNlead.data(), pot.data(), lbi.data(), alive.data(),
+                             rutilRM.data(), m.rBroker.data(), flags.data(), pBrokers.data(), plno.data(),
+                             m.topicCountDense.data());
     m.dev = s->device.get();
     s->engine = std::make_unique<ccmi::Engine>(m, s->device.get());
     s->initDist = replicaDist(m);

@@ -22,12 +22,8 @@ hipError_t launchScanSwap(const DevTables& T, const DevProgram& prog, const int3
 hipError_t launchScanPairs(const DevTables& T, const MutTables& M, const UpdateList& U, const DevProgram& prog,
                            const int32_t* pr, const int32_t* pb, int n, unsigned long long* result, unsigned int* done,
                            unsigned long long* mail, unsigned long long seq, hipStream_t st);
-hipError_t launchPrep(double* bUtil, int32_t* bNrep, int32_t* bNlead, double* bPot, uint8_t* bAlive, int B,
-                      const BrokerRow* brows, int nb, double* rUtil, int32_t* rBroker, uint8_t* rFlags, int R,
-                      const ReplicaRow* rrows, int nr, const int32_t* pOff, int32_t* pBrokers,
-                      const PartitionRow* prows, int np, int32_t* topicCount, int ldB, const TopicCountDelta* tdel,
-                      int nt, const int4* req, int4* dReq, int nReq4, unsigned long long* result, unsigned int* done,
-                      hipStream_t st);
+hipError_t launchPrep(const MutTables& M, int B, int R, const int32_t* pOff, const UpdateList& U, const int4* req,
+                      int4* dReq, int nReq4, unsigned long long* result, unsigned int* done, hipStream_t st);
 hipError_t launchStats(const StatsParams& P, const int32_t* tc, const int32_t* topicNrep, const double* bUtil,
                        const double* bCap, const int32_t* bNrep, const int32_t* bNlead, const double* bPot,
                        const uint8_t* bAlive, const uint8_t* allowedAlive, TopicPartial* scratch, StatsOut* out,
@@ -72,6 +68,12 @@ Device::Device(int ordinal, int B, int R, int P, int T, int maxGoalSlots)
   dalloc(&pBrokers_, R);
   dalloc(&topicCount_, (size_t)T * ldB_);
   dalloc(&topicNrep_, T);
+  dalloc(&bRack_, B);
+  dalloc(&bLeadNwIn_, B);
+  dalloc(&pTopic_, P);
+  dalloc(&pLeadNwOut_, P);
+  dalloc(&tUpper_, T);
+  dalloc(&tLower_, T);
   dalloc(&dResult_, 4);
   dalloc(&dDone_, 4);
   hipCheck(hipMalloc(&topicScratch_, (size_t)(T ? T : 1) * sizeof(TopicPartial)), "hipMalloc");
@@ -94,7 +96,7 @@ Device::~Device() {
   if (ST) (void)hipStreamSynchronize(ST);
   void* ps[] = {bUtil_, bCap_, bPot_, bNrep_, bNlead_, bAlive_, allowed_, allowedAlive_, rUtil_, rPart_, rBroker_,
                 rOrig_, rFlags_, pOff_, pBrokers_, topicCount_, topicNrep_, topicScratch_, statsOut_, dReq_,
-                rowVisited_, dResult_, dDone_};
+                rowVisited_, dResult_, dDone_, bRack_, bLeadNwIn_, pTopic_, pLeadNwOut_, tUpper_, tLower_};
   for (void* p : ps)
     if (p) (void)hipFree(p);
   if (hStage_) (void)hipHostFree(hStage_);
@@ -144,31 +146,46 @@ DevTables Device::tables() const {
   t.rFlags = rFlags_;
   t.pOff = pOff_;
   t.pBrokers = pBrokers_;
+  t.bRack = bRack_;
+  t.bNlead = bNlead_;
+  t.bPot = bPot_;
+  t.bLeadNwIn = bLeadNwIn_;
+  t.pTopic = pTopic_;
+  t.pLeadNwOut = pLeadNwOut_;
+  t.topicCount = topicCount_;
+  t.tUpper = tUpper_;
+  t.tLower = tLower_;
   t.B = B_;
   t.R = R_;
   t.P = P_;
+  t.ldB = ldB_;
   return t;
 }
 
 void Device::uploadStatic(const double* bCapRM, const int32_t* rPart, const int32_t* rOrig, const int32_t* pOff,
-                          const int32_t* topicNrep) {
+                          const int32_t* topicNrep, const int32_t* bRack, const int32_t* pTopic) {
   hipCheck(hipSetDevice(ordinal_), "hipSetDevice");
   hipCheck(hipMemcpy(bCap_, bCapRM, sizeof(double) * 4 * B_, hipMemcpyHostToDevice), "upload bCap");
   hipCheck(hipMemcpy(rPart_, rPart, sizeof(int32_t) * R_, hipMemcpyHostToDevice), "upload rPart");
   hipCheck(hipMemcpy(rOrig_, rOrig, sizeof(int32_t) * R_, hipMemcpyHostToDevice), "upload rOrig");
   hipCheck(hipMemcpy(pOff_, pOff, sizeof(int32_t) * (P_ + 1), hipMemcpyHostToDevice), "upload pOff");
   hipCheck(hipMemcpy(topicNrep_, topicNrep, sizeof(int32_t) * T_, hipMemcpyHostToDevice), "upload topicNrep");
+  hipCheck(hipMemcpy(bRack_, bRack, sizeof(int32_t) * B_, hipMemcpyHostToDevice), "upload bRack");
+  hipCheck(hipMemcpy(pTopic_, pTopic, sizeof(int32_t) * P_, hipMemcpyHostToDevice), "upload pTopic");
 }
 
 void Device::uploadDynamic(const double* bUtilRM, const int32_t* bNrep, const int32_t* bNlead, const double* bPot,
-                           const uint8_t* bAlive, const double* rUtilRM, const int32_t* rBroker, const uint8_t* rFlags,
-                           const int32_t* pBrokers, const int32_t* topicCountDense) {
+                           const double* bLeadNwIn, const uint8_t* bAlive, const double* rUtilRM,
+                           const int32_t* rBroker, const uint8_t* rFlags, const int32_t* pBrokers,
+                           const double* pLeadNwOut, const int32_t* topicCountDense) {
   hipCheck(hipSetDevice(ordinal_), "hipSetDevice");
   hipCheck(hipMemcpy(bUtil_, bUtilRM, sizeof(double) * 4 * B_, hipMemcpyHostToDevice), "upload bUtil");
   hipCheck(hipMemcpy(bNrep_, bNrep, sizeof(int32_t) * B_, hipMemcpyHostToDevice), "upload bNrep");
   hipCheck(hipMemcpy(bNlead_, bNlead, sizeof(int32_t) * B_, hipMemcpyHostToDevice), "upload bNlead");
   hipCheck(hipMemcpy(bPot_, bPot, sizeof(double) * B_, hipMemcpyHostToDevice), "upload bPot");
   hipCheck(hipMemcpy(bAlive_, bAlive, B_, hipMemcpyHostToDevice), "upload bAlive");
+  hipCheck(hipMemcpy(bLeadNwIn_, bLeadNwIn, sizeof(double) * B_, hipMemcpyHostToDevice), "upload bLeadNwIn");
+  hipCheck(hipMemcpy(pLeadNwOut_, pLeadNwOut, sizeof(double) * P_, hipMemcpyHostToDevice), "upload pLeadNwOut");
   hipCheck(hipMemcpy(rUtil_, rUtilRM, sizeof(double) * 4 * R_, hipMemcpyHostToDevice), "upload rUtil");
   hipCheck(hipMemcpy(rBroker_, rBroker, sizeof(int32_t) * R_, hipMemcpyHostToDevice), "upload rBroker");
   hipCheck(hipMemcpy(rFlags_, rFlags, R_, hipMemcpyHostToDevice), "upload rFlags");
@@ -180,6 +197,12 @@ void Device::uploadDynamic(const double* bUtilRM, const int32_t* bNrep, const in
 void Device::setAllowed(int slot, const uint8_t* allowedB) {
   if (slot < 0 || slot >= G_) throw std::runtime_error("goal slot out of range");
   hipCheck(hipMemcpyAsync(allowed_ + (size_t)slot * B_, allowedB, B_, hipMemcpyHostToDevice, ST), "upload allowed");
+  hipCheck(hipStreamSynchronize(ST), "sync");
+}
+
+void Device::setTopicLimits(const int32_t* upper, const int32_t* lower) {
+  hipCheck(hipMemcpyAsync(tUpper_, upper, sizeof(int32_t) * T_, hipMemcpyHostToDevice, ST), "upload tUpper");
+  hipCheck(hipMemcpyAsync(tLower_, lower, sizeof(int32_t) * T_, hipMemcpyHostToDevice, ST), "upload tLower");
   hipCheck(hipStreamSynchronize(ST), "sync");
 }
 
@@ -219,11 +242,8 @@ Device::Staged Device::packUpdates(size_t extra) {
 void Device::launchPrepFor(const Staged& g, size_t reqBytes, bool scan) {
   const int nReq4 = (int)(align16(reqBytes) / 16);
   if (nReq4) ensureReq((size_t)nReq4 * 16);
-  hipCheck(launchPrep(bUtil_, bNrep_, bNlead_, bPot_, bAlive_, B_, (const BrokerRow*)(hStageDev_ + g.obr), g.nb,
-                      rUtil_, rBroker_, rFlags_, R_, (const ReplicaRow*)(hStageDev_ + g.orr), g.nr, pOff_, pBrokers_,
-                      (const PartitionRow*)(hStageDev_ + g.opr), g.np, topicCount_, ldB_,
-                      (const TopicCountDelta*)(hStageDev_ + g.otd), g.nt, (const int4*)(hStageDev_ + g.end),
-                      (int4*)dReq_, nReq4, scan ? dResult_ : nullptr, scan ? dDone_ : nullptr, ST),
+  hipCheck(launchPrep(mutTables(), B_, R_, pOff_, stagedList(g), (const int4*)(hStageDev_ + g.end), (int4*)dReq_, nReq4,
+                      scan ? dResult_ : nullptr, scan ? dDone_ : nullptr, ST),
            "prep");
 }
 
@@ -273,6 +293,8 @@ int64_t Device::finishScan() {
 constexpr int kOverlayRows = 32;
 constexpr size_t kDirectRequestBytes = 16 << 10;
 
+UpdateList Device::stagedList(const Staged& g) const { return overlayFor(g); }
+
 UpdateList Device::overlayFor(const Staged& g) const {
   UpdateList u;
   u.brows = (const BrokerRow*)(hStageDev_ + g.obr);
@@ -287,13 +309,17 @@ UpdateList Device::overlayFor(const Staged& g) const {
 }
 
 MutTables Device::mutTables() const {
-  return MutTables{bUtil_, bNrep_, bNlead_, bPot_, bAlive_, rUtil_, rBroker_, rFlags_, pBrokers_, topicCount_, ldB_};
+  return MutTables{bUtil_, bNrep_, bNlead_, bPot_, bLeadNwIn_, pLeadNwOut_, bAlive_, rUtil_, rBroker_, rFlags_,
+                   pBrokers_, topicCount_, ldB_};
 }
 
 // Returns the request base the scan reads (host-mapped staging or the HBM copy) and the update list it
 // applies itself (empty when prep ran).
-const char* Device::stageScan(const Staged& g, size_t req, UpdateList& u) {
-  const bool fits = g.nb <= kOverlayRows && g.nr <= kOverlayRows && g.np <= kOverlayRows;
+// Topic-count deltas are atomics applied by workgroup 0 during the launch, so a program that reads topic counts
+// always has them applied by `prep` first.
+const char* Device::stageScan(const Staged& g, size_t req, bool readsTopicCounts, UpdateList& u) {
+  const bool fits = g.nb <= kOverlayRows && g.nr <= kOverlayRows && g.np <= kOverlayRows &&
+                    !(readsTopicCounts && g.nt > 0);
   if (fits && req <= kDirectRequestBytes) {
     u = overlayFor(g);
     perf.singleLaunch++;
@@ -313,7 +339,7 @@ int64_t Device::scanCross(const DevProgram& prog, const int32_t* reps, int K, co
   std::memcpy(hStage_ + g.end, reps, (size_t)K * 4);
   std::memcpy(hStage_ + g.end + oCand, cands, (size_t)N * 4);
   UpdateList u;
-  const char* base = stageScan(g, req, u);
+  const char* base = stageScan(g, req, (prog.needs & NEED_TOPIC) != 0, u);
   ++seq_;
   if (timing) (void)hipEventRecord(EV0, ST);
   hipCheck(launchScanCross(tables(), mutTables(), u, prog, (const int32_t*)base, (const int32_t*)(base + oCand), K, N,
@@ -366,7 +392,7 @@ int64_t Device::scanPairs(const DevProgram& prog, const int32_t* pr, const int32
   std::memcpy(hStage_ + g.end, pr, (size_t)n * 4);
   std::memcpy(hStage_ + g.end + oB, pb, (size_t)n * 4);
   UpdateList u;
-  const char* base = stageScan(g, req, u);
+  const char* base = stageScan(g, req, (prog.needs & NEED_TOPIC) != 0, u);
   ++seq_;
   if (timing) (void)hipEventRecord(EV0, ST);
   hipCheck(launchScanPairs(tables(), mutTables(), u, prog, (const int32_t*)base, (const int32_t*)(base + oB), n,

@@ -42,11 +42,14 @@ class Device {
 
   // initial upload (host arrays in device layout)
   void uploadStatic(const double* bCapRM, const int32_t* rPart, const int32_t* rOrig, const int32_t* pOff,
-                    const int32_t* topicNrep);
+                    const int32_t* topicNrep, const int32_t* bRack, const int32_t* pTopic);
   void uploadDynamic(const double* bUtilRM, const int32_t* bNrep, const int32_t* bNlead, const double* bPot,
-                     const uint8_t* bAlive, const double* rUtilRM, const int32_t* rBroker, const uint8_t* rFlags,
-                     const int32_t* pBrokers, const int32_t* topicCountDense /* [T][ldB] */);
+                     const double* bLeadNwIn, const uint8_t* bAlive, const double* rUtilRM, const int32_t* rBroker,
+                     const uint8_t* rFlags, const int32_t* pBrokers, const double* pLeadNwOut,
+                     const int32_t* topicCountDense /* [T][ldB] */);
   void setAllowed(int slot, const uint8_t* allowedB);
+  // TopicReplicaDistributionGoal balance limits per topic (frozen at its initGoalState)
+  void setTopicLimits(const int32_t* upper, const int32_t* lower);
 
   // pending row updates (flushed with the next launch)
   std::vector<BrokerRow> brows;
@@ -73,6 +76,8 @@ class Device {
   double *bUtil_ = nullptr, *bCap_ = nullptr, *bPot_ = nullptr, *rUtil_ = nullptr;
   int32_t *bNrep_ = nullptr, *bNlead_ = nullptr, *rPart_ = nullptr, *rBroker_ = nullptr, *rOrig_ = nullptr;
   int32_t *pOff_ = nullptr, *pBrokers_ = nullptr, *topicCount_ = nullptr, *topicNrep_ = nullptr;
+  int32_t *bRack_ = nullptr, *pTopic_ = nullptr, *tUpper_ = nullptr, *tLower_ = nullptr;
+  double *bLeadNwIn_ = nullptr, *pLeadNwOut_ = nullptr;
   uint8_t *bAlive_ = nullptr, *allowed_ = nullptr, *rFlags_ = nullptr, *allowedAlive_ = nullptr;
   void *topicScratch_ = nullptr, *statsOut_ = nullptr;
   // staging (host-coherent, mapped) and the request copy in HBM
@@ -99,9 +104,10 @@ class Device {
   void ensureStage(size_t bytes);
   void ensureReq(size_t bytes);
   void launchPrepFor(const Staged& g, size_t reqBytes, bool scan);
+  UpdateList stagedList(const Staged& g) const;
   UpdateList overlayFor(const Staged& g) const;
   MutTables mutTables() const;
-  const char* stageScan(const Staged& g, size_t req, UpdateList& u);
+  const char* stageScan(const Staged& g, size_t req, bool readsTopicCounts, UpdateList& u);
   void waitMail(unsigned long long seq);
   int64_t finishScan();
   int32_t* rowVisited_ = nullptr;

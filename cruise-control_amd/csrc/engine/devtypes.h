@@ -8,6 +8,9 @@
 //   partitions    pOff[P+1] i32, pBrokers[R] i32 (current broker of every replica slot, Partition._replicas order)
 //   topics        topicCount[T][B] i32 (dense Broker._topicReplicas sizes, for ClusterModelStats topic stats)
 //   goal state    allowed[G][B] u8 (per optimized goal: _brokersAllowedReplicaMove, frozen at initGoalState)
+//   more broker   bRack[B] i32 (static), bLeadNwIn[B] f64 (Broker._leadershipLoadForNwResources NW_IN)
+//   more part.    pTopic[P] i32 (static), pLeadNwOut[P] f64 (NW_OUT utilization of the partition's leader)
+//   topic limits  tUpper[T], tLower[T] i32 (TopicReplicaDistributionGoal balance limits, frozen at init)
 // Resource-major broker columns make a candidate row (consecutive destination brokers) a coalesced read.
 #pragma once
 #include <stdint.h>
@@ -17,7 +20,26 @@ namespace ccmi {
 constexpr int kMaxGoals = 20;
 constexpr int kMaxRf = 8;
 
-enum DevGoalKind : int32_t { DG_REPLICA_DISTRIBUTION = 0, DG_RESOURCE_DISTRIBUTION = 1 };
+enum DevGoalKind : int32_t {
+  DG_REPLICA_DISTRIBUTION = 0,
+  DG_RESOURCE_DISTRIBUTION = 1,
+  DG_ACCEPT_ALL = 2,  // MinTopicLeadersPerBrokerGoal without configured topics
+  DG_RACK_AWARE = 3,
+  DG_REPLICA_CAPACITY = 4,
+  DG_CAPACITY = 5,
+  DG_POTENTIAL_NW_OUT = 6,
+  DG_TOPIC_REPLICA_DISTRIBUTION = 7,
+  DG_LEADER_REPLICA_DISTRIBUTION = 8,
+  DG_LEADER_BYTES_IN = 9
+};
+// Operands a program's predicates read beyond the base broker/replica/partition record (DevProgram.needs).
+enum DevNeed : uint32_t { NEED_RACK = 1, NEED_POT = 2, NEED_LEAD = 4, NEED_LBI = 8, NEED_TOPIC = 16 };
+// Candidate filters applied inside a CROSS scan before the predicate conjunction (the reference builds these
+// candidate lists per replica; the kernel skips the excluded destinations instead).
+enum DevFilter : int32_t {
+  FILTER_NONE = 0,
+  FILTER_RACK_AWARE = 1  // RackAwareGoal.rackAwareEligibleBrokers: rack not among the partition's other racks
+};
 enum DevAction : int32_t { DA_MOVE = 0, DA_LEADERSHIP = 1, DA_SWAP = 2 };
 enum RFlag : uint8_t { RF_LEADER = 1, RF_ORIG_OFFLINE = 2 };
 
@@ -29,6 +51,13 @@ struct DevGoal {
   double upperThr, lowerThr;   // ResourceDistributionGoal._balanceUpperThreshold/_balanceLowerThreshold
   int32_t fixOffline;          // _fixOfflineReplicasOnly
   int32_t allowedSlot;         // row of DevTables.allowed
+  int32_t selfHealing;         // ReplicaCapacityGoal._isSelfHealingMode (unused by predicates; kept for parity)
+  int32_t pad0;
+  int64_t maxReplicas;         // BalancingConstraint.maxReplicasPerBroker (ReplicaCapacityGoal)
+  double capThr;               // capacity threshold of `resource` (CapacityGoal, PotentialNwOutGoal: NW_OUT)
+  double lbiMean;              // LeaderBytesInDistributionGoal._meanLeaderBytesIn (cached on first use)
+  double lbiBalance;           // resource balance percentage of NW_IN
+  double lbiLowUtil;           // low utilization threshold of NW_IN
 };
 
 // goals[0] is the goal being optimized (selfSatisfied); goals[1..n) are the optimized goals in the order
@@ -36,6 +65,8 @@ struct DevGoal {
 struct DevProgram {
   int32_t nGoals;
   int32_t action;
+  uint32_t needs;   // DevNeed bits over all goals of the program
+  int32_t filter;   // DevFilter of a CROSS scan
   DevGoal goals[kMaxGoals];
 };
 
@@ -52,7 +83,16 @@ struct DevTables {
   const uint8_t* rFlags;
   const int32_t* pOff;
   const int32_t* pBrokers;
-  int32_t B, R, P;
+  const int32_t* bRack;
+  const int32_t* bNlead;
+  const double* bPot;
+  const double* bLeadNwIn;
+  const int32_t* pTopic;
+  const double* pLeadNwOut;
+  const int32_t* topicCount;  // [T][ldB]
+  const int32_t* tUpper;
+  const int32_t* tLower;
+  int32_t B, R, P, ldB;
 };
 
 // Row updates the host flushes to the device before a scan (only rows touched since the last flush).
@@ -60,7 +100,7 @@ struct BrokerRow {
   int32_t b, nrep, nlead, alive;
   double util[4];
   double potNwOut;
-  double pad;
+  double leadNwIn;
 };
 struct ReplicaRow {
   int32_t r, broker, flags, pad;
@@ -69,6 +109,7 @@ struct ReplicaRow {
 struct PartitionRow {
   int32_t p, n;
   int32_t brokers[kMaxRf];
+  double leadNwOut;
 };
 struct TopicCountDelta {
   int32_t topic, broker, delta, pad;
@@ -80,6 +121,8 @@ struct MutTables {
   int32_t* bNrep;
   int32_t* bNlead;
   double* bPot;
+  double* bLeadNwIn;
+  double* pLeadNwOut;
   uint8_t* bAlive;
   double* rUtil;
   int32_t* rBroker;

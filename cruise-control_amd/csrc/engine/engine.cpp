@@ -20,6 +20,8 @@ constexpr double kBalanceMargin = 0.9;  // ResourceDistributionGoal.BALANCE_MARG
 struct HostView {
   const Model& m;
   const std::vector<const std::vector<uint8_t>*>& allowedBySlot;
+  const std::vector<int32_t>& tUp;
+  const std::vector<int32_t>& tLo;
   double bu(int b, int res) const { return m.bu(b, res); }
   double bcap(int b, int res) const { return m.cap(b, res); }
   int nrep(int b) const { return m.nrep(b); }
@@ -38,9 +40,32 @@ struct HostView {
     for (int i = pbegin(p); i < pend(p); ++i) has |= (pbroker(i) == b);
     return has;
   }
+  int rack(int b) const { return m.bRack[b]; }
+  bool otherOnRack(int p, int self, int rk) const {
+    for (int i = pbegin(p); i < pend(p); ++i)
+      if (pbroker(i) != self && m.bRack[pbroker(i)] == rk) return true;
+    return false;
+  }
+  int nlead(int b) const { return m.bNlead[b]; }
+  double pot(int b) const { return m.potNwOut(b); }
+  double lnwin(int b) const { return m.leadNwIn(b); }
+  double pLeadNwOut(int p) const { return m.pLeadNwOut(p); }
+  int ptopic(int p) const { return m.pTopic[p]; }
+  int tcount(int t, int b) const { return m.tcount(t, b); }
+  int tUpper(int t) const { return tUp[t]; }
+  int tLower(int t) const { return tLo[t]; }
 };
 
-Model::Spec makeSpec() { return Model::Spec(); }
+uint32_t needsOf(const DevGoal& g) {
+  switch (g.kind) {
+    case DG_RACK_AWARE: return NEED_RACK;
+    case DG_POTENTIAL_NW_OUT: return NEED_POT;
+    case DG_TOPIC_REPLICA_DISTRIBUTION: return NEED_TOPIC;
+    case DG_LEADER_REPLICA_DISTRIBUTION: return NEED_LEAD;
+    case DG_LEADER_BYTES_IN: return NEED_LBI;
+    default: return 0;
+  }
+}
 
 }  // namespace
 
@@ -69,6 +94,9 @@ DevProgram Engine::program(const GoalImpl& self, int action) const {
   if (p.nGoals > kMaxGoals) throw Unsupported("too many goals in one chain");
   p.goals[0] = self.dg;
   for (size_t i = 0; i < optimized.size(); ++i) p.goals[i + 1] = optimized[i]->dg;
+  p.needs = 0;
+  for (int i = 0; i < p.nGoals; ++i) p.needs |= needsOf(p.goals[i]);
+  p.filter = FILTER_NONE;
   return p;
 }
 
@@ -86,23 +114,25 @@ void Engine::eligible(const std::vector<int32_t>& in, int action, std::vector<in
 }
 
 int64_t Engine::crossScan(GoalImpl& self, int action, const std::vector<int32_t>& reps, size_t r0,
-                          const std::vector<int32_t>& cands) {
-  const int K = (int)(reps.size() - r0), N = (int)cands.size();
+                          const std::vector<int32_t>& cands, int filter, bool count, size_t r1) {
+  const size_t end = r1 == (size_t)-1 ? reps.size() : std::min(r1, reps.size());
+  const int K = (int)(end - r0), N = (int)cands.size();
   if (K <= 0) return -1;
   if (N == 0) return -1;  // every replica visits an empty eligible list
   PhaseScope ps(PH_DEV_SCAN);
   m.flushToDevice();
-  const int64_t key = dev->scanCross(program(self, action), reps.data() + r0, K, cands.data(), N);
-
-  candidates += key >= 0 ? key + 1 : (int64_t)K * N;
+  DevProgram prog = program(self, action);
+  prog.filter = filter;
+  const int64_t key = dev->scanCross(prog, reps.data() + r0, K, cands.data(), N);
+  if (count) candidates += key >= 0 ? key + 1 : (int64_t)K * N;
   return key;
 }
 
-int64_t Engine::pairScan(GoalImpl& self, const std::vector<int32_t>& pr, const std::vector<int32_t>& pb) {
+int64_t Engine::pairScan(GoalImpl& self, const std::vector<int32_t>& pr, const std::vector<int32_t>& pb, int action) {
   if (pr.empty()) return -1;
   PhaseScope ps(PH_DEV_SCAN);
   m.flushToDevice();
-  const int64_t key = dev->scanPairs(program(self, DA_LEADERSHIP), pr.data(), pb.data(), (int)pr.size());
+  const int64_t key = dev->scanPairs(program(self, action), pr.data(), pb.data(), (int)pr.size());
   candidates += key >= 0 ? key + 1 : (int64_t)pr.size();
   return key;
 }
@@ -122,7 +152,7 @@ int64_t Engine::swapScan(GoalImpl& self, const std::vector<int32_t>& srcs, const
 int Engine::acceptance(int gi, const ccmi_action& a) {
   std::vector<const std::vector<uint8_t>*> allowedBySlot;
   for (auto& g : optimized) allowedBySlot.push_back(&g->allowed);
-  HostView v{m, allowedBySlot};
+  HostView v{m, allowedBySlot, topicUpper, topicLower};
   const GoalImpl& g = *optimized.at(gi);
   const int sr = m.replicaOn(a.partition, a.source_broker);
   if (sr < 0) throw std::invalid_argument("no replica of the partition on the source broker");
@@ -1024,7 +1054,7 @@ std::unique_ptr<GoalImpl> makeGoal(int kind) {
     case CCMI_GOAL_NW_IN_USAGE_DISTRIBUTION:
     case CCMI_GOAL_NW_OUT_USAGE_DISTRIBUTION:
     case CCMI_GOAL_CPU_USAGE_DISTRIBUTION: return std::make_unique<ResourceDistribution>(kind);
-    default: throw Unsupported("goal kind " + std::to_string(kind) + " is not implemented in this build");
+    default: return makeMoreGoal(kind);
   }
 }
 

@@ -33,6 +33,9 @@ struct Options {  // OptimizationOptions
 struct Constraint {  // BalancingConstraint
   double resBalance[4], capThreshold[4], lowUtil[4];
   double replicaBalance, goalViolationMultiplier;
+  double leaderReplicaBalance, topicReplicaBalance;
+  int32_t topicMinGap, topicMaxGap;
+  int64_t maxReplicasPerBroker;
 };
 
 class Engine;
@@ -63,6 +66,7 @@ class Engine {
   std::vector<std::unique_ptr<GoalImpl>> optimized;  // optimized goals, priority order
   int64_t candidates = 0;
   std::vector<uint8_t> scratchB;  // per-broker scratch flags for the goal drivers
+  std::vector<int32_t> topicUpper, topicLower;  // TopicReplicaDistributionGoal limits (device copy: setTopicLimits)
 
   // one Goal.optimize; throws OptimizationFailure / StateError
   bool optimizeGoal(std::unique_ptr<GoalImpl> g, ccmi_goal_result* res);
@@ -70,9 +74,13 @@ class Engine {
   int acceptance(int goalIndex, const ccmi_action& a);
 
   // device scans: return winning index or -1; add reference-equivalent candidate counts
+  //   crossScan: rows reps[r0, r1) x cands, key = k * N + j; `count` adds the reference-equivalent candidates
+  //   (callers with candidate filters or early exits count themselves)
   int64_t crossScan(GoalImpl& self, int action, const std::vector<int32_t>& reps, size_t r0,
-                    const std::vector<int32_t>& cands);
-  int64_t pairScan(GoalImpl& self, const std::vector<int32_t>& pr, const std::vector<int32_t>& pb);
+                    const std::vector<int32_t>& cands, int filter = FILTER_NONE, bool count = true,
+                    size_t r1 = (size_t)-1);
+  int64_t pairScan(GoalImpl& self, const std::vector<int32_t>& pr, const std::vector<int32_t>& pb,
+                   int action = DA_LEADERSHIP);
   int64_t swapScan(GoalImpl& self, const std::vector<int32_t>& srcs, const std::vector<int32_t>& cbOff,
                    const std::vector<int32_t>& cbRep);
   void eligible(const std::vector<int32_t>& in, int action, std::vector<int32_t>& out) const;
@@ -85,6 +93,7 @@ class Engine {
 };
 
 std::unique_ptr<GoalImpl> makeGoal(int kind);
+std::unique_ptr<GoalImpl> makeMoreGoal(int kind);  // engine_goals.cpp: the remaining default goals
 
 struct OptimizationFailure : std::runtime_error {
   using std::runtime_error::runtime_error;

@@ -1,0 +1,1147 @@
+// Goal drivers for the rest of the default goal list (engine.h has the engine; engine.cpp the distribution goals).
+//
+// Each driver restates the reference goal's control flow on the host — which brokers it visits, which
+// replicas it tries in which order, which candidate list each replica gets, when it stops — and hands every
+// candidate-predicate evaluation to a device scan. Where consecutive replicas share one candidate list the
+// driver scans them as one batch (rows = replicas, columns = candidates, winner = smallest (row, column)),
+// replays the host-side bookkeeping of the rows before the winner, and resumes right after it.
+//
+// Reference code restated here (paths under cruise-control/src/main/java/com/linkedin/kafka/cruisecontrol/):
+//   RackAwareGoal / AbstractRackAwareGoal   analyzer/goals/RackAwareGoal.java:82-225, AbstractRackAwareGoal.java:144-170
+//   MinTopicLeadersPerBrokerGoal            analyzer/goals/MinTopicLeadersPerBrokerGoal.java:276-330,444-466
+//   ReplicaCapacityGoal                     analyzer/goals/ReplicaCapacityGoal.java:100-290
+//   CapacityGoal (+ Disk/NwIn/NwOut/Cpu)    analyzer/goals/CapacityGoal.java:120-355
+//   PotentialNwOutGoal                      analyzer/goals/PotentialNwOutGoal.java:140-331
+//   TopicReplicaDistributionGoal            analyzer/goals/TopicReplicaDistributionGoal.java:225-570
+//   LeaderReplicaDistributionGoal           analyzer/goals/LeaderReplicaDistributionGoal.java:137-364,
+//                                           ReplicaDistributionAbstractGoal.java:60-160
+//   LeaderBytesInDistributionGoal           analyzer/goals/LeaderBytesInDistributionGoal.java:142-271
+//   GoalUtils.ensureNoOfflineReplicas       analyzer/goals/GoalUtils.java:307-318
+#include <algorithm>
+#include <cmath>
+#include <set>
+
+#include "device.h"
+#include "engine.h"
+#include "predicates.h"
+#include "prof.h"
+
+namespace ccmi {
+
+namespace {
+
+constexpr double kBalanceMargin = 0.9;
+
+// sort-name ids of the tracked SortedReplicas: replicaSortName(goal, reverse, leaderOnly)
+int sortId(int kind, bool reverse, bool leaderOnly) { return 100 + 8 * kind + (reverse ? 1 : 0) + (leaderOnly ? 2 : 0); }
+
+std::vector<int32_t> aliveById(const Model& m) {  // ClusterModel.aliveBrokers() iteration (HashSet<Broker>, ids < table)
+  std::vector<int32_t> v;
+  for (int b = 0; b < m.B; ++b)
+    if (m.alive(b)) v.push_back(b);
+  return v;
+}
+
+bool hasOffline(const Model& m, int b) { return m.bOfflineSet[b].size() > 0; }  // !currentOfflineReplicas().isEmpty()
+
+// GoalUtils.ensureNoOfflineReplicas
+void ensureNoOfflineReplicas(const Model& m, const std::string& name) {
+  for (int r = 0; r < m.R; ++r)
+    if (m.selfHealing[r] && m.curOffline(r))
+      throw OptimizationFailure("[" + name + "] Cannot remove replica from broker " + std::to_string(m.bId[m.rBroker[r]]));
+}
+
+// GoalUtils.aliveBrokersNotExcludedForReplicaMove
+int allowedForReplicaMove(const Engine& e, std::vector<uint8_t>& allowed) {
+  allowed.assign(e.m.B, 0);
+  int n = 0;
+  for (int b = 0; b < e.m.B; ++b)
+    if (e.m.alive(b) && !(e.opt.anyExclMove && e.opt.exclMove[b])) {
+      allowed[b] = 1;
+      n++;
+    }
+  return n;
+}
+
+template <class C>
+void stableSortBy(std::vector<int32_t>& v, C cmp) {
+  std::stable_sort(v.begin(), v.end(), [&](int a, int b) { return cmp(a, b) < 0; });
+}
+
+int cmpStd(double after, double before) {  // stats comparator on a standard deviation (AnalyzerUtils.compare, 1e-5)
+  if (after - before > 1e-5) return -1;
+  if (before - after > 1e-5) return 1;
+  return 0;
+}
+
+// ======================================================================================= RackAwareGoal
+class RackAware : public GoalImpl {
+ public:
+  RackAware() {
+    kind = CCMI_GOAL_RACK_AWARE;
+    name = "RackAwareGoal";
+  }
+  std::vector<int32_t> alive;
+
+  // initGoalState (RackAwareGoal.java:82-124)
+  void init(Engine& e) override {
+    Model& m = e.m;
+    allowedForReplicaMove(e, allowed);
+    std::set<int> racks;
+    for (int b = 0; b < m.B; ++b)
+      if (m.alive(b)) racks.insert(m.bRack[b]);
+    if (m.maxRf > (int)racks.size())
+      throw OptimizationFailure("[" + name + "] Insufficient number of racks to distribute each replica (Current: " +
+                                std::to_string(racks.size()) + ", Needed: " + std::to_string(m.maxRf) + ").");
+    Model::Spec s;
+    s.selImmigrants = e.opt.onlyImmigrants;
+    for (int b = 0; b < m.B; ++b) m.track(b, sortId(kind, false, false), s);
+    alive = aliveById(m);
+    dg = DevGoal{};
+    dg.kind = DG_RACK_AWARE;
+    dg.allowedSlot = (int)e.optimized.size();
+  }
+
+  // shouldKeepInTheCurrentBroker (:214-225)
+  static bool keep(const Model& m, int r) {
+    const int self = m.rBroker[r], rk = m.bRack[self], p = m.rPart[r];
+    for (int i = m.pOff[p]; i < m.pOff[p + 1]; ++i) {
+      const int x = m.rBroker[m.pSlots[i]];
+      if (x != self && m.bRack[x] == rk) return false;
+    }
+    return true;
+  }
+  // candidates of `cands[0, upto)` that rackAwareEligibleBrokers keeps (:193-211)
+  static int64_t eligibleCount(const Model& m, int r, const std::vector<int32_t>& cands, size_t upto) {
+    int racks[kMaxRf];
+    int n = 0;
+    const int p = m.rPart[r];
+    for (int i = m.pOff[p]; i < m.pOff[p + 1]; ++i) racks[n++] = m.bRack[m.rBroker[m.pSlots[i]]];
+    for (int i = 0; i < n; ++i)
+      if (racks[i] == m.bRack[m.rBroker[r]]) {
+        racks[i] = racks[--n];
+        break;
+      }
+    int64_t c = 0;
+    for (size_t j = 0; j < upto; ++j) {
+      bool in = true;
+      for (int i = 0; i < n; ++i) in &= racks[i] != m.bRack[cands[j]];
+      c += in;
+    }
+    return c;
+  }
+
+  // AbstractRackAwareGoal.rebalanceForBroker (:144-170), throwExceptionIfCannotMove = true
+  void rebalance(Engine& e, int b) override {
+    PhaseScope ps(PH_OTHER_GOALS);
+    Model& m = e.m;
+    const std::vector<int32_t> list = m.sorted(b, sortId(kind, false, false));
+    std::vector<int32_t> one(1), cands;
+    e.eligible(alive, DA_MOVE, cands);
+    for (int r : list) {
+      if (m.alive(b) && !m.curOffline(r) && keep(m, r)) continue;
+      one[0] = r;
+      const int64_t key = e.crossScan(*this, DA_MOVE, one, 0, cands, FILTER_RACK_AWARE, false);
+      e.candidates += eligibleCount(m, r, cands, key >= 0 ? (size_t)key + 1 : cands.size());
+      if (key < 0)
+        throw OptimizationFailure("[" + name + "] Cannot move replica of partition " + std::to_string(m.rPart[r]) +
+                                  " to a rack-aware broker.");
+      m.relocateReplica(m.rPart[r], b, cands[key]);
+    }
+  }
+
+  // updateGoalState (:131-143) + ensureRackAware (:159-185)
+  void update(Engine& e) override {
+    Model& m = e.m;
+    for (int p = 0; p < m.P; ++p) {
+      int racks[kMaxRf];
+      const int n = m.pOff[p + 1] - m.pOff[p];
+      for (int i = 0; i < n; ++i) {
+        racks[i] = m.bRack[m.rBroker[m.pSlots[m.pOff[p] + i]]];
+        for (int j = 0; j < i; ++j)
+          if (racks[j] == racks[i])
+            throw OptimizationFailure("[" + name + "] Partition " + std::to_string(p) + " is not rack-aware.");
+      }
+    }
+    ensureNoOfflineReplicas(m, name);
+    finished = true;
+  }
+  int compareStats(const ccmi_cluster_stats&, const ccmi_cluster_stats&) const override { return 0; }
+};
+
+// ======================================================================================= MinTopicLeadersPerBrokerGoal
+// With the default topics.with.min.leaders.per.broker (no topic matches) the goal accepts every action and only
+// moves offline replicas away (moveAwayOfflineReplicas).
+class MinTopicLeaders : public GoalImpl {
+ public:
+  MinTopicLeaders() {
+    kind = CCMI_GOAL_MIN_TOPIC_LEADERS_PER_BROKER;
+    name = "MinTopicLeadersPerBrokerGoal";
+  }
+  void init(Engine& e) override {
+    allowedForReplicaMove(e, allowed);
+    dg = DevGoal{};
+    dg.kind = DG_ACCEPT_ALL;
+    dg.allowedSlot = (int)e.optimized.size();
+  }
+  // moveAwayOfflineReplicas (:444-466)
+  void rebalance(Engine& e, int b) override {
+    PhaseScope ps(PH_OTHER_GOALS);
+    Model& m = e.m;
+    if (!hasOffline(m, b)) return;
+    std::vector<int32_t> order = aliveById(m), cands, offline, one(1);
+    std::sort(order.begin(), order.end(), [&](int x, int y) {  // TreeSet by (replica count, id), built once
+      return m.nrep(x) != m.nrep(y) ? m.nrep(x) < m.nrep(y) : x < y;
+    });
+    e.eligible(order, DA_MOVE, cands);
+    ReplicaSet copy;  // new HashSet<>(srcBroker.currentOfflineReplicas())
+    copy.assignCopy(m.bOfflineSet[b]);
+    copy.order(offline);
+    for (int r : offline) {
+      one[0] = r;
+      const int64_t key = e.crossScan(*this, DA_MOVE, one, 0, cands);
+      if (key < 0)
+        throw OptimizationFailure("[" + name + "] Cannot remove offline replica from broker " + std::to_string(m.bId[b]));
+      m.relocateReplica(m.rPart[r], b, cands[key]);
+    }
+  }
+  void update(Engine& e) override {
+    ensureNoOfflineReplicas(e.m, name);
+    finished = true;
+  }
+  int compareStats(const ccmi_cluster_stats&, const ccmi_cluster_stats&) const override { return 0; }
+};
+
+// ======================================================================================= ReplicaCapacityGoal
+class ReplicaCapacity : public GoalImpl {
+ public:
+  ReplicaCapacity() {
+    kind = CCMI_GOAL_REPLICA_CAPACITY;
+    name = "ReplicaCapacityGoal";
+  }
+  bool selfHealingMode = false;
+  int64_t maxR = 0;
+
+  // initGoalState (:100-150)
+  void init(Engine& e) override {
+    Model& m = e.m;
+    maxR = e.bc.maxReplicasPerBroker;
+    selfHealingMode = m.numDead > 0 || m.numBadDisk > 0;
+    const int n = allowedForReplicaMove(e, allowed);
+    const int64_t maxInCluster = maxR * n;
+    if ((int64_t)m.R > maxInCluster)
+      throw OptimizationFailure("[" + name + "] Total replicas in cluster: " + std::to_string(m.R) +
+                                " exceeds the maximum allowed replicas in cluster: " + std::to_string(maxInCluster));
+    Model::Spec s;
+    s.selImmigrants = e.opt.onlyImmigrants;
+    for (int b = 0; b < m.B; ++b) m.track(b, sortId(kind, false, false), s);
+    dg = DevGoal{};
+    dg.kind = DG_REPLICA_CAPACITY;
+    dg.maxReplicas = maxR;
+    dg.allowedSlot = (int)e.optimized.size();
+  }
+
+  // rebalanceForBroker (:221-263): rows that share one eligibleBrokers list (it only changes after a move) are
+  // scanned together; failed rows before the winner are checked for the dead-broker / offline-replica failures.
+  void rebalance(Engine& e, int b) override {
+    PhaseScope ps(PH_OTHER_GOALS);
+    Model& m = e.m;
+    const std::vector<int32_t> list = m.sorted(b, sortId(kind, false, false));
+    std::vector<int32_t> order, cands;
+    auto fail = [&](int r) {
+      if (!m.alive(b)) throw OptimizationFailure("[" + name + "] Failed to move dead broker replica.");
+      if (m.curOffline(r)) throw OptimizationFailure("[" + name + "] Failed to move offline replica.");
+    };
+    size_t i = 0;
+    while (i < list.size()) {
+      size_t end = i;
+      while (end < list.size() && !((int64_t)m.nrep(b) <= maxR && !m.curOffline(list[end]))) ++end;
+      if (end == i) return;  // the break of the reference loop
+      order.clear();
+      for (int x = 0; x < m.B; ++x)
+        if (m.alive(x) && (selfHealingMode || (int64_t)m.nrep(x) < maxR) && x != b) order.push_back(x);
+      std::sort(order.begin(), order.end(), [&](int x, int y) {
+        return m.nrep(x) != m.nrep(y) ? m.nrep(x) < m.nrep(y) : x < y;
+      });
+      e.eligible(order, DA_MOVE, cands);
+      const int64_t key = e.crossScan(*this, DA_MOVE, list, i, cands, FILTER_NONE, true, end);
+      if (key < 0) {
+        for (size_t q = i; q < end; ++q) fail(list[q]);
+        i = end;
+        continue;
+      }
+      const size_t k = i + (size_t)(key / (int64_t)cands.size());
+      for (size_t q = i; q < k; ++q) fail(list[q]);
+      m.relocateReplica(m.rPart[list[k]], b, cands[key % (int64_t)cands.size()]);
+      i = k + 1;
+    }
+  }
+
+  // updateGoalState (:165-181) + ensureReplicaCapacitySatisfied (:183-196)
+  void update(Engine& e) override {
+    Model& m = e.m;
+    ensureNoOfflineReplicas(m, name);
+    if (!selfHealingMode) {
+      for (int b = 0; b < m.B; ++b)
+        if ((int64_t)m.nrep(b) > maxR)
+          throw OptimizationFailure("[" + name + "] Replica count in broker " + std::to_string(b) +
+                                    " exceeds the maximum allowed number of replicas per broker.");
+      finished = true;
+    } else {
+      selfHealingMode = false;
+    }
+  }
+  int compareStats(const ccmi_cluster_stats&, const ccmi_cluster_stats&) const override { return 0; }
+};
+
+// ======================================================================================= CapacityGoal
+class Capacity : public GoalImpl {
+ public:
+  explicit Capacity(int kindIn) {
+    kind = kindIn;
+    switch (kindIn) {
+      case CCMI_GOAL_CPU_CAPACITY: res = R_CPU; name = "CpuCapacityGoal"; break;
+      case CCMI_GOAL_NW_IN_CAPACITY: res = R_NW_IN; name = "NetworkInboundCapacityGoal"; break;
+      case CCMI_GOAL_NW_OUT_CAPACITY: res = R_NW_OUT; name = "NetworkOutboundCapacityGoal"; break;
+      default: res = R_DISK; name = "DiskCapacityGoal"; break;
+    }
+  }
+  int res = 0;
+  double thr = 0;
+  static const char* resName(int r) {
+    switch (r) {
+      case R_CPU: return "CPU";
+      case R_NW_IN: return "NW_IN";
+      case R_NW_OUT: return "NW_OUT";
+      default: return "DISK";
+    }
+  }
+
+  // initGoalState (:120-170)
+  void init(Engine& e) override {
+    Model& m = e.m;
+    thr = e.bc.capThreshold[res];
+    const int n = allowedForReplicaMove(e, allowed);
+    const double existing = m.clusterUtil(res);
+    const double capacity = m.capacityWithAllowedReplicaMoves(res, e.opt.exclMove);
+    if (capacity * thr < existing) {
+      if (n == 0) throw OptimizationFailure("[" + name + "] All alive brokers are excluded from replica moves.");
+      throw OptimizationFailure("[" + name + "] Insufficient capacity for " + resName(res) + ".");
+    }
+    const bool selfHealing = m.numSelfHealing > 0;
+    Model::Spec all;
+    all.selImmigrants = e.opt.onlyImmigrants;
+    all.prioOffline = selfHealing;
+    all.prioImmigrants = !e.opt.onlyImmigrants;
+    all.scoreRes = res;
+    all.scoreReverse = true;
+    Model::Spec leaders;
+    leaders.selLeaders = true;
+    leaders.selImmigrants = e.opt.onlyImmigrants;
+    leaders.prioImmigrants = !e.opt.onlyImmigrants;
+    leaders.scoreRes = res;
+    leaders.scoreReverse = true;
+    for (int b = 0; b < m.B; ++b) {
+      m.track(b, sortId(kind, true, false), all);
+      m.track(b, sortId(kind, true, true), leaders);
+    }
+    dg = DevGoal{};
+    dg.kind = DG_CAPACITY;
+    dg.resource = res;
+    dg.capThr = thr;
+    dg.allowedSlot = (int)e.optimized.size();
+  }
+
+  // isUtilizationOverLimit (:410-428); the host is the broker
+  bool over(const Model& m, int b) const { return m.nrep(b) > 0 && m.bu(b, res) > m.cap(b, res) * thr; }
+
+  // rebalanceForBroker (:274-349)
+  void rebalance(Engine& e, int b) override {
+    PhaseScope ps(PH_OTHER_GOALS);
+    Model& m = e.m;
+    bool isOver = over(m, b);
+    if (!isOver && !hasOffline(m, b)) return;
+    if (res == R_NW_OUT || res == R_CPU) {
+      const std::vector<int32_t> leaders = m.sorted(b, sortId(kind, true, true));
+      std::vector<int32_t> pr, pb, owner, fol, elig;
+      size_t i = 0;
+      while (i < leaders.size()) {
+        // every remaining leader with its online followers' brokers by (utilization, id)
+        pr.clear();
+        pb.clear();
+        owner.clear();
+        for (size_t q = i; q < leaders.size(); ++q) {
+          const int r = leaders[q];
+          m.onlineFollowerBrokers(m.rPart[r], fol);
+          std::sort(fol.begin(), fol.end(), [&](int x, int y) {
+            const int c = jcmpDouble(m.bu(x, res), m.bu(y, res));
+            return c ? c < 0 : x < y;
+          });
+          e.eligible(fol, DA_LEADERSHIP, elig);
+          for (int x : elig) {
+            pr.push_back(r);
+            pb.push_back(x);
+            owner.push_back((int)q);
+          }
+        }
+        const int64_t key = e.pairScan(*this, pr, pb);
+        if (key < 0) break;
+        const size_t k = (size_t)owner[key];
+        m.relocateLeadership(m.rPart[leaders[k]], b, pb[key]);
+        isOver = over(m, b);
+        if (!isOver) break;
+        i = k + 1;
+      }
+    }
+    if (isOver || hasOffline(m, b)) {
+      // sortedAliveBrokersUnderThreshold (ClusterModel.java:1049-1095): a snapshot list
+      std::vector<int32_t> under, cands;
+      for (int x = 0; x < m.B; ++x)
+        if (m.alive(x) && !(m.bu(x, res) >= m.cap(x, res) * thr)) under.push_back(x);
+      stableSortBy(under, [&](int x, int y) { return jcmpDouble(m.bu(x, res), m.bu(y, res)); });
+      e.eligible(under, DA_MOVE, cands);
+      const std::vector<int32_t> list = m.sorted(b, sortId(kind, true, false));
+      size_t i = 0;
+      while (i < list.size()) {
+        const int64_t key = e.crossScan(*this, DA_MOVE, list, i, cands);
+        if (key < 0) break;
+        const size_t k = i + (size_t)(key / (int64_t)cands.size());
+        m.relocateReplica(m.rPart[list[k]], b, cands[key % (int64_t)cands.size()]);
+        isOver = over(m, b);
+        if (!isOver && !hasOffline(m, b)) break;
+        i = k + 1;
+      }
+    }
+    // postSanityCheck (:332-355)
+    if (isOver)
+      throw OptimizationFailure("[" + name + "] Utilization of broker " + std::to_string(b) +
+                                " violated capacity limit for resource " + resName(res) + ".");
+    if (hasOffline(m, b))
+      throw OptimizationFailure("[" + name + "] Cannot remove offline replicas from broker " + std::to_string(b) + ".");
+  }
+
+  // updateGoalState (:180-190) + ensureUtilizationUnderCapacity (:192-225)
+  void update(Engine& e) override {
+    Model& m = e.m;
+    for (int b = 0; b < m.B; ++b)
+      if (m.nrep(b) > 0 && m.bu(b, res) > m.cap(b, res) * thr)
+        throw OptimizationFailure("[" + name + "] utilization for broker is above capacity limit.");
+    ensureNoOfflineReplicas(m, name);
+    finished = true;
+  }
+  int compareStats(const ccmi_cluster_stats&, const ccmi_cluster_stats&) const override { return 0; }
+};
+
+// ======================================================================================= PotentialNwOutGoal
+class PotentialNwOut : public GoalImpl {
+ public:
+  PotentialNwOut() {
+    kind = CCMI_GOAL_POTENTIAL_NW_OUT;
+    name = "PotentialNwOutGoal";
+  }
+  bool fix = false;
+  double thr = 0;
+
+  void init(Engine& e) override {  // initGoalState (:185-195)
+    Model& m = e.m;
+    allowedForReplicaMove(e, allowed);
+    thr = e.bc.capThreshold[R_NW_OUT];
+    fix = false;
+    Model::Spec s;
+    s.selImmigrants = e.opt.onlyImmigrants;
+    for (int b = 0; b < m.B; ++b) m.track(b, sortId(kind, false, false), s);
+    dg = DevGoal{};
+    dg.kind = DG_POTENTIAL_NW_OUT;
+    dg.capThr = thr;
+    dg.allowedSlot = (int)e.optimized.size();
+  }
+  // brokersToBalance (:140-150): the broken brokers if any, else all
+  std::vector<int> brokersToBalance(Engine& e) override {
+    if (e.m.numDead == 0) return GoalImpl::brokersToBalance(e);
+    std::vector<int> v;
+    for (int b = 0; b < e.m.B; ++b)
+      if (!e.m.alive(b)) v.push_back(b);
+    return v;
+  }
+  bool over(const Model& m, int b) const { return m.nrep(b) > 0 && m.potNwOut(b) > m.cap(b, R_NW_OUT) * thr; }
+
+  // rebalanceForBroker (:270-331). The reference re-sorts the candidate list per replica; the sorted order only
+  // changes after a move, so the remaining replicas are scanned against the whole sorted list at once: a
+  // partition broker fails legitMove exactly where the reference had removed it, and is left out of the count.
+  void rebalance(Engine& e, int b) override {
+    PhaseScope ps(PH_OTHER_GOALS);
+    Model& m = e.m;
+    bool isOver = over(m, b);
+    if (!isOver && !(fix && hasOffline(m, b))) return;
+    std::vector<int32_t> candidates;
+    if (fix) {
+      candidates = aliveById(m);
+    } else {
+      std::vector<int> under;
+      for (int x = 0; x < m.B; ++x)
+        if (m.alive(x) && m.potNwOut(x) < m.cap(x, R_NW_OUT) * thr) under.push_back(x);
+      std::vector<int> ord;
+      javaHashSetOrder(under, ord);  // brokersUnderEstimatedMaxPossibleNwOut: a HashSet
+      candidates.assign(ord.begin(), ord.end());
+    }
+    const std::vector<int32_t> list = m.sorted(b, sortId(kind, false, false));
+    std::vector<int32_t> sortedC, cands, pos(m.B, -1);
+    size_t i = 0;
+    while (i < list.size()) {
+      sortedC = candidates;
+      stableSortBy(sortedC, [&](int x, int y) {
+        return jcmpDouble(m.ops.util(m.bLnw[y], R_NW_OUT), m.ops.util(m.bLnw[x], R_NW_OUT));
+      });
+      e.eligible(sortedC, DA_MOVE, cands);
+      for (size_t j = 0; j < cands.size(); ++j) pos[cands[j]] = (int)j;
+      const int64_t key = e.crossScan(*this, DA_MOVE, list, i, cands, FILTER_NONE, false);
+      const size_t N = cands.size();
+      const size_t kEnd = key < 0 ? list.size() : i + (size_t)(key / (int64_t)std::max<size_t>(N, 1));
+      auto rowCount = [&](int r, size_t upto) {  // visited eligible brokers of one row: partition brokers removed
+        int64_t c = (int64_t)upto;
+        const int p = m.rPart[r];
+        for (int s = m.pOff[p]; s < m.pOff[p + 1]; ++s) {
+          const int x = pos[m.rBroker[m.pSlots[s]]];
+          if (x >= 0 && (size_t)x < upto) c--;
+        }
+        return c;
+      };
+      for (size_t q = i; q < kEnd && q < list.size(); ++q) e.candidates += rowCount(list[q], N);
+      if (key >= 0) e.candidates += rowCount(list[kEnd], (size_t)(key % (int64_t)N) + 1);
+      for (int x : cands) pos[x] = -1;
+      if (key < 0) break;
+      const int dst = cands[key % (int64_t)N];
+      m.relocateReplica(m.rPart[list[kEnd]], b, dst);
+      isOver = over(m, b);
+      if (!isOver && !(fix && hasOffline(m, b))) break;
+      if (!fix && m.potNwOut(dst) > m.cap(dst, R_NW_OUT) * thr)
+        candidates.erase(std::find(candidates.begin(), candidates.end(), dst));
+      i = kEnd + 1;
+    }
+    if (isOver) succeeded = false;
+  }
+  // updateGoalState (:197-213)
+  void update(Engine& e) override {
+    Model& m = e.m;
+    for (int r = 0; r < m.R; ++r)
+      if (m.selfHealing[r] && m.curOffline(r)) {
+        if (fix) throw OptimizationFailure("[" + name + "] Cannot remove replica from broker " +
+                                           std::to_string(m.bId[m.rBroker[r]]));
+        fix = true;
+        dg.fixOffline = 1;
+        return;
+      }
+    finished = true;
+  }
+  int compareStats(const ccmi_cluster_stats& after, const ccmi_cluster_stats& before) const override {
+    return jcmpInt(after.num_brokers_under_potential_nw_out, before.num_brokers_under_potential_nw_out);
+  }
+};
+
+// ======================================================================================= TopicReplicaDistributionGoal
+class TopicReplicaDistribution : public GoalImpl {
+ public:
+  TopicReplicaDistribution() {
+    kind = CCMI_GOAL_TOPIC_REPLICA_DISTRIBUTION;
+    name = "TopicReplicaDistributionGoal";
+  }
+  bool fix = false, anyAbove = false, anyUnder = false;
+  std::vector<uint8_t> rebalanceTopic;
+  std::vector<int32_t> upper, lower;
+  int sid() const { return sortId(kind, false, false); }
+  bool excluded(int b) const { return !allowed[b]; }
+
+  // initGoalState (:225-270) with the gap-based limits (:95-150)
+  void init(Engine& e) override {
+    Model& m = e.m;
+    const int n = allowedForReplicaMove(e, allowed);
+    if (n == 0) throw OptimizationFailure("[" + name + "] All alive brokers are excluded from replica moves.");
+    const bool selfHealing = m.numSelfHealing > 0;
+    rebalanceTopic.assign(m.T, selfHealing ? 0 : 1);
+    if (selfHealing)
+      for (int r = 0; r < m.R; ++r)
+        if (m.selfHealing[r]) rebalanceTopic[m.pTopic[m.rPart[r]]] = 1;
+    const double margin = (e.bc.topicReplicaBalance - 1) * kBalanceMargin;
+    upper.assign(m.T, 0);
+    lower.assign(m.T, 0);
+    for (int t = 0; t < m.T; ++t) {
+      const double avg = m.topicNrep[t] / (double)n;
+      const int cu = (int)std::ceil(avg * (1 + margin));
+      const int umin = (int)(std::ceil(avg) + e.bc.topicMinGap), umax = (int)(std::ceil(avg) + e.bc.topicMaxGap);
+      upper[t] = std::max(umin, std::min(cu, umax));
+      const int cl = (int)std::floor(avg * jmax(0, (1 - margin)));
+      const int lmax = std::max(0, (int)(std::floor(avg) - e.bc.topicMinGap));
+      const int lmin = std::max(0, (int)(std::floor(avg) - e.bc.topicMaxGap));
+      lower[t] = std::max(lmin, std::min(cl, lmax));
+    }
+    for (int b = 0; b < m.B; ++b) {
+      Model::Spec s;
+      s.selImmigrants = e.opt.onlyImmigrants;
+      s.selImmOrOffline = selfHealing && m.alive(b);
+      m.track(b, sid(), s);
+    }
+    fix = false;
+    e.topicUpper = upper;
+    e.topicLower = lower;
+    e.dev->setTopicLimits(upper.data(), lower.data());
+    dg = DevGoal{};
+    dg.kind = DG_TOPIC_REPLICA_DISTRIBUTION;
+    dg.allowedSlot = (int)e.optimized.size();
+  }
+
+  // updateGoalState (:318-345)
+  void update(Engine& e) override {
+    if (anyAbove) succeeded = false;
+    if (anyUnder) succeeded = false;
+    anyAbove = anyUnder = false;
+    Model& m = e.m;
+    for (int r = 0; r < m.R; ++r)
+      if (m.selfHealing[r] && m.curOffline(r)) {
+        if (fix) throw OptimizationFailure("[" + name + "] Cannot remove replica from broker " +
+                                           std::to_string(m.bId[m.rBroker[r]]));
+        fix = true;
+        dg.fixOffline = 1;
+        return;
+      }
+    finished = true;
+  }
+  int compareStats(const ccmi_cluster_stats& after, const ccmi_cluster_stats& before) const override {
+    return cmpStd(after.topic_replica_std, before.topic_replica_std);
+  }
+
+  // rebalanceForBroker (:386-443) + skipBrokerRebalance (:348-377)
+  void rebalance(Engine& e, int b) override {
+    PhaseScope ps(PH_OTHER_GOALS);
+    Model& m = e.m;
+    std::vector<int32_t> topics;
+    m.bTopicKeys[b].order(topics);  // Broker.topics(): HashMap key order
+    // per-topic (offline count, has immigrant) of this broker's replicas, one pass (recounted after moves)
+    std::vector<std::pair<int, std::pair<int, int>>> per;
+    auto recount = [&]() {
+      per.clear();
+      for (int r : m.bRepl[b]) {
+        const int t = m.pTopic[m.rPart[r]];
+        bool found = false;
+        for (auto& x : per)
+          if (x.first == t) {
+            x.second.first += m.rInOff[r];
+            x.second.second |= m.rInImm[r];
+            found = true;
+            break;
+          }
+        if (!found) per.push_back({t, {m.rInOff[r], m.rInImm[r]}});
+      }
+    };
+    recount();
+    for (int t : topics) {
+      if (!rebalanceTopic[t]) continue;
+      int nOff = 0, hasImm = 0;
+      for (auto& x : per)
+        if (x.first == t) {
+          nOff = x.second.first;
+          hasImm = x.second.second;
+          break;
+        }
+      const int n = m.tcount(t, b);
+      const bool excl = excluded(b);
+      const bool requireLess = nOff > 0 || n > upper[t] || excl;
+      const bool requireMore = !excl && m.alive(b) && n - nOff < lower[t];
+      if (m.alive(b) && !requireMore && !requireLess) continue;
+      if (m.numNew > 0 && !m.isNew(b) && !requireLess) continue;
+      if (m.numSelfHealing > 0 && requireLess && nOff == 0 && !hasImm) continue;
+      if (e.opt.onlyImmigrants && requireLess && !hasImm) continue;
+      if (requireLess && moveOut(e, b, t)) anyAbove = true;
+      if (requireMore && moveIn(e, b, t)) anyUnder = true;
+      if (requireLess || requireMore) recount();  // the moves changed this broker's replicas
+    }
+  }
+
+  // replicasToMoveOut (:445-451): the topic's replicas of b that the tracked set selects, ordered by
+  // Broker.replicaComparator (offline first, immigrants first, partition number)
+  void replicasToMoveOut(Model& m, int b, int t, std::vector<int32_t>& out) {
+    out.clear();
+    for (int r : m.bRepl[b])
+      if (m.pTopic[m.rPart[r]] == t && selected(m, b, r)) out.push_back(r);
+    std::sort(out.begin(), out.end(), [&](int x, int y) {
+      const bool ox = m.rInOff[x] != 0, oy = m.rInOff[y] != 0;
+      if (ox != oy) return ox;
+      const bool ix = m.rInImm[x] != 0, iy = m.rInImm[y] != 0;
+      if (ix != iy) return ix;
+      return m.pNumber[m.rPart[x]] < m.pNumber[m.rPart[y]];
+    });
+  }
+  // membership in the tracked SortedReplicas of b (its selection functions, evaluated on live state)
+  bool selected(const Model& m, int b, int r) const {
+    for (const auto& t : m.tracked[b])
+      if (t.nameId == sid()) return m.selects(t.spec, r);
+    return true;
+  }
+
+  // rebalanceByMovingReplicasOut (:453-505): consecutive rows share the live TreeSet's in-order list until a move
+  bool moveOut(Engine& e, int b, int t) {
+    Model& m = e.m;
+    auto cmp = [&m, t](int x, int y) {
+      const int c = jcmpInt(m.tcount(t, x), m.tcount(t, y));
+      return c ? c : jcmpInt(m.bId[x], m.bId[y]);
+    };
+    RbTreeSet<decltype(cmp)> cand(cmp);
+    {
+      std::vector<int> ins, order;
+      for (int x = 0; x < m.B; ++x)
+        if (m.alive(x) && (fix || m.tcount(t, x) < upper[t])) ins.push_back(x);
+      if (fix) order = ins;
+      else javaHashSetOrder(ins, order);  // Collectors.toSet()
+      for (int x : order) cand.add(x);
+    }
+    int n = m.tcount(t, b), nOff = 0;
+    for (int r : m.bRepl[b])
+      if (m.pTopic[m.rPart[r]] == t && m.rInOff[r]) nOff++;
+    const int upperSrc = excluded(b) ? 0 : upper[t];
+    bool wasUnable = false;
+    std::vector<int32_t> list, inorder, cands;
+    replicasToMoveOut(m, b, t, list);
+    size_t i = 0;
+    while (i < list.size()) {
+      // a run of rows with equal offline status: the early return is decided at the run's first row
+      if (wasUnable && !m.curOffline(list[i]) && n <= upperSrc) return false;
+      const bool runOffline = m.curOffline(list[i]);
+      size_t end = i;
+      while (end < list.size() && m.curOffline(list[end]) == runOffline) ++end;
+      cand.inorder(inorder);
+      e.eligible(inorder, DA_MOVE, cands);
+      const int64_t key = e.crossScan(*this, DA_MOVE, list, i, cands, FILTER_NONE, true, end);
+      if (key < 0) {
+        if (runOffline) wasUnable = true;
+        i = end;
+        continue;
+      }
+      const size_t N = cands.size();
+      const size_t k = i + (size_t)(key / (int64_t)N);
+      if (runOffline && k > i) wasUnable = true;
+      const int r = list[k], dst = cands[key % (int64_t)N];
+      const bool wasOffline = m.curOffline(r);
+      m.relocateReplica(m.rPart[r], b, dst);
+      if (wasOffline) nOff--;
+      if (--n <= (nOff == 0 ? upperSrc : 0)) return false;
+      cand.remove(dst);
+      if (m.tcount(t, dst) < upper[t] || fix) cand.add(dst);
+      i = k + 1;
+    }
+    return m.tcount(t, b) != 0;
+  }
+
+  // rebalanceByMovingReplicasIn (:507-570)
+  bool moveIn(Engine& e, int dest, int t) {
+    Model& m = e.m;
+    auto offCount = [&](int x) {
+      int k = 0;
+      for (int r : m.bRepl[x])
+        if (m.pTopic[m.rPart[r]] == t && m.rInOff[r]) k++;
+      return k;
+    };
+    auto cmp = [&](int b1, int b2) {
+      const int r = jcmpInt(offCount(b2), offCount(b1));
+      if (r == 0) {
+        const int r2 = jcmpInt(m.tcount(t, b2), m.tcount(t, b1));
+        return r2 == 0 ? jcmpInt(m.bId[b1], m.bId[b2]) : r2;
+      }
+      return r;
+    };
+    JavaPQ<decltype(cmp)> pq(cmp);
+    for (int s = 0; s < m.B; ++s) {
+      if (fix) {
+        if (s != dest) pq.add(s);
+      } else if (m.tcount(t, s) > lower[t] || hasOffline(m, s) || excluded(s)) {
+        pq.add(s);
+      }
+    }
+    int n = m.tcount(t, dest);
+    std::vector<int32_t> single{dest}, cands, toMove;
+    e.eligible(single, DA_MOVE, cands);
+    while (!pq.empty()) {
+      const int src = pq.poll();
+      replicasToMoveOut(m, src, t, toMove);
+      int nOff = 0;
+      for (int r : toMove)
+        if (m.rInOff[r]) nOff++;
+      size_t i = 0;
+      while (i < toMove.size()) {
+        const int64_t key = cands.empty() ? -1 : e.crossScan(*this, DA_MOVE, toMove, i, cands);
+        if (key < 0) break;
+        const size_t k = i + (size_t)key;
+        const bool wasOffline = m.curOffline(toMove[k]);
+        m.relocateReplica(m.rPart[toMove[k]], src, dest);
+        if (wasOffline) nOff--;
+        if (++n >= lower[t]) return false;
+        if (!pq.empty() && nOff == 0 && m.tcount(t, src) < m.tcount(t, pq.peek())) {
+          pq.add(src);
+          break;
+        }
+        i = k + 1;
+      }
+    }
+    return true;
+  }
+};
+
+// ======================================================================================= LeaderReplicaDistributionGoal
+class LeaderReplicaDistribution : public GoalImpl {
+ public:
+  LeaderReplicaDistribution() {
+    kind = CCMI_GOAL_LEADER_REPLICA_DISTRIBUTION;
+    name = "LeaderReplicaDistributionGoal";
+  }
+  bool fix = false, anyAbove = false, anyUnder = false;
+  int upper = 0, lower = 0;
+  bool excluded(int b) const { return !allowed[b]; }
+
+  // ReplicaDistributionAbstractGoal.initGoalState (:124-152), numInterestedReplicas = number of leaders
+  void init(Engine& e) override {
+    Model& m = e.m;
+    const int n = allowedForReplicaMove(e, allowed);
+    if (n == 0) throw OptimizationFailure("[" + name + "] All alive brokers are excluded from replica moves.");
+    const double avg = m.numLeaderReplicas() / (double)n;
+    fix = false;
+    const double adj = (e.bc.leaderReplicaBalance - 1) * kBalanceMargin;
+    upper = (int)std::ceil(avg * (1 + adj));
+    lower = (int)std::floor(avg * jmax(0, (1 - adj)));
+    dg = DevGoal{};
+    dg.kind = DG_LEADER_REPLICA_DISTRIBUTION;
+    dg.upper = upper;
+    dg.lower = lower;
+    dg.allowedSlot = (int)e.optimized.size();
+  }
+  // updateGoalState (ReplicaDistributionAbstractGoal.java:183-223)
+  void update(Engine& e) override {
+    if (anyAbove) succeeded = false;
+    if (anyUnder) succeeded = false;
+    anyAbove = anyUnder = false;
+    Model& m = e.m;
+    for (int r = 0; r < m.R; ++r)
+      if (m.selfHealing[r] && m.curOffline(r)) {
+        if (fix) throw OptimizationFailure("[" + name + "] Cannot remove replica from broker " +
+                                           std::to_string(m.bId[m.rBroker[r]]));
+        fix = true;
+        dg.fixOffline = 1;
+        return;
+      }
+    finished = true;
+  }
+  int compareStats(const ccmi_cluster_stats& after, const ccmi_cluster_stats& before) const override {
+    return cmpStd(after.leader_std, before.leader_std);
+  }
+
+  // rebalanceForBroker (:137-166)
+  void rebalance(Engine& e, int b) override {
+    PhaseScope ps(PH_OTHER_GOALS);
+    Model& m = e.m;
+    const int nl = m.bNlead[b];
+    const bool excl = excluded(b);
+    const bool lessLeaders = m.alive(b) && nl > (excl ? 0 : upper);
+    const bool moreLeaders = !excl && m.alive(b) && nl < lower;
+    const bool lessReplicas = fix && hasOffline(m, b);
+    if (((lessLeaders && moveLeadershipOut(e, b)) || lessReplicas) && moveReplicasOut(e, b)) {
+      if (!lessReplicas) anyAbove = true;
+    } else if (moreLeaders && moveLeadershipIn(e, b) && moveLeaderReplicasIn(e, b)) {
+      anyUnder = true;
+    }
+  }
+
+  // rebalanceByMovingLeadershipOut (:168-203): every leader's candidate set is fixed, so all remaining leaders
+  // are scanned as one pair list and the scan resumes after each winner
+  bool moveLeadershipOut(Engine& e, int b) {
+    Model& m = e.m;
+    if (m.numDead > 0) return true;
+    const int upperSrc = excluded(b) ? 0 : upper;
+    int nl = m.bNlead[b];
+    ReplicaSet copy;  // new HashSet<>(broker.leaderReplicas())
+    copy.assignCopy(m.bLeaderSet[b]);
+    std::vector<int32_t> leaders;
+    copy.order(leaders);
+    std::vector<int32_t> pr, pb, owner;
+    std::vector<int> ins, hs, hs2, elig;
+    for (size_t q = 0; q < leaders.size(); ++q) {
+      const int r = leaders[q], p = m.rPart[r];
+      ins.clear();
+      for (int s = m.pOff[p]; s < m.pOff[p + 1]; ++s) ins.push_back(m.rBroker[m.pSlots[s]]);
+      javaHashSetOrder(ins, hs);  // Partition.partitionBrokers()
+      ins.clear();
+      for (int x : hs)
+        if (x != b && !m.curOffline(m.replicaOn(p, x))) ins.push_back(x);
+      javaHashSetOrder(ins, hs2);  // Collectors.toSet()
+      std::vector<int32_t> c32(hs2.begin(), hs2.end()), el;
+      e.eligible(c32, DA_LEADERSHIP, el);
+      for (int x : el) {
+        pr.push_back(r);
+        pb.push_back(x);
+        owner.push_back((int)q);
+      }
+    }
+    size_t start = 0;
+    std::vector<int32_t> spr, spb;
+    while (start < pr.size()) {
+      spr.assign(pr.begin() + start, pr.end());
+      spb.assign(pb.begin() + start, pb.end());
+      const int64_t key = e.pairScan(*this, spr, spb);
+      if (key < 0) break;
+      const size_t at = start + (size_t)key;
+      const int r = pr[at];
+      m.relocateLeadership(m.rPart[r], b, pb[at]);
+      if (--nl <= upperSrc) return false;
+      start = at + 1;
+      while (start < pr.size() && owner[start] == owner[at]) ++start;  // next leader
+    }
+    return true;
+  }
+
+  // rebalanceByMovingLeadershipIn (:205-240)
+  bool moveLeadershipIn(Engine& e, int b) {
+    Model& m = e.m;
+    if (m.numDead > 0 || (e.opt.anyExclLead && e.opt.exclLead[b])) return true;
+    int nl = m.bNlead[b];
+    std::vector<int32_t> reps, pr, pb;
+    m.bReplicaSet[b].order(reps);  // Broker.replicas(): HashSet order
+    std::vector<int32_t> single{b}, cands;
+    e.eligible(single, DA_LEADERSHIP, cands);
+    if (cands.empty()) return true;
+    for (int r : reps) {
+      if (m.rLeader[r] || m.curOffline(r)) continue;
+      pr.push_back(m.pLeader[m.rPart[r]]);
+      pb.push_back(b);
+    }
+    size_t start = 0;
+    std::vector<int32_t> spr, spb;
+    while (start < pr.size()) {
+      spr.assign(pr.begin() + start, pr.end());
+      spb.assign(pb.begin() + start, pb.end());
+      const int64_t key = e.pairScan(*this, spr, spb);
+      if (key < 0) break;
+      const size_t at = start + (size_t)key;
+      m.relocateLeadership(m.rPart[pr[at]], m.rBroker[pr[at]], b);
+      if (++nl >= lower) return false;
+      start = at + 1;
+    }
+    return true;
+  }
+
+  // rebalanceByMovingReplicasOut (:242-300)
+  bool moveReplicasOut(Engine& e, int b) {
+    Model& m = e.m;
+    const bool f = fix;
+    auto cmp = [&m, f](int x, int y) {
+      const int c = f ? jcmpInt(m.nrep(x), m.nrep(y)) : jcmpInt(m.bNlead[x], m.bNlead[y]);
+      return c ? c : jcmpInt(m.bId[x], m.bId[y]);
+    };
+    RbTreeSet<decltype(cmp)> cand(cmp);
+    if (fix) {
+      for (int x : aliveById(m)) cand.add(x);
+    } else {
+      std::vector<int> ins, order;
+      for (int x = 0; x < m.B; ++x)
+        if (m.alive(x) && m.bNlead[x] < upper) ins.push_back(x);
+      javaHashSetOrder(ins, order);
+      for (int x : order) cand.add(x);
+    }
+    const int upperLimit = fix ? 0 : upper;
+    const int id = sortId(kind, false, !fix);
+    Model::Spec s;
+    s.selLeaders = !fix;
+    s.selOffline = fix;
+    s.selImmigrants = (!fix && m.numSelfHealing > 0) || e.opt.onlyImmigrants;
+    m.track(b, id, s);
+    const std::vector<int32_t> list = m.sorted(b, id);
+    int n = (int)list.size();
+    std::vector<int32_t> inorder, cands;
+    size_t i = 0;
+    while (i < list.size()) {
+      cand.inorder(inorder);
+      e.eligible(inorder, DA_MOVE, cands);
+      const int64_t key = e.crossScan(*this, DA_MOVE, list, i, cands);
+      if (key < 0) break;
+      const size_t N = cands.size();
+      const size_t k = i + (size_t)(key / (int64_t)N);
+      const int dst = cands[key % (int64_t)N];
+      m.relocateReplica(m.rPart[list[k]], b, dst);
+      if (--n <= upperLimit) {
+        m.untrack(b, id);
+        return false;
+      }
+      cand.remove(dst);
+      if (m.bNlead[dst] < upper || fix) cand.add(dst);
+      i = k + 1;
+    }
+    m.untrack(b, id);
+    return true;
+  }
+
+  // rebalanceByMovingLeaderReplicasIn (:302-352)
+  bool moveLeaderReplicasIn(Engine& e, int b) {
+    Model& m = e.m;
+    if (e.opt.anyExclLead && e.opt.exclLead[b]) return true;
+    auto cmp = [&m](int b1, int b2) {
+      const int r = jcmpInt(m.bNlead[b2], m.bNlead[b1]);
+      return r == 0 ? jcmpInt(m.bId[b1], m.bId[b2]) : r;
+    };
+    JavaPQ<decltype(cmp)> pq(cmp);
+    for (int x = 0; x < m.B; ++x)
+      if (m.alive(x) && m.bNlead[x] > lower) pq.add(x);
+    const int id = sortId(kind, false, true);
+    Model::Spec s;
+    s.selLeaders = true;
+    s.selImmigrants = m.numDead > 0 || m.numBadDisk > 0 || e.opt.onlyImmigrants;
+    for (int x = 0; x < m.B; ++x) m.track(x, id, s);
+    int nl = m.bNlead[b];
+    std::vector<int32_t> single{b}, cands;
+    e.eligible(single, DA_MOVE, cands);
+    while (!pq.empty()) {
+      const int src = pq.poll();
+      const std::vector<int32_t> list = m.sorted(src, id);
+      size_t i = 0;
+      while (i < list.size()) {
+        const int64_t key = cands.empty() ? -1 : e.crossScan(*this, DA_MOVE, list, i, cands);
+        if (key < 0) break;
+        const size_t k = i + (size_t)key;
+        m.relocateReplica(m.rPart[list[k]], src, b);
+        if (++nl >= lower) {
+          m.untrackAll(id);
+          return false;
+        }
+        if (!pq.empty() && m.bNlead[src] < m.bNlead[pq.peek()]) {
+          pq.add(src);
+          break;
+        }
+        i = k + 1;
+      }
+    }
+    m.untrackAll(id);
+    return true;
+  }
+};
+
+// ======================================================================================= LeaderBytesInDistributionGoal
+class LeaderBytesIn : public GoalImpl {
+ public:
+  LeaderBytesIn() {
+    kind = CCMI_GOAL_LEADER_BYTES_IN_DISTRIBUTION;
+    name = "LeaderBytesInDistributionGoal";
+  }
+  double mean = 0.0;
+  int numAllowed = 0;
+  bool overLimit = false;
+  double balance = 0, lowUtil = 0;
+
+  // initMeanLeaderBytesIn (:250-257): cached on first use (recomputed while it is 0.0)
+  void initMean(Engine& e) {
+    if (mean == 0.0) {
+      JDoubleSum s;
+      for (int b = 0; b < e.m.B; ++b)
+        if (e.m.alive(b)) s.add(e.m.leadNwIn(b));
+      mean = s.result() / numAllowed;
+      dg.lbiMean = mean;
+    }
+  }
+  // balanceThreshold (:264-271)
+  double threshold(Engine& e, int b) {
+    initMean(e);
+    return jmax(mean * balance, lowUtil * e.m.cap(b, R_NW_IN));
+  }
+  void init(Engine& e) override {  // initGoalState (:162-185)
+    Model& m = e.m;
+    numAllowed = allowedForReplicaMove(e, allowed);
+    if (numAllowed == 0) throw OptimizationFailure("[" + name + "] All alive brokers are excluded from replica moves.");
+    mean = 0.0;
+    overLimit = false;
+    balance = e.bc.resBalance[R_NW_IN];
+    lowUtil = e.bc.lowUtil[R_NW_IN];
+    Model::Spec s;
+    s.selLeaders = true;
+    s.scoreRes = R_NW_IN;
+    s.scoreReverse = true;
+    for (int b = 0; b < m.B; ++b) m.track(b, sortId(kind, true, true), s);
+    dg = DevGoal{};
+    dg.kind = DG_LEADER_BYTES_IN;
+    dg.lbiBalance = balance;
+    dg.lbiLowUtil = lowUtil;
+    dg.allowedSlot = (int)e.optimized.size();
+  }
+  // brokersToBalance (:142-152)
+  std::vector<int> brokersToBalance(Engine& e) override {
+    std::vector<int> v;
+    for (int b = 0; b < e.m.B; ++b)
+      if (e.m.leadNwIn(b) > threshold(e, b)) v.push_back(b);
+    return v;
+  }
+  // rebalanceForBroker (:203-233): all remaining leaders' follower lists in one pair scan; lists are rebuilt
+  // after each move because they are sorted by live leader bytes-in
+  void rebalance(Engine& e, int b) override {
+    PhaseScope ps(PH_OTHER_GOALS);
+    Model& m = e.m;
+    const double thr = threshold(e, b);
+    if (m.leadNwIn(b) < thr) return;
+    bool over = true;
+    const std::vector<int32_t> leaders = m.sorted(b, sortId(kind, true, true));
+    std::vector<int32_t> pr, pb, owner, fol, elig;
+    size_t i = 0;
+    while (over && i < leaders.size()) {
+      pr.clear();
+      pb.clear();
+      owner.clear();
+      for (size_t q = i; q < leaders.size(); ++q) {
+        const int r = leaders[q];
+        m.onlineFollowerBrokers(m.rPart[r], fol);
+        stableSortBy(fol, [&](int x, int y) { return jcmpDouble(m.leadNwIn(x), m.leadNwIn(y)); });
+        e.eligible(fol, DA_LEADERSHIP, elig);
+        for (int x : elig) {
+          pr.push_back(r);
+          pb.push_back(x);
+          owner.push_back((int)q);
+        }
+      }
+      const int64_t key = e.pairScan(*this, pr, pb);
+      if (key < 0) break;
+      const size_t k = (size_t)owner[key];
+      m.relocateLeadership(m.rPart[leaders[k]], b, pb[key]);
+      over = m.leadNwIn(b) > thr;
+      i = k + 1;
+    }
+    if (over) overLimit = true;
+  }
+  void update(Engine&) override {  // updateGoalState (:194-201)
+    if (overLimit) succeeded = false;
+    overLimit = false;
+    finished = true;
+  }
+  // LeaderBytesInDistributionGoalStatsComparator (:273-300)
+  int compareStats(const ccmi_cluster_stats& after, const ccmi_cluster_stats& before) const override {
+    const double meanPre = after.resource_avg[R_NW_IN];
+    const double thr = meanPre * balance;
+    if (after.resource_max[R_NW_IN] <= thr) return 1;
+    const double d1 = std::sqrt(before.resource_std[R_NW_IN]), d2 = std::sqrt(after.resource_std[R_NW_IN]);
+    // AnalyzerUtils.compare(d1, d2, Resource.NW_IN): Resource.epsilon = max(10, 0.0008 * (d1 + d2))
+    const double eps = jmax(10.0, 0.0008 * (d1 + d2));
+    if (d2 - d1 > eps) return -1;
+    if (d1 - d2 > eps) return 1;
+    return 0;
+  }
+};
+
+}  // namespace
+
+std::unique_ptr<GoalImpl> makeMoreGoal(int kind) {
+  switch (kind) {
+    case CCMI_GOAL_RACK_AWARE: return std::make_unique<RackAware>();
+    case CCMI_GOAL_MIN_TOPIC_LEADERS_PER_BROKER: return std::make_unique<MinTopicLeaders>();
+    case CCMI_GOAL_REPLICA_CAPACITY: return std::make_unique<ReplicaCapacity>();
+    case CCMI_GOAL_DISK_CAPACITY:
+    case CCMI_GOAL_NW_IN_CAPACITY:
+    case CCMI_GOAL_NW_OUT_CAPACITY:
+    case CCMI_GOAL_CPU_CAPACITY: return std::make_unique<Capacity>(kind);
+    case CCMI_GOAL_POTENTIAL_NW_OUT: return std::make_unique<PotentialNwOut>();
+    case CCMI_GOAL_TOPIC_REPLICA_DISTRIBUTION: return std::make_unique<TopicReplicaDistribution>();
+    case CCMI_GOAL_LEADER_REPLICA_DISTRIBUTION: return std::make_unique<LeaderReplicaDistribution>();
+    case CCMI_GOAL_LEADER_BYTES_IN_DISTRIBUTION: return std::make_unique<LeaderBytesIn>();
+    default: throw Unsupported("goal kind " + std::to_string(kind) + " is not implemented in this build");
+  }
+}
+
+}  // namespace ccmi

@@ -9,6 +9,22 @@
 
 namespace ccmi {
 
+// Replica.compareTo (Replica.java:349-377): offline first, then partition number, original broker id, topic
+int ReplicaOrder::cmp(int a, int b) const {
+  const bool oa = m->curOffline(a), ob = m->curOffline(b);
+  if (oa != ob) return oa ? -1 : 1;
+  const int na = m->pNumber[m->rPart[a]], nb = m->pNumber[m->rPart[b]];
+  if (na != nb) return na > nb ? 1 : -1;
+  const int ia = m->bId[m->rOrig[a]], ib = m->bId[m->rOrig[b]];
+  if (ia != ib) return ia > ib ? 1 : -1;
+  const int ta = m->topicRank[m->pTopic[m->rPart[a]]], tb = m->topicRank[m->pTopic[m->rPart[b]]];
+  return ta == tb ? 0 : (ta < tb ? -1 : 1);
+}
+int TopicOrder::cmp(int a, int b) const {  // String.compareTo sign
+  const int ra = m->topicRank[a], rb = m->topicRank[b];
+  return ra == rb ? 0 : (ra < rb ? -1 : 1);
+}
+
 void Model::build(const ccmi_cluster_desc& d) {
   if (d.num_windows < 1 || d.num_windows > kMaxW) throw std::invalid_argument("num_windows must be in [1,5]");
   W = d.num_windows;
@@ -47,7 +63,15 @@ void Model::build(const ccmi_cluster_desc& d) {
   pSlots.assign(d.partition_replicas, d.partition_replicas + R);
   pLeader.assign(P, -1);
   topicNames.clear();
-  for (int t = 0; t < T; ++t) topicNames.emplace_back(d.topic_names[t]);
+  topicHash.assign(T, 0);
+  for (int t = 0; t < T; ++t) {
+    topicNames.emplace_back(d.topic_names[t]);
+    topicHash[t] = jStringHash(d.topic_names[t]);
+  }
+  bReplicaSet.assign(B, ReplicaSet(&replicaOrder));
+  bLeaderSet.assign(B, ReplicaSet(&replicaOrder));
+  bOfflineSet.assign(B, ReplicaSet(&replicaOrder));
+  bTopicKeys.assign(B, TopicSet(&topicOrder));
   {
     std::vector<int> idx(T);
     for (int t = 0; t < T; ++t) idx[t] = t;
@@ -111,6 +135,10 @@ void Model::build(const ccmi_cluster_desc& d) {
           rInOff[r] = 1;
           bNoff[b]++;
         }
+      // Broker.setState(DEAD): _currentOfflineReplicas.addAll(_replicas)
+      std::vector<int32_t> order;
+      bReplicaSet[b].order(order);
+      for (int r : order) bOfflineSet[b].add(r, replicaHash(r));
       for (int k = 0; k < 4; ++k) bCap[4 * b + k] = -1.0;
     }
     if (s == BState::NEW) numNew++;
@@ -134,7 +162,7 @@ void Model::build(const ccmi_cluster_desc& d) {
   rScoreC.assign((size_t)4 * R, 0.f);
   for (int b = 0; b < B; ++b) refreshBroker(b);
   for (int r = 0; r < R; ++r) refreshReplica(r);
-  const int ldB = (B + 3) & ~3;
+  ldB = (B + 3) & ~3;
   topicCountDense.assign((size_t)T * ldB, 0);
   for (int r = 0; r < R; ++r) topicCountDense[(size_t)pTopic[rPart[r]] * ldB + rBroker[r]]++;
   bDirty.assign(B, 0);
@@ -217,6 +245,10 @@ double Model::capacityWithAllowedReplicaMoves(int res, const std::vector<uint8_t
 void Model::brokerAdd(int b, int r) {
   rPos[r] = (int)bRepl[b].size();
   bRepl[b].push_back(r);
+  const int32_t h = replicaHash(r);
+  bReplicaSet[b].add(r, h);
+  const int t = pTopic[rPart[r]];
+  bTopicKeys[b].add(t, topicHash[t]);
   rInImm[r] = rInOff[r] = 0;
   if (rOrig[r] != b) {
     rInImm[r] = 1;
@@ -224,10 +256,12 @@ void Model::brokerAdd(int b, int r) {
   } else if (origOffline(r)) {
     rInOff[r] = 1;
     bNoff[b]++;
+    bOfflineSet[b].add(r, h);
   }
   if (rLeader[r]) {
     ops.addAll(bLnw[b], rLoad[r]);
     bNlead[b]++;
+    bLeaderSet[b].add(r, h);
   }
   ops.addAll(bLoad[b], rLoad[r]);
   sortedInsert(b, r);
@@ -242,10 +276,14 @@ int Model::brokerRemove(int b, int p) {
   rPos[v[pos]] = pos;
   v.pop_back();
   rPos[r] = -1;
+  const int32_t h = replicaHash(r);
+  bReplicaSet[b].remove(r, h);
+  bOfflineSet[b].remove(r, h);
   ops.subAll(bLoad[b], rLoad[r]);
   if (rLeader[r]) {
     ops.subAll(bLnw[b], rLoad[r]);
     bNlead[b]--;
+    bLeaderSet[b].remove(r, h);
   }
   if (rInImm[r]) bNimm[b]--;
   if (rInOff[r]) bNoff[b]--;
@@ -269,6 +307,10 @@ void Model::relocateReplica(int p, int src, int dst) {
   refreshBroker(src);
   refreshBroker(dst);
   log.push_back({CCMI_INTER_BROKER_REPLICA_MOVEMENT, p, src, dst, -1});
+  if (!topicCountDense.empty()) {
+    topicCountDense[(size_t)pTopic[p] * ldB + src]--;
+    topicCountDense[(size_t)pTopic[p] * ldB + dst]++;
+  }
   if (dev) {
     markB(src);
     markB(dst);
@@ -319,6 +361,7 @@ bool Model::relocateLeadership(int p, int src, int dst) {
   refreshReplica(sr);
   if (bLoad[src].mask) ops.subAll(bLoad[src], delta);
   bNlead[src]--;
+  bLeaderSet[src].remove(sr, replicaHash(sr));
   sortedInsert(src, sr);
   // Broker.makeLeader(dst)
   sortedErase(dst, dr);
@@ -328,6 +371,7 @@ bool Model::relocateLeadership(int p, int src, int dst) {
   ops.addAll(bLnw[dst], rLoad[dr]);
   if (bLoad[dst].mask) ops.addAll(bLoad[dst], delta);
   bNlead[dst]++;
+  bLeaderSet[dst].add(dr, replicaHash(dr));
   sortedInsert(dst, dr);
   // Partition.relocateLeadership: swap positions 0 and indexOf(dr)
   int pos = pOff[p];
@@ -356,8 +400,8 @@ void Model::flushToDevice() {
     row.nlead = bNlead[b];
     row.alive = alive(b) ? 1 : 0;
     for (int k = 0; k < 4; ++k) row.util[k] = bUtilC[4 * b + k];
-    row.potNwOut = ops.util(bPot[b], R_NW_OUT);
-    row.pad = 0;
+    row.potNwOut = potNwOut(b);
+    row.leadNwIn = leadNwIn(b);
     dev->brows.push_back(row);
     bDirty[b] = 0;
   }
@@ -378,6 +422,8 @@ void Model::flushToDevice() {
     row.p = p;
     row.n = pOff[p + 1] - pOff[p];
     for (int k = 0; k < row.n; ++k) row.brokers[k] = rBroker[pSlots[pOff[p] + k]];
+    for (int k = row.n; k < kMaxRf; ++k) row.brokers[k] = -1;
+    row.leadNwOut = pLeadNwOut(p);
     dev->prows.push_back(row);
     pDirty[p] = 0;
   }
@@ -390,6 +436,7 @@ bool Model::selects(const Spec& s, int r) const {
   if (s.selFollowers && rLeader[r]) return false;
   if (s.selImmigrants && !immigrant(r)) return false;
   if (s.selImmOrOffline && !(immigrant(r) || curOffline(r))) return false;
+  if (s.selOffline && !curOffline(r)) return false;
   if (s.selAboveRes >= 0 && !(ru(r, s.selAboveRes) > s.aboveLimit)) return false;
   if (s.selBelowRes >= 0 && !(ru(r, s.selBelowRes) < s.belowLimit)) return false;
   return true;

@@ -106,6 +106,19 @@ struct ActionRec {
 };
 
 class Device;
+class Model;
+
+// Element orders of the broker HashSets: Replica.compareTo (Replica.java:349-377) and String.compareTo.
+struct ReplicaOrder {
+  const Model* m;
+  int cmp(int a, int b) const;
+};
+struct TopicOrder {
+  const Model* m;
+  int cmp(int a, int b) const;
+};
+using ReplicaSet = JHashSet<ReplicaOrder>;
+using TopicSet = JHashSet<TopicOrder>;
 
 class Model {
  public:
@@ -118,6 +131,18 @@ class Model {
   std::vector<std::vector<int32_t>> bRepl;  // replica ids hosted (HashSet contents; order unused)
   std::vector<int32_t> bNlead, bNimm, bNoff;
   std::vector<LoadVec> bLoad, bLnw, bPot;
+  // Broker._replicas, _leaderReplicas, _currentOfflineReplicas (HashSet<Replica>) and _topicReplicas' key set
+  // (HashMap<String, ...>), emulated for their iteration order
+  std::vector<ReplicaSet> bReplicaSet, bLeaderSet, bOfflineSet;
+  std::vector<TopicSet> bTopicKeys;
+  ReplicaOrder replicaOrder{this};
+  TopicOrder topicOrder{this};
+  std::vector<int32_t> topicHash;           // String.hashCode of every topic name
+  int32_t replicaHash(int r) const {        // Objects.hash(TopicPartition, originalBroker.id())
+    const int p = rPart[r];
+    const int32_t tp = jMix(jMix(1, pNumber[p]), topicHash[pTopic[p]]);  // TopicPartition.hashCode
+    return jMix(jMix(1, tp), bId[rOrig[r]]);
+  }
   std::vector<double> bUtilC;               // cache [B][4] of ops.util(bLoad[b], res)
   std::vector<double> bPctC;                // cache [B][4] of GoalUtils.utilization: util / cap, 1.0 if cap <= 0
   // All brokers ordered by (utilization %, id) per resource — the order every utilization-keyed TreeSet /
@@ -138,7 +163,9 @@ class Model {
   // topics
   std::vector<std::string> topicNames;
   std::vector<int32_t> topicRank, topicNrep;
-  std::vector<int32_t> topicCountDense;     // [T][ldB] (host copy only at build time)
+  std::vector<int32_t> topicCountDense;     // [T][ldB] live Broker.numReplicasOfTopicInBroker counts
+  int ldB = 4;
+  int tcount(int t, int b) const { return topicCountDense[(size_t)t * ldB + b]; }
   // cluster
   LoadVec cLoad;
   double clusterCap[4] = {0, 0, 0, 0};
@@ -199,6 +226,10 @@ class Model {
   }
   double capacityWithAllowedReplicaMoves(int res, const std::vector<uint8_t>& excludedReplicaMove) const;
   double clusterUtil(int res) const { return ops.util(cLoad, res); }
+  double potNwOut(int b) const { return ops.util(bPot[b], R_NW_OUT); }   // potentialLeadershipLoadFor(b) NW_OUT
+  double leadNwIn(int b) const { return ops.util(bLnw[b], R_NW_IN); }    // leadershipLoadForNwResources NW_IN
+  double pLeadNwOut(int p) const { return ru(pLeader[p], R_NW_OUT); }    // partition(tp).leader() NW_OUT
+  int numLeaderReplicas() const { return P; }
 
   // ---- mutations (record into the action log, mark dirty rows)
   void relocateReplica(int p, int src, int dst);
@@ -207,6 +238,7 @@ class Model {
   // ---- sorted replica tracking (sorted-vector implementation of SortedReplicas)
   struct Spec {
     bool selLeaders = false, selFollowers = false, selImmigrants = false, selImmOrOffline = false;
+    bool selOffline = false;
     int selAboveRes = -1, selBelowRes = -1;
     double aboveLimit = 0, belowLimit = 0;
     bool prioOffline = false, prioImmigrants = false;
@@ -214,6 +246,7 @@ class Model {
     bool scoreReverse = false;
     bool operator==(const Spec& o) const {
       return selLeaders == o.selLeaders && selFollowers == o.selFollowers && selImmigrants == o.selImmigrants &&
+             selOffline == o.selOffline &&
              selImmOrOffline == o.selImmOrOffline && selAboveRes == o.selAboveRes && selBelowRes == o.selBelowRes &&
              aboveLimit == o.aboveLimit && belowLimit == o.belowLimit && prioOffline == o.prioOffline &&
              prioImmigrants == o.prioImmigrants && scoreRes == o.scoreRes && scoreReverse == o.scoreReverse;

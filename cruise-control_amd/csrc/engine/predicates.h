@@ -10,6 +10,13 @@
 //   isLoad{Above,Under}Balance…AfterChange        ResourceDistributionGoal.java:880-927
 //   isGettingMoreBalanced / isSwapViolating…      ResourceDistributionGoal.java:943-1037
 //   GoalUtils.legitMove                           GoalUtils.java:213-226
+//   RackAwareGoal / AbstractRackAwareGoal         RackAwareGoal.java:57-66, AbstractRackAwareGoal.java:76-117
+//   ReplicaCapacityGoal                           ReplicaCapacityGoal.java:69-82,165-168
+//   CapacityGoal (+ Disk/NwIn leadership ACCEPT)  CapacityGoal.java:75-133,431-475, DiskCapacityGoal.java:40-43
+//   PotentialNwOutGoal                            PotentialNwOutGoal.java:73-113,152-183
+//   TopicReplicaDistributionGoal                  TopicReplicaDistributionGoal.java:153-214,300-314
+//   LeaderReplicaDistributionGoal                 LeaderReplicaDistributionGoal.java:91-123
+//   LeaderBytesInDistributionGoal                 LeaderBytesInDistributionGoal.java:69-127,264-271
 // One broker per host (RandomCluster names hosts after brokers), so the host-resource branch equals the
 // broker branch bit for bit and is folded into it.
 #pragma once
@@ -27,8 +34,8 @@
 namespace ccmi {
 
 // V must provide: bu(b,res) bcap(b,res) nrep(b) alive(b) allowed(slot,b) ru(r,res) flags(r) rbroker(r)
-// rorig(r) rpart(r) and, for partition membership, hosts(p,b) — or pbegin(p) pend(p) pbroker(i) through
-// hostsPartition's generic form.
+// rorig(r) rpart(r) hosts(p,b), and for the goals that read them: rack(b) otherOnRack(p,self,rack) nlead(b)
+// pot(b) lnwin(b) pLeadNwOut(p) ptopic(p) tcount(t,b) tUpper(t) tLower(t).
 template <class V>
 CCMI_HD bool currentOffline(const V& v, int r) {
   const int orig = v.rorig(r), br = v.rbroker(r);
@@ -124,17 +131,117 @@ CCMI_HD int resAcceptSwap(const DevGoal& g, const V& v, int sr, int sb, int dr, 
   return resGettingMoreBalanced(g, v, sb, delta, db) ? 0 : 1;
 }
 
+// ---------------------------------------------------------------- RackAwareGoal
+// doesReplicaMoveViolateActionAcceptance: another broker of the partition sits on the destination's rack
+template <class V>
+CCMI_HD bool rackViolates(const V& v, int r, int dst) {
+  return v.otherOnRack(v.rpart(r), v.rbroker(r), v.rack(dst));
+}
+
+// ---------------------------------------------------------------- CapacityGoal
+// isUtilizationUnderLimitAfterAddingLoad (host == broker: the host check is the broker check negated)
+template <class V>
+CCMI_HD bool capUnderAfterAdding(const DevGoal& g, const V& v, int b, double u) {
+  return v.bu(b, g.resource) + u < v.bcap(b, g.resource) * g.capThr;
+}
+
+// ---------------------------------------------------------------- PotentialNwOutGoal
+template <class V>
+CCMI_HD bool potSelfSatisfiedMove(const DevGoal& g, const V& v, int action, int r, int dst) {
+  if (g.fixOffline && currentOffline(v, r)) return action == DA_MOVE;
+  const double destCap = v.bcap(dst, 2) * g.capThr;
+  return destCap >= v.pot(dst) + v.pLeadNwOut(v.rpart(r));
+}
+template <class V>
+CCMI_HD bool potAcceptMove(const DevGoal& g, const V& v, int action, int r, int src, int dst) {
+  if (action == DA_LEADERSHIP) return true;
+  if (potSelfSatisfiedMove(g, v, action, r, dst)) return true;
+  const double du = v.pot(dst), su = v.pot(src);
+  const double mx = du >= su ? (du == su && du == 0.0 ? (__builtin_signbit(du) ? su : du) : du) : su;  // Math.max
+  return du + v.pLeadNwOut(v.rpart(r)) <= mx;
+}
+
+// ---------------------------------------------------------------- TopicReplicaDistributionGoal
+template <class V>
+CCMI_HD bool topicUnderUpperAfterAdd(const V& v, int t, int b) {
+  return v.tcount(t, b) + 1 <= (v.alive(b) ? v.tUpper(t) : 0);
+}
+template <class V>
+CCMI_HD bool topicAboveLowerAfterRemove(const V& v, int t, int b) {
+  return v.tcount(t, b) - 1 >= (v.alive(b) ? v.tLower(t) : 0);
+}
+template <class V>
+CCMI_HD bool topicAcceptMove(const DevGoal& g, const V& v, int action, int r, int src, int dst) {
+  if (action == DA_LEADERSHIP) return true;
+  const int t = v.ptopic(v.rpart(r));
+  return topicUnderUpperAfterAdd(v, t, dst) && (!v.allowed(g.allowedSlot, src) || topicAboveLowerAfterRemove(v, t, src));
+}
+
+// ---------------------------------------------------------------- LeaderReplicaDistributionGoal
+template <class V>
+CCMI_HD bool leaderMovementSatisfiable(const DevGoal& g, const V& v, int src, int dst) {
+  if (!(v.nlead(dst) + 1 <= (v.alive(dst) ? g.upper : 0))) return false;
+  if (!v.allowed(g.allowedSlot, src)) return true;
+  return v.nlead(src) - 1 >= (v.alive(src) ? g.lower : 0);
+}
+template <class V>
+CCMI_HD bool leadAcceptMove(const DevGoal& g, const V& v, int action, int r, int src, int dst) {
+  if (action == DA_MOVE && !(v.flags(r) & RF_LEADER)) return true;
+  return leaderMovementSatisfiable(g, v, src, dst);
+}
+
+// ---------------------------------------------------------------- LeaderBytesInDistributionGoal
+template <class V>
+CCMI_HD double lbiThreshold(const DevGoal& g, const V& v, int b) {
+  const double low = g.lbiLowUtil * v.bcap(b, 1);
+  const double m = g.lbiMean * g.lbiBalance;
+  return m >= low ? (m == low && m == 0.0 ? (__builtin_signbit(m) ? low : m) : m) : low;  // Math.max
+}
+template <class V>
+CCMI_HD bool lbiAcceptMove(const DevGoal& g, const V& v, int action, int r, int dst) {
+  if (!(v.flags(r) & RF_LEADER)) return true;  // replica move of a follower (leadership moves start at a leader)
+  const double newDest = v.lnwin(dst) + v.ru(r, 1);
+  return !(newDest > lbiThreshold(g, v, dst));
+}
+
 // ---------------------------------------------------------------- dispatch
 template <class V>
 CCMI_HD bool goalAcceptMove(const DevGoal& g, const V& v, int action, int r, int src, int dst) {
-  if (g.kind == DG_REPLICA_DISTRIBUTION) return rdAccept(g, v, action, src, dst);
-  return resAcceptMove(g, v, action, r, src, dst);
+  switch (g.kind) {
+    case DG_REPLICA_DISTRIBUTION: return rdAccept(g, v, action, src, dst);
+    case DG_RESOURCE_DISTRIBUTION: return resAcceptMove(g, v, action, r, src, dst);
+    case DG_RACK_AWARE: return action == DA_LEADERSHIP || !rackViolates(v, r, dst);
+    case DG_REPLICA_CAPACITY: return action == DA_LEADERSHIP || (int64_t)v.nrep(dst) < g.maxReplicas;
+    case DG_CAPACITY:
+      if (action == DA_LEADERSHIP && (g.resource == 3 /*DISK*/ || g.resource == 1 /*NW_IN*/)) return true;
+      return capUnderAfterAdding(g, v, dst, v.ru(r, g.resource));
+    case DG_POTENTIAL_NW_OUT: return potAcceptMove(g, v, action, r, src, dst);
+    case DG_TOPIC_REPLICA_DISTRIBUTION: return topicAcceptMove(g, v, action, r, src, dst);
+    case DG_LEADER_REPLICA_DISTRIBUTION: return leadAcceptMove(g, v, action, r, src, dst);
+    case DG_LEADER_BYTES_IN: return lbiAcceptMove(g, v, action, r, dst);
+    default: return true;  // DG_ACCEPT_ALL
+  }
 }
 template <class V>
 CCMI_HD bool goalSelfSatisfiedMove(const DevGoal& g, const V& v, int action, int r, int src, int dst) {
-  if (g.kind == DG_REPLICA_DISTRIBUTION) {
-    if (g.fixOffline && currentOffline(v, r)) return true;
-    return rdAccept(g, v, action, src, dst);
+  switch (g.kind) {
+    case DG_REPLICA_DISTRIBUTION:
+      if (g.fixOffline && currentOffline(v, r)) return true;
+      return rdAccept(g, v, action, src, dst);
+    case DG_RESOURCE_DISTRIBUTION: break;
+    case DG_RACK_AWARE: return true;
+    case DG_ACCEPT_ALL: return action == DA_MOVE;  // MinTopicLeadersPerBrokerGoal moves offline replicas only
+    case DG_REPLICA_CAPACITY: return (int64_t)v.nrep(dst) < g.maxReplicas;
+    case DG_CAPACITY: return capUnderAfterAdding(g, v, dst, v.ru(r, g.resource));
+    case DG_POTENTIAL_NW_OUT: return potSelfSatisfiedMove(g, v, action, r, dst);
+    case DG_TOPIC_REPLICA_DISTRIBUTION:
+      if (g.fixOffline && currentOffline(v, r)) return action == DA_MOVE;
+      return topicAcceptMove(g, v, DA_MOVE, r, src, dst);
+    case DG_LEADER_REPLICA_DISTRIBUTION:
+      if (g.fixOffline && currentOffline(v, r)) return true;
+      return leadAcceptMove(g, v, action, r, src, dst);
+    case DG_LEADER_BYTES_IN: return lbiAcceptMove(g, v, action, r, dst);
+    default: return true;
   }
   if (g.fixOffline && currentOffline(v, r)) return action == DA_MOVE;
   const double ru = v.ru(r, g.resource);
@@ -143,8 +250,56 @@ CCMI_HD bool goalSelfSatisfiedMove(const DevGoal& g, const V& v, int action, int
 // returns 0 ACCEPT, 1 REPLICA_REJECT, 2 BROKER_REJECT
 template <class V>
 CCMI_HD int goalAcceptSwap(const DevGoal& g, const V& v, int sr, int sb, int dr, int db) {
-  if (g.kind == DG_REPLICA_DISTRIBUTION) return 0;
-  return resAcceptSwap(g, v, sr, sb, dr, db);
+  switch (g.kind) {
+    case DG_RESOURCE_DISTRIBUTION: return resAcceptSwap(g, v, sr, sb, dr, db);
+    case DG_RACK_AWARE:
+      if (rackViolates(v, sr, db)) return 2;
+      return rackViolates(v, dr, sb) ? 1 : 0;
+    case DG_CAPACITY: {
+      const double su = v.ru(sr, g.resource), du = v.ru(dr, g.resource);
+      const double delta = du - su;
+      return (delta > 0 ? capUnderAfterAdding(g, v, sb, delta) : capUnderAfterAdding(g, v, db, -delta)) ? 0 : 1;
+    }
+    case DG_POTENTIAL_NW_OUT: {
+      // selfSatisfied (swap form) first, then the max-utilization bound
+      const double sU = v.pLeadNwOut(v.rpart(sr)), dU = v.pLeadNwOut(v.rpart(dr));
+      const double destU = v.pot(db), srcU = v.pot(sb);
+      bool self;
+      if (g.fixOffline && currentOffline(v, sr)) {
+        self = false;
+      } else {
+        const double destCap = v.bcap(db, 2) * g.capThr, srcCap = v.bcap(sb, 2) * g.capThr;
+        self = !(destCap < destU + sU - dU) && srcCap >= srcU + dU - sU;
+      }
+      if (self) return 0;
+      const double mx = destU >= srcU ? (destU == srcU && destU == 0.0 ? (__builtin_signbit(destU) ? srcU : destU) : destU)
+                                      : srcU;
+      if (srcU + dU - sU > mx) return 1;
+      return destU + sU - dU <= mx ? 0 : 1;
+    }
+    case DG_TOPIC_REPLICA_DISTRIBUTION: {
+      const int st = v.ptopic(v.rpart(sr)), dt = v.ptopic(v.rpart(dr));
+      if (st == dt) return 0;
+      const bool s2d = topicUnderUpperAfterAdd(v, st, db) && topicAboveLowerAfterRemove(v, st, sb);
+      return (s2d && topicUnderUpperAfterAdd(v, dt, sb) && topicAboveLowerAfterRemove(v, dt, db)) ? 0 : 1;
+    }
+    case DG_LEADER_REPLICA_DISTRIBUTION: {
+      const bool sl = (v.flags(sr) & RF_LEADER) != 0, dl = (v.flags(dr) & RF_LEADER) != 0;
+      if (sl && !dl) return leaderMovementSatisfiable(g, v, sb, db) ? 0 : 1;
+      if (!sl && dl) return leaderMovementSatisfiable(g, v, db, sb) ? 0 : 1;
+      return 0;
+    }
+    case DG_LEADER_BYTES_IN: {
+      const bool sl = (v.flags(sr) & RF_LEADER) != 0, dl = (v.flags(dr) & RF_LEADER) != 0;
+      if (!sl && !dl) return 0;
+      const double srU = v.ru(sr, 1), drU = v.ru(dr, 1);
+      const double newDest = v.lnwin(db) + srU - drU;
+      const double newSrc = v.lnwin(sb) + drU - srU;
+      if (newSrc > lbiThreshold(g, v, sb)) return 1;
+      return !(newDest > lbiThreshold(g, v, db)) ? 0 : 1;
+    }
+    default: return 0;  // ReplicaDistribution, ReplicaCapacity, MinTopicLeaders accept swaps
+  }
 }
 template <class V>
 CCMI_HD bool goalSelfSatisfiedSwap(const DevGoal& g, const V& v, int sr, int sb, int dr, int db) {

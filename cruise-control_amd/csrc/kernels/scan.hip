@@ -46,6 +46,23 @@ struct DevView {
     for (int i = pbegin(p); i < pend(p); ++i) has |= (pbroker(i) == b);
     return has;
   }
+  __device__ __forceinline__ int rack(int b) const { return t.bRack[b]; }
+  __device__ __forceinline__ bool otherOnRack(int p, int self, int rk) const {
+    bool any = false;
+    for (int i = pbegin(p); i < pend(p); ++i) {
+      const int x = pbroker(i);
+      any |= (x != self) && (t.bRack[x] == rk);
+    }
+    return any;
+  }
+  __device__ __forceinline__ int nlead(int b) const { return t.bNlead[b]; }
+  __device__ __forceinline__ double pot(int b) const { return t.bPot[b]; }
+  __device__ __forceinline__ double lnwin(int b) const { return t.bLeadNwIn[b]; }
+  __device__ __forceinline__ double pLeadNwOut(int p) const { return t.pLeadNwOut[p]; }
+  __device__ __forceinline__ int ptopic(int p) const { return t.pTopic[p]; }
+  __device__ __forceinline__ int tcount(int tp, int b) const { return t.topicCount[(size_t)tp * t.ldB + b]; }
+  __device__ __forceinline__ int tUpper(int tp) const { return t.tUpper[tp]; }
+  __device__ __forceinline__ int tLower(int tp) const { return t.tLower[tp]; }
 };
 
 // Row updates a cross/pair scan applies itself (instead of a separate launch): every workgroup stages the
@@ -94,6 +111,7 @@ __device__ __forceinline__ void applyRowsBlock(const MutTables& M, int B, int R,
     M.bNrep[x.b] = x.nrep;
     M.bNlead[x.b] = x.nlead;
     M.bPot[x.b] = x.potNwOut;
+    M.bLeadNwIn[x.b] = x.leadNwIn;
     M.bAlive[x.b] = (uint8_t)x.alive;
   }
   for (int i = first; i < nr; i += stride) {
@@ -107,6 +125,7 @@ __device__ __forceinline__ void applyRowsBlock(const MutTables& M, int B, int R,
     const PartitionRow& x = prows[i];
     const int o = pOff[x.p];
     for (int k = 0; k < x.n; ++k) M.pBrokers[o + k] = x.brokers[k];
+    M.pLeadNwOut[x.p] = x.leadNwOut;
   }
   for (int i = first; i < nt; i += stride) {
     const TopicCountDelta d = tdel[i];
@@ -137,6 +156,8 @@ __device__ __forceinline__ void overlayBegin(OverlayLds& ov, const UpdateList& U
 // its partition's brokers; destination side: one broker record), so the predicate conjunction runs on
 // registers instead of a chain of control-dependent loads. Accessors answer only for the ids a move
 // predicate asks about (the replica r, its source/original broker, the destination, r's partition).
+// Operands only some goals read (racks, potential NW_OUT, leader counts, leader bytes-in, topic counts) are
+// loaded when the program's `needs` mask asks for them (a wave-uniform branch).
 struct PreView {
   int r, src, orig, p, rflags, dst, snrep, dnrep;
   uint32_t aliveBits;   // bit 0 src, bit 1 orig, bit 2 dst (values, never addressed: keeps the view in VGPRs)
@@ -144,6 +165,10 @@ struct PreView {
   int pb0, pb1, pb2, pb3, pb4, pb5, pb6, pb7;
   double ru0, ru1, ru2, ru3, sbu0, sbu1, sbu2, sbu3, scap0, scap1, scap2, scap3;
   double dbu0, dbu1, dbu2, dbu3, dcap0, dcap1, dcap2, dcap3;
+  // optional operands
+  int drack, prk0, prk1, prk2, prk3, prk4, prk5, prk6, prk7;
+  double spot, dpot, plno, slbi, dlbi;
+  int snlead, dnlead, topic, stc, dtc, tup, tlo;
 
   static __device__ __forceinline__ double sel(int k, double a, double b, double c, double d) {
     return k == 0 ? a : (k == 1 ? b : (k == 2 ? c : d));
@@ -181,6 +206,7 @@ struct PreView {
       pb5 = pn > 5 ? x.brokers[5] : -1;
       pb6 = pn > 6 ? x.brokers[6] : -1;
       pb7 = pn > 7 ? x.brokers[7] : -1;
+      plno = x.leadNwOut;
     } else {
       const int o0 = t.pOff[p], pn = t.pOff[p + 1] - o0;
       const int32_t* q = t.pBrokers + o0;
@@ -192,6 +218,7 @@ struct PreView {
       pb5 = pn > 5 ? q[5] : -1;
       pb6 = pn > 6 ? q[6] : -1;
       pb7 = pn > 7 ? q[7] : -1;
+      plno = (prog.needs & NEED_POT) ? t.pLeadNwOut[p] : 0.0;
     }
     const int oi = ov.broker(orig);
     const bool aOrig = oi >= 0 ? ov.b[oi].alive != 0 : t.bAlive[orig] != 0;
@@ -205,6 +232,9 @@ struct PreView {
       sbu1 = x.util[1];
       sbu2 = x.util[2];
       sbu3 = x.util[3];
+      snlead = x.nlead;
+      spot = x.potNwOut;
+      slbi = x.leadNwIn;
     } else {
       aSrc = t.bAlive[src] != 0;
       snrep = t.bNrep[src];
@@ -212,6 +242,9 @@ struct PreView {
       sbu1 = t.bUtil[(size_t)t.B + src];
       sbu2 = t.bUtil[(size_t)2 * t.B + src];
       sbu3 = t.bUtil[(size_t)3 * t.B + src];
+      snlead = (prog.needs & NEED_LEAD) ? t.bNlead[src] : 0;
+      spot = (prog.needs & NEED_POT) ? t.bPot[src] : 0.0;
+      slbi = (prog.needs & NEED_LBI) ? t.bLeadNwIn[src] : 0.0;
     }
     aliveBits = (aSrc ? 1u : 0u) | (aOrig ? 2u : 0u);
     scap0 = t.bCap[src];
@@ -223,8 +256,24 @@ struct PreView {
       const int slot = prog.goals[i].allowedSlot;
       srcAllowed |= (t.allowed[(size_t)slot * t.B + src] ? 1u : 0u) << slot;
     }
+    if (prog.needs & NEED_RACK) {
+      prk0 = pb0 >= 0 ? t.bRack[pb0] : -1;
+      prk1 = pb1 >= 0 ? t.bRack[pb1] : -1;
+      prk2 = pb2 >= 0 ? t.bRack[pb2] : -1;
+      prk3 = pb3 >= 0 ? t.bRack[pb3] : -1;
+      prk4 = pb4 >= 0 ? t.bRack[pb4] : -1;
+      prk5 = pb5 >= 0 ? t.bRack[pb5] : -1;
+      prk6 = pb6 >= 0 ? t.bRack[pb6] : -1;
+      prk7 = pb7 >= 0 ? t.bRack[pb7] : -1;
+    }
+    if (prog.needs & NEED_TOPIC) {
+      topic = t.pTopic[p];
+      tup = t.tUpper[topic];
+      tlo = t.tLower[topic];
+      stc = t.topicCount[(size_t)topic * t.ldB + src];
+    }
   }
-  __device__ __forceinline__ void loadDst(const DevTables& t, int d, const OverlayLds& ov) {
+  __device__ __forceinline__ void loadDst(const DevTables& t, const DevProgram& prog, int d, const OverlayLds& ov) {
     dst = d;
     const int di = ov.broker(d);
     bool aDst;
@@ -236,6 +285,9 @@ struct PreView {
       dbu1 = x.util[1];
       dbu2 = x.util[2];
       dbu3 = x.util[3];
+      dnlead = x.nlead;
+      dpot = x.potNwOut;
+      dlbi = x.leadNwIn;
     } else {
       aDst = t.bAlive[d] != 0;
       dnrep = t.bNrep[d];
@@ -243,12 +295,17 @@ struct PreView {
       dbu1 = t.bUtil[(size_t)t.B + d];
       dbu2 = t.bUtil[(size_t)2 * t.B + d];
       dbu3 = t.bUtil[(size_t)3 * t.B + d];
+      dnlead = (prog.needs & NEED_LEAD) ? t.bNlead[d] : 0;
+      dpot = (prog.needs & NEED_POT) ? t.bPot[d] : 0.0;
+      dlbi = (prog.needs & NEED_LBI) ? t.bLeadNwIn[d] : 0.0;
     }
     aliveBits = (aliveBits & 3u) | (aDst ? 4u : 0u);
     dcap0 = t.bCap[d];
     dcap1 = t.bCap[(size_t)t.B + d];
     dcap2 = t.bCap[(size_t)2 * t.B + d];
     dcap3 = t.bCap[(size_t)3 * t.B + d];
+    if (prog.needs & NEED_RACK) drack = t.bRack[d];
+    if (prog.needs & NEED_TOPIC) dtc = t.topicCount[(size_t)topic * t.ldB + d];
   }
   __device__ __forceinline__ double bu(int b, int k) const {
     return b == dst ? sel(k, dbu0, dbu1, dbu2, dbu3) : sel(k, sbu0, sbu1, sbu2, sbu3);
@@ -269,6 +326,46 @@ struct PreView {
   __device__ __forceinline__ int rpart(int) const { return p; }
   __device__ __forceinline__ bool hosts(int /*p*/, int b) const {
     return (pb0 == b) | (pb1 == b) | (pb2 == b) | (pb3 == b) | (pb4 == b) | (pb5 == b) | (pb6 == b) | (pb7 == b);
+  }
+  __device__ __forceinline__ int rack(int /*b == dst*/) const { return drack; }
+  __device__ __forceinline__ bool otherOnRack(int /*p*/, int self, int rk) const {
+    return (pb0 >= 0 && pb0 != self && prk0 == rk) | (pb1 >= 0 && pb1 != self && prk1 == rk) |
+           (pb2 >= 0 && pb2 != self && prk2 == rk) | (pb3 >= 0 && pb3 != self && prk3 == rk) |
+           (pb4 >= 0 && pb4 != self && prk4 == rk) | (pb5 >= 0 && pb5 != self && prk5 == rk) |
+           (pb6 >= 0 && pb6 != self && prk6 == rk) | (pb7 >= 0 && pb7 != self && prk7 == rk);
+  }
+  __device__ __forceinline__ int nlead(int b) const { return b == dst ? dnlead : snlead; }
+  __device__ __forceinline__ double pot(int b) const { return b == dst ? dpot : spot; }
+  __device__ __forceinline__ double lnwin(int b) const { return b == dst ? dlbi : slbi; }
+  __device__ __forceinline__ double pLeadNwOut(int) const { return plno; }
+  __device__ __forceinline__ int ptopic(int) const { return topic; }
+  __device__ __forceinline__ int tcount(int, int b) const { return b == dst ? dtc : stc; }
+  __device__ __forceinline__ int tUpper(int) const { return tup; }
+  __device__ __forceinline__ int tLower(int) const { return tlo; }
+
+  // RackAwareGoal.rackAwareEligibleBrokers: the destination's rack is not in the partition's rack list with
+  // one occurrence of the replica's own rack removed (RackAwareGoal.java:193-211). Needs NEED_RACK.
+  __device__ __forceinline__ bool rackEligible() const {
+    int srk = -1;
+    if (pb0 == src) srk = prk0;
+    else if (pb1 == src) srk = prk1;
+    else if (pb2 == src) srk = prk2;
+    else if (pb3 == src) srk = prk3;
+    else if (pb4 == src) srk = prk4;
+    else if (pb5 == src) srk = prk5;
+    else if (pb6 == src) srk = prk6;
+    else if (pb7 == src) srk = prk7;
+    int cnt = 0;
+    cnt += (pb0 >= 0 && prk0 == drack);
+    cnt += (pb1 >= 0 && prk1 == drack);
+    cnt += (pb2 >= 0 && prk2 == drack);
+    cnt += (pb3 >= 0 && prk3 == drack);
+    cnt += (pb4 >= 0 && prk4 == drack);
+    cnt += (pb5 >= 0 && prk5 == drack);
+    cnt += (pb6 >= 0 && prk6 == drack);
+    cnt += (pb7 >= 0 && prk7 == drack);
+    if (srk == drack) cnt -= 1;
+    return cnt == 0;
   }
 };
 
@@ -346,8 +443,9 @@ __global__ __launch_bounds__(kBlock) void scan_cross(DevTables T, MutTables Mt, 
       const uint32_t j = q - k * (uint32_t)N;
       PreView v;
       v.loadRow(T, prog, reps[k], ov);
-      v.loadDst(T, cands[j], ov);
-      if (moveCandidateAccepted(prog, v, v.r, v.dst)) local = q;
+      v.loadDst(T, prog, cands[j], ov);
+      const bool inList = prog.filter != FILTER_RACK_AWARE || v.rackEligible();
+      if (inList && moveCandidateAccepted(prog, v, v.r, v.dst)) local = q;
     }
     const unsigned long long m = blockMin(local);
     if (m != kNone) {
@@ -442,7 +540,7 @@ __global__ __launch_bounds__(kBlock) void scan_pairs(DevTables T, MutTables Mt, 
     if (q < n) {
       PreView v;
       v.loadRow(T, prog, pr[q], ov);
-      v.loadDst(T, pb[q], ov);
+      v.loadDst(T, prog, pb[q], ov);
       if (moveCandidateAccepted(prog, v, v.r, v.dst)) local = (unsigned long long)q;
     }
     const unsigned long long m = blockMin(local);
@@ -454,45 +552,17 @@ __global__ __launch_bounds__(kBlock) void scan_pairs(DevTables T, MutTables Mt, 
   publishLast(result, done, mail, seq);
 }
 
-__global__ __launch_bounds__(256) void prep(double* bUtil, int32_t* bNrep, int32_t* bNlead, double* bPot,
-                                            uint8_t* bAlive, int B, const BrokerRow* __restrict__ brows, int nb,
-                                            double* rUtil, int32_t* rBroker, uint8_t* rFlags, int R,
+__global__ __launch_bounds__(256) void prep(MutTables M, int B, int R, const int32_t* __restrict__ pOff,
+                                            const BrokerRow* __restrict__ brows, int nb,
                                             const ReplicaRow* __restrict__ rrows, int nr,
-                                            const int32_t* __restrict__ pOff, int32_t* pBrokers,
-                                            const PartitionRow* __restrict__ prows, int np, int32_t* topicCount,
-                                            int ldB, const TopicCountDelta* __restrict__ tdel, int nt,
+                                            const PartitionRow* __restrict__ prows, int np,
+                                            const TopicCountDelta* __restrict__ tdel, int nt,
                                             const int4* __restrict__ req, int4* __restrict__ dReq, int nReq4,
                                             unsigned long long* __restrict__ result, unsigned int* __restrict__ done) {
   const int stride = gridDim.x * blockDim.x;
-  for (int i = blockIdx.x * blockDim.x + threadIdx.x;; i += stride) {
-    if (i >= nb && i >= nr && i >= np && i >= nt && i >= nReq4) break;
-    if (i < nb) {
-      const BrokerRow x = brows[i];
-#pragma unroll
-      for (int k = 0; k < 4; ++k) bUtil[(size_t)k * B + x.b] = x.util[k];
-      bNrep[x.b] = x.nrep;
-      bNlead[x.b] = x.nlead;
-      bPot[x.b] = x.potNwOut;
-      bAlive[x.b] = (uint8_t)x.alive;
-    }
-    if (i < nr) {
-      const ReplicaRow x = rrows[i];
-#pragma unroll
-      for (int k = 0; k < 4; ++k) rUtil[(size_t)k * R + x.r] = x.util[k];
-      rBroker[x.r] = x.broker;
-      rFlags[x.r] = (uint8_t)x.flags;
-    }
-    if (i < np) {
-      const PartitionRow x = prows[i];
-      const int o = pOff[x.p];
-      for (int k = 0; k < x.n; ++k) pBrokers[o + k] = x.brokers[k];
-    }
-    if (i < nt) {
-      const TopicCountDelta d = tdel[i];
-      atomicAdd(&topicCount[(size_t)d.topic * ldB + d.broker], d.delta);
-    }
-    if (i < nReq4) dReq[i] = req[i];
-  }
+  const int first = blockIdx.x * blockDim.x + threadIdx.x;
+  applyRowsBlock(M, B, R, brows, nb, rrows, nr, pOff, prows, np, tdel, nt, first, stride);
+  for (int i = first; i < nReq4; i += stride) dReq[i] = req[i];
   if (blockIdx.x == 0 && threadIdx.x == 0 && result) {
     result[0] = kNone;
     result[1] = 0;
@@ -539,22 +609,17 @@ hipError_t launchScanPairs(const DevTables& T, const MutTables& M, const UpdateL
   return hipGetLastError();
 }
 
-hipError_t launchPrep(double* bUtil, int32_t* bNrep, int32_t* bNlead, double* bPot, uint8_t* bAlive, int B,
-                      const BrokerRow* brows, int nb, double* rUtil, int32_t* rBroker, uint8_t* rFlags, int R,
-                      const ReplicaRow* rrows, int nr, const int32_t* pOff, int32_t* pBrokers,
-                      const PartitionRow* prows, int np, int32_t* topicCount, int ldB, const TopicCountDelta* tdel,
-                      int nt, const int4* req, int4* dReq, int nReq4, unsigned long long* result, unsigned int* done,
-                      hipStream_t st) {
-  int n = nb;
-  if (nr > n) n = nr;
-  if (np > n) n = np;
-  if (nt > n) n = nt;
+hipError_t launchPrep(const MutTables& M, int B, int R, const int32_t* pOff, const UpdateList& U, const int4* req,
+                      int4* dReq, int nReq4, unsigned long long* result, unsigned int* done, hipStream_t st) {
+  int n = U.nb;
+  if (U.nr > n) n = U.nr;
+  if (U.np > n) n = U.np;
+  if (U.nt > n) n = U.nt;
   if (nReq4 > n) n = nReq4;
   if (n == 0 && !result) return hipSuccess;
   const unsigned blocks = gridFor((uint64_t)(n ? n : 1), 256);
-  hipLaunchKernelGGL(prep, dim3(blocks), dim3(256), 0, st, bUtil, bNrep, bNlead, bPot, bAlive, B, brows, nb, rUtil,
-                     rBroker, rFlags, R, rrows, nr, pOff, pBrokers, prows, np, topicCount, ldB, tdel, nt, req, dReq,
-                     nReq4, result, done);
+  hipLaunchKernelGGL(prep, dim3(blocks), dim3(256), 0, st, M, B, R, pOff, U.brows, U.nb, U.rrows, U.nr, U.prows, U.np,
+                     U.tdel, U.nt, req, dReq, nReq4, result, done);
   return hipGetLastError();
 }
 

@@ -275,8 +275,10 @@ bool CapacityGoal::swapAcceptable(ClusterModel& cm, int sr, int dr) const {
   return delta > 0 ? underLimitAfterAdding(cm, cm.replicas[sr].broker, delta)
                    : underLimitAfterAdding(cm, cm.replicas[dr].broker, -delta);
 }
-// CapacityGoal.actionAcceptance (:75-90)
+// CapacityGoal.actionAcceptance (:75-90); DiskCapacityGoal / NetworkInboundCapacityGoal accept every leadership
+// movement (DiskCapacityGoal.java:40-43, NetworkInboundCapacityGoal.java:40-43)
 Acceptance CapacityGoal::actionAcceptance(const BalancingAction& a, ClusterModel& cm) {
+  if (a.type == ActionType::LEADERSHIP_MOVEMENT && (resource_ == DISK || resource_ == NW_IN)) return Acceptance::ACCEPT;
   const int sr = cm.replicaOnBroker(a.partition, a.sourceBroker);
   switch (a.type) {
     case ActionType::INTER_BROKER_REPLICA_SWAP:

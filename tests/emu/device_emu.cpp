@@ -18,8 +18,9 @@ namespace ccmi {
 namespace {
 struct Emu {
   int B, R, P, T, ldB, G;
-  std::vector<double> bUtil, bCap, bPot, rUtil;
+  std::vector<double> bUtil, bCap, bPot, rUtil, bLeadNwIn, pLeadNwOut;
   std::vector<int32_t> bNrep, bNlead, rPart, rBroker, rOrig, pOff, pBrokers, topicCount, topicNrep;
+  std::vector<int32_t> bRack, pTopic, tUpper, tLower;
   std::vector<uint8_t> bAlive, allowed, rFlags;
 };
 struct View {
@@ -42,6 +43,33 @@ struct View {
     for (int i = pbegin(p); i < pend(p); ++i) has |= (pbroker(i) == b);
     return has;
   }
+  int rack(int b) const { return e.bRack[b]; }
+  bool otherOnRack(int p, int self, int rk) const {
+    for (int i = pbegin(p); i < pend(p); ++i)
+      if (pbroker(i) != self && e.bRack[pbroker(i)] == rk) return true;
+    return false;
+  }
+  int nlead(int b) const { return e.bNlead[b]; }
+  double pot(int b) const { return e.bPot[b]; }
+  double lnwin(int b) const { return e.bLeadNwIn[b]; }
+  double pLeadNwOut(int p) const { return e.pLeadNwOut[p]; }
+  int ptopic(int p) const { return e.pTopic[p]; }
+  int tcount(int t, int b) const { return e.topicCount[(size_t)t * e.ldB + b]; }
+  int tUpper(int t) const { return e.tUpper[t]; }
+  int tLower(int t) const { return e.tLower[t]; }
+  // RackAwareGoal.rackAwareEligibleBrokers membership for (replica r, destination d)
+  bool rackEligible(int r, int d) const {
+    std::vector<int> racks;
+    for (int i = pbegin(rpart(r)); i < pend(rpart(r)); ++i) racks.push_back(e.bRack[pbroker(i)]);
+    for (size_t i = 0; i < racks.size(); ++i)
+      if (racks[i] == e.bRack[rbroker(r)]) {
+        racks.erase(racks.begin() + i);
+        break;
+      }
+    for (int x : racks)
+      if (x == e.bRack[d]) return false;
+    return true;
+  }
 };
 Emu& E(void* st) { return *static_cast<Emu*>(st); }
 }  // namespace
@@ -61,8 +89,12 @@ Device::Device(int ordinal, int B, int R, int P, int T, int maxGoalSlots)
 Device::~Device() { delete static_cast<Emu*>(st_); }
 
 void Device::uploadStatic(const double* bCapRM, const int32_t* rPart, const int32_t* rOrig, const int32_t* pOff,
-                          const int32_t* topicNrep) {
+                          const int32_t* topicNrep, const int32_t* bRack, const int32_t* pTopic) {
   Emu& e = E(st_);
+  e.bRack.assign(bRack, bRack + B_);
+  e.pTopic.assign(pTopic, pTopic + P_);
+  e.tUpper.assign(T_, 0);
+  e.tLower.assign(T_, 0);
   e.bCap.assign(bCapRM, bCapRM + 4 * (size_t)B_);
   e.rPart.assign(rPart, rPart + R_);
   e.rOrig.assign(rOrig, rOrig + R_);
@@ -70,9 +102,12 @@ void Device::uploadStatic(const double* bCapRM, const int32_t* rPart, const int3
   e.topicNrep.assign(topicNrep, topicNrep + T_);
 }
 void Device::uploadDynamic(const double* bUtilRM, const int32_t* bNrep, const int32_t* bNlead, const double* bPot,
-                           const uint8_t* bAlive, const double* rUtilRM, const int32_t* rBroker, const uint8_t* rFlags,
-                           const int32_t* pBrokers, const int32_t* tc) {
+                           const double* bLeadNwIn, const uint8_t* bAlive, const double* rUtilRM,
+                           const int32_t* rBroker, const uint8_t* rFlags, const int32_t* pBrokers,
+                           const double* pLeadNwOut, const int32_t* tc) {
   Emu& e = E(st_);
+  e.bLeadNwIn.assign(bLeadNwIn, bLeadNwIn + B_);
+  e.pLeadNwOut.assign(pLeadNwOut, pLeadNwOut + P_);
   e.bUtil.assign(bUtilRM, bUtilRM + 4 * (size_t)B_);
   e.bNrep.assign(bNrep, bNrep + B_);
   e.bNlead.assign(bNlead, bNlead + B_);
@@ -87,6 +122,10 @@ void Device::uploadDynamic(const double* bUtilRM, const int32_t* bNrep, const in
 void Device::setAllowed(int slot, const uint8_t* a) {
   std::memcpy(E(st_).allowed.data() + (size_t)slot * B_, a, B_);
 }
+void Device::setTopicLimits(const int32_t* upper, const int32_t* lower) {
+  E(st_).tUpper.assign(upper, upper + T_);
+  E(st_).tLower.assign(lower, lower + T_);
+}
 
 void Device::flushOnly() {
   Emu& e = E(st_);
@@ -95,6 +134,7 @@ void Device::flushOnly() {
     e.bNrep[x.b] = x.nrep;
     e.bNlead[x.b] = x.nlead;
     e.bPot[x.b] = x.potNwOut;
+    e.bLeadNwIn[x.b] = x.leadNwIn;
     e.bAlive[x.b] = (uint8_t)x.alive;
   }
   for (const ReplicaRow& x : rrows) {
@@ -102,8 +142,10 @@ void Device::flushOnly() {
     e.rBroker[x.r] = x.broker;
     e.rFlags[x.r] = (uint8_t)x.flags;
   }
-  for (const PartitionRow& x : prows)
+  for (const PartitionRow& x : prows) {
     for (int k = 0; k < x.n; ++k) e.pBrokers[e.pOff[x.p] + k] = x.brokers[k];
+    e.pLeadNwOut[x.p] = x.leadNwOut;
+  }
   for (const TopicCountDelta& d : tdeltas) e.topicCount[(size_t)d.topic * ldB_ + d.broker] += d.delta;
   brows.clear();
   rrows.clear();
@@ -117,8 +159,10 @@ int64_t Device::scanCross(const DevProgram& prog, const int32_t* reps, int K, co
   perf.scanLaunches++;
   perf.scanPairs += (int64_t)K * N;
   for (int k = 0; k < K; ++k)
-    for (int j = 0; j < N; ++j)
+    for (int j = 0; j < N; ++j) {
+      if (prog.filter == FILTER_RACK_AWARE && !v.rackEligible(reps[k], cands[j])) continue;
       if (moveCandidateAccepted(prog, v, reps[k], cands[j])) return (int64_t)k * N + j;
+    }
   return -1;
 }
 

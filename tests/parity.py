@@ -17,24 +17,27 @@ def golden(name):
         return json.load(f)
 
 
-def constraint(balance):
+def constraint(balance, max_replicas=None):
     bc = ccmi.BalancingConstraint()
     if balance is not None:
         bc.set_resource_balance_percentage(balance)
         bc.set_capacity_threshold(0.8)
+    if max_replicas is not None:
+        bc.max_replicas_per_broker = max_replicas
     return bc
 
 
-def run_product(lib, props, goals, balance, device=0):
+def run_product(lib, props, goals, balance, device=0, max_replicas=None):
     buf = ccmi.RandomCluster.generate(lib, **props)
     cm = ccmi.ClusterModel.from_buffers(buf, device=device)
-    res = ccmi.GoalOptimizer(constraint(balance)).optimizations(cm, ccmi.goals_from_names(goals))
+    res = ccmi.GoalOptimizer(constraint(balance, max_replicas)).optimizations(cm, ccmi.goals_from_names(goals))
     return buf, cm, res
 
 
 def check_product_against_golden(lib, name):
     g = golden(name)
-    buf, cm, res = run_product(lib, g["props"], g["goals"], g["resource_balance_percentage"])
+    buf, cm, res = run_product(lib, g["props"], g["goals"], g["resource_balance_percentage"],
+                               max_replicas=g.get("max_replicas_per_broker"))
     check_against_golden(g, cm.actions(), cm.replica_distribution(), cm.leader_distribution(), res.goal_results,
                          res.goal_results[-1].stats)
     return cm, res
@@ -51,12 +54,26 @@ def _key(p):
     return p.partition, p.partition_size, p.old_leader, tuple(p.old_replicas), tuple(p.new_replicas)
 
 
-def check_product_against_oracle(lib, props, goals, balance=None, device=0):
+def check_product_against_oracle(lib, props, goals, balance=None, device=0, max_replicas=None):
     """Live parity: same flattened input into both; action log, final assignment/leaders, per-goal results and
-    every goal's post-optimization ClusterModelStats."""
-    buf, cm, res = run_product(lib, props, goals, balance, device)
+    every goal's post-optimization ClusterModelStats. A chain that fails (OptimizationFailureException for a hard
+    goal) must fail in both with the same exception and message after the same action log."""
+    buf = ccmi.RandomCluster.generate(lib, **props)
+    cm = ccmi.ClusterModel.from_buffers(buf, device=device)
     oc = OracleCluster.from_desc(buf.desc)
-    ores = oc.optimize(goals, constraint(balance))
+    perr = oerr = None
+    try:
+        res = ccmi.GoalOptimizer(constraint(balance, max_replicas)).optimizations(cm, ccmi.goals_from_names(goals))
+    except ccmi.CruiseControlError as e:
+        perr = e
+    try:
+        ores = oc.optimize(goals, constraint(balance, max_replicas))
+    except Exception as e:  # noqa: BLE001 - the oracle binding raises the same exception classes
+        oerr = e
+    if perr is not None or oerr is not None:
+        assert (type(perr).__name__, str(perr)) == (type(oerr).__name__, str(oerr))
+        assert cm.actions() == oc.actions()
+        return cm, None, oc
     pa, oa = cm.actions(), oc.actions()
     for i, (x, y) in enumerate(zip(pa, oa)):
         assert x == y, f"first action mismatch at {i}: {x} vs {y}"

@@ -2,13 +2,15 @@
 test-only sequential Device emulation (tests/emu) — same C ABI, same predicates as the gfx950 kernels."""
 import pytest
 
+import ccmi
 from parity import check_product_against_golden, check_product_against_oracle
+from test_oracle_kat import GOLDEN_CASES
 
-C1_GOALS = ["ReplicaDistributionGoal", "DiskUsageDistributionGoal", "NetworkInboundUsageDistributionGoal",
-            "NetworkOutboundUsageDistributionGoal", "CpuUsageDistributionGoal"]
+C1_GOALS = list(ccmi.C1_GOALS)
+DEFAULT_GOALS = list(ccmi.DEFAULT_GOALS)
 
 
-@pytest.mark.parametrize("name", ["small_20b", "dead_2of10", "rack_aware_dead", "c0", "c1"])
+@pytest.mark.parametrize("name", GOLDEN_CASES)
 def test_emu_matches_golden(emu_lib, oracle_lib, name):
     check_product_against_golden(emu_lib, name)
 
@@ -29,4 +31,28 @@ def test_emu_matches_oracle(emu_lib, oracle_lib, props, balance):
                                    ["DiskUsageDistributionGoal", "DiskUsageDistributionGoal"]])
 def test_emu_goal_subsets(emu_lib, oracle_lib, goals):
     check_product_against_oracle(emu_lib, dict(num_racks=5, num_brokers=20, num_replicas=6000, num_topics=300),
+                                 goals, 1.05)
+
+
+# RandomClusterTest (src/test/java/.../analyzer/RandomClusterTest.java:98-183) parameter rows, default goals,
+# balance 1.05 / capacity 0.8 / max.replicas.per.broker 1500 (3000 from the replica-count rows on), scaled down
+# in broker/replica counts so the CPU suite stays fast; the GPU suite runs the full-size rows.
+@pytest.mark.parametrize("props,max_replicas", [
+    (dict(num_racks=5, num_brokers=20, num_replicas=6000, num_topics=300), 1500),
+    (dict(num_racks=4, num_brokers=16, num_replicas=2400, num_topics=60, min_replication=4, max_replication=4), 3000),
+    (dict(num_racks=6, num_brokers=24, num_replicas=4800, num_topics=30, num_dead_brokers=3), 1500),
+    (dict(num_racks=3, num_brokers=9, num_replicas=2700, num_topics=60, num_dead_brokers=3, rack_aware=1), 1500),
+    (dict(num_racks=4, num_brokers=16, num_replicas=2400, num_topics=60), 140),  # ReplicaCapacityGoal must move
+])
+def test_emu_default_goals_match_oracle(emu_lib, oracle_lib, props, max_replicas):
+    check_product_against_oracle(emu_lib, props, DEFAULT_GOALS, 1.05, max_replicas=max_replicas)
+
+
+@pytest.mark.parametrize("goals", [DEFAULT_GOALS[::-1], DEFAULT_GOALS[7:] + DEFAULT_GOALS[:7],
+                                   ["LeaderBytesInDistributionGoal", "TopicReplicaDistributionGoal",
+                                    "LeaderReplicaDistributionGoal", "NetworkOutboundCapacityGoal", "RackAwareGoal"]])
+def test_emu_goal_orders(emu_lib, oracle_lib, goals):
+    """Other priority orders: every goal's actionAcceptance runs as a prior-goal predicate of the others (a hard goal
+    that cannot be satisfied must fail identically in both)."""
+    check_product_against_oracle(emu_lib, dict(num_racks=4, num_brokers=16, num_replicas=2400, num_topics=60),
                                  goals, 1.05)

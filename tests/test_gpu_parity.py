@@ -5,14 +5,15 @@ import pytest
 import ccmi
 from oracle_binding import OracleCluster
 from parity import check_product_against_golden, check_product_against_oracle, compare_stats, constraint
+from test_oracle_kat import GOLDEN_CASES
 
 pytestmark = pytest.mark.gpu
 
-C1_GOALS = ["ReplicaDistributionGoal", "DiskUsageDistributionGoal", "NetworkInboundUsageDistributionGoal",
-            "NetworkOutboundUsageDistributionGoal", "CpuUsageDistributionGoal"]
+C1_GOALS = list(ccmi.C1_GOALS)
+DEFAULT_GOALS = list(ccmi.DEFAULT_GOALS)
 
 
-@pytest.mark.parametrize("name", ["small_20b", "dead_2of10", "rack_aware_dead", "c0", "c1"])
+@pytest.mark.parametrize("name", GOLDEN_CASES)
 def test_gpu_matches_golden(gpu_lib, oracle_lib, name):
     cm, res = check_product_against_golden(gpu_lib, name)
     # the device path ran (no host fallback exists; this guards the counters the bench relies on)
@@ -30,6 +31,31 @@ def test_gpu_matches_golden(gpu_lib, oracle_lib, name):
 ])
 def test_gpu_matches_oracle(gpu_lib, oracle_lib, props, balance):
     check_product_against_oracle(gpu_lib, props, C1_GOALS, balance)
+
+
+# RandomClusterTest (src/test/java/.../analyzer/RandomClusterTest.java:139-183) rows on TestConstants.BASE_PROPERTIES
+# with the default goal list: broker count 80/140, replica count 65006..75008 (max replicas 3000), topic count
+# 7000/8000, replication factor 4/5.
+@pytest.mark.parametrize("props,max_replicas", [
+    (dict(num_brokers=80), 1500),
+    (dict(num_brokers=140), 1500),
+    (dict(num_replicas=65006), 3000),
+    (dict(num_replicas=75008), 3000),
+    (dict(num_topics=7000), 3000),
+    (dict(num_replicas=50000, min_replication=4, max_replication=4), 3000),
+    (dict(num_replicas=50000 - (50000 % 5), min_replication=5, max_replication=5), 3000),
+    (dict(num_dead_brokers=5, rack_aware=1, leader_in_first_position=1), 3000),
+])
+def test_gpu_random_cluster_default_goals(gpu_lib, oracle_lib, props, max_replicas):
+    check_product_against_oracle(gpu_lib, props, DEFAULT_GOALS, 1.05, max_replicas=max_replicas)
+
+
+@pytest.mark.parametrize("goals", [DEFAULT_GOALS[::-1], DEFAULT_GOALS[7:] + DEFAULT_GOALS[:7],
+                                   ["LeaderBytesInDistributionGoal", "TopicReplicaDistributionGoal",
+                                    "LeaderReplicaDistributionGoal", "NetworkOutboundCapacityGoal", "RackAwareGoal"]])
+def test_gpu_goal_orders(gpu_lib, oracle_lib, goals):
+    check_product_against_oracle(gpu_lib, dict(num_racks=4, num_brokers=16, num_replicas=2400, num_topics=60),
+                                 goals, 1.05)
 
 
 @pytest.mark.parametrize("goals", [["CpuUsageDistributionGoal"],

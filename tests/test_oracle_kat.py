@@ -102,6 +102,8 @@ def _constraint(g):
     if g["resource_balance_percentage"] is not None:
         bc.set_resource_balance_percentage(g["resource_balance_percentage"])
         bc.set_capacity_threshold(0.8)
+    if g.get("max_replicas_per_broker") is not None:
+        bc.max_replicas_per_broker = g["max_replicas_per_broker"]
     return bc
 
 
@@ -123,7 +125,11 @@ def check_against_golden(g, actions, replica_dist, leader_dist, goal_results, fi
             assert x == pytest.approx(y, rel=rel, abs=1e-12), k
 
 
-@pytest.mark.parametrize("name", ["small_20b", "dead_2of10", "rack_aware_dead", "c0", "c1"])
+GOLDEN_CASES = ["small_20b", "dead_2of10", "rack_aware_dead", "c0", "c1", "small_20b_default", "dead_3of24_default",
+                "rack_aware_dead_default", "c0_default"]
+
+
+@pytest.mark.parametrize("name", GOLDEN_CASES)
 def test_oracle_matches_golden(oracle_lib, name):
     g = _golden(name)
     oc = OracleCluster.random(**g["props"])

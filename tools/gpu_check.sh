@@ -1,7 +1,7 @@
 #!/bin/bash
 # One GPU-box pass: smoke, GPU parity tests, bench, optional rocprofv3 kernel-trace summary and PMC passes.
 # Every GPU step has its own time limit; a crash/abort/timeout (anything but pass/fail) stops the script.
-#   env: PYTEST_ARGS, BENCH_ARGS, PROFILE=1, PMC=1, C2=1, SKIP_TESTS=1
+#   env: PYTEST_ARGS, BENCH_ARGS, PROFILE=1, PMC=1, C2=1, SKIP_TESTS=1, SKIP_BENCH=1, PROBE=<workload>
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out
 step() {  # step <name> <seconds> <cmd...>
@@ -17,9 +17,14 @@ step() {  # step <name> <seconds> <cmd...>
 make -C cruise-control_amd -j16 > gpurun_out/make.log 2>&1 && make -C oracle -j16 >> gpurun_out/make.log 2>&1 || exit 1
 if [ -z "${SKIP_TESTS:-}" ]; then
   step smoke 400 python -c "import __graft_entry__ as g; g.smoke()"
-  step pytest_gpu 900 python -m pytest tests -m gpu -x -q ${PYTEST_ARGS:-}
+  step pytest_gpu 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread ${PYTEST_ARGS:-}
 fi
-step bench 600 python bench.py ${BENCH_ARGS:-}
+if [ -n "${PROBE:-}" ]; then
+  step probe 900 python -u tools/probe.py --workload "$PROBE"
+fi
+if [ -z "${SKIP_BENCH:-}" ]; then
+  step bench 600 python bench.py ${BENCH_ARGS:-}
+fi
 if [ -n "${PROFILE:-}" ]; then
   step rocprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o bench -- \
     python3 bench.py --no-cpu-baseline --steps 2 --warmup 1

@@ -1,0 +1,30 @@
+"""One optimization of a BASELINE workload with per-goal wall time, candidates and device launches (GPU box)."""
+import argparse
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "cruise-control_amd"))
+sys.path.insert(0, REPO)
+import ccmi  # noqa: E402
+from bench import WORKLOADS  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--workload", default="c2")
+ap.add_argument("--goals", type=int, default=16)
+a = ap.parse_args()
+props, goals, name = WORKLOADS[a.workload]
+lib = ccmi.Library.get()
+t0 = time.time()
+buf = ccmi.RandomCluster.generate(lib, **props)
+t1 = time.time()
+cm = ccmi.ClusterModel.from_buffers(buf, device=0)
+t2 = time.time()
+print(f"{name}: generate {t1 - t0:.2f}s, session {t2 - t1:.2f}s", flush=True)
+res = ccmi.GoalOptimizer(ccmi.BalancingConstraint()).optimizations(cm, ccmi.goals_from_names(goals[:a.goals]))
+t3 = time.time()
+for g in res.goal_results:
+    print(f"  {g.name:40s} ok={g.succeeded} {g.seconds:8.3f}s cand={g.candidates:>12d} act={g.actions:>7d} "
+          f"launches={g.device_launches}", flush=True)
+print(f"total {t3 - t2:.2f}s, {res.candidates} candidates, {len(cm.actions())} actions, {len(res.proposals)} proposals")
