@@ -252,17 +252,20 @@ class ReplicaCapacity : public GoalImpl {
       if (!m.alive(b)) throw OptimizationFailure("[" + name + "] Failed to move dead broker replica.");
       if (m.curOffline(r)) throw OptimizationFailure("[" + name + "] Failed to move offline replica.");
     };
+    auto less = [&](int x, int y) { return m.nrep(x) != m.nrep(y) ? m.nrep(x) < m.nrep(y) : x < y; };
+    bool built = false;
     size_t i = 0;
     while (i < list.size()) {
       size_t end = i;
       while (end < list.size() && !((int64_t)m.nrep(b) <= maxR && !m.curOffline(list[end]))) ++end;
       if (end == i) return;  // the break of the reference loop
-      order.clear();
-      for (int x = 0; x < m.B; ++x)
-        if (m.alive(x) && (selfHealingMode || (int64_t)m.nrep(x) < maxR) && x != b) order.push_back(x);
-      std::sort(order.begin(), order.end(), [&](int x, int y) {
-        return m.nrep(x) != m.nrep(y) ? m.nrep(x) < m.nrep(y) : x < y;
-      });
+      if (!built) {  // eligibleBrokers: a TreeSet by (replica count, id), rebuilt per replica in the reference;
+                     // between replicas only the last destination's count changes, so it is repositioned below
+        for (int x = 0; x < m.B; ++x)
+          if (m.alive(x) && (selfHealingMode || (int64_t)m.nrep(x) < maxR) && x != b) order.push_back(x);
+        std::sort(order.begin(), order.end(), less);
+        built = true;
+      }
       e.eligible(order, DA_MOVE, cands);
       const int64_t key = e.crossScan(*this, DA_MOVE, list, i, cands, FILTER_NONE, true, end);
       if (key < 0) {
@@ -272,7 +275,11 @@ class ReplicaCapacity : public GoalImpl {
       }
       const size_t k = i + (size_t)(key / (int64_t)cands.size());
       for (size_t q = i; q < k; ++q) fail(list[q]);
-      m.relocateReplica(m.rPart[list[k]], b, cands[key % (int64_t)cands.size()]);
+      const int dst = cands[key % (int64_t)cands.size()];
+      order.erase(std::find(order.begin(), order.end(), dst));  // key (count) of dst changes with the move
+      m.relocateReplica(m.rPart[list[k]], b, dst);
+      if (selfHealingMode || (int64_t)m.nrep(dst) < maxR)
+        order.insert(std::lower_bound(order.begin(), order.end(), dst, less), dst);
       i = k + 1;
     }
   }
@@ -974,7 +981,10 @@ class LeaderReplicaDistribution : public GoalImpl {
     return true;
   }
 
-  // rebalanceByMovingLeaderReplicasIn (:302-352)
+  // rebalanceByMovingLeaderReplicasIn (:302-352). Queued brokers never change key while queued (moves go from
+  // the polled source to b, and b is not queued), so the queue polls in comparator order and speculatively
+  // polled sources can be put back: the next sources' sorted leaders are scanned together with the current
+  // one's (growing the batch while nothing is accepted), exactly as RDG moveIn does.
   bool moveLeaderReplicasIn(Engine& e, int b) {
     Model& m = e.m;
     if (e.opt.anyExclLead && e.opt.exclLead[b]) return true;
@@ -993,24 +1003,54 @@ class LeaderReplicaDistribution : public GoalImpl {
     int nl = m.bNlead[b];
     std::vector<int32_t> single{b}, cands;
     e.eligible(single, DA_MOVE, cands);
-    while (!pq.empty()) {
-      const int src = pq.poll();
-      const std::vector<int32_t> list = m.sorted(src, id);
-      size_t i = 0;
-      while (i < list.size()) {
-        const int64_t key = cands.empty() ? -1 : e.crossScan(*this, DA_MOVE, list, i, cands);
-        if (key < 0) break;
-        const size_t k = i + (size_t)key;
-        m.relocateReplica(m.rPart[list[k]], src, b);
-        if (++nl >= lower) {
-          m.untrackAll(id);
-          return false;
-        }
-        if (!pq.empty() && m.bNlead[src] < m.bNlead[pq.peek()]) {
-          pq.add(src);
-          break;
-        }
-        i = k + 1;
+    struct Seg {
+      int src;
+      std::vector<int32_t> list;  // clone of the source's sorted leaders
+      size_t start;
+    };
+    std::vector<Seg> segs;
+    std::vector<int32_t> flat;
+    size_t target = 64;
+    bool haveCur = false;
+    Seg cur;
+    while (haveCur || !pq.empty()) {
+      segs.clear();
+      flat.clear();
+      if (haveCur) {  // the source being iterated continues first, after its winner
+        segs.push_back(std::move(cur));
+        haveCur = false;
+        flat.insert(flat.end(), segs.back().list.begin() + segs.back().start, segs.back().list.end());
+      }
+      while (!pq.empty() && (segs.empty() || flat.size() < target)) {
+        const int src = pq.poll();
+        segs.push_back({src, m.sorted(src, id), 0});
+        flat.insert(flat.end(), segs.back().list.begin(), segs.back().list.end());
+      }
+      const int64_t key = cands.empty() ? -1 : e.crossScan(*this, DA_MOVE, flat, 0, cands);
+      if (key < 0) {
+        target = std::min<size_t>(target * 4, 1 << 16);
+        continue;  // every polled source exhausted; none is re-enqueued
+      }
+      target = 64;
+      size_t q = (size_t)key, mi = 0;
+      while (q >= segs[mi].list.size() - segs[mi].start) {
+        q -= segs[mi].list.size() - segs[mi].start;
+        ++mi;
+      }
+      Seg& hit = segs[mi];
+      const size_t idx = hit.start + q;
+      m.relocateReplica(m.rPart[hit.list[idx]], hit.src, b);
+      if (++nl >= lower) {
+        m.untrackAll(id);
+        return false;
+      }
+      for (size_t t = mi + 1; t < segs.size(); ++t) pq.add(segs[t].src);  // un-poll speculative sources
+      if (!pq.empty() && m.bNlead[hit.src] < m.bNlead[pq.peek()]) {
+        pq.add(hit.src);
+      } else if (idx + 1 < hit.list.size()) {
+        cur = std::move(hit);
+        cur.start = idx + 1;
+        haveCur = true;
       }
     }
     m.untrackAll(id);

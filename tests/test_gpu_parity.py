@@ -34,13 +34,13 @@ def test_gpu_matches_oracle(gpu_lib, oracle_lib, props, balance):
 
 
 # RandomClusterTest (src/test/java/.../analyzer/RandomClusterTest.java:139-183) rows on TestConstants.BASE_PROPERTIES
-# with the default goal list: broker count 80/140, replica count 65006..75008 (max replicas 3000), topic count
+# with the default goal list: broker count 80/140, replica count 65004..75006 (max replicas 3000), topic count
 # 7000/8000, replication factor 4/5.
 @pytest.mark.parametrize("props,max_replicas", [
     (dict(num_brokers=80), 1500),
     (dict(num_brokers=140), 1500),
-    (dict(num_replicas=65006), 3000),
-    (dict(num_replicas=75008), 3000),
+    (dict(num_replicas=65004), 3000),
+    (dict(num_replicas=75006), 3000),
     (dict(num_topics=7000), 3000),
     (dict(num_replicas=50000, min_replication=4, max_replication=4), 3000),
     (dict(num_replicas=50000 - (50000 % 5), min_replication=5, max_replication=5), 3000),
