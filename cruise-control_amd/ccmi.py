@@ -175,7 +175,10 @@ EXPORTED_SYMBOLS = (
     "ccmi_session_destroy", "ccmi_optimizations", "ccmi_goal_optimize", "ccmi_action_acceptance",
     "ccmi_compute_cluster_stats", "ccmi_action_log_count", "ccmi_action_log_copy", "ccmi_replica_distribution",
     "ccmi_leader_distribution", "ccmi_proposal_count", "ccmi_proposals", "ccmi_perf", "ccmi_perf_reset",
-    "ccmi_set_kernel_timing")
+    "ccmi_set_kernel_timing", "ccmi_session_set_shard", "ccmi_rccl_unique_id", "ccmi_session_attach_rccl")
+
+# int (*)(void* ctx, int64_t* key): replace *key by the MIN over all shards, return 0 (include/ccmi.h)
+AllreduceMinFn = C.CFUNCTYPE(C.c_int, C.c_void_p, C.POINTER(C.c_int64))
 
 
 class Library:
@@ -214,6 +217,9 @@ class Library:
         L.ccmi_perf.argtypes = [C.c_void_p, C.POINTER(PerfStruct)]
         L.ccmi_perf_reset.argtypes = [C.c_void_p]
         L.ccmi_set_kernel_timing.argtypes = [C.c_void_p, C.c_int32]
+        L.ccmi_session_set_shard.argtypes = [C.c_void_p, C.c_int32, C.c_int32, AllreduceMinFn, C.c_void_p]
+        L.ccmi_rccl_unique_id.argtypes = [C.POINTER(C.c_uint8)]
+        L.ccmi_session_attach_rccl.argtypes = [C.c_void_p, C.c_int32, C.c_int32, C.POINTER(C.c_uint8)]
         L.ccmi_default_constraint.argtypes = [C.POINTER(ConstraintStruct)]
         L.ccmi_default_random_cluster_props.argtypes = [C.POINTER(RandomClusterProps)]
 
@@ -512,6 +518,35 @@ class ClusterModel:
 
     def set_kernel_timing(self, enabled: bool) -> None:
         self.lib.lib.ccmi_set_kernel_timing(self.handle, int(enabled))
+
+    def set_shard(self, rank: int, count: int, combine_min) -> None:
+        """Destination-sharded mode with a caller-supplied combiner: combine_min(local_key:int) -> global min key
+        (None / -1 for no candidate on this shard). Used with torch.distributed gloo in the CPU tests."""
+        none = (1 << 63) - 1
+
+        def _fn(_ctx, key_ptr):
+            try:
+                k = key_ptr[0]
+                key_ptr[0] = int(combine_min(k if k != none else none))
+                return 0
+            except Exception:  # noqa: BLE001 - reported as a failed combine by the engine
+                return 1
+
+        self._combine_cb = AllreduceMinFn(_fn)  # keep the trampoline alive with the session
+        self.lib.check(self.lib.lib.ccmi_session_set_shard(self.handle, rank, count, self._combine_cb, None))
+
+    def attach_rccl(self, rank: int, count: int, unique_id: bytes) -> None:
+        """Destination-sharded mode over the built-in RCCL combiner (one int64 MIN allreduce per scan)."""
+        buf = (C.c_uint8 * 128).from_buffer_copy(unique_id)
+        self.lib.check(self.lib.lib.ccmi_session_attach_rccl(self.handle, rank, count, buf))
+
+
+def rccl_unique_id(lib: Optional["Library"] = None) -> bytes:
+    """ncclGetUniqueId through libccmi (rank 0 broadcasts it to the other ranks)."""
+    lib = lib or Library.get()
+    buf = (C.c_uint8 * 128)()
+    lib.check(lib.lib.ccmi_rccl_unique_id(buf))
+    return bytes(buf)
 
 
 class GoalOptimizer:

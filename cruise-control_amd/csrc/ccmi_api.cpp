@@ -11,15 +11,19 @@
 #include "engine/engine.h"
 #include "engine/model.h"
 #include "engine/prof.h"
+#include "engine/shard_rccl.h"
 
 namespace ccmi {
 ccmi_cluster_buffers* generateRandomCluster(const ccmi_random_cluster_props& p);
 }
 
 struct ccmi_session {
+  ~ccmi_session() { ccmi::rcclDestroy(rccl); }
   ccmi::Model model;
   std::unique_ptr<ccmi::Device> device;
   std::unique_ptr<ccmi::Engine> engine;
+  ccmi::RcclShard* rccl = nullptr;
+  int deviceOrdinal = 0;
   std::vector<int32_t> initDist, initLeaders;  // for ExecutionProposal diffs
   struct Prop {
     int32_t partition, size, oldLeader;
@@ -188,6 +192,7 @@ ccmi_status ccmi_session_create(int32_t device_ordinal, const ccmi_cluster_desc*
     s->model.build(*desc);
     ccmi::Model& m = s->model;
     s->device = std::make_unique<ccmi::Device>(device_ordinal, m.B, m.R, m.P, m.T, ccmi::kMaxGoals);
+    s->deviceOrdinal = device_ordinal;
     // device layout: resource-major broker/replica columns
     std::vector<double> capRM((size_t)4 * m.B), utilRM((size_t)4 * m.B), rutilRM((size_t)4 * m.R), pot(m.B);
     std::vector<double> lbi(m.B), plno(m.P);
@@ -219,6 +224,36 @@ ccmi_status ccmi_session_create(int32_t device_ordinal, const ccmi_cluster_desc*
     s->initDist = replicaDist(m);
     s->initLeaders = leaderDist(m);
     *out = s.release();
+    return CCMI_OK;
+  });
+}
+
+ccmi_status ccmi_session_set_shard(ccmi_session* s, int32_t rank, int32_t count, ccmi_allreduce_min_fn fn, void* ctx) {
+  return guarded([&] {
+    if (!s) throw std::invalid_argument("null session");
+    if (count < 1 || rank < 0 || rank >= count) throw std::invalid_argument("shard rank out of range");
+    if (count > 1 && !fn) throw std::invalid_argument("a sharded session needs a combiner");
+    s->engine->shard = ccmi::Shard{rank, count, fn, ctx};
+    return CCMI_OK;
+  });
+}
+
+ccmi_status ccmi_rccl_unique_id(uint8_t out[128]) {
+  return guarded([&] {
+    if (!out) throw std::invalid_argument("null argument");
+    if (!ccmi::rcclUniqueId(out)) throw std::runtime_error("RCCL device error: ncclGetUniqueId failed");
+    return CCMI_OK;
+  });
+}
+
+ccmi_status ccmi_session_attach_rccl(ccmi_session* s, int32_t rank, int32_t count, const uint8_t unique_id[128]) {
+  return guarded([&] {
+    if (!s || !unique_id) throw std::invalid_argument("null argument");
+    if (count < 1 || rank < 0 || rank >= count) throw std::invalid_argument("shard rank out of range");
+    ccmi::rcclDestroy(s->rccl);
+    s->rccl = nullptr;
+    s->rccl = ccmi::rcclCreate(s->deviceOrdinal, rank, count, unique_id);
+    s->engine->shard = ccmi::Shard{rank, count, &ccmi::rcclMin, s->rccl};
     return CCMI_OK;
   });
 }

@@ -13,15 +13,16 @@ namespace ccmi {
 #define EV1 ((hipEvent_t)ev1_)
 
 hipError_t launchScanCross(const DevTables& T, const MutTables& M, const UpdateList& U, const DevProgram& prog,
-                           const int32_t* reps, const int32_t* cands, int K, int N, unsigned long long* result,
-                           unsigned int* done, unsigned long long* mail, unsigned long long seq, hipStream_t st);
+                           const int32_t* reps, const int32_t* cands, int K, int Nr, int N, int c0,
+                           unsigned long long* result, unsigned int* done, unsigned long long* mail,
+                           unsigned long long seq, hipStream_t st);
 hipError_t launchScanSwap(const DevTables& T, const DevProgram& prog, const int32_t* srcs, int S, const int32_t* cbOff,
                           const int32_t* cbRep, int M, unsigned long long* result, int32_t* rowVisited,
                           unsigned long long* mail, unsigned long long seq, hipStream_t st, hipEvent_t ev0,
                           hipEvent_t ev1);
 hipError_t launchScanPairs(const DevTables& T, const MutTables& M, const UpdateList& U, const DevProgram& prog,
-                           const int32_t* pr, const int32_t* pb, int n, unsigned long long* result, unsigned int* done,
-                           unsigned long long* mail, unsigned long long seq, hipStream_t st);
+                           const int32_t* pr, const int32_t* pb, int n, int keyBase, unsigned long long* result,
+                           unsigned int* done, unsigned long long* mail, unsigned long long seq, hipStream_t st);
 hipError_t launchPrep(const MutTables& M, int B, int R, const int32_t* pOff, const UpdateList& U, const int4* req,
                       int4* dReq, int nReq4, unsigned long long* result, unsigned int* done, hipStream_t st);
 hipError_t launchStats(const StatsParams& P, const int32_t* tc, const int32_t* topicNrep, const double* bUtil,
@@ -267,6 +268,11 @@ void Device::waitMail(unsigned long long seq) {
   perf.syncs++;
 }
 
+// A shard with nothing to scan still applies its pending row updates so every shard's tables stay identical.
+void Device::flushPending() {
+  if (!brows.empty() || !rrows.empty() || !prows.empty() || !tdeltas.empty()) flushOnly();
+}
+
 void Device::flushOnly() {
   if (brows.empty() && rrows.empty() && prows.empty() && tdeltas.empty()) return;
   const Staged g = packUpdates(0);
@@ -330,25 +336,30 @@ const char* Device::stageScan(const Staged& g, size_t req, bool readsTopicCounts
   return dReq_;
 }
 
-int64_t Device::scanCross(const DevProgram& prog, const int32_t* reps, int K, const int32_t* cands, int N) {
-  if (K <= 0 || N <= 0) return -1;
+int64_t Device::scanCross(const DevProgram& prog, const int32_t* reps, int K, const int32_t* cands, int N, int c0,
+                          int c1) {
+  const int Nr = c1 - c0;
+  if (K <= 0 || Nr <= 0) {
+    flushPending();
+    return -1;
+  }
   if ((uint64_t)K * (uint64_t)N >= (1ull << 31)) throw std::runtime_error("scan too large");
   const size_t oCand = align16((size_t)K * 4);
-  const size_t req = oCand + align16((size_t)N * 4);
+  const size_t req = oCand + align16((size_t)Nr * 4);
   const Staged g = packUpdates(req);
   std::memcpy(hStage_ + g.end, reps, (size_t)K * 4);
-  std::memcpy(hStage_ + g.end + oCand, cands, (size_t)N * 4);
+  std::memcpy(hStage_ + g.end + oCand, cands + c0, (size_t)Nr * 4);
   UpdateList u;
   const char* base = stageScan(g, req, (prog.needs & NEED_TOPIC) != 0, u);
   ++seq_;
   if (timing) (void)hipEventRecord(EV0, ST);
-  hipCheck(launchScanCross(tables(), mutTables(), u, prog, (const int32_t*)base, (const int32_t*)(base + oCand), K, N,
-                           dResult_, dDone_, hResultDev_, seq_, ST),
+  hipCheck(launchScanCross(tables(), mutTables(), u, prog, (const int32_t*)base, (const int32_t*)(base + oCand), K, Nr,
+                           N, c0, dResult_, dDone_, hResultDev_, seq_, ST),
            "scan_cross");
   if (timing) (void)hipEventRecord(EV1, ST);
   perf.scanLaunches++;
-  perf.scanPairs += (int64_t)K * N;
-  perf.scanBytes += (int64_t)K * N * kBytesPerCandidate;
+  perf.scanPairs += (int64_t)K * Nr;
+  perf.scanBytes += (int64_t)K * Nr * kBytesPerCandidate;
   return finishScan();
 }
 
@@ -384,18 +395,22 @@ int64_t Device::scanSwap(const DevProgram& prog, const int32_t* srcs, int S, con
   return best == ~0ull ? -1 : (int64_t)best;
 }
 
-int64_t Device::scanPairs(const DevProgram& prog, const int32_t* pr, const int32_t* pb, int n) {
-  if (n <= 0) return -1;
+int64_t Device::scanPairs(const DevProgram& prog, const int32_t* pr, const int32_t* pb, int p0, int p1) {
+  const int n = p1 - p0;
+  if (n <= 0) {
+    flushPending();
+    return -1;
+  }
   const size_t oB = align16((size_t)n * 4);
   const size_t req = oB + align16((size_t)n * 4);
   const Staged g = packUpdates(req);
-  std::memcpy(hStage_ + g.end, pr, (size_t)n * 4);
-  std::memcpy(hStage_ + g.end + oB, pb, (size_t)n * 4);
+  std::memcpy(hStage_ + g.end, pr + p0, (size_t)n * 4);
+  std::memcpy(hStage_ + g.end + oB, pb + p0, (size_t)n * 4);
   UpdateList u;
   const char* base = stageScan(g, req, (prog.needs & NEED_TOPIC) != 0, u);
   ++seq_;
   if (timing) (void)hipEventRecord(EV0, ST);
-  hipCheck(launchScanPairs(tables(), mutTables(), u, prog, (const int32_t*)base, (const int32_t*)(base + oB), n,
+  hipCheck(launchScanPairs(tables(), mutTables(), u, prog, (const int32_t*)base, (const int32_t*)(base + oB), n, p0,
                            dResult_, dDone_, hResultDev_, seq_, ST),
            "scan_pairs");
   if (timing) (void)hipEventRecord(EV1, ST);

@@ -57,13 +57,15 @@ class Device {
   std::vector<PartitionRow> prows;
   std::vector<TopicCountDelta> tdeltas;
 
-  // returns the winning key or -1
-  int64_t scanCross(const DevProgram& prog, const int32_t* reps, int K, const int32_t* cands, int N);
+  // returns the winning key or -1. Cross: rows reps[0,K) x columns [c0,c1) of cands[0,N), key = k*N + j.
+  // Pairs: pairs [p0,p1) of (pr, pb), key = pair index. Keys are global, so shards MIN-combine them.
+  int64_t scanCross(const DevProgram& prog, const int32_t* reps, int K, const int32_t* cands, int N, int c0, int c1);
   int64_t scanSwap(const DevProgram& prog, const int32_t* srcs, int S, const int32_t* cbOff, int M,
                    const int32_t* cbRep, int nCand, int64_t* visited);
-  int64_t scanPairs(const DevProgram& prog, const int32_t* pr, const int32_t* pb, int n);
+  int64_t scanPairs(const DevProgram& prog, const int32_t* pr, const int32_t* pb, int p0, int p1);
   void stats(const StatsParams& P, const uint8_t* allowedAliveHost, StatsOut* out);
   void flushOnly();
+  void flushPending();
 
   DevicePerf perf;
   bool timing = false;  // record HIP events around kernels (bench/profiling)

@@ -123,16 +123,26 @@ int64_t Engine::crossScan(GoalImpl& self, int action, const std::vector<int32_t>
   m.flushToDevice();
   DevProgram prog = program(self, action);
   prog.filter = filter;
-  const int64_t key = dev->scanCross(prog, reps.data() + r0, K, cands.data(), N);
+  const int c0 = (int)((int64_t)N * shard.rank / shard.count), c1 = (int)((int64_t)N * (shard.rank + 1) / shard.count);
+  const int64_t key = combine(dev->scanCross(prog, reps.data() + r0, K, cands.data(), N, c0, c1));
   if (count) candidates += key >= 0 ? key + 1 : (int64_t)K * N;
   return key;
+}
+
+int64_t Engine::combine(int64_t localKey) const {
+  if (shard.count <= 1) return localKey;
+  int64_t k = localKey < 0 ? INT64_MAX : localKey;
+  if (!shard.fn || shard.fn(shard.ctx, &k) != 0) throw std::runtime_error("shard combine (MIN allreduce) failed");
+  return k == INT64_MAX ? -1 : k;
 }
 
 int64_t Engine::pairScan(GoalImpl& self, const std::vector<int32_t>& pr, const std::vector<int32_t>& pb, int action) {
   if (pr.empty()) return -1;
   PhaseScope ps(PH_DEV_SCAN);
   m.flushToDevice();
-  const int64_t key = dev->scanPairs(program(self, action), pr.data(), pb.data(), (int)pr.size());
+  const int n = (int)pr.size();
+  const int p0 = (int)((int64_t)n * shard.rank / shard.count), p1 = (int)((int64_t)n * (shard.rank + 1) / shard.count);
+  const int64_t key = combine(dev->scanPairs(program(self, action), pr.data(), pb.data(), p0, p1));
   candidates += key >= 0 ? key + 1 : (int64_t)pr.size();
   return key;
 }

@@ -40,6 +40,15 @@ struct Constraint {  // BalancingConstraint
 
 class Engine;
 
+// Destination-sharded scans: every shard runs the same host drivers on an identical replica of
+// the model and scans only its slice of each candidate list; `combine` MIN-reduces the shards' first-fit keys
+// (keys are global list positions, so the minimum is the reference's first accepted candidate).
+struct Shard {
+  int rank = 0, count = 1;
+  ccmi_allreduce_min_fn fn = nullptr;
+  void* ctx = nullptr;
+};
+
 class GoalImpl {
  public:
   virtual ~GoalImpl() = default;
@@ -63,6 +72,7 @@ class Engine {
   Device* dev;
   Options opt;
   Constraint bc{};
+  Shard shard;
   std::vector<std::unique_ptr<GoalImpl>> optimized;  // optimized goals, priority order
   int64_t candidates = 0;
   std::vector<uint8_t> scratchB;  // per-broker scratch flags for the goal drivers
@@ -89,6 +99,7 @@ class Engine {
 
  private:
   DevProgram program(const GoalImpl& self, int action) const;
+  int64_t combine(int64_t localKey) const;
   void refreshAllowed(GoalImpl& g);
 };
 

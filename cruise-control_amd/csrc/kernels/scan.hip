@@ -425,27 +425,31 @@ __device__ __forceinline__ void publishLast(unsigned long long* __restrict__ res
   }
 }
 
+// Rows reps[0, K) x candidate columns [c0, c0 + Nr) of an N-column candidate list; key = k * N + c0 + jj. A sharded
+// session scans only its own column range; keys stay global, so a MIN over shards is the global first fit.
 __global__ __launch_bounds__(kBlock) void scan_cross(DevTables T, MutTables Mt, UpdateList U, DevProgram prog,
                                                      const int32_t* __restrict__ reps,
-                                                     const int32_t* __restrict__ cands, int K, int N,
+                                                     const int32_t* __restrict__ cands, int K, int Nr, int N, int c0,
                                                      unsigned long long* __restrict__ result,
                                                      unsigned int* __restrict__ done,
                                                      unsigned long long* __restrict__ mail, unsigned long long seq) {
   __shared__ OverlayLds ov;
   overlayBegin(ov, U, Mt, T);
-  const uint32_t total = (uint32_t)K * (uint32_t)N;
+  const uint32_t total = (uint32_t)K * (uint32_t)Nr;
   for (uint32_t base = blockIdx.x * kBlock; base < total; base += gridDim.x * kBlock) {
-    if (blockBest(result) <= base) break;  // an earlier pair already won: nothing later can (block-uniform)
+    const uint32_t kb = base / (uint32_t)Nr;
+    const unsigned long long keyBase = (unsigned long long)kb * N + c0 + (base - kb * (uint32_t)Nr);
+    if (blockBest(result) <= keyBase) break;  // an earlier pair already won: nothing later can (block-uniform)
     unsigned long long local = kNone;
     const uint32_t q = base + threadIdx.x;
     if (q < total) {
-      const uint32_t k = q / (uint32_t)N;
-      const uint32_t j = q - k * (uint32_t)N;
+      const uint32_t k = q / (uint32_t)Nr;
+      const uint32_t j = q - k * (uint32_t)Nr;
       PreView v;
       v.loadRow(T, prog, reps[k], ov);
       v.loadDst(T, prog, cands[j], ov);
       const bool inList = prog.filter != FILTER_RACK_AWARE || v.rackEligible();
-      if (inList && moveCandidateAccepted(prog, v, v.r, v.dst)) local = q;
+      if (inList && moveCandidateAccepted(prog, v, v.r, v.dst)) local = (unsigned long long)k * N + c0 + j;
     }
     const unsigned long long m = blockMin(local);
     if (m != kNone) {
@@ -527,21 +531,21 @@ __global__ __launch_bounds__(1024) void swap_visited_sum(const int32_t* __restri
 // PAIRS: explicit (replica, broker) list in iteration order (leadership moves: per-replica follower lists).
 __global__ __launch_bounds__(kBlock) void scan_pairs(DevTables T, MutTables Mt, UpdateList U, DevProgram prog,
                                                      const int32_t* __restrict__ pr,
-                                                     const int32_t* __restrict__ pb, int n,
+                                                     const int32_t* __restrict__ pb, int n, int keyBase,
                                                      unsigned long long* __restrict__ result,
                                                      unsigned int* __restrict__ done,
                                                      unsigned long long* __restrict__ mail, unsigned long long seq) {
   __shared__ OverlayLds ov;
   overlayBegin(ov, U, Mt, T);
   for (int base = blockIdx.x * kBlock; base < n; base += gridDim.x * kBlock) {
-    if (blockBest(result) <= (unsigned long long)base) break;
+    if (blockBest(result) <= (unsigned long long)(keyBase + base)) break;
     unsigned long long local = kNone;
     const int q = base + threadIdx.x;
     if (q < n) {
       PreView v;
       v.loadRow(T, prog, pr[q], ov);
       v.loadDst(T, prog, pb[q], ov);
-      if (moveCandidateAccepted(prog, v, v.r, v.dst)) local = (unsigned long long)q;
+      if (moveCandidateAccepted(prog, v, v.r, v.dst)) local = (unsigned long long)(keyBase + q);
     }
     const unsigned long long m = blockMin(local);
     if (m != kNone) {
@@ -579,11 +583,12 @@ static unsigned gridFor(uint64_t work, uint64_t perBlock) {
 }
 
 hipError_t launchScanCross(const DevTables& T, const MutTables& M, const UpdateList& U, const DevProgram& prog,
-                           const int32_t* reps, const int32_t* cands, int K, int N, unsigned long long* result,
-                           unsigned int* done, unsigned long long* mail, unsigned long long seq, hipStream_t st) {
-  const unsigned blocks = gridFor((uint64_t)K * (uint64_t)N, (uint64_t)kBlock);
-  hipLaunchKernelGGL(scan_cross, dim3(blocks), dim3(kBlock), 0, st, T, M, U, prog, reps, cands, K, N, result, done,
-                     mail, seq);
+                           const int32_t* reps, const int32_t* cands, int K, int Nr, int N, int c0,
+                           unsigned long long* result, unsigned int* done, unsigned long long* mail,
+                           unsigned long long seq, hipStream_t st) {
+  const unsigned blocks = gridFor((uint64_t)K * (uint64_t)Nr, (uint64_t)kBlock);
+  hipLaunchKernelGGL(scan_cross, dim3(blocks), dim3(kBlock), 0, st, T, M, U, prog, reps, cands, K, Nr, N, c0, result,
+                     done, mail, seq);
   return hipGetLastError();
 }
 
@@ -602,10 +607,11 @@ hipError_t launchScanSwap(const DevTables& T, const DevProgram& prog, const int3
 }
 
 hipError_t launchScanPairs(const DevTables& T, const MutTables& M, const UpdateList& U, const DevProgram& prog,
-                           const int32_t* pr, const int32_t* pb, int n, unsigned long long* result, unsigned int* done,
-                           unsigned long long* mail, unsigned long long seq, hipStream_t st) {
+                           const int32_t* pr, const int32_t* pb, int n, int keyBase, unsigned long long* result,
+                           unsigned int* done, unsigned long long* mail, unsigned long long seq, hipStream_t st) {
   const unsigned blocks = gridFor((uint64_t)n, (uint64_t)kBlock);
-  hipLaunchKernelGGL(scan_pairs, dim3(blocks), dim3(kBlock), 0, st, T, M, U, prog, pr, pb, n, result, done, mail, seq);
+  hipLaunchKernelGGL(scan_pairs, dim3(blocks), dim3(kBlock), 0, st, T, M, U, prog, pr, pb, n, keyBase, result, done,
+                     mail, seq);
   return hipGetLastError();
 }
 

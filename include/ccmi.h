@@ -258,6 +258,20 @@ int64_t ccmi_proposal_count(const ccmi_session* s);
 ccmi_status ccmi_proposals(const ccmi_session* s, int32_t max_rf, int32_t* partition, int32_t* size,
                            int32_t* old_leader, int32_t* old_out, int32_t* new_out);
 
+/*
+ * Destination-sharded mode (one process per GPU): every rank creates a session on its own device from the same
+ * desc, runs the same goal chain, and scans only its slice [N*rank/count, N*(rank+1)/count) of every candidate
+ * list. After each scan the engine calls `fn(ctx, key)`, which must replace *key by the MIN over all ranks
+ * (INT64_MAX = no accepted candidate) and return 0; the result is the reference's first accepted candidate, so
+ * every rank applies the same move. Swap scans and statistics run unsharded on every rank.
+ * ccmi_session_attach_rccl installs the built-in RCCL combiner (one int64 MIN allreduce over xGMI per scan);
+ * ccmi_rccl_unique_id produces the 128-byte id rank 0 broadcasts to the others.
+ */
+typedef int (*ccmi_allreduce_min_fn)(void* ctx, int64_t* key);
+ccmi_status ccmi_session_set_shard(ccmi_session* s, int32_t rank, int32_t count, ccmi_allreduce_min_fn fn, void* ctx);
+ccmi_status ccmi_rccl_unique_id(uint8_t out[128]);
+ccmi_status ccmi_session_attach_rccl(ccmi_session* s, int32_t rank, int32_t count, const uint8_t unique_id[128]);
+
 /* Measurement hooks used by bench.py: device time of the last optimization's scan kernels (HIP events
  * on the engine stream) and their algorithmic bytes. */
 typedef struct ccmi_perf_counters {

@@ -12,8 +12,16 @@
 
 #include "device.h"
 #include "predicates.h"
+#include "shard_rccl.h"
 
 namespace ccmi {
+
+// No RCCL in the emulation: sharded emulation sessions use ccmi_session_set_shard with a test combiner.
+struct RcclShard {};
+bool rcclUniqueId(uint8_t*) { return false; }
+RcclShard* rcclCreate(int, int, int, const uint8_t*) { throw std::runtime_error("RCCL device error: emulation build"); }
+void rcclDestroy(RcclShard*) {}
+int rcclMin(void*, int64_t*) { return 1; }
 
 namespace {
 struct Emu {
@@ -127,6 +135,8 @@ void Device::setTopicLimits(const int32_t* upper, const int32_t* lower) {
   E(st_).tLower.assign(lower, lower + T_);
 }
 
+void Device::flushPending() { flushOnly(); }
+
 void Device::flushOnly() {
   Emu& e = E(st_);
   for (const BrokerRow& x : brows) {
@@ -153,25 +163,26 @@ void Device::flushOnly() {
   tdeltas.clear();
 }
 
-int64_t Device::scanCross(const DevProgram& prog, const int32_t* reps, int K, const int32_t* cands, int N) {
+int64_t Device::scanCross(const DevProgram& prog, const int32_t* reps, int K, const int32_t* cands, int N, int c0,
+                          int c1) {
   flushOnly();
   View v{E(st_)};
   perf.scanLaunches++;
-  perf.scanPairs += (int64_t)K * N;
+  perf.scanPairs += (int64_t)K * (c1 - c0);
   for (int k = 0; k < K; ++k)
-    for (int j = 0; j < N; ++j) {
+    for (int j = c0; j < c1; ++j) {
       if (prog.filter == FILTER_RACK_AWARE && !v.rackEligible(reps[k], cands[j])) continue;
       if (moveCandidateAccepted(prog, v, reps[k], cands[j])) return (int64_t)k * N + j;
     }
   return -1;
 }
 
-int64_t Device::scanPairs(const DevProgram& prog, const int32_t* pr, const int32_t* pb, int n) {
+int64_t Device::scanPairs(const DevProgram& prog, const int32_t* pr, const int32_t* pb, int p0, int p1) {
   flushOnly();
   View v{E(st_)};
   perf.scanLaunches++;
-  perf.scanPairs += n;
-  for (int q = 0; q < n; ++q)
+  perf.scanPairs += p1 - p0;
+  for (int q = p0; q < p1; ++q)
     if (moveCandidateAccepted(prog, v, pr[q], pb[q])) return q;
   return -1;
 }
