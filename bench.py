@@ -1,24 +1,26 @@
 """Headline benchmark: candidate moves evaluated/s + proposal wall time (BASELINE.json `metric`).
 
-Workload (BASELINE.json configs[1], the largest single-GPU config): RandomCluster with 20 racks, 1 000 brokers,
-99 999 + 2 000 replicas (R = 101 999), 3 001 topics, W = 1; goals ReplicaDistributionGoal,
-DiskUsageDistributionGoal, NetworkInboundUsageDistributionGoal, NetworkOutboundUsageDistributionGoal,
-CpuUsageDistributionGoal (default priority order), default BalancingConstraint.
+Workload (default, BASELINE.json configs[2] — the configuration the metric is quoted on, and it fits one GPU):
+RandomCluster C2 = 100 racks, 10 000 brokers, 999 999 + 20 000 replicas (R = 1 019 999), 10 001 topics, W = 1,
+uniform loads, TestConstants seeds; the 16 default goals in default priority order; default BalancingConstraint.
+--workload c1 / c0 / c2_c1goals select the other BASELINE configs (parity-test cases, not headline lines).
 
-A "step" is one full GoalOptimizer.optimizations over that cluster (all five goals, stats after every goal,
+A "step" is one full GoalOptimizer.optimizations over that cluster (every goal, ClusterModelStats after every goal,
 final ExecutionProposals). Each step works on its own device session, uploaded to HBM before the timed region
 starts; the step count K therefore means K independent proposal computations per GPU.
 
 value = reference-equivalent candidate moves evaluated/s summed over all ranks (the candidates the reference's
 first-fit loops would visit), ms_per_step = proposal wall time.
 
-Multi-GPU (torchrun, one process per GPU): every rank runs its own independent what-if proposal request
-(weak scaling, no data-path collective); timing is max over ranks.
+Multi-GPU (torchrun, one process per GPU): by default every rank runs its own independent what-if proposal
+request (weak scaling, no data-path collective); timing is max over ranks. --sharded instead shards ONE proposal's
+candidate space by destination broker over the ranks (one RCCL MIN allreduce per scan, strong scaling).
 
-Roofline: the dominant kernel is the candidate scan. Its HIP-event duration is measured in a separate
-instrumented pass after the timed region (events on the engine stream); algorithmic bytes = 96 B per
-reference-equivalent candidate. cpu_baseline = the single-threaded C++ restatement
-(oracle/, "port") on one full optimization of the same workload, rank 0 / N = 1 only.
+Roofline: the dominant kernel is the candidate scan. Its HIP-event duration is measured during the warmup
+proposal(s) (events on the engine stream, outside the timed region); algorithmic bytes = 96 B per
+reference-equivalent candidate. traffic = HBM bytes per scan launch from the committed rocprofv3
+PMC summary of this workload. cpu_baseline = the single-threaded C++ restatement (oracle/, "port") on rank 0 at
+N = 1: the whole chain for C0/C1, a goal-prefix sample of the chain for C2.
 """
 from __future__ import annotations
 
@@ -45,21 +47,30 @@ BYTES_PER_CANDIDATE = 96
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E (MI355X_MICROARCH.md)
 
 
-def cpu_baseline(buf) -> dict:
-    """The oracle restatement, single thread, one full optimization of the same cluster (rank 0, N=1 only).
-    At C1 this is ~4-9 s of CPU work; at C2 sizes it takes ~20 min, so it is only run for the C1 workload."""
+# CPU-baseline sample of the C2 workload: the first goals of the default chain on the same C2 cluster (the whole
+# chain takes the single-threaded restatement about an hour: every goal pays ~30 s of ClusterModelStats over the
+# T x B topic-replica counts at C2; the first goal alone is ~30 s of CPU work).
+C2_CPU_SAMPLE_GOALS = 1
+
+
+def cpu_baseline(buf, workload: str, goal_names) -> dict:
+    """The oracle restatement (oracle/, "port"), single thread, on rank 0 at N=1: the whole chain for C0/C1, a
+    goal-prefix sample of the chain for C2 (same cluster, same constraint)."""
     sys.path.insert(0, os.path.join(REPO, "tests"))
     from oracle_binding import OracleCluster
 
+    goals = list(goal_names) if workload in ("c0", "c1") else list(goal_names)[:C2_CPU_SAMPLE_GOALS]
     oc = OracleCluster.from_desc(buf.desc)
     t0 = time.perf_counter()
-    res = oc.optimize(C1_GOALS, ccmi.BalancingConstraint())
+    res = oc.optimize(goals, ccmi.BalancingConstraint())
     dt = time.perf_counter() - t0
     cands = sum(r.candidates for r in res)
+    what = "one full optimizations()" if len(goals) == len(goal_names) else \
+        f"optimizations() over the first {len(goals)} goals of the chain ({goals[0]} .. {goals[-1]})"
     return {"value": cands / dt, "unit": "candidate moves evaluated/s", "cores": 1, "kind": "port",
-            "sample": f"one full optimizations() of the C1 workload ({cands} candidates, {len(oc.actions())} actions) "
-                      f"in {dt:.2f} s by the single-threaded C++ restatement (oracle/)",
-            "proposal_wall_s": dt}
+            "sample": f"{what} of the {workload.upper()} workload: {cands} candidates, {len(oc.actions())} actions in "
+                      f"{dt:.2f} s by the single-threaded C++ restatement (oracle/)",
+            "goals": goals, "wall_s": dt}
 
 
 SCAN_KERNELS = ("scan_cross", "scan_pairs", "scan_swap")
@@ -83,10 +94,13 @@ def pmc_traffic(workload: str):
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=2)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--workload", choices=sorted(WORKLOADS), default="c1")
+    ap.add_argument("--workload", choices=sorted(WORKLOADS), default="c2")
+    ap.add_argument("--sharded", action="store_true",
+                    help="N>1: one proposal sharded by destination broker over all ranks (RCCL MIN per scan) "
+                         "instead of one independent what-if proposal per rank")
     args = ap.parse_args()
 
     import torch
@@ -106,12 +120,29 @@ def main() -> None:
     buf = ccmi.RandomCluster.generate(lib, **props)
     goals = ccmi.goals_from_names(goal_names)
     opt = ccmi.GoalOptimizer(ccmi.BalancingConstraint())
+    sharded = args.sharded and world > 1
+    uid = None
+    if sharded:  # rank 0's RCCL id reaches the other ranks over the default process group
+        obj = [ccmi.rccl_unique_id(lib) if rank == 0 else None]
+        dist.broadcast_object_list(obj, src=0)
+        uid = obj[0]
 
     def session():
-        return ccmi.ClusterModel.from_buffers(buf, device=device)
+        s = ccmi.ClusterModel.from_buffers(buf, device=device)
+        if sharded:
+            s.attach_rccl(rank, world, uid)
+        return s
 
-    for _ in range(args.warmup):
-        opt.optimizations(session(), goals)
+    # Warmup proposals double as the instrumented pass: HIP events around every scan kernel on the engine stream
+    # (outside the timed region).
+    inst_perf = inst_cands = None
+    for w in range(max(1, args.warmup)):
+        ws = session()
+        ws.set_kernel_timing(True)
+        ws.reset_perf()
+        r = opt.optimizations(ws, goals)
+        inst_perf, inst_cands = ws.perf(), r.candidates
+        del ws
 
     sessions = [session() for _ in range(args.steps)]  # cluster resident in HBM before timing starts
     torch.cuda.synchronize()
@@ -133,15 +164,12 @@ def main() -> None:
         dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
         dist.all_reduce(t, op=dist.ReduceOp.SUM)
         elapsed, cands = float(tmax[0]), float(t[1])
+        if sharded:  # every rank made the same decisions: one proposal's candidates per step
+            cands = float(sum(r.candidates for r in results))
 
-    # Instrumented pass (outside the timed region): HIP events around every scan kernel on the engine stream.
-    inst = session()
-    inst.set_kernel_timing(True)
-    inst.reset_perf()
-    r_inst = opt.optimizations(inst, goals)
-    perf = inst.perf()
+    perf = inst_perf
     scan_avg_ms = perf.scan_kernel_ms / max(1, perf.scan_launches)
-    ref_bytes_per_launch = r_inst.candidates * BYTES_PER_CANDIDATE / max(1, perf.scan_launches)
+    ref_bytes_per_launch = inst_cands * BYTES_PER_CANDIDATE / max(1, perf.scan_launches)
     achieved = ref_bytes_per_launch / (scan_avg_ms * 1e-3) / 1e9 if scan_avg_ms > 0 else 0.0
 
     if rank != 0:
@@ -158,14 +186,15 @@ def main() -> None:
         "warmup": args.warmup,
         "ms_per_step": elapsed * 1e3 / args.steps,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if sharded else "weak",
         "vs_baseline": None,
         "dtype": "f64",
         "data": "synthetic (RandomCluster restatement, TestConstants seeds)",
         "config": {"workload": workload_name,
                    "brokers": buf.desc.num_brokers, "replicas": buf.desc.num_replicas,
                    "partitions": buf.desc.num_partitions, "topics": buf.desc.num_topics,
-                   "goals": goal_names, "parallelism": f"independent what-if per GPU x{world}"},
+                   "goals": goal_names, "parallelism": (f"destination-sharded x{world} (RCCL MIN allreduce per scan)" if sharded
+                                   else f"independent what-if per GPU x{world}")},
         "proposal_wall_s": elapsed / args.steps,
         "candidates_per_step": first.candidates,
         "actions_per_step": len(first.actions),
@@ -181,8 +210,8 @@ def main() -> None:
                      "host_syncs_per_step": perf.host_syncs},
         "cpu_baseline": None,
     }
-    if world == 1 and not args.no_cpu_baseline and args.workload == "c1":
-        line["cpu_baseline"] = cpu_baseline(buf)
+    if world == 1 and not args.no_cpu_baseline:
+        line["cpu_baseline"] = cpu_baseline(buf, args.workload, goal_names)
     print(json.dumps(line))
     if world > 1:
         dist.destroy_process_group()

@@ -27,13 +27,13 @@ if [ -z "${SKIP_BENCH:-}" ]; then
 fi
 if [ -n "${PROFILE:-}" ]; then
   step rocprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o bench -- \
-    python3 bench.py --no-cpu-baseline --steps 2 --warmup 1
+    python3 bench.py --no-cpu-baseline --steps 1 --warmup 0 ${PROF_ARGS:-}
 fi
 if [ -n "${PMC:-}" ]; then
   step pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc_fetch -o bench -- \
-    python3 bench.py --no-cpu-baseline --steps 1 --warmup 0
+    python3 bench.py --no-cpu-baseline --steps 1 --warmup 0 ${PROF_ARGS:-}
   step pmc_write 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc_write -o bench -- \
-    python3 bench.py --no-cpu-baseline --steps 1 --warmup 0
+    python3 bench.py --no-cpu-baseline --steps 1 --warmup 0 ${PROF_ARGS:-}
 fi
 if [ -n "${C2:-}" ]; then
   step bench_c2 900 python bench.py --workload c2 --steps 1 --warmup 0
