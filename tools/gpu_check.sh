@@ -28,12 +28,16 @@ fi
 if [ -n "${PROFILE:-}" ]; then
   step rocprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o bench -- \
     python3 bench.py --no-cpu-baseline --steps 1 --warmup 0 ${PROF_ARGS:-}
+  rm -f gpurun_out/prof/*_kernel_trace.csv  # one row per dispatch: too large to bring back; the stats stay
 fi
 if [ -n "${PMC:-}" ]; then
   step pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc_fetch -o bench -- \
     python3 bench.py --no-cpu-baseline --steps 1 --warmup 0 ${PROF_ARGS:-}
   step pmc_write 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc_write -o bench -- \
     python3 bench.py --no-cpu-baseline --steps 1 --warmup 0 ${PROF_ARGS:-}
+  python3 tools/pmc_summary.py gpurun_out/pmc_fetch/bench_counter_collection.csv \
+    gpurun_out/pmc_write/bench_counter_collection.csv > gpurun_out/pmc_summary.json
+  rm -f gpurun_out/pmc_fetch/*_counter_collection.csv gpurun_out/pmc_write/*_counter_collection.csv
 fi
 if [ -n "${C2:-}" ]; then
   step bench_c2 900 python bench.py --workload c2 --steps 1 --warmup 0
