@@ -1,5 +1,6 @@
 // Device tables, staging and launch protocol (see device.h).
 #include "device.h"
+#include "prof.h"
 
 #include <hip/hip_runtime.h>
 
@@ -251,6 +252,7 @@ void Device::launchPrepFor(const Staged& g, size_t reqBytes, bool scan) {
 // Spin on the host-mapped mailbox for `seq`; a stream error (or a stream that drained without publishing)
 // is reported instead of spinning forever.
 void Device::waitMail(unsigned long long seq) {
+  PhaseScope ps(PH_SCAN_WAIT);
   volatile unsigned long long* mail = hResult_;
   const unsigned long long want = seq & 0xffffffffull;
   uint64_t spins = 0;
@@ -346,11 +348,15 @@ int64_t Device::scanCross(const DevProgram& prog, const int32_t* reps, int K, co
   if ((uint64_t)K * (uint64_t)N >= (1ull << 31)) throw std::runtime_error("scan too large");
   const size_t oCand = align16((size_t)K * 4);
   const size_t req = oCand + align16((size_t)Nr * 4);
-  const Staged g = packUpdates(req);
-  std::memcpy(hStage_ + g.end, reps, (size_t)K * 4);
-  std::memcpy(hStage_ + g.end + oCand, cands + c0, (size_t)Nr * 4);
   UpdateList u;
-  const char* base = stageScan(g, req, (prog.needs & NEED_TOPIC) != 0, u);
+  const char* base;
+  {
+    PhaseScope ps(PH_SCAN_STAGE);
+    const Staged g = packUpdates(req);
+    std::memcpy(hStage_ + g.end, reps, (size_t)K * 4);
+    std::memcpy(hStage_ + g.end + oCand, cands + c0, (size_t)Nr * 4);
+    base = stageScan(g, req, (prog.needs & NEED_TOPIC) != 0, u);
+  }
   ++seq_;
   if (timing) (void)hipEventRecord(EV0, ST);
   hipCheck(launchScanCross(tables(), mutTables(), u, prog, (const int32_t*)base, (const int32_t*)(base + oCand), K, Nr,

@@ -640,6 +640,11 @@ class ResourceDistribution : public GoalImpl {
 
   // sortedCandidateReplicas (:543-569)
   int trackCandidates(Engine& e, int b, double limit, bool asc, bool followersOnly, bool leadersOnly, bool immOnly) {
+    const int id = nameId(!asc, leadersOnly);
+    e.m.track(b, id, candidateSpec(e, limit, asc, followersOnly, leadersOnly, immOnly));
+    return id;
+  }
+  Model::Spec candidateSpec(Engine& e, double limit, bool asc, bool followersOnly, bool leadersOnly, bool immOnly) {
     Model& m = e.m;
     Model::Spec s;
     s.selFollowers = followersOnly;
@@ -658,9 +663,7 @@ class ResourceDistribution : public GoalImpl {
       s.scoreReverse = true;
     }
     s.scoreRes = res;
-    const int id = nameId(!asc, leadersOnly);
-    m.track(b, id, s);
-    return id;
+    return s;
   }
 
   double firstOnlineLoad(const Model& m, const std::vector<int32_t>& v, bool wantMax) const {
@@ -722,11 +725,37 @@ class ResourceDistribution : public GoalImpl {
         if (o.first == x) return;
       entryKey.push_back({x, m.pct(x, res)});
     };
+    std::vector<int32_t> rank;
     auto materialise = [&]() {
       PhaseScope pi(PH_TREE_BUILD);
       ovr = entryKey;
-      for (int x = 0; x < m.B; ++x)
-        if (entryIn[x]) cand.add(x);
+      // Entry-time (key, id) order of the members: the maintained live order with the few brokers whose key
+      // moved since entry put back at their entry keys; the tree is then built by the same put sequence (ids in
+      // aliveBrokers order) with integer rank compares.
+      {
+        std::vector<int32_t> order;
+        order.reserve(m.B);
+        std::vector<uint8_t>& changed = e.scratchB2;
+        changed.assign(m.B, 0);
+        for (const auto& o : entryKey) changed[o.first] = 1;
+        for (int x : m.brokersByPct(res))
+          if (entryIn[x] && !changed[x]) order.push_back(x);
+        for (const auto& o : entryKey) {
+          if (!entryIn[o.first]) continue;
+          auto less = [&](int y, const std::pair<int, double>& k) {
+            const int c = jcmpDouble(m.pct(y, res), k.second);
+            return c ? c < 0 : m.bId[y] < m.bId[k.first];
+          };
+          order.insert(std::lower_bound(order.begin(), order.end(), o, less), o.first);
+        }
+        rank.assign(m.B, 0);
+        for (size_t i = 0; i < order.size(); ++i) rank[order[i]] = (int32_t)i;
+        std::vector<int> ids;
+        ids.reserve(order.size());
+        for (int x = 0; x < m.B; ++x)
+          if (entryIn[x]) ids.push_back(x);
+        cand.buildByRank(ids, rank);
+      }
       for (const Step& h : hist) {
         for (auto& o : ovr)
           if (o.first == h.dst) o.second = h.keyAfter;
@@ -862,14 +891,10 @@ class ResourceDistribution : public GoalImpl {
     if (m.numNew > 0 && !m.isNew(b)) return true;
     const bool followersOnly = e.opt.anyExclLead && e.opt.exclLead[b];
     auto rcmp = [this, &m](int x, int y) { return cmpBroker(m, y, x); };
-    // SortedReplicas are lazily initialised (SortedReplicas.java:47-193), so registering a candidate broker's
-    // set when it is first polled is equivalent to trackSortedReplicas over all candidates up front.
-    int id = -1;
-    std::vector<int> trackedCb;
-    auto trackCb = [&](int c) {
-      id = trackCandidates(e, c, 0.0, false, followersOnly, res == R_NW_OUT, immOnly);
-      trackedCb.push_back(c);
-    };
+    // SortedReplicas are lazily initialised (SortedReplicas.java:47-193) and every key change re-inserts the
+    // replica, so a polled candidate broker's live view is the snapshot of a fresh initialisation: nothing needs
+    // to be tracked (the reference restarts its live iteration with indicesToSkip after an accept, :484-522).
+    const Model::Spec spec = candidateSpec(e, 0.0, false, followersOnly, res == R_NW_OUT, immOnly);
     LiveQueue<decltype(rcmp)> pq(rcmp);
     {
       PhaseScope pi(PH_PQ_INIT);
@@ -888,30 +913,28 @@ class ResourceDistribution : public GoalImpl {
     struct Seg {
       int cb;
       size_t skip;
-      size_t len;
+      std::shared_ptr<const std::vector<int32_t>> v;
+      size_t len() const { return v->size() > skip ? v->size() - skip : 0; }
     };
     std::vector<Seg> segs;
     std::vector<int32_t> flat;
     size_t target = 256;
     bool haveCur = false;
-    Seg cur{0, 0, 0};
+    Seg cur{0, 0, nullptr};
     auto cond = [&]() { return action == DA_MOVE || m.bNlead[b] != m.nrep(b); };
     while (haveCur || (!pq.empty() && cond())) {
       segs.clear();
       flat.clear();
       if (haveCur) {
-        const auto& v = m.sorted(cur.cb, id);
-        cur.len = v.size() > cur.skip ? v.size() - cur.skip : 0;
+        cur.v = m.snapshot(cur.cb, spec);
         segs.push_back(cur);
-        for (size_t q = cur.skip; q < v.size(); ++q) flat.push_back(v[q]);
+        flat.insert(flat.end(), cur.v->begin() + std::min(cur.skip, cur.v->size()), cur.v->end());
         haveCur = false;
       }
       while (!pq.empty() && (segs.empty() || flat.size() < target) && cond()) {
         const int cb = pq.poll();
-        trackCb(cb);
-        const auto& v = m.sorted(cb, id);
-        segs.push_back({cb, 0, v.size()});
-        flat.insert(flat.end(), v.begin(), v.end());
+        segs.push_back({cb, 0, m.snapshot(cb, spec)});
+        flat.insert(flat.end(), segs.back().v->begin(), segs.back().v->end());
       }
       if (segs.empty()) break;
       const int64_t key = cands.empty() ? -1 : e.crossScan(*this, action, flat, 0, cands);
@@ -921,28 +944,24 @@ class ResourceDistribution : public GoalImpl {
       }
       target = 256;
       size_t q = (size_t)key, mi = 0;
-      while (q >= segs[mi].len) {
-        q -= segs[mi].len;
+      while (q >= segs[mi].len()) {
+        q -= segs[mi].len();
         ++mi;
       }
       const Seg hit = segs[mi];
       const size_t idx = hit.skip + q;  // index in cb's live view == iteratedIndices at the hit
-      const int r = m.sorted(hit.cb, id)[idx];
+      const int r = (*hit.v)[idx];
       if (action == DA_MOVE) m.relocateReplica(m.rPart[r], hit.cb, b);
       else m.relocateLeadership(m.rPart[r], hit.cb, b);
-      if (aboveLower(m, b)) {
-        for (int c : trackedCb) m.untrack(c, id);
-        return false;
-      }
+      if (aboveLower(m, b)) return false;
       for (size_t t = mi + 1; t < segs.size(); ++t) pq.add(segs[t].cb);  // un-poll speculative brokers
       if (!pq.empty() && m.pct(hit.cb, res) < m.pct(pq.peek(), res)) {
         pq.add(hit.cb);
       } else {
-        cur = {hit.cb, idx, 0};
+        cur = {hit.cb, idx, nullptr};
         haveCur = true;
       }
     }
-    for (int c : trackedCb) m.untrack(c, id);
     return true;
   }
 
@@ -950,13 +969,12 @@ class ResourceDistribution : public GoalImpl {
     PhaseScope ps(PH_SWAP);
     Model& m = e.m;
     if (!m.alive(b) || (e.opt.anyExclMove && e.opt.exclMove[b])) return true;
-    const int srcId = out ? trackCandidates(e, b, 0.0, false, false, res == R_NW_OUT, immOnly)
-                          : trackCandidates(e, b, 1.7976931348623157e308, true, false, false, immOnly);
-    if (m.sorted(b, srcId).empty()) {
-      m.untrack(b, srcId);
-      return true;
-    }
-    const double limit = firstOnlineLoad(m, m.sorted(b, srcId), out);
+    // The source's and the polled candidates' SortedReplicas are read as fresh snapshots (see moveIn): their
+    // names are distinct and untracked when the swap phase ends.
+    const Model::Spec srcSpec = out ? candidateSpec(e, 0.0, false, false, res == R_NW_OUT, immOnly)
+                                    : candidateSpec(e, 1.7976931348623157e308, true, false, false, immOnly);
+    if (m.snapshot(b, srcSpec)->empty()) return true;
+    const double limit = firstOnlineLoad(m, *m.snapshot(b, srcSpec), out);
     const bool followersOnly = e.opt.anyExclLead && e.opt.exclLead[b];
     auto cmpUp = [this, &m](int x, int y) { return cmpBroker(m, x, y); };
     auto cmpDown = [this, &m](int x, int y) { return cmpBroker(m, y, x); };
@@ -968,7 +986,6 @@ class ResourceDistribution : public GoalImpl {
       if (out) pqUp.add(x);
       else pqDown.add(x);
     };
-    int candId = -1;
     {
       PhaseScope pi(PH_PQ_INIT);
       // candidates: out = alive brokers under the upper limit hosting replicas (a Collectors.toSet() whose
@@ -1004,11 +1021,8 @@ class ResourceDistribution : public GoalImpl {
         }
       }
     }
-    // candidate brokers' SortedReplicas are registered when first polled (lazy init, as in moveIn)
-    auto trackCb = [&](int c) {
-      candId = out ? trackCandidates(e, c, limit, true, followersOnly, false, immOnly)
-                   : trackCandidates(e, c, limit, false, followersOnly, res == R_NW_OUT, immOnly);
-    };
+    const Model::Spec candSpec = out ? candidateSpec(e, limit, true, followersOnly, false, immOnly)
+                                     : candidateSpec(e, limit, false, followersOnly, res == R_NW_OUT, immOnly);
     std::vector<int32_t> srcs, cbOff, cbRep, polled;
     size_t target = 4;
     while (!pqEmpty()) {
@@ -1018,12 +1032,11 @@ class ResourceDistribution : public GoalImpl {
       while (!pqEmpty() && (polled.empty() || polled.size() < target)) {
         const int cb = pqPoll();
         polled.push_back(cb);
-        trackCb(cb);
-        const auto& v = m.sorted(cb, candId);
-        cbRep.insert(cbRep.end(), v.begin(), v.end());
+        const auto v = m.snapshot(cb, candSpec);
+        cbRep.insert(cbRep.end(), v->begin(), v->end());
         cbOff.push_back((int32_t)cbRep.size());
       }
-      srcs = m.sorted(b, srcId);
+      srcs = *m.snapshot(b, srcSpec);
       const int64_t key = e.swapScan(*this, srcs, cbOff, cbRep);
       if (key < 0) {
         target = std::min<size_t>(target * 2, 1024);
@@ -1041,14 +1054,10 @@ class ResourceDistribution : public GoalImpl {
       m.relocateReplica(m.rPart[sr], b, cb);
       m.relocateReplica(dp, cb, b);
       const bool done = out ? underUpper(m, b, upperThr) : aboveLower(m, b);
-      if (done) {
-        m.clearTracked();
-        return false;
-      }
+      if (done) return false;
       for (size_t t = mi + 1; t < polled.size(); ++t) pqAdd(polled[t]);  // un-poll speculative brokers
       pqAdd(cb);
     }
-    m.clearTracked();
     return true;
   }
   bool swapOut(Engine& e, int b, bool immOnly) { return swapCommon(e, b, true, immOnly); }

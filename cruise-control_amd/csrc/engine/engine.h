@@ -75,7 +75,7 @@ class Engine {
   Shard shard;
   std::vector<std::unique_ptr<GoalImpl>> optimized;  // optimized goals, priority order
   int64_t candidates = 0;
-  std::vector<uint8_t> scratchB;  // per-broker scratch flags for the goal drivers
+  std::vector<uint8_t> scratchB, scratchB2;  // per-broker scratch flags for the goal drivers
   std::vector<int32_t> topicUpper, topicLower;  // TopicReplicaDistributionGoal limits (device copy: setTopicLimits)
 
   // one Goal.optimize; throws OptimizationFailure / StateError

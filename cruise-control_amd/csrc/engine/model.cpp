@@ -492,42 +492,42 @@ void Model::clearTracked() {
 }
 void Model::clearTracked(int b) { tracked[b].clear(); }
 
+std::shared_ptr<const std::vector<int32_t>> Model::snapshot(int b, const Spec& s) {
+  PhaseScope ps(PH_SORTED_INIT);
+  auto& cache = sortedCache[b];
+  for (auto& c : cache)
+    if (c.ver == bVer[b] && c.spec == s) return c.v;
+  auto v = std::make_shared<std::vector<int32_t>>();
+  for (int r : bRepl[b])
+    if (selects(s, r)) v->push_back(r);
+  std::sort(v->begin(), v->end(), [&](int x, int y) { return cmpReplica(s, x, y) < 0; });
+  SortedCacheEntry* slot = nullptr;
+  for (auto& c : cache)
+    if (c.spec == s || c.ver != bVer[b]) {
+      slot = &c;
+      break;
+    }
+  if (!slot) {
+    if (cache.size() < 4) {
+      cache.emplace_back();
+      slot = &cache.back();
+    } else {
+      slot = &cache[bVer[b] & 3];
+    }
+  }
+  slot->spec = s;
+  slot->ver = bVer[b];
+  slot->v = v;
+  return v;
+}
+
 const std::vector<int32_t>& Model::sorted(int b, int nameId) {
   for (auto& t : tracked[b])
     if (t.nameId == nameId) {
       if (!t.init) {
-        PhaseScope ps(PH_SORTED_INIT);
         t.init = true;
         t.owned = false;
-        auto& cache = sortedCache[b];
-        for (auto& c : cache)
-          if (c.ver == bVer[b] && c.spec == t.spec) {
-            t.shared = c.v;
-            return t.view();
-          }
-        auto v = std::make_shared<std::vector<int32_t>>();
-        for (int r : bRepl[b])
-          if (selects(t.spec, r)) v->push_back(r);
-        const Spec& s = t.spec;
-        std::sort(v->begin(), v->end(), [&](int x, int y) { return cmpReplica(s, x, y) < 0; });
-        t.shared = v;
-        SortedCacheEntry* slot = nullptr;
-        for (auto& c : cache)
-          if (c.spec == t.spec || c.ver != bVer[b]) {
-            slot = &c;
-            break;
-          }
-        if (!slot) {
-          if (cache.size() < 4) {
-            cache.emplace_back();
-            slot = &cache.back();
-          } else {
-            slot = &cache[bVer[b] & 3];
-          }
-        }
-        slot->spec = t.spec;
-        slot->ver = bVer[b];
-        slot->v = t.shared;
+        t.shared = snapshot(b, t.spec);
       }
       return t.view();
     }

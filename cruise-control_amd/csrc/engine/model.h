@@ -286,6 +286,9 @@ class Model {
   void clearTracked();
   void clearTracked(int b);
   const std::vector<int32_t>& sorted(int b, int nameId);  // lazily initialized live view
+  // Contents a SortedReplicas(b, s) initialised now would have (shared with the initialisation cache): equal to
+  // the live view of a set tracked earlier, because every key change re-inserts the replica.
+  std::shared_ptr<const std::vector<int32_t>> snapshot(int b, const Spec& s);
   bool selects(const Spec& s, int r) const;
   int cmpReplica(const Spec& s, int a, int b) const;
 

@@ -10,7 +10,7 @@ namespace ccmi {
 
 enum Phase {
   PH_RDG_OUT, PH_RDG_IN, PH_RES_OUT, PH_RES_IN, PH_SWAP, PH_DEV_SCAN, PH_DEV_STATS, PH_RELOCATE, PH_CAND_BUILD,
-  PH_SORTED_INIT, PH_UPDATE, PH_PQ_INIT, PH_FLATTEN, PH_TREE_BUILD, PH_ORDER, PH_OTHER_GOALS, PH_COUNT
+  PH_SORTED_INIT, PH_UPDATE, PH_PQ_INIT, PH_FLATTEN, PH_TREE_BUILD, PH_ORDER, PH_OTHER_GOALS, PH_SCAN_STAGE, PH_SCAN_WAIT, PH_COUNT
 };
 
 struct PhaseProf {
@@ -21,7 +21,7 @@ struct PhaseProf {
     static const char* names[PH_COUNT] = {"rdg.moveOut", "rdg.moveIn", "res.moveOut", "res.moveIn", "res.swap",
                                           "device.scan", "device.stats", "relocate", "cand.build", "sorted.init",
                                           "goal.update", "pq.init", "flatten", "tree.build", "order.repair",
-                                          "other.goals"};
+                                          "other.goals", "scan.stage", "scan.wait"};
     if (!on) return;
     std::fprintf(stderr, "[ccmi profile %s]\n", tag);
     for (int i = 0; i < PH_COUNT; ++i)
