@@ -133,9 +133,9 @@ __device__ __forceinline__ void applyRowsBlock(const MutTables& M, int B, int R,
   }
 }
 
-// Stage the update list into LDS (all workgroups) and apply it to HBM (workgroup 0).
-__device__ __forceinline__ void overlayBegin(OverlayLds& ov, const UpdateList& U, const MutTables& M,
-                                             const DevTables& T) {
+// Stage the update list into LDS (every workgroup that evaluates pairs) and apply it to HBM (workgroup 0, which
+// always evaluates the first chunk). Workgroups whose first chunk is already beaten exit without staging.
+__device__ __forceinline__ void overlayStage(OverlayLds& ov, const UpdateList& U) {
   if (threadIdx.x == 0) {
     ov.nb = U.nb;
     ov.nr = U.nr;
@@ -147,6 +147,9 @@ __device__ __forceinline__ void overlayBegin(OverlayLds& ov, const UpdateList& U
     stageRows<PartitionRow, kOvP>(ov.p, U.prows, U.np);
   }
   __syncthreads();
+}
+__device__ __forceinline__ void overlayApply(const OverlayLds& ov, const UpdateList& U, const MutTables& M,
+                                             const DevTables& T) {
   if (blockIdx.x == 0 && (U.nb | U.nr | U.np | U.nt))
     applyRowsBlock(M, T.B, T.R, ov.b, ov.nb, ov.r, ov.nr, T.pOff, ov.p, ov.np, U.tdel, U.nt, threadIdx.x,
                    blockDim.x);
@@ -434,12 +437,17 @@ __global__ __launch_bounds__(kBlock) void scan_cross(DevTables T, MutTables Mt, 
                                                      unsigned int* __restrict__ done,
                                                      unsigned long long* __restrict__ mail, unsigned long long seq) {
   __shared__ OverlayLds ov;
-  overlayBegin(ov, U, Mt, T);
+  bool staged = false;
   const uint32_t total = (uint32_t)K * (uint32_t)Nr;
   for (uint32_t base = blockIdx.x * kBlock; base < total; base += gridDim.x * kBlock) {
     const uint32_t kb = base / (uint32_t)Nr;
     const unsigned long long keyBase = (unsigned long long)kb * N + c0 + (base - kb * (uint32_t)Nr);
     if (blockBest(result) <= keyBase) break;  // an earlier pair already won: nothing later can (block-uniform)
+    if (!staged) {
+      overlayStage(ov, U);
+      overlayApply(ov, U, Mt, T);
+      staged = true;
+    }
     unsigned long long local = kNone;
     const uint32_t q = base + threadIdx.x;
     if (q < total) {
@@ -536,9 +544,14 @@ __global__ __launch_bounds__(kBlock) void scan_pairs(DevTables T, MutTables Mt, 
                                                      unsigned int* __restrict__ done,
                                                      unsigned long long* __restrict__ mail, unsigned long long seq) {
   __shared__ OverlayLds ov;
-  overlayBegin(ov, U, Mt, T);
+  bool staged = false;
   for (int base = blockIdx.x * kBlock; base < n; base += gridDim.x * kBlock) {
     if (blockBest(result) <= (unsigned long long)(keyBase + base)) break;
+    if (!staged) {
+      overlayStage(ov, U);
+      overlayApply(ov, U, Mt, T);
+      staged = true;
+    }
     unsigned long long local = kNone;
     const int q = base + threadIdx.x;
     if (q < n) {
@@ -575,9 +588,14 @@ __global__ __launch_bounds__(256) void prep(MutTables M, int B, int R, const int
 }
 
 // ------------------------------------------------------------------------------------------------ launchers
-static unsigned gridFor(uint64_t work, uint64_t perBlock) {
+// First-fit scans cap their grid at what the chip holds resident at once (256 CUs x 4 workgroups of 256 threads
+// at the scan kernels' register budget): the blocks then sweep the pair space in order, chunk c in iteration
+// c / grid, and each chunk start is checked against the current best before any work — a launch whose winner
+// is early costs one chunk per block, and no workgroup is dispatched only to exit.
+constexpr uint64_t kResidentBlocks = 1024;
+static unsigned gridFor(uint64_t work, uint64_t perBlock, uint64_t cap = 4096) {
   uint64_t blocks = (work + perBlock - 1) / perBlock;
-  if (blocks > 4096) blocks = 4096;
+  if (blocks > cap) blocks = cap;
   if (blocks == 0) blocks = 1;
   return (unsigned)blocks;
 }
@@ -586,7 +604,7 @@ hipError_t launchScanCross(const DevTables& T, const MutTables& M, const UpdateL
                            const int32_t* reps, const int32_t* cands, int K, int Nr, int N, int c0,
                            unsigned long long* result, unsigned int* done, unsigned long long* mail,
                            unsigned long long seq, hipStream_t st) {
-  const unsigned blocks = gridFor((uint64_t)K * (uint64_t)Nr, (uint64_t)kBlock);
+  const unsigned blocks = gridFor((uint64_t)K * (uint64_t)Nr, (uint64_t)kBlock, kResidentBlocks);
   hipLaunchKernelGGL(scan_cross, dim3(blocks), dim3(kBlock), 0, st, T, M, U, prog, reps, cands, K, Nr, N, c0, result,
                      done, mail, seq);
   return hipGetLastError();
@@ -609,7 +627,7 @@ hipError_t launchScanSwap(const DevTables& T, const DevProgram& prog, const int3
 hipError_t launchScanPairs(const DevTables& T, const MutTables& M, const UpdateList& U, const DevProgram& prog,
                            const int32_t* pr, const int32_t* pb, int n, int keyBase, unsigned long long* result,
                            unsigned int* done, unsigned long long* mail, unsigned long long seq, hipStream_t st) {
-  const unsigned blocks = gridFor((uint64_t)n, (uint64_t)kBlock);
+  const unsigned blocks = gridFor((uint64_t)n, (uint64_t)kBlock, kResidentBlocks);
   hipLaunchKernelGGL(scan_pairs, dim3(blocks), dim3(kBlock), 0, st, T, M, U, prog, pr, pb, n, keyBase, result, done,
                      mail, seq);
   return hipGetLastError();
