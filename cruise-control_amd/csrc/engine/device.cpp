@@ -4,6 +4,8 @@
 
 #include <hip/hip_runtime.h>
 
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <stdexcept>
 
@@ -59,7 +61,8 @@ Device::Device(int ordinal, int B, int R, int P, int T, int maxGoalSlots)
   dalloc(&bNrep_, B);
   dalloc(&bNlead_, B);
   dalloc(&bAlive_, B);
-  dalloc(&allowed_, (size_t)G_ * B);
+  dalloc(&allowed_, (size_t)B);
+  allowedHost_.assign(B, 0u);
   dalloc(&allowedAlive_, ldB_);
   dalloc(&rUtil_, (size_t)4 * R);
   dalloc(&rPart_, R);
@@ -80,7 +83,7 @@ Device::Device(int ordinal, int B, int R, int P, int T, int maxGoalSlots)
   dalloc(&dDone_, 4);
   hipCheck(hipMalloc(&topicScratch_, (size_t)(T ? T : 1) * sizeof(TopicPartial)), "hipMalloc");
   hipCheck(hipMalloc(&statsOut_, 1024), "hipMalloc");
-  hipCheck(hipMemset(allowed_, 0, (size_t)G_ * B), "hipMemset");
+  hipCheck(hipMemset(allowed_, 0, (size_t)B * sizeof(uint32_t)), "hipMemset");
   hipCheck(hipMemset(dDone_, 0, 4 * sizeof(unsigned int)), "hipMemset");
   hipCheck(hipMemset(dResult_, 0xff, 2 * sizeof(unsigned long long)), "hipMemset");
   // host-coherent (fine-grained) mapped memory: kernels read the staging area and write the mailbox directly
@@ -89,6 +92,10 @@ Device::Device(int ordinal, int B, int R, int P, int T, int maxGoalSlots)
   std::memset(hResult_, 0, 1024);
   ensureStage(1 << 20);
   ensureReq(1 << 20);
+  if (std::getenv("CCMI_STAMPS")) {
+    dalloc(&stamps_, 1024 * 8);
+    hipCheck(hipMemset(stamps_, 0, 1024 * 8 * sizeof(unsigned long long)), "hipMemset");
+  }
   hipCheck(hipEventCreate((hipEvent_t*)&ev0_), "hipEventCreate");
   hipCheck(hipEventCreate((hipEvent_t*)&ev1_), "hipEventCreate");
 }
@@ -96,6 +103,24 @@ Device::Device(int ordinal, int B, int R, int P, int T, int maxGoalSlots)
 Device::~Device() {
   (void)hipSetDevice(ordinal_);
   if (ST) (void)hipStreamSynchronize(ST);
+  if (stamps_) {  // average in-launch phase times of the last 1024 cross/pair scans (workgroup 0)
+    std::vector<unsigned long long> h(1024 * 8);
+    if (hipMemcpy(h.data(), stamps_, h.size() * 8, hipMemcpyDeviceToHost) == hipSuccess) {
+      double acc[5] = {0, 0, 0, 0, 0};
+      int n = 0;
+      for (int i = 0; i < 1024; ++i) {
+        const unsigned long long* t = &h[i * 8];
+        if (!t[0] || !t[1] || !t[2] || !t[3] || !t[4] || !t[5] || t[5] < t[0]) continue;
+        for (int k = 0; k < 5; ++k) acc[k] += (double)(t[k + 1] - t[k]) * 0.01;  // 100 MHz -> us
+        n++;
+      }
+      if (n)
+        std::fprintf(stderr, "[ccmi stamps] %d launches: stage %.2f us, loads+predicate %.2f us, blockMin %.2f us, "
+                             "tail %.2f us, publish %.2f us\n",
+                     n, acc[0] / n, acc[1] / n, acc[2] / n, acc[3] / n, acc[4] / n);
+    }
+    (void)hipFree(stamps_);
+  }
   void* ps[] = {bUtil_, bCap_, bPot_, bNrep_, bNlead_, bAlive_, allowed_, allowedAlive_, rUtil_, rPart_, rBroker_,
                 rOrig_, rFlags_, pOff_, pBrokers_, topicCount_, topicNrep_, topicScratch_, statsOut_, dReq_,
                 rowVisited_, dResult_, dDone_, bRack_, bLeadNwIn_, pTopic_, pLeadNwOut_, tUpper_, tLower_};
@@ -140,7 +165,7 @@ DevTables Device::tables() const {
   t.bCap = bCap_;
   t.bNrep = bNrep_;
   t.bAlive = bAlive_;
-  t.allowed = allowed_;
+  t.allowedBits = allowed_;
   t.rUtil = rUtil_;
   t.rPart = rPart_;
   t.rBroker = rBroker_;
@@ -157,6 +182,7 @@ DevTables Device::tables() const {
   t.topicCount = topicCount_;
   t.tUpper = tUpper_;
   t.tLower = tLower_;
+  t.stamps = stamps_;
   t.B = B_;
   t.R = R_;
   t.P = P_;
@@ -198,7 +224,10 @@ void Device::uploadDynamic(const double* bUtilRM, const int32_t* bNrep, const in
 
 void Device::setAllowed(int slot, const uint8_t* allowedB) {
   if (slot < 0 || slot >= G_) throw std::runtime_error("goal slot out of range");
-  hipCheck(hipMemcpyAsync(allowed_ + (size_t)slot * B_, allowedB, B_, hipMemcpyHostToDevice, ST), "upload allowed");
+  for (int b = 0; b < B_; ++b)
+    allowedHost_[b] = (allowedHost_[b] & ~(1u << slot)) | (allowedB[b] ? (1u << slot) : 0u);
+  hipCheck(hipMemcpyAsync(allowed_, allowedHost_.data(), sizeof(uint32_t) * B_, hipMemcpyHostToDevice, ST),
+           "upload allowed");
   hipCheck(hipStreamSynchronize(ST), "sync");
 }
 

@@ -80,7 +80,9 @@ class Device {
   int32_t *pOff_ = nullptr, *pBrokers_ = nullptr, *topicCount_ = nullptr, *topicNrep_ = nullptr;
   int32_t *bRack_ = nullptr, *pTopic_ = nullptr, *tUpper_ = nullptr, *tLower_ = nullptr;
   double *bLeadNwIn_ = nullptr, *pLeadNwOut_ = nullptr;
-  uint8_t *bAlive_ = nullptr, *allowed_ = nullptr, *rFlags_ = nullptr, *allowedAlive_ = nullptr;
+  uint8_t *bAlive_ = nullptr, *rFlags_ = nullptr, *allowedAlive_ = nullptr;
+  uint32_t* allowed_ = nullptr;  // [B] goal-slot bit masks
+  std::vector<uint32_t> allowedHost_;
   void *topicScratch_ = nullptr, *statsOut_ = nullptr;
   // staging (host-coherent, mapped) and the request copy in HBM
   char* hStage_ = nullptr;
@@ -112,6 +114,7 @@ class Device {
   const char* stageScan(const Staged& g, size_t req, bool readsTopicCounts, UpdateList& u);
   void waitMail(unsigned long long seq);
   int64_t finishScan();
+  unsigned long long* stamps_ = nullptr;
   int32_t* rowVisited_ = nullptr;
   size_t rowVisitedCap_ = 0;
 };

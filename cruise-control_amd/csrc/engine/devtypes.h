@@ -7,7 +7,7 @@
 //   replica rows  rUtil[4][R] f64, rPart/rBroker/rOrig[R] i32, rFlags[R] u8 (bit0 leader, bit1 orig-offline)
 //   partitions    pOff[P+1] i32, pBrokers[R] i32 (current broker of every replica slot, Partition._replicas order)
 //   topics        topicCount[T][B] i32 (dense Broker._topicReplicas sizes, for ClusterModelStats topic stats)
-//   goal state    allowed[G][B] u8 (per optimized goal: _brokersAllowedReplicaMove, frozen at initGoalState)
+//   goal state    allowedBits[B] u32 (bit g: broker in goal slot g's _brokersAllowedReplicaMove, frozen at init)
 //   more broker   bRack[B] i32 (static), bLeadNwIn[B] f64 (Broker._leadershipLoadForNwResources NW_IN)
 //   more part.    pTopic[P] i32 (static), pLeadNwOut[P] f64 (NW_OUT utilization of the partition's leader)
 //   topic limits  tUpper[T], tLower[T] i32 (TopicReplicaDistributionGoal balance limits, frozen at init)
@@ -50,7 +50,7 @@ struct DevGoal {
   int32_t upper, lower;        // ReplicaDistributionAbstractGoal._balanceUpperLimit/_balanceLowerLimit
   double upperThr, lowerThr;   // ResourceDistributionGoal._balanceUpperThreshold/_balanceLowerThreshold
   int32_t fixOffline;          // _fixOfflineReplicasOnly
-  int32_t allowedSlot;         // row of DevTables.allowed
+  int32_t allowedSlot;         // bit of DevTables.allowedBits
   int32_t selfHealing;         // ReplicaCapacityGoal._isSelfHealingMode (unused by predicates; kept for parity)
   int32_t pad0;
   int64_t maxReplicas;         // BalancingConstraint.maxReplicasPerBroker (ReplicaCapacityGoal)
@@ -75,7 +75,7 @@ struct DevTables {
   const double* bCap;
   const int32_t* bNrep;
   const uint8_t* bAlive;
-  const uint8_t* allowed;
+  const uint32_t* allowedBits;
   const double* rUtil;
   const int32_t* rPart;
   const int32_t* rBroker;
@@ -92,6 +92,7 @@ struct DevTables {
   const int32_t* topicCount;  // [T][ldB]
   const int32_t* tUpper;
   const int32_t* tLower;
+  unsigned long long* stamps;  // diagnostics (CCMI_STAMPS=1): s_memrealtime stamps of workgroup 0, else null
   int32_t B, R, P, ldB;
 };
 

@@ -32,7 +32,7 @@ struct DevView {
   __device__ __forceinline__ double bcap(int b, int res) const { return t.bCap[(size_t)res * t.B + b]; }
   __device__ __forceinline__ int nrep(int b) const { return t.bNrep[b]; }
   __device__ __forceinline__ bool alive(int b) const { return t.bAlive[b] != 0; }
-  __device__ __forceinline__ bool allowed(int slot, int b) const { return t.allowed[(size_t)slot * t.B + b] != 0; }
+  __device__ __forceinline__ bool allowed(int slot, int b) const { return (t.allowedBits[b] >> slot) & 1u; }
   __device__ __forceinline__ double ru(int r, int res) const { return t.rUtil[(size_t)res * t.R + r]; }
   __device__ __forceinline__ int flags(int r) const { return t.rFlags[r]; }
   __device__ __forceinline__ int rbroker(int r) const { return t.rBroker[r]; }
@@ -254,11 +254,7 @@ struct PreView {
     scap1 = t.bCap[(size_t)t.B + src];
     scap2 = t.bCap[(size_t)2 * t.B + src];
     scap3 = t.bCap[(size_t)3 * t.B + src];
-    srcAllowed = 0;
-    for (int i = 0; i < prog.nGoals; ++i) {
-      const int slot = prog.goals[i].allowedSlot;
-      srcAllowed |= (t.allowed[(size_t)slot * t.B + src] ? 1u : 0u) << slot;
-    }
+    srcAllowed = t.allowedBits[src];
     if (prog.needs & NEED_RACK) {
       prk0 = pb0 >= 0 ? t.bRack[pb0] : -1;
       prk1 = pb1 >= 0 ? t.bRack[pb1] : -1;
@@ -373,6 +369,15 @@ struct PreView {
 };
 
 constexpr int kBlock = 256;
+
+// Diagnostics: workgroup 0 / thread 0 records s_memrealtime (100 MHz) at fixed points of a launch.
+#define CCMI_STAMP(T, seq, i)                                                                         \
+  do {                                                                                               \
+    if ((T).stamps && blockIdx.x == 0 && threadIdx.x == 0) {                                          \
+      __builtin_amdgcn_s_waitcnt(0); /* outstanding loads of this lane land before the stamp */        \
+      (T).stamps[((seq)&1023ull) * 8 + (i)] = __builtin_amdgcn_s_memrealtime();                       \
+    }                                                                                                 \
+  } while (0)
 constexpr unsigned long long kNone = ~0ull;
 
 __device__ __forceinline__ unsigned long long waveMin(unsigned long long v) {
@@ -437,6 +442,7 @@ __global__ __launch_bounds__(kBlock) void scan_cross(DevTables T, MutTables Mt, 
                                                      unsigned int* __restrict__ done,
                                                      unsigned long long* __restrict__ mail, unsigned long long seq) {
   __shared__ OverlayLds ov;
+  CCMI_STAMP(T, seq, 0);
   bool staged = false;
   const uint32_t total = (uint32_t)K * (uint32_t)Nr;
   for (uint32_t base = blockIdx.x * kBlock; base < total; base += gridDim.x * kBlock) {
@@ -447,6 +453,7 @@ __global__ __launch_bounds__(kBlock) void scan_cross(DevTables T, MutTables Mt, 
       overlayStage(ov, U);
       overlayApply(ov, U, Mt, T);
       staged = true;
+      CCMI_STAMP(T, seq, 1);
     }
     unsigned long long local = kNone;
     const uint32_t q = base + threadIdx.x;
@@ -459,13 +466,17 @@ __global__ __launch_bounds__(kBlock) void scan_cross(DevTables T, MutTables Mt, 
       const bool inList = prog.filter != FILTER_RACK_AWARE || v.rackEligible();
       if (inList && moveCandidateAccepted(prog, v, v.r, v.dst)) local = (unsigned long long)k * N + c0 + j;
     }
+    CCMI_STAMP(T, seq, 2);
     const unsigned long long m = blockMin(local);
+    CCMI_STAMP(T, seq, 3);
     if (m != kNone) {
       if (threadIdx.x == 0) atomicMin(result, m);
       break;
     }
   }
+  CCMI_STAMP(T, seq, 4);
   publishLast(result, done, mail, seq);
+  CCMI_STAMP(T, seq, 5);
 }
 
 // One wavefront per row (m, s). rowsPerBlock = kBlock / 64.
@@ -544,6 +555,7 @@ __global__ __launch_bounds__(kBlock) void scan_pairs(DevTables T, MutTables Mt, 
                                                      unsigned int* __restrict__ done,
                                                      unsigned long long* __restrict__ mail, unsigned long long seq) {
   __shared__ OverlayLds ov;
+  CCMI_STAMP(T, seq, 0);
   bool staged = false;
   for (int base = blockIdx.x * kBlock; base < n; base += gridDim.x * kBlock) {
     if (blockBest(result) <= (unsigned long long)(keyBase + base)) break;
@@ -551,6 +563,7 @@ __global__ __launch_bounds__(kBlock) void scan_pairs(DevTables T, MutTables Mt, 
       overlayStage(ov, U);
       overlayApply(ov, U, Mt, T);
       staged = true;
+      CCMI_STAMP(T, seq, 1);
     }
     unsigned long long local = kNone;
     const int q = base + threadIdx.x;
@@ -560,13 +573,17 @@ __global__ __launch_bounds__(kBlock) void scan_pairs(DevTables T, MutTables Mt, 
       v.loadDst(T, prog, pb[q], ov);
       if (moveCandidateAccepted(prog, v, v.r, v.dst)) local = (unsigned long long)(keyBase + q);
     }
+    CCMI_STAMP(T, seq, 2);
     const unsigned long long m = blockMin(local);
+    CCMI_STAMP(T, seq, 3);
     if (m != kNone) {
       if (threadIdx.x == 0) atomicMin(result, m);
       break;
     }
   }
+  CCMI_STAMP(T, seq, 4);
   publishLast(result, done, mail, seq);
+  CCMI_STAMP(T, seq, 5);
 }
 
 __global__ __launch_bounds__(256) void prep(MutTables M, int B, int R, const int32_t* __restrict__ pOff,

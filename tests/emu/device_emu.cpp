@@ -29,7 +29,8 @@ struct Emu {
   std::vector<double> bUtil, bCap, bPot, rUtil, bLeadNwIn, pLeadNwOut;
   std::vector<int32_t> bNrep, bNlead, rPart, rBroker, rOrig, pOff, pBrokers, topicCount, topicNrep;
   std::vector<int32_t> bRack, pTopic, tUpper, tLower;
-  std::vector<uint8_t> bAlive, allowed, rFlags;
+  std::vector<uint8_t> bAlive, rFlags;
+  std::vector<uint32_t> allowed;
 };
 struct View {
   const Emu& e;
@@ -37,7 +38,7 @@ struct View {
   double bcap(int b, int res) const { return e.bCap[(size_t)res * e.B + b]; }
   int nrep(int b) const { return e.bNrep[b]; }
   bool alive(int b) const { return e.bAlive[b] != 0; }
-  bool allowed(int slot, int b) const { return e.allowed[(size_t)slot * e.B + b] != 0; }
+  bool allowed(int slot, int b) const { return (e.allowed[b] >> slot) & 1u; }
   double ru(int r, int res) const { return e.rUtil[(size_t)res * e.R + r]; }
   int flags(int r) const { return e.rFlags[r]; }
   int rbroker(int r) const { return e.rBroker[r]; }
@@ -91,7 +92,7 @@ Device::Device(int ordinal, int B, int R, int P, int T, int maxGoalSlots)
   e->T = T;
   e->ldB = ldB_;
   e->G = maxGoalSlots;
-  e->allowed.assign((size_t)maxGoalSlots * B, 0);
+  e->allowed.assign(B, 0u);
   st_ = e;
 }
 Device::~Device() { delete static_cast<Emu*>(st_); }
@@ -128,7 +129,8 @@ void Device::uploadDynamic(const double* bUtilRM, const int32_t* bNrep, const in
   e.topicCount.assign(tc, tc + (size_t)T_ * ldB_);
 }
 void Device::setAllowed(int slot, const uint8_t* a) {
-  std::memcpy(E(st_).allowed.data() + (size_t)slot * B_, a, B_);
+  auto& al = E(st_).allowed;
+  for (int b = 0; b < B_; ++b) al[b] = (al[b] & ~(1u << slot)) | (a[b] ? (1u << slot) : 0u);
 }
 void Device::setTopicLimits(const int32_t* upper, const int32_t* lower) {
   E(st_).tUpper.assign(upper, upper + T_);
