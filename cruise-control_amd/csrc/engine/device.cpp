@@ -26,12 +26,11 @@ hipError_t launchScanSwap(const DevTables& T, const DevProgram& prog, const int3
 hipError_t launchScanPairs(const DevTables& T, const MutTables& M, const UpdateList& U, const DevProgram& prog,
                            const int32_t* pr, const int32_t* pb, int n, int keyBase, unsigned long long* result,
                            unsigned int* done, unsigned long long* mail, unsigned long long seq, hipStream_t st);
-hipError_t launchPrep(const MutTables& M, int B, int R, const int32_t* pOff, const UpdateList& U, const int4* req,
-                      int4* dReq, int nReq4, unsigned long long* result, unsigned int* done, hipStream_t st);
-hipError_t launchStats(const StatsParams& P, const int32_t* tc, const int32_t* topicNrep, const double* bUtil,
-                       const double* bCap, const int32_t* bNrep, const int32_t* bNlead, const double* bPot,
-                       const uint8_t* bAlive, const uint8_t* allowedAlive, TopicPartial* scratch, StatsOut* out,
-                       int ldB, hipStream_t st, hipEvent_t evTopic0, hipEvent_t evTopic1);
+hipError_t launchPrep(const MutTables& M, const UpdateList& U, const int4* req, int4* dReq, int nReq4,
+                      unsigned long long* result, unsigned int* done, hipStream_t st);
+hipError_t launchStats(const StatsParams& P, const int32_t* tc, const int32_t* topicNrep, const BrokerRec* brokers,
+                       const uint8_t* allowedAlive, TopicPartial* scratch, StatsOut* out, int ldB, hipStream_t st,
+                       hipEvent_t evTopic0, hipEvent_t evTopic1);
 
 static void hipCheck(hipError_t e, const char* what) {
   if (e != hipSuccess) throw std::runtime_error(std::string("HIP error in ") + what + ": " + hipGetErrorString(e));
@@ -55,35 +54,21 @@ Device::Device(int ordinal, int B, int R, int P, int T, int maxGoalSlots)
   if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
     throw std::runtime_error(std::string("libccmi is built for gfx950, device is ") + prop.gcnArchName);
   hipCheck(hipStreamCreateWithFlags((hipStream_t*)&st_, hipStreamNonBlocking), "hipStreamCreate");
-  dalloc(&bUtil_, (size_t)4 * B);
-  dalloc(&bCap_, (size_t)4 * B);
-  dalloc(&bPot_, B);
-  dalloc(&bNrep_, B);
-  dalloc(&bNlead_, B);
-  dalloc(&bAlive_, B);
-  dalloc(&allowed_, (size_t)B);
+  dalloc(&brokers_, (size_t)B);
+  dalloc(&replicas_, (size_t)R);
+  dalloc(&parts_, (size_t)P);
+  hBrokers_.assign(B, BrokerRec{});
+  hParts_.assign(P, PartitionRec{});
   allowedHost_.assign(B, 0u);
   dalloc(&allowedAlive_, ldB_);
-  dalloc(&rUtil_, (size_t)4 * R);
-  dalloc(&rPart_, R);
-  dalloc(&rBroker_, R);
-  dalloc(&rOrig_, R);
-  dalloc(&rFlags_, R);
-  dalloc(&pOff_, (size_t)P + 1);
-  dalloc(&pBrokers_, R);
   dalloc(&topicCount_, (size_t)T * ldB_);
   dalloc(&topicNrep_, T);
-  dalloc(&bRack_, B);
-  dalloc(&bLeadNwIn_, B);
-  dalloc(&pTopic_, P);
-  dalloc(&pLeadNwOut_, P);
   dalloc(&tUpper_, T);
   dalloc(&tLower_, T);
   dalloc(&dResult_, 4);
   dalloc(&dDone_, 4);
   hipCheck(hipMalloc(&topicScratch_, (size_t)(T ? T : 1) * sizeof(TopicPartial)), "hipMalloc");
   hipCheck(hipMalloc(&statsOut_, 1024), "hipMalloc");
-  hipCheck(hipMemset(allowed_, 0, (size_t)B * sizeof(uint32_t)), "hipMemset");
   hipCheck(hipMemset(dDone_, 0, 4 * sizeof(unsigned int)), "hipMemset");
   hipCheck(hipMemset(dResult_, 0xff, 2 * sizeof(unsigned long long)), "hipMemset");
   // host-coherent (fine-grained) mapped memory: kernels read the staging area and write the mailbox directly
@@ -121,9 +106,8 @@ Device::~Device() {
     }
     (void)hipFree(stamps_);
   }
-  void* ps[] = {bUtil_, bCap_, bPot_, bNrep_, bNlead_, bAlive_, allowed_, allowedAlive_, rUtil_, rPart_, rBroker_,
-                rOrig_, rFlags_, pOff_, pBrokers_, topicCount_, topicNrep_, topicScratch_, statsOut_, dReq_,
-                rowVisited_, dResult_, dDone_, bRack_, bLeadNwIn_, pTopic_, pLeadNwOut_, tUpper_, tLower_};
+  void* ps[] = {brokers_, replicas_, parts_, allowedAlive_, topicCount_, topicNrep_, topicScratch_, statsOut_, dReq_,
+                rowVisited_, dResult_, dDone_, tUpper_, tLower_};
   for (void* p : ps)
     if (p) (void)hipFree(p);
   if (hStage_) (void)hipHostFree(hStage_);
@@ -161,24 +145,9 @@ void Device::ensureReq(size_t bytes) {
 
 DevTables Device::tables() const {
   DevTables t;
-  t.bUtil = bUtil_;
-  t.bCap = bCap_;
-  t.bNrep = bNrep_;
-  t.bAlive = bAlive_;
-  t.allowedBits = allowed_;
-  t.rUtil = rUtil_;
-  t.rPart = rPart_;
-  t.rBroker = rBroker_;
-  t.rOrig = rOrig_;
-  t.rFlags = rFlags_;
-  t.pOff = pOff_;
-  t.pBrokers = pBrokers_;
-  t.bRack = bRack_;
-  t.bNlead = bNlead_;
-  t.bPot = bPot_;
-  t.bLeadNwIn = bLeadNwIn_;
-  t.pTopic = pTopic_;
-  t.pLeadNwOut = pLeadNwOut_;
+  t.brokers = brokers_;
+  t.replicas = replicas_;
+  t.parts = parts_;
   t.topicCount = topicCount_;
   t.tUpper = tUpper_;
   t.tLower = tLower_;
@@ -190,16 +159,25 @@ DevTables Device::tables() const {
   return t;
 }
 
+// Static columns are kept in host copies of the broker / partition records until uploadDynamic packs and
+// uploads the whole records (the caller uploads static columns first).
 void Device::uploadStatic(const double* bCapRM, const int32_t* rPart, const int32_t* rOrig, const int32_t* pOff,
                           const int32_t* topicNrep, const int32_t* bRack, const int32_t* pTopic) {
   hipCheck(hipSetDevice(ordinal_), "hipSetDevice");
-  hipCheck(hipMemcpy(bCap_, bCapRM, sizeof(double) * 4 * B_, hipMemcpyHostToDevice), "upload bCap");
-  hipCheck(hipMemcpy(rPart_, rPart, sizeof(int32_t) * R_, hipMemcpyHostToDevice), "upload rPart");
-  hipCheck(hipMemcpy(rOrig_, rOrig, sizeof(int32_t) * R_, hipMemcpyHostToDevice), "upload rOrig");
-  hipCheck(hipMemcpy(pOff_, pOff, sizeof(int32_t) * (P_ + 1), hipMemcpyHostToDevice), "upload pOff");
+  for (int b = 0; b < B_; ++b) {
+    BrokerRec& x = hBrokers_[b];
+    for (int k = 0; k < 4; ++k) x.cap[k] = bCapRM[(size_t)k * B_ + b];
+    x.rack = bRack[b];
+  }
+  hRPart_.assign(rPart, rPart + R_);
+  hROrig_.assign(rOrig, rOrig + R_);
+  hPOff_.assign(pOff, pOff + P_ + 1);
+  for (int p = 0; p < P_; ++p) {
+    hParts_[p].topic = pTopic[p];
+    hParts_[p].n = pOff[p + 1] - pOff[p];
+  }
+  bRackHost_.assign(bRack, bRack + B_);
   hipCheck(hipMemcpy(topicNrep_, topicNrep, sizeof(int32_t) * T_, hipMemcpyHostToDevice), "upload topicNrep");
-  hipCheck(hipMemcpy(bRack_, bRack, sizeof(int32_t) * B_, hipMemcpyHostToDevice), "upload bRack");
-  hipCheck(hipMemcpy(pTopic_, pTopic, sizeof(int32_t) * P_, hipMemcpyHostToDevice), "upload pTopic");
 }
 
 void Device::uploadDynamic(const double* bUtilRM, const int32_t* bNrep, const int32_t* bNlead, const double* bPot,
@@ -207,26 +185,51 @@ void Device::uploadDynamic(const double* bUtilRM, const int32_t* bNrep, const in
                            const int32_t* rBroker, const uint8_t* rFlags, const int32_t* pBrokers,
                            const double* pLeadNwOut, const int32_t* topicCountDense) {
   hipCheck(hipSetDevice(ordinal_), "hipSetDevice");
-  hipCheck(hipMemcpy(bUtil_, bUtilRM, sizeof(double) * 4 * B_, hipMemcpyHostToDevice), "upload bUtil");
-  hipCheck(hipMemcpy(bNrep_, bNrep, sizeof(int32_t) * B_, hipMemcpyHostToDevice), "upload bNrep");
-  hipCheck(hipMemcpy(bNlead_, bNlead, sizeof(int32_t) * B_, hipMemcpyHostToDevice), "upload bNlead");
-  hipCheck(hipMemcpy(bPot_, bPot, sizeof(double) * B_, hipMemcpyHostToDevice), "upload bPot");
-  hipCheck(hipMemcpy(bAlive_, bAlive, B_, hipMemcpyHostToDevice), "upload bAlive");
-  hipCheck(hipMemcpy(bLeadNwIn_, bLeadNwIn, sizeof(double) * B_, hipMemcpyHostToDevice), "upload bLeadNwIn");
-  hipCheck(hipMemcpy(pLeadNwOut_, pLeadNwOut, sizeof(double) * P_, hipMemcpyHostToDevice), "upload pLeadNwOut");
-  hipCheck(hipMemcpy(rUtil_, rUtilRM, sizeof(double) * 4 * R_, hipMemcpyHostToDevice), "upload rUtil");
-  hipCheck(hipMemcpy(rBroker_, rBroker, sizeof(int32_t) * R_, hipMemcpyHostToDevice), "upload rBroker");
-  hipCheck(hipMemcpy(rFlags_, rFlags, R_, hipMemcpyHostToDevice), "upload rFlags");
-  hipCheck(hipMemcpy(pBrokers_, pBrokers, sizeof(int32_t) * R_, hipMemcpyHostToDevice), "upload pBrokers");
+  for (int b = 0; b < B_; ++b) {
+    BrokerRec& x = hBrokers_[b];
+    for (int k = 0; k < 4; ++k) x.util[k] = bUtilRM[(size_t)k * B_ + b];
+    x.nrep = bNrep[b];
+    x.nlead = bNlead[b];
+    x.pot = bPot[b];
+    x.lbi = bLeadNwIn[b];
+    x.alive = bAlive[b];
+    x.allowedBits = allowedHost_[b];
+  }
+  std::vector<ReplicaRec> reps(R_);
+  for (int r = 0; r < R_; ++r) {
+    ReplicaRec& x = reps[r];
+    std::memset(&x, 0, sizeof(x));
+    for (int k = 0; k < 4; ++k) x.util[k] = rUtilRM[(size_t)k * R_ + r];
+    x.broker = rBroker[r];
+    x.part = hRPart_[r];
+    x.orig = hROrig_[r];
+    x.flags = rFlags[r] | (bAlive[hROrig_[r]] ? 0 : RF_ORIG_DEAD);
+  }
+  for (int p = 0; p < P_; ++p) {
+    PartitionRec& x = hParts_[p];
+    for (int k = 0; k < kMaxRf; ++k) {
+      const bool in = k < x.n;
+      x.brokers[k] = in ? pBrokers[hPOff_[p] + k] : -1;
+      x.racks[k] = (int16_t)(in ? bRackHost_[x.brokers[k]] : -1);
+    }
+    x.leadNwOut = pLeadNwOut[p];
+  }
+  hipCheck(hipMemcpy(brokers_, hBrokers_.data(), sizeof(BrokerRec) * B_, hipMemcpyHostToDevice), "upload brokers");
+  hipCheck(hipMemcpy(replicas_, reps.data(), sizeof(ReplicaRec) * R_, hipMemcpyHostToDevice), "upload replicas");
+  hipCheck(hipMemcpy(parts_, hParts_.data(), sizeof(PartitionRec) * P_, hipMemcpyHostToDevice), "upload partitions");
   hipCheck(hipMemcpy(topicCount_, topicCountDense, sizeof(int32_t) * (size_t)T_ * ldB_, hipMemcpyHostToDevice),
            "upload topicCount");
+  hRPart_.clear();
+  hROrig_.clear();
 }
 
 void Device::setAllowed(int slot, const uint8_t* allowedB) {
   if (slot < 0 || slot >= G_) throw std::runtime_error("goal slot out of range");
   for (int b = 0; b < B_; ++b)
     allowedHost_[b] = (allowedHost_[b] & ~(1u << slot)) | (allowedB[b] ? (1u << slot) : 0u);
-  hipCheck(hipMemcpyAsync(allowed_, allowedHost_.data(), sizeof(uint32_t) * B_, hipMemcpyHostToDevice, ST),
+  // strided write of BrokerRec::allowedBits (the rest of every record is left alone)
+  hipCheck(hipMemcpy2DAsync(&brokers_[0].allowedBits, sizeof(BrokerRec), allowedHost_.data(), sizeof(uint32_t),
+                            sizeof(uint32_t), B_, hipMemcpyHostToDevice, ST),
            "upload allowed");
   hipCheck(hipStreamSynchronize(ST), "sync");
 }
@@ -273,7 +276,7 @@ Device::Staged Device::packUpdates(size_t extra) {
 void Device::launchPrepFor(const Staged& g, size_t reqBytes, bool scan) {
   const int nReq4 = (int)(align16(reqBytes) / 16);
   if (nReq4) ensureReq((size_t)nReq4 * 16);
-  hipCheck(launchPrep(mutTables(), B_, R_, pOff_, stagedList(g), (const int4*)(hStageDev_ + g.end), (int4*)dReq_, nReq4,
+  hipCheck(launchPrep(mutTables(), stagedList(g), (const int4*)(hStageDev_ + g.end), (int4*)dReq_, nReq4,
                       scan ? dResult_ : nullptr, scan ? dDone_ : nullptr, ST),
            "prep");
 }
@@ -346,8 +349,7 @@ UpdateList Device::overlayFor(const Staged& g) const {
 }
 
 MutTables Device::mutTables() const {
-  return MutTables{bUtil_, bNrep_, bNlead_, bPot_, bLeadNwIn_, pLeadNwOut_, bAlive_, rUtil_, rBroker_, rFlags_,
-                   pBrokers_, topicCount_, ldB_};
+  return MutTables{brokers_, replicas_, parts_, topicCount_, ldB_};
 }
 
 // Returns the request base the scan reads (host-mapped staging or the HBM copy) and the update list it
@@ -461,9 +463,8 @@ void Device::stats(const StatsParams& P, const uint8_t* allowedAliveHost, StatsO
   std::memcpy(hStage_ + g.end, allowedAliveHost, (size_t)ldB_);
   launchPrepFor(g, req, false);
   hipCheck(hipMemcpyAsync(allowedAlive_, dReq_, (size_t)ldB_, hipMemcpyDeviceToDevice, ST), "allowedAlive");
-  hipCheck(launchStats(P, topicCount_, topicNrep_, bUtil_, bCap_, bNrep_, bNlead_, bPot_, bAlive_, allowedAlive_,
-                       (TopicPartial*)topicScratch_, (StatsOut*)statsOut_, ldB_, ST, timing ? EV0 : nullptr,
-                       timing ? EV1 : nullptr),
+  hipCheck(launchStats(P, topicCount_, topicNrep_, brokers_, allowedAlive_, (TopicPartial*)topicScratch_,
+                       (StatsOut*)statsOut_, ldB_, ST, timing ? EV0 : nullptr, timing ? EV1 : nullptr),
            "stats");
   hipCheck(hipMemcpyAsync(statsHost_, statsOut_, sizeof(StatsOut), hipMemcpyDeviceToHost, ST), "D2H stats");
   hipCheck(hipStreamSynchronize(ST), "sync");

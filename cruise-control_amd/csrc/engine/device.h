@@ -74,14 +74,15 @@ class Device {
  private:
   int ordinal_, B_, R_, P_, T_, ldB_, G_;
   void* st_ = nullptr;  // hipStream_t
-  // tables
-  double *bUtil_ = nullptr, *bCap_ = nullptr, *bPot_ = nullptr, *rUtil_ = nullptr;
-  int32_t *bNrep_ = nullptr, *bNlead_ = nullptr, *rPart_ = nullptr, *rBroker_ = nullptr, *rOrig_ = nullptr;
-  int32_t *pOff_ = nullptr, *pBrokers_ = nullptr, *topicCount_ = nullptr, *topicNrep_ = nullptr;
-  int32_t *bRack_ = nullptr, *pTopic_ = nullptr, *tUpper_ = nullptr, *tLower_ = nullptr;
-  double *bLeadNwIn_ = nullptr, *pLeadNwOut_ = nullptr;
-  uint8_t *bAlive_ = nullptr, *rFlags_ = nullptr, *allowedAlive_ = nullptr;
-  uint32_t* allowed_ = nullptr;  // [B] goal-slot bit masks
+  // tables (records, devtypes.h) and the host copies used to assemble them
+  BrokerRec* brokers_ = nullptr;
+  ReplicaRec* replicas_ = nullptr;
+  PartitionRec* parts_ = nullptr;
+  int32_t *topicCount_ = nullptr, *topicNrep_ = nullptr, *tUpper_ = nullptr, *tLower_ = nullptr;
+  uint8_t* allowedAlive_ = nullptr;
+  std::vector<BrokerRec> hBrokers_;
+  std::vector<PartitionRec> hParts_;
+  std::vector<int32_t> hRPart_, hROrig_, hPOff_, bRackHost_;
   std::vector<uint32_t> allowedHost_;
   void *topicScratch_ = nullptr, *statsOut_ = nullptr;
   // staging (host-coherent, mapped) and the request copy in HBM

@@ -1,7 +1,8 @@
 // Device-resident structure-of-arrays mirror of the cluster model, and the scan request formats.
 // Shared by host engine code and gfx950 kernels (plain POD, no HIP types).
 //
-// Layout in HBM (one session, B brokers, R replicas, P partitions, T topics):
+// Layout in HBM (one session, B brokers, R replicas, P partitions, T topics) — the logical columns below are
+// packed into per-entity records (BrokerRec / ReplicaRec / PartitionRec, further down):
 //   broker rows   bUtil[4][B] f64 (expected utilization, ModelUtils.expectedUtilizationFor),
 //                 bCap[4][B] f64, bNrep[B] i32, bNlead[B] i32, bPotNwOut[B] f64, bAlive[B] u8
 //   replica rows  rUtil[4][R] f64, rPart/rBroker/rOrig[R] i32, rFlags[R] u8 (bit0 leader, bit1 orig-offline)
@@ -41,7 +42,7 @@ enum DevFilter : int32_t {
   FILTER_RACK_AWARE = 1  // RackAwareGoal.rackAwareEligibleBrokers: rack not among the partition's other racks
 };
 enum DevAction : int32_t { DA_MOVE = 0, DA_LEADERSHIP = 1, DA_SWAP = 2 };
-enum RFlag : uint8_t { RF_LEADER = 1, RF_ORIG_OFFLINE = 2 };
+enum RFlag : uint8_t { RF_LEADER = 1, RF_ORIG_OFFLINE = 2, RF_ORIG_DEAD = 4 /* original broker dead (static) */ };
 
 // Frozen per-goal state needed by selfSatisfied/actionAcceptance (a goal's initGoalState output).
 struct DevGoal {
@@ -70,25 +71,36 @@ struct DevProgram {
   DevGoal goals[kMaxGoals];
 };
 
+// HBM records. One candidate pair reads one replica record, one partition record and two broker records, each
+// a whole 64/128-byte line set fetched in one round trip: the dependency chain of a candidate is
+// request -> replica + destination broker -> partition + source broker (-> topic counts for the topic goal).
+struct alignas(64) BrokerRec {
+  double util[4];         // ModelUtils.expectedUtilizationFor per resource
+  double cap[4];          // capacity (-1 for dead brokers)
+  double pot;             // potential leadership NW_OUT (ClusterModel.potentialLeadershipLoadFor)
+  double lbi;             // leadership NW_IN (Broker.leadershipLoadForNwResources)
+  int32_t nrep, nlead, rack;
+  uint32_t allowedBits;   // bit g: in goal slot g's _brokersAllowedReplicaMove
+  int32_t alive;
+  int32_t pad[7];
+};
+struct alignas(64) ReplicaRec {
+  double util[4];
+  int32_t broker, part, orig, flags;  // flags: RFlag bits
+  int32_t pad[4];
+};
+struct alignas(64) PartitionRec {
+  int32_t n, topic;
+  int32_t brokers[kMaxRf];  // current broker of every replica slot (Partition._replicas order, leader first)
+  double leadNwOut;         // NW_OUT utilization of the leader replica
+  int16_t racks[kMaxRf];    // racks of `brokers`
+};
+static_assert(sizeof(BrokerRec) == 128 && sizeof(ReplicaRec) == 64 && sizeof(PartitionRec) == 64, "record sizes");
+
 struct DevTables {
-  const double* bUtil;
-  const double* bCap;
-  const int32_t* bNrep;
-  const uint8_t* bAlive;
-  const uint32_t* allowedBits;
-  const double* rUtil;
-  const int32_t* rPart;
-  const int32_t* rBroker;
-  const int32_t* rOrig;
-  const uint8_t* rFlags;
-  const int32_t* pOff;
-  const int32_t* pBrokers;
-  const int32_t* bRack;
-  const int32_t* bNlead;
-  const double* bPot;
-  const double* bLeadNwIn;
-  const int32_t* pTopic;
-  const double* pLeadNwOut;
+  const BrokerRec* brokers;
+  const ReplicaRec* replicas;
+  const PartitionRec* parts;
   const int32_t* topicCount;  // [T][ldB]
   const int32_t* tUpper;
   const int32_t* tLower;
@@ -111,6 +123,7 @@ struct PartitionRow {
   int32_t p, n;
   int32_t brokers[kMaxRf];
   double leadNwOut;
+  int16_t racks[kMaxRf];
 };
 struct TopicCountDelta {
   int32_t topic, broker, delta, pad;
@@ -118,17 +131,9 @@ struct TopicCountDelta {
 
 // Writable views of the dynamic tables (row application inside a scan) and a staged update list.
 struct MutTables {
-  double* bUtil;
-  int32_t* bNrep;
-  int32_t* bNlead;
-  double* bPot;
-  double* bLeadNwIn;
-  double* pLeadNwOut;
-  uint8_t* bAlive;
-  double* rUtil;
-  int32_t* rBroker;
-  uint8_t* rFlags;
-  int32_t* pBrokers;
+  BrokerRec* brokers;
+  ReplicaRec* replicas;
+  PartitionRec* parts;
   int32_t* topicCount;
   int32_t ldB;
 };

@@ -31,6 +31,7 @@ struct HostView {
   int flags(int r) const { return (m.rLeader[r] ? RF_LEADER : 0) | (m.rOrigOff[r] ? RF_ORIG_OFFLINE : 0); }
   int rbroker(int r) const { return m.rBroker[r]; }
   int rorig(int r) const { return m.rOrig[r]; }
+  bool origOff(int r) const { return m.origOffline(r); }
   int rpart(int r) const { return m.rPart[r]; }
   int pbegin(int p) const { return m.pOff[p]; }
   int pend(int p) const { return m.pOff[p + 1]; }

@@ -35,6 +35,8 @@ void Model::build(const ccmi_cluster_desc& d) {
   T = d.num_topics;
   bState.assign(B, BState::ALIVE);
   bRack.assign(d.broker_rack, d.broker_rack + B);
+  for (int b = 0; b < B; ++b)
+    if (bRack[b] < 0 || bRack[b] > 32767) throw std::invalid_argument("broker rack index must be in [0, 32767]");
   bId.assign(B, 0);
   for (int b = 0; b < B; ++b) {
     bId[b] = d.broker_id[b];
@@ -410,7 +412,7 @@ void Model::flushToDevice() {
     ReplicaRow row;
     row.r = r;
     row.broker = rBroker[r];
-    row.flags = (rLeader[r] ? RF_LEADER : 0) | (rOrigOff[r] ? RF_ORIG_OFFLINE : 0);
+    row.flags = (rLeader[r] ? RF_LEADER : 0) | (rOrigOff[r] ? RF_ORIG_OFFLINE : 0) | (alive(rOrig[r]) ? 0 : RF_ORIG_DEAD);
     row.pad = 0;
     for (int k = 0; k < 4; ++k) row.util[k] = rUtilC[4 * r + k];
     dev->rrows.push_back(row);
@@ -421,8 +423,10 @@ void Model::flushToDevice() {
     PartitionRow row;
     row.p = p;
     row.n = pOff[p + 1] - pOff[p];
-    for (int k = 0; k < row.n; ++k) row.brokers[k] = rBroker[pSlots[pOff[p] + k]];
-    for (int k = row.n; k < kMaxRf; ++k) row.brokers[k] = -1;
+    for (int k = 0; k < kMaxRf; ++k) {
+      row.brokers[k] = k < row.n ? rBroker[pSlots[pOff[p] + k]] : -1;
+      row.racks[k] = (int16_t)(k < row.n ? bRack[row.brokers[k]] : -1);
+    }
     row.leadNwOut = pLeadNwOut(p);
     dev->prows.push_back(row);
     pDirty[p] = 0;

@@ -34,13 +34,13 @@
 namespace ccmi {
 
 // V must provide: bu(b,res) bcap(b,res) nrep(b) alive(b) allowed(slot,b) ru(r,res) flags(r) rbroker(r)
-// rorig(r) rpart(r) hosts(p,b), and for the goals that read them: rack(b) otherOnRack(p,self,rack) nlead(b)
+// rorig(r) origOff(r) rpart(r) hosts(p,b), and for the goals that read them: rack(b) otherOnRack(p,self,rack) nlead(b)
 // pot(b) lnwin(b) pLeadNwOut(p) ptopic(p) tcount(t,b) tUpper(t) tLower(t).
+// Replica.isCurrentOffline; V::origOff(r) = isOriginalOffline || original broker dead
 template <class V>
 CCMI_HD bool currentOffline(const V& v, int r) {
   const int orig = v.rorig(r), br = v.rbroker(r);
-  const bool origOffline = (v.flags(r) & RF_ORIG_OFFLINE) || !v.alive(orig);
-  return (origOffline && br == orig) || !v.alive(br);
+  return (v.origOff(r) && br == orig) || !v.alive(br);
 }
 
 template <class V>

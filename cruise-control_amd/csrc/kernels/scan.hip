@@ -28,38 +28,37 @@ namespace ccmi {
 
 struct DevView {
   DevTables t;
-  __device__ __forceinline__ double bu(int b, int res) const { return t.bUtil[(size_t)res * t.B + b]; }
-  __device__ __forceinline__ double bcap(int b, int res) const { return t.bCap[(size_t)res * t.B + b]; }
-  __device__ __forceinline__ int nrep(int b) const { return t.bNrep[b]; }
-  __device__ __forceinline__ bool alive(int b) const { return t.bAlive[b] != 0; }
-  __device__ __forceinline__ bool allowed(int slot, int b) const { return (t.allowedBits[b] >> slot) & 1u; }
-  __device__ __forceinline__ double ru(int r, int res) const { return t.rUtil[(size_t)res * t.R + r]; }
-  __device__ __forceinline__ int flags(int r) const { return t.rFlags[r]; }
-  __device__ __forceinline__ int rbroker(int r) const { return t.rBroker[r]; }
-  __device__ __forceinline__ int rorig(int r) const { return t.rOrig[r]; }
-  __device__ __forceinline__ int rpart(int r) const { return t.rPart[r]; }
-  __device__ __forceinline__ int pbegin(int p) const { return t.pOff[p]; }
-  __device__ __forceinline__ int pend(int p) const { return t.pOff[p + 1]; }
-  __device__ __forceinline__ int pbroker(int i) const { return t.pBrokers[i]; }
+  __device__ __forceinline__ double bu(int b, int res) const { return t.brokers[b].util[res]; }
+  __device__ __forceinline__ double bcap(int b, int res) const { return t.brokers[b].cap[res]; }
+  __device__ __forceinline__ int nrep(int b) const { return t.brokers[b].nrep; }
+  __device__ __forceinline__ bool alive(int b) const { return t.brokers[b].alive != 0; }
+  __device__ __forceinline__ bool allowed(int slot, int b) const { return (t.brokers[b].allowedBits >> slot) & 1u; }
+  __device__ __forceinline__ double ru(int r, int res) const { return t.replicas[r].util[res]; }
+  __device__ __forceinline__ int flags(int r) const { return t.replicas[r].flags; }
+  __device__ __forceinline__ int rbroker(int r) const { return t.replicas[r].broker; }
+  __device__ __forceinline__ int rorig(int r) const { return t.replicas[r].orig; }
+  __device__ __forceinline__ bool origOff(int r) const {
+    return (t.replicas[r].flags & (RF_ORIG_OFFLINE | RF_ORIG_DEAD)) != 0;
+  }
+  __device__ __forceinline__ int rpart(int r) const { return t.replicas[r].part; }
   __device__ __forceinline__ bool hosts(int p, int b) const {
+    const PartitionRec& x = t.parts[p];
     bool has = false;
-    for (int i = pbegin(p); i < pend(p); ++i) has |= (pbroker(i) == b);
+    for (int i = 0; i < x.n; ++i) has |= (x.brokers[i] == b);
     return has;
   }
-  __device__ __forceinline__ int rack(int b) const { return t.bRack[b]; }
+  __device__ __forceinline__ int rack(int b) const { return t.brokers[b].rack; }
   __device__ __forceinline__ bool otherOnRack(int p, int self, int rk) const {
+    const PartitionRec& x = t.parts[p];
     bool any = false;
-    for (int i = pbegin(p); i < pend(p); ++i) {
-      const int x = pbroker(i);
-      any |= (x != self) && (t.bRack[x] == rk);
-    }
+    for (int i = 0; i < x.n; ++i) any |= (x.brokers[i] != self) && (x.racks[i] == rk);
     return any;
   }
-  __device__ __forceinline__ int nlead(int b) const { return t.bNlead[b]; }
-  __device__ __forceinline__ double pot(int b) const { return t.bPot[b]; }
-  __device__ __forceinline__ double lnwin(int b) const { return t.bLeadNwIn[b]; }
-  __device__ __forceinline__ double pLeadNwOut(int p) const { return t.pLeadNwOut[p]; }
-  __device__ __forceinline__ int ptopic(int p) const { return t.pTopic[p]; }
+  __device__ __forceinline__ int nlead(int b) const { return t.brokers[b].nlead; }
+  __device__ __forceinline__ double pot(int b) const { return t.brokers[b].pot; }
+  __device__ __forceinline__ double lnwin(int b) const { return t.brokers[b].lbi; }
+  __device__ __forceinline__ double pLeadNwOut(int p) const { return t.parts[p].leadNwOut; }
+  __device__ __forceinline__ int ptopic(int p) const { return t.parts[p].topic; }
   __device__ __forceinline__ int tcount(int tp, int b) const { return t.topicCount[(size_t)tp * t.ldB + b]; }
   __device__ __forceinline__ int tUpper(int tp) const { return t.tUpper[tp]; }
   __device__ __forceinline__ int tLower(int tp) const { return t.tLower[tp]; }
@@ -100,32 +99,37 @@ __device__ __forceinline__ void stageRows(Row* dst, const Row* __restrict__ src,
     reinterpret_cast<int32_t*>(dst)[w] = reinterpret_cast<const int32_t*>(src)[w];
 }
 
-__device__ __forceinline__ void applyRowsBlock(const MutTables& M, int B, int R, const BrokerRow* brows, int nb,
-                                               const ReplicaRow* rrows, int nr, const int32_t* __restrict__ pOff,
-                                               const PartitionRow* prows, int np, const TopicCountDelta* tdel,
-                                               int nt, int first, int stride) {
+__device__ __forceinline__ void applyRowsBlock(const MutTables& M, const BrokerRow* brows, int nb,
+                                               const ReplicaRow* rrows, int nr, const PartitionRow* prows, int np,
+                                               const TopicCountDelta* tdel, int nt, int first, int stride) {
   for (int i = first; i < nb; i += stride) {
     const BrokerRow& x = brows[i];
+    BrokerRec& d = M.brokers[x.b];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) M.bUtil[(size_t)k * B + x.b] = x.util[k];
-    M.bNrep[x.b] = x.nrep;
-    M.bNlead[x.b] = x.nlead;
-    M.bPot[x.b] = x.potNwOut;
-    M.bLeadNwIn[x.b] = x.leadNwIn;
-    M.bAlive[x.b] = (uint8_t)x.alive;
+    for (int k = 0; k < 4; ++k) d.util[k] = x.util[k];
+    d.nrep = x.nrep;
+    d.nlead = x.nlead;
+    d.pot = x.potNwOut;
+    d.lbi = x.leadNwIn;
+    d.alive = x.alive;
   }
   for (int i = first; i < nr; i += stride) {
     const ReplicaRow& x = rrows[i];
+    ReplicaRec& d = M.replicas[x.r];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) M.rUtil[(size_t)k * R + x.r] = x.util[k];
-    M.rBroker[x.r] = x.broker;
-    M.rFlags[x.r] = (uint8_t)x.flags;
+    for (int k = 0; k < 4; ++k) d.util[k] = x.util[k];
+    d.broker = x.broker;
+    d.flags = x.flags;
   }
   for (int i = first; i < np; i += stride) {
     const PartitionRow& x = prows[i];
-    const int o = pOff[x.p];
-    for (int k = 0; k < x.n; ++k) M.pBrokers[o + k] = x.brokers[k];
-    M.pLeadNwOut[x.p] = x.leadNwOut;
+    PartitionRec& d = M.parts[x.p];
+#pragma unroll
+    for (int k = 0; k < kMaxRf; ++k) {
+      d.brokers[k] = x.brokers[k];
+      d.racks[k] = x.racks[k];
+    }
+    d.leadNwOut = x.leadNwOut;
   }
   for (int i = first; i < nt; i += stride) {
     const TopicCountDelta d = tdel[i];
@@ -151,8 +155,7 @@ __device__ __forceinline__ void overlayStage(OverlayLds& ov, const UpdateList& U
 __device__ __forceinline__ void overlayApply(const OverlayLds& ov, const UpdateList& U, const MutTables& M,
                                              const DevTables& T) {
   if (blockIdx.x == 0 && (U.nb | U.nr | U.np | U.nt))
-    applyRowsBlock(M, T.B, T.R, ov.b, ov.nb, ov.r, ov.nr, T.pOff, ov.p, ov.np, U.tdel, U.nt, threadIdx.x,
-                   blockDim.x);
+    applyRowsBlock(M, ov.b, ov.nb, ov.r, ov.nr, ov.p, ov.np, U.tdel, U.nt, threadIdx.x, blockDim.x);
 }
 
 // A move candidate's operands gathered up front with independent loads (row side: the replica, its broker,
@@ -163,9 +166,9 @@ __device__ __forceinline__ void overlayApply(const OverlayLds& ov, const UpdateL
 // loaded when the program's `needs` mask asks for them (a wave-uniform branch).
 struct PreView {
   int r, src, orig, p, rflags, dst, snrep, dnrep;
-  uint32_t aliveBits;   // bit 0 src, bit 1 orig, bit 2 dst (values, never addressed: keeps the view in VGPRs)
-  uint32_t srcAllowed;  // bit `slot` = allowed(slot, src)
-  int pb0, pb1, pb2, pb3, pb4, pb5, pb6, pb7;
+  uint32_t aliveBits;   // bit 0 src, bit 2 dst (values, never addressed: keeps the view in VGPRs)
+  uint32_t srcAllowed;  // allowedBits of src
+  int pn, pb0, pb1, pb2, pb3, pb4, pb5, pb6, pb7;
   double ru0, ru1, ru2, ru3, sbu0, sbu1, sbu2, sbu3, scap0, scap1, scap2, scap3;
   double dbu0, dbu1, dbu2, dbu3, dcap0, dcap1, dcap2, dcap3;
   // optional operands
@@ -176,10 +179,32 @@ struct PreView {
   static __device__ __forceinline__ double sel(int k, double a, double b, double c, double d) {
     return k == 0 ? a : (k == 1 ? b : (k == 2 ? c : d));
   }
+  __device__ __forceinline__ void setPartition(const PartitionRec& x) {  // x: LDS overlay row or HBM record
+    pn = x.n;
+    pb0 = x.brokers[0];
+    pb1 = x.brokers[1];
+    pb2 = x.brokers[2];
+    pb3 = x.brokers[3];
+    pb4 = x.brokers[4];
+    pb5 = x.brokers[5];
+    pb6 = x.brokers[6];
+    pb7 = x.brokers[7];
+    plno = x.leadNwOut;
+    topic = x.topic;
+    prk0 = x.racks[0];
+    prk1 = x.racks[1];
+    prk2 = x.racks[2];
+    prk3 = x.racks[3];
+    prk4 = x.racks[4];
+    prk5 = x.racks[5];
+    prk6 = x.racks[6];
+    prk7 = x.racks[7];
+  }
   __device__ __forceinline__ void loadRow(const DevTables& t, const DevProgram& prog, int rr, const OverlayLds& ov) {
     r = rr;
-    orig = t.rOrig[r];
-    p = t.rPart[r];
+    const ReplicaRec& rec = t.replicas[r];
+    orig = rec.orig;
+    p = rec.part;
     const int ri = ov.replica(r);
     if (ri >= 0) {
       const ReplicaRow& x = ov.r[ri];
@@ -190,41 +215,39 @@ struct PreView {
       ru2 = x.util[2];
       ru3 = x.util[3];
     } else {
-      src = t.rBroker[r];
-      rflags = t.rFlags[r];
-      ru0 = t.rUtil[r];
-      ru1 = t.rUtil[(size_t)t.R + r];
-      ru2 = t.rUtil[(size_t)2 * t.R + r];
-      ru3 = t.rUtil[(size_t)3 * t.R + r];
+      src = rec.broker;
+      rflags = rec.flags;
+      ru0 = rec.util[0];
+      ru1 = rec.util[1];
+      ru2 = rec.util[2];
+      ru3 = rec.util[3];
     }
     const int pi = ov.partition(p);
     if (pi >= 0) {
       const PartitionRow& x = ov.p[pi];
-      const int pn = x.n;
-      pb0 = pn > 0 ? x.brokers[0] : -1;
-      pb1 = pn > 1 ? x.brokers[1] : -1;
-      pb2 = pn > 2 ? x.brokers[2] : -1;
-      pb3 = pn > 3 ? x.brokers[3] : -1;
-      pb4 = pn > 4 ? x.brokers[4] : -1;
-      pb5 = pn > 5 ? x.brokers[5] : -1;
-      pb6 = pn > 6 ? x.brokers[6] : -1;
-      pb7 = pn > 7 ? x.brokers[7] : -1;
+      pn = x.n;
+      pb0 = x.brokers[0];
+      pb1 = x.brokers[1];
+      pb2 = x.brokers[2];
+      pb3 = x.brokers[3];
+      pb4 = x.brokers[4];
+      pb5 = x.brokers[5];
+      pb6 = x.brokers[6];
+      pb7 = x.brokers[7];
       plno = x.leadNwOut;
+      prk0 = x.racks[0];
+      prk1 = x.racks[1];
+      prk2 = x.racks[2];
+      prk3 = x.racks[3];
+      prk4 = x.racks[4];
+      prk5 = x.racks[5];
+      prk6 = x.racks[6];
+      prk7 = x.racks[7];
+      topic = t.parts[p].topic;
     } else {
-      const int o0 = t.pOff[p], pn = t.pOff[p + 1] - o0;
-      const int32_t* q = t.pBrokers + o0;
-      pb0 = pn > 0 ? q[0] : -1;
-      pb1 = pn > 1 ? q[1] : -1;
-      pb2 = pn > 2 ? q[2] : -1;
-      pb3 = pn > 3 ? q[3] : -1;
-      pb4 = pn > 4 ? q[4] : -1;
-      pb5 = pn > 5 ? q[5] : -1;
-      pb6 = pn > 6 ? q[6] : -1;
-      pb7 = pn > 7 ? q[7] : -1;
-      plno = (prog.needs & NEED_POT) ? t.pLeadNwOut[p] : 0.0;
+      setPartition(t.parts[p]);
     }
-    const int oi = ov.broker(orig);
-    const bool aOrig = oi >= 0 ? ov.b[oi].alive != 0 : t.bAlive[orig] != 0;
+    const BrokerRec& sb = t.brokers[src];
     const int si = ov.broker(src);
     bool aSrc;
     if (si >= 0) {
@@ -239,34 +262,23 @@ struct PreView {
       spot = x.potNwOut;
       slbi = x.leadNwIn;
     } else {
-      aSrc = t.bAlive[src] != 0;
-      snrep = t.bNrep[src];
-      sbu0 = t.bUtil[src];
-      sbu1 = t.bUtil[(size_t)t.B + src];
-      sbu2 = t.bUtil[(size_t)2 * t.B + src];
-      sbu3 = t.bUtil[(size_t)3 * t.B + src];
-      snlead = (prog.needs & NEED_LEAD) ? t.bNlead[src] : 0;
-      spot = (prog.needs & NEED_POT) ? t.bPot[src] : 0.0;
-      slbi = (prog.needs & NEED_LBI) ? t.bLeadNwIn[src] : 0.0;
+      aSrc = sb.alive != 0;
+      snrep = sb.nrep;
+      sbu0 = sb.util[0];
+      sbu1 = sb.util[1];
+      sbu2 = sb.util[2];
+      sbu3 = sb.util[3];
+      snlead = sb.nlead;
+      spot = sb.pot;
+      slbi = sb.lbi;
     }
-    aliveBits = (aSrc ? 1u : 0u) | (aOrig ? 2u : 0u);
-    scap0 = t.bCap[src];
-    scap1 = t.bCap[(size_t)t.B + src];
-    scap2 = t.bCap[(size_t)2 * t.B + src];
-    scap3 = t.bCap[(size_t)3 * t.B + src];
-    srcAllowed = t.allowedBits[src];
-    if (prog.needs & NEED_RACK) {
-      prk0 = pb0 >= 0 ? t.bRack[pb0] : -1;
-      prk1 = pb1 >= 0 ? t.bRack[pb1] : -1;
-      prk2 = pb2 >= 0 ? t.bRack[pb2] : -1;
-      prk3 = pb3 >= 0 ? t.bRack[pb3] : -1;
-      prk4 = pb4 >= 0 ? t.bRack[pb4] : -1;
-      prk5 = pb5 >= 0 ? t.bRack[pb5] : -1;
-      prk6 = pb6 >= 0 ? t.bRack[pb6] : -1;
-      prk7 = pb7 >= 0 ? t.bRack[pb7] : -1;
-    }
+    aliveBits = aSrc ? 1u : 0u;
+    scap0 = sb.cap[0];
+    scap1 = sb.cap[1];
+    scap2 = sb.cap[2];
+    scap3 = sb.cap[3];
+    srcAllowed = sb.allowedBits;
     if (prog.needs & NEED_TOPIC) {
-      topic = t.pTopic[p];
       tup = t.tUpper[topic];
       tlo = t.tLower[topic];
       stc = t.topicCount[(size_t)topic * t.ldB + src];
@@ -274,6 +286,7 @@ struct PreView {
   }
   __device__ __forceinline__ void loadDst(const DevTables& t, const DevProgram& prog, int d, const OverlayLds& ov) {
     dst = d;
+    const BrokerRec& db = t.brokers[d];
     const int di = ov.broker(d);
     bool aDst;
     if (di >= 0) {
@@ -288,22 +301,22 @@ struct PreView {
       dpot = x.potNwOut;
       dlbi = x.leadNwIn;
     } else {
-      aDst = t.bAlive[d] != 0;
-      dnrep = t.bNrep[d];
-      dbu0 = t.bUtil[d];
-      dbu1 = t.bUtil[(size_t)t.B + d];
-      dbu2 = t.bUtil[(size_t)2 * t.B + d];
-      dbu3 = t.bUtil[(size_t)3 * t.B + d];
-      dnlead = (prog.needs & NEED_LEAD) ? t.bNlead[d] : 0;
-      dpot = (prog.needs & NEED_POT) ? t.bPot[d] : 0.0;
-      dlbi = (prog.needs & NEED_LBI) ? t.bLeadNwIn[d] : 0.0;
+      aDst = db.alive != 0;
+      dnrep = db.nrep;
+      dbu0 = db.util[0];
+      dbu1 = db.util[1];
+      dbu2 = db.util[2];
+      dbu3 = db.util[3];
+      dnlead = db.nlead;
+      dpot = db.pot;
+      dlbi = db.lbi;
     }
-    aliveBits = (aliveBits & 3u) | (aDst ? 4u : 0u);
-    dcap0 = t.bCap[d];
-    dcap1 = t.bCap[(size_t)t.B + d];
-    dcap2 = t.bCap[(size_t)2 * t.B + d];
-    dcap3 = t.bCap[(size_t)3 * t.B + d];
-    if (prog.needs & NEED_RACK) drack = t.bRack[d];
+    aliveBits = (aliveBits & 1u) | (aDst ? 4u : 0u);
+    dcap0 = db.cap[0];
+    dcap1 = db.cap[1];
+    dcap2 = db.cap[2];
+    dcap3 = db.cap[3];
+    drack = db.rack;
     if (prog.needs & NEED_TOPIC) dtc = t.topicCount[(size_t)topic * t.ldB + d];
   }
   __device__ __forceinline__ double bu(int b, int k) const {
@@ -313,15 +326,14 @@ struct PreView {
     return b == dst ? sel(k, dcap0, dcap1, dcap2, dcap3) : sel(k, scap0, scap1, scap2, scap3);
   }
   __device__ __forceinline__ int nrep(int b) const { return b == dst ? dnrep : snrep; }
-  __device__ __forceinline__ bool alive(int b) const {
-    const uint32_t bit = b == dst ? 4u : (b == src ? 1u : 2u);
-    return (aliveBits & bit) != 0;
-  }
+  // asked for src and dst only (the original broker's liveness is folded into origOff)
+  __device__ __forceinline__ bool alive(int b) const { return (aliveBits & (b == dst ? 4u : 1u)) != 0; }
   __device__ __forceinline__ bool allowed(int slot, int /*b == src*/) const { return (srcAllowed >> slot) & 1u; }
   __device__ __forceinline__ double ru(int /*r*/, int k) const { return sel(k, ru0, ru1, ru2, ru3); }
   __device__ __forceinline__ int flags(int) const { return rflags; }
   __device__ __forceinline__ int rbroker(int) const { return src; }
   __device__ __forceinline__ int rorig(int) const { return orig; }
+  __device__ __forceinline__ bool origOff(int) const { return (rflags & (RF_ORIG_OFFLINE | RF_ORIG_DEAD)) != 0; }
   __device__ __forceinline__ int rpart(int) const { return p; }
   __device__ __forceinline__ bool hosts(int /*p*/, int b) const {
     return (pb0 == b) | (pb1 == b) | (pb2 == b) | (pb3 == b) | (pb4 == b) | (pb5 == b) | (pb6 == b) | (pb7 == b);
@@ -343,7 +355,7 @@ struct PreView {
   __device__ __forceinline__ int tLower(int) const { return tlo; }
 
   // RackAwareGoal.rackAwareEligibleBrokers: the destination's rack is not in the partition's rack list with
-  // one occurrence of the replica's own rack removed (RackAwareGoal.java:193-211). Needs NEED_RACK.
+  // one occurrence of the replica's own rack removed (RackAwareGoal.java:193-211).
   __device__ __forceinline__ bool rackEligible() const {
     int srk = -1;
     if (pb0 == src) srk = prk0;
@@ -500,7 +512,7 @@ __global__ __launch_bounds__(kBlock) void scan_swap(DevTables T, DevProgram prog
       if (lane == 0) rowVisited[row] = 0;
       continue;
     }
-    const int db = v.rbroker(cbRep[c0]);
+    const int db = v.rbroker(cbRep[c0]);  // every row's candidates live on one broker
     int visited = c1 - c0;
     for (int base = c0; base < c1; base += 64) {
       const int idx = base + lane;
@@ -586,7 +598,7 @@ __global__ __launch_bounds__(kBlock) void scan_pairs(DevTables T, MutTables Mt, 
   CCMI_STAMP(T, seq, 5);
 }
 
-__global__ __launch_bounds__(256) void prep(MutTables M, int B, int R, const int32_t* __restrict__ pOff,
+__global__ __launch_bounds__(256) void prep(MutTables M,
                                             const BrokerRow* __restrict__ brows, int nb,
                                             const ReplicaRow* __restrict__ rrows, int nr,
                                             const PartitionRow* __restrict__ prows, int np,
@@ -595,7 +607,7 @@ __global__ __launch_bounds__(256) void prep(MutTables M, int B, int R, const int
                                             unsigned long long* __restrict__ result, unsigned int* __restrict__ done) {
   const int stride = gridDim.x * blockDim.x;
   const int first = blockIdx.x * blockDim.x + threadIdx.x;
-  applyRowsBlock(M, B, R, brows, nb, rrows, nr, pOff, prows, np, tdel, nt, first, stride);
+  applyRowsBlock(M, brows, nb, rrows, nr, prows, np, tdel, nt, first, stride);
   for (int i = first; i < nReq4; i += stride) dReq[i] = req[i];
   if (blockIdx.x == 0 && threadIdx.x == 0 && result) {
     result[0] = kNone;
@@ -650,7 +662,7 @@ hipError_t launchScanPairs(const DevTables& T, const MutTables& M, const UpdateL
   return hipGetLastError();
 }
 
-hipError_t launchPrep(const MutTables& M, int B, int R, const int32_t* pOff, const UpdateList& U, const int4* req,
+hipError_t launchPrep(const MutTables& M, const UpdateList& U, const int4* req,
                       int4* dReq, int nReq4, unsigned long long* result, unsigned int* done, hipStream_t st) {
   int n = U.nb;
   if (U.nr > n) n = U.nr;
@@ -659,7 +671,7 @@ hipError_t launchPrep(const MutTables& M, int B, int R, const int32_t* pOff, con
   if (nReq4 > n) n = nReq4;
   if (n == 0 && !result) return hipSuccess;
   const unsigned blocks = gridFor((uint64_t)(n ? n : 1), 256);
-  hipLaunchKernelGGL(prep, dim3(blocks), dim3(256), 0, st, M, B, R, pOff, U.brows, U.nb, U.rrows, U.nr, U.prows, U.np,
+  hipLaunchKernelGGL(prep, dim3(blocks), dim3(256), 0, st, M, U.brows, U.nb, U.rrows, U.nr, U.prows, U.np,
                      U.tdel, U.nt, req, dReq, nReq4, result, done);
   return hipGetLastError();
 }

@@ -82,10 +82,7 @@ __global__ __launch_bounds__(kTB) void stats_topics(const int32_t* __restrict__ 
   }
 }
 
-__global__ __launch_bounds__(1024) void stats_final(StatsParams P, const double* __restrict__ bUtil,
-                                                    const double* __restrict__ bCap, const int32_t* __restrict__ bNrep,
-                                                    const int32_t* __restrict__ bNlead, const double* __restrict__ bPot,
-                                                    const uint8_t* __restrict__ bAlive,
+__global__ __launch_bounds__(1024) void stats_final(StatsParams P, const BrokerRec* __restrict__ br,
                                                     const uint8_t* __restrict__ allowedAlive,
                                                     const TopicPartial* __restrict__ topics, StatsOut* __restrict__ out) {
   __shared__ double sd[16];
@@ -96,12 +93,12 @@ __global__ __launch_bounds__(1024) void stats_final(StatsParams P, const double*
     double hot = 0.0, cold = 1.7976931348623157e308, varSum = 0.0;
     int bal = 0;
     for (int b = threadIdx.x; b < B; b += blockDim.x) {
-      if (!bAlive[b]) continue;
-      const double u = bUtil[(size_t)res * B + b];
+      if (!br[b].alive) continue;
+      const double u = br[b].util[res];
       hot = u > hot ? u : hot;
       cold = u < cold ? u : cold;
       if (allowedAlive[b]) {
-        const double cap = bCap[(size_t)res * B + b];
+        const double cap = br[b].cap[res];
         const double pct = u / cap;
         if (pct >= P.lowerThr[res] && pct <= P.upperThr[res]) bal++;
         const double d = u - P.avgPct[res] * cap;
@@ -124,15 +121,15 @@ __global__ __launch_bounds__(1024) void stats_final(StatsParams P, const double*
   {
     double s = 0.0;
     for (int b = threadIdx.x; b < B; b += blockDim.x)
-      if (bAlive[b] && allowedAlive[b]) s += bPot[b];
+      if (br[b].alive && allowedAlive[b]) s += br[b].pot;
     s = blockReduce(s, OpAdd(), sd);
     const double avgPct = s / P.potCapacity;
     double hot = 0.0, cold = 1.7976931348623157e308, varSum = 0.0;
     int under = 0;
     for (int b = threadIdx.x; b < B; b += blockDim.x) {
-      if (!bAlive[b]) continue;
-      const double u = bPot[b];
-      const double cap = bCap[(size_t)2 * B + b];
+      if (!br[b].alive) continue;
+      const double u = br[b].pot;
+      const double cap = br[b].cap[2];
       hot = u > hot ? u : hot;
       cold = u < cold ? u : cold;
       if (allowedAlive[b]) {
@@ -155,10 +152,9 @@ __global__ __launch_bounds__(1024) void stats_final(StatsParams P, const double*
   }
   // replica and leader counts (populateReplicaStats: totals/max/min over all brokers, variance over allowed)
   for (int which = 0; which < 2; ++which) {
-    const int32_t* cnt = which == 0 ? bNrep : bNlead;
     int total = 0, mx = 0, mn = 0x7fffffff;
     for (int b = threadIdx.x; b < B; b += blockDim.x) {
-      const int n = cnt[b];
+      const int n = which == 0 ? br[b].nrep : br[b].nlead;
       total += n;
       mx = n > mx ? n : mx;
       mn = n < mn ? n : mn;
@@ -169,8 +165,8 @@ __global__ __launch_bounds__(1024) void stats_final(StatsParams P, const double*
     const double avg = ((double)total) / na;
     double var = 0.0;
     for (int b = threadIdx.x; b < B; b += blockDim.x)
-      if (bAlive[b] && allowedAlive[b]) {
-        const double d = (double)cnt[b] - avg;
+      if (br[b].alive && allowedAlive[b]) {
+        const double d = (double)(which == 0 ? br[b].nrep : br[b].nlead) - avg;
         var += (d * d) / na;
       }
     var = blockReduce(var, OpAdd(), sd);
@@ -212,18 +208,16 @@ __global__ __launch_bounds__(1024) void stats_final(StatsParams P, const double*
   }
 }
 
-hipError_t launchStats(const StatsParams& P, const int32_t* tc, const int32_t* topicNrep, const double* bUtil,
-                       const double* bCap, const int32_t* bNrep, const int32_t* bNlead, const double* bPot,
-                       const uint8_t* bAlive, const uint8_t* allowedAlive, TopicPartial* scratch, StatsOut* out,
-                       int ldB, hipStream_t st, hipEvent_t evTopic0, hipEvent_t evTopic1) {
+hipError_t launchStats(const StatsParams& P, const int32_t* tc, const int32_t* topicNrep, const BrokerRec* brokers,
+                       const uint8_t* allowedAlive, TopicPartial* scratch, StatsOut* out, int ldB, hipStream_t st,
+                       hipEvent_t evTopic0, hipEvent_t evTopic1) {
   int blocks = P.T < 8192 ? P.T : 8192;
   if (blocks < 1) blocks = 1;
   if (evTopic0) (void)hipEventRecord(evTopic0, st);
   hipLaunchKernelGGL(stats_topics, dim3(blocks), dim3(kTB), 0, st, tc, topicNrep, allowedAlive, P.B, ldB, P.T,
                      P.numAllowed, scratch);
   if (evTopic1) (void)hipEventRecord(evTopic1, st);
-  hipLaunchKernelGGL(stats_final, dim3(1), dim3(1024), 0, st, P, bUtil, bCap, bNrep, bNlead, bPot, bAlive, allowedAlive,
-                     scratch, out);
+  hipLaunchKernelGGL(stats_final, dim3(1), dim3(1024), 0, st, P, brokers, allowedAlive, scratch, out);
   return hipGetLastError();
 }
 

@@ -43,6 +43,7 @@ struct View {
   int flags(int r) const { return e.rFlags[r]; }
   int rbroker(int r) const { return e.rBroker[r]; }
   int rorig(int r) const { return e.rOrig[r]; }
+  bool origOff(int r) const { return (e.rFlags[r] & RF_ORIG_OFFLINE) || !alive(e.rOrig[r]); }
   int rpart(int r) const { return e.rPart[r]; }
   int pbegin(int p) const { return e.pOff[p]; }
   int pend(int p) const { return e.pOff[p + 1]; }
