@@ -21,6 +21,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <cstdlib>
+
 #include "../engine/devtypes.h"
 #include "../engine/predicates.h"
 
@@ -621,7 +623,13 @@ __global__ __launch_bounds__(256) void prep(MutTables M,
 // at the scan kernels' register budget): the blocks then sweep the pair space in order, chunk c in iteration
 // c / grid, and each chunk start is checked against the current best before any work — a launch whose winner
 // is early costs one chunk per block, and no workgroup is dispatched only to exit.
-constexpr uint64_t kResidentBlocks = 1024;
+static uint64_t residentBlocks() {  // CCMI_GRID_CAP overrides (diagnostics)
+  static const uint64_t v = [] {
+    const char* e = std::getenv("CCMI_GRID_CAP");
+    return e ? (uint64_t)std::strtoull(e, nullptr, 10) : (uint64_t)1024;
+  }();
+  return v;
+}
 static unsigned gridFor(uint64_t work, uint64_t perBlock, uint64_t cap = 4096) {
   uint64_t blocks = (work + perBlock - 1) / perBlock;
   if (blocks > cap) blocks = cap;
@@ -633,7 +641,7 @@ hipError_t launchScanCross(const DevTables& T, const MutTables& M, const UpdateL
                            const int32_t* reps, const int32_t* cands, int K, int Nr, int N, int c0,
                            unsigned long long* result, unsigned int* done, unsigned long long* mail,
                            unsigned long long seq, hipStream_t st) {
-  const unsigned blocks = gridFor((uint64_t)K * (uint64_t)Nr, (uint64_t)kBlock, kResidentBlocks);
+  const unsigned blocks = gridFor((uint64_t)K * (uint64_t)Nr, (uint64_t)kBlock, residentBlocks());
   hipLaunchKernelGGL(scan_cross, dim3(blocks), dim3(kBlock), 0, st, T, M, U, prog, reps, cands, K, Nr, N, c0, result,
                      done, mail, seq);
   return hipGetLastError();
@@ -656,7 +664,7 @@ hipError_t launchScanSwap(const DevTables& T, const DevProgram& prog, const int3
 hipError_t launchScanPairs(const DevTables& T, const MutTables& M, const UpdateList& U, const DevProgram& prog,
                            const int32_t* pr, const int32_t* pb, int n, int keyBase, unsigned long long* result,
                            unsigned int* done, unsigned long long* mail, unsigned long long seq, hipStream_t st) {
-  const unsigned blocks = gridFor((uint64_t)n, (uint64_t)kBlock, kResidentBlocks);
+  const unsigned blocks = gridFor((uint64_t)n, (uint64_t)kBlock, residentBlocks());
   hipLaunchKernelGGL(scan_pairs, dim3(blocks), dim3(kBlock), 0, st, T, M, U, prog, pr, pb, n, keyBase, result, done,
                      mail, seq);
   return hipGetLastError();
