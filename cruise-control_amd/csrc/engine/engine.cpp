@@ -4,6 +4,8 @@
 #include <algorithm>
 #include <chrono>
 #include <cmath>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 
 #include "device.h"
@@ -741,14 +743,27 @@ class ResourceDistribution : public GoalImpl {
         for (const auto& o : entryKey) changed[o.first] = 1;
         for (int x : m.brokersByPct(res))
           if (entryIn[x] && !changed[x]) order.push_back(x);
-        for (const auto& o : entryKey) {
-          if (!entryIn[o.first]) continue;
-          auto less = [&](int y, const std::pair<int, double>& k) {
-            const int c = jcmpDouble(m.pct(y, res), k.second);
-            return c ? c < 0 : m.bId[y] < m.bId[k.first];
-          };
-          order.insert(std::lower_bound(order.begin(), order.end(), o, less), o.first);
+        // the changed members sorted by their entry keys, merged into the unchanged ones (whose live key is the
+        // entry key)
+        std::vector<std::pair<int, double>> moved;
+        for (const auto& o : entryKey)
+          if (entryIn[o.first]) moved.push_back(o);
+        auto lessKey = [&](double ka, int a, double kb, int bb) {
+          const int c = jcmpDouble(ka, kb);
+          return c ? c < 0 : m.bId[a] < m.bId[bb];
+        };
+        std::sort(moved.begin(), moved.end(), [&](const std::pair<int, double>& x, const std::pair<int, double>& y) {
+          return lessKey(x.second, x.first, y.second, y.first);
+        });
+        std::vector<int32_t> merged;
+        merged.reserve(order.size() + moved.size());
+        size_t u = 0;
+        for (const auto& o : moved) {
+          while (u < order.size() && lessKey(m.pct(order[u], res), order[u], o.second, o.first)) merged.push_back(order[u++]);
+          merged.push_back(o.first);
         }
+        while (u < order.size()) merged.push_back(order[u++]);
+        order.swap(merged);
         rank.assign(m.B, 0);
         for (size_t i = 0; i < order.size(); ++i) rank[order[i]] = (int32_t)i;
         std::vector<int> ids;

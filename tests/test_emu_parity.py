@@ -43,6 +43,10 @@ def test_emu_goal_subsets(emu_lib, oracle_lib, goals):
     (dict(num_racks=6, num_brokers=24, num_replicas=4800, num_topics=30, num_dead_brokers=3), 1500),
     (dict(num_racks=3, num_brokers=9, num_replicas=2700, num_topics=60, num_dead_brokers=3, rack_aware=1), 1500),
     (dict(num_racks=4, num_brokers=16, num_replicas=2400, num_topics=60), 140),  # ReplicaCapacityGoal must move
+    # full-size RandomClusterTest rows (BASE_PROPERTIES): many moves per broker exercise the candidate-tree
+    # materialisation with several moved brokers
+    (dict(num_topics=7000), 3000),
+    (dict(num_brokers=80), 1500),
 ])
 def test_emu_default_goals_match_oracle(emu_lib, oracle_lib, props, max_replicas):
     check_product_against_oracle(emu_lib, props, DEFAULT_GOALS, 1.05, max_replicas=max_replicas)
