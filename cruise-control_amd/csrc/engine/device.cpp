@@ -331,7 +331,9 @@ int64_t Device::finishScan() {
 // small enough to read straight from host memory; otherwise `prep` applies the rows and copies the request
 // into HBM first.
 constexpr int kOverlayRows = 32;
-constexpr size_t kDirectRequestBytes = 16 << 10;
+// Requests are read by the scan straight from the host-mapped staging area (rows that lose to an earlier winner
+// are never read, so copying the request into HBM first would only add a launch and a full PCIe read).
+constexpr size_t kDirectRequestBytes = 8 << 20;
 
 UpdateList Device::stagedList(const Staged& g) const { return overlayFor(g); }
 

@@ -18,6 +18,11 @@ namespace {
 
 constexpr double kBalanceMargin = 0.9;  // ResourceDistributionGoal.BALANCE_MARGIN / ReplicaDistributionAbstractGoal
 
+// Speculative move-in batches: a scan launch costs about as much as evaluating ~10^4 more rows (the rows of one
+// batch are evaluated in one sweep of the resident workgroups and the launch is latency bound), so batches
+// start at a few thousand rows and grow fast while nothing is accepted.
+constexpr size_t kFirstBatchRows = 2048, kBatchGrowth = 8, kMaxBatchRows = (size_t)1 << 18;
+
 // Host view of the model for predicates.h (same expressions the kernels evaluate).
 struct HostView {
   const Model& m;
@@ -482,7 +487,7 @@ class ReplicaDistribution : public GoalImpl {
     };
     std::vector<Seg> segs;
     std::vector<int32_t> flat;
-    size_t target = 256;
+    size_t target = kFirstBatchRows;
     bool haveCur = false;
     Seg cur;
     while (haveCur || !pq.empty()) {
@@ -500,10 +505,10 @@ class ReplicaDistribution : public GoalImpl {
       }
       const int64_t key = e.crossScan(*this, DA_MOVE, flat, 0, cands);
       if (key < 0) {
-        target = std::min<size_t>(target * 2, 1 << 16);
+        target = std::min<size_t>(target * kBatchGrowth, kMaxBatchRows);
         continue;  // all segments exhausted; sources are not re-enqueued
       }
-      target = 256;
+      target = kFirstBatchRows;
       size_t q = (size_t)key, mIdx = 0;
       while (q >= segs[mIdx].list.size() - segs[mIdx].start) {
         q -= segs[mIdx].list.size() - segs[mIdx].start;
@@ -934,7 +939,7 @@ class ResourceDistribution : public GoalImpl {
     };
     std::vector<Seg> segs;
     std::vector<int32_t> flat;
-    size_t target = 256;
+    size_t target = kFirstBatchRows;
     bool haveCur = false;
     Seg cur{0, 0, nullptr};
     auto cond = [&]() { return action == DA_MOVE || m.bNlead[b] != m.nrep(b); };
@@ -955,10 +960,10 @@ class ResourceDistribution : public GoalImpl {
       if (segs.empty()) break;
       const int64_t key = cands.empty() ? -1 : e.crossScan(*this, action, flat, 0, cands);
       if (key < 0) {
-        target = std::min<size_t>(target * 2, 1 << 16);
+        target = std::min<size_t>(target * kBatchGrowth, kMaxBatchRows);
         continue;
       }
-      target = 256;
+      target = kFirstBatchRows;
       size_t q = (size_t)key, mi = 0;
       while (q >= segs[mi].len()) {
         q -= segs[mi].len();

@@ -1010,7 +1010,7 @@ class LeaderReplicaDistribution : public GoalImpl {
     };
     std::vector<Seg> segs;
     std::vector<int32_t> flat;
-    size_t target = 64;
+    size_t target = 2048;
     bool haveCur = false;
     Seg cur;
     while (haveCur || !pq.empty()) {
@@ -1028,10 +1028,10 @@ class LeaderReplicaDistribution : public GoalImpl {
       }
       const int64_t key = cands.empty() ? -1 : e.crossScan(*this, DA_MOVE, flat, 0, cands);
       if (key < 0) {
-        target = std::min<size_t>(target * 4, 1 << 16);
+        target = std::min<size_t>(target * 8, (size_t)1 << 18);
         continue;  // every polled source exhausted; none is re-enqueued
       }
-      target = 64;
+      target = 2048;
       size_t q = (size_t)key, mi = 0;
       while (q >= segs[mi].list.size() - segs[mi].start) {
         q -= segs[mi].list.size() - segs[mi].start;

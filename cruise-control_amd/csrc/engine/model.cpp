@@ -497,10 +497,10 @@ void Model::clearTracked() {
 void Model::clearTracked(int b) { tracked[b].clear(); }
 
 std::shared_ptr<const std::vector<int32_t>> Model::snapshot(int b, const Spec& s) {
-  PhaseScope ps(PH_SORTED_INIT);
   auto& cache = sortedCache[b];
   for (auto& c : cache)
     if (c.ver == bVer[b] && c.spec == s) return c.v;
+  PhaseScope ps(PH_SORTED_INIT);
   auto v = std::make_shared<std::vector<int32_t>>();
   for (int r : bRepl[b])
     if (selects(s, r)) v->push_back(r);
