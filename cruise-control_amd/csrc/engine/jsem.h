@@ -9,8 +9,7 @@
 //   * java.util.PriorityQueue sift order (ResourceDistributionGoal.java:452,630,720);
 //   * iteration order of HashSet<Broker> built by Collectors.toSet() (Broker.hashCode() == id);
 //   * java.util.Random (fixture generator, RandomCluster.java:465-478).
-// The tree is kept in flat struct-of-arrays form (parent/left/right/key/colour vectors) so an in-order
-// snapshot for a device scan is one linear walk.
+// The tree is kept in a flat node array (index links) so an in-order snapshot for a device scan is one walk.
 #pragma once
 #include <algorithm>
 #include <cstdint>
@@ -69,6 +68,7 @@ struct JavaRandom {
 
 // ----------------------------------------------------------------------------------------------
 // java.util.TreeMap<Integer-like key> with an external live comparator. Cmp: int(int a, int b).
+// Nodes are one 24-byte record each (key, links, colour, build rank) so a search step is one cache line.
 template <class Cmp>
 class RbTreeSet {
  public:
@@ -79,53 +79,101 @@ class RbTreeSet {
     if (t < 0) {
       root_ = alloc(k, -1);
       size_ = 1;
+      if (seqOn_) {
+        seqId_.assign(1, root_);
+        seqKey_.assign(1, k);
+      }
       return true;
     }
     int parent = -1, c = 0;
     while (t >= 0) {
       parent = t;
-      c = cmp_(k, key_[t]);
-      if (c < 0) t = left_[t];
-      else if (c > 0) t = right_[t];
+      c = cmp_(k, n_[t].key);
+      if (c < 0) t = n_[t].left;
+      else if (c > 0) t = n_[t].right;
       else return false;
     }
     int e = alloc(k, parent);
-    (c < 0 ? left_[parent] : right_[parent]) = e;
+    (c < 0 ? n_[parent].left : n_[parent].right) = e;
+    if (seqOn_) {  // a new leaf sits right before (left child) or after (right child) its parent in order
+      const size_t at = seqPos(parent) + (c < 0 ? 0 : 1);
+      seqId_.insert(seqId_.begin() + at, e);
+      seqKey_.insert(seqKey_.begin() + at, k);
+    }
     insertFix(e);
     ++size_;
     return true;
   }
-  // Insert `ids` in order into an EMPTY tree whose comparator agrees with `rank` (distinct ranks) on these
-  // elements: the same sequence of TreeMap.put calls and therefore the same structure, with integer compares.
+  // Insert `ids` in order into an EMPTY tree whose comparator agrees with `rank` (distinct ranks in [0, n)) on
+  // these elements: the same sequence of TreeMap.put calls and therefore the same structure. The search is not
+  // walked: a put lands on the one empty link between the new key's in-order neighbours (the predecessor's right
+  // link when that is empty, else the successor's left link), found in a two-level bitmap over the ranks.
   void buildByRank(const std::vector<int>& ids, const std::vector<int32_t>& rank) {
-    const size_t n = ids.size();
-    key_.reserve(n);
-    left_.reserve(n);
-    right_.reserve(n);
-    parent_.reserve(n);
-    red_.reserve(n);
-    nodeRank_.resize(n);
+    n_.reserve(ids.size());
+    int32_t nr = 0;
+    for (int k : ids) nr = std::max(nr, rank[k] + 1);
+    const int nw = (nr + 63) >> 6, ns = (nw + 63) >> 6;
+    std::vector<uint64_t> w(nw, 0), sw(ns, 0);
+    std::vector<int32_t> nodeOf(nr, -1);
+    auto pred = [&](int32_t r) -> int32_t {  // largest set rank < r, or -1
+      int wi = r >> 6;
+      uint64_t m = w[wi] & ((1ull << (r & 63)) - 1);
+      if (m) return (wi << 6) | (63 - __builtin_clzll(m));
+      int si = wi >> 6;
+      uint64_t sm = sw[si] & ((1ull << (wi & 63)) - 1);
+      while (!sm) {
+        if (--si < 0) return -1;
+        sm = sw[si];
+      }
+      wi = (si << 6) | (63 - __builtin_clzll(sm));
+      return (wi << 6) | (63 - __builtin_clzll(w[wi]));
+    };
+    auto succ = [&](int32_t r) -> int32_t {  // smallest set rank > r, or -1
+      int wi = r >> 6;
+      uint64_t m = (r & 63) == 63 ? 0 : w[wi] & (~0ull << ((r & 63) + 1));
+      if (m) return (wi << 6) | __builtin_ctzll(m);
+      int si = wi >> 6;
+      uint64_t sm = (wi & 63) == 63 ? 0 : sw[si] & (~0ull << ((wi & 63) + 1));
+      while (!sm) {
+        if (++si >= ns) return -1;
+        sm = sw[si];
+      }
+      wi = (si << 6) | __builtin_ctzll(sm);
+      return (wi << 6) | __builtin_ctzll(w[wi]);
+    };
     for (int k : ids) {
       const int32_t rk = rank[k];
+      int e;
       if (root_ < 0) {
-        root_ = alloc(k, -1);
-        nodeRank_[root_] = rk;
+        e = root_ = alloc(k, -1);
         size_ = 1;
-        continue;
+      } else {
+        const int32_t pr = pred(rk);
+        int parent;
+        bool goLeft;
+        if (pr >= 0 && n_[nodeOf[pr]].right < 0) {
+          parent = nodeOf[pr];
+          goLeft = false;
+        } else {
+          parent = nodeOf[succ(rk)];
+          goLeft = true;
+        }
+        e = alloc(k, parent);
+        (goLeft ? n_[parent].left : n_[parent].right) = e;
+        insertFix(e);
+        ++size_;
       }
-      int t = root_, parent = -1;
-      bool goLeft = false;
-      while (t >= 0) {
-        parent = t;
-        goLeft = rk < nodeRank_[t];
-        t = goLeft ? left_[t] : right_[t];
-      }
-      const int e = alloc(k, parent);
-      nodeRank_[e] = rk;
-      (goLeft ? left_[parent] : right_[parent]) = e;
-      insertFix(e);
-      ++size_;
+      nodeOf[rk] = e;
+      w[rk >> 6] |= 1ull << (rk & 63);
+      sw[rk >> 12] |= 1ull << ((rk >> 6) & 63);
     }
+    // from here on the in-order sequence is maintained next to the tree (rotations do not change it)
+    seqId_.clear();
+    for (int32_t r = 0; r < nr; ++r)
+      if (nodeOf[r] >= 0) seqId_.push_back(nodeOf[r]);
+    seqKey_.resize(seqId_.size());
+    for (size_t i = 0; i < seqId_.size(); ++i) seqKey_[i] = n_[seqId_[i]].key;
+    seqOn_ = true;
   }
   bool remove(int k) {
     int p = find(k);
@@ -135,97 +183,104 @@ class RbTreeSet {
   }
   bool contains(int k) const { return find(k) >= 0; }
   void inorder(std::vector<int>& out) const {
+    if (seqOn_) {
+      out.assign(seqKey_.begin(), seqKey_.end());
+      return;
+    }
     out.clear();
     int p = root_;
     if (p < 0) return;
-    while (left_[p] >= 0) p = left_[p];
-    for (; p >= 0; p = succ(p)) out.push_back(key_[p]);
+    while (n_[p].left >= 0) p = n_[p].left;
+    for (; p >= 0; p = succ(p)) out.push_back(n_[p].key);
   }
 
  private:
+  struct Node {
+    int key, left, right, parent;
+    int32_t red;
+  };
   Cmp cmp_;
-  std::vector<int> key_, left_, right_, parent_;
-  std::vector<int32_t> nodeRank_;  // buildByRank only
-  std::vector<uint8_t> red_;
+  std::vector<Node> n_;
   std::vector<int> free_;
   int root_ = -1, size_ = 0;
+  bool seqOn_ = false;
+  std::vector<int> seqId_, seqKey_;  // node ids / keys in order (after buildByRank)
+
+  size_t seqPos(int node) const { return (size_t)(std::find(seqId_.begin(), seqId_.end(), node) - seqId_.begin()); }
 
   int alloc(int k, int parent) {
     int id;
     if (!free_.empty()) {
       id = free_.back();
       free_.pop_back();
-      key_[id] = k;
-      left_[id] = right_[id] = -1;
-      parent_[id] = parent;
-      red_[id] = 0;
+      n_[id] = Node{k, -1, -1, parent, 0};
     } else {
-      id = (int)key_.size();
-      key_.push_back(k);
-      left_.push_back(-1);
-      right_.push_back(-1);
-      parent_.push_back(parent);
-      red_.push_back(0);
+      id = (int)n_.size();
+      n_.push_back(Node{k, -1, -1, parent, 0});
     }
     return id;
   }
   int find(int k) const {
     int p = root_;
     while (p >= 0) {
-      int c = cmp_(k, key_[p]);
+      int c = cmp_(k, n_[p].key);
       if (c == 0) return p;
-      p = c < 0 ? left_[p] : right_[p];
+      p = c < 0 ? n_[p].left : n_[p].right;
     }
     return -1;
   }
   int succ(int t) const {
-    if (right_[t] >= 0) {
-      int p = right_[t];
-      while (left_[p] >= 0) p = left_[p];
+    if (n_[t].right >= 0) {
+      int p = n_[t].right;
+      while (n_[p].left >= 0) p = n_[p].left;
       return p;
     }
-    int p = parent_[t], ch = t;
-    while (p >= 0 && ch == right_[p]) {
+    int p = n_[t].parent, ch = t;
+    while (p >= 0 && ch == n_[p].right) {
       ch = p;
-      p = parent_[p];
+      p = n_[p].parent;
     }
     return p;
   }
-  bool isRed(int p) const { return p >= 0 && red_[p]; }
-  int par(int p) const { return p < 0 ? -1 : parent_[p]; }
-  int lft(int p) const { return p < 0 ? -1 : left_[p]; }
-  int rgt(int p) const { return p < 0 ? -1 : right_[p]; }
+  bool isRed(int p) const { return p >= 0 && n_[p].red; }
+  int par(int p) const { return p < 0 ? -1 : n_[p].parent; }
+  int lft(int p) const { return p < 0 ? -1 : n_[p].left; }
+  int rgt(int p) const { return p < 0 ? -1 : n_[p].right; }
   void paint(int p, bool red) {
-    if (p >= 0) red_[p] = red;
+    if (p >= 0) n_[p].red = red;
   }
   void rotL(int p) {
     if (p < 0) return;
-    int r = right_[p];
-    right_[p] = left_[r];
-    if (left_[r] >= 0) parent_[left_[r]] = p;
-    parent_[r] = parent_[p];
-    if (parent_[p] < 0) root_ = r;
-    else if (left_[parent_[p]] == p) left_[parent_[p]] = r;
-    else right_[parent_[p]] = r;
-    left_[r] = p;
-    parent_[p] = r;
+    Node& P = n_[p];
+    const int r = P.right;
+    Node& Rn = n_[r];
+    P.right = Rn.left;
+    if (Rn.left >= 0) n_[Rn.left].parent = p;
+    Rn.parent = P.parent;
+    if (P.parent < 0) root_ = r;
+    else if (n_[P.parent].left == p) n_[P.parent].left = r;
+    else n_[P.parent].right = r;
+    Rn.left = p;
+    P.parent = r;
   }
   void rotR(int p) {
     if (p < 0) return;
-    int l = left_[p];
-    left_[p] = right_[l];
-    if (right_[l] >= 0) parent_[right_[l]] = p;
-    parent_[l] = parent_[p];
-    if (parent_[p] < 0) root_ = l;
-    else if (right_[parent_[p]] == p) right_[parent_[p]] = l;
-    else left_[parent_[p]] = l;
-    right_[l] = p;
-    parent_[p] = l;
+    Node& P = n_[p];
+    const int l = P.left;
+    Node& L = n_[l];
+    P.left = L.right;
+    if (L.right >= 0) n_[L.right].parent = p;
+    L.parent = P.parent;
+    if (P.parent < 0) root_ = l;
+    else if (n_[P.parent].right == p) n_[P.parent].right = l;
+    else n_[P.parent].left = l;
+    L.right = p;
+    P.parent = l;
   }
   // TreeMap.fixAfterInsertion
   void insertFix(int x) {
-    red_[x] = 1;
-    while (x >= 0 && x != root_ && red_[parent_[x]]) {
+    n_[x].red = 1;
+    while (x >= 0 && x != root_ && n_[n_[x].parent].red) {
       int g = par(par(x));
       if (par(x) == lft(g)) {
         int y = rgt(g);
@@ -261,33 +316,45 @@ class RbTreeSet {
         }
       }
     }
-    red_[root_] = 0;
+    n_[root_].red = 0;
   }
   // TreeMap.deleteEntry (successor key copied into the doomed node) + fixAfterDeletion
   void erase(int p) {
     --size_;
-    if (left_[p] >= 0 && right_[p] >= 0) {
+    if (seqOn_) {  // the doomed key leaves the sequence at p's position (p takes its successor's key below)
+      const size_t at = seqPos(p);
+      if (n_[p].left >= 0 && n_[p].right >= 0) {
+        seqKey_[at] = seqKey_[at + 1];
+        seqId_.erase(seqId_.begin() + at + 1);
+        seqKey_.erase(seqKey_.begin() + at + 1);
+      } else {
+        seqId_.erase(seqId_.begin() + at);
+        seqKey_.erase(seqKey_.begin() + at);
+      }
+    }
+    if (n_[p].left >= 0 && n_[p].right >= 0) {
       int s = succ(p);
-      key_[p] = key_[s];
+      n_[p].key = n_[s].key;
       p = s;
     }
-    int rep = left_[p] >= 0 ? left_[p] : right_[p];
+    int rep = n_[p].left >= 0 ? n_[p].left : n_[p].right;
     if (rep >= 0) {
-      parent_[rep] = parent_[p];
-      if (parent_[p] < 0) root_ = rep;
-      else if (p == left_[parent_[p]]) left_[parent_[p]] = rep;
-      else right_[parent_[p]] = rep;
-      left_[p] = right_[p] = parent_[p] = -1;
-      if (!red_[p]) deleteFix(rep);
-    } else if (parent_[p] < 0) {
+      const int pp = n_[p].parent;
+      n_[rep].parent = pp;
+      if (pp < 0) root_ = rep;
+      else if (p == n_[pp].left) n_[pp].left = rep;
+      else n_[pp].right = rep;
+      n_[p].left = n_[p].right = n_[p].parent = -1;
+      if (!n_[p].red) deleteFix(rep);
+    } else if (n_[p].parent < 0) {
       root_ = -1;
     } else {
-      if (!red_[p]) deleteFix(p);
-      int pp = parent_[p];
+      if (!n_[p].red) deleteFix(p);
+      int pp = n_[p].parent;
       if (pp >= 0) {
-        if (p == left_[pp]) left_[pp] = -1;
-        else if (p == right_[pp]) right_[pp] = -1;
-        parent_[p] = -1;
+        if (p == n_[pp].left) n_[pp].left = -1;
+        else if (p == n_[pp].right) n_[pp].right = -1;
+        n_[p].parent = -1;
       }
     }
     free_.push_back(p);

@@ -2,6 +2,7 @@
 #include "model.h"
 
 #include <algorithm>
+#include <cstring>
 #include <stdexcept>
 
 #include "device.h"
@@ -81,6 +82,7 @@ void Model::build(const ccmi_cluster_desc& d) {
     topicRank.assign(T, 0);
     for (int i = 0; i < T; ++i) topicRank[idx[i]] = i;
   }
+  if (R >= (1 << 29)) throw std::invalid_argument("more than 2^29 replicas are not supported");
   topicNrep.assign(T, 0);
   selfHealing.assign(R, 0);
   tracked.assign(B, {});
@@ -164,6 +166,22 @@ void Model::build(const ccmi_cluster_desc& d) {
   rScoreC.assign((size_t)4 * R, 0.f);
   for (int b = 0; b < B; ++b) refreshBroker(b);
   for (int r = 0; r < R; ++r) refreshReplica(r);
+  {
+    // dense rank of the static tail of Replica.compareTo (partition number, original broker id, topic name)
+    std::vector<int32_t> idx(R);
+    for (int r = 0; r < R; ++r) idx[r] = r;
+    auto tail = [&](int a, int b) {
+      const int na = pNumber[rPart[a]], nb = pNumber[rPart[b]];
+      if (na != nb) return na > nb ? 1 : -1;
+      const int ia = bId[rOrig[a]], ib = bId[rOrig[b]];
+      if (ia != ib) return ia > ib ? 1 : -1;
+      const int ta = topicRank[pTopic[rPart[a]]], tb = topicRank[pTopic[rPart[b]]];
+      return ta == tb ? 0 : (ta < tb ? -1 : 1);
+    };
+    std::sort(idx.begin(), idx.end(), [&](int a, int b) { return tail(a, b) < 0; });
+    rStatic.assign(R, 0);
+    for (int i = 1; i < R; ++i) rStatic[idx[i]] = rStatic[idx[i - 1]] + (tail(idx[i - 1], idx[i]) != 0);
+  }
   ldB = (B + 3) & ~3;
   topicCountDense.assign((size_t)T * ldB, 0);
   for (int r = 0; r < R; ++r) topicCountDense[(size_t)pTopic[rPart[r]] * ldB + rBroker[r]]++;
@@ -446,33 +464,34 @@ bool Model::selects(const Spec& s, int r) const {
   return true;
 }
 
-// SortedReplicas comparator: priority functions, score (Double.compare), Replica.compareTo
-int Model::cmpReplica(const Spec& s, int a, int b) const {
-  if (s.prioOffline) {
-    const int pa = curOffline(a) ? 0 : 1, pb = curOffline(b) ? 0 : 1;
-    if (pa != pb) return pa < pb ? -1 : 1;
-  }
-  if (s.prioImmigrants) {
-    const int pa = immigrant(a) ? 0 : 1, pb = immigrant(b) ? 0 : 1;
-    if (pa != pb) return pa < pb ? -1 : 1;
-  }
+// SortedReplicas comparator (priority functions, score by Double.compare, Replica.compareTo) as one 64-bit key:
+// [prioOffline | prioImmigrant | Double.compare-ordered float score | offline | static tail rank (29 bits)].
+// Replica.compareTo's tail (partition number, original broker id, topic) never changes, so it is ranked once.
+uint64_t Model::replicaKey(const Spec& s, int r) const {
+  const bool off = curOffline(r);
+  uint64_t k = 0;
+  if (s.prioOffline && !off) k |= 1ull << 63;
+  if (s.prioImmigrants && !immigrant(r)) k |= 1ull << 62;
   if (s.scoreRes >= 0) {
-    double sa = (double)rScoreC[4 * a + s.scoreRes], sb = (double)rScoreC[4 * b + s.scoreRes];
-    if (s.scoreReverse) {
-      sa = -sa;
-      sb = -sb;
+    // (double)float compared with Double.compare: -0.0 < 0.0, every NaN equal and above +Infinity
+    const float f = rScoreC[4 * r + s.scoreRes];
+    uint32_t u;
+    if (f != f) {
+      u = 0xFFFFFFFFu;
+    } else {
+      uint32_t bits;
+      memcpy(&bits, &f, 4);
+      u = (bits & 0x80000000u) ? ~bits : (bits | 0x80000000u);
+      if (s.scoreReverse) u = ~u;  // Double.compare(-a, -b): exactly the reversed order for non-NaN a, b
     }
-    const int c = jcmpDouble(sa, sb);
-    if (c) return c;
+    k |= (uint64_t)u << 30;
   }
-  const bool oa = curOffline(a), ob = curOffline(b);
-  if (oa != ob) return oa ? -1 : 1;
-  const int na = pNumber[rPart[a]], nb = pNumber[rPart[b]];
-  if (na != nb) return na > nb ? 1 : -1;
-  const int ia = bId[rOrig[a]], ib = bId[rOrig[b]];
-  if (ia != ib) return ia > ib ? 1 : -1;
-  const int ta = topicRank[pTopic[rPart[a]]], tb = topicRank[pTopic[rPart[b]]];
-  return ta == tb ? 0 : (ta < tb ? -1 : 1);
+  if (!off) k |= 1ull << 29;
+  return k | (uint64_t)rStatic[r];
+}
+int Model::cmpReplica(const Spec& s, int a, int b) const {
+  const uint64_t ka = replicaKey(s, a), kb = replicaKey(s, b);
+  return ka == kb ? 0 : (ka < kb ? -1 : 1);
 }
 
 void Model::track(int b, int nameId, const Spec& s) {
@@ -502,9 +521,13 @@ std::shared_ptr<const std::vector<int32_t>> Model::snapshot(int b, const Spec& s
     if (c.ver == bVer[b] && c.spec == s) return c.v;
   PhaseScope ps(PH_SORTED_INIT);
   auto v = std::make_shared<std::vector<int32_t>>();
+  std::vector<std::pair<uint64_t, int32_t>>& keyed = snapKeys_;
+  keyed.clear();
   for (int r : bRepl[b])
-    if (selects(s, r)) v->push_back(r);
-  std::sort(v->begin(), v->end(), [&](int x, int y) { return cmpReplica(s, x, y) < 0; });
+    if (selects(s, r)) keyed.push_back({replicaKey(s, r), r});
+  std::sort(keyed.begin(), keyed.end());
+  v->reserve(keyed.size());
+  for (const auto& kr : keyed) v->push_back(kr.second);
   SortedCacheEntry* slot = nullptr;
   for (auto& c : cache)
     if (c.spec == s || c.ver != bVer[b]) {
@@ -542,10 +565,10 @@ void Model::sortedInsert(int b, int r) {
   for (auto& t : tracked[b]) {
     if (!t.init || !selects(t.spec, r)) continue;
     const Spec& s = t.spec;
-    auto less = [&](int x, int y) { return cmpReplica(s, x, y) < 0; };
+    const uint64_t kr = replicaKey(s, r);
     const auto& cv = t.view();
-    auto cit = std::lower_bound(cv.begin(), cv.end(), r, less);
-    if (cit != cv.end() && cmpReplica(s, *cit, r) == 0) continue;  // TreeSet.add of an equal element
+    auto cit = std::lower_bound(cv.begin(), cv.end(), kr, [&](int x, uint64_t k) { return replicaKey(s, x) < k; });
+    if (cit != cv.end() && replicaKey(s, *cit) == kr) continue;  // TreeSet.add of an equal element
     const size_t pos = (size_t)(cit - cv.begin());
     auto& v = t.mut();
     v.insert(v.begin() + pos, r);
@@ -555,9 +578,9 @@ void Model::sortedErase(int b, int r) {
   for (auto& t : tracked[b]) {
     if (!t.init) continue;
     const Spec& s = t.spec;
-    auto less = [&](int x, int y) { return cmpReplica(s, x, y) < 0; };
+    const uint64_t kr = replicaKey(s, r);
     const auto& cv = t.view();
-    auto cit = std::lower_bound(cv.begin(), cv.end(), r, less);
+    auto cit = std::lower_bound(cv.begin(), cv.end(), kr, [&](int x, uint64_t k) { return replicaKey(s, x) < k; });
     if (cit != cv.end() && *cit == r) {
       const size_t pos = (size_t)(cit - cv.begin());
       auto& v = t.mut();

@@ -163,6 +163,8 @@ class Model {
   // topics
   std::vector<std::string> topicNames;
   std::vector<int32_t> topicRank, topicNrep;
+  std::vector<std::pair<uint64_t, int32_t>> snapKeys_;  // snapshot() scratch
+  std::vector<int32_t> rStatic;  // dense rank of (partition number, original broker id, topic) — Replica.compareTo tail
   std::vector<int32_t> topicCountDense;     // [T][ldB] live Broker.numReplicasOfTopicInBroker counts
   int ldB = 4;
   int tcount(int t, int b) const { return topicCountDense[(size_t)t * ldB + b]; }
@@ -290,6 +292,7 @@ class Model {
   // the live view of a set tracked earlier, because every key change re-inserts the replica.
   std::shared_ptr<const std::vector<int32_t>> snapshot(int b, const Spec& s);
   bool selects(const Spec& s, int r) const;
+  uint64_t replicaKey(const Spec& s, int r) const;
   int cmpReplica(const Spec& s, int a, int b) const;
 
   // Replays the desc construction order documented in include/ccmi.h (ClusterModel.createReplica +
