@@ -262,8 +262,12 @@ bool Engine::optimizeGoal(std::unique_ptr<GoalImpl> g, ccmi_goal_result* res) {
   const int64_t l0 = dev->perf.scanLaunches, p0 = dev->perf.scanPairs;
   struct Clear {
     Model& m;
-    ~Clear() { m.clearTracked(); }
+    ~Clear() {
+      m.clearTracked();
+      prof().candCounter = nullptr;
+    }
   } guard{m};
+  prof().candCounter = &candidates;
   g->succeeded = true;
   const ccmi_cluster_stats before = stats();
   g->finished = false;
@@ -944,18 +948,21 @@ class ResourceDistribution : public GoalImpl {
     Seg cur{0, 0, nullptr};
     auto cond = [&]() { return action == DA_MOVE || m.bNlead[b] != m.nrep(b); };
     while (haveCur || (!pq.empty() && cond())) {
-      segs.clear();
-      flat.clear();
-      if (haveCur) {
-        cur.v = m.snapshot(cur.cb, spec);
-        segs.push_back(cur);
-        flat.insert(flat.end(), cur.v->begin() + std::min(cur.skip, cur.v->size()), cur.v->end());
-        haveCur = false;
-      }
-      while (!pq.empty() && (segs.empty() || flat.size() < target) && cond()) {
-        const int cb = pq.poll();
-        segs.push_back({cb, 0, m.snapshot(cb, spec)});
-        flat.insert(flat.end(), segs.back().v->begin(), segs.back().v->end());
+      {
+        PhaseScope pf(PH_FLATTEN);
+        segs.clear();
+        flat.clear();
+        if (haveCur) {
+          cur.v = m.snapshot(cur.cb, spec);
+          segs.push_back(cur);
+          flat.insert(flat.end(), cur.v->begin() + std::min(cur.skip, cur.v->size()), cur.v->end());
+          haveCur = false;
+        }
+        while (!pq.empty() && (segs.empty() || flat.size() < target) && cond()) {
+          const int cb = pq.poll();
+          segs.push_back({cb, 0, m.snapshot(cb, spec)});
+          flat.insert(flat.end(), segs.back().v->begin(), segs.back().v->end());
+        }
       }
       if (segs.empty()) break;
       const int64_t key = cands.empty() ? -1 : e.crossScan(*this, action, flat, 0, cands);

@@ -160,6 +160,7 @@ void Model::build(const ccmi_cluster_desc& d) {
   }
   bVer.assign(B, 0);
   sortedCache.assign(B, {});
+  filteredCache.assign(B, {});
   bUtilC.assign((size_t)4 * B, 0.0);
   bPctC.assign((size_t)4 * B, 0.0);
   rUtilC.assign((size_t)4 * R, 0.0);
@@ -515,22 +516,18 @@ void Model::clearTracked() {
 }
 void Model::clearTracked(int b) { tracked[b].clear(); }
 
-std::shared_ptr<const std::vector<int32_t>> Model::snapshot(int b, const Spec& s) {
-  auto& cache = sortedCache[b];
+// Per-broker cache of a few snapshots (Spec -> sorted list), valid while the broker's version is unchanged.
+static std::shared_ptr<const std::vector<int32_t>>* cacheFind(std::vector<Model::SortedCacheEntry>& cache,
+                                                                uint32_t ver, const Model::Spec& s) {
   for (auto& c : cache)
-    if (c.ver == bVer[b] && c.spec == s) return c.v;
-  PhaseScope ps(PH_SORTED_INIT);
-  auto v = std::make_shared<std::vector<int32_t>>();
-  std::vector<std::pair<uint64_t, int32_t>>& keyed = snapKeys_;
-  keyed.clear();
-  for (int r : bRepl[b])
-    if (selects(s, r)) keyed.push_back({replicaKey(s, r), r});
-  std::sort(keyed.begin(), keyed.end());
-  v->reserve(keyed.size());
-  for (const auto& kr : keyed) v->push_back(kr.second);
-  SortedCacheEntry* slot = nullptr;
+    if (c.ver == ver && c.spec == s) return &c.v;
+  return nullptr;
+}
+static void cachePut(std::vector<Model::SortedCacheEntry>& cache, uint32_t ver, const Model::Spec& s,
+                     std::shared_ptr<const std::vector<int32_t>> v) {
+  Model::SortedCacheEntry* slot = nullptr;
   for (auto& c : cache)
-    if (c.spec == s || c.ver != bVer[b]) {
+    if (c.spec == s || c.ver != ver) {
       slot = &c;
       break;
     }
@@ -539,12 +536,41 @@ std::shared_ptr<const std::vector<int32_t>> Model::snapshot(int b, const Spec& s
       cache.emplace_back();
       slot = &cache.back();
     } else {
-      slot = &cache[bVer[b] & 3];
+      slot = &cache[ver & 3];
     }
   }
   slot->spec = s;
-  slot->ver = bVer[b];
-  slot->v = v;
+  slot->ver = ver;
+  slot->v = std::move(v);
+}
+
+std::shared_ptr<const std::vector<int32_t>> Model::snapshot(int b, const Spec& s) {
+  const bool limited = s.selAboveRes >= 0 || s.selBelowRes >= 0;
+  auto& cache = limited ? filteredCache[b] : sortedCache[b];
+  if (auto* hit = cacheFind(cache, bVer[b], s)) return *hit;
+  std::shared_ptr<std::vector<int32_t>> v = std::make_shared<std::vector<int32_t>>();
+  if (limited) {
+    // The utilization limit only filters: the limit-free snapshot (cached across limits) filtered in order.
+    Spec base = s;
+    base.selAboveRes = base.selBelowRes = -1;
+    base.aboveLimit = base.belowLimit = 0;
+    const auto v0 = snapshot(b, base);
+    v->reserve(v0->size());
+    for (int r : *v0)
+      if ((s.selAboveRes < 0 || ru(r, s.selAboveRes) > s.aboveLimit) &&
+          (s.selBelowRes < 0 || ru(r, s.selBelowRes) < s.belowLimit))
+        v->push_back(r);
+  } else {
+    PhaseScope ps(PH_SORTED_INIT);
+    std::vector<std::pair<uint64_t, int32_t>>& keyed = snapKeys_;
+    keyed.clear();
+    for (int r : bRepl[b])
+      if (selects(s, r)) keyed.push_back({replicaKey(s, r), r});
+    std::sort(keyed.begin(), keyed.end());
+    v->reserve(keyed.size());
+    for (const auto& kr : keyed) v->push_back(kr.second);
+  }
+  cachePut(cache, bVer[b], s, v);
   return v;
 }
 

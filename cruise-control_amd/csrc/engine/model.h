@@ -281,7 +281,8 @@ class Model {
     std::shared_ptr<const std::vector<int32_t>> v;
   };
   std::vector<uint32_t> bVer;
-  std::vector<std::vector<SortedCacheEntry>> sortedCache;  // per broker, a few Specs
+  std::vector<std::vector<SortedCacheEntry>> sortedCache;    // per broker, a few limit-free Specs
+  std::vector<std::vector<SortedCacheEntry>> filteredCache;  // per broker, a few Specs with a utilization limit
   void track(int b, int nameId, const Spec& s);
   void untrackAll(int nameId);
   void untrack(int b, int nameId);

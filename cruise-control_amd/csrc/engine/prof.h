@@ -16,6 +16,12 @@ enum Phase {
 struct PhaseProf {
   double ms[PH_COUNT] = {};
   int64_t n[PH_COUNT] = {};
+  // device scans attributed to the innermost enclosing driver phase (rdg/res/swap/other goals)
+  int driver = -1;
+  double scanMs[PH_COUNT] = {};
+  int64_t scans[PH_COUNT] = {};
+  const int64_t* candCounter = nullptr;  // the engine's reference-equivalent candidate count
+  int64_t cands[PH_COUNT] = {};
   bool on = std::getenv("CCMI_PROFILE") != nullptr;
   void print(const char* tag) const {
     static const char* names[PH_COUNT] = {"rdg.moveOut", "rdg.moveIn", "res.moveOut", "res.moveIn", "res.swap",
@@ -25,8 +31,14 @@ struct PhaseProf {
     if (!on) return;
     std::fprintf(stderr, "[ccmi profile %s]\n", tag);
     for (int i = 0; i < PH_COUNT; ++i)
-      if (n[i]) std::fprintf(stderr, "  %-14s %10.1f ms %10lld calls %8.2f us/call\n", names[i], ms[i], (long long)n[i],
-                             1e3 * ms[i] / n[i]);
+      if (n[i]) {
+        std::fprintf(stderr, "  %-14s %10.1f ms %10lld calls %8.2f us/call", names[i], ms[i], (long long)n[i],
+                     1e3 * ms[i] / n[i]);
+        if (scans[i])
+          std::fprintf(stderr, "   [%lld scans, %.1f ms in scans, %lld candidates]", (long long)scans[i], scanMs[i],
+                       (long long)cands[i]);
+        std::fprintf(stderr, "\n");
+      }
   }
 };
 
@@ -35,17 +47,39 @@ inline PhaseProf& prof() {
   return p;
 }
 
+inline bool isDriverPhase(int p) {
+  return p == PH_RDG_OUT || p == PH_RDG_IN || p == PH_RES_OUT || p == PH_RES_IN || p == PH_SWAP || p == PH_OTHER_GOALS;
+}
+
 struct PhaseScope {
   int ph;
   bool on;
+  int prevDriver = -1;
+  int64_t c0 = 0;
   std::chrono::steady_clock::time_point t0;
   explicit PhaseScope(int p) : ph(p), on(prof().on) {
-    if (on) t0 = std::chrono::steady_clock::now();
+    if (!on) return;
+    t0 = std::chrono::steady_clock::now();
+    if (isDriverPhase(p)) {
+      prevDriver = prof().driver;
+      prof().driver = p;
+      if (prof().candCounter) c0 = *prof().candCounter;
+    }
   }
   ~PhaseScope() {
     if (!on) return;
-    prof().ms[ph] += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
-    prof().n[ph]++;
+    PhaseProf& P = prof();
+    const double dt = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    P.ms[ph] += dt;
+    P.n[ph]++;
+    if (isDriverPhase(ph)) {
+      P.driver = prevDriver;
+      if (P.candCounter) P.cands[ph] += *P.candCounter - c0;
+    }
+    if (ph == PH_DEV_SCAN && P.driver >= 0) {
+      P.scans[P.driver]++;
+      P.scanMs[P.driver] += dt;
+    }
   }
 };
 

@@ -13,9 +13,10 @@ from bench import WORKLOADS  # noqa: E402
 ap = argparse.ArgumentParser()
 ap.add_argument("--workload", default="c2")
 ap.add_argument("--goals", type=int, default=16)
+ap.add_argument("--lib", default=None, help="alternative libccmi build (e.g. tests/emu/libccmi_emu.so on CPU)")
 a = ap.parse_args()
 props, goals, name = WORKLOADS[a.workload]
-lib = ccmi.Library.get()
+lib = ccmi.Library.get(a.lib) if a.lib else ccmi.Library.get()
 t0 = time.time()
 buf = ccmi.RandomCluster.generate(lib, **props)
 t1 = time.time()
