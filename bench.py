@@ -37,12 +37,19 @@ import ccmi  # noqa: E402
 
 C1_PROPS = dict(num_racks=20, num_brokers=1000, num_replicas=99999, num_topics=3000)
 C2_PROPS = dict(num_racks=100, num_brokers=10000, num_replicas=999999, num_topics=10000)
+# C3: RandomSelfHealingTest-style placement (6-arg populate, rack-aware, leader first; RandomCluster.java:119-124)
+C3_PROPS = dict(C2_PROPS, num_dead_brokers=500, rack_aware=1, leader_in_first_position=1)
 C1_GOALS = list(ccmi.C1_GOALS)
 DEFAULT_GOALS = list(ccmi.DEFAULT_GOALS)
 WORKLOADS = {"c1": (C1_PROPS, C1_GOALS, "C1: 1K brokers x 100K replicas, 5 distribution goals (BASELINE configs[1])"),
              "c2": (C2_PROPS, DEFAULT_GOALS, "C2: 10K brokers x 1M replicas, the 16 default goals (BASELINE configs[2])"),
              "c2_c1goals": (C2_PROPS, C1_GOALS, "C2 cluster with the C1 goal list"),
+             "c3": (C3_PROPS, DEFAULT_GOALS, "C3: C2 with brokers 0..499 DEAD, requested destinations 500..1499, the 16 "
+                                           "default goals (BASELINE configs[3], RemoveBrokersRunnable options)"),
              "c0": ({}, DEFAULT_GOALS, "C0: TestConstants.BASE_PROPERTIES, the 16 default goals (BASELINE configs[0])")}
+# Per-workload OptimizationOptions (C3: the 7-arg options RemoveBrokersRunnable.java:107-126 builds)
+WORKLOAD_OPTIONS = {"c3": lambda: ccmi.OptimizationOptions(requested_destination_broker_ids=list(range(500, 1500)),
+                                                           fast_mode=False)}
 BYTES_PER_CANDIDATE = 96
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E (MI355X_MICROARCH.md)
 
@@ -62,7 +69,8 @@ def cpu_baseline(buf, workload: str, goal_names) -> dict:
     goals = list(goal_names) if workload in ("c0", "c1") else list(goal_names)[:C2_CPU_SAMPLE_GOALS]
     oc = OracleCluster.from_desc(buf.desc)
     t0 = time.perf_counter()
-    res = oc.optimize(goals, ccmi.BalancingConstraint())
+    opts = WORKLOAD_OPTIONS[workload]() if workload in WORKLOAD_OPTIONS else None
+    res = oc.optimize(goals, ccmi.BalancingConstraint(), opts)
     dt = time.perf_counter() - t0
     cands = sum(r.candidates for r in res)
     what = "one full optimizations()" if len(goals) == len(goal_names) else \
@@ -119,6 +127,7 @@ def main() -> None:
     props, goal_names, workload_name = WORKLOADS[args.workload]
     buf = ccmi.RandomCluster.generate(lib, **props)
     goals = ccmi.goals_from_names(goal_names)
+    options = WORKLOAD_OPTIONS[args.workload]() if args.workload in WORKLOAD_OPTIONS else None
     opt = ccmi.GoalOptimizer(ccmi.BalancingConstraint())
     sharded = args.sharded and world > 1
     uid = None
@@ -140,7 +149,7 @@ def main() -> None:
         ws = session()
         ws.set_kernel_timing(True)
         ws.reset_perf()
-        r = opt.optimizations(ws, goals)
+        r = opt.optimizations(ws, goals, options)
         inst_perf, inst_cands = ws.perf(), r.candidates
         del ws
 
@@ -150,7 +159,7 @@ def main() -> None:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    results = [opt.optimizations(s, goals) for s in sessions]
+    results = [opt.optimizations(s, goals, options) for s in sessions]
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()

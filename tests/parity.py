@@ -54,7 +54,7 @@ def _key(p):
     return p.partition, p.partition_size, p.old_leader, tuple(p.old_replicas), tuple(p.new_replicas)
 
 
-def check_product_against_oracle(lib, props, goals, balance=None, device=0, max_replicas=None):
+def check_product_against_oracle(lib, props, goals, balance=None, device=0, max_replicas=None, options=None):
     """Live parity: same flattened input into both; action log, final assignment/leaders, per-goal results and
     every goal's post-optimization ClusterModelStats. A chain that fails (OptimizationFailureException for a hard
     goal) must fail in both with the same exception and message after the same action log."""
@@ -63,11 +63,12 @@ def check_product_against_oracle(lib, props, goals, balance=None, device=0, max_
     oc = OracleCluster.from_desc(buf.desc)
     perr = oerr = None
     try:
-        res = ccmi.GoalOptimizer(constraint(balance, max_replicas)).optimizations(cm, ccmi.goals_from_names(goals))
+        res = ccmi.GoalOptimizer(constraint(balance, max_replicas)).optimizations(cm, ccmi.goals_from_names(goals),
+                                                                                   options)
     except ccmi.CruiseControlError as e:
         perr = e
     try:
-        ores = oc.optimize(goals, constraint(balance, max_replicas))
+        ores = oc.optimize(goals, constraint(balance, max_replicas), options)
     except Exception as e:  # noqa: BLE001 - the oracle binding raises the same exception classes
         oerr = e
     if perr is not None or oerr is not None:

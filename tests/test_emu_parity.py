@@ -60,3 +60,19 @@ def test_emu_goal_orders(emu_lib, oracle_lib, goals):
     that cannot be satisfied must fail identically in both)."""
     check_product_against_oracle(emu_lib, dict(num_racks=4, num_brokers=16, num_replicas=2400, num_topics=60),
                                  goals, 1.05)
+
+
+# C3 shape (BASELINE configs[3]): dead brokers (self-healing) with a requested destination broker set, as
+# RemoveBrokersRunnable builds OptimizationOptions (RemoveBrokersRunnable.java:107-126) — the 7-arg
+# OptimizationOptions with requestedDestinationBrokerIds, filtered by GoalUtils.eligibleBrokers
+# (GoalUtils.java:122-160); leadership moves ignore the requested set.
+@pytest.mark.parametrize("props,requested,goals", [
+    (dict(num_racks=6, num_brokers=24, num_replicas=4800, num_topics=30, num_dead_brokers=3, rack_aware=1,
+          leader_in_first_position=1), range(3, 12), DEFAULT_GOALS),
+    (dict(num_racks=4, num_brokers=16, num_replicas=2400, num_topics=60, num_dead_brokers=2, rack_aware=1,
+          leader_in_first_position=1), range(2, 10), DEFAULT_GOALS),
+    (dict(num_racks=5, num_brokers=20, num_replicas=6000, num_topics=300), [1, 4, 7, 9, 12, 15, 18], C1_GOALS),
+])
+def test_emu_requested_destinations_match_oracle(emu_lib, oracle_lib, props, requested, goals):
+    opts = ccmi.OptimizationOptions(requested_destination_broker_ids=list(requested), fast_mode=False)
+    check_product_against_oracle(emu_lib, props, goals, 1.05, max_replicas=3000, options=opts)

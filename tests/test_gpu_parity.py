@@ -106,3 +106,15 @@ def test_gpu_acceptance_after_optimization(gpu_lib):
     for gi in range(len(C1_GOALS)):
         # the reverse of the last applied action is a legal question to ask every optimized goal
         assert cm.action_acceptance(gi, a[0], a[1], a[3], a[2]) in ccmi.ACCEPTANCE
+
+
+# C3 shape (BASELINE configs[3]): dead brokers + requestedDestinationBrokerIds (RemoveBrokersRunnable.java:107-126),
+# at the RandomSelfHealingTest size (BASE_PROPERTIES, rack-aware leader-first placement) and a small cluster.
+@pytest.mark.parametrize("props,requested", [
+    (dict(num_dead_brokers=5, rack_aware=1, leader_in_first_position=1), range(5, 25)),
+    (dict(num_racks=6, num_brokers=24, num_replicas=4800, num_topics=30, num_dead_brokers=3, rack_aware=1,
+          leader_in_first_position=1), range(3, 12)),
+])
+def test_gpu_requested_destinations_match_oracle(gpu_lib, oracle_lib, props, requested):
+    opts = ccmi.OptimizationOptions(requested_destination_broker_ids=list(requested), fast_mode=False)
+    check_product_against_oracle(gpu_lib, props, DEFAULT_GOALS, 1.05, max_replicas=3000, options=opts)

@@ -8,7 +8,7 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(REPO, "cruise-control_amd"))
 sys.path.insert(0, REPO)
 import ccmi  # noqa: E402
-from bench import WORKLOADS  # noqa: E402
+from bench import WORKLOAD_OPTIONS, WORKLOADS  # noqa: E402
 
 ap = argparse.ArgumentParser()
 ap.add_argument("--workload", default="c2")
@@ -23,7 +23,8 @@ t1 = time.time()
 cm = ccmi.ClusterModel.from_buffers(buf, device=0)
 t2 = time.time()
 print(f"{name}: generate {t1 - t0:.2f}s, session {t2 - t1:.2f}s", flush=True)
-res = ccmi.GoalOptimizer(ccmi.BalancingConstraint()).optimizations(cm, ccmi.goals_from_names(goals[:a.goals]))
+opts = WORKLOAD_OPTIONS[a.workload]() if a.workload in WORKLOAD_OPTIONS else None
+res = ccmi.GoalOptimizer(ccmi.BalancingConstraint()).optimizations(cm, ccmi.goals_from_names(goals[:a.goals]), opts)
 t3 = time.time()
 for g in res.goal_results:
     print(f"  {g.name:40s} ok={g.succeeded} {g.seconds:8.3f}s cand={g.candidates:>12d} act={g.actions:>7d} "
