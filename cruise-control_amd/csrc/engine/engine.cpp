@@ -323,6 +323,11 @@ class LiveQueue {
     if (ordered_) oq_.add(x);
     else pq_.add(x);
   }
+  // speculatively polled entries whose keys did not change, in reverse poll order
+  void unpoll(int x) {
+    if (ordered_) oq_.unpoll(x);
+    else pq_.add(x);
+  }
 
  private:
   bool ordered_ = false;
@@ -982,7 +987,7 @@ class ResourceDistribution : public GoalImpl {
       if (action == DA_MOVE) m.relocateReplica(m.rPart[r], hit.cb, b);
       else m.relocateLeadership(m.rPart[r], hit.cb, b);
       if (aboveLower(m, b)) return false;
-      for (size_t t = mi + 1; t < segs.size(); ++t) pq.add(segs[t].cb);  // un-poll speculative brokers
+      for (size_t t = segs.size(); t-- > mi + 1;) pq.unpoll(segs[t].cb);  // un-poll speculative brokers
       if (!pq.empty() && m.pct(hit.cb, res) < m.pct(pq.peek(), res)) {
         pq.add(hit.cb);
       } else {
@@ -1013,6 +1018,10 @@ class ResourceDistribution : public GoalImpl {
     auto pqAdd = [&](int x) {
       if (out) pqUp.add(x);
       else pqDown.add(x);
+    };
+    auto pqUnpoll = [&](int x) {
+      if (out) pqUp.unpoll(x);
+      else pqDown.unpoll(x);
     };
     {
       PhaseScope pi(PH_PQ_INIT);
@@ -1083,7 +1092,7 @@ class ResourceDistribution : public GoalImpl {
       m.relocateReplica(dp, cb, b);
       const bool done = out ? underUpper(m, b, upperThr) : aboveLower(m, b);
       if (done) return false;
-      for (size_t t = mi + 1; t < polled.size(); ++t) pqAdd(polled[t]);  // un-poll speculative brokers
+      for (size_t t = polled.size(); t-- > mi + 1;) pqUnpoll(polled[t]);  // un-poll speculative brokers
       pqAdd(cb);
     }
     return true;

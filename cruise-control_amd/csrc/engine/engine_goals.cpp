@@ -999,32 +999,38 @@ class LeaderReplicaDistribution : public GoalImpl {
     Model::Spec s;
     s.selLeaders = true;
     s.selImmigrants = m.numDead > 0 || m.numBadDisk > 0 || e.opt.onlyImmigrants;
-    for (int x = 0; x < m.B; ++x) m.track(x, id, s);
+    // The sources' SortedReplicas are tracked only for this call (the reference tracks them on entry and untracks
+    // on exit) and initialised lazily on first poll; a source only loses replicas afterwards (moves go to b, whose
+    // view is never read), so its live view equals a fresh snapshot of its current replicas: snapshots (cached per
+    // broker version) replace the tracked views and their per-poll clones.
+    (void)id;
     int nl = m.bNlead[b];
     std::vector<int32_t> single{b}, cands;
     e.eligible(single, DA_MOVE, cands);
     struct Seg {
       int src;
-      std::vector<int32_t> list;  // clone of the source's sorted leaders
+      std::shared_ptr<const std::vector<int32_t>> v;  // the source's sorted leaders
       size_t start;
+      size_t len() const { return v->size() > start ? v->size() - start : 0; }
     };
     std::vector<Seg> segs;
     std::vector<int32_t> flat;
     size_t target = 2048;
     bool haveCur = false;
-    Seg cur;
+    Seg cur{0, nullptr, 0};
     while (haveCur || !pq.empty()) {
       segs.clear();
       flat.clear();
       if (haveCur) {  // the source being iterated continues first, after its winner
-        segs.push_back(std::move(cur));
+        cur.v = m.snapshot(cur.src, s);
+        segs.push_back(cur);
         haveCur = false;
-        flat.insert(flat.end(), segs.back().list.begin() + segs.back().start, segs.back().list.end());
+        flat.insert(flat.end(), cur.v->begin() + std::min(cur.start, cur.v->size()), cur.v->end());
       }
       while (!pq.empty() && (segs.empty() || flat.size() < target)) {
         const int src = pq.poll();
-        segs.push_back({src, m.sorted(src, id), 0});
-        flat.insert(flat.end(), segs.back().list.begin(), segs.back().list.end());
+        segs.push_back({src, m.snapshot(src, s), 0});
+        flat.insert(flat.end(), segs.back().v->begin(), segs.back().v->end());
       }
       const int64_t key = cands.empty() ? -1 : e.crossScan(*this, DA_MOVE, flat, 0, cands);
       if (key < 0) {
@@ -1033,27 +1039,25 @@ class LeaderReplicaDistribution : public GoalImpl {
       }
       target = 2048;
       size_t q = (size_t)key, mi = 0;
-      while (q >= segs[mi].list.size() - segs[mi].start) {
-        q -= segs[mi].list.size() - segs[mi].start;
+      while (q >= segs[mi].len()) {
+        q -= segs[mi].len();
         ++mi;
       }
-      Seg& hit = segs[mi];
+      const Seg hit = segs[mi];
       const size_t idx = hit.start + q;
-      m.relocateReplica(m.rPart[hit.list[idx]], hit.src, b);
-      if (++nl >= lower) {
-        m.untrackAll(id);
-        return false;
-      }
+      const size_t hitSize = hit.v->size();
+      m.relocateReplica(m.rPart[(*hit.v)[idx]], hit.src, b);
+      if (++nl >= lower) return false;
       for (size_t t = mi + 1; t < segs.size(); ++t) pq.add(segs[t].src);  // un-poll speculative sources
       if (!pq.empty() && m.bNlead[hit.src] < m.bNlead[pq.peek()]) {
         pq.add(hit.src);
-      } else if (idx + 1 < hit.list.size()) {
-        cur = std::move(hit);
-        cur.start = idx + 1;
+      } else if (idx + 1 < hitSize) {
+        // the live view lost exactly the moved replica: the entries after it keep their order, so the iteration
+        // continues at the same index of the source's fresh snapshot
+        cur = {hit.src, nullptr, idx};
         haveCur = true;
       }
     }
-    m.untrackAll(id);
     return true;
   }
 };

@@ -480,6 +480,13 @@ class OrderedQueue {
     return s_[pos_++];
   }
   void add(int x) { heap_.add(x); }
+  // Put back the most recently polled element (un-polls come in reverse poll order). An element that came from
+  // the sorted run and whose key did not change since returns to its slot in the run (O(1)); anything else goes
+  // through the heap. Either way the queue holds the same set, so the poll order is unchanged.
+  void unpoll(int x) {
+    if (pos_ > 0 && s_[pos_ - 1] == x) --pos_;
+    else heap_.add(x);
+  }
 
  private:
   Cmp cmp_;
