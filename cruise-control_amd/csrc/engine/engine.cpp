@@ -563,6 +563,7 @@ class ResourceDistribution : public GoalImpl {
   int res = 0;
   double upperThr = 0, lowerThr = 0;
   bool fix = false;
+  Model::SnapTable snapTab;  // moveIn's candidate-broker snapshots (one Spec per phase)
   int nameBase() const { return 4 * kind; }
   int nameId(bool reverse, bool leader) const { return nameBase() + (reverse ? 1 : 0) + (leader ? 2 : 0); }
   bool excluded(int b) const { return !allowed[b]; }
@@ -943,7 +944,7 @@ class ResourceDistribution : public GoalImpl {
     struct Seg {
       int cb;
       size_t skip;
-      std::shared_ptr<const std::vector<int32_t>> v;
+      const std::vector<int32_t>* v;  // valid until the next model change (snapTab holds it)
       size_t len() const { return v->size() > skip ? v->size() - skip : 0; }
     };
     std::vector<Seg> segs;
@@ -958,14 +959,14 @@ class ResourceDistribution : public GoalImpl {
         segs.clear();
         flat.clear();
         if (haveCur) {
-          cur.v = m.snapshot(cur.cb, spec);
+          cur.v = &m.snapshotIn(snapTab, cur.cb, spec);
           segs.push_back(cur);
           flat.insert(flat.end(), cur.v->begin() + std::min(cur.skip, cur.v->size()), cur.v->end());
           haveCur = false;
         }
         while (!pq.empty() && (segs.empty() || flat.size() < target) && cond()) {
           const int cb = pq.poll();
-          segs.push_back({cb, 0, m.snapshot(cb, spec)});
+          segs.push_back({cb, 0, &m.snapshotIn(snapTab, cb, spec)});
           flat.insert(flat.end(), segs.back().v->begin(), segs.back().v->end());
         }
       }

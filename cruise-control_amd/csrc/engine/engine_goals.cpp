@@ -985,6 +985,7 @@ class LeaderReplicaDistribution : public GoalImpl {
   // the polled source to b, and b is not queued), so the queue polls in comparator order and speculatively
   // polled sources can be put back: the next sources' sorted leaders are scanned together with the current
   // one's (growing the batch while nothing is accepted), exactly as RDG moveIn does.
+  Model::SnapTable snapTab;
   bool moveLeaderReplicasIn(Engine& e, int b) {
     Model& m = e.m;
     if (e.opt.anyExclLead && e.opt.exclLead[b]) return true;
@@ -1009,7 +1010,7 @@ class LeaderReplicaDistribution : public GoalImpl {
     e.eligible(single, DA_MOVE, cands);
     struct Seg {
       int src;
-      std::shared_ptr<const std::vector<int32_t>> v;  // the source's sorted leaders
+      const std::vector<int32_t>* v;  // the source's sorted leaders (held by snapTab until the next model change)
       size_t start;
       size_t len() const { return v->size() > start ? v->size() - start : 0; }
     };
@@ -1022,14 +1023,14 @@ class LeaderReplicaDistribution : public GoalImpl {
       segs.clear();
       flat.clear();
       if (haveCur) {  // the source being iterated continues first, after its winner
-        cur.v = m.snapshot(cur.src, s);
+        cur.v = &m.snapshotIn(snapTab, cur.src, s);
         segs.push_back(cur);
         haveCur = false;
         flat.insert(flat.end(), cur.v->begin() + std::min(cur.start, cur.v->size()), cur.v->end());
       }
       while (!pq.empty() && (segs.empty() || flat.size() < target)) {
         const int src = pq.poll();
-        segs.push_back({src, m.snapshot(src, s), 0});
+        segs.push_back({src, &m.snapshotIn(snapTab, src, s), 0});
         flat.insert(flat.end(), segs.back().v->begin(), segs.back().v->end());
       }
       const int64_t key = cands.empty() ? -1 : e.crossScan(*this, DA_MOVE, flat, 0, cands);

@@ -292,6 +292,29 @@ class Model {
   // Contents a SortedReplicas(b, s) initialised now would have (shared with the initialisation cache): equal to
   // the live view of a set tracked earlier, because every key change re-inserts the replica.
   std::shared_ptr<const std::vector<int32_t>> snapshot(int b, const Spec& s);
+  // One Spec's snapshots of every broker, looked up by broker id and version (no per-call cache search or
+  // reference counting): the drivers that poll many brokers per scan (moveIn, swap) keep one per Spec.
+  struct SnapTable {
+    Spec spec;
+    const void* owner = nullptr;  // the Model the table was filled from
+    bool bound = false;
+    std::vector<uint32_t> ver;  // bVer[b] + 1 of the stored snapshot, 0 = none
+    std::vector<std::shared_ptr<const std::vector<int32_t>>> v;
+  };
+  const std::vector<int32_t>& snapshotIn(SnapTable& t, int b, const Spec& s) {
+    if (!t.bound || t.owner != this || !(t.spec == s)) {
+      t.spec = s;
+      t.owner = this;
+      t.bound = true;
+      t.ver.assign(B, 0);
+      t.v.assign(B, nullptr);
+    }
+    if (t.ver[b] != bVer[b] + 1u) {
+      t.v[b] = snapshot(b, s);
+      t.ver[b] = bVer[b] + 1u;
+    }
+    return *t.v[b];
+  }
   bool selects(const Spec& s, int r) const;
   uint64_t replicaKey(const Spec& s, int r) const;
   int cmpReplica(const Spec& s, int a, int b) const;

@@ -170,12 +170,44 @@ int main() {
       spin(mail, g_seq);
     });
   }
-  // fine-grained device memory written by the CPU (needs a large BAR); report and skip if unavailable
+  // fine-grained device memory written by the CPU through the BAR (posted writes), read by the kernel from HBM
   int* fg = nullptr;
-  if (hipExtMallocWithFlags((void**)&fg, 1 << 16, hipDeviceMallocFinegrained) == hipSuccess) {
+  if (hipExtMallocWithFlags((void**)&fg, 1 << 20, hipDeviceMallocFinegrained) == hipSuccess) {
     hipPointerAttribute_t attr;
     const bool ok = hipPointerGetAttributes(&attr, fg) == hipSuccess;
     std::printf("fine-grained VRAM allocated (attr ok=%d, type=%d)\n", (int)ok, ok ? (int)attr.type : -1);
+    std::fflush(stdout);
+    // host store into it: only when the pointer is host-accessible (large BAR); a fault here ends the probe
+    volatile int* hv = fg;
+    hv[0] = 7;
+    std::printf("host store to fine-grained VRAM ok, readback %d\n", hv[0]);
+    std::fflush(stdout);
+    timeit("host writes 1 int to fine-grained VRAM + 2 dependent reads + mailbox", N, [&] {
+      ++g_seq;
+      hv[0] = (int)g_seq;
+      hipLaunchKernelGGL(k_read_chain, dim3(1), dim3(64), 0, st, fg, mailDev, g_seq);
+      spin(mail, g_seq);
+    });
+    static int buf[16384];
+    for (int n : {256, 4096, 16384}) {
+      char name[112];
+      std::snprintf(name, sizeof name, "host memcpy %d ints to fine-grained VRAM + wide read (64 blocks) + mailbox", n);
+      timeit(name, 500, [&] {
+        ++g_seq;
+        buf[0] = (int)g_seq;
+        std::memcpy(fg, buf, (size_t)n * 4);
+        hipLaunchKernelGGL(k_wide, dim3(64), dim3(256), 0, st, fg, n, mailDev, g_seq, done);
+        spin(mail, g_seq);
+      });
+      std::snprintf(name, sizeof name, "host memcpy %d ints to host-coherent + wide read (64 blocks) + mailbox", n);
+      timeit(name, 500, [&] {
+        ++g_seq;
+        buf[0] = (int)g_seq;
+        std::memcpy(hcoh, buf, (size_t)n * 4);
+        hipLaunchKernelGGL(k_wide, dim3(64), dim3(256), 0, st, hcohDev, n, mailDev, g_seq, done);
+        spin(mail, g_seq);
+      });
+    }
   } else {
     std::printf("fine-grained VRAM allocation failed\n");
   }
