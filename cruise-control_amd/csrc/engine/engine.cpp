@@ -434,6 +434,7 @@ class ReplicaDistribution : public GoalImpl {
       else javaHashSetOrder(ins, order);  // Collectors.toSet()
       for (int x : order) cand.add(x);
     }
+    cand.trackSequence();  // inorder() per accepted move is a copy
     const int upperSrc = excluded(b) ? 0 : upper;
     bool wasUnable = false;
     const std::vector<int32_t> list = m.sorted(b, kName);  // sortedReplicas(true): a clone

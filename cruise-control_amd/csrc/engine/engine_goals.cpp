@@ -700,6 +700,7 @@ class TopicReplicaDistribution : public GoalImpl {
       else javaHashSetOrder(ins, order);  // Collectors.toSet()
       for (int x : order) cand.add(x);
     }
+    cand.trackSequence();
     int n = m.tcount(t, b), nOff = 0;
     for (int r : m.bRepl[b])
       if (m.pTopic[m.rPart[r]] == t && m.rInOff[r]) nOff++;
@@ -949,6 +950,7 @@ class LeaderReplicaDistribution : public GoalImpl {
       javaHashSetOrder(ins, order);
       for (int x : order) cand.add(x);
     }
+    cand.trackSequence();
     const int upperLimit = fix ? 0 : upper;
     const int id = sortId(kind, false, !fix);
     Model::Spec s;

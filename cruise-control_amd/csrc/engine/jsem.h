@@ -175,6 +175,20 @@ class RbTreeSet {
     for (size_t i = 0; i < seqId_.size(); ++i) seqKey_[i] = n_[seqId_[i]].key;
     seqOn_ = true;
   }
+  // Maintain the in-order sequence next to the tree from now on (a tree built by add(): one traversal), so
+  // inorder() is a copy instead of a walk over every node.
+  void trackSequence() {
+    if (seqOn_) return;
+    seqId_.clear();
+    int p = root_;
+    if (p >= 0) {
+      while (n_[p].left >= 0) p = n_[p].left;
+      for (; p >= 0; p = succ(p)) seqId_.push_back(p);
+    }
+    seqKey_.resize(seqId_.size());
+    for (size_t i = 0; i < seqId_.size(); ++i) seqKey_[i] = n_[seqId_[i]].key;
+    seqOn_ = true;
+  }
   bool remove(int k) {
     int p = find(k);
     if (p < 0) return false;

@@ -94,10 +94,14 @@ struct OverlayLds {
   }
 };
 
-template <class Row, int Cap>
-__device__ __forceinline__ void stageRows(Row* dst, const Row* __restrict__ src, int n) {
-  const int words = n * (int)(sizeof(Row) / 4);
-  for (int w = threadIdx.x; w < words; w += blockDim.x)
+// Copy n rows (whole 32-bit words) from the host-mapped staging area into LDS. The first word of every thread is
+// loaded by the caller's single batch (stageLoad) so the three row kinds cost one PCIe round trip, not three.
+template <class Row>
+__device__ __forceinline__ int rowWords(int n) { return n * (int)(sizeof(Row) / 4); }
+template <class Row>
+__device__ __forceinline__ void stageRest(Row* dst, const Row* __restrict__ src, int n) {
+  const int words = rowWords<Row>(n);
+  for (int w = threadIdx.x + blockDim.x; w < words; w += blockDim.x)
     reinterpret_cast<int32_t*>(dst)[w] = reinterpret_cast<const int32_t*>(src)[w];
 }
 
@@ -148,9 +152,19 @@ __device__ __forceinline__ void overlayStage(OverlayLds& ov, const UpdateList& U
     ov.np = U.np;
   }
   if (U.nb | U.nr | U.np) {
-    stageRows<BrokerRow, kOvB>(ov.b, U.brows, U.nb);
-    stageRows<ReplicaRow, kOvR>(ov.r, U.rrows, U.nr);
-    stageRows<PartitionRow, kOvP>(ov.p, U.prows, U.np);
+    // one batch of independent host reads (a thread's first word of each row kind), then the stores
+    const int t = threadIdx.x;
+    const int wb = rowWords<BrokerRow>(U.nb), wr = rowWords<ReplicaRow>(U.nr), wp = rowWords<PartitionRow>(U.np);
+    int32_t xb = 0, xr = 0, xp = 0;
+    if (t < wb) xb = reinterpret_cast<const int32_t*>(U.brows)[t];
+    if (t < wr) xr = reinterpret_cast<const int32_t*>(U.rrows)[t];
+    if (t < wp) xp = reinterpret_cast<const int32_t*>(U.prows)[t];
+    if (t < wb) reinterpret_cast<int32_t*>(ov.b)[t] = xb;
+    if (t < wr) reinterpret_cast<int32_t*>(ov.r)[t] = xr;
+    if (t < wp) reinterpret_cast<int32_t*>(ov.p)[t] = xp;
+    stageRest<BrokerRow>(ov.b, U.brows, U.nb);
+    stageRest<ReplicaRow>(ov.r, U.rrows, U.nr);
+    stageRest<PartitionRow>(ov.p, U.prows, U.np);
   }
   __syncthreads();
 }
@@ -202,11 +216,19 @@ struct PreView {
     prk6 = x.racks[6];
     prk7 = x.racks[7];
   }
+  // Every HBM field is loaded unconditionally (independent loads the compiler can issue together) and then
+  // replaced from the LDS overlay when the entity is dirty in this launch.
   __device__ __forceinline__ void loadRow(const DevTables& t, const DevProgram& prog, int rr, const OverlayLds& ov) {
     r = rr;
     const ReplicaRec& rec = t.replicas[r];
     orig = rec.orig;
     p = rec.part;
+    src = rec.broker;
+    rflags = rec.flags;
+    ru0 = rec.util[0];
+    ru1 = rec.util[1];
+    ru2 = rec.util[2];
+    ru3 = rec.util[3];
     const int ri = ov.replica(r);
     if (ri >= 0) {
       const ReplicaRow& x = ov.r[ri];
@@ -216,14 +238,23 @@ struct PreView {
       ru1 = x.util[1];
       ru2 = x.util[2];
       ru3 = x.util[3];
-    } else {
-      src = rec.broker;
-      rflags = rec.flags;
-      ru0 = rec.util[0];
-      ru1 = rec.util[1];
-      ru2 = rec.util[2];
-      ru3 = rec.util[3];
     }
+    setPartition(t.parts[p]);
+    const BrokerRec& sb = t.brokers[src];
+    bool aSrc = sb.alive != 0;
+    snrep = sb.nrep;
+    sbu0 = sb.util[0];
+    sbu1 = sb.util[1];
+    sbu2 = sb.util[2];
+    sbu3 = sb.util[3];
+    snlead = sb.nlead;
+    spot = sb.pot;
+    slbi = sb.lbi;
+    scap0 = sb.cap[0];
+    scap1 = sb.cap[1];
+    scap2 = sb.cap[2];
+    scap3 = sb.cap[3];
+    srcAllowed = sb.allowedBits;
     const int pi = ov.partition(p);
     if (pi >= 0) {
       const PartitionRow& x = ov.p[pi];
@@ -245,13 +276,8 @@ struct PreView {
       prk5 = x.racks[5];
       prk6 = x.racks[6];
       prk7 = x.racks[7];
-      topic = t.parts[p].topic;
-    } else {
-      setPartition(t.parts[p]);
     }
-    const BrokerRec& sb = t.brokers[src];
     const int si = ov.broker(src);
-    bool aSrc;
     if (si >= 0) {
       const BrokerRow& x = ov.b[si];
       aSrc = x.alive != 0;
@@ -263,34 +289,35 @@ struct PreView {
       snlead = x.nlead;
       spot = x.potNwOut;
       slbi = x.leadNwIn;
-    } else {
-      aSrc = sb.alive != 0;
-      snrep = sb.nrep;
-      sbu0 = sb.util[0];
-      sbu1 = sb.util[1];
-      sbu2 = sb.util[2];
-      sbu3 = sb.util[3];
-      snlead = sb.nlead;
-      spot = sb.pot;
-      slbi = sb.lbi;
     }
-    aliveBits = aSrc ? 1u : 0u;
-    scap0 = sb.cap[0];
-    scap1 = sb.cap[1];
-    scap2 = sb.cap[2];
-    scap3 = sb.cap[3];
-    srcAllowed = sb.allowedBits;
+    aliveBits = (aliveBits & 4u) | (aSrc ? 1u : 0u);
     if (prog.needs & NEED_TOPIC) {
       tup = t.tUpper[topic];
       tlo = t.tLower[topic];
       stc = t.topicCount[(size_t)topic * t.ldB + src];
+      dtc = t.topicCount[(size_t)topic * t.ldB + dst];
     }
   }
-  __device__ __forceinline__ void loadDst(const DevTables& t, const DevProgram& prog, int d, const OverlayLds& ov) {
+  // The destination side, loaded BEFORE the row (it depends only on the destination id); the destination's
+  // topic count needs the row's topic and is read in loadRow.
+  __device__ __forceinline__ void loadDst(const DevTables& t, int d, const OverlayLds& ov) {
     dst = d;
     const BrokerRec& db = t.brokers[d];
+    bool aDst = db.alive != 0;
+    dnrep = db.nrep;
+    dbu0 = db.util[0];
+    dbu1 = db.util[1];
+    dbu2 = db.util[2];
+    dbu3 = db.util[3];
+    dnlead = db.nlead;
+    dpot = db.pot;
+    dlbi = db.lbi;
+    dcap0 = db.cap[0];
+    dcap1 = db.cap[1];
+    dcap2 = db.cap[2];
+    dcap3 = db.cap[3];
+    drack = db.rack;
     const int di = ov.broker(d);
-    bool aDst;
     if (di >= 0) {
       const BrokerRow& x = ov.b[di];
       aDst = x.alive != 0;
@@ -302,24 +329,8 @@ struct PreView {
       dnlead = x.nlead;
       dpot = x.potNwOut;
       dlbi = x.leadNwIn;
-    } else {
-      aDst = db.alive != 0;
-      dnrep = db.nrep;
-      dbu0 = db.util[0];
-      dbu1 = db.util[1];
-      dbu2 = db.util[2];
-      dbu3 = db.util[3];
-      dnlead = db.nlead;
-      dpot = db.pot;
-      dlbi = db.lbi;
     }
-    aliveBits = (aliveBits & 1u) | (aDst ? 4u : 0u);
-    dcap0 = db.cap[0];
-    dcap1 = db.cap[1];
-    dcap2 = db.cap[2];
-    dcap3 = db.cap[3];
-    drack = db.rack;
-    if (prog.needs & NEED_TOPIC) dtc = t.topicCount[(size_t)topic * t.ldB + d];
+    aliveBits = aDst ? 4u : 0u;
   }
   __device__ __forceinline__ double bu(int b, int k) const {
     return b == dst ? sel(k, dbu0, dbu1, dbu2, dbu3) : sel(k, sbu0, sbu1, sbu2, sbu3);
@@ -463,6 +474,15 @@ __global__ __launch_bounds__(kBlock) void scan_cross(DevTables T, MutTables Mt, 
     const uint32_t kb = base / (uint32_t)Nr;
     const unsigned long long keyBase = (unsigned long long)kb * N + c0 + (base - kb * (uint32_t)Nr);
     if (blockBest(result) <= keyBase) break;  // an earlier pair already won: nothing later can (block-uniform)
+    // the request's indices (host-mapped) are read before the overlay is staged: both round trips overlap
+    const uint32_t q = base + threadIdx.x;
+    const uint32_t k = q / (uint32_t)Nr;
+    const uint32_t j = q - k * (uint32_t)Nr;
+    int rq = 0, dq = 0;
+    if (q < total) {
+      rq = reps[k];
+      dq = cands[j];
+    }
     if (!staged) {
       overlayStage(ov, U);
       overlayApply(ov, U, Mt, T);
@@ -470,13 +490,10 @@ __global__ __launch_bounds__(kBlock) void scan_cross(DevTables T, MutTables Mt, 
       CCMI_STAMP(T, seq, 1);
     }
     unsigned long long local = kNone;
-    const uint32_t q = base + threadIdx.x;
     if (q < total) {
-      const uint32_t k = q / (uint32_t)Nr;
-      const uint32_t j = q - k * (uint32_t)Nr;
       PreView v;
-      v.loadRow(T, prog, reps[k], ov);
-      v.loadDst(T, prog, cands[j], ov);
+      v.loadDst(T, dq, ov);
+      v.loadRow(T, prog, rq, ov);
       const bool inList = prog.filter != FILTER_RACK_AWARE || v.rackEligible();
       if (inList && moveCandidateAccepted(prog, v, v.r, v.dst)) local = (unsigned long long)k * N + c0 + j;
     }
@@ -573,6 +590,12 @@ __global__ __launch_bounds__(kBlock) void scan_pairs(DevTables T, MutTables Mt, 
   bool staged = false;
   for (int base = blockIdx.x * kBlock; base < n; base += gridDim.x * kBlock) {
     if (blockBest(result) <= (unsigned long long)(keyBase + base)) break;
+    const int q = base + threadIdx.x;
+    int rq = 0, dq = 0;
+    if (q < n) {  // request reads overlap the overlay staging (see scan_cross)
+      rq = pr[q];
+      dq = pb[q];
+    }
     if (!staged) {
       overlayStage(ov, U);
       overlayApply(ov, U, Mt, T);
@@ -580,11 +603,10 @@ __global__ __launch_bounds__(kBlock) void scan_pairs(DevTables T, MutTables Mt, 
       CCMI_STAMP(T, seq, 1);
     }
     unsigned long long local = kNone;
-    const int q = base + threadIdx.x;
     if (q < n) {
       PreView v;
-      v.loadRow(T, prog, pr[q], ov);
-      v.loadDst(T, prog, pb[q], ov);
+      v.loadDst(T, dq, ov);
+      v.loadRow(T, prog, rq, ov);
       if (moveCandidateAccepted(prog, v, v.r, v.dst)) local = (unsigned long long)(keyBase + q);
     }
     CCMI_STAMP(T, seq, 2);
