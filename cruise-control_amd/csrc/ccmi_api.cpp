@@ -85,11 +85,19 @@ void setOptions(ccmi_session* s, const ccmi_balancing_constraint* c, const ccmi_
   opt.requested.assign(B, 0);
   if (o) {
     if (o->num_excluded_topics > 0) throw ccmi::Unsupported("excluded topics are outside ABI v1 scope");
-    if (o->num_excluded_brokers_for_leadership > 0)
-      throw ccmi::Unsupported("excluded brokers for leadership are outside ABI v1 scope");
-    if (o->num_excluded_brokers_for_replica_move > 0)
-      throw ccmi::Unsupported("excluded brokers for replica move are outside ABI v1 scope");
-    if (o->only_move_immigrant_replicas) throw ccmi::Unsupported("only_move_immigrant_replicas is outside ABI v1 scope");
+    for (int i = 0; i < o->num_excluded_brokers_for_leadership; ++i) {
+      const int b = o->excluded_brokers_for_leadership[i];
+      if (b < 0 || b >= B) throw std::invalid_argument("excluded broker for leadership out of range");
+      opt.exclLead[b] = 1;
+      opt.anyExclLead = true;
+    }
+    for (int i = 0; i < o->num_excluded_brokers_for_replica_move; ++i) {
+      const int b = o->excluded_brokers_for_replica_move[i];
+      if (b < 0 || b >= B) throw std::invalid_argument("excluded broker for replica move out of range");
+      opt.exclMove[b] = 1;
+      opt.anyExclMove = true;
+    }
+    opt.onlyImmigrants = o->only_move_immigrant_replicas != 0;
     for (int i = 0; i < o->num_requested_destination_broker_ids; ++i) {
       const int b = o->requested_destination_broker_ids[i];
       if (b < 0 || b >= B) throw std::invalid_argument("requested destination broker out of range");

@@ -234,6 +234,17 @@ void Device::setAllowed(int slot, const uint8_t* allowedB) {
   hipCheck(hipStreamSynchronize(ST), "sync");
 }
 
+void Device::setExclusions(const uint8_t* exclLead, const uint8_t* exclMove) {
+  const uint32_t mask = (1u << kExclLeadBit) | (1u << kExclMoveBit);
+  for (int b = 0; b < B_; ++b)
+    allowedHost_[b] = (allowedHost_[b] & ~mask) | (exclLead[b] ? (1u << kExclLeadBit) : 0u) |
+                      (exclMove[b] ? (1u << kExclMoveBit) : 0u);
+  hipCheck(hipMemcpy2DAsync(&brokers_[0].allowedBits, sizeof(BrokerRec), allowedHost_.data(), sizeof(uint32_t),
+                            sizeof(uint32_t), B_, hipMemcpyHostToDevice, ST),
+           "upload exclusions");
+  hipCheck(hipStreamSynchronize(ST), "sync");
+}
+
 void Device::setTopicLimits(const int32_t* upper, const int32_t* lower) {
   hipCheck(hipMemcpyAsync(tUpper_, upper, sizeof(int32_t) * T_, hipMemcpyHostToDevice, ST), "upload tUpper");
   hipCheck(hipMemcpyAsync(tLower_, lower, sizeof(int32_t) * T_, hipMemcpyHostToDevice, ST), "upload tLower");

@@ -48,6 +48,9 @@ class Device {
                      const uint8_t* rFlags, const int32_t* pBrokers, const double* pLeadNwOut,
                      const int32_t* topicCountDense /* [T][ldB] */);
   void setAllowed(int slot, const uint8_t* allowedB);
+  // OptimizationOptions.excludedBrokersFor{Leadership,ReplicaMove} as bits kExclLeadBit / kExclMoveBit of every
+  // broker's allowedBits
+  void setExclusions(const uint8_t* exclLead, const uint8_t* exclMove);
   // TopicReplicaDistributionGoal balance limits per topic (frozen at its initGoalState)
   void setTopicLimits(const int32_t* upper, const int32_t* lower);
 

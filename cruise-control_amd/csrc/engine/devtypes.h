@@ -19,6 +19,8 @@
 namespace ccmi {
 
 constexpr int kMaxGoals = 20;
+constexpr int kExclLeadBit = 31;  // allowedBits bit of a broker excluded for leadership (above every goal slot)
+constexpr int kExclMoveBit = 30;  // allowedBits bit of a broker excluded for replica moves
 constexpr int kMaxRf = 8;
 
 enum DevGoalKind : int32_t {
@@ -68,6 +70,8 @@ struct DevProgram {
   int32_t action;
   uint32_t needs;   // DevNeed bits over all goals of the program
   int32_t filter;   // DevFilter of a CROSS scan
+  int32_t exclLeadMove;  // replica moves: a leader replica may not go to a broker excluded for leadership
+  int32_t swapExcl;      // swaps: GoalUtils.eligibleReplicasForSwap exclusion rules apply
   DevGoal goals[kMaxGoals];
 };
 
@@ -80,7 +84,7 @@ struct alignas(64) BrokerRec {
   double pot;             // potential leadership NW_OUT (ClusterModel.potentialLeadershipLoadFor)
   double lbi;             // leadership NW_IN (Broker.leadershipLoadForNwResources)
   int32_t nrep, nlead, rack;
-  uint32_t allowedBits;   // bit g: in goal slot g's _brokersAllowedReplicaMove
+  uint32_t allowedBits;   // bit g: in goal slot g's _brokersAllowedReplicaMove; bit 31: excluded for leadership
   int32_t alive;
   int32_t pad[7];
 };

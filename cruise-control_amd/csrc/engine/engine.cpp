@@ -105,13 +105,20 @@ DevProgram Engine::program(const GoalImpl& self, int action) const {
   p.needs = 0;
   for (int i = 0; i < p.nGoals; ++i) p.needs |= needsOf(p.goals[i]);
   p.filter = FILTER_NONE;
+  // GoalUtils.eligibleBrokers (GoalUtils.java:122-160): without requested destinations a LEADER replica's move
+  // skips brokers excluded for leadership — replica-dependent, so it is checked per candidate on the device
+  p.exclLeadMove = (opt.anyExclLead && !opt.anyRequested && action == DA_MOVE) ? 1 : 0;
+  p.swapExcl = (action == DA_SWAP && (opt.anyExclLead || opt.anyExclMove)) ? 1 : 0;
   return p;
 }
 
-// GoalUtils.eligibleBrokers for the replica-independent option subset of ABI v1.
+// GoalUtils.eligibleBrokers (GoalUtils.java:122-160), the replica-independent part: requested destinations,
+// brokers excluded for replica moves, and (leadership moves) brokers excluded for leadership. The leader-replica
+// move case is the device's exclLeadMove check.
 void Engine::eligible(const std::vector<int32_t>& in, int action, std::vector<int32_t>& out) const {
   out.clear();
   for (int b : in) {
+    if (action == DA_LEADERSHIP && opt.anyExclLead && opt.exclLead[b]) continue;
     if (opt.anyRequested) {
       if (action != DA_LEADERSHIP && !opt.requested[b]) continue;
     } else if (opt.anyExclMove && action == DA_MOVE && opt.exclMove[b]) {
@@ -119,6 +126,25 @@ void Engine::eligible(const std::vector<int32_t>& in, int action, std::vector<in
     }
     out.push_back(b);
   }
+}
+
+// Reference-equivalent candidates of a cross scan whose leader rows skip brokers excluded for leadership:
+// every row before the hit visits its eligible list, the hit row up to and including the winner.
+int64_t Engine::exclLeadCount(const int32_t* reps, int K, const std::vector<int32_t>& cands, int64_t key) const {
+  const int N = (int)cands.size();
+  int nEx = 0;
+  for (int b : cands) nEx += opt.exclLead[b] ? 1 : 0;
+  const int rows = key >= 0 ? (int)(key / N) : K;
+  int64_t c = 0;
+  for (int k = 0; k < rows; ++k) c += N - (m.rLeader[reps[k]] ? nEx : 0);
+  if (key >= 0) {
+    const int j = (int)(key % N);
+    int exBefore = 0;
+    if (m.rLeader[reps[rows]])
+      for (int q = 0; q < j; ++q) exBefore += opt.exclLead[cands[q]] ? 1 : 0;
+    c += j + 1 - exBefore;
+  }
+  return c;
 }
 
 int64_t Engine::crossScan(GoalImpl& self, int action, const std::vector<int32_t>& reps, size_t r0,
@@ -133,7 +159,10 @@ int64_t Engine::crossScan(GoalImpl& self, int action, const std::vector<int32_t>
   prog.filter = filter;
   const int c0 = (int)((int64_t)N * shard.rank / shard.count), c1 = (int)((int64_t)N * (shard.rank + 1) / shard.count);
   const int64_t key = combine(dev->scanCross(prog, reps.data() + r0, K, cands.data(), N, c0, c1));
-  if (count) candidates += key >= 0 ? key + 1 : (int64_t)K * N;
+  if (count) {
+    if (prog.exclLeadMove) candidates += exclLeadCount(reps.data() + r0, K, cands, key);
+    else candidates += key >= 0 ? key + 1 : (int64_t)K * N;
+  }
   return key;
 }
 
@@ -150,8 +179,14 @@ int64_t Engine::pairScan(GoalImpl& self, const std::vector<int32_t>& pr, const s
   m.flushToDevice();
   const int n = (int)pr.size();
   const int p0 = (int)((int64_t)n * shard.rank / shard.count), p1 = (int)((int64_t)n * (shard.rank + 1) / shard.count);
-  const int64_t key = combine(dev->scanPairs(program(self, action), pr.data(), pb.data(), p0, p1));
-  candidates += key >= 0 ? key + 1 : (int64_t)pr.size();
+  const DevProgram prog = program(self, action);
+  const int64_t key = combine(dev->scanPairs(prog, pr.data(), pb.data(), p0, p1));
+  if (prog.exclLeadMove) {
+    const size_t end = key >= 0 ? (size_t)key + 1 : pr.size();
+    for (size_t q = 0; q < end; ++q) candidates += (m.rLeader[pr[q]] && opt.exclLead[pb[q]]) ? 0 : 1;
+  } else {
+    candidates += key >= 0 ? key + 1 : (int64_t)pr.size();
+  }
   return key;
 }
 
@@ -274,6 +309,12 @@ bool Engine::optimizeGoal(std::unique_ptr<GoalImpl> g, ccmi_goal_result* res) {
   g->dg.allowedSlot = (int)optimized.size();
   g->init(*this);
   dev->setAllowed(g->dg.allowedSlot, g->allowed.data());
+  if (opt.anyExclLead || opt.anyExclMove || exclOnDevice) {
+    const std::vector<uint8_t> none(m.B, 0);
+    dev->setExclusions(opt.anyExclLead ? opt.exclLead.data() : none.data(),
+                       opt.anyExclMove ? opt.exclMove.data() : none.data());
+    exclOnDevice = opt.anyExclLead || opt.anyExclMove;
+  }
   const bool brokenEmpty = m.numDead == 0 && m.numBadDisk == 0;
   bool exclWithReplicas = false;
   for (int b = 0; b < m.B; ++b)

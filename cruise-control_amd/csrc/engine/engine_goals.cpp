@@ -111,8 +111,11 @@ class RackAware : public GoalImpl {
     }
     return true;
   }
-  // candidates of `cands[0, upto)` that rackAwareEligibleBrokers keeps (:193-211)
-  static int64_t eligibleCount(const Model& m, int r, const std::vector<int32_t>& cands, size_t upto) {
+  // candidates of `cands[0, upto)` that rackAwareEligibleBrokers keeps (:193-211) and, for a leader replica,
+  // filterOutBrokersExcludedForLeadership leaves (GoalUtils.java:122-135)
+  static int64_t eligibleCount(const Engine& e, int r, const std::vector<int32_t>& cands, size_t upto) {
+    const Model& m = e.m;
+    const bool exclLead = e.opt.anyExclLead && !e.opt.anyRequested && m.rLeader[r];
     int racks[kMaxRf];
     int n = 0;
     const int p = m.rPart[r];
@@ -126,6 +129,7 @@ class RackAware : public GoalImpl {
     for (size_t j = 0; j < upto; ++j) {
       bool in = true;
       for (int i = 0; i < n; ++i) in &= racks[i] != m.bRack[cands[j]];
+      if (exclLead && e.opt.exclLead[cands[j]]) in = false;
       c += in;
     }
     return c;
@@ -142,7 +146,7 @@ class RackAware : public GoalImpl {
       if (m.alive(b) && !m.curOffline(r) && keep(m, r)) continue;
       one[0] = r;
       const int64_t key = e.crossScan(*this, DA_MOVE, one, 0, cands, FILTER_RACK_AWARE, false);
-      e.candidates += eligibleCount(m, r, cands, key >= 0 ? (size_t)key + 1 : cands.size());
+      e.candidates += eligibleCount(e, r, cands, key >= 0 ? (size_t)key + 1 : cands.size());
       if (key < 0)
         throw OptimizationFailure("[" + name + "] Cannot move replica of partition " + std::to_string(m.rPart[r]) +
                                   " to a rack-aware broker.");

@@ -325,6 +325,16 @@ CCMI_HD bool moveCandidateAccepted(const DevProgram& prog, const V& v, int r, in
   return true;
 }
 
+// GoalUtils.eligibleReplicasForSwap (GoalUtils.java:258-274): a swap row is empty when the destination broker is
+// excluded for leadership and the (originally online) source replica is a leader, or the destination is excluded
+// for replica moves and the source replica is originally online.
+template <class V>
+CCMI_HD bool swapRowExcluded(const DevProgram& prog, const V& v, int sr, int db) {
+  if (!prog.swapExcl || v.origOff(sr)) return false;
+  if (v.allowed(kExclMoveBit, db)) return true;
+  return (v.flags(sr) & RF_LEADER) && v.allowed(kExclLeadBit, db);
+}
+
 // One step of AbstractGoal.maybeApplySwapAction's loop for (source sr, destination replica dr on db):
 // returns 0 = continue, 1 = terminal ACCEPT, 2 = terminal null (return null).
 template <class V>

@@ -185,6 +185,7 @@ struct PreView {
   uint32_t aliveBits;   // bit 0 src, bit 2 dst (values, never addressed: keeps the view in VGPRs)
   uint32_t srcAllowed;  // allowedBits of src
   int pn, pb0, pb1, pb2, pb3, pb4, pb5, pb6, pb7;
+  uint32_t dAllowed;    // allowedBits of dst (bit kExclLeadBit: excluded for leadership)
   double ru0, ru1, ru2, ru3, sbu0, sbu1, sbu2, sbu3, scap0, scap1, scap2, scap3;
   double dbu0, dbu1, dbu2, dbu3, dcap0, dcap1, dcap2, dcap3;
   // optional operands
@@ -317,6 +318,7 @@ struct PreView {
     dcap2 = db.cap[2];
     dcap3 = db.cap[3];
     drack = db.rack;
+    dAllowed = db.allowedBits;
     const int di = ov.broker(d);
     if (di >= 0) {
       const BrokerRow& x = ov.b[di];
@@ -352,6 +354,10 @@ struct PreView {
     return (pb0 == b) | (pb1 == b) | (pb2 == b) | (pb3 == b) | (pb4 == b) | (pb5 == b) | (pb6 == b) | (pb7 == b);
   }
   __device__ __forceinline__ int rack(int /*b == dst*/) const { return drack; }
+  // GoalUtils.filterOutBrokersExcludedForLeadership for a leader replica's move (GoalUtils.java:170-180)
+  __device__ __forceinline__ bool exclLeadBlocked(const DevProgram& prog) const {
+    return prog.exclLeadMove && (rflags & RF_LEADER) && ((dAllowed >> kExclLeadBit) & 1u);
+  }
   __device__ __forceinline__ bool otherOnRack(int /*p*/, int self, int rk) const {
     return (pb0 >= 0 && pb0 != self && prk0 == rk) | (pb1 >= 0 && pb1 != self && prk1 == rk) |
            (pb2 >= 0 && pb2 != self && prk2 == rk) | (pb3 >= 0 && pb3 != self && prk3 == rk) |
@@ -494,7 +500,7 @@ __global__ __launch_bounds__(kBlock) void scan_cross(DevTables T, MutTables Mt, 
       PreView v;
       v.loadDst(T, dq, ov);
       v.loadRow(T, prog, rq, ov);
-      const bool inList = prog.filter != FILTER_RACK_AWARE || v.rackEligible();
+      const bool inList = (prog.filter != FILTER_RACK_AWARE || v.rackEligible()) && !v.exclLeadBlocked(prog);
       if (inList && moveCandidateAccepted(prog, v, v.r, v.dst)) local = (unsigned long long)k * N + c0 + j;
     }
     CCMI_STAMP(T, seq, 2);
@@ -532,6 +538,10 @@ __global__ __launch_bounds__(kBlock) void scan_swap(DevTables T, DevProgram prog
       continue;
     }
     const int db = v.rbroker(cbRep[c0]);  // every row's candidates live on one broker
+    if (swapRowExcluded(prog, v, sr, db)) {
+      if (lane == 0) rowVisited[row] = 0;
+      continue;
+    }
     int visited = c1 - c0;
     for (int base = c0; base < c1; base += 64) {
       const int idx = base + lane;
@@ -607,7 +617,8 @@ __global__ __launch_bounds__(kBlock) void scan_pairs(DevTables T, MutTables Mt, 
       PreView v;
       v.loadDst(T, dq, ov);
       v.loadRow(T, prog, rq, ov);
-      if (moveCandidateAccepted(prog, v, v.r, v.dst)) local = (unsigned long long)(keyBase + q);
+      if (!v.exclLeadBlocked(prog) && moveCandidateAccepted(prog, v, v.r, v.dst))
+        local = (unsigned long long)(keyBase + q);
     }
     CCMI_STAMP(T, seq, 2);
     const unsigned long long m = blockMin(local);

@@ -156,7 +156,7 @@ typedef struct ccmi_balancing_constraint {
 
 /* analyzer/OptimizationOptions.java (7-field form) */
 typedef struct ccmi_opt_options {
-  const int32_t* excluded_topics;
+  const int32_t* excluded_topics; /* must be empty: CCMI_E_UNSUPPORTED otherwise */
   int32_t num_excluded_topics;
   const int32_t* excluded_brokers_for_leadership;
   int32_t num_excluded_brokers_for_leadership;

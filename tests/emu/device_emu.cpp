@@ -133,6 +133,12 @@ void Device::setAllowed(int slot, const uint8_t* a) {
   auto& al = E(st_).allowed;
   for (int b = 0; b < B_; ++b) al[b] = (al[b] & ~(1u << slot)) | (a[b] ? (1u << slot) : 0u);
 }
+void Device::setExclusions(const uint8_t* lead, const uint8_t* move) {
+  Emu& e = E(st_);
+  const uint32_t mask = (1u << kExclLeadBit) | (1u << kExclMoveBit);
+  for (int b = 0; b < e.B; ++b)
+    e.allowed[b] = (e.allowed[b] & ~mask) | (lead[b] ? (1u << kExclLeadBit) : 0u) | (move[b] ? (1u << kExclMoveBit) : 0u);
+}
 void Device::setTopicLimits(const int32_t* upper, const int32_t* lower) {
   E(st_).tUpper.assign(upper, upper + T_);
   E(st_).tLower.assign(lower, lower + T_);
@@ -175,6 +181,7 @@ int64_t Device::scanCross(const DevProgram& prog, const int32_t* reps, int K, co
   for (int k = 0; k < K; ++k)
     for (int j = c0; j < c1; ++j) {
       if (prog.filter == FILTER_RACK_AWARE && !v.rackEligible(reps[k], cands[j])) continue;
+      if (prog.exclLeadMove && (v.flags(reps[k]) & RF_LEADER) && v.allowed(kExclLeadBit, cands[j])) continue;
       if (moveCandidateAccepted(prog, v, reps[k], cands[j])) return (int64_t)k * N + j;
     }
   return -1;
@@ -185,8 +192,10 @@ int64_t Device::scanPairs(const DevProgram& prog, const int32_t* pr, const int32
   View v{E(st_)};
   perf.scanLaunches++;
   perf.scanPairs += p1 - p0;
-  for (int q = p0; q < p1; ++q)
+  for (int q = p0; q < p1; ++q) {
+    if (prog.exclLeadMove && (v.flags(pr[q]) & RF_LEADER) && v.allowed(kExclLeadBit, pb[q])) continue;
     if (moveCandidateAccepted(prog, v, pr[q], pb[q])) return q;
+  }
   return -1;
 }
 
@@ -202,6 +211,7 @@ int64_t Device::scanSwap(const DevProgram& prog, const int32_t* srcs, int S, con
       const int c0 = cbOff[m], c1 = cbOff[m + 1];
       if (c0 == c1) continue;
       const int db = E(st_).rBroker[cbRep[c0]];
+      if (swapRowExcluded(prog, v, srcs[s], db)) continue;
       for (int j = c0; j < c1; ++j) {
         const int o = swapCandidateOutcome(prog, v, srcs[s], cbRep[j], db);
         (*visited)++;

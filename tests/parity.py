@@ -82,7 +82,8 @@ def check_product_against_oracle(lib, props, goals, balance=None, device=0, max_
     assert cm.replica_distribution() == oc.replica_distribution()
     assert cm.leader_distribution() == oc.leader_distribution()
     for r, o in zip(res.goal_results, ores):
-        assert (r.name, r.succeeded, r.candidates, r.actions) == (o.name, o.succeeded, o.candidates, o.actions)
+        assert (r.name, r.succeeded, r.candidates, r.actions) == (o.name, o.succeeded, o.candidates, o.actions), \
+            ((r.name, r.succeeded, r.candidates, r.actions), (o.name, o.succeeded, o.candidates, o.actions))
         compare_stats(r.stats, o.stats)
     # Set<ExecutionProposal>: order-free
     assert sorted(map(_key, res.proposals)) == sorted(map(_key, oc.proposals()))

@@ -76,3 +76,26 @@ def test_emu_goal_orders(emu_lib, oracle_lib, goals):
 def test_emu_requested_destinations_match_oracle(emu_lib, oracle_lib, props, requested, goals):
     opts = ccmi.OptimizationOptions(requested_destination_broker_ids=list(requested), fast_mode=False)
     check_product_against_oracle(emu_lib, props, goals, 1.05, max_replicas=3000, options=opts)
+
+
+# OptimizationOptions broker exclusions (GoalUtils.eligibleBrokers / filterOutBrokersExcludedFor{Leadership,
+# ReplicaMove}, GoalUtils.java:122-199; eligibleReplicasForSwap :258-274; ResourceDistributionGoal followers-only
+# phases :451,629,719) and onlyMoveImmigrantReplicas.
+EXCLUSION_CASES = [
+    (dict(num_racks=5, num_brokers=20, num_replicas=6000, num_topics=300),
+     dict(excluded_brokers_for_replica_move=[2, 5, 11]), DEFAULT_GOALS),
+    (dict(num_racks=5, num_brokers=20, num_replicas=6000, num_topics=300),
+     dict(excluded_brokers_for_leadership=[0, 3, 7]), DEFAULT_GOALS),
+    (dict(num_racks=6, num_brokers=24, num_replicas=4800, num_topics=30, num_dead_brokers=3),
+     dict(excluded_brokers_for_replica_move=[4, 9], excluded_brokers_for_leadership=[5, 13]), DEFAULT_GOALS),
+    (dict(num_racks=5, num_brokers=20, num_replicas=6000, num_topics=300),
+     dict(excluded_brokers_for_leadership=[1, 2], excluded_brokers_for_replica_move=[3]), C1_GOALS),
+    (dict(num_racks=6, num_brokers=24, num_replicas=4800, num_topics=30, num_dead_brokers=3),
+     dict(only_move_immigrant_replicas=True), DEFAULT_GOALS),
+]
+
+
+@pytest.mark.parametrize("props,opts,goals", EXCLUSION_CASES)
+def test_emu_broker_exclusions_match_oracle(emu_lib, oracle_lib, props, opts, goals):
+    check_product_against_oracle(emu_lib, props, goals, 1.05, max_replicas=3000,
+                                 options=ccmi.OptimizationOptions(fast_mode=False, **opts))

@@ -118,3 +118,19 @@ def test_gpu_acceptance_after_optimization(gpu_lib):
 def test_gpu_requested_destinations_match_oracle(gpu_lib, oracle_lib, props, requested):
     opts = ccmi.OptimizationOptions(requested_destination_broker_ids=list(requested), fast_mode=False)
     check_product_against_oracle(gpu_lib, props, DEFAULT_GOALS, 1.05, max_replicas=3000, options=opts)
+
+
+@pytest.mark.parametrize("props,opts,goals", [
+    (dict(num_racks=5, num_brokers=20, num_replicas=6000, num_topics=300),
+     dict(excluded_brokers_for_leadership=[0, 3, 7]), DEFAULT_GOALS),
+    (dict(num_racks=6, num_brokers=24, num_replicas=4800, num_topics=30, num_dead_brokers=3),
+     dict(excluded_brokers_for_replica_move=[4, 9], excluded_brokers_for_leadership=[5, 13]), DEFAULT_GOALS),
+    (dict(num_racks=5, num_brokers=20, num_replicas=6000, num_topics=300),
+     dict(excluded_brokers_for_leadership=[1, 2], excluded_brokers_for_replica_move=[3]), list(ccmi.C1_GOALS)),
+    (dict(num_brokers=40), dict(excluded_brokers_for_leadership=[0, 1, 2, 3], excluded_brokers_for_replica_move=[4]),
+     DEFAULT_GOALS),
+])
+def test_gpu_broker_exclusions_match_oracle(gpu_lib, oracle_lib, props, opts, goals):
+    """Leader-replica exclusion and swap-row exclusion run as device checks (allowedBits bits 30/31)."""
+    check_product_against_oracle(gpu_lib, props, goals, 1.05, max_replicas=3000,
+                                 options=ccmi.OptimizationOptions(fast_mode=False, **opts))
