@@ -983,6 +983,9 @@ class ResourceDistribution : public GoalImpl {
     }
     std::vector<int32_t> single{b}, cands;
     e.eligible(single, action, cands);
+    // b outside the eligible set (e.g. not a requested destination): every polled replica visits an empty
+    // candidate list, nothing moves and nothing is counted — the loop's outcome without walking every broker
+    if (cands.empty()) return true;
     struct Seg {
       int cb;
       size_t skip;

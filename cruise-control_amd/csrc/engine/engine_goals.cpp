@@ -1014,6 +1014,7 @@ class LeaderReplicaDistribution : public GoalImpl {
     int nl = m.bNlead[b];
     std::vector<int32_t> single{b}, cands;
     e.eligible(single, DA_MOVE, cands);
+    if (cands.empty()) return true;  // every source replica visits an empty candidate list: nothing moves
     struct Seg {
       int src;
       const std::vector<int32_t>* v;  // the source's sorted leaders (held by snapTab until the next model change)
