@@ -10,7 +10,10 @@ final ExecutionProposals). Each step works on its own device session, uploaded t
 starts; the step count K therefore means K independent proposal computations per GPU.
 
 value = reference-equivalent candidate moves evaluated/s summed over all ranks (the candidates the reference's
-first-fit loops would visit), ms_per_step = proposal wall time.
+first-fit loops would visit), ms_per_step = step wall time = proposal wall time at the default
+--requests-per-gpu 1. --requests-per-gpu S runs S independent what-if proposals concurrently per GPU in every step
+(one host thread + HIP stream per session, GoalOptimizer's precompute pool); proposal_wall_s is then the mean
+per-proposal latency.
 
 Multi-GPU (torchrun, one process per GPU): by default every rank runs its own independent what-if proposal
 request (weak scaling, no data-path collective); timing is max over ranks. --sharded instead shards ONE proposal's
@@ -106,6 +109,9 @@ def main() -> None:
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--workload", choices=sorted(WORKLOADS), default="c2")
+    ap.add_argument("--requests-per-gpu", type=int, default=1,
+                    help="S concurrent what-if proposals per GPU in every step (one host thread + HIP stream per "
+                         "session; the precompute pool of GoalOptimizer.java:117-119). Default 1: one proposal per step")
     ap.add_argument("--sharded", action="store_true",
                     help="N>1: one proposal sharded by destination broker over all ranks (RCCL MIN per scan) "
                          "instead of one independent what-if proposal per rank")
@@ -153,13 +159,24 @@ def main() -> None:
         inst_perf, inst_cands = ws.perf(), r.candidates
         del ws
 
-    sessions = [session() for _ in range(args.steps)]  # cluster resident in HBM before timing starts
+    S = max(1, args.requests_per_gpu) if not sharded else 1
+    # cluster resident in HBM before timing starts: one session per proposal
+    sessions = [[session() for _ in range(S)] for _ in range(args.steps)]
+    pool = None
+    if S > 1:
+        from concurrent.futures import ThreadPoolExecutor  # ctypes drops the GIL inside ccmi_optimizations
+        pool = ThreadPoolExecutor(S)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    results = [opt.optimizations(s, goals, options) for s in sessions]
+    results = []
+    for step_sessions in sessions:
+        if pool is None:
+            results.extend(opt.optimizations(s, goals, options) for s in step_sessions)
+        else:
+            results.extend(pool.map(lambda s: opt.optimizations(s, goals, options), step_sessions))
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -204,7 +221,8 @@ def main() -> None:
                    "partitions": buf.desc.num_partitions, "topics": buf.desc.num_topics,
                    "goals": goal_names, "parallelism": (f"destination-sharded x{world} (RCCL MIN allreduce per scan)" if sharded
                                    else f"independent what-if per GPU x{world}")},
-        "proposal_wall_s": elapsed / args.steps,
+        "requests_per_gpu": S,
+        "proposal_wall_s": sum(r.seconds for r in results) / len(results),
         "candidates_per_step": first.candidates,
         "actions_per_step": len(first.actions),
         "proposals_per_step": len(first.proposals),

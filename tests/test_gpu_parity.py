@@ -92,6 +92,27 @@ def test_gpu_sessions_are_independent(gpu_lib, oracle_lib):
     assert ra.candidates == rb.candidates
 
 
+def test_gpu_concurrent_sessions_match_sequential(gpu_lib, oracle_lib):
+    """Concurrent what-if requests on one device (one host thread and one HIP stream per session, the
+    precompute pool of GoalOptimizer.java:117-119; bench.py --requests-per-gpu) make the same decisions as a
+    sequential run and as the oracle."""
+    from concurrent.futures import ThreadPoolExecutor
+    props = dict(num_racks=5, num_brokers=40, num_replicas=12000, num_topics=400)
+    buf = ccmi.RandomCluster.generate(gpu_lib, **props)
+    opt = ccmi.GoalOptimizer(constraint(1.05))
+    seq = ccmi.ClusterModel.from_buffers(buf, device=0)
+    rs = opt.optimizations(seq, ccmi.goals_from_names(C1_GOALS))
+    sessions = [ccmi.ClusterModel.from_buffers(buf, device=0) for _ in range(6)]
+    with ThreadPoolExecutor(len(sessions)) as pool:
+        results = list(pool.map(lambda s: opt.optimizations(s, ccmi.goals_from_names(C1_GOALS)), sessions))
+    assert len(seq.actions()) > 0
+    for s, r in zip(sessions, results):
+        assert s.actions() == seq.actions()
+        assert r.candidates == rs.candidates
+        assert s.proposals() == seq.proposals()
+    check_product_against_oracle(gpu_lib, props, C1_GOALS, 1.05)
+
+
 def test_gpu_acceptance_after_optimization(gpu_lib):
     """Goal.actionAcceptance through the C ABI on the optimized goals of a session; an out-of-range goal index
     is an IllegalArgumentException."""
