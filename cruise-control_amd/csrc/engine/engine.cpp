@@ -21,7 +21,14 @@ constexpr double kBalanceMargin = 0.9;  // ResourceDistributionGoal.BALANCE_MARG
 // Speculative move-in batches: a scan launch costs about as much as evaluating ~10^4 more rows (the rows of one
 // batch are evaluated in one sweep of the resident workgroups and the launch is latency bound), so batches
 // start at a few thousand rows and grow fast while nothing is accepted.
-constexpr size_t kFirstBatchRows = 2048, kBatchGrowth = 8, kMaxBatchRows = (size_t)1 << 18;
+// CCMI_FIRST_BATCH / CCMI_BATCH_GROWTH override the first two (tuning diagnostics; results do not depend on them).
+size_t envSize(const char* name, size_t dflt) {
+  const char* v = std::getenv(name);
+  const size_t x = v ? (size_t)std::strtoull(v, nullptr, 10) : 0;
+  return x ? x : dflt;
+}
+const size_t kFirstBatchRows = envSize("CCMI_FIRST_BATCH", 2048), kBatchGrowth = envSize("CCMI_BATCH_GROWTH", 8);
+constexpr size_t kMaxBatchRows = (size_t)1 << 18;
 
 // Host view of the model for predicates.h (same expressions the kernels evaluate).
 struct HostView {
