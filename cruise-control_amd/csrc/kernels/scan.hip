@@ -400,6 +400,8 @@ struct PreView {
 };
 
 constexpr int kBlock = 256;
+constexpr uint32_t kXcds = 8;                // MI355X: 8 XCDs, each with its own L2
+constexpr uint32_t kXcdSliceMinCols = 2048;  // narrower scans keep the plain k-major tiling
 
 // Diagnostics: workgroup 0 / thread 0 records s_memrealtime (100 MHz) at fixed points of a launch.
 #define CCMI_STAMP(T, seq, i)                                                                         \
@@ -475,15 +477,29 @@ __global__ __launch_bounds__(kBlock) void scan_cross(DevTables T, MutTables Mt, 
   __shared__ OverlayLds ov;
   CCMI_STAMP(T, seq, 0);
   bool staged = false;
-  const uint32_t total = (uint32_t)K * (uint32_t)Nr;
-  for (uint32_t base = blockIdx.x * kBlock; base < total; base += gridDim.x * kBlock) {
-    const uint32_t kb = base / (uint32_t)Nr;
-    const unsigned long long keyBase = (unsigned long long)kb * N + c0 + (base - kb * (uint32_t)Nr);
+  // XCD-sliced tiling for wide scans: workgroups are dispatched round-robin over the 8 XCDs, so workgroup w
+  // (XCD w % 8) sweeps only destination columns [s*W, s*W + Ws) of slice s = w % 8, k-major within the slice.
+  // Each XCD's L2 then holds 1/8 of the destination broker records instead of all of them. Keys stay global
+  // and increase along every workgroup's tile sequence, so the early exits below remain exact.
+  const bool sliced = Nr >= kXcdSliceMinCols && (gridDim.x % kXcds) == 0;
+  uint32_t colStart = 0, Ws = (uint32_t)Nr, wg = blockIdx.x, wgs = gridDim.x;
+  if (sliced) {
+    const uint32_t W = ((uint32_t)Nr + kXcds - 1) / kXcds;
+    const uint32_t sl = blockIdx.x % kXcds;
+    colStart = sl * W;
+    Ws = colStart < (uint32_t)Nr ? min(W, (uint32_t)Nr - colStart) : 0u;
+    wg = blockIdx.x / kXcds;
+    wgs = gridDim.x / kXcds;
+  }
+  const uint32_t total = (uint32_t)K * Ws;
+  for (uint32_t base = wg * kBlock; base < total; base += wgs * kBlock) {
+    const uint32_t kb = base / Ws;
+    const unsigned long long keyBase = (unsigned long long)kb * N + c0 + colStart + (base - kb * Ws);
     if (blockBest(result) <= keyBase) break;  // an earlier pair already won: nothing later can (block-uniform)
     // the request's indices (host-mapped) are read before the overlay is staged: both round trips overlap
     const uint32_t q = base + threadIdx.x;
-    const uint32_t k = q / (uint32_t)Nr;
-    const uint32_t j = q - k * (uint32_t)Nr;
+    const uint32_t k = q / Ws;
+    const uint32_t j = colStart + (q - k * Ws);
     int rq = 0, dq = 0;
     if (q < total) {
       rq = reps[k];
@@ -674,7 +690,9 @@ hipError_t launchScanCross(const DevTables& T, const MutTables& M, const UpdateL
                            const int32_t* reps, const int32_t* cands, int K, int Nr, int N, int c0,
                            unsigned long long* result, unsigned int* done, unsigned long long* mail,
                            unsigned long long seq, hipStream_t st) {
-  const unsigned blocks = gridFor((uint64_t)K * (uint64_t)Nr, (uint64_t)kBlock, residentBlocks());
+  unsigned blocks = gridFor((uint64_t)K * (uint64_t)Nr, (uint64_t)kBlock, residentBlocks());
+  // wide scans: one slice of destination columns per XCD (the kernel slices when the grid is a multiple of 8)
+  if ((uint32_t)Nr >= kXcdSliceMinCols) blocks = (blocks + kXcds - 1) / kXcds * kXcds;
   hipLaunchKernelGGL(scan_cross, dim3(blocks), dim3(kBlock), 0, st, T, M, U, prog, reps, cands, K, Nr, N, c0, result,
                      done, mail, seq);
   return hipGetLastError();
