@@ -77,7 +77,7 @@ class ClusterDesc(C.Structure):
                 ("partition_replicas", C.POINTER(C.c_int32)), ("num_replicas", C.c_int32),
                 ("replica_partition", C.POINTER(C.c_int32)), ("replica_broker", C.POINTER(C.c_int32)),
                 ("replica_is_leader", C.POINTER(C.c_uint8)), ("replica_offline", C.POINTER(C.c_uint8)),
-                ("replica_load", C.POINTER(C.c_float))]
+                ("replica_load", C.POINTER(C.c_float)), ("replica_load_order", C.POINTER(C.c_int32))]
 
 
 class ConstraintStruct(C.Structure):
@@ -280,7 +280,11 @@ class OptimizationOptions:
     is_triggered_by_goal_violation: bool = False
     requested_destination_broker_ids: Sequence[int] = ()
     only_move_immigrant_replicas: bool = False
-    fast_mode: bool = True
+    # The reference defaults fastMode to true (OptimizationOptions 6-arg ctor), which caps every per-broker loop by a
+    # wall-clock timeout (fast.mode.per.broker.move.timeout.ms) and makes the result depend on host speed. The
+    # engine never cuts a loop short — the result fast mode reaches when no timeout fires — so the binding defaults
+    # to False to say so explicitly; fast_mode=True is accepted and behaves identically.
+    fast_mode: bool = False
 
     def to_struct(self):
         keep = []
@@ -420,6 +424,131 @@ class RandomCluster:
         h = C.c_void_p()
         lib.check(lib.lib.ccmi_random_cluster(C.byref(RandomCluster.props(**overrides)), C.byref(h)))
         return ClusterBuffers(lib, h.value)
+
+
+METRIC_OF_RESOURCE = {"CPU": 0, "NW_IN": 2, "NW_OUT": 3, "DISK": 1}  # first metric id of each resource group
+BROKER_STATES = {"ALIVE": 0, "DEAD": 1, "NEW": 2, "DEMOTED": 3, "BAD_DISKS": 4}
+
+
+class ClusterModelBuilder:
+    """Builds the flattened model (ccmi_cluster_desc) with the reference's ClusterModel construction API
+    (model/ClusterModel.java: createRack :948, createBroker :923, createReplica :800-880, setReplicaLoad :738-760,
+    setBrokerState :297-336) — the calls LoadMonitor.clusterModel and the test fixtures make. Construction order is
+    kept: replicas are indexed in createReplica order, every Partition._replicas list is built by list insertion at
+    the given index (Partition.addLeader/addFollower), and setReplicaLoad order becomes replica_load_order.
+
+    Loads follow KafkaCruiseControlUnitTestUtils.getAggregatedMetricValues: the whole resource value goes to the
+    first metric id of the resource group (KafkaCruiseControlUnitTestUtils.java:90-145). Broker ids must be 0..B-1.
+    An optional rack-id mapper (AnalyzerConfig rack.aware.goal.rack.id.mapper.class) is applied here: racks that map
+    to the same id become one rack index."""
+
+    def __init__(self, num_windows: int = 1, rack_id_mapper=None):
+        self.W = num_windows
+        self.mapper = rack_id_mapper or (lambda r: r)
+        self.rack_index: Dict[str, int] = {}
+        self.brokers: Dict[int, tuple] = {}   # id -> (rack index, capacity[4])
+        self.state: Dict[int, int] = {}
+        self.topics: List[str] = []
+        self.topic_index: Dict[str, int] = {}
+        self.parts: Dict[tuple, int] = {}     # (topic, partition) -> partition index
+        self.part_list: List[List[int]] = []  # Partition._replicas (replica indices)
+        self.rep_part: List[int] = []
+        self.rep_broker: List[int] = []
+        self.rep_leader: List[int] = []
+        self.rep_offline: List[int] = []
+        self.rep_load: List[Optional[List[float]]] = []
+        self.load_order: List[int] = []
+
+    def create_rack(self, rack_id: str) -> None:
+        self.rack_index.setdefault(str(self.mapper(str(rack_id))), len(self.rack_index))
+
+    def create_broker(self, rack_id: str, broker_id: int, capacity: Dict[str, float]) -> None:
+        self.create_rack(rack_id)
+        self.brokers[broker_id] = (self.rack_index[str(self.mapper(str(rack_id)))],
+                                   [float(capacity[r]) for r in RESOURCES])
+
+    def _replica(self, broker_id: int, topic: str, partition: int) -> int:
+        for r in self.part_list[self.parts[(topic, partition)]]:
+            if self.rep_broker[r] == broker_id:
+                return r
+        raise IllegalArgumentException(f"no replica of {topic}-{partition} on broker {broker_id}")
+
+    def create_replica(self, rack_id: str, broker_id: int, topic: str, partition: int, index: int, is_leader: bool,
+                       is_offline: bool = False) -> int:
+        if topic not in self.topic_index:
+            self.topic_index[topic] = len(self.topics)
+            self.topics.append(topic)
+        key = (topic, partition)
+        if key not in self.parts:
+            self.parts[key] = len(self.part_list)
+            self.part_list.append([])
+        r = len(self.rep_part)
+        self.rep_part.append(self.parts[key])
+        self.rep_broker.append(broker_id)
+        self.rep_leader.append(1 if is_leader else 0)
+        self.rep_offline.append(1 if is_offline else 0)
+        self.rep_load.append(None)
+        self.part_list[self.parts[key]].insert(index, r)
+        return r
+
+    def set_replica_load(self, rack_id: str, broker_id: int, topic: str, partition: int, cpu: float, nw_in: float,
+                         nw_out: float, disk: float) -> None:
+        r = self._replica(broker_id, topic, partition)
+        if self.rep_load[r] is not None:
+            raise IllegalStateException(f"The load for {topic}-{partition} on broker {broker_id} already has metric values.")
+        load = [0.0] * 6
+        for res, v in (("CPU", cpu), ("NW_IN", nw_in), ("NW_OUT", nw_out), ("DISK", disk)):
+            load[METRIC_OF_RESOURCE[res]] = float(v)
+        self.rep_load[r] = load
+        self.load_order.append(r)
+
+    def set_broker_state(self, broker_id: int, state: str) -> None:
+        self.state[broker_id] = BROKER_STATES[state]
+
+    def build(self) -> "FlatCluster":
+        return FlatCluster(self)
+
+
+class FlatCluster:
+    """Owner of the arrays behind a ClusterModelBuilder's desc (keep it alive while sessions use the desc)."""
+
+    def __init__(self, bld: ClusterModelBuilder):
+        B = len(bld.brokers)
+        if sorted(bld.brokers) != list(range(B)):
+            raise IllegalArgumentException("broker ids must be 0..B-1")
+        R, P, T, W = len(bld.rep_part), len(bld.part_list), len(bld.topics), bld.W
+        if any(x is None for x in bld.rep_load):
+            raise IllegalStateException("a replica has no load")
+        arr = lambda ct, xs: (ct * max(1, len(xs)))(*xs)  # noqa: E731
+        self.keep = dict(
+            broker_id=arr(C.c_int32, list(range(B))),
+            broker_rack=arr(C.c_int32, [bld.brokers[b][0] for b in range(B)]),
+            broker_state=arr(C.c_int32, [bld.state.get(b, 0) for b in range(B)]),
+            broker_capacity=arr(C.c_double, [c for b in range(B) for c in bld.brokers[b][1]]),
+            topic_names=arr(C.c_char_p, [t.encode() for t in bld.topics]),
+            partition_topic=arr(C.c_int32, [0] * P), partition_number=arr(C.c_int32, [0] * P),
+            partition_offset=arr(C.c_int32, [0] * (P + 1)),
+            partition_replicas=arr(C.c_int32, [r for lst in bld.part_list for r in lst]),
+            replica_partition=arr(C.c_int32, bld.rep_part), replica_broker=arr(C.c_int32, bld.rep_broker),
+            replica_is_leader=arr(C.c_uint8, bld.rep_leader), replica_offline=arr(C.c_uint8, bld.rep_offline),
+            replica_load=arr(C.c_float, [x for r in range(R) for x in bld.rep_load[r] for _ in range(W)]),
+            replica_load_order=arr(C.c_int32, bld.load_order))
+        for (topic, num), p in bld.parts.items():
+            self.keep["partition_topic"][p] = bld.topic_index[topic]
+            self.keep["partition_number"][p] = num
+        off = 0
+        for p, lst in enumerate(bld.part_list):
+            self.keep["partition_offset"][p] = off
+            off += len(lst)
+        self.keep["partition_offset"][P] = off
+        d = ClusterDesc()
+        d.num_windows, d.num_racks, d.num_brokers = W, len(bld.rack_index), B
+        d.num_topics, d.num_partitions, d.num_replicas = T, P, R
+        for k, v in self.keep.items():
+            setattr(d, k, C.cast(v, type(getattr(d, k))) if k != "topic_names" else v)
+        self.desc = d
+        self.topics = list(bld.topics)
+        self.partitions = {p: key for key, p in bld.parts.items()}
 
 
 class ClusterModel:

@@ -9,6 +9,8 @@
 #include <cstring>
 #include <stdexcept>
 
+#include <sched.h>
+
 namespace ccmi {
 
 #define ST ((hipStream_t)st_)
@@ -42,6 +44,21 @@ static void dalloc(T** p, size_t n) {
 }
 
 static size_t align16(size_t x) { return (x + 15) & ~(size_t)15; }
+
+// HIP's current device is per host thread and starts at 0; a session may run on a thread other than the one that
+// created it (the reference's precompute pool, bench.py --requests-per-gpu). Every public entry point that touches
+// the device makes the session's ordinal current for its duration and restores the caller's device afterwards.
+struct DeviceGuard {
+  int prev = -1;
+  explicit DeviceGuard(int ordinal) {
+    hipCheck(hipGetDevice(&prev), "hipGetDevice");
+    if (prev != ordinal) hipCheck(hipSetDevice(ordinal), "hipSetDevice");
+    else prev = -1;
+  }
+  ~DeviceGuard() {
+    if (prev >= 0) (void)hipSetDevice(prev);
+  }
+};
 
 Device::Device(int ordinal, int B, int R, int P, int T, int maxGoalSlots)
     : ordinal_(ordinal), B_(B), R_(R), P_(P), T_(T), ldB_((B + 3) & ~3), G_(maxGoalSlots) {
@@ -163,7 +180,7 @@ DevTables Device::tables() const {
 // uploads the whole records (the caller uploads static columns first).
 void Device::uploadStatic(const double* bCapRM, const int32_t* rPart, const int32_t* rOrig, const int32_t* pOff,
                           const int32_t* topicNrep, const int32_t* bRack, const int32_t* pTopic) {
-  hipCheck(hipSetDevice(ordinal_), "hipSetDevice");
+  DeviceGuard dg(ordinal_);
   for (int b = 0; b < B_; ++b) {
     BrokerRec& x = hBrokers_[b];
     for (int k = 0; k < 4; ++k) x.cap[k] = bCapRM[(size_t)k * B_ + b];
@@ -184,7 +201,7 @@ void Device::uploadDynamic(const double* bUtilRM, const int32_t* bNrep, const in
                            const double* bLeadNwIn, const uint8_t* bAlive, const double* rUtilRM,
                            const int32_t* rBroker, const uint8_t* rFlags, const int32_t* pBrokers,
                            const double* pLeadNwOut, const int32_t* topicCountDense) {
-  hipCheck(hipSetDevice(ordinal_), "hipSetDevice");
+  DeviceGuard dg(ordinal_);
   for (int b = 0; b < B_; ++b) {
     BrokerRec& x = hBrokers_[b];
     for (int k = 0; k < 4; ++k) x.util[k] = bUtilRM[(size_t)k * B_ + b];
@@ -224,6 +241,7 @@ void Device::uploadDynamic(const double* bUtilRM, const int32_t* bNrep, const in
 }
 
 void Device::setAllowed(int slot, const uint8_t* allowedB) {
+  DeviceGuard dg(ordinal_);
   if (slot < 0 || slot >= G_) throw std::runtime_error("goal slot out of range");
   for (int b = 0; b < B_; ++b)
     allowedHost_[b] = (allowedHost_[b] & ~(1u << slot)) | (allowedB[b] ? (1u << slot) : 0u);
@@ -235,6 +253,7 @@ void Device::setAllowed(int slot, const uint8_t* allowedB) {
 }
 
 void Device::setExclusions(const uint8_t* exclLead, const uint8_t* exclMove) {
+  DeviceGuard dg(ordinal_);
   const uint32_t mask = (1u << kExclLeadBit) | (1u << kExclMoveBit);
   for (int b = 0; b < B_; ++b)
     allowedHost_[b] = (allowedHost_[b] & ~mask) | (exclLead[b] ? (1u << kExclLeadBit) : 0u) |
@@ -246,6 +265,7 @@ void Device::setExclusions(const uint8_t* exclLead, const uint8_t* exclMove) {
 }
 
 void Device::setTopicLimits(const int32_t* upper, const int32_t* lower) {
+  DeviceGuard dg(ordinal_);
   hipCheck(hipMemcpyAsync(tUpper_, upper, sizeof(int32_t) * T_, hipMemcpyHostToDevice, ST), "upload tUpper");
   hipCheck(hipMemcpyAsync(tLower_, lower, sizeof(int32_t) * T_, hipMemcpyHostToDevice, ST), "upload tLower");
   hipCheck(hipStreamSynchronize(ST), "sync");
@@ -308,17 +328,22 @@ void Device::waitMail(unsigned long long seq) {
       }
       if (q != hipErrorNotReady) hipCheck(q, "scan");
     }
-    __builtin_ia32_pause();
+    // a scan is ~10-30 us; past ~1 ms of spinning the host core is yielded between polls so concurrent sessions
+    // (and the JVM's own threads) get it back
+    if (spins > (1u << 16)) sched_yield();
+    else __builtin_ia32_pause();
   }
   perf.syncs++;
 }
 
 // A shard with nothing to scan still applies its pending row updates so every shard's tables stay identical.
 void Device::flushPending() {
+  DeviceGuard dg(ordinal_);
   if (!brows.empty() || !rrows.empty() || !prows.empty() || !tdeltas.empty()) flushOnly();
 }
 
 void Device::flushOnly() {
+  DeviceGuard dg(ordinal_);
   if (brows.empty() && rrows.empty() && prows.empty() && tdeltas.empty()) return;
   const Staged g = packUpdates(0);
   launchPrepFor(g, 0, false);
@@ -341,7 +366,6 @@ int64_t Device::finishScan() {
 // A cross/pair scan is one launch when its update list fits the kernel's LDS overlay and its request is
 // small enough to read straight from host memory; otherwise `prep` applies the rows and copies the request
 // into HBM first.
-constexpr int kOverlayRows = 32;
 // Requests are read by the scan straight from the host-mapped staging area (rows that lose to an earlier winner
 // are never read, so copying the request into HBM first would only add a launch and a full PCIe read).
 constexpr size_t kDirectRequestBytes = 8 << 20;
@@ -384,6 +408,7 @@ const char* Device::stageScan(const Staged& g, size_t req, bool readsTopicCounts
 
 int64_t Device::scanCross(const DevProgram& prog, const int32_t* reps, int K, const int32_t* cands, int N, int c0,
                           int c1) {
+  DeviceGuard dg(ordinal_);
   const int Nr = c1 - c0;
   if (K <= 0 || Nr <= 0) {
     flushPending();
@@ -415,6 +440,7 @@ int64_t Device::scanCross(const DevProgram& prog, const int32_t* reps, int K, co
 
 int64_t Device::scanSwap(const DevProgram& prog, const int32_t* srcs, int S, const int32_t* cbOff, int M,
                          const int32_t* cbRep, int nCand, int64_t* visited) {
+  DeviceGuard dg(ordinal_);
   *visited = 0;
   if (S <= 0 || M <= 0 || nCand <= 0) return -1;
   const size_t rows = (size_t)S * M;
@@ -446,6 +472,7 @@ int64_t Device::scanSwap(const DevProgram& prog, const int32_t* srcs, int S, con
 }
 
 int64_t Device::scanPairs(const DevProgram& prog, const int32_t* pr, const int32_t* pb, int p0, int p1) {
+  DeviceGuard dg(ordinal_);
   const int n = p1 - p0;
   if (n <= 0) {
     flushPending();
@@ -471,6 +498,7 @@ int64_t Device::scanPairs(const DevProgram& prog, const int32_t* pr, const int32
 }
 
 void Device::stats(const StatsParams& P, const uint8_t* allowedAliveHost, StatsOut* out) {
+  DeviceGuard dg(ordinal_);
   const size_t req = align16((size_t)ldB_);
   const Staged g = packUpdates(req);
   std::memcpy(hStage_ + g.end, allowedAliveHost, (size_t)ldB_);

@@ -22,6 +22,9 @@ constexpr int kMaxGoals = 20;
 constexpr int kExclLeadBit = 31;  // allowedBits bit of a broker excluded for leadership (above every goal slot)
 constexpr int kExclMoveBit = 30;  // allowedBits bit of a broker excluded for replica moves
 constexpr int kMaxRf = 8;
+// Dirty rows of each kind a cross/pair scan stages into its LDS overlay itself (kernels/scan.hip OverlayLds); a
+// launch with more pending rows of any kind runs `prep` first (device.cpp stageScan). Shared by host and kernel.
+constexpr int kOverlayRows = 32;
 
 enum DevGoalKind : int32_t {
   DG_REPLICA_DISTRIBUTION = 0,
@@ -132,6 +135,10 @@ struct PartitionRow {
 struct TopicCountDelta {
   int32_t topic, broker, delta, pad;
 };
+// The LDS overlay of a scan workgroup (one copy of each row kind) stays well inside the 160 KB of a CU so four
+// resident scan workgroups per CU still fit.
+static_assert(kOverlayRows * (sizeof(BrokerRow) + sizeof(ReplicaRow) + sizeof(PartitionRow)) <= 16 * 1024,
+              "overlay LDS budget");
 
 // Writable views of the dynamic tables (row application inside a scan) and a staged update list.
 struct MutTables {

@@ -91,22 +91,19 @@ void Model::build(const ccmi_cluster_desc& d) {
       const int r = pSlots[i];
       if (r < 0 || r >= R || rPart[r] != p) throw std::invalid_argument("partition CSR inconsistent with replica_partition");
     }
-  // Replay createReplica + setReplicaLoad in replica index order.
-  std::vector<std::vector<int32_t>> created(P);
-  for (int r = 0; r < R; ++r) {
-    const int p = rPart[r], b = rBroker[r];
-    if (b < 0 || b >= B) throw std::invalid_argument("replica broker out of range");
-    brokerAdd(b, r);  // load still empty: only sets/counters change
-    topicNrep[pTopic[p]]++;
-    if (rLeader[r]) {
-      if (pLeader[p] >= 0) throw std::invalid_argument("partition has two leaders");
-      pLeader[p] = r;
-    } else if (pLeader[p] >= 0) {
-      ops.addAll(bPot[b], rLoad[pLeader[p]]);
+  // Replay createReplica + setReplicaLoad in replica index order (or: every createReplica, then setReplicaLoad in
+  // replica_load_order).
+  const int32_t* loadOrder = d.replica_load_order;
+  if (loadOrder) {
+    std::vector<uint8_t> seen(R, 0);
+    for (int i = 0; i < R; ++i) {
+      if (loadOrder[i] < 0 || loadOrder[i] >= R || seen[loadOrder[i]]) throw std::invalid_argument("replica_load_order is not a permutation");
+      seen[loadOrder[i]] = 1;
     }
-    created[p].push_back(r);
-    if ((int)created[p].size() > maxRf) maxRf = (int)created[p].size();
-    // setReplicaLoad
+  }
+  std::vector<std::vector<int32_t>> created(P);
+  auto setLoad = [&](int r) {  // ClusterModel.setReplicaLoad (ClusterModel.java:738-760)
+    const int p = rPart[r], b = rBroker[r];
     LoadVec amv;
     amv.mask = 0x3F;
     for (int k = 0; k < 6; ++k) {
@@ -122,7 +119,24 @@ void Model::build(const ccmi_cluster_desc& d) {
     ops.addAll(cLoad, amv);
     if (pLeader[p] >= 0 && rBroker[pLeader[p]] == b)
       for (int x : created[p]) ops.addAll(bPot[rBroker[x]], amv);
+  };
+  for (int r = 0; r < R; ++r) {  // ClusterModel.createReplica (ClusterModel.java:822-880)
+    const int p = rPart[r], b = rBroker[r];
+    if (b < 0 || b >= B) throw std::invalid_argument("replica broker out of range");
+    brokerAdd(b, r);  // load still empty: only sets/counters change
+    topicNrep[pTopic[p]]++;
+    if (rLeader[r]) {
+      if (pLeader[p] >= 0) throw std::invalid_argument("partition has two leaders");
+      pLeader[p] = r;
+    } else if (pLeader[p] >= 0) {
+      ops.addAll(bPot[b], rLoad[pLeader[p]]);
+    }
+    created[p].push_back(r);
+    if ((int)created[p].size() > maxRf) maxRf = (int)created[p].size();
+    if (!loadOrder) setLoad(r);
   }
+  if (loadOrder)
+    for (int i = 0; i < R; ++i) setLoad(loadOrder[i]);
   if (maxRf > kMaxRf) throw std::invalid_argument("replication factor above 8 is not supported");
   for (int p = 0; p < P; ++p)
     if (pLeader[p] < 0) throw std::invalid_argument("partition without leader");

@@ -70,12 +70,10 @@ struct DevView {
 // host's dirty rows from the host-mapped staging area into LDS and reads a dirty entity from there, while
 // workgroup 0 writes the rows into the HBM tables for the next launch. Only dirty rows are written and no
 // workgroup reads a dirty row from HBM during the launch, so there is no read/write race.
-constexpr int kOvB = 32, kOvR = 32, kOvP = 32;
-
-struct OverlayLds {
-  BrokerRow b[kOvB];
-  ReplicaRow r[kOvR];
-  PartitionRow p[kOvP];
+struct OverlayLds {  // kOverlayRows (devtypes.h): the host sends larger update lists through `prep`
+  BrokerRow b[kOverlayRows];
+  ReplicaRow r[kOverlayRows];
+  PartitionRow p[kOverlayRows];
   int nb, nr, np;
   __device__ __forceinline__ int broker(int x) const {
     for (int i = 0; i < nb; ++i)
@@ -401,7 +399,16 @@ struct PreView {
 
 constexpr int kBlock = 256;
 constexpr uint32_t kXcds = 8;                // MI355X: 8 XCDs, each with its own L2
-constexpr uint32_t kXcdSliceMinCols = 2048;  // narrower scans keep the plain k-major tiling
+// Scans with at least this many destination columns are XCD-sliced (narrower scans keep the plain k-major tiling).
+// CCMI_XCD_SLICE_MIN_COLS overrides it (diagnostics and the parity tests that force slicing on small clusters).
+static uint32_t xcdSliceMinCols() {
+  static const uint32_t v = [] {
+    const char* e = std::getenv("CCMI_XCD_SLICE_MIN_COLS");
+    const unsigned long x = e ? std::strtoul(e, nullptr, 10) : 0ul;
+    return x ? (uint32_t)x : 2048u;
+  }();
+  return v;
+}
 
 // Diagnostics: workgroup 0 / thread 0 records s_memrealtime (100 MHz) at fixed points of a launch.
 #define CCMI_STAMP(T, seq, i)                                                                         \
@@ -471,7 +478,7 @@ __device__ __forceinline__ void publishLast(unsigned long long* __restrict__ res
 __global__ __launch_bounds__(kBlock) void scan_cross(DevTables T, MutTables Mt, UpdateList U, DevProgram prog,
                                                      const int32_t* __restrict__ reps,
                                                      const int32_t* __restrict__ cands, int K, int Nr, int N, int c0,
-                                                     unsigned long long* __restrict__ result,
+                                                     int sliced, unsigned long long* __restrict__ result,
                                                      unsigned int* __restrict__ done,
                                                      unsigned long long* __restrict__ mail, unsigned long long seq) {
   __shared__ OverlayLds ov;
@@ -480,8 +487,8 @@ __global__ __launch_bounds__(kBlock) void scan_cross(DevTables T, MutTables Mt, 
   // XCD-sliced tiling for wide scans: workgroups are dispatched round-robin over the 8 XCDs, so workgroup w
   // (XCD w % 8) sweeps only destination columns [s*W, s*W + Ws) of slice s = w % 8, k-major within the slice.
   // Each XCD's L2 then holds 1/8 of the destination broker records instead of all of them. Keys stay global
-  // and increase along every workgroup's tile sequence, so the early exits below remain exact.
-  const bool sliced = Nr >= kXcdSliceMinCols && (gridDim.x % kXcds) == 0;
+  // and increase along every workgroup's tile sequence, so the early exits below remain exact. The launcher
+  // decides (`sliced`) and then guarantees gridDim.x % kXcds == 0.
   uint32_t colStart = 0, Ws = (uint32_t)Nr, wg = blockIdx.x, wgs = gridDim.x;
   if (sliced) {
     const uint32_t W = ((uint32_t)Nr + kXcds - 1) / kXcds;
@@ -680,6 +687,7 @@ static uint64_t residentBlocks() {  // CCMI_GRID_CAP overrides (diagnostics)
   return v;
 }
 static unsigned gridFor(uint64_t work, uint64_t perBlock, uint64_t cap = 4096) {
+  if (cap >= kXcds) cap -= cap % kXcds;  // an XCD-sliced grid rounds up to a multiple of 8 and stays under the cap
   uint64_t blocks = (work + perBlock - 1) / perBlock;
   if (blocks > cap) blocks = cap;
   if (blocks == 0) blocks = 1;
@@ -691,10 +699,11 @@ hipError_t launchScanCross(const DevTables& T, const MutTables& M, const UpdateL
                            unsigned long long* result, unsigned int* done, unsigned long long* mail,
                            unsigned long long seq, hipStream_t st) {
   unsigned blocks = gridFor((uint64_t)K * (uint64_t)Nr, (uint64_t)kBlock, residentBlocks());
-  // wide scans: one slice of destination columns per XCD (the kernel slices when the grid is a multiple of 8)
-  if ((uint32_t)Nr >= kXcdSliceMinCols) blocks = (blocks + kXcds - 1) / kXcds * kXcds;
-  hipLaunchKernelGGL(scan_cross, dim3(blocks), dim3(kBlock), 0, st, T, M, U, prog, reps, cands, K, Nr, N, c0, result,
-                     done, mail, seq);
+  // wide scans: one slice of destination columns per XCD
+  const int sliced = (uint32_t)Nr >= xcdSliceMinCols() ? 1 : 0;
+  if (sliced) blocks = (blocks + kXcds - 1) / kXcds * kXcds;
+  hipLaunchKernelGGL(scan_cross, dim3(blocks), dim3(kBlock), 0, st, T, M, U, prog, reps, cands, K, Nr, N, c0, sliced,
+                     result, done, mail, seq);
   return hipGetLastError();
 }
 

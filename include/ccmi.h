@@ -111,7 +111,8 @@ typedef enum ccmi_goal_kind {
  *   brokers are created in index order (broker_id[b] == b in ABI v1), then for r = 0..R-1 in index order
  *   replica r is created on replica_broker[r] (ClusterModel.createReplica) and its load is set
  *   (ClusterModel.setReplicaLoad) — so broker/host/cluster/potential-leadership aggregates accumulate in
- *   replica index order exactly as the Java model does; finally each partition's replica list is put in
+ *   replica index order exactly as the Java model does (or, with replica_load_order, all replicas are created
+ *   first and the loads are set in that order); finally each partition's replica list is put in
  *   partition_offset CSR order and broker states other than ALIVE are applied in broker index order
  *   (ClusterModel.setBrokerState).
  */
@@ -136,6 +137,11 @@ typedef struct ccmi_cluster_desc {
   const uint8_t* replica_is_leader;  /* [R] */
   const uint8_t* replica_offline;    /* [R] isOriginalOffline flag (replica on a broken disk) */
   const float* replica_load;         /* [R * 6 * W] float window values, ccmi_metric order, newest first */
+  /* Optional [R] permutation (NULL = interleaved). When set, every replica is created first (index order) and
+   * ClusterModel.setReplicaLoad is then called in this order — the construction order of hand-built models such as
+   * DeterministicCluster.mediumClusterModel (DeterministicCluster.java:1836-1879), where it changes the float
+   * rounding of the broker / potential-leadership aggregates. */
+  const int32_t* replica_load_order;
 } ccmi_cluster_desc;
 
 /* analyzer/BalancingConstraint.java; defaults AnalyzerConfig.java:58-464 via ccmi_default_constraint */
@@ -166,7 +172,10 @@ typedef struct ccmi_opt_options {
   const int32_t* requested_destination_broker_ids;
   int32_t num_requested_destination_broker_ids;
   int32_t only_move_immigrant_replicas;
-  int32_t fast_mode; /* accepted for API parity; the engine never applies wall-clock cut-offs */
+  int32_t fast_mode; /* accepted for API parity. The reference's fast mode (default true) cuts per-broker loops at a
+                        wall-clock timeout (AnalyzerConfig fast.mode.per.broker.move.timeout.ms, 500 ms), so its
+                        result depends on host speed; the engine never cuts a loop short, i.e. it always returns
+                        the result fast mode reaches when no timeout fires (= fast_mode 0). */
 } ccmi_opt_options;
 
 typedef struct ccmi_action {

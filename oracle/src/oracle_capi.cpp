@@ -133,6 +133,19 @@ void* oc_from_desc(const ccmi_cluster_desc* d) {
     }
     std::vector<char> created(d->num_partitions, 0);
     const int W = d->num_windows;
+    // ClusterModel.setReplicaLoad with getAggregatedMetricValues-style windows (KafkaCruiseControlUnitTestUtils)
+    auto setLoad = [&](int r) {
+      Load amv;
+      amv.mask = 0x3F;
+      for (int k = 0; k < NUM_METRICS; ++k) {
+        amv.m[k].sum = 0.0;
+        for (int w = 0; w < W; ++w) {
+          amv.m[k].v[w] = d->replica_load[((size_t)r * NUM_METRICS + k) * W + w];
+          amv.m[k].sum += (double)amv.m[k].v[w];
+        }
+      }
+      cm.setReplicaLoad(r, amv);
+    };
     for (int r = 0; r < d->num_replicas; ++r) {
       int p = d->replica_partition[r];
       if (!created[p]) {
@@ -143,17 +156,12 @@ void* oc_from_desc(const ccmi_cluster_desc* d) {
       int b = d->replica_broker[r];
       int idx = (int)cm.partitions[p].replicas.size();
       int rr = cm.createReplica(b, p, idx, d->replica_is_leader[r] != 0, d->replica_offline[r] != 0);
-      Load amv;
-      amv.mask = 0x3F;
-      for (int k = 0; k < NUM_METRICS; ++k) {
-        amv.m[k].sum = 0.0;
-        for (int w = 0; w < W; ++w) {
-          amv.m[k].v[w] = d->replica_load[((size_t)r * NUM_METRICS + k) * W + w];
-          amv.m[k].sum += (double)amv.m[k].v[w];
-        }
-      }
-      cm.setReplicaLoad(rr, amv);
+      if (rr != r) throw std::runtime_error("replica index mismatch");
+      if (!d->replica_load_order) setLoad(rr);
     }
+    // hand-built models: every createReplica first, then setReplicaLoad in the caller's order
+    if (d->replica_load_order)
+      for (int i = 0; i < d->num_replicas; ++i) setLoad(d->replica_load_order[i]);
     for (int p = 0; p < d->num_partitions; ++p) {
       auto& lst = cm.partitions[p].replicas;
       lst.assign(d->partition_replicas + d->partition_offset[p], d->partition_replicas + d->partition_offset[p + 1]);

@@ -59,16 +59,21 @@ def check_product_against_oracle(lib, props, goals, balance=None, device=0, max_
     every goal's post-optimization ClusterModelStats. A chain that fails (OptimizationFailureException for a hard
     goal) must fail in both with the same exception and message after the same action log."""
     buf = ccmi.RandomCluster.generate(lib, **props)
-    cm = ccmi.ClusterModel.from_buffers(buf, device=device)
-    oc = OracleCluster.from_desc(buf.desc)
+    return check_desc_against_oracle(lib, buf.desc, buf, goals, constraint(balance, max_replicas), options, device)
+
+
+def check_desc_against_oracle(lib, desc, keepalive, goals, bc, options=None, device=0):
+    """check_product_against_oracle on any flattened model (RandomCluster buffers or a ClusterModelBuilder's
+    FlatCluster). Returns (session, OptimizerResult or None when both raised, oracle cluster)."""
+    cm = ccmi.ClusterModel(desc, device=device, lib=lib, keepalive=keepalive)
+    oc = OracleCluster.from_desc(desc)
     perr = oerr = None
     try:
-        res = ccmi.GoalOptimizer(constraint(balance, max_replicas)).optimizations(cm, ccmi.goals_from_names(goals),
-                                                                                   options)
+        res = ccmi.GoalOptimizer(bc).optimizations(cm, ccmi.goals_from_names(goals), options)
     except ccmi.CruiseControlError as e:
         perr = e
     try:
-        ores = oc.optimize(goals, constraint(balance, max_replicas), options)
+        ores = oc.optimize(goals, bc, options)
     except Exception as e:  # noqa: BLE001 - the oracle binding raises the same exception classes
         oerr = e
     if perr is not None or oerr is not None:

@@ -1,0 +1,172 @@
+"""The reference's own hand-built clusters and invariants pin the oracle and the product.
+
+* DeterministicClusterTest decks (analyzer/DeterministicClusterTest.java:93-352) on the transcribed
+  DeterministicCluster models (tests/golden/deterministic_clusters.json, tests/golden/make_deterministic.py): the
+  reference test passes when OptimizationVerifier.executeGoalsFor returns true (NEW_BROKERS, BROKEN_BROKERS,
+  REGRESSION) or the chain fails with "Insufficient capacity for" (:355-365). Both the oracle and the product must
+  pass that test, and the product must match the oracle bit for bit.
+* RackAwareGoalTest (analyzer/RackAwareGoalTest.java:74-178): with the rack-id mapper exactly one proposal moving a
+  replica of the partition to broker 2; without it no proposal.
+* deadBroker (DeterministicCluster.java:1763-1826) with the default goals: BROKEN_BROKERS and the soft-goal rule.
+"""
+import pytest
+
+import ccmi
+from oracle_binding import OracleCluster
+from parity import check_desc_against_oracle
+from verifier import (build_model, deterministic_models, offline_replicas, verify_broken_brokers,
+                      verify_regression, verify_soft_goal_replica_movements)
+
+# DeterministicClusterTest.java:97-115 in priority order. Not yet in this build: RackAwareDistributionGoal,
+# PreferredLeaderElectionGoal (the deck runs without them).
+DECK_GOALS_ALL = ["RackAwareGoal", "RackAwareDistributionGoal", "MinTopicLeadersPerBrokerGoal", "ReplicaCapacityGoal",
+                  "DiskCapacityGoal", "NetworkInboundCapacityGoal", "NetworkOutboundCapacityGoal", "CpuCapacityGoal",
+                  "ReplicaDistributionGoal", "PotentialNwOutGoal", "DiskUsageDistributionGoal",
+                  "NetworkInboundUsageDistributionGoal", "NetworkOutboundUsageDistributionGoal",
+                  "CpuUsageDistributionGoal", "LeaderReplicaDistributionGoal", "LeaderBytesInDistributionGoal",
+                  "TopicReplicaDistributionGoal", "PreferredLeaderElectionGoal"]
+DECK_GOALS = [g for g in DECK_GOALS_ALL if g in ccmi.GOAL_KINDS]
+
+HIGH_BALANCE, MEDIUM_BALANCE, LOW_BALANCE = 1.65, 1.25, 1.05     # TestConstants.java:29-32
+HIGH_CAP, MEDIUM_CAP, LOW_CAP = 0.9, 0.8, 0.7                     # TestConstants.java:33-35
+
+
+def deck_constraint(balance, capacity):
+    """getDefaultCruiseControlProperties (DeterministicClusterTest.java:335-342): max.replicas.per.broker 6."""
+    bc = ccmi.BalancingConstraint()
+    bc.max_replicas_per_broker = 6
+    bc.set_resource_balance_percentage(balance)
+    bc.set_capacity_threshold(capacity)
+    return bc
+
+
+def decks():
+    out = []
+    # TEST DECK #3 / #4: capacity thresholds on the small and medium clusters (:152-170)
+    for model in ("smallClusterModel", "mediumClusterModel"):
+        for cap in (HIGH_CAP, MEDIUM_CAP, LOW_CAP):
+            out.append((f"deck34-{model}-cap{cap}", model, DECK_GOALS, deck_constraint(MEDIUM_BALANCE, cap)))
+    # TEST DECK #5: broker capacities; the constraint is the last one of deck #4 (:172-197)
+    for size in ("LARGE", "MEDIUM", "SMALL"):
+        for model in ("smallClusterModel", "mediumClusterModel"):
+            out.append((f"deck5-{model}-{size}", f"{model}_{size}", DECK_GOALS, deck_constraint(MEDIUM_BALANCE, LOW_CAP)))
+    # balance-percentage sweeps of decks #1 / #2 without the min-topic-leader topics (MinTopicLeadersPerBrokerGoal is
+    # then a no-op) (:120-150)
+    for model in ("smallClusterModel", "mediumClusterModel"):
+        for bal in (HIGH_BALANCE, MEDIUM_BALANCE, LOW_BALANCE):
+            out.append((f"deck12-{model}-bal{bal}", model, DECK_GOALS, deck_constraint(bal, MEDIUM_CAP)))
+    # the remaining DeterministicCluster models with the whole deck list
+    for model in ("unbalanced", "unbalanced2", "unbalancedWithAFollower", "rackAwareSatisfiable",
+                  "rackAwareSatisfiable2", "deadBroker"):
+        out.append((f"model-{model}", model, DECK_GOALS, deck_constraint(MEDIUM_BALANCE, MEDIUM_CAP)))
+    # three replicas of one partition on two racks: RackAwareGoal must fail (RackAwareGoal.java:112-121)
+    out.append(("model-rackAwareUnsatisfiable", "rackAwareUnsatisfiable", DECK_GOALS,
+                deck_constraint(MEDIUM_BALANCE, MEDIUM_CAP), "Insufficient number of racks"))
+    out.append(("deadBroker-default-goals", "deadBroker", list(ccmi.DEFAULT_GOALS), ccmi.BalancingConstraint()))
+    out.append(("deadBroker-soft-goals", "deadBroker", list(ccmi.C1_GOALS), ccmi.BalancingConstraint()))
+    return out
+
+
+DECKS = [d if len(d) == 5 else d + ("Insufficient capacity for",) for d in decks()]
+DECK_IDS = [d[0] for d in DECKS]
+
+
+def run_verified(runner, model_name, goals, bc, allowed_failure="Insufficient capacity for"):
+    """executeGoalsFor + the DeterministicClusterTest.test() acceptance rule (an OptimizationFailureException is a
+    pass only with the allowed message), on `runner` (oracle or product)."""
+    m = deterministic_models()[model_name]
+    flat = build_model(m)
+    pre, res, err = runner(flat, goals, bc)
+    if err is not None:
+        assert isinstance(err, ccmi.OptimizationFailureException) and allowed_failure in str(err), err
+        return flat, None
+    final, proposals, goal_results = res
+    problems = [verify_broken_brokers(m["dead"], final),
+                verify_soft_goal_replica_movements(proposals, offline_replicas(flat, m), goals)]
+    if not m["dead"]:  # REGRESSION applies when no replica is self-healing eligible
+        problems.append(verify_regression(goal_results, pre, bc))
+    problems = [p for p in problems if p]
+    assert not problems, problems
+    return flat, res
+
+
+def oracle_runner(flat, goals, bc):
+    oc = OracleCluster.from_desc(flat.desc)
+    pre = oc.stats(bc)
+    try:
+        res = oc.optimize(goals, bc)
+    except ccmi.CruiseControlError as e:
+        return pre, None, e
+    return pre, (oc.replica_distribution(), oc.proposals(), res), None
+
+
+def product_runner(lib):
+    def run(flat, goals, bc):
+        cm = ccmi.ClusterModel(flat.desc, device=0, lib=lib, keepalive=flat)
+        pre = cm.cluster_stats(bc)
+        try:
+            res = ccmi.GoalOptimizer(bc).optimizations(cm, ccmi.goals_from_names(goals))
+        except ccmi.CruiseControlError as e:
+            return pre, None, e
+        return pre, (cm.replica_distribution(), res.proposals, res.goal_results), None
+    return run
+
+
+@pytest.mark.parametrize("deck", DECKS, ids=DECK_IDS)
+def test_oracle_passes_deterministic_deck(oracle_lib, deck):
+    _, model, goals, bc, allowed = deck
+    run_verified(oracle_runner, model, goals, bc, allowed)
+
+
+def _rack_mapper_proposals(runner_lib, mapped):
+    m = deterministic_models()["rackIdMapper" if mapped else "withoutRackIdMapper"]
+    flat = build_model(m)
+    if runner_lib is None:
+        oc = OracleCluster.from_desc(flat.desc)
+        oc.optimize(["RackAwareGoal"], ccmi.BalancingConstraint())
+        return oc.proposals()
+    cm = ccmi.ClusterModel(flat.desc, device=0, lib=runner_lib, keepalive=flat)
+    return ccmi.GoalOptimizer().optimizations(cm, [ccmi.RackAwareGoal()]).proposals
+
+
+def check_rack_mapper_kat(runner_lib):
+    """RackAwareGoalTest.testRackIdMapper (:74-130) / testWithoutRackIdMapper (:137-178)."""
+    assert _rack_mapper_proposals(runner_lib, False) == []
+    props = _rack_mapper_proposals(runner_lib, True)
+    assert len(props) == 1
+    p = props[0]
+    assert p.partition == 0
+    assert set(p.old_replicas) - set(p.new_replicas) & {0, 1}
+    assert set(p.new_replicas) - set(p.old_replicas) == {2}
+
+
+def test_oracle_rack_id_mapper_kat(oracle_lib):
+    check_rack_mapper_kat(None)
+
+
+@pytest.mark.parametrize("deck", DECKS, ids=DECK_IDS)
+def test_emu_deterministic_deck_matches_oracle(emu_lib, oracle_lib, deck):
+    """The engine's host logic (test-only sequential Device emulation): the same deck passes and matches the oracle
+    bit for bit."""
+    _, model, goals, bc, allowed = deck
+    run_verified(product_runner(emu_lib), model, goals, bc, allowed)
+    flat = build_model(deterministic_models()[model])
+    check_desc_against_oracle(emu_lib, flat.desc, flat, goals, bc)
+
+
+def test_emu_rack_id_mapper_kat(emu_lib):
+    check_rack_mapper_kat(emu_lib)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("deck", DECKS, ids=DECK_IDS)
+def test_gpu_deterministic_deck_matches_oracle(gpu_lib, oracle_lib, deck):
+    _, model, goals, bc, allowed = deck
+    run_verified(product_runner(gpu_lib), model, goals, bc, allowed)
+    flat = build_model(deterministic_models()[model])
+    check_desc_against_oracle(gpu_lib, flat.desc, flat, goals, bc)
+
+
+@pytest.mark.gpu
+def test_gpu_rack_id_mapper_kat(gpu_lib):
+    check_rack_mapper_kat(gpu_lib)

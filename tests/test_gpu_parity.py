@@ -155,3 +155,30 @@ def test_gpu_broker_exclusions_match_oracle(gpu_lib, oracle_lib, props, opts, go
     """Leader-replica exclusion and swap-row exclusion run as device checks (allowedBits bits 30/31)."""
     check_product_against_oracle(gpu_lib, props, goals, 1.05, max_replicas=3000,
                                  options=ccmi.OptimizationOptions(fast_mode=False, **opts))
+
+
+@pytest.mark.parametrize("world", [1, 2])
+def test_gpu_xcd_sliced_scans_match_oracle(gpu_lib, oracle_lib, tmp_path, monkeypatch, world):
+    """The XCD-sliced scan_cross tiling (normally only for scans with >= 2048 destination columns) forced on for every
+    scan of a 301-broker cluster: uneven last slices (N not a multiple of 8), a grid cap that is not a multiple of 8,
+    and (world 2) the global keys of a destination-sharded session. Fresh processes read the overrides."""
+    import json
+
+    import torch.multiprocessing as mp
+
+    import shard_worker
+    from test_shard import _free_port
+
+    monkeypatch.setenv("CCMI_XCD_SLICE_MIN_COLS", "7")
+    monkeypatch.setenv("CCMI_GRID_CAP", "13")
+    props = dict(num_racks=7, num_brokers=301, num_replicas=30000, num_topics=900)
+    mp.start_processes(shard_worker.run, args=(world, _free_port(), props, DEFAULT_GOALS, 1.05, str(tmp_path),
+                                               gpu_lib.path), nprocs=world, join=True, start_method="spawn")
+    buf = ccmi.RandomCluster.generate(gpu_lib, **props)
+    oc = OracleCluster.from_desc(buf.desc)
+    ores = oc.optimize(DEFAULT_GOALS, constraint(1.05))
+    for r in range(world):
+        o = json.load(open(tmp_path / f"rank{r}.json"))
+        assert o["error"] is None
+        assert [tuple(a) for a in o["actions"]] == oc.actions()
+        assert [tuple(g) for g in o["goals"]] == [(x.name, x.succeeded, x.candidates, x.actions) for x in ores]
