@@ -227,6 +227,8 @@ ccmi_status ccmi_session_create(int32_t device_ordinal, const ccmi_cluster_desc*
     s->device->uploadDynamic(utilRM.data(), nrep.data(), m.bNlead.data(), pot.data(), lbi.data(), alive.data(),
                              rutilRM.data(), m.rBroker.data(), flags.data(), pBrokers.data(), plno.data(),
                              m.topicCountDense.data());
+    s->device->uploadLoads(m.W, m.rLoad.data(), m.bLoad.data(), m.bLnw.data(), m.bPot.data(), m.pSlots.data(),
+                           m.pLeader.data());
     m.dev = s->device.get();
     s->engine = std::make_unique<ccmi::Engine>(m, s->device.get());
     s->initDist = replicaDist(m);

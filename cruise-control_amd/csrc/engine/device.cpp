@@ -30,6 +30,13 @@ hipError_t launchScanPairs(const DevTables& T, const MutTables& M, const UpdateL
                            unsigned int* done, unsigned long long* mail, unsigned long long seq, hipStream_t st);
 hipError_t launchPrep(const MutTables& M, const UpdateList& U, const int4* req, int4* dReq, int nReq4,
                       unsigned long long* result, unsigned int* done, hipStream_t st);
+hipError_t launchChainPairs(const DevTables& T, const ChainTables& C, const DevProgram& prog, const int32_t* pr,
+                            const int32_t* pb, const int32_t* next, int n, int maxAccepts, int32_t* log,
+                            ChainResultDev* out, hipStream_t st);
+hipError_t launchChainRackRows(const DevTables& T, const ChainTables& C, const DevProgram& prog, const int32_t* rows,
+                               int n, const int32_t* cands, int N, int32_t* log, ChainResultDev* out, hipStream_t st);
+hipError_t launchSyncLoads(const ChainTables& C, const LoadRow* lrows, int nl, const SlotRow* srows, int ns,
+                           hipStream_t st);
 hipError_t launchStats(const StatsParams& P, const int32_t* tc, const int32_t* topicNrep, const BrokerRec* brokers,
                        const uint8_t* allowedAlive, TopicPartial* scratch, StatsOut* out, int ldB, hipStream_t st,
                        hipEvent_t evTopic0, hipEvent_t evTopic1);
@@ -124,7 +131,8 @@ Device::~Device() {
     (void)hipFree(stamps_);
   }
   void* ps[] = {brokers_, replicas_, parts_, allowedAlive_, topicCount_, topicNrep_, topicScratch_, statsOut_, dReq_,
-                rowVisited_, dResult_, dDone_, tUpper_, tLower_};
+                rowVisited_, dResult_, dDone_, tUpper_, tLower_, dRLoad_, dBLoad_, dBLnw_, dBPot_, dPOff_, dPSlots_,
+                dPLeader_, dChainLog_, dChainOut_};
   for (void* p : ps)
     if (p) (void)hipFree(p);
   if (hStage_) (void)hipHostFree(hStage_);
@@ -518,6 +526,167 @@ void Device::stats(const StatsParams& P, const uint8_t* allowedAliveHost, StatsO
     perf.statsKernelMs += ms;
   }
   std::memcpy((void*)out, statsHost_, sizeof(StatsOut));
+}
+
+}  // namespace ccmi
+
+namespace ccmi {
+
+// ------------------------------------------------------------------------------------------------ chains
+void Device::uploadLoads(int W, const LoadVec* rLoad, const LoadVec* bLoad, const LoadVec* bLnw, const LoadVec* bPot,
+                         const int32_t* pSlots, const int32_t* pLeader) {
+  DeviceGuard dg(ordinal_);
+  W_ = W;
+  dalloc(&dRLoad_, (size_t)R_);
+  dalloc(&dBLoad_, (size_t)B_);
+  dalloc(&dBLnw_, (size_t)B_);
+  dalloc(&dBPot_, (size_t)B_);
+  dalloc(&dPOff_, (size_t)P_ + 1);
+  dalloc(&dPSlots_, (size_t)R_);
+  dalloc(&dPLeader_, (size_t)P_);
+  dalloc(&dChainOut_, 1);
+  hipCheck(hipMemcpy(dRLoad_, rLoad, sizeof(LoadVec) * R_, hipMemcpyHostToDevice), "upload replica loads");
+  hipCheck(hipMemcpy(dBLoad_, bLoad, sizeof(LoadVec) * B_, hipMemcpyHostToDevice), "upload broker loads");
+  hipCheck(hipMemcpy(dBLnw_, bLnw, sizeof(LoadVec) * B_, hipMemcpyHostToDevice), "upload leadership loads");
+  hipCheck(hipMemcpy(dBPot_, bPot, sizeof(LoadVec) * B_, hipMemcpyHostToDevice), "upload potential loads");
+  hipCheck(hipMemcpy(dPOff_, hPOff_.data(), sizeof(int32_t) * (P_ + 1), hipMemcpyHostToDevice), "upload pOff");
+  hipCheck(hipMemcpy(dPSlots_, pSlots, sizeof(int32_t) * R_, hipMemcpyHostToDevice), "upload pSlots");
+  hipCheck(hipMemcpy(dPLeader_, pLeader, sizeof(int32_t) * P_, hipMemcpyHostToDevice), "upload pLeader");
+}
+
+ChainTables Device::chainTables() const {
+  ChainTables c;
+  c.brokers = brokers_;
+  c.replicas = replicas_;
+  c.parts = parts_;
+  c.topicCount = topicCount_;
+  c.ldB = ldB_;
+  c.W = W_;
+  c.rLoad = dRLoad_;
+  c.bLoad = dBLoad_;
+  c.bLnw = dBLnw_;
+  c.bPot = dBPot_;
+  c.pOff = dPOff_;
+  c.pSlots = dPSlots_;
+  c.pLeader = dPLeader_;
+  return c;
+}
+
+// [row updates | load rows | slot rows | request]; launches sync_loads and prep (rows applied, request copied into
+// HBM at dReq_). `fill` writes the request into the staging area.
+template <class F>
+size_t Device::stageChainCopy(size_t reqBytes, Staged& g, size_t& oReq, F fill) {
+  if (!dRLoad_) throw std::runtime_error("device chain state not uploaded");
+  const size_t nl = lrows.size(), ns = srows.size();
+  const size_t oL = 0, oS = align16(nl * sizeof(LoadRow)), oR = oS + align16(ns * sizeof(SlotRow));
+  g = packUpdates(oR + reqBytes);
+  std::memcpy(hStage_ + g.end + oL, lrows.data(), nl * sizeof(LoadRow));
+  std::memcpy(hStage_ + g.end + oS, srows.data(), ns * sizeof(SlotRow));
+  fill(hStage_ + g.end + oR);
+  hipCheck(launchSyncLoads(chainTables(), (const LoadRow*)(hStageDev_ + g.end + oL), (int)nl,
+                           (const SlotRow*)(hStageDev_ + g.end + oS), (int)ns, ST),
+           "sync_loads");
+  lrows.clear();
+  srows.clear();
+  // prep copies [g.end + oR, + reqBytes) into dReq_ when given the request at that offset
+  Staged h = g;
+  h.end = g.end + oR;
+  launchPrepFor(h, reqBytes, false);
+  oReq = 0;
+  return g.end + oR;
+}
+
+Device::ChainResult Device::chainPairs(const DevProgram& prog, const int32_t* pr, const int32_t* pb,
+                                       const int32_t* next, int n, int maxAccepts, std::vector<int32_t>& log) {
+  DeviceGuard dg(ordinal_);
+  ChainResult res;
+  log.clear();
+  if (n <= 0) {
+    flushPending();
+    return res;
+  }
+  const size_t oB = align16((size_t)n * 4), oN = oB + align16((size_t)n * 4), req = oN + align16((size_t)n * 4);
+  Staged g;
+  size_t oReq = 0;
+  const size_t at = stageChainCopy(req, g, oReq, [&](char* base) {
+    std::memcpy(base, pr, (size_t)n * 4);
+    std::memcpy(base + oB, pb, (size_t)n * 4);
+    std::memcpy(base + oN, next, (size_t)n * 4);
+  });
+  (void)at;
+  if ((size_t)n > chainLogCap_) {
+    if (dChainLog_) (void)hipFree(dChainLog_);
+    chainLogCap_ = (size_t)n * 2;
+    dalloc(&dChainLog_, chainLogCap_);
+  }
+  if (timing) (void)hipEventRecord(EV0, ST);
+  hipCheck(launchChainPairs(tables(), chainTables(), prog, (const int32_t*)dReq_, (const int32_t*)(dReq_ + oB),
+                            (const int32_t*)(dReq_ + oN), n, maxAccepts, dChainLog_, dChainOut_, ST),
+           "chain_pairs");
+  if (timing) (void)hipEventRecord(EV1, ST);
+  ChainResultDev out;
+  hipCheck(hipMemcpyAsync(&out, dChainOut_, sizeof(out), hipMemcpyDeviceToHost, ST), "chain result");
+  hipCheck(hipStreamSynchronize(ST), "chain");
+  perf.syncs++;
+  perf.scanLaunches++;
+  perf.chainLaunches++;
+  perf.scanPairs += (int64_t)out.visited;
+  if (timing) {
+    float ms = 0.f;
+    hipCheck(hipEventElapsedTime(&ms, EV0, EV1), "hipEventElapsedTime");
+    perf.scanKernelMs += ms;
+  }
+  res.accepts = (int64_t)out.accepts;
+  res.visited = (int64_t)out.visited;
+  log.resize((size_t)res.accepts);
+  if (res.accepts)
+    hipCheck(hipMemcpy(log.data(), dChainLog_, sizeof(int32_t) * res.accepts, hipMemcpyDeviceToHost), "chain log");
+  return res;
+}
+
+Device::ChainResult Device::chainRackRows(const DevProgram& prog, const int32_t* rows, int n, const int32_t* cands,
+                                          int N, std::vector<int32_t>& log) {
+  DeviceGuard dg(ordinal_);
+  ChainResult res;
+  log.clear();
+  if (n <= 0) {
+    flushPending();
+    return res;
+  }
+  const size_t oC = align16((size_t)n * 4), req = oC + align16((size_t)N * 4);
+  Staged g;
+  size_t oReq = 0;
+  (void)stageChainCopy(req, g, oReq, [&](char* base) {
+    std::memcpy(base, rows, (size_t)n * 4);
+    std::memcpy(base + oC, cands, (size_t)N * 4);
+  });
+  if ((size_t)2 * n > chainLogCap_) {
+    if (dChainLog_) (void)hipFree(dChainLog_);
+    chainLogCap_ = (size_t)4 * n;
+    dalloc(&dChainLog_, chainLogCap_);
+  }
+  if (timing) (void)hipEventRecord(EV0, ST);
+  hipCheck(launchChainRackRows(tables(), chainTables(), prog, (const int32_t*)dReq_, n, (const int32_t*)(dReq_ + oC), N,
+                               dChainLog_, dChainOut_, ST),
+           "chain_rack_rows");
+  if (timing) (void)hipEventRecord(EV1, ST);
+  ChainResultDev out;
+  hipCheck(hipMemcpyAsync(&out, dChainOut_, sizeof(out), hipMemcpyDeviceToHost, ST), "chain result");
+  hipCheck(hipStreamSynchronize(ST), "chain");
+  perf.syncs++;
+  perf.scanLaunches++;
+  perf.chainLaunches++;
+  if (timing) {
+    float ms = 0.f;
+    hipCheck(hipEventElapsedTime(&ms, EV0, EV1), "hipEventElapsedTime");
+    perf.scanKernelMs += ms;
+  }
+  res.accepts = (int64_t)out.accepts;
+  res.failRow = (int64_t)out.failRow;
+  log.resize((size_t)res.accepts * 2);
+  if (res.accepts)
+    hipCheck(hipMemcpy(log.data(), dChainLog_, sizeof(int32_t) * 2 * res.accepts, hipMemcpyDeviceToHost), "chain log");
+  return res;
 }
 
 }  // namespace ccmi

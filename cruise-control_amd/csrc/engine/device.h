@@ -31,6 +31,7 @@ struct DevicePerf {
   int64_t statsBytes = 0;
   int64_t syncs = 0;
   int64_t singleLaunch = 0;  // scans that applied their rows in-kernel and read the request from host memory
+  int64_t chainLaunches = 0; // K7 chains (several decisions per launch)
 };
 
 class Device {
@@ -67,6 +68,23 @@ class Device {
                    const int32_t* cbRep, int nCand, int64_t* visited);
   int64_t scanPairs(const DevProgram& prog, const int32_t* pr, const int32_t* pb, int p0, int p1);
   void stats(const StatsParams& P, const uint8_t* allowedAliveHost, StatsOut* out);
+
+  // Chains (K7, kernels/scan.hip): decisions applied on the device inside one launch. uploadLoads gives the device
+  // the Java loads and partition slot order (once per session); lrows / srows carry the entities the host changed
+  // without the device since the last chain and are sent first.
+  void uploadLoads(int W, const LoadVec* rLoad, const LoadVec* bLoad, const LoadVec* bLnw, const LoadVec* bPot,
+                   const int32_t* pSlots, const int32_t* pLeader);
+  std::vector<LoadRow> lrows;
+  std::vector<SlotRow> srows;
+  struct ChainResult {
+    int64_t accepts = 0, visited = 0, failRow = 0;
+  };
+  // PAIRS chain; log receives the accepted pair indices in order
+  ChainResult chainPairs(const DevProgram& prog, const int32_t* pr, const int32_t* pb, const int32_t* next, int n,
+                         int maxAccepts, std::vector<int32_t>& log);
+  // RACK_ROWS chain; log receives (row, candidate index) per accepted row
+  ChainResult chainRackRows(const DevProgram& prog, const int32_t* rows, int n, const int32_t* cands, int N,
+                            std::vector<int32_t>& log);
   void flushOnly();
   void flushPending();
 
@@ -121,6 +139,16 @@ class Device {
   unsigned long long* stamps_ = nullptr;
   int32_t* rowVisited_ = nullptr;
   size_t rowVisitedCap_ = 0;
+  // chain state
+  int W_ = 1;
+  LoadVec *dRLoad_ = nullptr, *dBLoad_ = nullptr, *dBLnw_ = nullptr, *dBPot_ = nullptr;
+  int32_t *dPOff_ = nullptr, *dPSlots_ = nullptr, *dPLeader_ = nullptr;
+  int32_t* dChainLog_ = nullptr;
+  size_t chainLogCap_ = 0;
+  ChainResultDev* dChainOut_ = nullptr;
+  ChainTables chainTables() const;
+  template <class F>
+  size_t stageChainCopy(size_t reqBytes, Staged& g, size_t& oReq, F fill);
 };
 
 

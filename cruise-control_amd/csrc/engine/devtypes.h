@@ -16,6 +16,8 @@
 #pragma once
 #include <stdint.h>
 
+#include "loadops.h"
+
 namespace ccmi {
 
 constexpr int kMaxGoals = 20;
@@ -168,6 +170,40 @@ struct ScanHeader {
   int32_t K;     // CROSS: number of replicas; SWAP: number of source replicas S
   int32_t N;     // CROSS: number of candidates; SWAP: number of segments M
   int32_t nCand; // SWAP: total candidate replicas
+};
+
+// Device-resident Java loads and partition slot order, so chain kernels can apply moves themselves (apply.h).
+struct ChainTables {
+  BrokerRec* brokers;
+  ReplicaRec* replicas;
+  PartitionRec* parts;
+  int32_t* topicCount;
+  int32_t ldB;
+  int32_t W;
+  LoadVec* rLoad;    // [R]  Replica.load()
+  LoadVec* bLoad;    // [B]  Broker.load()
+  LoadVec* bLnw;     // [B]  Broker._leadershipLoadForNwResources
+  LoadVec* bPot;     // [B]  ClusterModel._potentialLeadershipLoadByBrokerId
+  const int32_t* pOff;  // [P+1]
+  int32_t* pSlots;   // [R]  replica ids in Partition._replicas order (leader first)
+  int32_t* pLeader;  // [P]
+};
+// Host-side changes to those loads since the last chain launch (moves the host applied without the device).
+enum LoadRowKind : int32_t { LR_REPLICA = 0, LR_BROKER = 1, LR_LEADERSHIP_NW = 2, LR_POTENTIAL = 3 };
+struct LoadRow {
+  int32_t kind, id;
+  LoadVec v;
+};
+struct SlotRow {
+  int32_t p, leader;
+  int32_t slots[kMaxRf];
+};
+// Chain request: PAIRS = explicit (replica, destination) pairs in reference order with a group structure (after an
+// accept the scan resumes at next[accepted]), stopping after maxAccepts; RACK_ROWS = RackAwareGoal's per-replica rows
+// over one candidate list, each row re-checked against shouldKeepInTheCurrentBroker when reached.
+enum ChainMode : int32_t { CM_PAIRS = 0, CM_RACK_ROWS = 1 };
+struct ChainResultDev {
+  unsigned long long accepts, visited, failRow;  // failRow: row + 1 of a RACK_ROWS row with no accepted candidate
 };
 
 // ClusterModelStats reduction (kernels/stats.hip)

@@ -180,7 +180,8 @@ int64_t Engine::combine(int64_t localKey) const {
   return k == INT64_MAX ? -1 : k;
 }
 
-int64_t Engine::pairScan(GoalImpl& self, const std::vector<int32_t>& pr, const std::vector<int32_t>& pb, int action) {
+int64_t Engine::pairScan(GoalImpl& self, const std::vector<int32_t>& pr, const std::vector<int32_t>& pb, int action,
+                         bool count) {
   if (pr.empty()) return -1;
   PhaseScope ps(PH_DEV_SCAN);
   m.flushToDevice();
@@ -188,6 +189,7 @@ int64_t Engine::pairScan(GoalImpl& self, const std::vector<int32_t>& pr, const s
   const int p0 = (int)((int64_t)n * shard.rank / shard.count), p1 = (int)((int64_t)n * (shard.rank + 1) / shard.count);
   const DevProgram prog = program(self, action);
   const int64_t key = combine(dev->scanPairs(prog, pr.data(), pb.data(), p0, p1));
+  if (!count) return key;
   if (prog.exclLeadMove) {
     const size_t end = key >= 0 ? (size_t)key + 1 : pr.size();
     for (size_t q = 0; q < end; ++q) candidates += (m.rLeader[pr[q]] && opt.exclLead[pb[q]]) ? 0 : 1;
@@ -207,6 +209,34 @@ int64_t Engine::swapScan(GoalImpl& self, const std::vector<int32_t>& srcs, const
                                     (int)cbOff.size() - 1, cbRep.data(), (int)cbRep.size(), &visited);
   candidates += visited;
   return key;
+}
+
+bool Engine::chainsOn() const {
+  static const bool off = std::getenv("CCMI_NO_CHAINS") != nullptr;
+  return !off && shard.count <= 1;
+}
+
+int64_t Engine::chainPairs(GoalImpl& self, int action, const std::vector<int32_t>& pr, const std::vector<int32_t>& pb,
+                           const std::vector<int32_t>& next, int maxAccepts, std::vector<int32_t>& log) {
+  PhaseScope ps(PH_DEV_SCAN);
+  m.flushToDevice();
+  m.flushChainLoads();
+  const Device::ChainResult r =
+      dev->chainPairs(program(self, action), pr.data(), pb.data(), next.data(), (int)pr.size(), maxAccepts, log);
+  candidates += r.visited;
+  return r.accepts;
+}
+
+int64_t Engine::chainRackRows(GoalImpl& self, const std::vector<int32_t>& rows, const std::vector<int32_t>& cands,
+                              std::vector<int32_t>& log) {
+  PhaseScope ps(PH_DEV_SCAN);
+  m.flushToDevice();
+  m.flushChainLoads();
+  DevProgram prog = program(self, DA_MOVE);
+  prog.filter = FILTER_RACK_AWARE;
+  const Device::ChainResult r = dev->chainRackRows(prog, rows.data(), (int)rows.size(), cands.data(),
+                                                   (int)cands.size(), log);
+  return r.failRow;
 }
 
 int Engine::acceptance(int gi, const ccmi_action& a) {
@@ -327,7 +357,8 @@ bool Engine::optimizeGoal(std::unique_ptr<GoalImpl> g, ccmi_goal_result* res) {
   for (int b = 0; b < m.B; ++b)
     if (m.alive(b) && opt.anyExclMove && opt.exclMove[b] && m.nrep(b) > 0) exclWithReplicas = true;
   while (!g->finished) {
-    for (int b : g->brokersToBalance(*this)) g->rebalance(*this, b);
+    if (!g->rebalanceAll(*this))
+      for (int b : g->brokersToBalance(*this)) g->rebalance(*this, b);
     PhaseScope ps(PH_UPDATE);
     g->update(*this);
   }
@@ -613,6 +644,7 @@ class ResourceDistribution : public GoalImpl {
   double upperThr = 0, lowerThr = 0;
   bool fix = false;
   Model::SnapTable snapTab;  // moveIn's candidate-broker snapshots (one Spec per phase)
+  std::vector<uint8_t> queued;  // moveIn: broker is in the candidate queue
   int nameBase() const { return 4 * kind; }
   int nameId(bool reverse, bool leader) const { return nameBase() + (reverse ? 1 : 0) + (leader ? 2 : 0); }
   bool excluded(int b) const { return !allowed[b]; }
@@ -942,12 +974,16 @@ class ResourceDistribution : public GoalImpl {
       else m.relocateLeadership(m.rPart[list[hitIdx]], b, dst);
       first = false;
       if (underUpper(m, b, upperSrc) && !(fix && m.bNoff[b] > 0)) {
+        prof().count(10, "out.done");
         m.clearTracked(b);
         return false;
       }
       const bool add = m.pct(dst, res) < upperThr;
+      prof().count(lead ? 6 : 7, lead ? "out.lead.accept" : "out.move.accept");
+      if (built) prof().count(8, "out.built.accept");
       if (!built) {
         if (memberBetween(dst, dstBefore, m.pct(dst, res))) {
+          prof().count(9, "out.materialise");
           materialise();
         } else {  // the removal finds dst's node: the set stays clean
           hist.push_back({dst, m.pct(dst, res), add});
@@ -982,8 +1018,12 @@ class ResourceDistribution : public GoalImpl {
       auto member = [&](int c) { return m.alive(c) && m.pct(c, res) > (excluded(c) ? 0.0 : lowerThr); };
       // only b's key changes while brokers are queued (moves go cb -> b, cb polled): exact unless b is queued
       pq.init(m.B, !member(b));
+      queued.assign(m.B, 0);
       for (auto it = ord.rbegin(); it != ord.rend(); ++it)
-        if (member(*it)) pq.push_sorted(*it);
+        if (member(*it)) {
+          pq.push_sorted(*it);
+          queued[*it] = 1;
+        }
       if (!pq.ordered())
         for (int c = 0; c < m.B; ++c)
           if (member(c)) pq.add(c);
@@ -993,6 +1033,7 @@ class ResourceDistribution : public GoalImpl {
     // b outside the eligible set (e.g. not a requested destination): every polled replica visits an empty
     // candidate list, nothing moves and nothing is counted — the loop's outcome without walking every broker
     if (cands.empty()) return true;
+    if (action == DA_LEADERSHIP && pq.ordered() && e.shard.count <= 1) return moveInLeadership(e, b, pq, spec);
     struct Seg {
       int cb;
       size_t skip;
@@ -1039,13 +1080,115 @@ class ResourceDistribution : public GoalImpl {
       const int r = (*hit.v)[idx];
       if (action == DA_MOVE) m.relocateReplica(m.rPart[r], hit.cb, b);
       else m.relocateLeadership(m.rPart[r], hit.cb, b);
-      if (aboveLower(m, b)) return false;
+      if (aboveLower(m, b)) {
+        prof().count(action == DA_MOVE ? 0 : 3, action == DA_MOVE ? "in.move.done" : "in.lead.done");
+        return false;
+      }
       for (size_t t = segs.size(); t-- > mi + 1;) pq.unpoll(segs[t].cb);  // un-poll speculative brokers
       if (!pq.empty() && m.pct(hit.cb, res) < m.pct(pq.peek(), res)) {
+        prof().count(action == DA_MOVE ? 1 : 4, action == DA_MOVE ? "in.move.readd" : "in.lead.readd");
         pq.add(hit.cb);
       } else {
+        prof().count(action == DA_MOVE ? 2 : 5, action == DA_MOVE ? "in.move.continue" : "in.lead.continue");
         cur = {hit.cb, idx, nullptr};
         haveCur = true;
+      }
+    }
+    return true;
+  }
+
+  // rebalanceByMovingLoadIn for LEADERSHIP_MOVEMENT (:437-526) with an ordered candidate queue. A row (replica r on
+  // candidate broker cb) can only be accepted when GoalUtils.legitMove holds (GoalUtils.java:213-226): r is a leader
+  // and b hosts a replica of r's partition — so the only acceptable rows are the leaders of b's own follower
+  // partitions. Each scan sends exactly those rows to the device, in the reference's row order (the current broker's
+  // remaining view first, then the queued brokers in poll order = comparator order, each in its sorted-replica
+  // order); the rows between them are walked by the reference without a possible accept, so they are counted as
+  // reference-equivalent candidates from the snapshot sizes but not evaluated.
+  template <class Q>
+  bool moveInLeadership(Engine& e, int b, Q& pq, const Model::Spec& spec) {
+    Model& m = e.m;
+    struct Row {
+      int cb;
+      size_t idx;
+      int r;
+    };
+    std::vector<Row> rows;
+    std::vector<int32_t> pr, pb;
+    int curCb = -1;
+    size_t curSkip = 0;
+    auto cond = [&]() { return m.bNlead[b] != m.nrep(b); };
+    auto size = [&](int c) { return m.snapshotIn(snapTab, c, spec).size(); };
+    auto indexOf = [&](int c, int r) {
+      const auto& v = m.snapshotIn(snapTab, c, spec);
+      const uint64_t k = m.replicaKey(spec, r);
+      return (size_t)(std::lower_bound(v.begin(), v.end(), k, [&](int x, uint64_t kk) { return m.replicaKey(spec, x) < kk; }) -
+                      v.begin());
+    };
+    while (curCb >= 0 || (!pq.empty() && cond())) {
+      {
+        PhaseScope pf(PH_FLATTEN);
+        rows.clear();
+        for (int rb : m.bRepl[b]) {
+          if (m.rLeader[rb]) continue;  // b leads that partition: no leader row elsewhere
+          const int lr = m.pLeader[m.rPart[rb]];
+          const int cb = m.rBroker[lr];
+          if (cb != curCb && !queued[cb]) continue;
+          if (!m.selects(spec, lr)) continue;
+          const size_t idx = indexOf(cb, lr);
+          if (cb == curCb && idx < curSkip) continue;
+          rows.push_back({cb, idx, lr});
+        }
+        std::sort(rows.begin(), rows.end(), [&](const Row& x, const Row& y) {
+          if (x.cb != y.cb) {
+            if (x.cb == curCb || y.cb == curCb) return x.cb == curCb;
+            return cmpBroker(m, y.cb, x.cb) < 0;  // poll order: the queue's reversed broker comparator
+          }
+          return x.idx < y.idx;
+        });
+        pr.clear();
+        pb.clear();
+        for (const Row& x : rows) {
+          pr.push_back(x.r);
+          pb.push_back(b);
+        }
+      }
+      const int64_t key = rows.empty() ? -1 : e.pairScan(*this, pr, pb, DA_LEADERSHIP, false);
+      // reference-equivalent rows visited up to the accepted row (or everything left when nothing is accepted)
+      int64_t visited = 0;
+      const Row* hit = key >= 0 ? &rows[(size_t)key] : nullptr;
+      if (curCb >= 0) {
+        if (hit && hit->cb == curCb) {
+          visited += (int64_t)(hit->idx - curSkip + 1);
+        } else {
+          const size_t n = size(curCb);
+          visited += n > curSkip ? (int64_t)(n - curSkip) : 0;
+          curCb = -1;
+        }
+      }
+      if (!(hit && hit->cb == curCb)) {
+        while (!pq.empty() && (hit || cond())) {
+          const int c = pq.poll();
+          queued[c] = 0;
+          if (hit && c == hit->cb) {
+            visited += (int64_t)hit->idx + 1;
+            break;
+          }
+          visited += (int64_t)size(c);
+        }
+      }
+      e.candidates += visited;
+      if (!hit) break;
+      const int cb = hit->cb;
+      const size_t idx = hit->idx;
+      m.relocateLeadership(m.rPart[hit->r], cb, b);
+      if (aboveLower(m, b)) return false;
+      if (!pq.empty() && m.pct(cb, res) < m.pct(pq.peek(), res)) {
+        pq.add(cb);
+        queued[cb] = 1;
+        curCb = -1;
+      } else {
+        curCb = cb;
+        curSkip = idx;
       }
     }
     return true;

@@ -62,6 +62,8 @@ class GoalImpl {
   virtual void rebalance(Engine& e, int b) = 0;
   virtual void update(Engine& e) = 0;
   virtual std::vector<int> brokersToBalance(Engine& e);
+  // One device chain for the whole broker loop of a round (returns false when the goal has none, or chains are off)
+  virtual bool rebalanceAll(Engine&) { return false; }
   virtual int compareStats(const ccmi_cluster_stats& after, const ccmi_cluster_stats& before) const = 0;
 };
 
@@ -92,12 +94,21 @@ class Engine {
   int64_t exclLeadCount(const int32_t* reps, int K, const std::vector<int32_t>& cands, int64_t key) const;
   bool exclOnDevice = false;  // the device's broker exclusion bits are set
   int64_t pairScan(GoalImpl& self, const std::vector<int32_t>& pr, const std::vector<int32_t>& pb,
-                   int action = DA_LEADERSHIP);
+                   int action = DA_LEADERSHIP, bool count = true);
   int64_t swapScan(GoalImpl& self, const std::vector<int32_t>& srcs, const std::vector<int32_t>& cbOff,
                    const std::vector<int32_t>& cbRep);
   void eligible(const std::vector<int32_t>& in, int action, std::vector<int32_t>& out) const;
 
   double threshold(double avgPct, int res, bool lower) const;  // GoalUtils.computeResourceUtilizationBalanceThreshold
+
+  // Chains (Device::chainPairs / chainRackRows, kernel K7): the device makes a sequence of the reference loop's
+  // decisions in one launch, applying each move before the next; the engine replays the logged moves into the host
+  // model (Model::replaying). Not used for destination-sharded sessions. CCMI_NO_CHAINS=1 turns them off.
+  bool chainsOn() const;
+  int64_t chainPairs(GoalImpl& self, int action, const std::vector<int32_t>& pr, const std::vector<int32_t>& pb,
+                     const std::vector<int32_t>& next, int maxAccepts, std::vector<int32_t>& log);
+  int64_t chainRackRows(GoalImpl& self, const std::vector<int32_t>& rows, const std::vector<int32_t>& cands,
+                        std::vector<int32_t>& log);
 
  private:
   DevProgram program(const GoalImpl& self, int action) const;

@@ -135,6 +135,51 @@ class RackAware : public GoalImpl {
     return c;
   }
 
+  // The whole broker loop as ONE device chain: the rows are, broker by broker (brokersToBalance order) and in each
+  // broker's sorted-replica order, the replicas that violate rack awareness or are offline when the goal starts. A
+  // replica can only stop violating during the loop (every move goes to a rack the partition does not use yet), and
+  // replicas moved onto later brokers are rack-aware there, so the device re-checks each row's
+  // shouldKeepInTheCurrentBroker when it reaches it and skips it if it now holds; everything else it decides and
+  // applies in order. The host replays the logged moves and counts the reference-equivalent candidates.
+  bool rebalanceAll(Engine& e) override {
+    if (!e.chainsOn()) return false;
+    PhaseScope ps(PH_OTHER_GOALS);
+    Model& m = e.m;
+    const std::vector<int> order = brokersToBalance(e);
+    std::vector<std::vector<int32_t>> byBroker(m.B);
+    for (int r = 0; r < m.R; ++r) {
+      const int b = m.rBroker[r];
+      if (m.alive(b) && !m.curOffline(r) && keep(m, r)) continue;
+      if (e.opt.onlyImmigrants && !m.immigrant(r)) continue;  // the tracked selection (immigrants only)
+      byBroker[b].push_back(r);
+    }
+    Model::Spec spec;
+    spec.selImmigrants = e.opt.onlyImmigrants;
+    std::vector<int32_t> rows, cands, log;
+    for (int b : order) {
+      auto& v = byBroker[b];
+      std::sort(v.begin(), v.end(), [&](int x, int y) { return m.replicaKey(spec, x) < m.replicaKey(spec, y); });
+      rows.insert(rows.end(), v.begin(), v.end());
+    }
+    e.eligible(alive, DA_MOVE, cands);
+    const int64_t failRow = e.chainRackRows(*this, rows, cands, log);
+    {
+      Model::Replay rp(m);
+      for (size_t i = 0; i + 1 < log.size(); i += 2) {
+        const int r = rows[log[i]], j = log[i + 1];
+        e.candidates += eligibleCount(e, r, cands, (size_t)j + 1);
+        m.relocateReplica(m.rPart[r], m.rBroker[r], cands[j]);
+      }
+    }
+    if (failRow > 0) {
+      const int r = rows[failRow - 1];
+      e.candidates += eligibleCount(e, r, cands, cands.size());
+      throw OptimizationFailure("[" + name + "] Cannot move replica of partition " + std::to_string(m.rPart[r]) +
+                                " to a rack-aware broker.");
+    }
+    return true;
+  }
+
   // AbstractRackAwareGoal.rebalanceForBroker (:144-170), throwExceptionIfCannotMove = true
   void rebalance(Engine& e, int b) override {
     PhaseScope ps(PH_OTHER_GOALS);
@@ -889,6 +934,19 @@ class LeaderReplicaDistribution : public GoalImpl {
         owner.push_back((int)q);
       }
     }
+    if (e.chainsOn()) {  // one device chain: after an accept the scan resumes at the next leader's pairs
+      std::vector<int32_t> next(pr.size()), log;
+      int ng = (int)pr.size();
+      for (int q = (int)pr.size() - 1; q >= 0; --q) {
+        if (q + 1 < (int)pr.size() && owner[q + 1] != owner[q]) ng = q + 1;
+        next[q] = ng;
+      }
+      const int want = nl - upperSrc;
+      const int64_t acc = e.chainPairs(*this, DA_LEADERSHIP, pr, pb, next, want, log);
+      Model::Replay rp(m);
+      for (int q : log) m.relocateLeadership(m.rPart[pr[q]], b, pb[q]);
+      return acc < want;
+    }
     size_t start = 0;
     std::vector<int32_t> spr, spb;
     while (start < pr.size()) {
@@ -920,6 +978,16 @@ class LeaderReplicaDistribution : public GoalImpl {
       if (m.rLeader[r] || m.curOffline(r)) continue;
       pr.push_back(m.pLeader[m.rPart[r]]);
       pb.push_back(b);
+    }
+    if (e.chainsOn()) {  // one device chain over the fixed pair list
+      if (pr.empty()) return true;
+      std::vector<int32_t> next(pr.size()), log;
+      for (size_t q = 0; q < pr.size(); ++q) next[q] = (int32_t)q + 1;
+      const int want = lower - nl;
+      const int64_t acc = e.chainPairs(*this, DA_LEADERSHIP, pr, pb, next, want, log);
+      Model::Replay rp(m);
+      for (int q : log) m.relocateLeadership(m.rPart[pr[q]], m.rBroker[pr[q]], b);
+      return acc < want;
     }
     size_t start = 0;
     std::vector<int32_t> spr, spb;

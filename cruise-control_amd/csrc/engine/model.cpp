@@ -203,6 +203,9 @@ void Model::build(const ccmi_cluster_desc& d) {
   bDirty.assign(B, 0);
   rDirty.assign(R, 0);
   pDirty.assign(P, 0);
+  cDirtyB.assign(B, 0);
+  cDirtyR.assign(R, 0);
+  cDirtyP.assign(P, 0);
 }
 
 void Model::refreshBroker(int b) {
@@ -346,7 +349,9 @@ void Model::relocateReplica(int p, int src, int dst) {
     topicCountDense[(size_t)pTopic[p] * ldB + src]--;
     topicCountDense[(size_t)pTopic[p] * ldB + dst]++;
   }
-  if (dev) {
+  if (dev && !replaying) {
+    markChain(cDirtyB, cDirtyBList, src);
+    markChain(cDirtyB, cDirtyBList, dst);
     markB(src);
     markB(dst);
     markR(r);
@@ -368,30 +373,8 @@ bool Model::relocateLeadership(int p, int src, int dst) {
   ops.subAll(bLnw[src], rLoad[sr]);
   sortedErase(src, sr);
   LoadVec& L = rLoad[sr];
-  Window totOut, totIn, chg;
-  ops.zero(totOut);
-  ops.add(totOut, L.m[M_LBO]);
-  ops.add(totOut, L.m[M_RBO]);
-  ops.zero(totIn);
-  ops.add(totIn, L.m[M_LBI]);
-  ops.add(totIn, L.m[M_RBI]);
-  ops.zero(chg);
-  for (int i = 0; i < W; ++i) {
-    const double in = (double)totIn.v[i], out = (double)totOut.v[i], c = (double)L.m[M_CPU].v[i];
-    const double follower = (in == 0.0 && out == 0.0) ? 0.0 : c * (0.15 * in) / (0.7 * in + 0.15 * out);
-    ops.set(chg, i, (double)L.m[M_CPU].v[i] - follower);
-    ops.set(L.m[M_CPU], i, follower);
-  }
   LoadVec delta;
-  delta.mask = (1 << M_CPU) | (1 << M_LBO) | (1 << M_RBO);
-  ops.zero(delta.m[M_CPU]);
-  ops.add(delta.m[M_CPU], chg);
-  ops.zero(delta.m[M_LBO]);
-  ops.add(delta.m[M_LBO], L.m[M_LBO]);
-  ops.zero(delta.m[M_RBO]);
-  ops.add(delta.m[M_RBO], L.m[M_RBO]);
-  ops.zero(L.m[M_LBO]);
-  ops.zero(L.m[M_RBO]);
+  ldMakeFollower(L, delta, W);
   rLeader[sr] = 0;
   refreshReplica(sr);
   if (bLoad[src].mask) ops.subAll(bLoad[src], delta);
@@ -416,7 +399,12 @@ bool Model::relocateLeadership(int p, int src, int dst) {
   refreshBroker(src);
   refreshBroker(dst);
   log.push_back({CCMI_LEADERSHIP_MOVEMENT, p, src, dst, -1});
-  if (dev) {
+  if (dev && !replaying) {
+    markChain(cDirtyB, cDirtyBList, src);
+    markChain(cDirtyB, cDirtyBList, dst);
+    markChain(cDirtyR, cDirtyRList, sr);
+    markChain(cDirtyR, cDirtyRList, dr);
+    markChain(cDirtyP, cDirtyPList, p);
     markB(src);
     markB(dst);
     markR(sr);
@@ -465,6 +453,31 @@ void Model::flushToDevice() {
     pDirty[p] = 0;
   }
   pDirtyList.clear();
+}
+
+void Model::flushChainLoads() {
+  if (!dev) return;
+  for (int b : cDirtyBList) {
+    dev->lrows.push_back({LR_BROKER, b, bLoad[b]});
+    dev->lrows.push_back({LR_LEADERSHIP_NW, b, bLnw[b]});
+    dev->lrows.push_back({LR_POTENTIAL, b, bPot[b]});
+    cDirtyB[b] = 0;
+  }
+  cDirtyBList.clear();
+  for (int r : cDirtyRList) {
+    dev->lrows.push_back({LR_REPLICA, r, rLoad[r]});
+    cDirtyR[r] = 0;
+  }
+  cDirtyRList.clear();
+  for (int p : cDirtyPList) {
+    SlotRow row;
+    row.p = p;
+    row.leader = pLeader[p];
+    for (int k = 0; k < kMaxRf; ++k) row.slots[k] = k < pOff[p + 1] - pOff[p] ? pSlots[pOff[p] + k] : -1;
+    dev->srows.push_back(row);
+    cDirtyP[p] = 0;
+  }
+  cDirtyPList.clear();
 }
 
 // ------------------------------------------------------------------------------- sorted replicas

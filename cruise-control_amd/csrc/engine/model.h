@@ -17,77 +17,26 @@
 #include "ccmi.h"
 #include "devtypes.h"
 #include "jsem.h"
+#include "loadops.h"
 
 namespace ccmi {
 
-enum Res { R_CPU = 0, R_NW_IN = 1, R_NW_OUT = 2, R_DISK = 3 };
-enum Met { M_CPU = 0, M_DISK = 1, M_LBI = 2, M_LBO = 3, M_RBI = 4, M_RBO = 5 };
-constexpr int kMaxW = 5;
-
-struct Window {  // one MetricValues
-  float v[kMaxW];
-  double sum;
-};
-struct LoadVec {  // AggregatedMetricValues over the 6 resource metrics
-  uint8_t mask = 0;
-  Window m[6];
-};
-
-class LoadOps {
+class LoadOps {  // loadops.h arithmetic with the session's window count
  public:
   explicit LoadOps(int W) : W(W) {}
   int W;
-  void zero(Window& x) const {
-    for (int i = 0; i < W; ++i) x.v[i] = 0.f;
-    x.sum = 0.0;
-  }
-  void add(Window& a, const Window& b) const {
-    for (int i = 0; i < W; ++i) {
-      const double d = (double)b.v[i];
-      a.v[i] = (float)((double)a.v[i] + d);
-      a.sum += d;
-    }
-  }
-  void sub(Window& a, const Window& b) const {
-    for (int i = 0; i < W; ++i) {
-      const double d = (double)b.v[i];
-      a.v[i] = (float)((double)a.v[i] - d);
-      a.sum -= d;
-    }
-  }
-  void set(Window& a, int i, double x) const {
-    a.sum += x - (double)a.v[i];
-    a.v[i] = (float)x;
-  }
-  float avg(const Window& a) const { return (float)(a.sum / W); }
-  void addAll(LoadVec& d, const LoadVec& s) const {  // AggregatedMetricValues.add
-    for (int k = 0; k < 6; ++k)
-      if (s.mask >> k & 1) {
-        if (!(d.mask >> k & 1)) {
-          zero(d.m[k]);
-          d.mask |= (uint8_t)(1 << k);
-        }
-        add(d.m[k], s.m[k]);
-      }
-  }
+  void zero(Window& x) const { ldZero(x, W); }
+  void add(Window& a, const Window& b) const { ldAdd(a, b, W); }
+  void sub(Window& a, const Window& b) const { ldSub(a, b, W); }
+  void set(Window& a, int i, double x) const { ldSet(a, i, x); }
+  float avg(const Window& a) const { return ldAvg(a, W); }
+  void addAll(LoadVec& d, const LoadVec& s) const { ldAddAll(d, s, W); }
   void subAll(LoadVec& d, const LoadVec& s) const {
     for (int k = 0; k < 6; ++k)
-      if (s.mask >> k & 1) {
-        if (!(d.mask >> k & 1)) throw std::runtime_error("subtract from a missing metric");
-        sub(d.m[k], s.m[k]);
-      }
+      if ((s.mask >> k & 1) && !(d.mask >> k & 1)) throw std::runtime_error("subtract from a missing metric");
+    ldSubAll(d, s, W);
   }
-  double util(const LoadVec& l, int res) const {  // ModelUtils.expectedUtilizationFor
-    if (!l.mask) return 0.0;
-    double r = 0;
-    switch (res) {
-      case R_CPU: r += (double)avg(l.m[M_CPU]); break;
-      case R_DISK: r += (double)l.m[M_DISK].v[0]; break;
-      case R_NW_IN: r += (double)avg(l.m[M_LBI]); r += (double)avg(l.m[M_RBI]); break;
-      default: r += (double)avg(l.m[M_LBO]); r += (double)avg(l.m[M_RBO]); break;
-    }
-    return jmax(r, 0.0);
-  }
+  double util(const LoadVec& l, int res) const { return ldUtil(l, res, W); }
   float groupAvg(const LoadVec& l, int res) const {  // valuesForGroup(group, def, shareValueArray=true).avg()
     if (res == R_CPU) return avg(l.m[M_CPU]);
     if (res == R_DISK) return avg(l.m[M_DISK]);
@@ -202,6 +151,24 @@ class Model {
     }
   }
   void flushToDevice();  // turn dirty rows into Device::brows/rrows/prows
+  // Chains (device.h): entities whose Java loads / slot order the host changed since the last chain launch, sent as
+  // Device::lrows / srows before the next one. While `replaying` the host re-applies moves the device already made:
+  // nothing is marked.
+  bool replaying = false;
+  std::vector<uint8_t> cDirtyB, cDirtyR, cDirtyP;
+  std::vector<int32_t> cDirtyBList, cDirtyRList, cDirtyPList;
+  void markChain(std::vector<uint8_t>& f, std::vector<int32_t>& l, int x) {
+    if (!f[x]) {
+      f[x] = 1;
+      l.push_back(x);
+    }
+  }
+  void flushChainLoads();
+  struct Replay {  // scope in which relocations re-apply moves a device chain already made
+    Model& m;
+    explicit Replay(Model& mm) : m(mm) { m.replaying = true; }
+    ~Replay() { m.replaying = false; }
+  };
 
   // ---- queries
   bool alive(int b) const { return bState[b] != BState::DEAD; }

@@ -23,6 +23,15 @@ struct PhaseProf {
   const int64_t* candCounter = nullptr;  // the engine's reference-equivalent candidate count
   int64_t cands[PH_COUNT] = {};
   bool on = std::getenv("CCMI_PROFILE") != nullptr;
+  // named event counters (diagnostics of the drivers' control flow)
+  static constexpr int kCounters = 16;
+  const char* counterName[kCounters] = {};
+  int64_t counter[kCounters] = {};
+  void count(int i, const char* name, int64_t d = 1) {
+    if (!on) return;
+    counterName[i] = name;
+    counter[i] += d;
+  }
   void print(const char* tag) const {
     static const char* names[PH_COUNT] = {"rdg.moveOut", "rdg.moveIn", "res.moveOut", "res.moveIn", "res.swap",
                                           "device.scan", "device.stats", "relocate", "cand.build", "sorted.init",
@@ -39,6 +48,8 @@ struct PhaseProf {
                        (long long)cands[i]);
         std::fprintf(stderr, "\n");
       }
+    for (int i = 0; i < kCounters; ++i)
+      if (counterName[i]) std::fprintf(stderr, "  #%-28s %12lld\n", counterName[i], (long long)counter[i]);
   }
 };
 

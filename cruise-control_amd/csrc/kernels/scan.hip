@@ -23,6 +23,7 @@
 
 #include <cstdlib>
 
+#include "../engine/apply.h"
 #include "../engine/devtypes.h"
 #include "../engine/predicates.h"
 
@@ -656,6 +657,166 @@ __global__ __launch_bounds__(kBlock) void scan_pairs(DevTables T, MutTables Mt, 
   CCMI_STAMP(T, seq, 5);
 }
 
+// ------------------------------------------------------------------------------------------------ chains
+// K7: first-fit decisions applied on the device, one after the other, inside ONE launch. One workgroup: every
+// decision evaluates the remaining candidates in blocks of kBlock (first accepted = block minimum), thread 0 applies
+// the winning move to the device records and loads (apply.h, the host model's exact arithmetic), and the workgroup
+// continues with the state the next decision of the reference loop would see. The host replays the logged moves
+// into its own model afterwards.
+struct DevApply {
+  ChainTables c;
+  int W;
+  __device__ __forceinline__ LoadVec& rLoad(int r) { return c.rLoad[r]; }
+  __device__ __forceinline__ LoadVec& bLoad(int b) { return c.bLoad[b]; }
+  __device__ __forceinline__ LoadVec& bLnw(int b) { return c.bLnw[b]; }
+  __device__ __forceinline__ LoadVec& bPot(int b) { return c.bPot[b]; }
+  __device__ __forceinline__ ReplicaRec& rep(int r) { return c.replicas[r]; }
+  __device__ __forceinline__ BrokerRec& brk(int b) { return c.brokers[b]; }
+  __device__ __forceinline__ PartitionRec& part(int p) { return c.parts[p]; }
+  __device__ __forceinline__ int& slot(int p, int i) { return c.pSlots[c.pOff[p] + i]; }
+  __device__ __forceinline__ int& leader(int p) { return c.pLeader[p]; }
+  __device__ __forceinline__ void topicAdd(int t, int b, int d) { c.topicCount[(size_t)t * c.ldB + b] += d; }
+};
+
+// thread 0's record writes become visible to the whole workgroup, and nobody keeps a stale L1 line of them
+__device__ __forceinline__ void chainSync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+  __syncthreads();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+}
+
+// First accepted pair q in [start, n) on the current state (kNone if none), block-uniform.
+__device__ __forceinline__ unsigned long long chainFirstPair(const DevTables& T, const DevProgram& prog,
+                                                             const OverlayLds& ov, const int32_t* pr,
+                                                             const int32_t* pb, int start, int n) {
+  for (int base = start; base < n; base += kBlock) {
+    const int q = base + threadIdx.x;
+    unsigned long long local = kNone;
+    if (q < n) {
+      PreView v;
+      v.loadDst(T, pb[q], ov);
+      v.loadRow(T, prog, pr[q], ov);
+      if (!v.exclLeadBlocked(prog) && moveCandidateAccepted(prog, v, v.r, v.dst)) local = (unsigned long long)q;
+    }
+    const unsigned long long m = blockMin(local);
+    if (m != kNone) return m;
+  }
+  return kNone;
+}
+
+// PAIRS: pairs (pr[q], pb[q]) in reference order; after accepting q the loop resumes at next[q]; at most
+// maxAccepts moves (the callers' stop counts). visited = reference-equivalent candidates of the sequence of scans.
+__global__ __launch_bounds__(kBlock) void chain_pairs(DevTables T, ChainTables C, DevProgram prog,
+                                                      const int32_t* __restrict__ pr, const int32_t* __restrict__ pb,
+                                                      const int32_t* __restrict__ next, int n, int maxAccepts,
+                                                      int32_t* __restrict__ log, ChainResultDev* __restrict__ out) {
+  __shared__ OverlayLds ov;
+  if (threadIdx.x == 0) ov.nb = ov.nr = ov.np = 0;
+  __syncthreads();
+  DevApply S{C, C.W};
+  int start = 0, acc = 0;
+  unsigned long long visited = 0;
+  while (start < n && acc < maxAccepts) {
+    const unsigned long long best = chainFirstPair(T, prog, ov, pr, pb, start, n);
+    if (best == kNone) {
+      visited += (unsigned long long)(n - start);
+      break;
+    }
+    visited += best - (unsigned long long)start + 1;
+    const int q = (int)best;
+    if (threadIdx.x == 0) {
+      log[acc] = q;
+      const ReplicaRec& rr = C.replicas[pr[q]];
+      if (prog.action == DA_LEADERSHIP) applyRelocateLeadership(S, rr.part, rr.broker, pb[q]);
+      else applyRelocateReplica(S, pr[q], pb[q]);
+    }
+    ++acc;
+    chainSync();
+    start = next[q];
+  }
+  if (threadIdx.x == 0) {
+    out->accepts = (unsigned long long)acc;
+    out->visited = visited;
+    out->failRow = 0;
+  }
+}
+
+// RACK_ROWS: AbstractRackAwareGoal.rebalanceForBroker (AbstractRackAwareGoal.java:144-170) over the rows of every
+// broker in order. A row is skipped when its broker is alive, the replica online and shouldKeepInTheCurrentBroker
+// holds on the CURRENT partition state (RackAwareGoal.java:214-225); otherwise the first candidate in cands[0, N)
+// that rackAwareEligibleBrokers keeps and the predicate conjunction accepts wins. No winner: failRow = row + 1.
+__global__ __launch_bounds__(kBlock) void chain_rack_rows(DevTables T, ChainTables C, DevProgram prog,
+                                                          const int32_t* __restrict__ rows, int n,
+                                                          const int32_t* __restrict__ cands, int N,
+                                                          int32_t* __restrict__ log, ChainResultDev* __restrict__ out) {
+  __shared__ OverlayLds ov;
+  if (threadIdx.x == 0) ov.nb = ov.nr = ov.np = 0;
+  __syncthreads();
+  DevApply S{C, C.W};
+  int acc = 0;
+  unsigned long long fail = 0;
+  for (int k = 0; k < n; ++k) {
+    const int r = rows[k];
+    const ReplicaRec rr = C.replicas[r];
+    const BrokerRec& sb = C.brokers[rr.broker];
+    const bool off = ((rr.flags & (RF_ORIG_OFFLINE | RF_ORIG_DEAD)) && rr.broker == rr.orig) || !sb.alive;
+    const PartitionRec& pp = C.parts[rr.part];
+    bool keep = true;
+    for (int i = 0; i < pp.n; ++i) keep &= !(pp.brokers[i] != rr.broker && pp.racks[i] == sb.rack);
+    if (sb.alive && !off && keep) continue;
+    unsigned long long best = kNone;
+    for (int base = 0; base < N; base += kBlock) {
+      const int j = base + threadIdx.x;
+      unsigned long long local = kNone;
+      if (j < N) {
+        PreView v;
+        v.loadDst(T, cands[j], ov);
+        v.loadRow(T, prog, r, ov);
+        if (v.rackEligible() && !v.exclLeadBlocked(prog) && moveCandidateAccepted(prog, v, v.r, v.dst))
+          local = (unsigned long long)j;
+      }
+      const unsigned long long m = blockMin(local);
+      if (m != kNone) {
+        best = m;
+        break;
+      }
+    }
+    if (best == kNone) {
+      fail = (unsigned long long)k + 1;
+      break;
+    }
+    if (threadIdx.x == 0) {
+      log[2 * acc] = k;
+      log[2 * acc + 1] = (int)best;
+      applyRelocateReplica(S, r, cands[best]);
+    }
+    ++acc;
+    chainSync();
+  }
+  if (threadIdx.x == 0) {
+    out->accepts = (unsigned long long)acc;
+    out->visited = 0;
+    out->failRow = fail;
+  }
+}
+
+// Host-side load changes since the last chain (LoadRow / SlotRow lists staged in host-mapped memory).
+__global__ __launch_bounds__(256) void sync_loads(ChainTables C, const LoadRow* __restrict__ lrows, int nl,
+                                                  const SlotRow* __restrict__ srows, int ns) {
+  const int stride = gridDim.x * blockDim.x;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < nl; i += stride) {
+    const LoadRow& x = lrows[i];
+    LoadVec* dst = x.kind == LR_REPLICA ? C.rLoad : (x.kind == LR_BROKER ? C.bLoad : (x.kind == LR_LEADERSHIP_NW ? C.bLnw : C.bPot));
+    dst[x.id] = x.v;
+  }
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < ns; i += stride) {
+    const SlotRow& x = srows[i];
+    const int o = C.pOff[x.p], n = C.pOff[x.p + 1] - o;
+    for (int k = 0; k < n; ++k) C.pSlots[o + k] = x.slots[k];
+    C.pLeader[x.p] = x.leader;
+  }
+}
+
 __global__ __launch_bounds__(256) void prep(MutTables M,
                                             const BrokerRow* __restrict__ brows, int nb,
                                             const ReplicaRow* __restrict__ rrows, int nr,
@@ -727,6 +888,27 @@ hipError_t launchScanPairs(const DevTables& T, const MutTables& M, const UpdateL
   const unsigned blocks = gridFor((uint64_t)n, (uint64_t)kBlock, residentBlocks());
   hipLaunchKernelGGL(scan_pairs, dim3(blocks), dim3(kBlock), 0, st, T, M, U, prog, pr, pb, n, keyBase, result, done,
                      mail, seq);
+  return hipGetLastError();
+}
+
+hipError_t launchChainPairs(const DevTables& T, const ChainTables& C, const DevProgram& prog, const int32_t* pr,
+                            const int32_t* pb, const int32_t* next, int n, int maxAccepts, int32_t* log,
+                            ChainResultDev* out, hipStream_t st) {
+  hipLaunchKernelGGL(chain_pairs, dim3(1), dim3(kBlock), 0, st, T, C, prog, pr, pb, next, n, maxAccepts, log, out);
+  return hipGetLastError();
+}
+
+hipError_t launchChainRackRows(const DevTables& T, const ChainTables& C, const DevProgram& prog, const int32_t* rows,
+                               int n, const int32_t* cands, int N, int32_t* log, ChainResultDev* out, hipStream_t st) {
+  hipLaunchKernelGGL(chain_rack_rows, dim3(1), dim3(kBlock), 0, st, T, C, prog, rows, n, cands, N, log, out);
+  return hipGetLastError();
+}
+
+hipError_t launchSyncLoads(const ChainTables& C, const LoadRow* lrows, int nl, const SlotRow* srows, int ns,
+                           hipStream_t st) {
+  if (nl + ns == 0) return hipSuccess;
+  const unsigned blocks = gridFor((uint64_t)(nl > ns ? nl : ns), 256, 1024);
+  hipLaunchKernelGGL(sync_loads, dim3(blocks), dim3(256), 0, st, C, lrows, nl, srows, ns);
   return hipGetLastError();
 }
 

@@ -10,6 +10,7 @@
 #include <stdexcept>
 #include <vector>
 
+#include "apply.h"
 #include "device.h"
 #include "predicates.h"
 #include "shard_rccl.h"
@@ -31,6 +32,10 @@ struct Emu {
   std::vector<int32_t> bRack, pTopic, tUpper, tLower;
   std::vector<uint8_t> bAlive, rFlags;
   std::vector<uint32_t> allowed;
+  // chain state (device.h uploadLoads)
+  int W = 1;
+  std::vector<LoadVec> lRep, lBrk, lLnw, lPot;
+  std::vector<int32_t> pSlots, pLeader;
 };
 struct View {
   const Emu& e;
@@ -220,6 +225,195 @@ int64_t Device::scanSwap(const DevProgram& prog, const int32_t* srcs, int S, con
       }
     }
   return -1;
+}
+
+// ------------------------------------------------------------------------------------------------ chains
+// The chain kernels' decisions, one candidate at a time, with apply.h on record mirrors of the emulated tables.
+namespace {
+struct EmuApply {
+  Emu& e;
+  int W;
+  std::vector<BrokerRec> brokers;
+  std::vector<ReplicaRec> replicas;
+  std::vector<PartitionRec> parts;
+  explicit EmuApply(Emu& em) : e(em), W(em.W) {
+    brokers.assign(e.B, BrokerRec{});
+    for (int b = 0; b < e.B; ++b) {
+      BrokerRec& x = brokers[b];
+      for (int k = 0; k < 4; ++k) {
+        x.util[k] = e.bUtil[(size_t)k * e.B + b];
+        x.cap[k] = e.bCap[(size_t)k * e.B + b];
+      }
+      x.pot = e.bPot[b];
+      x.lbi = e.bLeadNwIn[b];
+      x.nrep = e.bNrep[b];
+      x.nlead = e.bNlead[b];
+      x.rack = e.bRack[b];
+      x.allowedBits = e.allowed[b];
+      x.alive = e.bAlive[b];
+    }
+    replicas.assign(e.R, ReplicaRec{});
+    for (int r = 0; r < e.R; ++r) {
+      ReplicaRec& x = replicas[r];
+      for (int k = 0; k < 4; ++k) x.util[k] = e.rUtil[(size_t)k * e.R + r];
+      x.broker = e.rBroker[r];
+      x.part = e.rPart[r];
+      x.orig = e.rOrig[r];
+      x.flags = e.rFlags[r];
+    }
+    parts.assign(e.P, PartitionRec{});
+    for (int p = 0; p < e.P; ++p) {
+      PartitionRec& x = parts[p];
+      x.n = e.pOff[p + 1] - e.pOff[p];
+      x.topic = e.pTopic[p];
+      for (int k = 0; k < kMaxRf; ++k) {
+        x.brokers[k] = k < x.n ? e.pBrokers[e.pOff[p] + k] : -1;
+        x.racks[k] = (int16_t)(k < x.n ? e.bRack[x.brokers[k]] : -1);
+      }
+      x.leadNwOut = e.pLeadNwOut[p];
+    }
+  }
+  LoadVec& rLoad(int r) { return e.lRep[r]; }
+  LoadVec& bLoad(int b) { return e.lBrk[b]; }
+  LoadVec& bLnw(int b) { return e.lLnw[b]; }
+  LoadVec& bPot(int b) { return e.lPot[b]; }
+  ReplicaRec& rep(int r) { return replicas[r]; }
+  BrokerRec& brk(int b) { return brokers[b]; }
+  PartitionRec& part(int p) { return parts[p]; }
+  int& slot(int p, int i) { return e.pSlots[e.pOff[p] + i]; }
+  int& leader(int p) { return e.pLeader[p]; }
+  void topicAdd(int t, int b, int d) { e.topicCount[(size_t)t * e.ldB + b] += d; }
+  // the records a move touched, back into the emulated columns the predicates read
+  void writeBroker(int b) {
+    const BrokerRec& x = brokers[b];
+    for (int k = 0; k < 4; ++k) e.bUtil[(size_t)k * e.B + b] = x.util[k];
+    e.bPot[b] = x.pot;
+    e.bLeadNwIn[b] = x.lbi;
+    e.bNrep[b] = x.nrep;
+    e.bNlead[b] = x.nlead;
+  }
+  void writeReplica(int r) {
+    const ReplicaRec& x = replicas[r];
+    for (int k = 0; k < 4; ++k) e.rUtil[(size_t)k * e.R + r] = x.util[k];
+    e.rBroker[r] = x.broker;
+    e.rFlags[r] = (uint8_t)x.flags;
+  }
+  void writePartition(int p) {
+    const PartitionRec& x = parts[p];
+    for (int k = 0; k < x.n; ++k) e.pBrokers[e.pOff[p] + k] = x.brokers[k];
+    e.pLeadNwOut[p] = x.leadNwOut;
+  }
+  void moveReplica(int r, int dst) {
+    const int src = replicas[r].broker, p = replicas[r].part;
+    applyRelocateReplica(*this, r, dst);
+    writeBroker(src);
+    writeBroker(dst);
+    writeReplica(r);
+    writePartition(p);
+  }
+  void moveLeadership(int p, int src, int dst) {
+    std::vector<int> reps;
+    for (int i = 0; i < parts[p].n; ++i) reps.push_back(slot(p, i));
+    applyRelocateLeadership(*this, p, src, dst);
+    writeBroker(src);
+    writeBroker(dst);
+    for (int r : reps) writeReplica(r);
+    writePartition(p);
+  }
+};
+}  // namespace
+
+void Device::uploadLoads(int W, const LoadVec* rLoad, const LoadVec* bLoad, const LoadVec* bLnw, const LoadVec* bPot,
+                         const int32_t* pSlots, const int32_t* pLeader) {
+  Emu& e = E(st_);
+  e.W = W;
+  e.lRep.assign(rLoad, rLoad + R_);
+  e.lBrk.assign(bLoad, bLoad + B_);
+  e.lLnw.assign(bLnw, bLnw + B_);
+  e.lPot.assign(bPot, bPot + B_);
+  e.pSlots.assign(pSlots, pSlots + R_);
+  e.pLeader.assign(pLeader, pLeader + P_);
+}
+
+static void emuSyncLoads(Emu& e, std::vector<LoadRow>& lrows, std::vector<SlotRow>& srows) {
+  for (const LoadRow& x : lrows) {
+    std::vector<LoadVec>& v = x.kind == LR_REPLICA ? e.lRep : (x.kind == LR_BROKER ? e.lBrk : (x.kind == LR_LEADERSHIP_NW ? e.lLnw : e.lPot));
+    v[x.id] = x.v;
+  }
+  for (const SlotRow& x : srows) {
+    for (int k = 0; k < e.pOff[x.p + 1] - e.pOff[x.p]; ++k) e.pSlots[e.pOff[x.p] + k] = x.slots[k];
+    e.pLeader[x.p] = x.leader;
+  }
+  lrows.clear();
+  srows.clear();
+}
+
+Device::ChainResult Device::chainPairs(const DevProgram& prog, const int32_t* pr, const int32_t* pb, const int32_t* next,
+                                       int n, int maxAccepts, std::vector<int32_t>& log) {
+  flushOnly();
+  Emu& e = E(st_);
+  emuSyncLoads(e, lrows, srows);
+  ChainResult res;
+  log.clear();
+  if (n <= 0) return res;
+  perf.scanLaunches++;
+  perf.chainLaunches++;
+  EmuApply A(e);
+  View v{e};
+  int start = 0;
+  while (start < n && res.accepts < maxAccepts) {
+    int best = -1;
+    for (int q = start; q < n && best < 0; ++q) {
+      if (prog.exclLeadMove && (v.flags(pr[q]) & RF_LEADER) && v.allowed(kExclLeadBit, pb[q])) continue;
+      if (moveCandidateAccepted(prog, v, pr[q], pb[q])) best = q;
+    }
+    if (best < 0) {
+      res.visited += n - start;
+      break;
+    }
+    res.visited += best - start + 1;
+    log.push_back(best);
+    res.accepts++;
+    if (prog.action == DA_LEADERSHIP) A.moveLeadership(e.rPart[pr[best]], e.rBroker[pr[best]], pb[best]);
+    else A.moveReplica(pr[best], pb[best]);
+    start = next[best];
+  }
+  perf.scanPairs += res.visited;
+  return res;
+}
+
+Device::ChainResult Device::chainRackRows(const DevProgram& prog, const int32_t* rows, int n, const int32_t* cands,
+                                          int N, std::vector<int32_t>& log) {
+  flushOnly();
+  Emu& e = E(st_);
+  emuSyncLoads(e, lrows, srows);
+  ChainResult res;
+  log.clear();
+  if (n <= 0) return res;
+  perf.scanLaunches++;
+  perf.chainLaunches++;
+  EmuApply A(e);
+  View v{e};
+  for (int k = 0; k < n; ++k) {
+    const int r = rows[k], src = e.rBroker[r];
+    const bool keep = !v.otherOnRack(e.rPart[r], src, e.bRack[src]);
+    if (v.alive(src) && !currentOffline(v, r) && keep) continue;
+    int best = -1;
+    for (int j = 0; j < N && best < 0; ++j) {
+      if (!v.rackEligible(r, cands[j])) continue;
+      if (prog.exclLeadMove && (v.flags(r) & RF_LEADER) && v.allowed(kExclLeadBit, cands[j])) continue;
+      if (moveCandidateAccepted(prog, v, r, cands[j])) best = j;
+    }
+    if (best < 0) {
+      res.failRow = k + 1;
+      break;
+    }
+    log.push_back(k);
+    log.push_back(best);
+    res.accepts++;
+    A.moveReplica(r, cands[best]);
+  }
+  return res;
 }
 
 void Device::stats(const StatsParams& P, const uint8_t* aa, StatsOut* out) {
