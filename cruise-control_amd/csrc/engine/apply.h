@@ -8,96 +8,159 @@
 //   Broker.addReplica / removeReplica / makeFollower / makeLeader  model/Broker.java:336-510
 //   Replica.makeFollower / makeLeader model/Replica.java:210-310
 //   Partition.relocateLeadership     model/Partition.java:243-247
+//
+// A move changes up to six load aggregates, each by exactly one add or subtract, so the aggregates are updated by
+// "lanes" that run in parallel on the device (one wavefront, lane-dependent addresses, one memory round trip) and one
+// after the other in the emulation. Steps separate the lanes that depend on each other (leadership: the follower
+// CPU delta first). The record fields each lane writes are disjoint.
 #pragma once
 #include "devtypes.h"
 #include "loadops.h"
 
 namespace ccmi {
 
-// S provides: W; LoadVec& rLoad(r), bLoad(b), bLnw(b), bPot(b); ReplicaRec& rep(r); BrokerRec& brk(b);
-// PartitionRec& part(p); int& slot(p, i) (replica id of partition slot i); int& leader(p); void topicAdd(t, b, d).
-template <class S>
-CCMI_LD void applyRefreshBroker(S& s, int b) {
-  BrokerRec& x = s.brk(b);
-  for (int k = 0; k < 4; ++k) x.util[k] = ldUtil(s.bLoad(b), k, s.W);
-  x.pot = ldUtil(s.bPot(b), R_NW_OUT, s.W);
-  x.lbi = ldUtil(s.bLnw(b), R_NW_IN, s.W);
+CCMI_LD void ldCopy(LoadVec& d, const LoadVec& s, int W) {  // the W live windows of every metric
+  d.mask = s.mask;
+  for (int k = 0; k < 6; ++k) {
+    for (int i = 0; i < W; ++i) d.m[k].v[i] = s.m[k].v[i];
+    d.m[k].sum = s.m[k].sum;
+  }
 }
-template <class S>
-CCMI_LD void applyRefreshReplica(S& s, int r) {
-  for (int k = 0; k < 4; ++k) s.rep(r).util[k] = ldUtil(s.rLoad(r), k, s.W);
+// ldAddAll (neg = false) / ldSubAll (neg = true): x - y is x + (-y) in IEEE arithmetic, so one instruction stream
+// serves both; a missing metric is created only by an add (a subtract always finds it)
+CCMI_LD void ldAddSignedAll(LoadVec& d, const LoadVec& s, int W, bool neg) {
+  for (int k = 0; k < 6; ++k)
+    if (s.mask >> k & 1) {
+      if (!(d.mask >> k & 1)) {
+        ldZero(d.m[k], W);
+        d.mask |= (uint8_t)(1 << k);
+      }
+      for (int i = 0; i < W; ++i) {
+        const double x = neg ? -(double)s.m[k].v[i] : (double)s.m[k].v[i];
+        d.m[k].v[i] = (float)((double)d.m[k].v[i] + x);
+        d.m[k].sum += x;
+      }
+    }
 }
 
-// relocateReplica(tp, src, dst) of replica r (its broker is the source)
+// S provides: W; LoadVec& rLoad(r), bLoad(b), bLnw(b), bPot(b), scratch(i) (i = 0, 1: step-to-step values);
+// ReplicaRec& rep(r); BrokerRec& brk(b); PartitionRec& part(p); int& slot(p, i) (replica id of partition slot i);
+// int& leader(p); void topicAdd(t, b, d).
+
+// ---- relocateReplica(tp, src, dst) of replica r: lanes 0..5, then applyReplicaFinish
+//   lane 0/1 Broker.load() of src (-= r) / dst (+= r)         -> util[4]
+//   lane 2/3 potential leadership load of src / dst (+-= leader of p) -> pot
+//   lane 4/5 leadership NW load of src / dst (+-= r, leaders only)    -> lbi
+constexpr int kReplicaLanes = 6;
 template <class S>
-CCMI_LD void applyRelocateReplica(S& s, int r, int dst) {
-  ReplicaRec& rr = s.rep(r);
-  const int src = rr.broker, p = rr.part;
-  const bool lead = (rr.flags & RF_LEADER) != 0;
-  // Broker.removeReplica(src)
-  ldSubAll(s.bLoad(src), s.rLoad(r), s.W);
-  if (lead) {
-    ldSubAll(s.bLnw(src), s.rLoad(r), s.W);
-    s.brk(src).nlead -= 1;
+CCMI_LD void applyReplicaLane(S& s, int lane, int r, int src, int dst, int lr, bool lead) {
+  if (lane >= kReplicaLanes || (lane >= 4 && !lead)) return;
+  const int b = (lane & 1) ? dst : src;
+  LoadVec& t = lane < 2 ? s.bLoad(b) : (lane < 4 ? s.bPot(b) : s.bLnw(b));
+  LoadVec x, o;
+  ldCopy(x, t, s.W);
+  ldCopy(o, (lane == 2 || lane == 3) ? s.rLoad(lr) : s.rLoad(r), s.W);
+  ldAddSignedAll(x, o, s.W, !(lane & 1));
+  ldCopy(t, x, s.W);
+  BrokerRec& rec = s.brk(b);
+  if (lane < 2) {
+    for (int k = 0; k < 4; ++k) rec.util[k] = ldUtil(x, k, s.W);
+  } else if (lane < 4) {
+    rec.pot = ldUtil(x, R_NW_OUT, s.W);
+  } else {
+    rec.lbi = ldUtil(x, R_NW_IN, s.W);
   }
+}
+// counts, the replica's broker, its partition slot and the topic counts (one thread, after the lanes)
+template <class S>
+CCMI_LD void applyReplicaFinish(S& s, int r, int src, int dst, bool lead) {
   s.brk(src).nrep -= 1;
-  // _potentialLeadershipLoadByBrokerId
-  const int lr = s.leader(p);
-  ldSubAll(s.bPot(src), s.rLoad(lr), s.W);
-  rr.broker = dst;
-  // Broker.addReplica(dst)
+  s.brk(dst).nrep += 1;
   if (lead) {
-    ldAddAll(s.bLnw(dst), s.rLoad(r), s.W);
+    s.brk(src).nlead -= 1;
     s.brk(dst).nlead += 1;
   }
-  ldAddAll(s.bLoad(dst), s.rLoad(r), s.W);
-  s.brk(dst).nrep += 1;
-  ldAddAll(s.bPot(dst), s.rLoad(lr), s.W);
-  applyRefreshBroker(s, src);
-  applyRefreshBroker(s, dst);
+  const int p = s.rep(r).part;
+  s.rep(r).broker = dst;
   PartitionRec& pr = s.part(p);
-  for (int i = 0; i < pr.n; ++i)
-    if (s.slot(p, i) == r) {
+  const int16_t rk = (int16_t)s.brk(dst).rack;
+  for (int i = 0; i < kMaxRf; ++i)
+    if (i < pr.n && s.slot(p, i) == r) {
       pr.brokers[i] = dst;
-      pr.racks[i] = (int16_t)s.brk(dst).rack;
+      pr.racks[i] = rk;
     }
   s.topicAdd(pr.topic, src, -1);
   s.topicAdd(pr.topic, dst, +1);
 }
 
-// relocateLeadership(tp, src, dst): src's replica of p must be the leader, dst's a follower
+// ---- relocateLeadership(tp, src, dst) of the leader sr (on src) to the follower dr (on dst)
+//   step 0: lane 0 leadership NW load of src -= sr (its load before makeFollower)            -> src lbi
+//           lane 1 makeFollower on a copy of sr's load: scratch(0) = delta, scratch(1) = new load of sr
+//   step 1: lane 0 Broker.load() of src -= delta (when it has metrics)                          -> src util
+//           lane 1 Broker.load() of dst += delta (when it has metrics)                          -> dst util
+//           lane 2 dr's load += delta (when it has metrics)                                    -> dr util, leader flag
+//           lane 3 sr's load = scratch(1)                                                       -> sr util, leader flag
+//   step 2: lane 0 leadership NW load of dst += dr's new load                                  -> dst lbi
+// then applyLeadershipFinish: leader counts, Partition.relocateLeadership and the partition record
+constexpr int kLeadershipSteps = 3;
 template <class S>
-CCMI_LD void applyRelocateLeadership(S& s, int p, int src, int dst) {
-  PartitionRec& pr = s.part(p);
-  int sr = -1, dr = -1, dpos = 0;
-  for (int i = 0; i < pr.n; ++i) {
-    const int x = s.slot(p, i);
-    if (s.rep(x).broker == src) sr = x;
-    if (s.rep(x).broker == dst) {
-      dr = x;
-      dpos = i;
+CCMI_LD void applyLeadershipLane(S& s, int step, int lane, int sr, int dr, int src, int dst) {
+  LoadVec x, o;
+  if (step == 0) {
+    if (lane == 0) {
+      ldCopy(x, s.bLnw(src), s.W);
+      ldCopy(o, s.rLoad(sr), s.W);
+      ldAddSignedAll(x, o, s.W, true);
+      ldCopy(s.bLnw(src), x, s.W);
+      s.brk(src).lbi = ldUtil(x, R_NW_IN, s.W);
+    } else if (lane == 1) {
+      ldCopy(x, s.rLoad(sr), s.W);
+      ldMakeFollower(x, o, s.W);
+      ldCopy(s.scratch(0), o, s.W);
+      ldCopy(s.scratch(1), x, s.W);
     }
+  } else if (step == 1) {
+    if (lane > 3) return;
+    if (lane == 3) {
+      ldCopy(x, s.scratch(1), s.W);
+      ldCopy(s.rLoad(sr), x, s.W);
+      ReplicaRec& rec = s.rep(sr);
+      rec.flags &= ~(int32_t)RF_LEADER;
+      for (int k = 0; k < 4; ++k) rec.util[k] = ldUtil(x, k, s.W);
+      return;
+    }
+    LoadVec& t = lane == 0 ? s.bLoad(src) : (lane == 1 ? s.bLoad(dst) : s.rLoad(dr));
+    ldCopy(x, t, s.W);
+    if (x.mask) {
+      ldCopy(o, s.scratch(0), s.W);
+      ldAddSignedAll(x, o, s.W, lane == 0);
+      ldCopy(t, x, s.W);
+    }
+    if (lane < 2) {
+      BrokerRec& rec = s.brk(lane == 0 ? src : dst);
+      for (int k = 0; k < 4; ++k) rec.util[k] = ldUtil(x, k, s.W);
+    } else {
+      ReplicaRec& rec = s.rep(dr);
+      rec.flags |= (int32_t)RF_LEADER;
+      for (int k = 0; k < 4; ++k) rec.util[k] = ldUtil(x, k, s.W);
+    }
+  } else if (lane == 0) {
+    ldCopy(x, s.bLnw(dst), s.W);
+    ldCopy(o, s.rLoad(dr), s.W);
+    ldAddSignedAll(x, o, s.W, false);
+    ldCopy(s.bLnw(dst), x, s.W);
+    s.brk(dst).lbi = ldUtil(x, R_NW_IN, s.W);
   }
-  // Broker.makeFollower(src)
-  ldSubAll(s.bLnw(src), s.rLoad(sr), s.W);
-  LoadVec delta;
-  ldMakeFollower(s.rLoad(sr), delta, s.W);
-  s.rep(sr).flags &= ~(int32_t)RF_LEADER;
-  applyRefreshReplica(s, sr);
-  if (s.bLoad(src).mask) ldSubAll(s.bLoad(src), delta, s.W);
+}
+template <class S>
+CCMI_LD void applyLeadershipFinish(S& s, int p, int dr, int dpos, int src, int dst) {
   s.brk(src).nlead -= 1;
-  // Broker.makeLeader(dst)
-  s.rep(dr).flags |= (int32_t)RF_LEADER;
-  if (s.rLoad(dr).mask) ldAddAll(s.rLoad(dr), delta, s.W);
-  applyRefreshReplica(s, dr);
-  ldAddAll(s.bLnw(dst), s.rLoad(dr), s.W);
-  if (s.bLoad(dst).mask) ldAddAll(s.bLoad(dst), delta, s.W);
   s.brk(dst).nlead += 1;
-  // Partition.relocateLeadership: swap positions 0 and indexOf(dr)
   const int first = s.slot(p, 0);
   s.slot(p, 0) = dr;
   s.slot(p, dpos) = first;
   s.leader(p) = dr;
+  PartitionRec& pr = s.part(p);
   const int b0 = pr.brokers[0];
   pr.brokers[0] = pr.brokers[dpos];
   pr.brokers[dpos] = b0;
@@ -105,8 +168,38 @@ CCMI_LD void applyRelocateLeadership(S& s, int p, int src, int dst) {
   pr.racks[0] = pr.racks[dpos];
   pr.racks[dpos] = k0;
   pr.leadNwOut = s.rep(dr).util[R_NW_OUT];
-  applyRefreshBroker(s, src);
-  applyRefreshBroker(s, dst);
+}
+// the two replicas of p on src and dst, and dr's slot
+template <class S>
+CCMI_LD void leadershipReplicas(S& s, int p, int src, int dst, int& sr, int& dr, int& dpos) {
+  const PartitionRec& pr = s.part(p);
+  sr = dr = -1;
+  dpos = 0;
+  for (int i = 0; i < kMaxRf; ++i) {
+    if (i >= pr.n) break;
+    if (pr.brokers[i] == src) sr = s.slot(p, i);
+    if (pr.brokers[i] == dst) {
+      dr = s.slot(p, i);
+      dpos = i;
+    }
+  }
+}
+
+// Sequential form (emulation): every lane of every step in order.
+template <class S>
+inline void applyRelocateReplica(S& s, int r, int dst) {
+  const int src = s.rep(r).broker, lr = s.leader(s.rep(r).part);
+  const bool lead = (s.rep(r).flags & RF_LEADER) != 0;
+  for (int l = 0; l < kReplicaLanes; ++l) applyReplicaLane(s, l, r, src, dst, lr, lead);
+  applyReplicaFinish(s, r, src, dst, lead);
+}
+template <class S>
+inline void applyRelocateLeadership(S& s, int p, int src, int dst) {
+  int sr, dr, dpos;
+  leadershipReplicas(s, p, src, dst, sr, dr, dpos);
+  for (int st = 0; st < kLeadershipSteps; ++st)
+    for (int l = 0; l < 4; ++l) applyLeadershipLane(s, st, l, sr, dr, src, dst);
+  applyLeadershipFinish(s, p, dr, dpos, src, dst);
 }
 
 }  // namespace ccmi

@@ -917,21 +917,24 @@ class LeaderReplicaDistribution : public GoalImpl {
     copy.order(leaders);
     std::vector<int32_t> pr, pb, owner;
     std::vector<int> ins, hs, hs2, elig;
-    for (size_t q = 0; q < leaders.size(); ++q) {
-      const int r = leaders[q], p = m.rPart[r];
-      ins.clear();
-      for (int s = m.pOff[p]; s < m.pOff[p + 1]; ++s) ins.push_back(m.rBroker[m.pSlots[s]]);
-      javaHashSetOrder(ins, hs);  // Partition.partitionBrokers()
-      ins.clear();
-      for (int x : hs)
-        if (x != b && !m.curOffline(m.replicaOn(p, x))) ins.push_back(x);
-      javaHashSetOrder(ins, hs2);  // Collectors.toSet()
-      std::vector<int32_t> c32(hs2.begin(), hs2.end()), el;
-      e.eligible(c32, DA_LEADERSHIP, el);
-      for (int x : el) {
-        pr.push_back(r);
-        pb.push_back(x);
-        owner.push_back((int)q);
+    {
+      PhaseScope pc(PH_CAND_BUILD);
+      for (size_t q = 0; q < leaders.size(); ++q) {
+        const int r = leaders[q], p = m.rPart[r];
+        ins.clear();
+        for (int s = m.pOff[p]; s < m.pOff[p + 1]; ++s) ins.push_back(m.rBroker[m.pSlots[s]]);
+        javaHashSetOrder(ins, hs);  // Partition.partitionBrokers()
+        ins.clear();
+        for (int x : hs)
+          if (x != b && !m.curOffline(m.replicaOn(p, x))) ins.push_back(x);
+        javaHashSetOrder(ins, hs2);  // Collectors.toSet()
+        std::vector<int32_t> c32(hs2.begin(), hs2.end()), el;
+        e.eligible(c32, DA_LEADERSHIP, el);
+        for (int x : el) {
+          pr.push_back(r);
+          pb.push_back(x);
+          owner.push_back((int)q);
+        }
       }
     }
     if (e.chainsOn()) {  // one device chain: after an accept the scan resumes at the next leader's pairs
@@ -1013,14 +1016,21 @@ class LeaderReplicaDistribution : public GoalImpl {
       return c ? c : jcmpInt(m.bId[x], m.bId[y]);
     };
     RbTreeSet<decltype(cmp)> cand(cmp);
-    if (fix) {
-      for (int x : aliveById(m)) cand.add(x);
-    } else {
-      std::vector<int> ins, order;
-      for (int x = 0; x < m.B; ++x)
-        if (m.alive(x) && m.bNlead[x] < upper) ins.push_back(x);
-      javaHashSetOrder(ins, order);
-      for (int x : order) cand.add(x);
+    {
+      PhaseScope pi(PH_PQ_INIT);
+      if (fix) {
+        for (int x : aliveById(m)) cand.add(x);
+      } else {
+        std::vector<int> ins, order;
+        for (int x = 0; x < m.B; ++x)
+          if (m.alive(x) && m.bNlead[x] < upper) ins.push_back(x);
+        javaHashSetOrder(ins, order);  // Collectors.toSet()
+        // the same TreeSet.add sequence, placed by rank (the comparator is a total order on these brokers)
+        std::vector<int32_t> byKey(ins.begin(), ins.end()), rank(m.B, 0);
+        std::sort(byKey.begin(), byKey.end(), [&](int x, int y) { return cmp(x, y) < 0; });
+        for (size_t i = 0; i < byKey.size(); ++i) rank[byKey[i]] = (int32_t)i;
+        cand.buildByRank(order, rank);
+      }
     }
     cand.trackSequence();
     const int upperLimit = fix ? 0 : upper;

@@ -511,33 +511,75 @@ class OrderedQueue {
 
 // Iteration order of a HashSet<Broker> filled by add() in `ins` order (Broker.hashCode() == id).
 inline void javaHashSetOrder(const std::vector<int>& ins, std::vector<int>& out) {
-  unsigned cap = 16;
-  size_t n = 0;
-  std::vector<std::vector<int>> bins(cap);
   auto slot = [](int h, unsigned c) { return (unsigned)(h ^ (int)((unsigned)h >> 16)) & (c - 1); };
-  auto grow = [&]() {
-    unsigned nc = cap << 1;
-    std::vector<std::vector<int>> nb(nc);
-    for (auto& b : bins)
-      for (int k : b) nb[slot(k, nc)].push_back(k);
-    bins.swap(nb);
+  if (ins.size() <= 8) {  // the default 16-bucket table never resizes or treeifies: bucket order, insertion order within
+    int ks[8];
+    unsigned sl[8];
+    int m = 0;
+    for (int k : ins) {
+      bool dup = false;
+      for (int i = 0; i < m; ++i) dup |= ks[i] == k;
+      if (dup) continue;
+      int j = m++;
+      const unsigned s0 = slot(k, 16);
+      while (j > 0 && sl[j - 1] > s0) {
+        ks[j] = ks[j - 1];
+        sl[j] = sl[j - 1];
+        --j;
+      }
+      ks[j] = k;
+      sl[j] = s0;
+    }
+    out.assign(ks, ks + m);
+    return;
+  }
+  // General case: the JDK 11 HashMap insertion (bucket lists appended at the tail; a resize splits every list in
+  // order, so each bucket keeps insertion order; a list reaching 9 nodes resizes a table below 64 buckets), on flat
+  // arrays.
+  unsigned cap = 16;
+  const size_t N = ins.size();
+  std::vector<int> key(N), nxt(N), head(cap, -1), tail(cap, -1), cnt(cap, 0);
+  size_t n = 0;
+  auto rehash = [&]() {
+    const unsigned nc = cap << 1;
+    std::vector<int> nh(nc, -1), nt(nc, -1), nn(nc, 0);
+    for (unsigned b = 0; b < cap; ++b)
+      for (int e = head[b]; e >= 0;) {
+        const int following = nxt[e];
+        const unsigned t = slot(key[e], nc);
+        nxt[e] = -1;
+        if (nt[t] < 0) nh[t] = e;
+        else nxt[nt[t]] = e;
+        nt[t] = e;
+        nn[t]++;
+        e = following;
+      }
+    head.swap(nh);
+    tail.swap(nt);
+    cnt.swap(nn);
     cap = nc;
   };
   for (int k : ins) {
-    auto& b = bins[slot(k, cap)];
+    const unsigned b = slot(k, cap);
     bool dup = false;
-    for (int x : b) dup |= (x == k);
+    for (int e = head[b]; e >= 0 && !dup; e = nxt[e]) dup = key[e] == k;
     if (dup) continue;
-    b.push_back(k);
-    if (b.size() >= 9) {
-      if (cap < 64) grow();
+    const int e = (int)n;
+    key[e] = k;
+    nxt[e] = -1;
+    if (tail[b] < 0) head[b] = e;
+    else nxt[tail[b]] = e;
+    tail[b] = e;
+    if (++cnt[b] >= 9) {
+      if (cap < 64) rehash();
       else throw std::runtime_error("HashSet tree bin order is not emulated");
     }
-    if (++n > (size_t)(cap * 3 / 4)) grow();
+    if (++n > (size_t)(cap * 3 / 4)) rehash();
   }
   out.clear();
-  for (auto& b : bins)
-    for (int k : b) out.push_back(k);
+  out.reserve(n);
+  for (unsigned b = 0; b < cap; ++b)
+    for (int e = head[b]; e >= 0; e = nxt[e]) out.push_back(key[e]);
 }
 
 inline int32_t jStringHash(const char* s) {  // String.hashCode

@@ -663,13 +663,16 @@ __global__ __launch_bounds__(kBlock) void scan_pairs(DevTables T, MutTables Mt, 
 // the winning move to the device records and loads (apply.h, the host model's exact arithmetic), and the workgroup
 // continues with the state the next decision of the reference loop would see. The host replays the logged moves
 // into its own model afterwards.
+template <int WC>  // WC > 0: the window count as a compile-time constant (the lanes' copies stay in registers)
 struct DevApply {
   ChainTables c;
-  int W;
+  LoadVec* sc;  // two LoadVecs in LDS: the leadership steps' hand-over
+  static constexpr int W = WC;
   __device__ __forceinline__ LoadVec& rLoad(int r) { return c.rLoad[r]; }
   __device__ __forceinline__ LoadVec& bLoad(int b) { return c.bLoad[b]; }
   __device__ __forceinline__ LoadVec& bLnw(int b) { return c.bLnw[b]; }
   __device__ __forceinline__ LoadVec& bPot(int b) { return c.bPot[b]; }
+  __device__ __forceinline__ LoadVec& scratch(int i) { return sc[i]; }
   __device__ __forceinline__ ReplicaRec& rep(int r) { return c.replicas[r]; }
   __device__ __forceinline__ BrokerRec& brk(int b) { return c.brokers[b]; }
   __device__ __forceinline__ PartitionRec& part(int p) { return c.parts[p]; }
@@ -678,11 +681,46 @@ struct DevApply {
   __device__ __forceinline__ void topicAdd(int t, int b, int d) { c.topicCount[(size_t)t * c.ldB + b] += d; }
 };
 
-// thread 0's record writes become visible to the whole workgroup, and nobody keeps a stale L1 line of them
+// thread 0's record writes become visible to the whole workgroup (one CU: workgroup scope; the next launch sees them
+// through the kernel boundary)
 __device__ __forceinline__ void chainSync() {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
   __syncthreads();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+
+// Apply one move with the whole workgroup (apply.h lanes on threads 0..5, one step at a time); every thread calls it.
+template <int WC>
+__device__ void chainApply(const ChainTables& C, LoadVec* sc, int action, int r, int dst) {
+  DevApply<WC> S{C, sc};
+  const ReplicaRec rr = C.replicas[r];
+  const int src = rr.broker, p = rr.part;
+  const int t = threadIdx.x;
+  if (action == DA_LEADERSHIP) {
+    int sr, dr, dpos;
+    leadershipReplicas(S, p, src, dst, sr, dr, dpos);
+    for (int st = 0; st < kLeadershipSteps; ++st) {
+      if (t < 4) applyLeadershipLane(S, st, t, sr, dr, src, dst);
+      chainSync();
+    }
+    if (t == 0) applyLeadershipFinish(S, p, dr, dpos, src, dst);
+  } else {
+    const bool lead = (rr.flags & RF_LEADER) != 0;
+    const int lr = C.pLeader[p];
+    if (t < kReplicaLanes) applyReplicaLane(S, t, r, src, dst, lr, lead);
+    chainSync();
+    if (t == 0) applyReplicaFinish(S, r, src, dst, lead);
+  }
+  chainSync();
+}
+__device__ __forceinline__ void chainApplyAny(const ChainTables& C, LoadVec* sc, int action, int r, int dst) {
+  switch (C.W) {  // block-uniform
+    case 1: chainApply<1>(C, sc, action, r, dst); break;
+    case 2: chainApply<2>(C, sc, action, r, dst); break;
+    case 3: chainApply<3>(C, sc, action, r, dst); break;
+    case 4: chainApply<4>(C, sc, action, r, dst); break;
+    default: chainApply<5>(C, sc, action, r, dst); break;
+  }
 }
 
 // First accepted pair q in [start, n) on the current state (kNone if none), block-uniform.
@@ -711,9 +749,10 @@ __global__ __launch_bounds__(kBlock) void chain_pairs(DevTables T, ChainTables C
                                                       const int32_t* __restrict__ next, int n, int maxAccepts,
                                                       int32_t* __restrict__ log, ChainResultDev* __restrict__ out) {
   __shared__ OverlayLds ov;
+  __shared__ alignas(8) unsigned char scRaw[2 * sizeof(LoadVec)];  // LoadVec has a member initializer
+  LoadVec* sc = reinterpret_cast<LoadVec*>(scRaw);
   if (threadIdx.x == 0) ov.nb = ov.nr = ov.np = 0;
   __syncthreads();
-  DevApply S{C, C.W};
   int start = 0, acc = 0;
   unsigned long long visited = 0;
   while (start < n && acc < maxAccepts) {
@@ -724,14 +763,9 @@ __global__ __launch_bounds__(kBlock) void chain_pairs(DevTables T, ChainTables C
     }
     visited += best - (unsigned long long)start + 1;
     const int q = (int)best;
-    if (threadIdx.x == 0) {
-      log[acc] = q;
-      const ReplicaRec& rr = C.replicas[pr[q]];
-      if (prog.action == DA_LEADERSHIP) applyRelocateLeadership(S, rr.part, rr.broker, pb[q]);
-      else applyRelocateReplica(S, pr[q], pb[q]);
-    }
+    if (threadIdx.x == 0) log[acc] = q;
+    chainApplyAny(C, sc, prog.action, pr[q], pb[q]);
     ++acc;
-    chainSync();
     start = next[q];
   }
   if (threadIdx.x == 0) {
@@ -750,9 +784,10 @@ __global__ __launch_bounds__(kBlock) void chain_rack_rows(DevTables T, ChainTabl
                                                           const int32_t* __restrict__ cands, int N,
                                                           int32_t* __restrict__ log, ChainResultDev* __restrict__ out) {
   __shared__ OverlayLds ov;
+  __shared__ alignas(8) unsigned char scRaw[2 * sizeof(LoadVec)];  // LoadVec has a member initializer
+  LoadVec* sc = reinterpret_cast<LoadVec*>(scRaw);
   if (threadIdx.x == 0) ov.nb = ov.nr = ov.np = 0;
   __syncthreads();
-  DevApply S{C, C.W};
   int acc = 0;
   unsigned long long fail = 0;
   for (int k = 0; k < n; ++k) {
@@ -788,10 +823,9 @@ __global__ __launch_bounds__(kBlock) void chain_rack_rows(DevTables T, ChainTabl
     if (threadIdx.x == 0) {
       log[2 * acc] = k;
       log[2 * acc + 1] = (int)best;
-      applyRelocateReplica(S, r, cands[best]);
     }
+    chainApplyAny(C, sc, DA_MOVE, r, cands[best]);
     ++acc;
-    chainSync();
   }
   if (threadIdx.x == 0) {
     out->accepts = (unsigned long long)acc;

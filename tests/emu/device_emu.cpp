@@ -273,6 +273,8 @@ struct EmuApply {
       x.leadNwOut = e.pLeadNwOut[p];
     }
   }
+  LoadVec sc[2];
+  LoadVec& scratch(int i) { return sc[i]; }
   LoadVec& rLoad(int r) { return e.lRep[r]; }
   LoadVec& bLoad(int b) { return e.lBrk[b]; }
   LoadVec& bLnw(int b) { return e.lLnw[b]; }
