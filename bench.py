@@ -3,33 +3,40 @@
 Workload (default, BASELINE.json configs[2] — the configuration the metric is quoted on, and it fits one GPU):
 RandomCluster C2 = 100 racks, 10 000 brokers, 999 999 + 20 000 replicas (R = 1 019 999), 10 001 topics, W = 1,
 uniform loads, TestConstants seeds; the 16 default goals in default priority order; default BalancingConstraint.
---workload c1 / c0 / c2_c1goals select the other BASELINE configs (parity-test cases, not headline lines).
+--workload c1 / c3 / c2_c1goals / c0 select the other BASELINE configs (parity-test cases, not headline lines).
 
 A "step" is one full GoalOptimizer.optimizations over that cluster (every goal, ClusterModelStats after every goal,
 final ExecutionProposals). Each step works on its own device session, uploaded to HBM before the timed region
-starts; the step count K therefore means K independent proposal computations per GPU.
+starts (the session upload — the ClusterModel the caller hands over — is outside the timed region, as the reference
+does not time model building either; its time is reported as session_upload_s); K steps = K independent proposals.
 
 value = reference-equivalent candidate moves evaluated/s summed over all ranks (the candidates the reference's
-first-fit loops would visit), ms_per_step = step wall time = proposal wall time at the default
+first-fit loops visit), ms_per_step = step wall time = proposal wall time at the default
 --requests-per-gpu 1. --requests-per-gpu S runs S independent what-if proposals concurrently per GPU in every step
 (one host thread + HIP stream per session, GoalOptimizer's precompute pool); proposal_wall_s is then the mean
 per-proposal latency.
+
+Parity: the first timed proposal is checked against the committed oracle golden of the workload (tests/golden/:
+action log, final assignment and leaders, per-goal results, every goal's stats within 1e-9) -> "parity".
 
 Multi-GPU (torchrun, one process per GPU): by default every rank runs its own independent what-if proposal
 request (weak scaling, no data-path collective); timing is max over ranks. --sharded instead shards ONE proposal's
 candidate space by destination broker over the ranks (one RCCL MIN allreduce per scan, strong scaling).
 
-Roofline: the dominant kernel is the candidate scan. Its HIP-event duration is measured during the warmup
-proposal(s) (events on the engine stream, outside the timed region); algorithmic bytes = 96 B per
-reference-equivalent candidate. traffic = HBM bytes per scan launch from the committed rocprofv3
-PMC summary of this workload. cpu_baseline = the single-threaded C++ restatement (oracle/, "port") on rank 0 at
-N = 1: the whole chain for C0/C1, a goal-prefix sample of the chain for C2.
+Roofline: the dominant kernels are the candidate scans (scan_cross / scan_pairs / scan_swap / chain_pairs /
+chain_rack_rows). Their HIP-event duration is measured during the warmup proposal(s) (events on the engine stream,
+outside the timed region); algorithmic bytes = 96 B per candidate the launches had to evaluate (every device list up
+to its winner: ccmi_perf_counters.scan_required). traffic = HBM bytes per scan launch from the
+committed rocprofv3 PMC summary of this workload. cpu_baseline = the single-threaded C++ restatement (oracle/,
+"port") on rank 0 at N = 1 (see cpu_baseline()).
 """
 from __future__ import annotations
 
 import argparse
+import hashlib
 import json
 import os
+import struct
 import sys
 import time
 
@@ -53,38 +60,151 @@ WORKLOADS = {"c1": (C1_PROPS, C1_GOALS, "C1: 1K brokers x 100K replicas, 5 distr
 # Per-workload OptimizationOptions (C3: the 7-arg options RemoveBrokersRunnable.java:107-126 builds)
 WORKLOAD_OPTIONS = {"c3": lambda: ccmi.OptimizationOptions(requested_destination_broker_ids=list(range(500, 1500)),
                                                            fast_mode=False)}
+# committed oracle goldens of the workloads (tests/golden/make_golden.py)
+WORKLOAD_GOLDEN = {"c1": "c1", "c2": "c2_default", "c2_c1goals": "c2_c1goals", "c3": "c3_default"}
 BYTES_PER_CANDIDATE = 96
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E (MI355X_MICROARCH.md)
+# candidate-heavy C2 goal the CPU baseline samples on the box (the reference's costliest goal at C2)
+C2_SAMPLE_GOAL = "CpuUsageDistributionGoal"
 
 
-# CPU-baseline sample of the C2 workload: the first goals of the default chain on the same C2 cluster (the whole
-# chain takes the single-threaded restatement about an hour: every goal pays ~30 s of ClusterModelStats over the
-# T x B topic-replica counts at C2; the first goal alone is ~30 s of CPU work).
-C2_CPU_SAMPLE_GOALS = 1
+def _sha(ints):
+    return hashlib.sha256(struct.pack(f"<{len(ints)}q", *ints)).hexdigest()
 
 
-def cpu_baseline(buf, workload: str, goal_names) -> dict:
-    """The oracle restatement (oracle/, "port"), single thread, on rank 0 at N=1: the whole chain for C0/C1, a
-    goal-prefix sample of the chain for C2 (same cluster, same constraint)."""
+def check_parity(workload: str, cm, result) -> dict:
+    """The first timed proposal against the workload's committed oracle golden."""
+    name = WORKLOAD_GOLDEN.get(workload)
+    path = os.path.join(REPO, "tests", "golden", f"{name}.json") if name else None
+    if not path or not os.path.exists(path):
+        return {"golden": None, "status": "no golden for this workload"}
+    with open(path) as f:
+        g = json.load(f)
+    problems = []
+    acts = cm.actions()
+    if len(acts) != g["num_actions"]:
+        problems.append(f"{len(acts)} actions vs {g['num_actions']}")
+    if _sha([x for a in acts for x in a]) != g["actions_sha256"]:
+        problems.append("action log")
+    if _sha(cm.replica_distribution()) != g["replica_distribution_sha256"]:
+        problems.append("replica distribution")
+    if _sha(cm.leader_distribution()) != g["leader_distribution_sha256"]:
+        problems.append("leader distribution")
+    worst = 0.0
+    for r, e in zip(result.goal_results, g["goals_result"]):
+        if (r.name, r.succeeded, r.candidates, r.actions) != (e["name"], e["succeeded"], e["candidates"], e["actions"]):
+            problems.append(f"goal {r.name}")
+        for k, v in (e.get("stats") or {}).items():
+            got = r.stats[k]
+            for x, y in zip(got if isinstance(got, list) else [got], v if isinstance(v, list) else [v]):
+                if x != y:
+                    rel = abs(x - y) / max(abs(y), 1e-300)
+                    if abs(x - y) > 1e-12 and rel > worst:
+                        worst = rel
+    if worst > 1e-9:
+        problems.append(f"stats rel {worst:.2e}")
+    return {"golden": os.path.relpath(path, REPO), "status": "ok" if not problems else "MISMATCH: " + ", ".join(problems),
+            "actions": len(acts), "max_stats_rel_diff": worst,
+            "checked": "action log + final assignment + leaders (SHA-256), per-goal (name, succeeded, candidates, "
+                       "actions), every goal's ClusterModelStats within 1e-9 relative"}
+
+
+def _cpu_model() -> str:
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def _c1_chain_procs(n: int):
+    """n independent what-if proposals of the C1 chain in the restatement, one child process each
+    (tools/cpu_whatif.py); returns [(candidates, seconds)] and the wall time of the whole batch."""
+    import subprocess
+    cmd = [sys.executable, os.path.join(REPO, "tools", "cpu_whatif.py"), json.dumps(C1_PROPS), json.dumps(C1_GOALS)]
+    t0 = time.perf_counter()
+    procs = [subprocess.Popen(cmd, stdout=subprocess.PIPE, text=True) for _ in range(n)]
+    outs = [json.loads(p.communicate()[0]) for p in procs]
+    wall = time.perf_counter() - t0
+    if any(p.returncode for p in procs):
+        raise RuntimeError("a CPU what-if worker failed")
+    return [(o["candidates"], o["seconds"]) for o in outs], wall
+
+
+def cpu_baseline(lib, buf, workload: str, goal_names, options, gpu_result, device: int, sample_s: float,
+                 what_if_procs: int) -> dict:
+    """The oracle restatement (oracle/, "port"), single thread, on the GPU box's host cores (rank 0, N = 1):
+
+    * value — a bounded sample of THIS workload: the restatement runs `C2_SAMPLE_GOAL` (the costliest goal) on the
+      same cluster for `sample_s` seconds of wall time (its ClusterModelStats calls included, as in the reference);
+      the GPU runs the same single-goal optimization to completion beside it (gpu_same_sample).
+    * c1_chain — the whole C1 chain (BASELINE configs[1]), 1 thread, next to the GPU's C1 chain.
+    * what_if_all_cores — `what_if_procs` independent C1 proposals at once, one process each (the reference's
+      precompute pool with num.proposal.precompute.threads = what_if_procs).
+    * per_goal_full_chain — the whole chain's per-goal restatement seconds from the committed golden (measured in
+      the build container when the golden was generated) beside this run's per-goal GPU seconds.
+    """
     sys.path.insert(0, os.path.join(REPO, "tests"))
     from oracle_binding import OracleCluster
-
-    goals = list(goal_names) if workload in ("c0", "c1") else list(goal_names)[:C2_CPU_SAMPLE_GOALS]
+    out = {"unit": "candidate moves evaluated/s", "cores": 1, "kind": "port",
+           "nproc": os.cpu_count(), "cpu_share": len(os.sched_getaffinity(0)), "cpu_model": _cpu_model(),
+           "num.proposal.precompute.threads": 1}
+    # (1) bounded sample of the same workload
+    goal = C2_SAMPLE_GOAL if workload in ("c2", "c3", "c2_c1goals") else goal_names[0]
     oc = OracleCluster.from_desc(buf.desc)
     t0 = time.perf_counter()
-    opts = WORKLOAD_OPTIONS[workload]() if workload in WORKLOAD_OPTIONS else None
-    res = oc.optimize(goals, ccmi.BalancingConstraint(), opts)
+    done, cands, stats_s = oc.optimize_until([goal], sample_s, ccmi.BalancingConstraint(), options)
     dt = time.perf_counter() - t0
-    cands = sum(r.candidates for r in res)
-    what = "one full optimizations()" if len(goals) == len(goal_names) else \
-        f"optimizations() over the first {len(goals)} goals of the chain ({goals[0]} .. {goals[-1]})"
-    return {"value": cands / dt, "unit": "candidate moves evaluated/s", "cores": 1, "kind": "port",
-            "sample": f"{what} of the {workload.upper()} workload: {cands} candidates, {len(oc.actions())} actions in "
-                      f"{dt:.2f} s by the single-threaded C++ restatement (oracle/)",
-            "goals": goals, "wall_s": dt}
+    del oc
+    s = ccmi.ClusterModel.from_buffers(buf, device=device)
+    r = ccmi.GoalOptimizer(ccmi.BalancingConstraint()).optimizations(s, ccmi.goals_from_names([goal]), options)
+    del s
+    out["value"] = cands / dt
+    out["sample"] = (f"{goal} alone on the {workload.upper()} cluster, restatement stopped after {dt:.1f} s "
+                     f"({'completed' if done else 'deadline'}): {cands} candidates, {stats_s:.1f} s of it in "
+                     f"ClusterModelStats")
+    out["sample_loop_rate"] = cands / max(1e-9, dt - stats_s)
+    out["gpu_same_sample"] = {"goal": goal, "seconds": r.seconds, "candidates": r.candidates,
+                              "value": r.candidates / r.seconds}
+    # (2) the whole C1 chain, 1 thread, and the GPU's C1 chain
+    ((c1c, c1t),), _ = _c1_chain_procs(1)
+    b1 = ccmi.RandomCluster.generate(lib, **C1_PROPS)
+    s1 = ccmi.ClusterModel.from_buffers(b1, device=device)
+    r1 = ccmi.GoalOptimizer(ccmi.BalancingConstraint()).optimizations(s1, ccmi.goals_from_names(C1_GOALS))
+    del s1
+    out["c1_chain"] = {"restatement_s": c1t, "candidates": c1c, "restatement_value": c1c / c1t,
+                       "gpu_s": r1.seconds, "gpu_value": r1.candidates / r1.seconds}
+    # (3) independent what-if proposals on all host cores of this box's share
+    n = max(1, min(what_if_procs, out["cpu_share"]))
+    rs, wall = _c1_chain_procs(n)
+    out["what_if_all_cores"] = {"processes": n, "proposals": n, "batch_wall_s": wall,
+                                "slowest_proposal_s": max(t for _, t in rs),
+                                "value": sum(c for c, _ in rs) / max(t for _, t in rs),
+                                "workload": "C1 chain per process (num.proposal.precompute.threads = processes)"}
+    # (4) per-goal full-chain restatement seconds (golden) beside the GPU's
+    name = WORKLOAD_GOLDEN.get(workload)
+    path = os.path.join(REPO, "tests", "golden", f"{name}.json") if name else None
+    if path and os.path.exists(path):
+        with open(path) as f:
+            g = json.load(f)
+        rows = []
+        for e, rr in zip(g["goals_result"], gpu_result.goal_results):
+            if "seconds" in e:
+                rows.append({"goal": e["name"], "candidates": e["candidates"], "restatement_s": round(e["seconds"], 3),
+                             "gpu_s": round(rr.seconds, 4)})
+        if rows:
+            tot = sum(x["restatement_s"] for x in rows)
+            out["per_goal_full_chain"] = {
+                "source": f"{os.path.relpath(path, REPO)} (restatement timed in the build container, 1 thread)",
+                "restatement_total_s": tot, "gpu_total_s": sum(x["gpu_s"] for x in rows),
+                "restatement_value": sum(x["candidates"] for x in rows) / tot, "goals": rows}
+    return out
 
 
-SCAN_KERNELS = ("scan_cross", "scan_pairs", "scan_swap")
+SCAN_KERNELS = ("scan_cross", "scan_pairs", "scan_swap", "chain_pairs", "chain_rack_rows")
 
 
 def pmc_traffic(workload: str):
@@ -108,6 +228,8 @@ def main() -> None:
     ap.add_argument("--steps", type=int, default=2)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-sample-seconds", type=float, default=25.0)
+    ap.add_argument("--what-if-procs", type=int, default=16)
     ap.add_argument("--workload", choices=sorted(WORKLOADS), default="c2")
     ap.add_argument("--requests-per-gpu", type=int, default=1,
                     help="S concurrent what-if proposals per GPU in every step (one host thread + HIP stream per "
@@ -161,7 +283,9 @@ def main() -> None:
 
     S = max(1, args.requests_per_gpu) if not sharded else 1
     # cluster resident in HBM before timing starts: one session per proposal
+    t_up = time.perf_counter()
     sessions = [[session() for _ in range(S)] for _ in range(args.steps)]
+    upload_s = (time.perf_counter() - t_up) / max(1, args.steps * S)
     pool = None
     if S > 1:
         from concurrent.futures import ThreadPoolExecutor  # ctypes drops the GIL inside ccmi_optimizations
@@ -194,14 +318,16 @@ def main() -> None:
             cands = float(sum(r.candidates for r in results))
 
     perf = inst_perf
-    scan_avg_ms = perf.scan_kernel_ms / max(1, perf.scan_launches)
-    ref_bytes_per_launch = inst_cands * BYTES_PER_CANDIDATE / max(1, perf.scan_launches)
-    achieved = ref_bytes_per_launch / (scan_avg_ms * 1e-3) / 1e9 if scan_avg_ms > 0 else 0.0
+    launches = max(1, perf.scan_launches)
+    scan_avg_ms = perf.scan_kernel_ms / launches
+    required_bytes_per_launch = perf.scan_required * BYTES_PER_CANDIDATE / launches
+    achieved = required_bytes_per_launch / (scan_avg_ms * 1e-3) / 1e9 if scan_avg_ms > 0 else 0.0
 
     if rank != 0:
         dist.destroy_process_group()
         return
     first = results[0]
+    parity = check_parity(args.workload, sessions[0][0], first)
     traffic, traffic_src = pmc_traffic(args.workload)
     line = {
         "metric": "candidate moves evaluated/s + proposal wall time, 10K brokers/1M replicas",
@@ -221,24 +347,32 @@ def main() -> None:
                    "partitions": buf.desc.num_partitions, "topics": buf.desc.num_topics,
                    "goals": goal_names, "parallelism": (f"destination-sharded x{world} (RCCL MIN allreduce per scan)" if sharded
                                    else f"independent what-if per GPU x{world}")},
+        "parity": parity,
         "requests_per_gpu": S,
         "proposal_wall_s": sum(r.seconds for r in results) / len(results),
+        "session_upload_s": upload_s,
+        "timed_region": "GoalOptimizer.optimizations on sessions already resident in HBM (upload excluded)",
         "candidates_per_step": first.candidates,
         "actions_per_step": len(first.actions),
         "proposals_per_step": len(first.proposals),
+        "per_goal_gpu_s": {g.name: round(g.seconds, 4) for g in first.goal_results},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_unit": "HBM bytes per scan launch",
                      "traffic_source": traffic_src,
-                     "kernel": "scan (scan_cross/scan_pairs/scan_swap)", "avg_launch_us": scan_avg_ms * 1e3,
-                     "launches_per_step": perf.scan_launches,
-                     "algorithmic_bytes_per_launch": ref_bytes_per_launch,
+                     "kernel": "candidate scans (scan_cross/scan_pairs/scan_swap/chain_pairs/chain_rack_rows)",
+                     "avg_launch_us": scan_avg_ms * 1e3,
+                     "launches_per_step": perf.scan_launches, "chain_launches_per_step": perf.chain_launches,
+                     "algorithmic_bytes_per_launch": required_bytes_per_launch,
+                     "required_candidates_per_step": perf.scan_required,
+                     "reference_equivalent_candidates_per_step": inst_cands,
                      "stats_avg_launch_us": perf.stats_kernel_ms * 1e3 / max(1, perf.stats_launches),
                      "stats_bytes_per_launch": perf.stats_bytes / max(1, perf.stats_launches),
                      "host_syncs_per_step": perf.host_syncs},
         "cpu_baseline": None,
     }
     if world == 1 and not args.no_cpu_baseline:
-        line["cpu_baseline"] = cpu_baseline(buf, args.workload, goal_names)
+        line["cpu_baseline"] = cpu_baseline(lib, buf, args.workload, goal_names, options, first, device,
+                                            args.cpu_sample_seconds, args.what_if_procs)
     print(json.dumps(line))
     if world > 1:
         dist.destroy_process_group()

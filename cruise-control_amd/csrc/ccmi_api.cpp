@@ -396,6 +396,8 @@ ccmi_status ccmi_perf(const ccmi_session* s, ccmi_perf_counters* out) {
     out->stats_kernel_ms = p.statsKernelMs;
     out->stats_bytes = p.statsBytes;
     out->host_syncs = p.syncs;
+    out->scan_required = p.scanRequired;
+    out->chain_launches = p.chainLaunches;
     return CCMI_OK;
   });
 }

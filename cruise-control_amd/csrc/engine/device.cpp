@@ -443,7 +443,10 @@ int64_t Device::scanCross(const DevProgram& prog, const int32_t* reps, int K, co
   perf.scanLaunches++;
   perf.scanPairs += (int64_t)K * Nr;
   perf.scanBytes += (int64_t)K * Nr * kBytesPerCandidate;
-  return finishScan();
+  const int64_t key = finishScan();
+  // candidates this launch had to evaluate: every row before the winner's and the winner's row up to the winner
+  perf.scanRequired += key < 0 ? (int64_t)K * Nr : (key / N) * Nr + (key % N - c0) + 1;
+  return key;
 }
 
 int64_t Device::scanSwap(const DevProgram& prog, const int32_t* srcs, int S, const int32_t* cbOff, int M,
@@ -476,6 +479,7 @@ int64_t Device::scanSwap(const DevProgram& prog, const int32_t* srcs, int S, con
   (void)finishScan();
   const unsigned long long best = hResult_[1];
   *visited = (int64_t)hResult_[2];
+  perf.scanRequired += *visited;
   return best == ~0ull ? -1 : (int64_t)best;
 }
 
@@ -502,7 +506,9 @@ int64_t Device::scanPairs(const DevProgram& prog, const int32_t* pr, const int32
   perf.scanLaunches++;
   perf.scanPairs += n;
   perf.scanBytes += (int64_t)n * kBytesPerCandidate;
-  return finishScan();
+  const int64_t key = finishScan();
+  perf.scanRequired += key < 0 ? (int64_t)n : key - p0 + 1;
+  return key;
 }
 
 void Device::stats(const StatsParams& P, const uint8_t* allowedAliveHost, StatsOut* out) {
@@ -631,6 +637,7 @@ Device::ChainResult Device::chainPairs(const DevProgram& prog, const int32_t* pr
   perf.scanLaunches++;
   perf.chainLaunches++;
   perf.scanPairs += (int64_t)out.visited;
+  perf.scanRequired += (int64_t)out.visited;
   if (timing) {
     float ms = 0.f;
     hipCheck(hipEventElapsedTime(&ms, EV0, EV1), "hipEventElapsedTime");
@@ -686,6 +693,10 @@ Device::ChainResult Device::chainRackRows(const DevProgram& prog, const int32_t*
   log.resize((size_t)res.accepts * 2);
   if (res.accepts)
     hipCheck(hipMemcpy(log.data(), dChainLog_, sizeof(int32_t) * 2 * res.accepts, hipMemcpyDeviceToHost), "chain log");
+  int64_t evaluated = res.failRow ? N : 0;
+  for (size_t i = 1; i < log.size(); i += 2) evaluated += log[i] + 1;
+  perf.scanPairs += evaluated;
+  perf.scanRequired += evaluated;
   return res;
 }
 

@@ -32,6 +32,7 @@ struct DevicePerf {
   int64_t syncs = 0;
   int64_t singleLaunch = 0;  // scans that applied their rows in-kernel and read the request from host memory
   int64_t chainLaunches = 0; // K7 chains (several decisions per launch)
+  int64_t scanRequired = 0;  // candidates the launches had to evaluate: each first-fit list up to its winner
 };
 
 class Device {

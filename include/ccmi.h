@@ -291,6 +291,10 @@ typedef struct ccmi_perf_counters {
   double stats_kernel_ms;
   int64_t stats_bytes;
   int64_t host_syncs;
+  int64_t scan_required;       /* candidates the scans had to evaluate: every device list up to its winner (the
+                                  algorithmic work; smaller than `candidates` where the engine never sends rows that
+                                  cannot be accepted, e.g. non-legit leadership rows) */
+  int64_t chain_launches;      /* K7 chain launches (several decisions applied on the device per launch) */
 } ccmi_perf_counters;
 ccmi_status ccmi_perf(const ccmi_session* s, ccmi_perf_counters* out);
 void ccmi_perf_reset(ccmi_session* s);

@@ -142,7 +142,7 @@ int AbstractGoal::maybeApplyBalancingAction(ClusterModel& cm, int replica, const
                                             ActionType action, const GoalList& g, const OptimizationOptions& o) {
   std::vector<int> eligible = eligibleBrokers(cm, replica, candidates, action, o);
   for (int b : eligible) {
-    cm.candidatesEvaluated++;
+    cm.countCandidate();
     BalancingAction proposal{cm.replicas[replica].partition, cm.replicas[replica].broker, b, action, -1};
     if (!legitMove(cm, replica, b, action)) continue;
     if (!selfSatisfied(cm, proposal)) continue;
@@ -176,7 +176,7 @@ int AbstractGoal::maybeApplySwapAction(ClusterModel& cm, int src, const std::vec
     return -1;
   }
   for (int dr : candidates) {
-    cm.candidatesEvaluated++;
+    cm.countCandidate();
     BalancingAction swap{sr.partition, srcBroker, destBroker, ActionType::INTER_BROKER_REPLICA_SWAP,
                          cm.replicas[dr].partition};
     if (!legitMove(cm, src, destBroker, ActionType::INTER_BROKER_REPLICA_MOVEMENT)) return -1;

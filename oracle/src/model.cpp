@@ -7,6 +7,8 @@
 //   ModelUtils.getFollowerCpuUtilFromLeaderLoad             ModelUtils.java:64-80 (weights 0.7/0.15/0.15)
 #include "model.h"
 
+#include <chrono>
+
 #include <algorithm>
 #include <stdexcept>
 
@@ -514,6 +516,11 @@ bool ClusterModel::relocateLeadership(int p, int src, int dst) {
   part.leader = dr;
   if (recordActions) actionLog.push_back({(int)ActionType::LEADERSHIP_MOVEMENT, p, src, dst, -1});
   return true;
+}
+
+void ClusterModel::checkDeadline() const {
+  const double now = std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+  if (now > deadline) throw DeadlineReached();
 }
 
 }  // namespace oracle

@@ -157,6 +157,10 @@ struct Partition {
   std::unordered_set<int> ineligibleBrokers;
 };
 
+struct DeadlineReached : std::exception {
+  const char* what() const noexcept override { return "deadline reached"; }
+};
+
 class ClusterModel;
 
 // SortedReplicas selection / priority / score functions (ReplicaSortFunctionFactory.java)
@@ -264,6 +268,14 @@ class ClusterModel {
   bool recordActions = true;
   // instrumentation: reference-equivalent candidate evaluations
   int64_t candidatesEvaluated = 0;
+  // CPU-baseline sampling (bench.py): stop the optimization at a wall-clock deadline (steady clock, seconds) and
+  // account the time spent in ClusterModelStats separately. 0 = no deadline.
+  double deadline = 0;
+  mutable double statsSeconds = 0;
+  void countCandidate() {
+    if ((++candidatesEvaluated & 4095) == 0 && deadline > 0) checkDeadline();
+  }
+  void checkDeadline() const;
 
   // --- construction (ClusterModel.createRack/createBroker/createReplica/setReplicaLoad)
   int createRack(const std::string& id);

@@ -239,6 +239,9 @@ int oc_optimize(void* hv, const int32_t* goals, int n, const ccmi_balancing_cons
       toCStats(g.stats, &r.stats);
     }
     return 0;
+  } catch (DeadlineReached&) {
+    h->err = "deadline reached";
+    return 99;
   } catch (OptimizationFailure& e) {
     h->err = e.what();
     return CCMI_E_OPT_FAILURE;
@@ -251,6 +254,13 @@ int oc_optimize(void* hv, const int32_t* goals, int n, const ccmi_balancing_cons
   }
 }
 const char* oc_error(void* hv) { return ((Handle*)hv)->err.c_str(); }
+// CPU-baseline sampling: the next oc_optimize stops (status 99) once `seconds` of wall time have passed
+void oc_set_deadline(void* hv, double seconds) {
+  auto* h = (Handle*)hv;
+  const double now = std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+  h->cm.deadline = seconds > 0 ? now + seconds : 0;
+}
+double oc_stats_seconds(void* hv) { return ((Handle*)hv)->cm.statsSeconds; }
 double oc_last_seconds(void* hv) { return ((Handle*)hv)->last.seconds; }
 int64_t oc_candidates(void* hv) { return ((Handle*)hv)->cm.candidatesEvaluated; }
 

@@ -5,6 +5,8 @@
 // topic AVG/ST_DEV sums (parity for stats is 1e-9 relative, BASELINE.json north_star).
 #include "stats.h"
 
+#include <chrono>
+
 #include <climits>
 #include <cmath>
 
@@ -26,7 +28,16 @@ double computeResourceUtilizationBalanceThreshold(double avg, int resource, cons
   return thr;
 }
 
+namespace {
+struct StatsTimer {  // ClusterModel::statsSeconds += the time of one ClusterModelStats.populate
+  const ClusterModel& cm;
+  std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now();
+  ~StatsTimer() { cm.statsSeconds += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count(); }
+};
+}  // namespace
+
 ClusterModelStats computeStats(const ClusterModel& cm, const BalancingConstraint& bc, const OptimizationOptions& o) {
+  StatsTimer timer{cm};
   ClusterModelStats s{};
   const int B = (int)cm.brokers.size();
   std::vector<int> alive = cm.aliveBrokers();

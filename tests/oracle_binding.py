@@ -66,6 +66,9 @@ class Oracle:
             L.oc_java_random_probe.restype = C.c_int64
             L.oc_java_random_probe.argtypes = [C.c_int64, C.c_int, C.c_int, C.POINTER(C.c_int32),
                                                C.POINTER(C.c_double)]
+            L.oc_set_deadline.argtypes = [C.c_void_p, C.c_double]
+            L.oc_stats_seconds.restype = C.c_double
+            L.oc_stats_seconds.argtypes = [C.c_void_p]
             L.oc_balance_threshold.restype = C.c_double
             L.oc_balance_threshold.argtypes = [C.c_double, C.c_int, C.c_double, C.c_double, C.c_double, C.c_int,
                                                C.c_double, C.c_int]
@@ -130,6 +133,20 @@ class OracleCluster:
 
     def seconds(self) -> float:
         return self.L.oc_last_seconds(self.h)
+
+    def optimize_until(self, goal_names: List[str], seconds: float, constraint=None, options=None):
+        """CPU-baseline sample: run the chain until `seconds` of wall time have passed (or it completes).
+        Returns (completed, candidates evaluated, seconds spent in ClusterModelStats)."""
+        kinds = (C.c_int32 * len(goal_names))(*[ccmi.GOAL_KINDS[n] for n in goal_names])
+        res = (ccmi.GoalResultStruct * len(goal_names))()
+        o, keep = (options or ccmi.OptimizationOptions()).to_struct()
+        c = (constraint or ccmi.BalancingConstraint()).to_struct()
+        self.L.oc_set_deadline(self.h, seconds)
+        st = self.L.oc_optimize(self.h, kinds, len(goal_names), C.byref(c), C.byref(o), res)
+        self.L.oc_set_deadline(self.h, 0.0)
+        if st not in (0, 99):
+            raise ccmi._STATUS.get(st, RuntimeError)(self.L.oc_error(self.h).decode())
+        return st == 0, self.L.oc_candidates(self.h), self.L.oc_stats_seconds(self.h)
 
     def actions(self) -> List[tuple]:
         n = self.L.oc_action_count(self.h)

@@ -27,19 +27,30 @@ def constraint(balance, max_replicas=None):
     return bc
 
 
-def run_product(lib, props, goals, balance, device=0, max_replicas=None):
+def run_product(lib, props, goals, balance, device=0, max_replicas=None, options=None):
     buf = ccmi.RandomCluster.generate(lib, **props)
     cm = ccmi.ClusterModel.from_buffers(buf, device=device)
-    res = ccmi.GoalOptimizer(constraint(balance, max_replicas)).optimizations(cm, ccmi.goals_from_names(goals))
+    res = ccmi.GoalOptimizer(constraint(balance, max_replicas)).optimizations(cm, ccmi.goals_from_names(goals),
+                                                                               options)
     return buf, cm, res
 
 
-def check_product_against_golden(lib, name):
+def golden_options(g):
+    return ccmi.OptimizationOptions(**g["options"]) if g.get("options") else None
+
+
+def check_product_against_golden(lib, name, per_goal_stats=False):
+    """The product on a golden case: action log, assignment, leaders, per-goal (name, succeeded, candidates,
+    actions) and final stats; with per_goal_stats every goal's ClusterModelStats (goldens that store them)."""
     g = golden(name)
     buf, cm, res = run_product(lib, g["props"], g["goals"], g["resource_balance_percentage"],
-                               max_replicas=g.get("max_replicas_per_broker"))
+                               max_replicas=g.get("max_replicas_per_broker"), options=golden_options(g))
     check_against_golden(g, cm.actions(), cm.replica_distribution(), cm.leader_distribution(), res.goal_results,
                          res.goal_results[-1].stats)
+    if per_goal_stats:
+        for r, e in zip(res.goal_results, g["goals_result"]):
+            if "stats" in e:
+                compare_stats(r.stats, e["stats"])
     return cm, res
 
 

@@ -21,6 +21,14 @@ def test_gpu_matches_golden(gpu_lib, oracle_lib, name):
     assert cm.perf().scan_launches > 0
 
 
+# The headline configurations (BASELINE configs[2] and [3]) and C2 with the C1 goal chain, against committed oracle
+# goldens (tests/golden/make_golden.py: c2_c1goals, c2_default, c3_default; the oracle needs about an hour for each).
+@pytest.mark.parametrize("name", ["c2_c1goals", "c2_default", "c3_default"])
+def test_gpu_matches_headline_golden(gpu_lib, name):
+    cm, res = check_product_against_golden(gpu_lib, name, per_goal_stats=True)
+    assert cm.perf().scan_launches > 0
+
+
 @pytest.mark.parametrize("props,balance", [
     (dict(num_racks=2, num_brokers=4, num_replicas=300, num_topics=10), None),
     (dict(num_racks=3, num_brokers=7, num_replicas=1400, num_topics=40, min_replication=2, max_replication=2), 1.02),
