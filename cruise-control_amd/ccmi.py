@@ -58,8 +58,10 @@ DEFAULT_GOALS = ("RackAwareGoal", "MinTopicLeadersPerBrokerGoal", "ReplicaCapaci
 # config C1's chain
 C1_GOALS = ("ReplicaDistributionGoal", "DiskUsageDistributionGoal", "NetworkInboundUsageDistributionGoal",
             "NetworkOutboundUsageDistributionGoal", "CpuUsageDistributionGoal")
+# intra.broker.goals (AnalyzerConfig INTRA_BROKER_GOALS default, IntraBrokerRebalanceTest.java:105-106)
+INTRA_BROKER_GOALS = ("IntraBrokerDiskCapacityGoal", "IntraBrokerDiskUsageDistributionGoal")
 # Goals whose drivers are implemented in this build.
-IMPLEMENTED = DEFAULT_GOALS
+IMPLEMENTED = DEFAULT_GOALS + INTRA_BROKER_GOALS
 
 ACTION_TYPES = ("INTER_BROKER_REPLICA_MOVEMENT", "LEADERSHIP_MOVEMENT", "INTER_BROKER_REPLICA_SWAP",
                 "INTRA_BROKER_REPLICA_MOVEMENT", "INTRA_BROKER_REPLICA_SWAP")
@@ -77,7 +79,11 @@ class ClusterDesc(C.Structure):
                 ("partition_replicas", C.POINTER(C.c_int32)), ("num_replicas", C.c_int32),
                 ("replica_partition", C.POINTER(C.c_int32)), ("replica_broker", C.POINTER(C.c_int32)),
                 ("replica_is_leader", C.POINTER(C.c_uint8)), ("replica_offline", C.POINTER(C.c_uint8)),
-                ("replica_load", C.POINTER(C.c_float)), ("replica_load_order", C.POINTER(C.c_int32))]
+                ("replica_load", C.POINTER(C.c_float)), ("replica_load_order", C.POINTER(C.c_int32)),
+                ("num_disks", C.c_int32), ("disk_broker", C.POINTER(C.c_int32)),
+                ("disk_logdir", C.POINTER(C.c_char_p)), ("disk_capacity", C.POINTER(C.c_double)),
+                ("replica_disk", C.POINTER(C.c_int32)), ("num_disk_assignments", C.c_int32),
+                ("disk_assign_replica", C.POINTER(C.c_int32)), ("disk_assign_disk", C.POINTER(C.c_int32))]
 
 
 class ConstraintStruct(C.Structure):
@@ -103,7 +109,8 @@ class OptionsStruct(C.Structure):
 
 class ActionStruct(C.Structure):
     _fields_ = [("type", C.c_int32), ("partition", C.c_int32), ("source_broker", C.c_int32),
-                ("destination_broker", C.c_int32), ("destination_partition", C.c_int32)]
+                ("destination_broker", C.c_int32), ("destination_partition", C.c_int32),
+                ("source_disk", C.c_int32), ("destination_disk", C.c_int32)]
 
 
 class StatsStruct(C.Structure):
@@ -132,13 +139,15 @@ class RandomClusterProps(C.Structure):
                 ("num_brokers_with_bad_disk", C.c_int32), ("num_replicas", C.c_int32), ("num_topics", C.c_int32),
                 ("min_replication", C.c_int32), ("max_replication", C.c_int32), ("mean_cpu", C.c_double),
                 ("mean_disk", C.c_double), ("mean_nw_in", C.c_double), ("mean_nw_out", C.c_double),
-                ("distribution", C.c_int32), ("rack_aware", C.c_int32), ("leader_in_first_position", C.c_int32)]
+                ("distribution", C.c_int32), ("rack_aware", C.c_int32), ("leader_in_first_position", C.c_int32),
+                ("jbod", C.c_int32), ("num_logdirs", C.c_int32), ("logdir_capacity", C.c_double * 8)]
 
 
 class PerfStruct(C.Structure):
     _fields_ = [("scan_launches", C.c_int64), ("scan_kernel_ms", C.c_double), ("scan_bytes", C.c_int64),
                 ("stats_launches", C.c_int64), ("stats_kernel_ms", C.c_double), ("stats_bytes", C.c_int64),
-                ("host_syncs", C.c_int64), ("scan_required", C.c_int64), ("chain_launches", C.c_int64)]
+                ("host_syncs", C.c_int64), ("scan_required", C.c_int64), ("chain_launches", C.c_int64),
+                ("intra_launches", C.c_int64), ("intra_kernel_ms", C.c_double), ("intra_bytes", C.c_int64)]
 
 
 # ----------------------------------------------------------------------------------------------- errors
@@ -214,6 +223,8 @@ class Library:
         L.ccmi_proposal_count.restype = C.c_int64
         L.ccmi_proposal_count.argtypes = [C.c_void_p]
         L.ccmi_proposals.argtypes = [C.c_void_p, C.c_int32] + [C.POINTER(C.c_int32)] * 5
+        L.ccmi_proposal_disks.argtypes = [C.c_void_p, C.c_int32] + [C.POINTER(C.c_int32)] * 2
+        L.ccmi_replica_disks.argtypes = [C.c_void_p, C.POINTER(C.c_int32)]
         L.ccmi_perf.argtypes = [C.c_void_p, C.POINTER(PerfStruct)]
         L.ccmi_perf_reset.argtypes = [C.c_void_p]
         L.ccmi_set_kernel_timing.argtypes = [C.c_void_p, C.c_int32]
@@ -350,6 +361,8 @@ class ExecutionProposal:
     old_leader: int
     old_replicas: List[int]
     new_replicas: List[int]
+    old_disks: Optional[List[int]] = None  # logdir half of ReplicaPlacementInfo (disk indices; JBOD models)
+    new_disks: Optional[List[int]] = None
 
 
 @dataclass
@@ -415,6 +428,8 @@ class RandomCluster:
         d.update(overrides)
         p = RandomClusterProps()
         for k, v in d.items():
+            if k == "logdir_capacity":
+                v = (C.c_double * 8)(*(list(v) + [0.0] * (8 - len(v))))
             setattr(p, k, v)
         return p
 
@@ -458,14 +473,23 @@ class ClusterModelBuilder:
         self.rep_offline: List[int] = []
         self.rep_load: List[Optional[List[float]]] = []
         self.load_order: List[int] = []
+        self.disks: List[tuple] = []          # (broker, logdir, capacity) in creation order
+        self.disk_index: Dict[tuple, int] = {}
+        self.rep_disk: List[int] = []
 
     def create_rack(self, rack_id: str) -> None:
         self.rack_index.setdefault(str(self.mapper(str(rack_id))), len(self.rack_index))
 
-    def create_broker(self, rack_id: str, broker_id: int, capacity: Dict[str, float]) -> None:
+    def create_broker(self, rack_id: str, broker_id: int, capacity: Dict[str, float],
+                      disk_capacity_by_logdir: Optional[Dict[str, float]] = None) -> None:
+        """createBroker with a BrokerCapacityInfo; disk_capacity_by_logdir populates the replica placement over
+        disks (Broker.java:80-83; negative capacity = dead disk)."""
         self.create_rack(rack_id)
         self.brokers[broker_id] = (self.rack_index[str(self.mapper(str(rack_id)))],
                                    [float(capacity[r]) for r in RESOURCES])
+        for logdir, cap in (disk_capacity_by_logdir or {}).items():
+            self.disk_index[(broker_id, logdir)] = len(self.disks)
+            self.disks.append((broker_id, logdir, float(cap)))
 
     def _replica(self, broker_id: int, topic: str, partition: int) -> int:
         for r in self.part_list[self.parts[(topic, partition)]]:
@@ -474,7 +498,7 @@ class ClusterModelBuilder:
         raise IllegalArgumentException(f"no replica of {topic}-{partition} on broker {broker_id}")
 
     def create_replica(self, rack_id: str, broker_id: int, topic: str, partition: int, index: int, is_leader: bool,
-                       is_offline: bool = False) -> int:
+                       is_offline: bool = False, logdir: Optional[str] = None) -> int:
         if topic not in self.topic_index:
             self.topic_index[topic] = len(self.topics)
             self.topics.append(topic)
@@ -488,6 +512,9 @@ class ClusterModelBuilder:
         self.rep_leader.append(1 if is_leader else 0)
         self.rep_offline.append(1 if is_offline else 0)
         self.rep_load.append(None)
+        if logdir is not None and (broker_id, logdir) not in self.disk_index:
+            raise IllegalStateException(f"Missing disk information for disk {logdir} on broker {broker_id}")
+        self.rep_disk.append(self.disk_index[(broker_id, logdir)] if logdir is not None else -1)
         self.part_list[self.parts[key]].insert(index, r)
         return r
 
@@ -533,6 +560,12 @@ class FlatCluster:
             replica_is_leader=arr(C.c_uint8, bld.rep_leader), replica_offline=arr(C.c_uint8, bld.rep_offline),
             replica_load=arr(C.c_float, [x for r in range(R) for x in bld.rep_load[r] for _ in range(W)]),
             replica_load_order=arr(C.c_int32, bld.load_order))
+        D = len(bld.disks)
+        if D:
+            self.keep.update(disk_broker=arr(C.c_int32, [x[0] for x in bld.disks]),
+                             disk_logdir=arr(C.c_char_p, [x[1].encode() for x in bld.disks]),
+                             disk_capacity=arr(C.c_double, [x[2] for x in bld.disks]),
+                             replica_disk=arr(C.c_int32, bld.rep_disk))
         for (topic, num), p in bld.parts.items():
             self.keep["partition_topic"][p] = bld.topic_index[topic]
             self.keep["partition_number"][p] = num
@@ -544,8 +577,9 @@ class FlatCluster:
         d = ClusterDesc()
         d.num_windows, d.num_racks, d.num_brokers = W, len(bld.rack_index), B
         d.num_topics, d.num_partitions, d.num_replicas = T, P, R
+        d.num_disks = D
         for k, v in self.keep.items():
-            setattr(d, k, C.cast(v, type(getattr(d, k))) if k != "topic_names" else v)
+            setattr(d, k, C.cast(v, type(getattr(d, k))) if k not in ("topic_names", "disk_logdir") else v)
         self.desc = d
         self.topics = list(bld.topics)
         self.partitions = {p: key for key, p in bld.parts.items()}
@@ -587,8 +621,10 @@ class ClusterModel:
         return res
 
     def action_acceptance(self, optimized_goal_index: int, action_type: int, partition: int, source: int,
-                          destination: int, destination_partition: int = -1) -> str:
-        a = ActionStruct(action_type, partition, source, destination, destination_partition)
+                          destination: int, destination_partition: int = -1, source_disk: int = -1,
+                          destination_disk: int = -1) -> str:
+        a = ActionStruct(action_type, partition, source, destination, destination_partition, source_disk,
+                         destination_disk)
         out = C.c_int32()
         self.lib.check(self.lib.lib.ccmi_action_acceptance(self.handle, optimized_goal_index, C.byref(a),
                                                            C.byref(out)))
@@ -607,12 +643,18 @@ class ClusterModel:
         buf = (ActionStruct * max(1, n))()
         if n:
             self.lib.check(self.lib.lib.ccmi_action_log_copy(self.handle, 0, n, buf))
-        return [(a.type, a.partition, a.source_broker, a.destination_broker, a.destination_partition)
-                for a in buf[:n]]
+        return [(a.type, a.partition, a.source_broker, a.destination_broker, a.destination_partition,
+                 a.source_disk, a.destination_disk) for a in buf[:n]]
 
     def replica_distribution(self) -> List[int]:
         out = (C.c_int32 * self.num_replicas)()
         self.lib.check(self.lib.lib.ccmi_replica_distribution(self.handle, out))
+        return list(out)
+
+    def replica_disks(self) -> List[int]:
+        """Disk index of every replica slot in partition order (the logdir of getReplicaDistribution)."""
+        out = (C.c_int32 * self.num_replicas)()
+        self.lib.check(self.lib.lib.ccmi_replica_disks(self.handle, out))
         return list(out)
 
     def leader_distribution(self) -> List[int]:
@@ -630,11 +672,15 @@ class ClusterModel:
         old_r = (C.c_int32 * (n * max_rf))()
         new_r = (C.c_int32 * (n * max_rf))()
         self.lib.check(self.lib.lib.ccmi_proposals(self.handle, max_rf, part, size, old_leader, old_r, new_r))
+        old_d = (C.c_int32 * (n * max_rf))()
+        new_d = (C.c_int32 * (n * max_rf))()
+        self.lib.check(self.lib.lib.ccmi_proposal_disks(self.handle, max_rf, old_d, new_d))
         out = []
         for i in range(n):
-            o = [x for x in old_r[i * max_rf:(i + 1) * max_rf] if x >= 0]
-            nw = [x for x in new_r[i * max_rf:(i + 1) * max_rf] if x >= 0]
-            out.append(ExecutionProposal(part[i], size[i], old_leader[i], o, nw))
+            rf = sum(1 for x in old_r[i * max_rf:(i + 1) * max_rf] if x >= 0)
+            sl = slice(i * max_rf, i * max_rf + rf)
+            out.append(ExecutionProposal(part[i], size[i], old_leader[i], list(old_r[sl]), list(new_r[sl]),
+                                         list(old_d[sl]), list(new_d[sl])))
         return out
 
     def perf(self) -> PerfStruct:

@@ -25,9 +25,10 @@ struct ccmi_session {
   ccmi::RcclShard* rccl = nullptr;
   int deviceOrdinal = 0;
   std::vector<int32_t> initDist, initLeaders;  // for ExecutionProposal diffs
+  std::vector<int32_t> initDisks, initLeaderDisks;  // the logdir half of ReplicaPlacementInfo (JBOD)
   struct Prop {
     int32_t partition, size, oldLeader;
-    std::vector<int32_t> oldR, newR;
+    std::vector<int32_t> oldR, newR, oldD, newD;
   };
   std::vector<Prop> proposals;
 };
@@ -83,8 +84,14 @@ void setOptions(ccmi_session* s, const ccmi_balancing_constraint* c, const ccmi_
   opt.exclMove.assign(B, 0);
   opt.exclLead.assign(B, 0);
   opt.requested.assign(B, 0);
+  opt.exclTopic.assign(s->model.T, 0);
   if (o) {
-    if (o->num_excluded_topics > 0) throw ccmi::Unsupported("excluded topics are outside ABI v1 scope");
+    for (int i = 0; i < o->num_excluded_topics; ++i) {
+      const int t = o->excluded_topics[i];
+      if (t < 0 || t >= s->model.T) throw std::invalid_argument("excluded topic out of range");
+      opt.exclTopic[t] = 1;
+      opt.anyExclTopic = true;
+    }
     for (int i = 0; i < o->num_excluded_brokers_for_leadership; ++i) {
       const int b = o->excluded_brokers_for_leadership[i];
       if (b < 0 || b >= B) throw std::invalid_argument("excluded broker for leadership out of range");
@@ -120,25 +127,60 @@ std::vector<int32_t> leaderDist(const ccmi::Model& m) {
   for (int p = 0; p < m.P; ++p) v[p] = m.rBroker[m.pLeader[p]];
   return v;
 }
+std::vector<int32_t> leaderDiskDist(const ccmi::Model& m) {
+  std::vector<int32_t> v(m.P);
+  for (int p = 0; p < m.P; ++p) v[p] = m.rDisk[m.pLeader[p]];
+  return v;
+}
+// ClusterModel.getReplicaDistribution / getLeaderDistribution with ReplicaPlacementInfo(broker, logdir)
+struct Placement {
+  std::vector<int32_t> dist, leaders, disks, leaderDisks;
+  explicit Placement(const ccmi::Model& m)
+      : dist(replicaDist(m)), leaders(leaderDist(m)), disks(m.replicaDisks()), leaderDisks(leaderDiskDist(m)) {}
+  bool operator!=(const Placement& o) const {
+    return dist != o.dist || leaders != o.leaders || disks != o.disks || leaderDisks != o.leaderDisks;
+  }
+};
 
+// A chain is either broker-granularity or disk-granularity: each kind's actionAcceptance rejects the other's actions
+// with IllegalArgumentException (e.g. ResourceDistributionGoal.actionAcceptance default branch,
+// IntraBrokerDiskCapacityGoal.actionAcceptance :120-124), so a mixed chain is refused up front.
+void validateChain(const ccmi_session* s, const int32_t* kinds, int n) {
+  int intra = 0;
+  for (int i = 0; i < n; ++i) intra += ccmi::isIntraGoalKind(kinds[i]) ? 1 : 0;
+  for (auto& g : s->engine->optimized) intra += ccmi::isIntraGoalKind(g->kind) ? 1 : 0;
+  const int total = n + (int)s->engine->optimized.size();
+  if (intra != 0 && intra != total)
+    throw std::invalid_argument("intra-broker goals cannot be optimized together with inter-broker goals");
+  if (intra == 0) {
+    if (s->engine->opt.anyExclTopic) throw ccmi::Unsupported("excluded topics are supported by the intra-broker goals only");
+    if (s->model.numBadDisk > 0) throw ccmi::Unsupported("inter-broker goals with BAD_DISKS brokers are not implemented");
+  }
+}
+
+// AnalyzerUtils.getDiff (AnalyzerUtils.java:63-93) against the session's initial placement
 void buildProposals(ccmi_session* s) {
   const ccmi::Model& m = s->model;
   s->proposals.clear();
-  const std::vector<int32_t> fin = replicaDist(m);
+  const std::vector<int32_t> fin = replicaDist(m), finD = m.replicaDisks();
   for (int p = 0; p < m.P; ++p) {
     const int a = m.pOff[p], n = m.pOff[p + 1] - a;
     std::vector<int32_t> oldR(s->initDist.begin() + a, s->initDist.begin() + a + n);
     std::vector<int32_t> newR(fin.begin() + a, fin.begin() + a + n);
-    const int finalLeader = m.rBroker[m.pLeader[p]];
-    if (oldR == newR && s->initLeaders[p] == finalLeader) continue;
-    if (newR[0] != finalLeader) {
-      int pos = 0;
-      for (int k = 0; k < n; ++k)
-        if (newR[k] == finalLeader) pos = k;
-      newR[pos] = newR[0];
-      newR[0] = finalLeader;
-    }
-    s->proposals.push_back({p, (int32_t)m.ru(m.pLeader[p], ccmi::R_DISK), s->initLeaders[p], oldR, newR});
+    std::vector<int32_t> oldD(s->initDisks.begin() + a, s->initDisks.begin() + a + n);
+    std::vector<int32_t> newD(finD.begin() + a, finD.begin() + a + n);
+    const int finalLeader = m.rBroker[m.pLeader[p]], finalLeaderDisk = m.rDisk[m.pLeader[p]];
+    if (oldR == newR && oldD == newD && s->initLeaders[p] == finalLeader && s->initLeaderDisks[p] == finalLeaderDisk)
+      continue;
+    int pos = 0;  // finalReplicas.indexOf(finalLeaderPlacementInfo), then swapped with slot 0
+    for (int k = 0; k < n; ++k)
+      if (newR[k] == finalLeader && newD[k] == finalLeaderDisk) {
+        pos = k;
+        break;
+      }
+    std::swap(newR[pos], newR[0]);
+    std::swap(newD[pos], newD[0]);
+    s->proposals.push_back({p, (int32_t)m.ru(m.pLeader[p], ccmi::R_DISK), s->initLeaders[p], oldR, newR, oldD, newD});
   }
 }
 }  // namespace
@@ -229,10 +271,26 @@ ccmi_status ccmi_session_create(int32_t device_ordinal, const ccmi_cluster_desc*
                              m.topicCountDense.data());
     s->device->uploadLoads(m.W, m.rLoad.data(), m.bLoad.data(), m.bLnw.data(), m.bPot.data(), m.pSlots.data(),
                            m.pLeader.data());
+    if (m.D > 0) {
+      std::vector<uint8_t> bAlive(m.B), dAlive(m.dAlive);
+      std::vector<double> rDu(m.R);
+      std::vector<float> rScore(m.R);
+      for (int b = 0; b < m.B; ++b) bAlive[b] = m.alive(b) ? 1 : 0;
+      for (int r = 0; r < m.R; ++r) {
+        rDu[r] = m.ru(r, ccmi::R_DISK);
+        rScore[r] = m.rScoreC[4 * (size_t)r + ccmi::R_DISK];
+      }
+      s->device->uploadDisks(m.D, m.bDiskOff.data(), m.bDisks.data(), m.dCap.data(), dAlive.data(), bAlive.data(),
+                             m.rOrigDisk.data(), rDu.data(), rScore.data(), m.rStatic.data());
+      s->device->setDiskUtil(m.dUtil.data());
+      m.diskDirty = false;
+    }
     m.dev = s->device.get();
     s->engine = std::make_unique<ccmi::Engine>(m, s->device.get());
     s->initDist = replicaDist(m);
     s->initLeaders = leaderDist(m);
+    s->initDisks = m.replicaDisks();
+    s->initLeaderDisks = leaderDiskDist(m);
     *out = s.release();
     return CCMI_OK;
   });
@@ -282,12 +340,13 @@ ccmi_status ccmi_goal_optimize(ccmi_session* s, int32_t goal_kind, const ccmi_ba
   return guarded([&] {
     if (!s) throw std::invalid_argument("null session");
     setOptions(s, c, o);
+    validateChain(s, &goal_kind, 1);
     auto g = ccmi::makeGoal(goal_kind);
     ccmi_goal_result tmp;
     std::memset(&tmp, 0, sizeof(tmp));
-    const std::vector<int32_t> pre = replicaDist(s->model), preL = leaderDist(s->model);
+    const Placement pre(s->model);
     s->engine->optimizeGoal(std::move(g), &tmp);
-    tmp.has_diff = (replicaDist(s->model) != pre || leaderDist(s->model) != preL) ? 1 : 0;
+    tmp.has_diff = Placement(s->model) != pre ? 1 : 0;
     if (result) *result = tmp;
     buildProposals(s);
     return CCMI_OK;
@@ -300,13 +359,14 @@ ccmi_status ccmi_optimizations(ccmi_session* s, const int32_t* goal_kinds, int32
     if (!s || (!goal_kinds && n_goals > 0)) throw std::invalid_argument("null argument");
     if (n_goals <= 0) throw std::invalid_argument("At least one goal must be provided to get an optimization result.");
     setOptions(s, c, o);
+    validateChain(s, goal_kinds, n_goals);
     for (int i = 0; i < n_goals; ++i) (void)ccmi::makeGoal(goal_kinds[i]);  // fail fast on unsupported kinds
     for (int i = 0; i < n_goals; ++i) {
       ccmi_goal_result tmp;
       std::memset(&tmp, 0, sizeof(tmp));
-      const std::vector<int32_t> pre = replicaDist(s->model), preL = leaderDist(s->model);
+      const Placement pre(s->model);
       s->engine->optimizeGoal(ccmi::makeGoal(goal_kinds[i]), &tmp);
-      tmp.has_diff = (replicaDist(s->model) != pre || leaderDist(s->model) != preL) ? 1 : 0;
+      tmp.has_diff = Placement(s->model) != pre ? 1 : 0;
       if (results) results[i] = tmp;
     }
     buildProposals(s);
@@ -341,7 +401,7 @@ ccmi_status ccmi_action_log_copy(const ccmi_session* s, int64_t first, int64_t c
     if (first < 0 || count < 0 || first + count > (int64_t)s->model.log.size()) throw std::invalid_argument("range");
     for (int64_t i = 0; i < count; ++i) {
       const ccmi::ActionRec& a = s->model.log[first + i];
-      out[i] = {a.type, a.partition, a.src, a.dst, a.destPartition};
+      out[i] = {a.type, a.partition, a.src, a.dst, a.destPartition, a.srcDisk, a.dstDisk};
     }
     return CCMI_OK;
   });
@@ -365,7 +425,30 @@ ccmi_status ccmi_leader_distribution(const ccmi_session* s, int32_t* out) {
   });
 }
 
+ccmi_status ccmi_replica_disks(const ccmi_session* s, int32_t* out) {
+  return guarded([&] {
+    if (!s || !out) throw std::invalid_argument("null argument");
+    const auto v = s->model.replicaDisks();
+    std::memcpy(out, v.data(), v.size() * sizeof(int32_t));
+    return CCMI_OK;
+  });
+}
+
 int64_t ccmi_proposal_count(const ccmi_session* s) { return s ? (int64_t)s->proposals.size() : 0; }
+
+ccmi_status ccmi_proposal_disks(const ccmi_session* s, int32_t max_rf, int32_t* old_disk_out, int32_t* new_disk_out) {
+  return guarded([&] {
+    if (!s || !old_disk_out || !new_disk_out) throw std::invalid_argument("null argument");
+    for (size_t i = 0; i < s->proposals.size(); ++i) {
+      const auto& p = s->proposals[i];
+      for (int k = 0; k < max_rf; ++k) {
+        old_disk_out[i * max_rf + k] = k < (int)p.oldD.size() ? p.oldD[k] : -1;
+        new_disk_out[i * max_rf + k] = k < (int)p.newD.size() ? p.newD[k] : -1;
+      }
+    }
+    return CCMI_OK;
+  });
+}
 
 ccmi_status ccmi_proposals(const ccmi_session* s, int32_t max_rf, int32_t* partition, int32_t* size,
                            int32_t* old_leader, int32_t* old_out, int32_t* new_out) {
@@ -398,6 +481,9 @@ ccmi_status ccmi_perf(const ccmi_session* s, ccmi_perf_counters* out) {
     out->host_syncs = p.syncs;
     out->scan_required = p.scanRequired;
     out->chain_launches = p.chainLaunches;
+    out->intra_launches = p.intraLaunches;
+    out->intra_kernel_ms = p.intraKernelMs;
+    out->intra_bytes = p.intraBytes;
     return CCMI_OK;
   });
 }

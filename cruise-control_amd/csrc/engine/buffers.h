@@ -15,4 +15,9 @@ struct ccmi_cluster_buffers {
   std::vector<int32_t> repPart, repBroker;
   std::vector<uint8_t> repLeader, repOffline;
   std::vector<float> repLoad;
+  // JBOD placement
+  std::vector<int32_t> diskBroker, diskAssignReplica, diskAssignDisk;
+  std::vector<std::string> diskStr;
+  std::vector<const char*> diskPtr;
+  std::vector<double> diskCap;
 };

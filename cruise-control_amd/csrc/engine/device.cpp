@@ -1,5 +1,6 @@
 // Device tables, staging and launch protocol (see device.h).
 #include "device.h"
+#include "intra.h"
 #include "prof.h"
 
 #include <hip/hip_runtime.h>
@@ -40,6 +41,14 @@ hipError_t launchSyncLoads(const ChainTables& C, const LoadRow* lrows, int nl, c
 hipError_t launchStats(const StatsParams& P, const int32_t* tc, const int32_t* topicNrep, const BrokerRec* brokers,
                        const uint8_t* allowedAlive, TopicPartial* scratch, StatsOut* out, int ldB, hipStream_t st,
                        hipEvent_t evTopic0, hipEvent_t evTopic1);
+
+hipError_t launchIntra(const IntraArgs& A, hipStream_t st);
+hipError_t launchIntraCompact(const int32_t* brokers, int n, const int64_t* logOff, const int32_t* count,
+                              const int64_t* cOff, const int32_t* rep, const int32_t* src, const int32_t* dst,
+                              int32_t* cRep, int32_t* cSrc, int32_t* cDst, hipStream_t st);
+hipError_t launchStatsDisks(const int32_t* bDiskOff, const int32_t* bDisks, const double* dCap, const uint8_t* dAlive,
+                            const double* dUtil, const uint8_t* bAlive, int B, double balance, DiskStatsOut* out,
+                            hipStream_t st);
 
 static void hipCheck(hipError_t e, const char* what) {
   if (e != hipSuccess) throw std::runtime_error(std::string("HIP error in ") + what + ": " + hipGetErrorString(e));
@@ -134,6 +143,8 @@ Device::~Device() {
                 rowVisited_, dResult_, dDone_, tUpper_, tLower_, dRLoad_, dBLoad_, dBLnw_, dBPot_, dPOff_, dPSlots_,
                 dPLeader_, dChainLog_, dChainOut_};
   for (void* p : ps)
+    if (p) (void)hipFree(p);
+  for (void* p : intraAllocs_)
     if (p) (void)hipFree(p);
   if (hStage_) (void)hipHostFree(hStage_);
   if (hResult_) (void)hipHostFree(hResult_);
@@ -698,6 +709,264 @@ Device::ChainResult Device::chainRackRows(const DevProgram& prog, const int32_t*
   perf.scanPairs += evaluated;
   perf.scanRequired += evaluated;
   return res;
+}
+
+}  // namespace ccmi
+
+namespace ccmi {
+
+// ------------------------------------------------------------------------------------------------ K6 intra-broker
+namespace {
+template <class T>
+void dallocTracked(T** p, size_t n, std::vector<void*>& owned) {
+  if (*p) {
+    for (auto& q : owned)
+      if (q == (void*)*p) q = nullptr;
+    (void)hipFree(*p);
+  }
+  hipCheck(hipMalloc((void**)p, (n ? n : 1) * sizeof(T)), "hipMalloc");
+  owned.push_back((void*)*p);
+}
+// grow three int32 device arrays sharing one capacity to n elements, keeping their first `keep` elements
+void growTriple(int32_t** a, int32_t** b, int32_t** c, size_t& cap, size_t n, size_t keep, std::vector<void*>& owned,
+                hipStream_t st) {
+  if (n <= cap && *a) return;
+  size_t nc = cap ? cap : 1024;
+  while (nc < n) nc *= 2;
+  int32_t** arrs[3] = {a, b, c};
+  for (int32_t** p : arrs) {
+    int32_t* q = nullptr;
+    hipCheck(hipMalloc((void**)&q, nc * sizeof(int32_t)), "hipMalloc");
+    if (*p && keep) hipCheck(hipMemcpyAsync(q, *p, keep * sizeof(int32_t), hipMemcpyDeviceToDevice, st), "grow copy");
+    if (*p) {
+      hipCheck(hipStreamSynchronize(st), "sync");
+      for (auto& x : owned)
+        if (x == (void*)*p) x = nullptr;
+      (void)hipFree(*p);
+    }
+    owned.push_back((void*)q);
+    *p = q;
+  }
+  cap = nc;
+}
+}  // namespace
+
+void Device::uploadDisks(int D, const int32_t* bDiskOff, const int32_t* bDisks, const double* dCap,
+                         const uint8_t* dAlive, const uint8_t* bAlive, const int32_t* rOrigDisk, const double* rDu,
+                         const float* rScore, const int32_t* rTie) {
+  DeviceGuard dg(ordinal_);
+  D_ = D;
+  auto& o = intraAllocs_;
+  dallocTracked(&dBDiskOff_, (size_t)B_ + 1, o);
+  dallocTracked(&dBDisks_, (size_t)D, o);
+  dallocTracked(&dDCap_, (size_t)D, o);
+  dallocTracked(&dDAlive_, (size_t)D, o);
+  dallocTracked(&dDUtilIn_, (size_t)D, o);
+  dallocTracked(&dDUtil_, (size_t)D, o);
+  dallocTracked(&dBAlive_, (size_t)B_, o);
+  dallocTracked(&dROrigDisk_, (size_t)R_, o);
+  dallocTracked(&dRDu_, (size_t)R_, o);
+  dallocTracked(&dRScore_, (size_t)R_, o);
+  dallocTracked(&dRTie_, (size_t)R_, o);
+  dallocTracked(&dRSel_, (size_t)R_, o);
+  dallocTracked(&dUpper_, (size_t)G_ * B_, o);
+  dallocTracked(&dLower_, (size_t)G_ * B_, o);
+  dallocTracked(&dHist_, (size_t)B_ * kIntraHist * (kIntraMaxDisks + 1), o);
+  dallocTracked(&dBrokers_, (size_t)B_, o);
+  dallocTracked(&dLogCap_, (size_t)B_, o);
+  dallocTracked(&dCount_, (size_t)B_, o);
+  dallocTracked(&dStatus_, (size_t)B_, o);
+  dallocTracked(&dLogOff_, (size_t)B_, o);
+  dallocTracked(&dCand_, (size_t)B_, o);
+  dallocTracked(&dCOff_, (size_t)B_ + 1, o);
+  dallocTracked(&dEOff_, (size_t)B_ + 1, o);
+  dallocTracked(&dDiskStats_, 1, o);
+  hipCheck(hipMemcpy(dBDiskOff_, bDiskOff, sizeof(int32_t) * (B_ + 1), hipMemcpyHostToDevice), "upload bDiskOff");
+  hipCheck(hipMemcpy(dBDisks_, bDisks, sizeof(int32_t) * D, hipMemcpyHostToDevice), "upload bDisks");
+  hipCheck(hipMemcpy(dDCap_, dCap, sizeof(double) * D, hipMemcpyHostToDevice), "upload dCap");
+  hipCheck(hipMemcpy(dDAlive_, dAlive, D, hipMemcpyHostToDevice), "upload dAlive");
+  hipCheck(hipMemcpy(dBAlive_, bAlive, B_, hipMemcpyHostToDevice), "upload bAlive");
+  hipCheck(hipMemcpy(dROrigDisk_, rOrigDisk, sizeof(int32_t) * R_, hipMemcpyHostToDevice), "upload rOrigDisk");
+  hipCheck(hipMemcpy(dRDu_, rDu, sizeof(double) * R_, hipMemcpyHostToDevice), "upload rDu");
+  hipCheck(hipMemcpy(dRScore_, rScore, sizeof(float) * R_, hipMemcpyHostToDevice), "upload rScore");
+  hipCheck(hipMemcpy(dRTie_, rTie, sizeof(int32_t) * R_, hipMemcpyHostToDevice), "upload rTie");
+  hBDiskOff_.assign(bDiskOff, bDiskOff + B_ + 1);
+}
+
+void Device::setDiskUtil(const double* dUtil) {
+  DeviceGuard dg(ordinal_);
+  hipCheck(hipMemcpyAsync(dDUtilIn_, dUtil, sizeof(double) * D_, hipMemcpyHostToDevice, ST), "upload dUtil");
+}
+
+void Device::intraRun(const IntraRequest& q, IntraResult& out) {
+  DeviceGuard dg(ordinal_);
+  if (!dBDiskOff_) throw std::runtime_error("intraRun before uploadDisks");
+  const size_t E = (size_t)q.eOff[B_];
+  auto& o = intraAllocs_;
+  if (E > entCap_ || !dERep_) {
+    size_t c = 1024;
+    while (c < E) c *= 2;
+    dallocTracked(&dERep_, c, o);
+    dallocTracked(&dEDiskIn_, c, o);
+    dallocTracked(&dEDisk_, c, o);
+    dallocTracked(&dSnapA_, c, o);
+    dallocTracked(&dSnapB_, c, o);
+    entCap_ = c;
+  }
+  hipCheck(hipMemcpyAsync(dEOff_, q.eOff, sizeof(int32_t) * (B_ + 1), hipMemcpyHostToDevice, ST), "eOff");
+  hipCheck(hipMemcpyAsync(dERep_, q.eRep, sizeof(int32_t) * E, hipMemcpyHostToDevice, ST), "eRep");
+  hipCheck(hipMemcpyAsync(dEDiskIn_, q.eDisk, sizeof(int32_t) * E, hipMemcpyHostToDevice, ST), "eDisk");
+  hipCheck(hipMemcpyAsync(dRSel_, q.rSel, R_, hipMemcpyHostToDevice, ST), "rSel");
+  hipCheck(hipMemcpyAsync(dBrokers_, q.brokers, sizeof(int32_t) * q.nBrokers, hipMemcpyHostToDevice, ST), "brokers");
+  hipCheck(hipMemsetAsync(dCount_, 0, sizeof(int32_t) * B_, ST), "memset");
+  hipCheck(hipMemsetAsync(dStatus_, 0, sizeof(int32_t) * B_, ST), "memset");
+  hipCheck(hipMemsetAsync(dCand_, 0, sizeof(int64_t) * B_, ST), "memset");
+  // log ranges: 2 records per replica + 64 first; a broker that runs out is re-run with the bound of its program
+  std::vector<int64_t> logOff(B_, 0);
+  std::vector<int32_t> cap(B_, 0);
+  int64_t total = 0;
+  for (int i = 0; i < q.nBrokers; ++i) {
+    const int b = q.brokers[i];
+    logOff[b] = total;
+    cap[b] = 2 * (q.eOff[b + 1] - q.eOff[b]) + 64;
+    total += cap[b];
+  }
+  growTriple(&dLogRep_, &dLogSrc_, &dLogDst_, logCap_, (size_t)total, 0, o, ST);
+  IntraArgs A{};
+  A.goal = q.goal;
+  A.capThr = q.capThr;
+  A.margin = q.margin;
+  A.nPrior = q.nPrior;
+  if (q.nPrior > kIntraMaxPrior) throw std::invalid_argument("too many optimized intra-broker goals");
+  for (int k = 0; k < q.nPrior; ++k) {
+    A.prior[k].kind = q.priorKind[k];
+    A.prior[k].upper = dUpper_ + (size_t)q.priorSlot[k] * B_;
+    A.prior[k].lower = dLower_ + (size_t)q.priorSlot[k] * B_;
+  }
+  A.brokers = dBrokers_;
+  A.nBrokers = q.nBrokers;
+  A.bDiskOff = dBDiskOff_;
+  A.bDisks = dBDisks_;
+  A.dCap = dDCap_;
+  A.dAlive = dDAlive_;
+  A.dUtilIn = dDUtilIn_;
+  A.dUtil = dDUtil_;
+  A.eOff = dEOff_;
+  A.eRep = dERep_;
+  A.eDiskIn = dEDiskIn_;
+  A.eDisk = dEDisk_;
+  A.rDu = dRDu_;
+  A.rScore = dRScore_;
+  A.rTie = dRTie_;
+  A.rOrigDisk = dROrigDisk_;
+  A.rSel = dRSel_;
+  A.snapA = dSnapA_;
+  A.snapB = dSnapB_;
+  A.hist = dHist_;
+  A.upperOut = dUpper_ + (size_t)q.slot * B_;
+  A.lowerOut = dLower_ + (size_t)q.slot * B_;
+  A.logOff = dLogOff_;
+  A.logCap = dLogCap_;
+  A.logRep = dLogRep_;
+  A.logSrc = dLogSrc_;
+  A.logDst = dLogDst_;
+  A.logCount = dCount_;
+  A.status = dStatus_;
+  A.cand = dCand_;
+  float msTotal = 0.f;
+  auto launch = [&](const IntraArgs& a) {
+    hipCheck(hipMemcpyAsync(dLogOff_, logOff.data(), sizeof(int64_t) * B_, hipMemcpyHostToDevice, ST), "logOff");
+    hipCheck(hipMemcpyAsync(dLogCap_, cap.data(), sizeof(int32_t) * B_, hipMemcpyHostToDevice, ST), "logCap");
+    if (timing) hipCheck(hipEventRecord(EV0, ST), "event");
+    hipCheck(launchIntra(a, ST), "intra_brokers");
+    if (timing) hipCheck(hipEventRecord(EV1, ST), "event");
+    out.status.resize(B_);
+    hipCheck(hipMemcpyAsync(out.status.data(), dStatus_, sizeof(int32_t) * B_, hipMemcpyDeviceToHost, ST), "status");
+    hipCheck(hipStreamSynchronize(ST), "intra sync");
+    perf.syncs++;
+    perf.intraLaunches++;
+    if (timing) {
+      float ms = 0.f;
+      hipCheck(hipEventElapsedTime(&ms, EV0, EV1), "hipEventElapsedTime");
+      msTotal += ms;
+    }
+  };
+  launch(A);
+  std::vector<int32_t> rerun;
+  for (int i = 0; i < q.nBrokers; ++i)
+    if (out.status[q.brokers[i]] == IS_LOG_FULL) rerun.push_back(q.brokers[i]);
+  if (!rerun.empty()) {
+    const int64_t keep = total;
+    for (int b : rerun) {
+      const int64_t n = q.eOff[b + 1] - q.eOff[b];
+      const int64_t nd = hBDiskOff_[b + 1] - hBDiskOff_[b];
+      logOff[b] = total;
+      cap[b] = (int32_t)(6 * (nd + 1) * n + 64);
+      total += cap[b];
+    }
+    growTriple(&dLogRep_, &dLogSrc_, &dLogDst_, logCap_, (size_t)total, (size_t)keep, o, ST);
+    A.logRep = dLogRep_;
+    A.logSrc = dLogSrc_;
+    A.logDst = dLogDst_;
+    hipCheck(hipMemcpyAsync(dBrokers_, rerun.data(), sizeof(int32_t) * rerun.size(), hipMemcpyHostToDevice, ST),
+             "rerun brokers");
+    A.nBrokers = (int)rerun.size();
+    launch(A);
+    for (int b : rerun)
+      if (out.status[b] == IS_LOG_FULL) throw std::runtime_error("device intra-broker log overflow");
+    hipCheck(hipMemcpyAsync(dBrokers_, q.brokers, sizeof(int32_t) * q.nBrokers, hipMemcpyHostToDevice, ST), "brokers");
+  }
+  perf.intraKernelMs += msTotal;
+  out.count.resize(B_);
+  out.cand.resize(B_);
+  hipCheck(hipMemcpyAsync(out.count.data(), dCount_, sizeof(int32_t) * B_, hipMemcpyDeviceToHost, ST), "count");
+  hipCheck(hipMemcpyAsync(out.cand.data(), dCand_, sizeof(int64_t) * B_, hipMemcpyDeviceToHost, ST), "cand");
+  hipCheck(hipStreamSynchronize(ST), "intra sync");
+  out.off.assign(B_ + 1, 0);
+  for (int b = 0; b < B_; ++b) out.off[b + 1] = out.off[b] + out.count[b];
+  const size_t nrec = (size_t)out.off[B_];
+  growTriple(&dCRep_, &dCSrc_, &dCDst_, compactCap_, nrec, 0, o, ST);
+  hipCheck(hipMemcpyAsync(dCOff_, out.off.data(), sizeof(int64_t) * (B_ + 1), hipMemcpyHostToDevice, ST), "cOff");
+  hipCheck(hipMemcpyAsync(dLogOff_, logOff.data(), sizeof(int64_t) * B_, hipMemcpyHostToDevice, ST), "logOff");
+  hipCheck(launchIntraCompact(dBrokers_, q.nBrokers, dLogOff_, dCount_, dCOff_, dLogRep_, dLogSrc_, dLogDst_, dCRep_,
+                              dCSrc_, dCDst_, ST),
+           "intra_compact");
+  out.rep.resize(nrec);
+  out.src.resize(nrec);
+  out.dst.resize(nrec);
+  if (nrec) {
+    hipCheck(hipMemcpyAsync(out.rep.data(), dCRep_, sizeof(int32_t) * nrec, hipMemcpyDeviceToHost, ST), "rep");
+    hipCheck(hipMemcpyAsync(out.src.data(), dCSrc_, sizeof(int32_t) * nrec, hipMemcpyDeviceToHost, ST), "src");
+    hipCheck(hipMemcpyAsync(out.dst.data(), dCDst_, sizeof(int32_t) * nrec, hipMemcpyDeviceToHost, ST), "dst");
+  }
+  if (q.goal == IG_USAGE) {
+    out.upper.resize(B_);
+    out.lower.resize(B_);
+    hipCheck(hipMemcpyAsync(out.upper.data(), dUpper_ + (size_t)q.slot * B_, sizeof(double) * B_,
+                            hipMemcpyDeviceToHost, ST), "upper");
+    hipCheck(hipMemcpyAsync(out.lower.data(), dLower_ + (size_t)q.slot * B_, sizeof(double) * B_,
+                            hipMemcpyDeviceToHost, ST), "lower");
+  }
+  hipCheck(hipStreamSynchronize(ST), "intra sync");
+  perf.syncs++;
+  // algorithmic bytes: every processed broker's disk records and replica entries read once
+  int64_t bytes = 0;
+  for (int i = 0; i < q.nBrokers; ++i) {
+    const int b = q.brokers[i];
+    bytes += (int64_t)(hBDiskOff_[b + 1] - hBDiskOff_[b]) * kIntraBytesPerDisk +
+             (int64_t)(q.eOff[b + 1] - q.eOff[b]) * kIntraBytesPerEntry;
+  }
+  perf.intraBytes += bytes;
+}
+
+void Device::statsDisks(double diskBalance, DiskStatsOut* out) {
+  DeviceGuard dg(ordinal_);
+  hipCheck(launchStatsDisks(dBDiskOff_, dBDisks_, dDCap_, dDAlive_, dDUtilIn_, dBAlive_, B_, diskBalance, dDiskStats_,
+                            ST),
+           "stats_disks");
+  hipCheck(hipMemcpyAsync(out, dDiskStats_, sizeof(DiskStatsOut), hipMemcpyDeviceToHost, ST), "disk stats");
+  hipCheck(hipStreamSynchronize(ST), "sync");
+  perf.syncs++;
 }
 
 }  // namespace ccmi

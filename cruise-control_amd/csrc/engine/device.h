@@ -20,6 +20,10 @@ namespace ccmi {
 // Algorithmic bytes per evaluated candidate: destination-broker record 4x f64 util, 4x f64 capacity,
 // f64 potential NW_OUT, f64 leader NW_IN, i32 replica/leader/rack/topic-replica counts = 96 B.
 constexpr int64_t kBytesPerCandidate = 96;
+// K6 algorithmic bytes: per disk capacity + utilization + alive (17 B); per replica entry the replica id, disk,
+// DISK utilization, score, Replica.compareTo rank, original disk and selection flag (29 B).
+constexpr int64_t kIntraBytesPerDisk = 17;
+constexpr int64_t kIntraBytesPerEntry = 29;
 
 struct DevicePerf {
   int64_t scanLaunches = 0;
@@ -33,6 +37,36 @@ struct DevicePerf {
   int64_t singleLaunch = 0;  // scans that applied their rows in-kernel and read the request from host memory
   int64_t chainLaunches = 0; // K7 chains (several decisions per launch)
   int64_t scanRequired = 0;  // candidates the launches had to evaluate: each first-fit list up to its winner
+  int64_t intraLaunches = 0;  // K6 intra-broker launches
+  double intraKernelMs = 0;
+  int64_t intraBytes = 0;     // algorithmic bytes of K6 (per broker record + per replica entry)
+};
+
+// K6 (kernels/intra.hip, intra.h): one intra-broker goal over every broker in one launch.
+struct IntraRequest {
+  int32_t goal;               // IntraGoal
+  double capThr, margin;
+  int32_t nPrior = 0;
+  int32_t priorKind[4] = {0, 0, 0, 0};
+  int32_t priorSlot[4] = {0, 0, 0, 0};  // threshold slots of prior IG_USAGE goals
+  int32_t slot = 0;               // this goal's threshold slot (IG_USAGE)
+  const int32_t* brokers = nullptr;  // ascending broker ids to rebalance
+  int32_t nBrokers = 0;
+  const int32_t* eOff = nullptr;  // [B+1] CSR of the replicas on each broker's disks
+  const int32_t* eRep = nullptr;
+  const int32_t* eDisk = nullptr;
+  const uint8_t* rSel = nullptr;  // [R] tracked-sorted-replica selection
+};
+struct IntraResult {
+  std::vector<int32_t> count, status;  // [B] records / IntraStatus per broker
+  std::vector<int64_t> cand;           // [B]
+  std::vector<int64_t> off;            // [B+1] compact record offsets (broker-id order)
+  std::vector<int32_t> rep, src, dst;  // records
+  std::vector<double> upper, lower;    // [B] this goal's thresholds (IG_USAGE)
+};
+struct DiskStatsOut {  // ClusterModelStats.populateStatsForDisks partials
+  double varSum;
+  int32_t unbalanced, numAlive;
 };
 
 class Device {
@@ -88,6 +122,15 @@ class Device {
                             std::vector<int32_t>& log);
   void flushOnly();
   void flushPending();
+
+  // Disks (JBOD): the static disk / replica tables once per session; setDiskUtil whenever the host changed a disk's
+  // utilization; intraRun = one intra-broker goal (K6); statsDisks = the disk part of ClusterModelStats.
+  void uploadDisks(int D, const int32_t* bDiskOff, const int32_t* bDisks, const double* dCap, const uint8_t* dAlive,
+                   const uint8_t* bAlive, const int32_t* rOrigDisk, const double* rDu, const float* rScore,
+                   const int32_t* rTie);
+  void setDiskUtil(const double* dUtil);
+  void intraRun(const IntraRequest& q, IntraResult& out);
+  void statsDisks(double diskBalance, DiskStatsOut* out);
 
   DevicePerf perf;
   bool timing = false;  // record HIP events around kernels (bench/profiling)
@@ -150,6 +193,22 @@ class Device {
   ChainTables chainTables() const;
   template <class F>
   size_t stageChainCopy(size_t reqBytes, Staged& g, size_t& oReq, F fill);
+  // disk state (K6)
+  int D_ = 0;
+  int32_t *dBDiskOff_ = nullptr, *dBDisks_ = nullptr, *dROrigDisk_ = nullptr, *dRTie_ = nullptr;
+  double *dDCap_ = nullptr, *dDUtilIn_ = nullptr, *dDUtil_ = nullptr, *dRDu_ = nullptr;
+  uint8_t *dDAlive_ = nullptr, *dBAlive_ = nullptr, *dRSel_ = nullptr;
+  float* dRScore_ = nullptr;
+  double *dUpper_ = nullptr, *dLower_ = nullptr;  // [G][B] usage-goal thresholds
+  int32_t *dEOff_ = nullptr, *dERep_ = nullptr, *dEDiskIn_ = nullptr, *dEDisk_ = nullptr, *dSnapA_ = nullptr,
+          *dSnapB_ = nullptr, *dHist_ = nullptr, *dBrokers_ = nullptr, *dLogCap_ = nullptr, *dCount_ = nullptr,
+          *dStatus_ = nullptr, *dLogRep_ = nullptr, *dLogSrc_ = nullptr, *dLogDst_ = nullptr, *dCRep_ = nullptr,
+          *dCSrc_ = nullptr, *dCDst_ = nullptr;
+  int64_t *dLogOff_ = nullptr, *dCand_ = nullptr, *dCOff_ = nullptr;
+  size_t entCap_ = 0, logCap_ = 0, compactCap_ = 0;
+  DiskStatsOut* dDiskStats_ = nullptr;
+  std::vector<void*> intraAllocs_;
+  std::vector<int32_t> hBDiskOff_;
 };
 
 

@@ -240,6 +240,12 @@ int64_t Engine::chainRackRows(GoalImpl& self, const std::vector<int32_t>& rows, 
 }
 
 int Engine::acceptance(int gi, const ccmi_action& a) {
+  {
+    const int ia = intraAcceptance(*optimized.at(gi), *this, a);
+    if (ia >= 0) return ia;
+    if (a.type == CCMI_INTRA_BROKER_REPLICA_MOVEMENT || a.type == CCMI_INTRA_BROKER_REPLICA_SWAP)
+      throw std::invalid_argument("Unsupported balancing action " + std::to_string(a.type) + " is provided.");
+  }
   std::vector<const std::vector<uint8_t>*> allowedBySlot;
   for (auto& g : optimized) allowedBySlot.push_back(&g->allowed);
   HostView v{m, allowedBySlot, topicUpper, topicLower};
@@ -312,6 +318,16 @@ ccmi_cluster_stats Engine::stats() {
   s.num_brokers = m.B;
   s.num_replicas_in_cluster = m.R;
   s.num_topics = m.T;
+  if (m.D > 0) {  // ClusterModelStats.populateStatsForDisks (ClusterModelStats.java:489-511)
+    if (m.diskDirty) {
+      dev->setDiskUtil(m.dUtil.data());
+      m.diskDirty = false;
+    }
+    DiskStatsOut ds{};
+    dev->statsDisks(bc.resBalance[R_DISK], &ds);
+    s.num_unbalanced_disks = ds.unbalanced;
+    s.disk_utilization_std = ds.numAlive > 0 ? std::sqrt(ds.varSum / ds.numAlive) : 0.0;
+  }
   {
     std::vector<uint8_t> seen(m.P, 0);
     int n = 0;
@@ -331,7 +347,7 @@ bool Engine::optimizeGoal(std::unique_ptr<GoalImpl> g, ccmi_goal_result* res) {
   const auto t0 = clk::now();
   const int64_t c0 = candidates;
   const size_t a0 = m.log.size();
-  const int64_t l0 = dev->perf.scanLaunches, p0 = dev->perf.scanPairs;
+  const int64_t l0 = dev->perf.scanLaunches + dev->perf.intraLaunches, p0 = dev->perf.scanPairs;
   struct Clear {
     Model& m;
     ~Clear() {
@@ -371,7 +387,7 @@ bool Engine::optimizeGoal(std::unique_ptr<GoalImpl> g, ccmi_goal_result* res) {
     res->succeeded = ok ? 1 : 0;
     res->candidates = candidates - c0;
     res->actions = (int64_t)(m.log.size() - a0);
-    res->device_launches = dev->perf.scanLaunches - l0;
+    res->device_launches = dev->perf.scanLaunches + dev->perf.intraLaunches - l0;
     res->device_candidates = dev->perf.scanPairs - p0;
   }
   m.clearTracked();
@@ -1300,6 +1316,7 @@ class ResourceDistribution : public GoalImpl {
 }  // namespace
 
 std::unique_ptr<GoalImpl> makeGoal(int kind) {
+  if (isIntraGoalKind(kind)) return makeIntraGoal(kind);
   switch (kind) {
     case CCMI_GOAL_REPLICA_DISTRIBUTION: return std::make_unique<ReplicaDistribution>();
     case CCMI_GOAL_DISK_USAGE_DISTRIBUTION:

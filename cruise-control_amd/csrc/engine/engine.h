@@ -18,6 +18,7 @@
 
 #include "ccmi.h"
 #include "devtypes.h"
+#include "errors.h"
 #include "model.h"
 
 namespace ccmi {
@@ -26,7 +27,8 @@ class Device;
 
 struct Options {  // OptimizationOptions
   std::vector<uint8_t> exclMove, exclLead, requested;  // [B] flags
-  bool anyExclMove = false, anyExclLead = false, anyRequested = false;
+  std::vector<uint8_t> exclTopic;                      // [T] excludedTopics (intra-broker goals)
+  bool anyExclMove = false, anyExclLead = false, anyRequested = false, anyExclTopic = false;
   bool triggered = false, onlyImmigrants = false;
 };
 
@@ -118,15 +120,10 @@ class Engine {
 
 std::unique_ptr<GoalImpl> makeGoal(int kind);
 std::unique_ptr<GoalImpl> makeMoreGoal(int kind);  // engine_goals.cpp: the remaining default goals
+std::unique_ptr<GoalImpl> makeIntraGoal(int kind);  // engine_intra.cpp: the intra-broker (JBOD) goals
+bool isIntraGoalKind(int kind);
+// Goal.actionAcceptance of an intra-broker goal (host model), or -1 when `g` is not one
+int intraAcceptance(const GoalImpl& g, const Engine& e, const ccmi_action& a);
 
-struct OptimizationFailure : std::runtime_error {
-  using std::runtime_error::runtime_error;
-};
-struct StateError : std::runtime_error {
-  using std::runtime_error::runtime_error;
-};
-struct Unsupported : std::runtime_error {
-  using std::runtime_error::runtime_error;
-};
 
 }  // namespace ccmi

@@ -144,8 +144,9 @@ void Model::build(const ccmi_cluster_desc& d) {
   for (int b = 0; b < B; ++b) {
     const BState s = (BState)d.broker_state[b];
     if (s == BState::ALIVE) continue;
-    if (s == BState::BAD_DISKS) throw std::invalid_argument("BAD_DISKS brokers are outside ABI v1 scope");
+    if (s < BState::ALIVE || s > BState::BAD_DISKS) throw std::invalid_argument("unknown broker state");
     bState[b] = s;
+    if (s == BState::BAD_DISKS) numBadDisk++;
     if (s == BState::DEAD) {
       numDead++;
       for (int r : bRepl[b])
@@ -181,6 +182,7 @@ void Model::build(const ccmi_cluster_desc& d) {
   rScoreC.assign((size_t)4 * R, 0.f);
   for (int b = 0; b < B; ++b) refreshBroker(b);
   for (int r = 0; r < R; ++r) refreshReplica(r);
+  buildDisks(d);
   {
     // dense rank of the static tail of Replica.compareTo (partition number, original broker id, topic name)
     std::vector<int32_t> idx(R);
@@ -206,6 +208,123 @@ void Model::build(const ccmi_cluster_desc& d) {
   cDirtyB.assign(B, 0);
   cDirtyR.assign(R, 0);
   cDirtyP.assign(P, 0);
+}
+
+// Disks (ccmi.h desc fields): created with their broker, logdir order per broker, replica_disk given to
+// createReplica (utilization accumulates when the load is set: Disk.addReplicaLoad), then the disk_assign replay of
+// Disk.addReplica (the fixture's placement step).
+void Model::buildDisks(const ccmi_cluster_desc& d) {
+  D = d.num_disks;
+  if (D < 0) throw std::invalid_argument("num_disks < 0");
+  dBroker.assign(D, 0);
+  dLogdir.assign(D, std::string());
+  dCap.assign(D, 0.0);
+  dUtil.assign(D, 0.0);
+  dAlive.assign(D, 1);
+  dMembers.assign(D, {});
+  rDisk.assign(R, -1);
+  rOrigDisk.assign(R, -1);
+  std::vector<std::vector<int32_t>> per(B);
+  for (int k = 0; k < D; ++k) {
+    const int b = d.disk_broker[k];
+    if (b < 0 || b >= B) throw std::invalid_argument("disk broker out of range");
+    dBroker[k] = b;
+    dLogdir[k] = d.disk_logdir[k] ? d.disk_logdir[k] : "";
+    const double c = d.disk_capacity[k];
+    dCap[k] = c < 0 ? -1.0 : c;  // Disk(logDir, broker, capacity): negative = dead
+    dAlive[k] = c < 0 ? 0 : 1;
+    per[b].push_back(k);
+  }
+  bDiskOff.assign(B + 1, 0);
+  bDisks.clear();
+  for (int b = 0; b < B; ++b) {
+    auto& v = per[b];
+    std::sort(v.begin(), v.end(), [&](int x, int y) { return dLogdir[x] < dLogdir[y]; });  // String.compareTo (ASCII)
+    for (size_t i = 1; i < v.size(); ++i)
+      if (dLogdir[v[i]] == dLogdir[v[i - 1]]) throw std::invalid_argument("duplicate logdir on a broker");
+    if ((int)v.size() > kMaxDisksPerBroker) throw std::invalid_argument("more than 31 logdirs on a broker");
+    bDiskOff[b] = (int)bDisks.size();
+    bDisks.insert(bDisks.end(), v.begin(), v.end());
+  }
+  bDiskOff[B] = (int)bDisks.size();
+  for (int b = 0; b < B; ++b)
+    if (!alive(b))
+      for (int k = bDiskOff[b]; k < bDiskOff[b + 1]; ++k) {  // Broker.setState(DEAD): Disk.setState(DEAD)
+        dAlive[bDisks[k]] = 0;
+        dCap[bDisks[k]] = -1.0;
+      }
+  if (D == 0) return;
+  if (d.replica_disk)
+    for (int r = 0; r < R; ++r) {
+      const int k = d.replica_disk[r];
+      if (k < -1 || k >= D) throw std::invalid_argument("replica disk out of range");
+      if (k >= 0 && dBroker[k] != rBroker[r]) throw std::invalid_argument("replica disk on another broker");
+      if (k < 0) continue;
+      rDisk[r] = rOrigDisk[r] = k;
+      dMembers[k].push_back(r);
+      dUtil[k] += ru(r, R_DISK);  // Disk.addReplica (load still empty: += 0.0) then Disk.addReplicaLoad
+    }
+  for (int i = 0; i < d.num_disk_assignments; ++i) {
+    const int r = d.disk_assign_replica[i], k = d.disk_assign_disk[i];
+    if (r < 0 || r >= R || k < 0 || k >= D || dBroker[k] != rBroker[r])
+      throw std::invalid_argument("disk assignment out of range");
+    diskAdd(k, r);
+  }
+}
+
+int Model::diskOf(int b, const std::string& logdir) const {
+  for (int k = bDiskOff[b]; k < bDiskOff[b + 1]; ++k)
+    if (dLogdir[bDisks[k]] == logdir) return bDisks[k];
+  return -1;
+}
+double Model::avgDiskPct(int b) const {
+  double cap = 0, util = 0;
+  for (int k = bDiskOff[b]; k < bDiskOff[b + 1]; ++k) {
+    const int d = bDisks[k];
+    if (dAlive[d]) {
+      cap += dCap[d];
+      util += dUtil[d];
+    }
+  }
+  return cap > 0 ? util / cap : 1.0;
+}
+void Model::diskAdd(int d, int r) {
+  auto& v = dMembers[d];
+  if (std::find(v.begin(), v.end(), r) != v.end())
+    throw StateError("Disk " + dLogdir[d] + " already has replica " + topicNames[pTopic[rPart[r]]] + "-" +
+                     std::to_string(pNumber[rPart[r]]));
+  dUtil[d] += ru(r, R_DISK);
+  v.push_back(r);
+  rDisk[r] = d;
+  diskDirty = true;
+}
+void Model::diskRemove(int d, int r) {
+  auto& v = dMembers[d];
+  auto it = std::find(v.begin(), v.end(), r);
+  if (it == v.end())
+    throw StateError("Disk " + dLogdir[d] + " does not has replica " + topicNames[pTopic[rPart[r]]] + "-" +
+                     std::to_string(pNumber[rPart[r]]));
+  dUtil[d] -= ru(r, R_DISK);
+  *it = v.back();
+  v.pop_back();
+  diskDirty = true;
+}
+void Model::relocateReplicaToDisk(int p, int b, int dst) {
+  const int r = replicaOn(p, b);
+  if (r < 0 || rDisk[r] < 0) throw std::runtime_error("Replica is not in the cluster.");
+  const int src = diskOf(b, dLogdir[rDisk[r]]);  // Broker.moveReplicaBetweenDisks(tp, replica.disk().logDir(), ...)
+  if (src < 0 || dst < 0 || dBroker[dst] != b) throw std::runtime_error("NullPointerException: logdir not on broker");
+  diskRemove(src, r);
+  diskAdd(dst, r);
+  ActionRec a{CCMI_INTRA_BROKER_REPLICA_MOVEMENT, p, b, b, -1};
+  a.srcDisk = src;
+  a.dstDisk = dst;
+  log.push_back(a);
+}
+std::vector<int32_t> Model::replicaDisks() const {
+  std::vector<int32_t> v(R);
+  for (int i = 0; i < R; ++i) v[i] = rDisk[pSlots[i]];
+  return v;
 }
 
 void Model::refreshBroker(int b) {
@@ -340,6 +459,13 @@ void Model::relocateReplica(int p, int src, int dst) {
   ops.subAll(bPot[src], rLoad[pLeader[p]]);
   rBroker[r] = dst;
   brokerAdd(dst, r);
+  if (rDisk[r] >= 0) {  // Broker.addReplica: _diskByLogdir.get(replica.disk().logDir()).addReplica(replica)
+    const int dd = diskOf(dst, dLogdir[rDisk[r]]);
+    if (dd < 0) throw std::runtime_error("NullPointerException: broker " + std::to_string(bId[dst]) + " has no logdir " +
+                                         dLogdir[rDisk[r]]);
+    diskGhosts++;  // the source disk keeps the replica (Broker.removeReplica does not touch disks)
+    diskAdd(dd, r);
+  }
   ops.addAll(cLoad, rLoad[r]);
   ops.addAll(bPot[dst], rLoad[pLeader[p]]);
   refreshBroker(src);

@@ -16,10 +16,13 @@
 
 #include "ccmi.h"
 #include "devtypes.h"
+#include "errors.h"
 #include "jsem.h"
 #include "loadops.h"
 
 namespace ccmi {
+
+constexpr int kMaxDisksPerBroker = 31;  // intra.h kIntraMaxDisks (TimSort binary-insertion range)
 
 class LoadOps {  // loadops.h arithmetic with the session's window count
  public:
@@ -52,6 +55,7 @@ enum class BState : int32_t { ALIVE = 0, DEAD = 1, NEW = 2, DEMOTED = 3, BAD_DIS
 
 struct ActionRec {
   int32_t type, partition, src, dst, destPartition;
+  int32_t srcDisk = -1, dstDisk = -1;  // intra-broker moves
 };
 
 class Device;
@@ -117,6 +121,27 @@ class Model {
   std::vector<int32_t> topicCountDense;     // [T][ldB] live Broker.numReplicasOfTopicInBroker counts
   int ldB = 4;
   int tcount(int t, int b) const { return topicCountDense[(size_t)t * ldB + b]; }
+  // disks: replica placement over logdirs (JBOD; Broker._diskByLogdir TreeMap, model/Disk.java)
+  int D = 0;
+  std::vector<int32_t> dBroker;
+  std::vector<std::string> dLogdir;
+  std::vector<double> dCap, dUtil;          // Disk._capacity (-1 dead), Disk._utilization
+  std::vector<uint8_t> dAlive;
+  std::vector<std::vector<int32_t>> dMembers;  // Disk._replicas (a HashSet; its order is never observed)
+  std::vector<int32_t> bDiskOff, bDisks;    // CSR: each broker's disks in logdir order
+  std::vector<int32_t> rDisk, rOrigDisk;    // Replica._disk / _originalDisk (-1 = null)
+  // Disk._replicas entries left behind by inter-broker moves (Broker.removeReplica keeps the replica on its disk)
+  int64_t diskGhosts = 0;
+  bool diskDirty = true;                    // device copy of dUtil is stale
+  int diskOf(int b, const std::string& logdir) const;
+  double diskPct(int d) const { return dCap[d] > 0 ? dUtil[d] / dCap[d] : 1.0; }  // GoalUtils.diskUtilizationPercentage
+  double avgDiskPct(int b) const;            // GoalUtils.averageDiskUtilizationPercentage
+  void diskAdd(int d, int r);                // Disk.addReplica (Disk.java:113-121)
+  void diskRemove(int d, int r);             // Disk.removeReplica (Disk.java:139-146)
+  // ClusterModel.relocateReplica(tp, brokerId, destinationLogdir) (ClusterModel.java:362-366), logged
+  void relocateReplicaToDisk(int p, int b, int dst);
+  std::vector<int32_t> replicaDisks() const;  // [R] disk of every replica slot in partition order
+
   // cluster
   LoadVec cLoad;
   double clusterCap[4] = {0, 0, 0, 0};
@@ -291,6 +316,7 @@ class Model {
   void build(const ccmi_cluster_desc& d);
 
  private:
+  void buildDisks(const ccmi_cluster_desc& d);
   void brokerAdd(int b, int r);
   int brokerRemove(int b, int p);
   void refreshBroker(int b);

@@ -1,7 +1,10 @@
 // Synthetic input generator: the reference's RandomCluster fixture (src/test/java/.../model/RandomCluster.java
 // :53-92 generate, :119-336 populate, :352-391 dead-broker marking; seeds TestConstants.java:19-26; capacities
 // src/test/resources/DefaultCapacityConfig.json) emitted directly in the flattened desc layout, so benches and
-// tests can build the 10K-broker / 1M-replica configurations without a JVM.
+// tests can build the 10K-broker / 1M-replica configurations without a JVM. JBOD (POPULATE_REPLICA_PLACEMENT_INFO):
+// logdirs from src/test/resources/testCapacityConfigJBOD.json (or the C4 layout), replicas placed on disks by
+// RandomCluster.java:315-331 (Broker.replicas() HashSet order) and bad disks marked by :430-443.
+#include <algorithm>
 #include <cmath>
 #include <cstring>
 #include <stdexcept>
@@ -18,12 +21,49 @@ namespace ccmi {
 namespace {
 int uniform(int lo, int hi, int64_t seed) { return JavaRandom(seed).nextInt(hi - lo + 1) + lo; }
 double expRandom(double mean, JavaRandom& r) { return std::log(1.0 - r.nextDouble()) * (-mean); }
+
+// Replica.compareTo on the generated arrays (all replicas online at placement time)
+struct GenReplicaOrder {
+  const ccmi_cluster_buffers* o;
+  const std::vector<int32_t>* topicRank;
+  int cmp(int a, int b) const {
+    const int na = o->partNumber[o->repPart[a]], nb = o->partNumber[o->repPart[b]];
+    if (na != nb) return na > nb ? 1 : -1;
+    const int ia = o->repBroker[a], ib = o->repBroker[b];
+    if (ia != ib) return ia > ib ? 1 : -1;
+    const int ta = (*topicRank)[o->partTopic[o->repPart[a]]], tb = (*topicRank)[o->partTopic[o->repPart[b]]];
+    return ta == tb ? 0 : (ta < tb ? -1 : 1);
+  }
+};
+
+// logdir -> capacity of broker b (BrokerCapacityConfigFileResolver; TreeMap order is applied by the model)
+std::vector<std::pair<std::string, double>> logdirsOf(const ccmi_random_cluster_props& p, int b) {
+  std::vector<std::pair<std::string, double>> v;
+  if (p.jbod == 1) {  // testCapacityConfigJBOD.json
+    if (b == 0) {
+      v = {{"/tmp/kafka-logs", 2000000.0}};
+    } else if (b == 1 || b == 2) {
+      v = {{"/tmp/kafka-logs-1", 350000.0}, {"/tmp/kafka-logs-2", 550000.0}};
+      if (b == 2) v.insert(v.end(), {{"/tmp/kafka-logs-3", 750000.0}, {"/tmp/kafka-logs-4", 950000.0}});
+    } else {
+      for (int k = 1; k <= 10; ++k) v.push_back({"/tmp/kafka-logs-" + std::to_string(k), k == 1 ? 400000.0 : 200000.0});
+    }
+  } else if (p.jbod == 2) {
+    for (int k = 0; k < p.num_logdirs; ++k) v.push_back({"/mnt/data-" + std::to_string(k + 1), p.logdir_capacity[k]});
+  }
+  return v;
+}
 }  // namespace
 
 ccmi_cluster_buffers* generateRandomCluster(const ccmi_random_cluster_props& p) {
   const int B = p.num_brokers;
   if (p.num_racks > B || B <= 0 || p.num_racks <= 0) throw std::invalid_argument("Random cluster generation failed due to bad input.");
-  if (p.num_dead_brokers < 0 || p.num_brokers_with_bad_disk != 0 || B < p.num_dead_brokers || p.num_topics <= 0 ||
+  if (p.jbod < 0 || p.jbod > 2 || (p.jbod == 2 && (p.num_logdirs < 1 || p.num_logdirs > 8)))
+    throw std::invalid_argument("jbod must be 0, 1 or 2 (2: 1..8 logdirs)");
+  if (p.num_brokers_with_bad_disk != 0 && !p.jbod)
+    throw std::invalid_argument("bad-disk brokers need replica placement over disks (jbod)");
+  if (p.num_dead_brokers < 0 || p.num_brokers_with_bad_disk < 0 ||
+      B < p.num_dead_brokers + p.num_brokers_with_bad_disk || p.num_topics <= 0 ||
       p.min_replication > p.max_replication || (p.leader_in_first_position && p.min_replication < 2) ||
       p.max_replication > B || p.num_topics > p.num_replicas ||
       (p.min_replication == p.max_replication && p.num_replicas % p.min_replication != 0))
@@ -43,6 +83,24 @@ ccmi_cluster_buffers* generateRandomCluster(const ccmi_random_cluster_props& p) 
     o.brokerCap[4 * b + CCMI_NW_IN] = small ? 150000.0 : 300000.0;
     o.brokerCap[4 * b + CCMI_NW_OUT] = small ? 150000.0 : 200000.0;
     o.brokerCap[4 * b + CCMI_DISK] = small ? 150000.0 : 300000.0;
+    if (p.jbod == 1) {
+      const double cpu = b == 0 ? 200.0 : (b <= 2 ? 300.0 : 100.0);
+      const double nin = b == 0 ? 200000.0 : (b <= 2 ? 300000.0 : 100000.0);
+      const double nout = b == 0 ? 200000.0 : (b <= 2 ? 200000.0 : 100000.0);
+      o.brokerCap[4 * b + CCMI_CPU] = cpu;
+      o.brokerCap[4 * b + CCMI_NW_IN] = nin;
+      o.brokerCap[4 * b + CCMI_NW_OUT] = nout;
+    }
+    if (p.jbod) {
+      double total = 0.0;
+      for (const auto& l : logdirsOf(p, b)) {
+        total += l.second;
+        o.diskBroker.push_back(b);
+        o.diskStr.push_back(l.first);
+        o.diskCap.push_back(l.second);
+      }
+      o.brokerCap[4 * b + CCMI_DISK] = total;
+    }
   }
   // populate(): topic replication factors and leader counts
   const int T0 = p.num_topics;
@@ -164,11 +222,75 @@ ccmi_cluster_buffers* generateRandomCluster(const ccmi_random_cluster_props& p) 
     }
   }
   o.repOffline.assign(o.repPart.size(), 0);
+  std::vector<int32_t> repDisk;
+  if (p.jbod) {
+    // Uniform-randomly assign replicas to disks: brokers by id, Broker.replicas() (HashSet<Replica>) order, the
+    // conflict resolver counting per broker (RandomCluster.java:315-331)
+    std::vector<int32_t> topicRank(T);
+    {
+      std::vector<int> idx(T);
+      for (int t = 0; t < T; ++t) idx[t] = t;
+      std::sort(idx.begin(), idx.end(), [&](int a, int b) { return o.topicStr[a] < o.topicStr[b]; });
+      for (int i = 0; i < T; ++i) topicRank[idx[i]] = i;
+    }
+    std::vector<int32_t> topicHash(T);
+    for (int t = 0; t < T; ++t) topicHash[t] = jStringHash(o.topicStr[t].c_str());
+    GenReplicaOrder ord{&o, &topicRank};
+    std::vector<JHashSet<GenReplicaOrder>> sets(B, JHashSet<GenReplicaOrder>(&ord));
+    for (size_t r = 0; r < o.repPart.size(); ++r) {
+      const int part = o.repPart[r];
+      const int32_t tp = jMix(jMix(1, o.partNumber[part]), topicHash[o.partTopic[part]]);
+      sets[o.repBroker[r]].add((int)r, jMix(jMix(1, tp), o.repBroker[r]));
+    }
+    std::vector<std::vector<int32_t>> disksOf(B);  // logdir order
+    for (size_t k = 0; k < o.diskBroker.size(); ++k) disksOf[o.diskBroker[k]].push_back((int32_t)k);
+    for (int b = 0; b < B; ++b)
+      std::sort(disksOf[b].begin(), disksOf[b].end(), [&](int x, int y) { return o.diskStr[x] < o.diskStr[y]; });
+    std::vector<double> util(o.diskBroker.size(), 0.0);
+    repDisk.assign(o.repPart.size(), -1);
+    std::vector<int32_t> members;
+    for (int b = 0; b < B; ++b) {
+      const auto& dl = disksOf[b];
+      const int n = (int)dl.size();
+      int resolver = 0, idx = 0;
+      sets[b].order(members);
+      for (int r : members) {
+        const double f = (double)o.repLoad[(size_t)r * 6 + CCMI_M_DISK_USAGE];
+        const double du = f > 0.0 ? f : (f != f ? f : 0.0);  // expectedUtilizationFor(DISK)
+        int a = uniform(0, n - 1, 1240 + idx);
+        while (o.diskCap[dl[a]] < util[dl[a]] + du) {
+          resolver++;
+          a = uniform(0, n - 1, 1240 + idx + resolver);
+        }
+        util[dl[a]] += du;
+        repDisk[r] = dl[a];
+        o.diskAssignReplica.push_back(r);
+        o.diskAssignDisk.push_back(dl[a]);
+        idx++;
+      }
+    }
+    // markBrokenBrokers with disks: the first disk (logdir order) of the first alive brokers dies
+    // (ClusterModel.markDiskDead: broker DISK capacity -= disk capacity, the disk's replicas original-offline)
+    int marked = 0;
+    for (int b = 0; b < B && marked < p.num_brokers_with_bad_disk; ++b) {
+      if (b < p.num_dead_brokers || disksOf[b].empty()) continue;
+      const int d = disksOf[b].front();
+      o.brokerCap[4 * (size_t)b + CCMI_DISK] -= o.diskCap[d];
+      o.diskCap[d] = -1.0;
+      for (size_t r = 0; r < repDisk.size(); ++r)
+        if (repDisk[r] == d) o.repOffline[r] = 1;
+      o.brokerState[b] = CCMI_BROKER_BAD_DISKS;
+      marked++;
+    }
+  }
   // markBrokenBrokers: brokers 0..numDead-1 become DEAD
-  // (Broker.setState(DEAD) also overwrites the capacity with DEAD_BROKER_CAPACITY, Broker.java:322-329)
+  // (Broker.setState(DEAD) also overwrites the capacity with DEAD_BROKER_CAPACITY, Broker.java:322-329, and kills
+  // the broker's disks)
   for (int b = 0; b < p.num_dead_brokers; ++b) {
     o.brokerState[b] = CCMI_BROKER_DEAD;
     for (int k = 0; k < 4; ++k) o.brokerCap[4 * (size_t)b + k] = -1.0;
+    for (size_t k = 0; k < o.diskBroker.size(); ++k)
+      if (o.diskBroker[k] == b) o.diskCap[k] = -1.0;
   }
   for (auto& s : o.topicStr) o.topicPtr.push_back(s.c_str());
   ccmi_cluster_desc& d = o.desc;
@@ -193,6 +315,17 @@ ccmi_cluster_buffers* generateRandomCluster(const ccmi_random_cluster_props& p) 
   d.replica_is_leader = o.repLeader.data();
   d.replica_offline = o.repOffline.data();
   d.replica_load = o.repLoad.data();
+  if (p.jbod) {
+    for (auto& x : o.diskStr) o.diskPtr.push_back(x.c_str());
+    d.num_disks = (int32_t)o.diskBroker.size();
+    d.disk_broker = o.diskBroker.data();
+    d.disk_logdir = o.diskPtr.data();
+    d.disk_capacity = o.diskCap.data();
+    d.replica_disk = nullptr;  // created without a disk; placed by the disk_assign replay
+    d.num_disk_assignments = (int32_t)o.diskAssignReplica.size();
+    d.disk_assign_replica = o.diskAssignReplica.data();
+    d.disk_assign_disk = o.diskAssignDisk.data();
+  }
   return out;
 }
 

@@ -1,0 +1,129 @@
+// K6: intra-broker (JBOD) goals on gfx950 (engine/intra.h holds the per-broker program) and the disk part of the
+// ClusterModelStats reduction (model/ClusterModelStats.java:489-511).
+//
+// intra_brokers : one thread per broker. A broker's rebalance touches only its own disks and replicas, so the B
+//                 programs of a goal are independent; each reads its replicas' records (contiguous CSR range) and its
+//                 disks, and writes its ordered action records into its own log range.
+// intra_compact : packs the per-broker log ranges into one array in broker-id order (the reference's action order).
+// stats_disks   : one workgroup: per alive broker the average disk utilization percentage and its disks'
+//                 deviations; unbalanced-disk count and variance sum reduced through LDS (tree-ordered sum: the stats
+//                 parity bar is 1e-9 relative).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../engine/device.h"
+#include "../engine/intra.h"
+
+namespace ccmi {
+
+__global__ __launch_bounds__(64) void intra_brokers(IntraArgs A) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= A.nBrokers) return;
+  IntraBroker ib(A, A.brokers[i]);
+  ib.run();
+}
+
+__global__ __launch_bounds__(256) void intra_compact(const int32_t* __restrict__ brokers, int n,
+                                                     const int64_t* __restrict__ logOff,
+                                                     const int32_t* __restrict__ count,
+                                                     const int64_t* __restrict__ cOff, const int32_t* __restrict__ rep,
+                                                     const int32_t* __restrict__ src, const int32_t* __restrict__ dst,
+                                                     int32_t* __restrict__ cRep, int32_t* __restrict__ cSrc,
+                                                     int32_t* __restrict__ cDst) {
+  // one wavefront per broker, lanes over its records (coalesced)
+  const int wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6, lane = threadIdx.x & 63;
+  if (wave >= n) return;
+  const int b = brokers[wave];
+  const int64_t s = logOff[b], d = cOff[b];
+  for (int k = lane; k < count[b]; k += 64) {
+    cRep[d + k] = rep[s + k];
+    cSrc[d + k] = src[s + k];
+    cDst[d + k] = dst[s + k];
+  }
+}
+
+__global__ __launch_bounds__(1024) void stats_disks(const int32_t* __restrict__ bDiskOff,
+                                                    const int32_t* __restrict__ bDisks, const double* __restrict__ dCap,
+                                                    const uint8_t* __restrict__ dAlive,
+                                                    const double* __restrict__ dUtil,
+                                                    const uint8_t* __restrict__ bAlive, int B, double balance,
+                                                    DiskStatsOut* __restrict__ out) {
+  __shared__ double sv[16];
+  __shared__ int su[16], sa[16];
+  double var = 0.0;
+  int unb = 0, na = 0;
+  for (int b = threadIdx.x; b < B; b += blockDim.x) {
+    if (!bAlive[b]) continue;
+    double cap = 0, util = 0;
+    for (int k = bDiskOff[b]; k < bDiskOff[b + 1]; ++k) {
+      const int d = bDisks[k];
+      if (dAlive[d]) {
+        cap += dCap[d];
+        util += dUtil[d];
+      }
+    }
+    const double avg = cap > 0 ? util / cap : 1.0;  // GoalUtils.averageDiskUtilizationPercentage
+    const double upper = avg * balance;
+    const double lm = 2 - balance;
+    const double lower = avg * (lm > 0 ? lm : 0.0);
+    for (int k = bDiskOff[b]; k < bDiskOff[b + 1]; ++k) {
+      const int d = bDisks[k];
+      if (!dAlive[d]) continue;
+      const double pct = dCap[d] > 0 ? dUtil[d] / dCap[d] : 1.0;
+      if (pct > upper || pct < lower) unb++;
+      const double x = pct - avg;
+      var += x * x;
+      na++;
+    }
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    var += __shfl_xor(var, off, 64);
+    unb += __shfl_xor(unb, off, 64);
+    na += __shfl_xor(na, off, 64);
+  }
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  if (lane == 0) {
+    sv[w] = var;
+    su[w] = unb;
+    sa[w] = na;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double v = 0;
+    int u = 0, a = 0;
+    for (int k = 0; k < (int)(blockDim.x >> 6); ++k) {
+      v += sv[k];
+      u += su[k];
+      a += sa[k];
+    }
+    out->varSum = v;
+    out->unbalanced = u;
+    out->numAlive = a;
+  }
+}
+
+hipError_t launchIntra(const IntraArgs& A, hipStream_t st) {
+  if (A.nBrokers <= 0) return hipSuccess;
+  hipLaunchKernelGGL(intra_brokers, dim3((A.nBrokers + 63) / 64), dim3(64), 0, st, A);
+  return hipGetLastError();
+}
+
+hipError_t launchIntraCompact(const int32_t* brokers, int n, const int64_t* logOff, const int32_t* count,
+                              const int64_t* cOff, const int32_t* rep, const int32_t* src, const int32_t* dst,
+                              int32_t* cRep, int32_t* cSrc, int32_t* cDst, hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(intra_compact, dim3((n + 3) / 4), dim3(256), 0, st, brokers, n, logOff, count, cOff, rep, src, dst,
+                     cRep, cSrc, cDst);
+  return hipGetLastError();
+}
+
+hipError_t launchStatsDisks(const int32_t* bDiskOff, const int32_t* bDisks, const double* dCap, const uint8_t* dAlive,
+                            const double* dUtil, const uint8_t* bAlive, int B, double balance, DiskStatsOut* out,
+                            hipStream_t st) {
+  hipLaunchKernelGGL(stats_disks, dim3(1), dim3(1024), 0, st, bDiskOff, bDisks, dCap, dAlive, dUtil, bAlive, B,
+                     balance, out);
+  return hipGetLastError();
+}
+
+}  // namespace ccmi

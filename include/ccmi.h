@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define CCMI_ABI_VERSION 1
+#define CCMI_ABI_VERSION 2
 
 typedef enum ccmi_status {
   CCMI_OK = 0,
@@ -142,6 +142,22 @@ typedef struct ccmi_cluster_desc {
    * DeterministicCluster.mediumClusterModel (DeterministicCluster.java:1836-1879), where it changes the float
    * rounding of the broker / potential-leadership aggregates. */
   const int32_t* replica_load_order;
+  /* Replica placement over disks (JBOD; Broker._diskByLogdir, model/Broker.java:56,80-83, model/Disk.java).
+   * num_disks = 0: no placement information (Replica.disk() == null everywhere). Otherwise disk d belongs to
+   * broker disk_broker[d], is named disk_logdir[d] (a broker's disks iterate in logdir String order, the TreeMap)
+   * and has disk_capacity[d] (negative = dead disk, Disk.java:58-66; a dead broker's disks are dead).
+   * replica_disk[r] is the disk given to ClusterModel.createReplica (the replica's original disk, -1 = none); its
+   * utilization accumulates when the replica's load is set (Disk.addReplicaLoad). After the model is built, the
+   * disk_assign pairs replay Disk.addReplica(replica) in order — the test fixture's placement step
+   * (RandomCluster.java:315-331) for replicas created without a disk (their original disk stays null). */
+  int32_t num_disks;
+  const int32_t* disk_broker;        /* [D] */
+  const char* const* disk_logdir;    /* [D] */
+  const double* disk_capacity;       /* [D] */
+  const int32_t* replica_disk;       /* [R] or NULL (all -1) */
+  int32_t num_disk_assignments;
+  const int32_t* disk_assign_replica; /* [num_disk_assignments] */
+  const int32_t* disk_assign_disk;    /* [num_disk_assignments] */
 } ccmi_cluster_desc;
 
 /* analyzer/BalancingConstraint.java; defaults AnalyzerConfig.java:58-464 via ccmi_default_constraint */
@@ -162,7 +178,8 @@ typedef struct ccmi_balancing_constraint {
 
 /* analyzer/OptimizationOptions.java (7-field form) */
 typedef struct ccmi_opt_options {
-  const int32_t* excluded_topics; /* must be empty: CCMI_E_UNSUPPORTED otherwise */
+  const int32_t* excluded_topics; /* topic indices; honoured by the intra-broker goals (selectReplicasBasedOnExcludedTopics),
+                                     CCMI_E_UNSUPPORTED for the inter-broker goals */
   int32_t num_excluded_topics;
   const int32_t* excluded_brokers_for_leadership;
   int32_t num_excluded_brokers_for_leadership;
@@ -184,6 +201,8 @@ typedef struct ccmi_action {
   int32_t source_broker;
   int32_t destination_broker;
   int32_t destination_partition; /* swaps only, else -1 */
+  int32_t source_disk;           /* intra-broker actions: disk indices (desc order), else -1. The action log records */
+  int32_t destination_disk;      /* an intra-broker swap as its two relocateReplica(tp, broker, logdir) calls. */
 } ccmi_action;
 
 /* model/ClusterModelStats.java fields */
@@ -223,6 +242,12 @@ typedef struct ccmi_random_cluster_props {
   int32_t distribution;          /* 0 UNIFORM, 1 LINEAR, 2 EXPONENTIAL */
   int32_t rack_aware;
   int32_t leader_in_first_position;
+  /* POPULATE_REPLICA_PLACEMENT_INFO: 0 none; 1 the reference's JBOD capacity file (testCapacityConfigJBOD.json:
+   * brokers 0/1/2 overridden, default broker 10 logdirs); 2 every broker num_logdirs logdirs "/mnt/d<i>" with
+   * capacities logdir_capacity[i] (the C4 layout; non-disk capacities from DefaultCapacityConfig.json). */
+  int32_t jbod;
+  int32_t num_logdirs;
+  double logdir_capacity[8];
 } ccmi_random_cluster_props;
 
 typedef struct ccmi_session ccmi_session;
@@ -261,11 +286,15 @@ ccmi_status ccmi_action_log_copy(const ccmi_session* s, int64_t first, int64_t c
 /* [R] current broker of each replica slot in partition CSR order / [P] leader broker per partition */
 ccmi_status ccmi_replica_distribution(const ccmi_session* s, int32_t* out);
 ccmi_status ccmi_leader_distribution(const ccmi_session* s, int32_t* out);
+/* [R] current disk of each replica slot in partition CSR order (-1 = no disk) */
+ccmi_status ccmi_replica_disks(const ccmi_session* s, int32_t* out);
 /* ExecutionProposals: count, then per proposal: partition, size, old leader, RF; old and new broker lists
  * (new list leader-first) packed into old_out/new_out with stride max_rf. */
 int64_t ccmi_proposal_count(const ccmi_session* s);
 ccmi_status ccmi_proposals(const ccmi_session* s, int32_t max_rf, int32_t* partition, int32_t* size,
                            int32_t* old_leader, int32_t* old_out, int32_t* new_out);
+/* The logdir half of the proposals' ReplicaPlacementInfo lists (disk indices, -1 = none), same packing. */
+ccmi_status ccmi_proposal_disks(const ccmi_session* s, int32_t max_rf, int32_t* old_disk_out, int32_t* new_disk_out);
 
 /*
  * Destination-sharded mode (one process per GPU): every rank creates a session on its own device from the same
@@ -295,6 +324,9 @@ typedef struct ccmi_perf_counters {
                                   algorithmic work; smaller than `candidates` where the engine never sends rows that
                                   cannot be accepted, e.g. non-legit leadership rows) */
   int64_t chain_launches;      /* K7 chain launches (several decisions applied on the device per launch) */
+  int64_t intra_launches;      /* K6 intra-broker launches (one per intra-broker goal, plus overflow re-runs) */
+  double intra_kernel_ms;      /* HIP-event duration of the K6 launches */
+  int64_t intra_bytes;         /* algorithmic bytes of K6 */
 } ccmi_perf_counters;
 ccmi_status ccmi_perf(const ccmi_session* s, ccmi_perf_counters* out);
 void ccmi_perf_reset(ccmi_session* s);

@@ -56,6 +56,11 @@ class AbstractGoal : public Goal {
   // candidates: in-order snapshot of the candidate broker's tracked sorted set (live view at call time)
   int maybeApplySwapAction(ClusterModel& cm, int srcReplica, const std::vector<int>& candidateReplicas,
                            const GoalList& g, const OptimizationOptions& o);
+  // AbstractGoal.maybeMoveReplicaBetweenDisks / maybeSwapReplicaBetweenDisks (AbstractGoal.java:351-430)
+  int maybeMoveReplicaBetweenDisks(ClusterModel& cm, int replica, const std::vector<int>& candidateDisks,
+                                   const GoalList& g);
+  int maybeSwapReplicaBetweenDisks(ClusterModel& cm, int srcReplica, const std::vector<int>& candidateReplicas,
+                                   const GoalList& g);
   std::string replicaSortName(bool reverse, bool leaderOnly) const {
     return name() + (reverse ? "-REVERSE" : "") + (leaderOnly ? "-LEADER" : "");
   }
@@ -358,6 +363,60 @@ class LeaderBytesInDistributionGoal : public AbstractGoal {
   double mean_ = 0.0;
   int numAllowed_ = 0;
   bool overLimit_ = false;
+};
+
+// ===================================================================== intra-broker (JBOD) goals
+//   IntraBrokerDiskCapacityGoal             analyzer/goals/IntraBrokerDiskCapacityGoal.java:40-291
+//   IntraBrokerDiskUsageDistributionGoal    analyzer/goals/IntraBrokerDiskUsageDistributionGoal.java:50-543
+//   GoalUtils.legitMoveBetweenDisks         analyzer/goals/GoalUtils.java:237-244
+// The per-disk swap timeout (PER_DISK_SWAP_TIMEOUT_MS, 500 ms) is treated as infinite like the fast-mode timeouts.
+
+class IntraBrokerDiskCapacityGoal : public AbstractGoal {
+ public:
+  using AbstractGoal::AbstractGoal;
+  std::string name() const override { return "IntraBrokerDiskCapacityGoal"; }
+  bool isHardGoal() const override { return true; }
+  Acceptance actionAcceptance(const BalancingAction& a, ClusterModel& cm) override;
+  int compareStats(const ClusterModelStats&, const ClusterModelStats&) const override { return 0; }
+
+ protected:
+  void initGoalState(ClusterModel& cm, const OptimizationOptions& o) override;
+  void updateGoalState(ClusterModel& cm, const OptimizationOptions& o) override;
+  void rebalanceForBroker(int broker, ClusterModel& cm, const GoalList& g, const OptimizationOptions& o) override;
+  bool selfSatisfied(ClusterModel& cm, const BalancingAction& a) override;
+  std::vector<int> brokersToBalance(ClusterModel& cm) override { return cm.aliveBrokers(); }
+
+ private:
+  bool overLimit(const ClusterModel& cm, int d) const;
+  bool underLimitAfterAdding(const ClusterModel& cm, int d, double util) const;
+};
+
+class IntraBrokerDiskUsageDistributionGoal : public AbstractGoal {
+ public:
+  using AbstractGoal::AbstractGoal;
+  std::string name() const override { return "IntraBrokerDiskUsageDistributionGoal"; }
+  bool isHardGoal() const override { return false; }
+  Acceptance actionAcceptance(const BalancingAction& a, ClusterModel& cm) override;
+  int compareStats(const ClusterModelStats& s1, const ClusterModelStats& s2) const override;
+  double upperThreshold(int b) const { return upper_[b]; }
+  double lowerThreshold(int b) const { return lower_[b]; }
+
+ protected:
+  void initGoalState(ClusterModel& cm, const OptimizationOptions& o) override;
+  void updateGoalState(ClusterModel& cm, const OptimizationOptions& o) override;
+  void rebalanceForBroker(int broker, ClusterModel& cm, const GoalList& g, const OptimizationOptions& o) override;
+  bool selfSatisfied(ClusterModel& cm, const BalancingAction& a) override;
+  std::vector<int> brokersToBalance(ClusterModel& cm) override { return cm.aliveBrokers(); }
+
+ private:
+  double sourceUtilizationDelta(const BalancingAction& a, ClusterModel& cm) const;
+  bool isChangeViolatingLimit(const ClusterModel& cm, double delta, int srcDisk, int dstDisk) const;
+  bool isGettingMoreBalanced(const ClusterModel& cm, int srcDisk, int dstDisk, double delta) const;
+  bool moveLoadIn(int disk, ClusterModel& cm, const GoalList& g);
+  bool moveLoadOut(int disk, ClusterModel& cm, const GoalList& g);
+  void swapLoadOut(int disk, ClusterModel& cm, const GoalList& g);
+  void swapLoadIn(int disk, ClusterModel& cm, const GoalList& g);
+  std::vector<double> upper_, lower_;  // _balanceUpperThresholdByBroker / _balanceLowerThresholdByBroker
 };
 
 }  // namespace oracle

@@ -394,6 +394,7 @@ class JPriorityQueue {
     q_[k] = x;
   }
   int peek() const { return q_.front(); }
+  const std::vector<int>& heap() const { return q_; }
   int poll() {
     int result = q_[0];
     int n = (int)q_.size() - 1;

@@ -5,6 +5,8 @@
 //   Broker.addReplica/removeReplica/makeFollower/makeLeader Broker.java:336-510
 //   Replica.makeFollower/computeCpuLoadAsFollower/makeLeader Replica.java:210-310
 //   ModelUtils.getFollowerCpuUtilFromLeaderLoad             ModelUtils.java:64-80 (weights 0.7/0.15/0.15)
+//   Disk.addReplica/removeReplica/addReplicaLoad, Broker.moveReplicaBetweenDisks/markDiskDead
+//                                                           Disk.java:113-146, Broker.java:519-543
 #include "model.h"
 
 #include <chrono>
@@ -32,6 +34,9 @@ int ReplicaCmp::compare(int a, int b) const {
     if (p == PrioFn::IMMIGRANTS) {
       p1 = cm->isImmigrant(a) ? 0 : 1;
       p2 = cm->isImmigrant(b) ? 0 : 1;
+    } else if (p == PrioFn::DISK_IMMIGRANTS) {  // r.originalDisk() != r.disk() ? 0 : 1
+      p1 = cm->replicas[a].origDisk != cm->replicas[a].disk ? 0 : 1;
+      p2 = cm->replicas[b].origDisk != cm->replicas[b].disk ? 0 : 1;
     } else {
       p1 = cm->isCurrentOffline(a) ? 0 : 1;
       p2 = cm->isCurrentOffline(b) ? 0 : 1;
@@ -81,7 +86,9 @@ bool ClusterModel::passesSelection(const SortSpec& spec, int r) const {
       case SelFn::OFFLINE: ok = isCurrentOffline(r); break;
       case SelFn::IMMIGRANTS: ok = isImmigrant(r); break;
       case SelFn::IMMIGRANT_OR_OFFLINE: ok = isImmigrant(r) || isCurrentOffline(r); break;
-      case SelFn::EXCLUDED_TOPICS: ok = true; break;  // resolved by caller-provided excluded set (empty in scope)
+      case SelFn::EXCLUDED_TOPICS:  // r.isOriginalOffline() || !excludedTopics.contains(topic)
+        ok = isOriginalOffline(r) || !excludedTopicsSel.count(partitions[rep.partition].topic);
+        break;
       case SelFn::ABOVE_LIMIT: ok = replicaUtil(r, s.resource) > s.limit; break;
       case SelFn::BELOW_LIMIT: ok = replicaUtil(r, s.resource) < s.limit; break;
     }
@@ -90,18 +97,50 @@ bool ClusterModel::passesSelection(const SortSpec& spec, int r) const {
   return true;
 }
 
+// Broker.trackSortedReplicas (Broker.java:398-408): the broker's own set and one per disk
 void ClusterModel::trackSortedReplicas(int b, const std::string& name, const SortSpec& spec) {
   auto& m = brokers[b].sorted;
   if (m.find(name) == m.end()) m.emplace(name, std::make_unique<SortedReplicas>(this, spec, b));  // putIfAbsent
+  for (int d : brokers[b].disks) {
+    auto& dm = disks[d].sorted;
+    if (dm.find(name) == dm.end()) {
+      auto sr = std::make_unique<SortedReplicas>(this, spec, b);
+      sr->disk = d;
+      dm.emplace(name, std::move(sr));
+    }
+  }
 }
 void ClusterModel::untrackSortedReplicas(const std::string& name) {
   for (auto& br : brokers) br.sorted.erase(name);
+  for (auto& dk : disks) dk.sorted.erase(name);
 }
-void ClusterModel::brokerUntrackSortedReplicas(int b, const std::string& name) { brokers[b].sorted.erase(name); }
+void ClusterModel::brokerUntrackSortedReplicas(int b, const std::string& name) {
+  brokers[b].sorted.erase(name);
+  for (int d : brokers[b].disks) disks[d].sorted.erase(name);
+}
 void ClusterModel::clearSortedReplicas() {
   for (auto& br : brokers) br.sorted.clear();
+  for (auto& dk : disks) dk.sorted.clear();
 }
-void ClusterModel::brokerClearSortedReplicas(int b) { brokers[b].sorted.clear(); }
+void ClusterModel::brokerClearSortedReplicas(int b) {
+  brokers[b].sorted.clear();
+  for (int d : brokers[b].disks) disks[d].sorted.clear();
+}
+SortedReplicas& ClusterModel::trackedDiskSortedReplicas(int d, const std::string& name) {
+  auto it = disks[d].sorted.find(name);
+  if (it == disks[d].sorted.end()) throw std::runtime_error("The sort name " + name + " is not found.");
+  SortedReplicas& sr = *it->second;
+  if (!sr.initialized) {  // SortedReplicas.ensureInitialize: _disk.replicas().forEach(this::add)
+    sr.initialized = true;
+    for (int r : disks[d].replicas)
+      if (passesSelection(sr.spec, r)) sr.set.insert(r);
+  }
+  return sr;
+}
+std::vector<int> ClusterModel::diskSortedReplicasClone(int d, const std::string& name) {
+  const auto& s = trackedDiskSortedReplicas(d, name).set;
+  return std::vector<int>(s.begin(), s.end());
+}
 
 SortedReplicas& ClusterModel::trackedSortedReplicas(int b, const std::string& name) {
   auto it = brokers[b].sorted.find(name);
@@ -183,11 +222,12 @@ int ClusterModel::createPartition(int topic, int number) {
   return (int)partitions.size() - 1;
 }
 
-int ClusterModel::createReplica(int brokerIdx, int p, int index, bool isLeader, bool isOffline) {
+int ClusterModel::createReplica(int brokerIdx, int p, int index, bool isLeader, bool isOffline, int disk) {
   int topic = partitions[p].topic;
   Replica rep;
   rep.broker = brokerIdx;
   rep.origBroker = brokerIdx;
+  rep.disk = rep.origDisk = disk;
   rep.isLeader = isLeader;
   rep.origOfflineFlag = isOffline;
   int r = (int)replicas.size();
@@ -223,6 +263,7 @@ void ClusterModel::setReplicaLoad(int r, const Load& amv) {
   amvAdd(brokers[b].load, amv, W);
   // (host and rack loads receive identical operations; host == broker here, rack load unused)
   amvAdd(load, amv, W);  // cluster
+  if (rep.disk >= 0) disks[rep.disk].utilization += replicaUtil(r, DISK);  // Disk.addReplicaLoad
   const Partition& part = partitions[rep.partition];
   if (part.leader >= 0 && replicas[part.leader].broker == b) {
     for (int x : part.replicas) amvAdd(potentialLeadershipLoad[replicas[x].broker], amv, W);
@@ -250,6 +291,10 @@ void ClusterModel::setBrokerState(int b, BrokerState s) {
       }
     }
     for (int k = 0; k < NUM_RESOURCES; ++k) br.capacity[k] = -1.0;
+    for (int d : br.disks) {  // Disk.setState(DEAD)
+      disks[d].alive = false;
+      disks[d].capacity = -1.0;
+    }
   }
   for (int r : br.replicas)
     if (replicas[r].inBrokerOffline) selfHealingEligibleReplicas.insert(r);
@@ -379,6 +424,12 @@ void ClusterModel::brokerAddReplica(int b, int r) {
   }
   loadAddLoad(br.load, rep.load, W);
   sortedAdd(b, r);
+  if (rep.disk >= 0) {  // _diskByLogdir.get(replica.disk().logDir()).addReplica(replica)
+    const int dd = diskOf(b, disks[rep.disk].logdir);
+    if (dd < 0) throw std::runtime_error("NullPointerException: broker " + std::to_string(br.id) + " has no logdir " +
+                                         disks[rep.disk].logdir);
+    diskAddReplica(dd, r);
+  }
 }
 
 int ClusterModel::brokerRemoveReplica(int b, int partition) {
@@ -516,6 +567,101 @@ bool ClusterModel::relocateLeadership(int p, int src, int dst) {
   part.leader = dr;
   if (recordActions) actionLog.push_back({(int)ActionType::LEADERSHIP_MOVEMENT, p, src, dst, -1});
   return true;
+}
+
+// ------------------------------------------------------------------ disks
+int ClusterModel::createDisk(int b, const std::string& logdir, double capacity) {
+  Disk dk;
+  dk.broker = b;
+  dk.logdir = logdir;
+  if (capacity < 0) {  // Disk(logDir, broker, diskCapacity): negative capacity = dead disk
+    dk.capacity = -1.0;
+    dk.alive = false;
+  } else {
+    dk.capacity = capacity;
+  }
+  if (!brokers[b].isAlive()) {
+    dk.capacity = -1.0;
+    dk.alive = false;
+  }
+  const int d = (int)disks.size();
+  disks.push_back(std::move(dk));
+  auto& lst = brokers[b].disks;  // TreeMap<String, Disk>: String.compareTo order
+  auto it = lst.begin();
+  while (it != lst.end() && disks[*it].logdir < logdir) ++it;
+  if (it != lst.end() && disks[*it].logdir == logdir) throw std::invalid_argument("duplicate logdir " + logdir);
+  lst.insert(it, d);
+  return d;
+}
+int ClusterModel::diskOf(int b, const std::string& logdir) const {
+  for (int d : brokers[b].disks)
+    if (disks[d].logdir == logdir) return d;
+  return -1;
+}
+void ClusterModel::diskAddReplica(int d, int r) {
+  Disk& dk = disks[d];
+  if (dk.replicas.count(r)) throw std::logic_error("Disk " + dk.logdir + " already has replica");
+  dk.utilization += replicaUtil(r, DISK);
+  dk.replicas.insert(r);
+  replicas[r].disk = d;
+  for (auto& kv : dk.sorted) {
+    SortedReplicas& sr = *kv.second;
+    if (sr.initialized && passesSelection(sr.spec, r)) sr.set.insert(r);
+  }
+}
+void ClusterModel::diskRemoveReplica(int d, int r) {
+  Disk& dk = disks[d];
+  if (!dk.replicas.count(r)) throw std::logic_error("Disk " + dk.logdir + " does not has replica");
+  dk.utilization -= replicaUtil(r, DISK);
+  dk.replicas.erase(r);
+  for (auto& kv : dk.sorted) {
+    SortedReplicas& sr = *kv.second;
+    if (sr.initialized) sr.set.erase(r);
+  }
+}
+void ClusterModel::markDiskDead(int b, int d) {
+  Broker& br = brokers[b];
+  br.capacity[DISK] -= disks[d].capacity;
+  disks[d].alive = false;
+  disks[d].capacity = -1.0;
+  for (int r : disks[d].replicas) {  // Replica.markOriginalOffline
+    Replica& rep = replicas[r];
+    if (rep.broker != rep.origBroker) throw std::logic_error("Cannot mark an immigrant replica as offline.");
+    rep.origOfflineFlag = true;
+    if (!rep.inBrokerOffline) {
+      rep.inBrokerOffline = true;
+      brokers[rep.origBroker].numOffline++;
+      brokers[rep.origBroker].offlineSet.add(r, replicaHash(r));
+    }
+  }
+  for (int r : br.replicas)
+    if (replicas[r].inBrokerOffline) selfHealingEligibleReplicas.insert(r);
+  refreshCapacity();
+}
+double ClusterModel::averageDiskUtilizationPct(int b) const {
+  double cap = 0, util = 0;
+  for (int d : brokers[b].disks)
+    if (disks[d].alive) {
+      cap += disks[d].capacity;
+      util += disks[d].utilization;
+    }
+  return cap > 0 ? util / cap : 1.0;
+}
+std::vector<int> ClusterModel::replicaDiskFlat() const {
+  std::vector<int> out;
+  for (const Partition& p : partitions)
+    for (int r : p.replicas) out.push_back(replicas[r].disk);
+  return out;
+}
+void ClusterModel::relocateReplicaToDisk(int p, int b, int dst) {
+  const int r = replicaOnBroker(p, b);
+  if (r < 0) throw std::runtime_error("Replica is not in the cluster.");
+  const int src = diskOf(b, disks[replicas[r].disk].logdir);  // Broker.moveReplicaBetweenDisks
+  if (src < 0 || disks[dst].broker != b) throw std::runtime_error("NullPointerException: logdir not on broker");
+  diskRemoveReplica(src, r);
+  diskAddReplica(dst, r);
+  if (recordActions)
+    actionLog.push_back({(int)ActionType::INTRA_BROKER_REPLICA_MOVEMENT, p, b, b, -1, src, dst});
 }
 
 void ClusterModel::checkDeadline() const {

@@ -10,6 +10,7 @@
 //   ClusterModel        .../model/ClusterModel.java:362-441,546-564,1049-1126
 //   SortedReplicas(+Helper, ReplicaSortFunctionFactory)  .../model/SortedReplicas.java,
 //                       SortedReplicasHelper.java, ReplicaSortFunctionFactory.java
+//   Disk                .../model/Disk.java (JBOD: Broker._diskByLogdir TreeMap, Broker.java:56,80-83,336-366,519-543)
 // Modelling assumption (asserted): one broker per host (RandomCluster names each host after its
 // broker, RandomCluster.java:80,87), so Host load/capacity are bit-identical to the broker's.
 #pragma once
@@ -147,6 +148,7 @@ struct Replica {
   // membership flags in the current broker's HashSets
   bool inBrokerLeaders = false, inBrokerImmigrants = false, inBrokerOffline = false;
   int posInBroker = -1;
+  int disk = -1, origDisk = -1;  // Replica._disk / _originalDisk (-1 = null)
 };
 
 struct Partition {
@@ -171,7 +173,7 @@ struct Selection {
   int resource = 0;
   double limit = 0.0;
 };
-enum class PrioFn { IMMIGRANTS, OFFLINE };
+enum class PrioFn { IMMIGRANTS, OFFLINE, DISK_IMMIGRANTS };
 enum class ScoreFn { NONE, BY_GROUP, REVERSE_BY_GROUP };
 struct SortSpec {
   std::vector<Selection> selection;
@@ -191,8 +193,19 @@ struct SortedReplicas {
   SortSpec spec;
   bool initialized = false;
   std::set<int, ReplicaCmp> set;
-  int owner;  // broker index
+  int owner;       // broker index
+  int disk = -1;   // disk index for a disk's SortedReplicas (initialised from Disk.replicas())
   SortedReplicas(const ClusterModel* cm, SortSpec s, int broker);
+};
+
+struct Disk {  // model/Disk.java
+  int broker = -1;
+  std::string logdir;
+  double capacity = 0;  // -1 when dead (DEAD_DISK_CAPACITY)
+  bool alive = true;
+  double utilization = 0;
+  std::set<int> replicas;  // Disk._replicas (HashSet; iteration order never used)
+  std::map<std::string, std::unique_ptr<SortedReplicas>> sorted;
 };
 
 struct Broker {
@@ -210,6 +223,7 @@ struct Broker {
   // Broker._topicReplicas key set (HashMap<String, ...>, keys never removed)
   JHashSet replicaSet, leaderSet, topicKeys;
   JHashSet offlineSet;  // Broker._currentOfflineReplicas
+  std::vector<int> disks;  // Broker._diskByLogdir values (TreeMap: logdir order)
   bool isAlive() const { return state != BrokerState::DEAD; }
   bool isNew() const { return state == BrokerState::NEW; }
   bool hasBadDisks() const { return state == BrokerState::BAD_DISKS; }
@@ -226,6 +240,7 @@ struct BalancingAction {
   int destinationBroker;
   ActionType type;
   int destPartition = -1;  // swap
+  int sourceDisk = -1, destinationDisk = -1;  // intra-broker actions (sourceBrokerLogdir / destinationBrokerLogdir)
 };
 
 struct ActionRecord {
@@ -234,6 +249,7 @@ struct ActionRecord {
   int src;
   int dst;
   int destPartition;
+  int srcDisk = -1, dstDisk = -1;
 };
 
 struct OptimizationOptions {
@@ -266,6 +282,9 @@ class ClusterModel {
   double clusterCapacity[NUM_RESOURCES] = {0, 0, 0, 0};
   std::vector<ActionRecord> actionLog;
   bool recordActions = true;
+  std::vector<Disk> disks;
+  std::vector<std::pair<int, int>> diskAssignLog;  // (replica, disk) of fixture Disk.addReplica calls (desc replay)
+  std::unordered_set<int> excludedTopicsSel;  // ReplicaSortFunctionFactory.selectReplicasBasedOnExcludedTopics set
   // instrumentation: reference-equivalent candidate evaluations
   int64_t candidatesEvaluated = 0;
   // CPU-baseline sampling (bench.py): stop the optimization at a wall-clock deadline (steady clock, seconds) and
@@ -282,11 +301,26 @@ class ClusterModel {
   int createBroker(int rackIdx, int brokerId, const double cap[NUM_RESOURCES]);
   int ensureTopic(const std::string& name);
   int createPartition(int topic, int number);
-  int createReplica(int brokerIdx, int partition, int index, bool isLeader, bool isOffline);
+  int createReplica(int brokerIdx, int partition, int index, bool isLeader, bool isOffline, int disk = -1);
   void setReplicaLoad(int replica, const Load& amv);  // amv carries the MetricValues as created by the caller
   void finalizeTopics();
   void setBrokerState(int brokerIdx, BrokerState s);
   void refreshCapacity();
+  // --- disks (JBOD)
+  int createDisk(int brokerIdx, const std::string& logdir, double capacity);  // BrokerCapacityInfo logdir entry
+  int diskOf(int brokerIdx, const std::string& logdir) const;                  // Broker.disk(logdir), -1 = null
+  void diskAddReplica(int d, int r);     // Disk.addReplica (Disk.java:113-121)
+  void diskRemoveReplica(int d, int r);  // Disk.removeReplica (:139-146)
+  void markDiskDead(int brokerIdx, int d);  // ClusterModel.markDiskDead -> Broker.markDiskDead (Broker.java:537-543)
+  double diskUtilizationPct(int d) const {  // GoalUtils.diskUtilizationPercentage (GoalUtils.java:397-400)
+    return disks[d].capacity > 0 ? disks[d].utilization / disks[d].capacity : 1.0;
+  }
+  double averageDiskUtilizationPct(int b) const;  // GoalUtils.averageDiskUtilizationPercentage (:379-389)
+  std::vector<int> replicaDiskFlat() const;       // [P][RF] disk of each replica slot (-1 = null)
+  // ClusterModel.relocateReplica(tp, brokerId, destinationLogdir) (ClusterModel.java:362-366)
+  void relocateReplicaToDisk(int partition, int brokerIdx, int dstDisk);
+  SortedReplicas& trackedDiskSortedReplicas(int d, const std::string& name);
+  std::vector<int> diskSortedReplicasClone(int d, const std::string& name);
 
   // --- queries
   Broker& broker(int idx) { return brokers[idx]; }
@@ -358,5 +392,13 @@ class ClusterModel {
   void sortedAdd(int b, int r);
   void sortedRemove(int b, int r);
 };
+
+// ((Double) x).intValue(): NaN -> 0, saturating, truncation toward zero (JLS 5.1.3)
+inline int32_t jDoubleToInt(double x) {
+  if (x != x) return 0;
+  if (x >= 2147483647.0) return 2147483647;
+  if (x <= -2147483648.0) return (int32_t)0x80000000;
+  return (int32_t)x;
+}
 
 }  // namespace oracle

@@ -25,33 +25,56 @@ std::unique_ptr<Goal> makeGoal(int kind, const BalancingConstraint& bc) {
     case CCMI_GOAL_NW_IN_USAGE_DISTRIBUTION: return std::make_unique<ResourceDistributionGoal>(bc, NW_IN);
     case CCMI_GOAL_NW_OUT_USAGE_DISTRIBUTION: return std::make_unique<ResourceDistributionGoal>(bc, NW_OUT);
     case CCMI_GOAL_CPU_USAGE_DISTRIBUTION: return std::make_unique<ResourceDistributionGoal>(bc, CPU);
+    case CCMI_GOAL_INTRA_BROKER_DISK_CAPACITY: return std::make_unique<IntraBrokerDiskCapacityGoal>(bc);
+    case CCMI_GOAL_INTRA_BROKER_DISK_USAGE_DISTRIBUTION:
+      return std::make_unique<IntraBrokerDiskUsageDistributionGoal>(bc);
     default: throw std::invalid_argument("goal kind not in oracle scope: " + std::to_string(kind));
   }
 }
 
-// GoalOptimizer.optimizations (GoalOptimizer.java:435-524)
+bool isIntraBrokerGoal(int kind) {
+  return kind == CCMI_GOAL_INTRA_BROKER_DISK_CAPACITY || kind == CCMI_GOAL_INTRA_BROKER_DISK_USAGE_DISTRIBUTION;
+}
+
+// GoalOptimizer.optimizations (GoalOptimizer.java:435-524). Distributions are ReplicaPlacementInfo lists: the broker
+// and (with JBOD placement) the disk of every replica slot (ClusterModel.getReplicaDistribution :167-182).
 OptimizerResult optimizations(ClusterModel& cm, const std::vector<int>& goalKinds, const BalancingConstraint& bc,
                               const OptimizationOptions& o) {
   using clk = std::chrono::steady_clock;
   auto t0 = clk::now();
   OptimizerResult res;
+  // Broker- and disk-granularity goals reject each other's actions with IllegalArgumentException (e.g.
+  // ResourceDistributionGoal.actionAcceptance default branch, IntraBrokerDiskCapacityGoal.actionAcceptance :120-124);
+  // a chain mixing them is refused up front.
+  int intra = 0;
+  for (int k : goalKinds) intra += isIntraBrokerGoal(k) ? 1 : 0;
+  if (intra != 0 && intra != (int)goalKinds.size())
+    throw std::invalid_argument("intra-broker goals cannot be optimized together with inter-broker goals");
+  if (intra != 0 && cm.disks.empty()) throw std::invalid_argument("intra-broker goals need replica placement over disks");
+  if (!o.excludedTopics.empty() && intra == 0)
+    throw std::invalid_argument("excluded topics are supported by the intra-broker goals only");
   std::vector<std::unique_ptr<Goal>> owned;
   for (int k : goalKinds) owned.push_back(makeGoal(k, bc));
-  std::vector<int> initDist = cm.replicaDistributionFlat();
-  std::vector<int> initLeaders = cm.leaderDistribution();
+  const std::vector<int> initDist = cm.replicaDistributionFlat(), initDisks = cm.replicaDiskFlat();
+  const std::vector<int> initLeaders = cm.leaderDistribution();
+  auto leaderDisks = [&]() {
+    std::vector<int> out;
+    for (const Partition& p : cm.partitions) out.push_back(cm.replicas[p.leader].disk);
+    return out;
+  };
+  const std::vector<int> initLeaderDisks = leaderDisks();
   res.initStats = computeStats(cm, bc, o);
   GoalList optimized;
-  std::vector<int> preDist, preLeaders;
+  std::vector<int> preDist = initDist, preDisks = initDisks, preLeaders = initLeaders, preLeaderDisks = initLeaderDisks;
   bool first = true;
   for (auto& g : owned) {
-    if (first) {
-      preDist = initDist;
-      preLeaders = initLeaders;
-      first = false;
-    } else {
+    if (!first) {
       preDist = cm.replicaDistributionFlat();
+      preDisks = cm.replicaDiskFlat();
       preLeaders = cm.leaderDistribution();
+      preLeaderDisks = leaderDisks();
     }
+    first = false;
     auto gs = clk::now();
     int64_t c0 = cm.candidatesEvaluated;
     size_t a0 = cm.actionLog.size();
@@ -64,33 +87,39 @@ OptimizerResult optimizations(ClusterModel& cm, const std::vector<int>& goalKind
     gr.seconds = std::chrono::duration<double>(clk::now() - gs).count();
     gr.candidates = cm.candidatesEvaluated - c0;
     gr.actions = (int64_t)(cm.actionLog.size() - a0);
-    gr.hasDiff = (cm.replicaDistributionFlat() != preDist) || (cm.leaderDistribution() != preLeaders);
+    gr.hasDiff = cm.replicaDistributionFlat() != preDist || cm.replicaDiskFlat() != preDisks ||
+                 cm.leaderDistribution() != preLeaders || leaderDisks() != preLeaderDisks;
     res.goals.push_back(gr);
   }
-  // AnalyzerUtils.getDiff
-  std::vector<int> finalDist = cm.replicaDistributionFlat();
+  // AnalyzerUtils.getDiff (AnalyzerUtils.java:63-93)
+  const std::vector<int> finalDist = cm.replicaDistributionFlat(), finalDisks = cm.replicaDiskFlat();
   size_t off = 0;
   for (size_t p = 0; p < cm.partitions.size(); ++p) {
     const Partition& part = cm.partitions[p];
-    size_t n = part.replicas.size();
+    const size_t n = part.replicas.size();
     std::vector<int> oldR(initDist.begin() + off, initDist.begin() + off + n);
     std::vector<int> newR(finalDist.begin() + off, finalDist.begin() + off + n);
+    std::vector<int> oldD(initDisks.begin() + off, initDisks.begin() + off + n);
+    std::vector<int> newD(finalDisks.begin() + off, finalDisks.begin() + off + n);
     off += n;
-    int finalLeader = cm.replicas[part.leader].broker;
-    if (oldR == newR && initLeaders[p] == finalLeader) continue;
-    if (newR[0] != finalLeader) {
-      int pos = 0;
-      for (size_t k = 0; k < n; ++k)
-        if (newR[k] == finalLeader) pos = (int)k;
-      newR[pos] = newR[0];
-      newR[0] = finalLeader;
-    }
+    const int finalLeader = cm.replicas[part.leader].broker, finalLeaderDisk = cm.replicas[part.leader].disk;
+    if (oldR == newR && oldD == newD && initLeaders[p] == finalLeader && initLeaderDisks[p] == finalLeaderDisk) continue;
+    int pos = 0;  // finalReplicas.indexOf(finalLeaderPlacementInfo), then swap with slot 0
+    for (size_t k = 0; k < n; ++k)
+      if (newR[k] == finalLeader && newD[k] == finalLeaderDisk) {
+        pos = (int)k;
+        break;
+      }
+    std::swap(newR[pos], newR[0]);
+    std::swap(newD[pos], newD[0]);
     Proposal pr;
     pr.partition = (int)p;
     pr.partitionSize = (int)cm.replicaUtil(part.leader, DISK);
     pr.oldLeader = initLeaders[p];
     pr.oldReplicas = oldR;
     pr.newReplicas = newR;
+    pr.oldDisks = oldD;
+    pr.newDisks = newD;
     res.proposals.push_back(std::move(pr));
   }
   res.seconds = std::chrono::duration<double>(clk::now() - t0).count();

@@ -25,6 +25,7 @@ struct Proposal {  // ExecutionProposal (executor/ExecutionProposal.java:58-)
   int partitionSize;  // (int) leader DISK util
   int oldLeader;
   std::vector<int> oldReplicas, newReplicas;  // broker ids, new list has the leader first
+  std::vector<int> oldDisks, newDisks;        // the logdir half of ReplicaPlacementInfo (disk index, -1 = null)
 };
 
 struct OptimizerResult {
@@ -36,6 +37,7 @@ struct OptimizerResult {
 };
 
 std::unique_ptr<Goal> makeGoal(int kind, const BalancingConstraint& bc);  // kinds: include/ccmi.h ccmi_goal_kind
+bool isIntraBrokerGoal(int kind);
 
 OptimizerResult optimizations(ClusterModel& cm, const std::vector<int>& goalKinds, const BalancingConstraint& bc,
                               const OptimizationOptions& o);

@@ -108,6 +108,9 @@ void* oc_random_cluster(const ccmi_random_cluster_props* p) {
   cp.distribution = p->distribution;
   cp.rackAware = p->rack_aware != 0;
   cp.leaderInFirstPosition = p->leader_in_first_position != 0;
+  cp.jbod = p->jbod;
+  cp.numLogdirs = p->num_logdirs;
+  for (int i = 0; i < 8; ++i) cp.logdirCapacity[i] = p->logdir_capacity[i];
   try {
     randomCluster(h->cm, cp);
   } catch (std::exception& e) {
@@ -130,6 +133,10 @@ void* oc_from_desc(const ccmi_cluster_desc* d) {
       cm.topicHash.push_back(jStringHash(cm.topicNames.back()));
       cm.numReplicasByTopic.push_back(0);
       cm.replicationFactorByTopic.push_back(0);
+    }
+    for (int k = 0; k < d->num_disks; ++k) {
+      if (cm.createDisk(d->disk_broker[k], d->disk_logdir[k], d->disk_capacity[k]) != k)
+        throw std::runtime_error("disk index mismatch");
     }
     std::vector<char> created(d->num_partitions, 0);
     const int W = d->num_windows;
@@ -155,7 +162,8 @@ void* oc_from_desc(const ccmi_cluster_desc* d) {
       }
       int b = d->replica_broker[r];
       int idx = (int)cm.partitions[p].replicas.size();
-      int rr = cm.createReplica(b, p, idx, d->replica_is_leader[r] != 0, d->replica_offline[r] != 0);
+      const int disk = (d->num_disks > 0 && d->replica_disk) ? d->replica_disk[r] : -1;
+      int rr = cm.createReplica(b, p, idx, d->replica_is_leader[r] != 0, d->replica_offline[r] != 0, disk);
       if (rr != r) throw std::runtime_error("replica index mismatch");
       if (!d->replica_load_order) setLoad(rr);
     }
@@ -167,6 +175,7 @@ void* oc_from_desc(const ccmi_cluster_desc* d) {
       lst.assign(d->partition_replicas + d->partition_offset[p], d->partition_replicas + d->partition_offset[p + 1]);
     }
     cm.finalizeTopics();
+    for (int i = 0; i < d->num_disk_assignments; ++i) cm.diskAddReplica(d->disk_assign_disk[i], d->disk_assign_replica[i]);
     for (int b = 0; b < d->num_brokers; ++b)
       if (d->broker_state[b] != CCMI_BROKER_ALIVE) cm.setBrokerState(b, (BrokerState)d->broker_state[b]);
   } catch (std::exception& e) {
@@ -220,6 +229,32 @@ void oc_export(void* hv, int32_t* broker_rack, int32_t* broker_state, double* ca
   }
 }
 
+// Disks of the initial model (valid before any optimization): count, then per disk broker / capacity / logdir, and
+// the Disk.addReplica replay (replicas created without a disk that were placed afterwards) in placement order.
+int32_t oc_num_disks(void* hv) { return (int32_t)((Handle*)hv)->cm.disks.size(); }
+const char* oc_disk_logdir(void* hv, int d) { return ((Handle*)hv)->cm.disks[d].logdir.c_str(); }
+void oc_export_disks(void* hv, int32_t* disk_broker, double* disk_capacity, int32_t* replica_disk) {
+  auto* h = (Handle*)hv;
+  for (size_t d = 0; d < h->cm.disks.size(); ++d) {
+    disk_broker[d] = h->cm.disks[d].broker;
+    disk_capacity[d] = h->cm.disks[d].capacity;
+  }
+  for (size_t r = 0; r < h->cm.replicas.size(); ++r) replica_disk[r] = h->cm.replicas[r].origDisk;
+}
+int64_t oc_num_disk_assignments(void* hv) { return (int64_t)((Handle*)hv)->cm.diskAssignLog.size(); }
+void oc_disk_assignments(void* hv, int32_t* replica, int32_t* disk) {
+  auto* h = (Handle*)hv;
+  for (size_t i = 0; i < h->cm.diskAssignLog.size(); ++i) {
+    replica[i] = h->cm.diskAssignLog[i].first;
+    disk[i] = h->cm.diskAssignLog[i].second;
+  }
+}
+void oc_replica_disks(void* hv, int32_t* out) {
+  auto v = ((Handle*)hv)->cm.replicaDiskFlat();
+  std::memcpy(out, v.data(), v.size() * sizeof(int32_t));
+}
+double oc_disk_utilization(void* hv, int d) { return ((Handle*)hv)->cm.disks[d].utilization; }
+
 int oc_optimize(void* hv, const int32_t* goals, int n, const ccmi_balancing_constraint* c, const ccmi_opt_options* o,
                 ccmi_goal_result* results) {
   auto* h = (Handle*)hv;
@@ -269,7 +304,7 @@ void oc_actions(void* hv, ccmi_action* out) {
   auto* h = (Handle*)hv;
   for (size_t i = 0; i < h->cm.actionLog.size(); ++i) {
     const ActionRecord& a = h->cm.actionLog[i];
-    out[i] = {a.type, a.partition, a.src, a.dst, a.destPartition};
+    out[i] = {a.type, a.partition, a.src, a.dst, a.destPartition, a.srcDisk, a.dstDisk};
   }
 }
 void oc_replica_distribution(void* hv, int32_t* out) {
@@ -296,6 +331,16 @@ void oc_proposals(void* hv, int max_rf, int32_t* partition, int32_t* size, int32
     for (int k = 0; k < max_rf; ++k) {
       old_out[i * max_rf + k] = k < (int)p.oldReplicas.size() ? p.oldReplicas[k] : -1;
       new_out[i * max_rf + k] = k < (int)p.newReplicas.size() ? p.newReplicas[k] : -1;
+    }
+  }
+}
+void oc_proposal_disks(void* hv, int max_rf, int32_t* old_out, int32_t* new_out) {
+  auto* h = (Handle*)hv;
+  for (size_t i = 0; i < h->last.proposals.size(); ++i) {
+    const Proposal& p = h->last.proposals[i];
+    for (int k = 0; k < max_rf; ++k) {
+      old_out[i * max_rf + k] = k < (int)p.oldDisks.size() ? p.oldDisks[k] : -1;
+      new_out[i * max_rf + k] = k < (int)p.newDisks.size() ? p.newDisks[k] : -1;
     }
   }
 }

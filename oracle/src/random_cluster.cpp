@@ -1,6 +1,7 @@
 // ORACLE — test infrastructure only (see jsem.h header).
 // RandomCluster.java:53-92 (generate), :119-336 (populate), :352-391 (dead broker marking),
-// :465-478 (uniformlyRandom / exponentialRandom). Math.log is glibc log (HotSpot's intrinsic is
+// :465-478 (uniformlyRandom / exponentialRandom), JBOD placement :315-331 with src/test/resources/
+// testCapacityConfigJBOD.json (BrokerCapacityConfigFileResolver: DISK = sum of the logdir capacities). Math.log is glibc log (HotSpot's intrinsic is
 // within 1 ulp; a rare last-bit difference is a documented residual generator risk).
 #include "random_cluster.h"
 
@@ -32,13 +33,39 @@ void randomCluster(ClusterModel& cm, const ClusterProperties& p) {
   if (p.numRacks > p.numBrokers || p.numBrokers <= 0 || p.numRacks <= 0) throw std::invalid_argument("bad input");
   cm.W = 1;
   for (int i = 0; i < p.numRacks; ++i) cm.createRack(std::to_string(i));
-  const double defCap[NUM_RESOURCES] = {100.0, 300000.0, 200000.0, 300000.0};  // CPU, NW_IN, NW_OUT, DISK
-  const double b1Cap[NUM_RESOURCES] = {100.0, 150000.0, 150000.0, 150000.0};
-  for (int i = 0; i < p.numRacks; ++i) cm.createBroker(i, i, i == 1 ? b1Cap : defCap);
-  for (int i = p.numRacks; i < p.numBrokers; ++i) {
-    int rack = uniformlyRandom(0, p.numRacks - 1, SEED_BASE + i);
-    cm.createBroker(rack, i, i == 1 ? b1Cap : defCap);
-  }
+  auto create = [&](int rack, int i) {
+    double cap[NUM_RESOURCES] = {100.0, 300000.0, 200000.0, 300000.0};  // CPU, NW_IN, NW_OUT, DISK
+    if (i == 1) {
+      cap[NW_IN] = 150000.0;
+      cap[NW_OUT] = 150000.0;
+      cap[DISK] = 150000.0;
+    }
+    std::vector<std::pair<std::string, double>> logdirs;
+    if (p.jbod == 1) {  // testCapacityConfigJBOD.json
+      if (i == 0) {
+        cap[CPU] = 200.0, cap[NW_IN] = 200000.0, cap[NW_OUT] = 200000.0;
+        logdirs = {{"/tmp/kafka-logs", 2000000.0}};
+      } else if (i == 1 || i == 2) {
+        cap[CPU] = 300.0, cap[NW_IN] = 300000.0, cap[NW_OUT] = 200000.0;
+        logdirs = {{"/tmp/kafka-logs-1", 350000.0}, {"/tmp/kafka-logs-2", 550000.0}};
+        if (i == 2) logdirs.insert(logdirs.end(), {{"/tmp/kafka-logs-3", 750000.0}, {"/tmp/kafka-logs-4", 950000.0}});
+      } else {
+        cap[CPU] = 100.0, cap[NW_IN] = 100000.0, cap[NW_OUT] = 100000.0;
+        for (int k = 1; k <= 10; ++k) logdirs.push_back({"/tmp/kafka-logs-" + std::to_string(k), k == 1 ? 400000.0 : 200000.0});
+      }
+    } else if (p.jbod == 2) {
+      for (int k = 0; k < p.numLogdirs; ++k) logdirs.push_back({"/mnt/data-" + std::to_string(k + 1), p.logdirCapacity[k]});
+    }
+    if (p.jbod) {
+      double total = 0.0;
+      for (const auto& l : logdirs) total += l.second;
+      cap[DISK] = total;
+    }
+    cm.createBroker(rack, i, cap);
+    for (const auto& l : logdirs) cm.createDisk(i, l.first, l.second);
+  };
+  for (int i = 0; i < p.numRacks; ++i) create(i, i);
+  for (int i = p.numRacks; i < p.numBrokers; ++i) create(uniformlyRandom(0, p.numRacks - 1, SEED_BASE + i), i);
   // populate
   const int numBrokers = p.numBrokers;
   if (p.numDeadBrokers < 0 || p.numBrokersWithBadDisk < 0 || numBrokers < p.numDeadBrokers + p.numBrokersWithBadDisk ||
@@ -156,6 +183,26 @@ void randomCluster(ClusterModel& cm, const ClusterProperties& p) {
     }
   }
   cm.finalizeTopics();
+  // Uniform-randomly assign replicas to disks (RandomCluster.java:315-331): brokers by id, Broker.replicas() HashSet
+  // order, conflict resolver per broker
+  if (p.jbod) {
+    for (int b = 0; b < (int)cm.brokers.size(); ++b) {
+      int resolver = 0, idx = 0;
+      const std::vector<int> dl = cm.brokers[b].disks;
+      const int n = (int)dl.size();
+      for (int r : cm.brokers[b].replicaSet.order()) {
+        const double du = cm.replicaUtil(r, DISK);
+        int a = uniformlyRandom(0, n - 1, REPLICA_ASSIGNMENT_SEED + idx);
+        while (cm.disks[dl[a]].capacity < cm.disks[dl[a]].utilization + du) {
+          resolver++;
+          a = uniformlyRandom(0, n - 1, REPLICA_ASSIGNMENT_SEED + idx + resolver);
+        }
+        cm.diskAddReplica(dl[a], r);
+        cm.diskAssignLog.push_back({r, dl[a]});
+        idx++;
+      }
+    }
+  }
   // markBrokenBrokers: dead brokers (no excluded topics in scope)
   if (p.numDeadBrokers > 0) {
     int idx = 0;
@@ -164,7 +211,16 @@ void randomCluster(ClusterModel& cm, const ClusterProperties& p) {
       idx++;
     }
   }
-  if (p.numBrokersWithBadDisk > 0) throw std::runtime_error("bad-disk marking not in round-1 scope");
+  if (p.numBrokersWithBadDisk > 0) {
+    if (!p.jbod) throw std::runtime_error("bad-disk marking without disks is not restated");
+    int marked = 0;  // one (the first, TreeMap order) disk of each of the first alive brokers
+    for (int b = 0; b < (int)cm.brokers.size() && marked < p.numBrokersWithBadDisk; ++b) {
+      if (!cm.brokers[b].isAlive()) continue;
+      cm.markDiskDead(b, cm.brokers[b].disks.front());
+      cm.setBrokerState(b, BrokerState::BAD_DISKS);
+      marked++;
+    }
+  }
 }
 
 }  // namespace oracle

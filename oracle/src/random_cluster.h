@@ -23,6 +23,11 @@ struct ClusterProperties {
   int distribution = 0;  // 0 UNIFORM, 1 LINEAR, 2 EXPONENTIAL
   bool rackAware = false;
   bool leaderInFirstPosition = true;
+  // POPULATE_REPLICA_PLACEMENT_INFO (ccmi_random_cluster_props.jbod): 1 = testCapacityConfigJBOD.json,
+  // 2 = numLogdirs logdirs "/mnt/data-<i>" with logdirCapacity[] on every broker
+  int jbod = 0;
+  int numLogdirs = 0;
+  double logdirCapacity[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 };
 
 // generate() + populate(); returns a fully loaded model (W = 1).

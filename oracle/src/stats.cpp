@@ -160,9 +160,26 @@ ClusterModelStats computeStats(const ClusterModel& cm, const BalancingConstraint
     s.topicMin = mnAcc;
     s.topicStd = stdAcc / s.numTopics;
   }
-  // populateStatsForDisks: no JBOD disks in the in-scope configs C0-C3
-  s.numUnbalancedDisks = 0;
-  s.diskUtilizationStDev = 0.0;
+  // populateStatsForDisks (ClusterModelStats.java:489-511)
+  {
+    double totalVariance = 0;
+    int numAliveDisks = 0;
+    s.numUnbalancedDisks = 0;
+    s.diskUtilizationStDev = 0.0;
+    for (int b : alive) {
+      const double brokerPct = cm.averageDiskUtilizationPct(b);
+      const double upper = brokerPct * bc.resourceBalancePercentage[DISK];
+      const double lower = brokerPct * jmax(0, (2 - bc.resourceBalancePercentage[DISK]));
+      for (int d : cm.brokers[b].disks) {
+        if (!cm.disks[d].alive) continue;
+        const double pct = cm.diskUtilizationPct(d);
+        if (pct > upper || pct < lower) s.numUnbalancedDisks++;
+        totalVariance += std::pow(pct - brokerPct, 2);
+        numAliveDisks++;
+      }
+    }
+    if (numAliveDisks > 0) s.diskUtilizationStDev = std::sqrt(totalVariance / numAliveDisks);
+  }
   return s;
 }
 

@@ -12,6 +12,7 @@
 
 #include "apply.h"
 #include "device.h"
+#include "intra.h"
 #include "predicates.h"
 #include "shard_rccl.h"
 
@@ -36,6 +37,13 @@ struct Emu {
   int W = 1;
   std::vector<LoadVec> lRep, lBrk, lLnw, lPot;
   std::vector<int32_t> pSlots, pLeader;
+  // disk state (device.h uploadDisks)
+  int D = 0;
+  std::vector<int32_t> bDiskOff, bDisks, rOrigDisk, rTie;
+  std::vector<double> dCap, dUtilIn, dUtil, rDu, upper, lower;
+  std::vector<uint8_t> dAlive, dbAlive;
+  std::vector<float> rScore;
+  std::vector<int32_t> hist;
 };
 struct View {
   const Emu& e;
@@ -521,6 +529,142 @@ void Device::stats(const StatsParams& P, const uint8_t* aa, StatsOut* out) {
   out->topicStd = sdSum / P.T;
   out->topicMax = tmx;
   out->topicMin = tmn;
+}
+
+// ------------------------------------------------------------------------------------------------ K6 (sequential)
+void Device::uploadDisks(int D, const int32_t* bDiskOff, const int32_t* bDisks, const double* dCap,
+                         const uint8_t* dAlive, const uint8_t* bAlive, const int32_t* rOrigDisk, const double* rDu,
+                         const float* rScore, const int32_t* rTie) {
+  Emu& e = E(st_);
+  e.D = D;
+  e.bDiskOff.assign(bDiskOff, bDiskOff + B_ + 1);
+  e.bDisks.assign(bDisks, bDisks + D);
+  e.dCap.assign(dCap, dCap + D);
+  e.dAlive.assign(dAlive, dAlive + D);
+  e.dbAlive.assign(bAlive, bAlive + B_);
+  e.rOrigDisk.assign(rOrigDisk, rOrigDisk + R_);
+  e.rDu.assign(rDu, rDu + R_);
+  e.rScore.assign(rScore, rScore + R_);
+  e.rTie.assign(rTie, rTie + R_);
+  e.dUtilIn.assign(D, 0.0);
+  e.dUtil.assign(D, 0.0);
+  e.upper.assign((size_t)G_ * B_, 0.0);
+  e.lower.assign((size_t)G_ * B_, 0.0);
+  e.hist.assign((size_t)B_ * kIntraHist * (kIntraMaxDisks + 1), 0);
+}
+
+void Device::setDiskUtil(const double* dUtil) {
+  Emu& e = E(st_);
+  e.dUtilIn.assign(dUtil, dUtil + e.D);
+}
+
+void Device::intraRun(const IntraRequest& q, IntraResult& out) {
+  Emu& e = E(st_);
+  const int E_ = q.eOff[B_];
+  std::vector<int32_t> eDisk(q.eDisk, q.eDisk + E_), snapA(E_ + 1), snapB(E_ + 1);
+  std::vector<int64_t> logOff(B_, 0);
+  std::vector<int32_t> cap(B_, 0);
+  int64_t total = 0;
+  for (int i = 0; i < q.nBrokers; ++i) {  // the bound of a broker's program (device.cpp re-runs with it)
+    const int b = q.brokers[i];
+    logOff[b] = total;
+    cap[b] = (int32_t)(6 * (e.bDiskOff[b + 1] - e.bDiskOff[b] + 1) * (q.eOff[b + 1] - q.eOff[b]) + 64);
+    total += cap[b];
+  }
+  std::vector<int32_t> rep(total + 1), src(total + 1), dst(total + 1);
+  out.count.assign(B_, 0);
+  out.status.assign(B_, 0);
+  out.cand.assign(B_, 0);
+  IntraArgs A{};
+  A.goal = q.goal;
+  A.capThr = q.capThr;
+  A.margin = q.margin;
+  A.nPrior = q.nPrior;
+  for (int k = 0; k < q.nPrior; ++k) {
+    A.prior[k].kind = q.priorKind[k];
+    A.prior[k].upper = e.upper.data() + (size_t)q.priorSlot[k] * B_;
+    A.prior[k].lower = e.lower.data() + (size_t)q.priorSlot[k] * B_;
+  }
+  A.brokers = q.brokers;
+  A.nBrokers = q.nBrokers;
+  A.bDiskOff = e.bDiskOff.data();
+  A.bDisks = e.bDisks.data();
+  A.dCap = e.dCap.data();
+  A.dAlive = e.dAlive.data();
+  A.dUtilIn = e.dUtilIn.data();
+  A.dUtil = e.dUtil.data();
+  A.eOff = q.eOff;
+  A.eRep = q.eRep;
+  A.eDiskIn = q.eDisk;
+  A.eDisk = eDisk.data();
+  A.rDu = e.rDu.data();
+  A.rScore = e.rScore.data();
+  A.rTie = e.rTie.data();
+  A.rOrigDisk = e.rOrigDisk.data();
+  A.rSel = q.rSel;
+  A.snapA = snapA.data();
+  A.snapB = snapB.data();
+  A.hist = e.hist.data();
+  A.upperOut = e.upper.data() + (size_t)q.slot * B_;
+  A.lowerOut = e.lower.data() + (size_t)q.slot * B_;
+  A.logOff = logOff.data();
+  A.logCap = cap.data();
+  A.logRep = rep.data();
+  A.logSrc = src.data();
+  A.logDst = dst.data();
+  A.logCount = out.count.data();
+  A.status = out.status.data();
+  A.cand = out.cand.data();
+  for (int i = 0; i < q.nBrokers; ++i) {
+    IntraBroker ib(A, q.brokers[i]);
+    ib.run();
+  }
+  perf.intraLaunches++;
+  out.off.assign(B_ + 1, 0);
+  for (int b = 0; b < B_; ++b) out.off[b + 1] = out.off[b] + out.count[b];
+  out.rep.resize(out.off[B_]);
+  out.src.resize(out.off[B_]);
+  out.dst.resize(out.off[B_]);
+  for (int b = 0; b < B_; ++b)
+    for (int k = 0; k < out.count[b]; ++k) {
+      out.rep[out.off[b] + k] = rep[logOff[b] + k];
+      out.src[out.off[b] + k] = src[logOff[b] + k];
+      out.dst[out.off[b] + k] = dst[logOff[b] + k];
+    }
+  if (q.goal == IG_USAGE) {
+    out.upper.assign(e.upper.begin() + (size_t)q.slot * B_, e.upper.begin() + (size_t)(q.slot + 1) * B_);
+    out.lower.assign(e.lower.begin() + (size_t)q.slot * B_, e.lower.begin() + (size_t)(q.slot + 1) * B_);
+  }
+}
+
+void Device::statsDisks(double balance, DiskStatsOut* out) {
+  Emu& e = E(st_);
+  double var = 0;
+  int unb = 0, na = 0;
+  for (int b = 0; b < B_; ++b) {
+    if (!e.dbAlive[b]) continue;
+    double cap = 0, util = 0;
+    for (int k = e.bDiskOff[b]; k < e.bDiskOff[b + 1]; ++k) {
+      const int d = e.bDisks[k];
+      if (e.dAlive[d]) {
+        cap += e.dCap[d];
+        util += e.dUtilIn[d];
+      }
+    }
+    const double avg = cap > 0 ? util / cap : 1.0;
+    const double upper = avg * balance, lm = 2 - balance, lower = avg * (lm > 0 ? lm : 0.0);
+    for (int k = e.bDiskOff[b]; k < e.bDiskOff[b + 1]; ++k) {
+      const int d = e.bDisks[k];
+      if (!e.dAlive[d]) continue;
+      const double pct = e.dCap[d] > 0 ? e.dUtilIn[d] / e.dCap[d] : 1.0;
+      if (pct > upper || pct < lower) unb++;
+      var += (pct - avg) * (pct - avg);
+      na++;
+    }
+  }
+  out->varSum = var;
+  out->unbalanced = unb;
+  out->numAlive = na;
 }
 
 }  // namespace ccmi

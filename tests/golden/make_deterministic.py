@@ -7,6 +7,8 @@ given per model, paths relative to cruise-control/src/test/java/com/linkedin/kaf
   loads     ClusterModel.setReplicaLoad(rack, broker, tp, getAggregatedMetricValues(cpu, nwIn, nwOut, disk))
             in call order (KafkaCruiseControlUnitTestUtils.java:90-100)
   dead      ClusterModel.setBrokerState(id, DEAD)
+  logdirs   JBOD models: every broker's disk capacity by logdir (getHomogeneousCluster diskCapacityByLogDir) and the
+            logdir given to createReplica (6th replica field)
 The tests replay the calls through ccmi.ClusterModelBuilder (every createReplica first, then the loads in their
 call order; for the models here that yields the same aggregates as the Java call interleaving, because every
 follower created after its leader's load would receive exactly the leader's load either way).
@@ -38,8 +40,8 @@ class Model:
         self.d = dict(source=source, racks={str(b): str(r) for b, r in rack_by_broker.items()},
                       capacity=dict(capacity or BROKER_CAPACITY), replicas=[], loads=[], dead=[])
 
-    def create(self, broker, topic, partition, index, leader):
-        self.d["replicas"].append([broker, topic, partition, index, bool(leader)])
+    def create(self, broker, topic, partition, index, leader, logdir=None):
+        self.d["replicas"].append([broker, topic, partition, index, bool(leader)] + ([logdir] if logdir else []))
         return self
 
     def load(self, broker, topic, partition, cpu, nw_in, nw_out, disk):
@@ -162,6 +164,27 @@ def medium_cluster_model(capacity=None, tag=""):  # DeterministicCluster.java:18
     return m
 
 
+# common/TestConstants.java:100-110
+LOGDIR0, LOGDIR1 = "/mnt/i00", "/mnt/i01"
+DISK_CAPACITY = {LOGDIR0: LARGE_BROKER_CAPACITY / 2, LOGDIR1: LARGE_BROKER_CAPACITY / 2}
+
+
+def create_unbalanced(topics, num_partitions, source):  # DeterministicCluster.java:81-108 createUnbalanced
+    m = Model(source, {0: 0, 1: 1})
+    m.d["logdirs"] = dict(DISK_CAPACITY)
+    for topic in topics:
+        for i in range(num_partitions):
+            broker = 1 if i > 3 else 0
+            logdir = LOGDIR0 if i % 4 < 2 else LOGDIR1
+            m.create(broker, topic, i, 0, True, logdir)
+            f = i / 2.0 - 1.5
+            m.load(broker, topic, i, TYPICAL_CPU_CAPACITY / 5 + TYPICAL_CPU_CAPACITY / 50 * f,
+                   LARGE_BROKER_CAPACITY / 5 + LARGE_BROKER_CAPACITY / 50 * f,
+                   MEDIUM_BROKER_CAPACITY / 5 + MEDIUM_BROKER_CAPACITY / 50 * f,
+                   LARGE_BROKER_CAPACITY / 5 + LARGE_BROKER_CAPACITY / 50 * f)
+    return m
+
+
 def rack_id_mapper_cluster(mapped):  # analyzer/RackAwareGoalTest.java:74-100 and :137-161
     # brokerToRack = {0: "A::0", 1: "B::0", 2: "C::1"}; IgnorePrefixRackIdMapper strips the "X::" prefix
     racks = {0: "A::0", 1: "B::0", 2: "C::1"}
@@ -187,6 +210,9 @@ def models():
         "smallClusterModel": small_cluster_model(), "mediumClusterModel": medium_cluster_model(),
         "deadBroker": dead_broker(),
         "rackIdMapper": rack_id_mapper_cluster(True), "withoutRackIdMapper": rack_id_mapper_cluster(False),
+        "unbalanced4": create_unbalanced([T1], 8, "DeterministicCluster.java:77-108 unbalanced4()"),
+        # Set.of(T1, T2) iterates in a per-JVM salted order; transcribed as T1 then T2
+        "unbalanced5": create_unbalanced([T1, T2], 14, "DeterministicCluster.java:113-116 unbalanced5() (T1, T2)"),
     }
     # DeterministicClusterTest deck #5 (DeterministicClusterTest.java:181-197): uniform capacities
     for name, c in (("LARGE", LARGE_BROKER_CAPACITY), ("MEDIUM", MEDIUM_BROKER_CAPACITY),

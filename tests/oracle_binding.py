@@ -69,6 +69,19 @@ class Oracle:
             L.oc_set_deadline.argtypes = [C.c_void_p, C.c_double]
             L.oc_stats_seconds.restype = C.c_double
             L.oc_stats_seconds.argtypes = [C.c_void_p]
+            L.oc_num_disks.restype = C.c_int32
+            L.oc_num_disks.argtypes = [C.c_void_p]
+            L.oc_disk_logdir.restype = C.c_char_p
+            L.oc_disk_logdir.argtypes = [C.c_void_p, C.c_int]
+            L.oc_export_disks.argtypes = [C.c_void_p, C.POINTER(C.c_int32), C.POINTER(C.c_double),
+                                          C.POINTER(C.c_int32)]
+            L.oc_num_disk_assignments.restype = C.c_int64
+            L.oc_num_disk_assignments.argtypes = [C.c_void_p]
+            L.oc_disk_assignments.argtypes = [C.c_void_p, C.POINTER(C.c_int32), C.POINTER(C.c_int32)]
+            L.oc_replica_disks.argtypes = [C.c_void_p, C.POINTER(C.c_int32)]
+            L.oc_disk_utilization.restype = C.c_double
+            L.oc_disk_utilization.argtypes = [C.c_void_p, C.c_int]
+            L.oc_proposal_disks.argtypes = [C.c_void_p, C.c_int] + [C.POINTER(C.c_int32)] * 2
             L.oc_balance_threshold.restype = C.c_double
             L.oc_balance_threshold.argtypes = [C.c_double, C.c_int, C.c_double, C.c_double, C.c_double, C.c_int,
                                                C.c_double, C.c_int]
@@ -115,6 +128,17 @@ class OracleCluster:
                          a["replica_broker"], a["is_leader"], a["offline"], a["load"])
         out = {k: list(v) for k, v in a.items()}
         out["topics"] = [self.L.oc_topic_name(self.h, t).decode() for t in range(T)]
+        D = self.L.oc_num_disks(self.h)
+        out["num_disks"] = D
+        if D:
+            db, dc, rd = (C.c_int32 * D)(), (C.c_double * D)(), (C.c_int32 * R)()
+            self.L.oc_export_disks(self.h, db, dc, rd)
+            n = self.L.oc_num_disk_assignments(self.h)
+            ar, ad = (C.c_int32 * max(1, n))(), (C.c_int32 * max(1, n))()
+            self.L.oc_disk_assignments(self.h, ar, ad)
+            out.update(disk_broker=list(db), disk_capacity=list(dc), replica_disk=list(rd),
+                       disk_logdir=[self.L.oc_disk_logdir(self.h, d).decode() for d in range(D)],
+                       disk_assign_replica=list(ar[:n]), disk_assign_disk=list(ad[:n]))
         return out
 
     def optimize(self, goal_names: List[str], constraint: Optional[ccmi.BalancingConstraint] = None,
@@ -152,8 +176,16 @@ class OracleCluster:
         n = self.L.oc_action_count(self.h)
         buf = (ccmi.ActionStruct * max(1, n))()
         self.L.oc_actions(self.h, buf)
-        return [(a.type, a.partition, a.source_broker, a.destination_broker, a.destination_partition)
-                for a in buf[:n]]
+        return [(a.type, a.partition, a.source_broker, a.destination_broker, a.destination_partition,
+                 a.source_disk, a.destination_disk) for a in buf[:n]]
+
+    def replica_disks(self) -> List[int]:
+        out = (C.c_int32 * self.R)()
+        self.L.oc_replica_disks(self.h, out)
+        return list(out)
+
+    def disk_utilization(self, d: int) -> float:
+        return self.L.oc_disk_utilization(self.h, d)
 
     def replica_distribution(self) -> List[int]:
         out = (C.c_int32 * self.R)()
@@ -179,18 +211,32 @@ class OracleCluster:
         part, size, old_leader = (C.c_int32 * n)(), (C.c_int32 * n)(), (C.c_int32 * n)()
         old_r, new_r = (C.c_int32 * (n * max_rf))(), (C.c_int32 * (n * max_rf))()
         self.L.oc_proposals(self.h, max_rf, part, size, old_leader, old_r, new_r)
-        return [ccmi.ExecutionProposal(part[i], size[i], old_leader[i],
-                                       [x for x in old_r[i * max_rf:(i + 1) * max_rf] if x >= 0],
-                                       [x for x in new_r[i * max_rf:(i + 1) * max_rf] if x >= 0]) for i in range(n)]
+        old_d, new_d = (C.c_int32 * (n * max_rf))(), (C.c_int32 * (n * max_rf))()
+        self.L.oc_proposal_disks(self.h, max_rf, old_d, new_d)
+        out = []
+        for i in range(n):
+            rf = sum(1 for x in old_r[i * max_rf:(i + 1) * max_rf] if x >= 0)
+            out.append(ccmi.ExecutionProposal(part[i], size[i], old_leader[i], list(old_r[i * max_rf:i * max_rf + rf]),
+                                              list(new_r[i * max_rf:i * max_rf + rf]),
+                                              list(old_d[i * max_rf:i * max_rf + rf]),
+                                              list(new_d[i * max_rf:i * max_rf + rf])))
+        return out
 
 
 def desc_arrays(desc: ccmi.ClusterDesc) -> dict:
     """Flattened desc as python lists (same keys as OracleCluster.export)."""
     B, P, R, W, T = desc.num_brokers, desc.num_partitions, desc.num_replicas, desc.num_windows, desc.num_topics
-    return dict(broker_rack=desc.broker_rack[:B], broker_state=desc.broker_state[:B],
+    out = dict(broker_rack=desc.broker_rack[:B], broker_state=desc.broker_state[:B],
                 cap=desc.broker_capacity[:4 * B], partition_topic=desc.partition_topic[:P],
                 partition_number=desc.partition_number[:P], partition_offset=desc.partition_offset[:P + 1],
                 partition_replicas=desc.partition_replicas[:R], replica_partition=desc.replica_partition[:R],
                 replica_broker=desc.replica_broker[:R], is_leader=desc.replica_is_leader[:R],
                 offline=desc.replica_offline[:R], load=desc.replica_load[:R * 6 * W],
-                topics=[desc.topic_names[t].decode() for t in range(T)])
+                topics=[desc.topic_names[t].decode() for t in range(T)], num_disks=desc.num_disks)
+    D, n = desc.num_disks, desc.num_disk_assignments
+    if D:
+        out.update(disk_broker=desc.disk_broker[:D], disk_capacity=desc.disk_capacity[:D],
+                   replica_disk=desc.replica_disk[:R] if desc.replica_disk else [-1] * R,
+                   disk_logdir=[desc.disk_logdir[d].decode() for d in range(D)],
+                   disk_assign_replica=desc.disk_assign_replica[:n], disk_assign_disk=desc.disk_assign_disk[:n])
+    return out

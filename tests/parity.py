@@ -17,21 +17,23 @@ def golden(name):
         return json.load(f)
 
 
-def constraint(balance, max_replicas=None):
+def constraint(balance, max_replicas=None, capacity=None):
     bc = ccmi.BalancingConstraint()
     if balance is not None:
         bc.set_resource_balance_percentage(balance)
         bc.set_capacity_threshold(0.8)
+    if capacity is not None:
+        bc.set_capacity_threshold(capacity)
     if max_replicas is not None:
         bc.max_replicas_per_broker = max_replicas
     return bc
 
 
-def run_product(lib, props, goals, balance, device=0, max_replicas=None, options=None):
+def run_product(lib, props, goals, balance, device=0, max_replicas=None, options=None, capacity=None):
     buf = ccmi.RandomCluster.generate(lib, **props)
     cm = ccmi.ClusterModel.from_buffers(buf, device=device)
-    res = ccmi.GoalOptimizer(constraint(balance, max_replicas)).optimizations(cm, ccmi.goals_from_names(goals),
-                                                                               options)
+    res = ccmi.GoalOptimizer(constraint(balance, max_replicas, capacity)).optimizations(
+        cm, ccmi.goals_from_names(goals), options)
     return buf, cm, res
 
 
@@ -44,9 +46,10 @@ def check_product_against_golden(lib, name, per_goal_stats=False):
     actions) and final stats; with per_goal_stats every goal's ClusterModelStats (goldens that store them)."""
     g = golden(name)
     buf, cm, res = run_product(lib, g["props"], g["goals"], g["resource_balance_percentage"],
-                               max_replicas=g.get("max_replicas_per_broker"), options=golden_options(g))
+                               max_replicas=g.get("max_replicas_per_broker"), options=golden_options(g),
+                               capacity=g.get("capacity_threshold"))
     check_against_golden(g, cm.actions(), cm.replica_distribution(), cm.leader_distribution(), res.goal_results,
-                         res.goal_results[-1].stats)
+                         res.goal_results[-1].stats, replica_disks=cm.replica_disks())
     if per_goal_stats:
         for r, e in zip(res.goal_results, g["goals_result"]):
             if "stats" in e:
@@ -62,7 +65,8 @@ def compare_stats(a, b, rel=1e-9):
 
 
 def _key(p):
-    return p.partition, p.partition_size, p.old_leader, tuple(p.old_replicas), tuple(p.new_replicas)
+    return (p.partition, p.partition_size, p.old_leader, tuple(p.old_replicas), tuple(p.new_replicas),
+            tuple(p.old_disks or ()), tuple(p.new_disks or ()))
 
 
 def check_product_against_oracle(lib, props, goals, balance=None, device=0, max_replicas=None, options=None):
@@ -97,6 +101,7 @@ def check_desc_against_oracle(lib, desc, keepalive, goals, bc, options=None, dev
     assert len(pa) == len(oa)
     assert cm.replica_distribution() == oc.replica_distribution()
     assert cm.leader_distribution() == oc.leader_distribution()
+    assert cm.replica_disks() == oc.replica_disks()
     for r, o in zip(res.goal_results, ores):
         assert (r.name, r.succeeded, r.candidates, r.actions) == (o.name, o.succeeded, o.candidates, o.actions), \
             ((r.name, r.succeeded, r.candidates, r.actions), (o.name, o.succeeded, o.candidates, o.actions))

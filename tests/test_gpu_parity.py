@@ -18,7 +18,7 @@ def test_gpu_matches_golden(gpu_lib, oracle_lib, name):
     cm, res = check_product_against_golden(gpu_lib, name)
     # the device path ran (no host fallback exists; this guards the counters the bench relies on)
     assert sum(g.device_launches for g in res.goal_results) > 0
-    assert cm.perf().scan_launches > 0
+    assert cm.perf().scan_launches + cm.perf().intra_launches > 0
 
 
 # The headline configurations (BASELINE configs[2] and [3]) and C2 with the C1 goal chain, against committed oracle

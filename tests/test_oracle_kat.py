@@ -102,13 +102,25 @@ def _constraint(g):
     if g["resource_balance_percentage"] is not None:
         bc.set_resource_balance_percentage(g["resource_balance_percentage"])
         bc.set_capacity_threshold(0.8)
+    if g.get("capacity_threshold") is not None:
+        bc.set_capacity_threshold(g["capacity_threshold"])
     if g.get("max_replicas_per_broker") is not None:
         bc.max_replicas_per_broker = g["max_replicas_per_broker"]
     return bc
 
 
-def check_against_golden(g, actions, replica_dist, leader_dist, goal_results, final_stats, rel=1e-9):
+def golden_action(a):
+    """Action tuples of models without disks keep their 5-field golden form (the disk fields are -1)."""
+    a = tuple(a)
+    return a[:5] if len(a) == 7 and a[5] == -1 and a[6] == -1 else a
+
+
+def check_against_golden(g, actions, replica_dist, leader_dist, goal_results, final_stats, rel=1e-9,
+                         replica_disks=None):
     """Shared by the oracle, emulation and GPU tests."""
+    actions = [golden_action(a) for a in actions]
+    if "replica_disks_sha256" in g:  # JBOD goldens: the logdir half of every ReplicaPlacementInfo
+        assert replica_disks is not None and _sha(replica_disks) == g["replica_disks_sha256"]
     if "actions" in g:
         for i, (x, y) in enumerate(zip(actions, g["actions"])):
             assert tuple(x) == tuple(y), f"first action mismatch at {i}"
@@ -126,7 +138,7 @@ def check_against_golden(g, actions, replica_dist, leader_dist, goal_results, fi
 
 
 GOLDEN_CASES = ["small_20b", "dead_2of10", "rack_aware_dead", "c0", "c1", "small_20b_default", "dead_3of24_default",
-                "rack_aware_dead_default", "c0_default"]
+                "rack_aware_dead_default", "c0_default", "jbod_base", "jbod_base_cap15"]
 
 
 @pytest.mark.parametrize("name", GOLDEN_CASES)
@@ -136,4 +148,4 @@ def test_oracle_matches_golden(oracle_lib, name):
     assert (oc.B, oc.T, oc.P, oc.R) == tuple(g["sizes"][k] for k in ("brokers", "topics", "partitions", "replicas"))
     res = oc.optimize(g["goals"], _constraint(g))
     check_against_golden(g, oc.actions(), oc.replica_distribution(), oc.leader_distribution(), res, res[-1].stats,
-                         rel=0.0)
+                         rel=0.0, replica_disks=oc.replica_disks())

@@ -60,6 +60,13 @@ def _leader_bytes_in_cmp(after, before, bc):  # LeaderBytesInDistributionGoal.ja
     return _compare_res(math.sqrt(before["resource_std"][1]), math.sqrt(after["resource_std"][1]), 1)
 
 
+def _intra_usage_cmp(after, before, bc):  # IntraBrokerDiskUsageDistributionGoal.java:501-517
+    if (after["num_unbalanced_disks"] > before["num_unbalanced_disks"]
+            or after["disk_utilization_std"] > before["disk_utilization_std"]):
+        return -1
+    return 1
+
+
 def _potential_nw_out_cmp(after, before, bc):  # PotentialNwOutGoal.java:350-360
     a, b = after["num_brokers_under_potential_nw_out"], before["num_brokers_under_potential_nw_out"]
     return (a > b) - (a < b)
@@ -75,6 +82,7 @@ COMPARATORS = {
     "NetworkOutboundUsageDistributionGoal": _resource_distribution_cmp(2),
     "DiskUsageDistributionGoal": _resource_distribution_cmp(3),
     "LeaderBytesInDistributionGoal": _leader_bytes_in_cmp,
+    "IntraBrokerDiskUsageDistributionGoal": _intra_usage_cmp,
 }  # hard goals, MinTopicLeaders, PreferredLeaderElection: comparisons are irrelevant (return 0)
 
 
@@ -118,9 +126,9 @@ def build_model(m: dict) -> ccmi.FlatCluster:
     """Replay one transcribed DeterministicCluster model through ClusterModelBuilder."""
     b = ccmi.ClusterModelBuilder()
     for bid in sorted(m["racks"], key=int):
-        b.create_broker(m["racks"][bid], int(bid), m["capacity"])
-    for broker, topic, part, index, leader in m["replicas"]:
-        b.create_replica(m["racks"][str(broker)], broker, topic, part, index, leader)
+        b.create_broker(m["racks"][bid], int(bid), m["capacity"], m.get("logdirs"))
+    for broker, topic, part, index, leader, *logdir in m["replicas"]:
+        b.create_replica(m["racks"][str(broker)], broker, topic, part, index, leader, logdir=logdir[0] if logdir else None)
     for broker, topic, part, cpu, nw_in, nw_out, disk in m["loads"]:
         b.set_replica_load(m["racks"][str(broker)], broker, topic, part, cpu, nw_in, nw_out, disk)
     for d in m["dead"]:
