@@ -3,7 +3,8 @@
 Workload (default, BASELINE.json configs[2] — the configuration the metric is quoted on, and it fits one GPU):
 RandomCluster C2 = 100 racks, 10 000 brokers, 999 999 + 20 000 replicas (R = 1 019 999), 10 001 topics, W = 1,
 uniform loads, TestConstants seeds; the 16 default goals in default priority order; default BalancingConstraint.
---workload c1 / c3 / c2_c1goals / c0 select the other BASELINE configs (parity-test cases, not headline lines).
+--workload c1 / c3 / c4 / c2_c1goals / c0 select the other BASELINE configs (parity-test cases, not headline lines);
+c4 (JBOD, the intra-broker goals) reports the K6 kernel in its roofline.
 
 A "step" is one full GoalOptimizer.optimizations over that cluster (every goal, ClusterModelStats after every goal,
 final ExecutionProposals). Each step works on its own device session, uploaded to HBM before the timed region
@@ -49,19 +50,35 @@ C1_PROPS = dict(num_racks=20, num_brokers=1000, num_replicas=99999, num_topics=3
 C2_PROPS = dict(num_racks=100, num_brokers=10000, num_replicas=999999, num_topics=10000)
 # C3: RandomSelfHealingTest-style placement (6-arg populate, rack-aware, leader first; RandomCluster.java:119-124)
 C3_PROPS = dict(C2_PROPS, num_dead_brokers=500, rack_aware=1, leader_in_first_position=1)
+# C4: the C2 cluster on 4 x 75 000 MB logdirs per broker, rack-aware populate (tests/golden/make_golden.py C4_PROPS)
+C4_PROPS = dict(C2_PROPS, rack_aware=1, leader_in_first_position=1, jbod=2, num_logdirs=4,
+                logdir_capacity=[75000.0] * 4)
 C1_GOALS = list(ccmi.C1_GOALS)
 DEFAULT_GOALS = list(ccmi.DEFAULT_GOALS)
+INTRA_GOALS = list(ccmi.INTRA_BROKER_GOALS)
 WORKLOADS = {"c1": (C1_PROPS, C1_GOALS, "C1: 1K brokers x 100K replicas, 5 distribution goals (BASELINE configs[1])"),
              "c2": (C2_PROPS, DEFAULT_GOALS, "C2: 10K brokers x 1M replicas, the 16 default goals (BASELINE configs[2])"),
              "c2_c1goals": (C2_PROPS, C1_GOALS, "C2 cluster with the C1 goal list"),
              "c3": (C3_PROPS, DEFAULT_GOALS, "C3: C2 with brokers 0..499 DEAD, requested destinations 500..1499, the 16 "
                                            "default goals (BASELINE configs[3], RemoveBrokersRunnable options)"),
+             "c4": (C4_PROPS, INTRA_GOALS, "C4: JBOD C2 cluster x 4 logdirs, IntraBrokerDiskCapacityGoal + "
+                                          "IntraBrokerDiskUsageDistributionGoal with its swap phase (BASELINE configs[4])"),
              "c0": ({}, DEFAULT_GOALS, "C0: TestConstants.BASE_PROPERTIES, the 16 default goals (BASELINE configs[0])")}
+
+
+def workload_constraint(workload: str) -> "ccmi.BalancingConstraint":
+    """Default BalancingConstraint; C4 uses IntraBrokerRebalanceTest's (IntraBrokerRebalanceTest.java:103-111)."""
+    bc = ccmi.BalancingConstraint()
+    if workload == "c4":
+        bc.max_replicas_per_broker = 2000
+        bc.set_resource_balance_percentage(1.05)
+        bc.set_capacity_threshold(0.8)
+    return bc
 # Per-workload OptimizationOptions (C3: the 7-arg options RemoveBrokersRunnable.java:107-126 builds)
 WORKLOAD_OPTIONS = {"c3": lambda: ccmi.OptimizationOptions(requested_destination_broker_ids=list(range(500, 1500)),
                                                            fast_mode=False)}
 # committed oracle goldens of the workloads (tests/golden/make_golden.py)
-WORKLOAD_GOLDEN = {"c1": "c1", "c2": "c2_default", "c2_c1goals": "c2_c1goals", "c3": "c3_default"}
+WORKLOAD_GOLDEN = {"c1": "c1", "c2": "c2_default", "c2_c1goals": "c2_c1goals", "c3": "c3_default", "c4": "c4"}
 BYTES_PER_CANDIDATE = 96
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E (MI355X_MICROARCH.md)
 # candidate-heavy C2 goal the CPU baseline samples on the box (the reference's costliest goal at C2)
@@ -84,8 +101,11 @@ def check_parity(workload: str, cm, result) -> dict:
     acts = cm.actions()
     if len(acts) != g["num_actions"]:
         problems.append(f"{len(acts)} actions vs {g['num_actions']}")
-    if _sha([x for a in acts for x in a]) != g["actions_sha256"]:
+    norm = [a[:5] if len(a) == 7 and a[5] == -1 and a[6] == -1 else a for a in acts]  # make_golden.flat_actions
+    if _sha([x for a in norm for x in a]) != g["actions_sha256"]:
         problems.append("action log")
+    if "replica_disks_sha256" in g and _sha(cm.replica_disks()) != g["replica_disks_sha256"]:
+        problems.append("replica disks")
     if _sha(cm.replica_distribution()) != g["replica_distribution_sha256"]:
         problems.append("replica distribution")
     if _sha(cm.leader_distribution()) != g["leader_distribution_sha256"]:
@@ -105,8 +125,8 @@ def check_parity(workload: str, cm, result) -> dict:
         problems.append(f"stats rel {worst:.2e}")
     return {"golden": os.path.relpath(path, REPO), "status": "ok" if not problems else "MISMATCH: " + ", ".join(problems),
             "actions": len(acts), "max_stats_rel_diff": worst,
-            "checked": "action log + final assignment + leaders (SHA-256), per-goal (name, succeeded, candidates, "
-                       "actions), every goal's ClusterModelStats within 1e-9 relative"}
+            "checked": "action log + final assignment + leaders (+ disks for JBOD) (SHA-256), per-goal (name, "
+                       "succeeded, candidates, actions), every goal's ClusterModelStats within 1e-9 relative"}
 
 
 def _cpu_model() -> str:
@@ -153,14 +173,16 @@ def cpu_baseline(lib, buf, workload: str, goal_names, options, gpu_result, devic
            "nproc": os.cpu_count(), "cpu_share": len(os.sched_getaffinity(0)), "cpu_model": _cpu_model(),
            "num.proposal.precompute.threads": 1}
     # (1) bounded sample of the same workload
-    goal = C2_SAMPLE_GOAL if workload in ("c2", "c3", "c2_c1goals") else goal_names[0]
+    goal = {"c2": C2_SAMPLE_GOAL, "c3": C2_SAMPLE_GOAL, "c2_c1goals": C2_SAMPLE_GOAL,
+            "c4": "IntraBrokerDiskUsageDistributionGoal"}.get(workload, goal_names[0])
+    bc = workload_constraint(workload)
     oc = OracleCluster.from_desc(buf.desc)
     t0 = time.perf_counter()
-    done, cands, stats_s = oc.optimize_until([goal], sample_s, ccmi.BalancingConstraint(), options)
+    done, cands, stats_s = oc.optimize_until([goal], sample_s, bc, options)
     dt = time.perf_counter() - t0
     del oc
     s = ccmi.ClusterModel.from_buffers(buf, device=device)
-    r = ccmi.GoalOptimizer(ccmi.BalancingConstraint()).optimizations(s, ccmi.goals_from_names([goal]), options)
+    r = ccmi.GoalOptimizer(bc).optimizations(s, ccmi.goals_from_names([goal]), options)
     del s
     out["value"] = cands / dt
     out["sample"] = (f"{goal} alone on the {workload.upper()} cluster, restatement stopped after {dt:.1f} s "
@@ -169,7 +191,11 @@ def cpu_baseline(lib, buf, workload: str, goal_names, options, gpu_result, devic
     out["sample_loop_rate"] = cands / max(1e-9, dt - stats_s)
     out["gpu_same_sample"] = {"goal": goal, "seconds": r.seconds, "candidates": r.candidates,
                               "value": r.candidates / r.seconds}
+    if workload == "c4":  # the C1-chain comparisons below are about the inter-broker goals
+        what_if_procs = 0
     # (2) the whole C1 chain, 1 thread, and the GPU's C1 chain
+    if what_if_procs == 0:
+        return _per_goal_from_golden(out, workload, gpu_result)
     ((c1c, c1t),), _ = _c1_chain_procs(1)
     b1 = ccmi.RandomCluster.generate(lib, **C1_PROPS)
     s1 = ccmi.ClusterModel.from_buffers(b1, device=device)
@@ -184,7 +210,11 @@ def cpu_baseline(lib, buf, workload: str, goal_names, options, gpu_result, devic
                                 "slowest_proposal_s": max(t for _, t in rs),
                                 "value": sum(c for c, _ in rs) / max(t for _, t in rs),
                                 "workload": "C1 chain per process (num.proposal.precompute.threads = processes)"}
-    # (4) per-goal full-chain restatement seconds (golden) beside the GPU's
+    return _per_goal_from_golden(out, workload, gpu_result)
+
+
+def _per_goal_from_golden(out: dict, workload: str, gpu_result) -> dict:
+    """(4) per-goal full-chain restatement seconds (golden) beside the GPU's."""
     name = WORKLOAD_GOLDEN.get(workload)
     path = os.path.join(REPO, "tests", "golden", f"{name}.json") if name else None
     if path and os.path.exists(path):
@@ -205,9 +235,10 @@ def cpu_baseline(lib, buf, workload: str, goal_names, options, gpu_result, devic
 
 
 SCAN_KERNELS = ("scan_cross", "scan_pairs", "scan_swap", "chain_pairs", "chain_rack_rows")
+INTRA_KERNELS = ("intra_brokers",)
 
 
-def pmc_traffic(workload: str):
+def pmc_traffic(workload: str, kernels=SCAN_KERNELS):
     """HBM bytes per scan launch from the newest committed PMC summary of this workload (profiles/rNN/
     <workload>_pmc_summary.json, written by tools/pmc_summary.py from separate rocprofv3 --pmc FETCH_SIZE /
     WRITE_SIZE passes of this same bench command). PMC counters cannot be read inside the timed process."""
@@ -217,8 +248,8 @@ def pmc_traffic(workload: str):
         return None, None
     with open(paths[-1]) as f:
         ks = json.load(f)["kernels"]
-    n = sum(ks[k]["launches"] for k in SCAN_KERNELS if k in ks)
-    b = sum(ks[k]["launches"] * ks[k]["hbm_bytes_per_launch"] for k in SCAN_KERNELS if k in ks)
+    n = sum(ks[k]["launches"] for k in kernels if k in ks)
+    b = sum(ks[k]["launches"] * ks[k]["hbm_bytes_per_launch"] for k in kernels if k in ks)
     return (b / n if n else None), os.path.relpath(paths[-1], REPO)
 
 
@@ -256,7 +287,7 @@ def main() -> None:
     buf = ccmi.RandomCluster.generate(lib, **props)
     goals = ccmi.goals_from_names(goal_names)
     options = WORKLOAD_OPTIONS[args.workload]() if args.workload in WORKLOAD_OPTIONS else None
-    opt = ccmi.GoalOptimizer(ccmi.BalancingConstraint())
+    opt = ccmi.GoalOptimizer(workload_constraint(args.workload))
     sharded = args.sharded and world > 1
     uid = None
     if sharded:  # rank 0's RCCL id reaches the other ranks over the default process group
@@ -318,9 +349,15 @@ def main() -> None:
             cands = float(sum(r.candidates for r in results))
 
     perf = inst_perf
-    launches = max(1, perf.scan_launches)
-    scan_avg_ms = perf.scan_kernel_ms / launches
-    required_bytes_per_launch = perf.scan_required * BYTES_PER_CANDIDATE / launches
+    intra = args.workload == "c4"  # JBOD: the dominant kernel is K6 (intra_brokers)
+    if intra:
+        launches = max(1, perf.intra_launches)
+        scan_avg_ms = perf.intra_kernel_ms / launches
+        required_bytes_per_launch = perf.intra_bytes / launches
+    else:
+        launches = max(1, perf.scan_launches)
+        scan_avg_ms = perf.scan_kernel_ms / launches
+        required_bytes_per_launch = perf.scan_required * BYTES_PER_CANDIDATE / launches
     achieved = required_bytes_per_launch / (scan_avg_ms * 1e-3) / 1e9 if scan_avg_ms > 0 else 0.0
 
     if rank != 0:
@@ -328,7 +365,7 @@ def main() -> None:
         return
     first = results[0]
     parity = check_parity(args.workload, sessions[0][0], first)
-    traffic, traffic_src = pmc_traffic(args.workload)
+    traffic, traffic_src = pmc_traffic(args.workload, INTRA_KERNELS if intra else SCAN_KERNELS)
     line = {
         "metric": "candidate moves evaluated/s + proposal wall time, 10K brokers/1M replicas",
         "value": cands / elapsed,
@@ -359,9 +396,12 @@ def main() -> None:
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_unit": "HBM bytes per scan launch",
                      "traffic_source": traffic_src,
-                     "kernel": "candidate scans (scan_cross/scan_pairs/scan_swap/chain_pairs/chain_rack_rows)",
+                     "kernel": ("K6 intra_brokers (one thread per broker; algorithmic bytes = 17 B per disk + 29 B per "
+                                "replica entry read once)" if intra else
+                                "candidate scans (scan_cross/scan_pairs/scan_swap/chain_pairs/chain_rack_rows)"),
                      "avg_launch_us": scan_avg_ms * 1e3,
-                     "launches_per_step": perf.scan_launches, "chain_launches_per_step": perf.chain_launches,
+                     "launches_per_step": perf.intra_launches if intra else perf.scan_launches,
+                     "chain_launches_per_step": perf.chain_launches,
                      "algorithmic_bytes_per_launch": required_bytes_per_launch,
                      "required_candidates_per_step": perf.scan_required,
                      "reference_equivalent_candidates_per_step": inst_cands,

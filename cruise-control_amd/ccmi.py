@@ -378,13 +378,32 @@ class GoalResult:
     stats: Dict[str, object]
 
 
-@dataclass
 class OptimizerResult:
-    goal_results: List[GoalResult]
-    proposals: List[ExecutionProposal]
-    actions: List[tuple]
-    seconds: float
-    violated_goals_after: List[str] = field(default_factory=list)
+    """analyzer/OptimizerResult.java: per-goal results, the ExecutionProposals and the ordered action log. The
+    proposals and the action log are read from the session on first access (the session keeps them until its next
+    optimization), so a caller that only needs the statistics does not pay for converting them."""
+
+    def __init__(self, goal_results: List[GoalResult], cluster: "ClusterModel", seconds: float,
+                 violated_goals_after: List[str]):
+        self.goal_results = goal_results
+        self.seconds = seconds
+        self.violated_goals_after = violated_goals_after
+        self._cluster = cluster
+        self._num_actions = cluster.lib.lib.ccmi_action_log_count(cluster.handle)
+        self._proposals: Optional[List[ExecutionProposal]] = None
+        self._actions: Optional[List[tuple]] = None
+
+    @property
+    def proposals(self) -> List[ExecutionProposal]:
+        if self._proposals is None:
+            self._proposals = self._cluster.proposals()
+        return self._proposals
+
+    @property
+    def actions(self) -> List[tuple]:
+        if self._actions is None:
+            self._actions = self._cluster.actions()[:self._num_actions]
+        return self._actions
 
     @property
     def candidates(self) -> int:
@@ -745,8 +764,7 @@ class GoalOptimizer:
         dt = time.perf_counter() - t0
         grs = [GoalResult(GOAL_NAMES[r.goal_kind], bool(r.succeeded), bool(r.has_diff), r.seconds, r.candidates,
                           r.device_candidates, r.device_launches, r.actions, stats_to_dict(r.stats)) for r in results]
-        return OptimizerResult(grs, cluster.proposals(), cluster.actions(), dt,
-                               [g.name for g in grs if not g.succeeded])
+        return OptimizerResult(grs, cluster, dt, [g.name for g in grs if not g.succeeded])
 
 
 def goals_from_names(names: Sequence[str], constraint: Optional[BalancingConstraint] = None) -> List[Goal]:

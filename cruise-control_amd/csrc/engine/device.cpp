@@ -811,6 +811,8 @@ void Device::intraRun(const IntraRequest& q, IntraResult& out) {
     dallocTracked(&dEDisk_, c, o);
     dallocTracked(&dSnapA_, c, o);
     dallocTracked(&dSnapB_, c, o);
+    dallocTracked(&dOrdRev_, c, o);
+    dallocTracked(&dOrdFwd_, c, o);
     entCap_ = c;
   }
   hipCheck(hipMemcpyAsync(dEOff_, q.eOff, sizeof(int32_t) * (B_ + 1), hipMemcpyHostToDevice, ST), "eOff");
@@ -862,6 +864,8 @@ void Device::intraRun(const IntraRequest& q, IntraResult& out) {
   A.rSel = dRSel_;
   A.snapA = dSnapA_;
   A.snapB = dSnapB_;
+  A.ordRev = dOrdRev_;
+  A.ordFwd = dOrdFwd_;
   A.hist = dHist_;
   A.upperOut = dUpper_ + (size_t)q.slot * B_;
   A.lowerOut = dLower_ + (size_t)q.slot * B_;

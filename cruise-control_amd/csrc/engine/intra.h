@@ -60,6 +60,8 @@ struct IntraArgs {
   const uint8_t* rSel;     // [R] selectOnlineReplicas && selectReplicasBasedOnExcludedTopics
   int32_t* snapA;          // [entries] scratch (the broker's CSR range)
   int32_t* snapB;
+  int32_t* ordRev;         // [entries] scratch: the broker's selected entries in reverse-score order (see run())
+  int32_t* ordFwd;         //            and in score order
   int32_t* hist;           // [B][kIntraHist][kIntraMaxDisks + 1] scratch
   double* upperOut;        // [B] thresholds of this goal (IG_USAGE)
   double* lowerOut;
@@ -104,6 +106,16 @@ class IntraBroker {
   CCMI_LD void run() {
     for (int k = d0; k < d1; ++k) A.dUtil[A.bDisks[k]] = A.dUtilIn[A.bDisks[k]];
     for (int i = e0; i < e1; ++i) A.eDisk[i] = A.eDiskIn[i];
+    // Every key of the SortedReplicas comparator but the disk-immigrant priority is fixed while the goal runs
+    // (intra-broker moves change neither loads nor offline status), so the selected entries are sorted once per
+    // order; a snapshot of disk d is then two passes over that order (immigrants of d first, then the others).
+    nSel = 0;
+    for (int i = e0; i < e1; ++i) {
+      if (!A.rSel[A.eRep[i]]) continue;
+      insertSorted(A.ordRev + e0, nSel, i, true);
+      insertSorted(A.ordFwd + e0, nSel, i, false);
+      ++nSel;
+    }
     if (A.goal == IG_CAPACITY) capacityRebalance();
     else usageRebalance();
     A.logCount[b] = nLog;
@@ -119,6 +131,7 @@ class IntraBroker {
   int32_t status = IS_OK;
   int64_t cand = 0;
   double up = 0, lo = 0;  // this goal's thresholds (IG_USAGE)
+  int nSel = 0;           // selected entries (ordRev / ordFwd length)
 
   CCMI_LD double pct(int d) const { return A.dCap[d] > 0 ? A.dUtil[d] / A.dCap[d] : 1.0; }
   CCMI_LD double avgPct() const {
@@ -134,11 +147,10 @@ class IntraBroker {
   }
   CCMI_LD double du(int i) const { return A.rDu[A.eRep[i]]; }
 
-  // SortedReplicas order of two entries: disk-immigrant priority, score (DISK avg, negated when reverse), compareTo
-  CCMI_LD bool less(int i, int j, bool reverse) const {
+  // SortedReplicas order of two entries without the priority function: score (DISK avg, negated when reverse,
+  // Double.compare), then Replica.compareTo (online replicas: its static tail rank)
+  CCMI_LD bool lessStatic(int i, int j, bool reverse) const {
     const int ri = A.eRep[i], rj = A.eRep[j];
-    const int pi = A.rOrigDisk[ri] != A.eDisk[i] ? 0 : 1, pj = A.rOrigDisk[rj] != A.eDisk[j] ? 0 : 1;
-    if (pi != pj) return pi < pj;
     double si = (double)A.rScore[ri], sj = (double)A.rScore[rj];
     if (reverse) {
       si = -si;
@@ -148,18 +160,24 @@ class IntraBroker {
     if (c != 0) return c < 0;
     return A.rTie[ri] < A.rTie[rj];
   }
-  // the disk's tracked sorted replicas (a clone), as entry indices into out[0..n)
-  CCMI_LD int snapshot(int d, bool reverse, int32_t* out) const {
-    int n = 0;
-    for (int i = e0; i < e1; ++i) {
-      if (A.eDisk[i] != d || !A.rSel[A.eRep[i]]) continue;
-      int k = n++;
-      while (k > 0 && less(i, out[k - 1], reverse)) {
-        out[k] = out[k - 1];
-        --k;
-      }
-      out[k] = i;
+  CCMI_LD void insertSorted(int32_t* ord, int n, int i, bool reverse) const {
+    int k = n;
+    while (k > 0 && lessStatic(i, ord[k - 1], reverse)) {
+      ord[k] = ord[k - 1];
+      --k;
     }
+    ord[k] = i;
+  }
+  // the disk's tracked sorted replicas (a clone), as entry indices into out[0..n): prioritizeDiskImmigrants puts the
+  // replicas whose original disk is not d first, each group in the static order
+  CCMI_LD int snapshot(int d, bool reverse, int32_t* out) const {
+    const int32_t* ord = (reverse ? A.ordRev : A.ordFwd) + e0;
+    int n = 0;
+    for (int pass = 0; pass < 2; ++pass)
+      for (int k = 0; k < nSel; ++k) {
+        const int i = ord[k];
+        if (A.eDisk[i] == d && ((A.rOrigDisk[A.eRep[i]] != d) == (pass == 0))) out[n++] = i;
+      }
     return n;
   }
 

@@ -224,6 +224,7 @@ void Model::buildDisks(const ccmi_cluster_desc& d) {
   dMembers.assign(D, {});
   rDisk.assign(R, -1);
   rOrigDisk.assign(R, -1);
+  rDiskPos.assign(R, -1);
   std::vector<std::vector<int32_t>> per(B);
   for (int k = 0; k < D; ++k) {
     const int b = d.disk_broker[k];
@@ -261,6 +262,7 @@ void Model::buildDisks(const ccmi_cluster_desc& d) {
       if (k >= 0 && dBroker[k] != rBroker[r]) throw std::invalid_argument("replica disk on another broker");
       if (k < 0) continue;
       rDisk[r] = rOrigDisk[r] = k;
+      rDiskPos[r] = (int32_t)dMembers[k].size();
       dMembers[k].push_back(r);
       dUtil[k] += ru(r, R_DISK);  // Disk.addReplica (load still empty: += 0.0) then Disk.addReplicaLoad
     }
@@ -288,25 +290,38 @@ double Model::avgDiskPct(int b) const {
   }
   return cap > 0 ? util / cap : 1.0;
 }
+// Membership: without ghosts (Disk._replicas entries left by inter-broker moves) a replica is a member of exactly
+// its current disk, tracked by rDiskPos (O(1)); with ghosts the member lists are searched.
 void Model::diskAdd(int d, int r) {
   auto& v = dMembers[d];
-  if (std::find(v.begin(), v.end(), r) != v.end())
+  const bool member = diskGhosts ? std::find(v.begin(), v.end(), r) != v.end() : (rDisk[r] == d && rDiskPos[r] >= 0);
+  if (member)
     throw StateError("Disk " + dLogdir[d] + " already has replica " + topicNames[pTopic[rPart[r]]] + "-" +
                      std::to_string(pNumber[rPart[r]]));
   dUtil[d] += ru(r, R_DISK);
-  v.push_back(r);
   rDisk[r] = d;
+  rDiskPos[r] = (int32_t)v.size();
+  v.push_back(r);
   diskDirty = true;
 }
 void Model::diskRemove(int d, int r) {
   auto& v = dMembers[d];
-  auto it = std::find(v.begin(), v.end(), r);
-  if (it == v.end())
+  int pos = -1;
+  if (rDisk[r] == d && rDiskPos[r] >= 0 && rDiskPos[r] < (int)v.size() && v[rDiskPos[r]] == r) {
+    pos = rDiskPos[r];
+  } else if (diskGhosts) {
+    auto it = std::find(v.begin(), v.end(), r);
+    if (it != v.end()) pos = (int)(it - v.begin());
+  }
+  if (pos < 0)
     throw StateError("Disk " + dLogdir[d] + " does not has replica " + topicNames[pTopic[rPart[r]]] + "-" +
                      std::to_string(pNumber[rPart[r]]));
   dUtil[d] -= ru(r, R_DISK);
-  *it = v.back();
+  const int last = v.back();
+  v[pos] = last;
+  if (rDisk[last] == d) rDiskPos[last] = pos;
   v.pop_back();
+  if (rDisk[r] == d) rDiskPos[r] = -1;
   diskDirty = true;
 }
 void Model::relocateReplicaToDisk(int p, int b, int dst) {

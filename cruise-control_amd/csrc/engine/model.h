@@ -130,6 +130,7 @@ class Model {
   std::vector<std::vector<int32_t>> dMembers;  // Disk._replicas (a HashSet; its order is never observed)
   std::vector<int32_t> bDiskOff, bDisks;    // CSR: each broker's disks in logdir order
   std::vector<int32_t> rDisk, rOrigDisk;    // Replica._disk / _originalDisk (-1 = null)
+  std::vector<int32_t> rDiskPos;            // index of the replica in dMembers[rDisk[r]] (-1 = not a member)
   // Disk._replicas entries left behind by inter-broker moves (Broker.removeReplica keeps the replica on its disk)
   int64_t diskGhosts = 0;
   bool diskDirty = true;                    // device copy of dUtil is stale

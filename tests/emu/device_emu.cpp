@@ -561,7 +561,7 @@ void Device::setDiskUtil(const double* dUtil) {
 void Device::intraRun(const IntraRequest& q, IntraResult& out) {
   Emu& e = E(st_);
   const int E_ = q.eOff[B_];
-  std::vector<int32_t> eDisk(q.eDisk, q.eDisk + E_), snapA(E_ + 1), snapB(E_ + 1);
+  std::vector<int32_t> eDisk(q.eDisk, q.eDisk + E_), snapA(E_ + 1), snapB(E_ + 1), ordRev(E_ + 1), ordFwd(E_ + 1);
   std::vector<int64_t> logOff(B_, 0);
   std::vector<int32_t> cap(B_, 0);
   int64_t total = 0;
@@ -604,6 +604,8 @@ void Device::intraRun(const IntraRequest& q, IntraResult& out) {
   A.rSel = q.rSel;
   A.snapA = snapA.data();
   A.snapB = snapB.data();
+  A.ordRev = ordRev.data();
+  A.ordFwd = ordFwd.data();
   A.hist = e.hist.data();
   A.upperOut = e.upper.data() + (size_t)q.slot * B_;
   A.lowerOut = e.lower.data() + (size_t)q.slot * B_;
