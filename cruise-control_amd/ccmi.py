@@ -183,7 +183,8 @@ EXPORTED_SYMBOLS = (
     "ccmi_random_cluster", "ccmi_cluster_buffers_desc", "ccmi_cluster_buffers_free", "ccmi_session_create",
     "ccmi_session_destroy", "ccmi_optimizations", "ccmi_goal_optimize", "ccmi_action_acceptance",
     "ccmi_compute_cluster_stats", "ccmi_action_log_count", "ccmi_action_log_copy", "ccmi_replica_distribution",
-    "ccmi_leader_distribution", "ccmi_proposal_count", "ccmi_proposals", "ccmi_perf", "ccmi_perf_reset",
+    "ccmi_leader_distribution", "ccmi_replica_disks", "ccmi_proposal_count", "ccmi_proposals",
+    "ccmi_proposal_disks", "ccmi_perf", "ccmi_perf_reset",
     "ccmi_set_kernel_timing", "ccmi_session_set_shard", "ccmi_rccl_unique_id", "ccmi_session_attach_rccl")
 
 # int (*)(void* ctx, int64_t* key): replace *key by the MIN over all shards, return 0 (include/ccmi.h)

@@ -92,24 +92,25 @@ void setOptions(ccmi_session* s, const ccmi_balancing_constraint* c, const ccmi_
       opt.exclTopic[t] = 1;
       opt.anyExclTopic = true;
     }
+    // broker-id sets of OptimizationOptions: ids of brokers that are not in the cluster match nothing (Set.contains)
     for (int i = 0; i < o->num_excluded_brokers_for_leadership; ++i) {
       const int b = o->excluded_brokers_for_leadership[i];
-      if (b < 0 || b >= B) throw std::invalid_argument("excluded broker for leadership out of range");
+      if (b < 0 || b >= B) continue;
       opt.exclLead[b] = 1;
       opt.anyExclLead = true;
     }
     for (int i = 0; i < o->num_excluded_brokers_for_replica_move; ++i) {
       const int b = o->excluded_brokers_for_replica_move[i];
-      if (b < 0 || b >= B) throw std::invalid_argument("excluded broker for replica move out of range");
+      if (b < 0 || b >= B) continue;
       opt.exclMove[b] = 1;
       opt.anyExclMove = true;
     }
     opt.onlyImmigrants = o->only_move_immigrant_replicas != 0;
     for (int i = 0; i < o->num_requested_destination_broker_ids; ++i) {
+      opt.anyRequested = true;  // a non-empty set filters candidates even when none of its ids is a broker
       const int b = o->requested_destination_broker_ids[i];
-      if (b < 0 || b >= B) throw std::invalid_argument("requested destination broker out of range");
+      if (b < 0 || b >= B) continue;
       opt.requested[b] = 1;
-      opt.anyRequested = true;
     }
     opt.triggered = o->triggered_by_goal_violation != 0;
   }

@@ -43,6 +43,7 @@ hipError_t launchStats(const StatsParams& P, const int32_t* tc, const int32_t* t
                        hipEvent_t evTopic0, hipEvent_t evTopic1);
 
 hipError_t launchIntra(const IntraArgs& A, hipStream_t st);
+hipError_t launchIntraSort(const IntraArgs& A, hipStream_t st);
 hipError_t launchIntraCompact(const int32_t* brokers, int n, const int64_t* logOff, const int32_t* count,
                               const int64_t* cOff, const int32_t* rep, const int32_t* src, const int32_t* dst,
                               int32_t* cRep, int32_t* cSrc, int32_t* cDst, hipStream_t st);
@@ -780,6 +781,7 @@ void Device::uploadDisks(int D, const int32_t* bDiskOff, const int32_t* bDisks, 
   dallocTracked(&dCand_, (size_t)B_, o);
   dallocTracked(&dCOff_, (size_t)B_ + 1, o);
   dallocTracked(&dEOff_, (size_t)B_ + 1, o);
+  dallocTracked(&dNSel_, (size_t)B_, o);
   dallocTracked(&dDiskStats_, 1, o);
   hipCheck(hipMemcpy(dBDiskOff_, bDiskOff, sizeof(int32_t) * (B_ + 1), hipMemcpyHostToDevice), "upload bDiskOff");
   hipCheck(hipMemcpy(dBDisks_, bDisks, sizeof(int32_t) * D, hipMemcpyHostToDevice), "upload bDisks");
@@ -866,6 +868,7 @@ void Device::intraRun(const IntraRequest& q, IntraResult& out) {
   A.snapB = dSnapB_;
   A.ordRev = dOrdRev_;
   A.ordFwd = dOrdFwd_;
+  A.nSel = dNSel_;
   A.hist = dHist_;
   A.upperOut = dUpper_ + (size_t)q.slot * B_;
   A.lowerOut = dLower_ + (size_t)q.slot * B_;
@@ -878,10 +881,13 @@ void Device::intraRun(const IntraRequest& q, IntraResult& out) {
   A.status = dStatus_;
   A.cand = dCand_;
   float msTotal = 0.f;
+  bool sorted = false;
   auto launch = [&](const IntraArgs& a) {
     hipCheck(hipMemcpyAsync(dLogOff_, logOff.data(), sizeof(int64_t) * B_, hipMemcpyHostToDevice, ST), "logOff");
     hipCheck(hipMemcpyAsync(dLogCap_, cap.data(), sizeof(int32_t) * B_, hipMemcpyHostToDevice, ST), "logCap");
     if (timing) hipCheck(hipEventRecord(EV0, ST), "event");
+    if (!sorted) hipCheck(launchIntraSort(a, ST), "intra_sort");
+    sorted = true;
     hipCheck(launchIntra(a, ST), "intra_brokers");
     if (timing) hipCheck(hipEventRecord(EV1, ST), "event");
     out.status.resize(B_);

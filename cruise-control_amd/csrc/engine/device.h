@@ -201,7 +201,7 @@ class Device {
   float* dRScore_ = nullptr;
   double *dUpper_ = nullptr, *dLower_ = nullptr;  // [G][B] usage-goal thresholds
   int32_t *dEOff_ = nullptr, *dERep_ = nullptr, *dEDiskIn_ = nullptr, *dEDisk_ = nullptr, *dSnapA_ = nullptr,
-          *dSnapB_ = nullptr, *dOrdRev_ = nullptr, *dOrdFwd_ = nullptr, *dHist_ = nullptr, *dBrokers_ = nullptr, *dLogCap_ = nullptr, *dCount_ = nullptr,
+          *dSnapB_ = nullptr, *dOrdRev_ = nullptr, *dOrdFwd_ = nullptr, *dNSel_ = nullptr, *dHist_ = nullptr, *dBrokers_ = nullptr, *dLogCap_ = nullptr, *dCount_ = nullptr,
           *dStatus_ = nullptr, *dLogRep_ = nullptr, *dLogSrc_ = nullptr, *dLogDst_ = nullptr, *dCRep_ = nullptr,
           *dCSrc_ = nullptr, *dCDst_ = nullptr;
   int64_t *dLogOff_ = nullptr, *dCand_ = nullptr, *dCOff_ = nullptr;

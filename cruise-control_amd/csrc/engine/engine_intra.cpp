@@ -211,13 +211,15 @@ bool IntraGoalImpl::rebalanceAll(Engine& e) {
     upper = res.upper;
     lower = res.lower;
   }
+  m.log.reserve(m.log.size() + res.rep.size());
   for (int b : brokers) {
     e.candidates += res.cand[b];
     for (int64_t i = res.off[b]; i < res.off[b + 1]; ++i) {
-      const int r = res.rep[i];
-      if (r < 0 || r >= m.R || m.rBroker[r] != b || m.rDisk[r] != res.src[i])
+      const int r = res.rep[i], dst = res.dst[i];
+      if (r < 0 || r >= m.R || m.rBroker[r] != b || m.rDisk[r] != res.src[i] || dst < 0 || dst >= m.D ||
+          m.dBroker[dst] != b)
         throw std::runtime_error("device intra-broker record does not match the host model");
-      m.relocateReplicaToDisk(m.rPart[r], b, res.dst[i]);
+      m.replayDiskMove(r, res.src[i], dst);  // ClusterModel.relocateReplica(tp, broker, logdir)
     }
   }
   return true;

@@ -60,8 +60,9 @@ struct IntraArgs {
   const uint8_t* rSel;     // [R] selectOnlineReplicas && selectReplicasBasedOnExcludedTopics
   int32_t* snapA;          // [entries] scratch (the broker's CSR range)
   int32_t* snapB;
-  int32_t* ordRev;         // [entries] scratch: the broker's selected entries in reverse-score order (see run())
-  int32_t* ordFwd;         //            and in score order
+  int32_t* ordRev;         // [entries] the broker's selected entries in reverse-score order (intraSortKeys)
+  int32_t* ordFwd;         //           and in score order
+  int32_t* nSel;           // [B] selected entries per broker
   int32_t* hist;           // [B][kIntraHist][kIntraMaxDisks + 1] scratch
   double* upperOut;        // [B] thresholds of this goal (IG_USAGE)
   double* lowerOut;
@@ -92,6 +93,23 @@ CCMI_LD int32_t intraD2I(double x) {
   return (int32_t)x;
 }
 
+// The SortedReplicas comparator without its priority function as one unique 64-bit key: the score
+// ((double) DISK average, negated for the reverse order) in Double.compare order, then Replica.compareTo's static
+// tail rank (online replicas). Double.compare(-a, -b) is exactly the reversed order for non-NaN a, b; NaN is the
+// largest score in both orders.
+CCMI_LD uint64_t intraSortKey(float score, int32_t tie, bool reverse) {
+  uint32_t bits;
+  __builtin_memcpy(&bits, &score, 4);
+  uint32_t u;
+  if (score != score) {
+    u = 0xFFFFFFFFu;
+  } else {
+    u = (bits & 0x80000000u) ? ~bits : (bits | 0x80000000u);
+    if (reverse) u = ~u;
+  }
+  return ((uint64_t)u << 32) | (uint32_t)tie;
+}
+
 class IntraBroker {
  public:
   CCMI_LD IntraBroker(const IntraArgs& a, int broker) : A(a), b(broker) {
@@ -103,19 +121,14 @@ class IntraBroker {
     logCap = A.logCap[b];
   }
 
+  // ordRev / ordFwd / nSel hold the broker's selected entries sorted by intraSortKey (kernels/intra.hip intra_sort,
+  // or the emulation's sort): every key of the SortedReplicas comparator but the disk-immigrant priority is fixed
+  // while the goal runs (intra-broker moves change neither loads nor offline status), so a snapshot of disk d is
+  // two passes over that order (immigrants of d first, then the others).
   CCMI_LD void run() {
     for (int k = d0; k < d1; ++k) A.dUtil[A.bDisks[k]] = A.dUtilIn[A.bDisks[k]];
     for (int i = e0; i < e1; ++i) A.eDisk[i] = A.eDiskIn[i];
-    // Every key of the SortedReplicas comparator but the disk-immigrant priority is fixed while the goal runs
-    // (intra-broker moves change neither loads nor offline status), so the selected entries are sorted once per
-    // order; a snapshot of disk d is then two passes over that order (immigrants of d first, then the others).
-    nSel = 0;
-    for (int i = e0; i < e1; ++i) {
-      if (!A.rSel[A.eRep[i]]) continue;
-      insertSorted(A.ordRev + e0, nSel, i, true);
-      insertSorted(A.ordFwd + e0, nSel, i, false);
-      ++nSel;
-    }
+    nSel = A.nSel[b];
     if (A.goal == IG_CAPACITY) capacityRebalance();
     else usageRebalance();
     A.logCount[b] = nLog;
@@ -147,27 +160,6 @@ class IntraBroker {
   }
   CCMI_LD double du(int i) const { return A.rDu[A.eRep[i]]; }
 
-  // SortedReplicas order of two entries without the priority function: score (DISK avg, negated when reverse,
-  // Double.compare), then Replica.compareTo (online replicas: its static tail rank)
-  CCMI_LD bool lessStatic(int i, int j, bool reverse) const {
-    const int ri = A.eRep[i], rj = A.eRep[j];
-    double si = (double)A.rScore[ri], sj = (double)A.rScore[rj];
-    if (reverse) {
-      si = -si;
-      sj = -sj;
-    }
-    const int c = intraDcmp(si, sj);
-    if (c != 0) return c < 0;
-    return A.rTie[ri] < A.rTie[rj];
-  }
-  CCMI_LD void insertSorted(int32_t* ord, int n, int i, bool reverse) const {
-    int k = n;
-    while (k > 0 && lessStatic(i, ord[k - 1], reverse)) {
-      ord[k] = ord[k - 1];
-      --k;
-    }
-    ord[k] = i;
-  }
   // the disk's tracked sorted replicas (a clone), as entry indices into out[0..n): prioritizeDiskImmigrants puts the
   // replicas whose original disk is not d first, each group in the static order
   CCMI_LD int snapshot(int d, bool reverse, int32_t* out) const {

@@ -336,6 +336,14 @@ void Model::relocateReplicaToDisk(int p, int b, int dst) {
   a.dstDisk = dst;
   log.push_back(a);
 }
+void Model::replayDiskMove(int r, int src, int dst) {
+  diskRemove(src, r);
+  diskAdd(dst, r);
+  ActionRec a{CCMI_INTRA_BROKER_REPLICA_MOVEMENT, rPart[r], dBroker[src], dBroker[src], -1};
+  a.srcDisk = src;
+  a.dstDisk = dst;
+  log.push_back(a);
+}
 std::vector<int32_t> Model::replicaDisks() const {
   std::vector<int32_t> v(R);
   for (int i = 0; i < R; ++i) v[i] = rDisk[pSlots[i]];

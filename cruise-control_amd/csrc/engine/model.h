@@ -141,6 +141,8 @@ class Model {
   void diskRemove(int d, int r);             // Disk.removeReplica (Disk.java:139-146)
   // ClusterModel.relocateReplica(tp, brokerId, destinationLogdir) (ClusterModel.java:362-366), logged
   void relocateReplicaToDisk(int p, int b, int dst);
+  // the same relocation for a K6 record whose replica and source disk are known (replay of a device decision)
+  void replayDiskMove(int r, int src, int dst);
   std::vector<int32_t> replicaDisks() const;  // [R] disk of every replica slot in partition order
 
   // cluster

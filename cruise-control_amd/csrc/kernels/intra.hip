@@ -1,6 +1,8 @@
 // K6: intra-broker (JBOD) goals on gfx950 (engine/intra.h holds the per-broker program) and the disk part of the
 // ClusterModelStats reduction (model/ClusterModelStats.java:489-511).
 //
+// intra_sort    : one wavefront per broker: its replicas' fixed sort orders (reverse / forward DISK score, then
+//                 Replica.compareTo) by rank counting over LDS tiles.
 // intra_brokers : one thread per broker. A broker's rebalance touches only its own disks and replicas, so the B
 //                 programs of a goal are independent; each reads its replicas' records (contiguous CSR range) and its
 //                 disks, and writes its ordered action records into its own log range.
@@ -15,6 +17,53 @@
 #include "../engine/intra.h"
 
 namespace ccmi {
+
+// One wavefront per broker: rank of every selected entry under both orders (ranks are a permutation: keys are
+// unique), the key tiles staged through LDS; ordRev / ordFwd[e0 + rank] = entry.
+constexpr int kSortTile = 512;
+__global__ __launch_bounds__(64) void intra_sort(IntraArgs A) {
+  __shared__ uint64_t kRev[kSortTile], kFwd[kSortTile];
+  __shared__ uint8_t kSel[kSortTile];
+  const int b = A.brokers[blockIdx.x];
+  const int e0 = A.eOff[b], n = A.eOff[b + 1] - e0;
+  const int lane = threadIdx.x;
+  int selCount = 0;
+  for (int ic = 0; ic < n; ic += 64) {
+    const int i = ic + lane;
+    bool mine = false;
+    uint64_t rev = 0, fwd = 0;
+    if (i < n) {
+      const int r = A.eRep[e0 + i];
+      mine = A.rSel[r] != 0;
+      rev = intraSortKey(A.rScore[r], A.rTie[r], true);
+      fwd = intraSortKey(A.rScore[r], A.rTie[r], false);
+    }
+    int rankRev = 0, rankFwd = 0;
+    for (int jt = 0; jt < n; jt += kSortTile) {
+      const int m = n - jt < kSortTile ? n - jt : kSortTile;
+      __syncthreads();
+      for (int j = lane; j < m; j += 64) {
+        const int r = A.eRep[e0 + jt + j];
+        kSel[j] = A.rSel[r];
+        kRev[j] = intraSortKey(A.rScore[r], A.rTie[r], true);
+        kFwd[j] = intraSortKey(A.rScore[r], A.rTie[r], false);
+      }
+      __syncthreads();
+      if (mine)
+        for (int j = 0; j < m; ++j) {
+          if (!kSel[j]) continue;
+          rankRev += kRev[j] < rev ? 1 : 0;
+          rankFwd += kFwd[j] < fwd ? 1 : 0;
+        }
+    }
+    if (mine) {
+      A.ordRev[e0 + rankRev] = e0 + i;
+      A.ordFwd[e0 + rankFwd] = e0 + i;
+    }
+    selCount += __popcll(__ballot(mine));
+  }
+  if (lane == 0) A.nSel[b] = selCount;
+}
 
 __global__ __launch_bounds__(64) void intra_brokers(IntraArgs A) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -101,6 +150,12 @@ __global__ __launch_bounds__(1024) void stats_disks(const int32_t* __restrict__ 
     out->unbalanced = u;
     out->numAlive = a;
   }
+}
+
+hipError_t launchIntraSort(const IntraArgs& A, hipStream_t st) {
+  if (A.nBrokers <= 0) return hipSuccess;
+  hipLaunchKernelGGL(intra_sort, dim3(A.nBrokers), dim3(64), 0, st, A);
+  return hipGetLastError();
 }
 
 hipError_t launchIntra(const IntraArgs& A, hipStream_t st) {

@@ -5,6 +5,7 @@
 // decoding, resumption) can be parity-checked against the CPU oracle on machines without a GPU. It
 // evaluates the same predicates.h conjunctions as the gfx950 kernels, pair by pair in reference order.
 // The product library always uses the HIP implementation (device.cpp) and fails loudly without a gfx950.
+#include <algorithm>
 #include <cmath>
 #include <cstring>
 #include <stdexcept>
@@ -606,6 +607,22 @@ void Device::intraRun(const IntraRequest& q, IntraResult& out) {
   A.snapB = snapB.data();
   A.ordRev = ordRev.data();
   A.ordFwd = ordFwd.data();
+  std::vector<int32_t> nSel(B_, 0);
+  A.nSel = nSel.data();
+  for (int i = 0; i < q.nBrokers; ++i) {  // kernels/intra.hip intra_sort: selected entries by their unique keys
+    const int b = q.brokers[i];
+    for (int pass = 0; pass < 2; ++pass) {
+      std::vector<std::pair<uint64_t, int32_t>> keyed;
+      for (int k = q.eOff[b]; k < q.eOff[b + 1]; ++k) {
+        const int r = q.eRep[k];
+        if (q.rSel[r]) keyed.push_back({intraSortKey(e.rScore[r], e.rTie[r], pass == 0), k});
+      }
+      std::sort(keyed.begin(), keyed.end());
+      int32_t* ord = (pass == 0 ? ordRev.data() : ordFwd.data()) + q.eOff[b];
+      for (size_t k = 0; k < keyed.size(); ++k) ord[k] = keyed[k].second;
+      nSel[b] = (int)keyed.size();
+    }
+  }
   A.hist = e.hist.data();
   A.upperOut = e.upper.data() + (size_t)q.slot * B_;
   A.lowerOut = e.lower.data() + (size_t)q.slot * B_;
