@@ -116,6 +116,7 @@ void setOptions(ccmi_session* s, const ccmi_balancing_constraint* c, const ccmi_
   }
   if (s->model.numNew > 0) throw ccmi::Unsupported("NEW brokers are outside ABI v1 scope");
   e.opt = std::move(opt);
+  s->model.setExcludedTopicSelection(e.opt.exclTopic);
 }
 
 std::vector<int32_t> replicaDist(const ccmi::Model& m) {
@@ -154,7 +155,6 @@ void validateChain(const ccmi_session* s, const int32_t* kinds, int n) {
   if (intra != 0 && intra != total)
     throw std::invalid_argument("intra-broker goals cannot be optimized together with inter-broker goals");
   if (intra == 0) {
-    if (s->engine->opt.anyExclTopic) throw ccmi::Unsupported("excluded topics are supported by the intra-broker goals only");
     if (s->model.numBadDisk > 0) throw ccmi::Unsupported("inter-broker goals with BAD_DISKS brokers are not implemented");
   }
 }

@@ -468,6 +468,7 @@ class ReplicaDistribution : public GoalImpl {
       Model::Spec s;
       s.selImmigrants = e.opt.onlyImmigrants;
       s.selImmOrOffline = selfHealing && m.alive(b);
+      s.selExclTopics = e.opt.anyExclTopic;
       s.prioOffline = selfHealing;
       s.prioImmigrants = !e.opt.onlyImmigrants;
       s.scoreRes = R_DISK;
@@ -765,6 +766,7 @@ class ResourceDistribution : public GoalImpl {
     s.selFollowers = followersOnly;
     s.selLeaders = leadersOnly;
     s.selImmigrants = immOnly;
+    s.selExclTopics = e.opt.anyExclTopic;
     s.prioOffline = m.numSelfHealing > 0;
     if (asc) {
       if (limit < 1.7976931348623157e308) {
@@ -920,6 +922,7 @@ class ResourceDistribution : public GoalImpl {
     s.selLeaders = lead;
     s.selImmigrants = e.opt.onlyImmigrants;
     s.selImmOrOffline = selfHealing && m.alive(b);
+    s.selExclTopics = e.opt.anyExclTopic;
     s.prioOffline = selfHealing;
     s.prioImmigrants = !e.opt.onlyImmigrants;
     s.scoreRes = res;

@@ -90,11 +90,31 @@ class RackAware : public GoalImpl {
     std::set<int> racks;
     for (int b = 0; b < m.B; ++b)
       if (m.alive(b)) racks.insert(m.bRack[b]);
-    if (m.maxRf > (int)racks.size())
+    const int numRacks = (int)racks.size();
+    if (e.opt.anyExclTopic) {
+      // replicationFactorByTopic entries in HashMap<String, Integer> order: the first included topic whose
+      // replication factor exceeds the alive racks names the shortfall (:77-94)
+      std::vector<int> rf(m.T, 1);
+      for (int p = 0; p < m.P; ++p) rf[m.pTopic[p]] = std::max(rf[m.pTopic[p]], m.pOff[p + 1] - m.pOff[p]);
+      TopicSet byTopic(&m.topicOrder);
+      for (int t = 0; t < m.T; ++t) byTopic.add(t, m.topicHash[t]);
+      std::vector<int32_t> order;
+      byTopic.order(order);
+      int maxIncluded = 1;
+      for (int t : order) {
+        if (e.opt.exclTopic[t]) continue;
+        maxIncluded = std::max(maxIncluded, rf[t]);
+        if (maxIncluded > numRacks)
+          throw OptimizationFailure("[" + name + "] Insufficient number of racks to distribute included replicas (Current: " +
+                                    std::to_string(numRacks) + ", Needed: " + std::to_string(maxIncluded) + ").");
+      }
+    } else if (m.maxRf > numRacks) {
       throw OptimizationFailure("[" + name + "] Insufficient number of racks to distribute each replica (Current: " +
-                                std::to_string(racks.size()) + ", Needed: " + std::to_string(m.maxRf) + ").");
+                                std::to_string(numRacks) + ", Needed: " + std::to_string(m.maxRf) + ").");
+    }
     Model::Spec s;
     s.selImmigrants = e.opt.onlyImmigrants;
+    s.selExclTopics = e.opt.anyExclTopic;
     for (int b = 0; b < m.B; ++b) m.track(b, sortId(kind, false, false), s);
     alive = aliveById(m);
     dg = DevGoal{};
@@ -150,11 +170,13 @@ class RackAware : public GoalImpl {
     for (int r = 0; r < m.R; ++r) {
       const int b = m.rBroker[r];
       if (m.alive(b) && !m.curOffline(r) && keep(m, r)) continue;
-      if (e.opt.onlyImmigrants && !m.immigrant(r)) continue;  // the tracked selection (immigrants only)
+      if (e.opt.onlyImmigrants && !m.immigrant(r)) continue;  // the tracked selection (immigrants only,
+      if (e.opt.anyExclTopic && !m.origOffline(r) && e.opt.exclTopic[m.pTopic[m.rPart[r]]]) continue;  // topics)
       byBroker[b].push_back(r);
     }
     Model::Spec spec;
     spec.selImmigrants = e.opt.onlyImmigrants;
+    spec.selExclTopics = e.opt.anyExclTopic;
     std::vector<int32_t> rows, cands, log;
     for (int b : order) {
       auto& v = byBroker[b];
@@ -203,6 +225,7 @@ class RackAware : public GoalImpl {
   void update(Engine& e) override {
     Model& m = e.m;
     for (int p = 0; p < m.P; ++p) {
+      if (e.opt.anyExclTopic && e.opt.exclTopic[m.pTopic[p]]) continue;  // excluded topics are not checked
       int racks[kMaxRf];
       const int n = m.pOff[p + 1] - m.pOff[p];
       for (int i = 0; i < n; ++i) {
@@ -276,6 +299,20 @@ class ReplicaCapacity : public GoalImpl {
     Model& m = e.m;
     maxR = e.bc.maxReplicasPerBroker;
     selfHealingMode = m.numDead > 0 || m.numBadDisk > 0;
+    if (e.opt.anyExclTopic) {
+      // replicas of excluded topics stay where they are (:116-139); on a BAD_DISKS broker the offline ones leave
+      for (int b = 0; b < m.B; ++b) {
+        if (!m.alive(b)) continue;
+        const bool badDisks = m.bState[b] == BState::BAD_DISKS;
+        int64_t excluded = 0;
+        for (int r : m.bRepl[b])
+          if (e.opt.exclTopic[m.pTopic[m.rPart[r]]] && !(badDisks && m.curOffline(r))) excluded++;
+        if (excluded > maxR)
+          throw OptimizationFailure("[" + name + "] Replicas of excluded topics in broker: " + std::to_string(excluded) +
+                                    " exceeds the maximum allowed number of replicas per broker: " +
+                                    std::to_string(maxR) + ".");
+      }
+    }
     const int n = allowedForReplicaMove(e, allowed);
     const int64_t maxInCluster = maxR * n;
     if ((int64_t)m.R > maxInCluster)
@@ -283,6 +320,7 @@ class ReplicaCapacity : public GoalImpl {
                                 " exceeds the maximum allowed replicas in cluster: " + std::to_string(maxInCluster));
     Model::Spec s;
     s.selImmigrants = e.opt.onlyImmigrants;
+    s.selExclTopics = e.opt.anyExclTopic;
     for (int b = 0; b < m.B; ++b) m.track(b, sortId(kind, false, false), s);
     dg = DevGoal{};
     dg.kind = DG_REPLICA_CAPACITY;
@@ -387,6 +425,7 @@ class Capacity : public GoalImpl {
     const bool selfHealing = m.numSelfHealing > 0;
     Model::Spec all;
     all.selImmigrants = e.opt.onlyImmigrants;
+    all.selExclTopics = e.opt.anyExclTopic;
     all.prioOffline = selfHealing;
     all.prioImmigrants = !e.opt.onlyImmigrants;
     all.scoreRes = res;
@@ -394,6 +433,7 @@ class Capacity : public GoalImpl {
     Model::Spec leaders;
     leaders.selLeaders = true;
     leaders.selImmigrants = e.opt.onlyImmigrants;
+    leaders.selExclTopics = e.opt.anyExclTopic;
     leaders.prioImmigrants = !e.opt.onlyImmigrants;
     leaders.scoreRes = res;
     leaders.scoreReverse = true;
@@ -505,6 +545,7 @@ class PotentialNwOut : public GoalImpl {
     fix = false;
     Model::Spec s;
     s.selImmigrants = e.opt.onlyImmigrants;
+    s.selExclTopics = e.opt.anyExclTopic;
     for (int b = 0; b < m.B; ++b) m.track(b, sortId(kind, false, false), s);
     dg = DevGoal{};
     dg.kind = DG_POTENTIAL_NW_OUT;
@@ -617,6 +658,9 @@ class TopicReplicaDistribution : public GoalImpl {
     if (selfHealing)
       for (int r = 0; r < m.R; ++r)
         if (m.selfHealing[r]) rebalanceTopic[m.pTopic[m.rPart[r]]] = 1;
+    if (!selfHealing && e.opt.anyExclTopic)  // GoalUtils.topicsToRebalance (GoalUtils.java:439-452)
+      for (int t = 0; t < m.T; ++t)
+        if (e.opt.exclTopic[t]) rebalanceTopic[t] = 0;
     const double margin = (e.bc.topicReplicaBalance - 1) * kBalanceMargin;
     upper.assign(m.T, 0);
     lower.assign(m.T, 0);
@@ -634,6 +678,7 @@ class TopicReplicaDistribution : public GoalImpl {
       Model::Spec s;
       s.selImmigrants = e.opt.onlyImmigrants;
       s.selImmOrOffline = selfHealing && m.alive(b);
+      s.selExclTopics = e.opt.anyExclTopic;
       m.track(b, sid(), s);
     }
     fix = false;
@@ -921,6 +966,7 @@ class LeaderReplicaDistribution : public GoalImpl {
       PhaseScope pc(PH_CAND_BUILD);
       for (size_t q = 0; q < leaders.size(); ++q) {
         const int r = leaders[q], p = m.rPart[r];
+        if (e.opt.anyExclTopic && e.opt.exclTopic[m.pTopic[p]]) continue;  // leaders of excluded topics stay
         ins.clear();
         for (int s = m.pOff[p]; s < m.pOff[p + 1]; ++s) ins.push_back(m.rBroker[m.pSlots[s]]);
         javaHashSetOrder(ins, hs);  // Partition.partitionBrokers()
@@ -978,7 +1024,7 @@ class LeaderReplicaDistribution : public GoalImpl {
     e.eligible(single, DA_LEADERSHIP, cands);
     if (cands.empty()) return true;
     for (int r : reps) {
-      if (m.rLeader[r] || m.curOffline(r)) continue;
+      if (m.rLeader[r] || m.curOffline(r) || (e.opt.anyExclTopic && e.opt.exclTopic[m.pTopic[m.rPart[r]]])) continue;
       pr.push_back(m.pLeader[m.rPart[r]]);
       pb.push_back(b);
     }
@@ -1039,6 +1085,7 @@ class LeaderReplicaDistribution : public GoalImpl {
     s.selLeaders = !fix;
     s.selOffline = fix;
     s.selImmigrants = (!fix && m.numSelfHealing > 0) || e.opt.onlyImmigrants;
+    s.selExclTopics = e.opt.anyExclTopic;
     m.track(b, id, s);
     const std::vector<int32_t> list = m.sorted(b, id);
     int n = (int)list.size();
@@ -1084,6 +1131,7 @@ class LeaderReplicaDistribution : public GoalImpl {
     Model::Spec s;
     s.selLeaders = true;
     s.selImmigrants = m.numDead > 0 || m.numBadDisk > 0 || e.opt.onlyImmigrants;
+    s.selExclTopics = e.opt.anyExclTopic;
     // The sources' SortedReplicas are tracked only for this call (the reference tracks them on entry and untracks
     // on exit) and initialised lazily on first poll; a source only loses replicas afterwards (moves go to b, whose
     // view is never read), so its live view equals a fresh snapshot of its current replicas: snapshots (cached per
@@ -1185,6 +1233,7 @@ class LeaderBytesIn : public GoalImpl {
     lowUtil = e.bc.lowUtil[R_NW_IN];
     Model::Spec s;
     s.selLeaders = true;
+    s.selExclTopics = e.opt.anyExclTopic;
     s.scoreRes = R_NW_IN;
     s.scoreReverse = true;
     for (int b = 0; b < m.B; ++b) m.track(b, sortId(kind, true, true), s);

@@ -176,6 +176,7 @@ void Model::build(const ccmi_cluster_desc& d) {
   bVer.assign(B, 0);
   sortedCache.assign(B, {});
   filteredCache.assign(B, {});
+  exclTopicSel.assign(T, 0);
   bUtilC.assign((size_t)4 * B, 0.0);
   bPctC.assign((size_t)4 * B, 0.0);
   rUtilC.assign((size_t)4 * R, 0.0);
@@ -636,6 +637,8 @@ bool Model::selects(const Spec& s, int r) const {
   if (s.selImmigrants && !immigrant(r)) return false;
   if (s.selImmOrOffline && !(immigrant(r) || curOffline(r))) return false;
   if (s.selOffline && !curOffline(r)) return false;
+  // ReplicaSortFunctionFactory.selectReplicasBasedOnExcludedTopics (:135-146)
+  if (s.selExclTopics && !origOffline(r) && exclTopicSel[pTopic[rPart[r]]]) return false;
   if (s.selAboveRes >= 0 && !(ru(r, s.selAboveRes) > s.aboveLimit)) return false;
   if (s.selBelowRes >= 0 && !(ru(r, s.selBelowRes) < s.belowLimit)) return false;
   return true;
@@ -718,6 +721,13 @@ static void cachePut(std::vector<Model::SortedCacheEntry>& cache, uint32_t ver, 
   slot->spec = s;
   slot->ver = ver;
   slot->v = std::move(v);
+}
+
+void Model::setExcludedTopicSelection(const std::vector<uint8_t>& t) {
+  if (t == exclTopicSel) return;
+  exclTopicSel = t;
+  for (auto& c : sortedCache) c.clear();
+  for (auto& c : filteredCache) c.clear();
 }
 
 std::shared_ptr<const std::vector<int32_t>> Model::snapshot(int b, const Spec& s) {

@@ -236,6 +236,7 @@ class Model {
   struct Spec {
     bool selLeaders = false, selFollowers = false, selImmigrants = false, selImmOrOffline = false;
     bool selOffline = false;
+    bool selExclTopics = false;  // selectReplicasBasedOnExcludedTopics over exclTopicSel
     int selAboveRes = -1, selBelowRes = -1;
     double aboveLimit = 0, belowLimit = 0;
     bool prioOffline = false, prioImmigrants = false;
@@ -243,7 +244,7 @@ class Model {
     bool scoreReverse = false;
     bool operator==(const Spec& o) const {
       return selLeaders == o.selLeaders && selFollowers == o.selFollowers && selImmigrants == o.selImmigrants &&
-             selOffline == o.selOffline &&
+             selOffline == o.selOffline && selExclTopics == o.selExclTopics &&
              selImmOrOffline == o.selImmOrOffline && selAboveRes == o.selAboveRes && selBelowRes == o.selBelowRes &&
              aboveLimit == o.aboveLimit && belowLimit == o.belowLimit && prioOffline == o.prioOffline &&
              prioImmigrants == o.prioImmigrants && scoreRes == o.scoreRes && scoreReverse == o.scoreReverse;
@@ -278,6 +279,10 @@ class Model {
   std::vector<uint32_t> bVer;
   std::vector<std::vector<SortedCacheEntry>> sortedCache;    // per broker, a few limit-free Specs
   std::vector<std::vector<SortedCacheEntry>> filteredCache;  // per broker, a few Specs with a utilization limit
+  // OptimizationOptions.excludedTopics as the selection function sees it ([T] flags); setting a different set
+  // drops the cached snapshots (their Specs do not carry the set)
+  std::vector<uint8_t> exclTopicSel;
+  void setExcludedTopicSelection(const std::vector<uint8_t>& t);
   void track(int b, int nameId, const Spec& s);
   void untrackAll(int nameId);
   void untrack(int b, int nameId);

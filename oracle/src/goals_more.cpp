@@ -70,19 +70,35 @@ void RackAwareGoal::initGoalState(ClusterModel& cm, const OptimizationOptions& o
   std::set<int> aliveRacks;
   for (int b : cm.aliveBrokers()) aliveRacks.insert(cm.brokers[b].rack);
   const int numAliveRacks = (int)aliveRacks.size();
-  if (!o.excludedTopics.empty()) throw std::invalid_argument("excluded topics are outside the oracle scope");
-  if (cm.maxReplicationFactor > numAliveRacks)
+  if (!o.excludedTopics.empty()) {
+    // replicationFactorByTopic entries in HashMap<String, Integer> order: the first included topic whose
+    // replication factor exceeds the alive racks names the shortfall (RackAwareGoal.java:77-94)
+    JHashSet byTopic([&cm](int x, int y) { return cm.topicNames[x].compare(cm.topicNames[y]); });
+    for (int t = 0; t < cm.numTopics(); ++t) byTopic.add(t, cm.topicHash[t]);
+    int maxIncluded = 1;
+    for (int t : byTopic.order()) {
+      if (o.excludedTopics.count(t)) continue;
+      maxIncluded = std::max(maxIncluded, cm.replicationFactorByTopic[t]);
+      if (maxIncluded > numAliveRacks)
+        throw OptimizationFailure("[RackAwareGoal] Insufficient number of racks to distribute included replicas (Current: " +
+                                  std::to_string(numAliveRacks) + ", Needed: " + std::to_string(maxIncluded) + ").");
+    }
+  } else if (cm.maxReplicationFactor > numAliveRacks) {
     throw OptimizationFailure("[RackAwareGoal] Insufficient number of racks to distribute each replica (Current: " +
                               std::to_string(numAliveRacks) + ", Needed: " + std::to_string(cm.maxReplicationFactor) +
                               ").");
+  }
   SortSpec spec;
   if (o.onlyMoveImmigrantReplicas) spec.selection.push_back({SelFn::IMMIGRANTS});
+  if (!o.excludedTopics.empty()) spec.selection.push_back({SelFn::EXCLUDED_TOPICS});
   for (size_t b = 0; b < cm.brokers.size(); ++b) cm.trackSortedReplicas((int)b, replicaSortName(false, false), spec);
 }
 
-// RackAwareGoal.updateGoalState (RackAwareGoal.java:131-143) + ensureRackAware (:159-185)
-void RackAwareGoal::updateGoalState(ClusterModel& cm, const OptimizationOptions&) {
+// RackAwareGoal.updateGoalState (RackAwareGoal.java:131-143) + ensureRackAware (:159-185): partitions of excluded
+// topics are not checked
+void RackAwareGoal::updateGoalState(ClusterModel& cm, const OptimizationOptions& o) {
   for (size_t p = 0; p < cm.partitions.size(); ++p) {
+    if (o.excludedTopics.count(cm.partitions[p].topic)) continue;
     std::set<int> racks;
     for (int r : cm.partitions[p].replicas) racks.insert(cm.brokers[cm.replicas[r].broker].rack);
     if (racks.size() != cm.partitions[p].replicas.size())
@@ -187,15 +203,26 @@ Acceptance ReplicaCapacityGoal::actionAcceptance(const BalancingAction& a, Clust
 }
 // ReplicaCapacityGoal.initGoalState (:100-150)
 void ReplicaCapacityGoal::initGoalState(ClusterModel& cm, const OptimizationOptions& o) {
-  if (!o.excludedTopics.empty()) throw std::invalid_argument("excluded topics are outside the oracle scope");
   int64_t total = 0;
   for (size_t b = 0; b < cm.brokers.size(); ++b) {
-    total += (int64_t)cm.brokers[b].replicas.size();
-    if (!cm.brokers[b].isAlive()) {
+    const Broker& br = cm.brokers[b];
+    total += (int64_t)br.replicas.size();
+    if (!br.isAlive()) {
       selfHealingMode_ = true;
       continue;
     }
-    if (cm.brokers[b].hasBadDisks()) selfHealingMode_ = true;
+    // replicas of excluded topics stay where they are (:125-138); on a BAD_DISKS broker the offline ones leave
+    if (br.hasBadDisks()) selfHealingMode_ = true;
+    if (o.excludedTopics.empty()) continue;
+    int64_t excluded = 0;
+    for (int r : br.replicas)
+      if (o.excludedTopics.count(cm.partitions[cm.replicas[r].partition].topic) &&
+          !(br.hasBadDisks() && cm.isCurrentOffline(r)))
+        excluded++;
+    if (excluded > bc_.maxReplicasPerBroker)
+      throw OptimizationFailure("[ReplicaCapacityGoal] Replicas of excluded topics in broker: " + std::to_string(excluded) +
+                                " exceeds the maximum allowed number of replicas per broker: " +
+                                std::to_string(bc_.maxReplicasPerBroker) + ".");
   }
   int allowed = 0;
   allowedForReplicaMove(cm, o, &allowed);
@@ -205,6 +232,7 @@ void ReplicaCapacityGoal::initGoalState(ClusterModel& cm, const OptimizationOpti
                               " exceeds the maximum allowed replicas in cluster: " + std::to_string(maxInCluster));
   SortSpec spec;
   if (o.onlyMoveImmigrantReplicas) spec.selection.push_back({SelFn::IMMIGRANTS});
+  if (!o.excludedTopics.empty()) spec.selection.push_back({SelFn::EXCLUDED_TOPICS});
   for (size_t b = 0; b < cm.brokers.size(); ++b) cm.trackSortedReplicas((int)b, replicaSortName(false, false), spec);
 }
 bool ReplicaCapacityGoal::selfSatisfied(ClusterModel& cm, const BalancingAction& a) {
@@ -309,6 +337,7 @@ void CapacityGoal::initGoalState(ClusterModel& cm, const OptimizationOptions& o)
   const bool selfHealing = !cm.selfHealingEligibleReplicas.empty();
   SortSpec all;
   if (o.onlyMoveImmigrantReplicas) all.selection.push_back({SelFn::IMMIGRANTS});
+  if (!o.excludedTopics.empty()) all.selection.push_back({SelFn::EXCLUDED_TOPICS});
   if (selfHealing) all.priority.push_back(PrioFn::OFFLINE);
   if (!o.onlyMoveImmigrantReplicas) all.priority.push_back(PrioFn::IMMIGRANTS);
   all.score = ScoreFn::REVERSE_BY_GROUP;
@@ -316,6 +345,7 @@ void CapacityGoal::initGoalState(ClusterModel& cm, const OptimizationOptions& o)
   SortSpec leaders;
   leaders.selection.push_back({SelFn::LEADERS});
   if (o.onlyMoveImmigrantReplicas) leaders.selection.push_back({SelFn::IMMIGRANTS});
+  if (!o.excludedTopics.empty()) leaders.selection.push_back({SelFn::EXCLUDED_TOPICS});
   if (!o.onlyMoveImmigrantReplicas) leaders.priority.push_back(PrioFn::IMMIGRANTS);
   leaders.score = ScoreFn::REVERSE_BY_GROUP;
   leaders.scoreResource = resource_;
@@ -441,6 +471,7 @@ void PotentialNwOutGoal::initGoalState(ClusterModel& cm, const OptimizationOptio
   fixOfflineReplicasOnly_ = false;
   SortSpec spec;
   if (o.onlyMoveImmigrantReplicas) spec.selection.push_back({SelFn::IMMIGRANTS});
+  if (!o.excludedTopics.empty()) spec.selection.push_back({SelFn::EXCLUDED_TOPICS});
   for (size_t b = 0; b < cm.brokers.size(); ++b) cm.trackSortedReplicas((int)b, replicaSortName(false, false), spec);
 }
 // PotentialNwOutGoal.updateGoalState (:197-213)
@@ -539,13 +570,15 @@ int TopicReplicaDistributionGoal::compareStats(const ClusterModelStats& s1, cons
 }
 // TopicReplicaDistributionGoal.initGoalState (:225-270) with balance limits (:103-145)
 void TopicReplicaDistributionGoal::initGoalState(ClusterModel& cm, const OptimizationOptions& o) {
-  if (!o.excludedTopics.empty()) throw std::invalid_argument("excluded topics are outside the oracle scope");
   int numAllowed = 0;
   allowed_ = allowedForReplicaMove(cm, o, &numAllowed);
   if (numAllowed == 0) throw OptimizationFailure("[" + name() + "] All alive brokers are excluded from replica moves.");
-  // topicsToRebalance: the self-healing replicas' topics, or all topics
+  // GoalUtils.topicsToRebalance (GoalUtils.java:439-452): the self-healing replicas' topics, or all topics but the
+  // excluded ones
   rebalanceTopic_.assign(cm.numTopics(), cm.selfHealingEligibleReplicas.empty() ? 1 : 0);
   for (int r : cm.selfHealingEligibleReplicas) rebalanceTopic_[cm.partitions[cm.replicas[r].partition].topic] = 1;
+  if (cm.selfHealingEligibleReplicas.empty())
+    for (int t : o.excludedTopics) rebalanceTopic_[t] = 0;
   const double margin = (bc_.topicReplicaBalancePercentage - 1) * 0.9;
   upper_.assign(cm.numTopics(), 0);
   lower_.assign(cm.numTopics(), 0);
@@ -565,6 +598,7 @@ void TopicReplicaDistributionGoal::initGoalState(ClusterModel& cm, const Optimiz
     SortSpec spec;
     if (o.onlyMoveImmigrantReplicas) spec.selection.push_back({SelFn::IMMIGRANTS});
     if (selfHealing && cm.brokers[b].isAlive()) spec.selection.push_back({SelFn::IMMIGRANT_OR_OFFLINE});
+    if (!o.excludedTopics.empty()) spec.selection.push_back({SelFn::EXCLUDED_TOPICS});
     cm.trackSortedReplicas((int)b, replicaSortName(false, false), spec);
   }
   fixOfflineReplicasOnly_ = false;
@@ -826,6 +860,7 @@ bool LeaderReplicaDistributionGoal::moveLeadershipOut(int b, ClusterModel& cm, c
   // new HashSet<>(broker.leaderReplicas())
   const std::vector<int> leaders = JHashSet::copyOf(cm.brokers[b].leaderSet).order();
   for (int leader : leaders) {
+    if (o.excludedTopics.count(cm.partitions[cm.replicas[leader].partition].topic)) continue;
     // partition brokers (a HashSet) minus b and brokers hosting an offline replica, collected into a HashSet
     std::vector<int> cands;
     for (int x : cm.partitionBrokersSet(cm.replicas[leader].partition)) {
@@ -847,7 +882,8 @@ bool LeaderReplicaDistributionGoal::moveLeadershipIn(int b, ClusterModel& cm, co
   int nl = cm.brokers[b].numLeaders;
   const std::vector<int> candidates{b};
   for (int r : cm.brokers[b].replicaSet.order()) {  // Broker.replicas(): HashSet order
-    if (cm.replicas[r].isLeader || cm.isCurrentOffline(r)) continue;
+    if (cm.replicas[r].isLeader || cm.isCurrentOffline(r) || o.excludedTopics.count(cm.partitions[cm.replicas[r].partition].topic))
+      continue;
     const int leader = cm.partitions[cm.replicas[r].partition].leader;
     if (maybeApplyBalancingAction(cm, leader, candidates, ActionType::LEADERSHIP_MOVEMENT, g, o) >= 0) {
       if (++nl >= lower_) return false;
@@ -882,6 +918,7 @@ bool LeaderReplicaDistributionGoal::moveReplicasOut(int b, ClusterModel& cm, con
   if (fixOfflineReplicasOnly_) spec.selection.push_back({SelFn::OFFLINE});
   if ((!fixOfflineReplicasOnly_ && !cm.selfHealingEligibleReplicas.empty()) || o.onlyMoveImmigrantReplicas)
     spec.selection.push_back({SelFn::IMMIGRANTS});
+  if (!o.excludedTopics.empty()) spec.selection.push_back({SelFn::EXCLUDED_TOPICS});
   cm.trackSortedReplicas(b, sortName, spec);
   std::vector<int> list = cm.sortedReplicasClone(b, sortName);
   int n = (int)list.size();
@@ -916,6 +953,7 @@ bool LeaderReplicaDistributionGoal::moveLeaderReplicasIn(int b, ClusterModel& cm
   spec.selection.push_back({SelFn::LEADERS});
   if (!cm.deadBrokers.empty() || !cm.brokersWithBadDisks.empty() || o.onlyMoveImmigrantReplicas)
     spec.selection.push_back({SelFn::IMMIGRANTS});
+  if (!o.excludedTopics.empty()) spec.selection.push_back({SelFn::EXCLUDED_TOPICS});
   for (size_t x = 0; x < cm.brokers.size(); ++x) cm.trackSortedReplicas((int)x, sortName, spec);
   int nl = cm.brokers[b].numLeaders;
   while (!pq.empty()) {
@@ -1019,6 +1057,7 @@ void LeaderBytesInDistributionGoal::initGoalState(ClusterModel& cm, const Optimi
   overLimit_ = false;
   SortSpec spec;
   spec.selection.push_back({SelFn::LEADERS});
+  if (!o.excludedTopics.empty()) spec.selection.push_back({SelFn::EXCLUDED_TOPICS});
   spec.score = ScoreFn::REVERSE_BY_GROUP;
   spec.scoreResource = NW_IN;
   for (size_t b = 0; b < cm.brokers.size(); ++b) cm.trackSortedReplicas((int)b, replicaSortName(true, true), spec);

@@ -51,8 +51,7 @@ OptimizerResult optimizations(ClusterModel& cm, const std::vector<int>& goalKind
   if (intra != 0 && intra != (int)goalKinds.size())
     throw std::invalid_argument("intra-broker goals cannot be optimized together with inter-broker goals");
   if (intra != 0 && cm.disks.empty()) throw std::invalid_argument("intra-broker goals need replica placement over disks");
-  if (!o.excludedTopics.empty() && intra == 0)
-    throw std::invalid_argument("excluded topics are supported by the intra-broker goals only");
+  cm.excludedTopicsSel = o.excludedTopics;  // ReplicaSortFunctionFactory.selectReplicasBasedOnExcludedTopics's set
   std::vector<std::unique_ptr<Goal>> owned;
   for (int k : goalKinds) owned.push_back(makeGoal(k, bc));
   const std::vector<int> initDist = cm.replicaDistributionFlat(), initDisks = cm.replicaDiskFlat();

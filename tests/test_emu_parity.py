@@ -92,6 +92,15 @@ EXCLUSION_CASES = [
      dict(excluded_brokers_for_leadership=[1, 2], excluded_brokers_for_replica_move=[3]), C1_GOALS),
     (dict(num_racks=6, num_brokers=24, num_replicas=4800, num_topics=30, num_dead_brokers=3),
      dict(only_move_immigrant_replicas=True), DEFAULT_GOALS),
+    # excludedTopics: ReplicaSortFunctionFactory.selectReplicasBasedOnExcludedTopics in every goal's sorted replicas,
+    # RackAwareGoal's included-topic rack check, ReplicaCapacityGoal's excluded-replica check,
+    # TopicReplicaDistributionGoal's topicsToRebalance, LeaderReplicaDistributionGoal's leadership loops
+    (dict(num_racks=5, num_brokers=20, num_replicas=6000, num_topics=300),
+     dict(excluded_topics=list(range(0, 300, 3))), DEFAULT_GOALS),
+    (dict(num_racks=6, num_brokers=24, num_replicas=4800, num_topics=30, num_dead_brokers=3),
+     dict(excluded_topics=[1, 2, 5, 8, 13, 21]), DEFAULT_GOALS),
+    (dict(num_racks=5, num_brokers=20, num_replicas=6000, num_topics=300, leader_in_first_position=1),
+     dict(excluded_topics=list(range(150))), C1_GOALS),
 ]
 
 

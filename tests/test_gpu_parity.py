@@ -158,6 +158,12 @@ def test_gpu_requested_destinations_match_oracle(gpu_lib, oracle_lib, props, req
      dict(excluded_brokers_for_leadership=[1, 2], excluded_brokers_for_replica_move=[3]), list(ccmi.C1_GOALS)),
     (dict(num_brokers=40), dict(excluded_brokers_for_leadership=[0, 1, 2, 3], excluded_brokers_for_replica_move=[4]),
      DEFAULT_GOALS),
+    # excludedTopics (selectReplicasBasedOnExcludedTopics in every goal; tests/test_excluded_topics.py for the KATs)
+    (dict(num_racks=5, num_brokers=20, num_replicas=6000, num_topics=300),
+     dict(excluded_topics=list(range(0, 300, 3))), DEFAULT_GOALS),
+    (dict(num_racks=6, num_brokers=24, num_replicas=4800, num_topics=30, num_dead_brokers=3),
+     dict(excluded_topics=[1, 2, 5, 8, 13, 21]), DEFAULT_GOALS),
+    (dict(num_brokers=40), dict(excluded_topics=list(range(0, 3000, 7))), list(ccmi.C1_GOALS)),
 ])
 def test_gpu_broker_exclusions_match_oracle(gpu_lib, oracle_lib, props, opts, goals):
     """Leader-replica exclusion and swap-row exclusion run as device checks (allowedBits bits 30/31)."""

@@ -144,14 +144,6 @@ def test_emu_intra_action_acceptance(emu_lib, oracle_lib):
         ccmi.GoalOptimizer(_zero_balance()).optimizations(cm, ccmi.goals_from_names(["DiskUsageDistributionGoal"]))
 
 
-def test_emu_excluded_topics_need_intra_goals(emu_lib):
-    buf = ccmi.RandomCluster.generate(emu_lib, num_racks=3, num_brokers=6, num_replicas=600, num_topics=20)
-    cm = ccmi.ClusterModel.from_buffers(buf)
-    with pytest.raises(ccmi.UnsupportedOperationException):
-        ccmi.GoalOptimizer().optimizations(cm, ccmi.goals_from_names(["ReplicaDistributionGoal"]),
-                                           ccmi.OptimizationOptions(excluded_topics=[1]))
-
-
 @pytest.mark.gpu
 @pytest.mark.parametrize("deck", DECKS, ids=IDS)
 def test_gpu_intra_broker_deck_matches_oracle(gpu_lib, oracle_lib, deck):
