@@ -114,7 +114,6 @@ void setOptions(ccmi_session* s, const ccmi_balancing_constraint* c, const ccmi_
     }
     opt.triggered = o->triggered_by_goal_violation != 0;
   }
-  if (s->model.numNew > 0) throw ccmi::Unsupported("NEW brokers are outside ABI v1 scope");
   e.opt = std::move(opt);
   s->model.setExcludedTopicSelection(e.opt.exclTopic);
 }
@@ -154,9 +153,6 @@ void validateChain(const ccmi_session* s, const int32_t* kinds, int n) {
   const int total = n + (int)s->engine->optimized.size();
   if (intra != 0 && intra != total)
     throw std::invalid_argument("intra-broker goals cannot be optimized together with inter-broker goals");
-  if (intra == 0) {
-    if (s->model.numBadDisk > 0) throw ccmi::Unsupported("inter-broker goals with BAD_DISKS brokers are not implemented");
-  }
 }
 
 // AnalyzerUtils.getDiff (AnalyzerUtils.java:63-93) against the session's initial placement
@@ -267,6 +263,7 @@ ccmi_status ccmi_session_create(int32_t device_ordinal, const ccmi_cluster_desc*
     for (int i = 0; i < m.R; ++i) pBrokers[i] = m.rBroker[m.pSlots[i]];
     s->device->uploadStatic(capRM.data(), m.rPart.data(), m.rOrig.data(), m.pOff.data(), m.topicNrep.data(),
                             m.bRack.data(), m.pTopic.data());
+    s->device->uploadIneligible(m.pIneligOff.data(), m.pIneligB.data(), (int)m.pIneligB.size());
     s->device->uploadDynamic(utilRM.data(), nrep.data(), m.bNlead.data(), pot.data(), lbi.data(), alive.data(),
                              rutilRM.data(), m.rBroker.data(), flags.data(), pBrokers.data(), plno.data(),
                              m.topicCountDense.data());

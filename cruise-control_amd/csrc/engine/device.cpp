@@ -142,7 +142,7 @@ Device::~Device() {
   }
   void* ps[] = {brokers_, replicas_, parts_, allowedAlive_, topicCount_, topicNrep_, topicScratch_, statsOut_, dReq_,
                 rowVisited_, dResult_, dDone_, tUpper_, tLower_, dRLoad_, dBLoad_, dBLnw_, dBPot_, dPOff_, dPSlots_,
-                dPLeader_, dChainLog_, dChainOut_};
+                dPLeader_, dChainLog_, dChainOut_, pIneligOff_, pIneligB_};
   for (void* p : ps)
     if (p) (void)hipFree(p);
   for (void* p : intraAllocs_)
@@ -189,6 +189,8 @@ DevTables Device::tables() const {
   t.tUpper = tUpper_;
   t.tLower = tLower_;
   t.stamps = stamps_;
+  t.pIneligOff = pIneligOff_;
+  t.pIneligB = pIneligB_;
   t.B = B_;
   t.R = R_;
   t.P = P_;
@@ -215,6 +217,15 @@ void Device::uploadStatic(const double* bCapRM, const int32_t* rPart, const int3
   }
   bRackHost_.assign(bRack, bRack + B_);
   hipCheck(hipMemcpy(topicNrep_, topicNrep, sizeof(int32_t) * T_, hipMemcpyHostToDevice), "upload topicNrep");
+}
+
+void Device::uploadIneligible(const int32_t* off, const int32_t* brokers, int n) {
+  DeviceGuard dg(ordinal_);
+  if (n <= 0) return;
+  hipCheck(hipMalloc((void**)&pIneligOff_, sizeof(int32_t) * (P_ + 1)), "hipMalloc pIneligOff");
+  hipCheck(hipMalloc((void**)&pIneligB_, sizeof(int32_t) * n), "hipMalloc pIneligB");
+  hipCheck(hipMemcpy(pIneligOff_, off, sizeof(int32_t) * (P_ + 1), hipMemcpyHostToDevice), "upload pIneligOff");
+  hipCheck(hipMemcpy(pIneligB_, brokers, sizeof(int32_t) * n, hipMemcpyHostToDevice), "upload pIneligB");
 }
 
 void Device::uploadDynamic(const double* bUtilRM, const int32_t* bNrep, const int32_t* bNlead, const double* bPot,
@@ -272,12 +283,12 @@ void Device::setAllowed(int slot, const uint8_t* allowedB) {
   hipCheck(hipStreamSynchronize(ST), "sync");
 }
 
-void Device::setExclusions(const uint8_t* exclLead, const uint8_t* exclMove) {
+void Device::setExclusions(const uint8_t* exclLead, const uint8_t* exclMove, const uint8_t* isNew) {
   DeviceGuard dg(ordinal_);
-  const uint32_t mask = (1u << kExclLeadBit) | (1u << kExclMoveBit);
+  const uint32_t mask = (1u << kExclLeadBit) | (1u << kExclMoveBit) | (1u << kNewBit);
   for (int b = 0; b < B_; ++b)
     allowedHost_[b] = (allowedHost_[b] & ~mask) | (exclLead[b] ? (1u << kExclLeadBit) : 0u) |
-                      (exclMove[b] ? (1u << kExclMoveBit) : 0u);
+                      (exclMove[b] ? (1u << kExclMoveBit) : 0u) | (isNew[b] ? (1u << kNewBit) : 0u);
   hipCheck(hipMemcpy2DAsync(&brokers_[0].allowedBits, sizeof(BrokerRec), allowedHost_.data(), sizeof(uint32_t),
                             sizeof(uint32_t), B_, hipMemcpyHostToDevice, ST),
            "upload exclusions");

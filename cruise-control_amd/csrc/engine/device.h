@@ -79,6 +79,8 @@ class Device {
   // initial upload (host arrays in device layout)
   void uploadStatic(const double* bCapRM, const int32_t* rPart, const int32_t* rOrig, const int32_t* pOff,
                     const int32_t* topicNrep, const int32_t* bRack, const int32_t* pTopic);
+  // Partition._ineligibleBrokers as CSR (n = list length; nothing is uploaded for n == 0)
+  void uploadIneligible(const int32_t* off, const int32_t* brokers, int n);
   void uploadDynamic(const double* bUtilRM, const int32_t* bNrep, const int32_t* bNlead, const double* bPot,
                      const double* bLeadNwIn, const uint8_t* bAlive, const double* rUtilRM, const int32_t* rBroker,
                      const uint8_t* rFlags, const int32_t* pBrokers, const double* pLeadNwOut,
@@ -86,7 +88,7 @@ class Device {
   void setAllowed(int slot, const uint8_t* allowedB);
   // OptimizationOptions.excludedBrokersFor{Leadership,ReplicaMove} as bits kExclLeadBit / kExclMoveBit of every
   // broker's allowedBits
-  void setExclusions(const uint8_t* exclLead, const uint8_t* exclMove);
+  void setExclusions(const uint8_t* exclLead, const uint8_t* exclMove, const uint8_t* isNew);
   // TopicReplicaDistributionGoal balance limits per topic (frozen at its initGoalState)
   void setTopicLimits(const int32_t* upper, const int32_t* lower);
 
@@ -144,6 +146,7 @@ class Device {
   ReplicaRec* replicas_ = nullptr;
   PartitionRec* parts_ = nullptr;
   int32_t *topicCount_ = nullptr, *topicNrep_ = nullptr, *tUpper_ = nullptr, *tLower_ = nullptr;
+  int32_t *pIneligOff_ = nullptr, *pIneligB_ = nullptr;
   uint8_t* allowedAlive_ = nullptr;
   std::vector<BrokerRec> hBrokers_;
   std::vector<PartitionRec> hParts_;

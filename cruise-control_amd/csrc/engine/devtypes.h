@@ -23,6 +23,8 @@ namespace ccmi {
 constexpr int kMaxGoals = 20;
 constexpr int kExclLeadBit = 31;  // allowedBits bit of a broker excluded for leadership (above every goal slot)
 constexpr int kExclMoveBit = 30;  // allowedBits bit of a broker excluded for replica moves
+constexpr int kNewBit = 29;       // allowedBits bit of a NEW broker (Broker.State.NEW)
+static_assert(kMaxGoals <= kNewBit, "goal slots overlap the broker flag bits");
 constexpr int kMaxRf = 8;
 // Dirty rows of each kind a cross/pair scan stages into its LDS overlay itself (kernels/scan.hip OverlayLds); a
 // launch with more pending rows of any kind runs `prep` first (device.cpp stageScan). Shared by host and kernel.
@@ -77,6 +79,10 @@ struct DevProgram {
   int32_t filter;   // DevFilter of a CROSS scan
   int32_t exclLeadMove;  // replica moves: a leader replica may not go to a broker excluded for leadership
   int32_t swapExcl;      // swaps: GoalUtils.eligibleReplicasForSwap exclusion rules apply
+  // new brokers in the cluster: moves / leadership go only to NEW brokers or the replica's original broker
+  // (GoalUtils.eligibleBrokers :193-198); swaps follow eligibleReplicasForSwap's CASE#1/#3 (:276-297)
+  int32_t newOnly;
+  int32_t pad1;
   DevGoal goals[kMaxGoals];
 };
 
@@ -114,6 +120,10 @@ struct DevTables {
   const int32_t* tUpper;
   const int32_t* tLower;
   unsigned long long* stamps;  // diagnostics (CCMI_STAMPS=1): s_memrealtime stamps of workgroup 0, else null
+  // Partition._ineligibleBrokers (BAD_DISKS brokers that held an offline replica of the partition, static):
+  // CSR [P + 1] / list; null when the model has none
+  const int32_t* pIneligOff;
+  const int32_t* pIneligB;
   int32_t B, R, P, ldB;
 };
 

@@ -56,6 +56,7 @@ struct HostView {
     return has;
   }
   int rack(int b) const { return m.bRack[b]; }
+  bool ineligible(int p, int b) const { return m.ineligible(p, b); }
   bool otherOnRack(int p, int self, int rk) const {
     for (int i = pbegin(p); i < pend(p); ++i)
       if (pbroker(i) != self && m.bRack[pbroker(i)] == rk) return true;
@@ -116,7 +117,17 @@ DevProgram Engine::program(const GoalImpl& self, int action) const {
   // skips brokers excluded for leadership — replica-dependent, so it is checked per candidate on the device
   p.exclLeadMove = (opt.anyExclLead && !opt.anyRequested && action == DA_MOVE) ? 1 : 0;
   p.swapExcl = (action == DA_SWAP && (opt.anyExclLead || opt.anyExclMove)) ? 1 : 0;
+  // GoalUtils.eligibleBrokers returns before the new-broker filter when destinations are requested (:189-191);
+  // eligibleReplicasForSwap has no such return
+  p.newOnly = (m.numNew > 0 && (action == DA_SWAP || !opt.anyRequested)) ? 1 : 0;
   return p;
+}
+
+// The replica-dependent candidate filters of GoalUtils.eligibleBrokers, as the device applies them
+// (predicates.h candidateBlocked): a (replica, destination) candidate the reference never visits.
+bool Engine::blocked(const DevProgram& prog, int r, int b) const {
+  if (prog.exclLeadMove && m.rLeader[r] && opt.exclLead[b]) return true;
+  return prog.newOnly && !m.isNew(b) && b != m.rOrig[r];
 }
 
 // GoalUtils.eligibleBrokers (GoalUtils.java:122-160), the replica-independent part: requested destinations,
@@ -135,10 +146,20 @@ void Engine::eligible(const std::vector<int32_t>& in, int action, std::vector<in
   }
 }
 
-// Reference-equivalent candidates of a cross scan whose leader rows skip brokers excluded for leadership:
+// Reference-equivalent candidates of a cross scan whose rows skip replica-dependent ineligible brokers (blocked):
 // every row before the hit visits its eligible list, the hit row up to and including the winner.
-int64_t Engine::exclLeadCount(const int32_t* reps, int K, const std::vector<int32_t>& cands, int64_t key) const {
+int64_t Engine::exclLeadCount(const DevProgram& prog, const int32_t* reps, int K, const std::vector<int32_t>& cands,
+                              int64_t key) const {
   const int N = (int)cands.size();
+  if (prog.newOnly) {
+    const int rows = key >= 0 ? (int)(key / N) : K;
+    int64_t c = 0;
+    for (int k = 0; k <= rows && k < K; ++k) {
+      const int upto = k < rows ? N : (int)(key % N) + 1;
+      for (int j = 0; j < upto; ++j) c += blocked(prog, reps[k], cands[j]) ? 0 : 1;
+    }
+    return c;
+  }
   int nEx = 0;
   for (int b : cands) nEx += opt.exclLead[b] ? 1 : 0;
   const int rows = key >= 0 ? (int)(key / N) : K;
@@ -167,7 +188,7 @@ int64_t Engine::crossScan(GoalImpl& self, int action, const std::vector<int32_t>
   const int c0 = (int)((int64_t)N * shard.rank / shard.count), c1 = (int)((int64_t)N * (shard.rank + 1) / shard.count);
   const int64_t key = combine(dev->scanCross(prog, reps.data() + r0, K, cands.data(), N, c0, c1));
   if (count) {
-    if (prog.exclLeadMove) candidates += exclLeadCount(reps.data() + r0, K, cands, key);
+    if (prog.exclLeadMove || prog.newOnly) candidates += exclLeadCount(prog, reps.data() + r0, K, cands, key);
     else candidates += key >= 0 ? key + 1 : (int64_t)K * N;
   }
   return key;
@@ -190,9 +211,9 @@ int64_t Engine::pairScan(GoalImpl& self, const std::vector<int32_t>& pr, const s
   const DevProgram prog = program(self, action);
   const int64_t key = combine(dev->scanPairs(prog, pr.data(), pb.data(), p0, p1));
   if (!count) return key;
-  if (prog.exclLeadMove) {
+  if (prog.exclLeadMove || prog.newOnly) {
     const size_t end = key >= 0 ? (size_t)key + 1 : pr.size();
-    for (size_t q = 0; q < end; ++q) candidates += (m.rLeader[pr[q]] && opt.exclLead[pb[q]]) ? 0 : 1;
+    for (size_t q = 0; q < end; ++q) candidates += blocked(prog, pr[q], pb[q]) ? 0 : 1;
   } else {
     candidates += key >= 0 ? key + 1 : (int64_t)pr.size();
   }
@@ -205,8 +226,32 @@ int64_t Engine::swapScan(GoalImpl& self, const std::vector<int32_t>& srcs, const
   PhaseScope ps(PH_DEV_SCAN);
   m.flushToDevice();
   int64_t visited = 0;
-  const int64_t key = dev->scanSwap(program(self, DA_SWAP), srcs.data(), (int)srcs.size(), cbOff.data(),
-                                    (int)cbOff.size() - 1, cbRep.data(), (int)cbRep.size(), &visited);
+  const DevProgram prog = program(self, DA_SWAP);
+  // eligibleReplicasForSwap CASE#2 (GoalUtils.java:289-294): an old source broker and a NEW destination make the
+  // reference call removeIf on an unmodifiable SortedSet view; the first such row (rows are candidate-broker major)
+  // throws unless an earlier row accepts a swap
+  int64_t throwRow = -1;
+  if (prog.newOnly) {
+    const int S = (int)srcs.size();
+    for (int g = 0; g + 1 < (int)cbOff.size() && throwRow < 0; ++g) {
+      if (cbOff[g] == cbOff[g + 1]) continue;
+      const int db = m.rBroker[cbRep[cbOff[g]]];
+      if (!m.isNew(db)) continue;
+      for (int s = 0; s < S; ++s) {
+        const int sr = srcs[s];
+        const bool excl = prog.swapExcl && !m.origOffline(sr) &&
+                          ((opt.anyExclMove && opt.exclMove[db]) || (m.rLeader[sr] && opt.anyExclLead && opt.exclLead[db]));
+        if (!excl && !m.isNew(m.rBroker[sr])) {
+          throwRow = (int64_t)g * S + s;
+          break;
+        }
+      }
+    }
+  }
+  const int64_t key = dev->scanSwap(prog, srcs.data(), (int)srcs.size(), cbOff.data(), (int)cbOff.size() - 1,
+                                    cbRep.data(), (int)cbRep.size(), &visited);
+  if (throwRow >= 0 && (key < 0 || (key >> 24) > throwRow))
+    throw Unsupported("UnsupportedOperationException: removeIf on an unmodifiable sorted replica view");
   candidates += visited;
   return key;
 }
@@ -221,9 +266,26 @@ int64_t Engine::chainPairs(GoalImpl& self, int action, const std::vector<int32_t
   PhaseScope ps(PH_DEV_SCAN);
   m.flushToDevice();
   m.flushChainLoads();
+  const DevProgram prog = program(self, action);
   const Device::ChainResult r =
-      dev->chainPairs(program(self, action), pr.data(), pb.data(), next.data(), (int)pr.size(), maxAccepts, log);
-  candidates += r.visited;
+      dev->chainPairs(prog, pr.data(), pb.data(), next.data(), (int)pr.size(), maxAccepts, log);
+  if (prog.exclLeadMove || prog.newOnly) {
+    // the device counts every pair it passes; the reference never visits the blocked ones (the filters are static
+    // over a leadership chain: original brokers, NEW states and exclusions do not change)
+    int64_t visited = 0;
+    int start = 0;
+    auto add = [&](int a, int b) {
+      for (int q = a; q < b; ++q) visited += blocked(prog, pr[q], pb[q]) ? 0 : 1;
+    };
+    for (size_t i = 0; i < (size_t)r.accepts; ++i) {
+      add(start, log[i] + 1);
+      start = next[log[i]];
+    }
+    if (r.accepts < maxAccepts) add(start, (int)pr.size());
+    candidates += visited;
+  } else {
+    candidates += r.visited;
+  }
   return r.accepts;
 }
 
@@ -362,11 +424,13 @@ bool Engine::optimizeGoal(std::unique_ptr<GoalImpl> g, ccmi_goal_result* res) {
   g->dg.allowedSlot = (int)optimized.size();
   g->init(*this);
   dev->setAllowed(g->dg.allowedSlot, g->allowed.data());
-  if (opt.anyExclLead || opt.anyExclMove || exclOnDevice) {
+  if (opt.anyExclLead || opt.anyExclMove || m.numNew > 0 || exclOnDevice) {
     const std::vector<uint8_t> none(m.B, 0);
+    std::vector<uint8_t> isNew(m.B, 0);
+    for (int b = 0; b < m.B; ++b) isNew[b] = m.isNew(b) ? 1 : 0;
     dev->setExclusions(opt.anyExclLead ? opt.exclLead.data() : none.data(),
-                       opt.anyExclMove ? opt.exclMove.data() : none.data());
-    exclOnDevice = opt.anyExclLead || opt.anyExclMove;
+                       opt.anyExclMove ? opt.exclMove.data() : none.data(), isNew.data());
+    exclOnDevice = opt.anyExclLead || opt.anyExclMove || m.numNew > 0;
   }
   const bool brokenEmpty = m.numDead == 0 && m.numBadDisk == 0;
   bool exclWithReplicas = false;

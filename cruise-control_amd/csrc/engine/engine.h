@@ -93,7 +93,9 @@ class Engine {
   int64_t crossScan(GoalImpl& self, int action, const std::vector<int32_t>& reps, size_t r0,
                     const std::vector<int32_t>& cands, int filter = FILTER_NONE, bool count = true,
                     size_t r1 = (size_t)-1);
-  int64_t exclLeadCount(const int32_t* reps, int K, const std::vector<int32_t>& cands, int64_t key) const;
+  int64_t exclLeadCount(const DevProgram& prog, const int32_t* reps, int K, const std::vector<int32_t>& cands,
+                        int64_t key) const;
+  bool blocked(const DevProgram& prog, int r, int b) const;
   bool exclOnDevice = false;  // the device's broker exclusion bits are set
   int64_t pairScan(GoalImpl& self, const std::vector<int32_t>& pr, const std::vector<int32_t>& pb,
                    int action = DA_LEADERSHIP, bool count = true);

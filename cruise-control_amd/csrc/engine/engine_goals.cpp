@@ -136,6 +136,7 @@ class RackAware : public GoalImpl {
   static int64_t eligibleCount(const Engine& e, int r, const std::vector<int32_t>& cands, size_t upto) {
     const Model& m = e.m;
     const bool exclLead = e.opt.anyExclLead && !e.opt.anyRequested && m.rLeader[r];
+    const bool newOnly = m.numNew > 0 && !e.opt.anyRequested;  // GoalUtils.eligibleBrokers :193-198
     int racks[kMaxRf];
     int n = 0;
     const int p = m.rPart[r];
@@ -150,6 +151,7 @@ class RackAware : public GoalImpl {
       bool in = true;
       for (int i = 0; i < n; ++i) in &= racks[i] != m.bRack[cands[j]];
       if (exclLead && e.opt.exclLead[cands[j]]) in = false;
+      if (newOnly && !m.isNew(cands[j]) && cands[j] != m.rOrig[r]) in = false;
       c += in;
     }
     return c;
@@ -594,9 +596,16 @@ class PotentialNwOut : public GoalImpl {
       const int64_t key = e.crossScan(*this, DA_MOVE, list, i, cands, FILTER_NONE, false);
       const size_t N = cands.size();
       const size_t kEnd = key < 0 ? list.size() : i + (size_t)(key / (int64_t)std::max<size_t>(N, 1));
+      const bool newOnly = m.numNew > 0 && !e.opt.anyRequested;
       auto rowCount = [&](int r, size_t upto) {  // visited eligible brokers of one row: partition brokers removed
         int64_t c = (int64_t)upto;
         const int p = m.rPart[r];
+        if (newOnly) {  // only NEW brokers or the replica's original broker are eligible (GoalUtils.java:193-198)
+          c = 0;
+          for (size_t j = 0; j < upto; ++j)
+            if ((m.isNew(cands[j]) || cands[j] == m.rOrig[r]) && m.replicaOn(p, cands[j]) < 0) c++;
+          return c;
+        }
         for (int s = m.pOff[p]; s < m.pOff[p + 1]; ++s) {
           const int x = pos[m.rBroker[m.pSlots[s]]];
           if (x >= 0 && (size_t)x < upto) c--;

@@ -167,6 +167,21 @@ void Model::build(const ccmi_cluster_desc& d) {
         numSelfHealing++;
       }
   }
+  {
+    std::vector<std::vector<int32_t>> inel(P);
+    for (int b = 0; b < B; ++b)
+      if (bState[b] == BState::BAD_DISKS)
+        for (int r : bRepl[b]) {
+          auto& v = inel[rPart[r]];
+          if (rInOff[r] && std::find(v.begin(), v.end(), b) == v.end()) v.push_back(b);
+        }
+    pIneligOff.assign(P + 1, 0);
+    pIneligB.clear();
+    for (int p = 0; p < P; ++p) {
+      pIneligB.insert(pIneligB.end(), inel[p].begin(), inel[p].end());
+      pIneligOff[p + 1] = (int32_t)pIneligB.size();
+    }
+  }
   for (int k = 0; k < 4; ++k) {
     double c = 0;
     for (int b = 0; b < B; ++b)

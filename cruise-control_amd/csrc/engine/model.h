@@ -151,6 +151,14 @@ class Model {
   std::vector<uint8_t> selfHealing;         // per replica: in _selfHealingEligibleReplicas
   int64_t numSelfHealing = 0;
   int numDead = 0, numNew = 0, numBadDisk = 0;
+  // Partition._ineligibleBrokers: a BAD_DISKS broker holding an offline replica of the partition may not receive
+  // one of its replicas (ClusterModel.setBrokerState :325-331); CSR over partitions, static
+  std::vector<int32_t> pIneligOff, pIneligB;
+  bool ineligible(int p, int b) const {
+    for (int k = pIneligOff[p]; k < pIneligOff[p + 1]; ++k)
+      if (pIneligB[k] == b) return true;
+    return false;
+  }
   int maxRf = 1;
   // action log + counters
   std::vector<ActionRec> log;

@@ -51,7 +51,8 @@ CCMI_HD bool hostsPartition(const V& v, int p, int b) {
 template <class V>
 CCMI_HD bool legitMove(const V& v, int r, int dst, int action) {
   const bool has = hostsPartition(v, v.rpart(r), dst);
-  if (action == DA_MOVE) return !has;  // no broken-disk ineligibility in ABI v1 (no BAD_DISKS brokers)
+  // Partition.canAssignReplicaToBroker: not one of the partition's ineligible (broken-disk) brokers
+  if (action == DA_MOVE) return !has && !v.ineligible(v.rpart(r), dst);
   if (action == DA_LEADERSHIP) return (v.flags(r) & RF_LEADER) && has;
   return false;
 }
@@ -328,11 +329,29 @@ CCMI_HD bool moveCandidateAccepted(const DevProgram& prog, const V& v, int r, in
 // GoalUtils.eligibleReplicasForSwap (GoalUtils.java:258-274): a swap row is empty when the destination broker is
 // excluded for leadership and the (originally online) source replica is a leader, or the destination is excluded
 // for replica moves and the source replica is originally online.
+// GoalUtils.eligibleBrokers' replica-dependent filters for a (replica, destination) candidate of a move or
+// leadership scan: a leader replica's move skips brokers excluded for leadership (GoalUtils.java:170-180), and with
+// NEW brokers only new brokers or the replica's original broker are eligible (:193-198). (PreView, which caches the
+// destination's bits, has its own copy: exclLeadBlocked.)
+template <class V>
+CCMI_HD bool candidateBlocked(const DevProgram& prog, const V& v, int r, int db) {
+  if (prog.exclLeadMove && (v.flags(r) & RF_LEADER) && v.allowed(kExclLeadBit, db)) return true;
+  return prog.newOnly && !v.allowed(kNewBit, db) && db != v.rorig(r);
+}
+
+// With NEW brokers, a row is kept only when the source broker is new and the destination is new or the source
+// replica's original broker (CASE#1); the CASE#2 rows (old source, new destination) are the host's (Engine::swapScan).
 template <class V>
 CCMI_HD bool swapRowExcluded(const DevProgram& prog, const V& v, int sr, int db) {
-  if (!prog.swapExcl || v.origOff(sr)) return false;
-  if (v.allowed(kExclMoveBit, db)) return true;
-  return (v.flags(sr) & RF_LEADER) && v.allowed(kExclLeadBit, db);
+  if (prog.swapExcl && !v.origOff(sr)) {
+    if (v.allowed(kExclMoveBit, db)) return true;
+    if ((v.flags(sr) & RF_LEADER) && v.allowed(kExclLeadBit, db)) return true;
+  }
+  if (prog.newOnly) {
+    const int sb = v.rbroker(sr);
+    if (!(v.allowed(kNewBit, sb) && (v.allowed(kNewBit, db) || v.rorig(sr) == db))) return true;
+  }
+  return false;
 }
 
 // One step of AbstractGoal.maybeApplySwapAction's loop for (source sr, destination replica dr on db):

@@ -60,8 +60,8 @@ ccmi_cluster_buffers* generateRandomCluster(const ccmi_random_cluster_props& p) 
   if (p.num_racks > B || B <= 0 || p.num_racks <= 0) throw std::invalid_argument("Random cluster generation failed due to bad input.");
   if (p.jbod < 0 || p.jbod > 2 || (p.jbod == 2 && (p.num_logdirs < 1 || p.num_logdirs > 8)))
     throw std::invalid_argument("jbod must be 0, 1 or 2 (2: 1..8 logdirs)");
-  if (p.num_brokers_with_bad_disk != 0 && !p.jbod)
-    throw std::invalid_argument("bad-disk brokers need replica placement over disks (jbod)");
+  if (p.num_brokers_with_bad_disk != 0 && !p.jbod && p.num_dead_brokers != 0)
+    throw std::invalid_argument("bad-disk brokers without disks next to dead brokers are not generated");
   if (p.num_dead_brokers < 0 || p.num_brokers_with_bad_disk < 0 ||
       B < p.num_dead_brokers + p.num_brokers_with_bad_disk || p.num_topics <= 0 ||
       p.min_replication > p.max_replication || (p.leader_in_first_position && p.min_replication < 2) ||
@@ -223,6 +223,36 @@ ccmi_cluster_buffers* generateRandomCluster(const ccmi_random_cluster_props& p) 
   }
   o.repOffline.assign(o.repPart.size(), 0);
   std::vector<int32_t> repDisk;
+  if (!p.jbod && p.num_brokers_with_bad_disk > 0) {
+    // markBrokenBrokers without disk information (RandomCluster.java:409-449, no excluded topics): the first replica
+    // in Broker.replicas() (HashSet<Replica>) order of each of the first alive brokers with replicas becomes
+    // original-offline, and the broker whose id is the running count becomes BAD_DISKS (the reference passes the
+    // count, not the broker's id)
+    std::vector<int32_t> topicRank(T), topicHash(T);
+    {
+      std::vector<int> idx(T);
+      for (int t = 0; t < T; ++t) idx[t] = t;
+      std::sort(idx.begin(), idx.end(), [&](int a, int b) { return o.topicStr[a] < o.topicStr[b]; });
+      for (int i = 0; i < T; ++i) topicRank[idx[i]] = i;
+    }
+    for (int t = 0; t < T; ++t) topicHash[t] = jStringHash(o.topicStr[t].c_str());
+    GenReplicaOrder ord{&o, &topicRank};
+    std::vector<JHashSet<GenReplicaOrder>> sets(B, JHashSet<GenReplicaOrder>(&ord));
+    for (size_t r = 0; r < o.repPart.size(); ++r) {
+      const int part = o.repPart[r];
+      const int32_t tp = jMix(jMix(1, o.partNumber[part]), topicHash[o.partTopic[part]]);
+      sets[o.repBroker[r]].add((int)r, jMix(jMix(1, tp), o.repBroker[r]));
+    }
+    std::vector<int32_t> members;
+    int idx = 0;
+    for (int b = 0; b < B && idx < p.num_brokers_with_bad_disk; ++b) {
+      if (sets[b].size() == 0 || o.brokerState[b] == CCMI_BROKER_BAD_DISKS) continue;
+      sets[b].order(members);
+      o.repOffline[members.front()] = 1;
+      o.brokerState[idx] = CCMI_BROKER_BAD_DISKS;
+      idx++;
+    }
+  }
   if (p.jbod) {
     // Uniform-randomly assign replicas to disks: brokers by id, Broker.replicas() (HashSet<Replica>) order, the
     // conflict resolver counting per broker (RandomCluster.java:315-331)

@@ -51,6 +51,12 @@ struct DevView {
     return has;
   }
   __device__ __forceinline__ int rack(int b) const { return t.brokers[b].rack; }
+  __device__ __forceinline__ bool ineligible(int p, int b) const {
+    if (!t.pIneligOff) return false;
+    bool in = false;
+    for (int k = t.pIneligOff[p]; k < t.pIneligOff[p + 1]; ++k) in |= t.pIneligB[k] == b;
+    return in;
+  }
   __device__ __forceinline__ bool otherOnRack(int p, int self, int rk) const {
     const PartitionRec& x = t.parts[p];
     bool any = false;
@@ -191,6 +197,7 @@ struct PreView {
   int drack, prk0, prk1, prk2, prk3, prk4, prk5, prk6, prk7;
   double spot, dpot, plno, slbi, dlbi;
   int snlead, dnlead, topic, stc, dtc, tup, tlo;
+  bool inelig;  // dst is one of the row's partition's ineligible brokers
 
   static __device__ __forceinline__ double sel(int k, double a, double b, double c, double d) {
     return k == 0 ? a : (k == 1 ? b : (k == 2 ? c : d));
@@ -291,6 +298,9 @@ struct PreView {
       slbi = x.leadNwIn;
     }
     aliveBits = (aliveBits & 4u) | (aSrc ? 1u : 0u);
+    inelig = false;
+    if (t.pIneligOff)  // uniform: only models with BAD_DISKS brokers carry the table
+      for (int k = t.pIneligOff[p]; k < t.pIneligOff[p + 1]; ++k) inelig |= t.pIneligB[k] == dst;
     if (prog.needs & NEED_TOPIC) {
       tup = t.tUpper[topic];
       tlo = t.tLower[topic];
@@ -353,9 +363,13 @@ struct PreView {
     return (pb0 == b) | (pb1 == b) | (pb2 == b) | (pb3 == b) | (pb4 == b) | (pb5 == b) | (pb6 == b) | (pb7 == b);
   }
   __device__ __forceinline__ int rack(int /*b == dst*/) const { return drack; }
-  // GoalUtils.filterOutBrokersExcludedForLeadership for a leader replica's move (GoalUtils.java:170-180)
+  __device__ __forceinline__ bool ineligible(int /*p*/, int /*b == dst*/) const { return inelig; }
+  // GoalUtils.eligibleBrokers' replica-dependent filters: filterOutBrokersExcludedForLeadership for a leader
+  // replica's move (GoalUtils.java:170-180), and with NEW brokers only new brokers or the replica's original broker
+  // (:193-198)
   __device__ __forceinline__ bool exclLeadBlocked(const DevProgram& prog) const {
-    return prog.exclLeadMove && (rflags & RF_LEADER) && ((dAllowed >> kExclLeadBit) & 1u);
+    if (prog.exclLeadMove && (rflags & RF_LEADER) && ((dAllowed >> kExclLeadBit) & 1u)) return true;
+    return prog.newOnly && !((dAllowed >> kNewBit) & 1u) && dst != orig;
   }
   __device__ __forceinline__ bool otherOnRack(int /*p*/, int self, int rk) const {
     return (pb0 >= 0 && pb0 != self && prk0 == rk) | (pb1 >= 0 && pb1 != self && prk1 == rk) |

@@ -172,7 +172,7 @@ int AbstractGoal::maybeApplySwapAction(ClusterModel& cm, int src, const std::vec
   if (!(cm.newBrokers.empty() ||
         (cm.brokers[srcBroker].isNew() && (cm.brokers[destBroker].isNew() || sr.origBroker == destBroker)))) {
     if (cm.brokers[destBroker].isNew())
-      throw std::runtime_error("UnsupportedOperationException: removeIf on an unmodifiable sorted replica view");
+      throw UnsupportedOperation("UnsupportedOperationException: removeIf on an unmodifiable sorted replica view");
     return -1;
   }
   for (int dr : candidates) {

@@ -24,6 +24,10 @@ namespace oracle {
 struct OptimizationFailure : std::runtime_error {
   using std::runtime_error::runtime_error;
 };
+// java.lang.UnsupportedOperationException thrown inside the reference's goal code
+struct UnsupportedOperation : std::runtime_error {
+  using std::runtime_error::runtime_error;
+};
 
 class Goal;
 using GoalList = std::vector<Goal*>;

@@ -600,7 +600,8 @@ int ClusterModel::diskOf(int b, const std::string& logdir) const {
 }
 void ClusterModel::diskAddReplica(int d, int r) {
   Disk& dk = disks[d];
-  if (dk.replicas.count(r)) throw std::logic_error("Disk " + dk.logdir + " already has replica");
+  if (dk.replicas.count(r)) throw std::logic_error("Disk " + dk.logdir + " already has replica " + topicNames[partitions[replicas[r].partition].topic] +
+                                               "-" + std::to_string(partitions[replicas[r].partition].number));
   dk.utilization += replicaUtil(r, DISK);
   dk.replicas.insert(r);
   replicas[r].disk = d;
@@ -611,12 +612,24 @@ void ClusterModel::diskAddReplica(int d, int r) {
 }
 void ClusterModel::diskRemoveReplica(int d, int r) {
   Disk& dk = disks[d];
-  if (!dk.replicas.count(r)) throw std::logic_error("Disk " + dk.logdir + " does not has replica");
+  if (!dk.replicas.count(r)) throw std::logic_error("Disk " + dk.logdir + " does not has replica " + topicNames[partitions[replicas[r].partition].topic] +
+                                               "-" + std::to_string(partitions[replicas[r].partition].number));
   dk.utilization -= replicaUtil(r, DISK);
   dk.replicas.erase(r);
   for (auto& kv : dk.sorted) {
     SortedReplicas& sr = *kv.second;
     if (sr.initialized) sr.set.erase(r);
+  }
+}
+// Replica.markOriginalOffline (Replica.java:91-97)
+void ClusterModel::markReplicaOriginalOffline(int r) {
+  Replica& rep = replicas[r];
+  if (rep.broker != rep.origBroker) throw std::logic_error("Cannot mark an immigrant replica as offline.");
+  rep.origOfflineFlag = true;
+  if (!rep.inBrokerOffline) {
+    rep.inBrokerOffline = true;
+    brokers[rep.origBroker].numOffline++;
+    brokers[rep.origBroker].offlineSet.add(r, replicaHash(r));
   }
 }
 void ClusterModel::markDiskDead(int b, int d) {

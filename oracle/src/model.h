@@ -311,6 +311,7 @@ class ClusterModel {
   int diskOf(int brokerIdx, const std::string& logdir) const;                  // Broker.disk(logdir), -1 = null
   void diskAddReplica(int d, int r);     // Disk.addReplica (Disk.java:113-121)
   void diskRemoveReplica(int d, int r);  // Disk.removeReplica (:139-146)
+  void markReplicaOriginalOffline(int r);
   void markDiskDead(int brokerIdx, int d);  // ClusterModel.markDiskDead -> Broker.markDiskDead (Broker.java:537-543)
   double diskUtilizationPct(int d) const {  // GoalUtils.diskUtilizationPercentage (GoalUtils.java:397-400)
     return disks[d].capacity > 0 ? disks[d].utilization / disks[d].capacity : 1.0;

@@ -280,6 +280,9 @@ int oc_optimize(void* hv, const int32_t* goals, int n, const ccmi_balancing_cons
   } catch (OptimizationFailure& e) {
     h->err = e.what();
     return CCMI_E_OPT_FAILURE;
+  } catch (UnsupportedOperation& e) {
+    h->err = e.what();
+    return CCMI_E_UNSUPPORTED;
   } catch (std::logic_error& e) {
     h->err = e.what();
     return CCMI_E_STATE;

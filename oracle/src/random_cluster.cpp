@@ -212,7 +212,22 @@ void randomCluster(ClusterModel& cm, const ClusterProperties& p) {
     }
   }
   if (p.numBrokersWithBadDisk > 0) {
-    if (!p.jbod) throw std::runtime_error("bad-disk marking without disks is not restated");
+    if (!p.jbod) {
+      // Without disk information (RandomCluster.java:409-449, no excluded topics): the first replica in
+      // Broker.replicas() (HashSet) order of each of the first alive brokers with replicas becomes original-offline,
+      // and the broker whose id is the running count is set to BAD_DISKS (the reference passes the count, not the id)
+      if (p.numDeadBrokers > 0)
+        throw std::invalid_argument("bad-disk brokers without disks next to dead brokers are outside the oracle scope");
+      int idx = 0;
+      for (int b = 0; b < (int)cm.brokers.size() && idx < p.numBrokersWithBadDisk; ++b) {
+        const Broker& br = cm.brokers[b];
+        if (br.replicas.empty() || !br.isAlive() || br.hasBadDisks()) continue;
+        cm.markReplicaOriginalOffline(br.replicaSet.order().front());
+        cm.setBrokerState(idx, BrokerState::BAD_DISKS);
+        idx++;
+      }
+      return;
+    }
     int marked = 0;  // one (the first, TreeMap order) disk of each of the first alive brokers
     for (int b = 0; b < (int)cm.brokers.size() && marked < p.numBrokersWithBadDisk; ++b) {
       if (!cm.brokers[b].isAlive()) continue;

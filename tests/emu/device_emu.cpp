@@ -32,6 +32,7 @@ struct Emu {
   std::vector<double> bUtil, bCap, bPot, rUtil, bLeadNwIn, pLeadNwOut;
   std::vector<int32_t> bNrep, bNlead, rPart, rBroker, rOrig, pOff, pBrokers, topicCount, topicNrep;
   std::vector<int32_t> bRack, pTopic, tUpper, tLower;
+  std::vector<int32_t> pIneligOff, pIneligB;  // Partition._ineligibleBrokers (empty: none)
   std::vector<uint8_t> bAlive, rFlags;
   std::vector<uint32_t> allowed;
   // chain state (device.h uploadLoads)
@@ -68,6 +69,12 @@ struct View {
     return has;
   }
   int rack(int b) const { return e.bRack[b]; }
+  bool ineligible(int p, int b) const {
+    if (e.pIneligOff.empty()) return false;
+    for (int k = e.pIneligOff[p]; k < e.pIneligOff[p + 1]; ++k)
+      if (e.pIneligB[k] == b) return true;
+    return false;
+  }
   bool otherOnRack(int p, int self, int rk) const {
     for (int i = pbegin(p); i < pend(p); ++i)
       if (pbroker(i) != self && e.bRack[pbroker(i)] == rk) return true;
@@ -112,6 +119,12 @@ Device::Device(int ordinal, int B, int R, int P, int T, int maxGoalSlots)
 }
 Device::~Device() { delete static_cast<Emu*>(st_); }
 
+void Device::uploadIneligible(const int32_t* off, const int32_t* brokers, int n) {
+  if (n <= 0) return;
+  Emu& e = E(st_);
+  e.pIneligOff.assign(off, off + P_ + 1);
+  e.pIneligB.assign(brokers, brokers + n);
+}
 void Device::uploadStatic(const double* bCapRM, const int32_t* rPart, const int32_t* rOrig, const int32_t* pOff,
                           const int32_t* topicNrep, const int32_t* bRack, const int32_t* pTopic) {
   Emu& e = E(st_);
@@ -147,11 +160,12 @@ void Device::setAllowed(int slot, const uint8_t* a) {
   auto& al = E(st_).allowed;
   for (int b = 0; b < B_; ++b) al[b] = (al[b] & ~(1u << slot)) | (a[b] ? (1u << slot) : 0u);
 }
-void Device::setExclusions(const uint8_t* lead, const uint8_t* move) {
+void Device::setExclusions(const uint8_t* lead, const uint8_t* move, const uint8_t* isNew) {
   Emu& e = E(st_);
-  const uint32_t mask = (1u << kExclLeadBit) | (1u << kExclMoveBit);
+  const uint32_t mask = (1u << kExclLeadBit) | (1u << kExclMoveBit) | (1u << kNewBit);
   for (int b = 0; b < e.B; ++b)
-    e.allowed[b] = (e.allowed[b] & ~mask) | (lead[b] ? (1u << kExclLeadBit) : 0u) | (move[b] ? (1u << kExclMoveBit) : 0u);
+    e.allowed[b] = (e.allowed[b] & ~mask) | (lead[b] ? (1u << kExclLeadBit) : 0u) |
+                   (move[b] ? (1u << kExclMoveBit) : 0u) | (isNew[b] ? (1u << kNewBit) : 0u);
 }
 void Device::setTopicLimits(const int32_t* upper, const int32_t* lower) {
   E(st_).tUpper.assign(upper, upper + T_);
@@ -195,7 +209,7 @@ int64_t Device::scanCross(const DevProgram& prog, const int32_t* reps, int K, co
   for (int k = 0; k < K; ++k)
     for (int j = c0; j < c1; ++j) {
       if (prog.filter == FILTER_RACK_AWARE && !v.rackEligible(reps[k], cands[j])) continue;
-      if (prog.exclLeadMove && (v.flags(reps[k]) & RF_LEADER) && v.allowed(kExclLeadBit, cands[j])) continue;
+      if (candidateBlocked(prog, v, reps[k], cands[j])) continue;
       if (moveCandidateAccepted(prog, v, reps[k], cands[j])) return (int64_t)k * N + j;
     }
   return -1;
@@ -207,7 +221,7 @@ int64_t Device::scanPairs(const DevProgram& prog, const int32_t* pr, const int32
   perf.scanLaunches++;
   perf.scanPairs += p1 - p0;
   for (int q = p0; q < p1; ++q) {
-    if (prog.exclLeadMove && (v.flags(pr[q]) & RF_LEADER) && v.allowed(kExclLeadBit, pb[q])) continue;
+    if (candidateBlocked(prog, v, pr[q], pb[q])) continue;
     if (moveCandidateAccepted(prog, v, pr[q], pb[q])) return q;
   }
   return -1;
@@ -375,7 +389,7 @@ Device::ChainResult Device::chainPairs(const DevProgram& prog, const int32_t* pr
   while (start < n && res.accepts < maxAccepts) {
     int best = -1;
     for (int q = start; q < n && best < 0; ++q) {
-      if (prog.exclLeadMove && (v.flags(pr[q]) & RF_LEADER) && v.allowed(kExclLeadBit, pb[q])) continue;
+      if (candidateBlocked(prog, v, pr[q], pb[q])) continue;
       if (moveCandidateAccepted(prog, v, pr[q], pb[q])) best = q;
     }
     if (best < 0) {
@@ -412,7 +426,7 @@ Device::ChainResult Device::chainRackRows(const DevProgram& prog, const int32_t*
     int best = -1;
     for (int j = 0; j < N && best < 0; ++j) {
       if (!v.rackEligible(r, cands[j])) continue;
-      if (prog.exclLeadMove && (v.flags(r) & RF_LEADER) && v.allowed(kExclLeadBit, cands[j])) continue;
+      if (candidateBlocked(prog, v, r, cands[j])) continue;
       if (moveCandidateAccepted(prog, v, r, cands[j])) best = j;
     }
     if (best < 0) {

@@ -240,3 +240,30 @@ def desc_arrays(desc: ccmi.ClusterDesc) -> dict:
                    disk_logdir=[desc.disk_logdir[d].decode() for d in range(D)],
                    disk_assign_replica=desc.disk_assign_replica[:n], disk_assign_disk=desc.disk_assign_disk[:n])
     return out
+
+
+class ArrayDesc:
+    """A ccmi_cluster_desc over python lists with the keys of OracleCluster.export (no disks): the inverse of
+    desc_arrays, for test models derived from another model's state (e.g. RandomClusterTest.testNewBrokers)."""
+
+    def __init__(self, a: dict, num_windows: int = 1):
+        B, P, R = len(a["broker_rack"]), len(a["partition_topic"]), len(a["replica_partition"])
+        T = len(a["topics"])
+        arr = lambda ct, xs: (ct * max(1, len(xs)))(*xs)  # noqa: E731
+        self.keep = dict(
+            broker_id=arr(C.c_int32, list(range(B))), broker_rack=arr(C.c_int32, a["broker_rack"]),
+            broker_state=arr(C.c_int32, a["broker_state"]), broker_capacity=arr(C.c_double, a["cap"]),
+            topic_names=arr(C.c_char_p, [t.encode() for t in a["topics"]]),
+            partition_topic=arr(C.c_int32, a["partition_topic"]), partition_number=arr(C.c_int32, a["partition_number"]),
+            partition_offset=arr(C.c_int32, a["partition_offset"]),
+            partition_replicas=arr(C.c_int32, a["partition_replicas"]),
+            replica_partition=arr(C.c_int32, a["replica_partition"]), replica_broker=arr(C.c_int32, a["replica_broker"]),
+            replica_is_leader=arr(C.c_uint8, a["is_leader"]), replica_offline=arr(C.c_uint8, a["offline"]),
+            replica_load=arr(C.c_float, a["load"]),
+            replica_load_order=arr(C.c_int32, a.get("load_order", list(range(R)))))
+        d = ccmi.ClusterDesc()
+        d.num_windows, d.num_racks, d.num_brokers = num_windows, max(a["broker_rack"]) + 1, B
+        d.num_topics, d.num_partitions, d.num_replicas = T, P, R
+        for k, v in self.keep.items():
+            setattr(d, k, C.cast(v, type(getattr(d, k))) if k != "topic_names" else v)
+        self.desc = d

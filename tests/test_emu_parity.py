@@ -108,3 +108,21 @@ EXCLUSION_CASES = [
 def test_emu_broker_exclusions_match_oracle(emu_lib, oracle_lib, props, opts, goals):
     check_product_against_oracle(emu_lib, props, goals, 1.05, max_replicas=3000,
                                  options=ccmi.OptimizationOptions(fast_mode=False, **opts))
+
+
+# Brokers with bad disks (Broker.State.BAD_DISKS) without disk information: RandomCluster marks one replica of each
+# broken broker original-offline (RandomCluster.java:409-449). Exercises Partition._ineligibleBrokers
+# (canAssignReplicaToBroker in GoalUtils.legitMove), the self-healing branches for BAD_DISKS brokers and
+# ensureReplicasMoveOffBrokersWithBadDisks.
+BAD_DISK_CASES = [
+    (dict(num_racks=5, num_brokers=20, num_replicas=6000, num_topics=300, num_brokers_with_bad_disk=3), DEFAULT_GOALS),
+    (dict(num_brokers_with_bad_disk=1), DEFAULT_GOALS),
+    (dict(num_racks=5, num_brokers=20, num_replicas=6000, num_topics=300, num_brokers_with_bad_disk=5), C1_GOALS),
+    (dict(num_racks=5, num_brokers=20, num_replicas=6000, num_topics=300, num_brokers_with_bad_disk=2),
+     DEFAULT_GOALS[::-1]),
+]
+
+
+@pytest.mark.parametrize("props,goals", BAD_DISK_CASES)
+def test_emu_bad_disk_brokers_match_oracle(emu_lib, oracle_lib, props, goals):
+    check_product_against_oracle(emu_lib, props, goals, 1.05, max_replicas=3000)

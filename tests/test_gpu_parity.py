@@ -196,3 +196,14 @@ def test_gpu_xcd_sliced_scans_match_oracle(gpu_lib, oracle_lib, tmp_path, monkey
         assert o["error"] is None
         assert [tuple(a) for a in o["actions"]] == oc.actions()
         assert [tuple(g) for g in o["goals"]] == [(x.name, x.succeeded, x.candidates, x.actions) for x in ores]
+
+
+@pytest.mark.parametrize("props,goals", [
+    (dict(num_racks=5, num_brokers=20, num_replicas=6000, num_topics=300, num_brokers_with_bad_disk=3), DEFAULT_GOALS),
+    (dict(num_brokers_with_bad_disk=1), DEFAULT_GOALS),
+    (dict(num_racks=5, num_brokers=20, num_replicas=6000, num_topics=300, num_brokers_with_bad_disk=5),
+     list(ccmi.C1_GOALS)),
+])
+def test_gpu_bad_disk_brokers_match_oracle(gpu_lib, oracle_lib, props, goals):
+    """Partition._ineligibleBrokers on the device (DevTables.pIneligOff/pIneligB in legitMove)."""
+    check_product_against_oracle(gpu_lib, props, goals, 1.05, max_replicas=3000)
