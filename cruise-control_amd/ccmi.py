@@ -182,6 +182,7 @@ EXPORTED_SYMBOLS = (
     "ccmi_last_error", "ccmi_abi_version", "ccmi_default_constraint", "ccmi_default_random_cluster_props",
     "ccmi_random_cluster", "ccmi_cluster_buffers_desc", "ccmi_cluster_buffers_free", "ccmi_session_create",
     "ccmi_session_destroy", "ccmi_optimizations", "ccmi_goal_optimize", "ccmi_action_acceptance",
+    "ccmi_action_acceptance_by_kind", "ccmi_session_apply",
     "ccmi_compute_cluster_stats", "ccmi_action_log_count", "ccmi_action_log_copy", "ccmi_replica_distribution",
     "ccmi_leader_distribution", "ccmi_replica_disks", "ccmi_proposal_count", "ccmi_proposals",
     "ccmi_proposal_disks", "ccmi_perf", "ccmi_perf_reset",
@@ -214,6 +215,9 @@ class Library:
         L.ccmi_goal_optimize.argtypes = [C.c_void_p, C.c_int32, C.POINTER(ConstraintStruct), C.POINTER(OptionsStruct),
                                          C.POINTER(GoalResultStruct)]
         L.ccmi_action_acceptance.argtypes = [C.c_void_p, C.c_int32, C.POINTER(ActionStruct), C.POINTER(C.c_int32)]
+        L.ccmi_action_acceptance_by_kind.argtypes = [C.c_void_p, C.c_int32, C.POINTER(ActionStruct),
+                                                     C.POINTER(C.c_int32)]
+        L.ccmi_session_apply.argtypes = [C.c_void_p, C.POINTER(ActionStruct), C.c_int64, C.POINTER(C.c_int64)]
         L.ccmi_compute_cluster_stats.argtypes = [C.c_void_p, C.POINTER(ConstraintStruct), C.POINTER(OptionsStruct),
                                                  C.POINTER(StatsStruct)]
         L.ccmi_action_log_count.restype = C.c_int64
@@ -649,6 +653,27 @@ class ClusterModel:
         self.lib.check(self.lib.lib.ccmi_action_acceptance(self.handle, optimized_goal_index, C.byref(a),
                                                            C.byref(out)))
         return ACCEPTANCE[out.value]
+
+    def action_acceptance_by_goal(self, goal_name: str, action_type: int, partition: int, source: int,
+                                  destination: int, destination_partition: int = -1, source_disk: int = -1,
+                                  destination_disk: int = -1) -> str:
+        """Goal.actionAcceptance of the optimized goal with this name (ccmi_action_acceptance_by_kind)."""
+        a = ActionStruct(action_type, partition, source, destination, destination_partition, source_disk,
+                         destination_disk)
+        out = C.c_int32()
+        self.lib.check(self.lib.lib.ccmi_action_acceptance_by_kind(self.handle, GOAL_KINDS[goal_name], C.byref(a),
+                                                                   C.byref(out)))
+        return ACCEPTANCE[out.value]
+
+    def apply(self, actions) -> int:
+        """Apply actions decided elsewhere (tuples in the action-log layout: type, partition, source,
+        destination, destination partition, source disk, destination disk) to the resident model
+        (ccmi_session_apply). Returns the number applied; raises on the first invalid one."""
+        acts = list(actions)
+        arr = (ActionStruct * max(1, len(acts)))(*[ActionStruct(*a) for a in acts])
+        done = C.c_int64()
+        self.lib.check(self.lib.lib.ccmi_session_apply(self.handle, arr, len(acts), C.byref(done)))
+        return done.value
 
     def cluster_stats(self, constraint: Optional[BalancingConstraint] = None,
                       options: Optional[OptimizationOptions] = None) -> Dict[str, object]:

@@ -381,6 +381,94 @@ ccmi_status ccmi_action_acceptance(ccmi_session* s, int32_t idx, const ccmi_acti
   });
 }
 
+ccmi_status ccmi_action_acceptance_by_kind(ccmi_session* s, int32_t kind, const ccmi_action* a, int32_t* acceptance) {
+  return guarded([&] {
+    if (!s || !a || !acceptance) throw std::invalid_argument("null argument");
+    const auto& opt = s->engine->optimized;
+    for (int i = (int)opt.size() - 1; i >= 0; --i)
+      if (opt[i]->kind == kind) {
+        *acceptance = s->engine->acceptance(i, *a);
+        return CCMI_OK;
+      }
+    throw std::invalid_argument("the session has not optimized goal kind " + std::to_string(kind));
+  });
+}
+
+ccmi_status ccmi_session_apply(ccmi_session* s, const ccmi_action* actions, int64_t n, int64_t* applied) {
+  if (applied) *applied = 0;
+  return guarded([&] {
+    if (!s || (n > 0 && !actions) || n < 0) throw std::invalid_argument("null argument");
+    ccmi::Model& m = s->model;
+    auto partition = [&](int p) {
+      if (p < 0 || p >= m.P) throw std::invalid_argument("partition out of range");
+    };
+    auto broker = [&](int b) {
+      if (b < 0 || b >= m.B) throw std::invalid_argument("broker out of range");
+    };
+    auto movable = [&](int p, int src, int dst) {  // ClusterModel.relocateReplica preconditions
+      partition(p);
+      broker(src);
+      broker(dst);
+      if (m.replicaOn(p, src) < 0) throw std::invalid_argument("source broker does not host the partition");
+      if (m.replicaOn(p, dst) >= 0) throw std::invalid_argument("destination broker already hosts the partition");
+    };
+    auto diskMove = [&](int p, int b, int sd, int dd) {
+      partition(p);
+      broker(b);
+      const int r = m.replicaOn(p, b);
+      if (r < 0) throw std::invalid_argument("broker does not host the partition");
+      if (sd < 0 || sd >= m.D || dd < 0 || dd >= m.D || m.dBroker[sd] != b || m.dBroker[dd] != b)
+        throw std::invalid_argument("disk out of range or not on the broker");
+      if (m.rDisk[r] != sd) throw std::invalid_argument("replica is not on the source disk");
+      m.relocateReplicaToDisk(p, b, dd);
+    };
+    for (int64_t i = 0; i < n; ++i) {
+      const ccmi_action& a = actions[i];
+      switch (a.type) {
+        case CCMI_INTER_BROKER_REPLICA_MOVEMENT:
+          movable(a.partition, a.source_broker, a.destination_broker);
+          m.relocateReplica(a.partition, a.source_broker, a.destination_broker);
+          break;
+        case CCMI_LEADERSHIP_MOVEMENT: {
+          partition(a.partition);
+          broker(a.source_broker);
+          broker(a.destination_broker);
+          const int sr = m.replicaOn(a.partition, a.source_broker), dr = m.replicaOn(a.partition, a.destination_broker);
+          if (sr < 0 || !m.rLeader[sr]) throw std::invalid_argument("source replica is not the leader");
+          if (dr < 0 || m.rLeader[dr]) throw std::invalid_argument("destination broker hosts no follower of the partition");
+          m.relocateLeadership(a.partition, a.source_broker, a.destination_broker);
+          break;
+        }
+        case CCMI_INTER_BROKER_REPLICA_SWAP:
+          movable(a.partition, a.source_broker, a.destination_broker);
+          partition(a.destination_partition);
+          if (m.replicaOn(a.destination_partition, a.destination_broker) < 0 ||
+              m.replicaOn(a.destination_partition, a.source_broker) >= 0)
+            throw std::invalid_argument("swap destination replica cannot move to the source broker");
+          m.relocateReplica(a.partition, a.source_broker, a.destination_broker);
+          m.relocateReplica(a.destination_partition, a.destination_broker, a.source_broker);
+          break;
+        case CCMI_INTRA_BROKER_REPLICA_MOVEMENT:
+          diskMove(a.partition, a.source_broker, a.source_disk, a.destination_disk);
+          break;
+        case CCMI_INTRA_BROKER_REPLICA_SWAP: {
+          partition(a.destination_partition);
+          const int r2 = m.replicaOn(a.destination_partition, a.source_broker);
+          if (r2 < 0 || m.rDisk[r2] != a.destination_disk)
+            throw std::invalid_argument("swap destination replica is not on the destination disk");
+          diskMove(a.partition, a.source_broker, a.source_disk, a.destination_disk);
+          diskMove(a.destination_partition, a.source_broker, a.destination_disk, a.source_disk);
+          break;
+        }
+        default:
+          throw std::invalid_argument("unknown action type");
+      }
+      if (applied) *applied = i + 1;
+    }
+    return CCMI_OK;
+  });
+}
+
 ccmi_status ccmi_compute_cluster_stats(ccmi_session* s, const ccmi_balancing_constraint* c, const ccmi_opt_options* o,
                                        ccmi_cluster_stats* out) {
   return guarded([&] {

@@ -278,6 +278,20 @@ ccmi_status ccmi_goal_optimize(ccmi_session* s, int32_t goal_kind, const ccmi_ba
 /* Acceptance of an action by the i-th goal this session has optimized. */
 ccmi_status ccmi_action_acceptance(ccmi_session* s, int32_t optimized_goal_index, const ccmi_action* action,
                                    int32_t* acceptance);
+/* Goal.actionAcceptance keyed by the goal plugin (ccmi_goal_kind) instead of the chain position: the most recently
+ * optimized goal of that kind (GoalOptimizer holds one instance per goal class). CCMI_E_INVALID when the session
+ * has not optimized that kind. */
+ccmi_status ccmi_action_acceptance_by_kind(ccmi_session* s, int32_t goal_kind, const ccmi_action* action,
+                                           int32_t* acceptance);
+/* Session update by deltas: apply actions decided outside this session (a JVM goal earlier in a mixed chain, an
+ * executed proposal batch) to the resident model, in order, as ClusterModel.relocateReplica /
+ * relocateLeadership / relocateReplica(tp, broker, logdir) do (a swap is its two relocateReplica calls,
+ * AbstractGoal.maybeApplySwapAction :316-317). Only the touched rows are re-sent to the device, so a mixed-chain hop
+ * costs O(actions), not an O(R) re-flatten. Actions are validated first (the replica exists on the source, the
+ * destination does not host the partition / hosts a follower, disks belong to the broker); the first invalid one
+ * fails the call with CCMI_E_INVALID and `*applied` (optional) = actions applied before it. Applied actions join
+ * the action log and the proposals (the diff against the session's initial placement). */
+ccmi_status ccmi_session_apply(ccmi_session* s, const ccmi_action* actions, int64_t n, int64_t* applied);
 ccmi_status ccmi_compute_cluster_stats(ccmi_session* s, const ccmi_balancing_constraint* constraint,
                                const ccmi_opt_options* options, ccmi_cluster_stats* out);
 

@@ -302,6 +302,44 @@ double oc_stats_seconds(void* hv) { return ((Handle*)hv)->cm.statsSeconds; }
 double oc_last_seconds(void* hv) { return ((Handle*)hv)->last.seconds; }
 int64_t oc_candidates(void* hv) { return ((Handle*)hv)->cm.candidatesEvaluated; }
 
+// Apply externally decided actions (ClusterModel.relocateReplica / relocateLeadership / relocateReplica to a logdir)
+// in order; returns 0 or CCMI_E_INVALID (message in oc_error).
+int32_t oc_apply(void* hv, const ccmi_action* a, int64_t n) {
+  auto* h = (Handle*)hv;
+  ClusterModel& cm = h->cm;
+  try {
+    for (int64_t i = 0; i < n; ++i) {
+      const ccmi_action& x = a[i];
+      switch (x.type) {
+        case CCMI_INTER_BROKER_REPLICA_MOVEMENT:
+          cm.relocateReplica(x.partition, x.source_broker, x.destination_broker);
+          break;
+        case CCMI_LEADERSHIP_MOVEMENT:
+          if (!cm.relocateLeadership(x.partition, x.source_broker, x.destination_broker))
+            throw std::invalid_argument("source replica is not the leader");
+          break;
+        case CCMI_INTER_BROKER_REPLICA_SWAP:
+          cm.relocateReplica(x.partition, x.source_broker, x.destination_broker);
+          cm.relocateReplica(x.destination_partition, x.destination_broker, x.source_broker);
+          break;
+        case CCMI_INTRA_BROKER_REPLICA_MOVEMENT:
+          cm.relocateReplicaToDisk(x.partition, x.source_broker, x.destination_disk);
+          break;
+        case CCMI_INTRA_BROKER_REPLICA_SWAP:
+          cm.relocateReplicaToDisk(x.partition, x.source_broker, x.destination_disk);
+          cm.relocateReplicaToDisk(x.destination_partition, x.source_broker, x.source_disk);
+          break;
+        default:
+          throw std::invalid_argument("unknown action type");
+      }
+    }
+    return 0;
+  } catch (std::exception& e) {
+    h->err = e.what();
+    return CCMI_E_INVALID;
+  }
+}
+
 int64_t oc_action_count(void* hv) { return (int64_t)((Handle*)hv)->cm.actionLog.size(); }
 void oc_actions(void* hv, ccmi_action* out) {
   auto* h = (Handle*)hv;

@@ -56,6 +56,8 @@ class Oracle:
             L.oc_action_count.restype = C.c_int64
             L.oc_action_count.argtypes = [C.c_void_p]
             L.oc_actions.argtypes = [C.c_void_p, C.POINTER(ccmi.ActionStruct)]
+            L.oc_apply.restype = C.c_int32
+            L.oc_apply.argtypes = [C.c_void_p, C.POINTER(ccmi.ActionStruct), C.c_int64]
             L.oc_replica_distribution.argtypes = [C.c_void_p, C.POINTER(C.c_int32)]
             L.oc_leader_distribution.argtypes = [C.c_void_p, C.POINTER(C.c_int32)]
             L.oc_stats.argtypes = [C.c_void_p, C.POINTER(ccmi.ConstraintStruct), C.POINTER(ccmi.OptionsStruct),
@@ -171,6 +173,13 @@ class OracleCluster:
         if st not in (0, 99):
             raise ccmi._STATUS.get(st, RuntimeError)(self.L.oc_error(self.h).decode())
         return st == 0, self.L.oc_candidates(self.h), self.L.oc_stats_seconds(self.h)
+
+    def apply(self, actions) -> None:
+        acts = list(actions)
+        arr = (ccmi.ActionStruct * max(1, len(acts)))(*[ccmi.ActionStruct(*a) for a in acts])
+        st = self.L.oc_apply(self.h, arr, len(acts))
+        if st != 0:
+            raise ccmi._STATUS.get(st, RuntimeError)(self.L.oc_error(self.h).decode())
 
     def actions(self) -> List[tuple]:
         n = self.L.oc_action_count(self.h)
