@@ -93,7 +93,7 @@ class ConstraintStruct(C.Structure):
                 ("topic_replica_balance_min_gap", C.c_int32), ("topic_replica_balance_max_gap", C.c_int32),
                 ("goal_violation_distribution_threshold_multiplier", C.c_double),
                 ("max_replicas_per_broker", C.c_int64), ("overprovisioned_max_replicas_per_broker", C.c_int64),
-                ("overprovisioned_min_brokers", C.c_int32)]
+                ("overprovisioned_min_brokers", C.c_int32), ("overprovisioned_min_extra_racks", C.c_int32)]
 
 
 class OptionsStruct(C.Structure):
@@ -128,10 +128,20 @@ class StatsStruct(C.Structure):
                 ("num_unbalanced_disks", C.c_int32), ("disk_utilization_std", C.c_double)]
 
 
+class ProvisionRecStruct(C.Structure):
+    _fields_ = [("status", C.c_int32), ("num_brokers", C.c_int32), ("num_racks", C.c_int32), ("num_disks", C.c_int32),
+                ("num_partitions", C.c_int32), ("typical_broker_id", C.c_int32), ("resource", C.c_int32),
+                ("pad", C.c_int32), ("typical_broker_capacity", C.c_double), ("total_capacity", C.c_double)]
+
+
+class ProvisionRespStruct(C.Structure):
+    _fields_ = [("status", C.c_int32), ("has_recommendation", C.c_int32), ("recommendation", ProvisionRecStruct)]
+
+
 class GoalResultStruct(C.Structure):
     _fields_ = [("goal_kind", C.c_int32), ("succeeded", C.c_int32), ("has_diff", C.c_int32), ("seconds", C.c_double),
                 ("candidates", C.c_int64), ("device_candidates", C.c_int64), ("device_launches", C.c_int64),
-                ("actions", C.c_int64), ("stats", StatsStruct)]
+                ("actions", C.c_int64), ("stats", StatsStruct), ("provision", ProvisionRespStruct)]
 
 
 class RandomClusterProps(C.Structure):
@@ -182,7 +192,7 @@ EXPORTED_SYMBOLS = (
     "ccmi_last_error", "ccmi_abi_version", "ccmi_default_constraint", "ccmi_default_random_cluster_props",
     "ccmi_random_cluster", "ccmi_cluster_buffers_desc", "ccmi_cluster_buffers_free", "ccmi_session_create",
     "ccmi_session_destroy", "ccmi_optimizations", "ccmi_goal_optimize", "ccmi_action_acceptance",
-    "ccmi_action_acceptance_by_kind", "ccmi_session_apply",
+    "ccmi_action_acceptance_by_kind", "ccmi_session_apply", "ccmi_last_failure_provision",
     "ccmi_compute_cluster_stats", "ccmi_action_log_count", "ccmi_action_log_copy", "ccmi_replica_distribution",
     "ccmi_leader_distribution", "ccmi_replica_disks", "ccmi_proposal_count", "ccmi_proposals",
     "ccmi_proposal_disks", "ccmi_perf", "ccmi_perf_reset",
@@ -218,6 +228,7 @@ class Library:
         L.ccmi_action_acceptance_by_kind.argtypes = [C.c_void_p, C.c_int32, C.POINTER(ActionStruct),
                                                      C.POINTER(C.c_int32)]
         L.ccmi_session_apply.argtypes = [C.c_void_p, C.POINTER(ActionStruct), C.c_int64, C.POINTER(C.c_int64)]
+        L.ccmi_last_failure_provision.argtypes = [C.c_void_p, C.POINTER(ProvisionRespStruct)]
         L.ccmi_compute_cluster_stats.argtypes = [C.c_void_p, C.POINTER(ConstraintStruct), C.POINTER(OptionsStruct),
                                                  C.POINTER(StatsStruct)]
         L.ccmi_action_log_count.restype = C.c_int64
@@ -264,6 +275,7 @@ class BalancingConstraint:
     topic_replica_balance_percentage: float = 3.00
     topic_replica_balance_min_gap: int = 2
     topic_replica_balance_max_gap: int = 40
+    overprovisioned_min_extra_racks: int = 2  # AnalyzerConfig.DEFAULT_OVERPROVISIONED_MIN_EXTRA_RACKS
 
     def set_resource_balance_percentage(self, p: float) -> None:  # BalancingConstraint.setResourceBalancePercentage
         self.resource_balance_percentage = (p, p, p, p)
@@ -285,6 +297,7 @@ class BalancingConstraint:
         s.max_replicas_per_broker = self.max_replicas_per_broker
         s.overprovisioned_max_replicas_per_broker = 1500
         s.overprovisioned_min_brokers = 3
+        s.overprovisioned_min_extra_racks = self.overprovisioned_min_extra_racks
         return s
 
 
@@ -359,6 +372,79 @@ for _n in GOAL_KINDS:
 
 
 # ----------------------------------------------------------------------------------------------- results
+PROVISION_STATUSES = ("UNDECIDED", "RIGHT_SIZED", "UNDER_PROVISIONED", "OVER_PROVISIONED")  # ProvisionStatus.java
+
+
+@dataclass
+class ProvisionRecommendation:
+    """analyzer/ProvisionRecommendation.java (-1 = unset; topic pattern and excluded rack ids not carried)."""
+    status: str
+    num_brokers: int = -1
+    num_racks: int = -1
+    num_disks: int = -1
+    num_partitions: int = -1
+    typical_broker_id: int = -1
+    resource: Optional[str] = None
+    typical_broker_capacity: float = -1.0
+    total_capacity: float = -1.0
+
+
+def _goal_of_message(msg: str) -> str:
+    """The goal name an OptimizationFailureException message starts with ("[GoalName] ...")."""
+    return msg[1:msg.index("]")] if msg.startswith("[") and "]" in msg else ""
+
+
+class ProvisionResponse:
+    """analyzer/ProvisionResponse.java: a status and the recommendations by recommender (goal name);
+    aggregate() follows ProvisionResponse.aggregate (:97-129)."""
+
+    def __init__(self, status: str = "UNDECIDED", recommendation: Optional[ProvisionRecommendation] = None,
+                 recommender: Optional[str] = None):
+        if recommendation is not None and status not in ("UNDER_PROVISIONED", "OVER_PROVISIONED"):
+            raise IllegalArgumentException(f"Recommendation is irrelevant for provision status {status}.")
+        self.status = status
+        self.recommendation_by_recommender: Dict[str, ProvisionRecommendation] = {}
+        if recommendation is not None:
+            if recommender is None:
+                raise IllegalArgumentException("The recommender cannot be null.")
+            self.recommendation_by_recommender[recommender] = recommendation
+
+    @staticmethod
+    def from_struct(p: "ProvisionRespStruct", recommender: str) -> "ProvisionResponse":
+        status = PROVISION_STATUSES[p.status]
+        if not p.has_recommendation:
+            return ProvisionResponse(status)
+        r = p.recommendation
+        rec = ProvisionRecommendation(PROVISION_STATUSES[r.status], r.num_brokers, r.num_racks, r.num_disks,
+                                      r.num_partitions, r.typical_broker_id,
+                                      RESOURCES[r.resource] if r.resource >= 0 else None, r.typical_broker_capacity,
+                                      r.total_capacity)
+        return ProvisionResponse(status, rec, recommender)
+
+    def aggregate(self, other: "ProvisionResponse") -> "ProvisionResponse":
+        if self.status == "UNDER_PROVISIONED":
+            if other.status == "UNDER_PROVISIONED":
+                self.recommendation_by_recommender.update(other.recommendation_by_recommender)
+        elif other.status == "UNDER_PROVISIONED":
+            self.status = "UNDER_PROVISIONED"
+            self.recommendation_by_recommender = dict(other.recommendation_by_recommender)
+        elif other.status == "RIGHT_SIZED":
+            self.status = "RIGHT_SIZED"
+            self.recommendation_by_recommender = {}
+        elif other.status == "OVER_PROVISIONED":
+            if self.status in ("OVER_PROVISIONED", "UNDECIDED"):
+                self.status = "OVER_PROVISIONED"
+                self.recommendation_by_recommender.update(other.recommendation_by_recommender)
+        return self
+
+    def __eq__(self, other) -> bool:
+        return isinstance(other, ProvisionResponse) and (self.status, self.recommendation_by_recommender) == \
+            (other.status, other.recommendation_by_recommender)
+
+    def __repr__(self) -> str:
+        return f"ProvisionResponse({self.status}, {self.recommendation_by_recommender})"
+
+
 @dataclass
 class ExecutionProposal:
     partition: int
@@ -381,6 +467,7 @@ class GoalResult:
     device_launches: int
     actions: int
     stats: Dict[str, object]
+    provision: Optional[ProvisionResponse] = None  # Goal.provisionResponse after the goal
 
 
 class OptimizerResult:
@@ -413,6 +500,15 @@ class OptimizerResult:
     @property
     def candidates(self) -> int:
         return sum(g.candidates for g in self.goal_results)
+
+    @property
+    def provision_response(self) -> ProvisionResponse:
+        """The aggregated provision response GoalOptimizer.optimizations reports (GoalOptimizer.java:456-496)."""
+        agg = ProvisionResponse("UNDECIDED")
+        for g in self.goal_results:
+            if g.provision is not None:
+                agg.aggregate(g.provision)
+        return agg
 
 
 def stats_to_dict(s: StatsStruct) -> Dict[str, object]:
@@ -641,8 +737,22 @@ class ClusterModel:
         res = GoalResultStruct()
         o, keep = (options or OptimizationOptions()).to_struct()
         c = (goal.constraint or BalancingConstraint()).to_struct()
-        self.lib.check(self.lib.lib.ccmi_goal_optimize(self.handle, goal.kind, C.byref(c), C.byref(o), C.byref(res)))
+        self._checked(self.lib.lib.ccmi_goal_optimize(self.handle, goal.kind, C.byref(c), C.byref(o), C.byref(res)))
+        goal.provision = ProvisionResponse.from_struct(res.provision, goal.name())
         return res
+
+    def _checked(self, status: int) -> None:
+        """lib.check, attaching the failed goal's provision response to an OptimizationFailureException."""
+        try:
+            self.lib.check(status)
+        except OptimizationFailureException as e:
+            e.provision = self.last_failure_provision(_goal_of_message(str(e)))
+            raise
+
+    def last_failure_provision(self, recommender: str = "") -> ProvisionResponse:
+        out = ProvisionRespStruct()
+        self.lib.check(self.lib.lib.ccmi_last_failure_provision(self.handle, C.byref(out)))
+        return ProvisionResponse.from_struct(out, recommender)
 
     def action_acceptance(self, optimized_goal_index: int, action_type: int, partition: int, source: int,
                           destination: int, destination_partition: int = -1, source_disk: int = -1,
@@ -785,11 +895,12 @@ class GoalOptimizer:
         c = self.constraint.to_struct()
         import time
         t0 = time.perf_counter()
-        cluster.lib.check(cluster.lib.lib.ccmi_optimizations(cluster.handle, kinds, len(goals_by_priority),
-                                                             C.byref(c), C.byref(o), results))
+        cluster._checked(cluster.lib.lib.ccmi_optimizations(cluster.handle, kinds, len(goals_by_priority),
+                                                            C.byref(c), C.byref(o), results))
         dt = time.perf_counter() - t0
         grs = [GoalResult(GOAL_NAMES[r.goal_kind], bool(r.succeeded), bool(r.has_diff), r.seconds, r.candidates,
-                          r.device_candidates, r.device_launches, r.actions, stats_to_dict(r.stats)) for r in results]
+                          r.device_candidates, r.device_launches, r.actions, stats_to_dict(r.stats),
+                          ProvisionResponse.from_struct(r.provision, GOAL_NAMES[r.goal_kind])) for r in results]
         return OptimizerResult(grs, cluster, dt, [g.name for g in grs if not g.succeeded])
 
 

@@ -79,6 +79,9 @@ void setOptions(ccmi_session* s, const ccmi_balancing_constraint* c, const ccmi_
   e.bc.topicMinGap = c->topic_replica_balance_min_gap;
   e.bc.topicMaxGap = c->topic_replica_balance_max_gap;
   e.bc.maxReplicasPerBroker = c->max_replicas_per_broker;
+  e.bc.overMaxReplicasPerBroker = c->overprovisioned_max_replicas_per_broker;
+  e.bc.overMinBrokers = c->overprovisioned_min_brokers;
+  e.bc.overprovisionedMinExtraRacks = c->overprovisioned_min_extra_racks;
   const int B = s->model.B;
   ccmi::Options opt;
   opt.exclMove.assign(B, 0);
@@ -203,6 +206,7 @@ void ccmi_default_constraint(ccmi_balancing_constraint* c) {
   c->max_replicas_per_broker = 10000;
   c->overprovisioned_max_replicas_per_broker = 1500;
   c->overprovisioned_min_brokers = 3;
+  c->overprovisioned_min_extra_racks = 2;
 }
 
 void ccmi_default_random_cluster_props(ccmi_random_cluster_props* p) {
@@ -377,6 +381,14 @@ ccmi_status ccmi_action_acceptance(ccmi_session* s, int32_t idx, const ccmi_acti
     if (!s || !a || !acceptance) throw std::invalid_argument("null argument");
     if (idx < 0 || idx >= (int)s->engine->optimized.size()) throw std::invalid_argument("optimized goal index out of range");
     *acceptance = s->engine->acceptance(idx, *a);
+    return CCMI_OK;
+  });
+}
+
+ccmi_status ccmi_last_failure_provision(const ccmi_session* s, ccmi_provision_response* out) {
+  return guarded([&] {
+    if (!s || !out) throw std::invalid_argument("null argument");
+    *out = s->engine->lastFailure;
     return CCMI_OK;
   });
 }

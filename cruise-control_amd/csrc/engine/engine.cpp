@@ -419,6 +419,36 @@ bool Engine::optimizeGoal(std::unique_ptr<GoalImpl> g, ccmi_goal_result* res) {
   } guard{m};
   prof().candCounter = &candidates;
   g->succeeded = true;
+  g->prov = provisionResponse(CCMI_PROVISION_UNDECIDED);  // AbstractGoal.java:87
+  try {
+    return optimizeGoalImpl(g, res, t0, c0, a0, l0, p0);
+  } catch (OptimizationFailure& f) {  // AbstractGoal.java:125-126
+    lastFailure = f.hasRec ? provisionResponse(CCMI_PROVISION_UNDER_PROVISIONED, f.rec)
+                           : provisionResponse(CCMI_PROVISION_UNDER_PROVISIONED);
+    throw;
+  }
+}
+
+// GoalUtils.validateProvisionResponse (GoalUtils.java:619-650)
+ccmi_provision_response validateProvision(const ccmi_provision_response& p, const Model& m, int minBrokers) {
+  if (p.status != CCMI_PROVISION_OVER_PROVISIONED) return p;
+  int alive = 0;
+  for (int b = 0; b < m.B; ++b) alive += m.alive(b) ? 1 : 0;
+  if (alive < minBrokers) return provisionResponse(CCMI_PROVISION_RIGHT_SIZED);
+  if (!p.has_recommendation) throw std::invalid_argument("Expected to have exactly 1 provision recommendation, but got: 0");
+  const int maxAllowedToDrop = alive - m.maxRf;
+  if (p.recommendation.num_brokers <= maxAllowedToDrop) return p;
+  if (maxAllowedToDrop > 0) {
+    ccmi_provision_recommendation r = provisionRec(CCMI_PROVISION_OVER_PROVISIONED);
+    r.num_brokers = maxAllowedToDrop;
+    return provisionResponse(CCMI_PROVISION_OVER_PROVISIONED, r);
+  }
+  return provisionResponse(CCMI_PROVISION_RIGHT_SIZED);
+}
+
+bool Engine::optimizeGoalImpl(std::unique_ptr<GoalImpl>& g, ccmi_goal_result* res, std::chrono::steady_clock::time_point t0,
+                              int64_t c0, size_t a0, int64_t l0, int64_t p0) {
+  using clk = std::chrono::steady_clock;
   const ccmi_cluster_stats before = stats();
   g->finished = false;
   g->dg.allowedSlot = (int)optimized.size();
@@ -446,7 +476,9 @@ bool Engine::optimizeGoal(std::unique_ptr<GoalImpl> g, ccmi_goal_result* res) {
   if (brokenEmpty && !exclWithReplicas && g->compareStats(after, before) < 0)
     throw StateError("Optimization for goal " + g->name + " failed because the optimized result is worse than before.");
   const bool ok = g->succeeded;
+  g->prov = validateProvision(g->prov, m, bc.overMinBrokers);
   if (res) {
+    res->provision = g->prov;
     res->goal_kind = g->kind;
     res->succeeded = ok ? 1 : 0;
     res->candidates = candidates - c0;
@@ -516,7 +548,8 @@ class ReplicaDistribution : public GoalImpl {
         allowed[b] = 1;
         n++;
       }
-    if (n == 0) throw OptimizationFailure("[" + name + "] All alive brokers are excluded from replica moves.");
+    if (n == 0)
+      throw OptimizationFailure("[" + name + "] All alive brokers are excluded from replica moves.", underBrokers(m.maxRf));
     const double avg = m.R / (double)n;
     const double adj = (e.bc.replicaBalance - 1) * kBalanceMargin;
     upper = (int)std::ceil(avg * (1 + adj));
@@ -541,18 +574,39 @@ class ReplicaDistribution : public GoalImpl {
     }
   }
 
+  // ReplicaDistributionAbstractGoal.updateGoalState (:187-229), then ReplicaDistributionGoal's provisioning
+  // (ReplicaDistributionGoal.java:85-107), every round
   void update(Engine& e) override {
     if (anyAbove) succeeded = false;
     if (anyUnder) succeeded = false;
     anyAbove = anyUnder = false;
     Model& m = e.m;
-    for (int r = 0; r < m.R; ++r)
-      if (m.selfHealing[r] && m.curOffline(r)) {
-        if (dg.fixOffline) throw OptimizationFailure("[" + name + "] Cannot remove offline replicas.");
-        dg.fixOffline = 1;
-        return;
-      }
-    finished = true;
+    [&] {
+      for (int r = 0; r < m.R; ++r)
+        if (m.selfHealing[r] && m.curOffline(r)) {
+          if (dg.fixOffline)  // GoalUtils.ensureNoOfflineReplicas rethrown
+            throw OptimizationFailure("[" + name + "] Cannot remove replica from broker " +
+                                          std::to_string(m.bId[m.rBroker[r]]),
+                                      underBrokers(1));
+          dg.fixOffline = 1;
+          return;
+        }
+      finished = true;
+    }();
+    int numAllowed = 0;
+    bool anyAboveMax = false;
+    for (int b = 0; b < m.B; ++b) {
+      numAllowed += allowed[b] ? 1 : 0;
+      if (m.alive(b) && (int64_t)m.nrep(b) > e.bc.overMaxReplicasPerBroker) anyAboveMax = true;
+    }
+    const int numBrokersToDrop = numAllowed - (int)(m.R / e.bc.overMaxReplicasPerBroker);
+    if (numBrokersToDrop > 0 && !anyAboveMax) {
+      ccmi_provision_recommendation rec = provisionRec(CCMI_PROVISION_OVER_PROVISIONED);
+      rec.num_brokers = numBrokersToDrop;
+      prov = provisionResponse(CCMI_PROVISION_OVER_PROVISIONED, rec);
+    } else {
+      prov = provisionResponse(CCMI_PROVISION_RIGHT_SIZED);
+    }
   }
 
   int compareStats(const ccmi_cluster_stats& after, const ccmi_cluster_stats& before) const override {
@@ -724,6 +778,8 @@ class ResourceDistribution : public GoalImpl {
   int res = 0;
   double upperThr = 0, lowerThr = 0;
   bool fix = false;
+  bool lowUtil = false;                   // _isLowUtilization
+  ccmi_provision_recommendation overRec{};  // _overProvisionedRecommendation
   Model::SnapTable snapTab;  // moveIn's candidate-broker snapshots (one Spec per phase)
   std::vector<uint8_t> queued;  // moveIn: broker is in the candidate queue
   int nameBase() const { return 4 * kind; }
@@ -756,13 +812,37 @@ class ResourceDistribution : public GoalImpl {
         allowed[b] = 1;
         n++;
       }
-    if (n == 0) throw OptimizationFailure("[" + name + "] All alive brokers are excluded from replica moves.");
+    if (n == 0)
+      throw OptimizationFailure("[" + name + "] All alive brokers are excluded from replica moves.", underBrokers(m.maxRf));
     fix = false;
     const double util = m.clusterUtil(res);
     const double capacity = m.capacityWithAllowedReplicaMoves(res, e.opt.exclMove);
     const double avgPct = util / capacity;
     upperThr = e.threshold(avgPct, res, false);
     lowerThr = e.threshold(avgPct, res, true);
+    lowUtil = avgPct <= e.bc.lowUtil[res];
+    if (lowUtil) {
+      // the over-provisioned recommendation with a typical broker of maximal capacity, first in the
+      // _brokersAllowedReplicaMove HashSet<Integer> order (ResourceDistributionGoal.java:262-296)
+      std::vector<int> ids, ord;
+      for (int b = 0; b < m.B; ++b)
+        if (allowed[b]) ids.push_back(b);
+      javaHashSetOrder(ids, ord);
+      int typical = -1;
+      double maxCapacity = 0.0;
+      for (int b : ord)
+        if (m.cap(b, res) > maxCapacity) {
+          typical = b;
+          maxCapacity = m.cap(b, res);
+        }
+      const double typicalCapacity = m.cap(typical, res);
+      const int allowedNumBrokers = (int)(util / e.bc.lowUtil[res] / typicalCapacity);
+      overRec = provisionRec(CCMI_PROVISION_OVER_PROVISIONED);
+      overRec.num_brokers = std::max(n - allowedNumBrokers, 1);
+      overRec.typical_broker_capacity = typicalCapacity;
+      overRec.typical_broker_id = m.bId[typical];
+      overRec.resource = res;
+    }
     dg = DevGoal{};
     dg.kind = DG_RESOURCE_DISTRIBUTION;
     dg.resource = res;
@@ -775,14 +855,21 @@ class ResourceDistribution : public GoalImpl {
   // updateGoalState (:301-349)
   void update(Engine& e) override {
     Model& m = e.m;
+    bool anyAboveUpper = false, anyUnderLower = false;
     for (int b = 0; b < m.B; ++b) {
       if (!m.alive(b)) continue;
-      if (!underUpper(m, b, upperThr)) succeeded = false;
-      if (!excluded(b) && !aboveLower(m, b)) succeeded = false;
+      if (!underUpper(m, b, upperThr)) anyAboveUpper = true;
+      if (!excluded(b) && !aboveLower(m, b)) anyUnderLower = true;
     }
+    if (anyAboveUpper) succeeded = false;
+    else if (lowUtil) prov = provisionResponse(CCMI_PROVISION_OVER_PROVISIONED, overRec);
+    if (anyUnderLower) succeeded = false;
+    else if (!anyAboveUpper && !lowUtil) prov = provisionResponse(CCMI_PROVISION_RIGHT_SIZED);
     for (int r = 0; r < m.R; ++r)
       if (m.selfHealing[r] && m.curOffline(r)) {
-        if (fix) throw OptimizationFailure("[" + name + "] Cannot remove offline replicas.");
+        if (fix)  // GoalUtils.ensureNoOfflineReplicas rethrown
+          throw OptimizationFailure("[" + name + "] Cannot remove replica from broker " + std::to_string(m.bId[m.rBroker[r]]),
+                                    underBrokers(1));
         fix = true;
         dg.fixOffline = 1;
         return;

@@ -12,6 +12,7 @@
 //   ReplicaDistributionAbstractGoal           analyzer/goals/ReplicaDistributionAbstractGoal.java:79-229
 //   ResourceDistributionGoal                  analyzer/goals/ResourceDistributionGoal.java:234-863
 #pragma once
+#include <chrono>
 #include <memory>
 #include <string>
 #include <vector>
@@ -38,6 +39,9 @@ struct Constraint {  // BalancingConstraint
   double leaderReplicaBalance, topicReplicaBalance;
   int32_t topicMinGap, topicMaxGap;
   int64_t maxReplicasPerBroker;
+  int64_t overMaxReplicasPerBroker;   // overprovisioned.max.replicas.per.broker
+  int32_t overMinBrokers;             // overprovisioned.min.brokers
+  int32_t overprovisionedMinExtraRacks;
 };
 
 class Engine;
@@ -60,6 +64,7 @@ class GoalImpl {
   std::vector<uint8_t> allowed;
   bool succeeded = true;
   bool finished = false;
+  ccmi_provision_response prov{};  // Goal.provisionResponse
   virtual void init(Engine& e) = 0;
   virtual void rebalance(Engine& e, int b) = 0;
   virtual void update(Engine& e) = 0;
@@ -79,11 +84,14 @@ class Engine {
   Shard shard;
   std::vector<std::unique_ptr<GoalImpl>> optimized;  // optimized goals, priority order
   int64_t candidates = 0;
+  ccmi_provision_response lastFailure{};  // provisionResponse of the goal whose OptimizationFailure ended the last call
   std::vector<uint8_t> scratchB, scratchB2;  // per-broker scratch flags for the goal drivers
   std::vector<int32_t> topicUpper, topicLower;  // TopicReplicaDistributionGoal limits (device copy: setTopicLimits)
 
   // one Goal.optimize; throws OptimizationFailure / StateError
   bool optimizeGoal(std::unique_ptr<GoalImpl> g, ccmi_goal_result* res);
+  bool optimizeGoalImpl(std::unique_ptr<GoalImpl>& g, ccmi_goal_result* res, std::chrono::steady_clock::time_point t0,
+                        int64_t c0, size_t a0, int64_t l0, int64_t p0);
   ccmi_cluster_stats stats();
   int acceptance(int goalIndex, const ccmi_action& a);
 

@@ -48,7 +48,8 @@ bool hasOffline(const Model& m, int b) { return m.bOfflineSet[b].size() > 0; }  
 void ensureNoOfflineReplicas(const Model& m, const std::string& name) {
   for (int r = 0; r < m.R; ++r)
     if (m.selfHealing[r] && m.curOffline(r))
-      throw OptimizationFailure("[" + name + "] Cannot remove replica from broker " + std::to_string(m.bId[m.rBroker[r]]));
+      throw OptimizationFailure("[" + name + "] Cannot remove replica from broker " + std::to_string(m.bId[m.rBroker[r]]),
+                                underBrokers(1));
 }
 
 // GoalUtils.aliveBrokersNotExcludedForReplicaMove
@@ -104,13 +105,27 @@ class RackAware : public GoalImpl {
       for (int t : order) {
         if (e.opt.exclTopic[t]) continue;
         maxIncluded = std::max(maxIncluded, rf[t]);
-        if (maxIncluded > numRacks)
+        if (maxIncluded > numRacks) {
+          ccmi_provision_recommendation rec = provisionRec();
+          rec.num_racks = maxIncluded - numRacks;
           throw OptimizationFailure("[" + name + "] Insufficient number of racks to distribute included replicas (Current: " +
-                                    std::to_string(numRacks) + ", Needed: " + std::to_string(maxIncluded) + ").");
+                                        std::to_string(numRacks) + ", Needed: " + std::to_string(maxIncluded) + ").",
+                                    rec);
+        }
       }
     } else if (m.maxRf > numRacks) {
+      ccmi_provision_recommendation rec = provisionRec();
+      rec.num_racks = m.maxRf - numRacks;
       throw OptimizationFailure("[" + name + "] Insufficient number of racks to distribute each replica (Current: " +
-                                std::to_string(numRacks) + ", Needed: " + std::to_string(m.maxRf) + ").");
+                                    std::to_string(numRacks) + ", Needed: " + std::to_string(m.maxRf) + ").",
+                                rec);
+    }
+    // over-provisioned in racks (RackAwareGoal.java:103-109)
+    const int numExtraRacks = numRacks - m.maxRf;
+    if (numExtraRacks >= e.bc.overprovisionedMinExtraRacks) {
+      ccmi_provision_recommendation rec = provisionRec(CCMI_PROVISION_OVER_PROVISIONED);
+      rec.num_racks = numExtraRacks - e.bc.overprovisionedMinExtraRacks + 1;
+      prov = provisionResponse(CCMI_PROVISION_OVER_PROVISIONED, rec);
     }
     Model::Spec s;
     s.selImmigrants = e.opt.onlyImmigrants;
@@ -199,7 +214,8 @@ class RackAware : public GoalImpl {
       const int r = rows[failRow - 1];
       e.candidates += eligibleCount(e, r, cands, cands.size());
       throw OptimizationFailure("[" + name + "] Cannot move replica of partition " + std::to_string(m.rPart[r]) +
-                                " to a rack-aware broker.");
+                                    " to a rack-aware broker.",
+                                underBrokers(1));
     }
     return true;
   }
@@ -218,7 +234,8 @@ class RackAware : public GoalImpl {
       e.candidates += eligibleCount(e, r, cands, key >= 0 ? (size_t)key + 1 : cands.size());
       if (key < 0)
         throw OptimizationFailure("[" + name + "] Cannot move replica of partition " + std::to_string(m.rPart[r]) +
-                                  " to a rack-aware broker.");
+                                      " to a rack-aware broker.",
+                                  underBrokers(1));
       m.relocateReplica(m.rPart[r], b, cands[key]);
     }
   }
@@ -233,11 +250,22 @@ class RackAware : public GoalImpl {
       for (int i = 0; i < n; ++i) {
         racks[i] = m.bRack[m.rBroker[m.pSlots[m.pOff[p] + i]]];
         for (int j = 0; j < i; ++j)
-          if (racks[j] == racks[i])
-            throw OptimizationFailure("[" + name + "] Partition " + std::to_string(p) + " is not rack-aware.");
+          if (racks[j] == racks[i]) {
+            int distinct = 0;  // ProvisionRecommendation.numRacks = replicas - distinct racks (:177-180)
+            for (int a = 0; a < n; ++a) {
+              const int rk = m.bRack[m.rBroker[m.pSlots[m.pOff[p] + a]]];
+              bool seen = false;
+              for (int c = 0; c < a; ++c) seen |= m.bRack[m.rBroker[m.pSlots[m.pOff[p] + c]]] == rk;
+              distinct += seen ? 0 : 1;
+            }
+            ccmi_provision_recommendation rec = provisionRec();
+            rec.num_racks = n - distinct;
+            throw OptimizationFailure("[" + name + "] Partition " + std::to_string(p) + " is not rack-aware.", rec);
+          }
       }
     }
     ensureNoOfflineReplicas(m, name);
+    if (prov.status != CCMI_PROVISION_OVER_PROVISIONED) prov = provisionResponse(CCMI_PROVISION_RIGHT_SIZED);
     finished = true;
   }
   int compareStats(const ccmi_cluster_stats&, const ccmi_cluster_stats&) const override { return 0; }
@@ -275,7 +303,8 @@ class MinTopicLeaders : public GoalImpl {
       one[0] = r;
       const int64_t key = e.crossScan(*this, DA_MOVE, one, 0, cands);
       if (key < 0)
-        throw OptimizationFailure("[" + name + "] Cannot remove offline replica from broker " + std::to_string(m.bId[b]));
+        throw OptimizationFailure("[" + name + "] Cannot remove offline replica from broker " + std::to_string(m.bId[b]),
+                                  underBrokers(1));
       m.relocateReplica(m.rPart[r], b, cands[key]);
     }
   }
@@ -317,9 +346,12 @@ class ReplicaCapacity : public GoalImpl {
     }
     const int n = allowedForReplicaMove(e, allowed);
     const int64_t maxInCluster = maxR * n;
-    if ((int64_t)m.R > maxInCluster)
+    if ((int64_t)m.R > maxInCluster) {
+      const int minRequired = (int)std::ceil(m.R / (double)maxR);  // ReplicaCapacityGoal.java:145-148
       throw OptimizationFailure("[" + name + "] Total replicas in cluster: " + std::to_string(m.R) +
-                                " exceeds the maximum allowed replicas in cluster: " + std::to_string(maxInCluster));
+                                    " exceeds the maximum allowed replicas in cluster: " + std::to_string(maxInCluster),
+                                underBrokers(minRequired - n));
+    }
     Model::Spec s;
     s.selImmigrants = e.opt.onlyImmigrants;
     s.selExclTopics = e.opt.anyExclTopic;
@@ -338,8 +370,8 @@ class ReplicaCapacity : public GoalImpl {
     const std::vector<int32_t> list = m.sorted(b, sortId(kind, false, false));
     std::vector<int32_t> order, cands;
     auto fail = [&](int r) {
-      if (!m.alive(b)) throw OptimizationFailure("[" + name + "] Failed to move dead broker replica.");
-      if (m.curOffline(r)) throw OptimizationFailure("[" + name + "] Failed to move offline replica.");
+      if (!m.alive(b)) throw OptimizationFailure("[" + name + "] Failed to move dead broker replica.", underBrokers(1));
+      if (m.curOffline(r)) throw OptimizationFailure("[" + name + "] Failed to move offline replica.", underBrokers(1));
     };
     auto less = [&](int x, int y) { return m.nrep(x) != m.nrep(y) ? m.nrep(x) < m.nrep(y) : x < y; };
     bool built = false;
@@ -381,7 +413,8 @@ class ReplicaCapacity : public GoalImpl {
       for (int b = 0; b < m.B; ++b)
         if ((int64_t)m.nrep(b) > maxR)
           throw OptimizationFailure("[" + name + "] Replica count in broker " + std::to_string(b) +
-                                    " exceeds the maximum allowed number of replicas per broker.");
+                                        " exceeds the maximum allowed number of replicas per broker.",
+                                    underBrokers(1));
       finished = true;
     } else {
       selfHealingMode = false;
@@ -421,8 +454,20 @@ class Capacity : public GoalImpl {
     const double existing = m.clusterUtil(res);
     const double capacity = m.capacityWithAllowedReplicaMoves(res, e.opt.exclMove);
     if (capacity * thr < existing) {
-      if (n == 0) throw OptimizationFailure("[" + name + "] All alive brokers are excluded from replica moves.");
-      throw OptimizationFailure("[" + name + "] Insufficient capacity for " + resName(res) + ".");
+      if (n == 0)
+        throw OptimizationFailure("[" + name + "] All alive brokers are excluded from replica moves.", underBrokers(m.maxRf));
+      // a typical broker: the first of aliveBrokersNotExcludedForReplicaMove (a HashSet<Integer>) (:160-166)
+      std::vector<int> ids, ord;
+      for (int b = 0; b < m.B; ++b)
+        if (allowed[b]) ids.push_back(b);
+      javaHashSetOrder(ids, ord);
+      const int typical = ord.front();
+      const double typicalCapacity = m.cap(typical, res);
+      ccmi_provision_recommendation rec =
+          underBrokers((int)std::ceil((existing - capacity * thr) / (typicalCapacity * thr)), res);
+      rec.typical_broker_capacity = typicalCapacity;
+      rec.typical_broker_id = m.bId[typical];
+      throw OptimizationFailure("[" + name + "] Insufficient capacity for " + resName(res) + ".", rec);
     }
     const bool selfHealing = m.numSelfHealing > 0;
     Model::Spec all;
@@ -513,17 +558,21 @@ class Capacity : public GoalImpl {
     // postSanityCheck (:332-355)
     if (isOver)
       throw OptimizationFailure("[" + name + "] Utilization of broker " + std::to_string(b) +
-                                " violated capacity limit for resource " + resName(res) + ".");
+                                    " violated capacity limit for resource " + resName(res) + ".",
+                                underBrokers(1, res));
     if (hasOffline(m, b))
-      throw OptimizationFailure("[" + name + "] Cannot remove offline replicas from broker " + std::to_string(b) + ".");
+      throw OptimizationFailure("[" + name + "] Cannot remove offline replicas from broker " + std::to_string(b) + ".",
+                                underBrokers(1, res));
   }
 
   // updateGoalState (:180-190) + ensureUtilizationUnderCapacity (:192-225)
   void update(Engine& e) override {
     Model& m = e.m;
     for (int b = 0; b < m.B; ++b)
-      if (m.nrep(b) > 0 && m.bu(b, res) > m.cap(b, res) * thr)
-        throw OptimizationFailure("[" + name + "] utilization for broker is above capacity limit.");
+      if (m.nrep(b) > 0 && m.bu(b, res) > m.cap(b, res) * thr)  // one broker per host: the host check comes first
+        throw OptimizationFailure("[" + name + "] utilization for " + (res != R_DISK ? "host" : "broker") +
+                                      " is above capacity limit.",
+                                  underBrokers(1, res));
     ensureNoOfflineReplicas(m, name);
     finished = true;
   }
@@ -631,8 +680,9 @@ class PotentialNwOut : public GoalImpl {
     Model& m = e.m;
     for (int r = 0; r < m.R; ++r)
       if (m.selfHealing[r] && m.curOffline(r)) {
-        if (fix) throw OptimizationFailure("[" + name + "] Cannot remove replica from broker " +
-                                           std::to_string(m.bId[m.rBroker[r]]));
+        if (fix)
+          throw OptimizationFailure("[" + name + "] Cannot remove replica from broker " + std::to_string(m.bId[m.rBroker[r]]),
+                                    underBrokers(1));
         fix = true;
         dg.fixOffline = 1;
         return;
@@ -661,7 +711,8 @@ class TopicReplicaDistribution : public GoalImpl {
   void init(Engine& e) override {
     Model& m = e.m;
     const int n = allowedForReplicaMove(e, allowed);
-    if (n == 0) throw OptimizationFailure("[" + name + "] All alive brokers are excluded from replica moves.");
+    if (n == 0)
+      throw OptimizationFailure("[" + name + "] All alive brokers are excluded from replica moves.", underBrokers(m.maxRf));
     const bool selfHealing = m.numSelfHealing > 0;
     rebalanceTopic.assign(m.T, selfHealing ? 0 : 1);
     if (selfHealing)
@@ -707,8 +758,9 @@ class TopicReplicaDistribution : public GoalImpl {
     Model& m = e.m;
     for (int r = 0; r < m.R; ++r)
       if (m.selfHealing[r] && m.curOffline(r)) {
-        if (fix) throw OptimizationFailure("[" + name + "] Cannot remove replica from broker " +
-                                           std::to_string(m.bId[m.rBroker[r]]));
+        if (fix)
+          throw OptimizationFailure("[" + name + "] Cannot remove replica from broker " + std::to_string(m.bId[m.rBroker[r]]),
+                                    underBrokers(1));
         fix = true;
         dg.fixOffline = 1;
         return;
@@ -910,7 +962,8 @@ class LeaderReplicaDistribution : public GoalImpl {
   void init(Engine& e) override {
     Model& m = e.m;
     const int n = allowedForReplicaMove(e, allowed);
-    if (n == 0) throw OptimizationFailure("[" + name + "] All alive brokers are excluded from replica moves.");
+    if (n == 0)
+      throw OptimizationFailure("[" + name + "] All alive brokers are excluded from replica moves.", underBrokers(m.maxRf));
     const double avg = m.numLeaderReplicas() / (double)n;
     fix = false;
     const double adj = (e.bc.leaderReplicaBalance - 1) * kBalanceMargin;
@@ -930,8 +983,9 @@ class LeaderReplicaDistribution : public GoalImpl {
     Model& m = e.m;
     for (int r = 0; r < m.R; ++r)
       if (m.selfHealing[r] && m.curOffline(r)) {
-        if (fix) throw OptimizationFailure("[" + name + "] Cannot remove replica from broker " +
-                                           std::to_string(m.bId[m.rBroker[r]]));
+        if (fix)
+          throw OptimizationFailure("[" + name + "] Cannot remove replica from broker " + std::to_string(m.bId[m.rBroker[r]]),
+                                    underBrokers(1));
         fix = true;
         dg.fixOffline = 1;
         return;
@@ -1235,7 +1289,8 @@ class LeaderBytesIn : public GoalImpl {
   void init(Engine& e) override {  // initGoalState (:162-185)
     Model& m = e.m;
     numAllowed = allowedForReplicaMove(e, allowed);
-    if (numAllowed == 0) throw OptimizationFailure("[" + name + "] All alive brokers are excluded from replica moves.");
+    if (numAllowed == 0)
+      throw OptimizationFailure("[" + name + "] All alive brokers are excluded from replica moves.", underBrokers(m.maxRf));
     mean = 0.0;
     overLimit = false;
     balance = e.bc.resBalance[R_NW_IN];

@@ -57,10 +57,14 @@ class IntraGoalImpl : public GoalImpl {
       for (int b = 0; b < m.B; ++b) {
         if (!m.alive(b)) continue;
         const double existing = m.bu(b, R_DISK), allowedCap = m.cap(b, R_DISK) * thr;
-        if (allowedCap < existing)
+        if (allowedCap < existing) {
+          ccmi_provision_recommendation rec = underBrokers(1);  // IntraBrokerDiskCapacityGoal.java:92-95
+          rec.total_capacity = existing / thr;
           throw OptimizationFailure(fmt2("[%s] Insufficient disk capacity at broker %d (Utilization %.2f, Allowed "
                                          "Capacity %.2f).",
-                                         name.c_str(), m.bId[b], existing, allowedCap));
+                                         name.c_str(), m.bId[b], existing, allowedCap),
+                                    rec);
+        }
       }
     }
   }
@@ -76,11 +80,16 @@ class IntraGoalImpl : public GoalImpl {
         if (!m.alive(b)) continue;
         for (int k = m.bDiskOff[b]; k < m.bDiskOff[b + 1]; ++k) {
           const int d = m.bDisks[k];
-          if (m.dAlive[d] && m.dUtil[d] > m.dCap[d] * thr)
+          if (m.dAlive[d] && m.dUtil[d] > m.dCap[d] * thr) {
+            ccmi_provision_recommendation rec = provisionRec();  // IntraBrokerDiskCapacityGoal.java:236-239
+            rec.num_disks = 1;
+            rec.total_capacity = m.dUtil[d] / thr;
             throw OptimizationFailure(fmt2("[%s] Utilization (%.2f) for disk Disk[logdir=%s,state=%s,capacity=%f,"
                                            "replicaCount=%d] on broker %d is above capacity limit.",
                                            name.c_str(), m.dUtil[d], m.dLogdir[d].c_str(), "ALIVE", m.dCap[d],
-                                           (int)m.dMembers[d].size(), m.bId[b]));
+                                           (int)m.dMembers[d].size(), m.bId[b]),
+                                      rec);
+          }
         }
       }
     } else {

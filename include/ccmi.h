@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define CCMI_ABI_VERSION 2
+#define CCMI_ABI_VERSION 3
 
 typedef enum ccmi_status {
   CCMI_OK = 0,
@@ -174,6 +174,7 @@ typedef struct ccmi_balancing_constraint {
   int64_t max_replicas_per_broker;
   int64_t overprovisioned_max_replicas_per_broker;
   int32_t overprovisioned_min_brokers;
+  int32_t overprovisioned_min_extra_racks;
 } ccmi_balancing_constraint;
 
 /* analyzer/OptimizationOptions.java (7-field form) */
@@ -222,6 +223,37 @@ typedef struct ccmi_cluster_stats {
   double disk_utilization_std;
 } ccmi_cluster_stats;
 
+/* analyzer/ProvisionStatus.java */
+typedef enum ccmi_provision_status {
+  CCMI_PROVISION_UNDECIDED = 0,
+  CCMI_PROVISION_RIGHT_SIZED = 1,
+  CCMI_PROVISION_UNDER_PROVISIONED = 2,
+  CCMI_PROVISION_OVER_PROVISIONED = 3
+} ccmi_provision_status;
+
+/* analyzer/ProvisionRecommendation.java: -1 = unset (DEFAULT_OPTIONAL_INT / DEFAULT_OPTIONAL_DOUBLE). The
+ * recommendation's topic pattern and excluded rack ids are not carried. */
+typedef struct ccmi_provision_recommendation {
+  int32_t status;                 /* a ccmi_provision_status: UNDER or OVER */
+  int32_t num_brokers, num_racks, num_disks, num_partitions;
+  int32_t typical_broker_id;      /* broker id */
+  int32_t resource;               /* ccmi resource index (CPU, NW_IN, NW_OUT, DISK) */
+  int32_t pad;
+  double typical_broker_capacity;
+  double total_capacity;
+} ccmi_provision_recommendation;
+
+/* One goal's Goal.provisionResponse() (analyzer/ProvisionResponse.java): its status and, when the goal recorded one,
+ * its own recommendation (recommendationByRecommender.get(goal name)). After an OptimizationFailureException the
+ * status is UNDER_PROVISIONED with the exception's recommendation (AbstractGoal.java:125-126); on success it has been
+ * through GoalUtils.validateProvisionResponse (:619-650). Aggregating goals' responses (ProvisionResponse.aggregate,
+ * OptimizerResult's provision status) is the caller's, over the per-goal results. */
+typedef struct ccmi_provision_response {
+  int32_t status;                 /* ccmi_provision_status */
+  int32_t has_recommendation;
+  ccmi_provision_recommendation recommendation;
+} ccmi_provision_response;
+
 typedef struct ccmi_goal_result {
   int32_t goal_kind;
   int32_t succeeded;            /* Goal.optimize return value */
@@ -232,6 +264,7 @@ typedef struct ccmi_goal_result {
   int64_t device_launches;      /* scan-kernel launches */
   int64_t actions;              /* relocate* calls recorded in the action log */
   ccmi_cluster_stats stats;     /* ClusterModelStats after the goal (GoalOptimizer.statsByGoalPriority) */
+  ccmi_provision_response provision;
 } ccmi_goal_result;
 
 /* Test fixture generator: RandomCluster properties (common/ClusterProperty.java + populate() flags) */
@@ -292,6 +325,9 @@ ccmi_status ccmi_action_acceptance_by_kind(ccmi_session* s, int32_t goal_kind, c
  * fails the call with CCMI_E_INVALID and `*applied` (optional) = actions applied before it. Applied actions join
  * the action log and the proposals (the diff against the session's initial placement). */
 ccmi_status ccmi_session_apply(ccmi_session* s, const ccmi_action* actions, int64_t n, int64_t* applied);
+/* Goal.provisionResponse of the goal whose OptimizationFailureException (CCMI_E_OPT_FAILURE) ended the session's last
+ * optimization call: UNDER_PROVISIONED with the exception's ProvisionRecommendation (AbstractGoal.java:125-130). */
+ccmi_status ccmi_last_failure_provision(const ccmi_session* s, ccmi_provision_response* out);
 ccmi_status ccmi_compute_cluster_stats(ccmi_session* s, const ccmi_balancing_constraint* constraint,
                                const ccmi_opt_options* options, ccmi_cluster_stats* out);
 

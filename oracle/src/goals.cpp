@@ -60,13 +60,14 @@ void ensureNoOfflineReplicas(ClusterModel& cm, const std::string& goal) {
   for (int r : cm.selfHealingEligibleReplicas)
     if (cm.isCurrentOffline(r))
       throw OptimizationFailure("[" + goal + "] Cannot remove replica from broker " +
-                                std::to_string(cm.brokers[cm.replicas[r].broker].id));
+                                    std::to_string(cm.brokers[cm.replicas[r].broker].id),
+                                underBrokers(1));
 }
 void ensureReplicasMoveOffBrokersWithBadDisks(ClusterModel& cm, const std::string& goal) {
   for (int b : cm.brokersWithBadDisks)
     for (int r : cm.brokers[b].replicas)
       if (cm.partitions[cm.replicas[r].partition].ineligibleBrokers.count(b))
-        throw OptimizationFailure("[" + goal + "] A replica was moved back to broker with broken disk.");
+        throw OptimizationFailure("[" + goal + "] A replica was moved back to broker with broken disk.", underBrokers(1));
 }
 
 // Iteration order of a java.util.HashSet<Broker> built by add() in the given order (Collectors.toSet()):
@@ -117,6 +118,15 @@ bool AbstractGoal::optimize(ClusterModel& cm, const GoalList& optimizedGoals, co
     ~Clear() { cm.clearSortedReplicas(); }
   } clearGuard{cm};
   succeeded_ = true;
+  provision_ = ProvisionResp{};  // UNDECIDED for every optimize call
+  try {
+    return optimizeImpl(cm, optimizedGoals, o);
+  } catch (OptimizationFailure& e) {
+    provision_ = ProvisionResp{PROV_UNDER, e.hasRec, e.rec};  // AbstractGoal.java:125-126
+    throw;
+  }
+}
+bool AbstractGoal::optimizeImpl(ClusterModel& cm, const GoalList& optimizedGoals, const OptimizationOptions& o) {
   ClusterModelStats before = computeStats(cm, bc_, o);
   finished_ = false;
   initGoalState(cm, o);
@@ -134,7 +144,25 @@ bool AbstractGoal::optimize(ClusterModel& cm, const GoalList& optimizedGoals, co
     if (compareStats(after, before) < 0)
       throw std::logic_error("Optimization for goal " + name() + " failed because the optimized result is worse than before.");
   }
+  provision_ = validateProvisionResponse(provision_, cm, bc_.overprovisionedMinBrokers);
   return succeeded_;
+}
+
+// GoalUtils.validateProvisionResponse (GoalUtils.java:619-650)
+ProvisionResp validateProvisionResponse(const ProvisionResp& p, ClusterModel& cm, int overprovisionedMinBrokers) {
+  if (p.status != PROV_OVER) return p;
+  const int alive = (int)cm.aliveBrokers().size();
+  if (alive < overprovisionedMinBrokers) return ProvisionResp{PROV_RIGHT_SIZED};
+  if (!p.hasRec) throw std::invalid_argument("Expected to have exactly 1 provision recommendation, but got: 0");
+  const int maxAllowedToDrop = alive - cm.maxReplicationFactor;
+  if (p.rec.numBrokers <= maxAllowedToDrop) return p;
+  if (maxAllowedToDrop > 0) {
+    ProvisionRec r;
+    r.status = PROV_OVER;
+    r.numBrokers = maxAllowedToDrop;
+    return ProvisionResp{PROV_OVER, true, r};
+  }
+  return ProvisionResp{PROV_RIGHT_SIZED};
 }
 
 // AbstractGoal.maybeApplyBalancingAction (AbstractGoal.java:230-272)
@@ -240,7 +268,9 @@ void ReplicaDistributionGoal::initGoalState(ClusterModel& cm, const Optimization
       allowed_[b] = 1;
       numAllowed_++;
     }
-  if (numAllowed_ == 0) throw OptimizationFailure("[" + name() + "] All alive brokers are excluded from replica moves.");
+  if (numAllowed_ == 0)
+    throw OptimizationFailure("[" + name() + "] All alive brokers are excluded from replica moves.",
+                              underBrokers(cm.maxReplicationFactor));
   avgReplicasOnAliveBroker_ = cm.numReplicas() / (double)numAllowed_;
   fixOfflineReplicasOnly_ = false;
   double adj = (bc_.replicaBalancePercentage - 1) * 0.9;
@@ -260,25 +290,41 @@ void ReplicaDistributionGoal::initGoalState(ClusterModel& cm, const Optimization
   }
 }
 
-// ReplicaDistributionAbstractGoal.updateGoalState (+ ReplicaDistributionGoal provisioning)
+// ReplicaDistributionAbstractGoal.updateGoalState (:187-229), then ReplicaDistributionGoal's provisioning
+// (ReplicaDistributionGoal.java:85-107), every round
 void ReplicaDistributionGoal::updateGoalState(ClusterModel& cm, const OptimizationOptions&) {
-  if (!aboveUpper_.empty()) {
-    aboveUpper_.clear();
-    succeeded_ = false;
+  [&] {
+    if (!aboveUpper_.empty()) {
+      aboveUpper_.clear();
+      succeeded_ = false;
+    }
+    if (!underLower_.empty()) {
+      underLower_.clear();
+      succeeded_ = false;
+    }
+    try {
+      ensureNoOfflineReplicas(cm, name());
+    } catch (OptimizationFailure&) {
+      if (fixOfflineReplicasOnly_) throw;
+      fixOfflineReplicasOnly_ = true;
+      return;
+    }
+    ensureReplicasMoveOffBrokersWithBadDisks(cm, name());
+    finished_ = true;
+  }();
+  const int allowedNumBrokers = (int)(cm.numReplicas() / bc_.overprovisionedMaxReplicasPerBroker);
+  const int numBrokersToDrop = numAllowed_ - allowedNumBrokers;
+  bool anyAboveMax = false;
+  for (int b : cm.aliveBrokers())
+    if ((int64_t)cm.brokers[b].replicas.size() > bc_.overprovisionedMaxReplicasPerBroker) anyAboveMax = true;
+  if (numBrokersToDrop > 0 && !anyAboveMax) {
+    ProvisionRec rec;
+    rec.status = PROV_OVER;
+    rec.numBrokers = numBrokersToDrop;
+    provision_ = ProvisionResp{PROV_OVER, true, rec};
+  } else {
+    provision_ = ProvisionResp{PROV_RIGHT_SIZED};
   }
-  if (!underLower_.empty()) {
-    underLower_.clear();
-    succeeded_ = false;
-  }
-  try {
-    ensureNoOfflineReplicas(cm, name());
-  } catch (OptimizationFailure&) {
-    if (fixOfflineReplicasOnly_) throw;
-    fixOfflineReplicasOnly_ = true;
-    return;
-  }
-  ensureReplicasMoveOffBrokersWithBadDisks(cm, name());
-  finished_ = true;
 }
 
 bool ReplicaDistributionGoal::selfSatisfied(ClusterModel& cm, const BalancingAction& a) {
@@ -535,7 +581,9 @@ void ResourceDistributionGoal::initGoalState(ClusterModel& cm, const Optimizatio
       allowed_[b] = 1;
       n++;
     }
-  if (n == 0) throw OptimizationFailure("[" + name() + "] All alive brokers are excluded from replica moves.");
+  if (n == 0)
+    throw OptimizationFailure("[" + name() + "] All alive brokers are excluded from replica moves.",
+                              underBrokers(cm.maxReplicationFactor));
   fixOfflineReplicasOnly_ = false;
   double resourceUtilization = expectedUtil(cm.load, resource_, cm.W);
   double capacity = cm.capacityWithAllowedReplicaMovesFor(resource_, o);
@@ -543,6 +591,28 @@ void ResourceDistributionGoal::initGoalState(ClusterModel& cm, const Optimizatio
   upperThr_ = computeResourceUtilizationBalanceThreshold(avgPct, resource_, bc_, o.triggeredByGoalViolation, 0.9, false);
   lowerThr_ = computeResourceUtilizationBalanceThreshold(avgPct, resource_, bc_, o.triggeredByGoalViolation, 0.9, true);
   isLowUtilization_ = avgPct <= bc_.lowUtilizationThreshold[resource_];
+  if (isLowUtilization_) {
+    // brokerIdWithMaxCapacity over _brokersAllowedReplicaMove (a HashSet<Integer>, strict >) (:268-296)
+    std::vector<int> ids;
+    for (int b : cm.aliveBrokers())
+      if (allowed_[b]) ids.push_back(b);
+    int typical = -1;
+    double maxCapacity = 0.0;
+    for (int b : javaHashSetOrderIntKeys(ids))
+      if (cm.brokers[b].capacity[resource_] > maxCapacity) {
+        typical = b;
+        maxCapacity = cm.brokers[b].capacity[resource_];
+      }
+    const double typicalCapacity = cm.brokers[typical].capacity[resource_];
+    const double allowedCapacity = resourceUtilization / bc_.lowUtilizationThreshold[resource_];
+    const int allowedNumBrokers = (int)(allowedCapacity / typicalCapacity);
+    overRec_ = ProvisionRec{};
+    overRec_.status = PROV_OVER;
+    overRec_.numBrokers = std::max(n - allowedNumBrokers, 1);
+    overRec_.typicalBrokerCapacity = typicalCapacity;
+    overRec_.typicalBrokerId = cm.brokers[typical].id;
+    overRec_.resource = resource_;
+  }
 }
 
 // ResourceDistributionGoal.updateGoalState (:301-349)
@@ -553,7 +623,9 @@ void ResourceDistributionGoal::updateGoalState(ClusterModel& cm, const Optimizat
     if (!isExcludedForReplicaMove(b) && !aboveLowerLimit(cm, b)) anyUnder = true;
   }
   if (anyAbove) succeeded_ = false;
+  else if (isLowUtilization_) provision_ = ProvisionResp{PROV_OVER, true, overRec_};
   if (anyUnder) succeeded_ = false;
+  else if (!anyAbove && !isLowUtilization_) provision_ = ProvisionResp{PROV_RIGHT_SIZED};
   try {
     ensureNoOfflineReplicas(cm, name());
   } catch (OptimizationFailure&) {

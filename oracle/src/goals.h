@@ -21,8 +21,32 @@
 
 namespace oracle {
 
+// analyzer/ProvisionStatus.java, ProvisionRecommendation.java (-1 = unset, DEFAULT_OPTIONAL_INT / _DOUBLE),
+// ProvisionResponse.java (one goal's response: its status and, for UNDER/OVER, its own recommendation or none)
+enum ProvisionStatus { PROV_UNDECIDED = 0, PROV_RIGHT_SIZED = 1, PROV_UNDER = 2, PROV_OVER = 3 };
+struct ProvisionRec {
+  int status = PROV_UNDER;
+  int numBrokers = -1, numRacks = -1, numDisks = -1, numPartitions = -1, typicalBrokerId = -1, resource = -1;
+  double typicalBrokerCapacity = -1.0, totalCapacity = -1.0;
+};
+inline ProvisionRec underBrokers(int n, int resource = -1) {
+  ProvisionRec r;
+  r.numBrokers = n;
+  r.resource = resource;
+  return r;
+}
+struct ProvisionResp {
+  int status = PROV_UNDECIDED;
+  bool hasRec = false;
+  ProvisionRec rec;
+};
+
+// OptimizationFailureException with its (optional) ProvisionRecommendation
 struct OptimizationFailure : std::runtime_error {
-  using std::runtime_error::runtime_error;
+  explicit OptimizationFailure(const std::string& m) : std::runtime_error(m) {}
+  OptimizationFailure(const std::string& m, const ProvisionRec& r) : std::runtime_error(m), hasRec(true), rec(r) {}
+  bool hasRec = false;
+  ProvisionRec rec;
 };
 // java.lang.UnsupportedOperationException thrown inside the reference's goal code
 struct UnsupportedOperation : std::runtime_error {
@@ -41,12 +65,18 @@ class Goal {
   virtual Acceptance actionAcceptance(const BalancingAction& a, ClusterModel& cm) = 0;
   // ClusterModelStatsComparator.compare(after, before): < 0 means "before" is preferred.
   virtual int compareStats(const ClusterModelStats& s1, const ClusterModelStats& s2) const = 0;
+  // Goal.provisionResponse (Goal.java:155-164)
+  const ProvisionResp& provision() const { return provision_; }
+
+ protected:
+  ProvisionResp provision_;
 };
 
 class AbstractGoal : public Goal {
  public:
   explicit AbstractGoal(const BalancingConstraint& bc) : bc_(bc) {}
   bool optimize(ClusterModel& cm, const GoalList& optimizedGoals, const OptimizationOptions& o) override;
+  bool optimizeImpl(ClusterModel& cm, const GoalList& optimizedGoals, const OptimizationOptions& o);
 
  protected:
   virtual void initGoalState(ClusterModel& cm, const OptimizationOptions& o) = 0;
@@ -75,6 +105,7 @@ class AbstractGoal : public Goal {
 };
 
 // GoalUtils helpers
+ProvisionResp validateProvisionResponse(const ProvisionResp& p, ClusterModel& cm, int overprovisionedMinBrokers);
 std::vector<int> eligibleBrokers(ClusterModel& cm, int replica, const std::vector<int>& candidates, ActionType a,
                                  const OptimizationOptions& o);
 bool legitMove(ClusterModel& cm, int replica, int destBroker, ActionType a);
@@ -170,6 +201,7 @@ class ResourceDistributionGoal : public AbstractGoal {
   double upperThr_ = 0, lowerThr_ = 0;
   std::vector<char> allowed_;
   bool isLowUtilization_ = false;
+  ProvisionRec overRec_;  // _overProvisionedRecommendation
 };
 
 // ===================================================================== remaining default goals

@@ -140,7 +140,9 @@ void IntraBrokerDiskCapacityGoal::initGoalState(ClusterModel& cm, const Optimiza
       std::snprintf(buf, sizeof(buf),
                     "[%s] Insufficient disk capacity at broker %d (Utilization %.2f, Allowed Capacity %.2f).",
                     name().c_str(), cm.brokers[b].id, existing, allowed);
-      throw OptimizationFailure(buf);
+      ProvisionRec rec = underBrokers(1);  // IntraBrokerDiskCapacityGoal.java:92-95
+      rec.totalCapacity = existing / thr;
+      throw OptimizationFailure(buf, rec);
     }
   }
   cm.excludedTopicsSel = o.excludedTopics;
@@ -179,7 +181,10 @@ void IntraBrokerDiskCapacityGoal::updateGoalState(ClusterModel& cm, const Optimi
         char buf[768];
         std::snprintf(buf, sizeof(buf), "[%s] Utilization (%.2f) for disk %s on broker %d is above capacity limit.",
                       name().c_str(), cm.disks[d].utilization, diskString(cm, d).c_str(), cm.brokers[b].id);
-        throw OptimizationFailure(buf);
+        ProvisionRec rec;  // IntraBrokerDiskCapacityGoal.java:236-239
+        rec.numDisks = 1;
+        rec.totalCapacity = cm.disks[d].utilization / bc_.capacityThreshold[DISK];
+        throw OptimizationFailure(buf, rec);
       }
   finished_ = true;
 }

@@ -79,14 +79,29 @@ void RackAwareGoal::initGoalState(ClusterModel& cm, const OptimizationOptions& o
     for (int t : byTopic.order()) {
       if (o.excludedTopics.count(t)) continue;
       maxIncluded = std::max(maxIncluded, cm.replicationFactorByTopic[t]);
-      if (maxIncluded > numAliveRacks)
+      if (maxIncluded > numAliveRacks) {
+        ProvisionRec rec;
+        rec.numRacks = maxIncluded - numAliveRacks;
         throw OptimizationFailure("[RackAwareGoal] Insufficient number of racks to distribute included replicas (Current: " +
-                                  std::to_string(numAliveRacks) + ", Needed: " + std::to_string(maxIncluded) + ").");
+                                      std::to_string(numAliveRacks) + ", Needed: " + std::to_string(maxIncluded) + ").",
+                                  rec);
+      }
     }
   } else if (cm.maxReplicationFactor > numAliveRacks) {
+    ProvisionRec rec;
+    rec.numRacks = cm.maxReplicationFactor - numAliveRacks;
     throw OptimizationFailure("[RackAwareGoal] Insufficient number of racks to distribute each replica (Current: " +
-                              std::to_string(numAliveRacks) + ", Needed: " + std::to_string(cm.maxReplicationFactor) +
-                              ").");
+                                  std::to_string(numAliveRacks) + ", Needed: " + std::to_string(cm.maxReplicationFactor) +
+                                  ").",
+                              rec);
+  }
+  // over-provisioned in racks (:103-109)
+  const int numExtraRacks = numAliveRacks - cm.maxReplicationFactor;
+  if (numExtraRacks >= bc_.overprovisionedMinExtraRacks) {
+    ProvisionRec rec;
+    rec.status = PROV_OVER;
+    rec.numRacks = numExtraRacks - bc_.overprovisionedMinExtraRacks + 1;
+    provision_ = ProvisionResp{PROV_OVER, true, rec};
   }
   SortSpec spec;
   if (o.onlyMoveImmigrantReplicas) spec.selection.push_back({SelFn::IMMIGRANTS});
@@ -101,11 +116,15 @@ void RackAwareGoal::updateGoalState(ClusterModel& cm, const OptimizationOptions&
     if (o.excludedTopics.count(cm.partitions[p].topic)) continue;
     std::set<int> racks;
     for (int r : cm.partitions[p].replicas) racks.insert(cm.brokers[cm.replicas[r].broker].rack);
-    if (racks.size() != cm.partitions[p].replicas.size())
-      throw OptimizationFailure("[RackAwareGoal] Partition " + std::to_string(p) + " is not rack-aware.");
+    if (racks.size() != cm.partitions[p].replicas.size()) {
+      ProvisionRec rec;
+      rec.numRacks = (int)(cm.partitions[p].replicas.size() - racks.size());
+      throw OptimizationFailure("[RackAwareGoal] Partition " + std::to_string(p) + " is not rack-aware.", rec);
+    }
   }
   ensureNoOfflineReplicas(cm, name());
   ensureReplicasMoveOffBrokersWithBadDisks(cm, name());
+  if (provision_.status != PROV_OVER) provision_ = ProvisionResp{PROV_RIGHT_SIZED};
   finished_ = true;
 }
 
@@ -139,7 +158,8 @@ void RackAwareGoal::rebalanceForBroker(int b, ClusterModel& cm, const GoalList& 
     std::vector<int> eligible = rackAwareEligibleBrokers(cm, r);
     if (maybeApplyBalancingAction(cm, r, eligible, ActionType::INTER_BROKER_REPLICA_MOVEMENT, g, o) < 0)
       throw OptimizationFailure("[RackAwareGoal] Cannot move replica of partition " +
-                                std::to_string(cm.replicas[r].partition) + " to a rack-aware broker.");
+                                    std::to_string(cm.replicas[r].partition) + " to a rack-aware broker.",
+                                underBrokers(1));  // AbstractRackAwareGoal.java:162-163 (excludedRackIds not carried)
   }
 }
 
@@ -183,7 +203,8 @@ void MinTopicLeadersPerBrokerGoal::rebalanceForBroker(int b, ClusterModel& cm, c
   for (int r : offline)
     if (maybeApplyBalancingAction(cm, r, eligible, ActionType::INTER_BROKER_REPLICA_MOVEMENT, g, o) < 0)
       throw OptimizationFailure("[MinTopicLeadersPerBrokerGoal] Cannot remove offline replica from broker " +
-                                std::to_string(cm.brokers[b].id));
+                                    std::to_string(cm.brokers[b].id),
+                                underBrokers(1));
 }
 
 // ===================================================================== ReplicaCapacityGoal
@@ -227,9 +248,12 @@ void ReplicaCapacityGoal::initGoalState(ClusterModel& cm, const OptimizationOpti
   int allowed = 0;
   allowedForReplicaMove(cm, o, &allowed);
   const int64_t maxInCluster = bc_.maxReplicasPerBroker * allowed;
-  if (total > maxInCluster)
+  if (total > maxInCluster) {
+    const int minRequired = (int)std::ceil(total / (double)bc_.maxReplicasPerBroker);  // :145-148
     throw OptimizationFailure("[ReplicaCapacityGoal] Total replicas in cluster: " + std::to_string(total) +
-                              " exceeds the maximum allowed replicas in cluster: " + std::to_string(maxInCluster));
+                                  " exceeds the maximum allowed replicas in cluster: " + std::to_string(maxInCluster),
+                              underBrokers(minRequired - allowed));
+  }
   SortSpec spec;
   if (o.onlyMoveImmigrantReplicas) spec.selection.push_back({SelFn::IMMIGRANTS});
   if (!o.excludedTopics.empty()) spec.selection.push_back({SelFn::EXCLUDED_TOPICS});
@@ -246,7 +270,8 @@ void ReplicaCapacityGoal::updateGoalState(ClusterModel& cm, const OptimizationOp
     for (size_t b = 0; b < cm.brokers.size(); ++b)
       if ((int64_t)cm.brokers[b].replicas.size() > bc_.maxReplicasPerBroker)
         throw OptimizationFailure("[ReplicaCapacityGoal] Replica count in broker " + std::to_string(b) +
-                                  " exceeds the maximum allowed number of replicas per broker.");
+                                      " exceeds the maximum allowed number of replicas per broker.",
+                                  underBrokers(1));
     finished_ = true;
   } else {
     selfHealingMode_ = false;
@@ -269,8 +294,8 @@ void ReplicaCapacityGoal::rebalanceForBroker(int b, ClusterModel& cm, const Goal
     });
     if (maybeApplyBalancingAction(cm, r, eligible, ActionType::INTER_BROKER_REPLICA_MOVEMENT, g, o) < 0) {
       if (!cm.brokers[b].isAlive())
-        throw OptimizationFailure("[ReplicaCapacityGoal] Failed to move dead broker replica.");
-      if (offline) throw OptimizationFailure("[ReplicaCapacityGoal] Failed to move offline replica.");
+        throw OptimizationFailure("[ReplicaCapacityGoal] Failed to move dead broker replica.", underBrokers(1));
+      if (offline) throw OptimizationFailure("[ReplicaCapacityGoal] Failed to move offline replica.", underBrokers(1));
     }
   }
 }
@@ -330,9 +355,22 @@ void CapacityGoal::initGoalState(ClusterModel& cm, const OptimizationOptions& o)
   const double allowedCapacity = capacity * bc_.capacityThreshold[resource_];
   if (allowedCapacity < existing) {
     int allowed = 0;
-    allowedForReplicaMove(cm, o, &allowed);
-    if (allowed == 0) throw OptimizationFailure("[" + name() + "] All alive brokers are excluded from replica moves.");
-    throw OptimizationFailure("[" + name() + "] Insufficient capacity for " + resourceName(resource_) + ".");
+    const std::vector<char> allowedB = allowedForReplicaMove(cm, o, &allowed);
+    if (allowed == 0)
+      throw OptimizationFailure("[" + name() + "] All alive brokers are excluded from replica moves.",
+                                underBrokers(cm.maxReplicationFactor));
+    // a typical broker: the first of aliveBrokersNotExcludedForReplicaMove (a HashSet<Integer>) (:160-166)
+    std::vector<int> ids;
+    for (int b : cm.aliveBrokers())
+      if (allowedB[b]) ids.push_back(b);
+    const int typical = javaHashSetOrderIntKeys(ids).front();
+    const double typicalCapacity = cm.brokers[typical].capacity[resource_];
+    const double missing = existing - allowedCapacity;
+    ProvisionRec rec = underBrokers((int)std::ceil(missing / (typicalCapacity * bc_.capacityThreshold[resource_])),
+                                    resource_);
+    rec.typicalBrokerCapacity = typicalCapacity;
+    rec.typicalBrokerId = cm.brokers[typical].id;
+    throw OptimizationFailure("[" + name() + "] Insufficient capacity for " + resourceName(resource_) + ".", rec);
   }
   const bool selfHealing = !cm.selfHealingEligibleReplicas.empty();
   SortSpec all;
@@ -360,10 +398,11 @@ void CapacityGoal::updateGoalState(ClusterModel& cm, const OptimizationOptions&)
   for (size_t b = 0; b < cm.brokers.size(); ++b) {
     const bool hasReplicas = !cm.brokers[b].replicas.empty();
     if (isHostResource(resource_) && hasReplicas && cm.hostUtil((int)b, resource_) > cm.hostCapacity((int)b, resource_) * thr)
-      throw OptimizationFailure("[" + name() + "] utilization for host is above capacity limit.");
+      throw OptimizationFailure("[" + name() + "] utilization for host is above capacity limit.", underBrokers(1, resource_));
     if (isBrokerResource(resource_) && hasReplicas &&
         cm.brokerUtil((int)b, resource_) > cm.brokers[b].capacity[resource_] * thr)
-      throw OptimizationFailure("[" + name() + "] utilization for broker is above capacity limit.");
+      throw OptimizationFailure("[" + name() + "] utilization for broker is above capacity limit.",
+                                underBrokers(1, resource_));
   }
   ensureNoOfflineReplicas(cm, name());
   ensureReplicasMoveOffBrokersWithBadDisks(cm, name());
@@ -413,10 +452,13 @@ void CapacityGoal::rebalanceForBroker(int b, ClusterModel& cm, const GoalList& g
       if (!over && !hasOfflineReplicas(cm, b)) break;
     }
   }
-  if (over) throw OptimizationFailure("[" + name() + "] Utilization of broker " + std::to_string(b) +
-                                      " violated capacity limit for resource " + resourceName(resource_) + ".");
+  if (over)
+    throw OptimizationFailure("[" + name() + "] Utilization of broker " + std::to_string(b) +
+                                  " violated capacity limit for resource " + resourceName(resource_) + ".",
+                              underBrokers(1, resource_));
   if (hasOfflineReplicas(cm, b))
-    throw OptimizationFailure("[" + name() + "] Cannot remove offline replicas from broker " + std::to_string(b) + ".");
+    throw OptimizationFailure("[" + name() + "] Cannot remove offline replicas from broker " + std::to_string(b) + ".",
+                              underBrokers(1, resource_));
 }
 
 // ===================================================================== PotentialNwOutGoal
@@ -572,7 +614,9 @@ int TopicReplicaDistributionGoal::compareStats(const ClusterModelStats& s1, cons
 void TopicReplicaDistributionGoal::initGoalState(ClusterModel& cm, const OptimizationOptions& o) {
   int numAllowed = 0;
   allowed_ = allowedForReplicaMove(cm, o, &numAllowed);
-  if (numAllowed == 0) throw OptimizationFailure("[" + name() + "] All alive brokers are excluded from replica moves.");
+  if (numAllowed == 0)
+    throw OptimizationFailure("[" + name() + "] All alive brokers are excluded from replica moves.",
+                              underBrokers(cm.maxReplicationFactor));
   // GoalUtils.topicsToRebalance (GoalUtils.java:439-452): the self-healing replicas' topics, or all topics but the
   // excluded ones
   rebalanceTopic_.assign(cm.numTopics(), cm.selfHealingEligibleReplicas.empty() ? 1 : 0);
@@ -768,7 +812,9 @@ bool TopicReplicaDistributionGoal::moveIn(int dest, int topic, ClusterModel& cm,
 void LeaderReplicaDistributionGoal::initGoalState(ClusterModel& cm, const OptimizationOptions& o) {
   int numAllowed = 0;
   allowed_ = allowedForReplicaMove(cm, o, &numAllowed);
-  if (numAllowed == 0) throw OptimizationFailure("[" + name() + "] All alive brokers are excluded from replica moves.");
+  if (numAllowed == 0)
+    throw OptimizationFailure("[" + name() + "] All alive brokers are excluded from replica moves.",
+                              underBrokers(cm.maxReplicationFactor));
   const double avg = cm.partitions.size() / (double)numAllowed;  // ClusterModel.numLeaderReplicas()
   fixOfflineReplicasOnly_ = false;
   const double adj = (bc_.leaderReplicaBalancePercentage - 1) * 0.9;
@@ -1052,7 +1098,9 @@ bool LeaderBytesInDistributionGoal::selfSatisfied(ClusterModel& cm, const Balanc
 // LeaderBytesInDistributionGoal.initGoalState (:162-185)
 void LeaderBytesInDistributionGoal::initGoalState(ClusterModel& cm, const OptimizationOptions& o) {
   allowedForReplicaMove(cm, o, &numAllowed_);
-  if (numAllowed_ == 0) throw OptimizationFailure("[" + name() + "] All alive brokers are excluded from replica moves.");
+  if (numAllowed_ == 0)
+    throw OptimizationFailure("[" + name() + "] All alive brokers are excluded from replica moves.",
+                              underBrokers(cm.maxReplicationFactor));
   mean_ = 0.0;
   overLimit_ = false;
   SortSpec spec;

@@ -32,6 +32,11 @@ std::unique_ptr<Goal> makeGoal(int kind, const BalancingConstraint& bc) {
   }
 }
 
+namespace {
+thread_local ProvisionResp g_lastFailure;
+}
+const ProvisionResp& lastFailureProvision() { return g_lastFailure; }
+
 bool isIntraBrokerGoal(int kind) {
   return kind == CCMI_GOAL_INTRA_BROKER_DISK_CAPACITY || kind == CCMI_GOAL_INTRA_BROKER_DISK_USAGE_DISTRIBUTION;
 }
@@ -77,7 +82,13 @@ OptimizerResult optimizations(ClusterModel& cm, const std::vector<int>& goalKind
     auto gs = clk::now();
     int64_t c0 = cm.candidatesEvaluated;
     size_t a0 = cm.actionLog.size();
-    bool succeeded = g->optimize(cm, optimized, o);
+    bool succeeded;
+    try {
+      succeeded = g->optimize(cm, optimized, o);
+    } catch (OptimizationFailure&) {
+      g_lastFailure = g->provision();
+      throw;
+    }
     optimized.push_back(g.get());
     GoalResult gr;
     gr.name = g->name();
@@ -86,6 +97,7 @@ OptimizerResult optimizations(ClusterModel& cm, const std::vector<int>& goalKind
     gr.seconds = std::chrono::duration<double>(clk::now() - gs).count();
     gr.candidates = cm.candidatesEvaluated - c0;
     gr.actions = (int64_t)(cm.actionLog.size() - a0);
+    gr.provision = g->provision();
     gr.hasDiff = cm.replicaDistributionFlat() != preDist || cm.replicaDiskFlat() != preDisks ||
                  cm.leaderDistribution() != preLeaders || leaderDisks() != preLeaderDisks;
     res.goals.push_back(gr);

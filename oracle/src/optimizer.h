@@ -18,7 +18,10 @@ struct GoalResult {
   ClusterModelStats stats;  // GoalOptimizer.statsByGoalPriority entry
   int64_t candidates;
   int64_t actions;
+  ProvisionResp provision;  // Goal.provisionResponse after the goal
 };
+// provisionResponse of the goal whose OptimizationFailure ended the last optimizations() call on this thread
+const ProvisionResp& lastFailureProvision();
 
 struct Proposal {  // ExecutionProposal (executor/ExecutionProposal.java:58-)
   int partition;

@@ -35,6 +35,7 @@ BalancingConstraint toBc(const ccmi_balancing_constraint* c) {
   bc.maxReplicasPerBroker = c->max_replicas_per_broker;
   bc.overprovisionedMaxReplicasPerBroker = c->overprovisioned_max_replicas_per_broker;
   bc.overprovisionedMinBrokers = c->overprovisioned_min_brokers;
+  bc.overprovisionedMinExtraRacks = c->overprovisioned_min_extra_racks;
   return bc;
 }
 
@@ -52,6 +53,22 @@ OptimizationOptions toOpts(const ccmi_opt_options* o) {
   oo.onlyMoveImmigrantReplicas = o->only_move_immigrant_replicas != 0;
   oo.fastMode = o->fast_mode != 0;
   return oo;
+}
+
+void toCProvision(const ProvisionResp& p, ccmi_provision_response* o) {
+  std::memset(o, 0, sizeof(*o));
+  o->status = p.status;
+  o->has_recommendation = p.hasRec ? 1 : 0;
+  ccmi_provision_recommendation& r = o->recommendation;
+  r.status = p.hasRec ? p.rec.status : 0;
+  r.num_brokers = p.hasRec ? p.rec.numBrokers : -1;
+  r.num_racks = p.hasRec ? p.rec.numRacks : -1;
+  r.num_disks = p.hasRec ? p.rec.numDisks : -1;
+  r.num_partitions = p.hasRec ? p.rec.numPartitions : -1;
+  r.typical_broker_id = p.hasRec ? p.rec.typicalBrokerId : -1;
+  r.resource = p.hasRec ? p.rec.resource : -1;
+  r.typical_broker_capacity = p.hasRec ? p.rec.typicalBrokerCapacity : -1.0;
+  r.total_capacity = p.hasRec ? p.rec.totalCapacity : -1.0;
 }
 
 void toCStats(const ClusterModelStats& s, ccmi_cluster_stats* o) {
@@ -272,6 +289,7 @@ int oc_optimize(void* hv, const int32_t* goals, int n, const ccmi_balancing_cons
       r.candidates = g.candidates;
       r.actions = g.actions;
       toCStats(g.stats, &r.stats);
+      toCProvision(g.provision, &r.provision);
     }
     return 0;
   } catch (DeadlineReached&) {
@@ -304,6 +322,8 @@ int64_t oc_candidates(void* hv) { return ((Handle*)hv)->cm.candidatesEvaluated; 
 
 // Apply externally decided actions (ClusterModel.relocateReplica / relocateLeadership / relocateReplica to a logdir)
 // in order; returns 0 or CCMI_E_INVALID (message in oc_error).
+void oc_last_failure_provision(void*, ccmi_provision_response* out) { toCProvision(lastFailureProvision(), out); }
+
 int32_t oc_apply(void* hv, const ccmi_action* a, int64_t n) {
   auto* h = (Handle*)hv;
   ClusterModel& cm = h->cm;

@@ -20,6 +20,7 @@ struct BalancingConstraint {
   int64_t maxReplicasPerBroker = 10000;
   int64_t overprovisionedMaxReplicasPerBroker = 1500;
   int overprovisionedMinBrokers = 3;
+  int overprovisionedMinExtraRacks = 2;  // AnalyzerConfig.DEFAULT_OVERPROVISIONED_MIN_EXTRA_RACKS
 };
 
 struct ClusterModelStats {

@@ -56,6 +56,7 @@ class Oracle:
             L.oc_action_count.restype = C.c_int64
             L.oc_action_count.argtypes = [C.c_void_p]
             L.oc_actions.argtypes = [C.c_void_p, C.POINTER(ccmi.ActionStruct)]
+            L.oc_last_failure_provision.argtypes = [C.c_void_p, C.POINTER(ccmi.ProvisionRespStruct)]
             L.oc_apply.restype = C.c_int32
             L.oc_apply.argtypes = [C.c_void_p, C.POINTER(ccmi.ActionStruct), C.c_int64]
             L.oc_replica_distribution.argtypes = [C.c_void_p, C.POINTER(C.c_int32)]
@@ -151,9 +152,16 @@ class OracleCluster:
         c = (constraint or ccmi.BalancingConstraint()).to_struct()
         st = self.L.oc_optimize(self.h, kinds, len(goal_names), C.byref(c), C.byref(o), res)
         if st != 0:
-            raise ccmi._STATUS.get(st, RuntimeError)(self.L.oc_error(self.h).decode())
+            err = ccmi._STATUS.get(st, RuntimeError)(self.L.oc_error(self.h).decode())
+            if isinstance(err, ccmi.OptimizationFailureException):
+                p = ccmi.ProvisionRespStruct()
+                self.L.oc_last_failure_provision(self.h, C.byref(p))
+                err.provision = ccmi.ProvisionResponse.from_struct(p, ccmi._goal_of_message(str(err)))
+            raise err
         self.last_results = [ccmi.GoalResult(ccmi.GOAL_NAMES[r.goal_kind], bool(r.succeeded), bool(r.has_diff),
-                                             r.seconds, r.candidates, 0, 0, r.actions, ccmi.stats_to_dict(r.stats))
+                                             r.seconds, r.candidates, 0, 0, r.actions, ccmi.stats_to_dict(r.stats),
+                                             ccmi.ProvisionResponse.from_struct(r.provision,
+                                                                                ccmi.GOAL_NAMES[r.goal_kind]))
                              for r in res]
         return self.last_results
 

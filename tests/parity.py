@@ -94,6 +94,8 @@ def check_desc_against_oracle(lib, desc, keepalive, goals, bc, options=None, dev
     if perr is not None or oerr is not None:
         assert (type(perr).__name__, str(perr)) == (type(oerr).__name__, str(oerr))
         assert cm.actions() == oc.actions()
+        # the failed goal's provision response (UNDER_PROVISIONED with the exception's recommendation)
+        assert getattr(perr, "provision", None) == getattr(oerr, "provision", None)
         return cm, None, oc
     pa, oa = cm.actions(), oc.actions()
     for i, (x, y) in enumerate(zip(pa, oa)):
@@ -105,6 +107,7 @@ def check_desc_against_oracle(lib, desc, keepalive, goals, bc, options=None, dev
     for r, o in zip(res.goal_results, ores):
         assert (r.name, r.succeeded, r.candidates, r.actions) == (o.name, o.succeeded, o.candidates, o.actions), \
             ((r.name, r.succeeded, r.candidates, r.actions), (o.name, o.succeeded, o.candidates, o.actions))
+        assert r.provision == o.provision, (r.name, r.provision, o.provision)
         compare_stats(r.stats, o.stats)
     # Set<ExecutionProposal>: order-free
     assert sorted(map(_key, res.proposals)) == sorted(map(_key, oc.proposals()))

@@ -179,11 +179,13 @@ def run_case(runner, suite, goal, excl, exc, model, dead, opt, props):
     flat = _model(model, dead)
     opts = _options(suite, excl)
     if exc is not None:
-        with pytest.raises(getattr(ccmi, exc)):
+        with pytest.raises(getattr(ccmi, exc)) as ei:
             runner(flat, goal, opts)
+        assert ei.value.provision.status == "UNDER_PROVISIONED"  # (:375 / :422)
         return
-    succeeded, proposals, leaders_before = runner(flat, goal, opts)
+    succeeded, proposals, provision = runner(flat, goal, opts)
     assert succeeded == opt
+    assert provision.status != "UNDER_PROVISIONED"  # the cluster cannot be under-provisioned (:357 / :404)
     if excl and suite == "leadership":
         # no leadership move from an online replica to a broker excluded for leadership
         for p in proposals:
@@ -198,7 +200,7 @@ def run_case(runner, suite, goal, excl, exc, model, dead, opt, props):
 def oracle_runner(flat, goal, opts):
     oc = OracleCluster.from_desc(flat.desc)
     res = oc.optimize([goal], goal_constraint(), opts)
-    return res[0].succeeded, oc.proposals(), None
+    return res[0].succeeded, oc.proposals(), res[0].provision
 
 
 def product_runner(lib):
@@ -206,7 +208,7 @@ def product_runner(lib):
         cm = ccmi.ClusterModel(flat.desc, device=0, lib=lib, keepalive=flat)
         g = getattr(ccmi, goal)(constraint=goal_constraint())
         ok = g.optimize(cm, opts)
-        return ok, cm.proposals(), None
+        return ok, cm.proposals(), g.provision
     return run
 
 

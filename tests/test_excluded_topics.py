@@ -122,11 +122,13 @@ def run_case(runner, goal, excl, exc, model, dead, opt, props, over):
     flat = _model(model, dead)
     opts = _options(flat, excl)
     if exc is not None:
-        with pytest.raises(getattr(ccmi, exc)):
+        with pytest.raises(getattr(ccmi, exc)) as ei:
             runner(flat, goal, opts, _constraint(over))
+        assert ei.value.provision.status == "UNDER_PROVISIONED"  # ExcludedTopicsTest.java:363
         return
-    succeeded, proposals = runner(flat, goal, opts, _constraint(over))
+    succeeded, proposals, provision = runner(flat, goal, opts, _constraint(over))
     assert succeeded == opt
+    assert provision.status != "UNDER_PROVISIONED"  # ExcludedTopicsTest.java:342
     if excl:
         assert bool(proposals) == props
         excluded_idx = {flat.topics.index(t) for t in excl}
@@ -139,7 +141,7 @@ def run_case(runner, goal, excl, exc, model, dead, opt, props, over):
 def oracle_runner(flat, goal, opts, bc):
     oc = OracleCluster.from_desc(flat.desc)
     res = oc.optimize([goal], bc, opts)
-    return res[0].succeeded, oc.proposals()
+    return res[0].succeeded, oc.proposals(), res[0].provision
 
 
 def product_runner(lib):
@@ -147,7 +149,7 @@ def product_runner(lib):
         cm = ccmi.ClusterModel(flat.desc, device=0, lib=lib, keepalive=flat)
         g = getattr(ccmi, goal)(constraint=bc)
         ok = g.optimize(cm, opts)
-        return ok, cm.proposals()
+        return ok, cm.proposals(), g.provision
     return run
 
 
