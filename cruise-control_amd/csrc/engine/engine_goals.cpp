@@ -1370,6 +1370,89 @@ class LeaderBytesIn : public GoalImpl {
 
 }  // namespace
 
+// ======================================================================================= PreferredLeaderElectionGoal
+// PreferredLeaderElectionGoal.optimize (PreferredLeaderElectionGoal.java:117-190), the no-argument constructor
+// (skipUrpDemotion = excludeFollowerDemotion = false). A one-pass leadership election with no candidate search: every
+// partition's leadership goes to its first alive, online replica (with demoted brokers: only the partitions they led,
+// after their replicas moved to the end of the replica lists), so it runs on the host model and the device only sees
+// the touched rows. Demoted disks are not in the flattened model.
+struct PartitionOrder {  // TopicPartition in a HashMap bin: (topic, partition)
+  const Model* m;
+  int cmp(int a, int b) const {
+    const int c = m->topicNames[m->pTopic[a]].compare(m->topicNames[m->pTopic[b]]);
+    return c ? c : jcmpInt(m->pNumber[a], m->pNumber[b]);
+  }
+};
+
+class PreferredLeaderElection : public GoalImpl {
+ public:
+  PreferredLeaderElection() {
+    kind = CCMI_GOAL_PREFERRED_LEADER_ELECTION;
+    name = "PreferredLeaderElectionGoal";
+  }
+  void init(Engine& e) override {
+    if (e.opt.triggered)  // sanityCheckOptimizationOptions (:79-83)
+      throw std::invalid_argument(name + " goal does not support use by goal violation detector.");
+    allowedForReplicaMove(e, allowed);
+    dg = DevGoal{};
+    dg.kind = DG_ACCEPT_ALL;  // actionAcceptance: ACCEPT
+    dg.allowedSlot = (int)e.optimized.size();
+  }
+  bool rebalanceAll(Engine& e) override {
+    PhaseScope ps(PH_OTHER_GOALS);
+    Model& m = e.m;
+    bool hasDemoted = false;
+    std::vector<uint8_t> toMove(m.P, 0);
+    std::vector<int> alive, ord;
+    for (int b = 0; b < m.B; ++b)
+      if (m.alive(b)) alive.push_back(b);
+    javaHashSetOrder(alive, ord);  // clusterModel.aliveBrokers(): a HashSet<Broker>
+    std::vector<int32_t> reps;
+    for (int b : ord) {
+      if (m.bState[b] != BState::DEMOTED) continue;
+      hasDemoted = true;
+      m.bReplicaSet[b].order(reps);  // Broker.replicas(): HashSet order
+      for (int r : reps) m.moveReplicaToEnd(r);
+      m.bLeaderSet[b].order(reps);
+      for (int r : reps) toMove[m.rPart[r]] = 1;
+    }
+    // clusterModel.getPartitionsByTopic(): topics by name, each topic's partitions in the model's
+    // HashMap<TopicPartition, Partition> iteration order
+    PartitionOrder po{&m};
+    JHashSet<PartitionOrder> all(&po);
+    for (int p = 0; p < m.P; ++p) all.add(p, jMix(jMix(1, m.pNumber[p]), m.topicHash[m.pTopic[p]]));
+    std::vector<int32_t> order;
+    all.order(order);
+    std::vector<std::vector<int32_t>> byTopic(m.T);
+    for (int p : order) byTopic[m.pTopic[p]].push_back(p);
+    std::vector<int> topics(m.T);
+    for (int t = 0; t < m.T; ++t) topics[t] = t;
+    std::sort(topics.begin(), topics.end(), [&m](int a, int b) { return m.topicNames[a] < m.topicNames[b]; });
+    bool relocated = false;
+    for (int t : topics)
+      for (int p : byTopic[t]) {
+        if (hasDemoted && !toMove[p]) continue;
+        for (int i = m.pOff[p]; i < m.pOff[p + 1]; ++i) {
+          if (!hasDemoted && i > m.pOff[p]) break;  // only the first (preferred) replica
+          const int r = m.pSlots[i], cand = m.rBroker[r];
+          if (!m.alive(cand)) continue;
+          if (m.curOffline(r)) continue;
+          if (!m.rLeader[r]) {
+            if (e.opt.anyExclLead && e.opt.exclLead[cand]) continue;
+            m.relocateLeadership(p, m.rBroker[m.pLeader[p]], cand);
+            relocated = true;
+          }
+          break;
+        }
+      }
+    succeeded = relocated;  // Goal.optimize returns whether a leadership moved
+    return true;
+  }
+  void rebalance(Engine&, int) override {}
+  void update(Engine&) override { finished = true; }
+  int compareStats(const ccmi_cluster_stats&, const ccmi_cluster_stats&) const override { return 0; }
+};
+
 std::unique_ptr<GoalImpl> makeMoreGoal(int kind) {
   switch (kind) {
     case CCMI_GOAL_RACK_AWARE: return std::make_unique<RackAware>();
@@ -1383,6 +1466,7 @@ std::unique_ptr<GoalImpl> makeMoreGoal(int kind) {
     case CCMI_GOAL_TOPIC_REPLICA_DISTRIBUTION: return std::make_unique<TopicReplicaDistribution>();
     case CCMI_GOAL_LEADER_REPLICA_DISTRIBUTION: return std::make_unique<LeaderReplicaDistribution>();
     case CCMI_GOAL_LEADER_BYTES_IN_DISTRIBUTION: return std::make_unique<LeaderBytesIn>();
+    case CCMI_GOAL_PREFERRED_LEADER_ELECTION: return std::make_unique<PreferredLeaderElection>();
     default: throw Unsupported("goal kind " + std::to_string(kind) + " is not implemented in this build");
   }
 }

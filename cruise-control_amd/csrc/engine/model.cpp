@@ -526,6 +526,19 @@ void Model::relocateReplica(int p, int src, int dst) {
   }
 }
 
+void Model::moveReplicaToEnd(int r) {
+  const int p = rPart[r];
+  int pos = pOff[p];
+  while (pos < pOff[p + 1] && pSlots[pos] != r) ++pos;
+  if (pos == pOff[p + 1]) throw StateError("Did not find replica for partition.");
+  for (int i = pos; i + 1 < pOff[p + 1]; ++i) pSlots[i] = pSlots[i + 1];
+  pSlots[pOff[p + 1] - 1] = r;
+  if (dev && !replaying) {
+    markChain(cDirtyP, cDirtyPList, p);
+    markP(p);
+  }
+}
+
 bool Model::relocateLeadership(int p, int src, int dst) {
   PhaseScope ps(PH_RELOCATE);
   bVer[src]++;

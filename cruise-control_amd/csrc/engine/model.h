@@ -239,6 +239,7 @@ class Model {
   // ---- mutations (record into the action log, mark dirty rows)
   void relocateReplica(int p, int src, int dst);
   bool relocateLeadership(int p, int src, int dst);
+  void moveReplicaToEnd(int r);  // Partition.moveReplicaToEnd (Partition.java:192-197): slot order only
 
   // ---- sorted replica tracking (sorted-vector implementation of SortedReplicas)
   struct Spec {

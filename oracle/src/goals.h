@@ -250,6 +250,19 @@ class MinTopicLeadersPerBrokerGoal : public AbstractGoal {
   bool selfSatisfied(ClusterModel& cm, const BalancingAction& a) override;
 };
 
+// PreferredLeaderElectionGoal (analyzer/goals/PreferredLeaderElectionGoal.java) with skipUrpDemotion = false,
+// excludeFollowerDemotion = false (the no-argument constructor GoalOptimizer uses). Demoted disks are not in the
+// flattened model, so only demoted brokers are considered.
+class PreferredLeaderElectionGoal : public Goal {
+ public:
+  explicit PreferredLeaderElectionGoal(const BalancingConstraint&) {}
+  std::string name() const override { return "PreferredLeaderElectionGoal"; }
+  bool isHardGoal() const override { return false; }
+  bool optimize(ClusterModel& cm, const GoalList& optimizedGoals, const OptimizationOptions& o) override;
+  Acceptance actionAcceptance(const BalancingAction&, ClusterModel&) override { return Acceptance::ACCEPT; }
+  int compareStats(const ClusterModelStats&, const ClusterModelStats&) const override { return 0; }
+};
+
 class ReplicaCapacityGoal : public AbstractGoal {
  public:
   using AbstractGoal::AbstractGoal;

@@ -207,6 +207,56 @@ void MinTopicLeadersPerBrokerGoal::rebalanceForBroker(int b, ClusterModel& cm, c
                                 underBrokers(1));
 }
 
+// ===================================================================== PreferredLeaderElectionGoal
+// PreferredLeaderElectionGoal.optimize (PreferredLeaderElectionGoal.java:117-190)
+bool PreferredLeaderElectionGoal::optimize(ClusterModel& cm, const GoalList&, const OptimizationOptions& o) {
+  provision_ = ProvisionResp{};
+  if (o.triggeredByGoalViolation)  // sanityCheckOptimizationOptions (:79-83)
+    throw std::invalid_argument(name() + " goal does not support use by goal violation detector.");
+  // demoted brokers: their replicas go to the end of the partitions' replica lists (Partition.moveReplicaToEnd),
+  // their leaders' partitions are the ones to re-elect (clusterModel.aliveBrokers(): a HashSet<Broker>)
+  bool hasDemoted = false;
+  std::set<int> partitionsToMove;
+  for (int b : javaHashSetOrderIntKeys(cm.aliveBrokers())) {
+    const Broker& br = cm.brokers[b];
+    if (br.state != BrokerState::DEMOTED) continue;
+    hasDemoted = true;
+    for (int r : br.replicaSet.order()) cm.moveReplicaToEnd(r);  // Broker.replicas(): HashSet order
+    for (int r : br.leaderSet.order()) partitionsToMove.insert(cm.replicas[r].partition);
+  }
+  // clusterModel.getPartitionsByTopic(): topics by name, each topic's partitions in the
+  // HashMap<TopicPartition, Partition> iteration order of the model's partitions
+  JHashSet all([&cm](int x, int y) {
+    const int c = cm.topicNames[cm.partitions[x].topic].compare(cm.topicNames[cm.partitions[y].topic]);
+    return c != 0 ? c : icompare(cm.partitions[x].number, cm.partitions[y].number);
+  });
+  for (size_t p = 0; p < cm.partitions.size(); ++p) all.add((int)p, cm.tpHash((int)p));
+  std::vector<std::vector<int>> byTopic(cm.numTopics());
+  for (int p : all.order()) byTopic[cm.partitions[p].topic].push_back(p);
+  std::vector<int> topics(cm.numTopics());
+  for (int t = 0; t < cm.numTopics(); ++t) topics[t] = t;
+  std::sort(topics.begin(), topics.end(), [&cm](int a, int b) { return cm.topicNames[a] < cm.topicNames[b]; });
+  bool relocated = false;
+  for (int t : topics)
+    for (int p : byTopic[t]) {
+      if (hasDemoted && !partitionsToMove.count(p)) continue;
+      const std::vector<int> reps = cm.partitions[p].replicas;
+      for (size_t i = 0; i < reps.size(); ++i) {
+        if (!hasDemoted && i > 0) break;  // only the first (preferred) replica
+        const int r = reps[i], cand = cm.replicas[r].broker;
+        if (!cm.brokers[cand].isAlive()) continue;
+        if (cm.isCurrentOffline(r)) continue;
+        if (!cm.replicas[r].isLeader) {
+          if (o.excludedBrokersForLeadership.count(cm.brokers[cand].id)) continue;
+          cm.relocateLeadership(p, cm.replicas[cm.partitions[p].leader].broker, cand);
+          relocated = true;
+        }
+        break;
+      }
+    }
+  return relocated;
+}
+
 // ===================================================================== ReplicaCapacityGoal
 // ReplicaCapacityGoal.actionAcceptance (ReplicaCapacityGoal.java:69-82)
 Acceptance ReplicaCapacityGoal::actionAcceptance(const BalancingAction& a, ClusterModel& cm) {

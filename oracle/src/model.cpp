@@ -554,6 +554,14 @@ void ClusterModel::relocateReplica(int p, int src, int dst) {
   if (recordActions) actionLog.push_back({(int)ActionType::INTER_BROKER_REPLICA_MOVEMENT, p, src, dst, -1});
 }
 
+void ClusterModel::moveReplicaToEnd(int r) {
+  std::vector<int>& v = partitions[replicas[r].partition].replicas;
+  auto it = std::find(v.begin(), v.end(), r);
+  if (it == v.end()) throw std::logic_error("Did not find replica for partition.");
+  v.erase(it);
+  v.push_back(r);
+}
+
 bool ClusterModel::relocateLeadership(int p, int src, int dst) {
   int sr = replicaOnBroker(p, src);
   if (!replicas[sr].isLeader) return false;

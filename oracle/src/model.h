@@ -368,6 +368,7 @@ class ClusterModel {
   // --- mutation (ClusterModel.relocateReplica / relocateLeadership)
   void relocateReplica(int partition, int srcBroker, int dstBroker);
   bool relocateLeadership(int partition, int srcBroker, int dstBroker);
+  void moveReplicaToEnd(int replica);  // Partition.moveReplicaToEnd (Partition.java:192-197)
 
   // --- sorted replicas (Broker.trackSortedReplicas / SortedReplicas)
   void trackSortedReplicas(int brokerIdx, const std::string& name, const SortSpec& spec);

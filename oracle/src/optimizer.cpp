@@ -28,6 +28,7 @@ std::unique_ptr<Goal> makeGoal(int kind, const BalancingConstraint& bc) {
     case CCMI_GOAL_INTRA_BROKER_DISK_CAPACITY: return std::make_unique<IntraBrokerDiskCapacityGoal>(bc);
     case CCMI_GOAL_INTRA_BROKER_DISK_USAGE_DISTRIBUTION:
       return std::make_unique<IntraBrokerDiskUsageDistributionGoal>(bc);
+    case CCMI_GOAL_PREFERRED_LEADER_ELECTION: return std::make_unique<PreferredLeaderElectionGoal>(bc);
     default: throw std::invalid_argument("goal kind not in oracle scope: " + std::to_string(kind));
   }
 }

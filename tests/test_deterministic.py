@@ -17,8 +17,8 @@ from parity import check_desc_against_oracle
 from verifier import (build_model, deterministic_models, offline_replicas, verify_broken_brokers,
                       verify_regression, verify_soft_goal_replica_movements)
 
-# DeterministicClusterTest.java:97-115 in priority order. Not yet in this build: RackAwareDistributionGoal,
-# PreferredLeaderElectionGoal (the deck runs without them).
+# DeterministicClusterTest.java:97-115 in priority order. Not yet in this build: RackAwareDistributionGoal
+# (the deck runs without it).
 DECK_GOALS_ALL = ["RackAwareGoal", "RackAwareDistributionGoal", "MinTopicLeadersPerBrokerGoal", "ReplicaCapacityGoal",
                   "DiskCapacityGoal", "NetworkInboundCapacityGoal", "NetworkOutboundCapacityGoal", "CpuCapacityGoal",
                   "ReplicaDistributionGoal", "PotentialNwOutGoal", "DiskUsageDistributionGoal",
