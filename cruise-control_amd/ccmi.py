@@ -390,6 +390,27 @@ class ProvisionRecommendation:
     total_capacity: float = -1.0
 
 
+RESOURCE_NAMES = {"CPU": "cpu", "NW_IN": "networkInbound", "NW_OUT": "networkOutbound", "DISK": "disk"}  # Resource.java
+
+
+def _recommendation_text(r: "ProvisionRecommendation") -> str:
+    s = f"{'Add' if r.status == 'UNDER_PROVISIONED' else 'Remove'} at least "
+    if r.num_brokers != -1:
+        s += f"{r.num_brokers} broker{'s' if r.num_brokers > 1 else ''}"
+    elif r.num_racks != -1:
+        s += f"{r.num_racks} rack{'s' if r.num_racks > 1 else ''} with brokers"
+    elif r.num_disks != -1:
+        s += f"{r.num_disks} disk{'s' if r.num_disks > 1 else ''}"
+    if r.typical_broker_id != -1:
+        s += f" with the same {RESOURCE_NAMES[r.resource]} capacity ({r.typical_broker_capacity:.2f}) as broker-" \
+             f"{r.typical_broker_id}"
+    elif r.resource is not None:
+        s += f" for {RESOURCE_NAMES[r.resource]}"
+    if r.total_capacity != -1.0:
+        s += f" with a total capacity of {r.total_capacity:.2f}"
+    return s + "."
+
+
 def _goal_of_message(msg: str) -> str:
     """The goal name an OptimizationFailureException message starts with ("[GoalName] ...")."""
     return msg[1:msg.index("]")] if msg.startswith("[") and "]" in msg else ""
@@ -437,6 +458,11 @@ class ProvisionResponse:
                 self.status = "OVER_PROVISIONED"
                 self.recommendation_by_recommender.update(other.recommendation_by_recommender)
         return self
+
+    def recommendation(self) -> str:
+        """ProvisionResponse.recommendation(): "[recommender] text" per recommendation (ProvisionRecommendation.toString,
+        ProvisionRecommendation.java:364-398)."""
+        return " ".join(f"[{k}] {_recommendation_text(v)}" for k, v in self.recommendation_by_recommender.items())
 
     def __eq__(self, other) -> bool:
         return isinstance(other, ProvisionResponse) and (self.status, self.recommendation_by_recommender) == \
@@ -501,6 +527,88 @@ class OptimizerResult:
     @property
     def candidates(self) -> int:
         return sum(g.candidates for g in self.goal_results)
+
+    # GoalOptimizer.optimizations (:480-485): a goal is violated before the optimization when it moved something or
+    # did not succeed, and after it when it did not succeed
+    @property
+    def violated_goals_before(self) -> List[str]:
+        return [g.name for g in self.goal_results if g.has_diff or not g.succeeded]
+
+    @property
+    def violated_goals_after_optimization(self) -> List[str]:
+        return list(self.violated_goals_after)
+
+    def _balancedness(self, violated: Sequence[str]) -> float:
+        """OptimizerResult.onDemandBalancednessScore (OptimizerResult.java:123-131)."""
+        score = MAX_BALANCEDNESS_SCORE
+        cost = getattr(self, "balancedness_cost_by_goal", {})
+        for g in self.goal_results:
+            if g.name in violated:
+                score -= cost.get(g.name, 0.0)
+        return score
+
+    @property
+    def on_demand_balancedness_score_before(self) -> float:
+        return self._balancedness(self.violated_goals_before)
+
+    @property
+    def on_demand_balancedness_score_after(self) -> float:
+        return self._balancedness(self.violated_goals_after)
+
+    def goal_result_description(self, goal_name: str) -> str:
+        """OptimizerResult.goalResultDescription (:243-246)."""
+        if goal_name not in self.violated_goals_before:
+            return "NO-ACTION"
+        return "VIOLATED" if goal_name in self.violated_goals_after else "FIXED"
+
+    def movement_stats(self) -> List[int]:
+        """OptimizerResult.getMovementStats (:259-279): inter-broker replica moves and MB, intra-broker replica moves
+        and MB, leadership moves, over the ExecutionProposals (replicasToAdd / replicasToRemove /
+        replicasToMoveBetweenDisksByBroker of ExecutionProposal.java:169-245)."""
+        n_inter = mb_inter = n_intra = mb_intra = n_lead = 0
+        for p in self.proposals:
+            # ExecutionProposal.java:74-78: additions / removals by broker id; a replica whose (broker, logdir) is new
+            # on a broker that keeps the partition moves between disks
+            old_b, new_b = set(p.old_replicas), set(p.new_replicas)
+            to_add, to_remove = new_b - old_b, old_b - new_b
+            old_pl = set(zip(p.old_replicas, p.old_disks or [-1] * len(p.old_replicas)))
+            between_disks = [b for b, d in zip(p.new_replicas, p.new_disks or [-1] * len(p.new_replicas))
+                             if b not in to_add and (b, d) not in old_pl]
+            if to_add or to_remove:
+                n_inter += 1
+                mb_inter += len(to_add) * p.partition_size
+            elif between_disks:
+                n_intra += len(between_disks)
+                mb_intra += p.partition_size * len(between_disks)
+            else:
+                n_lead += 1
+        return [n_inter, mb_inter, n_intra, mb_intra, n_lead]
+
+    def proposal_summary_json(self) -> Dict[str, object]:
+        """OptimizerResult.getProposalSummaryForJson (OptimizerResult.java:300-320)."""
+        m = self.movement_stats()
+        opts = getattr(self, "options", None) or OptimizationOptions()
+        names = self._cluster.topic_names()
+        prov = self.provision_response
+        return {
+            "numReplicaMovements": m[0], "dataToMoveMB": m[1], "numIntraBrokerReplicaMovements": m[2],
+            "intraBrokerDataToMoveMB": m[3], "numLeaderMovements": m[4],
+            "recentWindows": self._cluster.desc.num_windows, "monitoredPartitionsPercentage": 100.0,
+            "excludedTopics": sorted(names[t] for t in opts.excluded_topics),
+            "excludedBrokersForLeadership": sorted(opts.excluded_brokers_for_leadership),
+            "excludedBrokersForReplicaMove": sorted(opts.excluded_brokers_for_replica_move),
+            "onDemandBalancednessScoreBefore": self.on_demand_balancedness_score_before,
+            "onDemandBalancednessScoreAfter": self.on_demand_balancedness_score_after,
+            "provisionStatus": prov.status, "provisionRecommendation": prov.recommendation(),
+        }
+
+    def proposals_json(self) -> List[Dict[str, object]]:
+        """ExecutionProposal.getJsonStructure (ExecutionProposal.java:266-270) of every proposal."""
+        names = self._cluster.topic_names()
+        d = self._cluster.desc
+        return [{"topicPartition": f"{names[d.partition_topic[p.partition]]}-{d.partition_number[p.partition]}",
+                 "oldLeader": p.old_leader, "oldReplicas": list(p.old_replicas), "newReplicas": list(p.new_replicas)}
+                for p in self.proposals]
 
     @property
     def provision_response(self) -> ProvisionResponse:
@@ -719,6 +827,9 @@ class ClusterModel:
         self.num_partitions = desc.num_partitions
         self.num_replicas = desc.num_replicas
 
+    def topic_names(self) -> List[str]:
+        return [self.desc.topic_names[t].decode() for t in range(self.desc.num_topics)]
+
     @staticmethod
     def from_buffers(buf: ClusterBuffers, device: int = 0) -> "ClusterModel":
         return ClusterModel(buf.desc, device=device, lib=buf.lib, keepalive=buf)
@@ -881,10 +992,15 @@ def rccl_unique_id(lib: Optional["Library"] = None) -> bytes:
 
 
 class GoalOptimizer:
-    """GoalOptimizer.optimizations (GoalOptimizer.java:435-524) on a device session."""
+    """GoalOptimizer.optimizations (GoalOptimizer.java:435-524) on a device session. priority_weight /
+    strictness_weight: goal.balancedness.priority.weight / goal.balancedness.strictness.weight (AnalyzerConfig.java:
+    374-385) for the on-demand balancedness score."""
 
-    def __init__(self, constraint: Optional[BalancingConstraint] = None):
+    def __init__(self, constraint: Optional[BalancingConstraint] = None, priority_weight: float = 1.1,
+                 strictness_weight: float = 1.5):
         self.constraint = constraint or BalancingConstraint()
+        self.priority_weight = priority_weight
+        self.strictness_weight = strictness_weight
 
     def optimizations(self, cluster: ClusterModel, goals_by_priority: Sequence[Goal],
                       options: Optional[OptimizationOptions] = None) -> OptimizerResult:
@@ -902,7 +1018,104 @@ class GoalOptimizer:
         grs = [GoalResult(GOAL_NAMES[r.goal_kind], bool(r.succeeded), bool(r.has_diff), r.seconds, r.candidates,
                           r.device_candidates, r.device_launches, r.actions, stats_to_dict(r.stats),
                           ProvisionResponse.from_struct(r.provision, GOAL_NAMES[r.goal_kind])) for r in results]
-        return OptimizerResult(grs, cluster, dt, [g.name for g in grs if not g.succeeded])
+        res = OptimizerResult(grs, cluster, dt, [g.name for g in grs if not g.succeeded])
+        res.options = options or OptimizationOptions()
+        res.balancedness_cost_by_goal = balancedness_cost_by_goal(goals_by_priority, self.priority_weight,
+                                                                  self.strictness_weight)
+        return res
+
+
+MAX_BALANCEDNESS_SCORE = 100.0  # KafkaCruiseControlUtils.MAX_BALANCEDNESS_SCORE
+BALANCEDNESS_SCORE_WITH_OFFLINE_REPLICAS = -1.0  # GoalViolationDetector.java:69
+
+
+@dataclass
+class GoalViolations:
+    """detector/GoalViolations: the violated detection goals by fixability, the aggregated provision response and
+    the balancedness score GoalViolationDetector.run() leaves behind."""
+    fixable: List[str]
+    unfixable: List[str]
+    provision_response: "ProvisionResponse"
+    balancedness_score: float
+    skipped_due_to_offline_replicas: bool = False
+    seconds: float = 0.0
+
+
+class GoalViolationDetector:
+    """GoalViolationDetector.run (detector/GoalViolationDetector.java:176-332) as a what-if batch.
+
+    Each detection goal is optimized on its own, without optimized goals, with OptimizationOptions
+    (excluded topics / brokers, isTriggeredByGoalViolation = true; DefaultOptimizationOptionsGenerator.java:17-25):
+    an OptimizationFailureException makes it an unfixable violation, a diff a fixable one. The reference reuses the
+    model only after a goal that changed nothing, so every goal sees the initial model: the goals are independent and
+    run as concurrent device sessions (one host thread and HIP stream each, `max_concurrency` at a time) instead of
+    one after the other. A model with dead brokers or broken disks is skipped (skipDueToOfflineReplicas :259-273)."""
+
+    def __init__(self, detection_goals: Sequence[str], constraint: Optional[BalancingConstraint] = None,
+                 priority_weight: float = 1.1, strictness_weight: float = 1.5, lib: Optional[Library] = None,
+                 device: int = 0, max_concurrency: int = 8):
+        self.goals = list(detection_goals)
+        self.constraint = constraint or BalancingConstraint()
+        self.cost = balancedness_cost_by_goal(goals_from_names(self.goals), priority_weight, strictness_weight)
+        self.lib = lib or Library.get()
+        self.device = device
+        self.max_concurrency = max_concurrency
+
+    def detect(self, desc: ClusterDesc, keepalive=None, excluded_topics: Sequence[int] = (),
+               excluded_brokers_for_leadership: Sequence[int] = (),
+               excluded_brokers_for_replica_move: Sequence[int] = ()) -> GoalViolations:
+        import time
+        from concurrent.futures import ThreadPoolExecutor
+        t0 = time.perf_counter()
+        states = [desc.broker_state[b] for b in range(desc.num_brokers)]
+        if BROKER_STATES["DEAD"] in states or BROKER_STATES["BAD_DISKS"] in states:
+            return GoalViolations([], [], ProvisionResponse("UNDECIDED"), BALANCEDNESS_SCORE_WITH_OFFLINE_REPLICAS, True,
+                                  time.perf_counter() - t0)
+        opts = OptimizationOptions(excluded_topics=list(excluded_topics),
+                                   excluded_brokers_for_leadership=list(excluded_brokers_for_leadership),
+                                   excluded_brokers_for_replica_move=list(excluded_brokers_for_replica_move),
+                                   is_triggered_by_goal_violation=True)
+
+        def one(name: str):  # GoalViolationDetector.optimizeForGoal (:296-331)
+            cm = ClusterModel(desc, device=self.device, lib=self.lib, keepalive=keepalive)
+            goal = goals_from_names([name], self.constraint)[0]
+            try:
+                goal.optimize(cm, opts)
+            except OptimizationFailureException as e:
+                return name, "unfixable", e.provision
+            diff = cm.proposals()
+            return name, ("fixable" if diff else None), goal.provision
+
+        with ThreadPoolExecutor(max(1, min(self.max_concurrency, len(self.goals)))) as pool:
+            outcomes = list(pool.map(one, self.goals))
+        fixable = [n for n, v, _ in outcomes if v == "fixable"]
+        unfixable = [n for n, v, _ in outcomes if v == "unfixable"]
+        prov = ProvisionResponse("UNDECIDED")
+        for _, _, p in outcomes:
+            if p is not None:
+                prov.aggregate(p)
+        score = MAX_BALANCEDNESS_SCORE - sum(self.cost[n] for n in fixable + unfixable)  # refreshBalancednessScore
+        return GoalViolations(fixable, unfixable, prov, score, False, time.perf_counter() - t0)
+
+
+def balancedness_cost_by_goal(goals: Sequence[Goal], priority_weight: float = 1.1,
+                              strictness_weight: float = 1.5) -> Dict[str, float]:
+    """KafkaCruiseControlUtils.balancednessCostByGoal (KafkaCruiseControlUtils.java:844-870)."""
+    if not goals:
+        raise IllegalArgumentException("At least one goal must be provided to get the balancedness cost.")
+    if priority_weight <= 0 or strictness_weight <= 0:
+        raise IllegalArgumentException(f"Balancedness weights must be positive (priority:{priority_weight:f}, "
+                                       f"strictness:{strictness_weight:f}).")
+    cost: Dict[str, float] = {}
+    weight_sum = 0.0
+    previous = 1 / priority_weight
+    for g in reversed(list(goals)):
+        current = priority_weight * previous
+        c = current * (strictness_weight if g.is_hard_goal() else 1)
+        weight_sum += c
+        cost[g.name()] = c
+        previous = current
+    return {k: MAX_BALANCEDNESS_SCORE * v / weight_sum for k, v in cost.items()}
 
 
 def goals_from_names(names: Sequence[str], constraint: Optional[BalancingConstraint] = None) -> List[Goal]:
