@@ -39,7 +39,8 @@ hipError_t launchChainRackRows(const DevTables& T, const ChainTables& C, const D
 hipError_t launchSyncLoads(const ChainTables& C, const LoadRow* lrows, int nl, const SlotRow* srows, int ns,
                            hipStream_t st);
 hipError_t launchStats(const StatsParams& P, const int32_t* tc, const int32_t* topicNrep, const BrokerRec* brokers,
-                       const uint8_t* allowedAlive, TopicPartial* scratch, StatsOut* out, int ldB, hipStream_t st,
+                       const uint8_t* allowedAlive, TopicPartial* scratch, void* partials, StatsOut* out, int ldB,
+                       hipStream_t st,
                        hipEvent_t evTopic0, hipEvent_t evTopic1);
 
 hipError_t launchIntra(const IntraArgs& A, hipStream_t st);
@@ -103,6 +104,7 @@ Device::Device(int ordinal, int B, int R, int P, int T, int maxGoalSlots)
   dalloc(&dDone_, 4);
   hipCheck(hipMalloc(&topicScratch_, (size_t)(T ? T : 1) * sizeof(TopicPartial)), "hipMalloc");
   hipCheck(hipMalloc(&statsOut_, 1024), "hipMalloc");
+  hipCheck(hipMalloc(&statsPart_, (size_t)kStatsPartBlocks * (kStatD * 8 + kStatI * 4 + 8)), "hipMalloc");
   hipCheck(hipMemset(dDone_, 0, 4 * sizeof(unsigned int)), "hipMemset");
   hipCheck(hipMemset(dResult_, 0xff, 2 * sizeof(unsigned long long)), "hipMemset");
   // host-coherent (fine-grained) mapped memory: kernels read the staging area and write the mailbox directly
@@ -140,8 +142,8 @@ Device::~Device() {
     }
     (void)hipFree(stamps_);
   }
-  void* ps[] = {brokers_, replicas_, parts_, allowedAlive_, topicCount_, topicNrep_, topicScratch_, statsOut_, dReq_,
-                rowVisited_, dResult_, dDone_, tUpper_, tLower_, dRLoad_, dBLoad_, dBLnw_, dBPot_, dPOff_, dPSlots_,
+  void* ps[] = {brokers_, replicas_, parts_, allowedAlive_, topicCount_, topicNrep_, topicScratch_, statsOut_,
+                statsPart_, dReq_, rowVisited_, dResult_, dDone_, tUpper_, tLower_, dRLoad_, dBLoad_, dBLnw_, dBPot_, dPOff_, dPSlots_,
                 dPLeader_, dChainLog_, dChainOut_, pIneligOff_, pIneligB_};
   for (void* p : ps)
     if (p) (void)hipFree(p);
@@ -542,7 +544,7 @@ void Device::stats(const StatsParams& P, const uint8_t* allowedAliveHost, StatsO
   launchPrepFor(g, req, false);
   hipCheck(hipMemcpyAsync(allowedAlive_, dReq_, (size_t)ldB_, hipMemcpyDeviceToDevice, ST), "allowedAlive");
   hipCheck(launchStats(P, topicCount_, topicNrep_, brokers_, allowedAlive_, (TopicPartial*)topicScratch_,
-                       (StatsOut*)statsOut_, ldB_, ST, timing ? EV0 : nullptr, timing ? EV1 : nullptr),
+                       statsPart_, (StatsOut*)statsOut_, ldB_, ST, timing ? EV0 : nullptr, timing ? EV1 : nullptr),
            "stats");
   hipCheck(hipMemcpyAsync(statsHost_, statsOut_, sizeof(StatsOut), hipMemcpyDeviceToHost, ST), "D2H stats");
   hipCheck(hipStreamSynchronize(ST), "sync");

@@ -152,7 +152,7 @@ class Device {
   std::vector<PartitionRec> hParts_;
   std::vector<int32_t> hRPart_, hROrig_, hPOff_, bRackHost_;
   std::vector<uint32_t> allowedHost_;
-  void *topicScratch_ = nullptr, *statsOut_ = nullptr;
+  void *topicScratch_ = nullptr, *statsOut_ = nullptr, *statsPart_ = nullptr;
   // staging (host-coherent, mapped) and the request copy in HBM
   char* hStage_ = nullptr;
   char* hStageDev_ = nullptr;

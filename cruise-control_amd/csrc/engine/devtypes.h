@@ -229,7 +229,14 @@ struct StatsParams {
   double upperThr[4], lowerThr[4];
   double potCapacity;  // capacityWithAllowedReplicaMovesFor(NW_OUT)
   double nwOutCapThreshold;
+  double potSum;                 // sum of potential NW_OUT over alive allowed brokers (ClusterModelStats.java:334-340)
+  int64_t repTotal, leadTotal;   // replicas / leaders over all brokers (populateReplicaStats totals)
 };
+// stats_partials record layout: double fields [0,4) hot, [4,8) cold, [8,12) variance sums per resource, then the
+// named ones; int fields [0,4) balanced counts per resource, then the named ones.
+enum : int { kSdPHot = 12, kSdPCold, kSdPVar, kSdRepVar, kSdLeadVar, kSdTAvg, kSdTSd, kStatD };
+enum : int { kSiUnder = 4, kSiRepMx, kSiRepMn, kSiLeadMx, kSiLeadMn, kSiTMx, kSiTMn, kStatI };
+constexpr int kStatsPartBlocks = 64;
 struct StatsOut {
   double resAvg[4], resMax[4], resMin[4], resStd[4];
   int32_t numBalanced[4];

@@ -349,6 +349,11 @@ ccmi_cluster_stats Engine::stats() {
   }
   P.potCapacity = m.capacityWithAllowedReplicaMoves(R_NW_OUT, opt.exclMove);
   P.nwOutCapThreshold = bc.capThreshold[R_NW_OUT];
+  for (int b = 0; b < m.B; ++b) {
+    if (aa[b]) P.potSum += m.potNwOut(b);
+    P.repTotal += m.nrep(b);
+    P.leadTotal += m.bNlead[b];
+  }
   StatsOut o;
   dev->stats(P, aa.data(), &o);
   ccmi_cluster_stats s;

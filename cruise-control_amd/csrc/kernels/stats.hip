@@ -4,9 +4,10 @@
 //                numForAvgTopicReplicas loop (ClusterModelStats.java:446-476), the dominant HBM stream.
 //                Rows are read 16 B per lane (int4), max/min/variance reduced through LDS, one record
 //                per topic written out.
-// stats_final  : one workgroup: per-resource utilization stats (:267-322), potential NW_OUT (:332-362),
-//                replica / leader count stats (:371-436) over the broker columns, plus the reduction of
-//                the per-topic records. Sums are tree-ordered (parity bar for stats: 1e-9 relative).
+// stats_partials / stats_combine : per-resource utilization stats (:267-322), potential NW_OUT (:332-362),
+//                replica / leader count stats (:371-436) over the broker columns, plus the reduction of the
+//                per-topic records: a grid of up to kStatsPartBlocks workgroups, then one wave folding their
+//                partials in block order. Sums are tree-ordered (parity bar for stats: 1e-9 relative).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -82,134 +83,169 @@ __global__ __launch_bounds__(kTB) void stats_topics(const int32_t* __restrict__ 
   }
 }
 
-__global__ __launch_bounds__(1024) void stats_final(StatsParams P, const BrokerRec* __restrict__ br,
-                                                    const uint8_t* __restrict__ allowedAlive,
-                                                    const TopicPartial* __restrict__ topics, StatsOut* __restrict__ out) {
-  __shared__ double sd[16];
-  __shared__ int si[16];
-  const int B = P.B;
+// stats_partials + stats_combine: the broker-column and topic-record reductions as a grid of kPartBlocks
+// workgroups, each writing one StatsPartial, then one wave folding the partials in block order (deterministic).
+// The two averages a variance needs (potential NW_OUT sum, replica / leader totals) come from the host in
+// StatsParams, so every quantity is a single pass.
+struct StatsPartial {
+  double d[kStatD];
+  int32_t i[kStatI];
+};
+
+__device__ __forceinline__ double dOp(int k, double a, double b) {
+  return k < 4 || k == kSdPHot ? (a > b ? a : b) : (k < 8 || k == kSdPCold) ? (a < b ? a : b) : a + b;
+}
+__device__ __forceinline__ int32_t iOp(int k, int32_t a, int32_t b) {
+  return (k == kSiRepMx || k == kSiLeadMx || k == kSiTMx) ? (a > b ? a : b)
+         : (k == kSiRepMn || k == kSiLeadMn || k == kSiTMn) ? (a < b ? a : b)
+                                                              : a + b;
+}
+__device__ __forceinline__ double dInit(int k) {
+  return (k >= 4 && k < 8) || k == kSdPCold ? 1.7976931348623157e308 : 0.0;
+}
+__device__ __forceinline__ int32_t iInit(int k) {
+  return (k == kSiRepMn || k == kSiLeadMn || k == kSiTMn) ? 0x7fffffff : 0;
+}
+
+template <int N>
+__device__ __forceinline__ void waveFoldD(double (&v)[N]) {
+#pragma unroll
+  for (int k = 0; k < N; ++k)
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v[k] = dOp(k, v[k], __shfl_xor(v[k], off, 64));
+}
+template <int N>
+__device__ __forceinline__ void waveFoldI(int32_t (&v)[N]) {
+#pragma unroll
+  for (int k = 0; k < N; ++k)
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v[k] = iOp(k, v[k], __shfl_xor(v[k], off, 64));
+}
+
+__global__ __launch_bounds__(kTB) void stats_partials(StatsParams P, const BrokerRec* __restrict__ br,
+                                                      const uint8_t* __restrict__ allowedAlive,
+                                                      const TopicPartial* __restrict__ topics,
+                                                      StatsPartial* __restrict__ part) {
+  double d[kStatD];
+  int32_t iv[kStatI];
+#pragma unroll
+  for (int k = 0; k < kStatD; ++k) d[k] = dInit(k);
+#pragma unroll
+  for (int k = 0; k < kStatI; ++k) iv[k] = iInit(k);
   const int na = P.numAllowed;
-  for (int res = 0; res < 4; ++res) {
-    double hot = 0.0, cold = 1.7976931348623157e308, varSum = 0.0;
-    int bal = 0;
-    for (int b = threadIdx.x; b < B; b += blockDim.x) {
-      if (!br[b].alive) continue;
-      const double u = br[b].util[res];
-      hot = u > hot ? u : hot;
-      cold = u < cold ? u : cold;
-      if (allowedAlive[b]) {
-        const double cap = br[b].cap[res];
+  const double repAvg = (double)P.repTotal / na, leadAvg = (double)P.leadTotal / na;
+  const double potPct = P.potSum / P.potCapacity;
+  const int stride = gridDim.x * kTB;
+  for (int b = blockIdx.x * kTB + threadIdx.x; b < P.B; b += stride) {
+    const BrokerRec x = br[b];
+    const bool allowed = allowedAlive[b] != 0;
+    // replica / leader counts: max/min over every broker, variance over alive allowed ones
+    iv[kSiRepMx] = max(iv[kSiRepMx], x.nrep);
+    iv[kSiRepMn] = min(iv[kSiRepMn], x.nrep);
+    iv[kSiLeadMx] = max(iv[kSiLeadMx], x.nlead);
+    iv[kSiLeadMn] = min(iv[kSiLeadMn], x.nlead);
+    if (!x.alive) continue;
+#pragma unroll
+    for (int res = 0; res < 4; ++res) {
+      const double u = x.util[res];
+      d[res] = u > d[res] ? u : d[res];
+      d[4 + res] = u < d[4 + res] ? u : d[4 + res];
+      if (allowed) {
+        const double cap = x.cap[res];
         const double pct = u / cap;
-        if (pct >= P.lowerThr[res] && pct <= P.upperThr[res]) bal++;
-        const double d = u - P.avgPct[res] * cap;
-        varSum += d * d;
+        if (pct >= P.lowerThr[res] && pct <= P.upperThr[res]) iv[res]++;
+        const double dv = u - P.avgPct[res] * cap;
+        d[8 + res] += dv * dv;
       }
     }
-    hot = blockReduce(hot, OpMax(), sd);
-    cold = blockReduce(cold, OpMin(), sd);
-    varSum = blockReduce(varSum, OpAdd(), sd);
-    bal = blockReduce(bal, OpAdd(), si);
-    if (threadIdx.x == 0) {
-      out->numBalanced[res] = bal;
-      out->resAvg[res] = P.clusterUtil[res] / na;
-      out->resMax[res] = hot;
-      out->resMin[res] = cold;
-      out->resStd[res] = sqrt(varSum / na);
+    const double u = x.pot;
+    d[kSdPHot] = u > d[kSdPHot] ? u : d[kSdPHot];
+    d[kSdPCold] = u < d[kSdPCold] ? u : d[kSdPCold];
+    if (allowed) {
+      const double cap = x.cap[2];
+      if (u / cap <= P.nwOutCapThreshold) iv[kSiUnder]++;
+      const double dv = u - potPct * cap;
+      d[kSdPVar] += dv * dv;
+      const double dr = (double)x.nrep - repAvg, dl = (double)x.nlead - leadAvg;
+      d[kSdRepVar] += (dr * dr) / na;
+      d[kSdLeadVar] += (dl * dl) / na;
     }
   }
-  // potential NW_OUT
-  {
-    double s = 0.0;
-    for (int b = threadIdx.x; b < B; b += blockDim.x)
-      if (br[b].alive && allowedAlive[b]) s += br[b].pot;
-    s = blockReduce(s, OpAdd(), sd);
-    const double avgPct = s / P.potCapacity;
-    double hot = 0.0, cold = 1.7976931348623157e308, varSum = 0.0;
-    int under = 0;
-    for (int b = threadIdx.x; b < B; b += blockDim.x) {
-      if (!br[b].alive) continue;
-      const double u = br[b].pot;
-      const double cap = br[b].cap[2];
-      hot = u > hot ? u : hot;
-      cold = u < cold ? u : cold;
-      if (allowedAlive[b]) {
-        if (u / cap <= P.nwOutCapThreshold) under++;
-        const double d = u - avgPct * cap;
-        varSum += d * d;
-      }
-    }
-    hot = blockReduce(hot, OpMax(), sd);
-    cold = blockReduce(cold, OpMin(), sd);
-    varSum = blockReduce(varSum, OpAdd(), sd);
-    under = blockReduce(under, OpAdd(), si);
-    if (threadIdx.x == 0) {
-      out->pnwAvg = s / na;
-      out->pnwMax = hot;
-      out->pnwMin = cold;
-      out->pnwStd = sqrt(varSum / na);
-      out->numUnderPot = under;
-    }
+  for (int t = blockIdx.x * kTB + threadIdx.x; t < P.T; t += stride) {
+    const TopicPartial x = topics[t];
+    d[kSdTAvg] += x.avg;
+    d[kSdTSd] += x.sd;
+    iv[kSiTMx] = max(iv[kSiTMx], x.mx);
+    iv[kSiTMn] = min(iv[kSiTMn], x.mn);
   }
-  // replica and leader counts (populateReplicaStats: totals/max/min over all brokers, variance over allowed)
-  for (int which = 0; which < 2; ++which) {
-    int total = 0, mx = 0, mn = 0x7fffffff;
-    for (int b = threadIdx.x; b < B; b += blockDim.x) {
-      const int n = which == 0 ? br[b].nrep : br[b].nlead;
-      total += n;
-      mx = n > mx ? n : mx;
-      mn = n < mn ? n : mn;
-    }
-    total = blockReduce(total, OpAdd(), si);
-    mx = blockReduce(mx, OpMax(), si);
-    mn = blockReduce(mn, OpMin(), si);
-    const double avg = ((double)total) / na;
-    double var = 0.0;
-    for (int b = threadIdx.x; b < B; b += blockDim.x)
-      if (br[b].alive && allowedAlive[b]) {
-        const double d = (double)(which == 0 ? br[b].nrep : br[b].nlead) - avg;
-        var += (d * d) / na;
-      }
-    var = blockReduce(var, OpAdd(), sd);
-    if (threadIdx.x == 0) {
-      if (which == 0) {
-        out->repAvg = avg;
-        out->repStd = sqrt(var);
-        out->repMax = mx;
-        out->repMin = mn;
-      } else {
-        out->leadAvg = avg;
-        out->leadStd = sqrt(var);
-        out->leadMax = mx;
-        out->leadMin = mn;
-      }
-    }
+  waveFoldD(d);
+  waveFoldI(iv);
+  __shared__ double sd[kTB / 64][kStatD];
+  __shared__ int32_t si[kTB / 64][kStatI];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  if (lane == 0) {
+#pragma unroll
+    for (int k = 0; k < kStatD; ++k) sd[wave][k] = d[k];
+#pragma unroll
+    for (int k = 0; k < kStatI; ++k) si[wave][k] = iv[k];
   }
-  // topic records
-  {
-    double avgSum = 0.0, sdSum = 0.0;
-    int mx = 0, mn = 0x7fffffff;
-    for (int t = threadIdx.x; t < P.T; t += blockDim.x) {
-      const TopicPartial x = topics[t];
-      avgSum += x.avg;
-      sdSum += x.sd;
-      mx = x.mx > mx ? x.mx : mx;
-      mn = x.mn < mn ? x.mn : mn;
-    }
-    avgSum = blockReduce(avgSum, OpAdd(), sd);
-    sdSum = blockReduce(sdSum, OpAdd(), sd);
-    mx = blockReduce(mx, OpMax(), si);
-    mn = blockReduce(mn, OpMin(), si);
-    if (threadIdx.x == 0) {
-      out->topicAvg = avgSum / P.T;
-      out->topicStd = sdSum / P.T;
-      out->topicMax = mx;
-      out->topicMin = mn;
-    }
+  __syncthreads();
+  if (threadIdx.x < kStatD) {
+    const int k = threadIdx.x;
+    double r = sd[0][k];
+    for (int w = 1; w < kTB / 64; ++w) r = dOp(k, r, sd[w][k]);
+    part[blockIdx.x].d[k] = r;
+  } else if (threadIdx.x >= 64 && threadIdx.x < 64 + kStatI) {
+    const int k = threadIdx.x - 64;
+    int32_t r = si[0][k];
+    for (int w = 1; w < kTB / 64; ++w) r = iOp(k, r, si[w][k]);
+    part[blockIdx.x].i[k] = r;
   }
 }
 
+// one wave; lane g folds partial g (G <= 64)
+__global__ __launch_bounds__(64) void stats_combine(StatsParams P, const StatsPartial* __restrict__ part, int G,
+                                                    StatsOut* __restrict__ out) {
+  double d[kStatD];
+  int32_t iv[kStatI];
+  const int g = threadIdx.x;
+#pragma unroll
+  for (int k = 0; k < kStatD; ++k) d[k] = g < G ? part[g].d[k] : dInit(k);
+#pragma unroll
+  for (int k = 0; k < kStatI; ++k) iv[k] = g < G ? part[g].i[k] : iInit(k);
+  waveFoldD(d);
+  waveFoldI(iv);
+  if (threadIdx.x != 0) return;
+  const int na = P.numAllowed;
+  for (int res = 0; res < 4; ++res) {
+    out->numBalanced[res] = iv[res];
+    out->resAvg[res] = P.clusterUtil[res] / na;
+    out->resMax[res] = d[res];
+    out->resMin[res] = d[4 + res];
+    out->resStd[res] = sqrt(d[8 + res] / na);
+  }
+  out->pnwAvg = P.potSum / na;
+  out->pnwMax = d[kSdPHot];
+  out->pnwMin = d[kSdPCold];
+  out->pnwStd = sqrt(d[kSdPVar] / na);
+  out->numUnderPot = iv[kSiUnder];
+  out->repAvg = (double)P.repTotal / na;
+  out->repStd = sqrt(d[kSdRepVar]);
+  out->repMax = iv[kSiRepMx];
+  out->repMin = iv[kSiRepMn];
+  out->leadAvg = (double)P.leadTotal / na;
+  out->leadStd = sqrt(d[kSdLeadVar]);
+  out->leadMax = iv[kSiLeadMx];
+  out->leadMin = iv[kSiLeadMn];
+  out->topicAvg = d[kSdTAvg] / P.T;
+  out->topicStd = d[kSdTSd] / P.T;
+  out->topicMax = iv[kSiTMx];
+  out->topicMin = iv[kSiTMn];
+}
+
 hipError_t launchStats(const StatsParams& P, const int32_t* tc, const int32_t* topicNrep, const BrokerRec* brokers,
-                       const uint8_t* allowedAlive, TopicPartial* scratch, StatsOut* out, int ldB, hipStream_t st,
+                       const uint8_t* allowedAlive, TopicPartial* scratch, void* partials, StatsOut* out, int ldB,
+                       hipStream_t st,
                        hipEvent_t evTopic0, hipEvent_t evTopic1) {
   int blocks = P.T < 8192 ? P.T : 8192;
   if (blocks < 1) blocks = 1;
@@ -217,7 +253,12 @@ hipError_t launchStats(const StatsParams& P, const int32_t* tc, const int32_t* t
   hipLaunchKernelGGL(stats_topics, dim3(blocks), dim3(kTB), 0, st, tc, topicNrep, allowedAlive, P.B, ldB, P.T,
                      P.numAllowed, scratch);
   if (evTopic1) (void)hipEventRecord(evTopic1, st);
-  hipLaunchKernelGGL(stats_final, dim3(1), dim3(1024), 0, st, P, brokers, allowedAlive, scratch, out);
+  const int work = (P.B > P.T ? P.B : P.T);
+  int G = (work + kTB - 1) / kTB;
+  G = G < 1 ? 1 : (G > kStatsPartBlocks ? kStatsPartBlocks : G);
+  StatsPartial* part = reinterpret_cast<StatsPartial*>(partials);
+  hipLaunchKernelGGL(stats_partials, dim3(G), dim3(kTB), 0, st, P, brokers, allowedAlive, scratch, part);
+  hipLaunchKernelGGL(stats_combine, dim3(1), dim3(64), 0, st, P, part, G, out);
   return hipGetLastError();
 }
 

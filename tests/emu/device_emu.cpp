@@ -470,9 +470,7 @@ void Device::stats(const StatsParams& P, const uint8_t* aa, StatsOut* out) {
     out->resStd[res] = std::sqrt(var / na);
   }
   {
-    double s = 0;
-    for (int b = 0; b < B; ++b)
-      if (e.bAlive[b] && aa[b]) s += e.bPot[b];
+    const double s = P.potSum;
     const double avgPct = s / P.potCapacity;
     double hot = 0, cold = 1.7976931348623157e308, var = 0;
     int under = 0;
@@ -495,9 +493,9 @@ void Device::stats(const StatsParams& P, const uint8_t* aa, StatsOut* out) {
   }
   for (int which = 0; which < 2; ++which) {
     const std::vector<int32_t>& cnt = which == 0 ? e.bNrep : e.bNlead;
-    int total = 0, mx = 0, mn = 0x7fffffff;
+    const int64_t total = which == 0 ? P.repTotal : P.leadTotal;
+    int mx = 0, mn = 0x7fffffff;
     for (int b = 0; b < B; ++b) {
-      total += cnt[b];
       mx = cnt[b] > mx ? cnt[b] : mx;
       mn = cnt[b] < mn ? cnt[b] : mn;
     }
