@@ -253,6 +253,20 @@ def pmc_traffic(workload: str, kernels=SCAN_KERNELS):
     return (b / n if n else None), os.path.relpath(paths[-1], REPO)
 
 
+def scan_cross_line(perf, workload: str):
+    """scan_cross alone: its algorithmic bytes per launch (required candidates x BYTES_PER_CANDIDATE) next to its
+    calibrated HBM counter bytes per launch from the committed PMC summary (tools/pmc_calib: FETCH_SIZE x2 holds for
+    its 128-B record gathers, profiles/r02/calib_summary.json)."""
+    n = max(1, perf.cross_launches)
+    alg = perf.cross_required * BYTES_PER_CANDIDATE / n
+    traffic, src = pmc_traffic(workload, ("scan_cross",))
+    avg_us = perf.cross_kernel_ms * 1e3 / n
+    return {"launches_per_step": perf.cross_launches, "avg_launch_us": avg_us,
+            "algorithmic_bytes_per_launch": alg, "achieved_gbs": alg / (avg_us * 1e-6) / 1e9 if avg_us > 0 else 0.0,
+            "traffic_bytes_per_launch": traffic, "traffic_over_algorithmic": traffic / alg if traffic and alg else None,
+            "traffic_source": src}
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -407,7 +421,8 @@ def main() -> None:
                      "reference_equivalent_candidates_per_step": inst_cands,
                      "stats_avg_launch_us": perf.stats_kernel_ms * 1e3 / max(1, perf.stats_launches),
                      "stats_bytes_per_launch": perf.stats_bytes / max(1, perf.stats_launches),
-                     "host_syncs_per_step": perf.host_syncs},
+                     "host_syncs_per_step": perf.host_syncs,
+                     "scan_cross": scan_cross_line(perf, args.workload)},
         "cpu_baseline": None,
     }
     if world == 1 and not args.no_cpu_baseline:

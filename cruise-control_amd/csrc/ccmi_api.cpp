@@ -582,6 +582,9 @@ ccmi_status ccmi_perf(const ccmi_session* s, ccmi_perf_counters* out) {
     out->intra_launches = p.intraLaunches;
     out->intra_kernel_ms = p.intraKernelMs;
     out->intra_bytes = p.intraBytes;
+    out->cross_launches = p.crossLaunches;
+    out->cross_required = p.crossRequired;
+    out->cross_kernel_ms = p.crossKernelMs;
     return CCMI_OK;
   });
 }

@@ -468,9 +468,14 @@ int64_t Device::scanCross(const DevProgram& prog, const int32_t* reps, int K, co
   perf.scanLaunches++;
   perf.scanPairs += (int64_t)K * Nr;
   perf.scanBytes += (int64_t)K * Nr * kBytesPerCandidate;
+  const double ms0 = perf.scanKernelMs;
   const int64_t key = finishScan();
   // candidates this launch had to evaluate: every row before the winner's and the winner's row up to the winner
-  perf.scanRequired += key < 0 ? (int64_t)K * Nr : (key / N) * Nr + (key % N - c0) + 1;
+  const int64_t required = key < 0 ? (int64_t)K * Nr : (key / N) * Nr + (key % N - c0) + 1;
+  perf.scanRequired += required;
+  perf.crossLaunches++;
+  perf.crossRequired += required;
+  perf.crossKernelMs += perf.scanKernelMs - ms0;
   return key;
 }
 

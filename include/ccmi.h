@@ -378,6 +378,9 @@ typedef struct ccmi_perf_counters {
   int64_t intra_launches;      /* K6 intra-broker launches (one per intra-broker goal, plus overflow re-runs) */
   double intra_kernel_ms;      /* HIP-event duration of the K6 launches */
   int64_t intra_bytes;         /* algorithmic bytes of K6 */
+  int64_t cross_launches;      /* the scan_cross share of scan_launches / scan_required / scan_kernel_ms (the kernel */
+  int64_t cross_required;      /* tools/pmc_summary.py prices against its own FETCH_SIZE / WRITE_SIZE counters) */
+  double cross_kernel_ms;
 } ccmi_perf_counters;
 ccmi_status ccmi_perf(const ccmi_session* s, ccmi_perf_counters* out);
 void ccmi_perf_reset(ccmi_session* s);
