@@ -47,6 +47,7 @@ GOAL_KINDS: Dict[str, int] = {
     "IntraBrokerDiskCapacityGoal": 16,
     "IntraBrokerDiskUsageDistributionGoal": 17,
     "PreferredLeaderElectionGoal": 18,
+    "RackAwareDistributionGoal": 19,
 }
 GOAL_NAMES = {v: k for k, v in GOAL_KINDS.items()}
 # default.goals in priority order (config/constants/AnalyzerConfig.java:352-367, TestConstants.DEFAULT_GOALS_VALUES)
@@ -62,7 +63,7 @@ C1_GOALS = ("ReplicaDistributionGoal", "DiskUsageDistributionGoal", "NetworkInbo
 # intra.broker.goals (AnalyzerConfig INTRA_BROKER_GOALS default, IntraBrokerRebalanceTest.java:105-106)
 INTRA_BROKER_GOALS = ("IntraBrokerDiskCapacityGoal", "IntraBrokerDiskUsageDistributionGoal")
 # Goals whose drivers are implemented in this build.
-IMPLEMENTED = DEFAULT_GOALS + INTRA_BROKER_GOALS + ("PreferredLeaderElectionGoal",)
+IMPLEMENTED = DEFAULT_GOALS + INTRA_BROKER_GOALS + ("PreferredLeaderElectionGoal", "RackAwareDistributionGoal")
 
 ACTION_TYPES = ("INTER_BROKER_REPLICA_MOVEMENT", "LEADERSHIP_MOVEMENT", "INTER_BROKER_REPLICA_SWAP",
                 "INTRA_BROKER_REPLICA_MOVEMENT", "INTRA_BROKER_REPLICA_SWAP")

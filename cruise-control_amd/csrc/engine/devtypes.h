@@ -40,7 +40,8 @@ enum DevGoalKind : int32_t {
   DG_POTENTIAL_NW_OUT = 6,
   DG_TOPIC_REPLICA_DISTRIBUTION = 7,
   DG_LEADER_REPLICA_DISTRIBUTION = 8,
-  DG_LEADER_BYTES_IN = 9
+  DG_LEADER_BYTES_IN = 9,
+  DG_RACK_AWARE_DISTRIBUTION = 10
 };
 // Operands a program's predicates read beyond the base broker/replica/partition record (DevProgram.needs).
 enum DevNeed : uint32_t { NEED_RACK = 1, NEED_POT = 2, NEED_LEAD = 4, NEED_LBI = 8, NEED_TOPIC = 16 };

@@ -62,6 +62,12 @@ struct HostView {
       if (pbroker(i) != self && m.bRack[pbroker(i)] == rk) return true;
     return false;
   }
+  int slotRack(int, int b) const { return m.bRack[b]; }
+  int rackCount(int p, int rk) const {
+    int c = 0;
+    for (int i = pbegin(p); i < pend(p); ++i) c += m.bRack[pbroker(i)] == rk ? 1 : 0;
+    return c;
+  }
   int nlead(int b) const { return m.bNlead[b]; }
   double pot(int b) const { return m.potNwOut(b); }
   double lnwin(int b) const { return m.leadNwIn(b); }
@@ -74,7 +80,8 @@ struct HostView {
 
 uint32_t needsOf(const DevGoal& g) {
   switch (g.kind) {
-    case DG_RACK_AWARE: return NEED_RACK;
+    case DG_RACK_AWARE:
+    case DG_RACK_AWARE_DISTRIBUTION: return NEED_RACK;
     case DG_POTENTIAL_NW_OUT: return NEED_POT;
     case DG_TOPIC_REPLICA_DISTRIBUTION: return NEED_TOPIC;
     case DG_LEADER_REPLICA_DISTRIBUTION: return NEED_LEAD;
@@ -322,7 +329,11 @@ int Engine::acceptance(int gi, const ccmi_action& a) {
   const int action = a.type == CCMI_LEADERSHIP_MOVEMENT ? DA_LEADERSHIP : DA_MOVE;
   if (a.type != CCMI_INTER_BROKER_REPLICA_MOVEMENT && a.type != CCMI_LEADERSHIP_MOVEMENT)
     throw std::invalid_argument("Unsupported balancing action");
-  return goalAcceptMove(g.dg, v, action, sr, a.source_broker, a.destination_broker) ? CCMI_ACCEPT : CCMI_REPLICA_REJECT;
+  if (goalAcceptMove(g.dg, v, action, sr, a.source_broker, a.destination_broker)) return CCMI_ACCEPT;
+  // AbstractRackAwareGoal.actionAcceptance rejects a replica move with BROKER_REJECT (AbstractRackAwareGoal.java:
+  // 100-106); every other goal's rejected move or leadership move is a REPLICA_REJECT
+  const bool rack = g.dg.kind == DG_RACK_AWARE || g.dg.kind == DG_RACK_AWARE_DISTRIBUTION;
+  return rack && action == DA_MOVE ? CCMI_BROKER_REJECT : CCMI_REPLICA_REJECT;
 }
 
 ccmi_cluster_stats Engine::stats() {

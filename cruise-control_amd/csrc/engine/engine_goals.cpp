@@ -271,6 +271,170 @@ class RackAware : public GoalImpl {
   int compareStats(const ccmi_cluster_stats&, const ccmi_cluster_stats&) const override { return 0; }
 };
 
+struct PartitionOrder {  // TopicPartition in a HashMap bin: (topic, partition)
+  const Model* m;
+  int cmp(int a, int b) const {
+    const int c = m->topicNames[m->pTopic[a]].compare(m->topicNames[m->pTopic[b]]);
+    return c ? c : jcmpInt(m->pNumber[a], m->pNumber[b]);
+  }
+};
+
+// ======================================================================================= RackAwareDistributionGoal
+// RackAwareDistributionGoal.java:139-383 + AbstractRackAwareGoal.rebalanceForBroker (:144-170) with
+// throwExceptionIfCannotMove = false: replicas of a partition spread as evenly as possible over the alive racks
+// allowed replica moves (BalanceLimit :403-448: base = rf / racks, rf % racks racks hold one more). Each replica that
+// must move gets its own candidate list — the TreeSet of eligible brokers by (partition replicas on the broker's rack
+// after removing this one, broker id) — and one device scan over it.
+class RackAwareDist : public GoalImpl {
+ public:
+  RackAwareDist() {
+    kind = CCMI_GOAL_RACK_AWARE_DISTRIBUTION;
+    name = "RackAwareDistributionGoal";
+  }
+  std::vector<int32_t> alive;
+  int numRacks = 0;  // BalanceLimit._numAliveRacksAllowedReplicaMoves
+
+  // initGoalState (:139-164)
+  void init(Engine& e) override {
+    Model& m = e.m;
+    if (allowedForReplicaMove(e, allowed) == 0) {
+      ccmi_provision_recommendation rec = provisionRec();
+      rec.num_brokers = m.maxRf;
+      throw OptimizationFailure("[" + name + "] All alive brokers are excluded from replica moves.", rec);
+    }
+    std::set<int> racks;  // ClusterModel.aliveRacksAllowedReplicaMoves (ClusterModel.java:658-662)
+    for (int b = 0; b < m.B; ++b)
+      if (allowed[b]) racks.insert(m.bRack[b]);
+    numRacks = (int)racks.size();
+    const int numExtraRacks = numRacks - m.maxRf;
+    if (numExtraRacks >= e.bc.overprovisionedMinExtraRacks) {
+      ccmi_provision_recommendation rec = provisionRec(CCMI_PROVISION_OVER_PROVISIONED);
+      rec.num_racks = numExtraRacks - e.bc.overprovisionedMinExtraRacks + 1;
+      prov = provisionResponse(CCMI_PROVISION_OVER_PROVISIONED, rec);
+    }
+    Model::Spec s;
+    s.selImmigrants = e.opt.onlyImmigrants;
+    s.selExclTopics = e.opt.anyExclTopic;
+    for (int b = 0; b < m.B; ++b) m.track(b, sortId(kind, false, false), s);
+    alive = aliveById(m);
+    dg = DevGoal{};
+    dg.kind = DG_RACK_AWARE_DISTRIBUTION;
+    dg.allowedSlot = (int)e.optimized.size();
+  }
+
+  // numPartitionReplicasByRackId (:113-119) as (rack, count) pairs
+  static int rackCounts(const Model& m, int p, int* rk, int* cnt) {
+    int n = 0;
+    for (int i = m.pOff[p]; i < m.pOff[p + 1]; ++i) {
+      const int x = m.bRack[m.rBroker[m.pSlots[i]]];
+      int k = 0;
+      while (k < n && rk[k] != x) ++k;
+      if (k == n) {
+        rk[n] = x;
+        cnt[n++] = 0;
+      }
+      cnt[k]++;
+    }
+    return n;
+  }
+
+  // shouldKeepInTheCurrentBroker (:305-334)
+  bool keep(const Model& m, int r) const {
+    const int b = m.rBroker[r], p = m.rPart[r];
+    if (!allowed[b]) return false;
+    const int rf = m.pOff[p + 1] - m.pOff[p];
+    int rk[kMaxRf], cnt[kMaxRf];
+    const int n = rackCounts(m, p, rk, cnt);
+    const int base = rf / numRacks, extra = rf % numRacks, upper = base + (extra == 0 ? 0 : 1);
+    int mine = 0;
+    for (int k = 0; k < n; ++k)
+      if (rk[k] == m.bRack[b]) mine = cnt[k];
+    if (mine <= base) return true;
+    if (mine > upper) return false;
+    int over = 0;
+    for (int k = 0; k < n; ++k) over += cnt[k] > base ? 1 : 0;
+    return over <= extra;
+  }
+
+  // rackAwareEligibleBrokers (:246-302): the TreeSet order (count of the broker's rack, id)
+  void eligibleFor(const Model& m, int r, std::vector<int32_t>& out) const {
+    const int p = m.rPart[r];
+    const int rf = m.pOff[p + 1] - m.pOff[p];
+    int rk[kMaxRf], cnt[kMaxRf];
+    const int n = rackCounts(m, p, rk, cnt);
+    for (int k = 0; k < n; ++k)
+      if (rk[k] == m.bRack[m.rBroker[r]]) cnt[k]--;
+    const int base = rf / numRacks;
+    int over = 0;
+    for (int k = 0; k < n; ++k) over += cnt[k] > base ? 1 : 0;
+    const bool canMoveToBase = over < rf % numRacks;
+    auto countOf = [&](int b) {
+      for (int k = 0; k < n; ++k)
+        if (rk[k] == m.bRack[b]) return cnt[k];
+      return 0;
+    };
+    out.clear();
+    for (int b : alive) {
+      const int c = countOf(b);
+      if (!(c < base || (canMoveToBase && c == base))) continue;
+      bool hosts = false;
+      for (int i = m.pOff[p]; i < m.pOff[p + 1]; ++i) hosts |= m.rBroker[m.pSlots[i]] == b;
+      if (!hosts) out.push_back(b);
+    }
+    std::sort(out.begin(), out.end(), [&](int a, int b) {
+      const int ca = countOf(a), cb = countOf(b);
+      return ca != cb ? ca < cb : m.bId[a] < m.bId[b];
+    });
+  }
+
+  void rebalance(Engine& e, int b) override {
+    PhaseScope ps(PH_OTHER_GOALS);
+    Model& m = e.m;
+    const std::vector<int32_t> list = m.sorted(b, sortId(kind, false, false));
+    std::vector<int32_t> one(1), tree, cands;
+    for (int r : list) {
+      if (m.alive(b) && !m.curOffline(r) && keep(m, r)) continue;
+      eligibleFor(m, r, tree);
+      e.eligible(tree, DA_MOVE, cands);
+      one[0] = r;
+      const int64_t key = e.crossScan(*this, DA_MOVE, one, 0, cands);
+      if (key >= 0) m.relocateReplica(m.rPart[r], b, cands[key]);  // else: logged and skipped (:166)
+    }
+  }
+
+  // updateGoalState (:175-188) + ensureRackAwareDistribution (:342-383) over clusterModel.leaderReplicas() (a
+  // HashSet<Replica> of the partitions' leaders, filled in the model's partition-map order)
+  void update(Engine& e) override {
+    Model& m = e.m;
+    ensureNoOfflineReplicas(m, name);
+    PartitionOrder po{&m};
+    JHashSet<PartitionOrder> parts(&po);
+    for (int p = 0; p < m.P; ++p) parts.add(p, jMix(jMix(1, m.pNumber[p]), m.topicHash[m.pTopic[p]]));
+    std::vector<int32_t> order, leaders;
+    parts.order(order);
+    ReplicaSet ls(&m.replicaOrder);
+    for (int p : order) ls.add(m.pLeader[p], m.replicaHash(m.pLeader[p]));
+    ls.order(leaders);
+    for (int l : leaders) {
+      const int p = m.rPart[l];
+      if (e.opt.anyExclTopic && e.opt.exclTopic[m.pTopic[p]]) continue;
+      int rk[kMaxRf], cnt[kMaxRf];
+      const int n = rackCounts(m, p, rk, cnt);
+      int mx = 0, mn = 1 << 30;
+      for (int k = 0; k < n; ++k) {
+        mx = std::max(mx, cnt[k]);
+        mn = std::min(mn, cnt[k]);
+      }
+      if (mx > 1 && (n < numRacks || mx - mn > 1))
+        throw OptimizationFailure("[" + name + "] Partition " + std::to_string(p) + " is not rack-aware.",
+                                  underBrokers(1));  // .excludedRackIds(...) is not carried by the ABI
+    }
+    if (prov.status != CCMI_PROVISION_OVER_PROVISIONED) prov = provisionResponse(CCMI_PROVISION_RIGHT_SIZED);
+    finished = true;
+  }
+  int compareStats(const ccmi_cluster_stats&, const ccmi_cluster_stats&) const override { return 0; }
+};
+
 // ======================================================================================= MinTopicLeadersPerBrokerGoal
 // With the default topics.with.min.leaders.per.broker (no topic matches) the goal accepts every action and only
 // moves offline replicas away (moveAwayOfflineReplicas).
@@ -1376,13 +1540,6 @@ class LeaderBytesIn : public GoalImpl {
 // partition's leadership goes to its first alive, online replica (with demoted brokers: only the partitions they led,
 // after their replicas moved to the end of the replica lists), so it runs on the host model and the device only sees
 // the touched rows. Demoted disks are not in the flattened model.
-struct PartitionOrder {  // TopicPartition in a HashMap bin: (topic, partition)
-  const Model* m;
-  int cmp(int a, int b) const {
-    const int c = m->topicNames[m->pTopic[a]].compare(m->topicNames[m->pTopic[b]]);
-    return c ? c : jcmpInt(m->pNumber[a], m->pNumber[b]);
-  }
-};
 
 class PreferredLeaderElection : public GoalImpl {
  public:
@@ -1467,6 +1624,7 @@ std::unique_ptr<GoalImpl> makeMoreGoal(int kind) {
     case CCMI_GOAL_LEADER_REPLICA_DISTRIBUTION: return std::make_unique<LeaderReplicaDistribution>();
     case CCMI_GOAL_LEADER_BYTES_IN_DISTRIBUTION: return std::make_unique<LeaderBytesIn>();
     case CCMI_GOAL_PREFERRED_LEADER_ELECTION: return std::make_unique<PreferredLeaderElection>();
+    case CCMI_GOAL_RACK_AWARE_DISTRIBUTION: return std::make_unique<RackAwareDist>();
     default: throw Unsupported("goal kind " + std::to_string(kind) + " is not implemented in this build");
   }
 }

@@ -34,7 +34,8 @@
 namespace ccmi {
 
 // V must provide: bu(b,res) bcap(b,res) nrep(b) alive(b) allowed(slot,b) ru(r,res) flags(r) rbroker(r)
-// rorig(r) origOff(r) rpart(r) hosts(p,b), and for the goals that read them: rack(b) otherOnRack(p,self,rack) nlead(b)
+// rorig(r) origOff(r) rpart(r) hosts(p,b), and for the goals that read them: rack(b) otherOnRack(p,self,rack)
+// slotRack(p,b) (rack of partition p's replica on b) rackCount(p,rack) nlead(b)
 // pot(b) lnwin(b) pLeadNwOut(p) ptopic(p) tcount(t,b) tUpper(t) tLower(t).
 // Replica.isCurrentOffline; V::origOff(r) = isOriginalOffline || original broker dead
 template <class V>
@@ -139,6 +140,17 @@ CCMI_HD bool rackViolates(const V& v, int r, int dst) {
   return v.otherOnRack(v.rpart(r), v.rbroker(r), v.rack(dst));
 }
 
+// ---------------------------------------------------------------- RackAwareDistributionGoal
+// doesReplicaMoveViolateActionAcceptance (RackAwareDistributionGoal.java:88-104): a move to another rack may not
+// leave the destination rack with at least as many of the partition's replicas as the source rack had
+template <class V>
+CCMI_HD bool rackDistViolates(const V& v, int r, int dst) {
+  const int p = v.rpart(r);
+  const int srk = v.slotRack(p, v.rbroker(r)), drk = v.rack(dst);
+  if (srk == drk) return false;
+  return v.rackCount(p, drk) >= v.rackCount(p, srk);
+}
+
 // ---------------------------------------------------------------- CapacityGoal
 // isUtilizationUnderLimitAfterAddingLoad (host == broker: the host check is the broker check negated)
 template <class V>
@@ -212,6 +224,7 @@ CCMI_HD bool goalAcceptMove(const DevGoal& g, const V& v, int action, int r, int
     case DG_REPLICA_DISTRIBUTION: return rdAccept(g, v, action, src, dst);
     case DG_RESOURCE_DISTRIBUTION: return resAcceptMove(g, v, action, r, src, dst);
     case DG_RACK_AWARE: return action == DA_LEADERSHIP || !rackViolates(v, r, dst);
+    case DG_RACK_AWARE_DISTRIBUTION: return action == DA_LEADERSHIP || !rackDistViolates(v, r, dst);
     case DG_REPLICA_CAPACITY: return action == DA_LEADERSHIP || (int64_t)v.nrep(dst) < g.maxReplicas;
     case DG_CAPACITY:
       if (action == DA_LEADERSHIP && (g.resource == 3 /*DISK*/ || g.resource == 1 /*NW_IN*/)) return true;
@@ -230,7 +243,8 @@ CCMI_HD bool goalSelfSatisfiedMove(const DevGoal& g, const V& v, int action, int
       if (g.fixOffline && currentOffline(v, r)) return true;
       return rdAccept(g, v, action, src, dst);
     case DG_RESOURCE_DISTRIBUTION: break;
-    case DG_RACK_AWARE: return true;
+    case DG_RACK_AWARE:
+    case DG_RACK_AWARE_DISTRIBUTION: return true;
     case DG_ACCEPT_ALL: return action == DA_MOVE;  // MinTopicLeadersPerBrokerGoal moves offline replicas only
     case DG_REPLICA_CAPACITY: return (int64_t)v.nrep(dst) < g.maxReplicas;
     case DG_CAPACITY: return capUnderAfterAdding(g, v, dst, v.ru(r, g.resource));
@@ -256,6 +270,9 @@ CCMI_HD int goalAcceptSwap(const DevGoal& g, const V& v, int sr, int sb, int dr,
     case DG_RACK_AWARE:
       if (rackViolates(v, sr, db)) return 2;
       return rackViolates(v, dr, sb) ? 1 : 0;
+    case DG_RACK_AWARE_DISTRIBUTION:
+      if (rackDistViolates(v, sr, db)) return 2;
+      return rackDistViolates(v, dr, sb) ? 1 : 0;
     case DG_CAPACITY: {
       const double su = v.ru(sr, g.resource), du = v.ru(dr, g.resource);
       const double delta = du - su;

@@ -63,6 +63,13 @@ struct DevView {
     for (int i = 0; i < x.n; ++i) any |= (x.brokers[i] != self) && (x.racks[i] == rk);
     return any;
   }
+  __device__ __forceinline__ int slotRack(int /*p*/, int b) const { return t.brokers[b].rack; }
+  __device__ __forceinline__ int rackCount(int p, int rk) const {
+    const PartitionRec& x = t.parts[p];
+    int c = 0;
+    for (int i = 0; i < x.n; ++i) c += x.racks[i] == rk ? 1 : 0;
+    return c;
+  }
   __device__ __forceinline__ int nlead(int b) const { return t.brokers[b].nlead; }
   __device__ __forceinline__ double pot(int b) const { return t.brokers[b].pot; }
   __device__ __forceinline__ double lnwin(int b) const { return t.brokers[b].lbi; }
@@ -376,6 +383,15 @@ struct PreView {
            (pb2 >= 0 && pb2 != self && prk2 == rk) | (pb3 >= 0 && pb3 != self && prk3 == rk) |
            (pb4 >= 0 && pb4 != self && prk4 == rk) | (pb5 >= 0 && pb5 != self && prk5 == rk) |
            (pb6 >= 0 && pb6 != self && prk6 == rk) | (pb7 >= 0 && pb7 != self && prk7 == rk);
+  }
+  // rack of the partition's slot on broker b (b hosts the partition: the replica's own broker)
+  __device__ __forceinline__ int slotRack(int /*p*/, int b) const {
+    return pb0 == b ? prk0 : pb1 == b ? prk1 : pb2 == b ? prk2 : pb3 == b ? prk3
+         : pb4 == b ? prk4 : pb5 == b ? prk5 : pb6 == b ? prk6 : prk7;
+  }
+  __device__ __forceinline__ int rackCount(int /*p*/, int rk) const {
+    return (pb0 >= 0 && prk0 == rk) + (pb1 >= 0 && prk1 == rk) + (pb2 >= 0 && prk2 == rk) + (pb3 >= 0 && prk3 == rk) +
+           (pb4 >= 0 && prk4 == rk) + (pb5 >= 0 && prk5 == rk) + (pb6 >= 0 && prk6 == rk) + (pb7 >= 0 && prk7 == rk);
   }
   __device__ __forceinline__ int nlead(int b) const { return b == dst ? dnlead : snlead; }
   __device__ __forceinline__ double pot(int b) const { return b == dst ? dpot : spot; }

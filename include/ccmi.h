@@ -104,7 +104,8 @@ typedef enum ccmi_goal_kind {
   CCMI_GOAL_LEADER_BYTES_IN_DISTRIBUTION = 15,     /* LeaderBytesInDistributionGoal */
   CCMI_GOAL_INTRA_BROKER_DISK_CAPACITY = 16,       /* IntraBrokerDiskCapacityGoal */
   CCMI_GOAL_INTRA_BROKER_DISK_USAGE_DISTRIBUTION = 17, /* IntraBrokerDiskUsageDistributionGoal */
-  CCMI_GOAL_PREFERRED_LEADER_ELECTION = 18          /* PreferredLeaderElectionGoal (not in default.goals) */
+  CCMI_GOAL_PREFERRED_LEADER_ELECTION = 18,         /* PreferredLeaderElectionGoal (not in default.goals) */
+  CCMI_GOAL_RACK_AWARE_DISTRIBUTION = 19            /* RackAwareDistributionGoal (not in default.goals) */
 } ccmi_goal_kind;
 
 /*

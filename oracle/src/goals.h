@@ -11,6 +11,7 @@
 // Wall-clock fast-mode timeouts are treated as infinite (parity mode).
 #pragma once
 #include <functional>
+#include <map>
 #include <set>
 #include <stdexcept>
 #include <string>
@@ -233,6 +234,32 @@ class RackAwareGoal : public AbstractGoal {
   bool violates(ClusterModel& cm, int replica, int destBroker) const;
   bool shouldKeepInTheCurrentBroker(ClusterModel& cm, int replica) const;
   std::vector<int> rackAwareEligibleBrokers(ClusterModel& cm, int replica) const;
+};
+
+//   RackAwareDistributionGoal              analyzer/goals/RackAwareDistributionGoal.java (not in default.goals)
+class RackAwareDistributionGoal : public AbstractGoal {
+ public:
+  using AbstractGoal::AbstractGoal;
+  std::string name() const override { return "RackAwareDistributionGoal"; }
+  bool isHardGoal() const override { return true; }
+  Acceptance actionAcceptance(const BalancingAction& a, ClusterModel& cm) override;
+  int compareStats(const ClusterModelStats&, const ClusterModelStats&) const override { return 0; }
+
+ protected:
+  void initGoalState(ClusterModel& cm, const OptimizationOptions& o) override;
+  void updateGoalState(ClusterModel& cm, const OptimizationOptions& o) override;
+  void rebalanceForBroker(int broker, ClusterModel& cm, const GoalList& g, const OptimizationOptions& o) override;
+  bool selfSatisfied(ClusterModel&, const BalancingAction&) override { return true; }
+
+ private:
+  std::map<int, int> numReplicasByRack(const ClusterModel& cm, int p) const;
+  bool violates(ClusterModel& cm, int replica, int destBroker) const;
+  bool shouldKeepInTheCurrentBroker(ClusterModel& cm, int replica) const;
+  std::vector<int> rackAwareEligibleBrokers(ClusterModel& cm, int replica) const;
+  int baseLimit(int rf) const { return rf / numRacks_; }
+  int numRacksWithOneMoreReplica(int rf) const { return rf % numRacks_; }
+  std::vector<char> allowed_;
+  int numRacks_ = 0;  // BalanceLimit._numAliveRacksAllowedReplicaMoves
 };
 
 class MinTopicLeadersPerBrokerGoal : public AbstractGoal {

@@ -163,6 +163,155 @@ void RackAwareGoal::rebalanceForBroker(int b, ClusterModel& cm, const GoalList& 
   }
 }
 
+// ===================================================================== RackAwareDistributionGoal
+// numPartitionReplicasByRackId (RackAwareDistributionGoal.java:113-119): Partition.partitionBrokers() by rack
+std::map<int, int> RackAwareDistributionGoal::numReplicasByRack(const ClusterModel& cm, int p) const {
+  std::map<int, int> out;
+  for (int b : cm.partitionBrokersSet(p)) out[cm.brokers[b].rack] += 1;
+  return out;
+}
+
+static int getOrZero(const std::map<int, int>& m, int k) {
+  auto it = m.find(k);
+  return it == m.end() ? 0 : it->second;
+}
+
+// doesReplicaMoveViolateActionAcceptance (:88-104)
+bool RackAwareDistributionGoal::violates(ClusterModel& cm, int r, int dst) const {
+  const int dstRack = cm.brokers[dst].rack, srcRack = cm.brokers[cm.replicas[r].broker].rack;
+  if (srcRack == dstRack) return false;
+  const std::map<int, int> n = numReplicasByRack(cm, cm.replicas[r].partition);
+  return getOrZero(n, dstRack) >= getOrZero(n, srcRack);
+}
+
+// AbstractRackAwareGoal.actionAcceptance (AbstractRackAwareGoal.java:96-118)
+Acceptance RackAwareDistributionGoal::actionAcceptance(const BalancingAction& a, ClusterModel& cm) {
+  switch (a.type) {
+    case ActionType::LEADERSHIP_MOVEMENT:
+      return Acceptance::ACCEPT;
+    case ActionType::INTER_BROKER_REPLICA_MOVEMENT:
+    case ActionType::INTER_BROKER_REPLICA_SWAP:
+      if (violates(cm, cm.replicaOnBroker(a.partition, a.sourceBroker), a.destinationBroker))
+        return Acceptance::BROKER_REJECT;
+      if (a.type == ActionType::INTER_BROKER_REPLICA_SWAP &&
+          violates(cm, cm.replicaOnBroker(a.destPartition, a.destinationBroker), a.sourceBroker))
+        return Acceptance::REPLICA_REJECT;
+      return Acceptance::ACCEPT;
+    default:
+      throw std::invalid_argument("Unsupported balancing action");
+  }
+}
+
+// initGoalState (:139-164) with BalanceLimit (:407-427)
+void RackAwareDistributionGoal::initGoalState(ClusterModel& cm, const OptimizationOptions& o) {
+  int n = 0;
+  allowed_ = allowedForReplicaMove(cm, o, &n);
+  if (n == 0) {
+    ProvisionRec rec;
+    rec.numBrokers = cm.maxReplicationFactor;
+    throw OptimizationFailure("[" + name() + "] All alive brokers are excluded from replica moves.", rec);
+  }
+  std::set<int> racks;  // ClusterModel.aliveRacksAllowedReplicaMoves (ClusterModel.java:658-662, Rack.java:146-153)
+  for (size_t b = 0; b < cm.brokers.size(); ++b)
+    if (allowed_[b]) racks.insert(cm.brokers[b].rack);
+  numRacks_ = (int)racks.size();
+  if (numRacks_ == 0) {
+    ProvisionRec rec;
+    rec.numRacks = cm.maxReplicationFactor;
+    throw OptimizationFailure("All alive racks are excluded from replica moves.", rec);
+  }
+  const int numExtraRacks = numRacks_ - cm.maxReplicationFactor;
+  if (numExtraRacks >= bc_.overprovisionedMinExtraRacks) {
+    ProvisionRec rec;
+    rec.status = PROV_OVER;
+    rec.numRacks = numExtraRacks - bc_.overprovisionedMinExtraRacks + 1;
+    provision_ = ProvisionResp{PROV_OVER, true, rec};
+  }
+  SortSpec spec;
+  if (o.onlyMoveImmigrantReplicas) spec.selection.push_back({SelFn::IMMIGRANTS});
+  if (!o.excludedTopics.empty()) spec.selection.push_back({SelFn::EXCLUDED_TOPICS});
+  for (size_t b = 0; b < cm.brokers.size(); ++b) cm.trackSortedReplicas((int)b, replicaSortName(false, false), spec);
+}
+
+// shouldKeepInTheCurrentBroker (:305-334)
+bool RackAwareDistributionGoal::shouldKeepInTheCurrentBroker(ClusterModel& cm, int r) const {
+  const int b = cm.replicas[r].broker;
+  if (!allowed_[b]) return false;
+  const int p = cm.replicas[r].partition;
+  const int rf = (int)cm.partitionBrokersSet(p).size();
+  const std::map<int, int> n = numReplicasByRack(cm, p);
+  const int base = baseLimit(rf), limit = numRacksWithOneMoreReplica(rf);
+  const int upper = base + (limit == 0 ? 0 : 1);
+  const int here = n.at(cm.brokers[b].rack);
+  if (here <= base) return true;
+  if (here > upper) return false;
+  int over = 0;
+  for (const auto& kv : n) over += kv.second > base ? 1 : 0;
+  return over <= limit;
+}
+
+// rackAwareEligibleBrokers (:246-302): TreeSet by (replicas of the partition on the broker's rack, broker id)
+std::vector<int> RackAwareDistributionGoal::rackAwareEligibleBrokers(ClusterModel& cm, int r) const {
+  const int p = cm.replicas[r].partition;
+  const std::vector<int> partitionBrokers = cm.partitionBrokersSet(p);
+  std::map<int, int> n = numReplicasByRack(cm, p);
+  n[cm.brokers[cm.replicas[r].broker].rack] -= 1;  // merge(rack, -1, Integer::sum): a 0 entry stays
+  const int rf = (int)partitionBrokers.size();
+  const int base = baseLimit(rf);
+  int over = 0;
+  for (const auto& kv : n) over += kv.second > base ? 1 : 0;
+  const bool canMoveToRacksAtBaseLimit = over < numRacksWithOneMoreReplica(rf);
+  std::vector<int> out;
+  for (int b : cm.aliveBrokers()) {
+    const int here = getOrZero(n, cm.brokers[b].rack);
+    if (here < base || (canMoveToRacksAtBaseLimit && here == base))
+      if (std::find(partitionBrokers.begin(), partitionBrokers.end(), b) == partitionBrokers.end()) out.push_back(b);
+  }
+  std::sort(out.begin(), out.end(), [&](int a, int b) {
+    const int ca = getOrZero(n, cm.brokers[a].rack), cb = getOrZero(n, cm.brokers[b].rack);
+    return ca != cb ? ca < cb : cm.brokers[a].id < cm.brokers[b].id;
+  });
+  return out;
+}
+
+// AbstractRackAwareGoal.rebalanceForBroker (AbstractRackAwareGoal.java:144-170), throwExceptionIfCannotMove = false
+void RackAwareDistributionGoal::rebalanceForBroker(int b, ClusterModel& cm, const GoalList& g,
+                                                   const OptimizationOptions& o) {
+  for (int r : cm.sortedReplicasClone(b, replicaSortName(false, false))) {
+    if (cm.brokers[b].isAlive() && !cm.isCurrentOffline(r) && shouldKeepInTheCurrentBroker(cm, r)) continue;
+    maybeApplyBalancingAction(cm, r, rackAwareEligibleBrokers(cm, r), ActionType::INTER_BROKER_REPLICA_MOVEMENT, g, o);
+  }
+}
+
+// updateGoalState (:175-188) and ensureRackAwareDistribution (:342-383) over clusterModel.leaderReplicas(): a
+// HashSet<Replica> filled from the model's partition map
+void RackAwareDistributionGoal::updateGoalState(ClusterModel& cm, const OptimizationOptions& o) {
+  ensureNoOfflineReplicas(cm, name());
+  JHashSet parts([&cm](int x, int y) {
+    const int c = cm.topicNames[cm.partitions[x].topic].compare(cm.topicNames[cm.partitions[y].topic]);
+    return c != 0 ? c : icompare(cm.partitions[x].number, cm.partitions[y].number);
+  });
+  for (size_t p = 0; p < cm.partitions.size(); ++p) parts.add((int)p, cm.tpHash((int)p));
+  JHashSet leaders([&cm](int x, int y) { return cm.replicaCompareTo(x, y); });
+  for (int p : parts.order()) leaders.add(cm.partitions[p].leader, cm.replicaHash(cm.partitions[p].leader));
+  for (int l : leaders.order()) {
+    const int p = cm.replicas[l].partition;
+    if (o.excludedTopics.count(cm.partitions[p].topic)) continue;
+    const std::map<int, int> n = numReplicasByRack(cm, p);
+    int mx = 0, mn = 1 << 30;
+    for (const auto& kv : n) {
+      mx = std::max(mx, kv.second);
+      mn = std::min(mn, kv.second);
+    }
+    if (mx > 1 && ((int)n.size() < numRacks_ || mx - mn > 1))
+      throw OptimizationFailure("[" + name() + "] Partition " + std::to_string(p) + " is not rack-aware.",
+                                underBrokers(1));  // .excludedRackIds(...) not carried
+  }
+  ensureReplicasMoveOffBrokersWithBadDisks(cm, name());
+  if (provision_.status != PROV_OVER) provision_ = ProvisionResp{PROV_RIGHT_SIZED};
+  finished_ = true;
+}
+
 // ===================================================================== MinTopicLeadersPerBrokerGoal
 // With the default topics.with.min.leaders.per.broker ("", matches no topic) the goal accepts every action
 // (actionAffectsRelevantTopics is false, MinTopicLeadersPerBrokerGoal.java:263-269) and only moves offline

@@ -29,6 +29,7 @@ std::unique_ptr<Goal> makeGoal(int kind, const BalancingConstraint& bc) {
     case CCMI_GOAL_INTRA_BROKER_DISK_USAGE_DISTRIBUTION:
       return std::make_unique<IntraBrokerDiskUsageDistributionGoal>(bc);
     case CCMI_GOAL_PREFERRED_LEADER_ELECTION: return std::make_unique<PreferredLeaderElectionGoal>(bc);
+    case CCMI_GOAL_RACK_AWARE_DISTRIBUTION: return std::make_unique<RackAwareDistributionGoal>(bc);
     default: throw std::invalid_argument("goal kind not in oracle scope: " + std::to_string(kind));
   }
 }
@@ -58,7 +59,7 @@ OptimizerResult optimizations(ClusterModel& cm, const std::vector<int>& goalKind
     throw std::invalid_argument("intra-broker goals cannot be optimized together with inter-broker goals");
   if (intra != 0 && cm.disks.empty()) throw std::invalid_argument("intra-broker goals need replica placement over disks");
   cm.excludedTopicsSel = o.excludedTopics;  // ReplicaSortFunctionFactory.selectReplicasBasedOnExcludedTopics's set
-  std::vector<std::unique_ptr<Goal>> owned;
+  std::vector<std::shared_ptr<Goal>> owned;
   for (int k : goalKinds) owned.push_back(makeGoal(k, bc));
   const std::vector<int> initDist = cm.replicaDistributionFlat(), initDisks = cm.replicaDiskFlat();
   const std::vector<int> initLeaders = cm.leaderDistribution();
@@ -136,6 +137,7 @@ OptimizerResult optimizations(ClusterModel& cm, const std::vector<int>& goalKind
   }
   res.seconds = std::chrono::duration<double>(clk::now() - t0).count();
   res.candidates = cm.candidatesEvaluated;
+  res.optimizedGoals = owned;
   return res;
 }
 

@@ -37,6 +37,7 @@ struct OptimizerResult {
   std::vector<Proposal> proposals;
   double seconds = 0;
   int64_t candidates = 0;
+  std::vector<std::shared_ptr<Goal>> optimizedGoals;  // kept for Goal.actionAcceptance queries after the run
 };
 
 std::unique_ptr<Goal> makeGoal(int kind, const BalancingConstraint& bc);  // kinds: include/ccmi.h ccmi_goal_kind

@@ -360,6 +360,27 @@ int32_t oc_apply(void* hv, const ccmi_action* a, int64_t n) {
   }
 }
 
+// Goal.actionAcceptance of the gi-th goal of the last oc_optimize on the current model: 0/1/2 (ccmi_acceptance),
+// or -1 with the message in oc_error (an action the goal does not support, an unknown replica)
+int32_t oc_action_acceptance(void* hv, int32_t gi, const ccmi_action* a) {
+  auto* h = (Handle*)hv;
+  try {
+    if (gi < 0 || gi >= (int32_t)h->last.optimizedGoals.size()) throw std::invalid_argument("goal index out of range");
+    BalancingAction ba;
+    ba.type = (ActionType)a->type;
+    ba.partition = a->partition;
+    ba.sourceBroker = a->source_broker;
+    ba.destinationBroker = a->destination_broker;
+    ba.destPartition = a->destination_partition;
+    ba.sourceDisk = a->source_disk;
+    ba.destinationDisk = a->destination_disk;
+    return (int32_t)h->last.optimizedGoals[gi]->actionAcceptance(ba, h->cm);
+  } catch (std::exception& e) {
+    h->err = e.what();
+    return -1;
+  }
+}
+
 int64_t oc_action_count(void* hv) { return (int64_t)((Handle*)hv)->cm.actionLog.size(); }
 void oc_actions(void* hv, ccmi_action* out) {
   auto* h = (Handle*)hv;

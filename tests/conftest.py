@@ -15,7 +15,11 @@ def pytest_configure(config):
 
 
 def _make(path):
-    subprocess.run(["make", "-C", path, "-j8"], check=True, capture_output=True)
+    """make under an exclusive lock: pytest-xdist workers reach the session fixtures concurrently."""
+    import fcntl
+    with open(os.path.join(path, ".make.lock"), "w") as lk:
+        fcntl.flock(lk, fcntl.LOCK_EX)
+        subprocess.run(["make", "-C", path, "-j8"], check=True, capture_output=True)
 
 
 @pytest.fixture(scope="session")

@@ -80,6 +80,12 @@ struct View {
       if (pbroker(i) != self && e.bRack[pbroker(i)] == rk) return true;
     return false;
   }
+  int slotRack(int, int b) const { return e.bRack[b]; }
+  int rackCount(int p, int rk) const {
+    int c = 0;
+    for (int i = pbegin(p); i < pend(p); ++i) c += e.bRack[pbroker(i)] == rk ? 1 : 0;
+    return c;
+  }
   int nlead(int b) const { return e.bNlead[b]; }
   double pot(int b) const { return e.bPot[b]; }
   double lnwin(int b) const { return e.bLeadNwIn[b]; }

@@ -57,6 +57,8 @@ class Oracle:
             L.oc_action_count.argtypes = [C.c_void_p]
             L.oc_actions.argtypes = [C.c_void_p, C.POINTER(ccmi.ActionStruct)]
             L.oc_last_failure_provision.argtypes = [C.c_void_p, C.POINTER(ccmi.ProvisionRespStruct)]
+            L.oc_action_acceptance.restype = C.c_int32
+            L.oc_action_acceptance.argtypes = [C.c_void_p, C.c_int32, C.POINTER(ccmi.ActionStruct)]
             L.oc_apply.restype = C.c_int32
             L.oc_apply.argtypes = [C.c_void_p, C.POINTER(ccmi.ActionStruct), C.c_int64]
             L.oc_replica_distribution.argtypes = [C.c_void_p, C.POINTER(C.c_int32)]
@@ -188,6 +190,15 @@ class OracleCluster:
         st = self.L.oc_apply(self.h, arr, len(acts))
         if st != 0:
             raise ccmi._STATUS.get(st, RuntimeError)(self.L.oc_error(self.h).decode())
+
+    def action_acceptance(self, goal_index: int, action_type: int, partition: int, source: int, destination: int,
+                          destination_partition: int = -1) -> str:
+        """Goal.actionAcceptance of the goal_index-th goal of the last optimize() on the current model."""
+        a = ccmi.ActionStruct(action_type, partition, source, destination, destination_partition, -1, -1)
+        v = self.L.oc_action_acceptance(self.h, goal_index, C.byref(a))
+        if v < 0:
+            raise ValueError(self.L.oc_error(self.h).decode())
+        return ccmi.ACCEPTANCE[v]
 
     def actions(self) -> List[tuple]:
         n = self.L.oc_action_count(self.h)

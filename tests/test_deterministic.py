@@ -17,8 +17,7 @@ from parity import check_desc_against_oracle
 from verifier import (build_model, deterministic_models, offline_replicas, verify_broken_brokers,
                       verify_regression, verify_soft_goal_replica_movements)
 
-# DeterministicClusterTest.java:97-115 in priority order. Not yet in this build: RackAwareDistributionGoal
-# (the deck runs without it).
+# DeterministicClusterTest.java:97-115 in priority order (every goal of the deck is in this build).
 DECK_GOALS_ALL = ["RackAwareGoal", "RackAwareDistributionGoal", "MinTopicLeadersPerBrokerGoal", "ReplicaCapacityGoal",
                   "DiskCapacityGoal", "NetworkInboundCapacityGoal", "NetworkOutboundCapacityGoal", "CpuCapacityGoal",
                   "ReplicaDistributionGoal", "PotentialNwOutGoal", "DiskUsageDistributionGoal",
@@ -118,21 +117,25 @@ def test_oracle_passes_deterministic_deck(oracle_lib, deck):
     run_verified(oracle_runner, model, goals, bc, allowed)
 
 
-def _rack_mapper_proposals(runner_lib, mapped):
+# RackAwareGoalTest.goalNames (:57-61): the test runs for both rack goals
+RACK_GOALS = ["RackAwareDistributionGoal", "RackAwareGoal"]
+
+
+def _rack_mapper_proposals(runner_lib, mapped, goal):
     m = deterministic_models()["rackIdMapper" if mapped else "withoutRackIdMapper"]
     flat = build_model(m)
     if runner_lib is None:
         oc = OracleCluster.from_desc(flat.desc)
-        oc.optimize(["RackAwareGoal"], ccmi.BalancingConstraint())
+        oc.optimize([goal], ccmi.BalancingConstraint())
         return oc.proposals()
     cm = ccmi.ClusterModel(flat.desc, device=0, lib=runner_lib, keepalive=flat)
-    return ccmi.GoalOptimizer().optimizations(cm, [ccmi.RackAwareGoal()]).proposals
+    return ccmi.GoalOptimizer().optimizations(cm, [getattr(ccmi, goal)()]).proposals
 
 
-def check_rack_mapper_kat(runner_lib):
+def check_rack_mapper_kat(runner_lib, goal):
     """RackAwareGoalTest.testRackIdMapper (:74-130) / testWithoutRackIdMapper (:137-178)."""
-    assert _rack_mapper_proposals(runner_lib, False) == []
-    props = _rack_mapper_proposals(runner_lib, True)
+    assert _rack_mapper_proposals(runner_lib, False, goal) == []
+    props = _rack_mapper_proposals(runner_lib, True, goal)
     assert len(props) == 1
     p = props[0]
     assert p.partition == 0
@@ -140,8 +143,9 @@ def check_rack_mapper_kat(runner_lib):
     assert set(p.new_replicas) - set(p.old_replicas) == {2}
 
 
-def test_oracle_rack_id_mapper_kat(oracle_lib):
-    check_rack_mapper_kat(None)
+@pytest.mark.parametrize("goal", RACK_GOALS)
+def test_oracle_rack_id_mapper_kat(oracle_lib, goal):
+    check_rack_mapper_kat(None, goal)
 
 
 @pytest.mark.parametrize("deck", DECKS, ids=DECK_IDS)
@@ -154,8 +158,9 @@ def test_emu_deterministic_deck_matches_oracle(emu_lib, oracle_lib, deck):
     check_desc_against_oracle(emu_lib, flat.desc, flat, goals, bc)
 
 
-def test_emu_rack_id_mapper_kat(emu_lib):
-    check_rack_mapper_kat(emu_lib)
+@pytest.mark.parametrize("goal", RACK_GOALS)
+def test_emu_rack_id_mapper_kat(emu_lib, goal):
+    check_rack_mapper_kat(emu_lib, goal)
 
 
 @pytest.mark.gpu
@@ -168,5 +173,6 @@ def test_gpu_deterministic_deck_matches_oracle(gpu_lib, oracle_lib, deck):
 
 
 @pytest.mark.gpu
-def test_gpu_rack_id_mapper_kat(gpu_lib):
-    check_rack_mapper_kat(gpu_lib)
+@pytest.mark.parametrize("goal", RACK_GOALS)
+def test_gpu_rack_id_mapper_kat(gpu_lib, goal):
+    check_rack_mapper_kat(gpu_lib, goal)
