@@ -199,7 +199,9 @@ EXPORTED_SYMBOLS = (
     "ccmi_compute_cluster_stats", "ccmi_action_log_count", "ccmi_action_log_copy", "ccmi_replica_distribution",
     "ccmi_leader_distribution", "ccmi_replica_disks", "ccmi_proposal_count", "ccmi_proposals",
     "ccmi_proposal_disks", "ccmi_perf", "ccmi_perf_reset",
-    "ccmi_set_kernel_timing", "ccmi_session_set_shard", "ccmi_rccl_unique_id", "ccmi_session_attach_rccl")
+    "ccmi_set_kernel_timing", "ccmi_session_set_shard", "ccmi_rccl_unique_id", "ccmi_session_attach_rccl",
+    "ccmi_builder_create", "ccmi_builder_destroy", "ccmi_builder_create_broker", "ccmi_builder_add_disk",
+    "ccmi_builder_populate_partition", "ccmi_builder_set_broker_state", "ccmi_builder_desc", "ccmi_builder_broker_ids")
 
 # int (*)(void* ctx, int64_t* key): replace *key by the MIN over all shards, return 0 (include/ccmi.h)
 AllreduceMinFn = C.CFUNCTYPE(C.c_int, C.c_void_p, C.POINTER(C.c_int64))
@@ -244,6 +246,18 @@ class Library:
         L.ccmi_proposals.argtypes = [C.c_void_p, C.c_int32] + [C.POINTER(C.c_int32)] * 5
         L.ccmi_proposal_disks.argtypes = [C.c_void_p, C.c_int32] + [C.POINTER(C.c_int32)] * 2
         L.ccmi_replica_disks.argtypes = [C.c_void_p, C.POINTER(C.c_int32)]
+        L.ccmi_builder_create.argtypes = [C.c_int32, C.POINTER(C.c_void_p)]
+        L.ccmi_builder_destroy.argtypes = [C.c_void_p]
+        L.ccmi_builder_destroy.restype = None
+        L.ccmi_builder_create_broker.argtypes = [C.c_void_p, C.c_char_p, C.c_char_p, C.c_int32,
+                                                 C.POINTER(C.c_double), C.c_int32]
+        L.ccmi_builder_add_disk.argtypes = [C.c_void_p, C.c_int32, C.c_char_p, C.c_double]
+        L.ccmi_builder_populate_partition.argtypes = [C.c_void_p, C.c_char_p, C.c_int32, C.POINTER(C.c_int32),
+                                                      C.c_int32, C.c_int32, C.POINTER(C.c_uint8),
+                                                      C.POINTER(C.c_char_p), C.POINTER(C.c_float)]
+        L.ccmi_builder_set_broker_state.argtypes = [C.c_void_p, C.c_int32, C.c_int32]
+        L.ccmi_builder_desc.argtypes = [C.c_void_p, C.POINTER(ClusterDesc)]
+        L.ccmi_builder_broker_ids.argtypes = [C.c_void_p, C.POINTER(C.c_int32)]
         L.ccmi_perf.argtypes = [C.c_void_p, C.POINTER(PerfStruct)]
         L.ccmi_perf_reset.argtypes = [C.c_void_p]
         L.ccmi_set_kernel_timing.argtypes = [C.c_void_p, C.c_int32]
@@ -814,6 +828,88 @@ class FlatCluster:
         self.desc = d
         self.topics = list(bld.topics)
         self.partitions = {p: key for key, p in bld.parts.items()}
+
+
+class LoadMonitorModel:
+    """Model ingestion through the native builder (ccmi_builder_*): the calls LoadMonitor.clusterModel makes
+    (monitor/LoadMonitor.java:491-543) — createRack/createBroker for every live node, handleDeadBroker for the brokers
+    only partitions name, MonitorUtils.populatePartitionLoad per partition with its aggregated leader metrics, and
+    setBadBrokerState — produce the flattened model directly. Replica loads are derived natively
+    (getAggregatedMetricValues: CPU to percentage, replication bytes out, follower NW_OUT / CPU).
+
+        m = LoadMonitorModel(num_windows=2)
+        m.create_broker("r0", "h0", 0, {"CPU": 100, "NW_IN": 1e5, "NW_OUT": 1e5, "DISK": 1e6})
+        m.populate_partition("T0", 0, replicas=[0, 1], leader=0, metrics={"CPU_USAGE": [0.115, 0.015], ...})
+        cm = ClusterModel(m.desc(), keepalive=m)
+    """
+
+    METRICS = ("CPU_USAGE", "DISK_USAGE", "LEADER_BYTES_IN", "LEADER_BYTES_OUT", "REPLICATION_BYTES_IN_RATE",
+               "REPLICATION_BYTES_OUT_RATE")
+
+    def __init__(self, num_windows: int = 1, lib: Optional[Library] = None):
+        self.lib = lib or Library.get()
+        self.W = num_windows
+        h = C.c_void_p()
+        self.lib.check(self.lib.lib.ccmi_builder_create(num_windows, C.byref(h)))
+        self.handle = h
+        self._desc = None
+
+    def __del__(self):
+        try:
+            self.lib.lib.ccmi_builder_destroy(self.handle)
+        except Exception:
+            pass
+
+    def create_broker(self, rack: str, host: str, broker_id: int, capacity: Dict[str, float],
+                      alive: bool = True, disk_capacity_by_logdir: Optional[Dict[str, float]] = None) -> None:
+        cap = (C.c_double * 4)(*[float(capacity[r]) for r in RESOURCES])
+        self.lib.check(self.lib.lib.ccmi_builder_create_broker(self.handle, rack.encode(), host.encode(), broker_id,
+                                                               cap, 1 if alive else 0))
+        for logdir, c in (disk_capacity_by_logdir or {}).items():
+            self.lib.check(self.lib.lib.ccmi_builder_add_disk(self.handle, broker_id, logdir.encode(), float(c)))
+
+    def populate_partition(self, topic: str, partition: int, replicas: Sequence[int], leader: Optional[int],
+                           metrics: Dict[str, Sequence[float]], offline: Sequence[int] = (),
+                           logdirs: Optional[Sequence[Optional[str]]] = None) -> None:
+        """metrics: aggregated leader values per metric name, newest window first (missing metrics are 0)."""
+        n = len(replicas)
+        vals = []
+        for m in self.METRICS:
+            w = list(metrics.get(m, [0.0] * self.W))
+            if len(w) != self.W:
+                raise IllegalArgumentException(f"{m}: {len(w)} windows, expected {self.W}")
+            vals += [float(x) for x in w]
+        off = (C.c_uint8 * n)(*[1 if b in set(offline) else 0 for b in replicas])
+        ld = (C.c_char_p * n)(*[(x.encode() if x else None) for x in logdirs]) if logdirs else None
+        self.lib.check(self.lib.lib.ccmi_builder_populate_partition(
+            self.handle, topic.encode(), partition, (C.c_int32 * n)(*replicas), n,
+            -1 if leader is None else leader, off, ld, (C.c_float * len(vals))(*vals)))
+        self._desc = None
+
+    def set_broker_state(self, broker_id: int, state: str) -> None:
+        self.lib.check(self.lib.lib.ccmi_builder_set_broker_state(self.handle, broker_id, BROKER_STATES[state]))
+        self._desc = None
+
+    def desc(self) -> ClusterDesc:
+        if self._desc is None:
+            d = ClusterDesc()
+            self.lib.check(self.lib.lib.ccmi_builder_desc(self.handle, C.byref(d)))
+            self._desc = d
+        return self._desc
+
+    def broker_ids(self) -> List[int]:
+        """Kafka broker id of every dense broker index of desc()."""
+        d = self.desc()
+        out = (C.c_int32 * d.num_brokers)()
+        self.lib.check(self.lib.lib.ccmi_builder_broker_ids(self.handle, out))
+        return list(out)
+
+    def replica_loads(self) -> List[List[List[float]]]:
+        """[replica][metric][window] of the flattened model (the values setReplicaLoad received)."""
+        d = self.desc()
+        W = d.num_windows
+        return [[[d.replica_load[(r * 6 + m) * W + w] for w in range(W)] for m in range(6)]
+                for r in range(d.num_replicas)]
 
 
 class ClusterModel:

@@ -41,6 +41,14 @@ ccmi_status fail(ccmi_status s, const std::string& msg) {
   return s;
 }
 
+}  // namespace
+
+namespace ccmi {
+void setLastError(const std::string& msg) { g_err = msg; }
+}  // namespace ccmi
+
+namespace {
+
 template <class F>
 ccmi_status guarded(F&& f) {
   try {

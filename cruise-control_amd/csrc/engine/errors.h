@@ -52,5 +52,7 @@ struct StateError : std::runtime_error {
 struct Unsupported : std::runtime_error {
   using std::runtime_error::runtime_error;
 };
+// the message ccmi_last_error returns (ccmi_api.cpp)
+void setLastError(const std::string& msg);
 
 }  // namespace ccmi

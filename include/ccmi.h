@@ -181,8 +181,8 @@ typedef struct ccmi_balancing_constraint {
 
 /* analyzer/OptimizationOptions.java (7-field form) */
 typedef struct ccmi_opt_options {
-  const int32_t* excluded_topics; /* topic indices; honoured by the intra-broker goals (selectReplicasBasedOnExcludedTopics),
-                                     CCMI_E_UNSUPPORTED for the inter-broker goals */
+  const int32_t* excluded_topics; /* topic indices (OptimizationOptions.excludedTopics; every goal's
+                                     selectReplicasBasedOnExcludedTopics and excluded-topic checks) */
   int32_t num_excluded_topics;
   const int32_t* excluded_brokers_for_leadership;
   int32_t num_excluded_brokers_for_leadership;
@@ -296,6 +296,43 @@ void ccmi_default_random_cluster_props(ccmi_random_cluster_props* out); /* TestC
 ccmi_status ccmi_random_cluster(const ccmi_random_cluster_props* props, ccmi_cluster_buffers** out);
 const ccmi_cluster_desc* ccmi_cluster_buffers_desc(const ccmi_cluster_buffers* buf);
 void ccmi_cluster_buffers_free(ccmi_cluster_buffers* buf);
+
+/*
+ * Model ingestion: LoadMonitor.clusterModel (monitor/LoadMonitor.java:491-543) builds the ClusterModel from the Kafka
+ * metadata, the broker capacities and each partition's aggregated leader metrics; this builder takes the same calls
+ * and produces the flattened ccmi_cluster_desc directly (no Java ClusterModel needed for the engine's side):
+ *   ccmi_builder_create_broker  ClusterModel.createRack + createBroker for a live node (populateClusterCapacity
+ *                               :563-600), or handleDeadBroker for a dead one (alive = 0; a no-op if it exists)
+ *   ccmi_builder_add_disk       a logdir of a JBOD broker (BrokerCapacityInfo.diskCapacityByLogDir)
+ *   ccmi_builder_populate_partition
+ *                               MonitorUtils.populatePartitionLoad (MonitorUtils.java:415-479): one createReplica +
+ *                               setReplicaLoad per replica of PartitionInfo.replicas() in order, the loads derived
+ *                               from the partition's aggregated leader metrics by getAggregatedMetricValues (:215-265):
+ *                               CPU unit interval -> percentage once per partition, the leader's replication bytes
+ *                               out = leader bytes in x followers, a follower's NW_OUT = 0 and CPU from
+ *                               ModelUtils.getFollowerCpuUtilFromLeaderLoad (0.7 / 0.15 / 0.15 weights), all in the
+ *                               reference's float MetricValues arithmetic. leader_broker_id < 0 = offline partition
+ *                               (no replicas created, LoadMonitor logs and skips it).
+ *   ccmi_builder_set_broker_state  setBadBrokerState (MonitorUtils.java:349-356) and NEW / DEMOTED marking
+ *   ccmi_builder_desc           the flattened model (valid until ccmi_builder_destroy). Brokers are indexed in
+ *                               ascending id order; broker_id[b] = b in the desc, and ccmi_builder_broker_ids maps an
+ *                               index back to the Kafka broker id (HashSet<Broker> iteration ties follow the dense
+ *                               index, which equals the reference's order when the ids are 0..B-1).
+ * leader_metrics: [6 * W] floats, ccmi_metric order, newest window first (ValuesAndExtrapolations.metricValues()).
+ */
+typedef struct ccmi_model_builder ccmi_model_builder;
+ccmi_status ccmi_builder_create(int32_t num_windows, ccmi_model_builder** out);
+void ccmi_builder_destroy(ccmi_model_builder* b);
+ccmi_status ccmi_builder_create_broker(ccmi_model_builder* b, const char* rack, const char* host, int32_t broker_id,
+                                       const double capacity[4], int32_t alive);
+ccmi_status ccmi_builder_add_disk(ccmi_model_builder* b, int32_t broker_id, const char* logdir, double capacity);
+ccmi_status ccmi_builder_populate_partition(ccmi_model_builder* b, const char* topic, int32_t partition,
+                                            const int32_t* replica_broker_ids, int32_t num_replicas,
+                                            int32_t leader_broker_id, const uint8_t* offline,
+                                            const char* const* logdirs, const float* leader_metrics);
+ccmi_status ccmi_builder_set_broker_state(ccmi_model_builder* b, int32_t broker_id, int32_t state);
+ccmi_status ccmi_builder_desc(ccmi_model_builder* b, ccmi_cluster_desc* out);
+ccmi_status ccmi_builder_broker_ids(const ccmi_model_builder* b, int32_t* out);
 
 /* device_ordinal: HIP device; num_devices > 1 shards the candidate space by destination broker across
  * device_ordinal .. device_ordinal+num_devices-1 inside one process (multi-process sharding uses RCCL
