@@ -160,7 +160,8 @@ class PerfStruct(C.Structure):
                 ("stats_launches", C.c_int64), ("stats_kernel_ms", C.c_double), ("stats_bytes", C.c_int64),
                 ("host_syncs", C.c_int64), ("scan_required", C.c_int64), ("chain_launches", C.c_int64),
                 ("intra_launches", C.c_int64), ("intra_kernel_ms", C.c_double), ("intra_bytes", C.c_int64),
-                ("cross_launches", C.c_int64), ("cross_required", C.c_int64), ("cross_kernel_ms", C.c_double)]
+                ("cross_launches", C.c_int64), ("cross_required", C.c_int64), ("cross_kernel_ms", C.c_double),
+                ("combines", C.c_int64)]
 
 
 # ----------------------------------------------------------------------------------------------- errors

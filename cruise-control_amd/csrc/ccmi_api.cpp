@@ -593,6 +593,7 @@ ccmi_status ccmi_perf(const ccmi_session* s, ccmi_perf_counters* out) {
     out->cross_launches = p.crossLaunches;
     out->cross_required = p.crossRequired;
     out->cross_kernel_ms = p.crossKernelMs;
+    out->combines = p.combines;
     return CCMI_OK;
   });
 }

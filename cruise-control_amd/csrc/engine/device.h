@@ -40,6 +40,7 @@ struct DevicePerf {
   int64_t intraLaunches = 0;  // K6 intra-broker launches
   double intraKernelMs = 0;
   int64_t intraBytes = 0;     // algorithmic bytes of K6 (per broker record + per replica entry)
+  int64_t combines = 0;       // shard-combiner calls (MIN allreduce of a scan's first-fit key)
   int64_t crossLaunches = 0;  // the scan_cross share of the scan counters
   int64_t crossRequired = 0;
   double crossKernelMs = 0;

@@ -201,8 +201,16 @@ int64_t Engine::crossScan(GoalImpl& self, int action, const std::vector<int32_t>
   return key;
 }
 
+// CCMI_FORCE_COMBINE=1 sends single-shard keys through the combiner too (diagnostics: exercises the RCCL path of a
+// one-rank communicator on a one-GPU box)
+static bool forceCombine() {
+  const char* e = std::getenv("CCMI_FORCE_COMBINE");  // read per call: only one-shard sessions with a combiner ask
+  return e && e[0] == '1';
+}
+
 int64_t Engine::combine(int64_t localKey) const {
-  if (shard.count <= 1) return localKey;
+  if (shard.count <= 1 && !(shard.fn && forceCombine())) return localKey;
+  dev->perf.combines++;
   int64_t k = localKey < 0 ? INT64_MAX : localKey;
   if (!shard.fn || shard.fn(shard.ctx, &k) != 0) throw std::runtime_error("shard combine (MIN allreduce) failed");
   return k == INT64_MAX ? -1 : k;

@@ -419,6 +419,7 @@ typedef struct ccmi_perf_counters {
   int64_t cross_launches;      /* the scan_cross share of scan_launches / scan_required / scan_kernel_ms (the kernel */
   int64_t cross_required;      /* tools/pmc_summary.py prices against its own FETCH_SIZE / WRITE_SIZE counters) */
   double cross_kernel_ms;
+  int64_t combines;            /* shard-combiner calls (RCCL / host MIN-allreduce of a scan's first-fit key) */
 } ccmi_perf_counters;
 ccmi_status ccmi_perf(const ccmi_session* s, ccmi_perf_counters* out);
 void ccmi_perf_reset(ccmi_session* s);

@@ -67,3 +67,24 @@ def test_gpu_sharded_scans_match_oracle(gpu_lib, oracle_lib, tmp_path):
         assert o["error"] is None and o["combines"] > 0
         assert [tuple(a) for a in o["actions"]] == oc.actions()
         assert [tuple(g) for g in o["goals"]] == [(r.name, r.succeeded, r.candidates, r.actions) for r in ores]
+
+
+@pytest.mark.gpu
+def test_gpu_rccl_combiner_one_rank(gpu_lib, oracle_lib, monkeypatch):
+    """The built-in RCCL combiner (shard_rccl.cpp: host -> HBM, ncclAllReduce MIN, HBM -> host per scan) on a
+    one-rank communicator, forced onto every scan with CCMI_FORCE_COMBINE=1: the same decisions as the oracle. (Two
+    RCCL ranks cannot share the one GPU of a test box; the multi-rank path runs in the driver's 8-GPU bench.)"""
+    monkeypatch.setenv("CCMI_FORCE_COMBINE", "1")
+    props = dict(num_racks=5, num_brokers=20, num_replicas=6000, num_topics=300)
+    goals = list(ccmi.C1_GOALS)
+    buf = ccmi.RandomCluster.generate(gpu_lib, **props)
+    cm = ccmi.ClusterModel.from_buffers(buf, device=0)
+    cm.attach_rccl(0, 1, ccmi.rccl_unique_id(gpu_lib))
+    cm.reset_perf()
+    res = ccmi.GoalOptimizer(constraint(1.05)).optimizations(cm, ccmi.goals_from_names(goals))
+    assert cm.perf().combines > 0
+    oc = OracleCluster.from_desc(buf.desc)
+    ores = oc.optimize(goals, constraint(1.05))
+    assert cm.actions() == oc.actions()
+    assert [(r.name, r.succeeded, r.candidates, r.actions) for r in res.goal_results] == \
+        [(r.name, r.succeeded, r.candidates, r.actions) for r in ores]
