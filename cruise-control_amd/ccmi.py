@@ -48,6 +48,7 @@ GOAL_KINDS: Dict[str, int] = {
     "IntraBrokerDiskUsageDistributionGoal": 17,
     "PreferredLeaderElectionGoal": 18,
     "RackAwareDistributionGoal": 19,
+    "BrokerSetAwareGoal": 20,
 }
 GOAL_NAMES = {v: k for k, v in GOAL_KINDS.items()}
 # default.goals in priority order (config/constants/AnalyzerConfig.java:352-367, TestConstants.DEFAULT_GOALS_VALUES)
@@ -63,7 +64,10 @@ C1_GOALS = ("ReplicaDistributionGoal", "DiskUsageDistributionGoal", "NetworkInbo
 # intra.broker.goals (AnalyzerConfig INTRA_BROKER_GOALS default, IntraBrokerRebalanceTest.java:105-106)
 INTRA_BROKER_GOALS = ("IntraBrokerDiskCapacityGoal", "IntraBrokerDiskUsageDistributionGoal")
 # Goals whose drivers are implemented in this build.
-IMPLEMENTED = DEFAULT_GOALS + INTRA_BROKER_GOALS + ("PreferredLeaderElectionGoal", "RackAwareDistributionGoal")
+IMPLEMENTED = DEFAULT_GOALS + INTRA_BROKER_GOALS + ("PreferredLeaderElectionGoal", "RackAwareDistributionGoal",
+                                                   "BrokerSetAwareGoal")
+# replica.to.broker.set.mapping.policy.class values (include/ccmi.h ccmi_broker_set_policy)
+BROKER_SET_POLICIES = {"TopicNameHashBrokerSetMappingPolicy": 0, "ReplicaToOriginalBrokerSetMappingPolicy": 1}
 
 ACTION_TYPES = ("INTER_BROKER_REPLICA_MOVEMENT", "LEADERSHIP_MOVEMENT", "INTER_BROKER_REPLICA_SWAP",
                 "INTRA_BROKER_REPLICA_MOVEMENT", "INTRA_BROKER_REPLICA_SWAP")
@@ -95,7 +99,10 @@ class ConstraintStruct(C.Structure):
                 ("topic_replica_balance_min_gap", C.c_int32), ("topic_replica_balance_max_gap", C.c_int32),
                 ("goal_violation_distribution_threshold_multiplier", C.c_double),
                 ("max_replicas_per_broker", C.c_int64), ("overprovisioned_max_replicas_per_broker", C.c_int64),
-                ("overprovisioned_min_brokers", C.c_int32), ("overprovisioned_min_extra_racks", C.c_int32)]
+                ("overprovisioned_min_brokers", C.c_int32), ("overprovisioned_min_extra_racks", C.c_int32),
+                ("num_broker_sets", C.c_int32), ("broker_set_policy", C.c_int32),
+                ("broker_set_names", C.POINTER(C.c_char_p)), ("broker_set_offset", C.POINTER(C.c_int32)),
+                ("broker_set_members", C.POINTER(C.c_int32))]
 
 
 class OptionsStruct(C.Structure):
@@ -201,6 +208,7 @@ EXPORTED_SYMBOLS = (
     "ccmi_leader_distribution", "ccmi_replica_disks", "ccmi_proposal_count", "ccmi_proposals",
     "ccmi_proposal_disks", "ccmi_perf", "ccmi_perf_reset",
     "ccmi_set_kernel_timing", "ccmi_session_set_shard", "ccmi_rccl_unique_id", "ccmi_session_attach_rccl",
+    "ccmi_topic_broker_set",
     "ccmi_builder_create", "ccmi_builder_destroy", "ccmi_builder_create_broker", "ccmi_builder_add_disk",
     "ccmi_builder_populate_partition", "ccmi_builder_set_broker_state", "ccmi_builder_desc", "ccmi_builder_broker_ids")
 
@@ -266,6 +274,8 @@ class Library:
         L.ccmi_rccl_unique_id.argtypes = [C.POINTER(C.c_uint8)]
         L.ccmi_session_attach_rccl.argtypes = [C.c_void_p, C.c_int32, C.c_int32, C.POINTER(C.c_uint8)]
         L.ccmi_default_constraint.argtypes = [C.POINTER(ConstraintStruct)]
+        L.ccmi_topic_broker_set.restype = C.c_int32
+        L.ccmi_topic_broker_set.argtypes = [C.c_char_p, C.c_int32]
         L.ccmi_default_random_cluster_props.argtypes = [C.POINTER(RandomClusterProps)]
 
     @classmethod
@@ -294,6 +304,11 @@ class BalancingConstraint:
     topic_replica_balance_min_gap: int = 2
     topic_replica_balance_max_gap: int = 40
     overprovisioned_min_extra_racks: int = 2  # AnalyzerConfig.DEFAULT_OVERPROVISIONED_MIN_EXTRA_RACKS
+    # BrokerSetAwareGoal: BalancingConstraint.brokerSetResolver() data (broker set id -> broker ids, the content of
+    # broker.set.config.file for BrokerSetFileResolver) and replica.to.broker.set.mapping.policy.class. Brokers in no
+    # set join "unmapped" (NoOpBrokerSetAssignmentPolicy, the default broker.set.assignment.policy.class).
+    broker_sets: Optional[Dict[str, Sequence[int]]] = None
+    broker_set_policy: str = "TopicNameHashBrokerSetMappingPolicy"
 
     def set_resource_balance_percentage(self, p: float) -> None:  # BalancingConstraint.setResourceBalancePercentage
         self.resource_balance_percentage = (p, p, p, p)
@@ -316,6 +331,22 @@ class BalancingConstraint:
         s.overprovisioned_max_replicas_per_broker = 1500
         s.overprovisioned_min_brokers = 3
         s.overprovisioned_min_extra_racks = self.overprovisioned_min_extra_racks
+        if self.broker_sets:
+            names = list(self.broker_sets)
+            members = [int(b) for n in names for b in self.broker_sets[n]]
+            offs = [0]
+            for n in names:
+                offs.append(offs[-1] + len(self.broker_sets[n]))
+            keep = [(C.c_char_p * len(names))(*[n.encode() for n in names]), (C.c_int32 * len(offs))(*offs),
+                    (C.c_int32 * max(1, len(members)))(*members)]
+            s._keep = keep  # the arrays live as long as the struct
+            s.num_broker_sets = len(names)
+            s.broker_set_names = C.cast(keep[0], C.POINTER(C.c_char_p))
+            s.broker_set_offset = C.cast(keep[1], C.POINTER(C.c_int32))
+            s.broker_set_members = C.cast(keep[2], C.POINTER(C.c_int32))
+        if self.broker_set_policy not in BROKER_SET_POLICIES:
+            raise IllegalArgumentException(f"unknown broker set mapping policy {self.broker_set_policy}")
+        s.broker_set_policy = BROKER_SET_POLICIES[self.broker_set_policy]
         return s
 
 

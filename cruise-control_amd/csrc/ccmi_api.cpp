@@ -90,6 +90,7 @@ void setOptions(ccmi_session* s, const ccmi_balancing_constraint* c, const ccmi_
   e.bc.overMaxReplicasPerBroker = c->overprovisioned_max_replicas_per_broker;
   e.bc.overMinBrokers = c->overprovisioned_min_brokers;
   e.bc.overprovisionedMinExtraRacks = c->overprovisioned_min_extra_racks;
+  e.brokerSets.resolve(c, s->model.bId);
   const int B = s->model.B;
   ccmi::Options opt;
   opt.exclMove.assign(B, 0);
@@ -197,6 +198,11 @@ extern "C" {
 
 const char* ccmi_last_error(void) { return g_err.c_str(); }
 int32_t ccmi_abi_version(void) { return CCMI_ABI_VERSION; }
+
+int32_t ccmi_topic_broker_set(const char* topic, int32_t num_broker_sets) {
+  if (!topic) return -1;
+  return ccmi::bsets::topicBrokerSet(topic, num_broker_sets);
+}
 
 void ccmi_default_constraint(ccmi_balancing_constraint* c) {
   std::memset(c, 0, sizeof(*c));

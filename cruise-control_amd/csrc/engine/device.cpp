@@ -304,6 +304,17 @@ void Device::setTopicLimits(const int32_t* upper, const int32_t* lower) {
   hipCheck(hipStreamSynchronize(ST), "sync");
 }
 
+void Device::setBrokerSets(const int32_t* brokerSet, const int32_t* replicaSet) {
+  DeviceGuard dg(ordinal_);
+  hipCheck(hipMemcpy2DAsync(&brokers_[0].bset, sizeof(BrokerRec), brokerSet, sizeof(int32_t), sizeof(int32_t), B_,
+                            hipMemcpyHostToDevice, ST),
+           "upload broker sets");
+  hipCheck(hipMemcpy2DAsync(&replicas_[0].bset, sizeof(ReplicaRec), replicaSet, sizeof(int32_t), sizeof(int32_t), R_,
+                            hipMemcpyHostToDevice, ST),
+           "upload replica broker sets");
+  hipCheck(hipStreamSynchronize(ST), "sync");
+}
+
 size_t Device::updatesBytes() const {
   return align16(brows.size() * sizeof(BrokerRow)) + align16(rrows.size() * sizeof(ReplicaRow)) +
          align16(prows.size() * sizeof(PartitionRow)) + align16(tdeltas.size() * sizeof(TopicCountDelta));

@@ -95,6 +95,9 @@ class Device {
   void setExclusions(const uint8_t* exclLead, const uint8_t* exclMove, const uint8_t* isNew);
   // TopicReplicaDistributionGoal balance limits per topic (frozen at its initGoalState)
   void setTopicLimits(const int32_t* upper, const int32_t* lower);
+  // BrokerSetAwareGoal: BrokerRec.bset [B] (broker set of every broker) and ReplicaRec.bset [R] (the set the mapping
+  // policy gives every replica), strided writes that leave the rest of the records alone
+  void setBrokerSets(const int32_t* brokerSet, const int32_t* replicaSet);
 
   // pending row updates (flushed with the next launch)
   std::vector<BrokerRow> brows;

@@ -41,8 +41,12 @@ enum DevGoalKind : int32_t {
   DG_TOPIC_REPLICA_DISTRIBUTION = 7,
   DG_LEADER_REPLICA_DISTRIBUTION = 8,
   DG_LEADER_BYTES_IN = 9,
-  DG_RACK_AWARE_DISTRIBUTION = 10
+  DG_RACK_AWARE_DISTRIBUTION = 10,
+  DG_BROKER_SET_AWARE = 11
 };
+// ReplicaRec.bset of a replica every broker set accepts (a topic of MinTopicLeadersPerBrokerGoal's
+// mustHaveTopicLeadersPerBroker set, BrokerSetAwareGoal.java:232-236)
+constexpr int32_t kBrokerSetAny = -2;
 // Operands a program's predicates read beyond the base broker/replica/partition record (DevProgram.needs).
 enum DevNeed : uint32_t { NEED_RACK = 1, NEED_POT = 2, NEED_LEAD = 4, NEED_LBI = 8, NEED_TOPIC = 16 };
 // Candidate filters applied inside a CROSS scan before the predicate conjunction (the reference builds these
@@ -98,12 +102,14 @@ struct alignas(64) BrokerRec {
   int32_t nrep, nlead, rack;
   uint32_t allowedBits;   // bit g: in goal slot g's _brokersAllowedReplicaMove; bit 31: excluded for leadership
   int32_t alive;
-  int32_t pad[7];
+  int32_t bset;           // broker set index (BrokerSetAwareGoal; static while a goal chain runs), -1 = none
+  int32_t pad[6];
 };
 struct alignas(64) ReplicaRec {
   double util[4];
   int32_t broker, part, orig, flags;  // flags: RFlag bits
-  int32_t pad[4];
+  int32_t bset;  // the broker set the replica belongs to (ReplicaToBrokerSetMappingPolicy), kBrokerSetAny, -1 = none
+  int32_t pad[3];
 };
 struct alignas(64) PartitionRec {
   int32_t n, topic;

@@ -36,6 +36,8 @@ struct HostView {
   const std::vector<const std::vector<uint8_t>*>& allowedBySlot;
   const std::vector<int32_t>& tUp;
   const std::vector<int32_t>& tLo;
+  const std::vector<int32_t>& bSet;  // BrokerSetAwareGoal: broker set of every broker / replica (empty: none)
+  const std::vector<int32_t>& rSet;
   double bu(int b, int res) const { return m.bu(b, res); }
   double bcap(int b, int res) const { return m.cap(b, res); }
   int nrep(int b) const { return m.nrep(b); }
@@ -76,6 +78,8 @@ struct HostView {
   int tcount(int t, int b) const { return m.tcount(t, b); }
   int tUpper(int t) const { return tUp[t]; }
   int tLower(int t) const { return tLo[t]; }
+  int bset(int b) const { return bSet.empty() ? -1 : bSet[b]; }
+  int rbset(int r) const { return rSet.empty() ? -1 : rSet[r]; }
 };
 
 uint32_t needsOf(const DevGoal& g) {
@@ -325,7 +329,7 @@ int Engine::acceptance(int gi, const ccmi_action& a) {
   }
   std::vector<const std::vector<uint8_t>*> allowedBySlot;
   for (auto& g : optimized) allowedBySlot.push_back(&g->allowed);
-  HostView v{m, allowedBySlot, topicUpper, topicLower};
+  HostView v{m, allowedBySlot, topicUpper, topicLower, brokerSetOf, replicaSetOf};
   const GoalImpl& g = *optimized.at(gi);
   const int sr = m.replicaOn(a.partition, a.source_broker);
   if (sr < 0) throw std::invalid_argument("no replica of the partition on the source broker");
@@ -340,7 +344,9 @@ int Engine::acceptance(int gi, const ccmi_action& a) {
   if (goalAcceptMove(g.dg, v, action, sr, a.source_broker, a.destination_broker)) return CCMI_ACCEPT;
   // AbstractRackAwareGoal.actionAcceptance rejects a replica move with BROKER_REJECT (AbstractRackAwareGoal.java:
   // 100-106); every other goal's rejected move or leadership move is a REPLICA_REJECT
-  const bool rack = g.dg.kind == DG_RACK_AWARE || g.dg.kind == DG_RACK_AWARE_DISTRIBUTION;
+  // BrokerSetAwareGoal.actionAcceptance: BROKER_REJECT too (BrokerSetAwareGoal.java:240-246)
+  const bool rack = g.dg.kind == DG_RACK_AWARE || g.dg.kind == DG_RACK_AWARE_DISTRIBUTION ||
+                    g.dg.kind == DG_BROKER_SET_AWARE;
   return rack && action == DA_MOVE ? CCMI_BROKER_REJECT : CCMI_REPLICA_REJECT;
 }
 

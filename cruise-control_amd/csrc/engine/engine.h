@@ -17,6 +17,7 @@
 #include <string>
 #include <vector>
 
+#include "brokersets.h"
 #include "ccmi.h"
 #include "devtypes.h"
 #include "errors.h"
@@ -87,6 +88,8 @@ class Engine {
   ccmi_provision_response lastFailure{};  // provisionResponse of the goal whose OptimizationFailure ended the last call
   std::vector<uint8_t> scratchB, scratchB2;  // per-broker scratch flags for the goal drivers
   std::vector<int32_t> topicUpper, topicLower;  // TopicReplicaDistributionGoal limits (device copy: setTopicLimits)
+  BrokerSets brokerSets;                        // BalancingConstraint broker sets of the current call
+  std::vector<int32_t> brokerSetOf, replicaSetOf;  // BrokerSetAwareGoal state (device copy: setBrokerSets)
 
   // one Goal.optimize; throws OptimizationFailure / StateError
   bool optimizeGoal(std::unique_ptr<GoalImpl> g, ccmi_goal_result* res);

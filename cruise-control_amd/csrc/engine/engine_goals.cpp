@@ -16,6 +16,7 @@
 //   LeaderReplicaDistributionGoal           analyzer/goals/LeaderReplicaDistributionGoal.java:137-364,
 //                                           ReplicaDistributionAbstractGoal.java:60-160
 //   LeaderBytesInDistributionGoal           analyzer/goals/LeaderBytesInDistributionGoal.java:142-271
+//   BrokerSetAwareGoal                      analyzer/goals/BrokerSetAwareGoal.java:80-275 (not in default.goals)
 //   GoalUtils.ensureNoOfflineReplicas       analyzer/goals/GoalUtils.java:307-318
 #include <algorithm>
 #include <cmath>
@@ -1610,6 +1611,116 @@ class PreferredLeaderElection : public GoalImpl {
   int compareStats(const ccmi_cluster_stats&, const ccmi_cluster_stats&) const override { return 0; }
 };
 
+// ======================================================================================= BrokerSetAwareGoal
+// A hard goal: every replica must sit in the broker set its mapping policy names (TopicNameHash: the topic's set;
+// ReplicaToOriginal: its original broker's set). Broker sets come with the call's BalancingConstraint (brokersets.h);
+// the device reads BrokerRec.bset / ReplicaRec.bset when this goal is the optimized one or a prior one.
+class BrokerSetAware : public GoalImpl {
+ public:
+  BrokerSetAware() {
+    kind = CCMI_GOAL_BROKER_SET_AWARE;
+    name = "BrokerSetAwareGoal";
+  }
+  std::vector<int32_t> alive;
+
+  static std::string idList(const Model& m, const std::vector<int32_t>& v) {
+    std::string out = "[";
+    for (size_t i = 0; i < v.size(); ++i) out += (i ? ", " : "") + std::to_string(m.bId[v[i]]);
+    return out + "]";
+  }
+
+  // initGoalState (BrokerSetAwareGoal.java:80-129)
+  void init(Engine& e) override {
+    Model& m = e.m;
+    if (allowedForReplicaMove(e, allowed) == 0)
+      throw OptimizationFailure("[" + name + "] All alive brokers are excluded from replica moves.", underBrokers(m.maxRf));
+    Model::Spec s;
+    s.selImmigrants = e.opt.onlyImmigrants;
+    s.selExclTopics = e.opt.anyExclTopic;  // _excludedTopics: no MinTopicLeadersPerBroker topics are configured
+    for (int b = 0; b < m.B; ++b) m.track(b, sortId(kind, false, false), s);
+    // BrokerSetResolutionHelper + the mapping policy, frozen for the goal (the policy caches per topic)
+    const BrokerSets& bs = e.brokerSets;
+    if (bs.numSets == 0) throw std::invalid_argument("[" + name + "] no broker sets (BrokerSetResolutionException)");
+    e.brokerSetOf = bs.ofBroker;
+    e.replicaSetOf.assign(m.R, -1);
+    std::vector<int32_t> topicSet;
+    if (bs.policy == CCMI_BROKER_SET_TOPIC_NAME_HASH) {
+      topicSet.resize(m.T);
+      for (int t = 0; t < m.T; ++t) topicSet[t] = bsets::topicBrokerSet(m.topicNames[t], bs.numSets);
+    }
+    for (int r = 0; r < m.R; ++r)
+      e.replicaSetOf[r] = bs.policy == CCMI_BROKER_SET_TOPIC_NAME_HASH ? topicSet[m.pTopic[m.rPart[r]]]
+                                                                       : e.brokerSetOf[m.rOrig[r]];
+    e.dev->setBrokerSets(e.brokerSetOf.data(), e.replicaSetOf.data());
+    alive = aliveById(m);
+    dg = DevGoal{};
+    dg.kind = DG_BROKER_SET_AWARE;
+    dg.allowedSlot = (int)e.optimized.size();
+  }
+
+  // rebalanceForBroker (:159-188): each misplaced replica goes to the first acceptable alive broker of its set in
+  // HashSet<Broker> order, or the goal fails
+  void rebalance(Engine& e, int b) override {
+    PhaseScope ps(PH_OTHER_GOALS);
+    Model& m = e.m;
+    const std::vector<int32_t> list = m.sorted(b, sortId(kind, false, false));
+    const int cur = e.brokerSetOf[b];
+    std::vector<int32_t> one(1), ins, order, cands;
+    for (int r : list) {
+      const int want = e.replicaSetOf[r];
+      if (m.alive(b) && want == cur) continue;
+      ins.clear();
+      for (int x : alive)
+        if (e.brokerSetOf[x] == want) ins.push_back(x);
+      javaHashSetOrder(ins, order);  // Collectors.toSet()
+      e.eligible(order, DA_MOVE, cands);
+      one[0] = r;
+      const int64_t key = cands.empty() ? -1 : e.crossScan(*this, DA_MOVE, one, 0, cands);
+      if (key < 0)
+        throw OptimizationFailure("[" + name + "] Cannot move replica " + m.topicNames[m.pTopic[m.rPart[r]]] + "-" +
+                                      std::to_string(m.pNumber[m.rPart[r]]) + " on broker " + std::to_string(m.bId[b]) +
+                                      " to " + idList(m, order) + " on brokerSet " + e.brokerSets.names[want],
+                                  underBrokers(m.maxRf));
+      m.relocateReplica(m.rPart[r], b, cands[key]);
+    }
+  }
+
+  // updateGoalState (:139-147) + ensureBrokerSetAware (:149-167)
+  void update(Engine& e) override {
+    Model& m = e.m;
+    ensureNoOfflineReplicas(m, name);
+    for (int b = 0; b < m.B; ++b)  // GoalUtils.ensureReplicasMoveOffBrokersWithBadDisks
+      if (m.bState[b] == BState::BAD_DISKS)
+        for (int r : m.bRepl[b])
+          if (m.ineligible(m.rPart[r], b))
+            throw OptimizationFailure("[" + name + "] A replica was moved back to broker with broken disk.",
+                                      underBrokers(1));
+    std::vector<int> topics(m.T);
+    for (int t = 0; t < m.T; ++t) topics[t] = t;
+    std::sort(topics.begin(), topics.end(), [&m](int a, int c) { return m.topicNames[a] < m.topicNames[c]; });
+    std::vector<std::vector<int32_t>> byTopic(m.T);
+    for (int p = 0; p < m.P; ++p)
+      for (int i = m.pOff[p]; i < m.pOff[p + 1]; ++i) byTopic[m.pTopic[p]].push_back(m.rBroker[m.pSlots[i]]);
+    std::vector<int32_t> ids, order;
+    for (int t : topics) {  // getPartitionsByTopic: a TreeMap by topic name
+      if (e.opt.anyExclTopic && e.opt.exclTopic[t]) continue;
+      const auto& v = byTopic[t];  // the topic's brokers in partition / slot order
+      const int set = v.empty() ? -1 : e.brokerSetOf[v[0]];
+      bool one = true;
+      for (int x : v) one &= e.brokerSetOf[x] == set;
+      if (one) continue;
+      ids.clear();  // first appearances (HashSet insertion order), then Collectors.toSet() iteration order
+      for (int x : v)
+        if (std::find(ids.begin(), ids.end(), x) == ids.end()) ids.push_back(x);
+      javaHashSetOrder(ids, order);
+      throw OptimizationFailure("[" + name + "] Topic " + m.topicNames[t] + " is not brokerSet-aware. brokers (" +
+                                idList(m, order) + ").");
+    }
+    finished = true;
+  }
+  int compareStats(const ccmi_cluster_stats&, const ccmi_cluster_stats&) const override { return 0; }
+};
+
 std::unique_ptr<GoalImpl> makeMoreGoal(int kind) {
   switch (kind) {
     case CCMI_GOAL_RACK_AWARE: return std::make_unique<RackAware>();
@@ -1625,6 +1736,7 @@ std::unique_ptr<GoalImpl> makeMoreGoal(int kind) {
     case CCMI_GOAL_LEADER_BYTES_IN_DISTRIBUTION: return std::make_unique<LeaderBytesIn>();
     case CCMI_GOAL_PREFERRED_LEADER_ELECTION: return std::make_unique<PreferredLeaderElection>();
     case CCMI_GOAL_RACK_AWARE_DISTRIBUTION: return std::make_unique<RackAwareDist>();
+    case CCMI_GOAL_BROKER_SET_AWARE: return std::make_unique<BrokerSetAware>();
     default: throw Unsupported("goal kind " + std::to_string(kind) + " is not implemented in this build");
   }
 }

@@ -36,7 +36,7 @@ namespace ccmi {
 // V must provide: bu(b,res) bcap(b,res) nrep(b) alive(b) allowed(slot,b) ru(r,res) flags(r) rbroker(r)
 // rorig(r) origOff(r) rpart(r) hosts(p,b), and for the goals that read them: rack(b) otherOnRack(p,self,rack)
 // slotRack(p,b) (rack of partition p's replica on b) rackCount(p,rack) nlead(b)
-// pot(b) lnwin(b) pLeadNwOut(p) ptopic(p) tcount(t,b) tUpper(t) tLower(t).
+// pot(b) lnwin(b) pLeadNwOut(p) ptopic(p) tcount(t,b) tUpper(t) tLower(t) bset(b) rbset(r) (broker sets).
 // Replica.isCurrentOffline; V::origOff(r) = isOriginalOffline || original broker dead
 template <class V>
 CCMI_HD bool currentOffline(const V& v, int r) {
@@ -151,6 +151,15 @@ CCMI_HD bool rackDistViolates(const V& v, int r, int dst) {
   return v.rackCount(p, drk) >= v.rackCount(p, srk);
 }
 
+// ---------------------------------------------------------------- BrokerSetAwareGoal
+// doesReplicaMoveViolateActionAcceptance (BrokerSetAwareGoal.java:262-275): the destination's broker set differs from
+// the set the mapping policy gives the replica
+template <class V>
+CCMI_HD bool bsetViolates(const V& v, int r, int dst) {
+  const int e = v.rbset(r);
+  return e != kBrokerSetAny && e != v.bset(dst);
+}
+
 // ---------------------------------------------------------------- CapacityGoal
 // isUtilizationUnderLimitAfterAddingLoad (host == broker: the host check is the broker check negated)
 template <class V>
@@ -225,6 +234,7 @@ CCMI_HD bool goalAcceptMove(const DevGoal& g, const V& v, int action, int r, int
     case DG_RESOURCE_DISTRIBUTION: return resAcceptMove(g, v, action, r, src, dst);
     case DG_RACK_AWARE: return action == DA_LEADERSHIP || !rackViolates(v, r, dst);
     case DG_RACK_AWARE_DISTRIBUTION: return action == DA_LEADERSHIP || !rackDistViolates(v, r, dst);
+    case DG_BROKER_SET_AWARE: return action == DA_LEADERSHIP || !bsetViolates(v, r, dst);
     case DG_REPLICA_CAPACITY: return action == DA_LEADERSHIP || (int64_t)v.nrep(dst) < g.maxReplicas;
     case DG_CAPACITY:
       if (action == DA_LEADERSHIP && (g.resource == 3 /*DISK*/ || g.resource == 1 /*NW_IN*/)) return true;
@@ -244,7 +254,8 @@ CCMI_HD bool goalSelfSatisfiedMove(const DevGoal& g, const V& v, int action, int
       return rdAccept(g, v, action, src, dst);
     case DG_RESOURCE_DISTRIBUTION: break;
     case DG_RACK_AWARE:
-    case DG_RACK_AWARE_DISTRIBUTION: return true;
+    case DG_RACK_AWARE_DISTRIBUTION:
+    case DG_BROKER_SET_AWARE: return true;
     case DG_ACCEPT_ALL: return action == DA_MOVE;  // MinTopicLeadersPerBrokerGoal moves offline replicas only
     case DG_REPLICA_CAPACITY: return (int64_t)v.nrep(dst) < g.maxReplicas;
     case DG_CAPACITY: return capUnderAfterAdding(g, v, dst, v.ru(r, g.resource));
@@ -273,6 +284,9 @@ CCMI_HD int goalAcceptSwap(const DevGoal& g, const V& v, int sr, int sb, int dr,
     case DG_RACK_AWARE_DISTRIBUTION:
       if (rackDistViolates(v, sr, db)) return 2;
       return rackDistViolates(v, dr, sb) ? 1 : 0;
+    case DG_BROKER_SET_AWARE:  // BROKER_REJECT for the source replica's side, REPLICA_REJECT for the other (:240-256)
+      if (bsetViolates(v, sr, db)) return 2;
+      return bsetViolates(v, dr, sb) ? 1 : 0;
     case DG_CAPACITY: {
       const double su = v.ru(sr, g.resource), du = v.ru(dr, g.resource);
       const double delta = du - su;

@@ -78,6 +78,8 @@ struct DevView {
   __device__ __forceinline__ int tcount(int tp, int b) const { return t.topicCount[(size_t)tp * t.ldB + b]; }
   __device__ __forceinline__ int tUpper(int tp) const { return t.tUpper[tp]; }
   __device__ __forceinline__ int tLower(int tp) const { return t.tLower[tp]; }
+  __device__ __forceinline__ int bset(int b) const { return t.brokers[b].bset; }
+  __device__ __forceinline__ int rbset(int r) const { return t.replicas[r].bset; }
 };
 
 // Row updates a cross/pair scan applies itself (instead of a separate launch): every workgroup stages the
@@ -204,6 +206,7 @@ struct PreView {
   int drack, prk0, prk1, prk2, prk3, prk4, prk5, prk6, prk7;
   double spot, dpot, plno, slbi, dlbi;
   int snlead, dnlead, topic, stc, dtc, tup, tlo;
+  int rbs, sbs, dbs;  // broker sets: the replica's (mapping policy), the source's, the destination's
   bool inelig;  // dst is one of the row's partition's ineligible brokers
 
   static __device__ __forceinline__ double sel(int k, double a, double b, double c, double d) {
@@ -239,6 +242,7 @@ struct PreView {
     p = rec.part;
     src = rec.broker;
     rflags = rec.flags;
+    rbs = rec.bset;
     ru0 = rec.util[0];
     ru1 = rec.util[1];
     ru2 = rec.util[2];
@@ -269,6 +273,7 @@ struct PreView {
     scap2 = sb.cap[2];
     scap3 = sb.cap[3];
     srcAllowed = sb.allowedBits;
+    sbs = sb.bset;
     const int pi = ov.partition(p);
     if (pi >= 0) {
       const PartitionRow& x = ov.p[pi];
@@ -335,6 +340,7 @@ struct PreView {
     dcap3 = db.cap[3];
     drack = db.rack;
     dAllowed = db.allowedBits;
+    dbs = db.bset;
     const int di = ov.broker(d);
     if (di >= 0) {
       const BrokerRow& x = ov.b[di];
@@ -401,6 +407,8 @@ struct PreView {
   __device__ __forceinline__ int tcount(int, int b) const { return b == dst ? dtc : stc; }
   __device__ __forceinline__ int tUpper(int) const { return tup; }
   __device__ __forceinline__ int tLower(int) const { return tlo; }
+  __device__ __forceinline__ int bset(int b) const { return b == dst ? dbs : sbs; }
+  __device__ __forceinline__ int rbset(int) const { return rbs; }
 
   // RackAwareGoal.rackAwareEligibleBrokers: the destination's rack is not in the partition's rack list with
   // one occurrence of the replica's own rack removed (RackAwareGoal.java:193-211).

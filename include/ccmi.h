@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define CCMI_ABI_VERSION 3
+#define CCMI_ABI_VERSION 4
 
 typedef enum ccmi_status {
   CCMI_OK = 0,
@@ -105,8 +105,15 @@ typedef enum ccmi_goal_kind {
   CCMI_GOAL_INTRA_BROKER_DISK_CAPACITY = 16,       /* IntraBrokerDiskCapacityGoal */
   CCMI_GOAL_INTRA_BROKER_DISK_USAGE_DISTRIBUTION = 17, /* IntraBrokerDiskUsageDistributionGoal */
   CCMI_GOAL_PREFERRED_LEADER_ELECTION = 18,         /* PreferredLeaderElectionGoal (not in default.goals) */
-  CCMI_GOAL_RACK_AWARE_DISTRIBUTION = 19            /* RackAwareDistributionGoal (not in default.goals) */
+  CCMI_GOAL_RACK_AWARE_DISTRIBUTION = 19,           /* RackAwareDistributionGoal (not in default.goals) */
+  CCMI_GOAL_BROKER_SET_AWARE = 20                   /* BrokerSetAwareGoal (not in default.goals) */
 } ccmi_goal_kind;
+
+/* AnalyzerConfig replica.to.broker.set.mapping.policy.class (config/ReplicaToBrokerSetMappingPolicy.java) */
+typedef enum ccmi_broker_set_policy {
+  CCMI_BROKER_SET_TOPIC_NAME_HASH = 0,  /* TopicNameHashBrokerSetMappingPolicy (the default) */
+  CCMI_BROKER_SET_ORIGINAL_BROKER = 1   /* ReplicaToOriginalBrokerSetMappingPolicy */
+} ccmi_broker_set_policy;
 
 /*
  * Flattened ClusterModel. Semantics of construction (mirrors the reference's model building):
@@ -177,6 +184,16 @@ typedef struct ccmi_balancing_constraint {
   int64_t overprovisioned_max_replicas_per_broker;
   int32_t overprovisioned_min_brokers;
   int32_t overprovisioned_min_extra_racks;
+  /* BrokerSetAwareGoal (ABI v4): BalancingConstraint.brokerSetResolver() — the broker set id -> broker ids data of
+   * BrokerSetFileResolver (config/BrokerSetFileResolver.java:42-82), whose brokers missing from every set the engine
+   * assigns as NoOpBrokerSetAssignmentPolicy does (to "unmapped", NoOpBrokerSetAssignmentPolicy.java:70-86) — and
+   * BalancingConstraint.replicaToBrokerSetMappingPolicy(). num_broker_sets = 0: no broker set data (BrokerSetAwareGoal
+   * then fails as a BrokerSetResolutionException would, CCMI_E_INVALID). Other goals ignore these fields. */
+  int32_t num_broker_sets;
+  int32_t broker_set_policy;              /* ccmi_broker_set_policy */
+  const char* const* broker_set_names;    /* [num_broker_sets] brokerSetId */
+  const int32_t* broker_set_offset;       /* [num_broker_sets + 1] CSR into broker_set_members */
+  const int32_t* broker_set_members;      /* Kafka broker ids */
 } ccmi_balancing_constraint;
 
 /* analyzer/OptimizationOptions.java (7-field form) */
@@ -294,6 +311,10 @@ void ccmi_default_constraint(ccmi_balancing_constraint* out);
 void ccmi_default_random_cluster_props(ccmi_random_cluster_props* out); /* TestConstants.BASE_PROPERTIES */
 
 ccmi_status ccmi_random_cluster(const ccmi_random_cluster_props* props, ccmi_cluster_buffers** out);
+/* TopicNameHashBrokerSetMappingPolicy.brokerSetIdForTopic (config/TopicNameHashBrokerSetMappingPolicy.java:60-70): the
+ * index, in String order of the broker set ids, of the set a topic maps to among num_broker_sets sets —
+ * Guava Hashing.consistentHash(|murmur3_128(topic, UTF-8).asInt()|, num_broker_sets). -1 if num_broker_sets < 1. */
+int32_t ccmi_topic_broker_set(const char* topic, int32_t num_broker_sets);
 const ccmi_cluster_desc* ccmi_cluster_buffers_desc(const ccmi_cluster_buffers* buf);
 void ccmi_cluster_buffers_free(ccmi_cluster_buffers* buf);
 

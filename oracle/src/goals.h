@@ -262,6 +262,32 @@ class RackAwareDistributionGoal : public AbstractGoal {
   int numRacks_ = 0;  // BalanceLimit._numAliveRacksAllowedReplicaMoves
 };
 
+//   BrokerSetAwareGoal                     analyzer/goals/BrokerSetAwareGoal.java (not in default.goals), with
+//                                          BrokerSetResolutionHelper + NoOpBrokerSetAssignmentPolicy (config/)
+class BrokerSetAwareGoal : public AbstractGoal {
+ public:
+  using AbstractGoal::AbstractGoal;
+  std::string name() const override { return "BrokerSetAwareGoal"; }
+  bool isHardGoal() const override { return true; }
+  Acceptance actionAcceptance(const BalancingAction& a, ClusterModel& cm) override;
+  int compareStats(const ClusterModelStats&, const ClusterModelStats&) const override { return 0; }
+
+ protected:
+  void initGoalState(ClusterModel& cm, const OptimizationOptions& o) override;
+  void updateGoalState(ClusterModel& cm, const OptimizationOptions& o) override;
+  void rebalanceForBroker(int broker, ClusterModel& cm, const GoalList& g, const OptimizationOptions& o) override;
+  bool selfSatisfied(ClusterModel&, const BalancingAction&) override { return true; }
+
+ private:
+  std::string brokerSetId(int brokerId) const;                      // BrokerSetResolutionHelper.brokerSetId
+  std::string brokerSetIdForReplica(ClusterModel& cm, int replica);  // ReplicaToBrokerSetMappingPolicy
+  bool violates(ClusterModel& cm, int replica, int destBroker);
+  std::map<std::string, std::set<int>> brokersByBrokerSet_;  // broker ids
+  std::map<int, std::string> brokerSetIdByBrokerId_;
+  std::map<std::string, std::string> brokerSetIdByTopic_;    // TopicNameHashBrokerSetMappingPolicy cache
+  std::set<int> excludedTopics_;
+};
+
 class MinTopicLeadersPerBrokerGoal : public AbstractGoal {
  public:
   using AbstractGoal::AbstractGoal;

@@ -6,6 +6,7 @@
 #include <algorithm>
 #include <cmath>
 
+#include "brokersets.h"
 #include "goals.h"
 
 namespace oracle {
@@ -1334,6 +1335,148 @@ void LeaderBytesInDistributionGoal::rebalanceForBroker(int b, ClusterModel& cm, 
     over = cm.leadershipNwIn(b) > thr;
   }
   if (over) overLimit_ = true;
+}
+
+}  // namespace oracle
+
+namespace oracle {
+
+// ===================================================================== BrokerSetAwareGoal (BrokerSetAwareGoal.java)
+
+// initGoalState (:80-129): BrokerSetResolutionHelper over the resolver data with NoOpBrokerSetAssignmentPolicy's
+// rackIdByBrokerId form (NoOpBrokerSetAssignmentPolicy.java:70-86: every broker in no set joins "unmapped")
+void BrokerSetAwareGoal::initGoalState(ClusterModel& cm, const OptimizationOptions& o) {
+  int n = 0;
+  allowedForReplicaMove(cm, o, &n);
+  if (n == 0) {
+    ProvisionRec rec;
+    rec.numBrokers = cm.maxReplicationFactor;
+    throw OptimizationFailure("[" + name() + "] All alive brokers are excluded from replica moves.", rec);
+  }
+  excludedTopics_.clear();  // no MinTopicLeadersPerBroker topics are configured
+  excludedTopics_.insert(o.excludedTopics.begin(), o.excludedTopics.end());
+  SortSpec spec;
+  if (o.onlyMoveImmigrantReplicas) spec.selection.push_back({SelFn::IMMIGRANTS});
+  if (!o.excludedTopics.empty()) spec.selection.push_back({SelFn::EXCLUDED_TOPICS});
+  for (size_t b = 0; b < cm.brokers.size(); ++b) cm.trackSortedReplicas((int)b, replicaSortName(false, false), spec);
+  if (bc_.brokerSets.empty()) throw std::invalid_argument("[" + name() + "] no broker sets (BrokerSetResolutionException)");
+  brokersByBrokerSet_.clear();
+  brokerSetIdByBrokerId_.clear();
+  brokerSetIdByTopic_.clear();
+  std::set<int> mapped;
+  for (const auto& kv : bc_.brokerSets)
+    for (int id : kv.second) {
+      brokersByBrokerSet_[kv.first].insert(id);
+      mapped.insert(id);
+    }
+  for (const auto& br : cm.brokers)
+    if (!mapped.count(br.id)) brokersByBrokerSet_["unmapped"].insert(br.id);
+  for (const auto& kv : brokersByBrokerSet_)
+    for (int id : kv.second) brokerSetIdByBrokerId_[id] = kv.first;
+}
+
+std::string BrokerSetAwareGoal::brokerSetId(int brokerId) const {
+  auto it = brokerSetIdByBrokerId_.find(brokerId);
+  if (it == brokerSetIdByBrokerId_.end())
+    throw std::invalid_argument("Failed to resolve BrokerSet for Broker " + std::to_string(brokerId));
+  return it->second;
+}
+
+std::string BrokerSetAwareGoal::brokerSetIdForReplica(ClusterModel& cm, int r) {
+  if (bc_.brokerSetPolicy == 1)  // ReplicaToOriginalBrokerSetMappingPolicy.java:20-26
+    return brokerSetId(cm.brokers[cm.replicas[r].origBroker].id);
+  // TopicNameHashBrokerSetMappingPolicy.java:30-70: consistent hash of the topic over the sorted set ids
+  const std::string& topic = cm.topicNames[cm.partitions[cm.replicas[r].partition].topic];
+  auto it = brokerSetIdByTopic_.find(topic);
+  if (it != brokerSetIdByTopic_.end()) return it->second;
+  std::vector<std::string> sorted;
+  for (const auto& kv : brokersByBrokerSet_) sorted.push_back(kv.first);
+  std::sort(sorted.begin(), sorted.end());
+  const std::string id = sorted[topicNameHashBucket(topic, (int)sorted.size())];
+  brokerSetIdByTopic_[topic] = id;
+  return id;
+}
+
+// doesReplicaMoveViolateActionAcceptance (:262-275)
+bool BrokerSetAwareGoal::violates(ClusterModel& cm, int r, int dst) {
+  try {
+    return brokerSetIdForReplica(cm, r) != brokerSetId(cm.brokers[dst].id);
+  } catch (std::invalid_argument&) {
+    return true;
+  }
+}
+
+// actionAcceptance (:229-257)
+Acceptance BrokerSetAwareGoal::actionAcceptance(const BalancingAction& a, ClusterModel& cm) {
+  switch (a.type) {
+    case ActionType::LEADERSHIP_MOVEMENT:
+      return Acceptance::ACCEPT;
+    case ActionType::INTER_BROKER_REPLICA_MOVEMENT:
+    case ActionType::INTER_BROKER_REPLICA_SWAP:
+      if (violates(cm, cm.replicaOnBroker(a.partition, a.sourceBroker), a.destinationBroker))
+        return Acceptance::BROKER_REJECT;
+      if (a.type == ActionType::INTER_BROKER_REPLICA_SWAP &&
+          violates(cm, cm.replicaOnBroker(a.destPartition, a.destinationBroker), a.sourceBroker))
+        return Acceptance::REPLICA_REJECT;
+      return Acceptance::ACCEPT;
+    default:
+      throw std::invalid_argument("Unsupported balancing action");
+  }
+}
+
+// rebalanceForBroker (:159-188)
+void BrokerSetAwareGoal::rebalanceForBroker(int b, ClusterModel& cm, const GoalList& g, const OptimizationOptions& o) {
+  const std::string current = brokerSetId(cm.brokers[b].id);
+  for (int r : cm.sortedReplicasClone(b, replicaSortName(false, false))) {
+    const std::string want = brokerSetIdForReplica(cm, r);
+    if (cm.brokers[b].isAlive() && want == current) continue;
+    std::vector<int> in;  // aliveBrokers() filtered by the set, Collectors.toSet()
+    for (int x : cm.aliveBrokers())
+      if (brokersByBrokerSet_.at(want).count(cm.brokers[x].id)) in.push_back(x);
+    const std::vector<int> eligible = javaHashSetOrderIntKeys(in);
+    if (maybeApplyBalancingAction(cm, r, eligible, ActionType::INTER_BROKER_REPLICA_MOVEMENT, g, o) < 0) {
+      std::string ids = "[";
+      for (size_t i = 0; i < eligible.size(); ++i) ids += (i ? ", " : "") + std::to_string(cm.brokers[eligible[i]].id);
+      ProvisionRec rec;
+      rec.numBrokers = cm.maxReplicationFactor;
+      const int p = cm.replicas[r].partition;
+      throw OptimizationFailure("[" + name() + "] Cannot move replica " + cm.topicNames[cm.partitions[p].topic] + "-" +
+                                    std::to_string(cm.partitions[p].number) + " on broker " +
+                                    std::to_string(cm.brokers[b].id) + " to " + ids + "] on brokerSet " + want,
+                                rec);
+    }
+  }
+}
+
+// updateGoalState (:139-147) + ensureBrokerSetAware (:149-167) over getPartitionsByTopic (a TreeMap by name)
+void BrokerSetAwareGoal::updateGoalState(ClusterModel& cm, const OptimizationOptions& o) {
+  ensureNoOfflineReplicas(cm, name());
+  ensureReplicasMoveOffBrokersWithBadDisks(cm, name());
+  std::map<std::string, std::vector<int>> byTopic;
+  for (size_t p = 0; p < cm.partitions.size(); ++p) byTopic[cm.topicNames[cm.partitions[p].topic]].push_back((int)p);
+  for (const auto& kv : byTopic) {
+    const int t = cm.partitions[kv.second.front()].topic;
+    if (excludedTopics_.count(t)) continue;
+    std::set<int> ids;
+    std::vector<int> insertion;
+    for (int p : kv.second)
+      for (int r : cm.partitions[p].replicas) {
+        const int id = cm.brokers[cm.replicas[r].broker].id;
+        if (ids.insert(id).second) insertion.push_back(id);
+      }
+    bool contained = false;
+    for (const auto& bs : brokersByBrokerSet_) {
+      bool all = true;
+      for (int id : ids) all = all && bs.second.count(id);
+      contained = contained || all;
+    }
+    if (contained) continue;
+    std::string s = "[";
+    const std::vector<int> order = javaHashSetOrderIntKeys(insertion);
+    for (size_t i = 0; i < order.size(); ++i) s += (i ? ", " : "") + std::to_string(order[i]);
+    throw OptimizationFailure("[" + name() + "] Topic " + kv.first + " is not brokerSet-aware. brokers (" + s + "]).");
+  }
+  finished_ = true;
 }
 
 }  // namespace oracle

@@ -30,6 +30,7 @@ std::unique_ptr<Goal> makeGoal(int kind, const BalancingConstraint& bc) {
       return std::make_unique<IntraBrokerDiskUsageDistributionGoal>(bc);
     case CCMI_GOAL_PREFERRED_LEADER_ELECTION: return std::make_unique<PreferredLeaderElectionGoal>(bc);
     case CCMI_GOAL_RACK_AWARE_DISTRIBUTION: return std::make_unique<RackAwareDistributionGoal>(bc);
+    case CCMI_GOAL_BROKER_SET_AWARE: return std::make_unique<BrokerSetAwareGoal>(bc);
     default: throw std::invalid_argument("goal kind not in oracle scope: " + std::to_string(kind));
   }
 }

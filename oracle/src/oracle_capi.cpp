@@ -6,6 +6,7 @@
 #include <string>
 
 #include "../../include/ccmi.h"
+#include "brokersets.h"
 #include "optimizer.h"
 #include "random_cluster.h"
 
@@ -36,6 +37,11 @@ BalancingConstraint toBc(const ccmi_balancing_constraint* c) {
   bc.overprovisionedMaxReplicasPerBroker = c->overprovisioned_max_replicas_per_broker;
   bc.overprovisionedMinBrokers = c->overprovisioned_min_brokers;
   bc.overprovisionedMinExtraRacks = c->overprovisioned_min_extra_racks;
+  for (int i = 0; i < c->num_broker_sets; ++i) {
+    auto& v = bc.brokerSets[c->broker_set_names[i]];
+    for (int k = c->broker_set_offset[i]; k < c->broker_set_offset[i + 1]; ++k) v.push_back(c->broker_set_members[k]);
+  }
+  bc.brokerSetPolicy = c->broker_set_policy;
   return bc;
 }
 
@@ -379,6 +385,11 @@ int32_t oc_action_acceptance(void* hv, int32_t gi, const ccmi_action* a) {
     h->err = e.what();
     return -1;
   }
+}
+
+// TopicNameHashBrokerSetMappingPolicy's bucket for a topic among num_sets sorted broker set ids
+int32_t oc_topic_broker_set(const char* topic, int32_t num_sets) {
+  return num_sets < 1 ? -1 : topicNameHashBucket(topic, num_sets);
 }
 
 int64_t oc_action_count(void* hv) { return (int64_t)((Handle*)hv)->cm.actionLog.size(); }

@@ -3,6 +3,9 @@
 // plus the BalancingConstraint analyzer knobs it reads (analyzer/BalancingConstraint.java:54-105,
 // defaults config/constants/AnalyzerConfig.java:58-464).
 #pragma once
+#include <map>
+#include <string>
+#include <vector>
 #include "model.h"
 
 namespace oracle {
@@ -21,6 +24,10 @@ struct BalancingConstraint {
   int64_t overprovisionedMaxReplicasPerBroker = 1500;
   int overprovisionedMinBrokers = 3;
   int overprovisionedMinExtraRacks = 2;  // AnalyzerConfig.DEFAULT_OVERPROVISIONED_MIN_EXTRA_RACKS
+  // BrokerSetAwareGoal: brokerSetResolver() data (BrokerSetFileResolver: broker set id -> broker ids) and
+  // replicaToBrokerSetMappingPolicy() (0 TopicNameHash, 1 ReplicaToOriginal)
+  std::map<std::string, std::vector<int>> brokerSets;
+  int brokerSetPolicy = 0;
 };
 
 struct ClusterModelStats {

@@ -31,7 +31,7 @@ struct Emu {
   int B, R, P, T, ldB, G;
   std::vector<double> bUtil, bCap, bPot, rUtil, bLeadNwIn, pLeadNwOut;
   std::vector<int32_t> bNrep, bNlead, rPart, rBroker, rOrig, pOff, pBrokers, topicCount, topicNrep;
-  std::vector<int32_t> bRack, pTopic, tUpper, tLower;
+  std::vector<int32_t> bRack, pTopic, tUpper, tLower, bSet, rSet;
   std::vector<int32_t> pIneligOff, pIneligB;  // Partition._ineligibleBrokers (empty: none)
   std::vector<uint8_t> bAlive, rFlags;
   std::vector<uint32_t> allowed;
@@ -94,6 +94,8 @@ struct View {
   int tcount(int t, int b) const { return e.topicCount[(size_t)t * e.ldB + b]; }
   int tUpper(int t) const { return e.tUpper[t]; }
   int tLower(int t) const { return e.tLower[t]; }
+  int bset(int b) const { return e.bSet.empty() ? -1 : e.bSet[b]; }
+  int rbset(int r) const { return e.rSet.empty() ? -1 : e.rSet[r]; }
   // RackAwareGoal.rackAwareEligibleBrokers membership for (replica r, destination d)
   bool rackEligible(int r, int d) const {
     std::vector<int> racks;
@@ -176,6 +178,11 @@ void Device::setExclusions(const uint8_t* lead, const uint8_t* move, const uint8
 void Device::setTopicLimits(const int32_t* upper, const int32_t* lower) {
   E(st_).tUpper.assign(upper, upper + T_);
   E(st_).tLower.assign(lower, lower + T_);
+}
+
+void Device::setBrokerSets(const int32_t* brokerSet, const int32_t* replicaSet) {
+  E(st_).bSet.assign(brokerSet, brokerSet + B_);
+  E(st_).rSet.assign(replicaSet, replicaSet + R_);
 }
 
 void Device::flushPending() { flushOnly(); }

@@ -57,6 +57,8 @@ class Oracle:
             L.oc_action_count.argtypes = [C.c_void_p]
             L.oc_actions.argtypes = [C.c_void_p, C.POINTER(ccmi.ActionStruct)]
             L.oc_last_failure_provision.argtypes = [C.c_void_p, C.POINTER(ccmi.ProvisionRespStruct)]
+            L.oc_topic_broker_set.restype = C.c_int32
+            L.oc_topic_broker_set.argtypes = [C.c_char_p, C.c_int32]
             L.oc_action_acceptance.restype = C.c_int32
             L.oc_action_acceptance.argtypes = [C.c_void_p, C.c_int32, C.POINTER(ccmi.ActionStruct)]
             L.oc_apply.restype = C.c_int32
