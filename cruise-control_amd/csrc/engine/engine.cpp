@@ -537,6 +537,7 @@ class LiveQueue {
   void init(int /*capacity*/, bool ordered) { ordered_ = ordered; }
   bool ordered() const { return ordered_; }
   void push_sorted(int x) { oq_.sorted().push_back(x); }
+  std::vector<int>& sortedRun() { return oq_.sorted(); }
   bool empty() const { return ordered_ ? oq_.empty() : pq_.empty(); }
   int peek() const { return ordered_ ? oq_.peek() : pq_.peek(); }
   int poll() { return ordered_ ? oq_.poll() : pq_.poll(); }
@@ -808,6 +809,8 @@ class ResourceDistribution : public GoalImpl {
   int res = 0;
   double upperThr = 0, lowerThr = 0;
   bool fix = false;
+  bool exclAlive = false;                 // an alive broker is excluded for replica moves
+  bool posCap = true;                     // every broker has a positive capacity of `res`
   bool lowUtil = false;                   // _isLowUtilization
   ccmi_provision_recommendation overRec{};  // _overProvisionedRecommendation
   Model::SnapTable snapTab;  // moveIn's candidate-broker snapshots (one Spec per phase)
@@ -844,6 +847,12 @@ class ResourceDistribution : public GoalImpl {
       }
     if (n == 0)
       throw OptimizationFailure("[" + name + "] All alive brokers are excluded from replica moves.", underBrokers(m.maxRf));
+    exclAlive = false;
+    posCap = true;
+    for (int b = 0; b < m.B; ++b) {
+      exclAlive |= m.alive(b) && !allowed[b];
+      posCap &= m.cap(b, res) > 0;
+    }
     fix = false;
     const double util = m.clusterUtil(res);
     const double capacity = m.capacityWithAllowedReplicaMoves(res, e.opt.exclMove);
@@ -1003,11 +1012,28 @@ class ResourceDistribution : public GoalImpl {
     std::vector<int32_t> inorder;
     {
       PhaseScope pi(PH_PQ_INIT);
-      for (int x : m.brokersByPct(res)) {
-        if (!m.alive(x)) continue;
-        if (!fix && m.bu(x, res) >= m.cap(x, res) * upperThr) continue;  // aliveBrokersUnderThreshold
-        inSet[x] = 1;
-        inorder.push_back(x);
+      const auto& ord = m.brokersByPct(res);
+      auto under = [&](int x) { return fix || m.bu(x, res) < m.cap(x, res) * upperThr; };  // aliveBrokersUnderThreshold
+      if (m.numDead == 0 && posCap && !ord.empty() && upperThr > 0) {
+        // every broker alive with a positive capacity: membership is a prefix of the (pct, id) order except within a
+        // relative 1e-9 band around the threshold, where the exact product test decides each broker
+        size_t lo = (size_t)(std::partition_point(ord.begin(), ord.end(),
+                                                  [&](int x) { return m.pct(x, res) < upperThr * (1 - 1e-9); }) -
+                             ord.begin());
+        size_t hi = (size_t)(std::partition_point(ord.begin() + lo, ord.end(),
+                                                        [&](int x) { return m.pct(x, res) <= upperThr * (1 + 1e-9); }) -
+                                   ord.begin());
+        if (fix) lo = hi = ord.size();
+        inorder.assign(ord.begin(), ord.begin() + lo);
+        for (size_t k = lo; k < hi; ++k)
+          if (under(ord[k])) inorder.push_back(ord[k]);
+        for (int x : inorder) inSet[x] = 1;
+      } else {
+        for (int x : ord) {
+          if (!m.alive(x) || !under(x)) continue;
+          inSet[x] = 1;
+          inorder.push_back(x);
+        }
       }
     }
     struct Step {
@@ -1218,12 +1244,22 @@ class ResourceDistribution : public GoalImpl {
       auto member = [&](int c) { return m.alive(c) && m.pct(c, res) > (excluded(c) ? 0.0 : lowerThr); };
       // only b's key changes while brokers are queued (moves go cb -> b, cb polled): exact unless b is queued
       pq.init(m.B, !member(b));
-      queued.assign(m.B, 0);
-      for (auto it = ord.rbegin(); it != ord.rend(); ++it)
-        if (member(*it)) {
-          pq.push_sorted(*it);
-          queued[*it] = 1;
-        }
+      const bool lead = action == DA_LEADERSHIP;  // `queued` is read by the leadership driver only
+      if (lead) queued.assign(m.B, 0);
+      if (pq.ordered() && m.numDead == 0 && !exclAlive && !ord.empty() && m.pct(ord.back(), res) == m.pct(ord.back(), res)) {
+        // every broker is alive and allowed, and no key is NaN: the members are exactly the suffix of the (pct, id)
+        // order above the lower threshold, queued in reverse
+        const auto first = std::partition_point(ord.begin(), ord.end(), [&](int c) { return !(m.pct(c, res) > lowerThr); });
+        pq.sortedRun().assign(ord.rbegin(), std::make_reverse_iterator(first));
+        if (lead)
+          for (int c : pq.sortedRun()) queued[c] = 1;
+      } else {
+        for (auto it = ord.rbegin(); it != ord.rend(); ++it)
+          if (member(*it)) {
+            pq.push_sorted(*it);
+            if (lead) queued[*it] = 1;
+          }
+      }
       if (!pq.ordered())
         for (int c = 0; c < m.B; ++c)
           if (member(c)) pq.add(c);
