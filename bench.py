@@ -290,11 +290,16 @@ def main() -> None:
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", init_method="env://")
-    device = local_rank if world > 1 else 0
+    ndev = max(1, torch.cuda.device_count())
+    # one rank per GPU with the bookkeeping collectives over RCCL; more ranks than GPUs (a rehearsal of the N-rank
+    # path on a smaller box) share the cards round-robin and time over gloo (RCCL refuses two ranks on one GPU)
+    over_gloo = world > ndev
+    device = local_rank % ndev if world > 1 else 0
     torch.cuda.set_device(device)
+    if world > 1:
+        dist.init_process_group("gloo" if over_gloo else "nccl", init_method="env://")
+    if over_gloo and args.sharded:
+        raise SystemExit("--sharded needs one GPU per rank (the RCCL combiner)")
 
     lib = ccmi.Library.get()
     props, goal_names, workload_name = WORKLOADS[args.workload]
@@ -354,7 +359,7 @@ def main() -> None:
 
     cands = sum(r.candidates for r in results)
     if world > 1:
-        t = torch.tensor([elapsed, float(cands)], dtype=torch.float64, device=f"cuda:{device}")
+        t = torch.tensor([elapsed, float(cands)], dtype=torch.float64, device="cpu" if over_gloo else f"cuda:{device}")
         tmax = t.clone()
         dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
         dist.all_reduce(t, op=dist.ReduceOp.SUM)
