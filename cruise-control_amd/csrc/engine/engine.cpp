@@ -1492,6 +1492,14 @@ class ResourceDistribution : public GoalImpl {
     }
     const Model::Spec candSpec = out ? candidateSpec(e, limit, true, followersOnly, false, immOnly)
                                      : candidateSpec(e, limit, false, followersOnly, res == R_NW_OUT, immOnly);
+    // The limit filter does not enter the sort key, so a candidate's list is its limit-free sorted snapshot (cached
+    // per broker version across swap calls with different limits) filtered by the limit: the same list, no re-sort.
+    Model::Spec baseSpec = candSpec;
+    const Model::Spec noLimit;
+    baseSpec.selAboveRes = noLimit.selAboveRes;
+    baseSpec.aboveLimit = noLimit.aboveLimit;
+    baseSpec.selBelowRes = noLimit.selBelowRes;
+    baseSpec.belowLimit = noLimit.belowLimit;
     std::vector<int32_t> srcs, cbOff, cbRep, polled;
     size_t target = 4;
     while (!pqEmpty()) {
@@ -1501,8 +1509,9 @@ class ResourceDistribution : public GoalImpl {
       while (!pqEmpty() && (polled.empty() || polled.size() < target)) {
         const int cb = pqPoll();
         polled.push_back(cb);
-        const auto v = m.snapshot(cb, candSpec);
-        cbRep.insert(cbRep.end(), v->begin(), v->end());
+        const auto v = m.snapshot(cb, baseSpec);
+        for (int r : *v)
+          if (m.selects(candSpec, r)) cbRep.push_back(r);
         cbOff.push_back((int32_t)cbRep.size());
       }
       srcs = *m.snapshot(b, srcSpec);
