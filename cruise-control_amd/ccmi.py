@@ -89,7 +89,8 @@ class ClusterDesc(C.Structure):
                 ("num_disks", C.c_int32), ("disk_broker", C.POINTER(C.c_int32)),
                 ("disk_logdir", C.POINTER(C.c_char_p)), ("disk_capacity", C.POINTER(C.c_double)),
                 ("replica_disk", C.POINTER(C.c_int32)), ("num_disk_assignments", C.c_int32),
-                ("disk_assign_replica", C.POINTER(C.c_int32)), ("disk_assign_disk", C.POINTER(C.c_int32))]
+                ("disk_assign_replica", C.POINTER(C.c_int32)), ("disk_assign_disk", C.POINTER(C.c_int32)),
+                ("num_replica_loads", C.c_int32)]
 
 
 class ConstraintStruct(C.Structure):
@@ -102,7 +103,8 @@ class ConstraintStruct(C.Structure):
                 ("overprovisioned_min_brokers", C.c_int32), ("overprovisioned_min_extra_racks", C.c_int32),
                 ("num_broker_sets", C.c_int32), ("broker_set_policy", C.c_int32),
                 ("broker_set_names", C.POINTER(C.c_char_p)), ("broker_set_offset", C.POINTER(C.c_int32)),
-                ("broker_set_members", C.POINTER(C.c_int32))]
+                ("broker_set_members", C.POINTER(C.c_int32)), ("min_leader_topics", C.POINTER(C.c_int32)),
+                ("num_min_leader_topics", C.c_int32), ("min_topic_leaders_per_broker", C.c_int32)]
 
 
 class OptionsStruct(C.Structure):
@@ -309,6 +311,11 @@ class BalancingConstraint:
     # set join "unmapped" (NoOpBrokerSetAssignmentPolicy, the default broker.set.assignment.policy.class).
     broker_sets: Optional[Dict[str, Sequence[int]]] = None
     broker_set_policy: str = "TopicNameHashBrokerSetMappingPolicy"
+    # topics.with.min.leaders.per.broker (a regex; "" matches no topic) and min.topic.leaders.per.broker
+    # (AnalyzerConfig.java:401-414). The pattern is matched against the session's topic names as
+    # Utils.getTopicNamesMatchedWithPattern does (Pattern.matcher(topic).matches() = re.fullmatch; common/Utils.java:26-36).
+    topics_with_min_leaders_per_broker: str = ""
+    min_topic_leaders_per_broker: int = 1
 
     def set_resource_balance_percentage(self, p: float) -> None:  # BalancingConstraint.setResourceBalancePercentage
         self.resource_balance_percentage = (p, p, p, p)
@@ -316,7 +323,17 @@ class BalancingConstraint:
     def set_capacity_threshold(self, t: float) -> None:
         self.capacity_threshold = (t, t, t, t)
 
-    def to_struct(self) -> ConstraintStruct:
+    def min_leader_topics(self, topic_names: Optional[Sequence[str]]) -> List[int]:
+        """Topic indices topics.with.min.leaders.per.broker matches (Utils.getTopicNamesMatchedWithPattern)."""
+        if not self.topics_with_min_leaders_per_broker:
+            return []
+        import re
+        pat = re.compile(self.topics_with_min_leaders_per_broker)
+        if topic_names is None:
+            raise IllegalArgumentException("topics.with.min.leaders.per.broker needs the cluster's topic names")
+        return [t for t, n in enumerate(topic_names) if pat.fullmatch(n)]
+
+    def to_struct(self, topic_names: Optional[Sequence[str]] = None) -> ConstraintStruct:
         s = ConstraintStruct()
         s.resource_balance_percentage[:] = list(self.resource_balance_percentage)
         s.capacity_threshold[:] = list(self.capacity_threshold)
@@ -347,6 +364,15 @@ class BalancingConstraint:
         if self.broker_set_policy not in BROKER_SET_POLICIES:
             raise IllegalArgumentException(f"unknown broker set mapping policy {self.broker_set_policy}")
         s.broker_set_policy = BROKER_SET_POLICIES[self.broker_set_policy]
+        if self.min_topic_leaders_per_broker < 0:  # ConfigDef atLeast(0)
+            raise IllegalArgumentException("min.topic.leaders.per.broker must be at least 0")
+        s.min_topic_leaders_per_broker = self.min_topic_leaders_per_broker
+        mlt = self.min_leader_topics(topic_names)
+        if mlt:
+            a = (C.c_int32 * len(mlt))(*mlt)
+            s._keep_mlt = a
+            s.min_leader_topics = C.cast(a, C.POINTER(C.c_int32))
+            s.num_min_leader_topics = len(mlt)
         return s
 
 
@@ -403,9 +429,14 @@ class Goal:
     def kind(self) -> int:
         return GOAL_KINDS[self._name]
 
+    # Goal.isHardGoal(): AbstractRackAwareGoal (both rack goals), BrokerSetAwareGoal, CapacityGoal, ReplicaCapacityGoal,
+    # IntraBrokerDiskCapacityGoal return true (analyzer/goals/*.java)
+    HARD_GOALS = ("RackAwareGoal", "RackAwareDistributionGoal", "BrokerSetAwareGoal", "ReplicaCapacityGoal",
+                  "DiskCapacityGoal", "NetworkInboundCapacityGoal", "NetworkOutboundCapacityGoal", "CpuCapacityGoal",
+                  "IntraBrokerDiskCapacityGoal")
+
     def is_hard_goal(self) -> bool:
-        return self._name in ("RackAwareGoal", "ReplicaCapacityGoal", "DiskCapacityGoal", "NetworkInboundCapacityGoal", "NetworkOutboundCapacityGoal",
-                              "CpuCapacityGoal")
+        return self._name in self.HARD_GOALS
 
     def optimize(self, cluster: "ClusterModel", options: Optional[OptimizationOptions] = None) -> bool:
         """Goal.optimize: the session remembers this goal as optimized afterwards."""
@@ -821,8 +852,7 @@ class FlatCluster:
         if sorted(bld.brokers) != list(range(B)):
             raise IllegalArgumentException("broker ids must be 0..B-1")
         R, P, T, W = len(bld.rep_part), len(bld.part_list), len(bld.topics), bld.W
-        if any(x is None for x in bld.rep_load):
-            raise IllegalStateException("a replica has no load")
+        # a replica without setReplicaLoad keeps an empty Load (it is left out of replica_load_order)
         arr = lambda ct, xs: (ct * max(1, len(xs)))(*xs)  # noqa: E731
         self.keep = dict(
             broker_id=arr(C.c_int32, list(range(B))),
@@ -835,7 +865,7 @@ class FlatCluster:
             partition_replicas=arr(C.c_int32, [r for lst in bld.part_list for r in lst]),
             replica_partition=arr(C.c_int32, bld.rep_part), replica_broker=arr(C.c_int32, bld.rep_broker),
             replica_is_leader=arr(C.c_uint8, bld.rep_leader), replica_offline=arr(C.c_uint8, bld.rep_offline),
-            replica_load=arr(C.c_float, [x for r in range(R) for x in bld.rep_load[r] for _ in range(W)]),
+            replica_load=arr(C.c_float, [x for r in range(R) for x in (bld.rep_load[r] or [0.0] * 6) for _ in range(W)]),
             replica_load_order=arr(C.c_int32, bld.load_order))
         D = len(bld.disks)
         if D:
@@ -855,6 +885,7 @@ class FlatCluster:
         d.num_windows, d.num_racks, d.num_brokers = W, len(bld.rack_index), B
         d.num_topics, d.num_partitions, d.num_replicas = T, P, R
         d.num_disks = D
+        d.num_replica_loads = len(bld.load_order)
         for k, v in self.keep.items():
             setattr(d, k, C.cast(v, type(getattr(d, k))) if k not in ("topic_names", "disk_logdir") else v)
         self.desc = d
@@ -978,7 +1009,7 @@ class ClusterModel:
     def _goal_optimize(self, goal: Goal, options: Optional[OptimizationOptions]) -> GoalResultStruct:
         res = GoalResultStruct()
         o, keep = (options or OptimizationOptions()).to_struct()
-        c = (goal.constraint or BalancingConstraint()).to_struct()
+        c = (goal.constraint or BalancingConstraint()).to_struct(self.topic_names())
         self._checked(self.lib.lib.ccmi_goal_optimize(self.handle, goal.kind, C.byref(c), C.byref(o), C.byref(res)))
         goal.provision = ProvisionResponse.from_struct(res.provision, goal.name())
         return res
@@ -1031,7 +1062,7 @@ class ClusterModel:
                       options: Optional[OptimizationOptions] = None) -> Dict[str, object]:
         s = StatsStruct()
         o, keep = (options or OptimizationOptions()).to_struct()
-        c = (constraint or BalancingConstraint()).to_struct()
+        c = (constraint or BalancingConstraint()).to_struct(self.topic_names())
         self.lib.check(self.lib.lib.ccmi_compute_cluster_stats(self.handle, C.byref(c), C.byref(o), C.byref(s)))
         return stats_to_dict(s)
 
@@ -1139,7 +1170,7 @@ class GoalOptimizer:
         kinds = (C.c_int32 * len(goals_by_priority))(*[g.kind for g in goals_by_priority])
         results = (GoalResultStruct * len(goals_by_priority))()
         o, keep = (options or OptimizationOptions()).to_struct()
-        c = self.constraint.to_struct()
+        c = self.constraint.to_struct(cluster.topic_names())
         import time
         t0 = time.perf_counter()
         cluster._checked(cluster.lib.lib.ccmi_optimizations(cluster.handle, kinds, len(goals_by_priority),

@@ -1,5 +1,6 @@
 // C ABI of libccmi.so (include/ccmi.h). Exceptions never cross the boundary: every entry point maps them to a
 // ccmi_status and keeps the message for ccmi_last_error() (thread-local).
+#include <algorithm>
 #include <cstring>
 #include <memory>
 #include <mutex>
@@ -91,6 +92,18 @@ void setOptions(ccmi_session* s, const ccmi_balancing_constraint* c, const ccmi_
   e.bc.overMinBrokers = c->overprovisioned_min_brokers;
   e.bc.overprovisionedMinExtraRacks = c->overprovisioned_min_extra_racks;
   e.brokerSets.resolve(c, s->model.bId);
+  e.bc.minLeaderTopics.clear();
+  if (c->num_min_leader_topics > 0 && !c->min_leader_topics) throw std::invalid_argument("null min_leader_topics");
+  for (int i = 0; i < c->num_min_leader_topics; ++i) {
+    const int t = c->min_leader_topics[i];
+    if (t < 0 || t >= s->model.T) throw std::invalid_argument("min-leader topic out of range");
+    e.bc.minLeaderTopics.push_back(t);
+  }
+  std::sort(e.bc.minLeaderTopics.begin(), e.bc.minLeaderTopics.end());
+  e.bc.minLeaderTopics.erase(std::unique(e.bc.minLeaderTopics.begin(), e.bc.minLeaderTopics.end()),
+                             e.bc.minLeaderTopics.end());
+  if (c->min_topic_leaders_per_broker < 0) throw std::invalid_argument("min.topic.leaders.per.broker must be >= 0");
+  e.bc.minTopicLeadersPerBroker = c->min_topic_leaders_per_broker;
   const int B = s->model.B;
   ccmi::Options opt;
   opt.exclMove.assign(B, 0);
@@ -128,6 +141,9 @@ void setOptions(ccmi_session* s, const ccmi_balancing_constraint* c, const ccmi_
   }
   e.opt = std::move(opt);
   s->model.setExcludedTopicSelection(e.opt.exclTopic);
+  std::vector<uint8_t> must(s->model.T, 0);
+  for (int t : e.bc.minLeaderTopics) must[t] = 1;
+  s->model.setMustTopicSelection(must);
 }
 
 std::vector<int32_t> replicaDist(const ccmi::Model& m) {
@@ -221,6 +237,7 @@ void ccmi_default_constraint(ccmi_balancing_constraint* c) {
   c->overprovisioned_max_replicas_per_broker = 1500;
   c->overprovisioned_min_brokers = 3;
   c->overprovisioned_min_extra_racks = 2;
+  c->min_topic_leaders_per_broker = 1;  // AnalyzerConfig.DEFAULT_MIN_TOPIC_LEADERS_PER_BROKER
 }
 
 void ccmi_default_random_cluster_props(ccmi_random_cluster_props* p) {
@@ -422,6 +439,13 @@ ccmi_status ccmi_action_acceptance_by_kind(ccmi_session* s, int32_t kind, const 
 
 ccmi_status ccmi_session_apply(ccmi_session* s, const ccmi_action* actions, int64_t n, int64_t* applied) {
   if (applied) *applied = 0;
+  // the proposals are the diff against the initial placement after every action applied, also when a later one fails
+  struct Rebuild {
+    ccmi_session* s;
+    ~Rebuild() {
+      if (s) buildProposals(s);
+    }
+  } rebuild{s};
   return guarded([&] {
     if (!s || (n > 0 && !actions) || n < 0) throw std::invalid_argument("null argument");
     ccmi::Model& m = s->model;

@@ -45,7 +45,7 @@ CCMI_LD void ldAddSignedAll(LoadVec& d, const LoadVec& s, int W, bool neg) {
 
 // S provides: W; LoadVec& rLoad(r), bLoad(b), bLnw(b), bPot(b), scratch(i) (i = 0, 1: step-to-step values);
 // ReplicaRec& rep(r); BrokerRec& brk(b); PartitionRec& part(p); int& slot(p, i) (replica id of partition slot i);
-// int& leader(p); void topicAdd(t, b, d).
+// int& leader(p); void topicAdd(t, b, d); void topicLeadAdd(t, b, d) (a no-op unless leader counts are kept).
 
 // ---- relocateReplica(tp, src, dst) of replica r: lanes 0..5, then applyReplicaFinish
 //   lane 0/1 Broker.load() of src (-= r) / dst (+= r)         -> util[4]
@@ -91,6 +91,10 @@ CCMI_LD void applyReplicaFinish(S& s, int r, int src, int dst, bool lead) {
     }
   s.topicAdd(pr.topic, src, -1);
   s.topicAdd(pr.topic, dst, +1);
+  if (lead) {
+    s.topicLeadAdd(pr.topic, src, -1);
+    s.topicLeadAdd(pr.topic, dst, +1);
+  }
 }
 
 // ---- relocateLeadership(tp, src, dst) of the leader sr (on src) to the follower dr (on dst)
@@ -168,6 +172,8 @@ CCMI_LD void applyLeadershipFinish(S& s, int p, int dr, int dpos, int src, int d
   pr.racks[0] = pr.racks[dpos];
   pr.racks[dpos] = k0;
   pr.leadNwOut = s.rep(dr).util[R_NW_OUT];
+  s.topicLeadAdd(pr.topic, src, -1);
+  s.topicLeadAdd(pr.topic, dst, +1);
 }
 // the two replicas of p on src and dst, and dr's slot
 template <class S>

@@ -144,7 +144,7 @@ Device::~Device() {
   }
   void* ps[] = {brokers_, replicas_, parts_, allowedAlive_, topicCount_, topicNrep_, topicScratch_, statsOut_,
                 statsPart_, dReq_, rowVisited_, dResult_, dDone_, tUpper_, tLower_, dRLoad_, dBLoad_, dBLnw_, dBPot_, dPOff_, dPSlots_,
-                dPLeader_, dChainLog_, dChainOut_, pIneligOff_, pIneligB_};
+                dPLeader_, dChainLog_, dChainOut_, pIneligOff_, pIneligB_, topicLead_, tMinLead_};
   for (void* p : ps)
     if (p) (void)hipFree(p);
   for (void* p : intraAllocs_)
@@ -193,6 +193,8 @@ DevTables Device::tables() const {
   t.stamps = stamps_;
   t.pIneligOff = pIneligOff_;
   t.pIneligB = pIneligB_;
+  t.topicLead = topicLead_;
+  t.tMinLead = tMinLead_;
   t.B = B_;
   t.R = R_;
   t.P = P_;
@@ -302,6 +304,18 @@ void Device::setTopicLimits(const int32_t* upper, const int32_t* lower) {
   hipCheck(hipMemcpyAsync(tUpper_, upper, sizeof(int32_t) * T_, hipMemcpyHostToDevice, ST), "upload tUpper");
   hipCheck(hipMemcpyAsync(tLower_, lower, sizeof(int32_t) * T_, hipMemcpyHostToDevice, ST), "upload tLower");
   hipCheck(hipStreamSynchronize(ST), "sync");
+}
+
+void Device::enableTopicLeaders(const int32_t* dense) {
+  DeviceGuard dg(ordinal_);
+  if (!topicLead_) dalloc(&topicLead_, (size_t)T_ * ldB_);
+  hipCheck(hipMemcpy(topicLead_, dense, sizeof(int32_t) * (size_t)T_ * ldB_, hipMemcpyHostToDevice), "upload topicLead");
+}
+
+void Device::setMinLeaders(const int32_t* tMin) {
+  DeviceGuard dg(ordinal_);
+  if (!tMinLead_) dalloc(&tMinLead_, (size_t)T_);
+  hipCheck(hipMemcpy(tMinLead_, tMin, sizeof(int32_t) * (size_t)T_, hipMemcpyHostToDevice), "upload tMinLead");
 }
 
 void Device::setBrokerSets(const int32_t* brokerSet, const int32_t* replicaSet) {
@@ -430,7 +444,7 @@ UpdateList Device::overlayFor(const Staged& g) const {
 }
 
 MutTables Device::mutTables() const {
-  return MutTables{brokers_, replicas_, parts_, topicCount_, ldB_};
+  return MutTables{brokers_, replicas_, parts_, topicCount_, topicLead_, ldB_};
 }
 
 // Returns the request base the scan reads (host-mapped staging or the HBM copy) and the update list it
@@ -468,7 +482,7 @@ int64_t Device::scanCross(const DevProgram& prog, const int32_t* reps, int K, co
     const Staged g = packUpdates(req);
     std::memcpy(hStage_ + g.end, reps, (size_t)K * 4);
     std::memcpy(hStage_ + g.end + oCand, cands + c0, (size_t)Nr * 4);
-    base = stageScan(g, req, (prog.needs & NEED_TOPIC) != 0, u);
+    base = stageScan(g, req, (prog.needs & (NEED_TOPIC | NEED_TLEAD)) != 0, u);
   }
   ++seq_;
   if (timing) (void)hipEventRecord(EV0, ST);
@@ -537,7 +551,7 @@ int64_t Device::scanPairs(const DevProgram& prog, const int32_t* pr, const int32
   std::memcpy(hStage_ + g.end, pr + p0, (size_t)n * 4);
   std::memcpy(hStage_ + g.end + oB, pb + p0, (size_t)n * 4);
   UpdateList u;
-  const char* base = stageScan(g, req, (prog.needs & NEED_TOPIC) != 0, u);
+  const char* base = stageScan(g, req, (prog.needs & (NEED_TOPIC | NEED_TLEAD)) != 0, u);
   ++seq_;
   if (timing) (void)hipEventRecord(EV0, ST);
   hipCheck(launchScanPairs(tables(), mutTables(), u, prog, (const int32_t*)base, (const int32_t*)(base + oB), n, p0,
@@ -607,6 +621,7 @@ ChainTables Device::chainTables() const {
   c.replicas = replicas_;
   c.parts = parts_;
   c.topicCount = topicCount_;
+  c.topicLead = topicLead_;
   c.ldB = ldB_;
   c.W = W_;
   c.rLoad = dRLoad_;

@@ -98,6 +98,10 @@ class Device {
   // BrokerSetAwareGoal: BrokerRec.bset [B] (broker set of every broker) and ReplicaRec.bset [R] (the set the mapping
   // policy gives every replica), strided writes that leave the rest of the records alone
   void setBrokerSets(const int32_t* brokerSet, const int32_t* replicaSet);
+  // Broker.numLeadersFor counts [T][ldB] (the host model's dense table), kept on the device from now on (deltas of
+  // kind 1 and the chain kernels update them); MinTopicLeadersPerBrokerGoal's minimum per topic [T] (-1 = not its topic)
+  void enableTopicLeaders(const int32_t* topicLeadDense);
+  void setMinLeaders(const int32_t* tMin);
 
   // pending row updates (flushed with the next launch)
   std::vector<BrokerRow> brows;
@@ -154,6 +158,7 @@ class Device {
   PartitionRec* parts_ = nullptr;
   int32_t *topicCount_ = nullptr, *topicNrep_ = nullptr, *tUpper_ = nullptr, *tLower_ = nullptr;
   int32_t *pIneligOff_ = nullptr, *pIneligB_ = nullptr;
+  int32_t *topicLead_ = nullptr, *tMinLead_ = nullptr;
   uint8_t* allowedAlive_ = nullptr;
   std::vector<BrokerRec> hBrokers_;
   std::vector<PartitionRec> hParts_;

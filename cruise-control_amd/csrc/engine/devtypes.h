@@ -42,13 +42,15 @@ enum DevGoalKind : int32_t {
   DG_LEADER_REPLICA_DISTRIBUTION = 8,
   DG_LEADER_BYTES_IN = 9,
   DG_RACK_AWARE_DISTRIBUTION = 10,
-  DG_BROKER_SET_AWARE = 11
+  DG_BROKER_SET_AWARE = 11,
+  DG_MIN_TOPIC_LEADERS = 12  // MinTopicLeadersPerBrokerGoal with configured topics
 };
-// ReplicaRec.bset of a replica every broker set accepts (a topic of MinTopicLeadersPerBrokerGoal's
-// mustHaveTopicLeadersPerBroker set, BrokerSetAwareGoal.java:232-236)
-constexpr int32_t kBrokerSetAny = -2;
+// ReplicaRec.bset flag of a replica of one of MinTopicLeadersPerBrokerGoal's topics: BrokerSetAwareGoal accepts every
+// action on such a replica (BrokerSetAwareGoal.java:258-264) and leaves it out of its own moves (:136-151). Broker set
+// indices stay below the flag; a negative bset is "none".
+constexpr int32_t kBsetMust = 1 << 24;
 // Operands a program's predicates read beyond the base broker/replica/partition record (DevProgram.needs).
-enum DevNeed : uint32_t { NEED_RACK = 1, NEED_POT = 2, NEED_LEAD = 4, NEED_LBI = 8, NEED_TOPIC = 16 };
+enum DevNeed : uint32_t { NEED_RACK = 1, NEED_POT = 2, NEED_LEAD = 4, NEED_LBI = 8, NEED_TOPIC = 16, NEED_TLEAD = 32 };
 // Candidate filters applied inside a CROSS scan before the predicate conjunction (the reference builds these
 // candidate lists per replica; the kernel skips the excluded destinations instead).
 enum DevFilter : int32_t {
@@ -108,7 +110,7 @@ struct alignas(64) BrokerRec {
 struct alignas(64) ReplicaRec {
   double util[4];
   int32_t broker, part, orig, flags;  // flags: RFlag bits
-  int32_t bset;  // the broker set the replica belongs to (ReplicaToBrokerSetMappingPolicy), kBrokerSetAny, -1 = none
+  int32_t bset;  // the broker set the replica belongs to (ReplicaToBrokerSetMappingPolicy) | kBsetMust, -1 = none
   int32_t pad[3];
 };
 struct alignas(64) PartitionRec {
@@ -131,6 +133,10 @@ struct DevTables {
   // CSR [P + 1] / list; null when the model has none
   const int32_t* pIneligOff;
   const int32_t* pIneligB;
+  // Broker.numLeadersFor(topic) counts [T][ldB] (kept once a goal needs them, else null) and MinTopicLeadersPerBrokerGoal's
+  // minimum per topic [T] (-1: not one of its topics; null when the goal has no topics)
+  const int32_t* topicLead;
+  const int32_t* tMinLead;
   int32_t B, R, P, ldB;
 };
 
@@ -151,8 +157,9 @@ struct PartitionRow {
   double leadNwOut;
   int16_t racks[kMaxRf];
 };
+// kind 0: topicCount (replicas of the topic on the broker), 1: topicLead (leaders of the topic on the broker)
 struct TopicCountDelta {
-  int32_t topic, broker, delta, pad;
+  int32_t topic, broker, delta, kind;
 };
 // The LDS overlay of a scan workgroup (one copy of each row kind) stays well inside the 160 KB of a CU so four
 // resident scan workgroups per CU still fit.
@@ -165,6 +172,7 @@ struct MutTables {
   ReplicaRec* replicas;
   PartitionRec* parts;
   int32_t* topicCount;
+  int32_t* topicLead;  // null unless kept
   int32_t ldB;
 };
 struct UpdateList {
@@ -195,6 +203,7 @@ struct ChainTables {
   ReplicaRec* replicas;
   PartitionRec* parts;
   int32_t* topicCount;
+  int32_t* topicLead;  // null unless kept
   int32_t ldB;
   int32_t W;
   LoadVec* rLoad;    // [R]  Replica.load()

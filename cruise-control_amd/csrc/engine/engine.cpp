@@ -38,6 +38,7 @@ struct HostView {
   const std::vector<int32_t>& tLo;
   const std::vector<int32_t>& bSet;  // BrokerSetAwareGoal: broker set of every broker / replica (empty: none)
   const std::vector<int32_t>& rSet;
+  const std::vector<int32_t>& tMin;  // MinTopicLeadersPerBrokerGoal minima (empty: none)
   double bu(int b, int res) const { return m.bu(b, res); }
   double bcap(int b, int res) const { return m.cap(b, res); }
   int nrep(int b) const { return m.nrep(b); }
@@ -80,6 +81,8 @@ struct HostView {
   int tLower(int t) const { return tLo[t]; }
   int bset(int b) const { return bSet.empty() ? -1 : bSet[b]; }
   int rbset(int r) const { return rSet.empty() ? -1 : rSet[r]; }
+  int tlead(int t, int b) const { return m.tlead(t, b); }
+  int tMinLead(int t) const { return tMin.empty() ? -1 : tMin[t]; }
 };
 
 uint32_t needsOf(const DevGoal& g) {
@@ -90,6 +93,7 @@ uint32_t needsOf(const DevGoal& g) {
     case DG_TOPIC_REPLICA_DISTRIBUTION: return NEED_TOPIC;
     case DG_LEADER_REPLICA_DISTRIBUTION: return NEED_LEAD;
     case DG_LEADER_BYTES_IN: return NEED_LBI;
+    case DG_MIN_TOPIC_LEADERS: return NEED_TLEAD;
     default: return 0;
   }
 }
@@ -329,7 +333,7 @@ int Engine::acceptance(int gi, const ccmi_action& a) {
   }
   std::vector<const std::vector<uint8_t>*> allowedBySlot;
   for (auto& g : optimized) allowedBySlot.push_back(&g->allowed);
-  HostView v{m, allowedBySlot, topicUpper, topicLower, brokerSetOf, replicaSetOf};
+  HostView v{m, allowedBySlot, topicUpper, topicLower, brokerSetOf, replicaSetOf, minLeadOf};
   const GoalImpl& g = *optimized.at(gi);
   const int sr = m.replicaOn(a.partition, a.source_broker);
   if (sr < 0) throw std::invalid_argument("no replica of the partition on the source broker");

@@ -43,6 +43,9 @@ struct Constraint {  // BalancingConstraint
   int64_t overMaxReplicasPerBroker;   // overprovisioned.max.replicas.per.broker
   int32_t overMinBrokers;             // overprovisioned.min.brokers
   int32_t overprovisionedMinExtraRacks;
+  // topics.with.min.leaders.per.broker as the matched topic indices (ascending) and min.topic.leaders.per.broker
+  std::vector<int32_t> minLeaderTopics;
+  int32_t minTopicLeadersPerBroker = 1;
 };
 
 class Engine;
@@ -90,6 +93,7 @@ class Engine {
   std::vector<int32_t> topicUpper, topicLower;  // TopicReplicaDistributionGoal limits (device copy: setTopicLimits)
   BrokerSets brokerSets;                        // BalancingConstraint broker sets of the current call
   std::vector<int32_t> brokerSetOf, replicaSetOf;  // BrokerSetAwareGoal state (device copy: setBrokerSets)
+  std::vector<int32_t> minLeadOf;  // MinTopicLeadersPerBrokerGoal's minimum per topic, -1 = not its topic (setMinLeaders)
 
   // one Goal.optimize; throws OptimizationFailure / StateError
   bool optimizeGoal(std::unique_ptr<GoalImpl> g, ccmi_goal_result* res);

@@ -53,6 +53,15 @@ void ensureNoOfflineReplicas(const Model& m, const std::string& name) {
                                 underBrokers(1));
 }
 
+// GoalUtils.ensureReplicasMoveOffBrokersWithBadDisks (GoalUtils.java:327-338)
+void ensureReplicasMoveOffBadDisks(const Model& m, const std::string& name) {
+  for (int b = 0; b < m.B; ++b)
+    if (m.bState[b] == BState::BAD_DISKS)
+      for (int r : m.bRepl[b])
+        if (m.ineligible(m.rPart[r], b))
+          throw OptimizationFailure("[" + name + "] A replica was moved back to broker with broken disk.", underBrokers(1));
+}
+
 // GoalUtils.aliveBrokersNotExcludedForReplicaMove
 int allowedForReplicaMove(const Engine& e, std::vector<uint8_t>& allowed) {
   allowed.assign(e.m.B, 0);
@@ -438,21 +447,154 @@ class RackAwareDist : public GoalImpl {
 
 // ======================================================================================= MinTopicLeadersPerBrokerGoal
 // With the default topics.with.min.leaders.per.broker (no topic matches) the goal accepts every action and only
-// moves offline replicas away (moveAwayOfflineReplicas).
+// moves offline replicas away (moveAwayOfflineReplicas). With topics, every eligible broker gets at least the minimum
+// number of leaders of each: first by leadership moves from the partitions' leaders (single-candidate pair scans), then
+// by moving a leader replica in from the broker with the most leaders of the topic (one cross scan over its leaders).
+// The per-(topic, broker) leader counts live in the model and on the device (Model::enableTopicLeaders).
 class MinTopicLeaders : public GoalImpl {
  public:
   MinTopicLeaders() {
     kind = CCMI_GOAL_MIN_TOPIC_LEADERS_PER_BROKER;
     name = "MinTopicLeadersPerBrokerGoal";
   }
+  std::vector<int32_t> mustOrder;  // _mustHaveTopicMinLeadersPerBroker.keySet() iteration order
+  std::vector<int32_t> minOf;      // [T] minimum, -1 = not a topic of the goal
+
+  bool eligibleToHaveLeaders(const Engine& e, int b) const {  // isEligibleToHaveLeaders (:439-442)
+    return !(e.opt.anyExclLead && e.opt.exclLead[b]) && !(e.opt.anyExclMove && e.opt.exclMove[b]);
+  }
+
+  // HashSet<String> iteration order of topics added in `ins` order
+  static std::vector<int32_t> topicSetOrder(const Model& m, const std::vector<int32_t>& ins) {
+    TopicSet s(&m.topicOrder);
+    for (int t : ins) s.add(t, m.topicHash[t]);
+    std::vector<int32_t> out;
+    s.order(out);
+    return out;
+  }
+
+  // initGoalState (:163-192) with validateTopicsWithMinLeaderIsNotExcluded / validateEnoughLeaderToDistribute /
+  // validateBrokersAllowedReplicaMoveExist (:198-241)
   void init(Engine& e) override {
-    allowedForReplicaMove(e, allowed);
+    Model& m = e.m;
+    const int nAllowed = allowedForReplicaMove(e, allowed);
     dg = DevGoal{};
     dg.kind = DG_ACCEPT_ALL;
     dg.allowedSlot = (int)e.optimized.size();
+    mustOrder.clear();
+    minOf.assign(m.T, -1);
+    if (e.bc.minLeaderTopics.empty()) return;
+    {  // Utils.getTopicNamesMatchedWithPattern: clusterModel.topics() (a HashSet) streamed into Collectors.toSet()
+      std::vector<int32_t> all(m.T), matched;
+      for (int t = 0; t < m.T; ++t) all[t] = t;
+      std::vector<uint8_t> match(m.T, 0);
+      for (int t : e.bc.minLeaderTopics) match[t] = 1;
+      for (int t : topicSetOrder(m, all))
+        if (match[t]) matched.push_back(t);
+      mustOrder = topicSetOrder(m, matched);
+    }
+    std::vector<int32_t> numLeaders(m.T, 0);  // clusterModel.numLeadersPerTopic: one leader per partition
+    for (int p = 0; p < m.P; ++p) numLeaders[m.pTopic[p]]++;
+    int eligible = 0;
+    for (int b = 0; b < m.B; ++b) eligible += m.alive(b) && eligibleToHaveLeaders(e, b) ? 1 : 0;
+    const int cfg = e.bc.minTopicLeadersPerBroker;
+    for (int t : mustOrder) minOf[t] = cfg == 0 ? (eligible == 0 ? 0 : numLeaders[t] / eligible) : cfg;
+    if (e.opt.anyExclTopic) {
+      std::vector<int32_t> bad;
+      for (int t : mustOrder)
+        if (e.opt.exclTopic[t]) bad.push_back(t);
+      if (!bad.empty()) {
+        std::string s;
+        for (int t : topicSetOrder(m, bad)) s += (s.empty() ? "" : ", ") + m.topicNames[t];
+        throw OptimizationFailure("[" + name + "] Topics that must have a minimum number of leaders per broker cannot be "
+                                  "excluded. This error implies a config error. Topics should not be excluded=[" + s +
+                                  "] (see topics.with.min.leaders.per.broker).");
+      }
+    }
+    for (int t : mustOrder) {
+      const int total = eligible * minOf[t];
+      if (numLeaders[t] < total) {
+        ccmi_provision_recommendation rec = provisionRec();
+        rec.num_partitions = total;
+        throw OptimizationFailure("[" + name + "] Cannot distribute " + std::to_string(numLeaders[t]) + " leaders over " +
+                                      std::to_string(eligible) +
+                                      " broker(s) with minimum required per broker leader count " +
+                                      std::to_string(minOf[t]) + " for topic " + m.topicNames[t] + ".",
+                                  rec);
+      }
+    }
+    if (nAllowed == 0)
+      throw OptimizationFailure("[" + name + "] All alive brokers are excluded from replica moves.", underBrokers(m.maxRf));
+    Model::Spec s;
+    s.selImmigrants = e.opt.onlyImmigrants;
+    s.selMustTopics = true;
+    s.prioImmigrants = !e.opt.onlyImmigrants;
+    for (int b = 0; b < m.B; ++b) m.track(b, sortId(kind, false, false), s);
+    m.enableTopicLeaders();
+    e.minLeadOf = minOf;
+    e.dev->setMinLeaders(minOf.data());
+    dg.kind = DG_MIN_TOPIC_LEADERS;
   }
-  // moveAwayOfflineReplicas (:444-466)
+
+  // maybeMoveLeaderOfTopicToBroker (:336-409) with getBrokersWithExcessiveLeaderToMove (:418-430). The queue's keys (live
+  // leader counts) change only for the broker just polled: a move goes from it to `b`, which is never queued (its count
+  // is below the minimum). So polling the largest (count, then smallest id) is the PriorityQueue's order.
+  void moveLeaderOfTopic(Engine& e, int t, int b) {
+    Model& m = e.m;
+    const int mn = minOf[t];
+    int recv = m.tlead(t, b);
+    if (recv >= mn) return;
+    const int id = sortId(kind, false, false);
+    std::vector<int32_t> followers, pr(1), pb(1, b), one(1, b), cands;
+    for (int r : m.sorted(b, id))
+      if (!m.rLeader[r] && m.pTopic[m.rPart[r]] == t) followers.push_back(r);
+    e.eligible(one, DA_LEADERSHIP, cands);
+    for (int f : followers) {
+      const int leader = m.pLeader[m.rPart[f]];
+      if (m.tlead(t, m.rBroker[leader]) <= mn) continue;
+      if (cands.empty()) continue;  // maybeApplyBalancingAction over an empty eligible list
+      pr[0] = leader;
+      if (e.pairScan(*this, pr, pb, DA_LEADERSHIP) < 0) continue;
+      m.relocateLeadership(m.rPart[leader], m.rBroker[leader], b);
+      if (++recv >= mn) return;
+    }
+    std::vector<int32_t> queue;
+    for (int x : aliveById(m))
+      if (m.tlead(t, x) > mn) queue.push_back(x);
+    e.eligible(one, DA_MOVE, cands);
+    std::vector<int32_t> leaders;
+    while (!queue.empty()) {
+      size_t best = 0;
+      for (size_t i = 1; i < queue.size(); ++i) {
+        const int ci = m.tlead(t, queue[i]), cb = m.tlead(t, queue[best]);
+        if (ci > cb || (ci == cb && m.bId[queue[i]] < m.bId[queue[best]])) best = i;
+      }
+      const int giver = queue[best];
+      queue.erase(queue.begin() + (long)best);
+      leaders.clear();
+      for (int r : m.sorted(giver, id))
+        if (m.rLeader[r] && m.pTopic[m.rPart[r]] == t) leaders.push_back(r);
+      int giverCount = (int)leaders.size();
+      const int64_t key = e.crossScan(*this, DA_MOVE, leaders, 0, cands);
+      if (key < 0) continue;
+      const int r = leaders[key / (int64_t)cands.size()];
+      m.relocateReplica(m.rPart[r], giver, b);
+      if (++recv >= mn) return;
+      if (--giverCount > mn) queue.push_back(giver);
+    }
+  }
+
+  // rebalanceForBroker (:317-334)
   void rebalance(Engine& e, int b) override {
+    moveAwayOffline(e, b);
+    if (mustOrder.empty()) return;
+    PhaseScope ps(PH_OTHER_GOALS);
+    if (!(e.m.alive(b) && eligibleToHaveLeaders(e, b))) return;
+    for (int t : mustOrder) moveLeaderOfTopic(e, t, b);
+  }
+
+  // moveAwayOfflineReplicas (:444-464)
+  void moveAwayOffline(Engine& e, int b) {
     PhaseScope ps(PH_OTHER_GOALS);
     Model& m = e.m;
     if (!hasOffline(m, b)) return;
@@ -473,8 +615,10 @@ class MinTopicLeaders : public GoalImpl {
       m.relocateReplica(m.rPart[r], b, cands[key]);
     }
   }
+  // updateGoalState (:279-288): the leader-count check only logs
   void update(Engine& e) override {
     ensureNoOfflineReplicas(e.m, name);
+    ensureReplicasMoveOffBadDisks(e.m, name);
     finished = true;
   }
   int compareStats(const ccmi_cluster_stats&, const ccmi_cluster_stats&) const override { return 0; }
@@ -814,10 +958,18 @@ class PotentialNwOut : public GoalImpl {
       auto rowCount = [&](int r, size_t upto) {  // visited eligible brokers of one row: partition brokers removed
         int64_t c = (int64_t)upto;
         const int p = m.rPart[r];
-        if (newOnly) {  // only NEW brokers or the replica's original broker are eligible (GoalUtils.java:193-198)
+        // a leader replica skips brokers excluded for leadership (GoalUtils.java:170-180); with NEW brokers only NEW
+        // brokers or the replica's original broker are eligible (:193-198)
+        const bool exclLead = e.opt.anyExclLead && !e.opt.anyRequested && m.rLeader[r];
+        if (newOnly || exclLead) {
           c = 0;
-          for (size_t j = 0; j < upto; ++j)
-            if ((m.isNew(cands[j]) || cands[j] == m.rOrig[r]) && m.replicaOn(p, cands[j]) < 0) c++;
+          for (size_t j = 0; j < upto; ++j) {
+            const int x = cands[j];
+            if (m.replicaOn(p, x) >= 0) continue;
+            if (newOnly && !(m.isNew(x) || x == m.rOrig[r])) continue;
+            if (exclLead && e.opt.exclLead[x]) continue;
+            c++;
+          }
           return c;
         }
         for (int s = m.pOff[p]; s < m.pOff[p + 1]; ++s) {
@@ -1634,9 +1786,10 @@ class BrokerSetAware : public GoalImpl {
     Model& m = e.m;
     if (allowedForReplicaMove(e, allowed) == 0)
       throw OptimizationFailure("[" + name + "] All alive brokers are excluded from replica moves.", underBrokers(m.maxRf));
+    // _excludedTopics = MinTopicLeadersPerBrokerGoal's topics + the options' excluded topics (:136-139)
     Model::Spec s;
     s.selImmigrants = e.opt.onlyImmigrants;
-    s.selExclTopics = e.opt.anyExclTopic;  // _excludedTopics: no MinTopicLeadersPerBroker topics are configured
+    s.selExclMust = e.opt.anyExclTopic || !e.bc.minLeaderTopics.empty();
     for (int b = 0; b < m.B; ++b) m.track(b, sortId(kind, false, false), s);
     // BrokerSetResolutionHelper + the mapping policy, frozen for the goal (the policy caches per topic)
     const BrokerSets& bs = e.brokerSets;
@@ -1649,8 +1802,9 @@ class BrokerSetAware : public GoalImpl {
       for (int t = 0; t < m.T; ++t) topicSet[t] = bsets::topicBrokerSet(m.topicNames[t], bs.numSets);
     }
     for (int r = 0; r < m.R; ++r)
-      e.replicaSetOf[r] = bs.policy == CCMI_BROKER_SET_TOPIC_NAME_HASH ? topicSet[m.pTopic[m.rPart[r]]]
-                                                                       : e.brokerSetOf[m.rOrig[r]];
+      e.replicaSetOf[r] = (bs.policy == CCMI_BROKER_SET_TOPIC_NAME_HASH ? topicSet[m.pTopic[m.rPart[r]]]
+                                                                        : e.brokerSetOf[m.rOrig[r]]) |
+                          (m.mustTopicSel[m.pTopic[m.rPart[r]]] ? kBsetMust : 0);
     e.dev->setBrokerSets(e.brokerSetOf.data(), e.replicaSetOf.data());
     alive = aliveById(m);
     dg = DevGoal{};
@@ -1667,7 +1821,7 @@ class BrokerSetAware : public GoalImpl {
     const int cur = e.brokerSetOf[b];
     std::vector<int32_t> one(1), ins, order, cands;
     for (int r : list) {
-      const int want = e.replicaSetOf[r];
+      const int want = bsetIndex(e.replicaSetOf[r]);
       if (m.alive(b) && want == cur) continue;
       ins.clear();
       for (int x : alive)
@@ -1703,7 +1857,7 @@ class BrokerSetAware : public GoalImpl {
       for (int i = m.pOff[p]; i < m.pOff[p + 1]; ++i) byTopic[m.pTopic[p]].push_back(m.rBroker[m.pSlots[i]]);
     std::vector<int32_t> ids, order;
     for (int t : topics) {  // getPartitionsByTopic: a TreeMap by topic name
-      if (e.opt.anyExclTopic && e.opt.exclTopic[t]) continue;
+      if ((e.opt.anyExclTopic && e.opt.exclTopic[t]) || m.mustTopicSel[t]) continue;
       const auto& v = byTopic[t];  // the topic's brokers in partition / slot order
       const int set = v.empty() ? -1 : e.brokerSetOf[v[0]];
       bool one = true;

@@ -94,10 +94,13 @@ void Model::build(const ccmi_cluster_desc& d) {
   // Replay createReplica + setReplicaLoad in replica index order (or: every createReplica, then setReplicaLoad in
   // replica_load_order).
   const int32_t* loadOrder = d.replica_load_order;
+  const int nLoads = loadOrder && d.num_replica_loads > 0 ? d.num_replica_loads : R;
   if (loadOrder) {
+    if (nLoads > R) throw std::invalid_argument("num_replica_loads above num_replicas");
     std::vector<uint8_t> seen(R, 0);
-    for (int i = 0; i < R; ++i) {
-      if (loadOrder[i] < 0 || loadOrder[i] >= R || seen[loadOrder[i]]) throw std::invalid_argument("replica_load_order is not a permutation");
+    for (int i = 0; i < nLoads; ++i) {
+      if (loadOrder[i] < 0 || loadOrder[i] >= R || seen[loadOrder[i]])
+        throw std::invalid_argument("replica_load_order repeats a replica or is out of range");
       seen[loadOrder[i]] = 1;
     }
   }
@@ -136,7 +139,7 @@ void Model::build(const ccmi_cluster_desc& d) {
     if (!loadOrder) setLoad(r);
   }
   if (loadOrder)
-    for (int i = 0; i < R; ++i) setLoad(loadOrder[i]);
+    for (int i = 0; i < nLoads; ++i) setLoad(loadOrder[i]);
   if (maxRf > kMaxRf) throw std::invalid_argument("replication factor above 8 is not supported");
   for (int p = 0; p < P; ++p)
     if (pLeader[p] < 0) throw std::invalid_argument("partition without leader");
@@ -192,6 +195,7 @@ void Model::build(const ccmi_cluster_desc& d) {
   sortedCache.assign(B, {});
   filteredCache.assign(B, {});
   exclTopicSel.assign(T, 0);
+  mustTopicSel.assign(T, 0);
   bUtilC.assign((size_t)4 * B, 0.0);
   bPctC.assign((size_t)4 * B, 0.0);
   rUtilC.assign((size_t)4 * R, 0.0);
@@ -514,6 +518,11 @@ void Model::relocateReplica(int p, int src, int dst) {
     topicCountDense[(size_t)pTopic[p] * ldB + src]--;
     topicCountDense[(size_t)pTopic[p] * ldB + dst]++;
   }
+  const bool lead = rLeader[r] && !topicLeadDense.empty();
+  if (lead) {
+    topicLeadDense[(size_t)pTopic[p] * ldB + src]--;
+    topicLeadDense[(size_t)pTopic[p] * ldB + dst]++;
+  }
   if (dev && !replaying) {
     markChain(cDirtyB, cDirtyBList, src);
     markChain(cDirtyB, cDirtyBList, dst);
@@ -523,6 +532,21 @@ void Model::relocateReplica(int p, int src, int dst) {
     markP(p);
     dev->tdeltas.push_back({pTopic[p], src, -1, 0});
     dev->tdeltas.push_back({pTopic[p], dst, +1, 0});
+    if (lead) {
+      dev->tdeltas.push_back({pTopic[p], src, -1, 1});
+      dev->tdeltas.push_back({pTopic[p], dst, +1, 1});
+    }
+  }
+}
+
+void Model::enableTopicLeaders() {
+  if (!topicLeadDense.empty()) return;
+  topicLeadDense.assign((size_t)T * ldB, 0);
+  for (int p = 0; p < P; ++p) topicLeadDense[(size_t)pTopic[p] * ldB + rBroker[pLeader[p]]]++;
+  if (dev) {
+    flushToDevice();  // pending rows first: the device table starts from the host's current state
+    dev->flushOnly();
+    dev->enableTopicLeaders(topicLeadDense.data());
   }
 }
 
@@ -577,7 +601,15 @@ bool Model::relocateLeadership(int p, int src, int dst) {
   refreshBroker(src);
   refreshBroker(dst);
   log.push_back({CCMI_LEADERSHIP_MOVEMENT, p, src, dst, -1});
+  if (!topicLeadDense.empty()) {
+    topicLeadDense[(size_t)pTopic[p] * ldB + src]--;
+    topicLeadDense[(size_t)pTopic[p] * ldB + dst]++;
+  }
   if (dev && !replaying) {
+    if (!topicLeadDense.empty()) {
+      dev->tdeltas.push_back({pTopic[p], src, -1, 1});
+      dev->tdeltas.push_back({pTopic[p], dst, +1, 1});
+    }
     markChain(cDirtyB, cDirtyBList, src);
     markChain(cDirtyB, cDirtyBList, dst);
     markChain(cDirtyR, cDirtyRList, sr);
@@ -667,6 +699,8 @@ bool Model::selects(const Spec& s, int r) const {
   if (s.selOffline && !curOffline(r)) return false;
   // ReplicaSortFunctionFactory.selectReplicasBasedOnExcludedTopics (:135-146)
   if (s.selExclTopics && !origOffline(r) && exclTopicSel[pTopic[rPart[r]]]) return false;
+  if (s.selExclMust && !origOffline(r) && (exclTopicSel[pTopic[rPart[r]]] || mustTopicSel[pTopic[rPart[r]]])) return false;
+  if (s.selMustTopics && !mustTopicSel[pTopic[rPart[r]]]) return false;  // ReplicaSortFunctionFactory.java:153-155
   if (s.selAboveRes >= 0 && !(ru(r, s.selAboveRes) > s.aboveLimit)) return false;
   if (s.selBelowRes >= 0 && !(ru(r, s.selBelowRes) < s.belowLimit)) return false;
   return true;
@@ -749,6 +783,13 @@ static void cachePut(std::vector<Model::SortedCacheEntry>& cache, uint32_t ver, 
   slot->spec = s;
   slot->ver = ver;
   slot->v = std::move(v);
+}
+
+void Model::setMustTopicSelection(const std::vector<uint8_t>& t) {
+  if (t == mustTopicSel) return;
+  mustTopicSel = t;
+  for (auto& c : sortedCache) c.clear();
+  for (auto& c : filteredCache) c.clear();
 }
 
 void Model::setExcludedTopicSelection(const std::vector<uint8_t>& t) {

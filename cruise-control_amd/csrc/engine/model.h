@@ -121,6 +121,10 @@ class Model {
   std::vector<int32_t> topicCountDense;     // [T][ldB] live Broker.numReplicasOfTopicInBroker counts
   int ldB = 4;
   int tcount(int t, int b) const { return topicCountDense[(size_t)t * ldB + b]; }
+  // [T][ldB] live Broker.numLeadersFor counts, kept (here and on the device) once a goal asked for them
+  std::vector<int32_t> topicLeadDense;
+  int tlead(int t, int b) const { return topicLeadDense[(size_t)t * ldB + b]; }
+  void enableTopicLeaders();
   // disks: replica placement over logdirs (JBOD; Broker._diskByLogdir TreeMap, model/Disk.java)
   int D = 0;
   std::vector<int32_t> dBroker;
@@ -246,6 +250,8 @@ class Model {
     bool selLeaders = false, selFollowers = false, selImmigrants = false, selImmOrOffline = false;
     bool selOffline = false;
     bool selExclTopics = false;  // selectReplicasBasedOnExcludedTopics over exclTopicSel
+    bool selExclMust = false;    // ... over exclTopicSel + mustTopicSel (BrokerSetAwareGoal._excludedTopics)
+    bool selMustTopics = false;  // selectReplicasBasedOnIncludedTopics over mustTopicSel (MinTopicLeadersPerBrokerGoal)
     int selAboveRes = -1, selBelowRes = -1;
     double aboveLimit = 0, belowLimit = 0;
     bool prioOffline = false, prioImmigrants = false;
@@ -253,7 +259,8 @@ class Model {
     bool scoreReverse = false;
     bool operator==(const Spec& o) const {
       return selLeaders == o.selLeaders && selFollowers == o.selFollowers && selImmigrants == o.selImmigrants &&
-             selOffline == o.selOffline && selExclTopics == o.selExclTopics &&
+             selOffline == o.selOffline && selExclTopics == o.selExclTopics && selExclMust == o.selExclMust &&
+             selMustTopics == o.selMustTopics &&
              selImmOrOffline == o.selImmOrOffline && selAboveRes == o.selAboveRes && selBelowRes == o.selBelowRes &&
              aboveLimit == o.aboveLimit && belowLimit == o.belowLimit && prioOffline == o.prioOffline &&
              prioImmigrants == o.prioImmigrants && scoreRes == o.scoreRes && scoreReverse == o.scoreReverse;
@@ -292,6 +299,9 @@ class Model {
   // drops the cached snapshots (their Specs do not carry the set)
   std::vector<uint8_t> exclTopicSel;
   void setExcludedTopicSelection(const std::vector<uint8_t>& t);
+  // MinTopicLeadersPerBrokerGoal's topics ([T] flags) as selMustTopics / selExclMust see them (same cache rule)
+  std::vector<uint8_t> mustTopicSel;
+  void setMustTopicSelection(const std::vector<uint8_t>& t);
   void track(int b, int nameId, const Spec& s);
   void untrackAll(int nameId);
   void untrack(int b, int nameId);

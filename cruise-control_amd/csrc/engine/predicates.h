@@ -36,7 +36,8 @@ namespace ccmi {
 // V must provide: bu(b,res) bcap(b,res) nrep(b) alive(b) allowed(slot,b) ru(r,res) flags(r) rbroker(r)
 // rorig(r) origOff(r) rpart(r) hosts(p,b), and for the goals that read them: rack(b) otherOnRack(p,self,rack)
 // slotRack(p,b) (rack of partition p's replica on b) rackCount(p,rack) nlead(b)
-// pot(b) lnwin(b) pLeadNwOut(p) ptopic(p) tcount(t,b) tUpper(t) tLower(t) bset(b) rbset(r) (broker sets).
+// pot(b) lnwin(b) pLeadNwOut(p) ptopic(p) tcount(t,b) tUpper(t) tLower(t) bset(b) rbset(r) (broker sets)
+// tlead(t,b) (Broker.numLeadersFor) tMinLead(t) (MinTopicLeadersPerBrokerGoal's minimum, -1 = not its topic).
 // Replica.isCurrentOffline; V::origOff(r) = isOriginalOffline || original broker dead
 template <class V>
 CCMI_HD bool currentOffline(const V& v, int r) {
@@ -152,12 +153,51 @@ CCMI_HD bool rackDistViolates(const V& v, int r, int dst) {
 }
 
 // ---------------------------------------------------------------- BrokerSetAwareGoal
-// doesReplicaMoveViolateActionAcceptance (BrokerSetAwareGoal.java:262-275): the destination's broker set differs from
+CCMI_HD bool bsetMust(int e) { return e >= 0 && (e & kBsetMust) != 0; }
+CCMI_HD int bsetIndex(int e) { return e >= 0 ? (e & (kBsetMust - 1)) : e; }
+// doesReplicaMoveViolateActionAcceptance (BrokerSetAwareGoal.java:266-279): the destination's broker set differs from
 // the set the mapping policy gives the replica
 template <class V>
 CCMI_HD bool bsetViolates(const V& v, int r, int dst) {
-  const int e = v.rbset(r);
-  return e != kBrokerSetAny && e != v.bset(dst);
+  return bsetIndex(v.rbset(r)) != v.bset(dst);
+}
+// actionAcceptance (:256-283): a MinTopicLeadersPerBrokerGoal topic of the (source) replica is accepted whatever the
+// action; otherwise the source replica's side is a BROKER_REJECT and the swapped replica's side a REPLICA_REJECT
+template <class V>
+CCMI_HD bool bsetAcceptMove(const V& v, int action, int r, int dst) {
+  if (bsetMust(v.rbset(r)) || action == DA_LEADERSHIP) return true;
+  return !bsetViolates(v, r, dst);
+}
+template <class V>
+CCMI_HD int bsetAcceptSwap(const V& v, int sr, int sb, int dr, int db) {
+  if (bsetMust(v.rbset(sr))) return 0;
+  if (bsetViolates(v, sr, db)) return 2;
+  return bsetViolates(v, dr, sb) ? 1 : 0;
+}
+
+// ---------------------------------------------------------------- MinTopicLeadersPerBrokerGoal
+// doesLeaderRemoveViolateOptimizedGoal for replica r on broker b (MinTopicLeadersPerBrokerGoal.java:141-153)
+template <class V>
+CCMI_HD bool minLeadRemoveViolates(const V& v, int r, int b) {
+  if (!(v.flags(r) & RF_LEADER)) return false;
+  const int t = v.ptopic(v.rpart(r));
+  const int mn = v.tMinLead(t);
+  return mn >= 0 && v.tlead(t, b) <= mn;
+}
+// actionAcceptance (:97-131): actions on other topics are accepted (actionAffectsRelevantTopics :265-271); a move or
+// leadership move may not take the source below its minimum; acceptReplicaSwap (:116-131)
+template <class V>
+CCMI_HD bool minLeadAcceptMove(const V& v, int r, int src) {
+  return v.tMinLead(v.ptopic(v.rpart(r))) < 0 || !minLeadRemoveViolates(v, r, src);
+}
+template <class V>
+CCMI_HD int minLeadAcceptSwap(const V& v, int sr, int sb, int dr, int db) {
+  const int ts = v.ptopic(v.rpart(sr)), td = v.ptopic(v.rpart(dr));
+  if (v.tMinLead(ts) < 0 && v.tMinLead(td) < 0) return 0;
+  const bool sl = (v.flags(sr) & RF_LEADER) != 0, dl = (v.flags(dr) & RF_LEADER) != 0;
+  if (!sl && !dl) return 0;
+  if (sl && dl && ts == td) return 0;
+  return (minLeadRemoveViolates(v, sr, sb) || minLeadRemoveViolates(v, dr, db)) ? 1 : 0;
 }
 
 // ---------------------------------------------------------------- CapacityGoal
@@ -234,7 +274,8 @@ CCMI_HD bool goalAcceptMove(const DevGoal& g, const V& v, int action, int r, int
     case DG_RESOURCE_DISTRIBUTION: return resAcceptMove(g, v, action, r, src, dst);
     case DG_RACK_AWARE: return action == DA_LEADERSHIP || !rackViolates(v, r, dst);
     case DG_RACK_AWARE_DISTRIBUTION: return action == DA_LEADERSHIP || !rackDistViolates(v, r, dst);
-    case DG_BROKER_SET_AWARE: return action == DA_LEADERSHIP || !bsetViolates(v, r, dst);
+    case DG_BROKER_SET_AWARE: return bsetAcceptMove(v, action, r, dst);
+    case DG_MIN_TOPIC_LEADERS: return minLeadAcceptMove(v, r, src);
     case DG_REPLICA_CAPACITY: return action == DA_LEADERSHIP || (int64_t)v.nrep(dst) < g.maxReplicas;
     case DG_CAPACITY:
       if (action == DA_LEADERSHIP && (g.resource == 3 /*DISK*/ || g.resource == 1 /*NW_IN*/)) return true;
@@ -257,6 +298,11 @@ CCMI_HD bool goalSelfSatisfiedMove(const DevGoal& g, const V& v, int action, int
     case DG_RACK_AWARE_DISTRIBUTION:
     case DG_BROKER_SET_AWARE: return true;
     case DG_ACCEPT_ALL: return action == DA_MOVE;  // MinTopicLeadersPerBrokerGoal moves offline replicas only
+    case DG_MIN_TOPIC_LEADERS: {  // selfSatisfied (MinTopicLeadersPerBrokerGoal.java:252-263)
+      if (currentOffline(v, r)) return action == DA_MOVE;
+      const int t = v.ptopic(v.rpart(r));
+      return v.tlead(t, src) > v.tMinLead(t);
+    }
     case DG_REPLICA_CAPACITY: return (int64_t)v.nrep(dst) < g.maxReplicas;
     case DG_CAPACITY: return capUnderAfterAdding(g, v, dst, v.ru(r, g.resource));
     case DG_POTENTIAL_NW_OUT: return potSelfSatisfiedMove(g, v, action, r, dst);
@@ -284,9 +330,8 @@ CCMI_HD int goalAcceptSwap(const DevGoal& g, const V& v, int sr, int sb, int dr,
     case DG_RACK_AWARE_DISTRIBUTION:
       if (rackDistViolates(v, sr, db)) return 2;
       return rackDistViolates(v, dr, sb) ? 1 : 0;
-    case DG_BROKER_SET_AWARE:  // BROKER_REJECT for the source replica's side, REPLICA_REJECT for the other (:240-256)
-      if (bsetViolates(v, sr, db)) return 2;
-      return bsetViolates(v, dr, sb) ? 1 : 0;
+    case DG_BROKER_SET_AWARE: return bsetAcceptSwap(v, sr, sb, dr, db);
+    case DG_MIN_TOPIC_LEADERS: return minLeadAcceptSwap(v, sr, sb, dr, db);
     case DG_CAPACITY: {
       const double su = v.ru(sr, g.resource), du = v.ru(dr, g.resource);
       const double delta = du - su;

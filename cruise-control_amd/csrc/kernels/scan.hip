@@ -80,6 +80,8 @@ struct DevView {
   __device__ __forceinline__ int tLower(int tp) const { return t.tLower[tp]; }
   __device__ __forceinline__ int bset(int b) const { return t.brokers[b].bset; }
   __device__ __forceinline__ int rbset(int r) const { return t.replicas[r].bset; }
+  __device__ __forceinline__ int tlead(int tp, int b) const { return t.topicLead[(size_t)tp * t.ldB + b]; }
+  __device__ __forceinline__ int tMinLead(int tp) const { return t.tMinLead ? t.tMinLead[tp] : -1; }
 };
 
 // Row updates a cross/pair scan applies itself (instead of a separate launch): every workgroup stages the
@@ -153,7 +155,7 @@ __device__ __forceinline__ void applyRowsBlock(const MutTables& M, const BrokerR
   }
   for (int i = first; i < nt; i += stride) {
     const TopicCountDelta d = tdel[i];
-    atomicAdd(&M.topicCount[(size_t)d.topic * M.ldB + d.broker], d.delta);
+    atomicAdd(&(d.kind ? M.topicLead : M.topicCount)[(size_t)d.topic * M.ldB + d.broker], d.delta);
   }
 }
 
@@ -207,6 +209,7 @@ struct PreView {
   double spot, dpot, plno, slbi, dlbi;
   int snlead, dnlead, topic, stc, dtc, tup, tlo;
   int rbs, sbs, dbs;  // broker sets: the replica's (mapping policy), the source's, the destination's
+  int stl, dtl, tmn;  // leaders of the row's topic on the source / destination, MinTopicLeaders' minimum of it
   bool inelig;  // dst is one of the row's partition's ineligible brokers
 
   static __device__ __forceinline__ double sel(int k, double a, double b, double c, double d) {
@@ -319,6 +322,11 @@ struct PreView {
       stc = t.topicCount[(size_t)topic * t.ldB + src];
       dtc = t.topicCount[(size_t)topic * t.ldB + dst];
     }
+    if (prog.needs & NEED_TLEAD) {
+      tmn = t.tMinLead ? t.tMinLead[topic] : -1;
+      stl = t.topicLead[(size_t)topic * t.ldB + src];
+      dtl = t.topicLead[(size_t)topic * t.ldB + dst];
+    }
   }
   // The destination side, loaded BEFORE the row (it depends only on the destination id); the destination's
   // topic count needs the row's topic and is read in loadRow.
@@ -409,6 +417,8 @@ struct PreView {
   __device__ __forceinline__ int tLower(int) const { return tlo; }
   __device__ __forceinline__ int bset(int b) const { return b == dst ? dbs : sbs; }
   __device__ __forceinline__ int rbset(int) const { return rbs; }
+  __device__ __forceinline__ int tlead(int, int b) const { return b == dst ? dtl : stl; }
+  __device__ __forceinline__ int tMinLead(int) const { return tmn; }
 
   // RackAwareGoal.rackAwareEligibleBrokers: the destination's rack is not in the partition's rack list with
   // one occurrence of the replica's own rack removed (RackAwareGoal.java:193-211).
@@ -717,6 +727,9 @@ struct DevApply {
   __device__ __forceinline__ int& slot(int p, int i) { return c.pSlots[c.pOff[p] + i]; }
   __device__ __forceinline__ int& leader(int p) { return c.pLeader[p]; }
   __device__ __forceinline__ void topicAdd(int t, int b, int d) { c.topicCount[(size_t)t * c.ldB + b] += d; }
+  __device__ __forceinline__ void topicLeadAdd(int t, int b, int d) {
+    if (c.topicLead) c.topicLead[(size_t)t * c.ldB + b] += d;
+  }
 };
 
 // thread 0's record writes become visible to the whole workgroup (one CU: workgroup scope; the next launch sees them

@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define CCMI_ABI_VERSION 4
+#define CCMI_ABI_VERSION 5
 
 typedef enum ccmi_status {
   CCMI_OK = 0,
@@ -167,6 +167,10 @@ typedef struct ccmi_cluster_desc {
   int32_t num_disk_assignments;
   const int32_t* disk_assign_replica; /* [num_disk_assignments] */
   const int32_t* disk_assign_disk;    /* [num_disk_assignments] */
+  /* ABI v5: entries of replica_load_order (0 = num_replicas). A replica the order omits never gets
+   * ClusterModel.setReplicaLoad: its Load stays empty (model/Load.java isEmpty), as in hand-built fixtures such as
+   * DeterministicCluster.minLeaderReplicaPerBrokerSatisfiable (DeterministicCluster.java:321-361). */
+  int32_t num_replica_loads;
 } ccmi_cluster_desc;
 
 /* analyzer/BalancingConstraint.java; defaults AnalyzerConfig.java:58-464 via ccmi_default_constraint */
@@ -194,6 +198,15 @@ typedef struct ccmi_balancing_constraint {
   const char* const* broker_set_names;    /* [num_broker_sets] brokerSetId */
   const int32_t* broker_set_offset;       /* [num_broker_sets + 1] CSR into broker_set_members */
   const int32_t* broker_set_members;      /* Kafka broker ids */
+  /* MinTopicLeadersPerBrokerGoal (ABI v5): the topics topics.with.min.leaders.per.broker matches — the caller's
+   * Utils.getTopicNamesMatchedWithPattern(BalancingConstraint.topicsWithMinLeadersPerBrokerPattern(), topics)
+   * (common/Utils.java:26-36, BalancingConstraint.java:92,275-277), as topic indices of the session's desc (0 topics =
+   * the default empty pattern) — and min.topic.leaders.per.broker (BalancingConstraint.java:93,285-287; 0 = the
+   * dynamic leaders / eligible brokers). BrokerSetAwareGoal reads the same topic set (BrokerSetAwareGoal.java:
+   * 136-139,262). */
+  const int32_t* min_leader_topics;
+  int32_t num_min_leader_topics;
+  int32_t min_topic_leaders_per_broker;
 } ccmi_balancing_constraint;
 
 /* analyzer/OptimizationOptions.java (7-field form) */
@@ -355,9 +368,8 @@ ccmi_status ccmi_builder_set_broker_state(ccmi_model_builder* b, int32_t broker_
 ccmi_status ccmi_builder_desc(ccmi_model_builder* b, ccmi_cluster_desc* out);
 ccmi_status ccmi_builder_broker_ids(const ccmi_model_builder* b, int32_t* out);
 
-/* device_ordinal: HIP device; num_devices > 1 shards the candidate space by destination broker across
- * device_ordinal .. device_ordinal+num_devices-1 inside one process (multi-process sharding uses RCCL
- * from the host harness instead). */
+/* device_ordinal: the HIP device the session's tables live on (one session = one device). Destination-sharded
+ * sessions are one per process and GPU, joined by ccmi_session_set_shard / ccmi_session_attach_rccl below. */
 ccmi_status ccmi_session_create(int32_t device_ordinal, const ccmi_cluster_desc* desc, ccmi_session** out);
 ccmi_status ccmi_session_destroy(ccmi_session* s);
 

@@ -285,7 +285,7 @@ class BrokerSetAwareGoal : public AbstractGoal {
   std::map<std::string, std::set<int>> brokersByBrokerSet_;  // broker ids
   std::map<int, std::string> brokerSetIdByBrokerId_;
   std::map<std::string, std::string> brokerSetIdByTopic_;    // TopicNameHashBrokerSetMappingPolicy cache
-  std::set<int> excludedTopics_;
+  std::set<int> excludedTopics_, mustHaveTopics_;
 };
 
 class MinTopicLeadersPerBrokerGoal : public AbstractGoal {
@@ -301,7 +301,17 @@ class MinTopicLeadersPerBrokerGoal : public AbstractGoal {
   void updateGoalState(ClusterModel& cm, const OptimizationOptions& o) override;
   void rebalanceForBroker(int broker, ClusterModel& cm, const GoalList& g, const OptimizationOptions& o) override;
   bool selfSatisfied(ClusterModel& cm, const BalancingAction& a) override;
+
+ private:
+  static bool eligibleToHaveLeaders(const ClusterModel& cm, int b, const OptimizationOptions& o);
+  bool leaderRemoveViolates(ClusterModel& cm, int r) const;
+  void moveAwayOfflineReplicas(int b, ClusterModel& cm, const GoalList& g, const OptimizationOptions& o);
+  void moveLeaderOfTopicToBroker(int t, int b, ClusterModel& cm, const GoalList& g, const OptimizationOptions& o);
+  std::vector<int> mustOrder_;   // _mustHaveTopicMinLeadersPerBroker.keySet() in HashMap iteration order
+  std::map<int, int> minLeaders_;  // topic -> minimum leaders per eligible broker
 };
+// iteration order of a HashSet<String> of topic names filled in `insertion` order
+std::vector<int> topicHashSetOrder(const ClusterModel& cm, const std::vector<int>& insertion);
 
 // PreferredLeaderElectionGoal (analyzer/goals/PreferredLeaderElectionGoal.java) with skipUrpDemotion = false,
 // excludeFollowerDemotion = false (the no-argument constructor GoalOptimizer uses). Demoted disks are not in the

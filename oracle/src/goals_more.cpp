@@ -314,34 +314,198 @@ void RackAwareDistributionGoal::updateGoalState(ClusterModel& cm, const Optimiza
 }
 
 // ===================================================================== MinTopicLeadersPerBrokerGoal
-// With the default topics.with.min.leaders.per.broker ("", matches no topic) the goal accepts every action
-// (actionAffectsRelevantTopics is false, MinTopicLeadersPerBrokerGoal.java:263-269) and only moves offline
-// replicas away (moveAwayOfflineReplicas, :455-478).
-Acceptance MinTopicLeadersPerBrokerGoal::actionAcceptance(const BalancingAction& a, ClusterModel&) {
+// MinTopicLeadersPerBrokerGoal.java. With the default topics.with.min.leaders.per.broker ("", matches no topic) the
+// map of topics is empty: the goal accepts every action (actionAffectsRelevantTopics is false, :265-271) and only
+// moves offline replicas away (moveAwayOfflineReplicas, :444-464).
+
+// the topic HashSet<String> a stream over clusterModel.topics() collects into (Utils.getTopicNamesMatchedWithPattern,
+// Collectors.toSet()), iterated as _mustHaveTopicMinLeadersPerBroker.keySet() (a HashMap filled in that order)
+std::vector<int> topicHashSetOrder(const ClusterModel& cm, const std::vector<int>& insertion) {
+  JHashSet s([&cm](int a, int b) { return icompare(cm.topicRank[a], cm.topicRank[b]); });
+  for (int t : insertion) s.add(t, cm.topicHash[t]);
+  return s.order();
+}
+
+// isEligibleToHaveLeaders (:439-442)
+bool MinTopicLeadersPerBrokerGoal::eligibleToHaveLeaders(const ClusterModel& cm, int b, const OptimizationOptions& o) {
+  const int id = cm.brokers[b].id;
+  return !o.excludedBrokersForLeadership.count(id) && !o.excludedBrokersForReplicaMove.count(id);
+}
+
+// doesLeaderRemoveViolateOptimizedGoal (:141-153)
+bool MinTopicLeadersPerBrokerGoal::leaderRemoveViolates(ClusterModel& cm, int r) const {
+  if (!cm.replicas[r].isLeader) return false;
+  const int t = cm.partitions[cm.replicas[r].partition].topic;
+  auto it = minLeaders_.find(t);
+  if (it == minLeaders_.end()) return false;
+  return cm.numLeadersFor(cm.replicas[r].broker, t) <= it->second;
+}
+
+// actionAcceptance (:97-131) with actionAffectsRelevantTopics (:265-271)
+Acceptance MinTopicLeadersPerBrokerGoal::actionAcceptance(const BalancingAction& a, ClusterModel& cm) {
+  const bool relevant = minLeaders_.count(cm.partitions[a.partition].topic) ||
+                        (a.type == ActionType::INTER_BROKER_REPLICA_SWAP &&
+                         minLeaders_.count(cm.partitions[a.destPartition].topic));
+  if (!relevant) return Acceptance::ACCEPT;
   switch (a.type) {
     case ActionType::LEADERSHIP_MOVEMENT:
     case ActionType::INTER_BROKER_REPLICA_MOVEMENT:
-    case ActionType::INTER_BROKER_REPLICA_SWAP:
+      return leaderRemoveViolates(cm, cm.replicaOnBroker(a.partition, a.sourceBroker)) ? Acceptance::REPLICA_REJECT
+                                                                                       : Acceptance::ACCEPT;
+    case ActionType::INTER_BROKER_REPLICA_SWAP: {  // acceptReplicaSwap (:116-131)
+      const int sr = cm.replicaOnBroker(a.partition, a.sourceBroker);
+      const int dr = cm.replicaOnBroker(a.destPartition, a.destinationBroker);
+      const bool sl = cm.replicas[sr].isLeader, dl = cm.replicas[dr].isLeader;
+      if (!sl && !dl) return Acceptance::ACCEPT;
+      if (sl && dl && cm.partitions[a.partition].topic == cm.partitions[a.destPartition].topic) return Acceptance::ACCEPT;
+      if (leaderRemoveViolates(cm, sr) || leaderRemoveViolates(cm, dr)) return Acceptance::REPLICA_REJECT;
       return Acceptance::ACCEPT;
+    }
     default:
       throw std::invalid_argument("Unsupported balancing action");
   }
 }
-void MinTopicLeadersPerBrokerGoal::initGoalState(ClusterModel&, const OptimizationOptions&) {}
+
+// initGoalState (:163-192) with its sanity checks (:198-241)
+void MinTopicLeadersPerBrokerGoal::initGoalState(ClusterModel& cm, const OptimizationOptions& o) {
+  minLeaders_.clear();
+  mustOrder_.clear();
+  if (bc_.minLeaderTopics.empty()) return;
+  {
+    std::vector<int> all(cm.topicNames.size());
+    for (size_t t = 0; t < all.size(); ++t) all[t] = (int)t;
+    std::vector<char> match(cm.topicNames.size(), 0);
+    for (int t : bc_.minLeaderTopics) match.at(t) = 1;
+    std::vector<int> matched;
+    for (int t : topicHashSetOrder(cm, all))  // clusterModel.topics(): a HashSet<String>
+      if (match[t]) matched.push_back(t);
+    mustOrder_ = topicHashSetOrder(cm, matched);
+  }
+  // clusterModel.numLeadersPerTopic: one leader per partition
+  std::map<int, int> numLeaders;
+  for (const Partition& p : cm.partitions)
+    if (std::find(mustOrder_.begin(), mustOrder_.end(), p.topic) != mustOrder_.end()) numLeaders[p.topic]++;
+  int eligible = 0;
+  for (int b : cm.aliveBrokers()) eligible += eligibleToHaveLeaders(cm, b, o) ? 1 : 0;
+  for (int t : mustOrder_)
+    minLeaders_[t] = bc_.minTopicLeadersPerBroker == 0 ? (eligible == 0 ? 0 : numLeaders[t] / eligible)
+                                                        : bc_.minTopicLeadersPerBroker;
+  // validateTopicsWithMinLeaderIsNotExcluded (:198-215): the excluded ones joined in HashSet<String> order
+  if (!o.excludedTopics.empty()) {
+    std::vector<int> bad;
+    for (int t : mustOrder_)
+      if (o.excludedTopics.count(t)) bad.push_back(t);
+    if (!bad.empty()) {
+      std::string s;
+      for (int t : topicHashSetOrder(cm, bad)) s += (s.empty() ? "" : ", ") + cm.topicNames[t];
+      throw OptimizationFailure("[" + name() + "] Topics that must have a minimum number of leaders per broker cannot be "
+                                "excluded. This error implies a config error. Topics should not be excluded=[" + s +
+                                "] (see topics.with.min.leaders.per.broker).");
+    }
+  }
+  // validateEnoughLeaderToDistribute (:217-230) over numLeadersByTopicNames (a HashMap<String, Integer>)
+  for (int t : mustOrder_) {
+    const int total = eligible * minLeaders_[t];
+    if (numLeaders[t] < total) {
+      ProvisionRec rec;
+      rec.numPartitions = total;
+      throw OptimizationFailure("[" + name() + "] Cannot distribute " + std::to_string(numLeaders[t]) + " leaders over " +
+                                    std::to_string(eligible) + " broker(s) with minimum required per broker leader count " +
+                                    std::to_string(minLeaders_[t]) + " for topic " + cm.topicNames[t] + ".",
+                                rec);
+    }
+  }
+  // validateBrokersAllowedReplicaMoveExist (:232-241)
+  int allowed = 0;
+  allowedForReplicaMove(cm, o, &allowed);
+  if (allowed == 0) {
+    ProvisionRec rec;
+    rec.numBrokers = cm.maxReplicationFactor;
+    throw OptimizationFailure("[" + name() + "] All alive brokers are excluded from replica moves.", rec);
+  }
+  SortSpec spec;
+  if (o.onlyMoveImmigrantReplicas) spec.selection.push_back({SelFn::IMMIGRANTS});
+  Selection incl{SelFn::INCLUDED_TOPICS};
+  incl.topics = std::make_shared<std::unordered_set<int>>(mustOrder_.begin(), mustOrder_.end());
+  spec.selection.push_back(incl);
+  if (!o.onlyMoveImmigrantReplicas) spec.priority.push_back(PrioFn::IMMIGRANTS);
+  for (size_t b = 0; b < cm.brokers.size(); ++b) cm.trackSortedReplicas((int)b, replicaSortName(false, false), spec);
+}
+
+// selfSatisfied (:252-263)
 bool MinTopicLeadersPerBrokerGoal::selfSatisfied(ClusterModel& cm, const BalancingAction& a) {
   const int r = cm.replicaOnBroker(a.partition, a.sourceBroker);
   if (cm.isCurrentOffline(r)) return a.type == ActionType::INTER_BROKER_REPLICA_MOVEMENT;
-  throw std::logic_error("MinTopicLeadersPerBrokerGoal moves only offline replicas without configured topics");
+  const int t = cm.partitions[a.partition].topic;
+  return cm.numLeadersFor(a.sourceBroker, t) > minLeaders_.at(t);
 }
-// MinTopicLeadersPerBrokerGoal.updateGoalState (:276-285)
+
+// updateGoalState (:279-288); ensureBrokersAllHaveEnoughLeaderOfTopics only logs
 void MinTopicLeadersPerBrokerGoal::updateGoalState(ClusterModel& cm, const OptimizationOptions&) {
   ensureNoOfflineReplicas(cm, name());
   ensureReplicasMoveOffBrokersWithBadDisks(cm, name());
   finished_ = true;
 }
-// MinTopicLeadersPerBrokerGoal.rebalanceForBroker (:311-330) -> moveAwayOfflineReplicas (:455-478)
+
+// rebalanceForBroker (:317-334)
 void MinTopicLeadersPerBrokerGoal::rebalanceForBroker(int b, ClusterModel& cm, const GoalList& g,
                                                       const OptimizationOptions& o) {
+  moveAwayOfflineReplicas(b, cm, g, o);
+  if (minLeaders_.empty()) return;
+  if (!(cm.brokers[b].isAlive() && eligibleToHaveLeaders(cm, b, o))) return;
+  for (int t : mustOrder_) moveLeaderOfTopicToBroker(t, b, cm, g, o);
+}
+
+// maybeMoveLeaderOfTopicToBroker (:336-409) with getBrokersWithExcessiveLeaderToMove (:418-430). The priority
+// queue's keys (live leader counts) only change for the broker just polled (a move goes from it to `b`, which is
+// never queued: its count is below the minimum), so polling the smallest (count desc, id) is the queue's order.
+void MinTopicLeadersPerBrokerGoal::moveLeaderOfTopicToBroker(int t, int b, ClusterModel& cm, const GoalList& g,
+                                                             const OptimizationOptions& o) {
+  const int mn = minLeaders_.at(t);
+  int recv = cm.numLeadersFor(b, t);
+  if (recv >= mn) return;
+  const std::string sortName = replicaSortName(false, false);
+  std::vector<int> followers;
+  for (int r : cm.sortedReplicasClone(b, sortName))
+    if (!cm.replicas[r].isLeader && cm.partitions[cm.replicas[r].partition].topic == t) followers.push_back(r);
+  for (int f : followers) {
+    const int leader = cm.partitions[cm.replicas[f].partition].leader;
+    if (cm.numLeadersFor(cm.replicas[leader].broker, t) > mn &&
+        maybeApplyBalancingAction(cm, leader, {b}, ActionType::LEADERSHIP_MOVEMENT, g, o) >= 0) {
+      if (++recv >= mn) return;
+    }
+  }
+  std::vector<int> pq;
+  for (int x : cm.aliveBrokers())
+    if (cm.numLeadersFor(x, t) > mn) pq.push_back(x);
+  while (!pq.empty()) {
+    size_t best = 0;
+    for (size_t i = 1; i < pq.size(); ++i) {
+      const int ci = cm.numLeadersFor(pq[i], t), cb = cm.numLeadersFor(pq[best], t);
+      if (ci > cb || (ci == cb && cm.brokers[pq[i]].id < cm.brokers[pq[best]].id)) best = i;
+    }
+    const int giver = pq[best];
+    pq.erase(pq.begin() + (long)best);
+    std::vector<int> leaders;
+    for (int r : cm.sortedReplicasClone(giver, sortName))
+      if (cm.replicas[r].isLeader && cm.partitions[cm.replicas[r].partition].topic == t) leaders.push_back(r);
+    bool moved = false;
+    int giverCount = (int)leaders.size();
+    for (int l : leaders)
+      if (maybeApplyBalancingAction(cm, l, {b}, ActionType::INTER_BROKER_REPLICA_MOVEMENT, g, o) >= 0) {
+        moved = true;
+        break;
+      }
+    if (moved) {
+      if (++recv >= mn) return;
+      if (--giverCount > mn) pq.push_back(giver);
+    }
+  }
+}
+
+// moveAwayOfflineReplicas (:444-464)
+void MinTopicLeadersPerBrokerGoal::moveAwayOfflineReplicas(int b, ClusterModel& cm, const GoalList& g,
+                                                           const OptimizationOptions& o) {
   if (!hasOfflineReplicas(cm, b)) return;
   // TreeSet by (replica count, id) over alive brokers: iterated in its construction order afterwards
   std::vector<int> eligible = sortedBy(cm.aliveBrokers(), [&](int x, int y) {
@@ -1353,11 +1517,20 @@ void BrokerSetAwareGoal::initGoalState(ClusterModel& cm, const OptimizationOptio
     rec.numBrokers = cm.maxReplicationFactor;
     throw OptimizationFailure("[" + name() + "] All alive brokers are excluded from replica moves.", rec);
   }
-  excludedTopics_.clear();  // no MinTopicLeadersPerBroker topics are configured
+  // _mustHaveTopicLeadersPerBroker (MinTopicLeadersPerBrokerGoal's topics) and _excludedTopics = those + the
+  // options' excluded topics (:136-139)
+  mustHaveTopics_.clear();
+  mustHaveTopics_.insert(bc_.minLeaderTopics.begin(), bc_.minLeaderTopics.end());
+  excludedTopics_.clear();
   excludedTopics_.insert(o.excludedTopics.begin(), o.excludedTopics.end());
+  excludedTopics_.insert(mustHaveTopics_.begin(), mustHaveTopics_.end());
   SortSpec spec;
   if (o.onlyMoveImmigrantReplicas) spec.selection.push_back({SelFn::IMMIGRANTS});
-  if (!o.excludedTopics.empty()) spec.selection.push_back({SelFn::EXCLUDED_TOPICS});
+  if (!excludedTopics_.empty()) {
+    Selection ex{SelFn::EXCLUDED_TOPICS};
+    ex.topics = std::make_shared<std::unordered_set<int>>(excludedTopics_.begin(), excludedTopics_.end());
+    spec.selection.push_back(ex);
+  }
   for (size_t b = 0; b < cm.brokers.size(); ++b) cm.trackSortedReplicas((int)b, replicaSortName(false, false), spec);
   if (bc_.brokerSets.empty()) throw std::invalid_argument("[" + name() + "] no broker sets (BrokerSetResolutionException)");
   brokersByBrokerSet_.clear();
@@ -1408,6 +1581,8 @@ bool BrokerSetAwareGoal::violates(ClusterModel& cm, int r, int dst) {
 
 // actionAcceptance (:229-257)
 Acceptance BrokerSetAwareGoal::actionAcceptance(const BalancingAction& a, ClusterModel& cm) {
+  // offline replicas MinTopicLeadersPerBrokerGoal moves: its topics are accepted whatever the action (:258-264)
+  if (mustHaveTopics_.count(cm.partitions[a.partition].topic)) return Acceptance::ACCEPT;
   switch (a.type) {
     case ActionType::LEADERSHIP_MOVEMENT:
       return Acceptance::ACCEPT;

@@ -87,7 +87,11 @@ bool ClusterModel::passesSelection(const SortSpec& spec, int r) const {
       case SelFn::IMMIGRANTS: ok = isImmigrant(r); break;
       case SelFn::IMMIGRANT_OR_OFFLINE: ok = isImmigrant(r) || isCurrentOffline(r); break;
       case SelFn::EXCLUDED_TOPICS:  // r.isOriginalOffline() || !excludedTopics.contains(topic)
-        ok = isOriginalOffline(r) || !excludedTopicsSel.count(partitions[rep.partition].topic);
+        ok = isOriginalOffline(r) ||
+             !(s.topics ? *s.topics : excludedTopicsSel).count(partitions[rep.partition].topic);
+        break;
+      case SelFn::INCLUDED_TOPICS:  // includedTopics.contains(topic) (ReplicaSortFunctionFactory.java:153-155)
+        ok = s.topics->count(partitions[rep.partition].topic) > 0;
         break;
       case SelFn::ABOVE_LIMIT: ok = replicaUtil(r, s.resource) > s.limit; break;
       case SelFn::BELOW_LIMIT: ok = replicaUtil(r, s.resource) < s.limit; break;
@@ -95,6 +99,13 @@ bool ClusterModel::passesSelection(const SortSpec& spec, int r) const {
     if (!ok) return false;
   }
   return true;
+}
+
+int ClusterModel::numLeadersFor(int b, int topic) const {
+  int n = 0;
+  for (int r : brokers[b].replicas)
+    if (replicas[r].isLeader && partitions[replicas[r].partition].topic == topic) ++n;
+  return n;
 }
 
 // Broker.trackSortedReplicas (Broker.java:398-408): the broker's own set and one per disk

@@ -167,11 +167,13 @@ class ClusterModel;
 
 // SortedReplicas selection / priority / score functions (ReplicaSortFunctionFactory.java)
 enum class SelFn { LEADERS, FOLLOWERS, ONLINE, OFFLINE, IMMIGRANTS, IMMIGRANT_OR_OFFLINE, EXCLUDED_TOPICS,
-                   ABOVE_LIMIT, BELOW_LIMIT };
+                   ABOVE_LIMIT, BELOW_LIMIT, INCLUDED_TOPICS };
 struct Selection {
   SelFn fn;
   int resource = 0;
   double limit = 0.0;
+  // EXCLUDED_TOPICS: the set (null = ClusterModel.excludedTopicsSel); INCLUDED_TOPICS: selectReplicasBasedOnIncludedTopics
+  std::shared_ptr<const std::unordered_set<int>> topics;
 };
 enum class PrioFn { IMMIGRANTS, OFFLINE, DISK_IMMIGRANTS };
 enum class ScoreFn { NONE, BY_GROUP, REVERSE_BY_GROUP };
@@ -327,6 +329,7 @@ class ClusterModel {
   Broker& broker(int idx) { return brokers[idx]; }
   const Broker& broker(int idx) const { return brokers[idx]; }
   int replicaOnBroker(int partition, int brokerIdx) const;  // Broker.replica(tp): -1 if none
+  int numLeadersFor(int brokerIdx, int topic) const;         // Broker.numLeadersFor (Broker.java:202-204)
   bool isOriginalOffline(int r) const {
     const Replica& rep = replicas[r];
     return rep.origOfflineFlag || !brokers[rep.origBroker].isAlive();

@@ -42,6 +42,8 @@ BalancingConstraint toBc(const ccmi_balancing_constraint* c) {
     for (int k = c->broker_set_offset[i]; k < c->broker_set_offset[i + 1]; ++k) v.push_back(c->broker_set_members[k]);
   }
   bc.brokerSetPolicy = c->broker_set_policy;
+  for (int i = 0; i < c->num_min_leader_topics; ++i) bc.minLeaderTopics.push_back(c->min_leader_topics[i]);
+  bc.minTopicLeadersPerBroker = c->min_topic_leaders_per_broker;
   return bc;
 }
 
@@ -191,8 +193,10 @@ void* oc_from_desc(const ccmi_cluster_desc* d) {
       if (!d->replica_load_order) setLoad(rr);
     }
     // hand-built models: every createReplica first, then setReplicaLoad in the caller's order
-    if (d->replica_load_order)
-      for (int i = 0; i < d->num_replicas; ++i) setLoad(d->replica_load_order[i]);
+    if (d->replica_load_order) {
+      const int n = d->num_replica_loads > 0 ? d->num_replica_loads : d->num_replicas;
+      for (int i = 0; i < n; ++i) setLoad(d->replica_load_order[i]);
+    }
     for (int p = 0; p < d->num_partitions; ++p) {
       auto& lst = cm.partitions[p].replicas;
       lst.assign(d->partition_replicas + d->partition_offset[p], d->partition_replicas + d->partition_offset[p + 1]);

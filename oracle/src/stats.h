@@ -28,6 +28,10 @@ struct BalancingConstraint {
   // replicaToBrokerSetMappingPolicy() (0 TopicNameHash, 1 ReplicaToOriginal)
   std::map<std::string, std::vector<int>> brokerSets;
   int brokerSetPolicy = 0;
+  // topics.with.min.leaders.per.broker as the topics it matches (topic indices), min.topic.leaders.per.broker
+  // (BalancingConstraint.java:92-93, AnalyzerConfig.java:401-414)
+  std::vector<int> minLeaderTopics;
+  int minTopicLeadersPerBroker = 1;
 };
 
 struct ClusterModelStats {

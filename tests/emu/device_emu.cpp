@@ -33,6 +33,7 @@ struct Emu {
   std::vector<int32_t> bNrep, bNlead, rPart, rBroker, rOrig, pOff, pBrokers, topicCount, topicNrep;
   std::vector<int32_t> bRack, pTopic, tUpper, tLower, bSet, rSet;
   std::vector<int32_t> pIneligOff, pIneligB;  // Partition._ineligibleBrokers (empty: none)
+  std::vector<int32_t> topicLead, tMinLead;   // Broker.numLeadersFor counts (empty: not kept), MinTopicLeaders minima
   std::vector<uint8_t> bAlive, rFlags;
   std::vector<uint32_t> allowed;
   // chain state (device.h uploadLoads)
@@ -96,6 +97,8 @@ struct View {
   int tLower(int t) const { return e.tLower[t]; }
   int bset(int b) const { return e.bSet.empty() ? -1 : e.bSet[b]; }
   int rbset(int r) const { return e.rSet.empty() ? -1 : e.rSet[r]; }
+  int tlead(int t, int b) const { return e.topicLead.at((size_t)t * e.ldB + b); }
+  int tMinLead(int t) const { return e.tMinLead.empty() ? -1 : e.tMinLead[t]; }
   // RackAwareGoal.rackAwareEligibleBrokers membership for (replica r, destination d)
   bool rackEligible(int r, int d) const {
     std::vector<int> racks;
@@ -180,6 +183,11 @@ void Device::setTopicLimits(const int32_t* upper, const int32_t* lower) {
   E(st_).tLower.assign(lower, lower + T_);
 }
 
+void Device::enableTopicLeaders(const int32_t* dense) {
+  E(st_).topicLead.assign(dense, dense + (size_t)T_ * ldB_);
+}
+void Device::setMinLeaders(const int32_t* tMin) { E(st_).tMinLead.assign(tMin, tMin + T_); }
+
 void Device::setBrokerSets(const int32_t* brokerSet, const int32_t* replicaSet) {
   E(st_).bSet.assign(brokerSet, brokerSet + B_);
   E(st_).rSet.assign(replicaSet, replicaSet + R_);
@@ -206,7 +214,7 @@ void Device::flushOnly() {
     for (int k = 0; k < x.n; ++k) e.pBrokers[e.pOff[x.p] + k] = x.brokers[k];
     e.pLeadNwOut[x.p] = x.leadNwOut;
   }
-  for (const TopicCountDelta& d : tdeltas) e.topicCount[(size_t)d.topic * ldB_ + d.broker] += d.delta;
+  for (const TopicCountDelta& d : tdeltas) (d.kind ? e.topicLead : e.topicCount).at((size_t)d.topic * ldB_ + d.broker) += d.delta;
   brows.clear();
   rrows.clear();
   prows.clear();
@@ -321,6 +329,9 @@ struct EmuApply {
   int& slot(int p, int i) { return e.pSlots[e.pOff[p] + i]; }
   int& leader(int p) { return e.pLeader[p]; }
   void topicAdd(int t, int b, int d) { e.topicCount[(size_t)t * e.ldB + b] += d; }
+  void topicLeadAdd(int t, int b, int d) {
+    if (!e.topicLead.empty()) e.topicLead[(size_t)t * e.ldB + b] += d;
+  }
   // the records a move touched, back into the emulated columns the predicates read
   void writeBroker(int b) {
     const BrokerRec& x = brokers[b];

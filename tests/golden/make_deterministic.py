@@ -198,6 +198,75 @@ def rack_id_mapper_cluster(mapped):  # analyzer/RackAwareGoalTest.java:74-100 an
     return m
 
 
+# MinTopicLeadersPerBrokerGoal models: common/TestConstants.java:14-18, DeterministicCluster.java:55-61
+TOPIC_MUST = "must_have_leader_replica_on_broker_topic"  # TestConstants.TOPIC_MUST_HAVE_LEADER_REPLICAS_ON_BROKERS
+TOPIC0, TOPIC1 = "topic0", "topic1"
+RACK_BY_BROKER3 = {0: 0, 1: 1, 2: 1, 3: 1}
+HALF = (TYPICAL_CPU_CAPACITY / 2, LARGE_BROKER_CAPACITY / 2, MEDIUM_BROKER_CAPACITY / 2, LARGE_BROKER_CAPACITY / 2)
+
+
+def min_leader_unsatisfiable():  # DeterministicCluster.java:296-316 minLeaderReplicaPerBrokerUnsatisfiable()
+    m = Model("DeterministicCluster.java:296-316 minLeaderReplicaPerBrokerUnsatisfiable()", RACK_BY_BROKER2)
+    m.create(0, TOPIC_MUST, 0, 0, True).create(1, TOPIC_MUST, 0, 1, False)
+    m.load(0, TOPIC_MUST, 0, *HALF).load(1, TOPIC_MUST, 0, *HALF)
+    return m
+
+
+def min_leader_satisfiable():  # DeterministicCluster.java:329-365 minLeaderReplicaPerBrokerSatisfiable()
+    m = Model("DeterministicCluster.java:329-365 minLeaderReplicaPerBrokerSatisfiable()", RACK_BY_BROKER2)
+    m.create(0, TOPIC_MUST, 0, 0, True).create(0, TOPIC_MUST, 1, 0, True)
+    m.create(1, TOPIC_MUST, 2, 0, True).create(1, TOPIC_MUST, 0, 1, False)
+    m.create(2, TOPIC_MUST, 2, 1, False).create(2, TOPIC_MUST, 1, 1, False)
+    # five setReplicaLoad calls: the T_P1 follower on broker 2 keeps an empty Load
+    for b, p in ((0, 0), (0, 1), (1, 0), (1, 2), (2, 2)):
+        m.load(b, TOPIC_MUST, p, *HALF)
+    return m
+
+
+def min_leader_satisfiable2():  # DeterministicCluster.java:378-416 minLeaderReplicaPerBrokerSatisfiable2()
+    m = Model("DeterministicCluster.java:378-416 minLeaderReplicaPerBrokerSatisfiable2()", RACK_BY_BROKER2)
+    m.create(0, TOPIC_MUST, 0, 0, True).create(0, TOPIC_MUST, 1, 0, True).create(0, TOPIC_MUST, 2, 0, True)
+    m.create(1, TOPIC_MUST, 1, 1, False)
+    m.create(2, TOPIC_MUST, 0, 1, False).create(2, TOPIC_MUST, 2, 1, False)
+    for b, p in ((0, 0), (2, 0), (0, 1), (1, 1), (2, 2), (0, 2)):
+        m.load(b, TOPIC_MUST, p, *HALF)
+    return m
+
+
+def min_leader_two_topics(partitions, source):  # DeterministicCluster.java:429-488 / :501-574 (Satisfiable4 / 5)
+    m = Model(source, RACK_BY_BROKER2)
+    tps = [(t, p) for t in (TOPIC0, TOPIC1) for p in range(partitions)]
+    for t, p in tps:
+        m.create(0, t, p, 0, True)
+    for t, p in tps:
+        m.create(1, t, p, 1, False)
+    for b in (0, 1):
+        for t, p in tps:
+            m.load(b, t, p, *HALF)
+    return m
+
+
+def min_leader_satisfiable3():  # DeterministicCluster.java:588-645 minLeaderReplicaPerBrokerSatisfiable3()
+    m = Model("DeterministicCluster.java:588-645 minLeaderReplicaPerBrokerSatisfiable3()", RACK_BY_BROKER3)
+    # create + setReplicaLoad interleaved; every load is the same, so the aggregates do not depend on the order.
+    # Every replica is created at index 0: a later one goes in front of the partition's earlier one.
+    for broker, parts, leader in ((1, range(0, 4), True), (1, range(4, 10), False), (2, range(4, 10), True),
+                                  (2, range(10, 16), False), (3, range(10, 16), True), (3, range(0, 4), False)):
+        for i in parts:
+            m.create(broker, TOPIC_MUST, i, 0, leader)
+            m.load(broker, TOPIC_MUST, i, *HALF)
+    return m
+
+
+def leader_replica_unsatisfiable():  # DeterministicCluster.java:1591-1620 leaderReplicaPerBrokerUnsatisfiable()
+    m = Model("DeterministicCluster.java:1591-1620 leaderReplicaPerBrokerUnsatisfiable()", RACK_BY_BROKER2)
+    m.create(0, TOPIC_MUST, 0, 0, True).create(0, TOPIC_MUST, 1, 0, True)
+    m.create(1, TOPIC_MUST, 1, 1, False).create(2, TOPIC_MUST, 0, 1, False)
+    for b, p in ((0, 0), (2, 0), (0, 1), (1, 1)):
+        m.load(b, TOPIC_MUST, p, *HALF)
+    return m
+
+
 def uniform(c):
     return dict(CPU=c, DISK=c, NW_IN=c, NW_OUT=c)
 
@@ -213,6 +282,15 @@ def models():
         "unbalanced4": create_unbalanced([T1], 8, "DeterministicCluster.java:77-108 unbalanced4()"),
         # Set.of(T1, T2) iterates in a per-JVM salted order; transcribed as T1 then T2
         "unbalanced5": create_unbalanced([T1, T2], 14, "DeterministicCluster.java:113-116 unbalanced5() (T1, T2)"),
+        "minLeaderReplicaPerBrokerUnsatisfiable": min_leader_unsatisfiable(),
+        "minLeaderReplicaPerBrokerSatisfiable": min_leader_satisfiable(),
+        "minLeaderReplicaPerBrokerSatisfiable2": min_leader_satisfiable2(),
+        "minLeaderReplicaPerBrokerSatisfiable3": min_leader_satisfiable3(),
+        "minLeaderReplicaPerBrokerSatisfiable4": min_leader_two_topics(
+            3, "DeterministicCluster.java:429-488 minLeaderReplicaPerBrokerSatisfiable4()"),
+        "minLeaderReplicaPerBrokerSatisfiable5": min_leader_two_topics(
+            4, "DeterministicCluster.java:501-574 minLeaderReplicaPerBrokerSatisfiable5()"),
+        "leaderReplicaPerBrokerUnsatisfiable": leader_replica_unsatisfiable(),
     }
     # DeterministicClusterTest deck #5 (DeterministicClusterTest.java:181-197): uniform capacities
     for name, c in (("LARGE", LARGE_BROKER_CAPACITY), ("MEDIUM", MEDIUM_BROKER_CAPACITY),

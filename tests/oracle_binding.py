@@ -117,6 +117,11 @@ class OracleCluster:
     def from_desc(desc: ccmi.ClusterDesc) -> "OracleCluster":
         return OracleCluster(Oracle.lib().oc_from_desc(C.byref(desc)))
 
+    def topic_names(self) -> List[str]:
+        if getattr(self, "_topics", None) is None:
+            self._topics = [self.L.oc_topic_name(self.h, t).decode() for t in range(self.T)]
+        return self._topics
+
     def __del__(self):
         try:
             self.L.oc_free(self.h)
@@ -153,7 +158,7 @@ class OracleCluster:
         kinds = (C.c_int32 * len(goal_names))(*[ccmi.GOAL_KINDS[n] for n in goal_names])
         res = (ccmi.GoalResultStruct * len(goal_names))()
         o, keep = (options or ccmi.OptimizationOptions()).to_struct()
-        c = (constraint or ccmi.BalancingConstraint()).to_struct()
+        c = (constraint or ccmi.BalancingConstraint()).to_struct(self.topic_names())
         st = self.L.oc_optimize(self.h, kinds, len(goal_names), C.byref(c), C.byref(o), res)
         if st != 0:
             err = ccmi._STATUS.get(st, RuntimeError)(self.L.oc_error(self.h).decode())
@@ -178,7 +183,7 @@ class OracleCluster:
         kinds = (C.c_int32 * len(goal_names))(*[ccmi.GOAL_KINDS[n] for n in goal_names])
         res = (ccmi.GoalResultStruct * len(goal_names))()
         o, keep = (options or ccmi.OptimizationOptions()).to_struct()
-        c = (constraint or ccmi.BalancingConstraint()).to_struct()
+        c = (constraint or ccmi.BalancingConstraint()).to_struct(self.topic_names())
         self.L.oc_set_deadline(self.h, seconds)
         st = self.L.oc_optimize(self.h, kinds, len(goal_names), C.byref(c), C.byref(o), res)
         self.L.oc_set_deadline(self.h, 0.0)
@@ -230,7 +235,7 @@ class OracleCluster:
     def stats(self, constraint=None, options=None) -> dict:
         s = ccmi.StatsStruct()
         o, keep = (options or ccmi.OptimizationOptions()).to_struct()
-        c = (constraint or ccmi.BalancingConstraint()).to_struct()
+        c = (constraint or ccmi.BalancingConstraint()).to_struct(self.topic_names())
         self.L.oc_stats(self.h, C.byref(c), C.byref(o), C.byref(s))
         return ccmi.stats_to_dict(s)
 

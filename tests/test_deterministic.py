@@ -30,13 +30,22 @@ HIGH_BALANCE, MEDIUM_BALANCE, LOW_BALANCE = 1.65, 1.25, 1.05     # TestConstants
 HIGH_CAP, MEDIUM_CAP, LOW_CAP = 0.9, 0.8, 0.7                     # TestConstants.java:33-35
 
 
-def deck_constraint(balance, capacity):
-    """getDefaultCruiseControlProperties (DeterministicClusterTest.java:335-342): max.replicas.per.broker 6."""
+def deck_constraint(balance=None, capacity=None, min_leader_topics="", min_leaders=1):
+    """getDefaultCruiseControlProperties (DeterministicClusterTest.java:338-345): max.replicas.per.broker 6; the deck's
+    topics.with.min.leaders.per.broker / min.topic.leaders.per.broker overrides."""
     bc = ccmi.BalancingConstraint()
     bc.max_replicas_per_broker = 6
-    bc.set_resource_balance_percentage(balance)
-    bc.set_capacity_threshold(capacity)
+    if balance is not None:
+        bc.set_resource_balance_percentage(balance)
+    if capacity is not None:
+        bc.set_capacity_threshold(capacity)
+    bc.topics_with_min_leaders_per_broker = min_leader_topics
+    bc.min_topic_leaders_per_broker = min_leaders
     return bc
+
+
+TOPIC_MUST = "must_have_leader_replica_on_broker_topic"  # TestConstants.TOPIC_MUST_HAVE_LEADER_REPLICAS_ON_BROKERS
+MIN_LEADER = ["MinTopicLeadersPerBrokerGoal"]
 
 
 def decks():
@@ -49,11 +58,23 @@ def decks():
     for size in ("LARGE", "MEDIUM", "SMALL"):
         for model in ("smallClusterModel", "mediumClusterModel"):
             out.append((f"deck5-{model}-{size}", f"{model}_{size}", DECK_GOALS, deck_constraint(MEDIUM_BALANCE, LOW_CAP)))
-    # balance-percentage sweeps of decks #1 / #2 without the min-topic-leader topics (MinTopicLeadersPerBrokerGoal is
-    # then a no-op) (:120-150)
-    for model in ("smallClusterModel", "mediumClusterModel"):
+    # TEST DECK #1 / #2: balance percentages with topics.with.min.leaders.per.broker = T2 (small) / A (medium)
+    # (:133-150)
+    for model, topic in (("smallClusterModel", "T2"), ("mediumClusterModel", "A")):
         for bal in (HIGH_BALANCE, MEDIUM_BALANCE, LOW_BALANCE):
-            out.append((f"deck12-{model}-bal{bal}", model, DECK_GOALS, deck_constraint(bal, MEDIUM_CAP)))
+            out.append((f"deck12-{model}-bal{bal}", model, DECK_GOALS, deck_constraint(bal, MEDIUM_CAP, topic)))
+    # MinTopicLeadersPerBrokerGoal decks (:217-253); leaderReplicaPerBrokerUnsatisfiable expects the failure
+    must = deck_constraint(min_leader_topics=TOPIC_MUST)
+    out.append(("minLeader-satisfiable", "minLeaderReplicaPerBrokerSatisfiable", MIN_LEADER, must))
+    out.append(("minLeader-satisfiable2", "minLeaderReplicaPerBrokerSatisfiable2", MIN_LEADER, must))
+    out.append(("minLeader-unsatisfiable", "leaderReplicaPerBrokerUnsatisfiable", MIN_LEADER, must, None, True))
+    # satisfiable3 sets only min.topic.leaders.per.broker = 4 (the topic pattern stays empty) (:232-235)
+    out.append(("minLeader-satisfiable3", "minLeaderReplicaPerBrokerSatisfiable3", MIN_LEADER,
+                deck_constraint(min_leaders=4)))
+    out.append(("minLeader-satisfiable4", "minLeaderReplicaPerBrokerSatisfiable4", MIN_LEADER,
+                deck_constraint(min_leader_topics=r"topic\d", min_leaders=1)))
+    out.append(("minLeader-satisfiable5", "minLeaderReplicaPerBrokerSatisfiable5", MIN_LEADER,
+                deck_constraint(min_leader_topics=r"topic\d", min_leaders=0)))
     # the remaining DeterministicCluster models with the whole deck list
     for model in ("unbalanced", "unbalanced2", "unbalancedWithAFollower", "rackAwareSatisfiable",
                   "rackAwareSatisfiable2", "deadBroker"):
@@ -66,23 +87,34 @@ def decks():
     return out
 
 
-DECKS = [d if len(d) == 5 else d + ("Insufficient capacity for",) for d in decks()]
+def _deck(d):
+    """(id, model, goals, constraint, allowed failure message, OptimizationFailureException expected)"""
+    d = tuple(d) + (None, False)[len(d) - 4:]
+    return d[:4] + (d[4] or "Insufficient capacity for", d[5])
+
+
+DECKS = [_deck(d) for d in decks()]
 DECK_IDS = [d[0] for d in DECKS]
 
 
-def run_verified(runner, model_name, goals, bc, allowed_failure="Insufficient capacity for"):
+def run_verified(runner, model_name, goals, bc, allowed_failure="Insufficient capacity for", expect_failure=False):
     """executeGoalsFor + the DeterministicClusterTest.test() acceptance rule (an OptimizationFailureException is a
-    pass only with the allowed message), on `runner` (oracle or product)."""
+    pass only with the allowed message, or whenever the deck expects it), on `runner` (oracle or product)."""
     m = deterministic_models()[model_name]
     flat = build_model(m)
     pre, res, err = runner(flat, goals, bc)
+    if expect_failure:
+        assert isinstance(err, ccmi.OptimizationFailureException), err
+        return flat, None
     if err is not None:
         assert isinstance(err, ccmi.OptimizationFailureException) and allowed_failure in str(err), err
         return flat, None
     final, proposals, goal_results = res
-    problems = [verify_broken_brokers(m["dead"], final),
-                verify_soft_goal_replica_movements(proposals, offline_replicas(flat, m), goals)]
-    if not m["dead"]:  # REGRESSION applies when no replica is self-healing eligible
+    problems = []
+    if m["dead"]:  # BROKEN_BROKERS (OptimizationVerifier.java:185-201): with dead brokers, and the soft-goal rule
+        problems += [verify_broken_brokers(m["dead"], final),
+                     verify_soft_goal_replica_movements(proposals, offline_replicas(flat, m), goals)]
+    else:  # REGRESSION applies when no replica is self-healing eligible
         problems.append(verify_regression(goal_results, pre, bc))
     problems = [p for p in problems if p]
     assert not problems, problems
@@ -113,8 +145,8 @@ def product_runner(lib):
 
 @pytest.mark.parametrize("deck", DECKS, ids=DECK_IDS)
 def test_oracle_passes_deterministic_deck(oracle_lib, deck):
-    _, model, goals, bc, allowed = deck
-    run_verified(oracle_runner, model, goals, bc, allowed)
+    _, model, goals, bc, allowed, expect = deck
+    run_verified(oracle_runner, model, goals, bc, allowed, expect)
 
 
 # RackAwareGoalTest.goalNames (:57-61): the test runs for both rack goals
@@ -152,8 +184,8 @@ def test_oracle_rack_id_mapper_kat(oracle_lib, goal):
 def test_emu_deterministic_deck_matches_oracle(emu_lib, oracle_lib, deck):
     """The engine's host logic (test-only sequential Device emulation): the same deck passes and matches the oracle
     bit for bit."""
-    _, model, goals, bc, allowed = deck
-    run_verified(product_runner(emu_lib), model, goals, bc, allowed)
+    _, model, goals, bc, allowed, expect = deck
+    run_verified(product_runner(emu_lib), model, goals, bc, allowed, expect)
     flat = build_model(deterministic_models()[model])
     check_desc_against_oracle(emu_lib, flat.desc, flat, goals, bc)
 
@@ -166,8 +198,8 @@ def test_emu_rack_id_mapper_kat(emu_lib, goal):
 @pytest.mark.gpu
 @pytest.mark.parametrize("deck", DECKS, ids=DECK_IDS)
 def test_gpu_deterministic_deck_matches_oracle(gpu_lib, oracle_lib, deck):
-    _, model, goals, bc, allowed = deck
-    run_verified(product_runner(gpu_lib), model, goals, bc, allowed)
+    _, model, goals, bc, allowed, expect = deck
+    run_verified(product_runner(gpu_lib), model, goals, bc, allowed, expect)
     flat = build_model(deterministic_models()[model])
     check_desc_against_oracle(gpu_lib, flat.desc, flat, goals, bc)
 

@@ -15,10 +15,16 @@ import pytest
 
 import ccmi
 from oracle_binding import OracleCluster
+from parity import check_desc_against_oracle
 from verifier import build_model, deterministic_models
 
 ALL3 = [0, 1, 2]  # RACK_BY_BROKER.keySet()
-MIN_LEADER = "MinTopicLeadersPerBrokerGoal(topics)"  # needs topics.with.min.leaders.per.broker
+MIN_LEADER = "MinTopicLeadersPerBrokerGoal"
+# topics.with.min.leaders.per.broker = TestConstants.TOPIC_MUST_HAVE_LEADER_REPLICAS_ON_BROKERS (configOverrides)
+MUST = {"topics_with_min_leaders_per_broker": "must_have_leader_replica_on_broker_topic"}
+SAT, SAT2 = "minLeaderReplicaPerBrokerSatisfiable", "minLeaderReplicaPerBrokerSatisfiable2"
+UNSAT, LUNSAT = "minLeaderReplicaPerBrokerUnsatisfiable", "leaderReplicaPerBrokerUnsatisfiable"
+OFE = "OptimizationFailureException"
 
 # (suite, tid, goal, excluded, exception, model, dead, expected_optimized, expected_proposals)
 LEADERSHIP = [
@@ -72,9 +78,19 @@ LEADERSHIP = [
     ("PreferredLeaderElectionGoal", [], None, "unbalanced3", [], True),
     ("PreferredLeaderElectionGoal", [1], None, "unbalanced3", [], False),
     ("PreferredLeaderElectionGoal", ALL3, None, "unbalanced3", [], False),
+] + [
+    # ExcludedBrokersForLeadershipTest.java:151-192 (MinTopicLeadersPerBrokerGoal with the must-have topic)
+    (MIN_LEADER, [1], None, SAT, [], True, MUST), (MIN_LEADER, [1], None, SAT2, [], True, MUST),
+    (MIN_LEADER, [], OFE, UNSAT, [], None, MUST), (MIN_LEADER, [0], OFE, UNSAT, [], None, MUST),
+    (MIN_LEADER, [0, 1], None, UNSAT, [], True, MUST),
+    (MIN_LEADER, [1], OFE, SAT, [0], False, MUST), (MIN_LEADER, [1], OFE, SAT2, [0], False, MUST),
+    (MIN_LEADER, [1], OFE, LUNSAT, [0], True, MUST),
+    (MIN_LEADER, [], None, SAT, [], True, MUST), (MIN_LEADER, [], None, SAT2, [], True, MUST),
+    (MIN_LEADER, [], None, SAT, [0], True, MUST), (MIN_LEADER, [], None, SAT2, [0], True, MUST),
+    (MIN_LEADER, [], None, LUNSAT, [0], True, MUST),
 ]
 # ExcludedBrokersForLeadershipTest.java:148-174 (the PotentialNwOutGoal rows) are the "PotentialNwOutGoal" rows above;
-# its MinTopicLeadersPerBrokerGoal (:109-141) and BrokerSetAwareGoal (:247-261) rows need goals outside this build.
+# its BrokerSetAwareGoal rows (:247-261) are in test_broker_set.py.
 
 REPLICA_MOVE = [
     ("RackAwareGoal", [1], None, "rackAwareSatisfiable", [], True, True),
@@ -131,12 +147,23 @@ REPLICA_MOVE = [
     ("LeaderReplicaDistributionGoal", ALL3, "OptimizationFailureException", "unbalanced3", [], None, None),
     ("LeaderReplicaDistributionGoal", [2], "OptimizationFailureException", "unbalanced3", [0], None, None),
     ("LeaderReplicaDistributionGoal", [0], None, "unbalanced3", [1], False, True),
+] + [
+    # ExcludedBrokersForReplicaMoveTest.java:226-271 (MinTopicLeadersPerBrokerGoal with the must-have topic)
+    (MIN_LEADER, [], None, SAT, [], True, True, MUST), (MIN_LEADER, [], None, SAT2, [], True, True, MUST),
+    (MIN_LEADER, [1], None, SAT, [], True, True, MUST), (MIN_LEADER, [1], None, SAT2, [], True, True, MUST),
+    (MIN_LEADER, [2], None, SAT, [], True, False, MUST), (MIN_LEADER, [2], None, SAT2, [], True, True, MUST),
+    (MIN_LEADER, [], None, SAT, [0], True, True, MUST), (MIN_LEADER, [], None, SAT2, [0], True, True, MUST),
+    (MIN_LEADER, [], None, SAT, [2], True, True, MUST), (MIN_LEADER, [], None, SAT2, [2], True, True, MUST),
+    (MIN_LEADER, [1], OFE, SAT, [2], None, None, MUST), (MIN_LEADER, [1], OFE, SAT2, [2], None, None, MUST),
+    (MIN_LEADER, [0], OFE, SAT, [2], None, None, MUST), (MIN_LEADER, [0], None, SAT2, [2], True, True, MUST),
 ]
 
 
-def goal_constraint():
-    """AnalyzerUnitTestUtils.goal (AnalyzerUnitTestUtils.java:28-37)."""
+def goal_constraint(overrides=None):
+    """AnalyzerUnitTestUtils.goal (AnalyzerUnitTestUtils.java:28-37) with the row's config overrides."""
     bc = ccmi.BalancingConstraint()
+    for k, v in (overrides or {}).items():
+        setattr(bc, k, v)
     bc.max_replicas_per_broker = 5
     bc.topic_replica_balance_percentage = 1.2
     bc.set_resource_balance_percentage(1.05)
@@ -147,6 +174,9 @@ def goal_constraint():
 def _rows(suite):
     out = []
     for i, row in enumerate(LEADERSHIP if suite == "leadership" else REPLICA_MOVE):
+        over = row[-1] if isinstance(row[-1], dict) else None
+        if over is not None:
+            row = row[:-1]
         goal, excl, exc, model, dead, opt = row[:6]
         props = row[6] if len(row) > 6 else None
         marks = []
@@ -154,7 +184,7 @@ def _rows(suite):
             marks.append(pytest.mark.skip(reason=f"{goal} is not in this build"))
         elif model not in deterministic_models():
             marks.append(pytest.mark.skip(reason=f"{model} is a JBOD model (logdirs)"))
-        out.append(pytest.param(suite, goal, excl, exc, model, dead, opt, props, marks=marks,
+        out.append(pytest.param(suite, goal, excl, exc, model, dead, opt, props, over, marks=marks,
                                 id=f"{suite}-{i}-{goal}-{model}-x{''.join(map(str, excl))}-d{''.join(map(str, dead))}"))
     return out
 
@@ -174,16 +204,17 @@ def _options(suite, excl):
     return ccmi.OptimizationOptions(excluded_brokers_for_replica_move=excl)
 
 
-def run_case(runner, suite, goal, excl, exc, model, dead, opt, props):
+def run_case(runner, suite, goal, excl, exc, model, dead, opt, props, over=None):
     """ExcludedBrokersFor{Leadership,ReplicaMove}Test.test(): returns (succeeded, proposals) or raises."""
     flat = _model(model, dead)
     opts = _options(suite, excl)
+    bc = goal_constraint(over)
     if exc is not None:
         with pytest.raises(getattr(ccmi, exc)) as ei:
-            runner(flat, goal, opts)
+            runner(flat, goal, opts, bc)
         assert ei.value.provision.status == "UNDER_PROVISIONED"  # (:375 / :422)
         return
-    succeeded, proposals, provision = runner(flat, goal, opts)
+    succeeded, proposals, provision = runner(flat, goal, opts, bc)
     assert succeeded == opt
     assert provision.status != "UNDER_PROVISIONED"  # the cluster cannot be under-provisioned (:357 / :404)
     if excl and suite == "leadership":
@@ -197,32 +228,48 @@ def run_case(runner, suite, goal, excl, exc, model, dead, opt, props):
             assert not (set(p.new_replicas) - set(p.old_replicas)) & set(excl), p
 
 
-def oracle_runner(flat, goal, opts):
+def oracle_runner(flat, goal, opts, bc):
     oc = OracleCluster.from_desc(flat.desc)
-    res = oc.optimize([goal], goal_constraint(), opts)
+    res = oc.optimize([goal], bc, opts)
     return res[0].succeeded, oc.proposals(), res[0].provision
 
 
 def product_runner(lib):
-    def run(flat, goal, opts):
+    def run(flat, goal, opts, bc):
         cm = ccmi.ClusterModel(flat.desc, device=0, lib=lib, keepalive=flat)
-        g = getattr(ccmi, goal)(constraint=goal_constraint())
+        g = getattr(ccmi, goal)(constraint=bc)
         ok = g.optimize(cm, opts)
         return ok, cm.proposals(), g.provision
     return run
 
 
-@pytest.mark.parametrize("suite,goal,excl,exc,model,dead,opt,props", CASES)
-def test_oracle_excluded_brokers_kat(oracle_lib, suite, goal, excl, exc, model, dead, opt, props):
-    run_case(oracle_runner, suite, goal, excl, exc, model, dead, opt, props)
+@pytest.mark.parametrize("suite,goal,excl,exc,model,dead,opt,props,over", CASES)
+def test_oracle_excluded_brokers_kat(oracle_lib, suite, goal, excl, exc, model, dead, opt, props, over):
+    run_case(oracle_runner, suite, goal, excl, exc, model, dead, opt, props, over)
 
 
-@pytest.mark.parametrize("suite,goal,excl,exc,model,dead,opt,props", CASES)
-def test_emu_excluded_brokers_kat(emu_lib, suite, goal, excl, exc, model, dead, opt, props):
-    run_case(product_runner(emu_lib), suite, goal, excl, exc, model, dead, opt, props)
+@pytest.mark.parametrize("suite,goal,excl,exc,model,dead,opt,props,over", CASES)
+def test_emu_excluded_brokers_kat(emu_lib, suite, goal, excl, exc, model, dead, opt, props, over):
+    run_case(product_runner(emu_lib), suite, goal, excl, exc, model, dead, opt, props, over)
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("suite,goal,excl,exc,model,dead,opt,props", CASES)
-def test_gpu_excluded_brokers_kat(gpu_lib, suite, goal, excl, exc, model, dead, opt, props):
-    run_case(product_runner(gpu_lib), suite, goal, excl, exc, model, dead, opt, props)
+@pytest.mark.parametrize("suite,goal,excl,exc,model,dead,opt,props,over", CASES)
+def test_gpu_excluded_brokers_kat(gpu_lib, suite, goal, excl, exc, model, dead, opt, props, over):
+    run_case(product_runner(gpu_lib), suite, goal, excl, exc, model, dead, opt, props, over)
+
+
+@pytest.mark.parametrize("suite,goal,excl,exc,model,dead,opt,props,over", CASES)
+def test_emu_excluded_brokers_matches_oracle(emu_lib, oracle_lib, suite, goal, excl, exc, model, dead, opt, props,
+                                             over):
+    """Move for move (or the same exception, message, action log and recommendation) against the oracle."""
+    flat = _model(model, dead)
+    check_desc_against_oracle(emu_lib, flat.desc, flat, [goal], goal_constraint(over), _options(suite, excl))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("suite,goal,excl,exc,model,dead,opt,props,over", CASES)
+def test_gpu_excluded_brokers_matches_oracle(gpu_lib, oracle_lib, suite, goal, excl, exc, model, dead, opt, props,
+                                             over):
+    flat = _model(model, dead)
+    check_desc_against_oracle(gpu_lib, flat.desc, flat, [goal], goal_constraint(over), _options(suite, excl))

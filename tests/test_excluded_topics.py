@@ -22,6 +22,8 @@ from verifier import build_model, deterministic_models
 T1, T2 = "T1", "T2"
 TOPIC0, TOPIC1 = "topic0", "topic1"  # TestConstants.TOPIC0 / TOPIC1
 MIN_GAP_40 = {"topic_replica_balance_min_gap": 40}
+TOPIC_MUST = "must_have_leader_replica_on_broker_topic"  # TestConstants.TOPIC_MUST_HAVE_LEADER_REPLICAS_ON_BROKERS
+MIN_LEADERS = {"topics_with_min_leaders_per_broker": TOPIC_MUST}
 
 # (goal, excluded, exception, model, dead, expected_optimized, expected_proposals, constraint overrides)
 ROWS = [
@@ -77,9 +79,14 @@ ROWS = [
     ("LeaderReplicaDistributionGoal", [T1], None, "unbalanced3", [], True, True),
     ("LeaderReplicaDistributionGoal", [T1, T2], None, "unbalanced3", [], False, False),
     ("LeaderReplicaDistributionGoal", [], None, "unbalanced3", [0], True, True),
+    # ExcludedTopicsTest.java:171-182: topics.with.min.leaders.per.broker = the must-have topic; excluding an unrelated
+    # topic optimizes, excluding the must-have topic is a config error
+    ("MinTopicLeadersPerBrokerGoal", [T1], None, "minLeaderReplicaPerBrokerSatisfiable", [], True, True, MIN_LEADERS),
+    ("MinTopicLeadersPerBrokerGoal", [TOPIC_MUST], "OptimizationFailureException",
+     "minLeaderReplicaPerBrokerSatisfiable", [], None, None, MIN_LEADERS),
 ]
-# ExcludedTopicsTest.java:171-182 (MinTopicLeadersPerBrokerGoal with topics.with.min.leaders.per.broker), :278-302
-# (KafkaAssignerEvenRackAwareGoal) and :304-320 (BrokerSetAwareGoal) need goals outside this build.
+# ExcludedTopicsTest.java:278-302 (KafkaAssignerEvenRackAwareGoal) needs a goal outside this build; the BrokerSetAwareGoal
+# rows (:304-320) are in test_broker_set.py.
 
 
 def _cases():
@@ -112,7 +119,8 @@ def _constraint(over):
 
 
 def _options(flat, excl):
-    idx = [flat.topics.index(t) for t in excl]
+    # a name the cluster does not have matches nothing (Set<String>.contains)
+    idx = [flat.topics.index(t) for t in excl if t in flat.topics]
     return ccmi.OptimizationOptions(excluded_topics=idx)
 
 
@@ -131,7 +139,7 @@ def run_case(runner, goal, excl, exc, model, dead, opt, props, over):
     assert provision.status != "UNDER_PROVISIONED"  # ExcludedTopicsTest.java:342
     if excl:
         assert bool(proposals) == props
-        excluded_idx = {flat.topics.index(t) for t in excl}
+        excluded_idx = {flat.topics.index(t) for t in excl if t in flat.topics}
         for p in proposals:
             if flat.desc.partition_topic[p.partition] in excluded_idx:
                 removed = set(p.old_replicas) - set(p.new_replicas)
@@ -165,8 +173,8 @@ def test_emu_excluded_topics_kat(emu_lib, goal, excl, exc, model, dead, opt, pro
 
 @pytest.mark.parametrize("goal,excl,exc,model,dead,opt,props,over", CASES)
 def test_emu_excluded_topics_matches_oracle(emu_lib, oracle_lib, goal, excl, exc, model, dead, opt, props, over):
-    if exc is not None:
-        pytest.skip("the row expects OptimizationFailureException")
+    # rows that expect an OptimizationFailureException compare the exception class, message, action log and
+    # recommendation (check_desc_against_oracle)
     flat = _model(model, dead)
     check_desc_against_oracle(emu_lib, flat.desc, flat, [goal], _constraint(over), _options(flat, excl))
 
@@ -180,7 +188,5 @@ def test_gpu_excluded_topics_kat(gpu_lib, goal, excl, exc, model, dead, opt, pro
 @pytest.mark.gpu
 @pytest.mark.parametrize("goal,excl,exc,model,dead,opt,props,over", CASES)
 def test_gpu_excluded_topics_matches_oracle(gpu_lib, oracle_lib, goal, excl, exc, model, dead, opt, props, over):
-    if exc is not None:
-        pytest.skip("the row expects OptimizationFailureException")
     flat = _model(model, dead)
     check_desc_against_oracle(gpu_lib, flat.desc, flat, [goal], _constraint(over), _options(flat, excl))

@@ -97,6 +97,13 @@ def verify_regression(goal_results, pre_stats: dict, bc: ccmi.BalancingConstrain
     return None
 
 
+def verify_goal_violations(goal_results) -> Optional[str]:
+    """verifyGoalViolations (:221-230): no goal is left violated after the optimization (GoalOptimizer.java:479-481:
+    violatedGoalNamesAfterOptimization holds the goals whose optimize() returned false)."""
+    violated = [g.name for g in goal_results if not g.succeeded]
+    return f"Failed to optimize goal {violated}" if violated else None
+
+
 def verify_broken_brokers(dead: Sequence[int], final_replica_brokers: Sequence[int]) -> Optional[str]:
     """verifyBrokenBrokers (:232-250): no replica remains on a dead broker."""
     left = set(final_replica_brokers) & set(dead)
