@@ -8,6 +8,7 @@ import pytest
 import ccmi
 from oracle_binding import OracleCluster
 from test_oracle_kat import check_against_golden
+from verifier import desc_facts, reference_verifications
 
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 
@@ -45,16 +46,34 @@ def check_product_against_golden(lib, name, per_goal_stats=False):
     """The product on a golden case: action log, assignment, leaders, per-goal (name, succeeded, candidates,
     actions) and final stats; with per_goal_stats every goal's ClusterModelStats (goldens that store them)."""
     g = golden(name)
-    buf, cm, res = run_product(lib, g["props"], g["goals"], g["resource_balance_percentage"],
-                               max_replicas=g.get("max_replicas_per_broker"), options=golden_options(g),
-                               capacity=g.get("capacity_threshold"))
+    bc = constraint(g["resource_balance_percentage"], g.get("max_replicas_per_broker"), g.get("capacity_threshold"))
+    buf = ccmi.RandomCluster.generate(lib, **g["props"])
+    cm = ccmi.ClusterModel.from_buffers(buf)
+    pre = cm.cluster_stats(bc)
+    res = ccmi.GoalOptimizer(bc).optimizations(cm, ccmi.goals_from_names(g["goals"]), golden_options(g))
     check_against_golden(g, cm.actions(), cm.replica_distribution(), cm.leader_distribution(), res.goal_results,
                          res.goal_results[-1].stats, replica_disks=cm.replica_disks())
     if per_goal_stats:
         for r, e in zip(res.goal_results, g["goals_result"]):
             if "stats" in e:
                 compare_stats(r.stats, e["stats"])
+    if "verifications" in g:  # the oracle's outcome, recorded when the golden was made
+        assert verify_like_reference(buf.desc, g["goals"], res, pre, bc, cm) == g["verifications"]
     return cm, res
+
+
+def verify_like_reference(desc, goals, res, pre, bc, cm):
+    """OptimizationVerifier on the product's result (tests/verifier.py). RandomClusterTest.java:126-128 and
+    RandomSelfHealingTest.java:132-134 require BROKEN_BROKERS and REGRESSION to pass for the default goals;
+    GOAL_VIOLATION is asserted by the reference only for the KafkaAssigner goals, so it is returned (and compared
+    with the oracle's / the golden's) rather than required. violatedGoalsAfterOptimization is the product's own
+    OptimizerResult field (GoalOptimizer.java:479-481); it must name the goals reported as not succeeded."""
+    assert res.violated_goals_after == [r.name for r in res.goal_results if not r.succeeded]
+    dead, offline = desc_facts(desc)
+    v = reference_verifications(dead, offline, goals, res.goal_results, pre, bc, cm.replica_distribution(),
+                                res.proposals)
+    assert v["BROKEN_BROKERS"] in (None, "n/a") and v["REGRESSION"] in (None, "n/a"), v
+    return v
 
 
 def compare_stats(a, b, rel=1e-9):
@@ -71,19 +90,24 @@ def _key(p):
             tuple(p.old_disks or ()), tuple(p.new_disks or ()))
 
 
-def check_product_against_oracle(lib, props, goals, balance=None, device=0, max_replicas=None, options=None):
+def check_product_against_oracle(lib, props, goals, balance=None, device=0, max_replicas=None, options=None,
+                                 verify=False):
     """Live parity: same flattened input into both; action log, final assignment/leaders, per-goal results and
     every goal's post-optimization ClusterModelStats. A chain that fails (OptimizationFailureException for a hard
     goal) must fail in both with the same exception and message after the same action log."""
     buf = ccmi.RandomCluster.generate(lib, **props)
-    return check_desc_against_oracle(lib, buf.desc, buf, goals, constraint(balance, max_replicas), options, device)
+    return check_desc_against_oracle(lib, buf.desc, buf, goals, constraint(balance, max_replicas), options, device,
+                                     verify)
 
 
-def check_desc_against_oracle(lib, desc, keepalive, goals, bc, options=None, device=0):
+def check_desc_against_oracle(lib, desc, keepalive, goals, bc, options=None, device=0, verify=False):
     """check_product_against_oracle on any flattened model (RandomCluster buffers or a ClusterModelBuilder's
     FlatCluster). Returns (session, OptimizerResult or None when both raised, oracle cluster)."""
     cm = ccmi.ClusterModel(desc, device=device, lib=lib, keepalive=keepalive)
     oc = OracleCluster.from_desc(desc)
+    if verify:  # pre-optimization ClusterModelStats for REGRESSION, themselves compared with the oracle's
+        pre = cm.cluster_stats(bc, options)
+        compare_stats(pre, oc.stats(bc, options))
     perr = oerr = None
     try:
         res = ccmi.GoalOptimizer(bc).optimizations(cm, ccmi.goals_from_names(goals), options)
@@ -113,4 +137,6 @@ def check_desc_against_oracle(lib, desc, keepalive, goals, bc, options=None, dev
         compare_stats(r.stats, o.stats)
     # Set<ExecutionProposal>: order-free
     assert sorted(map(_key, res.proposals)) == sorted(map(_key, oc.proposals()))
+    if verify:
+        verify_like_reference(desc, goals, res, pre, bc, cm)
     return cm, res, oc

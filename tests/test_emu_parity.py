@@ -49,7 +49,7 @@ def test_emu_goal_subsets(emu_lib, oracle_lib, goals):
     (dict(num_brokers=80), 1500),
 ])
 def test_emu_default_goals_match_oracle(emu_lib, oracle_lib, props, max_replicas):
-    check_product_against_oracle(emu_lib, props, DEFAULT_GOALS, 1.05, max_replicas=max_replicas)
+    check_product_against_oracle(emu_lib, props, DEFAULT_GOALS, 1.05, max_replicas=max_replicas, verify=True)
 
 
 @pytest.mark.parametrize("goals", [DEFAULT_GOALS[::-1], DEFAULT_GOALS[7:] + DEFAULT_GOALS[:7],

@@ -55,7 +55,8 @@ def test_gpu_matches_oracle(gpu_lib, oracle_lib, props, balance):
     (dict(num_dead_brokers=5, rack_aware=1, leader_in_first_position=1), 3000),
 ])
 def test_gpu_random_cluster_default_goals(gpu_lib, oracle_lib, props, max_replicas):
-    check_product_against_oracle(gpu_lib, props, DEFAULT_GOALS, 1.05, max_replicas=max_replicas)
+    # with OptimizationVerifier's BROKEN_BROKERS / REGRESSION (RandomClusterTest.java:126-128) on the product
+    check_product_against_oracle(gpu_lib, props, DEFAULT_GOALS, 1.05, max_replicas=max_replicas, verify=True)
 
 
 @pytest.mark.parametrize("goals", [DEFAULT_GOALS[::-1], DEFAULT_GOALS[7:] + DEFAULT_GOALS[:7],

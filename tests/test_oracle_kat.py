@@ -15,6 +15,7 @@ import pytest
 
 import ccmi
 from oracle_binding import Oracle, OracleCluster
+from verifier import model_facts, reference_verifications
 
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 BALANCE_MARGIN = 0.9  # ResourceDistributionGoal.BALANCE_MARGIN
@@ -146,6 +147,15 @@ def test_oracle_matches_golden(oracle_lib, name):
     g = _golden(name)
     oc = OracleCluster.random(**g["props"])
     assert (oc.B, oc.T, oc.P, oc.R) == tuple(g["sizes"][k] for k in ("brokers", "topics", "partitions", "replicas"))
-    res = oc.optimize(g["goals"], _constraint(g))
+    bc = _constraint(g)
+    a0 = oc.export()
+    facts = model_facts(a0["broker_state"], a0["replica_broker"], a0["replica_partition"], a0["offline"])
+    pre = oc.stats(bc)
+    res = oc.optimize(g["goals"], bc)
     check_against_golden(g, oc.actions(), oc.replica_distribution(), oc.leader_distribution(), res, res[-1].stats,
                          rel=0.0, replica_disks=oc.replica_disks())
+    # OptimizationVerifier on the oracle (RandomClusterTest.java:126-128): BROKEN_BROKERS and REGRESSION pass, and
+    # the recorded outcome of all three is reproduced
+    v = reference_verifications(*facts, g["goals"], res, pre, bc, oc.replica_distribution(), oc.proposals())
+    assert v == g["verifications"]
+    assert v["BROKEN_BROKERS"] in (None, "n/a") and v["REGRESSION"] in (None, "n/a"), v

@@ -155,3 +155,48 @@ def offline_replicas(flat: ccmi.FlatCluster, m: dict) -> Dict[int, set]:
 
 def final_replica_brokers(replica_distribution: List[int]) -> List[int]:
     return list(replica_distribution)
+
+
+def model_facts(broker_state: Sequence[int], replica_broker: Sequence[int], replica_partition: Sequence[int],
+                replica_offline: Sequence[int]):
+    """(dead broker ids, selfHealingEligibleReplicas by partition -> original brokers) of a flattened model before
+    optimization: replicas on DEAD brokers or flagged original-offline (ClusterModel.selfHealingEligibleReplicas,
+    ClusterModel.java:203-205, filled by setBrokerState DEAD and offline replicas; broker ids equal indices in the flattened ABI)."""
+    dead = [b for b, s in enumerate(broker_state) if s == ccmi.BROKER_STATES["DEAD"]]
+    dead_set = set(dead)
+    offline: Dict[int, set] = {}
+    for r, b in enumerate(replica_broker):
+        if b in dead_set or replica_offline[r]:
+            offline.setdefault(replica_partition[r], set()).add(b)
+    return dead, offline
+
+
+def desc_facts(desc):
+    n = desc.num_replicas
+    return model_facts([desc.broker_state[b] for b in range(desc.num_brokers)], desc.replica_broker[:n],
+                       desc.replica_partition[:n], desc.replica_offline[:n])
+
+
+def reference_verifications(dead, offline, goals, goal_results, pre_stats, bc, final_brokers=None, proposals=None) \
+        -> Dict[str, Optional[str]]:
+    """executeGoalsFor's verification switch (OptimizationVerifier.java:177-216) for one pass: the outcome of
+    GOAL_VIOLATION, BROKEN_BROKERS and REGRESSION (None = passes; "n/a" = the reference skips it for this model).
+    BROKEN_BROKERS runs only with dead brokers (:185-201) and needs the final assignment and the proposals;
+    REGRESSION only without self-healing eligible replicas (:203-209). NEW_BROKERS is test_new_brokers.py's."""
+    out: Dict[str, Optional[str]] = {"GOAL_VIOLATION": verify_goal_violations(goal_results)}
+    if not dead:
+        out["BROKEN_BROKERS"] = "n/a"
+    elif final_brokers is None:
+        out["BROKEN_BROKERS"] = "not evaluated"
+    else:
+        out["BROKEN_BROKERS"] = (verify_broken_brokers(dead, final_brokers)
+                                 or verify_soft_goal_replica_movements(proposals, offline, goals))
+    out["REGRESSION"] = "n/a" if offline else verify_regression(goal_results, pre_stats, bc)
+    return out
+
+
+class GoalRecord:
+    """A golden's goals_result entry in the shape verify_regression / verify_goal_violations read."""
+
+    def __init__(self, d: dict):
+        self.name, self.succeeded, self.stats = d["name"], d["succeeded"], d.get("stats")
