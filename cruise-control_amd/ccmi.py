@@ -90,7 +90,8 @@ class ClusterDesc(C.Structure):
                 ("disk_logdir", C.POINTER(C.c_char_p)), ("disk_capacity", C.POINTER(C.c_double)),
                 ("replica_disk", C.POINTER(C.c_int32)), ("num_disk_assignments", C.c_int32),
                 ("disk_assign_replica", C.POINTER(C.c_int32)), ("disk_assign_disk", C.POINTER(C.c_int32)),
-                ("num_replica_loads", C.c_int32)]
+                ("num_replica_loads", C.c_int32), ("broker_host", C.POINTER(C.c_int32)),
+                ("disk_demoted", C.POINTER(C.c_uint8))]
 
 
 class ConstraintStruct(C.Structure):
@@ -201,6 +202,7 @@ class DeviceError(CruiseControlError):
 _STATUS = {1: IllegalArgumentException, 2: DeviceError, 3: OptimizationFailureException, 4: IllegalStateException,
            5: UnsupportedOperationException}
 
+ABI_VERSION = 6  # CCMI_ABI_VERSION of include/ccmi.h
 EXPORTED_SYMBOLS = (
     "ccmi_last_error", "ccmi_abi_version", "ccmi_default_constraint", "ccmi_default_random_cluster_props",
     "ccmi_random_cluster", "ccmi_cluster_buffers_desc", "ccmi_cluster_buffers_free", "ccmi_session_create",
@@ -212,7 +214,8 @@ EXPORTED_SYMBOLS = (
     "ccmi_set_kernel_timing", "ccmi_session_set_shard", "ccmi_rccl_unique_id", "ccmi_session_attach_rccl",
     "ccmi_topic_broker_set",
     "ccmi_builder_create", "ccmi_builder_destroy", "ccmi_builder_create_broker", "ccmi_builder_add_disk",
-    "ccmi_builder_populate_partition", "ccmi_builder_set_broker_state", "ccmi_builder_desc", "ccmi_builder_broker_ids")
+    "ccmi_builder_populate_partition", "ccmi_builder_set_broker_state", "ccmi_builder_set_disk_state",
+    "ccmi_builder_desc", "ccmi_builder_broker_ids")
 
 # int (*)(void* ctx, int64_t* key): replace *key by the MIN over all shards, return 0 (include/ccmi.h)
 AllreduceMinFn = C.CFUNCTYPE(C.c_int, C.c_void_p, C.POINTER(C.c_int64))
@@ -229,6 +232,8 @@ class Library:
         self.path = path
         self.lib = C.CDLL(path)
         L = self.lib
+        if L.ccmi_abi_version() != ABI_VERSION:  # the struct layouts below are ABI_VERSION's (include/ccmi.h)
+            raise DeviceError(f"{path} has ABI {L.ccmi_abi_version()}, this binding needs {ABI_VERSION}: rebuild it")
         L.ccmi_last_error.restype = C.c_char_p
         L.ccmi_random_cluster.argtypes = [C.POINTER(RandomClusterProps), C.POINTER(C.c_void_p)]
         L.ccmi_cluster_buffers_desc.restype = C.POINTER(ClusterDesc)
@@ -267,6 +272,7 @@ class Library:
                                                       C.c_int32, C.c_int32, C.POINTER(C.c_uint8),
                                                       C.POINTER(C.c_char_p), C.POINTER(C.c_float)]
         L.ccmi_builder_set_broker_state.argtypes = [C.c_void_p, C.c_int32, C.c_int32]
+        L.ccmi_builder_set_disk_state.argtypes = [C.c_void_p, C.c_int32, C.c_char_p, C.c_int32]
         L.ccmi_builder_desc.argtypes = [C.c_void_p, C.POINTER(ClusterDesc)]
         L.ccmi_builder_broker_ids.argtypes = [C.c_void_p, C.POINTER(C.c_int32)]
         L.ccmi_perf.argtypes = [C.c_void_p, C.POINTER(PerfStruct)]
@@ -751,6 +757,7 @@ class RandomCluster:
 
 METRIC_OF_RESOURCE = {"CPU": 0, "NW_IN": 2, "NW_OUT": 3, "DISK": 1}  # first metric id of each resource group
 BROKER_STATES = {"ALIVE": 0, "DEAD": 1, "NEW": 2, "DEMOTED": 3, "BAD_DISKS": 4}
+DISK_STATES = {"ALIVE": 0, "DEAD": 1, "DEMOTED": 2}
 
 
 class ClusterModelBuilder:
@@ -783,16 +790,21 @@ class ClusterModelBuilder:
         self.load_order: List[int] = []
         self.disks: List[tuple] = []          # (broker, logdir, capacity) in creation order
         self.disk_index: Dict[tuple, int] = {}
+        self.disk_demoted: Dict[int, int] = {}
         self.rep_disk: List[int] = []
+        self.host: Dict[int, str] = {}        # broker id -> host name (Rack._hosts key); absent = its own host
 
     def create_rack(self, rack_id: str) -> None:
         self.rack_index.setdefault(str(self.mapper(str(rack_id))), len(self.rack_index))
 
     def create_broker(self, rack_id: str, broker_id: int, capacity: Dict[str, float],
-                      disk_capacity_by_logdir: Optional[Dict[str, float]] = None) -> None:
+                      disk_capacity_by_logdir: Optional[Dict[str, float]] = None, host: Optional[str] = None) -> None:
         """createBroker with a BrokerCapacityInfo; disk_capacity_by_logdir populates the replica placement over
-        disks (Broker.java:80-83; negative capacity = dead disk)."""
+        disks (Broker.java:80-83; negative capacity = dead disk). `host` names the broker's host within its rack
+        (Rack._hosts); brokers without one get a host of their own."""
         self.create_rack(rack_id)
+        if host is not None:
+            self.host[broker_id] = str(host)
         self.brokers[broker_id] = (self.rack_index[str(self.mapper(str(rack_id)))],
                                    [float(capacity[r]) for r in RESOURCES])
         for logdir, cap in (disk_capacity_by_logdir or {}).items():
@@ -840,6 +852,14 @@ class ClusterModelBuilder:
     def set_broker_state(self, broker_id: int, state: str) -> None:
         self.state[broker_id] = BROKER_STATES[state]
 
+    def set_disk_state(self, broker_id: int, logdir: str, state: str) -> None:
+        """Disk.setState: "DEMOTED" or "ALIVE" (DemoteBrokerRunnable.java:144-148)."""
+        if (broker_id, logdir) not in self.disk_index:
+            raise IllegalStateException(f"Broker {broker_id} does not have logdir {logdir}.")
+        if state not in ("ALIVE", "DEMOTED"):
+            raise IllegalArgumentException(f"unsupported disk state {state}")
+        self.disk_demoted[self.disk_index[(broker_id, logdir)]] = 1 if state == "DEMOTED" else 0
+
     def build(self) -> "FlatCluster":
         return FlatCluster(self)
 
@@ -872,7 +892,15 @@ class FlatCluster:
             self.keep.update(disk_broker=arr(C.c_int32, [x[0] for x in bld.disks]),
                              disk_logdir=arr(C.c_char_p, [x[1].encode() for x in bld.disks]),
                              disk_capacity=arr(C.c_double, [x[2] for x in bld.disks]),
-                             replica_disk=arr(C.c_int32, bld.rep_disk))
+                             replica_disk=arr(C.c_int32, bld.rep_disk),
+                             disk_demoted=arr(C.c_uint8, [bld.disk_demoted.get(k, 0) for k in range(D)]))
+        if bld.host:  # one host per (rack, name); a broker without a name is alone on its host
+            index: Dict[tuple, int] = {}
+            hosts = []
+            for b in range(B):
+                key = (bld.brokers[b][0], bld.host[b]) if b in bld.host else ("own", b)
+                hosts.append(index.setdefault(key, len(index)))
+            self.keep["broker_host"] = arr(C.c_int32, hosts)
         for (topic, num), p in bld.parts.items():
             self.keep["partition_topic"][p] = bld.topic_index[topic]
             self.keep["partition_number"][p] = num
@@ -951,6 +979,12 @@ class LoadMonitorModel:
 
     def set_broker_state(self, broker_id: int, state: str) -> None:
         self.lib.check(self.lib.lib.ccmi_builder_set_broker_state(self.handle, broker_id, BROKER_STATES[state]))
+        self._desc = None
+
+    def set_disk_state(self, broker_id: int, logdir: str, state: str) -> None:
+        """Disk.setState (DemoteBrokerRunnable.java:144-148): "ALIVE" or "DEMOTED"."""
+        self.lib.check(self.lib.lib.ccmi_builder_set_disk_state(self.handle, broker_id, logdir.encode(),
+                                                                DISK_STATES[state]))
         self._desc = None
 
     def desc(self) -> ClusterDesc:

@@ -146,6 +146,17 @@ void setOptions(ccmi_session* s, const ccmi_balancing_constraint* c, const ccmi_
   s->model.setMustTopicSelection(must);
 }
 
+// The scan server (device.h) never outlives the API call that started it.
+struct StopServerOnExit {
+  ccmi_session* s;
+  ~StopServerOnExit() {
+    try {
+      if (s && s->device) s->device->stopServer();
+    } catch (std::exception&) {
+    }
+  }
+};
+
 std::vector<int32_t> replicaDist(const ccmi::Model& m) {
   std::vector<int32_t> v(m.R);
   for (int i = 0; i < m.R; ++i) v[i] = m.rBroker[m.pSlots[i]];
@@ -181,6 +192,21 @@ void validateChain(const ccmi_session* s, const int32_t* kinds, int n) {
   const int total = n + (int)s->engine->optimized.size();
   if (intra != 0 && intra != total)
     throw std::invalid_argument("intra-broker goals cannot be optimized together with inter-broker goals");
+  // host resources (Resource.isHostResource: CPU, NW_IN, NW_OUT) are checked against the host's load and capacity by
+  // these goals; with two brokers on one host that differs from the per-broker evaluation of this build (ccmi.h)
+  if (s->model.sharedHosts)
+    for (int i = 0; i < n; ++i)
+      switch (kinds[i]) {
+        case CCMI_GOAL_CPU_CAPACITY:
+        case CCMI_GOAL_NW_IN_CAPACITY:
+        case CCMI_GOAL_NW_OUT_CAPACITY:
+        case CCMI_GOAL_CPU_USAGE_DISTRIBUTION:
+        case CCMI_GOAL_NW_IN_USAGE_DISTRIBUTION:
+        case CCMI_GOAL_NW_OUT_USAGE_DISTRIBUTION:
+          throw ccmi::Unsupported("goal kind " + std::to_string(kinds[i]) +
+                                  " reads host-level load, and this model has brokers sharing a host");
+        default: break;
+      }
 }
 
 // AnalyzerUtils.getDiff (AnalyzerUtils.java:63-93) against the session's initial placement
@@ -372,6 +398,7 @@ ccmi_status ccmi_goal_optimize(ccmi_session* s, int32_t goal_kind, const ccmi_ba
                                const ccmi_opt_options* o, ccmi_goal_result* result) {
   return guarded([&] {
     if (!s) throw std::invalid_argument("null session");
+    StopServerOnExit stop{s};
     setOptions(s, c, o);
     validateChain(s, &goal_kind, 1);
     auto g = ccmi::makeGoal(goal_kind);
@@ -391,6 +418,7 @@ ccmi_status ccmi_optimizations(ccmi_session* s, const int32_t* goal_kinds, int32
   return guarded([&] {
     if (!s || (!goal_kinds && n_goals > 0)) throw std::invalid_argument("null argument");
     if (n_goals <= 0) throw std::invalid_argument("At least one goal must be provided to get an optimization result.");
+    StopServerOnExit stop{s};
     setOptions(s, c, o);
     validateChain(s, goal_kinds, n_goals);
     for (int i = 0; i < n_goals; ++i) (void)ccmi::makeGoal(goal_kinds[i]);  // fail fast on unsupported kinds

@@ -10,6 +10,10 @@
 #include <cstring>
 #include <stdexcept>
 
+#include <atomic>
+#include <chrono>
+#include <mutex>
+
 #include <sched.h>
 
 namespace ccmi {
@@ -31,6 +35,10 @@ hipError_t launchScanPairs(const DevTables& T, const MutTables& M, const UpdateL
                            unsigned int* done, unsigned long long* mail, unsigned long long seq, hipStream_t st);
 hipError_t launchPrep(const MutTables& M, const UpdateList& U, const int4* req, int4* dReq, int nReq4,
                       unsigned long long* result, unsigned int* done, hipStream_t st);
+uint32_t scanXcdSliceMinCols();
+hipError_t launchScanServer(const DevTables& T, const MutTables& M, const ServerCmd* cmd, const char* pay,
+                            unsigned long long* result, unsigned int* done, unsigned long long* mail,
+                            unsigned long long* t0, unsigned long long startSeq, int blocks, hipStream_t st);
 hipError_t launchChainPairs(const DevTables& T, const ChainTables& C, const DevProgram& prog, const int32_t* pr,
                             const int32_t* pb, const int32_t* next, int n, int maxAccepts, int32_t* log,
                             ChainResultDev* out, hipStream_t st);
@@ -119,10 +127,31 @@ Device::Device(int ordinal, int B, int R, int P, int T, int maxGoalSlots)
   }
   hipCheck(hipEventCreate((hipEvent_t*)&ev0_), "hipEventCreate");
   hipCheck(hipEventCreate((hipEvent_t*)&ev1_), "hipEventCreate");
+  {  // scan server: on unless CCMI_SERVER=0; CCMI_SERVER_BLOCKS sets its workgroups (multiple of 8, <= 512)
+    const char* e = std::getenv("CCMI_SERVER");
+    serverUsable_ = !(e && e[0] == '0');
+    const char* nb = std::getenv("CCMI_SERVER_BLOCKS");
+    if (nb) serverBlocks_ = std::max(8, std::min(512, (int)std::strtol(nb, nullptr, 10) / 8 * 8));
+    // one workgroup per CU at most, so every workgroup of the server is resident with room for other kernels
+    serverBlocks_ = std::min(serverBlocks_, prop.multiProcessorCount / 8 * 8);
+    if (serverBlocks_ < 8) serverUsable_ = false;
+    if (serverUsable_) {
+      dalloc(&dServerT0_, 1);
+      try {
+        ensureFg(1 << 20);
+      } catch (std::exception&) {
+        serverUsable_ = false;  // no host-writable fine-grained VRAM: a launch per scan
+      }
+    }
+  }
 }
 
 Device::~Device() {
   (void)hipSetDevice(ordinal_);
+  try {
+    stopServer();
+  } catch (std::exception&) {
+  }
   if (ST) (void)hipStreamSynchronize(ST);
   if (stamps_) {  // average in-launch phase times of the last 1024 cross/pair scans (workgroup 0)
     std::vector<unsigned long long> h(1024 * 8);
@@ -149,6 +178,8 @@ Device::~Device() {
     if (p) (void)hipFree(p);
   for (void* p : intraAllocs_)
     if (p) (void)hipFree(p);
+  if (fg_) (void)hipFree(fg_);
+  if (dServerT0_) (void)hipFree(dServerT0_);
   if (hStage_) (void)hipHostFree(hStage_);
   if (hResult_) (void)hipHostFree(hResult_);
   if (ev0_) (void)hipEventDestroy(EV0);
@@ -182,6 +213,148 @@ void Device::ensureReq(size_t bytes) {
   reqCap_ = cap;
 }
 
+// ------------------------------------------------------------------------------------------------ scan server
+namespace {
+constexpr size_t kCmdBytes = 256;  // the ServerCmd block; the payload follows
+static_assert(sizeof(ServerCmd) <= kCmdBytes, "ServerCmd fits its block");
+// Persistent scan servers of this process per device and their workgroups: a session starts one only while the
+// device's total stays within kServerBudget workgroups, so every server's workgroups are resident together (a
+// server whose workgroups could not all be resident would never complete a command).
+constexpr int kServerBudget = 512;
+std::mutex g_serverMu;
+int g_serverWgs[64] = {};
+double nowSeconds() {
+  return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+inline void hostStoreFence() { __builtin_ia32_sfence(); }
+}  // namespace
+
+void Device::ensureFg(size_t bytes) {
+  if (bytes <= fgCap_) return;
+  stopServer();
+  size_t cap = fgCap_ ? fgCap_ : (1 << 20);
+  while (cap < bytes) cap <<= 1;
+  if (fg_) hipCheck(hipFree(fg_), "hipFree fine-grained");
+  fg_ = nullptr;
+  fgCap_ = 0;
+  hipCheck(hipExtMallocWithFlags((void**)&fg_, cap, hipDeviceMallocFinegrained), "hipExtMallocWithFlags fine-grained");
+  fgCap_ = cap;
+  // the command block starts with sequence 0 = "nothing new" (written through the BAR; never read back by the host)
+  ServerCmd z;
+  std::memset(&z, 0, sizeof(z));
+  z.seq = lastCmdSeq_;
+  std::memcpy(fg_, &z, sizeof(z));
+  hostStoreFence();
+  progSent_ = false;
+}
+
+void Device::stopServer() {
+  if (!serverOn_) return;
+  DeviceGuard dg(ordinal_);
+  ServerCmd* c = (ServerCmd*)fg_;
+  volatile int32_t* op = &c->op;
+  *op = SOP_EXIT;
+  hostStoreFence();
+  lastCmdSeq_ = ++seq_;
+  *(volatile unsigned long long*)&c->seq = lastCmdSeq_;
+  hostStoreFence();
+  serverOn_ = false;
+  {
+    std::lock_guard<std::mutex> lk(g_serverMu);
+    g_serverWgs[ordinal_ & 63] -= serverBlocks_;
+  }
+  hipCheck(hipStreamSynchronize(ST), "scan server exit");
+}
+
+// A cross / pair scan the running (or a newly started) server can take: its rows fit the LDS overlay and, when the
+// program reads topic counts, no topic delta is pending (those are applied by `prep` before any workgroup reads).
+bool Device::serveScan(const DevProgram& prog, const Staged& g, bool readsTopicCounts) {
+  (void)prog;
+  if (!serverUsable_) return false;
+  if (g.nb > kOverlayRows || g.nr > kOverlayRows || g.np > kOverlayRows) return false;
+  if (readsTopicCounts && g.nt > 0) return false;
+  return true;
+}
+
+// params: CROSS {K, Nr, N, c0, sliced, -}; PAIRS {n, keyBase, -, -, -, -}
+int64_t Device::serverRun(const DevProgram& prog, const Staged& g, int op, const int32_t* A, size_t nA,
+                          const int32_t* C, size_t nC, const int32_t params[6]) {
+  // payload: [program | rows | A | C]; the program slot is always reserved so offsets never depend on whether it is
+  // resent (a restarted server has no program in LDS: it gets the program again whatever the host sent before)
+  const size_t oProg = 0, oRows = align16(sizeof(DevProgram));
+  const size_t rows = g.end;  // [broker | replica | partition rows | topic deltas] as packUpdates laid them out
+  const size_t oA = oRows + rows, oC = oA + align16(nA * 4), end = oC + align16(nC * 4);
+  ensureFg(kCmdBytes + end);
+  const double now = nowSeconds();
+  if (serverOn_ && now - lastServerUse_ > 0.25) stopServer();  // far from the device watchdog (2 s idle)
+  if (!serverOn_) {
+    progSent_ = false;
+    bool ok;
+    {
+      std::lock_guard<std::mutex> lk(g_serverMu);
+      ok = g_serverWgs[ordinal_ & 63] + serverBlocks_ <= kServerBudget;
+      if (ok) g_serverWgs[ordinal_ & 63] += serverBlocks_;
+    }
+    if (!ok) return INT64_MIN;  // the device has its budget of servers: the caller launches instead
+    hipCheck(launchScanServer(tables(), mutTables(), (const ServerCmd*)fg_, fg_ + kCmdBytes, dResult_, dDone_,
+                              hResultDev_, dServerT0_, lastCmdSeq_, serverBlocks_, ST),
+             "scan_server");
+    serverOn_ = true;
+    perf.serverLaunches++;
+    perf.scanLaunches++;
+  }
+  const bool sendProg = !progSent_ || std::memcmp(&prog, &lastProg_, sizeof(DevProgram)) != 0;
+  char* pay = fg_ + kCmdBytes;
+  int ver = progVer_;
+  if (sendProg) {
+    std::memcpy(pay + oProg, &prog, sizeof(DevProgram));
+    lastProg_ = prog;
+    progSent_ = true;
+    ver = ++progVer_;
+  }
+  if (rows) std::memcpy(pay + oRows, hStage_, rows);
+  if (nA) std::memcpy(pay + oA, A, nA * 4);
+  if (nC) std::memcpy(pay + oC, C, nC * 4);
+  ServerCmd c;
+  std::memset(&c, 0, sizeof(c));
+  c.op = op;
+  if (op == SOP_CROSS) {
+    c.K = params[0];
+    c.Nr = params[1];
+    c.N = params[2];
+    c.c0 = params[3];
+    c.sliced = params[4];
+  } else {
+    c.n = params[0];
+    c.keyBase = params[1];
+  }
+  c.progVer = ver;
+  c.nb = g.nb;
+  c.nr = g.nr;
+  c.np = g.np;
+  c.nt = g.nt;
+  c.oProg = (uint32_t)oProg;
+  c.oB = (uint32_t)(oRows + g.obr);
+  c.oR = (uint32_t)(oRows + g.orr);
+  c.oP = (uint32_t)(oRows + g.opr);
+  c.oT = (uint32_t)(oRows + g.otd);
+  c.oA = (uint32_t)oA;
+  c.oC = (uint32_t)oC;
+  // every field but the sequence word, then (behind a store fence) the sequence word
+  std::memcpy(fg_ + sizeof(unsigned long long), (const char*)&c + sizeof(unsigned long long),
+              sizeof(ServerCmd) - sizeof(unsigned long long));
+  hostStoreFence();
+  lastCmdSeq_ = ++seq_;
+  *(volatile unsigned long long*)fg_ = lastCmdSeq_;
+  hostStoreFence();
+  waitMail(seq_);
+  lastServerUse_ = nowSeconds();
+  perf.serverScans++;
+  perf.serverBusyMs += (double)hResult_[1] * 1e-5;  // 100 MHz ticks
+  const unsigned long long lo = hResult_[0] & 0xffffffffull;
+  return lo == 0 ? -1 : (int64_t)(lo - 1);
+}
+
 DevTables Device::tables() const {
   DevTables t;
   t.brokers = brokers_;
@@ -207,6 +380,7 @@ DevTables Device::tables() const {
 void Device::uploadStatic(const double* bCapRM, const int32_t* rPart, const int32_t* rOrig, const int32_t* pOff,
                           const int32_t* topicNrep, const int32_t* bRack, const int32_t* pTopic) {
   DeviceGuard dg(ordinal_);
+  stopServer();
   for (int b = 0; b < B_; ++b) {
     BrokerRec& x = hBrokers_[b];
     for (int k = 0; k < 4; ++k) x.cap[k] = bCapRM[(size_t)k * B_ + b];
@@ -225,6 +399,7 @@ void Device::uploadStatic(const double* bCapRM, const int32_t* rPart, const int3
 
 void Device::uploadIneligible(const int32_t* off, const int32_t* brokers, int n) {
   DeviceGuard dg(ordinal_);
+  stopServer();
   if (n <= 0) return;
   hipCheck(hipMalloc((void**)&pIneligOff_, sizeof(int32_t) * (P_ + 1)), "hipMalloc pIneligOff");
   hipCheck(hipMalloc((void**)&pIneligB_, sizeof(int32_t) * n), "hipMalloc pIneligB");
@@ -237,6 +412,7 @@ void Device::uploadDynamic(const double* bUtilRM, const int32_t* bNrep, const in
                            const int32_t* rBroker, const uint8_t* rFlags, const int32_t* pBrokers,
                            const double* pLeadNwOut, const int32_t* topicCountDense) {
   DeviceGuard dg(ordinal_);
+  stopServer();
   for (int b = 0; b < B_; ++b) {
     BrokerRec& x = hBrokers_[b];
     for (int k = 0; k < 4; ++k) x.util[k] = bUtilRM[(size_t)k * B_ + b];
@@ -277,6 +453,7 @@ void Device::uploadDynamic(const double* bUtilRM, const int32_t* bNrep, const in
 
 void Device::setAllowed(int slot, const uint8_t* allowedB) {
   DeviceGuard dg(ordinal_);
+  stopServer();
   if (slot < 0 || slot >= G_) throw std::runtime_error("goal slot out of range");
   for (int b = 0; b < B_; ++b)
     allowedHost_[b] = (allowedHost_[b] & ~(1u << slot)) | (allowedB[b] ? (1u << slot) : 0u);
@@ -289,6 +466,7 @@ void Device::setAllowed(int slot, const uint8_t* allowedB) {
 
 void Device::setExclusions(const uint8_t* exclLead, const uint8_t* exclMove, const uint8_t* isNew) {
   DeviceGuard dg(ordinal_);
+  stopServer();
   const uint32_t mask = (1u << kExclLeadBit) | (1u << kExclMoveBit) | (1u << kNewBit);
   for (int b = 0; b < B_; ++b)
     allowedHost_[b] = (allowedHost_[b] & ~mask) | (exclLead[b] ? (1u << kExclLeadBit) : 0u) |
@@ -301,6 +479,7 @@ void Device::setExclusions(const uint8_t* exclLead, const uint8_t* exclMove, con
 
 void Device::setTopicLimits(const int32_t* upper, const int32_t* lower) {
   DeviceGuard dg(ordinal_);
+  stopServer();
   hipCheck(hipMemcpyAsync(tUpper_, upper, sizeof(int32_t) * T_, hipMemcpyHostToDevice, ST), "upload tUpper");
   hipCheck(hipMemcpyAsync(tLower_, lower, sizeof(int32_t) * T_, hipMemcpyHostToDevice, ST), "upload tLower");
   hipCheck(hipStreamSynchronize(ST), "sync");
@@ -308,18 +487,21 @@ void Device::setTopicLimits(const int32_t* upper, const int32_t* lower) {
 
 void Device::enableTopicLeaders(const int32_t* dense) {
   DeviceGuard dg(ordinal_);
+  stopServer();
   if (!topicLead_) dalloc(&topicLead_, (size_t)T_ * ldB_);
   hipCheck(hipMemcpy(topicLead_, dense, sizeof(int32_t) * (size_t)T_ * ldB_, hipMemcpyHostToDevice), "upload topicLead");
 }
 
 void Device::setMinLeaders(const int32_t* tMin) {
   DeviceGuard dg(ordinal_);
+  stopServer();
   if (!tMinLead_) dalloc(&tMinLead_, (size_t)T_);
   hipCheck(hipMemcpy(tMinLead_, tMin, sizeof(int32_t) * (size_t)T_, hipMemcpyHostToDevice), "upload tMinLead");
 }
 
 void Device::setBrokerSets(const int32_t* brokerSet, const int32_t* replicaSet) {
   DeviceGuard dg(ordinal_);
+  stopServer();
   hipCheck(hipMemcpy2DAsync(&brokers_[0].bset, sizeof(BrokerRec), brokerSet, sizeof(int32_t), sizeof(int32_t), B_,
                             hipMemcpyHostToDevice, ST),
            "upload broker sets");
@@ -360,9 +542,18 @@ Device::Staged Device::packUpdates(size_t extra) {
   return g;
 }
 
+// Put staged rows back into the pending lists (a scan the server declined goes through packUpdates again).
+void Device::unpackUpdates(const Staged& g) {
+  brows.assign((const BrokerRow*)(hStage_ + g.obr), (const BrokerRow*)(hStage_ + g.obr) + g.nb);
+  rrows.assign((const ReplicaRow*)(hStage_ + g.orr), (const ReplicaRow*)(hStage_ + g.orr) + g.nr);
+  prows.assign((const PartitionRow*)(hStage_ + g.opr), (const PartitionRow*)(hStage_ + g.opr) + g.np);
+  tdeltas.assign((const TopicCountDelta*)(hStage_ + g.otd), (const TopicCountDelta*)(hStage_ + g.otd) + g.nt);
+}
+
 // One `prep` launch: apply the staged rows, copy `reqBytes` of request (staged at g.end) into HBM, and (for a
 // scan) reset the result words and the arrival counter.
 void Device::launchPrepFor(const Staged& g, size_t reqBytes, bool scan) {
+  stopServer();
   const int nReq4 = (int)(align16(reqBytes) / 16);
   if (nReq4) ensureReq((size_t)nReq4 * 16);
   hipCheck(launchPrep(mutTables(), stagedList(g), (const int4*)(hStageDev_ + g.end), (int4*)dReq_, nReq4,
@@ -402,6 +593,7 @@ void Device::flushPending() {
 
 void Device::flushOnly() {
   DeviceGuard dg(ordinal_);
+  stopServer();
   if (brows.empty() && rrows.empty() && prows.empty() && tdeltas.empty()) return;
   const Staged g = packUpdates(0);
   launchPrepFor(g, 0, false);
@@ -475,6 +667,25 @@ int64_t Device::scanCross(const DevProgram& prog, const int32_t* reps, int K, co
   if ((uint64_t)K * (uint64_t)N >= (1ull << 31)) throw std::runtime_error("scan too large");
   const size_t oCand = align16((size_t)K * 4);
   const size_t req = oCand + align16((size_t)Nr * 4);
+  const bool readsTc = (prog.needs & (NEED_TOPIC | NEED_TLEAD)) != 0;
+  {
+    const Staged g = packUpdates(0);
+    if (serveScan(prog, g, readsTc)) {
+      const int32_t params[6] = {K, Nr, N, c0, Nr >= (int)scanXcdSliceMinCols() ? 1 : 0, 0};
+      const int64_t key = serverRun(prog, g, SOP_CROSS, reps, (size_t)K, cands + c0, (size_t)Nr, params);
+      if (key != INT64_MIN) {
+        perf.scanPairs += (int64_t)K * Nr;
+        perf.scanBytes += (int64_t)K * Nr * kBytesPerCandidate;
+        const int64_t required = key < 0 ? (int64_t)K * Nr : (key / N) * Nr + (key % N - c0) + 1;
+        perf.scanRequired += required;
+        perf.serverRequired += required;
+        perf.crossRequired += required;
+        return key;
+      }
+    }
+    unpackUpdates(g);
+  }
+  stopServer();
   UpdateList u;
   const char* base;
   {
@@ -482,7 +693,7 @@ int64_t Device::scanCross(const DevProgram& prog, const int32_t* reps, int K, co
     const Staged g = packUpdates(req);
     std::memcpy(hStage_ + g.end, reps, (size_t)K * 4);
     std::memcpy(hStage_ + g.end + oCand, cands + c0, (size_t)Nr * 4);
-    base = stageScan(g, req, (prog.needs & (NEED_TOPIC | NEED_TLEAD)) != 0, u);
+    base = stageScan(g, req, readsTc, u);
   }
   ++seq_;
   if (timing) (void)hipEventRecord(EV0, ST);
@@ -507,6 +718,7 @@ int64_t Device::scanCross(const DevProgram& prog, const int32_t* reps, int K, co
 int64_t Device::scanSwap(const DevProgram& prog, const int32_t* srcs, int S, const int32_t* cbOff, int M,
                          const int32_t* cbRep, int nCand, int64_t* visited) {
   DeviceGuard dg(ordinal_);
+  stopServer();
   *visited = 0;
   if (S <= 0 || M <= 0 || nCand <= 0) return -1;
   const size_t rows = (size_t)S * M;
@@ -547,11 +759,29 @@ int64_t Device::scanPairs(const DevProgram& prog, const int32_t* pr, const int32
   }
   const size_t oB = align16((size_t)n * 4);
   const size_t req = oB + align16((size_t)n * 4);
+  const bool readsTc = (prog.needs & (NEED_TOPIC | NEED_TLEAD)) != 0;
+  {
+    const Staged g0 = packUpdates(0);
+    if (serveScan(prog, g0, readsTc)) {
+      const int32_t params[6] = {n, p0, 0, 0, 0, 0};
+      const int64_t key = serverRun(prog, g0, SOP_PAIRS, pr + p0, (size_t)n, pb + p0, (size_t)n, params);
+      if (key != INT64_MIN) {
+        perf.scanPairs += n;
+        perf.scanBytes += (int64_t)n * kBytesPerCandidate;
+        const int64_t required = key < 0 ? (int64_t)n : key - p0 + 1;
+        perf.scanRequired += required;
+        perf.serverRequired += required;
+        return key;
+      }
+    }
+    unpackUpdates(g0);
+  }
+  stopServer();
   const Staged g = packUpdates(req);
   std::memcpy(hStage_ + g.end, pr + p0, (size_t)n * 4);
   std::memcpy(hStage_ + g.end + oB, pb + p0, (size_t)n * 4);
   UpdateList u;
-  const char* base = stageScan(g, req, (prog.needs & (NEED_TOPIC | NEED_TLEAD)) != 0, u);
+  const char* base = stageScan(g, req, readsTc, u);
   ++seq_;
   if (timing) (void)hipEventRecord(EV0, ST);
   hipCheck(launchScanPairs(tables(), mutTables(), u, prog, (const int32_t*)base, (const int32_t*)(base + oB), n, p0,
@@ -568,6 +798,7 @@ int64_t Device::scanPairs(const DevProgram& prog, const int32_t* pr, const int32
 
 void Device::stats(const StatsParams& P, const uint8_t* allowedAliveHost, StatsOut* out) {
   DeviceGuard dg(ordinal_);
+  stopServer();
   const size_t req = align16((size_t)ldB_);
   const Staged g = packUpdates(req);
   std::memcpy(hStage_ + g.end, allowedAliveHost, (size_t)ldB_);
@@ -597,6 +828,7 @@ namespace ccmi {
 void Device::uploadLoads(int W, const LoadVec* rLoad, const LoadVec* bLoad, const LoadVec* bLnw, const LoadVec* bPot,
                          const int32_t* pSlots, const int32_t* pLeader) {
   DeviceGuard dg(ordinal_);
+  stopServer();
   W_ = W;
   dalloc(&dRLoad_, (size_t)R_);
   dalloc(&dBLoad_, (size_t)B_);
@@ -661,6 +893,7 @@ size_t Device::stageChainCopy(size_t reqBytes, Staged& g, size_t& oReq, F fill) 
 Device::ChainResult Device::chainPairs(const DevProgram& prog, const int32_t* pr, const int32_t* pb,
                                        const int32_t* next, int n, int maxAccepts, std::vector<int32_t>& log) {
   DeviceGuard dg(ordinal_);
+  stopServer();
   ChainResult res;
   log.clear();
   if (n <= 0) {
@@ -710,6 +943,7 @@ Device::ChainResult Device::chainPairs(const DevProgram& prog, const int32_t* pr
 Device::ChainResult Device::chainRackRows(const DevProgram& prog, const int32_t* rows, int n, const int32_t* cands,
                                           int N, std::vector<int32_t>& log) {
   DeviceGuard dg(ordinal_);
+  stopServer();
   ChainResult res;
   log.clear();
   if (n <= 0) {
@@ -800,6 +1034,7 @@ void Device::uploadDisks(int D, const int32_t* bDiskOff, const int32_t* bDisks, 
                          const uint8_t* dAlive, const uint8_t* bAlive, const int32_t* rOrigDisk, const double* rDu,
                          const float* rScore, const int32_t* rTie) {
   DeviceGuard dg(ordinal_);
+  stopServer();
   D_ = D;
   auto& o = intraAllocs_;
   dallocTracked(&dBDiskOff_, (size_t)B_ + 1, o);
@@ -841,11 +1076,13 @@ void Device::uploadDisks(int D, const int32_t* bDiskOff, const int32_t* bDisks, 
 
 void Device::setDiskUtil(const double* dUtil) {
   DeviceGuard dg(ordinal_);
+  stopServer();
   hipCheck(hipMemcpyAsync(dDUtilIn_, dUtil, sizeof(double) * D_, hipMemcpyHostToDevice, ST), "upload dUtil");
 }
 
 void Device::intraRun(const IntraRequest& q, IntraResult& out) {
   DeviceGuard dg(ordinal_);
+  stopServer();
   if (!dBDiskOff_) throw std::runtime_error("intraRun before uploadDisks");
   const size_t E = (size_t)q.eOff[B_];
   auto& o = intraAllocs_;
@@ -1015,6 +1252,7 @@ void Device::intraRun(const IntraRequest& q, IntraResult& out) {
 
 void Device::statsDisks(double diskBalance, DiskStatsOut* out) {
   DeviceGuard dg(ordinal_);
+  stopServer();
   hipCheck(launchStatsDisks(dBDiskOff_, dBDisks_, dDCap_, dDAlive_, dDUtilIn_, dBAlive_, B_, diskBalance, dDiskStats_,
                             ST),
            "stats_disks");

@@ -44,6 +44,10 @@ struct DevicePerf {
   int64_t crossLaunches = 0;  // the scan_cross share of the scan counters
   int64_t crossRequired = 0;
   double crossKernelMs = 0;
+  int64_t serverLaunches = 0;  // K8 scan_server launches (each serves many scans)
+  int64_t serverScans = 0;     // scans served by a running scan_server (no launch each)
+  double serverBusyMs = 0;     // their device busy time (s_memrealtime, command seen -> result published)
+  int64_t serverRequired = 0;  // candidates those scans had to evaluate
 };
 
 // K6 (kernels/intra.hip, intra.h): one intra-broker goal over every broker in one launch.
@@ -148,6 +152,9 @@ class Device {
   DevicePerf perf;
   bool timing = false;  // record HIP events around kernels (bench/profiling)
   int ldB() const { return ldB_; }
+  // K8 scan server (kernels/scan.hip scan_server): cross / pair scans are served by one persistent launch while it
+  // runs; any other work on the session stream stops it first. CCMI_SERVER=0 turns it off (a launch per scan).
+  void stopServer();
 
  private:
   int ordinal_, B_, R_, P_, T_, ldB_, G_;
@@ -186,6 +193,7 @@ class Device {
   DevTables tables() const;
   size_t updatesBytes() const;
   Staged packUpdates(size_t extra);
+  void unpackUpdates(const Staged& g);
   void ensureStage(size_t bytes);
   void ensureReq(size_t bytes);
   void launchPrepFor(const Staged& g, size_t reqBytes, bool scan);
@@ -196,6 +204,22 @@ class Device {
   void waitMail(unsigned long long seq);
   int64_t finishScan();
   unsigned long long* stamps_ = nullptr;
+  // scan server state: the fine-grained VRAM block [ServerCmd | payload] the host writes through the BAR
+  char* fg_ = nullptr;
+  size_t fgCap_ = 0;
+  bool serverOn_ = false;
+  bool serverUsable_ = false;  // set in the constructor (gfx950, CCMI_SERVER, fine-grained VRAM host-writable)
+  int serverBlocks_ = 256;
+  int progVer_ = 0;
+  bool progSent_ = false;
+  DevProgram lastProg_{};
+  unsigned long long* dServerT0_ = nullptr;
+  unsigned long long lastCmdSeq_ = 0;  // the sequence word the command block holds
+  double lastServerUse_ = 0;  // steady-clock seconds of the last served scan (the host restarts an idle server)
+  bool serveScan(const DevProgram& prog, const Staged& g, bool readsTopicCounts);
+  int64_t serverRun(const DevProgram& prog, const Staged& g, int op, const int32_t* A, size_t nA, const int32_t* C,
+                    size_t nC, const int32_t params[6]);
+  void ensureFg(size_t bytes);
   int32_t* rowVisited_ = nullptr;
   size_t rowVisitedCap_ = 0;
   // chain state

@@ -197,6 +197,22 @@ struct ScanHeader {
   int32_t nCand; // SWAP: total candidate replicas
 };
 
+// Scan-server command (kernels/scan.hip scan_server), at the start of the fine-grained VRAM block the host writes;
+// `seq` is written last, behind a store fence. Offsets are bytes from the payload base.
+enum ServerOp : int32_t { SOP_CROSS = 0, SOP_PAIRS = 1, SOP_EXIT = 2 };
+struct alignas(16) ServerCmd {
+  unsigned long long seq;
+  int32_t op;
+  int32_t K, Nr, N, c0;  // SOP_CROSS: rows A[0, K) x columns C[0, Nr) of an N-column list starting at column c0
+  int32_t n, keyBase;    // SOP_PAIRS: pairs (A[q], C[q]), q < n, key = keyBase + q
+  int32_t sliced;
+  int32_t progVer;       // the DevProgram at oProg changes only with its version
+  int32_t nb, nr, np, nt;
+  uint32_t oProg, oB, oR, oP, oT, oA, oC;
+  int32_t pad[3];
+};
+static_assert(sizeof(ServerCmd) % 16 == 0, "ServerCmd words");
+
 // Device-resident Java loads and partition slot order, so chain kernels can apply moves themselves (apply.h).
 struct ChainTables {
   BrokerRec* brokers;

@@ -1514,8 +1514,10 @@ class ResourceDistribution : public GoalImpl {
         const int cb = pqPoll();
         polled.push_back(cb);
         const auto v = m.snapshot(cb, baseSpec);
-        for (int r : *v)
-          if (m.selects(candSpec, r)) cbRep.push_back(r);
+        for (int r : *v)  // baseSpec's other selections already hold: only the limit test remains
+          if ((candSpec.selAboveRes < 0 || m.ru(r, candSpec.selAboveRes) > candSpec.aboveLimit) &&
+              (candSpec.selBelowRes < 0 || m.ru(r, candSpec.selBelowRes) < candSpec.belowLimit))
+            cbRep.push_back(r);
         cbOff.push_back((int32_t)cbRep.size());
       }
       srcs = *m.snapshot(b, srcSpec);
@@ -1537,7 +1539,7 @@ class ResourceDistribution : public GoalImpl {
       m.relocateReplica(dp, cb, b);
       const bool done = out ? underUpper(m, b, upperThr) : aboveLower(m, b);
       if (done) return false;
-      for (size_t t = polled.size(); t-- > mi + 1;) pqUnpoll(polled[t]);  // un-poll speculative brokers
+      for (size_t t = polled.size(); t-- > (size_t)mi + 1;) pqUnpoll(polled[t]);  // un-poll speculative brokers
       pqAdd(cb);
     }
     return true;

@@ -1691,8 +1691,8 @@ class LeaderBytesIn : public GoalImpl {
 // PreferredLeaderElectionGoal.optimize (PreferredLeaderElectionGoal.java:117-190), the no-argument constructor
 // (skipUrpDemotion = excludeFollowerDemotion = false). A one-pass leadership election with no candidate search: every
 // partition's leadership goes to its first alive, online replica (with demoted brokers: only the partitions they led,
-// after their replicas moved to the end of the replica lists), so it runs on the host model and the device only sees
-// the touched rows. Demoted disks are not in the flattened model.
+// after their replicas moved to the end of the replica lists; the same for demoted disks of other alive brokers,
+// :114-124), so it runs on the host model and the device only sees the touched rows.
 
 class PreferredLeaderElection : public GoalImpl {
  public:
@@ -1719,7 +1719,20 @@ class PreferredLeaderElection : public GoalImpl {
     javaHashSetOrder(alive, ord);  // clusterModel.aliveBrokers(): a HashSet<Broker>
     std::vector<int32_t> reps;
     for (int b : ord) {
-      if (m.bState[b] != BState::DEMOTED) continue;
+      if (m.bState[b] != BState::DEMOTED) {
+        // demoted disks of a broker that is not demoted, in logdir order (Broker.disks(): the TreeMap's values)
+        for (int k = m.bDiskOff[b]; m.anyDemotedDisk && k < m.bDiskOff[b + 1]; ++k) {
+          const int d = m.bDisks[k];
+          if (!m.dDemoted[d]) continue;
+          hasDemoted = true;
+          // Disk.replicas(): the HashSet, which keeps replicas inter-broker moves took elsewhere
+          m.dReplicaSet[d].order(reps);
+          for (int r : reps) m.moveReplicaToEnd(r);
+          for (int r : reps)  // Disk.leaderReplicas(): the same set filtered by isLeader
+            if (m.rLeader[r]) toMove[m.rPart[r]] = 1;
+        }
+        continue;
+      }
       hasDemoted = true;
       m.bReplicaSet[b].order(reps);  // Broker.replicas(): HashSet order
       for (int r : reps) m.moveReplicaToEnd(r);

@@ -31,11 +31,13 @@ struct BrokerIn {
   int32_t rack;
   double cap[4];
   int32_t state;
+  std::string host;  // Rack._hosts key (handleDeadBroker: "UNKNOWN_HOST-<n>", a host of its own)
 };
 struct DiskIn {
   int32_t brokerId;
   std::string logdir;
   double cap;
+  uint8_t demoted = 0;
 };
 
 }  // namespace
@@ -56,7 +58,9 @@ struct ccmi_model_builder {
   std::vector<std::string> rLogdir;  // "" = none
   std::vector<float> rLoad;          // [R][6][W]
   // flattened output (ccmi_builder_desc)
-  std::vector<int32_t> oBrokerId, oRack, oState, oRBroker, oPartReplicas, oDiskBroker, oRDisk;
+  std::vector<int32_t> oBrokerId, oRack, oState, oRBroker, oPartReplicas, oDiskBroker, oRDisk, oHost;
+  std::vector<uint8_t> oDiskDemoted;
+  int32_t unknownHosts = 0;
   std::vector<double> oCap, oDiskCap;
   std::vector<const char*> oTopicNames, oDiskLogdir;
   std::vector<int32_t> sortedIds;
@@ -105,7 +109,7 @@ ccmi_status ccmi_builder_create(int32_t num_windows, ccmi_model_builder** out) {
 
 void ccmi_builder_destroy(ccmi_model_builder* b) { delete b; }
 
-ccmi_status ccmi_builder_create_broker(ccmi_model_builder* b, const char* rack, const char* /*host*/,
+ccmi_status ccmi_builder_create_broker(ccmi_model_builder* b, const char* rack, const char* host,
                                        int32_t broker_id, const double capacity[4], int32_t alive) {
   if (!b || !rack || !capacity || broker_id < 0) return CCMI_E_INVALID;
   return run([&] {
@@ -121,6 +125,8 @@ ccmi_status ccmi_builder_create_broker(ccmi_model_builder* b, const char* rack, 
     // handleDeadBroker creates the broker alive; setBadBrokerState marks it dead once the partitions are in — the
     // desc applies broker states after every replica is created, so the state is recorded now
     x.state = alive ? CCMI_BROKER_ALIVE : CCMI_BROKER_DEAD;
+    // a live node's host (LoadMonitor.java:602); a dead one gets UNKNOWN_HOST-<n> (ClusterModel.java:776-777)
+    x.host = alive && host ? std::string(host) : "UNKNOWN_HOST-" + std::to_string(b->unknownHosts++);
     b->brokerById.emplace(broker_id, b->brokers.size());
     b->brokers.push_back(x);
   });
@@ -151,6 +157,11 @@ ccmi_status ccmi_builder_populate_partition(ccmi_model_builder* b, const char* t
         if (replica_broker_ids[j] == replica_broker_ids[i]) throw std::invalid_argument("duplicate replica broker");
     }
     if (leader_broker_id < 0) return;  // offline partition: LoadMonitor skips its replicas
+    int leaders = 0;
+    for (int i = 0; i < num_replicas; ++i) leaders += replica_broker_ids[i] == leader_broker_id ? 1 : 0;
+    if (leaders != 1)
+      throw std::invalid_argument("partition " + std::string(topic) + "-" + std::to_string(partition) + ": leader broker " +
+                                  std::to_string(leader_broker_id) + " is not one of its replica brokers");
     const int W = b->W;
     auto ti = b->topicIndex.find(topic);
     int32_t t;
@@ -218,6 +229,19 @@ ccmi_status ccmi_builder_set_broker_state(ccmi_model_builder* b, int32_t broker_
   });
 }
 
+ccmi_status ccmi_builder_set_disk_state(ccmi_model_builder* b, int32_t broker_id, const char* logdir, int32_t state) {
+  if (!b || !logdir || (state != CCMI_DISK_ALIVE && state != CCMI_DISK_DEMOTED)) return CCMI_E_INVALID;
+  return run([&] {
+    for (DiskIn& d : b->disks)
+      if (d.brokerId == broker_id && d.logdir == logdir) {
+        d.demoted = state == CCMI_DISK_DEMOTED ? 1 : 0;
+        return;
+      }
+    // DemoteBrokerRunnable.java:144-146
+    throw std::invalid_argument("Broker " + std::to_string(broker_id) + " does not have logdir " + logdir + ".");
+  });
+}
+
 ccmi_status ccmi_builder_desc(ccmi_model_builder* b, ccmi_cluster_desc* out) {
   if (!b || !out) return CCMI_E_INVALID;
   return run([&] {
@@ -239,6 +263,16 @@ ccmi_status ccmi_builder_desc(ccmi_model_builder* b, ccmi_cluster_desc* out) {
       b->oState[i] = x.state;
       for (int k = 0; k < 4; ++k) b->oCap[(size_t)i * 4 + k] = x.cap[k];
     }
+    // hosts: one per (rack, host name) (Rack._hosts), indexed in first-broker order
+    {
+      std::map<std::pair<int32_t, std::string>, int32_t> hostIndex;
+      b->oHost.resize(B);
+      for (int i = 0; i < B; ++i) {
+        const BrokerIn& x = b->brokers[b->brokerById.at(b->sortedIds[i])];
+        auto it = hostIndex.emplace(std::make_pair(x.rack, x.host), (int32_t)hostIndex.size()).first;
+        b->oHost[i] = it->second;
+      }
+    }
     b->oRBroker.resize(R);
     for (int r = 0; r < R; ++r) b->oRBroker[r] = indexOf.at(b->rBrokerId[r]);
     b->oPartReplicas.resize(R);
@@ -255,7 +289,9 @@ ccmi_status ccmi_builder_desc(ccmi_model_builder* b, ccmi_cluster_desc* out) {
     b->oDiskBroker.clear();
     b->oDiskCap.clear();
     b->oDiskLogdir.clear();
+    b->oDiskDemoted.clear();
     for (size_t i : dOrder) {
+      b->oDiskDemoted.push_back(b->disks[i].demoted);
       b->oDiskBroker.push_back(indexOf.at(b->disks[i].brokerId));
       b->oDiskCap.push_back(b->brokers[b->brokerById.at(b->disks[i].brokerId)].state == CCMI_BROKER_DEAD
                                 ? -1.0
@@ -300,7 +336,9 @@ ccmi_status ccmi_builder_desc(ccmi_model_builder* b, ccmi_cluster_desc* out) {
       out->disk_logdir = b->oDiskLogdir.data();
       out->disk_capacity = b->oDiskCap.data();
       out->replica_disk = b->oRDisk.data();
+      out->disk_demoted = b->oDiskDemoted.data();
     }
+    out->broker_host = b->oHost.data();
   });
 }
 

@@ -191,6 +191,20 @@ void Model::build(const ccmi_cluster_desc& d) {
       if (alive(b)) c += bCap[4 * b + k];
     clusterCap[k] = c;
   }
+  sharedHosts = false;
+  if (d.broker_host) {  // Rack._hosts: a host index names one host of one rack
+    std::vector<int32_t> hostRack;
+    for (int b = 0; b < B; ++b) {
+      const int h = d.broker_host[b];
+      if (h < 0 || h >= B) throw std::invalid_argument("broker_host out of range");
+      if ((int)hostRack.size() <= h) hostRack.resize(h + 1, -1);
+      if (hostRack[h] >= 0) {
+        if (hostRack[h] != bRack[b]) throw std::invalid_argument("brokers of one host in different racks");
+        sharedHosts = true;
+      }
+      hostRack[h] = bRack[b];
+    }
+  }
   bVer.assign(B, 0);
   sortedCache.assign(B, {});
   filteredCache.assign(B, {});
@@ -268,6 +282,13 @@ void Model::buildDisks(const ccmi_cluster_desc& d) {
     bDisks.insert(bDisks.end(), v.begin(), v.end());
   }
   bDiskOff[B] = (int)bDisks.size();
+  dDemoted.assign(D, 0);
+  anyDemotedDisk = false;
+  dReplicaSet.clear();
+  if (d.disk_demoted)
+    for (int k = 0; k < D; ++k)
+      if (d.disk_demoted[k]) dDemoted[k] = 1, anyDemotedDisk = true;
+  if (anyDemotedDisk) dReplicaSet.assign(D, ReplicaSet(&replicaOrder));
   for (int b = 0; b < B; ++b)
     if (!alive(b))
       for (int k = bDiskOff[b]; k < bDiskOff[b + 1]; ++k) {  // Broker.setState(DEAD): Disk.setState(DEAD)
@@ -284,6 +305,7 @@ void Model::buildDisks(const ccmi_cluster_desc& d) {
       rDisk[r] = rOrigDisk[r] = k;
       rDiskPos[r] = (int32_t)dMembers[k].size();
       dMembers[k].push_back(r);
+      if (anyDemotedDisk) dReplicaSet[k].add(r, replicaHash(r));
       dUtil[k] += ru(r, R_DISK);  // Disk.addReplica (load still empty: += 0.0) then Disk.addReplicaLoad
     }
   for (int i = 0; i < d.num_disk_assignments; ++i) {
@@ -322,6 +344,7 @@ void Model::diskAdd(int d, int r) {
   rDisk[r] = d;
   rDiskPos[r] = (int32_t)v.size();
   v.push_back(r);
+  if (anyDemotedDisk) dReplicaSet[d].add(r, replicaHash(r));
   diskDirty = true;
 }
 void Model::diskRemove(int d, int r) {
@@ -342,6 +365,7 @@ void Model::diskRemove(int d, int r) {
   if (rDisk[last] == d) rDiskPos[last] = pos;
   v.pop_back();
   if (rDisk[r] == d) rDiskPos[r] = -1;
+  if (anyDemotedDisk) dReplicaSet[d].remove(r, replicaHash(r));
   diskDirty = true;
 }
 void Model::relocateReplicaToDisk(int p, int b, int dst) {

@@ -135,6 +135,11 @@ class Model {
   std::vector<int32_t> bDiskOff, bDisks;    // CSR: each broker's disks in logdir order
   std::vector<int32_t> rDisk, rOrigDisk;    // Replica._disk / _originalDisk (-1 = null)
   std::vector<int32_t> rDiskPos;            // index of the replica in dMembers[rDisk[r]] (-1 = not a member)
+  // Disk.State.DEMOTED (ccmi.h disk_demoted) and, when a disk is demoted, every disk's Disk._replicas as the Java
+  // HashSet it is (PreferredLeaderElectionGoal iterates a demoted disk's replicas)
+  std::vector<uint8_t> dDemoted;
+  bool anyDemotedDisk = false;
+  std::vector<ReplicaSet> dReplicaSet;
   // Disk._replicas entries left behind by inter-broker moves (Broker.removeReplica keeps the replica on its disk)
   int64_t diskGhosts = 0;
   bool diskDirty = true;                    // device copy of dUtil is stale
@@ -155,6 +160,8 @@ class Model {
   std::vector<uint8_t> selfHealing;         // per replica: in _selfHealingEligibleReplicas
   int64_t numSelfHealing = 0;
   int numDead = 0, numNew = 0, numBadDisk = 0;
+  // hosts (ccmi.h broker_host): true when some host holds two or more brokers (host-level capacity not modelled)
+  bool sharedHosts = false;
   // Partition._ineligibleBrokers: a BAD_DISKS broker holding an offline replica of the partition may not receive
   // one of its replicas (ClusterModel.setBrokerState :325-331); CSR over partitions, static
   std::vector<int32_t> pIneligOff, pIneligB;

@@ -459,6 +459,9 @@ static uint32_t xcdSliceMinCols() {
   return v;
 }
 
+// The slicing rule, for the scan server's host side (device.cpp)
+uint32_t scanXcdSliceMinCols() { return xcdSliceMinCols(); }
+
 // Diagnostics: workgroup 0 / thread 0 records s_memrealtime (100 MHz) at fixed points of a launch.
 #define CCMI_STAMP(T, seq, i)                                                                         \
   do {                                                                                               \
@@ -586,6 +589,197 @@ __global__ __launch_bounds__(kBlock) void scan_cross(DevTables T, MutTables Mt, 
   CCMI_STAMP(T, seq, 4);
   publishLast(result, done, mail, seq);
   CCMI_STAMP(T, seq, 5);
+}
+
+// ------------------------------------------------------------------------------------------------ scan server
+// K8 scan_server: ONE persistent launch serves a stream of cross / pair scans. The host writes each command (rows,
+// program, request arrays, then the sequence word behind a store fence) into fine-grained VRAM that the CPU writes
+// through the BAR; every workgroup polls the sequence word, evaluates its tiles exactly as scan_cross / scan_pairs
+// do, and the last workgroup to arrive publishes {seq, key} to the host mailbox. No launch and no PCIe read of the
+// request per scan. Everything the host wrote is read with system-scope loads (never from a cache line of an earlier
+// command); workgroup 0 writes the command's dirty rows to HBM and releases them before it arrives, and every
+// workgroup takes an agent-scope acquire when it sees the next command (MI355X_MICROARCH.md, inter-workgroup
+// visibility). The launch exits on SOP_EXIT or after kServerIdleTicks without a command (watchdog; the host stops the
+// server before any other work on the session stream and at the end of every API call, so it never relies on it).
+__device__ __forceinline__ int32_t ldSys(const int32_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ void copySys(void* dst, const void* src, int bytes) {  // whole 32-bit words, all threads
+  for (int w = threadIdx.x; w < bytes / 4; w += blockDim.x)
+    reinterpret_cast<int32_t*>(dst)[w] = ldSys(reinterpret_cast<const int32_t*>(src) + w);
+}
+template <class X>
+__device__ __forceinline__ void copySysOneThread(X* dst, const X* src) {
+  static_assert(sizeof(X) % 4 == 0, "whole words");
+  for (int w = 0; w < (int)(sizeof(X) / 4); ++w)
+    reinterpret_cast<int32_t*>(dst)[w] = ldSys(reinterpret_cast<const int32_t*>(src) + w);
+}
+constexpr unsigned long long kServerIdleTicks = 200000000ull;  // 2 s of s_memrealtime (100 MHz)
+
+__global__ __launch_bounds__(kBlock) void scan_server(DevTables T, MutTables Mt, const ServerCmd* __restrict__ cmd,
+                                                      const char* __restrict__ pay,
+                                                      unsigned long long* __restrict__ result,
+                                                      unsigned int* __restrict__ done,
+                                                      unsigned long long* __restrict__ mail,
+                                                      unsigned long long* __restrict__ t0,
+                                                      unsigned long long startSeq) {
+  __shared__ OverlayLds ov;
+  __shared__ DevProgram prog;
+  __shared__ ServerCmd c;
+  __shared__ int sExit;
+  unsigned long long last = startSeq;
+  int progVer = -1;
+  unsigned long long idleSince = __builtin_amdgcn_s_memrealtime();
+  for (;;) {
+    if (threadIdx.x == 0) {
+      int ex = 0;
+      for (int spin = 0;; ++spin) {
+        const unsigned long long s =
+            __hip_atomic_load(&cmd->seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (s != last) break;
+        if ((spin & 63) == 63 && __builtin_amdgcn_s_memrealtime() - idleSince > kServerIdleTicks) {
+          ex = 1;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(4);
+      }
+      // the rows workgroup 0 wrote for the previous command (released before its arrival) become visible here
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      if (!ex) copySysOneThread(&c, cmd);
+      if (blockIdx.x == 0) *t0 = __builtin_amdgcn_s_memrealtime();  // busy-time stamp (released with the rows)
+      sExit = ex;
+    }
+    __syncthreads();
+    if (sExit || c.op == SOP_EXIT) break;
+    if (c.progVer != progVer) {
+      copySys(&prog, pay + c.oProg, (int)sizeof(DevProgram));
+      progVer = c.progVer;
+    }
+    UpdateList U;
+    U.brows = (const BrokerRow*)(pay + c.oB);
+    U.rrows = (const ReplicaRow*)(pay + c.oR);
+    U.prows = (const PartitionRow*)(pay + c.oP);
+    U.tdel = (const TopicCountDelta*)(pay + c.oT);
+    U.nb = c.nb;
+    U.nr = c.nr;
+    U.np = c.np;
+    U.nt = c.nt;
+    __syncthreads();
+    bool staged = false;
+    auto stage = [&]() {
+      if (threadIdx.x == 0) {
+        ov.nb = U.nb;
+        ov.nr = U.nr;
+        ov.np = U.np;
+      }
+      copySys(ov.b, U.brows, U.nb * (int)sizeof(BrokerRow));
+      copySys(ov.r, U.rrows, U.nr * (int)sizeof(ReplicaRow));
+      copySys(ov.p, U.prows, U.np * (int)sizeof(PartitionRow));
+      __syncthreads();
+      if (blockIdx.x == 0 && (U.nb | U.nr | U.np | U.nt)) {
+        applyRowsBlock(Mt, ov.b, ov.nb, ov.r, ov.nr, ov.p, ov.np, nullptr, 0, threadIdx.x, blockDim.x);
+        for (int i = threadIdx.x; i < U.nt; i += blockDim.x) {
+          TopicCountDelta d;
+          copySysOneThread(&d, &U.tdel[i]);
+          atomicAdd(&(d.kind ? Mt.topicLead : Mt.topicCount)[(size_t)d.topic * Mt.ldB + d.broker], d.delta);
+        }
+      }
+      staged = true;
+    };
+    if (blockIdx.x == 0) stage();
+    const int32_t* A = (const int32_t*)(pay + c.oA);
+    const int32_t* C = (const int32_t*)(pay + c.oC);
+    if (c.op == SOP_CROSS) {
+      const int K = c.K, Nr = c.Nr, N = c.N, c0 = c.c0;
+      uint32_t colStart = 0, Ws = (uint32_t)Nr, wg = blockIdx.x, wgs = gridDim.x;
+      if (c.sliced) {
+        const uint32_t W = ((uint32_t)Nr + kXcds - 1) / kXcds;
+        const uint32_t sl = blockIdx.x % kXcds;
+        colStart = sl * W;
+        Ws = colStart < (uint32_t)Nr ? min(W, (uint32_t)Nr - colStart) : 0u;
+        wg = blockIdx.x / kXcds;
+        wgs = gridDim.x / kXcds;
+      }
+      const uint32_t total = (uint32_t)K * Ws;
+      for (uint32_t base = wg * kBlock; base < total; base += wgs * kBlock) {
+        const uint32_t kb = base / Ws;
+        const unsigned long long keyBase = (unsigned long long)kb * N + c0 + colStart + (base - kb * Ws);
+        if (blockBest(result) <= keyBase) break;
+        const uint32_t q = base + threadIdx.x;
+        const uint32_t k = q / Ws;
+        const uint32_t j = colStart + (q - k * Ws);
+        int rq = 0, dq = 0;
+        if (q < total) {
+          rq = ldSys(A + k);
+          dq = ldSys(C + j);
+        }
+        if (!staged) stage();
+        unsigned long long local = kNone;
+        if (q < total) {
+          PreView v;
+          v.loadDst(T, dq, ov);
+          v.loadRow(T, prog, rq, ov);
+          const bool inList = (prog.filter != FILTER_RACK_AWARE || v.rackEligible()) && !v.exclLeadBlocked(prog);
+          if (inList && moveCandidateAccepted(prog, v, v.r, v.dst)) local = (unsigned long long)k * N + c0 + j;
+        }
+        const unsigned long long m = blockMin(local);
+        if (m != kNone) {
+          if (threadIdx.x == 0) atomicMin(result, m);
+          break;
+        }
+      }
+    } else {  // SOP_PAIRS
+      const int n = c.n, keyBase = c.keyBase;
+      for (int base = blockIdx.x * kBlock; base < n; base += gridDim.x * kBlock) {
+        if (blockBest(result) <= (unsigned long long)(keyBase + base)) break;
+        const int q = base + threadIdx.x;
+        int rq = 0, dq = 0;
+        if (q < n) {
+          rq = ldSys(A + q);
+          dq = ldSys(C + q);
+        }
+        if (!staged) stage();
+        unsigned long long local = kNone;
+        if (q < n) {
+          PreView v;
+          v.loadDst(T, dq, ov);
+          v.loadRow(T, prog, rq, ov);
+          if (!v.exclLeadBlocked(prog) && moveCandidateAccepted(prog, v, v.r, v.dst))
+            local = (unsigned long long)(keyBase + q);
+        }
+        const unsigned long long m = blockMin(local);
+        if (m != kNone) {
+          if (threadIdx.x == 0) atomicMin(result, m);
+          break;
+        }
+      }
+    }
+    // arrival: workgroup 0's row writes are released first; the last workgroup publishes and resets
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      const unsigned int prev = __hip_atomic_fetch_add(done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (prev == gridDim.x - 1) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        const unsigned long long v = __hip_atomic_load(&result[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const unsigned long long lo = v == kNone ? 0ull : (v + 1) & 0xffffffffull;
+        __hip_atomic_store(&result[0], kNone, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        // mail[1]: the command's busy time (100 MHz ticks from workgroup 0 seeing it to this publish), then the word
+        __hip_atomic_store(&mail[1], __builtin_amdgcn_s_memrealtime() - *t0, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the busy time lands before the sequence word
+        __hip_atomic_store(&mail[0], ((c.seq & 0xffffffffull) << 32) | lo, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
+      }
+    }
+    last = c.seq;
+    idleSince = __builtin_amdgcn_s_memrealtime();
+    __syncthreads();
+  }
 }
 
 // One wavefront per row (m, s). rowsPerBlock = kBlock / 64.
@@ -973,6 +1167,16 @@ hipError_t launchScanPairs(const DevTables& T, const MutTables& M, const UpdateL
   const unsigned blocks = gridFor((uint64_t)n, (uint64_t)kBlock, residentBlocks());
   hipLaunchKernelGGL(scan_pairs, dim3(blocks), dim3(kBlock), 0, st, T, M, U, prog, pr, pb, n, keyBase, result, done,
                      mail, seq);
+  return hipGetLastError();
+}
+
+// One workgroup per CU slot: `blocks` workgroups of kBlock threads, all resident (the launcher caps it at 2 per CU).
+hipError_t launchScanServer(const DevTables& T, const MutTables& M, const ServerCmd* cmd, const char* pay,
+                            unsigned long long* result, unsigned int* done, unsigned long long* mail,
+                            unsigned long long* t0, unsigned long long startSeq, int blocks, hipStream_t st) {
+  if (blocks < (int)kXcds || blocks % (int)kXcds != 0 || blocks > 512) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(scan_server, dim3(blocks), dim3(kBlock), 0, st, T, M, cmd, pay, result, done, mail, t0,
+                     startSeq);
   return hipGetLastError();
 }
 

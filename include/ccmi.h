@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define CCMI_ABI_VERSION 5
+#define CCMI_ABI_VERSION 6
 
 typedef enum ccmi_status {
   CCMI_OK = 0,
@@ -70,6 +70,9 @@ typedef enum ccmi_broker_state {
   CCMI_BROKER_DEMOTED = 3,
   CCMI_BROKER_BAD_DISKS = 4
 } ccmi_broker_state;
+
+/* model/Disk.java State (ALIVE, DEAD, DEMOTED) */
+typedef enum ccmi_disk_state { CCMI_DISK_ALIVE = 0, CCMI_DISK_DEAD = 1, CCMI_DISK_DEMOTED = 2 } ccmi_disk_state;
 
 /* analyzer/ActionType.java */
 typedef enum ccmi_action_type {
@@ -171,6 +174,17 @@ typedef struct ccmi_cluster_desc {
    * ClusterModel.setReplicaLoad: its Load stays empty (model/Load.java isEmpty), as in hand-built fixtures such as
    * DeterministicCluster.minLeaderReplicaPerBrokerSatisfiable (DeterministicCluster.java:321-361). */
   int32_t num_replica_loads;
+  /* ABI v6: the host of every broker ([B] host index, or NULL = each broker on a host of its own). Hosts belong to
+   * a rack and are keyed by name within it (Rack._hosts.computeIfAbsent, model/Rack.java:256-262; LoadMonitor passes
+   * node.host(), LoadMonitor.java:602), so brokers sharing an index must share a rack. Host-level capacity
+   * (Resource.isHostResource: CPU, NW_IN, NW_OUT; CapacityGoal.java:230-239,395-399,457-466 and
+   * ResourceDistributionGoal.java:890-923) equals the broker's when the host has one broker, which is what this
+   * build evaluates: a chain with a CPU / NW_IN / NW_OUT capacity or usage-distribution goal on a model where two
+   * brokers share a host fails with CCMI_E_UNSUPPORTED instead of diverging from the reference. */
+  const int32_t* broker_host;
+  /* ABI v6: [D] 1 = the disk is Disk.State.DEMOTED (DemoteBrokerRunnable.java:144-148), or NULL. Only
+   * PreferredLeaderElectionGoal reads it (PreferredLeaderElectionGoal.java:114-124). */
+  const uint8_t* disk_demoted;
 } ccmi_cluster_desc;
 
 /* analyzer/BalancingConstraint.java; defaults AnalyzerConfig.java:58-464 via ccmi_default_constraint */
@@ -365,6 +379,9 @@ ccmi_status ccmi_builder_populate_partition(ccmi_model_builder* b, const char* t
                                             int32_t leader_broker_id, const uint8_t* offline,
                                             const char* const* logdirs, const float* leader_metrics);
 ccmi_status ccmi_builder_set_broker_state(ccmi_model_builder* b, int32_t broker_id, int32_t state);
+/* Disk.setState for a disk added with ccmi_builder_add_disk: CCMI_DISK_ALIVE or CCMI_DISK_DEMOTED (a dead disk is
+ * given by a negative capacity). */
+ccmi_status ccmi_builder_set_disk_state(ccmi_model_builder* b, int32_t broker_id, const char* logdir, int32_t state);
 ccmi_status ccmi_builder_desc(ccmi_model_builder* b, ccmi_cluster_desc* out);
 ccmi_status ccmi_builder_broker_ids(const ccmi_model_builder* b, int32_t* out);
 

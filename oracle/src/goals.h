@@ -314,8 +314,8 @@ class MinTopicLeadersPerBrokerGoal : public AbstractGoal {
 std::vector<int> topicHashSetOrder(const ClusterModel& cm, const std::vector<int>& insertion);
 
 // PreferredLeaderElectionGoal (analyzer/goals/PreferredLeaderElectionGoal.java) with skipUrpDemotion = false,
-// excludeFollowerDemotion = false (the no-argument constructor GoalOptimizer uses). Demoted disks are not in the
-// flattened model, so only demoted brokers are considered.
+// excludeFollowerDemotion = false (the no-argument constructor GoalOptimizer uses): demoted brokers, then demoted disks
+// (ccmi.h disk_demoted) of the other alive brokers.
 class PreferredLeaderElectionGoal : public Goal {
  public:
   explicit PreferredLeaderElectionGoal(const BalancingConstraint&) {}

@@ -533,7 +533,17 @@ bool PreferredLeaderElectionGoal::optimize(ClusterModel& cm, const GoalList&, co
   std::set<int> partitionsToMove;
   for (int b : javaHashSetOrderIntKeys(cm.aliveBrokers())) {
     const Broker& br = cm.brokers[b];
-    if (br.state != BrokerState::DEMOTED) continue;
+    if (br.state != BrokerState::DEMOTED) {
+      for (int d : br.disks) {  // Broker.disks(): logdir order (:114-124)
+        if (!cm.disks[d].demoted) continue;
+        hasDemoted = true;
+        const std::vector<int> reps = cm.disks[d].replicaSet.order();  // Disk.replicas()
+        for (int r : reps) cm.moveReplicaToEnd(r);
+        for (int r : reps)  // Disk.leaderReplicas()
+          if (cm.replicas[r].isLeader) partitionsToMove.insert(cm.replicas[r].partition);
+      }
+      continue;
+    }
     hasDemoted = true;
     for (int r : br.replicaSet.order()) cm.moveReplicaToEnd(r);  // Broker.replicas(): HashSet order
     for (int r : br.leaderSet.order()) partitionsToMove.insert(cm.replicas[r].partition);

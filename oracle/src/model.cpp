@@ -593,6 +593,7 @@ int ClusterModel::createDisk(int b, const std::string& logdir, double capacity) 
   Disk dk;
   dk.broker = b;
   dk.logdir = logdir;
+  dk.replicaSet.setComparator([this](int x, int y) { return replicaCompareTo(x, y); });
   if (capacity < 0) {  // Disk(logDir, broker, diskCapacity): negative capacity = dead disk
     dk.capacity = -1.0;
     dk.alive = false;
@@ -623,6 +624,7 @@ void ClusterModel::diskAddReplica(int d, int r) {
                                                "-" + std::to_string(partitions[replicas[r].partition].number));
   dk.utilization += replicaUtil(r, DISK);
   dk.replicas.insert(r);
+  dk.replicaSet.add(r, replicaHash(r));
   replicas[r].disk = d;
   for (auto& kv : dk.sorted) {
     SortedReplicas& sr = *kv.second;
@@ -635,6 +637,7 @@ void ClusterModel::diskRemoveReplica(int d, int r) {
                                                "-" + std::to_string(partitions[replicas[r].partition].number));
   dk.utilization -= replicaUtil(r, DISK);
   dk.replicas.erase(r);
+  dk.replicaSet.remove(r, replicaHash(r));
   for (auto& kv : dk.sorted) {
     SortedReplicas& sr = *kv.second;
     if (sr.initialized) sr.set.erase(r);

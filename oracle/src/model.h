@@ -206,7 +206,9 @@ struct Disk {  // model/Disk.java
   double capacity = 0;  // -1 when dead (DEAD_DISK_CAPACITY)
   bool alive = true;
   double utilization = 0;
-  std::set<int> replicas;  // Disk._replicas (HashSet; iteration order never used)
+  std::set<int> replicas;  // Disk._replicas contents
+  JHashSet replicaSet;     // Disk._replicas as the HashSet PreferredLeaderElectionGoal iterates (demoted disks)
+  bool demoted = false;    // Disk.State.DEMOTED (ccmi.h disk_demoted)
   std::map<std::string, std::unique_ptr<SortedReplicas>> sorted;
 };
 

@@ -162,6 +162,7 @@ void* oc_from_desc(const ccmi_cluster_desc* d) {
     for (int k = 0; k < d->num_disks; ++k) {
       if (cm.createDisk(d->disk_broker[k], d->disk_logdir[k], d->disk_capacity[k]) != k)
         throw std::runtime_error("disk index mismatch");
+      cm.disks[k].demoted = d->disk_demoted && d->disk_demoted[k];
     }
     std::vector<char> created(d->num_partitions, 0);
     const int W = d->num_windows;

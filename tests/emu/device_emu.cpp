@@ -723,3 +723,7 @@ void Device::statsDisks(double balance, DiskStatsOut* out) {
 }
 
 }  // namespace ccmi
+
+namespace ccmi {
+void Device::stopServer() {}  // the emulation has no scan server: every scan is evaluated in place
+}  // namespace ccmi
