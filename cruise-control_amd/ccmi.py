@@ -171,7 +171,9 @@ class PerfStruct(C.Structure):
                 ("host_syncs", C.c_int64), ("scan_required", C.c_int64), ("chain_launches", C.c_int64),
                 ("intra_launches", C.c_int64), ("intra_kernel_ms", C.c_double), ("intra_bytes", C.c_int64),
                 ("cross_launches", C.c_int64), ("cross_required", C.c_int64), ("cross_kernel_ms", C.c_double),
-                ("combines", C.c_int64)]
+                ("combines", C.c_int64), ("server_launches", C.c_int64), ("server_scans", C.c_int64),
+                ("server_required", C.c_int64), ("server_busy_ms", C.c_double),
+                ("server_payload_bytes", C.c_int64)]
 
 
 # ----------------------------------------------------------------------------------------------- errors

@@ -300,6 +300,7 @@ ccmi_status ccmi_session_create(int32_t device_ordinal, const ccmi_cluster_desc*
     s->model.build(*desc);
     ccmi::Model& m = s->model;
     s->device = std::make_unique<ccmi::Device>(device_ordinal, m.B, m.R, m.P, m.T, ccmi::kMaxGoals);
+    s->device->setRowSource(m.rBroker.data(), m.rPart.data(), m.pTopic.data());
     s->deviceOrdinal = device_ordinal;
     // device layout: resource-major broker/replica columns
     std::vector<double> capRM((size_t)4 * m.B), utilRM((size_t)4 * m.B), rutilRM((size_t)4 * m.R), pot(m.B);
@@ -652,6 +653,11 @@ ccmi_status ccmi_perf(const ccmi_session* s, ccmi_perf_counters* out) {
     out->cross_required = p.crossRequired;
     out->cross_kernel_ms = p.crossKernelMs;
     out->combines = p.combines;
+    out->server_launches = p.serverLaunches;
+    out->server_scans = p.serverScans;
+    out->server_required = p.serverRequired;
+    out->server_busy_ms = p.serverBusyMs;
+    out->server_payload_bytes = p.serverPayloadBytes;
     return CCMI_OK;
   });
 }

@@ -23,7 +23,7 @@ namespace ccmi {
 #define EV1 ((hipEvent_t)ev1_)
 
 hipError_t launchScanCross(const DevTables& T, const MutTables& M, const UpdateList& U, const DevProgram& prog,
-                           const int32_t* reps, const int32_t* cands, int K, int Nr, int N, int c0,
+                           const RowRef* reps, const int32_t* cands, int K, int Nr, int N, int c0,
                            unsigned long long* result, unsigned int* done, unsigned long long* mail,
                            unsigned long long seq, hipStream_t st);
 hipError_t launchScanSwap(const DevTables& T, const DevProgram& prog, const int32_t* srcs, int S, const int32_t* cbOff,
@@ -31,14 +31,15 @@ hipError_t launchScanSwap(const DevTables& T, const DevProgram& prog, const int3
                           unsigned long long* mail, unsigned long long seq, hipStream_t st, hipEvent_t ev0,
                           hipEvent_t ev1);
 hipError_t launchScanPairs(const DevTables& T, const MutTables& M, const UpdateList& U, const DevProgram& prog,
-                           const int32_t* pr, const int32_t* pb, int n, int keyBase, unsigned long long* result,
+                           const RowRef* pr, const int32_t* pb, int n, int keyBase, unsigned long long* result,
                            unsigned int* done, unsigned long long* mail, unsigned long long seq, hipStream_t st);
 hipError_t launchPrep(const MutTables& M, const UpdateList& U, const int4* req, int4* dReq, int nReq4,
                       unsigned long long* result, unsigned int* done, hipStream_t st);
 uint32_t scanXcdSliceMinCols();
 hipError_t launchScanServer(const DevTables& T, const MutTables& M, const ServerCmd* cmd, const char* pay,
-                            unsigned long long* result, unsigned int* done, unsigned long long* mail,
-                            unsigned long long* t0, unsigned long long startSeq, int blocks, hipStream_t st);
+                            const RowRef* pool, unsigned long long* result, unsigned int* done,
+                            unsigned long long* mail, unsigned long long* t0, unsigned long long startSeq, int blocks,
+                            hipStream_t st);
 hipError_t launchChainPairs(const DevTables& T, const ChainTables& C, const DevProgram& prog, const int32_t* pr,
                             const int32_t* pb, const int32_t* next, int n, int maxAccepts, int32_t* log,
                             ChainResultDev* out, hipStream_t st);
@@ -139,6 +140,10 @@ Device::Device(int ordinal, int B, int R, int P, int T, int maxGoalSlots)
       dalloc(&dServerT0_, 1);
       try {
         ensureFg(1 << 20);
+        // snapshot pool: 4M rows (64 MB), host-written like the command block
+        segCap_ = (size_t)4 << 20;
+        hipCheck(hipExtMallocWithFlags((void**)&segPool_, segCap_ * sizeof(RowRef), hipDeviceMallocFinegrained),
+                 "hipExtMallocWithFlags snapshot pool");
       } catch (std::exception&) {
         serverUsable_ = false;  // no host-writable fine-grained VRAM: a launch per scan
       }
@@ -179,6 +184,7 @@ Device::~Device() {
   for (void* p : intraAllocs_)
     if (p) (void)hipFree(p);
   if (fg_) (void)hipFree(fg_);
+  if (segPool_) (void)hipFree(segPool_);
   if (dServerT0_) (void)hipFree(dServerT0_);
   if (hStage_) (void)hipHostFree(hStage_);
   if (hResult_) (void)hipHostFree(hResult_);
@@ -277,13 +283,14 @@ bool Device::serveScan(const DevProgram& prog, const Staged& g, bool readsTopicC
 }
 
 // params: CROSS {K, Nr, N, c0, sliced, -}; PAIRS {n, keyBase, -, -, -, -}
-int64_t Device::serverRun(const DevProgram& prog, const Staged& g, int op, const int32_t* A, size_t nA,
+int64_t Device::serverRun(const DevProgram& prog, const Staged& g, int op, const void* A, size_t nA,
                           const int32_t* C, size_t nC, const int32_t params[6]) {
   // payload: [program | rows | A | C]; the program slot is always reserved so offsets never depend on whether it is
   // resent (a restarted server has no program in LDS: it gets the program again whatever the host sent before)
   const size_t oProg = 0, oRows = align16(sizeof(DevProgram));
   const size_t rows = g.end;  // [broker | replica | partition rows | topic deltas] as packUpdates laid them out
-  const size_t oA = oRows + rows, oC = oA + align16(nA * 4), end = oC + align16(nC * 4);
+  const size_t aBytes = op == SOP_SEGS ? nA * sizeof(SegEntry) : nA * sizeof(RowRef);
+  const size_t oA = oRows + rows, oC = oA + align16(aBytes), end = oC + align16(nC * 4);
   ensureFg(kCmdBytes + end);
   const double now = nowSeconds();
   if (serverOn_ && now - lastServerUse_ > 0.25) stopServer();  // far from the device watchdog (2 s idle)
@@ -296,8 +303,8 @@ int64_t Device::serverRun(const DevProgram& prog, const Staged& g, int op, const
       if (ok) g_serverWgs[ordinal_ & 63] += serverBlocks_;
     }
     if (!ok) return INT64_MIN;  // the device has its budget of servers: the caller launches instead
-    hipCheck(launchScanServer(tables(), mutTables(), (const ServerCmd*)fg_, fg_ + kCmdBytes, dResult_, dDone_,
-                              hResultDev_, dServerT0_, lastCmdSeq_, serverBlocks_, ST),
+    hipCheck(launchScanServer(tables(), mutTables(), (const ServerCmd*)fg_, fg_ + kCmdBytes, segPool_, dResult_,
+                              dDone_, hResultDev_, dServerT0_, lastCmdSeq_, serverBlocks_, ST),
              "scan_server");
     serverOn_ = true;
     perf.serverLaunches++;
@@ -312,18 +319,21 @@ int64_t Device::serverRun(const DevProgram& prog, const Staged& g, int op, const
     progSent_ = true;
     ver = ++progVer_;
   }
+  perf.serverPayloadBytes += (int64_t)((sendProg ? sizeof(DevProgram) : 0) + rows + aBytes + nC * 4);
   if (rows) std::memcpy(pay + oRows, hStage_, rows);
-  if (nA) std::memcpy(pay + oA, A, nA * 4);
+  if (op == SOP_SEGS) std::memcpy(pay + oA, A, aBytes);
+  else if (nA) writeRowRefs(pay + oA, (const int32_t*)A, nA);
   if (nC) std::memcpy(pay + oC, C, nC * 4);
   ServerCmd c;
   std::memset(&c, 0, sizeof(c));
   c.op = op;
-  if (op == SOP_CROSS) {
+  if (op == SOP_CROSS || op == SOP_SEGS) {
     c.K = params[0];
     c.Nr = params[1];
     c.N = params[2];
     c.c0 = params[3];
     c.sliced = params[4];
+    c.nSegs = params[5];
   } else {
     c.n = params[0];
     c.keyBase = params[1];
@@ -353,6 +363,19 @@ int64_t Device::serverRun(const DevProgram& prog, const Staged& g, int op, const
   perf.serverBusyMs += (double)hResult_[1] * 1e-5;  // 100 MHz ticks
   const unsigned long long lo = hResult_[0] & 0xffffffffull;
   return lo == 0 ? -1 : (int64_t)(lo - 1);
+}
+
+void Device::writeRowRefs(char* dst, const int32_t* reps, size_t n) const {
+  if (!rowBroker_) throw std::runtime_error("scan rows need the model's row source (Device::setRowSource)");
+  RowRef buf[64];  // built in cache, then copied out in 1 KB pieces (dst may be write-combined device memory)
+  for (size_t i = 0; i < n; i += 64) {
+    const size_t m = std::min<size_t>(64, n - i);
+    for (size_t k = 0; k < m; ++k) {
+      const int r = reps[i + k], p = rowPart_[r];
+      buf[k] = RowRef{r, rowBroker_[r], p, partTopic_[p]};
+    }
+    std::memcpy(dst + i * sizeof(RowRef), buf, m * sizeof(RowRef));
+  }
 }
 
 DevTables Device::tables() const {
@@ -665,7 +688,7 @@ int64_t Device::scanCross(const DevProgram& prog, const int32_t* reps, int K, co
     return -1;
   }
   if ((uint64_t)K * (uint64_t)N >= (1ull << 31)) throw std::runtime_error("scan too large");
-  const size_t oCand = align16((size_t)K * 4);
+  const size_t oCand = (size_t)K * sizeof(RowRef);
   const size_t req = oCand + align16((size_t)Nr * 4);
   const bool readsTc = (prog.needs & (NEED_TOPIC | NEED_TLEAD)) != 0;
   {
@@ -691,13 +714,13 @@ int64_t Device::scanCross(const DevProgram& prog, const int32_t* reps, int K, co
   {
     PhaseScope ps(PH_SCAN_STAGE);
     const Staged g = packUpdates(req);
-    std::memcpy(hStage_ + g.end, reps, (size_t)K * 4);
+    writeRowRefs(hStage_ + g.end, reps, (size_t)K);
     std::memcpy(hStage_ + g.end + oCand, cands + c0, (size_t)Nr * 4);
     base = stageScan(g, req, readsTc, u);
   }
   ++seq_;
   if (timing) (void)hipEventRecord(EV0, ST);
-  hipCheck(launchScanCross(tables(), mutTables(), u, prog, (const int32_t*)base, (const int32_t*)(base + oCand), K, Nr,
+  hipCheck(launchScanCross(tables(), mutTables(), u, prog, (const RowRef*)base, (const int32_t*)(base + oCand), K, Nr,
                            N, c0, dResult_, dDone_, hResultDev_, seq_, ST),
            "scan_cross");
   if (timing) (void)hipEventRecord(EV1, ST);
@@ -757,7 +780,7 @@ int64_t Device::scanPairs(const DevProgram& prog, const int32_t* pr, const int32
     flushPending();
     return -1;
   }
-  const size_t oB = align16((size_t)n * 4);
+  const size_t oB = (size_t)n * sizeof(RowRef);
   const size_t req = oB + align16((size_t)n * 4);
   const bool readsTc = (prog.needs & (NEED_TOPIC | NEED_TLEAD)) != 0;
   {
@@ -778,13 +801,13 @@ int64_t Device::scanPairs(const DevProgram& prog, const int32_t* pr, const int32
   }
   stopServer();
   const Staged g = packUpdates(req);
-  std::memcpy(hStage_ + g.end, pr + p0, (size_t)n * 4);
+  writeRowRefs(hStage_ + g.end, pr + p0, (size_t)n);
   std::memcpy(hStage_ + g.end + oB, pb + p0, (size_t)n * 4);
   UpdateList u;
   const char* base = stageScan(g, req, readsTc, u);
   ++seq_;
   if (timing) (void)hipEventRecord(EV0, ST);
-  hipCheck(launchScanPairs(tables(), mutTables(), u, prog, (const int32_t*)base, (const int32_t*)(base + oB), n, p0,
+  hipCheck(launchScanPairs(tables(), mutTables(), u, prog, (const RowRef*)base, (const int32_t*)(base + oB), n, p0,
                            dResult_, dDone_, hResultDev_, seq_, ST),
            "scan_pairs");
   if (timing) (void)hipEventRecord(EV1, ST);
@@ -794,6 +817,78 @@ int64_t Device::scanPairs(const DevProgram& prog, const int32_t* pr, const int32
   const int64_t key = finishScan();
   perf.scanRequired += key < 0 ? (int64_t)n : key - p0 + 1;
   return key;
+}
+
+int64_t Device::segUpload(const SegIn& sg) {
+  const void* key = sg.v.get();
+  auto it = segCache_.find(key);
+  if (it != segCache_.end()) return it->second.second;
+  const size_t n = sg.v->size();
+  const size_t span = (n + 7) & ~(size_t)7;  // whole 128-byte lines: no line holds rows of two uploads
+  if (span > segCap_) return -1;
+  if (segHead_ + span > segCap_) {
+    // wrap: the server is restarted before any reused line is read (a launch starts with clean caches)
+    stopServer();
+    segCache_.clear();
+    segHead_ = 0;
+  }
+  if (n) {
+    for (int r : *sg.v)
+      if (rowBroker_[r] != sg.cb) throw std::logic_error("snapshot segment is not current for its broker");
+    writeRowRefs((char*)(segPool_ + segHead_), sg.v->data(), n);
+  }
+  const uint32_t off = (uint32_t)segHead_;
+  segHead_ += span;
+  segCache_.emplace(key, std::make_pair(sg.v, off));
+  return off;
+}
+
+int64_t Device::scanSegs(const DevProgram& prog, const std::vector<SegIn>& segs, const int32_t* cands, int N, int c0,
+                         int c1) {
+  DeviceGuard dg(ordinal_);
+  const int Nr = c1 - c0;
+  size_t K = 0;
+  for (const SegIn& sg : segs) K += sg.v->size() > sg.skip ? sg.v->size() - sg.skip : 0;
+  const bool readsTc = (prog.needs & (NEED_TOPIC | NEED_TLEAD)) != 0;
+  bool served = serverUsable_ && K > 0 && Nr > 0 && segs.size() <= (size_t)kMaxSegs &&
+                (uint64_t)K * (uint64_t)N < (1ull << 31);
+  if (served) {
+    segTab_.clear();
+    int32_t start = 0;
+    for (const SegIn& sg : segs) {
+      const int64_t off = segUpload(sg);
+      if (off < 0) {
+        served = false;
+        break;
+      }
+      const size_t len = sg.v->size() > sg.skip ? sg.v->size() - sg.skip : 0;
+      segTab_.push_back(SegEntry{(uint32_t)(off + (int64_t)std::min(sg.skip, sg.v->size())), start});
+      start += (int32_t)len;
+    }
+    segTab_.push_back(SegEntry{0, start});
+  }
+  if (served) {
+    const Staged g = packUpdates(0);
+    if (serveScan(prog, g, readsTc)) {
+      const int S = (int)segs.size();
+      const int32_t params[6] = {(int32_t)K, Nr, N, c0, Nr >= (int)scanXcdSliceMinCols() ? 1 : 0, S};
+      const int64_t key = serverRun(prog, g, SOP_SEGS, segTab_.data(), (size_t)S + 1, cands + c0, (size_t)Nr, params);
+      if (key != INT64_MIN) {
+        perf.scanPairs += (int64_t)K * Nr;
+        perf.scanBytes += (int64_t)K * Nr * kBytesPerCandidate;
+        const int64_t required = key < 0 ? (int64_t)K * Nr : (key / N) * Nr + (key % N - c0) + 1;
+        perf.scanRequired += required;
+        perf.serverRequired += required;
+        perf.crossRequired += required;
+        return key;
+      }
+    }
+    unpackUpdates(g);
+  }
+  segFlat_.clear();
+  for (const SegIn& sg : segs)
+    if (sg.v->size() > sg.skip) segFlat_.insert(segFlat_.end(), sg.v->begin() + sg.skip, sg.v->end());
+  return scanCross(prog, segFlat_.data(), (int)segFlat_.size(), cands, N, c0, c1);
 }
 
 void Device::stats(const StatsParams& P, const uint8_t* allowedAliveHost, StatsOut* out) {

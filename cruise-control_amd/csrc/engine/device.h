@@ -10,9 +10,12 @@
 #pragma once
 #include <cstdint>
 #include <string>
+#include <unordered_map>
+#include <memory>
 #include <vector>
 
 #include "devtypes.h"
+#include "snapseg.h"
 
 namespace ccmi {
 
@@ -47,6 +50,7 @@ struct DevicePerf {
   int64_t serverLaunches = 0;  // K8 scan_server launches (each serves many scans)
   int64_t serverScans = 0;     // scans served by a running scan_server (no launch each)
   double serverBusyMs = 0;     // their device busy time (s_memrealtime, command seen -> result published)
+  int64_t serverPayloadBytes = 0;  // command payload written through the BAR (program, rows, request arrays)
   int64_t serverRequired = 0;  // candidates those scans had to evaluate
 };
 
@@ -94,6 +98,13 @@ class Device {
                      const uint8_t* rFlags, const int32_t* pBrokers, const double* pLeadNwOut,
                      const int32_t* topicCountDense /* [T][ldB] */);
   void setAllowed(int slot, const uint8_t* allowedB);
+  // The host model's replica -> broker, replica -> partition and partition -> topic arrays (stable for the session):
+  // cross / pair scans send each row with its broker, partition and topic (RowRef).
+  void setRowSource(const int32_t* rBroker, const int32_t* rPart, const int32_t* pTopic) {
+    rowBroker_ = rBroker;
+    rowPart_ = rPart;
+    partTopic_ = pTopic;
+  }
   // OptimizationOptions.excludedBrokersFor{Leadership,ReplicaMove} as bits kExclLeadBit / kExclMoveBit of every
   // broker's allowedBits
   void setExclusions(const uint8_t* exclLead, const uint8_t* exclMove, const uint8_t* isNew);
@@ -119,6 +130,13 @@ class Device {
   int64_t scanSwap(const DevProgram& prog, const int32_t* srcs, int S, const int32_t* cbOff, int M,
                    const int32_t* cbRep, int nCand, int64_t* visited);
   int64_t scanPairs(const DevProgram& prog, const int32_t* pr, const int32_t* pb, int p0, int p1);
+  // A cross scan whose rows are snapshot segments: segment i contributes (*v)[skip, end) (replicas on broker cb, the
+  // snapshot current for cb). Each snapshot is uploaded once into a device-resident pool and the scan sends only
+  // the segment table; keys are those of scanCross over the concatenated rows. Falls back to scanCross.
+  using SegIn = SnapSeg;
+  int64_t scanSegs(const DevProgram& prog, const std::vector<SegIn>& segs, const int32_t* cands, int N, int c0,
+                   int c1);
+  bool segsUsable() const { return serverUsable_; }
   void stats(const StatsParams& P, const uint8_t* allowedAliveHost, StatsOut* out);
 
   // Chains (K7, kernels/scan.hip): decisions applied on the device inside one launch. uploadLoads gives the device
@@ -217,8 +235,18 @@ class Device {
   unsigned long long lastCmdSeq_ = 0;  // the sequence word the command block holds
   double lastServerUse_ = 0;  // steady-clock seconds of the last served scan (the host restarts an idle server)
   bool serveScan(const DevProgram& prog, const Staged& g, bool readsTopicCounts);
-  int64_t serverRun(const DevProgram& prog, const Staged& g, int op, const int32_t* A, size_t nA, const int32_t* C,
+  const int32_t *rowBroker_ = nullptr, *rowPart_ = nullptr, *partTopic_ = nullptr;
+  void writeRowRefs(char* dst, const int32_t* reps, size_t n) const;
+  // A: replica ids sent as RowRefs (nA entries), or for SOP_SEGS the segment table (nA entries of SegEntry)
+  int64_t serverRun(const DevProgram& prog, const Staged& g, int op, const void* A, size_t nA, const int32_t* C,
                     size_t nC, const int32_t params[6]);
+  // snapshot pool (fine-grained VRAM, ring of RowRefs; a wrap restarts the server so no cache holds a reused line)
+  RowRef* segPool_ = nullptr;
+  size_t segCap_ = 0, segHead_ = 0;
+  std::unordered_map<const void*, std::pair<std::shared_ptr<const std::vector<int32_t>>, uint32_t>> segCache_;
+  std::vector<int32_t> segFlat_;
+  std::vector<SegEntry> segTab_;
+  int64_t segUpload(const SegIn& s);  // pool index of the snapshot's first entry, or -1 (does not fit)
   void ensureFg(size_t bytes);
   int32_t* rowVisited_ = nullptr;
   size_t rowVisitedCap_ = 0;

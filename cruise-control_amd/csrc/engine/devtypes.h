@@ -175,6 +175,14 @@ struct MutTables {
   int32_t* topicLead;  // null unless kept
   int32_t ldB;
 };
+// A scan row as the host knows it: the replica with its current broker, partition and topic, so the device loads
+// the replica, partition, broker and topic-count records together (one dependent level after the request instead of
+// three). K7 chains move replicas on the device and keep reading the broker from the replica record.
+struct alignas(16) RowRef {
+  int32_t r, src, p, topic;
+};
+static_assert(sizeof(RowRef) == 16, "RowRef is one 16-byte load");
+
 struct UpdateList {
   const BrokerRow* brows;
   const ReplicaRow* rrows;
@@ -199,7 +207,14 @@ struct ScanHeader {
 
 // Scan-server command (kernels/scan.hip scan_server), at the start of the fine-grained VRAM block the host writes;
 // `seq` is written last, behind a store fence. Offsets are bytes from the payload base.
-enum ServerOp : int32_t { SOP_CROSS = 0, SOP_PAIRS = 1, SOP_EXIT = 2 };
+enum ServerOp : int32_t { SOP_CROSS = 0, SOP_PAIRS = 1, SOP_EXIT = 2, SOP_SEGS = 3 };
+// SOP_SEGS: a cross scan whose rows are the concatenation of nSegs segments of the device-resident snapshot pool
+// (Device::scanSegs); the segment table at oA holds {first pool entry, first row} per segment plus {0, K} at the end.
+constexpr int kMaxSegs = 1024;
+struct SegEntry {
+  uint32_t off;   // pool index of the segment's first row
+  int32_t start;  // its row index in the concatenation
+};
 struct alignas(16) ServerCmd {
   unsigned long long seq;
   int32_t op;
@@ -209,7 +224,8 @@ struct alignas(16) ServerCmd {
   int32_t progVer;       // the DevProgram at oProg changes only with its version
   int32_t nb, nr, np, nt;
   uint32_t oProg, oB, oR, oP, oT, oA, oC;
-  int32_t pad[3];
+  int32_t nSegs;  // SOP_SEGS: entries of the segment table
+  int32_t pad[2];
 };
 static_assert(sizeof(ServerCmd) % 16 == 0, "ServerCmd words");
 

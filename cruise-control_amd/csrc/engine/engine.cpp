@@ -209,6 +209,30 @@ int64_t Engine::crossScan(GoalImpl& self, int action, const std::vector<int32_t>
   return key;
 }
 
+int64_t Engine::crossScanSegs(GoalImpl& self, int action, const std::vector<SnapSeg>& segs,
+                              const std::vector<int32_t>& cands) {
+  DevProgram prog = program(self, action);
+  if (!dev->segsUsable() || shard.count > 1 || prog.exclLeadMove || prog.newOnly) {
+    std::vector<int32_t> flat;
+    {
+      PhaseScope pf(PH_FLATTEN);
+      for (const SnapSeg& sg : segs)
+        if (sg.v->size() > sg.skip) flat.insert(flat.end(), sg.v->begin() + sg.skip, sg.v->end());
+    }
+    return crossScan(self, action, flat, 0, cands);
+  }
+  int64_t K = 0;
+  for (const SnapSeg& sg : segs) K += sg.v->size() > sg.skip ? (int64_t)(sg.v->size() - sg.skip) : 0;
+  const int N = (int)cands.size();
+  if (K <= 0 || N == 0) return -1;
+  PhaseScope ps(PH_DEV_SCAN);
+  m.flushToDevice();
+  prog.filter = FILTER_NONE;
+  const int64_t key = combine(dev->scanSegs(prog, segs, cands.data(), N, 0, N));
+  candidates += key >= 0 ? key + 1 : K * N;
+  return key;
+}
+
 // CCMI_FORCE_COMBINE=1 sends single-shard keys through the combiner too (diagnostics: exercises the RCCL path of a
 // one-rank communicator on a one-GPU box)
 static bool forceCombine() {
@@ -1274,45 +1298,41 @@ class ResourceDistribution : public GoalImpl {
     // candidate list, nothing moves and nothing is counted — the loop's outcome without walking every broker
     if (cands.empty()) return true;
     if (action == DA_LEADERSHIP && pq.ordered() && e.shard.count <= 1) return moveInLeadership(e, b, pq, spec);
-    struct Seg {
-      int cb;
-      size_t skip;
-      const std::vector<int32_t>* v;  // valid until the next model change (snapTab holds it)
-      size_t len() const { return v->size() > skip ? v->size() - skip : 0; }
-    };
+    // rows: the current broker's remaining view, then the polled brokers' snapshots (device-resident segments)
+    using Seg = SnapSeg;
+    auto segLen = [](const Seg& x) { return x.v->size() > x.skip ? x.v->size() - x.skip : 0; };
     std::vector<Seg> segs;
-    std::vector<int32_t> flat;
     size_t target = kFirstBatchRows;
     bool haveCur = false;
-    Seg cur{0, 0, nullptr};
+    Seg cur{nullptr, 0, 0};
     auto cond = [&]() { return action == DA_MOVE || m.bNlead[b] != m.nrep(b); };
     while (haveCur || (!pq.empty() && cond())) {
+      size_t rows = 0;
       {
         PhaseScope pf(PH_FLATTEN);
         segs.clear();
-        flat.clear();
         if (haveCur) {
-          cur.v = &m.snapshotIn(snapTab, cur.cb, spec);
+          cur.v = m.snapshotInShared(snapTab, cur.cb, spec);
           segs.push_back(cur);
-          flat.insert(flat.end(), cur.v->begin() + std::min(cur.skip, cur.v->size()), cur.v->end());
+          rows += segLen(cur);
           haveCur = false;
         }
-        while (!pq.empty() && (segs.empty() || flat.size() < target) && cond()) {
+        while (!pq.empty() && (segs.empty() || rows < target) && segs.size() < (size_t)kMaxSegs && cond()) {
           const int cb = pq.poll();
-          segs.push_back({cb, 0, &m.snapshotIn(snapTab, cb, spec)});
-          flat.insert(flat.end(), segs.back().v->begin(), segs.back().v->end());
+          segs.push_back({m.snapshotInShared(snapTab, cb, spec), cb, 0});
+          rows += segLen(segs.back());
         }
       }
       if (segs.empty()) break;
-      const int64_t key = cands.empty() ? -1 : e.crossScan(*this, action, flat, 0, cands);
+      const int64_t key = cands.empty() ? -1 : e.crossScanSegs(*this, action, segs, cands);
       if (key < 0) {
         target = std::min<size_t>(target * kBatchGrowth, kMaxBatchRows);
         continue;
       }
       target = kFirstBatchRows;
       size_t q = (size_t)key, mi = 0;
-      while (q >= segs[mi].len()) {
-        q -= segs[mi].len();
+      while (q >= segLen(segs[mi])) {
+        q -= segLen(segs[mi]);
         ++mi;
       }
       const Seg hit = segs[mi];
@@ -1330,7 +1350,7 @@ class ResourceDistribution : public GoalImpl {
         pq.add(hit.cb);
       } else {
         prof().count(action == DA_MOVE ? 2 : 5, action == DA_MOVE ? "in.move.continue" : "in.lead.continue");
-        cur = {hit.cb, idx, nullptr};
+        cur = {nullptr, hit.cb, idx};
         haveCur = true;
       }
     }

@@ -17,6 +17,7 @@
 #include <string>
 #include <vector>
 
+#include "snapseg.h"
 #include "brokersets.h"
 #include "ccmi.h"
 #include "devtypes.h"
@@ -108,6 +109,9 @@ class Engine {
   int64_t crossScan(GoalImpl& self, int action, const std::vector<int32_t>& reps, size_t r0,
                     const std::vector<int32_t>& cands, int filter = FILTER_NONE, bool count = true,
                     size_t r1 = (size_t)-1);
+  // crossScan over the concatenation of snapshot segments (Device::scanSegs: the rows stay device-resident)
+  int64_t crossScanSegs(GoalImpl& self, int action, const std::vector<SnapSeg>& segs,
+                        const std::vector<int32_t>& cands);
   int64_t exclLeadCount(const DevProgram& prog, const int32_t* reps, int K, const std::vector<int32_t>& cands,
                         int64_t key) const;
   bool blocked(const DevProgram& prog, int r, int b) const;

@@ -327,7 +327,8 @@ class Model {
     std::vector<uint32_t> ver;  // bVer[b] + 1 of the stored snapshot, 0 = none
     std::vector<std::shared_ptr<const std::vector<int32_t>>> v;
   };
-  const std::vector<int32_t>& snapshotIn(SnapTable& t, int b, const Spec& s) {
+  const std::vector<int32_t>& snapshotIn(SnapTable& t, int b, const Spec& s) { return *snapshotInShared(t, b, s); }
+  const std::shared_ptr<const std::vector<int32_t>>& snapshotInShared(SnapTable& t, int b, const Spec& s) {
     if (!t.bound || t.owner != this || !(t.spec == s)) {
       t.spec = s;
       t.owner = this;
@@ -339,7 +340,7 @@ class Model {
       t.v[b] = snapshot(b, s);
       t.ver[b] = bVer[b] + 1u;
     }
-    return *t.v[b];
+    return t.v[b];
   }
   bool selects(const Spec& s, int r) const;
   uint64_t replicaKey(const Spec& s, int r) const;

@@ -328,6 +328,98 @@ struct PreView {
       dtl = t.topicLead[(size_t)topic * t.ldB + dst];
     }
   }
+  // A row whose broker, partition and topic the host sent (RowRef): every record load is independent.
+  __device__ __forceinline__ void loadRowRef(const DevTables& t, const DevProgram& prog, const RowRef x,
+                                             const OverlayLds& ov) {
+    r = x.r;
+    src = x.src;
+    p = x.p;
+    topic = x.topic;
+    const ReplicaRec& rec = t.replicas[r];
+    orig = rec.orig;
+    rflags = rec.flags;
+    rbs = rec.bset;
+    ru0 = rec.util[0];
+    ru1 = rec.util[1];
+    ru2 = rec.util[2];
+    ru3 = rec.util[3];
+    const int ri = ov.replica(r);
+    if (ri >= 0) {
+      const ReplicaRow& y = ov.r[ri];
+      rflags = y.flags;
+      ru0 = y.util[0];
+      ru1 = y.util[1];
+      ru2 = y.util[2];
+      ru3 = y.util[3];
+    }
+    setPartition(t.parts[p]);
+    const BrokerRec& sb = t.brokers[src];
+    bool aSrc = sb.alive != 0;
+    snrep = sb.nrep;
+    sbu0 = sb.util[0];
+    sbu1 = sb.util[1];
+    sbu2 = sb.util[2];
+    sbu3 = sb.util[3];
+    snlead = sb.nlead;
+    spot = sb.pot;
+    slbi = sb.lbi;
+    scap0 = sb.cap[0];
+    scap1 = sb.cap[1];
+    scap2 = sb.cap[2];
+    scap3 = sb.cap[3];
+    srcAllowed = sb.allowedBits;
+    sbs = sb.bset;
+    if (prog.needs & NEED_TOPIC) {
+      tup = t.tUpper[topic];
+      tlo = t.tLower[topic];
+      stc = t.topicCount[(size_t)topic * t.ldB + src];
+      dtc = t.topicCount[(size_t)topic * t.ldB + dst];
+    }
+    if (prog.needs & NEED_TLEAD) {
+      tmn = t.tMinLead ? t.tMinLead[topic] : -1;
+      stl = t.topicLead[(size_t)topic * t.ldB + src];
+      dtl = t.topicLead[(size_t)topic * t.ldB + dst];
+    }
+    inelig = false;
+    if (t.pIneligOff)  // uniform: only models with BAD_DISKS brokers carry the table
+      for (int k = t.pIneligOff[p]; k < t.pIneligOff[p + 1]; ++k) inelig |= t.pIneligB[k] == dst;
+    const int pi = ov.partition(p);
+    if (pi >= 0) {
+      const PartitionRow& y = ov.p[pi];
+      pn = y.n;
+      pb0 = y.brokers[0];
+      pb1 = y.brokers[1];
+      pb2 = y.brokers[2];
+      pb3 = y.brokers[3];
+      pb4 = y.brokers[4];
+      pb5 = y.brokers[5];
+      pb6 = y.brokers[6];
+      pb7 = y.brokers[7];
+      plno = y.leadNwOut;
+      prk0 = y.racks[0];
+      prk1 = y.racks[1];
+      prk2 = y.racks[2];
+      prk3 = y.racks[3];
+      prk4 = y.racks[4];
+      prk5 = y.racks[5];
+      prk6 = y.racks[6];
+      prk7 = y.racks[7];
+    }
+    const int si = ov.broker(src);
+    if (si >= 0) {
+      const BrokerRow& y = ov.b[si];
+      aSrc = y.alive != 0;
+      snrep = y.nrep;
+      sbu0 = y.util[0];
+      sbu1 = y.util[1];
+      sbu2 = y.util[2];
+      sbu3 = y.util[3];
+      snlead = y.nlead;
+      spot = y.potNwOut;
+      slbi = y.leadNwIn;
+    }
+    aliveBits = (aliveBits & 4u) | (aSrc ? 1u : 0u);
+  }
   // The destination side, loaded BEFORE the row (it depends only on the destination id); the destination's
   // topic count needs the row's topic and is read in loadRow.
   __device__ __forceinline__ void loadDst(const DevTables& t, int d, const OverlayLds& ov) {
@@ -528,7 +620,7 @@ __device__ __forceinline__ void publishLast(unsigned long long* __restrict__ res
 // Rows reps[0, K) x candidate columns [c0, c0 + Nr) of an N-column candidate list; key = k * N + c0 + jj. A sharded
 // session scans only its own column range; keys stay global, so a MIN over shards is the global first fit.
 __global__ __launch_bounds__(kBlock) void scan_cross(DevTables T, MutTables Mt, UpdateList U, DevProgram prog,
-                                                     const int32_t* __restrict__ reps,
+                                                     const RowRef* __restrict__ reps,
                                                      const int32_t* __restrict__ cands, int K, int Nr, int N, int c0,
                                                      int sliced, unsigned long long* __restrict__ result,
                                                      unsigned int* __restrict__ done,
@@ -559,7 +651,8 @@ __global__ __launch_bounds__(kBlock) void scan_cross(DevTables T, MutTables Mt, 
     const uint32_t q = base + threadIdx.x;
     const uint32_t k = q / Ws;
     const uint32_t j = colStart + (q - k * Ws);
-    int rq = 0, dq = 0;
+    RowRef rq{0, 0, 0, 0};
+    int dq = 0;
     if (q < total) {
       rq = reps[k];
       dq = cands[j];
@@ -574,7 +667,7 @@ __global__ __launch_bounds__(kBlock) void scan_cross(DevTables T, MutTables Mt, 
     if (q < total) {
       PreView v;
       v.loadDst(T, dq, ov);
-      v.loadRow(T, prog, rq, ov);
+      v.loadRowRef(T, prog, rq, ov);
       const bool inList = (prog.filter != FILTER_RACK_AWARE || v.rackEligible()) && !v.exclLeadBlocked(prog);
       if (inList && moveCandidateAccepted(prog, v, v.r, v.dst)) local = (unsigned long long)k * N + c0 + j;
     }
@@ -604,20 +697,52 @@ __global__ __launch_bounds__(kBlock) void scan_cross(DevTables T, MutTables Mt, 
 __device__ __forceinline__ int32_t ldSys(const int32_t* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
+// Up to three [src, src + words) -> dst copies in one pass: every thread issues its system-scope loads (at most
+// kCopyBatch per thread per pass) before it stores any, so a command's tables cost one memory round trip, not one
+// per word a thread copies.
+constexpr int kCopyBatch = 12;
+__device__ __forceinline__ void copySys3(int32_t* d0, const int32_t* s0, int n0, int32_t* d1, const int32_t* s1,
+                                         int n1, int32_t* d2, const int32_t* s2, int n2) {
+  const int total = n0 + n1 + n2;
+  for (int base = 0; base < total; base += kBlock * kCopyBatch) {
+    int32_t v[kCopyBatch];
+#pragma unroll
+    for (int u = 0; u < kCopyBatch; ++u) {
+      const int w = base + u * kBlock + (int)threadIdx.x;
+      if (w < n0) v[u] = ldSys(s0 + w);
+      else if (w < n0 + n1) v[u] = ldSys(s1 + (w - n0));
+      else if (w < total) v[u] = ldSys(s2 + (w - n0 - n1));
+    }
+#pragma unroll
+    for (int u = 0; u < kCopyBatch; ++u) {
+      const int w = base + u * kBlock + (int)threadIdx.x;
+      if (w < n0) d0[w] = v[u];
+      else if (w < n0 + n1) d1[w - n0] = v[u];
+      else if (w < total) d2[w - n0 - n1] = v[u];
+    }
+  }
+}
 __device__ __forceinline__ void copySys(void* dst, const void* src, int bytes) {  // whole 32-bit words, all threads
-  for (int w = threadIdx.x; w < bytes / 4; w += blockDim.x)
-    reinterpret_cast<int32_t*>(dst)[w] = ldSys(reinterpret_cast<const int32_t*>(src) + w);
+  copySys3(reinterpret_cast<int32_t*>(dst), reinterpret_cast<const int32_t*>(src), bytes / 4, nullptr, nullptr, 0,
+           nullptr, nullptr, 0);
+}
+__device__ __forceinline__ RowRef ldSysRow(const int32_t* p) {  // four independent system-scope loads
+  return RowRef{ldSys(p), ldSys(p + 1), ldSys(p + 2), ldSys(p + 3)};
 }
 template <class X>
-__device__ __forceinline__ void copySysOneThread(X* dst, const X* src) {
+__device__ __forceinline__ void copySysOneThread(X* dst, const X* src) {  // all loads issued, then the stores
   static_assert(sizeof(X) % 4 == 0, "whole words");
-  for (int w = 0; w < (int)(sizeof(X) / 4); ++w)
-    reinterpret_cast<int32_t*>(dst)[w] = ldSys(reinterpret_cast<const int32_t*>(src) + w);
+  constexpr int n = (int)(sizeof(X) / 4);
+  int32_t v[n];
+#pragma unroll
+  for (int w = 0; w < n; ++w) v[w] = ldSys(reinterpret_cast<const int32_t*>(src) + w);
+#pragma unroll
+  for (int w = 0; w < n; ++w) reinterpret_cast<int32_t*>(dst)[w] = v[w];
 }
 constexpr unsigned long long kServerIdleTicks = 200000000ull;  // 2 s of s_memrealtime (100 MHz)
 
 __global__ __launch_bounds__(kBlock) void scan_server(DevTables T, MutTables Mt, const ServerCmd* __restrict__ cmd,
-                                                      const char* __restrict__ pay,
+                                                      const char* __restrict__ pay, const RowRef* __restrict__ pool,
                                                       unsigned long long* __restrict__ result,
                                                       unsigned int* __restrict__ done,
                                                       unsigned long long* __restrict__ mail,
@@ -627,8 +752,10 @@ __global__ __launch_bounds__(kBlock) void scan_server(DevTables T, MutTables Mt,
   __shared__ DevProgram prog;
   __shared__ ServerCmd c;
   __shared__ int sExit;
+  __shared__ SegEntry sSeg[kMaxSegs + 1];
   unsigned long long last = startSeq;
   int progVer = -1;
+  bool prevRows = false;  // the previous command had rows for workgroup 0 to write into the tables
   unsigned long long idleSince = __builtin_amdgcn_s_memrealtime();
   for (;;) {
     if (threadIdx.x == 0) {
@@ -643,10 +770,12 @@ __global__ __launch_bounds__(kBlock) void scan_server(DevTables T, MutTables Mt,
         }
         __builtin_amdgcn_s_sleep(4);
       }
-      // the rows workgroup 0 wrote for the previous command (released before its arrival) become visible here
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      // the rows workgroup 0 wrote for the previous command (released before its arrival) become visible here; a
+      // command after one without rows has nothing new to see in the tables
+      if (prevRows) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
       if (!ex) copySysOneThread(&c, cmd);
-      if (blockIdx.x == 0) *t0 = __builtin_amdgcn_s_memrealtime();  // busy-time stamp (released with the rows)
+      if (blockIdx.x == 0)  // busy-time stamp, read by the last workgroup to arrive
+        __hip_atomic_store(t0, __builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       sExit = ex;
     }
     __syncthreads();
@@ -672,9 +801,11 @@ __global__ __launch_bounds__(kBlock) void scan_server(DevTables T, MutTables Mt,
         ov.nr = U.nr;
         ov.np = U.np;
       }
-      copySys(ov.b, U.brows, U.nb * (int)sizeof(BrokerRow));
-      copySys(ov.r, U.rrows, U.nr * (int)sizeof(ReplicaRow));
-      copySys(ov.p, U.prows, U.np * (int)sizeof(PartitionRow));
+      copySys3(reinterpret_cast<int32_t*>(ov.b), reinterpret_cast<const int32_t*>(U.brows),
+               U.nb * (int)(sizeof(BrokerRow) / 4), reinterpret_cast<int32_t*>(ov.r),
+               reinterpret_cast<const int32_t*>(U.rrows), U.nr * (int)(sizeof(ReplicaRow) / 4),
+               reinterpret_cast<int32_t*>(ov.p), reinterpret_cast<const int32_t*>(U.prows),
+               U.np * (int)(sizeof(PartitionRow) / 4));
       __syncthreads();
       if (blockIdx.x == 0 && (U.nb | U.nr | U.np | U.nt)) {
         applyRowsBlock(Mt, ov.b, ov.nb, ov.r, ov.nr, ov.p, ov.np, nullptr, 0, threadIdx.x, blockDim.x);
@@ -689,7 +820,10 @@ __global__ __launch_bounds__(kBlock) void scan_server(DevTables T, MutTables Mt,
     if (blockIdx.x == 0) stage();
     const int32_t* A = (const int32_t*)(pay + c.oA);
     const int32_t* C = (const int32_t*)(pay + c.oC);
-    if (c.op == SOP_CROSS) {
+    if (c.op == SOP_CROSS || c.op == SOP_SEGS) {
+      const bool segs = c.op == SOP_SEGS;
+      bool segsLoaded = false;
+      const int nSegs = c.nSegs;
       const int K = c.K, Nr = c.Nr, N = c.N, c0 = c.c0;
       uint32_t colStart = 0, Ws = (uint32_t)Nr, wg = blockIdx.x, wgs = gridDim.x;
       if (c.sliced) {
@@ -708,9 +842,26 @@ __global__ __launch_bounds__(kBlock) void scan_server(DevTables T, MutTables Mt,
         const uint32_t q = base + threadIdx.x;
         const uint32_t k = q / Ws;
         const uint32_t j = colStart + (q - k * Ws);
-        int rq = 0, dq = 0;
-        if (q < total) {
-          rq = ldSys(A + k);
+        RowRef rq{0, 0, 0, 0};
+        int dq = 0;
+        if (segs) {
+          if (!segsLoaded) {  // the segment table (written for this command: system-scope loads) into LDS
+            copySys(sSeg, A, (nSegs + 1) * (int)sizeof(SegEntry));
+            __syncthreads();
+            segsLoaded = true;
+          }
+          if (q < total) {
+            int lo = 0, hi = nSegs - 1;  // the last segment starting at or before row k
+            while (lo < hi) {
+              const int mid = (lo + hi + 1) >> 1;
+              if (sSeg[mid].start <= (int)k) lo = mid;
+              else hi = mid - 1;
+            }
+            rq = pool[sSeg[lo].off + (k - (uint32_t)sSeg[lo].start)];  // written before any command read it
+            dq = ldSys(C + j);
+          }
+        } else if (q < total) {
+          rq = ldSysRow(A + 4 * (size_t)k);
           dq = ldSys(C + j);
         }
         if (!staged) stage();
@@ -718,7 +869,7 @@ __global__ __launch_bounds__(kBlock) void scan_server(DevTables T, MutTables Mt,
         if (q < total) {
           PreView v;
           v.loadDst(T, dq, ov);
-          v.loadRow(T, prog, rq, ov);
+          v.loadRowRef(T, prog, rq, ov);
           const bool inList = (prog.filter != FILTER_RACK_AWARE || v.rackEligible()) && !v.exclLeadBlocked(prog);
           if (inList && moveCandidateAccepted(prog, v, v.r, v.dst)) local = (unsigned long long)k * N + c0 + j;
         }
@@ -733,9 +884,10 @@ __global__ __launch_bounds__(kBlock) void scan_server(DevTables T, MutTables Mt,
       for (int base = blockIdx.x * kBlock; base < n; base += gridDim.x * kBlock) {
         if (blockBest(result) <= (unsigned long long)(keyBase + base)) break;
         const int q = base + threadIdx.x;
-        int rq = 0, dq = 0;
+        RowRef rq{0, 0, 0, 0};
+        int dq = 0;
         if (q < n) {
-          rq = ldSys(A + q);
+          rq = ldSysRow(A + 4 * (size_t)q);
           dq = ldSys(C + q);
         }
         if (!staged) stage();
@@ -743,7 +895,7 @@ __global__ __launch_bounds__(kBlock) void scan_server(DevTables T, MutTables Mt,
         if (q < n) {
           PreView v;
           v.loadDst(T, dq, ov);
-          v.loadRow(T, prog, rq, ov);
+          v.loadRowRef(T, prog, rq, ov);
           if (!v.exclLeadBlocked(prog) && moveCandidateAccepted(prog, v, v.r, v.dst))
             local = (unsigned long long)(keyBase + q);
         }
@@ -754,29 +906,33 @@ __global__ __launch_bounds__(kBlock) void scan_server(DevTables T, MutTables Mt,
         }
       }
     }
-    // arrival: workgroup 0's row writes are released first; the last workgroup publishes and resets
+    // arrival: workgroup 0's row writes are released first (the only plain stores of a command); every other
+    // workgroup only made device-scope atomics, which need no cache write-back: waiting for them to complete orders
+    // them before the arrival. The last workgroup publishes and resets with device-scope atomics as well.
+    const bool rows = (c.nb | c.nr | c.np | c.nt) != 0;
     __syncthreads();
     if (threadIdx.x == 0) {
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      if (blockIdx.x == 0 && rows) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       const unsigned int prev = __hip_atomic_fetch_add(done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (prev == gridDim.x - 1) {
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
         const unsigned long long v = __hip_atomic_load(&result[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         const unsigned long long lo = v == kNone ? 0ull : (v + 1) & 0xffffffffull;
         __hip_atomic_store(&result[0], kNone, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         // mail[1]: the command's busy time (100 MHz ticks from workgroup 0 seeing it to this publish), then the word
-        __hip_atomic_store(&mail[1], __builtin_amdgcn_s_memrealtime() - *t0, __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(&mail[1],
+                           __builtin_amdgcn_s_memrealtime() -
+                               __hip_atomic_load(t0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the busy time lands before the sequence word
         __hip_atomic_store(&mail[0], ((c.seq & 0xffffffffull) << 32) | lo, __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_SYSTEM);
       }
     }
     last = c.seq;
+    prevRows = rows;
     idleSince = __builtin_amdgcn_s_memrealtime();
     __syncthreads();
   }
@@ -856,7 +1012,7 @@ __global__ __launch_bounds__(1024) void swap_visited_sum(const int32_t* __restri
 
 // PAIRS: explicit (replica, broker) list in iteration order (leadership moves: per-replica follower lists).
 __global__ __launch_bounds__(kBlock) void scan_pairs(DevTables T, MutTables Mt, UpdateList U, DevProgram prog,
-                                                     const int32_t* __restrict__ pr,
+                                                     const RowRef* __restrict__ pr,
                                                      const int32_t* __restrict__ pb, int n, int keyBase,
                                                      unsigned long long* __restrict__ result,
                                                      unsigned int* __restrict__ done,
@@ -867,7 +1023,8 @@ __global__ __launch_bounds__(kBlock) void scan_pairs(DevTables T, MutTables Mt, 
   for (int base = blockIdx.x * kBlock; base < n; base += gridDim.x * kBlock) {
     if (blockBest(result) <= (unsigned long long)(keyBase + base)) break;
     const int q = base + threadIdx.x;
-    int rq = 0, dq = 0;
+    RowRef rq{0, 0, 0, 0};
+    int dq = 0;
     if (q < n) {  // request reads overlap the overlay staging (see scan_cross)
       rq = pr[q];
       dq = pb[q];
@@ -882,7 +1039,7 @@ __global__ __launch_bounds__(kBlock) void scan_pairs(DevTables T, MutTables Mt, 
     if (q < n) {
       PreView v;
       v.loadDst(T, dq, ov);
-      v.loadRow(T, prog, rq, ov);
+      v.loadRowRef(T, prog, rq, ov);
       if (!v.exclLeadBlocked(prog) && moveCandidateAccepted(prog, v, v.r, v.dst))
         local = (unsigned long long)(keyBase + q);
     }
@@ -1135,7 +1292,7 @@ static unsigned gridFor(uint64_t work, uint64_t perBlock, uint64_t cap = 4096) {
 }
 
 hipError_t launchScanCross(const DevTables& T, const MutTables& M, const UpdateList& U, const DevProgram& prog,
-                           const int32_t* reps, const int32_t* cands, int K, int Nr, int N, int c0,
+                           const RowRef* reps, const int32_t* cands, int K, int Nr, int N, int c0,
                            unsigned long long* result, unsigned int* done, unsigned long long* mail,
                            unsigned long long seq, hipStream_t st) {
   unsigned blocks = gridFor((uint64_t)K * (uint64_t)Nr, (uint64_t)kBlock, residentBlocks());
@@ -1162,7 +1319,7 @@ hipError_t launchScanSwap(const DevTables& T, const DevProgram& prog, const int3
 }
 
 hipError_t launchScanPairs(const DevTables& T, const MutTables& M, const UpdateList& U, const DevProgram& prog,
-                           const int32_t* pr, const int32_t* pb, int n, int keyBase, unsigned long long* result,
+                           const RowRef* pr, const int32_t* pb, int n, int keyBase, unsigned long long* result,
                            unsigned int* done, unsigned long long* mail, unsigned long long seq, hipStream_t st) {
   const unsigned blocks = gridFor((uint64_t)n, (uint64_t)kBlock, residentBlocks());
   hipLaunchKernelGGL(scan_pairs, dim3(blocks), dim3(kBlock), 0, st, T, M, U, prog, pr, pb, n, keyBase, result, done,
@@ -1172,10 +1329,11 @@ hipError_t launchScanPairs(const DevTables& T, const MutTables& M, const UpdateL
 
 // One workgroup per CU slot: `blocks` workgroups of kBlock threads, all resident (the launcher caps it at 2 per CU).
 hipError_t launchScanServer(const DevTables& T, const MutTables& M, const ServerCmd* cmd, const char* pay,
-                            unsigned long long* result, unsigned int* done, unsigned long long* mail,
-                            unsigned long long* t0, unsigned long long startSeq, int blocks, hipStream_t st) {
+                            const RowRef* pool, unsigned long long* result, unsigned int* done,
+                            unsigned long long* mail, unsigned long long* t0, unsigned long long startSeq, int blocks,
+                            hipStream_t st) {
   if (blocks < (int)kXcds || blocks % (int)kXcds != 0 || blocks > 512) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(scan_server, dim3(blocks), dim3(kBlock), 0, st, T, M, cmd, pay, result, done, mail, t0,
+  hipLaunchKernelGGL(scan_server, dim3(blocks), dim3(kBlock), 0, st, T, M, cmd, pay, pool, result, done, mail, t0,
                      startSeq);
   return hipGetLastError();
 }

@@ -470,6 +470,14 @@ typedef struct ccmi_perf_counters {
   int64_t cross_required;      /* tools/pmc_summary.py prices against its own FETCH_SIZE / WRITE_SIZE counters) */
   double cross_kernel_ms;
   int64_t combines;            /* shard-combiner calls (RCCL / host MIN-allreduce of a scan's first-fit key) */
+  /* ABI v6: the persistent scan server (K8): its launches (each also counts in scan_launches), the cross / pair scans
+   * it served (no launch each), their candidates up to the winner, and its busy time (first workgroup seeing a
+   * command to the result published, summed over commands) */
+  int64_t server_launches;
+  int64_t server_scans;
+  int64_t server_required;
+  double server_busy_ms;
+  int64_t server_payload_bytes; /* command payload the host wrote into device memory for the server */
 } ccmi_perf_counters;
 ccmi_status ccmi_perf(const ccmi_session* s, ccmi_perf_counters* out);
 void ccmi_perf_reset(ccmi_session* s);

@@ -726,4 +726,13 @@ void Device::statsDisks(double balance, DiskStatsOut* out) {
 
 namespace ccmi {
 void Device::stopServer() {}  // the emulation has no scan server: every scan is evaluated in place
+
+// no snapshot pool either (segsUsable() is false, so the engine flattens first; kept for the link)
+int64_t Device::scanSegs(const DevProgram& prog, const std::vector<SegIn>& segs, const int32_t* cands, int N, int c0,
+                         int c1) {
+  segFlat_.clear();
+  for (const SegIn& sg : segs)
+    if (sg.v->size() > sg.skip) segFlat_.insert(segFlat_.end(), sg.v->begin() + sg.skip, sg.v->end());
+  return scanCross(prog, segFlat_.data(), (int)segFlat_.size(), cands, N, c0, c1);
+}
 }  // namespace ccmi

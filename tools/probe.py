@@ -30,3 +30,7 @@ for g in res.goal_results:
     print(f"  {g.name:40s} ok={g.succeeded} {g.seconds:8.3f}s cand={g.candidates:>12d} act={g.actions:>7d} "
           f"launches={g.device_launches}", flush=True)
 print(f"total {t3 - t2:.2f}s, {res.candidates} candidates, {len(cm.actions())} actions, {len(res.proposals)} proposals")
+p = cm.perf()
+print(f"perf: scan launches {p.scan_launches} (server {p.server_launches}, chains {p.chain_launches}, cross "
+      f"{p.cross_launches}), server scans {p.server_scans} busy {p.server_busy_ms:.1f} ms, host syncs {p.host_syncs}, "
+      f"required {p.scan_required} (server {p.server_required}), server payload {p.server_payload_bytes / 1e6:.1f} MB")
