@@ -362,6 +362,9 @@ ccmi_status ccmi_session_set_shard(ccmi_session* s, int32_t rank, int32_t count,
     if (count < 1 || rank < 0 || rank >= count) throw std::invalid_argument("shard rank out of range");
     if (count > 1 && !fn) throw std::invalid_argument("a sharded session needs a combiner");
     s->engine->shard = ccmi::Shard{rank, count, fn, ctx};
+    // a combiner makes every scan wait for other ranks (or a collective kernel): a resident server could hold the
+    // hardware queue those need, so a combined session launches per scan
+    s->device->setServerAllowed(fn == nullptr);
     return CCMI_OK;
   });
 }
@@ -382,6 +385,7 @@ ccmi_status ccmi_session_attach_rccl(ccmi_session* s, int32_t rank, int32_t coun
     s->rccl = nullptr;
     s->rccl = ccmi::rcclCreate(s->deviceOrdinal, rank, count, unique_id);
     s->engine->shard = ccmi::Shard{rank, count, &ccmi::rcclMin, s->rccl};
+    s->device->setServerAllowed(false);  // the collective kernels must not queue behind a resident server
     return CCMI_OK;
   });
 }

@@ -123,8 +123,8 @@ Device::Device(int ordinal, int B, int R, int P, int T, int maxGoalSlots)
   ensureStage(1 << 20);
   ensureReq(1 << 20);
   if (std::getenv("CCMI_STAMPS")) {
-    dalloc(&stamps_, 1024 * 8);
-    hipCheck(hipMemset(stamps_, 0, 1024 * 8 * sizeof(unsigned long long)), "hipMemset");
+    dalloc(&stamps_, 1024 * 8 + 16);  // + the scan server's phase sums at [8192, 8208)
+    hipCheck(hipMemset(stamps_, 0, (1024 * 8 + 16) * sizeof(unsigned long long)), "hipMemset");
   }
   hipCheck(hipEventCreate((hipEvent_t*)&ev0_), "hipEventCreate");
   hipCheck(hipEventCreate((hipEvent_t*)&ev1_), "hipEventCreate");
@@ -159,8 +159,13 @@ Device::~Device() {
   }
   if (ST) (void)hipStreamSynchronize(ST);
   if (stamps_) {  // average in-launch phase times of the last 1024 cross/pair scans (workgroup 0)
-    std::vector<unsigned long long> h(1024 * 8);
+    std::vector<unsigned long long> h(1024 * 8 + 16);
     if (hipMemcpy(h.data(), stamps_, h.size() * 8, hipMemcpyDeviceToHost) == hipSuccess) {
+      if (h[8192])
+        std::fprintf(stderr, "[ccmi server stamps] %llu commands: copy+acquire %.2f us, stage %.2f us, first tile "
+                             "%.2f us, rest to arrival %.2f us (workgroup 0)\n",
+                     h[8192], h[8193] * 0.01 / h[8192], h[8194] * 0.01 / h[8192], h[8195] * 0.01 / h[8192],
+                     h[8196] * 0.01 / h[8192]);
       double acc[5] = {0, 0, 0, 0, 0};
       int n = 0;
       for (int i = 0; i < 1024; ++i) {
@@ -224,9 +229,9 @@ namespace {
 constexpr size_t kCmdBytes = 256;  // the ServerCmd block; the payload follows
 static_assert(sizeof(ServerCmd) <= kCmdBytes, "ServerCmd fits its block");
 // Persistent scan servers of this process per device and their workgroups: a session starts one only while the
-// device's total stays within kServerBudget workgroups, so every server's workgroups are resident together (a
-// server whose workgroups could not all be resident would never complete a command).
-constexpr int kServerBudget = 512;
+// device's total stays within kServerBudget workgroups — one server per device, so no other persistent launch holds
+// the CU slots a server's late-dispatched workgroups wait for; concurrent sessions beyond it launch per scan.
+constexpr int kServerBudget = 256;
 std::mutex g_serverMu;
 int g_serverWgs[64] = {};
 double nowSeconds() {
@@ -276,7 +281,7 @@ void Device::stopServer() {
 // program reads topic counts, no topic delta is pending (those are applied by `prep` before any workgroup reads).
 bool Device::serveScan(const DevProgram& prog, const Staged& g, bool readsTopicCounts) {
   (void)prog;
-  if (!serverUsable_) return false;
+  if (!serverUsable_ || !serverAllowed_) return false;
   if (g.nb > kOverlayRows || g.nr > kOverlayRows || g.np > kOverlayRows) return false;
   if (readsTopicCounts && g.nt > 0) return false;
   return true;
@@ -320,6 +325,10 @@ int64_t Device::serverRun(const DevProgram& prog, const Staged& g, int op, const
     ver = ++progVer_;
   }
   perf.serverPayloadBytes += (int64_t)((sendProg ? sizeof(DevProgram) : 0) + rows + aBytes + nC * 4);
+  prof().addPayload((int64_t)((sendProg ? sizeof(DevProgram) : 0) + rows + aBytes + nC * 4));
+  prof().count(11, "srv.bytes.rows", (int64_t)rows);
+  prof().count(12, "srv.bytes.A", (int64_t)aBytes);
+  prof().count(13, "srv.bytes.C", (int64_t)nC * 4);
   if (rows) std::memcpy(pay + oRows, hStage_, rows);
   if (op == SOP_SEGS) std::memcpy(pay + oA, A, aBytes);
   else if (nA) writeRowRefs(pay + oA, (const int32_t*)A, nA);
@@ -339,6 +348,12 @@ int64_t Device::serverRun(const DevProgram& prog, const Staged& g, int op, const
     c.keyBase = params[1];
   }
   c.progVer = ver;
+  {  // every tile of the first sweep gets its own workgroup; a smaller scan leaves the others out of the command
+    const uint64_t total = op == SOP_PAIRS ? (uint64_t)params[0] : (uint64_t)params[0] * (uint64_t)params[1];
+    uint64_t need = (total + 255) / 256;
+    need = std::max<uint64_t>(8, (need + 7) / 8 * 8);
+    c.nActive = (int32_t)std::min<uint64_t>(need, (uint64_t)serverBlocks_);
+  }
   c.nb = g.nb;
   c.nr = g.nr;
   c.np = g.np;
@@ -596,7 +611,13 @@ void Device::waitMail(unsigned long long seq) {
       const hipError_t q = hipStreamQuery(ST);
       if (q == hipSuccess) {
         if ((__atomic_load_n(&mail[0], __ATOMIC_ACQUIRE) >> 32) == want) break;
-        throw std::runtime_error("scan finished without publishing its result");
+        char msg[256];
+        std::snprintf(msg, sizeof(msg),
+                      "scan finished without publishing its result (seq %llu, mail %016llx, server %s, server exit "
+                      "%016llx)",
+                      (unsigned long long)seq, (unsigned long long)mail[0], serverOn_ ? "on" : "off",
+                      (unsigned long long)mail[3]);
+        throw std::runtime_error(msg);
       }
       if (q != hipErrorNotReady) hipCheck(q, "scan");
     }
@@ -836,6 +857,9 @@ int64_t Device::segUpload(const SegIn& sg) {
     for (int r : *sg.v)
       if (rowBroker_[r] != sg.cb) throw std::logic_error("snapshot segment is not current for its broker");
     writeRowRefs((char*)(segPool_ + segHead_), sg.v->data(), n);
+    perf.serverPayloadBytes += (int64_t)(n * sizeof(RowRef));
+    prof().addPayload((int64_t)(n * sizeof(RowRef)));
+    prof().count(14, "srv.bytes.pool", (int64_t)(n * sizeof(RowRef)));
   }
   const uint32_t off = (uint32_t)segHead_;
   segHead_ += span;
@@ -850,7 +874,7 @@ int64_t Device::scanSegs(const DevProgram& prog, const std::vector<SegIn>& segs,
   size_t K = 0;
   for (const SegIn& sg : segs) K += sg.v->size() > sg.skip ? sg.v->size() - sg.skip : 0;
   const bool readsTc = (prog.needs & (NEED_TOPIC | NEED_TLEAD)) != 0;
-  bool served = serverUsable_ && K > 0 && Nr > 0 && segs.size() <= (size_t)kMaxSegs &&
+  bool served = serverUsable_ && serverAllowed_ && K > 0 && Nr > 0 && segs.size() <= (size_t)kMaxSegs &&
                 (uint64_t)K * (uint64_t)N < (1ull << 31);
   if (served) {
     segTab_.clear();

@@ -136,7 +136,12 @@ class Device {
   using SegIn = SnapSeg;
   int64_t scanSegs(const DevProgram& prog, const std::vector<SegIn>& segs, const int32_t* cands, int N, int c0,
                    int c1);
-  bool segsUsable() const { return serverUsable_; }
+  bool segsUsable() const { return serverUsable_ && serverAllowed_; }
+  // the session's scans may (not) use the resident scan server (sessions whose scans wait on other ranks may not)
+  void setServerAllowed(bool on) {
+    if (!on) stopServer();
+    serverAllowed_ = on;
+  }
   void stats(const StatsParams& P, const uint8_t* allowedAliveHost, StatsOut* out);
 
   // Chains (K7, kernels/scan.hip): decisions applied on the device inside one launch. uploadLoads gives the device
@@ -227,6 +232,7 @@ class Device {
   size_t fgCap_ = 0;
   bool serverOn_ = false;
   bool serverUsable_ = false;  // set in the constructor (gfx950, CCMI_SERVER, fine-grained VRAM host-writable)
+  bool serverAllowed_ = true;   // setServerAllowed
   int serverBlocks_ = 256;
   int progVer_ = 0;
   bool progSent_ = false;

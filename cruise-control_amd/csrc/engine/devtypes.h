@@ -224,8 +224,9 @@ struct alignas(16) ServerCmd {
   int32_t progVer;       // the DevProgram at oProg changes only with its version
   int32_t nb, nr, np, nt;
   uint32_t oProg, oB, oR, oP, oT, oA, oC;
-  int32_t nSegs;  // SOP_SEGS: entries of the segment table
-  int32_t pad[2];
+  int32_t nSegs;    // SOP_SEGS: entries of the segment table
+  int32_t nActive;  // workgroups [0, nActive) take part (a multiple of 8); the others only follow the sequence
+  int32_t pad;
 };
 static_assert(sizeof(ServerCmd) % 16 == 0, "ServerCmd words");
 

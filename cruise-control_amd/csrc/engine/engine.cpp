@@ -1173,20 +1173,14 @@ class ResourceDistribution : public GoalImpl {
     std::vector<int32_t> cands, pr, pb, fol, elig;
     std::vector<int32_t> pairOwner;
     size_t i = 0;
-    bool first = true;
     while (i < list.size()) {
       int dst = -1;
       size_t hitIdx = 0;
       if (!lead) {
         {
           PhaseScope pc(PH_CAND_BUILD);
-          if (built) {
-            cand.inorder(inorder);
-          } else if (!first) {
-            inorder.clear();
-            for (int x : m.brokersByPct(res))
-              if (inSet[x]) inorder.push_back(x);
-          }
+          if (built) cand.inorder(inorder);
+          // (the lazy order is kept up to date after every accept below)
           e.eligible(inorder, DA_MOVE, cands);
         }
         const int64_t key = e.crossScan(*this, DA_MOVE, list, i, cands);
@@ -1226,7 +1220,6 @@ class ResourceDistribution : public GoalImpl {
       }
       if (!lead) m.relocateReplica(m.rPart[list[hitIdx]], b, dst);
       else m.relocateLeadership(m.rPart[list[hitIdx]], b, dst);
-      first = false;
       if (underUpper(m, b, upperSrc) && !(fix && m.bNoff[b] > 0)) {
         prof().count(10, "out.done");
         m.clearTracked(b);
@@ -1242,6 +1235,28 @@ class ResourceDistribution : public GoalImpl {
         } else {  // the removal finds dst's node: the set stays clean
           hist.push_back({dst, m.pct(dst, res), add});
           inSet[dst] = add ? 1 : 0;
+          if (!lead) {
+            // the members' (pct, id) order: only dst's key moved (b is no member on this path), so dst leaves its
+            // slot (found at its old key) and, still a member, re-enters at its new key (the leadership branch
+            // reads inSet directly)
+            PhaseScope pc(PH_CAND_BUILD);
+            const int idd = m.bId[dst];
+            auto before = [&](int x, double k, int id) {  // (key(x), id(x)) < (k, id)
+              const int c = jcmpDouble(m.pct(x, res), k);
+              return c ? c < 0 : m.bId[x] < id;
+            };
+            auto at = std::lower_bound(inorder.begin(), inorder.end(), dst, [&](int x, int) {
+              return x != dst && before(x, dstBefore, idd);
+            });
+            if (at != inorder.end() && *at == dst) inorder.erase(at);
+            else throw std::logic_error("moveOut: the lazy candidate order lost its destination");
+            if (add) {
+              const double kn = m.pct(dst, res);
+              inorder.insert(std::lower_bound(inorder.begin(), inorder.end(), dst,
+                                              [&](int x, int) { return before(x, kn, idd); }),
+                             dst);
+            }
+          }
           i = hitIdx + 1;
           continue;
         }

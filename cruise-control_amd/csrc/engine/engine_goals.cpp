@@ -1521,54 +1521,50 @@ class LeaderReplicaDistribution : public GoalImpl {
     std::vector<int32_t> single{b}, cands;
     e.eligible(single, DA_MOVE, cands);
     if (cands.empty()) return true;  // every source replica visits an empty candidate list: nothing moves
-    struct Seg {
-      int src;
-      const std::vector<int32_t>* v;  // the source's sorted leaders (held by snapTab until the next model change)
-      size_t start;
-      size_t len() const { return v->size() > start ? v->size() - start : 0; }
-    };
-    std::vector<Seg> segs;
-    std::vector<int32_t> flat;
+    // rows: the sources' sorted leaders (snapshots held by snapTab until the next model change; device-resident
+    // segments of the snapshot pool)
+    auto segLen = [](const SnapSeg& x) { return x.v->size() > x.skip ? x.v->size() - x.skip : 0; };
+    std::vector<SnapSeg> segs;
     size_t target = 2048;
     bool haveCur = false;
-    Seg cur{0, nullptr, 0};
+    SnapSeg cur{nullptr, 0, 0};
     while (haveCur || !pq.empty()) {
       segs.clear();
-      flat.clear();
+      size_t rows = 0;
       if (haveCur) {  // the source being iterated continues first, after its winner
-        cur.v = &m.snapshotIn(snapTab, cur.src, s);
+        cur.v = m.snapshotInShared(snapTab, cur.cb, s);
         segs.push_back(cur);
+        rows += segLen(cur);
         haveCur = false;
-        flat.insert(flat.end(), cur.v->begin() + std::min(cur.start, cur.v->size()), cur.v->end());
       }
-      while (!pq.empty() && (segs.empty() || flat.size() < target)) {
+      while (!pq.empty() && (segs.empty() || rows < target) && segs.size() < (size_t)kMaxSegs) {
         const int src = pq.poll();
-        segs.push_back({src, &m.snapshotIn(snapTab, src, s), 0});
-        flat.insert(flat.end(), segs.back().v->begin(), segs.back().v->end());
+        segs.push_back({m.snapshotInShared(snapTab, src, s), src, 0});
+        rows += segLen(segs.back());
       }
-      const int64_t key = cands.empty() ? -1 : e.crossScan(*this, DA_MOVE, flat, 0, cands);
+      const int64_t key = cands.empty() ? -1 : e.crossScanSegs(*this, DA_MOVE, segs, cands);
       if (key < 0) {
         target = std::min<size_t>(target * 8, (size_t)1 << 18);
         continue;  // every polled source exhausted; none is re-enqueued
       }
       target = 2048;
       size_t q = (size_t)key, mi = 0;
-      while (q >= segs[mi].len()) {
-        q -= segs[mi].len();
+      while (q >= segLen(segs[mi])) {
+        q -= segLen(segs[mi]);
         ++mi;
       }
-      const Seg hit = segs[mi];
-      const size_t idx = hit.start + q;
+      const SnapSeg hit = segs[mi];
+      const size_t idx = hit.skip + q;
       const size_t hitSize = hit.v->size();
-      m.relocateReplica(m.rPart[(*hit.v)[idx]], hit.src, b);
+      m.relocateReplica(m.rPart[(*hit.v)[idx]], hit.cb, b);
       if (++nl >= lower) return false;
-      for (size_t t = mi + 1; t < segs.size(); ++t) pq.add(segs[t].src);  // un-poll speculative sources
-      if (!pq.empty() && m.bNlead[hit.src] < m.bNlead[pq.peek()]) {
-        pq.add(hit.src);
+      for (size_t t = mi + 1; t < segs.size(); ++t) pq.add(segs[t].cb);  // un-poll speculative sources
+      if (!pq.empty() && m.bNlead[hit.cb] < m.bNlead[pq.peek()]) {
+        pq.add(hit.cb);
       } else if (idx + 1 < hitSize) {
         // the live view lost exactly the moved replica: the entries after it keep their order, so the iteration
         // continues at the same index of the source's fresh snapshot
-        cur = {hit.src, nullptr, idx};
+        cur = {nullptr, hit.cb, idx};
         haveCur = true;
       }
     }

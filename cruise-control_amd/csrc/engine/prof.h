@@ -22,6 +22,10 @@ struct PhaseProf {
   int64_t scans[PH_COUNT] = {};
   const int64_t* candCounter = nullptr;  // the engine's reference-equivalent candidate count
   int64_t cands[PH_COUNT] = {};
+  int64_t payload[PH_COUNT] = {};  // scan-server command bytes (rows, requests, snapshot uploads) per driver
+  void addPayload(int64_t b) {
+    if (on && driver >= 0) payload[driver] += b;
+  }
   bool on = std::getenv("CCMI_PROFILE") != nullptr;
   // named event counters (diagnostics of the drivers' control flow)
   static constexpr int kCounters = 16;
@@ -44,8 +48,8 @@ struct PhaseProf {
         std::fprintf(stderr, "  %-14s %10.1f ms %10lld calls %8.2f us/call", names[i], ms[i], (long long)n[i],
                      1e3 * ms[i] / n[i]);
         if (scans[i])
-          std::fprintf(stderr, "   [%lld scans, %.1f ms in scans, %lld candidates]", (long long)scans[i], scanMs[i],
-                       (long long)cands[i]);
+          std::fprintf(stderr, "   [%lld scans, %.1f ms in scans, %lld candidates, %.1f MB payload]",
+                       (long long)scans[i], scanMs[i], (long long)cands[i], payload[i] * 1e-6);
         std::fprintf(stderr, "\n");
       }
     for (int i = 0; i < kCounters; ++i)

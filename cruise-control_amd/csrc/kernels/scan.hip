@@ -159,6 +159,51 @@ __device__ __forceinline__ void applyRowsBlock(const MutTables& M, const BrokerR
   }
 }
 
+// applyRowsBlock with device-scope stores (the scan server): each store is written through to memory, so the rows
+// need no L2 write-back before workgroup 0 arrives — the next command's acquire (an L2 invalidate) is enough for every
+// workgroup to read them.
+__device__ __forceinline__ void stDev(double* p, double v) {
+  __hip_atomic_store(reinterpret_cast<unsigned long long*>(p), __double_as_longlong(v), __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void stDev(int32_t* p, int32_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void applyRowsCoherent(const MutTables& M, const BrokerRow* brows, int nb,
+                                                  const ReplicaRow* rrows, int nr, const PartitionRow* prows, int np,
+                                                  int first, int stride) {
+  for (int i = first; i < nb; i += stride) {
+    const BrokerRow& x = brows[i];
+    BrokerRec& d = M.brokers[x.b];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) stDev(&d.util[k], x.util[k]);
+    stDev(&d.nrep, x.nrep);
+    stDev(&d.nlead, x.nlead);
+    stDev(&d.pot, x.potNwOut);
+    stDev(&d.lbi, x.leadNwIn);
+    stDev(&d.alive, x.alive);
+  }
+  for (int i = first; i < nr; i += stride) {
+    const ReplicaRow& x = rrows[i];
+    ReplicaRec& d = M.replicas[x.r];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) stDev(&d.util[k], x.util[k]);
+    stDev(&d.broker, x.broker);
+    stDev(&d.flags, x.flags);
+  }
+  for (int i = first; i < np; i += stride) {
+    const PartitionRow& x = prows[i];
+    PartitionRec& d = M.parts[x.p];
+#pragma unroll
+    for (int k = 0; k < kMaxRf; ++k) stDev(&d.brokers[k], x.brokers[k]);
+    stDev(&d.leadNwOut, x.leadNwOut);
+    int32_t* rk = reinterpret_cast<int32_t*>(d.racks);  // the int16 racks as whole words
+    const int32_t* xr = reinterpret_cast<const int32_t*>(x.racks);
+#pragma unroll
+    for (int k = 0; k < kMaxRf / 2; ++k) stDev(&rk[k], xr[k]);
+  }
+}
+
 // Stage the update list into LDS (every workgroup that evaluates pairs) and apply it to HBM (workgroup 0, which
 // always evaluates the first chunk). Workgroups whose first chunk is already beaten exit without staging.
 __device__ __forceinline__ void overlayStage(OverlayLds& ov, const UpdateList& U) {
@@ -491,9 +536,11 @@ struct PreView {
            (pb6 >= 0 && pb6 != self && prk6 == rk) | (pb7 >= 0 && pb7 != self && prk7 == rk);
   }
   // rack of the partition's slot on broker b (b hosts the partition: the replica's own broker)
+  // (exactly one slot holds b; every term selects a value against a constant, so the compiler cannot turn the
+  // chain into a select of field addresses — that would keep the whole view in scratch memory)
   __device__ __forceinline__ int slotRack(int /*p*/, int b) const {
-    return pb0 == b ? prk0 : pb1 == b ? prk1 : pb2 == b ? prk2 : pb3 == b ? prk3
-         : pb4 == b ? prk4 : pb5 == b ? prk5 : pb6 == b ? prk6 : prk7;
+    return (pb0 == b ? prk0 : 0) | (pb1 == b ? prk1 : 0) | (pb2 == b ? prk2 : 0) | (pb3 == b ? prk3 : 0) |
+           (pb4 == b ? prk4 : 0) | (pb5 == b ? prk5 : 0) | (pb6 == b ? prk6 : 0) | (pb7 == b ? prk7 : 0);
   }
   __device__ __forceinline__ int rackCount(int /*p*/, int rk) const {
     return (pb0 >= 0 && prk0 == rk) + (pb1 >= 0 && prk1 == rk) + (pb2 >= 0 && prk2 == rk) + (pb3 >= 0 && prk3 == rk) +
@@ -562,7 +609,21 @@ uint32_t scanXcdSliceMinCols() { return xcdSliceMinCols(); }
       (T).stamps[((seq)&1023ull) * 8 + (i)] = __builtin_amdgcn_s_memrealtime();                       \
     }                                                                                                 \
   } while (0)
+// Scan-server phase stamps (CCMI_STAMPS): workgroup 0's thread 0 notes when it saw a command (0), had it copied (1),
+// staged its rows (2), finished its first tile (3) and arrived (4); the deltas are summed at stamps[8192 + i].
+#define SRV_STAMP(T, i)                                                                               \
+  do {                                                                                               \
+    if ((T).stamps && blockIdx.x == 0 && threadIdx.x == 0) {                                          \
+      __builtin_amdgcn_s_waitcnt(0);                                                                  \
+      srvT[i] = __builtin_amdgcn_s_memrealtime();                                                     \
+    }                                                                                                 \
+  } while (0)
 constexpr unsigned long long kNone = ~0ull;
+// Register budgets. A candidate's view (PreView: the replica, partition and both brokers' fields) has to stay in
+// VGPRs — a spilled view sends every predicate operand through scratch. The server and the one-workgroup chains
+// run one workgroup (4 waves) per CU, so one wave per SIMD and the whole register file; the launched scans keep two.
+constexpr int kServerWaves = 1;
+constexpr int kScanWaves = 2;
 
 __device__ __forceinline__ unsigned long long waveMin(unsigned long long v) {
 #pragma unroll
@@ -619,7 +680,7 @@ __device__ __forceinline__ void publishLast(unsigned long long* __restrict__ res
 
 // Rows reps[0, K) x candidate columns [c0, c0 + Nr) of an N-column candidate list; key = k * N + c0 + jj. A sharded
 // session scans only its own column range; keys stay global, so a MIN over shards is the global first fit.
-__global__ __launch_bounds__(kBlock) void scan_cross(DevTables T, MutTables Mt, UpdateList U, DevProgram prog,
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, kScanWaves))) void scan_cross(DevTables T, MutTables Mt, UpdateList U, DevProgram prog,
                                                      const RowRef* __restrict__ reps,
                                                      const int32_t* __restrict__ cands, int K, int Nr, int N, int c0,
                                                      int sliced, unsigned long long* __restrict__ result,
@@ -741,7 +802,7 @@ __device__ __forceinline__ void copySysOneThread(X* dst, const X* src) {  // all
 }
 constexpr unsigned long long kServerIdleTicks = 200000000ull;  // 2 s of s_memrealtime (100 MHz)
 
-__global__ __launch_bounds__(kBlock) void scan_server(DevTables T, MutTables Mt, const ServerCmd* __restrict__ cmd,
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, kServerWaves))) void scan_server(DevTables T, MutTables Mt, const ServerCmd* __restrict__ cmd,
                                                       const char* __restrict__ pay, const RowRef* __restrict__ pool,
                                                       unsigned long long* __restrict__ result,
                                                       unsigned int* __restrict__ done,
@@ -755,31 +816,60 @@ __global__ __launch_bounds__(kBlock) void scan_server(DevTables T, MutTables Mt,
   __shared__ SegEntry sSeg[kMaxSegs + 1];
   unsigned long long last = startSeq;
   int progVer = -1;
-  bool prevRows = false;  // the previous command had rows for workgroup 0 to write into the tables
+  bool needAcq = false;  // a command since this workgroup's last acquire had rows workgroup 0 wrote into the tables
   unsigned long long idleSince = __builtin_amdgcn_s_memrealtime();
+  unsigned long long srvT[5] = {0, 0, 0, 0, 0};
   for (;;) {
     if (threadIdx.x == 0) {
       int ex = 0;
+      // The idle clock starts once this workgroup sees its last command published: until then a workgroup that was
+      // dispatched late (the GPU busy with other sessions' kernels) is still working on it and the host is waiting.
+      bool published = last == startSeq;
       for (int spin = 0;; ++spin) {
         const unsigned long long s =
             __hip_atomic_load(&cmd->seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         if (s != last) break;
-        if ((spin & 63) == 63 && __builtin_amdgcn_s_memrealtime() - idleSince > kServerIdleTicks) {
-          ex = 1;
-          break;
+        if ((spin & 63) == 63) {
+          if (!published) {
+            const unsigned long long mw = __hip_atomic_load(&mail[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            if ((mw >> 32) == (last & 0xffffffffull)) {
+              published = true;
+              idleSince = __builtin_amdgcn_s_memrealtime();
+            }
+          } else if (__builtin_amdgcn_s_memrealtime() - idleSince > kServerIdleTicks) {
+            ex = 1;
+            break;
+          }
         }
         __builtin_amdgcn_s_sleep(4);
       }
-      // the rows workgroup 0 wrote for the previous command (released before its arrival) become visible here; a
-      // command after one without rows has nothing new to see in the tables
-      if (prevRows) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      SRV_STAMP(T, 0);
+      // the rows workgroup 0 wrote for earlier commands (released before its arrivals) become visible here; after
+      // commands without rows there is nothing new to see in the tables
+      if (needAcq) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      needAcq = false;
       if (!ex) copySysOneThread(&c, cmd);
+      SRV_STAMP(T, 1);
       if (blockIdx.x == 0)  // busy-time stamp, read by the last workgroup to arrive
         __hip_atomic_store(t0, __builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       sExit = ex;
     }
     __syncthreads();
-    if (sExit || c.op == SOP_EXIT) break;
+    if (sExit || c.op == SOP_EXIT) {
+      // exit record for the host's diagnostics: mail[3] = {reason (1 watchdog, 2 exit command) : 32 | last seq : 32}
+      if (blockIdx.x == 0 && threadIdx.x == 0)
+        __hip_atomic_store(&mail[3], ((unsigned long long)(sExit ? 1 : 2) << 32) | (last & 0xffffffffull),
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      break;
+    }
+    const bool rows = (c.nb | c.nr | c.np | c.nt) != 0;
+    const uint32_t nAct = (uint32_t)c.nActive;
+    if (blockIdx.x >= nAct) {  // not taking part: only the sequence (and a pending acquire) moves on
+      needAcq |= rows;
+      last = c.seq;
+      __syncthreads();
+      continue;
+    }
     if (c.progVer != progVer) {
       copySys(&prog, pay + c.oProg, (int)sizeof(DevProgram));
       progVer = c.progVer;
@@ -807,17 +897,11 @@ __global__ __launch_bounds__(kBlock) void scan_server(DevTables T, MutTables Mt,
                reinterpret_cast<int32_t*>(ov.p), reinterpret_cast<const int32_t*>(U.prows),
                U.np * (int)(sizeof(PartitionRow) / 4));
       __syncthreads();
-      if (blockIdx.x == 0 && (U.nb | U.nr | U.np | U.nt)) {
-        applyRowsBlock(Mt, ov.b, ov.nb, ov.r, ov.nr, ov.p, ov.np, nullptr, 0, threadIdx.x, blockDim.x);
-        for (int i = threadIdx.x; i < U.nt; i += blockDim.x) {
-          TopicCountDelta d;
-          copySysOneThread(&d, &U.tdel[i]);
-          atomicAdd(&(d.kind ? Mt.topicLead : Mt.topicCount)[(size_t)d.topic * Mt.ldB + d.broker], d.delta);
-        }
-      }
       staged = true;
     };
     if (blockIdx.x == 0) stage();
+    SRV_STAMP(T, 2);
+    bool firstTile = true;
     const int32_t* A = (const int32_t*)(pay + c.oA);
     const int32_t* C = (const int32_t*)(pay + c.oC);
     if (c.op == SOP_CROSS || c.op == SOP_SEGS) {
@@ -825,14 +909,14 @@ __global__ __launch_bounds__(kBlock) void scan_server(DevTables T, MutTables Mt,
       bool segsLoaded = false;
       const int nSegs = c.nSegs;
       const int K = c.K, Nr = c.Nr, N = c.N, c0 = c.c0;
-      uint32_t colStart = 0, Ws = (uint32_t)Nr, wg = blockIdx.x, wgs = gridDim.x;
+      uint32_t colStart = 0, Ws = (uint32_t)Nr, wg = blockIdx.x, wgs = nAct;
       if (c.sliced) {
         const uint32_t W = ((uint32_t)Nr + kXcds - 1) / kXcds;
         const uint32_t sl = blockIdx.x % kXcds;
         colStart = sl * W;
         Ws = colStart < (uint32_t)Nr ? min(W, (uint32_t)Nr - colStart) : 0u;
         wg = blockIdx.x / kXcds;
-        wgs = gridDim.x / kXcds;
+        wgs = nAct / kXcds;
       }
       const uint32_t total = (uint32_t)K * Ws;
       for (uint32_t base = wg * kBlock; base < total; base += wgs * kBlock) {
@@ -874,6 +958,10 @@ __global__ __launch_bounds__(kBlock) void scan_server(DevTables T, MutTables Mt,
           if (inList && moveCandidateAccepted(prog, v, v.r, v.dst)) local = (unsigned long long)k * N + c0 + j;
         }
         const unsigned long long m = blockMin(local);
+        if (firstTile) {
+          SRV_STAMP(T, 3);
+          firstTile = false;
+        }
         if (m != kNone) {
           if (threadIdx.x == 0) atomicMin(result, m);
           break;
@@ -881,7 +969,7 @@ __global__ __launch_bounds__(kBlock) void scan_server(DevTables T, MutTables Mt,
       }
     } else {  // SOP_PAIRS
       const int n = c.n, keyBase = c.keyBase;
-      for (int base = blockIdx.x * kBlock; base < n; base += gridDim.x * kBlock) {
+      for (int base = blockIdx.x * kBlock; base < n; base += (int)nAct * kBlock) {
         if (blockBest(result) <= (unsigned long long)(keyBase + base)) break;
         const int q = base + threadIdx.x;
         RowRef rq{0, 0, 0, 0};
@@ -900,22 +988,40 @@ __global__ __launch_bounds__(kBlock) void scan_server(DevTables T, MutTables Mt,
             local = (unsigned long long)(keyBase + q);
         }
         const unsigned long long m = blockMin(local);
+        if (firstTile) {
+          SRV_STAMP(T, 3);
+          firstTile = false;
+        }
         if (m != kNone) {
           if (threadIdx.x == 0) atomicMin(result, m);
           break;
         }
       }
     }
-    // arrival: workgroup 0's row writes are released first (the only plain stores of a command); every other
-    // workgroup only made device-scope atomics, which need no cache write-back: waiting for them to complete orders
-    // them before the arrival. The last workgroup publishes and resets with device-scope atomics as well.
-    const bool rows = (c.nb | c.nr | c.np | c.nt) != 0;
+    if (firstTile) SRV_STAMP(T, 3);
+    // Workgroup 0 writes the command's rows into the tables for the next commands (no workgroup reads them from the
+    // tables in this one: the LDS overlay has them) after its tiles, with write-through device-scope stores, and
+    // applies the topic-count deltas with device-scope atomics.
+    if (blockIdx.x == 0 && rows) {
+      applyRowsCoherent(Mt, ov.b, ov.nb, ov.r, ov.nr, ov.p, ov.np, threadIdx.x, blockDim.x);
+      for (int i = threadIdx.x; i < U.nt; i += blockDim.x) {
+        TopicCountDelta d;
+        copySysOneThread(&d, &U.tdel[i]);
+        atomicAdd(&(d.kind ? Mt.topicLead : Mt.topicCount)[(size_t)d.topic * Mt.ldB + d.broker], d.delta);
+      }
+    }
+    // arrival: every store and atomic of the command is device-scope, so waiting for them to complete orders them
+    // before the arrival (no cache write-back). The last workgroup publishes and resets with device-scope atomics.
     __syncthreads();
     if (threadIdx.x == 0) {
-      if (blockIdx.x == 0 && rows) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       const unsigned int prev = __hip_atomic_fetch_add(done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (prev == gridDim.x - 1) {
+      if (T.stamps && blockIdx.x == 0) {
+        srvT[4] = __builtin_amdgcn_s_memrealtime();
+        atomicAdd(&T.stamps[8192 + 0], 1ull);
+        for (int i = 0; i < 4; ++i) atomicAdd(&T.stamps[8192 + 1 + i], srvT[i + 1] - srvT[i]);
+      }
+      if (prev == nAct - 1) {
         const unsigned long long v = __hip_atomic_load(&result[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         const unsigned long long lo = v == kNone ? 0ull : (v + 1) & 0xffffffffull;
         __hip_atomic_store(&result[0], kNone, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -932,7 +1038,7 @@ __global__ __launch_bounds__(kBlock) void scan_server(DevTables T, MutTables Mt,
       }
     }
     last = c.seq;
-    prevRows = rows;
+    needAcq |= rows;
     idleSince = __builtin_amdgcn_s_memrealtime();
     __syncthreads();
   }
@@ -1011,7 +1117,7 @@ __global__ __launch_bounds__(1024) void swap_visited_sum(const int32_t* __restri
 }
 
 // PAIRS: explicit (replica, broker) list in iteration order (leadership moves: per-replica follower lists).
-__global__ __launch_bounds__(kBlock) void scan_pairs(DevTables T, MutTables Mt, UpdateList U, DevProgram prog,
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, kScanWaves))) void scan_pairs(DevTables T, MutTables Mt, UpdateList U, DevProgram prog,
                                                      const RowRef* __restrict__ pr,
                                                      const int32_t* __restrict__ pb, int n, int keyBase,
                                                      unsigned long long* __restrict__ result,
@@ -1146,7 +1252,7 @@ __device__ __forceinline__ unsigned long long chainFirstPair(const DevTables& T,
 
 // PAIRS: pairs (pr[q], pb[q]) in reference order; after accepting q the loop resumes at next[q]; at most
 // maxAccepts moves (the callers' stop counts). visited = reference-equivalent candidates of the sequence of scans.
-__global__ __launch_bounds__(kBlock) void chain_pairs(DevTables T, ChainTables C, DevProgram prog,
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, kServerWaves))) void chain_pairs(DevTables T, ChainTables C, DevProgram prog,
                                                       const int32_t* __restrict__ pr, const int32_t* __restrict__ pb,
                                                       const int32_t* __restrict__ next, int n, int maxAccepts,
                                                       int32_t* __restrict__ log, ChainResultDev* __restrict__ out) {
@@ -1181,7 +1287,7 @@ __global__ __launch_bounds__(kBlock) void chain_pairs(DevTables T, ChainTables C
 // broker in order. A row is skipped when its broker is alive, the replica online and shouldKeepInTheCurrentBroker
 // holds on the CURRENT partition state (RackAwareGoal.java:214-225); otherwise the first candidate in cands[0, N)
 // that rackAwareEligibleBrokers keeps and the predicate conjunction accepts wins. No winner: failRow = row + 1.
-__global__ __launch_bounds__(kBlock) void chain_rack_rows(DevTables T, ChainTables C, DevProgram prog,
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, kServerWaves))) void chain_rack_rows(DevTables T, ChainTables C, DevProgram prog,
                                                           const int32_t* __restrict__ rows, int n,
                                                           const int32_t* __restrict__ cands, int N,
                                                           int32_t* __restrict__ log, ChainResultDev* __restrict__ out) {

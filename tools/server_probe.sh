@@ -12,5 +12,5 @@ step() {
   if [ $rc -ne 0 ]; then echo "stopping: $name exited $rc"; exit $rc; fi
 }
 step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
-step pytest_gpu 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread -k "${PYTEST_K:-}"
+step pytest_gpu 900 python -u -m pytest tests -m gpu -x -v --timeout 150 --timeout-method thread -k "${PYTEST_K:-}"
 CCMI_PROFILE=1 step probe_server 600 python -u tools/probe.py --workload c2
