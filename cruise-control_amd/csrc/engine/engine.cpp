@@ -200,8 +200,33 @@ int64_t Engine::crossScan(GoalImpl& self, int action, const std::vector<int32_t>
   m.flushToDevice();
   DevProgram prog = program(self, action);
   prog.filter = filter;
-  const int c0 = (int)((int64_t)N * shard.rank / shard.count), c1 = (int)((int64_t)N * (shard.rank + 1) / shard.count);
-  const int64_t key = combine(dev->scanCross(prog, reps.data() + r0, K, cands.data(), N, c0, c1));
+  // Rows are scanned in windows: a first-fit winner in the first rows is the same winner whatever follows them,
+  // so a scan that is usually won early does not send (nor evaluate) every row. The first window can also be a
+  // probe of the first row's first kProbeCols columns, used while this goal's scans mostly end there.
+  constexpr int kRowWindow = 32, kProbeCols = 1024;
+  auto scanRows = [&](int k0, int nk, int cEnd) -> int64_t {  // rows [k0, k0 + nk) x columns [0, cEnd) of N
+    const int s0 = (int)((int64_t)cEnd * shard.rank / shard.count), s1 = (int)((int64_t)cEnd * (shard.rank + 1) / shard.count);
+    const int64_t k = combine(dev->scanCross(prog, reps.data() + r0 + k0, nk, cands.data(), N, s0, s1));
+    return k < 0 ? -1 : k + (int64_t)k0 * N;
+  };
+  static const bool windows = !std::getenv("CCMI_SCAN_NO_WINDOWS");  // A/B diagnostics: one scan over every row
+  int64_t key = -1;
+  int done = 0;  // rows fully scanned without a winner
+  bool found = !windows;
+  if (!windows) key = scanRows(0, K, N);
+  if (!found && N > 2 * kProbeCols && self.probeHitRate > 0.9) {
+    key = scanRows(0, 1, kProbeCols);
+    found = key >= 0;
+    self.probeHitRate = 0.95 * self.probeHitRate + (found ? 0.05 : 0.0);
+  }
+  if (!found && K > 2 * kRowWindow) {
+    key = scanRows(0, kRowWindow, N);
+    found = key >= 0;
+    done = kRowWindow;
+  }
+  if (!found) key = scanRows(done, K - done, N);
+  if (windows && key >= 0 && N > 2 * kProbeCols && !(self.probeHitRate > 0.9))  // learn whether the probe would win
+    self.probeHitRate = 0.95 * self.probeHitRate + (key < kProbeCols ? 0.05 : 0.0);
   if (count) {
     if (prog.exclLeadMove || prog.newOnly) candidates += exclLeadCount(prog, reps.data() + r0, K, cands, key);
     else candidates += key >= 0 ? key + 1 : (int64_t)K * N;
@@ -1068,6 +1093,7 @@ class ResourceDistribution : public GoalImpl {
       int dst;
       double keyAfter;
       bool add;
+      double bKeyAfter;  // b's key after the move (b may be a member whose node keeps its entry position)
     };
     std::vector<Step> hist;
     std::vector<std::pair<int, double>> entryKey;  // pct at entry of every broker a move changed
@@ -1122,21 +1148,21 @@ class ResourceDistribution : public GoalImpl {
         cand.buildByRank(ids, rank);
       }
       for (const Step& h : hist) {
-        for (auto& o : ovr)
+        for (auto& o : ovr) {
           if (o.first == h.dst) o.second = h.keyAfter;
+          if (o.first == b) o.second = h.bKeyAfter;
+        }
         cand.remove(h.dst);
         if (h.add) cand.add(h.dst);
       }
       ovr.clear();
       built = true;
     };
-    // b's own key changes with every move: if b is a member the lazy form does not apply
-    if (inSet[b]) {
-      entryIn = inSet;
-      materialise();
-    } else {
-      entryIn = inSet;
-    }
+    // b's own key changes with every move while its node stays where it was put. The replica-move form keeps
+    // the lazy order with b at that position as long as every member's live key still fits its place in the order
+    // (checked after each move); the leadership form, which keeps no order, builds the tree.
+    entryIn = inSet;
+    if (inSet[b] && action == DA_LEADERSHIP) materialise();
     auto memberBetween = [&](int dst, double k0, double k1) {
       // is a member other than dst strictly between (k0, id(dst)) and (k1, id(dst)) in (pct, id) order?
       const double lo = jcmpDouble(k0, k1) <= 0 ? k0 : k1, hi = jcmpDouble(k0, k1) <= 0 ? k1 : k0;
@@ -1229,33 +1255,39 @@ class ResourceDistribution : public GoalImpl {
       prof().count(lead ? 6 : 7, lead ? "out.lead.accept" : "out.move.accept");
       if (built) prof().count(8, "out.built.accept");
       if (!built) {
-        if (memberBetween(dst, dstBefore, m.pct(dst, res))) {
+        // The set is a consistent search tree iff its in-order sequence is sorted by the LIVE (key, id): then
+        // TreeMap.remove(dst) finds dst's node and add(dst) puts it at its sorted place. Only b's and dst's keys
+        // moved since the sequence was last sorted, so it is sorted iff each of them still fits between its
+        // neighbours (leadership form: no member strictly between dst's old and new key, b being no member).
+        bool clean;
+        size_t at = 0;
+        auto less = [&](int x, int y) { return m.cmpBrokerPct(res, x, y) < 0; };
+        if (lead) {
+          clean = !memberBetween(dst, dstBefore, m.pct(dst, res));
+        } else {
+          PhaseScope pc(PH_CAND_BUILD);
+          const size_t n = inorder.size();
+          at = (size_t)(std::find(inorder.begin(), inorder.end(), dst) - inorder.begin());
+          if (at == n) throw std::logic_error("moveOut: the lazy candidate order lost its destination");
+          auto fits = [&](size_t k) {
+            return (k == 0 || less(inorder[k - 1], inorder[k])) && (k + 1 == n || less(inorder[k], inorder[k + 1]));
+          };
+          clean = fits(at);
+          if (clean && inSet[b]) {
+            const size_t bj = (size_t)(std::find(inorder.begin(), inorder.end(), b) - inorder.begin());
+            clean = bj == n || fits(bj);
+          }
+        }
+        if (!clean) {
           prof().count(9, "out.materialise");
           materialise();
-        } else {  // the removal finds dst's node: the set stays clean
-          hist.push_back({dst, m.pct(dst, res), add});
+        } else {
+          hist.push_back({dst, m.pct(dst, res), add, m.pct(b, res)});
           inSet[dst] = add ? 1 : 0;
           if (!lead) {
-            // the members' (pct, id) order: only dst's key moved (b is no member on this path), so dst leaves its
-            // slot (found at its old key) and, still a member, re-enters at its new key (the leadership branch
-            // reads inSet directly)
             PhaseScope pc(PH_CAND_BUILD);
-            const int idd = m.bId[dst];
-            auto before = [&](int x, double k, int id) {  // (key(x), id(x)) < (k, id)
-              const int c = jcmpDouble(m.pct(x, res), k);
-              return c ? c < 0 : m.bId[x] < id;
-            };
-            auto at = std::lower_bound(inorder.begin(), inorder.end(), dst, [&](int x, int) {
-              return x != dst && before(x, dstBefore, idd);
-            });
-            if (at != inorder.end() && *at == dst) inorder.erase(at);
-            else throw std::logic_error("moveOut: the lazy candidate order lost its destination");
-            if (add) {
-              const double kn = m.pct(dst, res);
-              inorder.insert(std::lower_bound(inorder.begin(), inorder.end(), dst,
-                                              [&](int x, int) { return before(x, kn, idd); }),
-                             dst);
-            }
+            inorder.erase(inorder.begin() + (ptrdiff_t)at);
+            if (add) inorder.insert(std::lower_bound(inorder.begin(), inorder.end(), dst, less), dst);
           }
           i = hitIdx + 1;
           continue;

@@ -70,6 +70,8 @@ class GoalImpl {
   bool succeeded = true;
   bool finished = false;
   ccmi_provision_response prov{};  // Goal.provisionResponse
+  // crossScan's first-row probe (Engine::crossScan): recent share of scans won within the probe's columns
+  double probeHitRate = 0.0;
   virtual void init(Engine& e) = 0;
   virtual void rebalance(Engine& e, int b) = 0;
   virtual void update(Engine& e) = 0;

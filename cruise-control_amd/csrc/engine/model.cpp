@@ -206,6 +206,7 @@ void Model::build(const ccmi_cluster_desc& d) {
     }
   }
   bVer.assign(B, 0);
+  bDelta.assign(B, {});
   sortedCache.assign(B, {});
   filteredCache.assign(B, {});
   exclTopicSel.assign(T, 0);
@@ -522,6 +523,8 @@ void Model::relocateReplica(int p, int src, int dst) {
   bVer[dst]++;
   const int r = brokerRemove(src, p);
   if (r < 0) throw std::runtime_error("Replica is not in the cluster.");
+  noteDelta(src, r);
+  noteDelta(dst, r);
   ops.subAll(cLoad, rLoad[r]);
   ops.subAll(bPot[src], rLoad[pLeader[p]]);
   rBroker[r] = dst;
@@ -589,12 +592,14 @@ void Model::moveReplicaToEnd(int r) {
 
 bool Model::relocateLeadership(int p, int src, int dst) {
   PhaseScope ps(PH_RELOCATE);
-  bVer[src]++;
-  bVer[dst]++;
   const int sr = replicaOn(p, src);
   if (sr < 0 || !rLeader[sr]) return false;
   const int dr = replicaOn(p, dst);
   if (dr < 0 || rLeader[dr]) throw std::runtime_error("destination replica is a leader");
+  bVer[src]++;
+  bVer[dst]++;
+  noteDelta(src, sr);
+  noteDelta(dst, dr);
   // Broker.makeFollower(src)
   ops.subAll(bLnw[src], rLoad[sr]);
   sortedErase(src, sr);
@@ -823,6 +828,47 @@ void Model::setExcludedTopicSelection(const std::vector<uint8_t>& t) {
   for (auto& c : filteredCache) c.clear();
 }
 
+// The snapshot of version bVer[b] from the cached one of an earlier version with the same Spec: the replicas the
+// version log names leave, and those still on b that the Spec selects re-enter at their (key, index) position —
+// the order a full sort of (replicaKey, r) gives, since every other replica kept its key.
+bool Model::snapshotFromPrevious(int b, const Spec& s, std::vector<SortedCacheEntry>& cache, std::vector<int32_t>& out) {
+  static const bool off = std::getenv("CCMI_SNAPSHOT_FULL") != nullptr;  // diagnostics: always re-sort
+  if (off) return false;
+  const SortedCacheEntry* prev = nullptr;
+  for (const auto& c : cache)
+    if (c.spec == s && c.v && c.ver < bVer[b]) prev = &c;
+  if (!prev || bVer[b] - prev->ver > kDeltaLog) return false;
+  int32_t changed[kDeltaLog];
+  int nc = 0;
+  uint32_t covered = 0;
+  for (const auto& d : bDelta[b])
+    if (d.first > prev->ver && d.first <= bVer[b]) {
+      ++covered;
+      if (d.second >= 0) changed[nc++] = d.second;
+    }
+  if (covered != bVer[b] - prev->ver) return false;
+  out.clear();
+  out.reserve(prev->v->size() + nc);
+  for (int r : *prev->v) {
+    bool skip = false;
+    for (int i = 0; i < nc; ++i) skip |= changed[i] == r;
+    if (!skip) out.push_back(r);
+  }
+  for (int i = 0; i < nc; ++i) {
+    const int x = changed[i];
+    bool dup = false;
+    for (int j = 0; j < i; ++j) dup |= changed[j] == x;
+    if (dup || rBroker[x] != b || !selects(s, x)) continue;
+    const uint64_t kx = replicaKey(s, x);
+    auto at = std::lower_bound(out.begin(), out.end(), x, [&](int y, int) {
+      const uint64_t ky = replicaKey(s, y);
+      return ky != kx ? ky < kx : y < x;
+    });
+    out.insert(at, x);
+  }
+  return true;
+}
+
 std::shared_ptr<const std::vector<int32_t>> Model::snapshot(int b, const Spec& s) {
   const bool limited = s.selAboveRes >= 0 || s.selBelowRes >= 0;
   auto& cache = limited ? filteredCache[b] : sortedCache[b];
@@ -840,14 +886,21 @@ std::shared_ptr<const std::vector<int32_t>> Model::snapshot(int b, const Spec& s
           (s.selBelowRes < 0 || ru(r, s.selBelowRes) < s.belowLimit))
         v->push_back(r);
   } else {
-    PhaseScope ps(PH_SORTED_INIT);
-    std::vector<std::pair<uint64_t, int32_t>>& keyed = snapKeys_;
-    keyed.clear();
-    for (int r : bRepl[b])
-      if (selects(s, r)) keyed.push_back({replicaKey(s, r), r});
-    std::sort(keyed.begin(), keyed.end());
-    v->reserve(keyed.size());
-    for (const auto& kr : keyed) v->push_back(kr.second);
+    const bool derived = snapshotFromPrevious(b, s, cache, *v);
+    static const bool check = std::getenv("CCMI_SNAPSHOT_CHECK") != nullptr;  // tests: derived == re-sorted
+    if (!derived || check) {
+      PhaseScope ps(PH_SORTED_INIT);
+      std::vector<std::pair<uint64_t, int32_t>>& keyed = snapKeys_;
+      keyed.clear();
+      for (int r : bRepl[b])
+        if (selects(s, r)) keyed.push_back({replicaKey(s, r), r});
+      std::sort(keyed.begin(), keyed.end());
+      std::vector<int32_t> full;
+      full.reserve(keyed.size());
+      for (const auto& kr : keyed) full.push_back(kr.second);
+      if (derived && full != *v) throw std::logic_error("snapshot derived from the previous version differs");
+      *v = std::move(full);
+    }
   }
   cachePut(cache, bVer[b], s, v);
   return v;

@@ -300,6 +300,15 @@ class Model {
     std::shared_ptr<const std::vector<int32_t>> v;
   };
   std::vector<uint32_t> bVer;
+  // The replica whose membership or sort key changed at each of a broker's last kDeltaLog version bumps (-1: none),
+  // so a snapshot can be derived from the previous version's instead of re-sorting the broker.
+  static constexpr size_t kDeltaLog = 8;
+  std::vector<std::vector<std::pair<uint32_t, int32_t>>> bDelta;
+  void noteDelta(int b, int r) {
+    auto& d = bDelta[b];
+    if (d.size() == kDeltaLog) d.erase(d.begin());
+    d.push_back({bVer[b], r});
+  }
   std::vector<std::vector<SortedCacheEntry>> sortedCache;    // per broker, a few limit-free Specs
   std::vector<std::vector<SortedCacheEntry>> filteredCache;  // per broker, a few Specs with a utilization limit
   // OptimizationOptions.excludedTopics as the selection function sees it ([T] flags); setting a different set
@@ -318,6 +327,7 @@ class Model {
   // Contents a SortedReplicas(b, s) initialised now would have (shared with the initialisation cache): equal to
   // the live view of a set tracked earlier, because every key change re-inserts the replica.
   std::shared_ptr<const std::vector<int32_t>> snapshot(int b, const Spec& s);
+  bool snapshotFromPrevious(int b, const Spec& s, std::vector<SortedCacheEntry>& cache, std::vector<int32_t>& out);
   // One Spec's snapshots of every broker, looked up by broker id and version (no per-call cache search or
   // reference counting): the drivers that poll many brokers per scan (moveIn, swap) keep one per Spec.
   struct SnapTable {
