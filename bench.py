@@ -273,6 +273,7 @@ def main() -> None:
     ap.add_argument("--steps", type=int, default=2)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-launch-pass", action="store_true", help="skip the instrumented scan-server-off proposal")
     ap.add_argument("--cpu-sample-seconds", type=float, default=25.0)
     ap.add_argument("--what-if-procs", type=int, default=16)
     ap.add_argument("--workload", choices=sorted(WORKLOADS), default="c2")
@@ -320,8 +321,8 @@ def main() -> None:
             s.attach_rccl(rank, world, uid)
         return s
 
-    # Warmup proposals double as the instrumented pass: HIP events around every scan kernel on the engine stream
-    # (outside the timed region).
+    # Warmup proposals double as the instrumented pass: HIP events around every launched scan kernel and the scan
+    # server's in-kernel busy time per command (outside the timed region).
     inst_perf = inst_cands = None
     for w in range(max(1, args.warmup)):
         ws = session()
@@ -330,6 +331,20 @@ def main() -> None:
         r = opt.optimizations(ws, goals, options)
         inst_perf, inst_cands = ws.perf(), r.candidates
         del ws
+    # One more instrumented proposal with the scan server off (a launch per scan): the per-launch kernel times the
+    # rocprofv3 trace of the same path can be checked against (rank 0, single GPU, outside the timed region).
+    launch_perf = None
+    if world == 1 and not args.no_launch_pass and args.workload != "c4":
+        os.environ["CCMI_SERVER"] = "0"
+        try:
+            ls = session()
+        finally:
+            del os.environ["CCMI_SERVER"]
+        ls.set_kernel_timing(True)
+        ls.reset_perf()
+        opt.optimizations(ls, goals, options)
+        launch_perf = ls.perf()
+        del ls
 
     S = max(1, args.requests_per_gpu) if not sharded else 1
     # cluster resident in HBM before timing starts: one session per proposal
@@ -373,11 +388,18 @@ def main() -> None:
         launches = max(1, perf.intra_launches)
         scan_avg_ms = perf.intra_kernel_ms / launches
         required_bytes_per_launch = perf.intra_bytes / launches
+    elif perf.server_scans > 0:
+        # K8 scan_server: one resident launch serves the cross / pair / segment scans; its unit of work is a command
+        # and its time per command is measured inside the kernel (s_memrealtime, command seen -> result published)
+        launches = max(1, perf.server_scans)
+        scan_avg_ms = perf.server_busy_ms / launches
+        required_bytes_per_launch = perf.server_required * BYTES_PER_CANDIDATE / launches
     else:
         launches = max(1, perf.scan_launches)
         scan_avg_ms = perf.scan_kernel_ms / launches
         required_bytes_per_launch = perf.scan_required * BYTES_PER_CANDIDATE / launches
     achieved = required_bytes_per_launch / (scan_avg_ms * 1e-3) / 1e9 if scan_avg_ms > 0 else 0.0
+    server = perf.server_scans > 0 and not intra
 
     if rank != 0:
         dist.destroy_process_group()
@@ -417,9 +439,16 @@ def main() -> None:
                      "traffic_source": traffic_src,
                      "kernel": ("K6 intra_brokers (one thread per broker; algorithmic bytes = 17 B per disk + 29 B per "
                                 "replica entry read once)" if intra else
+                                "K8 scan_server (persistent; per command: in-kernel busy time, the command's required "
+                                "candidates x 96 B)" if server else
                                 "candidate scans (scan_cross/scan_pairs/scan_swap/chain_pairs/chain_rack_rows)"),
                      "avg_launch_us": scan_avg_ms * 1e3,
+                     "avg_unit": "per server command" if server else "per launch",
                      "launches_per_step": perf.intra_launches if intra else perf.scan_launches,
+                     "server_launches_per_step": perf.server_launches,
+                     "server_commands_per_step": perf.server_scans,
+                     "server_payload_bytes_per_step": perf.server_payload_bytes,
+                     "device_evaluated_candidates_per_s": perf.scan_required / (elapsed / args.steps),
                      "chain_launches_per_step": perf.chain_launches,
                      "algorithmic_bytes_per_launch": required_bytes_per_launch,
                      "required_candidates_per_step": perf.scan_required,
@@ -427,7 +456,13 @@ def main() -> None:
                      "stats_avg_launch_us": perf.stats_kernel_ms * 1e3 / max(1, perf.stats_launches),
                      "stats_bytes_per_launch": perf.stats_bytes / max(1, perf.stats_launches),
                      "host_syncs_per_step": perf.host_syncs,
-                     "scan_cross": scan_cross_line(perf, args.workload)},
+                     "scan_cross": scan_cross_line(launch_perf or perf, args.workload),
+                     "launch_path": None if launch_perf is None else {
+                         "scan_launches": launch_perf.scan_launches,
+                         "avg_scan_launch_us": launch_perf.scan_kernel_ms * 1e3 / max(1, launch_perf.scan_launches),
+                         "achieved_gbs": (launch_perf.scan_required * BYTES_PER_CANDIDATE / max(1, launch_perf.scan_launches))
+                                         / max(1e-12, launch_perf.scan_kernel_ms * 1e-3 / max(1, launch_perf.scan_launches)) / 1e9,
+                         "note": "the same proposal with CCMI_SERVER=0 (one launch per scan), HIP events per launch"}},
         "cpu_baseline": None,
     }
     if world == 1 and not args.no_cpu_baseline:

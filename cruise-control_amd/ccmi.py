@@ -49,6 +49,7 @@ GOAL_KINDS: Dict[str, int] = {
     "PreferredLeaderElectionGoal": 18,
     "RackAwareDistributionGoal": 19,
     "BrokerSetAwareGoal": 20,
+    "TopicLeaderReplicaDistributionGoal": 21,
 }
 GOAL_NAMES = {v: k for k, v in GOAL_KINDS.items()}
 # default.goals in priority order (config/constants/AnalyzerConfig.java:352-367, TestConstants.DEFAULT_GOALS_VALUES)
@@ -65,7 +66,7 @@ C1_GOALS = ("ReplicaDistributionGoal", "DiskUsageDistributionGoal", "NetworkInbo
 INTRA_BROKER_GOALS = ("IntraBrokerDiskCapacityGoal", "IntraBrokerDiskUsageDistributionGoal")
 # Goals whose drivers are implemented in this build.
 IMPLEMENTED = DEFAULT_GOALS + INTRA_BROKER_GOALS + ("PreferredLeaderElectionGoal", "RackAwareDistributionGoal",
-                                                   "BrokerSetAwareGoal")
+                                                   "BrokerSetAwareGoal", "TopicLeaderReplicaDistributionGoal")
 # replica.to.broker.set.mapping.policy.class values (include/ccmi.h ccmi_broker_set_policy)
 BROKER_SET_POLICIES = {"TopicNameHashBrokerSetMappingPolicy": 0, "ReplicaToOriginalBrokerSetMappingPolicy": 1}
 
@@ -105,7 +106,10 @@ class ConstraintStruct(C.Structure):
                 ("num_broker_sets", C.c_int32), ("broker_set_policy", C.c_int32),
                 ("broker_set_names", C.POINTER(C.c_char_p)), ("broker_set_offset", C.POINTER(C.c_int32)),
                 ("broker_set_members", C.POINTER(C.c_int32)), ("min_leader_topics", C.POINTER(C.c_int32)),
-                ("num_min_leader_topics", C.c_int32), ("min_topic_leaders_per_broker", C.c_int32)]
+                ("num_min_leader_topics", C.c_int32), ("min_topic_leaders_per_broker", C.c_int32),
+                ("topic_leader_replica_balance_percentage", C.c_double),
+                ("topic_leader_replica_balance_min_gap", C.c_int32), ("topic_leader_replica_balance_max_gap", C.c_int32),
+                ("topic_leader_replica_balance_margin", C.c_double)]
 
 
 class OptionsStruct(C.Structure):
@@ -204,7 +208,7 @@ class DeviceError(CruiseControlError):
 _STATUS = {1: IllegalArgumentException, 2: DeviceError, 3: OptimizationFailureException, 4: IllegalStateException,
            5: UnsupportedOperationException}
 
-ABI_VERSION = 6  # CCMI_ABI_VERSION of include/ccmi.h
+ABI_VERSION = 7  # CCMI_ABI_VERSION of include/ccmi.h
 EXPORTED_SYMBOLS = (
     "ccmi_last_error", "ccmi_abi_version", "ccmi_default_constraint", "ccmi_default_random_cluster_props",
     "ccmi_random_cluster", "ccmi_cluster_buffers_desc", "ccmi_cluster_buffers_free", "ccmi_session_create",
@@ -324,6 +328,12 @@ class BalancingConstraint:
     # Utils.getTopicNamesMatchedWithPattern does (Pattern.matcher(topic).matches() = re.fullmatch; common/Utils.java:26-36).
     topics_with_min_leaders_per_broker: str = ""
     min_topic_leaders_per_broker: int = 1
+    # TopicLeaderReplicaDistributionGoal: topic.leader.replica.count.balance.{threshold,min.gap,max.gap} and
+    # topic.leader.replica.distribution.goal.balance.margin (AnalyzerConfig.java:112-146)
+    topic_leader_replica_balance_percentage: float = 1.10
+    topic_leader_replica_balance_min_gap: int = 2
+    topic_leader_replica_balance_max_gap: int = 10
+    topic_leader_replica_balance_margin: float = 0.9
 
     def set_resource_balance_percentage(self, p: float) -> None:  # BalancingConstraint.setResourceBalancePercentage
         self.resource_balance_percentage = (p, p, p, p)
@@ -356,6 +366,10 @@ class BalancingConstraint:
         s.overprovisioned_max_replicas_per_broker = 1500
         s.overprovisioned_min_brokers = 3
         s.overprovisioned_min_extra_racks = self.overprovisioned_min_extra_racks
+        s.topic_leader_replica_balance_percentage = self.topic_leader_replica_balance_percentage
+        s.topic_leader_replica_balance_min_gap = self.topic_leader_replica_balance_min_gap
+        s.topic_leader_replica_balance_max_gap = self.topic_leader_replica_balance_max_gap
+        s.topic_leader_replica_balance_margin = self.topic_leader_replica_balance_margin
         if self.broker_sets:
             names = list(self.broker_sets)
             members = [int(b) for n in names for b in self.broker_sets[n]]

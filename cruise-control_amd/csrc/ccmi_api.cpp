@@ -87,6 +87,10 @@ void setOptions(ccmi_session* s, const ccmi_balancing_constraint* c, const ccmi_
   e.bc.topicReplicaBalance = c->topic_replica_balance_percentage;
   e.bc.topicMinGap = c->topic_replica_balance_min_gap;
   e.bc.topicMaxGap = c->topic_replica_balance_max_gap;
+  e.bc.topicLeaderBalance = c->topic_leader_replica_balance_percentage;
+  e.bc.topicLeaderMinGap = c->topic_leader_replica_balance_min_gap;
+  e.bc.topicLeaderMaxGap = c->topic_leader_replica_balance_max_gap;
+  e.bc.topicLeaderMargin = c->topic_leader_replica_balance_margin;
   e.bc.maxReplicasPerBroker = c->max_replicas_per_broker;
   e.bc.overMaxReplicasPerBroker = c->overprovisioned_max_replicas_per_broker;
   e.bc.overMinBrokers = c->overprovisioned_min_brokers;
@@ -264,6 +268,10 @@ void ccmi_default_constraint(ccmi_balancing_constraint* c) {
   c->overprovisioned_min_brokers = 3;
   c->overprovisioned_min_extra_racks = 2;
   c->min_topic_leaders_per_broker = 1;  // AnalyzerConfig.DEFAULT_MIN_TOPIC_LEADERS_PER_BROKER
+  c->topic_leader_replica_balance_percentage = 1.10;  // AnalyzerConfig.java:112-146
+  c->topic_leader_replica_balance_min_gap = 2;
+  c->topic_leader_replica_balance_max_gap = 10;
+  c->topic_leader_replica_balance_margin = 0.9;
 }
 
 void ccmi_default_random_cluster_props(ccmi_random_cluster_props* p) {

@@ -183,7 +183,7 @@ Device::~Device() {
   }
   void* ps[] = {brokers_, replicas_, parts_, allowedAlive_, topicCount_, topicNrep_, topicScratch_, statsOut_,
                 statsPart_, dReq_, rowVisited_, dResult_, dDone_, tUpper_, tLower_, dRLoad_, dBLoad_, dBLnw_, dBPot_, dPOff_, dPSlots_,
-                dPLeader_, dChainLog_, dChainOut_, pIneligOff_, pIneligB_, topicLead_, tMinLead_};
+                dPLeader_, dChainLog_, dChainOut_, pIneligOff_, pIneligB_, topicLead_, tMinLead_, tLeadLim_};
   for (void* p : ps)
     if (p) (void)hipFree(p);
   for (void* p : intraAllocs_)
@@ -406,6 +406,7 @@ DevTables Device::tables() const {
   t.pIneligB = pIneligB_;
   t.topicLead = topicLead_;
   t.tMinLead = tMinLead_;
+  t.tLeadLim = tLeadLim_;
   t.B = B_;
   t.R = R_;
   t.P = P_;
@@ -535,6 +536,13 @@ void Device::setMinLeaders(const int32_t* tMin) {
   stopServer();
   if (!tMinLead_) dalloc(&tMinLead_, (size_t)T_);
   hipCheck(hipMemcpy(tMinLead_, tMin, sizeof(int32_t) * (size_t)T_, hipMemcpyHostToDevice), "upload tMinLead");
+}
+
+void Device::setTopicLeadLimits(const int32_t* lim) {
+  DeviceGuard dg(ordinal_);
+  stopServer();
+  if (!tLeadLim_) dalloc(&tLeadLim_, 2 * (size_t)T_);
+  hipCheck(hipMemcpy(tLeadLim_, lim, sizeof(int32_t) * 2 * (size_t)T_, hipMemcpyHostToDevice), "upload tLeadLim");
 }
 
 void Device::setBrokerSets(const int32_t* brokerSet, const int32_t* replicaSet) {

@@ -117,6 +117,8 @@ class Device {
   // kind 1 and the chain kernels update them); MinTopicLeadersPerBrokerGoal's minimum per topic [T] (-1 = not its topic)
   void enableTopicLeaders(const int32_t* topicLeadDense);
   void setMinLeaders(const int32_t* tMin);
+  // TopicLeaderReplicaDistributionGoal's (upper, lower) leader limits per topic [T][2] (frozen at its initGoalState)
+  void setTopicLeadLimits(const int32_t* lim);
 
   // pending row updates (flushed with the next launch)
   std::vector<BrokerRow> brows;
@@ -188,7 +190,7 @@ class Device {
   PartitionRec* parts_ = nullptr;
   int32_t *topicCount_ = nullptr, *topicNrep_ = nullptr, *tUpper_ = nullptr, *tLower_ = nullptr;
   int32_t *pIneligOff_ = nullptr, *pIneligB_ = nullptr;
-  int32_t *topicLead_ = nullptr, *tMinLead_ = nullptr;
+  int32_t *topicLead_ = nullptr, *tMinLead_ = nullptr, *tLeadLim_ = nullptr;
   uint8_t* allowedAlive_ = nullptr;
   std::vector<BrokerRec> hBrokers_;
   std::vector<PartitionRec> hParts_;

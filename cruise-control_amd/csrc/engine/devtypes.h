@@ -43,14 +43,18 @@ enum DevGoalKind : int32_t {
   DG_LEADER_BYTES_IN = 9,
   DG_RACK_AWARE_DISTRIBUTION = 10,
   DG_BROKER_SET_AWARE = 11,
-  DG_MIN_TOPIC_LEADERS = 12  // MinTopicLeadersPerBrokerGoal with configured topics
+  DG_MIN_TOPIC_LEADERS = 12,  // MinTopicLeadersPerBrokerGoal with configured topics
+  DG_TOPIC_LEADER_DISTRIBUTION = 13  // TopicLeaderReplicaDistributionGoal
 };
 // ReplicaRec.bset flag of a replica of one of MinTopicLeadersPerBrokerGoal's topics: BrokerSetAwareGoal accepts every
 // action on such a replica (BrokerSetAwareGoal.java:258-264) and leaves it out of its own moves (:136-151). Broker set
 // indices stay below the flag; a negative bset is "none".
 constexpr int32_t kBsetMust = 1 << 24;
 // Operands a program's predicates read beyond the base broker/replica/partition record (DevProgram.needs).
-enum DevNeed : uint32_t { NEED_RACK = 1, NEED_POT = 2, NEED_LEAD = 4, NEED_LBI = 8, NEED_TOPIC = 16, NEED_TLEAD = 32 };
+enum DevNeed : uint32_t {
+  NEED_RACK = 1, NEED_POT = 2, NEED_LEAD = 4, NEED_LBI = 8, NEED_TOPIC = 16, NEED_TLEAD = 32,
+  NEED_TLLIM = 64  // TopicLeaderReplicaDistributionGoal's per-topic leader limits (with NEED_TLEAD)
+};
 // Candidate filters applied inside a CROSS scan before the predicate conjunction (the reference builds these
 // candidate lists per replica; the kernel skips the excluded destinations instead).
 enum DevFilter : int32_t {
@@ -137,6 +141,9 @@ struct DevTables {
   // minimum per topic [T] (-1: not one of its topics; null when the goal has no topics)
   const int32_t* topicLead;
   const int32_t* tMinLead;
+  // TopicLeaderReplicaDistributionGoal's _balanceUpperLimitByTopic / _balanceLowerLimitByTopic as [T][2] (upper,
+  // lower) pairs, one 8-byte load per row; null until the goal runs
+  const int32_t* tLeadLim;
   int32_t B, R, P, ldB;
 };
 

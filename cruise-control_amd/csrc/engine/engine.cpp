@@ -39,6 +39,7 @@ struct HostView {
   const std::vector<int32_t>& bSet;  // BrokerSetAwareGoal: broker set of every broker / replica (empty: none)
   const std::vector<int32_t>& rSet;
   const std::vector<int32_t>& tMin;  // MinTopicLeadersPerBrokerGoal minima (empty: none)
+  const std::vector<int32_t>& tLim;  // TopicLeaderReplicaDistributionGoal limits [T][2] (empty: none)
   double bu(int b, int res) const { return m.bu(b, res); }
   double bcap(int b, int res) const { return m.cap(b, res); }
   int nrep(int b) const { return m.nrep(b); }
@@ -83,6 +84,8 @@ struct HostView {
   int rbset(int r) const { return rSet.empty() ? -1 : rSet[r]; }
   int tlead(int t, int b) const { return m.tlead(t, b); }
   int tMinLead(int t) const { return tMin.empty() ? -1 : tMin[t]; }
+  int tLeadUpper(int t) const { return tLim[2 * t]; }
+  int tLeadLower(int t) const { return tLim[2 * t + 1]; }
 };
 
 uint32_t needsOf(const DevGoal& g) {
@@ -94,6 +97,7 @@ uint32_t needsOf(const DevGoal& g) {
     case DG_LEADER_REPLICA_DISTRIBUTION: return NEED_LEAD;
     case DG_LEADER_BYTES_IN: return NEED_LBI;
     case DG_MIN_TOPIC_LEADERS: return NEED_TLEAD;
+    case DG_TOPIC_LEADER_DISTRIBUTION: return NEED_TLEAD | NEED_TLLIM;
     default: return 0;
   }
 }
@@ -159,6 +163,21 @@ void Engine::eligible(const std::vector<int32_t>& in, int action, std::vector<in
     }
     out.push_back(b);
   }
+}
+
+int64_t Engine::visitCount(int action, int r, const int32_t* cands, size_t n, bool skipHosts) const {
+  DevProgram prog;
+  std::memset(&prog, 0, sizeof(prog));
+  prog.exclLeadMove = (opt.anyExclLead && !opt.anyRequested && action == DA_MOVE) ? 1 : 0;
+  prog.newOnly = (m.numNew > 0 && !opt.anyRequested) ? 1 : 0;
+  if (!skipHosts && !prog.exclLeadMove && !prog.newOnly) return (int64_t)n;
+  const int p = m.rPart[r];
+  int64_t c = 0;
+  for (size_t q = 0; q < n; ++q) {
+    if (skipHosts && m.replicaOn(p, cands[q]) >= 0) continue;
+    c += blocked(prog, r, cands[q]) ? 0 : 1;
+  }
+  return c;
 }
 
 // Reference-equivalent candidates of a cross scan whose rows skip replica-dependent ineligible brokers (blocked):
@@ -382,7 +401,7 @@ int Engine::acceptance(int gi, const ccmi_action& a) {
   }
   std::vector<const std::vector<uint8_t>*> allowedBySlot;
   for (auto& g : optimized) allowedBySlot.push_back(&g->allowed);
-  HostView v{m, allowedBySlot, topicUpper, topicLower, brokerSetOf, replicaSetOf, minLeadOf};
+  HostView v{m, allowedBySlot, topicUpper, topicLower, brokerSetOf, replicaSetOf, minLeadOf, topicLeadLim};
   const GoalImpl& g = *optimized.at(gi);
   const int sr = m.replicaOn(a.partition, a.source_broker);
   if (sr < 0) throw std::invalid_argument("no replica of the partition on the source broker");

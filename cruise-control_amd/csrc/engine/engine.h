@@ -40,6 +40,10 @@ struct Constraint {  // BalancingConstraint
   double replicaBalance, goalViolationMultiplier;
   double leaderReplicaBalance, topicReplicaBalance;
   int32_t topicMinGap, topicMaxGap;
+  // TopicLeaderReplicaDistributionGoal: topic.leader.replica.count.balance.{threshold,min.gap,max.gap} and
+  // topic.leader.replica.distribution.goal.balance.margin
+  double topicLeaderBalance = 1.10, topicLeaderMargin = 0.9;
+  int32_t topicLeaderMinGap = 2, topicLeaderMaxGap = 10;
   int64_t maxReplicasPerBroker;
   int64_t overMaxReplicasPerBroker;   // overprovisioned.max.replicas.per.broker
   int32_t overMinBrokers;             // overprovisioned.min.brokers
@@ -97,6 +101,7 @@ class Engine {
   BrokerSets brokerSets;                        // BalancingConstraint broker sets of the current call
   std::vector<int32_t> brokerSetOf, replicaSetOf;  // BrokerSetAwareGoal state (device copy: setBrokerSets)
   std::vector<int32_t> minLeadOf;  // MinTopicLeadersPerBrokerGoal's minimum per topic, -1 = not its topic (setMinLeaders)
+  std::vector<int32_t> topicLeadLim;  // TopicLeaderReplicaDistributionGoal (upper, lower) per topic (setTopicLeadLimits)
 
   // one Goal.optimize; throws OptimizationFailure / StateError
   bool optimizeGoal(std::unique_ptr<GoalImpl> g, ccmi_goal_result* res);
@@ -123,6 +128,10 @@ class Engine {
   int64_t swapScan(GoalImpl& self, const std::vector<int32_t>& srcs, const std::vector<int32_t>& cbOff,
                    const std::vector<int32_t>& cbRep);
   void eligible(const std::vector<int32_t>& in, int action, std::vector<int32_t>& out) const;
+  // Reference-visited candidates of replica r over cands[0, n) (eligible lists): the entries the replica-dependent
+  // filters of GoalUtils.eligibleBrokers keep (blocked), skipping brokers that host r's partition when
+  // `skipHosts` (candidate lists the device scans whole while the reference's list leaves the hosts out).
+  int64_t visitCount(int action, int r, const int32_t* cands, size_t n, bool skipHosts = false) const;
 
   double threshold(double avgPct, int res, bool lower) const;  // GoalUtils.computeResourceUtilizationBalanceThreshold
 

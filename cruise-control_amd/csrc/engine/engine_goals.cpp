@@ -17,10 +17,13 @@
 //                                           ReplicaDistributionAbstractGoal.java:60-160
 //   LeaderBytesInDistributionGoal           analyzer/goals/LeaderBytesInDistributionGoal.java:142-271
 //   BrokerSetAwareGoal                      analyzer/goals/BrokerSetAwareGoal.java:80-275 (not in default.goals)
+//   TopicLeaderReplicaDistributionGoal      analyzer/goals/TopicLeaderReplicaDistributionGoal.java:298-778 (in goals,
+//                                           not in default.goals)
 //   GoalUtils.ensureNoOfflineReplicas       analyzer/goals/GoalUtils.java:307-318
 #include <algorithm>
 #include <cmath>
 #include <set>
+#include <unordered_map>
 
 #include "device.h"
 #include "engine.h"
@@ -1264,6 +1267,406 @@ class TopicReplicaDistribution : public GoalImpl {
   }
 };
 
+// ======================================================================================= TopicLeaderReplicaDistributionGoal
+// Per-topic leader counts (Broker.numLeadersFor) live in the model and on the device (Model::enableTopicLeaders);
+// the goal's per-topic limits go to the device as (upper, lower) pairs.
+class TopicLeaderReplicaDistribution : public GoalImpl {
+ public:
+  TopicLeaderReplicaDistribution() {
+    kind = CCMI_GOAL_TOPIC_LEADER_REPLICA_DISTRIBUTION;
+    name = "TopicLeaderReplicaDistributionGoal";
+  }
+  bool fix = false, anyAbove = false, anyUnder = false;
+  std::vector<uint8_t> rebalanceTopic;  // the keys of _avgTopicLeaderReplicasOnAliveBroker (topicsToRebalance)
+  std::vector<int32_t> upper, lower;
+  Model::Spec specAlive, specDead;  // selection functions of the tracked leaders-only view (alive / dead broker)
+  bool excluded(int b) const { return !allowed[b]; }
+  const Model::Spec& spec(const Model& m, int b) const { return m.alive(b) ? specAlive : specDead; }
+
+  // initGoalState (:298-347) with the limits of balancePercentageWithMargin / clampLower / clampUpper (:101-168); an
+  // empty _brokersAllowedReplicaMove is allowed (leadership-only balancing): the average is then x / 0.0
+  void init(Engine& e) override {
+    Model& m = e.m;
+    const int n = allowedForReplicaMove(e, allowed);
+    const bool selfHealing = m.numSelfHealing > 0;
+    rebalanceTopic.assign(m.T, selfHealing ? 0 : 1);
+    if (selfHealing)
+      for (int r = 0; r < m.R; ++r)
+        if (m.selfHealing[r]) rebalanceTopic[m.pTopic[m.rPart[r]]] = 1;
+    if (!selfHealing && e.opt.anyExclTopic)  // GoalUtils.topicsToRebalance (GoalUtils.java:439-452)
+      for (int t = 0; t < m.T; ++t)
+        if (e.opt.exclTopic[t]) rebalanceTopic[t] = 0;
+    double pct = e.bc.topicLeaderBalance;
+    if (e.opt.triggered) pct *= e.bc.goalViolationMultiplier;
+    const double margin = (pct - 1) * e.bc.topicLeaderMargin;
+    std::vector<int32_t> leaders(m.T, 0);  // ClusterModel.numLeadersPerTopic: one leader per partition
+    for (int p = 0; p < m.P; ++p) leaders[m.pTopic[p]]++;
+    const int32_t minGap = e.bc.topicLeaderMinGap, maxGap = e.bc.topicLeaderMaxGap;
+    upper.assign(m.T, 0);
+    lower.assign(m.T, 0);
+    e.topicLeadLim.assign(2 * (size_t)m.T, 0);
+    for (int t = 0; t < m.T; ++t) {
+      const double avg = leaders[t] / (double)n;
+      const int32_t ceilAvg = jD2I(std::ceil(avg)), floorAvg = jD2I(std::floor(avg));
+      const int32_t cu = jD2I(std::ceil(avg * (1 + margin)));
+      upper[t] = std::max(jAddI(ceilAvg, minGap), std::min(cu, jAddI(ceilAvg, maxGap)));
+      const int32_t cl = jD2I(std::floor(avg * jmax(0, (1 - margin))));
+      lower[t] = std::max(std::max(0, jSubI(floorAvg, maxGap)), std::min(cl, std::max(0, jSubI(floorAvg, minGap))));
+      e.topicLeadLim[2 * (size_t)t] = upper[t];
+      e.topicLeadLim[2 * (size_t)t + 1] = lower[t];
+    }
+    specAlive = Model::Spec{};
+    specAlive.selLeaders = true;
+    specAlive.selImmigrants = e.opt.onlyImmigrants;
+    specAlive.selExclTopics = e.opt.anyExclTopic;
+    specDead = specAlive;
+    specAlive.selImmOrOffline = selfHealing;
+    fix = false;
+    m.enableTopicLeaders();
+    e.dev->setTopicLeadLimits(e.topicLeadLim.data());
+    dg = DevGoal{};
+    dg.kind = DG_TOPIC_LEADER_DISTRIBUTION;
+    dg.allowedSlot = (int)e.optimized.size();
+  }
+
+  // updateGoalState (:382-424)
+  void update(Engine& e) override {
+    if (anyAbove || anyUnder) succeeded = false;
+    anyAbove = anyUnder = false;
+    Model& m = e.m;
+    for (int r = 0; r < m.R; ++r)
+      if (m.selfHealing[r] && m.curOffline(r)) {
+        if (fix)
+          throw OptimizationFailure("[" + name + "] Cannot remove replica from broker " + std::to_string(m.bId[m.rBroker[r]]),
+                                    underBrokers(1));
+        fix = true;
+        dg.fixOffline = 1;
+        return;
+      }
+    ensureReplicasMoveOffBadDisks(m, name);
+    finished = true;
+  }
+  // GoalUtils.HardGoalStatsComparator (:269-272)
+  int compareStats(const ccmi_cluster_stats&, const ccmi_cluster_stats&) const override { return 0; }
+
+  // rebalanceForBroker (:518-583) + skipBrokerRebalance and its helpers (:426-504)
+  void rebalance(Engine& e, int b) override {
+    PhaseScope ps(PH_OTHER_GOALS);
+    Model& m = e.m;
+    std::vector<int32_t> topics;
+    m.bTopicKeys[b].order(topics);  // Broker.topics(): HashMap key order
+    // per topic: the tracked view's leaders, their offline count, whether one is an immigrant (recounted after moves)
+    struct Count {
+      int n = 0, off = 0;
+      bool imm = false;
+    };
+    std::unordered_map<int, Count> per;
+    auto recount = [&]() {
+      per.clear();
+      const Model::Spec& s = spec(m, b);
+      for (int r : m.bRepl[b]) {
+        if (!m.rLeader[r] || !m.selects(s, r)) continue;
+        Count& c = per[m.pTopic[m.rPart[r]]];
+        c.n++;
+        c.off += m.rInOff[r] ? 1 : 0;
+        c.imm |= m.rInImm[r] != 0;
+      }
+    };
+    recount();
+    for (int t : topics) {
+      if (!rebalanceTopic[t]) continue;
+      const auto it = per.find(t);
+      const Count c = it == per.end() ? Count{} : it->second;
+      const bool excl = excluded(b);
+      const bool requireLess = c.off > 0 || c.n > upper[t] || excl;
+      const bool requireMore = !excl && m.alive(b) && c.n - c.off < lower[t];
+      if (m.alive(b) && !requireMore && !requireLess) continue;
+      if (m.numNew > 0 && !m.isNew(b) && !requireLess) continue;
+      if (m.numSelfHealing > 0 && requireLess && c.off == 0 && !c.imm) continue;
+      if (e.opt.onlyImmigrants && requireLess && !c.imm) continue;
+      if (requireLess && moveOut(e, b, t)) anyAbove = true;
+      if (requireMore && moveIn(e, b, t)) anyUnder = true;
+      recount();
+    }
+  }
+
+  // replicasToMoveOut (:591-596): the topic's leaders of b that the tracked view selects, ordered by
+  // Broker.replicaComparator (offline first, immigrants first, partition number)
+  void replicasToMoveOut(const Model& m, int b, int t, std::vector<int32_t>& out) const {
+    out.clear();
+    const Model::Spec& s = spec(m, b);
+    for (int r : m.bRepl[b])
+      if (m.rLeader[r] && m.pTopic[m.rPart[r]] == t && m.selects(s, r)) out.push_back(r);
+    std::sort(out.begin(), out.end(), [&](int x, int y) {
+      const bool ox = m.rInOff[x] != 0, oy = m.rInOff[y] != 0;
+      if (ox != oy) return ox;
+      const bool ix = m.rInImm[x] != 0, iy = m.rInImm[y] != 0;
+      if (ix != iy) return ix;
+      return m.pNumber[m.rPart[x]] < m.pNumber[m.rPart[y]];
+    });
+  }
+
+  // rebalanceByMovingLeadersOut (:598-678). Every leader first tries a leadership transfer to the candidates
+  // hosting a follower, then a replica move to the candidates not hosting the partition, each over a HashSet built
+  // from the candidate TreeSet. Rows of one offline-status run are scanned together: one pair scan over all rows'
+  // leadership candidates, then cross scans of the rows before the first leadership winner; a replica-move list is
+  // the ascending-id list of all candidates (the device rejects the hosts) whenever the row's HashSet has no bucket
+  // collisions, else the row's own HashSet order.
+  bool moveOut(Engine& e, int b, int t) {
+    Model& m = e.m;
+    auto cmp = [&m, t](int x, int y) {
+      int c = jcmpInt(m.tlead(t, x), m.tlead(t, y));
+      if (c == 0) c = jcmpInt(m.bNlead[x], m.bNlead[y]);
+      return c ? c : jcmpInt(m.bId[x], m.bId[y]);
+    };
+    RbTreeSet<decltype(cmp)> cand(cmp);
+    {
+      PhaseScope pi(PH_PQ_INIT);
+      std::vector<int> ins, order;
+      for (int x = 0; x < m.B; ++x)
+        if (m.alive(x) && (fix || m.tlead(t, x) < upper[t])) ins.push_back(x);
+      if (fix) order = ins;  // ClusterModel.aliveBrokers(): ascending id
+      else javaHashSetOrder(ins, order);  // Collectors.toSet()
+      // the same TreeSet.add sequence, placed by rank (the comparator is a total order on these brokers)
+      std::vector<int32_t> byKey(ins.begin(), ins.end()), rank(m.B, 0);
+      std::sort(byKey.begin(), byKey.end(), [&](int x, int y) { return cmp(x, y) < 0; });
+      for (size_t i = 0; i < byKey.size(); ++i) rank[byKey[i]] = (int32_t)i;
+      cand.buildByRank(order, rank);
+    }
+    int n = 0, nOff = 0;
+    for (int r : m.bRepl[b])
+      if (m.rLeader[r] && m.pTopic[m.rPart[r]] == t) {
+        n++;
+        nOff += m.rInOff[r] ? 1 : 0;
+      }
+    const int upperSrc = upper[t];
+    std::vector<int32_t> list;
+    replicasToMoveOut(m, b, t, list);
+    bool wasUnable = false;
+    std::vector<int> inorder, ins, hs;
+    std::vector<int32_t> pos(m.B, -1), pr, pb, leadOff, ids, idElig, own, hs32;
+    size_t i = 0;
+    while (i < list.size()) {
+      if (wasUnable && !m.curOffline(list[i]) && n <= upperSrc) return false;
+      const bool runOffline = m.curOffline(list[i]);
+      size_t end = i;
+      while (end < list.size() && m.curOffline(list[end]) == runOffline) ++end;
+      for (int x : inorder) pos[x] = -1;
+      cand.inorder(inorder);
+      for (size_t q = 0; q < inorder.size(); ++q) pos[inorder[q]] = (int32_t)q;
+      // the candidates hosting one of the row's partition's replicas, in TreeSet order
+      auto hostsInOrder = [&](int r, bool followersOnly, std::vector<int>& out) {
+        out.clear();
+        const int p = m.rPart[r];
+        for (int s = m.pOff[p]; s < m.pOff[p + 1]; ++s) {
+          const int rr = m.pSlots[s], x = m.rBroker[rr];
+          if (pos[x] >= 0 && !(followersOnly && m.rLeader[rr])) out.push_back(x);
+        }
+        std::sort(out.begin(), out.end(), [&](int x, int y) { return pos[x] < pos[y]; });
+      };
+      // leadership candidates of every row: HashSet of the candidates in Partition.followerBrokers()
+      pr.clear();
+      pb.clear();
+      leadOff.assign(1, 0);
+      {
+        PhaseScope pc(PH_CAND_BUILD);
+        for (size_t k = i; k < end; ++k) {
+          hostsInOrder(list[k], true, ins);
+          javaHashSetOrder(ins, hs);
+          hs32.assign(hs.begin(), hs.end());
+          e.eligible(hs32, DA_LEADERSHIP, own);
+          for (int x : own) {
+            pr.push_back(list[k]);
+            pb.push_back(x);
+          }
+          leadOff.push_back((int32_t)pr.size());
+        }
+      }
+      const int64_t keyL = e.pairScan(*this, pr, pb, DA_LEADERSHIP, false);
+      size_t kL = end;  // the row owning pair keyL: the last row whose pairs start at or before it
+      if (keyL >= 0) kL = i + (size_t)(std::upper_bound(leadOff.begin(), leadOff.end(), (int32_t)keyL) - leadOff.begin()) - 1;
+      // replica-move candidates: ascending ids (the HashSet order when the row's set has no bucket collisions)
+      ids.assign(inorder.begin(), inorder.end());
+      std::sort(ids.begin(), ids.end());
+      e.eligible(ids, DA_MOVE, idElig);
+      auto idOrdered = [&](int r) {
+        hostsInOrder(r, false, ins);
+        const size_t size = inorder.size() - ins.size();
+        int32_t maxId = -1;
+        for (size_t q = ids.size(); q-- > 0;)
+          if (std::find(ins.begin(), ins.end(), ids[q]) == ins.end()) {
+            maxId = ids[q];
+            break;
+          }
+        return maxId < (int32_t)javaHashSetCapacity(size);
+      };
+      auto ownMoves = [&](int r, std::vector<int32_t>& out) {
+        hostsInOrder(r, false, ins);
+        std::vector<int> f;
+        for (int x : inorder)
+          if (std::find(ins.begin(), ins.end(), x) == ins.end()) f.push_back(x);
+        javaHashSetOrder(f, hs);
+        hs32.assign(hs.begin(), hs.end());
+        e.eligible(hs32, DA_MOVE, out);
+      };
+      size_t winRow = (size_t)-1;
+      int winDst = -1, winAction = DA_MOVE;
+      int64_t visited = 0;
+      for (size_t j = i; j < kL;) {
+        if (idOrdered(list[j])) {
+          size_t j2 = j + 1;
+          while (j2 < kL && idOrdered(list[j2])) ++j2;
+          const int64_t key = e.crossScan(*this, DA_MOVE, list, j, idElig, FILTER_NONE, false, j2);
+          const size_t N = idElig.size(), last = key >= 0 ? j + (size_t)(key / (int64_t)N) : j2;
+          for (size_t k = j; k < last; ++k)
+            visited += e.visitCount(DA_MOVE, list[k], idElig.data(), N, true);
+          if (key >= 0) {
+            winRow = last;
+            winDst = idElig[key % (int64_t)N];
+            visited += e.visitCount(DA_MOVE, list[last], idElig.data(), (size_t)(key % (int64_t)N) + 1, true);
+            break;
+          }
+          j = j2;
+        } else {
+          ownMoves(list[j], own);
+          const int64_t key = e.crossScan(*this, DA_MOVE, list, j, own, FILTER_NONE, false, j + 1);
+          visited += e.visitCount(DA_MOVE, list[j], own.data(), key >= 0 ? (size_t)key + 1 : own.size());
+          if (key >= 0) {
+            winRow = j;
+            winDst = own[key];
+            break;
+          }
+          ++j;
+        }
+      }
+      if (winRow == (size_t)-1 && kL < end) {
+        winRow = kL;
+        winDst = pb[keyL];
+        winAction = DA_LEADERSHIP;
+      }
+      // leadership candidates visited: every row before the winner's, the winner's up to a leadership winner
+      const size_t rowsDone = winRow == (size_t)-1 ? end : winRow;
+      for (size_t k = i; k < rowsDone; ++k)
+        visited += e.visitCount(DA_LEADERSHIP, list[k], pb.data() + leadOff[k - i], leadOff[k - i + 1] - leadOff[k - i]);
+      if (winRow != (size_t)-1) {
+        const int32_t a = leadOff[winRow - i], z = winAction == DA_LEADERSHIP ? (int32_t)keyL + 1 : leadOff[winRow - i + 1];
+        visited += e.visitCount(DA_LEADERSHIP, list[winRow], pb.data() + a, z - a);
+      }
+      e.candidates += visited;
+      if (winRow == (size_t)-1) {
+        if (runOffline) wasUnable = true;
+        i = end;
+        continue;
+      }
+      if (runOffline && winRow > i) wasUnable = true;
+      const int r = list[winRow];
+      const bool wasOffline = m.curOffline(r);
+      if (winAction == DA_LEADERSHIP) m.relocateLeadership(m.rPart[r], b, winDst);
+      else m.relocateReplica(m.rPart[r], b, winDst);
+      if (wasOffline) nOff--;
+      if (--n <= (nOff == 0 ? upperSrc : 0)) return false;
+      cand.removeIf([winDst](int x) { return x == winDst; });
+      if (m.tlead(t, winDst) < upper[t] || fix) cand.add(winDst);
+      i = winRow + 1;
+    }
+    return m.tlead(t, b) != 0;
+  }
+
+  // rebalanceByMovingLeadersIn (:680-778). The queue keys on the precomputed offline / topic-leader maps (updated
+  // for the source and b only) and the live leader counts, with JDK heap semantics for stale keys. A source's rows
+  // go to the device in runs of one action (b hosting the partition: leadership movement, else replica movement).
+  bool moveIn(Engine& e, int dest, int t) {
+    Model& m = e.m;
+    std::vector<int32_t> offBy(m.B, 0), tlBy(m.B, 0), offl;
+    for (int x = 0; x < m.B; ++x) {
+      tlBy[x] = m.tlead(t, x);
+      if (m.bOfflineSet[x].size() == 0) continue;
+      m.bOfflineSet[x].order(offl);
+      for (int r : offl) offBy[x] += (m.rLeader[r] && m.pTopic[m.rPart[r]] == t) ? 1 : 0;
+    }
+    auto cmp = [&](int b1, int b2) {
+      int c = jcmpInt(offBy[b2], offBy[b1]);
+      if (c == 0) c = jcmpInt(tlBy[b2], tlBy[b1]);
+      if (c == 0) c = jcmpInt(m.bNlead[b2], m.bNlead[b1]);
+      return c == 0 ? jcmpInt(m.bId[b2], m.bId[b1]) : c;
+    };
+    JavaPQ<decltype(cmp)> pq(cmp);
+    {
+      PhaseScope pi(PH_PQ_INIT);
+      for (int s = 0; s < m.B; ++s) {  // ClusterModel.brokers(): ascending id
+        if (fix) {
+          if (s != dest) pq.add(s);
+        } else if (m.tlead(t, s) > lower[t] || hasOffline(m, s) || excluded(s)) {
+          pq.add(s);
+        }
+      }
+    }
+    int n = m.tlead(t, dest);
+    const bool destExcl = excluded(dest);
+    std::vector<int32_t> single{dest}, candMove, candLead, toMove, rows, rowIdx, pbs;
+    e.eligible(single, DA_MOVE, candMove);
+    e.eligible(single, DA_LEADERSHIP, candLead);
+    auto actionOf = [&](int r) {  // -1: skipped (an excluded b cannot take a replica)
+      const bool has = m.replicaOn(m.rPart[r], dest) >= 0;
+      if (destExcl && !has) return -1;
+      return has ? (int)DA_LEADERSHIP : (int)DA_MOVE;
+    };
+    while (!pq.empty()) {
+      const int src = pq.poll();
+      replicasToMoveOut(m, src, t, toMove);
+      int nOff = 0;
+      for (int r : toMove) nOff += m.rInOff[r] ? 1 : 0;
+      size_t i = 0;
+      while (i < toMove.size()) {
+        const int act = actionOf(toMove[i]);
+        if (act < 0) {
+          ++i;
+          continue;
+        }
+        rows.clear();
+        rowIdx.clear();
+        size_t j = i;
+        for (; j < toMove.size(); ++j) {
+          const int a = actionOf(toMove[j]);
+          if (a < 0) continue;
+          if (a != act) break;
+          rows.push_back(toMove[j]);
+          rowIdx.push_back((int32_t)j);
+        }
+        int64_t key = -1;
+        if (act == DA_MOVE) {
+          if (!candMove.empty()) key = e.crossScan(*this, DA_MOVE, rows, 0, candMove);
+        } else if (!candLead.empty()) {
+          pbs.assign(rows.size(), dest);
+          key = e.pairScan(*this, rows, pbs, DA_LEADERSHIP, true);
+        }
+        if (key < 0) {
+          i = j;
+          continue;
+        }
+        const size_t k = (size_t)rowIdx[key];
+        const int r = toMove[k];
+        const bool wasOffline = m.curOffline(r);
+        if (act == DA_MOVE) m.relocateReplica(m.rPart[r], src, dest);
+        else m.relocateLeadership(m.rPart[r], src, dest);
+        if (wasOffline) {
+          nOff--;
+          offBy[src] = std::max(0, offBy[src] - 1);
+        }
+        tlBy[src] = std::max(0, tlBy[src] - 1);
+        tlBy[dest] += 1;
+        if (++n >= lower[t]) return false;
+        if (!pq.empty() && nOff == 0 && m.tlead(t, src) < m.tlead(t, pq.peek())) {
+          pq.add(src);
+          break;
+        }
+        i = k + 1;
+      }
+    }
+    return true;
+  }
+};
+
 // ======================================================================================= LeaderReplicaDistributionGoal
 class LeaderReplicaDistribution : public GoalImpl {
  public:
@@ -1895,6 +2298,7 @@ std::unique_ptr<GoalImpl> makeMoreGoal(int kind) {
     case CCMI_GOAL_CPU_CAPACITY: return std::make_unique<Capacity>(kind);
     case CCMI_GOAL_POTENTIAL_NW_OUT: return std::make_unique<PotentialNwOut>();
     case CCMI_GOAL_TOPIC_REPLICA_DISTRIBUTION: return std::make_unique<TopicReplicaDistribution>();
+    case CCMI_GOAL_TOPIC_LEADER_REPLICA_DISTRIBUTION: return std::make_unique<TopicLeaderReplicaDistribution>();
     case CCMI_GOAL_LEADER_REPLICA_DISTRIBUTION: return std::make_unique<LeaderReplicaDistribution>();
     case CCMI_GOAL_LEADER_BYTES_IN_DISTRIBUTION: return std::make_unique<LeaderBytesIn>();
     case CCMI_GOAL_PREFERRED_LEADER_ELECTION: return std::make_unique<PreferredLeaderElection>();

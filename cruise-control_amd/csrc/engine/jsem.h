@@ -196,6 +196,37 @@ class RbTreeSet {
     return true;
   }
   bool contains(int k) const { return find(k) >= 0; }
+  // Collection.removeIf over the TreeSet iterator: no comparator, so stale nodes are found too. TreeMap's
+  // PrivateEntryIterator.remove continues at the removed entry when it had two children (deleteEntry moved its
+  // successor's key in), which is the same in-order position of the sequence either way.
+  template <class Pred>
+  bool removeIf(Pred pred) {
+    bool removed = false;
+    if (seqOn_) {
+      for (size_t i = 0; i < seqKey_.size();) {
+        if (pred(seqKey_[i])) {
+          erase(seqId_[i]);
+          removed = true;
+        } else {
+          ++i;
+        }
+      }
+      return removed;
+    }
+    int p = root_;
+    if (p < 0) return false;
+    while (n_[p].left >= 0) p = n_[p].left;
+    while (p >= 0) {
+      int next = succ(p);
+      if (pred(n_[p].key)) {
+        if (n_[p].left >= 0 && n_[p].right >= 0) next = p;
+        erase(p);
+        removed = true;
+      }
+      p = next;
+    }
+    return removed;
+  }
   void inorder(std::vector<int>& out) const {
     if (seqOn_) {
       out.assign(seqKey_.begin(), seqKey_.end());
@@ -580,6 +611,23 @@ inline void javaHashSetOrder(const std::vector<int>& ins, std::vector<int>& out)
   out.reserve(n);
   for (unsigned b = 0; b < cap; ++b)
     for (int e = head[b]; e >= 0; e = nxt[e]) out.push_back(key[e]);
+}
+
+// ((Double) x).intValue() / (int) x: NaN -> 0, saturating, truncation toward zero (JLS 5.1.3)
+inline int32_t jD2I(double x) {
+  if (x != x) return 0;
+  if (x >= 2147483647.0) return 2147483647;
+  if (x <= -2147483648.0) return (int32_t)0x80000000;
+  return (int32_t)x;
+}
+inline int32_t jAddI(int32_t a, int32_t b) { return (int32_t)((uint32_t)a + (uint32_t)b); }  // Java int + (wraps)
+inline int32_t jSubI(int32_t a, int32_t b) { return (int32_t)((uint32_t)a - (uint32_t)b); }
+
+// HashSet<Broker> table capacity after n distinct add() calls from the default table (16 buckets, load .75)
+inline uint32_t javaHashSetCapacity(size_t n) {
+  uint32_t cap = 16;
+  while (n > (size_t)(cap / 4 * 3)) cap <<= 1;
+  return cap;
 }
 
 inline int32_t jStringHash(const char* s) {  // String.hashCode

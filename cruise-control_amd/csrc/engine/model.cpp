@@ -595,7 +595,11 @@ bool Model::relocateLeadership(int p, int src, int dst) {
   const int sr = replicaOn(p, src);
   if (sr < 0 || !rLeader[sr]) return false;
   const int dr = replicaOn(p, dst);
-  if (dr < 0 || rLeader[dr]) throw std::runtime_error("destination replica is a leader");
+  if (dr < 0) throw std::runtime_error("no destination replica");
+  if (rLeader[dr])  // IllegalArgumentException (ClusterModel.java:415-421)
+    throw std::invalid_argument("Cannot relocate leadership of partition " + topicNames[pTopic[p]] + "-" +
+                                std::to_string(pNumber[p]) + "from broker " + std::to_string(bId[src]) + " to broker " +
+                                std::to_string(bId[dst]) + " because the destination replica is a leader.");
   bVer[src]++;
   bVer[dst]++;
   noteDelta(src, sr);

@@ -17,6 +17,7 @@
 //   TopicReplicaDistributionGoal                  TopicReplicaDistributionGoal.java:153-214,300-314
 //   LeaderReplicaDistributionGoal                 LeaderReplicaDistributionGoal.java:91-123
 //   LeaderBytesInDistributionGoal                 LeaderBytesInDistributionGoal.java:69-127,264-271
+//   TopicLeaderReplicaDistributionGoal            TopicLeaderReplicaDistributionGoal.java:181-256,359-374
 // One broker per host (RandomCluster names hosts after brokers), so the host-resource branch equals the
 // broker branch bit for bit and is folded into it.
 #pragma once
@@ -37,7 +38,8 @@ namespace ccmi {
 // rorig(r) origOff(r) rpart(r) hosts(p,b), and for the goals that read them: rack(b) otherOnRack(p,self,rack)
 // slotRack(p,b) (rack of partition p's replica on b) rackCount(p,rack) nlead(b)
 // pot(b) lnwin(b) pLeadNwOut(p) ptopic(p) tcount(t,b) tUpper(t) tLower(t) bset(b) rbset(r) (broker sets)
-// tlead(t,b) (Broker.numLeadersFor) tMinLead(t) (MinTopicLeadersPerBrokerGoal's minimum, -1 = not its topic).
+// tlead(t,b) (Broker.numLeadersFor) tMinLead(t) (MinTopicLeadersPerBrokerGoal's minimum, -1 = not its topic)
+// tLeadUpper(t) tLeadLower(t) (TopicLeaderReplicaDistributionGoal's limits).
 // Replica.isCurrentOffline; V::origOff(r) = isOriginalOffline || original broker dead
 template <class V>
 CCMI_HD bool currentOffline(const V& v, int r) {
@@ -252,6 +254,32 @@ CCMI_HD bool leadAcceptMove(const DevGoal& g, const V& v, int action, int r, int
   return leaderMovementSatisfiable(g, v, src, dst);
 }
 
+// ---------------------------------------------------------------- TopicLeaderReplicaDistributionGoal
+// isLeadershipGoalSatisfiable (:231-256): one more leader of topic t on dst stays within its upper limit, and one
+// fewer on src stays within its lower limit unless src is excluded for replica moves
+template <class V>
+CCMI_HD bool tlSatisfiable(const DevGoal& g, const V& v, int t, int src, int dst) {
+  if (!(v.tlead(t, dst) + 1 <= (v.alive(dst) ? v.tLeadUpper(t) : 0))) return false;
+  if (!v.allowed(g.allowedSlot, src)) return true;
+  return v.tlead(t, src) - 1 >= (v.alive(src) ? v.tLeadLower(t) : 0);
+}
+// actionAcceptance (:181-229): a follower's replica move is accepted; a leader's move and a leadership move are not
+// if they unbalance the topic's leaders
+template <class V>
+CCMI_HD bool tlAcceptMove(const DevGoal& g, const V& v, int action, int r, int src, int dst) {
+  if (action == DA_MOVE && !(v.flags(r) & RF_LEADER)) return true;
+  return tlSatisfiable(g, v, v.ptopic(v.rpart(r)), src, dst);
+}
+template <class V>
+CCMI_HD int tlAcceptSwap(const DevGoal& g, const V& v, int sr, int sb, int dr, int db) {
+  const int st = v.ptopic(v.rpart(sr)), dt = v.ptopic(v.rpart(dr));
+  const bool sl = (v.flags(sr) & RF_LEADER) != 0, dl = (v.flags(dr) & RF_LEADER) != 0;
+  if ((st == dt && sl && dl) || (!sl && !dl)) return 0;
+  if (sl && !dl) return tlSatisfiable(g, v, st, sb, db) ? 0 : 1;
+  if (!sl && dl) return tlSatisfiable(g, v, dt, db, sb) ? 0 : 1;
+  return (tlSatisfiable(g, v, st, sb, db) && tlSatisfiable(g, v, dt, db, sb)) ? 0 : 1;
+}
+
 // ---------------------------------------------------------------- LeaderBytesInDistributionGoal
 template <class V>
 CCMI_HD double lbiThreshold(const DevGoal& g, const V& v, int b) {
@@ -284,6 +312,7 @@ CCMI_HD bool goalAcceptMove(const DevGoal& g, const V& v, int action, int r, int
     case DG_TOPIC_REPLICA_DISTRIBUTION: return topicAcceptMove(g, v, action, r, src, dst);
     case DG_LEADER_REPLICA_DISTRIBUTION: return leadAcceptMove(g, v, action, r, src, dst);
     case DG_LEADER_BYTES_IN: return lbiAcceptMove(g, v, action, r, dst);
+    case DG_TOPIC_LEADER_DISTRIBUTION: return tlAcceptMove(g, v, action, r, src, dst);
     default: return true;  // DG_ACCEPT_ALL
   }
 }
@@ -313,6 +342,9 @@ CCMI_HD bool goalSelfSatisfiedMove(const DevGoal& g, const V& v, int action, int
       if (g.fixOffline && currentOffline(v, r)) return true;
       return leadAcceptMove(g, v, action, r, src, dst);
     case DG_LEADER_BYTES_IN: return lbiAcceptMove(g, v, action, r, dst);
+    case DG_TOPIC_LEADER_DISTRIBUTION:  // selfSatisfied (:359-374)
+      if (g.fixOffline && currentOffline(v, r)) return action == DA_MOVE;
+      return tlSatisfiable(g, v, v.ptopic(v.rpart(r)), src, dst);
     default: return true;
   }
   if (g.fixOffline && currentOffline(v, r)) return action == DA_MOVE;
@@ -375,6 +407,7 @@ CCMI_HD int goalAcceptSwap(const DevGoal& g, const V& v, int sr, int sb, int dr,
       if (newSrc > lbiThreshold(g, v, sb)) return 1;
       return !(newDest > lbiThreshold(g, v, db)) ? 0 : 1;
     }
+    case DG_TOPIC_LEADER_DISTRIBUTION: return tlAcceptSwap(g, v, sr, sb, dr, db);
     default: return 0;  // ReplicaDistribution, ReplicaCapacity, MinTopicLeaders accept swaps
   }
 }

@@ -82,6 +82,8 @@ struct DevView {
   __device__ __forceinline__ int rbset(int r) const { return t.replicas[r].bset; }
   __device__ __forceinline__ int tlead(int tp, int b) const { return t.topicLead[(size_t)tp * t.ldB + b]; }
   __device__ __forceinline__ int tMinLead(int tp) const { return t.tMinLead ? t.tMinLead[tp] : -1; }
+  __device__ __forceinline__ int tLeadUpper(int tp) const { return t.tLeadLim[2 * tp]; }
+  __device__ __forceinline__ int tLeadLower(int tp) const { return t.tLeadLim[2 * tp + 1]; }
 };
 
 // Row updates a cross/pair scan applies itself (instead of a separate launch): every workgroup stages the
@@ -255,6 +257,7 @@ struct PreView {
   int snlead, dnlead, topic, stc, dtc, tup, tlo;
   int rbs, sbs, dbs;  // broker sets: the replica's (mapping policy), the source's, the destination's
   int stl, dtl, tmn;  // leaders of the row's topic on the source / destination, MinTopicLeaders' minimum of it
+  int tlu, tll;       // TopicLeaderReplicaDistributionGoal's leader limits of the row's topic
   bool inelig;  // dst is one of the row's partition's ineligible brokers
 
   static __device__ __forceinline__ double sel(int k, double a, double b, double c, double d) {
@@ -372,6 +375,11 @@ struct PreView {
       stl = t.topicLead[(size_t)topic * t.ldB + src];
       dtl = t.topicLead[(size_t)topic * t.ldB + dst];
     }
+    if (prog.needs & NEED_TLLIM) {
+      const int2 lim = reinterpret_cast<const int2*>(t.tLeadLim)[topic];
+      tlu = lim.x;
+      tll = lim.y;
+    }
   }
   // A row whose broker, partition and topic the host sent (RowRef): every record load is independent.
   __device__ __forceinline__ void loadRowRef(const DevTables& t, const DevProgram& prog, const RowRef x,
@@ -424,6 +432,11 @@ struct PreView {
       tmn = t.tMinLead ? t.tMinLead[topic] : -1;
       stl = t.topicLead[(size_t)topic * t.ldB + src];
       dtl = t.topicLead[(size_t)topic * t.ldB + dst];
+    }
+    if (prog.needs & NEED_TLLIM) {
+      const int2 lim = reinterpret_cast<const int2*>(t.tLeadLim)[topic];
+      tlu = lim.x;
+      tll = lim.y;
     }
     inelig = false;
     if (t.pIneligOff)  // uniform: only models with BAD_DISKS brokers carry the table
@@ -558,6 +571,8 @@ struct PreView {
   __device__ __forceinline__ int rbset(int) const { return rbs; }
   __device__ __forceinline__ int tlead(int, int b) const { return b == dst ? dtl : stl; }
   __device__ __forceinline__ int tMinLead(int) const { return tmn; }
+  __device__ __forceinline__ int tLeadUpper(int) const { return tlu; }
+  __device__ __forceinline__ int tLeadLower(int) const { return tll; }
 
   // RackAwareGoal.rackAwareEligibleBrokers: the destination's rack is not in the partition's rack list with
   // one occurrence of the replica's own rack removed (RackAwareGoal.java:193-211).

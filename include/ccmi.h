@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define CCMI_ABI_VERSION 6
+#define CCMI_ABI_VERSION 7
 
 typedef enum ccmi_status {
   CCMI_OK = 0,
@@ -109,7 +109,9 @@ typedef enum ccmi_goal_kind {
   CCMI_GOAL_INTRA_BROKER_DISK_USAGE_DISTRIBUTION = 17, /* IntraBrokerDiskUsageDistributionGoal */
   CCMI_GOAL_PREFERRED_LEADER_ELECTION = 18,         /* PreferredLeaderElectionGoal (not in default.goals) */
   CCMI_GOAL_RACK_AWARE_DISTRIBUTION = 19,           /* RackAwareDistributionGoal (not in default.goals) */
-  CCMI_GOAL_BROKER_SET_AWARE = 20                   /* BrokerSetAwareGoal (not in default.goals) */
+  CCMI_GOAL_BROKER_SET_AWARE = 20,                  /* BrokerSetAwareGoal (not in default.goals) */
+  CCMI_GOAL_TOPIC_LEADER_REPLICA_DISTRIBUTION = 21  /* TopicLeaderReplicaDistributionGoal (ABI v7; in goals, not in
+                                                       default.goals: AnalyzerConfig.java:297-319) */
 } ccmi_goal_kind;
 
 /* AnalyzerConfig replica.to.broker.set.mapping.policy.class (config/ReplicaToBrokerSetMappingPolicy.java) */
@@ -221,6 +223,14 @@ typedef struct ccmi_balancing_constraint {
   const int32_t* min_leader_topics;
   int32_t num_min_leader_topics;
   int32_t min_topic_leaders_per_broker;
+  /* TopicLeaderReplicaDistributionGoal (ABI v7): topic.leader.replica.count.balance.threshold (default 1.10),
+   * topic.leader.replica.count.balance.min.gap (2) / .max.gap (10) and
+   * topic.leader.replica.distribution.goal.balance.margin (0.9) (AnalyzerConfig.java:112-146,
+   * BalancingConstraint.java:85-88,145-167). */
+  double topic_leader_replica_balance_percentage;
+  int32_t topic_leader_replica_balance_min_gap;
+  int32_t topic_leader_replica_balance_max_gap;
+  double topic_leader_replica_balance_margin;
 } ccmi_balancing_constraint;
 
 /* analyzer/OptimizationOptions.java (7-field form) */

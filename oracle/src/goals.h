@@ -424,6 +424,39 @@ class TopicReplicaDistributionGoal : public AbstractGoal {
   bool anyAbove_ = false, anyUnder_ = false;
 };
 
+//   TopicLeaderReplicaDistributionGoal     analyzer/goals/TopicLeaderReplicaDistributionGoal.java (in `goals`, not in
+//                                          default.goals)
+class TopicLeaderReplicaDistributionGoal : public AbstractGoal {
+ public:
+  using AbstractGoal::AbstractGoal;
+  std::string name() const override { return "TopicLeaderReplicaDistributionGoal"; }
+  bool isHardGoal() const override { return false; }
+  Acceptance actionAcceptance(const BalancingAction& a, ClusterModel& cm) override;
+  // GoalUtils.HardGoalStatsComparator (TopicLeaderReplicaDistributionGoal.java:269-272)
+  int compareStats(const ClusterModelStats&, const ClusterModelStats&) const override { return 0; }
+  int upperLimit(int topic) const { return upper_[topic]; }
+  int lowerLimit(int topic) const { return lower_[topic]; }
+
+ protected:
+  void initGoalState(ClusterModel& cm, const OptimizationOptions& o) override;
+  void updateGoalState(ClusterModel& cm, const OptimizationOptions& o) override;
+  void rebalanceForBroker(int broker, ClusterModel& cm, const GoalList& g, const OptimizationOptions& o) override;
+  bool selfSatisfied(ClusterModel& cm, const BalancingAction& a) override;
+
+ private:
+  bool satisfiable(const ClusterModel& cm, int topic, int src, int dst) const;
+  std::vector<int> leadersOf(const ClusterModel& cm, int b, int topic) const;
+  std::vector<int> replicasToMoveOut(ClusterModel& cm, int b, int topic);
+  bool moveOut(int b, int topic, ClusterModel& cm, const GoalList& g, const OptimizationOptions& o);
+  bool moveIn(int b, int topic, ClusterModel& cm, const GoalList& g, const OptimizationOptions& o);
+  bool isExcluded(int b) const { return !allowed_[b]; }
+  bool fixOfflineReplicasOnly_ = false;
+  std::vector<int> upper_, lower_;
+  std::vector<char> rebalanceTopic_;
+  std::vector<char> allowed_;
+  bool anyAbove_ = false, anyUnder_ = false;
+};
+
 class LeaderReplicaDistributionGoal : public AbstractGoal {
  public:
   using AbstractGoal::AbstractGoal;

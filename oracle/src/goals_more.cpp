@@ -1180,6 +1180,272 @@ bool TopicReplicaDistributionGoal::moveIn(int dest, int topic, ClusterModel& cm,
   return true;
 }
 
+// ===================================================================== TopicLeaderReplicaDistributionGoal
+// (TopicLeaderReplicaDistributionGoal.java). Java int arithmetic wraps; the limits of a cluster whose alive brokers
+// are all excluded from replica moves come from an infinite or NaN average (x / 0.0).
+namespace {
+int32_t jAddInt(int32_t a, int32_t b) { return (int32_t)((uint32_t)a + (uint32_t)b); }
+int32_t jSubInt(int32_t a, int32_t b) { return (int32_t)((uint32_t)a - (uint32_t)b); }
+}  // namespace
+
+// isLeadershipGoalSatisfiable + isTopicLeaderCount{Under,Above}…AfterChange (:231-256)
+bool TopicLeaderReplicaDistributionGoal::satisfiable(const ClusterModel& cm, int topic, int src, int dst) const {
+  const int up = cm.brokers[dst].isAlive() ? upper_[topic] : 0;
+  if (!(cm.numLeadersFor(dst, topic) + 1 <= up)) return false;
+  if (isExcluded(src)) return true;
+  const int lo = cm.brokers[src].isAlive() ? lower_[topic] : 0;
+  return cm.numLeadersFor(src, topic) - 1 >= lo;
+}
+// actionAcceptance (:181-229)
+Acceptance TopicLeaderReplicaDistributionGoal::actionAcceptance(const BalancingAction& a, ClusterModel& cm) {
+  const int sb = a.sourceBroker, db = a.destinationBroker;
+  const int st = cm.partitions[a.partition].topic;
+  const int sr = cm.replicaOnBroker(a.partition, sb);
+  const bool sl = cm.replicas[sr].isLeader;
+  auto verdict = [](bool ok) { return ok ? Acceptance::ACCEPT : Acceptance::REPLICA_REJECT; };
+  switch (a.type) {
+    case ActionType::INTER_BROKER_REPLICA_SWAP: {
+      const int dt = cm.partitions[a.destPartition].topic;
+      const bool dl = cm.replicas[cm.replicaOnBroker(a.destPartition, db)].isLeader;
+      if (st == dt && sl && dl) return Acceptance::ACCEPT;
+      if (!sl && !dl) return Acceptance::ACCEPT;
+      if (sl && !dl) return verdict(satisfiable(cm, st, sb, db));
+      if (!sl && dl) return verdict(satisfiable(cm, dt, db, sb));
+      return verdict(satisfiable(cm, st, sb, db) && satisfiable(cm, dt, db, sb));
+    }
+    case ActionType::LEADERSHIP_MOVEMENT:
+      return verdict(satisfiable(cm, st, sb, db));
+    case ActionType::INTER_BROKER_REPLICA_MOVEMENT:
+      if (!sl) return Acceptance::ACCEPT;
+      return verdict(satisfiable(cm, st, sb, db));
+    default:
+      throw std::invalid_argument("Unsupported balancing action");
+  }
+}
+// initGoalState (:298-347) with balancePercentageWithMargin / clampLower / clampUpper / balance{Upper,Lower}Limit
+// (:101-168)
+void TopicLeaderReplicaDistributionGoal::initGoalState(ClusterModel& cm, const OptimizationOptions& o) {
+  int numAllowed = 0;
+  allowed_ = allowedForReplicaMove(cm, o, &numAllowed);  // an empty set is allowed: leadership-only balancing
+  // GoalUtils.topicsToRebalance (GoalUtils.java:439-452)
+  rebalanceTopic_.assign(cm.numTopics(), cm.selfHealingEligibleReplicas.empty() ? 1 : 0);
+  for (int r : cm.selfHealingEligibleReplicas) rebalanceTopic_[cm.partitions[cm.replicas[r].partition].topic] = 1;
+  if (cm.selfHealingEligibleReplicas.empty())
+    for (int t : o.excludedTopics) rebalanceTopic_[t] = 0;
+  double pct = bc_.topicLeaderReplicaBalancePercentage;
+  if (o.triggeredByGoalViolation) pct *= bc_.goalViolationDistributionThresholdMultiplier;
+  const double margin = (pct - 1) * bc_.topicLeaderReplicaDistributionGoalBalanceMargin;
+  // ClusterModel.numLeadersPerTopic (ClusterModel.java:276-285): one leader per partition
+  std::vector<int> numLeaders(cm.numTopics(), 0);
+  for (const Partition& p : cm.partitions) numLeaders[p.topic]++;
+  const int minGap = bc_.topicLeaderReplicaBalanceMinGap, maxGap = bc_.topicLeaderReplicaBalanceMaxGap;
+  upper_.assign(cm.numTopics(), 0);
+  lower_.assign(cm.numTopics(), 0);
+  for (int t = 0; t < cm.numTopics(); ++t) {
+    const double avg = numLeaders[t] / (double)numAllowed;
+    const int32_t ceilAvg = jDoubleToInt(std::ceil(avg)), floorAvg = jDoubleToInt(std::floor(avg));
+    const int32_t cu = jDoubleToInt(std::ceil(avg * (1 + margin)));
+    upper_[t] = std::max(jAddInt(ceilAvg, minGap), std::min(cu, jAddInt(ceilAvg, maxGap)));
+    const int32_t cl = jDoubleToInt(std::floor(avg * jmax(0, (1 - margin))));
+    const int32_t lmin = std::max(0, jSubInt(floorAvg, maxGap)), lmax = std::max(0, jSubInt(floorAvg, minGap));
+    lower_[t] = std::max(lmin, std::min(cl, lmax));
+  }
+  const bool selfHealing = !cm.selfHealingEligibleReplicas.empty();
+  for (size_t b = 0; b < cm.brokers.size(); ++b) {
+    SortSpec spec;
+    if (o.onlyMoveImmigrantReplicas) spec.selection.push_back({SelFn::IMMIGRANTS});
+    if (selfHealing && cm.brokers[b].isAlive()) spec.selection.push_back({SelFn::IMMIGRANT_OR_OFFLINE});
+    if (!o.excludedTopics.empty()) spec.selection.push_back({SelFn::EXCLUDED_TOPICS});
+    spec.selection.push_back({SelFn::LEADERS});
+    cm.trackSortedReplicas((int)b, replicaSortName(false, true), spec);
+  }
+  fixOfflineReplicasOnly_ = false;
+}
+// selfSatisfied (:359-374)
+bool TopicLeaderReplicaDistributionGoal::selfSatisfied(ClusterModel& cm, const BalancingAction& a) {
+  const int sr = cm.replicaOnBroker(a.partition, a.sourceBroker);
+  if (fixOfflineReplicasOnly_ && cm.isCurrentOffline(sr)) return a.type == ActionType::INTER_BROKER_REPLICA_MOVEMENT;
+  return satisfiable(cm, cm.partitions[a.partition].topic, a.sourceBroker, a.destinationBroker);
+}
+// updateGoalState (:382-424)
+void TopicLeaderReplicaDistributionGoal::updateGoalState(ClusterModel& cm, const OptimizationOptions&) {
+  if (anyAbove_ || anyUnder_) {
+    anyAbove_ = anyUnder_ = false;
+    succeeded_ = false;
+  }
+  try {
+    ensureNoOfflineReplicas(cm, name());
+  } catch (OptimizationFailure&) {
+    if (fixOfflineReplicasOnly_) throw;
+    fixOfflineReplicasOnly_ = true;
+    return;
+  }
+  ensureReplicasMoveOffBrokersWithBadDisks(cm, name());
+  finished_ = true;
+}
+// rebalanceForBroker (:518-583) + skipBrokerRebalance and its helpers (:426-504)
+void TopicLeaderReplicaDistributionGoal::rebalanceForBroker(int b, ClusterModel& cm, const GoalList& g,
+                                                            const OptimizationOptions& o) {
+  const Broker& br = cm.brokers[b];
+  for (int topic : br.topicKeys.order()) {  // Broker.topics(): HashMap key order
+    if (!rebalanceTopic_[topic]) continue;
+    // the tracked leaders-only view's leaders of the topic
+    int n = 0, nOff = 0;
+    bool hasImm = false;
+    for (int r : cm.sortedReplicasView(b, replicaSortName(false, true))) {
+      if (!cm.replicas[r].isLeader || cm.partitions[cm.replicas[r].partition].topic != topic) continue;
+      n++;
+      if (br.offlineSet.contains(r, cm.replicaHash(r))) nOff++;
+      if (cm.isImmigrant(r)) hasImm = true;
+    }
+    const bool excluded = isExcluded(b);
+    const bool requireLess = nOff > 0 || n > upper_[topic] || excluded;
+    const bool requireMore = !excluded && br.isAlive() && n - nOff < lower_[topic];
+    if (br.isAlive() && !requireMore && !requireLess) continue;
+    if (!cm.newBrokers.empty() && !br.isNew() && !requireLess) continue;
+    if (!cm.selfHealingEligibleReplicas.empty() && requireLess && nOff == 0 && !hasImm) continue;
+    if (o.onlyMoveImmigrantReplicas && requireLess && !hasImm) continue;
+    if (requireLess && moveOut(b, topic, cm, g, o)) anyAbove_ = true;
+    if (requireMore && moveIn(b, topic, cm, g, o)) anyUnder_ = true;
+  }
+}
+// leadersOfTopicInBroker (:585-589)
+std::vector<int> TopicLeaderReplicaDistributionGoal::leadersOf(const ClusterModel& cm, int b, int topic) const {
+  std::vector<int> out;
+  for (int r : cm.brokers[b].replicas)
+    if (cm.replicas[r].isLeader && cm.partitions[cm.replicas[r].partition].topic == topic) out.push_back(r);
+  return out;
+}
+// replicasToMoveOut (:591-596): TreeSet(broker.replicaComparator()) of the topic's leaders retained to the tracked
+// leaders-only view
+std::vector<int> TopicLeaderReplicaDistributionGoal::replicasToMoveOut(ClusterModel& cm, int b, int topic) {
+  const Broker& br = cm.brokers[b];
+  const auto& tracked = cm.sortedReplicasView(b, replicaSortName(false, true));
+  std::vector<int> out;
+  for (int r : leadersOf(cm, b, topic))
+    if (tracked.count(r)) out.push_back(r);
+  std::sort(out.begin(), out.end(), [&](int x, int y) {
+    const bool ox = br.offlineSet.contains(x, cm.replicaHash(x)), oy = br.offlineSet.contains(y, cm.replicaHash(y));
+    if (ox != oy) return ox;
+    const bool ix = cm.isImmigrant(x), iy = cm.isImmigrant(y);
+    if (ix != iy) return ix;
+    return cm.partitions[cm.replicas[x].partition].number < cm.partitions[cm.replicas[y].partition].number;
+  });
+  return out;
+}
+// rebalanceByMovingLeadersOut (:598-678)
+bool TopicLeaderReplicaDistributionGoal::moveOut(int b, int topic, ClusterModel& cm, const GoalList& g,
+                                                 const OptimizationOptions& o) {
+  JTreeSet candidates([&cm, topic](int x, int y) {
+    int c = icompare(cm.numLeadersFor(x, topic), cm.numLeadersFor(y, topic));
+    if (c == 0) c = icompare(cm.brokers[x].numLeaders, cm.brokers[y].numLeaders);
+    return c != 0 ? c : icompare(cm.brokers[x].id, cm.brokers[y].id);
+  });
+  std::vector<int> toAdd;
+  if (fixOfflineReplicasOnly_) {
+    toAdd = cm.aliveBrokers();
+  } else {
+    std::vector<int> filtered;
+    for (int x : cm.aliveBrokers())
+      if (cm.numLeadersFor(x, topic) < upper_[topic]) filtered.push_back(x);
+    toAdd = javaHashSetOrderIntKeys(filtered);  // Collectors.toSet()
+  }
+  for (int x : toAdd) candidates.add(x);
+  const std::vector<int> leaders = leadersOf(cm, b, topic);
+  int n = (int)leaders.size(), nOff = 0;
+  for (int r : leaders)
+    if (cm.brokers[b].offlineSet.contains(r, cm.replicaHash(r))) nOff++;
+  const int upperForSource = upper_[topic];
+  bool wasUnableToMoveOffline = false;
+  for (int r : replicasToMoveOut(cm, b, topic)) {
+    if (wasUnableToMoveOffline && !cm.isCurrentOffline(r) && n <= upperForSource) return false;
+    const bool wasOffline = cm.isCurrentOffline(r);
+    const int p = cm.replicas[r].partition;
+    // destination candidates per action type, each a HashSet built from the TreeSet's stream
+    std::vector<int> lead, move;
+    for (int x : candidates.toVector()) {
+      const int xr = cm.replicaOnBroker(p, x);
+      if (xr >= 0 && !cm.replicas[xr].isLeader) lead.push_back(x);  // Partition.followerBrokers()
+      if (xr < 0) move.push_back(x);
+    }
+    int dst = maybeApplyBalancingAction(cm, r, javaHashSetOrderIntKeys(lead), ActionType::LEADERSHIP_MOVEMENT, g, o);
+    if (dst < 0)
+      dst = maybeApplyBalancingAction(cm, r, javaHashSetOrderIntKeys(move), ActionType::INTER_BROKER_REPLICA_MOVEMENT,
+                                      g, o);
+    if (dst >= 0) {
+      if (wasOffline) nOff--;
+      if (--n <= (nOff == 0 ? upperForSource : 0)) return false;
+      candidates.removeIf([dst](int x) { return x == dst; });
+      if (cm.numLeadersFor(dst, topic) < upper_[topic] || fixOfflineReplicasOnly_) candidates.add(dst);
+    } else if (wasOffline) {
+      wasUnableToMoveOffline = true;
+    }
+  }
+  return !leadersOf(cm, b, topic).empty();
+}
+// rebalanceByMovingLeadersIn (:680-778)
+bool TopicLeaderReplicaDistributionGoal::moveIn(int dest, int topic, ClusterModel& cm, const GoalList& g,
+                                                const OptimizationOptions& o) {
+  const int B = (int)cm.brokers.size();
+  std::vector<int> offlineBy(B), leadersBy(B);  // offlineByBroker / topicLeadersByBroker
+  for (int x = 0; x < B; ++x) {
+    leadersBy[x] = cm.numLeadersFor(x, topic);
+    int k = 0;
+    for (int r : leadersOf(cm, x, topic))
+      if (cm.brokers[x].offlineSet.contains(r, cm.replicaHash(r))) k++;
+    offlineBy[x] = k;
+  }
+  JPriorityQueue pq([&](int b1, int b2) {
+    const int r = icompare(offlineBy[b2], offlineBy[b1]);
+    if (r != 0) return r;
+    const int r2 = icompare(leadersBy[b2], leadersBy[b1]);
+    if (r2 != 0) return r2;
+    const int r3 = icompare(cm.brokers[b2].numLeaders, cm.brokers[b1].numLeaders);
+    return r3 == 0 ? icompare(cm.brokers[b2].id, cm.brokers[b1].id) : r3;
+  });
+  for (int s = 0; s < B; ++s) {  // ClusterModel.brokers(): ascending id
+    if (fixOfflineReplicasOnly_) {
+      if (s != dest) pq.add(s);
+    } else if (cm.numLeadersFor(s, topic) > lower_[topic] || hasOfflineReplicas(cm, s) || isExcluded(s)) {
+      pq.add(s);
+    }
+  }
+  int n = cm.numLeadersFor(dest, topic);
+  const std::vector<int> candidates{dest};
+  while (!pq.empty()) {
+    const int src = pq.poll();
+    const std::vector<int> toMove = replicasToMoveOut(cm, src, topic);
+    int nOff = 0;
+    for (int r : toMove)
+      if (cm.brokers[src].offlineSet.contains(r, cm.replicaHash(r))) nOff++;
+    for (int r : toMove) {
+      const bool wasOffline = cm.isCurrentOffline(r);
+      const bool destHas = cm.replicaOnBroker(cm.replicas[r].partition, dest) >= 0;
+      ActionType action;
+      if (isExcluded(dest)) {
+        if (!destHas) continue;  // leadership transfer impossible
+        action = ActionType::LEADERSHIP_MOVEMENT;
+      } else {
+        action = destHas ? ActionType::LEADERSHIP_MOVEMENT : ActionType::INTER_BROKER_REPLICA_MOVEMENT;
+      }
+      if (maybeApplyBalancingAction(cm, r, candidates, action, g, o) >= 0) {
+        if (wasOffline) {
+          nOff--;
+          offlineBy[src] = std::max(0, offlineBy[src] - 1);
+        }
+        leadersBy[src] = std::max(0, leadersBy[src] - 1);
+        leadersBy[dest] += 1;
+        if (++n >= lower_[topic]) return false;
+        if (!pq.empty() && nOff == 0 && cm.numLeadersFor(src, topic) < cm.numLeadersFor(pq.peek(), topic)) {
+          pq.add(src);
+          break;
+        }
+      }
+    }
+  }
+  return true;
+}
+
 // ===================================================================== LeaderReplicaDistributionGoal
 // ReplicaDistributionAbstractGoal.initGoalState (ReplicaDistributionAbstractGoal.java:124-152) with
 // numInterestedReplicas = number of leaders and leader.replica.count.balance.threshold

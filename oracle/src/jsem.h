@@ -147,6 +147,23 @@ class JTreeSet {
     return true;
   }
   bool contains(int key) const { return getEntry(key) >= 0; }
+  // Collection.removeIf over the TreeSet iterator (no comparator: stale nodes are found too). TreeMap's
+  // PrivateEntryIterator.remove continues at the removed entry when it had two children: deleteEntry moved the
+  // successor's key into it.
+  template <class Pred>
+  bool removeIf(Pred pred) {
+    bool removed = false;
+    for (int e = firstEntry(); e >= 0;) {
+      int next = successor(e);
+      if (pred(nodes_[e].key)) {
+        if (nodes_[e].left >= 0 && nodes_[e].right >= 0) next = e;
+        deleteEntry(e);
+        removed = true;
+      }
+      e = next;
+    }
+    return removed;
+  }
 
   // In-order iteration (TreeMap iterator: getFirstEntry + successor).
   std::vector<int> toVector() const {

@@ -102,10 +102,8 @@ bool ClusterModel::passesSelection(const SortSpec& spec, int r) const {
 }
 
 int ClusterModel::numLeadersFor(int b, int topic) const {
-  int n = 0;
-  for (int r : brokers[b].replicas)
-    if (replicas[r].isLeader && partitions[replicas[r].partition].topic == topic) ++n;
-  return n;
+  const auto it = brokers[b].topicLeaderCount.find(topic);
+  return it == brokers[b].topicLeaderCount.end() ? 0 : it->second;
 }
 
 // Broker.trackSortedReplicas (Broker.java:398-408): the broker's own set and one per disk
@@ -428,6 +426,7 @@ void ClusterModel::brokerAddReplica(int b, int r) {
   }
   br.topicReplicaCount[partitions[rep.partition].topic] += 1;
   if (rep.isLeader) {
+    br.topicLeaderCount[partitions[rep.partition].topic] += 1;
     loadAddLoad(br.leadershipLoadForNwResources, rep.load, W);
     rep.inBrokerLeaders = true;
     br.numLeaders++;
@@ -460,6 +459,7 @@ int ClusterModel::brokerRemoveReplica(int b, int partition) {
   loadSubLoad(br.load, rep.load, W);
   br.topicReplicaCount[partitions[partition].topic] -= 1;
   if (rep.isLeader) {
+    br.topicLeaderCount[partitions[partition].topic] -= 1;
     loadSubLoad(br.leadershipLoadForNwResources, rep.load, W);
     if (rep.inBrokerLeaders) br.numLeaders--;
     br.leaderSet.remove(r, replicaHash(r));
@@ -517,6 +517,7 @@ Load ClusterModel::brokerMakeFollower(int b, int partition) {
   loadSubLoad(br.leadershipLoadForNwResources, replicas[r].load, W);
   sortedRemove(b, r);
   Load delta = replicaMakeFollower(r);
+  br.topicLeaderCount[partitions[partition].topic] -= 1;
   loadSubDelta(br.load, delta, W);
   if (replicas[r].inBrokerLeaders) {
     replicas[r].inBrokerLeaders = false;
@@ -531,6 +532,7 @@ void ClusterModel::brokerMakeLeader(int b, int partition, const Load& delta) {
   int r = replicaOnBroker(partition, b);
   Broker& br = brokers[b];
   sortedRemove(b, r);
+  if (!replicas[r].isLeader) br.topicLeaderCount[partitions[partition].topic] += 1;
   replicas[r].isLeader = true;
   loadAddDelta(replicas[r].load, delta, W);
   loadAddLoad(br.leadershipLoadForNwResources, replicas[r].load, W);
@@ -577,7 +579,11 @@ bool ClusterModel::relocateLeadership(int p, int src, int dst) {
   int sr = replicaOnBroker(p, src);
   if (!replicas[sr].isLeader) return false;
   int dr = replicaOnBroker(p, dst);
-  if (replicas[dr].isLeader) throw std::runtime_error("destination replica is a leader");
+  if (replicas[dr].isLeader)  // IllegalArgumentException (ClusterModel.java:415-421)
+    throw std::invalid_argument("Cannot relocate leadership of partition " + topicNames[partitions[p].topic] + "-" +
+                                std::to_string(partitions[p].number) + "from broker " + std::to_string(brokers[src].id) +
+                                " to broker " + std::to_string(brokers[dst].id) +
+                                " because the destination replica is a leader.");
   Load delta = brokerMakeFollower(src, p);
   brokerMakeLeader(dst, p, delta);
   Partition& part = partitions[p];

@@ -220,6 +220,7 @@ struct Broker {
   std::vector<int> replicas;  // HashSet<Replica> contents (order not semantically used)
   int numLeaders = 0, numImmigrants = 0, numOffline = 0;
   std::unordered_map<int, int> topicReplicaCount;  // _topicReplicas keyset -> count (keys never removed)
+  std::unordered_map<int, int> topicLeaderCount;   // Broker.numLeadersFor(topic), kept with every leader change
   Load load;
   Load leadershipLoadForNwResources;
   std::map<std::string, std::unique_ptr<SortedReplicas>> sorted;

@@ -18,6 +18,7 @@ std::unique_ptr<Goal> makeGoal(int kind, const BalancingConstraint& bc) {
     case CCMI_GOAL_CPU_CAPACITY: return std::make_unique<CapacityGoal>(bc, CPU);
     case CCMI_GOAL_POTENTIAL_NW_OUT: return std::make_unique<PotentialNwOutGoal>(bc);
     case CCMI_GOAL_TOPIC_REPLICA_DISTRIBUTION: return std::make_unique<TopicReplicaDistributionGoal>(bc);
+    case CCMI_GOAL_TOPIC_LEADER_REPLICA_DISTRIBUTION: return std::make_unique<TopicLeaderReplicaDistributionGoal>(bc);
     case CCMI_GOAL_LEADER_REPLICA_DISTRIBUTION: return std::make_unique<LeaderReplicaDistributionGoal>(bc);
     case CCMI_GOAL_LEADER_BYTES_IN_DISTRIBUTION: return std::make_unique<LeaderBytesInDistributionGoal>(bc);
     case CCMI_GOAL_REPLICA_DISTRIBUTION: return std::make_unique<ReplicaDistributionGoal>(bc);

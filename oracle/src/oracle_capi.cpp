@@ -44,6 +44,10 @@ BalancingConstraint toBc(const ccmi_balancing_constraint* c) {
   bc.brokerSetPolicy = c->broker_set_policy;
   for (int i = 0; i < c->num_min_leader_topics; ++i) bc.minLeaderTopics.push_back(c->min_leader_topics[i]);
   bc.minTopicLeadersPerBroker = c->min_topic_leaders_per_broker;
+  bc.topicLeaderReplicaBalancePercentage = c->topic_leader_replica_balance_percentage;
+  bc.topicLeaderReplicaBalanceMinGap = c->topic_leader_replica_balance_min_gap;
+  bc.topicLeaderReplicaBalanceMaxGap = c->topic_leader_replica_balance_max_gap;
+  bc.topicLeaderReplicaDistributionGoalBalanceMargin = c->topic_leader_replica_balance_margin;
   return bc;
 }
 
@@ -312,6 +316,9 @@ int oc_optimize(void* hv, const int32_t* goals, int n, const ccmi_balancing_cons
   } catch (UnsupportedOperation& e) {
     h->err = e.what();
     return CCMI_E_UNSUPPORTED;
+  } catch (std::invalid_argument& e) {  // IllegalArgumentException
+    h->err = e.what();
+    return CCMI_E_INVALID;
   } catch (std::logic_error& e) {
     h->err = e.what();
     return CCMI_E_STATE;

@@ -32,6 +32,11 @@ struct BalancingConstraint {
   // (BalancingConstraint.java:92-93, AnalyzerConfig.java:401-414)
   std::vector<int> minLeaderTopics;
   int minTopicLeadersPerBroker = 1;
+  // TopicLeaderReplicaDistributionGoal (BalancingConstraint.java:85-88, AnalyzerConfig.java:112-146)
+  double topicLeaderReplicaBalancePercentage = 1.10;
+  int topicLeaderReplicaBalanceMinGap = 2;
+  int topicLeaderReplicaBalanceMaxGap = 10;
+  double topicLeaderReplicaDistributionGoalBalanceMargin = 0.9;
 };
 
 struct ClusterModelStats {

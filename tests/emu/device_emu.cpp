@@ -34,6 +34,7 @@ struct Emu {
   std::vector<int32_t> bRack, pTopic, tUpper, tLower, bSet, rSet;
   std::vector<int32_t> pIneligOff, pIneligB;  // Partition._ineligibleBrokers (empty: none)
   std::vector<int32_t> topicLead, tMinLead;   // Broker.numLeadersFor counts (empty: not kept), MinTopicLeaders minima
+  std::vector<int32_t> tLeadLim;              // TopicLeaderReplicaDistributionGoal (upper, lower) per topic
   std::vector<uint8_t> bAlive, rFlags;
   std::vector<uint32_t> allowed;
   // chain state (device.h uploadLoads)
@@ -99,6 +100,8 @@ struct View {
   int rbset(int r) const { return e.rSet.empty() ? -1 : e.rSet[r]; }
   int tlead(int t, int b) const { return e.topicLead.at((size_t)t * e.ldB + b); }
   int tMinLead(int t) const { return e.tMinLead.empty() ? -1 : e.tMinLead[t]; }
+  int tLeadUpper(int t) const { return e.tLeadLim.at(2 * (size_t)t); }
+  int tLeadLower(int t) const { return e.tLeadLim.at(2 * (size_t)t + 1); }
   // RackAwareGoal.rackAwareEligibleBrokers membership for (replica r, destination d)
   bool rackEligible(int r, int d) const {
     std::vector<int> racks;
@@ -187,6 +190,7 @@ void Device::enableTopicLeaders(const int32_t* dense) {
   E(st_).topicLead.assign(dense, dense + (size_t)T_ * ldB_);
 }
 void Device::setMinLeaders(const int32_t* tMin) { E(st_).tMinLead.assign(tMin, tMin + T_); }
+void Device::setTopicLeadLimits(const int32_t* lim) { E(st_).tLeadLim.assign(lim, lim + 2 * (size_t)T_); }
 
 void Device::setBrokerSets(const int32_t* brokerSet, const int32_t* replicaSet) {
   E(st_).bSet.assign(brokerSet, brokerSet + B_);
