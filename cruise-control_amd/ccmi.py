@@ -210,7 +210,7 @@ _STATUS = {1: IllegalArgumentException, 2: DeviceError, 3: OptimizationFailureEx
 
 ABI_VERSION = 7  # CCMI_ABI_VERSION of include/ccmi.h
 EXPORTED_SYMBOLS = (
-    "ccmi_last_error", "ccmi_abi_version", "ccmi_default_constraint", "ccmi_default_random_cluster_props",
+    "ccmi_last_error", "ccmi_abi_version", "ccmi_device_count", "ccmi_default_constraint", "ccmi_default_random_cluster_props",
     "ccmi_random_cluster", "ccmi_cluster_buffers_desc", "ccmi_cluster_buffers_free", "ccmi_session_create",
     "ccmi_session_destroy", "ccmi_optimizations", "ccmi_goal_optimize", "ccmi_action_acceptance",
     "ccmi_action_acceptance_by_kind", "ccmi_session_apply", "ccmi_last_failure_provision",
@@ -291,6 +291,12 @@ class Library:
         L.ccmi_topic_broker_set.restype = C.c_int32
         L.ccmi_topic_broker_set.argtypes = [C.c_char_p, C.c_int32]
         L.ccmi_default_random_cluster_props.argtypes = [C.POINTER(RandomClusterProps)]
+        L.ccmi_device_count.restype = C.c_int32
+        L.ccmi_device_count.argtypes = []
+
+    def device_count(self) -> int:
+        """Visible gfx950 devices (ccmi_device_count)."""
+        return int(self.lib.ccmi_device_count())
 
     @classmethod
     def get(cls, path: str = DEFAULT_LIB) -> "Library":
@@ -1264,12 +1270,15 @@ class GoalViolationDetector:
 
     def __init__(self, detection_goals: Sequence[str], constraint: Optional[BalancingConstraint] = None,
                  priority_weight: float = 1.1, strictness_weight: float = 1.5, lib: Optional[Library] = None,
-                 device: int = 0, max_concurrency: int = 8):
+                 device: Optional[int] = None, max_concurrency: int = 8, devices: Optional[Sequence[int]] = None):
         self.goals = list(detection_goals)
         self.constraint = constraint or BalancingConstraint()
         self.cost = balancedness_cost_by_goal(goals_from_names(self.goals), priority_weight, strictness_weight)
         self.lib = lib or Library.get()
-        self.device = device
+        # the sessions go round-robin over `devices` (default: every visible gfx950; `device` pins them to one)
+        if devices is None:
+            devices = [device] if device is not None else list(range(max(1, self.lib.device_count())))
+        self.devices = list(devices)
         self.max_concurrency = max_concurrency
 
     def detect(self, desc: ClusterDesc, keepalive=None, excluded_topics: Sequence[int] = (),
@@ -1287,8 +1296,9 @@ class GoalViolationDetector:
                                    excluded_brokers_for_replica_move=list(excluded_brokers_for_replica_move),
                                    is_triggered_by_goal_violation=True)
 
-        def one(name: str):  # GoalViolationDetector.optimizeForGoal (:296-331)
-            cm = ClusterModel(desc, device=self.device, lib=self.lib, keepalive=keepalive)
+        def one(i_name):  # GoalViolationDetector.optimizeForGoal (:296-331)
+            i, name = i_name
+            cm = ClusterModel(desc, device=self.devices[i % len(self.devices)], lib=self.lib, keepalive=keepalive)
             goal = goals_from_names([name], self.constraint)[0]
             try:
                 goal.optimize(cm, opts)
@@ -1298,7 +1308,7 @@ class GoalViolationDetector:
             return name, ("fixable" if diff else None), goal.provision
 
         with ThreadPoolExecutor(max(1, min(self.max_concurrency, len(self.goals)))) as pool:
-            outcomes = list(pool.map(one, self.goals))
+            outcomes = list(pool.map(one, enumerate(self.goals)))
         fixable = [n for n, v, _ in outcomes if v == "fixable"]
         unfixable = [n for n, v, _ in outcomes if v == "unfixable"]
         prov = ProvisionResponse("UNDECIDED")

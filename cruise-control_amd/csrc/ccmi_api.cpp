@@ -244,6 +244,13 @@ extern "C" {
 
 const char* ccmi_last_error(void) { return g_err.c_str(); }
 int32_t ccmi_abi_version(void) { return CCMI_ABI_VERSION; }
+int32_t ccmi_device_count(void) {
+  try {
+    return ccmi::Device::countGfx950();
+  } catch (std::exception&) {
+    return 0;
+  }
+}
 
 int32_t ccmi_topic_broker_set(const char* topic, int32_t num_broker_sets) {
   if (!topic) return -1;

@@ -87,6 +87,17 @@ struct DeviceGuard {
   }
 };
 
+int Device::countGfx950() {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  int k = 0;
+  for (int i = 0; i < n; ++i) {
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, i) == hipSuccess && std::strncmp(prop.gcnArchName, "gfx950", 6) == 0) ++k;
+  }
+  return k;
+}
+
 Device::Device(int ordinal, int B, int R, int P, int T, int maxGoalSlots)
     : ordinal_(ordinal), B_(B), R_(R), P_(P), T_(T), ldB_((B + 3) & ~3), G_(maxGoalSlots) {
   int n = 0;

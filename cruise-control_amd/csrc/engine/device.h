@@ -84,6 +84,7 @@ struct DiskStatsOut {  // ClusterModelStats.populateStatsForDisks partials
 class Device {
  public:
   Device(int ordinal, int B, int R, int P, int T, int maxGoalSlots);
+  static int countGfx950();  // visible gfx950 devices
   ~Device();
   Device(const Device&) = delete;
   Device& operator=(const Device&) = delete;

@@ -7,6 +7,10 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <atomic>
+#include <condition_variable>
+#include <mutex>
+#include <thread>
 
 #include "device.h"
 #include "predicates.h"
@@ -867,6 +871,87 @@ class ReplicaDistribution : public GoalImpl {
 };
 
 // ======================================================================================= ResourceDistributionGoal
+// Builds ResourceDistributionGoal.moveOut's entry-state candidate TreeSet on a helper thread while the driver scans:
+// the same put sequence (members in ascending id, placed by their entry (key, id) rank) the driver would otherwise run
+// when its lazy candidate order stops being exact. Most calls never need the tree: a newer submission cancels the
+// build in flight and the driver never waits except in take(). Used for clusters of at least CCMI_TREE_WORKER_MIN
+// brokers (default 2048; smaller trees are cheaper to build on the driver thread); CCMI_NO_TREE_WORKER=1 disables it.
+class TreeWorker {
+ public:
+  struct RankOnly {  // buildByRank never compares
+    int operator()(int, int) const { return 0; }
+  };
+  using Tree = RbTreeSet<RankOnly>;
+  TreeWorker() : tree_(RankOnly{}), th_([this] { loop(); }) {}
+  ~TreeWorker() {
+    {
+      std::lock_guard<std::mutex> l(mu_);
+      stop_ = true;
+      cancel_.store(true);
+    }
+    cv_.notify_one();
+    th_.join();
+  }
+  // members in entry (key, id) order, over B brokers
+  void submit(const std::vector<int32_t>& order, int B) {
+    {
+      std::lock_guard<std::mutex> l(mu_);
+      next_.assign(order.begin(), order.end());
+      nextB_ = B;
+      ++gen_;
+      cancel_.store(true, std::memory_order_relaxed);  // the build in flight (if any) is stale
+    }
+    cv_.notify_one();
+  }
+  // the latest submission's tree (waits for it); its structure is handed over with RbTreeSet::adopt
+  Tree& take() {
+    const uint64_t want = gen_;  // only the driver thread submits
+    while (done_.load(std::memory_order_acquire) != want) std::this_thread::yield();
+    return tree_;
+  }
+
+ private:
+  void loop() {
+    uint64_t started = 0;
+    for (;;) {
+      uint64_t gen;
+      {
+        std::unique_lock<std::mutex> l(mu_);
+        cv_.wait(l, [&] { return stop_ || gen_ != started; });
+        if (stop_) return;
+        gen = started = gen_;
+        order_.swap(next_);
+        B_ = nextB_;
+        cancel_.store(false, std::memory_order_relaxed);
+      }
+      tree_.clear();
+      rank_.assign(B_, 0);
+      mark_.assign(B_, 0);
+      for (size_t i = 0; i < order_.size(); ++i) {
+        rank_[order_[i]] = (int32_t)i;
+        mark_[order_[i]] = 1;
+      }
+      ids_.clear();
+      for (int x = 0; x < B_; ++x)
+        if (mark_[x]) ids_.push_back(x);
+      tree_.buildByRank(ids_, rank_, &cancel_);
+      if (!cancel_.load(std::memory_order_relaxed)) done_.store(gen, std::memory_order_release);
+    }
+  }
+  Tree tree_;
+  std::vector<int32_t> next_, order_, rank_;
+  std::vector<int> ids_;
+  std::vector<uint8_t> mark_;
+  int nextB_ = 0, B_ = 0;
+  uint64_t gen_ = 0;             // submissions (guarded by mu_; read unguarded by the driver thread, its only writer)
+  std::atomic<uint64_t> done_{0};  // the submission whose tree is complete in tree_
+  std::atomic<bool> cancel_{false};
+  std::mutex mu_;
+  std::condition_variable cv_;
+  bool stop_ = false;
+  std::thread th_;
+};
+
 class ResourceDistribution : public GoalImpl {
  public:
   explicit ResourceDistribution(int kindIn) {
@@ -887,6 +972,7 @@ class ResourceDistribution : public GoalImpl {
   ccmi_provision_recommendation overRec{};  // _overProvisionedRecommendation
   Model::SnapTable snapTab;  // moveIn's candidate-broker snapshots (one Spec per phase)
   std::vector<uint8_t> queued;  // moveIn: broker is in the candidate queue
+  std::unique_ptr<TreeWorker> treeWorker;  // moveOut's entry-state trees
   int nameBase() const { return 4 * kind; }
   int nameId(bool reverse, bool leader) const { return nameBase() + (reverse ? 1 : 0) + (leader ? 2 : 0); }
   bool excluded(int b) const { return !allowed[b]; }
@@ -1108,6 +1194,13 @@ class ResourceDistribution : public GoalImpl {
         }
       }
     }
+    static const bool noWorker = std::getenv("CCMI_NO_TREE_WORKER") != nullptr;
+    const char* minEnv = std::getenv("CCMI_TREE_WORKER_MIN");
+    const bool useWorker = !noWorker && m.B >= (minEnv ? std::atoi(minEnv) : 2048);
+    if (useWorker) {
+      if (!treeWorker) treeWorker = std::make_unique<TreeWorker>();
+      treeWorker->submit(inorder, m.B);  // `inorder` is the members' entry (key, id) order
+    }
     struct Step {
       int dst;
       double keyAfter;
@@ -1126,10 +1219,12 @@ class ResourceDistribution : public GoalImpl {
     auto materialise = [&]() {
       PhaseScope pi(PH_TREE_BUILD);
       ovr = entryKey;
-      // Entry-time (key, id) order of the members: the maintained live order with the few brokers whose key
-      // moved since entry put back at their entry keys; the tree is then built by the same put sequence (ids in
-      // aliveBrokers order) with integer rank compares.
-      {
+      if (useWorker) {
+        cand.adopt(treeWorker->take());
+      } else {
+        // Entry-time (key, id) order of the members: the maintained live order with the few brokers whose key
+        // moved since entry put back at their entry keys; the tree is then built by the same put sequence (ids in
+        // aliveBrokers order) with integer rank compares.
         std::vector<int32_t> order;
         order.reserve(m.B);
         std::vector<uint8_t>& changed = e.scratchB2;

@@ -12,6 +12,7 @@
 // The tree is kept in a flat node array (index links) so an in-order snapshot for a device scan is one walk.
 #pragma once
 #include <algorithm>
+#include <atomic>
 #include <cstdint>
 #include <cstring>
 #include <cmath>
@@ -68,11 +69,39 @@ struct JavaRandom {
 
 // ----------------------------------------------------------------------------------------------
 // java.util.TreeMap<Integer-like key> with an external live comparator. Cmp: int(int a, int b).
-// Nodes are one 24-byte record each (key, links, colour, build rank) so a search step is one cache line.
+// Nodes are one 20-byte record each (key, links, colour) so a search step is one cache line.
+struct RbNode {
+  int key, left, right, parent;
+  int32_t red;
+};
 template <class Cmp>
 class RbTreeSet {
+  template <class>
+  friend class RbTreeSet;
+
  public:
   explicit RbTreeSet(Cmp c) : cmp_(c) {}
+  // Take over the structure (nodes, colours, in-order sequence) of a tree built elsewhere, e.g. by buildByRank on a
+  // helper thread; `o` is left with this tree's old structure.
+  template <class C2>
+  void adopt(RbTreeSet<C2>& o) {
+    n_.swap(o.n_);
+    free_.swap(o.free_);
+    std::swap(root_, o.root_);
+    std::swap(size_, o.size_);
+    std::swap(seqOn_, o.seqOn_);
+    seqId_.swap(o.seqId_);
+    seqKey_.swap(o.seqKey_);
+  }
+  void clear() {
+    n_.clear();
+    free_.clear();
+    root_ = -1;
+    size_ = 0;
+    seqOn_ = false;
+    seqId_.clear();
+    seqKey_.clear();
+  }
   int size() const { return size_; }
   bool add(int k) {
     int t = root_;
@@ -108,7 +137,9 @@ class RbTreeSet {
   // these elements: the same sequence of TreeMap.put calls and therefore the same structure. The search is not
   // walked: a put lands on the one empty link between the new key's in-order neighbours (the predecessor's right
   // link when that is empty, else the successor's left link), found in a two-level bitmap over the ranks.
-  void buildByRank(const std::vector<int>& ids, const std::vector<int32_t>& rank) {
+  // `cancel` (optional) stops the build early (the tree is then incomplete and must be discarded).
+  void buildByRank(const std::vector<int>& ids, const std::vector<int32_t>& rank,
+                   const std::atomic<bool>* cancel = nullptr) {
     n_.reserve(ids.size());
     int32_t nr = 0;
     for (int k : ids) nr = std::max(nr, rank[k] + 1);
@@ -141,7 +172,9 @@ class RbTreeSet {
       wi = (si << 6) | __builtin_ctzll(sm);
       return (wi << 6) | __builtin_ctzll(w[wi]);
     };
+    size_t done = 0;
     for (int k : ids) {
+      if (cancel && (++done & 511) == 0 && cancel->load(std::memory_order_relaxed)) return;
       const int32_t rk = rank[k];
       int e;
       if (root_ < 0) {
@@ -240,10 +273,7 @@ class RbTreeSet {
   }
 
  private:
-  struct Node {
-    int key, left, right, parent;
-    int32_t red;
-  };
+  using Node = RbNode;
   Cmp cmp_;
   std::vector<Node> n_;
   std::vector<int> free_;

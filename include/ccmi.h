@@ -344,6 +344,9 @@ typedef struct ccmi_cluster_buffers ccmi_cluster_buffers; /* owns the arrays beh
 
 const char* ccmi_last_error(void);
 int32_t ccmi_abi_version(void);
+/* Number of visible gfx950 devices (on an MI355X node: HIP ordinals 0..n-1, the `device` of ccmi_session_create);
+ * 0 when none. What-if batches (GoalViolationDetector) spread their sessions over them. */
+int32_t ccmi_device_count(void);
 void ccmi_default_constraint(ccmi_balancing_constraint* out);
 void ccmi_default_random_cluster_props(ccmi_random_cluster_props* out); /* TestConstants.BASE_PROPERTIES */
 

@@ -78,9 +78,10 @@ def test_emu_goal_violation_detector_skips_offline_replicas(emu_lib):
     assert v.skipped_due_to_offline_replicas and v.balancedness_score == -1.0 and not v.fixable
 
 
-def test_emu_proposal_summary_json(emu_lib, oracle_lib):
+def _check_proposal_summary_json(lib):
+    """OptimizerResult.getProposalSummaryForJson (OptimizerResult.java:301-319) over the product's proposals."""
     bc = constraint(1.05, 3000)
-    buf = ccmi.RandomCluster.generate(emu_lib, **PROPS)
+    buf = ccmi.RandomCluster.generate(lib, **PROPS)
     cm = ccmi.ClusterModel.from_buffers(buf)
     res = ccmi.GoalOptimizer(bc).optimizations(cm, ccmi.goals_from_names(DEFAULT_GOALS),
                                                ccmi.OptimizationOptions(excluded_topics=[1, 2],
@@ -108,6 +109,15 @@ def test_emu_proposal_summary_json(emu_lib, oracle_lib):
     oc.optimize(DEFAULT_GOALS, bc, ccmi.OptimizationOptions(excluded_topics=[1, 2], excluded_brokers_for_leadership=[3]))
     key = lambda p: (p.partition, tuple(p.old_replicas), tuple(p.new_replicas), p.old_leader)  # noqa: E731
     assert sorted(map(key, oc.proposals())) == sorted(map(key, props))
+
+
+def test_emu_proposal_summary_json(emu_lib, oracle_lib):
+    _check_proposal_summary_json(emu_lib)
+
+
+@pytest.mark.gpu
+def test_gpu_proposal_summary_json(gpu_lib, oracle_lib):
+    _check_proposal_summary_json(gpu_lib)
 
 
 def test_emu_intra_broker_summary(emu_lib):

@@ -14,3 +14,9 @@ f=$(find gpurun_out/prof_${TAG:-r03} -name '*kernel_trace.csv' | head -1)
 python3 tools/trace_hist.py "$f" > gpurun_out/trace_hist_${TAG:-r03}.txt
 find gpurun_out/prof_${TAG:-r03} -name '*kernel_trace.csv' -delete
 cat gpurun_out/trace_hist_${TAG:-r03}.txt | head -40
+if [ -n "${PYTEST_K:-}" ]; then
+  echo "== pytest -m gpu -k ${PYTEST_K} $(date +%T)"
+  timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 150 --timeout-method thread -k "${PYTEST_K}" \
+    > gpurun_out/pytest_${TAG:-r03}.log 2>&1
+  rc=$?; tail -5 gpurun_out/pytest_${TAG:-r03}.log; exit $rc
+fi
