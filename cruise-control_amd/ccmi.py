@@ -50,6 +50,8 @@ GOAL_KINDS: Dict[str, int] = {
     "RackAwareDistributionGoal": 19,
     "BrokerSetAwareGoal": 20,
     "TopicLeaderReplicaDistributionGoal": 21,
+    "KafkaAssignerEvenRackAwareGoal": 22,
+    "KafkaAssignerDiskUsageDistributionGoal": 23,
 }
 GOAL_NAMES = {v: k for k, v in GOAL_KINDS.items()}
 # default.goals in priority order (config/constants/AnalyzerConfig.java:352-367, TestConstants.DEFAULT_GOALS_VALUES)
@@ -66,7 +68,9 @@ C1_GOALS = ("ReplicaDistributionGoal", "DiskUsageDistributionGoal", "NetworkInbo
 INTRA_BROKER_GOALS = ("IntraBrokerDiskCapacityGoal", "IntraBrokerDiskUsageDistributionGoal")
 # Goals whose drivers are implemented in this build.
 IMPLEMENTED = DEFAULT_GOALS + INTRA_BROKER_GOALS + ("PreferredLeaderElectionGoal", "RackAwareDistributionGoal",
-                                                   "BrokerSetAwareGoal", "TopicLeaderReplicaDistributionGoal")
+                                                   "BrokerSetAwareGoal", "TopicLeaderReplicaDistributionGoal",
+                                                   "KafkaAssignerEvenRackAwareGoal",
+                                                   "KafkaAssignerDiskUsageDistributionGoal")
 # replica.to.broker.set.mapping.policy.class values (include/ccmi.h ccmi_broker_set_policy)
 BROKER_SET_POLICIES = {"TopicNameHashBrokerSetMappingPolicy": 0, "ReplicaToOriginalBrokerSetMappingPolicy": 1}
 
@@ -461,7 +465,8 @@ class Goal:
     # IntraBrokerDiskCapacityGoal return true (analyzer/goals/*.java)
     HARD_GOALS = ("RackAwareGoal", "RackAwareDistributionGoal", "BrokerSetAwareGoal", "ReplicaCapacityGoal",
                   "DiskCapacityGoal", "NetworkInboundCapacityGoal", "NetworkOutboundCapacityGoal", "CpuCapacityGoal",
-                  "IntraBrokerDiskCapacityGoal")
+                  "IntraBrokerDiskCapacityGoal", "KafkaAssignerEvenRackAwareGoal",
+                  "KafkaAssignerDiskUsageDistributionGoal")
 
     def is_hard_goal(self) -> bool:
         return self._name in self.HARD_GOALS

@@ -274,6 +274,8 @@ void Device::stopServer() {
   if (!serverOn_) return;
   DeviceGuard dg(ordinal_);
   ServerCmd* c = (ServerCmd*)fg_;
+  *(volatile unsigned long long*)&c->seq = (seq_ + 1) | kSeqBusy;  // seqlock (devtypes.h kSeqBusy)
+  hostStoreFence();
   volatile int32_t* op = &c->op;
   *op = SOP_EXIT;
   hostStoreFence();
@@ -376,14 +378,29 @@ int64_t Device::serverRun(const DevProgram& prog, const Staged& g, int op, const
   c.oT = (uint32_t)(oRows + g.otd);
   c.oA = (uint32_t)oA;
   c.oC = (uint32_t)oC;
-  // every field but the sequence word, then (behind a store fence) the sequence word
+  const bool rowsSent = (g.nb | g.nr | g.np | g.nt) != 0;
+  c.rowsEpoch = rowsEpoch_;
+  // seqlock: the sequence word marked busy, every other field, then (behind store fences) the sequence word
+  *(volatile unsigned long long*)fg_ = (seq_ + 1) | kSeqBusy;
+  hostStoreFence();
   std::memcpy(fg_ + sizeof(unsigned long long), (const char*)&c + sizeof(unsigned long long),
               sizeof(ServerCmd) - sizeof(unsigned long long));
   hostStoreFence();
   lastCmdSeq_ = ++seq_;
   *(volatile unsigned long long*)fg_ = lastCmdSeq_;
   hostStoreFence();
-  waitMail(seq_);
+  if (!waitMail(seq_, true)) {
+    // The server's idle watchdog ended it just before it could see this command (a session host that stayed away
+    // for seconds): nothing of the command ran, so it goes through a launch like any scan the server declines.
+    serverOn_ = false;
+    {
+      std::lock_guard<std::mutex> lk(g_serverMu);
+      g_serverWgs[ordinal_ & 63] -= serverBlocks_;
+    }
+    perf.serverIdleExits++;
+    return INT64_MIN;
+  }
+  if (rowsSent) ++rowsEpoch_;
   lastServerUse_ = nowSeconds();
   perf.serverScans++;
   perf.serverBusyMs += (double)hResult_[1] * 1e-5;  // 100 MHz ticks
@@ -619,8 +636,9 @@ void Device::launchPrepFor(const Staged& g, size_t reqBytes, bool scan) {
 }
 
 // Spin on the host-mapped mailbox for `seq`; a stream error (or a stream that drained without publishing)
-// is reported instead of spinning forever.
-void Device::waitMail(unsigned long long seq) {
+// is reported instead of spinning forever. With `serverCmd`, a server that its idle watchdog ended before it saw the
+// command (exit record {1, seq - 1}) returns false instead.
+bool Device::waitMail(unsigned long long seq, bool serverCmd) {
   PhaseScope ps(PH_SCAN_WAIT);
   volatile unsigned long long* mail = hResult_;
   const unsigned long long want = seq & 0xffffffffull;
@@ -630,6 +648,8 @@ void Device::waitMail(unsigned long long seq) {
       const hipError_t q = hipStreamQuery(ST);
       if (q == hipSuccess) {
         if ((__atomic_load_n(&mail[0], __ATOMIC_ACQUIRE) >> 32) == want) break;
+        const unsigned long long ex = __atomic_load_n(&mail[3], __ATOMIC_ACQUIRE);
+        if (serverCmd && (ex >> 32) == 1 && (ex & 0xffffffffull) == ((seq - 1) & 0xffffffffull)) return false;
         char msg[256];
         std::snprintf(msg, sizeof(msg),
                       "scan finished without publishing its result (seq %llu, mail %016llx, server %s, server exit "
@@ -646,6 +666,7 @@ void Device::waitMail(unsigned long long seq) {
     else __builtin_ia32_pause();
   }
   perf.syncs++;
+  return true;
 }
 
 // A shard with nothing to scan still applies its pending row updates so every shard's tables stay identical.
@@ -1199,7 +1220,7 @@ void Device::uploadDisks(int D, const int32_t* bDiskOff, const int32_t* bDisks, 
   dallocTracked(&dCOff_, (size_t)B_ + 1, o);
   dallocTracked(&dEOff_, (size_t)B_ + 1, o);
   dallocTracked(&dNSel_, (size_t)B_, o);
-  dallocTracked(&dDiskStats_, 1, o);
+  dallocTracked(&dDiskStats_, 1 + kDiskStatsBlocks, o);
   hipCheck(hipMemcpy(dBDiskOff_, bDiskOff, sizeof(int32_t) * (B_ + 1), hipMemcpyHostToDevice), "upload bDiskOff");
   hipCheck(hipMemcpy(dBDisks_, bDisks, sizeof(int32_t) * D, hipMemcpyHostToDevice), "upload bDisks");
   hipCheck(hipMemcpy(dDCap_, dCap, sizeof(double) * D, hipMemcpyHostToDevice), "upload dCap");

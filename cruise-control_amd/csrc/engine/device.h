@@ -48,6 +48,7 @@ struct DevicePerf {
   int64_t crossRequired = 0;
   double crossKernelMs = 0;
   int64_t serverLaunches = 0;  // K8 scan_server launches (each serves many scans)
+  int64_t serverIdleExits = 0;  // commands the server watchdog ended before it saw them (then launched)
   int64_t serverScans = 0;     // scans served by a running scan_server (no launch each)
   double serverBusyMs = 0;     // their device busy time (s_memrealtime, command seen -> result published)
   int64_t serverPayloadBytes = 0;  // command payload written through the BAR (program, rows, request arrays)
@@ -80,6 +81,7 @@ struct DiskStatsOut {  // ClusterModelStats.populateStatsForDisks partials
   double varSum;
   int32_t unbalanced, numAlive;
 };
+constexpr int kDiskStatsBlocks = 256;  // stats_disks workgroups (partials folded by one wave)
 
 class Device {
  public:
@@ -227,7 +229,7 @@ class Device {
   UpdateList overlayFor(const Staged& g) const;
   MutTables mutTables() const;
   const char* stageScan(const Staged& g, size_t req, bool readsTopicCounts, UpdateList& u);
-  void waitMail(unsigned long long seq);
+  bool waitMail(unsigned long long seq, bool serverCmd = false);
   int64_t finishScan();
   unsigned long long* stamps_ = nullptr;
   // scan server state: the fine-grained VRAM block [ServerCmd | payload] the host writes through the BAR
@@ -242,6 +244,7 @@ class Device {
   DevProgram lastProg_{};
   unsigned long long* dServerT0_ = nullptr;
   unsigned long long lastCmdSeq_ = 0;  // the sequence word the command block holds
+  int32_t rowsEpoch_ = 0;              // server commands with rows so far (ServerCmd.rowsEpoch)
   double lastServerUse_ = 0;  // steady-clock seconds of the last served scan (the host restarts an idle server)
   bool serveScan(const DevProgram& prog, const Staged& g, bool readsTopicCounts);
   const int32_t *rowBroker_ = nullptr, *rowPart_ = nullptr, *partTopic_ = nullptr;

@@ -233,8 +233,13 @@ struct alignas(16) ServerCmd {
   uint32_t oProg, oB, oR, oP, oT, oA, oC;
   int32_t nSegs;    // SOP_SEGS: entries of the segment table
   int32_t nActive;  // workgroups [0, nActive) take part (a multiple of 8); the others only follow the sequence
-  int32_t pad;
+  // commands with rows before this one since the session started: a workgroup takes an agent acquire before it reads
+  // the tables whenever this differs from the value it last acquired at (rows of commands it skipped included)
+  int32_t rowsEpoch;
 };
+// The sequence word is a seqlock: the host stores (next | kSeqBusy) before it rewrites the other fields and `next`
+// after; a workgroup accepts a header only when the word it read before and after its copy is the same, not busy.
+constexpr unsigned long long kSeqBusy = 1ull << 63;
 static_assert(sizeof(ServerCmd) % 16 == 0, "ServerCmd words");
 
 // Device-resident Java loads and partition slot order, so chain kernels can apply moves themselves (apply.h).

@@ -129,10 +129,13 @@ DevProgram Engine::program(const GoalImpl& self, int action) const {
   DevProgram p;
   std::memset(&p, 0, sizeof(p));
   p.action = action;
-  p.nGoals = 1 + (int)optimized.size();
+  // the conjunction of AnalyzerUtils.isProposalAcceptableForOptimizedGoals ends at a terminal goal (it throws)
+  size_t nOpt = 0;
+  while (nOpt < optimized.size() && !(nOpt > 0 && optimized[nOpt - 1]->terminal)) ++nOpt;
+  p.nGoals = 1 + (int)nOpt;
   if (p.nGoals > kMaxGoals) throw Unsupported("too many goals in one chain");
   p.goals[0] = self.dg;
-  for (size_t i = 0; i < optimized.size(); ++i) p.goals[i + 1] = optimized[i]->dg;
+  for (size_t i = 0; i < nOpt; ++i) p.goals[i + 1] = optimized[i]->dg;
   p.needs = 0;
   for (int i = 0; i < p.nGoals; ++i) p.needs |= needsOf(p.goals[i]);
   p.filter = FILTER_NONE;
@@ -250,6 +253,7 @@ int64_t Engine::crossScan(GoalImpl& self, int action, const std::vector<int32_t>
   if (!found) key = scanRows(done, K - done, N);
   if (windows && key >= 0 && N > 2 * kProbeCols && !(self.probeHitRate > 0.9))  // learn whether the probe would win
     self.probeHitRate = 0.95 * self.probeHitRate + (key < kProbeCols ? 0.05 : 0.0);
+  checkTerminal(key);
   if (count) {
     if (prog.exclLeadMove || prog.newOnly) candidates += exclLeadCount(prog, reps.data() + r0, K, cands, key);
     else candidates += key >= 0 ? key + 1 : (int64_t)K * N;
@@ -277,6 +281,7 @@ int64_t Engine::crossScanSegs(GoalImpl& self, int action, const std::vector<Snap
   m.flushToDevice();
   prog.filter = FILTER_NONE;
   const int64_t key = combine(dev->scanSegs(prog, segs, cands.data(), N, 0, N));
+  checkTerminal(key);
   candidates += key >= 0 ? key + 1 : K * N;
   return key;
 }
@@ -305,6 +310,7 @@ int64_t Engine::pairScan(GoalImpl& self, const std::vector<int32_t>& pr, const s
   const int p0 = (int)((int64_t)n * shard.rank / shard.count), p1 = (int)((int64_t)n * (shard.rank + 1) / shard.count);
   const DevProgram prog = program(self, action);
   const int64_t key = combine(dev->scanPairs(prog, pr.data(), pb.data(), p0, p1));
+  checkTerminal(key);
   if (!count) return key;
   if (prog.exclLeadMove || prog.newOnly) {
     const size_t end = key >= 0 ? (size_t)key + 1 : pr.size();
@@ -347,13 +353,25 @@ int64_t Engine::swapScan(GoalImpl& self, const std::vector<int32_t>& srcs, const
                                     cbRep.data(), (int)cbRep.size(), &visited);
   if (throwRow >= 0 && (key < 0 || (key >> 24) > throwRow))
     throw Unsupported("UnsupportedOperationException: removeIf on an unmodifiable sorted replica view");
+  checkTerminal(key);
   candidates += visited;
   return key;
 }
 
 bool Engine::chainsOn() const {
   static const bool off = std::getenv("CCMI_NO_CHAINS") != nullptr;
-  return !off && shard.count <= 1;
+  return !off && shard.count <= 1 && !terminalOptimized();  // a chain would apply the move a terminal goal refuses
+}
+
+bool Engine::terminalOptimized() const {
+  for (const auto& g : optimized)
+    if (g->terminal) return true;
+  return false;
+}
+void Engine::checkTerminal(int64_t key) const {
+  if (key < 0) return;
+  for (const auto& g : optimized)
+    if (g->terminal) throw StateError("No goal should be executed after " + g->name);
 }
 
 int64_t Engine::chainPairs(GoalImpl& self, int action, const std::vector<int32_t>& pr, const std::vector<int32_t>& pb,
@@ -403,6 +421,7 @@ int Engine::acceptance(int gi, const ccmi_action& a) {
     if (a.type == CCMI_INTRA_BROKER_REPLICA_MOVEMENT || a.type == CCMI_INTRA_BROKER_REPLICA_SWAP)
       throw std::invalid_argument("Unsupported balancing action " + std::to_string(a.type) + " is provided.");
   }
+  if (optimized.at(gi)->terminal) throw StateError("No goal should be executed after " + optimized.at(gi)->name);
   std::vector<const std::vector<uint8_t>*> allowedBySlot;
   for (auto& g : optimized) allowedBySlot.push_back(&g->allowed);
   HostView v{m, allowedBySlot, topicUpper, topicLower, brokerSetOf, replicaSetOf, minLeadOf, topicLeadLim};
@@ -528,9 +547,10 @@ bool Engine::optimizeGoal(std::unique_ptr<GoalImpl> g, ccmi_goal_result* res) {
   g->prov = provisionResponse(CCMI_PROVISION_UNDECIDED);  // AbstractGoal.java:87
   try {
     return optimizeGoalImpl(g, res, t0, c0, a0, l0, p0);
-  } catch (OptimizationFailure& f) {  // AbstractGoal.java:125-126
-    lastFailure = f.hasRec ? provisionResponse(CCMI_PROVISION_UNDER_PROVISIONED, f.rec)
-                           : provisionResponse(CCMI_PROVISION_UNDER_PROVISIONED);
+  } catch (OptimizationFailure& f) {  // AbstractGoal.java:125-126 (a Goal outside that template keeps its own response)
+    lastFailure = !g->abstractGoal ? g->prov
+                  : f.hasRec      ? provisionResponse(CCMI_PROVISION_UNDER_PROVISIONED, f.rec)
+                                  : provisionResponse(CCMI_PROVISION_UNDER_PROVISIONED);
     throw;
   }
 }

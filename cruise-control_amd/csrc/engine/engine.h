@@ -76,6 +76,10 @@ class GoalImpl {
   ccmi_provision_response prov{};  // Goal.provisionResponse
   // crossScan's first-row probe (Engine::crossScan): recent share of scans won within the probe's columns
   double probeHitRate = 0.0;
+  // Goal.actionAcceptance throws IllegalStateException (KafkaAssignerDiskUsageDistributionGoal): as an optimized goal
+  // it ends the optimization at the first candidate that reaches it (Engine::program stops the conjunction there)
+  bool terminal = false;
+  bool abstractGoal = true;  // extends AbstractGoal (its optimize turns an OptimizationFailureException into UNDER)
   virtual void init(Engine& e) = 0;
   virtual void rebalance(Engine& e, int b) = 0;
   virtual void update(Engine& e) = 0;
@@ -123,6 +127,8 @@ class Engine {
                         int64_t key) const;
   bool blocked(const DevProgram& prog, int r, int b) const;
   bool exclOnDevice = false;  // the device's broker exclusion bits are set
+  bool terminalOptimized() const;  // an optimized goal is `terminal`
+  void checkTerminal(int64_t key) const;  // a candidate reached a terminal optimized goal: IllegalStateException
   int64_t pairScan(GoalImpl& self, const std::vector<int32_t>& pr, const std::vector<int32_t>& pb,
                    int action = DA_LEADERSHIP, bool count = true);
   int64_t swapScan(GoalImpl& self, const std::vector<int32_t>& srcs, const std::vector<int32_t>& cbOff,

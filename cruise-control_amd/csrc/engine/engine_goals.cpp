@@ -22,6 +22,7 @@
 //   GoalUtils.ensureNoOfflineReplicas       analyzer/goals/GoalUtils.java:307-318
 #include <algorithm>
 #include <cmath>
+#include <limits>
 #include <set>
 #include <unordered_map>
 
@@ -2175,6 +2176,360 @@ class PreferredLeaderElection : public GoalImpl {
   int compareStats(const ccmi_cluster_stats&, const ccmi_cluster_stats&) const override { return 0; }
 };
 
+// ======================================================================================= Kafka-assigner mode goals
+// analyzer/kafkaassigner/KafkaAssignerEvenRackAwareGoal.java and KafkaAssignerDiskUsageDistributionGoal.java (in
+// `goals`, not in default.goals). Both implement Goal directly: no candidate conjunction over optimized goals, so
+// their decisions are made on the host (rack membership tests and replica-size searches over one broker pair);
+// as optimized goals they act through the device predicates (EvenRackAware: the rack-awareness predicate, identical
+// to RackAwareGoal's acceptance; DiskUsageDistribution: terminal, any later candidate ends the optimization).
+
+// getPartitionsByTopic: topics by name, each topic's partitions in HashMap<TopicPartition, Partition> order
+std::vector<std::vector<int32_t>> kaPartitionsByTopic(const Model& m) {
+  PartitionOrder po{&m};
+  JHashSet<PartitionOrder> all(&po);
+  for (int p = 0; p < m.P; ++p) all.add(p, jMix(jMix(1, m.pNumber[p]), m.topicHash[m.pTopic[p]]));
+  std::vector<int32_t> order;
+  all.order(order);
+  std::vector<std::vector<int32_t>> byTopic(m.T);
+  for (int p : order) byTopic[m.pTopic[p]].push_back(p);
+  std::vector<int> topics(m.T);
+  for (int t = 0; t < m.T; ++t) topics[t] = t;
+  std::sort(topics.begin(), topics.end(), [&m](int a, int b) { return m.topicNames[a] < m.topicNames[b]; });
+  std::vector<std::vector<int32_t>> out;
+  for (int t : topics)
+    if (!byTopic[t].empty()) out.push_back(std::move(byTopic[t]));
+  return out;
+}
+
+// KafkaAssignerUtils.sanityCheckOptimizationOptions (KafkaAssignerUtils.java:20-26)
+void kaSanityCheck(const Engine& e) {
+  if (e.opt.triggered) throw std::invalid_argument("Kafka Assigner goals do not support usage by goal violation detector.");
+  if (e.opt.onlyImmigrants)
+    throw std::invalid_argument("Kafka Assigner goals do not support usage of modifying topic replication factor.");
+}
+
+class KafkaAssignerEvenRackAware : public GoalImpl {
+ public:
+  KafkaAssignerEvenRackAware() {
+    kind = CCMI_GOAL_KAFKA_ASSIGNER_EVEN_RACK_AWARE;
+    name = "KafkaAssignerEvenRackAwareGoal";
+    abstractGoal = false;
+  }
+  void init(Engine& e) override {
+    kaSanityCheck(e);
+    if (!e.optimized.empty())
+      throw std::invalid_argument("Goals " + std::to_string(e.optimized.size()) + " cannot be optimized before " + name + ".");
+    allowed.assign(e.m.B, 1);
+    dg = DevGoal{};
+    dg.kind = DG_RACK_AWARE;  // actionAcceptance (:385-408): the rack-awareness test of RackAwareGoal
+    dg.allowedSlot = (int)e.optimized.size();
+  }
+  // Replica.toString (Replica.java:338-343); racks are named by their index
+  static std::string replicaString(const Model& m, int r) {
+    auto tf = [](bool v) { return std::string(v ? "true" : "false"); };
+    const int p = m.rPart[r], b = m.rBroker[r];
+    return "Replica[isLeader=" + tf(m.rLeader[r] != 0) + ",rack=" + std::to_string(m.bRack[b]) + ",broker=" +
+           std::to_string(m.bId[b]) + ",TopicPartition=" + m.topicNames[m.pTopic[p]] + "-" + std::to_string(m.pNumber[p]) +
+           ",origBroker=" + std::to_string(m.bId[m.rOrig[r]]) + ",isOriginalOffline=" + tf(m.origOffline(r)) +
+           ",isCurrentOffline=" + tf(m.curOffline(r)) + "]";
+  }
+  // optimize (:119-165)
+  bool rebalanceAll(Engine& e) override {
+    PhaseScope ps(PH_OTHER_GOALS);
+    Model& m = e.m;
+    auto excl = [&](int t) { return e.opt.anyExclTopic && e.opt.exclTopic[t] != 0; };
+    // ensureRackAwareSatisfiable (:318-343): distinct racks with an alive broker
+    std::vector<uint8_t> rackAlive(m.B + 1, 0);
+    int racks = 0;
+    for (int b = 0; b < m.B; ++b)
+      if (m.alive(b) && !rackAlive[m.bRack[b]]) {
+        rackAlive[m.bRack[b]] = 1;
+        ++racks;
+      }
+    std::vector<int32_t> rf(m.T, 0);
+    for (int p = 0; p < m.P; ++p) rf[m.pTopic[p]] = std::max<int32_t>(rf[m.pTopic[p]], m.pOff[p + 1] - m.pOff[p]);
+    if (e.opt.anyExclTopic) {
+      std::vector<int32_t> seen, order;
+      for (int t = 0; t < m.T; ++t) seen.push_back(t);
+      TopicOrder to{&m};
+      TopicSet ts(&to);
+      for (int t : seen) ts.add(t, m.topicHash[t]);
+      ts.order(order);  // _replicationFactorByTopic: a HashMap<String, Integer>
+      int maxRf = 1;
+      for (int t : order) {
+        if (excl(t)) continue;
+        maxRf = std::max(maxRf, (int)rf[t]);
+        if (maxRf > racks)
+          throw OptimizationFailure("[" + name + "] Insufficient number of racks to distribute included replicas (Current: " +
+                                    std::to_string(racks) + ", Needed: " + std::to_string(maxRf) + ").");
+      }
+    } else if (m.maxRf > racks) {
+      throw OptimizationFailure("[" + name + "] Insufficient number of racks to distribute each replica (Current: " +
+                                std::to_string(racks) + ", Needed: " + std::to_string(m.maxRf) + ").");
+    }
+    const auto byTopic = kaPartitionsByTopic(m);
+    // brokers by (replica count at the position, id); the count starts at the excluded topics' replicas there
+    std::vector<std::vector<int32_t>> excludedAt(m.maxRf, std::vector<int32_t>(m.B, 0));
+    for (const auto& parts : byTopic)
+      for (int p : parts) {
+        if (!excl(m.pTopic[p])) continue;
+        excludedAt[0][m.rBroker[m.pLeader[p]]]++;
+        int pos = 0;
+        for (int s = m.pOff[p]; s < m.pOff[p + 1]; ++s)
+          if (m.pSlots[s] != m.pLeader[p] && ++pos < m.maxRf) excludedAt[pos][m.rBroker[m.pSlots[s]]]++;
+      }
+    std::vector<std::set<std::pair<int, int>>> counts(m.maxRf);
+    for (int i = 0; i < m.maxRf; ++i)
+      for (int b = 0; b < m.B; ++b)
+        if (m.alive(b)) counts[i].insert({excludedAt[i][b], m.bId[b]});
+    // STEP1: the leader first
+    for (const auto& parts : byTopic)
+      for (int p : parts) {
+        int at = m.pOff[p];
+        while (m.pSlots[at] != m.pLeader[p]) ++at;
+        if (at != m.pOff[p]) m.swapSlots(p, 0, at - m.pOff[p]);
+      }
+    // STEP2: every position over every partition, the first (count, id) broker off the racks of the earlier positions
+    std::vector<int32_t> rackOfId(m.B);
+    for (int b = 0; b < m.B; ++b) rackOfId[m.bId[b]] = m.bRack[b];
+    for (int pos = 0; pos < m.maxRf; ++pos)
+      for (const auto& parts : byTopic)
+        for (int p : parts) {
+          const int n = m.pOff[p + 1] - m.pOff[p];
+          if (n <= pos) continue;
+          const int r = m.pSlots[m.pOff[p] + pos];
+          if (excl(m.pTopic[p]) && !m.origOffline(r)) continue;  // shouldExclude (:307-310)
+          int usedRacks[kMaxRf], nr = 0;
+          for (int q = 0; q < pos; ++q) usedRacks[nr++] = m.bRack[m.rBroker[m.pSlots[m.pOff[p] + q]]];
+          auto& set = counts[pos];
+          bool placed = false;
+          for (auto it = set.begin(); it != set.end(); ++it) {
+            const int dest = it->second;  // broker id == index (model.cpp)
+            bool rackUsed = false;
+            for (int q = 0; q < nr; ++q) rackUsed |= usedRacks[q] == rackOfId[dest];
+            if (rackUsed) continue;
+            const int src = m.rBroker[r];
+            const int there = m.replicaOn(p, dest);
+            if (there < 0) {
+              m.relocateReplica(p, src, dest);
+            } else if (dest != src && m.alive(src)) {
+              if (pos == 0) {
+                m.relocateLeadership(p, src, dest);
+              } else {
+                int at = 0;
+                while (m.rBroker[m.pSlots[m.pOff[p] + at]] != dest) ++at;
+                if (m.rLeader[m.pSlots[m.pOff[p] + pos]] || m.rLeader[m.pSlots[m.pOff[p] + at]])
+                  throw std::invalid_argument("not a follower");  // Partition.swapFollowerPositions (:162-172)
+                m.swapSlots(p, pos, at);
+              }
+            } else if (!m.alive(src)) {
+              continue;
+            }
+            const std::pair<int, int> up{it->first + 1, it->second};
+            set.erase(it);
+            set.insert(up);
+            placed = true;
+            break;
+          }
+          if (!placed)
+            throw OptimizationFailure("[" + name + "] Unable to apply move for replica " +
+                                      replicaString(m, m.pSlots[m.pOff[p] + pos]) + ".");
+        }
+    ensureNoOfflineReplicas(m, name);
+    // ensureRackAware (:351-373): every included partition on distinct racks
+    for (int p = 0; p < m.P; ++p) {
+      if (excl(m.pTopic[p])) continue;
+      for (int s = m.pOff[p]; s < m.pOff[p + 1]; ++s)
+        for (int u = s + 1; u < m.pOff[p + 1]; ++u)
+          if (m.bRack[m.rBroker[m.pSlots[s]]] == m.bRack[m.rBroker[m.pSlots[u]]])
+            throw OptimizationFailure("Optimization for goal " + name + " failed for rack-awareness of partition " +
+                                      m.topicNames[m.pTopic[p]] + "-" + std::to_string(m.pNumber[p]));
+    }
+    succeeded = true;
+    return true;
+  }
+  void rebalance(Engine&, int) override {}
+  void update(Engine&) override { finished = true; }
+  int compareStats(const ccmi_cluster_stats&, const ccmi_cluster_stats&) const override { return 0; }
+};
+
+class KafkaAssignerDiskUsageDistribution : public GoalImpl {
+ public:
+  KafkaAssignerDiskUsageDistribution() {
+    kind = CCMI_GOAL_KAFKA_ASSIGNER_DISK_USAGE_DISTRIBUTION;
+    name = "KafkaAssignerDiskUsageDistributionGoal";
+    terminal = true;  // actionAcceptance throws IllegalStateException (:540-543)
+    abstractGoal = false;
+  }
+  void init(Engine& e) override {
+    kaSanityCheck(e);
+    allowed.assign(e.m.B, 1);
+    dg = DevGoal{};
+    dg.kind = DG_ACCEPT_ALL;
+    dg.allowedSlot = (int)e.optimized.size();
+  }
+
+  // optimize (:107-144) with checkAndOptimize (:197-252), swapReplicas (:268-383), isOptimized (:156-181)
+  bool rebalanceAll(Engine& e) override {
+    PhaseScope ps(PH_OTHER_GOALS);
+    Model& m = e.m;
+    const ReplicaOrder ro{&m};
+    auto size = [&m](int r) { return m.ru(r, R_DISK); };
+    auto usage = [&m](int b) {  // diskUsage(Broker) (:577-581)
+      const double cap = m.cap(b, R_DISK);
+      return jcmpDouble(cap, 0.0) < 1 ? 0.0 : m.bu(b, R_DISK) / cap;
+    };
+    auto bsize = [&](int b) { return usage(b) * m.cap(b, R_DISK); };
+    auto excl = [&](int r) { return e.opt.anyExclTopic && e.opt.exclTopic[m.pTopic[m.rPart[r]]] != 0; };
+    const double mean = m.clusterUtil(R_DISK) / m.clusterCap[R_DISK];
+    const double margin = (e.bc.resBalance[R_DISK] - 1) * kBalanceMargin;
+    const double upper = mean * (1 + margin), lower = mean * jmax(0, (1 - margin));
+    // BrokerAndSortedReplicas: per alive broker a TreeSet by (replica size, Replica.compareTo) on live keys
+    auto rcmp = [&](int x, int y) {
+      const int c = jcmpDouble(size(x), size(y));
+      return c ? c : ro.cmp(x, y);
+    };
+    using Sorted = RbTreeSet<decltype(rcmp)>;
+    std::vector<std::unique_ptr<Sorted>> sorted(m.B);
+    std::vector<int32_t> reps, all;
+    for (int b = 0; b < m.B; ++b) {
+      if (!m.alive(b)) continue;
+      all.push_back(b);
+      sorted[b] = std::make_unique<Sorted>(rcmp);
+      m.bReplicaSet[b].order(reps);
+      for (int r : reps) sorted[b]->add(r);
+    }
+    auto brokerLess = [&](int x, int y) {
+      const int c = jcmpDouble(usage(x), usage(y));
+      return c ? c < 0 : m.bId[x] < m.bId[y];
+    };
+    std::sort(all.begin(), all.end(), brokerLess);
+    // a fresh TreeSet<ReplicaWrapper> of a broker's sorted replicas (followersOnly: !isLeader or excluded topic)
+    std::vector<int> tmp;
+    auto wrappers = [&](int b, bool followersOnly, std::vector<int32_t>& out) {
+      sorted[b]->inorder(tmp);
+      out.clear();
+      for (int r : tmp)
+        if (followersOnly ? (!m.rLeader[r] || excl(r)) : !excl(r)) out.push_back(r);
+      std::sort(out.begin(), out.end(), [&](int x, int y) { return rcmp(x, y) < 0; });
+      out.erase(std::unique(out.begin(), out.end(), [&](int x, int y) { return rcmp(x, y) == 0; }), out.end());
+    };
+    auto onRack = [&m](int p, int rack) {  // partition(tp).partitionRacks() contains rack
+      for (int s = m.pOff[p]; s < m.pOff[p + 1]; ++s)
+        if (m.bRack[m.rBroker[m.pSlots[s]]] == rack) return true;
+      return false;
+    };
+    auto canSwap = [&](int r1, int r2) {  // (:504-518)
+      const int b1 = m.rBroker[r1], b2 = m.rBroker[r2];
+      const bool sameRack = b1 != b2 && m.bRack[b1] == m.bRack[b2];
+      const bool aware = !onRack(m.rPart[r1], m.bRack[b2]) && !onRack(m.rPart[r2], m.bRack[b1]);
+      return (sameRack || aware) && m.rLeader[r1] == m.rLeader[r2];
+    };
+    // findReplicaToSwapWith (:398-466): nearest to the target size first, from both sides of it
+    auto findWith = [&](int r1, const std::vector<int32_t>& w, double target, double minS, double maxS) -> int {
+      if (minS > maxS) return -1;
+      if (jcmpDouble(minS, maxS) > 0) throw std::invalid_argument("fromKey > toKey");
+      const auto lo = std::partition_point(w.begin(), w.end(), [&](int r) { return jcmpDouble(size(r), minS) <= 0; });
+      const auto hi = std::partition_point(lo, w.end(), [&](int r) { return jcmpDouble(size(r), maxS) < 0; });
+      if (lo == hi) return -1;
+      const long upEnd = hi - w.begin(), downEnd = lo - w.begin();
+      bool asc = false, desc = false;
+      long up = 0, down = -1;
+      if (target <= minS) {
+        asc = true;
+        up = lo - w.begin();
+      } else if (target >= maxS) {
+        desc = true;
+        down = upEnd - 1;
+      } else {  // tailSet((MIN_REPLICA, target), true) ascending, headSet((MAX_REPLICA, target), true) descending
+        asc = desc = true;
+        up = std::partition_point(lo, hi, [&](int r) { return jcmpDouble(size(r), target) < 0; }) - w.begin();
+        down = (std::partition_point(lo, hi, [&](int r) { return jcmpDouble(size(r), target) <= 0; }) - w.begin()) - 1;
+      }
+      long low = -1, high = -1, cand = -1;
+      for (;;) {
+        if (cand == high) high = asc && up < upEnd ? up++ : -1;
+        if (cand == low) low = desc && down >= downEnd ? down-- : -1;
+        if (high < 0 && low < 0) return -1;
+        if (high < 0) cand = low;
+        else if (low < 0) cand = high;
+        else cand = (target - size(w[low])) <= (size(w[high]) - target) ? low : high;
+        if (canSwap(r1, w[cand])) return w[cand];
+      }
+    };
+    std::vector<int32_t> mine, leadW, follW;
+    auto swapReplicas = [&](int a, int bw) {
+      const double capA = m.cap(a, R_DISK), capW = m.cap(bw, R_DISK);
+      const double sizeToChange = capA * mean - bsize(a);
+      wrappers(a, false, mine);
+      wrappers(bw, false, leadW);
+      wrappers(bw, true, follW);
+      const size_t n = mine.size();
+      for (size_t k = 0; k < n; ++k) {
+        const int r = sizeToChange > 0 ? mine[k] : mine[n - 1 - k];
+        if (excl(r)) continue;
+        // possibleToMove (:481-491)
+        const int p = m.rPart[r];
+        if (!(!onRack(p, m.bRack[bw]) || (m.bRack[m.rBroker[r]] == m.bRack[bw] && m.replicaOn(p, bw) < 0))) continue;
+        const std::vector<int32_t>& w = m.rLeader[r] ? leadW : follW;
+        const double s = size(r);
+        if (sizeToChange < 0 && s == 0) break;
+        double maxSize = std::numeric_limits<double>::max(), minSize = std::numeric_limits<double>::denorm_min();
+        if (sizeToChange > 0) {
+          minSize = s;
+          maxSize = jmin(maxSize, usage(bw) * capA - (bsize(a) - s));
+          maxSize = jmin(maxSize, (bsize(bw) + s) - usage(a) * capW);
+        } else {
+          maxSize = s;
+          minSize = jmax(minSize, usage(bw) * capA - (bsize(a) - s));
+          minSize = jmax(minSize, (bsize(bw) + s) - usage(a) * capW);
+        }
+        minSize += 0.4;  // REPLICA_CONVERGENCE_DELTA
+        maxSize -= 0.4;
+        const int with = w.empty() ? -1 : findWith(r, w, s + sizeToChange, minSize, maxSize);
+        if (with < 0) continue;
+        m.relocateReplica(m.rPart[with], bw, a);
+        m.relocateReplica(p, a, bw);
+        sorted[a]->remove(r);
+        sorted[a]->add(with);
+        sorted[bw]->remove(with);
+        sorted[bw]->add(r);
+        return true;
+      }
+      return false;
+    };
+    bool improved;
+    do {
+      improved = false;
+      const std::vector<int32_t> snapshot = all;
+      for (int b : snapshot) {
+        const double u = usage(b);
+        const size_t at = (size_t)(std::find(all.begin(), all.end(), b) - all.begin());
+        std::vector<int32_t> cands;
+        if (u > upper) cands.assign(all.begin(), all.begin() + (ptrdiff_t)at);
+        else if (u < lower) cands.assign(all.rbegin(), all.rend() - (ptrdiff_t)at);
+        else continue;
+        for (int w : cands) {
+          if (w == b || std::fabs(usage(w) - usage(b)) < 0.0001) continue;  // USAGE_EQUALITY_DELTA
+          const bool swapped = swapReplicas(b, w);
+          if (swapped) {
+            std::sort(all.begin(), all.end(), brokerLess);
+            improved = true;
+            break;
+          }
+        }
+      }
+    } while (improved);
+    succeeded = true;
+    for (int b = 0; b < m.B; ++b)
+      if (m.alive(b) && (usage(b) < lower || usage(b) > upper)) succeeded = false;
+    return true;
+  }
+  void rebalance(Engine&, int) override {}
+  void update(Engine&) override { finished = true; }
+  int compareStats(const ccmi_cluster_stats&, const ccmi_cluster_stats&) const override { return 0; }
+};
+
 // ======================================================================================= BrokerSetAwareGoal
 // A hard goal: every replica must sit in the broker set its mapping policy names (TopicNameHash: the topic's set;
 // ReplicaToOriginal: its original broker's set). Broker sets come with the call's BalancingConstraint (brokersets.h);
@@ -2299,6 +2654,8 @@ std::unique_ptr<GoalImpl> makeMoreGoal(int kind) {
     case CCMI_GOAL_POTENTIAL_NW_OUT: return std::make_unique<PotentialNwOut>();
     case CCMI_GOAL_TOPIC_REPLICA_DISTRIBUTION: return std::make_unique<TopicReplicaDistribution>();
     case CCMI_GOAL_TOPIC_LEADER_REPLICA_DISTRIBUTION: return std::make_unique<TopicLeaderReplicaDistribution>();
+    case CCMI_GOAL_KAFKA_ASSIGNER_EVEN_RACK_AWARE: return std::make_unique<KafkaAssignerEvenRackAware>();
+    case CCMI_GOAL_KAFKA_ASSIGNER_DISK_USAGE_DISTRIBUTION: return std::make_unique<KafkaAssignerDiskUsageDistribution>();
     case CCMI_GOAL_LEADER_REPLICA_DISTRIBUTION: return std::make_unique<LeaderReplicaDistribution>();
     case CCMI_GOAL_LEADER_BYTES_IN_DISTRIBUTION: return std::make_unique<LeaderBytesIn>();
     case CCMI_GOAL_PREFERRED_LEADER_ELECTION: return std::make_unique<PreferredLeaderElection>();

@@ -577,6 +577,15 @@ void Model::enableTopicLeaders() {
   }
 }
 
+void Model::swapSlots(int p, int i, int j) {
+  if (i == j) return;
+  std::swap(pSlots[pOff[p] + i], pSlots[pOff[p] + j]);
+  if (dev && !replaying) {
+    markChain(cDirtyP, cDirtyPList, p);
+    markP(p);
+  }
+}
+
 void Model::moveReplicaToEnd(int r) {
   const int p = rPart[r];
   int pos = pOff[p];

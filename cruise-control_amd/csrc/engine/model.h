@@ -249,6 +249,8 @@ class Model {
 
   // ---- mutations (record into the action log, mark dirty rows)
   void relocateReplica(int p, int src, int dst);
+  // Partition.swapReplicaPositions / swapFollowerPositions (Partition.java:162-186): slots i and j (0-based within p)
+  void swapSlots(int p, int i, int j);
   bool relocateLeadership(int p, int src, int dst);
   void moveReplicaToEnd(int r);  // Partition.moveReplicaToEnd (Partition.java:192-197): slot order only
 

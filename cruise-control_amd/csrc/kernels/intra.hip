@@ -7,9 +7,10 @@
 //                 programs of a goal are independent; each reads its replicas' records (contiguous CSR range) and its
 //                 disks, and writes its ordered action records into its own log range.
 // intra_compact : packs the per-broker log ranges into one array in broker-id order (the reference's action order).
-// stats_disks   : one workgroup: per alive broker the average disk utilization percentage and its disks'
-//                 deviations; unbalanced-disk count and variance sum reduced through LDS (tree-ordered sum: the stats
-//                 parity bar is 1e-9 relative).
+// stats_disks   : per alive broker (one thread each, up to kDiskStatsBlocks workgroups) the average disk utilization
+//                 percentage and its disks' deviations; unbalanced-disk count and variance sum folded per workgroup,
+//                 then the workgroup partials in block order by one wave (deterministic; the stats parity bar is 1e-9
+//                 relative).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -91,20 +92,25 @@ __global__ __launch_bounds__(256) void intra_compact(const int32_t* __restrict__
   }
 }
 
-__global__ __launch_bounds__(1024) void stats_disks(const int32_t* __restrict__ bDiskOff,
-                                                    const int32_t* __restrict__ bDisks, const double* __restrict__ dCap,
-                                                    const uint8_t* __restrict__ dAlive,
-                                                    const double* __restrict__ dUtil,
-                                                    const uint8_t* __restrict__ bAlive, int B, double balance,
-                                                    DiskStatsOut* __restrict__ out) {
-  __shared__ double sv[16];
-  __shared__ int su[16], sa[16];
+// stats_disks_partials: one thread per broker over a grid of up to kDiskStatsBlocks workgroups; each workgroup folds
+// its brokers' unbalanced-disk counts and variance terms (wave shuffle, then the waves in order) into partial[block].
+// stats_disks_combine: one wave folds the partials in block order (deterministic: the parity bar is 1e-9 relative).
+__global__ __launch_bounds__(256) void stats_disks_partials(const int32_t* __restrict__ bDiskOff,
+                                                            const int32_t* __restrict__ bDisks,
+                                                            const double* __restrict__ dCap,
+                                                            const uint8_t* __restrict__ dAlive,
+                                                            const double* __restrict__ dUtil,
+                                                            const uint8_t* __restrict__ bAlive, int B, double balance,
+                                                            DiskStatsOut* __restrict__ partial) {
+  __shared__ double sv[4];
+  __shared__ int su[4], sa[4];
   double var = 0.0;
   int unb = 0, na = 0;
-  for (int b = threadIdx.x; b < B; b += blockDim.x) {
+  for (int b = blockIdx.x * blockDim.x + threadIdx.x; b < B; b += gridDim.x * blockDim.x) {
     if (!bAlive[b]) continue;
+    const int k0 = bDiskOff[b], k1 = bDiskOff[b + 1];
     double cap = 0, util = 0;
-    for (int k = bDiskOff[b]; k < bDiskOff[b + 1]; ++k) {
+    for (int k = k0; k < k1; ++k) {
       const int d = bDisks[k];
       if (dAlive[d]) {
         cap += dCap[d];
@@ -115,7 +121,7 @@ __global__ __launch_bounds__(1024) void stats_disks(const int32_t* __restrict__ 
     const double upper = avg * balance;
     const double lm = 2 - balance;
     const double lower = avg * (lm > 0 ? lm : 0.0);
-    for (int k = bDiskOff[b]; k < bDiskOff[b + 1]; ++k) {
+    for (int k = k0; k < k1; ++k) {
       const int d = bDisks[k];
       if (!dAlive[d]) continue;
       const double pct = dCap[d] > 0 ? dUtil[d] / dCap[d] : 1.0;
@@ -146,9 +152,30 @@ __global__ __launch_bounds__(1024) void stats_disks(const int32_t* __restrict__ 
       u += su[k];
       a += sa[k];
     }
-    out->varSum = v;
-    out->unbalanced = u;
-    out->numAlive = a;
+    partial[blockIdx.x] = DiskStatsOut{v, u, a};
+  }
+}
+
+__global__ __launch_bounds__(64) void stats_disks_combine(const DiskStatsOut* __restrict__ partial, int n,
+                                                          DiskStatsOut* __restrict__ out) {
+  // lane l folds partials l, l + 64, ... in order; then the lanes in order (lane 0 reads them back through LDS)
+  __shared__ DiskStatsOut s[64];
+  DiskStatsOut acc{0.0, 0, 0};
+  for (int i = threadIdx.x; i < n; i += 64) {
+    acc.varSum += partial[i].varSum;
+    acc.unbalanced += partial[i].unbalanced;
+    acc.numAlive += partial[i].numAlive;
+  }
+  s[threadIdx.x] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    DiskStatsOut t{0.0, 0, 0};
+    for (int l = 0; l < 64; ++l) {
+      t.varSum += s[l].varSum;
+      t.unbalanced += s[l].unbalanced;
+      t.numAlive += s[l].numAlive;
+    }
+    *out = t;
   }
 }
 
@@ -176,8 +203,12 @@ hipError_t launchIntraCompact(const int32_t* brokers, int n, const int64_t* logO
 hipError_t launchStatsDisks(const int32_t* bDiskOff, const int32_t* bDisks, const double* dCap, const uint8_t* dAlive,
                             const double* dUtil, const uint8_t* bAlive, int B, double balance, DiskStatsOut* out,
                             hipStream_t st) {
-  hipLaunchKernelGGL(stats_disks, dim3(1), dim3(1024), 0, st, bDiskOff, bDisks, dCap, dAlive, dUtil, bAlive, B,
-                     balance, out);
+  // out[0]: the result; out[1 .. kDiskStatsBlocks]: the workgroup partials
+  int blocks = (B + 255) / 256;
+  blocks = blocks < 1 ? 1 : (blocks > kDiskStatsBlocks ? kDiskStatsBlocks : blocks);
+  hipLaunchKernelGGL(stats_disks_partials, dim3(blocks), dim3(256), 0, st, bDiskOff, bDisks, dCap, dAlive, dUtil, bAlive,
+                     B, balance, out + 1);
+  hipLaunchKernelGGL(stats_disks_combine, dim3(1), dim3(64), 0, st, out + 1, blocks, out);
   return hipGetLastError();
 }
 

@@ -831,7 +831,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, kServ
   __shared__ SegEntry sSeg[kMaxSegs + 1];
   unsigned long long last = startSeq;
   int progVer = -1;
-  bool needAcq = false;  // a command since this workgroup's last acquire had rows workgroup 0 wrote into the tables
+  int acqEpoch = -1;  // ServerCmd.rowsEpoch of this workgroup's last acquire (-1: none since the launch)
   unsigned long long idleSince = __builtin_amdgcn_s_memrealtime();
   unsigned long long srvT[5] = {0, 0, 0, 0, 0};
   for (;;) {
@@ -843,7 +843,13 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, kServ
       for (int spin = 0;; ++spin) {
         const unsigned long long s =
             __hip_atomic_load(&cmd->seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        if (s != last) break;
+        if (s != last && !(s & kSeqBusy)) {
+          // a workgroup that did not take part in the last command may read the next header while the host writes
+          // it: the copy counts only when the sequence word did not change across it
+          copySysOneThread(&c, cmd);
+          if (__hip_atomic_load(&cmd->seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == s) break;
+          continue;
+        }
         if ((spin & 63) == 63) {
           if (!published) {
             const unsigned long long mw = __hip_atomic_load(&mail[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -859,11 +865,12 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, kServ
         __builtin_amdgcn_s_sleep(4);
       }
       SRV_STAMP(T, 0);
-      // the rows workgroup 0 wrote for earlier commands (released before its arrivals) become visible here; after
-      // commands without rows there is nothing new to see in the tables
-      if (needAcq) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      needAcq = false;
-      if (!ex) copySysOneThread(&c, cmd);
+      // the rows workgroup 0 wrote for earlier commands (released before its arrivals) become visible with an agent
+      // acquire; a command no earlier one wrote rows before needs none
+      if (!ex && c.rowsEpoch != acqEpoch && (uint32_t)blockIdx.x < (uint32_t)c.nActive) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        acqEpoch = c.rowsEpoch;
+      }
       SRV_STAMP(T, 1);
       if (blockIdx.x == 0)  // busy-time stamp, read by the last workgroup to arrive
         __hip_atomic_store(t0, __builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -879,8 +886,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, kServ
     }
     const bool rows = (c.nb | c.nr | c.np | c.nt) != 0;
     const uint32_t nAct = (uint32_t)c.nActive;
-    if (blockIdx.x >= nAct) {  // not taking part: only the sequence (and a pending acquire) moves on
-      needAcq |= rows;
+    if (blockIdx.x >= nAct) {  // not taking part: only the sequence moves on
       last = c.seq;
       __syncthreads();
       continue;
@@ -1053,7 +1059,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, kServ
       }
     }
     last = c.seq;
-    needAcq |= rows;
     idleSince = __builtin_amdgcn_s_memrealtime();
     __syncthreads();
   }

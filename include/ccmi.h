@@ -110,8 +110,10 @@ typedef enum ccmi_goal_kind {
   CCMI_GOAL_PREFERRED_LEADER_ELECTION = 18,         /* PreferredLeaderElectionGoal (not in default.goals) */
   CCMI_GOAL_RACK_AWARE_DISTRIBUTION = 19,           /* RackAwareDistributionGoal (not in default.goals) */
   CCMI_GOAL_BROKER_SET_AWARE = 20,                  /* BrokerSetAwareGoal (not in default.goals) */
-  CCMI_GOAL_TOPIC_LEADER_REPLICA_DISTRIBUTION = 21  /* TopicLeaderReplicaDistributionGoal (ABI v7; in goals, not in
+  CCMI_GOAL_TOPIC_LEADER_REPLICA_DISTRIBUTION = 21, /* TopicLeaderReplicaDistributionGoal (ABI v7; in goals, not in
                                                        default.goals: AnalyzerConfig.java:297-319) */
+  CCMI_GOAL_KAFKA_ASSIGNER_EVEN_RACK_AWARE = 22,     /* KafkaAssignerEvenRackAwareGoal (ABI v7; in goals) */
+  CCMI_GOAL_KAFKA_ASSIGNER_DISK_USAGE_DISTRIBUTION = 23 /* KafkaAssignerDiskUsageDistributionGoal (ABI v7; in goals) */
 } ccmi_goal_kind;
 
 /* AnalyzerConfig replica.to.broker.set.mapping.policy.class (config/ReplicaToBrokerSetMappingPolicy.java) */

@@ -313,6 +313,42 @@ class MinTopicLeadersPerBrokerGoal : public AbstractGoal {
 // iteration order of a HashSet<String> of topic names filled in `insertion` order
 std::vector<int> topicHashSetOrder(const ClusterModel& cm, const std::vector<int>& insertion);
 
+// Kafka-assigner mode goals (analyzer/kafkaassigner/; in `goals`, not in default.goals). They implement Goal directly
+// (no AbstractGoal template, no acceptance conjunction over optimized goals).
+class KafkaAssignerEvenRackAwareGoal : public Goal {
+ public:
+  explicit KafkaAssignerEvenRackAwareGoal(const BalancingConstraint&) {}
+  std::string name() const override { return "KafkaAssignerEvenRackAwareGoal"; }
+  bool isHardGoal() const override { return true; }
+  bool optimize(ClusterModel& cm, const GoalList& optimizedGoals, const OptimizationOptions& o) override;
+  Acceptance actionAcceptance(const BalancingAction& a, ClusterModel& cm) override;
+  int compareStats(const ClusterModelStats&, const ClusterModelStats&) const override { return 0; }
+
+ private:
+  bool maybeApplyMove(ClusterModel& cm, int p, int position);
+  bool violates(const ClusterModel& cm, int replica, int destBroker) const;
+  // _aliveBrokerReplicaCountByPosition: per position a TreeSet<BrokerReplicaCount> ordered by (count, id); an entry
+  // leaves through its iterator and comes back with the incremented count, so the set stays sorted
+  std::vector<std::set<std::pair<int, int>>> byPosition_;  // (replica count, broker id)
+};
+class KafkaAssignerDiskUsageDistributionGoal : public Goal {
+ public:
+  explicit KafkaAssignerDiskUsageDistributionGoal(const BalancingConstraint& bc) : bc_(bc) {}
+  std::string name() const override { return "KafkaAssignerDiskUsageDistributionGoal"; }
+  bool isHardGoal() const override { return true; }
+  bool optimize(ClusterModel& cm, const GoalList& optimizedGoals, const OptimizationOptions& o) override;
+  Acceptance actionAcceptance(const BalancingAction& a, ClusterModel& cm) override;
+  // DiskDistributionGoalStatsComparator (:608-632)
+  int compareStats(const ClusterModelStats& s1, const ClusterModelStats& s2) const override {
+    return s2.numBalancedBrokersByResource[DISK] > s1.numBalancedBrokersByResource[DISK] ? -1 : 1;
+  }
+
+ private:
+  BalancingConstraint bc_;
+};
+// KafkaAssignerUtils.sanityCheckOptimizationOptions (KafkaAssignerUtils.java:20-26)
+void kafkaAssignerSanityCheck(const OptimizationOptions& o);
+
 // PreferredLeaderElectionGoal (analyzer/goals/PreferredLeaderElectionGoal.java) with skipUrpDemotion = false,
 // excludeFollowerDemotion = false (the no-argument constructor GoalOptimizer uses): demoted brokers, then demoted disks
 // (ccmi.h disk_demoted) of the other alive brokers.

@@ -32,6 +32,9 @@ std::unique_ptr<Goal> makeGoal(int kind, const BalancingConstraint& bc) {
     case CCMI_GOAL_PREFERRED_LEADER_ELECTION: return std::make_unique<PreferredLeaderElectionGoal>(bc);
     case CCMI_GOAL_RACK_AWARE_DISTRIBUTION: return std::make_unique<RackAwareDistributionGoal>(bc);
     case CCMI_GOAL_BROKER_SET_AWARE: return std::make_unique<BrokerSetAwareGoal>(bc);
+    case CCMI_GOAL_KAFKA_ASSIGNER_EVEN_RACK_AWARE: return std::make_unique<KafkaAssignerEvenRackAwareGoal>(bc);
+    case CCMI_GOAL_KAFKA_ASSIGNER_DISK_USAGE_DISTRIBUTION:
+      return std::make_unique<KafkaAssignerDiskUsageDistributionGoal>(bc);
     default: throw std::invalid_argument("goal kind not in oracle scope: " + std::to_string(kind));
   }
 }

@@ -82,6 +82,13 @@ def decks():
     # three replicas of one partition on two racks: RackAwareGoal must fail (RackAwareGoal.java:112-121)
     out.append(("model-rackAwareUnsatisfiable", "rackAwareUnsatisfiable", DECK_GOALS,
                 deck_constraint(MEDIUM_BALANCE, MEDIUM_CAP), "Insufficient number of racks"))
+    # Kafka-assigner decks (:200-215): verifications BROKEN_BROKERS and REGRESSION, the constraint of deck #5;
+    # rackAwareUnsatisfiable expects the OptimizationFailureException
+    ka = ["KafkaAssignerEvenRackAwareGoal", "KafkaAssignerDiskUsageDistributionGoal"]
+    for model in ("smallClusterModel", "mediumClusterModel", "rackAwareSatisfiable"):
+        out.append((f"kafkaAssigner-{model}", model, ka, deck_constraint(MEDIUM_BALANCE, LOW_CAP)))
+    out.append(("kafkaAssigner-rackAwareUnsatisfiable", "rackAwareUnsatisfiable", ka,
+                deck_constraint(MEDIUM_BALANCE, LOW_CAP), None, True))
     out.append(("deadBroker-default-goals", "deadBroker", list(ccmi.DEFAULT_GOALS), ccmi.BalancingConstraint()))
     out.append(("deadBroker-soft-goals", "deadBroker", list(ccmi.C1_GOALS), ccmi.BalancingConstraint()))
     return out

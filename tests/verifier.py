@@ -83,6 +83,9 @@ COMPARATORS = {
     "DiskUsageDistributionGoal": _resource_distribution_cmp(3),
     "LeaderBytesInDistributionGoal": _leader_bytes_in_cmp,
     "IntraBrokerDiskUsageDistributionGoal": _intra_usage_cmp,
+    # DiskDistributionGoalStatsComparator (KafkaAssignerDiskUsageDistributionGoal.java:608-632)
+    "KafkaAssignerDiskUsageDistributionGoal": lambda after, before, bc: (
+        -1 if before["num_balanced_brokers_by_resource"][3] > after["num_balanced_brokers_by_resource"][3] else 1),
 }  # hard goals, MinTopicLeaders, PreferredLeaderElection: comparisons are irrelevant (return 0)
 
 
