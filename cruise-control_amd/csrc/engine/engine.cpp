@@ -613,6 +613,13 @@ bool Engine::optimizeGoalImpl(std::unique_ptr<GoalImpl>& g, ccmi_goal_result* re
     res->device_candidates = dev->perf.scanPairs - p0;
   }
   m.clearTracked();
+  static const bool perGoalProfile = std::getenv("CCMI_PROFILE") && std::string(std::getenv("CCMI_PROFILE")) == "goal";
+  if (perGoalProfile) {  // CCMI_PROFILE=goal: one phase profile per goal
+    prof().print(g->name.c_str());
+    PhaseProf fresh;
+    fresh.candCounter = prof().candCounter;
+    prof() = fresh;
+  }
   optimized.push_back(std::move(g));
   if (res) {
     res->stats = stats();  // GoalOptimizer.statsByGoalPriority
@@ -895,7 +902,9 @@ class ReplicaDistribution : public GoalImpl {
 // the same put sequence (members in ascending id, placed by their entry (key, id) rank) the driver would otherwise run
 // when its lazy candidate order stops being exact. Most calls never need the tree: a newer submission cancels the
 // build in flight and the driver never waits except in take(). Used for clusters of at least CCMI_TREE_WORKER_MIN
-// brokers (default 2048; smaller trees are cheaper to build on the driver thread); CCMI_NO_TREE_WORKER=1 disables it.
+// brokers (default 2048; smaller trees are cheaper to build on the driver thread) when CCMI_TREE_WORKER=1. Off by
+// default: on the GPU box the second busy host thread made whole C2 proposals 1.3-2.5 s slower in some runs (the
+// scan-wait and in-kernel server times grew with it) for a best-case gain of 0.3 s (profiles/r03/c2_ab_worker_v2.txt).
 class TreeWorker {
  public:
   struct RankOnly {  // buildByRank never compares
@@ -1214,9 +1223,9 @@ class ResourceDistribution : public GoalImpl {
         }
       }
     }
-    static const bool noWorker = std::getenv("CCMI_NO_TREE_WORKER") != nullptr;
+    static const bool worker = std::getenv("CCMI_TREE_WORKER") != nullptr;
     const char* minEnv = std::getenv("CCMI_TREE_WORKER_MIN");
-    const bool useWorker = !noWorker && m.B >= (minEnv ? std::atoi(minEnv) : 2048);
+    const bool useWorker = worker && m.B >= (minEnv ? std::atoi(minEnv) : 2048);
     if (useWorker) {
       if (!treeWorker) treeWorker = std::make_unique<TreeWorker>();
       treeWorker->submit(inorder, m.B);  // `inorder` is the members' entry (key, id) order

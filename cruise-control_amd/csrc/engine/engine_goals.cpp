@@ -1669,6 +1669,11 @@ class TopicLeaderReplicaDistribution : public GoalImpl {
 };
 
 // ======================================================================================= LeaderReplicaDistributionGoal
+// CCMI_NO_PAIR_CHAINS=1: the leadership loops use one pair scan per decision instead of a K7 chain (A/B switch)
+inline bool pairChainsOn(const Engine& e) {
+  static const bool off = std::getenv("CCMI_NO_PAIR_CHAINS") != nullptr;
+  return !off && e.chainsOn();
+}
 class LeaderReplicaDistribution : public GoalImpl {
  public:
   LeaderReplicaDistribution() {
@@ -1737,6 +1742,7 @@ class LeaderReplicaDistribution : public GoalImpl {
   // are scanned as one pair list and the scan resumes after each winner
   bool moveLeadershipOut(Engine& e, int b) {
     Model& m = e.m;
+    PhaseScope lp(PH_LEAD_OUT);
     if (m.numDead > 0) return true;
     const int upperSrc = excluded(b) ? 0 : upper;
     int nl = m.bNlead[b];
@@ -1767,7 +1773,7 @@ class LeaderReplicaDistribution : public GoalImpl {
         }
       }
     }
-    if (e.chainsOn()) {  // one device chain: after an accept the scan resumes at the next leader's pairs
+    if (pairChainsOn(e)) {  // one device chain: after an accept the scan resumes at the next leader's pairs
       std::vector<int32_t> next(pr.size()), log;
       int ng = (int)pr.size();
       for (int q = (int)pr.size() - 1; q >= 0; --q) {
@@ -1800,6 +1806,7 @@ class LeaderReplicaDistribution : public GoalImpl {
   // rebalanceByMovingLeadershipIn (:205-240)
   bool moveLeadershipIn(Engine& e, int b) {
     Model& m = e.m;
+    PhaseScope lp(PH_LEAD_IN);
     if (m.numDead > 0 || (e.opt.anyExclLead && e.opt.exclLead[b])) return true;
     int nl = m.bNlead[b];
     std::vector<int32_t> reps, pr, pb;
@@ -1812,7 +1819,7 @@ class LeaderReplicaDistribution : public GoalImpl {
       pr.push_back(m.pLeader[m.rPart[r]]);
       pb.push_back(b);
     }
-    if (e.chainsOn()) {  // one device chain over the fixed pair list
+    if (pairChainsOn(e)) {  // one device chain over the fixed pair list
       if (pr.empty()) return true;
       std::vector<int32_t> next(pr.size()), log;
       for (size_t q = 0; q < pr.size(); ++q) next[q] = (int32_t)q + 1;
@@ -1840,6 +1847,7 @@ class LeaderReplicaDistribution : public GoalImpl {
   // rebalanceByMovingReplicasOut (:242-300)
   bool moveReplicasOut(Engine& e, int b) {
     Model& m = e.m;
+    PhaseScope lp(PH_REP_OUT);
     const bool f = fix;
     auto cmp = [&m, f](int x, int y) {
       const int c = f ? jcmpInt(m.nrep(x), m.nrep(y)) : jcmpInt(m.bNlead[x], m.bNlead[y]);
@@ -1856,8 +1864,20 @@ class LeaderReplicaDistribution : public GoalImpl {
           if (m.alive(x) && m.bNlead[x] < upper) ins.push_back(x);
         javaHashSetOrder(ins, order);  // Collectors.toSet()
         // the same TreeSet.add sequence, placed by rank (the comparator is a total order on these brokers)
-        std::vector<int32_t> byKey(ins.begin(), ins.end()), rank(m.B, 0);
-        std::sort(byKey.begin(), byKey.end(), [&](int x, int y) { return cmp(x, y) < 0; });
+        std::vector<int32_t> byKey, rank(m.B, 0);
+        bool idsAsc = true;
+        for (int x = 1; x < m.B && idsAsc; ++x) idsAsc = m.bId[x - 1] < m.bId[x];
+        if (idsAsc && std::is_sorted(ins.begin(), ins.end()) && !ins.empty()) {
+          // counting sort by leader count (0 <= count < upper); `ins` is in ascending index = id order
+          std::vector<int32_t> start(upper + 1, 0);
+          for (int x : ins) start[m.bNlead[x] + 1]++;
+          for (int c = 0; c < upper; ++c) start[c + 1] += start[c];
+          byKey.resize(ins.size());
+          for (int x : ins) byKey[start[m.bNlead[x]]++] = x;
+        } else {
+          byKey.assign(ins.begin(), ins.end());
+          std::sort(byKey.begin(), byKey.end(), [&](int x, int y) { return cmp(x, y) < 0; });
+        }
         for (size_t i = 0; i < byKey.size(); ++i) rank[byKey[i]] = (int32_t)i;
         cand.buildByRank(order, rank);
       }
@@ -1903,6 +1923,7 @@ class LeaderReplicaDistribution : public GoalImpl {
   Model::SnapTable snapTab;
   bool moveLeaderReplicasIn(Engine& e, int b) {
     Model& m = e.m;
+    PhaseScope lp(PH_REP_IN);
     if (e.opt.anyExclLead && e.opt.exclLead[b]) return true;
     auto cmp = [&m](int b1, int b2) {
       const int r = jcmpInt(m.bNlead[b2], m.bNlead[b1]);

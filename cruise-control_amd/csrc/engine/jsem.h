@@ -571,6 +571,13 @@ class OrderedQueue {
 };
 
 // Iteration order of a HashSet<Broker> filled by add() in `ins` order (Broker.hashCode() == id).
+// HashSet<Broker> table capacity after n distinct add() calls from the default table (16 buckets, load .75)
+inline uint32_t javaHashSetCapacity(size_t n) {
+  uint32_t cap = 16;
+  while (n > (size_t)(cap / 4 * 3)) cap <<= 1;
+  return cap;
+}
+
 inline void javaHashSetOrder(const std::vector<int>& ins, std::vector<int>& out) {
   auto slot = [](int h, unsigned c) { return (unsigned)(h ^ (int)((unsigned)h >> 16)) & (c - 1); };
   if (ins.size() <= 8) {  // the default 16-bucket table never resizes or treeifies: bucket order, insertion order within
@@ -594,11 +601,22 @@ inline void javaHashSetOrder(const std::vector<int>& ins, std::vector<int>& out)
     out.assign(ks, ks + m);
     return;
   }
+  const size_t N = ins.size();
+  {
+    // Strictly ascending non-negative keys below both the final table capacity and 2^16 (where the hash spread is the
+    // identity): every key ends in a bucket of its own, whatever resizes or tree bins happened on the way, so the
+    // iteration order is the keys' ascending order — the input itself.
+    bool asc = ins.front() >= 0;
+    for (size_t i = 1; i < N && asc; ++i) asc = ins[i - 1] < ins[i];
+    if (asc && (size_t)ins.back() < std::min<size_t>(javaHashSetCapacity(N), 65536)) {
+      out.assign(ins.begin(), ins.end());
+      return;
+    }
+  }
   // General case: the JDK 11 HashMap insertion (bucket lists appended at the tail; a resize splits every list in
   // order, so each bucket keeps insertion order; a list reaching 9 nodes resizes a table below 64 buckets), on flat
   // arrays.
   unsigned cap = 16;
-  const size_t N = ins.size();
   std::vector<int> key(N), nxt(N), head(cap, -1), tail(cap, -1), cnt(cap, 0);
   size_t n = 0;
   auto rehash = [&]() {
@@ -652,13 +670,6 @@ inline int32_t jD2I(double x) {
 }
 inline int32_t jAddI(int32_t a, int32_t b) { return (int32_t)((uint32_t)a + (uint32_t)b); }  // Java int + (wraps)
 inline int32_t jSubI(int32_t a, int32_t b) { return (int32_t)((uint32_t)a - (uint32_t)b); }
-
-// HashSet<Broker> table capacity after n distinct add() calls from the default table (16 buckets, load .75)
-inline uint32_t javaHashSetCapacity(size_t n) {
-  uint32_t cap = 16;
-  while (n > (size_t)(cap / 4 * 3)) cap <<= 1;
-  return cap;
-}
 
 inline int32_t jStringHash(const char* s) {  // String.hashCode
   uint32_t h = 0;

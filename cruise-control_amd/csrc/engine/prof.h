@@ -10,7 +10,8 @@ namespace ccmi {
 
 enum Phase {
   PH_RDG_OUT, PH_RDG_IN, PH_RES_OUT, PH_RES_IN, PH_SWAP, PH_DEV_SCAN, PH_DEV_STATS, PH_RELOCATE, PH_CAND_BUILD,
-  PH_SORTED_INIT, PH_UPDATE, PH_PQ_INIT, PH_FLATTEN, PH_TREE_BUILD, PH_ORDER, PH_OTHER_GOALS, PH_SCAN_STAGE, PH_SCAN_WAIT, PH_COUNT
+  PH_SORTED_INIT, PH_UPDATE, PH_PQ_INIT, PH_FLATTEN, PH_TREE_BUILD, PH_ORDER, PH_OTHER_GOALS, PH_SCAN_STAGE, PH_SCAN_WAIT,
+  PH_LEAD_OUT, PH_LEAD_IN, PH_REP_OUT, PH_REP_IN, PH_COUNT
 };
 
 struct PhaseProf {
@@ -40,7 +41,8 @@ struct PhaseProf {
     static const char* names[PH_COUNT] = {"rdg.moveOut", "rdg.moveIn", "res.moveOut", "res.moveIn", "res.swap",
                                           "device.scan", "device.stats", "relocate", "cand.build", "sorted.init",
                                           "goal.update", "pq.init", "flatten", "tree.build", "order.repair",
-                                          "other.goals", "scan.stage", "scan.wait"};
+                                          "other.goals", "scan.stage", "scan.wait",
+                                          "lrd.leadOut", "lrd.leadIn", "lrd.repOut", "lrd.repIn"};
     if (!on) return;
     std::fprintf(stderr, "[ccmi profile %s]\n", tag);
     for (int i = 0; i < PH_COUNT; ++i)
@@ -63,7 +65,8 @@ inline PhaseProf& prof() {
 }
 
 inline bool isDriverPhase(int p) {
-  return p == PH_RDG_OUT || p == PH_RDG_IN || p == PH_RES_OUT || p == PH_RES_IN || p == PH_SWAP || p == PH_OTHER_GOALS;
+  return p == PH_RDG_OUT || p == PH_RDG_IN || p == PH_RES_OUT || p == PH_RES_IN || p == PH_SWAP || p == PH_OTHER_GOALS ||
+         p == PH_LEAD_OUT || p == PH_LEAD_IN || p == PH_REP_OUT || p == PH_REP_IN;
 }
 
 struct PhaseScope {

@@ -6,7 +6,7 @@ make -C cruise-control_amd -j16 > gpurun_out/make.log 2>&1 || exit 1
 for spec in ${AB_ENVS:-base:CCMI_PROFILE=1}; do
   name=${spec%%:*}; envs=${spec#*:}
   echo "== $name ($envs) $(date +%T)"
-  env $(echo "$envs" | tr ',' ' ') CCMI_PROFILE=1 timeout -k 10 600 python -u tools/probe.py --workload ${WORKLOAD:-c2} > gpurun_out/ab_$name.log 2>&1
+  env CCMI_PROFILE=1 $(echo "$envs" | tr ',' ' ') timeout -k 10 600 python -u tools/probe.py --workload ${WORKLOAD:-c2} > gpurun_out/ab_$name.log 2>&1
   rc=$?
   grep -E "^total|^perf|scan.wait|device.scan" gpurun_out/ab_$name.log
   if [ $rc -ne 0 ]; then echo "stopping: $name exited $rc"; tail -5 gpurun_out/ab_$name.log; exit $rc; fi
