@@ -177,6 +177,10 @@ Device::~Device() {
                              "%.2f us, rest to arrival %.2f us (workgroup 0)\n",
                      h[8192], h[8193] * 0.01 / h[8192], h[8194] * 0.01 / h[8192], h[8195] * 0.01 / h[8192],
                      h[8196] * 0.01 / h[8192]);
+      if (h[8200])
+        std::fprintf(stderr, "[ccmi chain stamps] %llu chain_pairs launches, %llu accepts: %.2f us per launch in "
+                             "evaluation, %.2f us applying, %.2f us in total (thread 0)\n",
+                     h[8200], h[8201], h[8202] * 0.01 / h[8200], h[8203] * 0.01 / h[8200], h[8204] * 0.01 / h[8200]);
       double acc[5] = {0, 0, 0, 0, 0};
       int n = 0;
       for (int i = 0; i < 1024; ++i) {

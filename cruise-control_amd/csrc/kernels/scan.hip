@@ -625,7 +625,8 @@ uint32_t scanXcdSliceMinCols() { return xcdSliceMinCols(); }
     }                                                                                                 \
   } while (0)
 // Scan-server phase stamps (CCMI_STAMPS): workgroup 0's thread 0 notes when it saw a command (0), had it copied (1),
-// staged its rows (2), finished its first tile (3) and arrived (4); the deltas are summed at stamps[8192 + i].
+// was ready for its first tile (2), finished its first tile (3, rows staged with it) and arrived (4); the deltas are
+// summed at stamps[8192 + i].
 #define SRV_STAMP(T, i)                                                                               \
   do {                                                                                               \
     if ((T).stamps && blockIdx.x == 0 && threadIdx.x == 0) {                                          \
@@ -770,6 +771,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, kScan
 // workgroup takes an agent-scope acquire when it sees the next command (MI355X_MICROARCH.md, inter-workgroup
 // visibility). The launch exits on SOP_EXIT or after kServerIdleTicks without a command (watchdog; the host stops the
 // server before any other work on the session stream and at the end of every API call, so it never relies on it).
+typedef unsigned long long MailPair __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ int32_t ldSys(const int32_t* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
@@ -920,7 +922,11 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, kServ
       __syncthreads();
       staged = true;
     };
-    if (blockIdx.x == 0) stage();
+    // The command's rows go into the tables (for the next commands) from the last active workgroup, which has the
+    // fewest tiles (none on a short command), so the row writes run next to workgroup 0's tiles instead of after
+    // them; every workgroup stages the rows into its LDS overlay with its first tile (overlapping that tile's
+    // request loads).
+    const bool writer = blockIdx.x == nAct - 1;
     SRV_STAMP(T, 2);
     bool firstTile = true;
     const int32_t* A = (const int32_t*)(pay + c.oA);
@@ -943,7 +949,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, kServ
       for (uint32_t base = wg * kBlock; base < total; base += wgs * kBlock) {
         const uint32_t kb = base / Ws;
         const unsigned long long keyBase = (unsigned long long)kb * N + c0 + colStart + (base - kb * Ws);
-        if (blockBest(result) <= keyBase) break;
+        // (the first tile skips the early-exit check: a winner can hardly exist yet, and its round trip would delay
+        // the tile's request loads; a superfluous tile only loses to the smaller key in atomicMin)
+        if (!firstTile && blockBest(result) <= keyBase) break;
         const uint32_t q = base + threadIdx.x;
         const uint32_t k = q / Ws;
         const uint32_t j = colStart + (q - k * Ws);
@@ -991,7 +999,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, kServ
     } else {  // SOP_PAIRS
       const int n = c.n, keyBase = c.keyBase;
       for (int base = blockIdx.x * kBlock; base < n; base += (int)nAct * kBlock) {
-        if (blockBest(result) <= (unsigned long long)(keyBase + base)) break;
+        if (!firstTile && blockBest(result) <= (unsigned long long)(keyBase + base)) break;
         const int q = base + threadIdx.x;
         RowRef rq{0, 0, 0, 0};
         int dq = 0;
@@ -1020,10 +1028,11 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, kServ
       }
     }
     if (firstTile) SRV_STAMP(T, 3);
-    // Workgroup 0 writes the command's rows into the tables for the next commands (no workgroup reads them from the
-    // tables in this one: the LDS overlay has them) after its tiles, with write-through device-scope stores, and
-    // applies the topic-count deltas with device-scope atomics.
-    if (blockIdx.x == 0 && rows) {
+    // The writer workgroup writes the command's rows into the tables for the next commands (no workgroup reads them
+    // from the tables in this one: the LDS overlay has them) after its tiles, with write-through device-scope stores,
+    // and applies the topic-count deltas with device-scope atomics.
+    if (writer && rows) {
+      if (!staged) stage();
       applyRowsCoherent(Mt, ov.b, ov.nb, ov.r, ov.nr, ov.p, ov.np, threadIdx.x, blockDim.x);
       for (int i = threadIdx.x; i < U.nt; i += blockDim.x) {
         TopicCountDelta d;
@@ -1047,15 +1056,15 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, kServ
         const unsigned long long lo = v == kNone ? 0ull : (v + 1) & 0xffffffffull;
         __hip_atomic_store(&result[0], kNone, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const unsigned long long busy =
+            __builtin_amdgcn_s_memrealtime() - __hip_atomic_load(t0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        // mail[1]: the command's busy time (100 MHz ticks from workgroup 0 seeing it to this publish), then the word
-        __hip_atomic_store(&mail[1],
-                           __builtin_amdgcn_s_memrealtime() -
-                               __hip_atomic_load(t0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
-                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the busy time lands before the sequence word
-        __hip_atomic_store(&mail[0], ((c.seq & 0xffffffffull) << 32) | lo, __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_SYSTEM);
+        // mail[0] = the word, mail[1] = the command's busy time (100 MHz ticks from workgroup 0 seeing it to this
+        // publish): ONE aligned 16-byte store into the host-coherent mailbox (one PCIe write, so the host that sees the
+        // word sees the busy time next to it, without a second store and its completion wait)
+        // (sc0 sc1: system scope, written through to host memory like the system-scope atomic stores elsewhere)
+        const MailPair w = {((c.seq & 0xffffffffull) << 32) | lo, busy};
+        asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1" ::"v"(mail), "v"(w) : "memory");
       }
     }
     last = c.seq;
@@ -1283,8 +1292,17 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, kServ
   __syncthreads();
   int start = 0, acc = 0;
   unsigned long long visited = 0;
+  // CCMI_STAMPS: thread 0 sums the time in candidate evaluation and in applying moves (stamps[8200 .. 8203])
+  const bool st = T.stamps && threadIdx.x == 0;
+  unsigned long long tEval = 0, tApply = 0, t = st ? __builtin_amdgcn_s_memrealtime() : 0;
+  const unsigned long long tStart = t;
   while (start < n && acc < maxAccepts) {
     const unsigned long long best = chainFirstPair(T, prog, ov, pr, pb, start, n);
+    if (st) {
+      const unsigned long long u = __builtin_amdgcn_s_memrealtime();
+      tEval += u - t;
+      t = u;
+    }
     if (best == kNone) {
       visited += (unsigned long long)(n - start);
       break;
@@ -1293,8 +1311,21 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, kServ
     const int q = (int)best;
     if (threadIdx.x == 0) log[acc] = q;
     chainApplyAny(C, sc, prog.action, pr[q], pb[q]);
+    if (st) {
+      __builtin_amdgcn_s_waitcnt(0);
+      const unsigned long long u = __builtin_amdgcn_s_memrealtime();
+      tApply += u - t;
+      t = u;
+    }
     ++acc;
     start = next[q];
+  }
+  if (st) {
+    atomicAdd(&T.stamps[8200], 1ull);
+    atomicAdd(&T.stamps[8201], (unsigned long long)acc);
+    atomicAdd(&T.stamps[8202], tEval);
+    atomicAdd(&T.stamps[8203], tApply);
+    atomicAdd(&T.stamps[8204], __builtin_amdgcn_s_memrealtime() - tStart);
   }
   if (threadIdx.x == 0) {
     out->accepts = (unsigned long long)acc;
