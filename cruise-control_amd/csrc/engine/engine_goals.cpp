@@ -1929,9 +1929,34 @@ class LeaderReplicaDistribution : public GoalImpl {
       const int r = jcmpInt(m.bNlead[b2], m.bNlead[b1]);
       return r == 0 ? jcmpInt(m.bId[b1], m.bId[b2]) : r;
     };
-    JavaPQ<decltype(cmp)> pq(cmp);
-    for (int x = 0; x < m.B; ++x)
-      if (m.alive(x) && m.bNlead[x] > lower) pq.add(x);
+    // No queued broker changes key while queued, so the PriorityQueue polls in comparator order: an OrderedQueue over
+    // the members sorted by (leader count descending, id) — a counting sort when indices are in id order
+    OrderedQueue<decltype(cmp)> pq(cmp);
+    {
+      PhaseScope pi(PH_PQ_INIT);
+      std::vector<int>& run = pq.sorted();
+      bool idsAsc = true;
+      for (int x = 1; x < m.B && idsAsc; ++x) idsAsc = m.bId[x - 1] < m.bId[x];
+      int maxLead = 0;
+      for (int x = 0; x < m.B; ++x) maxLead = std::max(maxLead, m.bNlead[x]);
+      if (idsAsc && maxLead < (1 << 20)) {
+        std::vector<int32_t> start(maxLead + 2, 0);
+        size_t n = 0;
+        for (int x = 0; x < m.B; ++x)
+          if (m.alive(x) && m.bNlead[x] > lower) {
+            start[maxLead - m.bNlead[x] + 1]++;
+            ++n;
+          }
+        for (int c = 0; c <= maxLead; ++c) start[c + 1] += start[c];
+        run.resize(n);
+        for (int x = 0; x < m.B; ++x)
+          if (m.alive(x) && m.bNlead[x] > lower) run[start[maxLead - m.bNlead[x]]++] = x;
+      } else {
+        for (int x = 0; x < m.B; ++x)
+          if (m.alive(x) && m.bNlead[x] > lower) run.push_back(x);
+        std::sort(run.begin(), run.end(), [&](int x, int y) { return cmp(x, y) < 0; });
+      }
+    }
     const int id = sortId(kind, false, true);
     Model::Spec s;
     s.selLeaders = true;
@@ -1983,7 +2008,7 @@ class LeaderReplicaDistribution : public GoalImpl {
       const size_t hitSize = hit.v->size();
       m.relocateReplica(m.rPart[(*hit.v)[idx]], hit.cb, b);
       if (++nl >= lower) return false;
-      for (size_t t = mi + 1; t < segs.size(); ++t) pq.add(segs[t].cb);  // un-poll speculative sources
+      for (size_t t = segs.size(); t-- > mi + 1;) pq.unpoll(segs[t].cb);  // un-poll speculative sources
       if (!pq.empty() && m.bNlead[hit.cb] < m.bNlead[pq.peek()]) {
         pq.add(hit.cb);
       } else if (idx + 1 < hitSize) {

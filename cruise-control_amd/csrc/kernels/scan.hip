@@ -771,7 +771,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, kScan
 // workgroup takes an agent-scope acquire when it sees the next command (MI355X_MICROARCH.md, inter-workgroup
 // visibility). The launch exits on SOP_EXIT or after kServerIdleTicks without a command (watchdog; the host stops the
 // server before any other work on the session stream and at the end of every API call, so it never relies on it).
-typedef unsigned long long MailPair __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ int32_t ldSys(const int32_t* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
@@ -1056,15 +1055,17 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, kServ
         const unsigned long long lo = v == kNone ? 0ull : (v + 1) & 0xffffffffull;
         __hip_atomic_store(&result[0], kNone, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const unsigned long long busy =
-            __builtin_amdgcn_s_memrealtime() - __hip_atomic_load(t0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        // mail[0] = the word, mail[1] = the command's busy time (100 MHz ticks from workgroup 0 seeing it to this
-        // publish): ONE aligned 16-byte store into the host-coherent mailbox (one PCIe write, so the host that sees the
-        // word sees the busy time next to it, without a second store and its completion wait)
-        // (sc0 sc1: system scope, written through to host memory like the system-scope atomic stores elsewhere)
-        const MailPair w = {((c.seq & 0xffffffffull) << 32) | lo, busy};
-        asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1" ::"v"(mail), "v"(w) : "memory");
+        // mail[1]: the command's busy time (100 MHz ticks from workgroup 0 seeing it to this publish), then the word
+        __hip_atomic_store(&mail[1],
+                           __builtin_amdgcn_s_memrealtime() -
+                               __hip_atomic_load(t0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        // the busy time lands before the sequence word (one 16-byte system-scope store of both words instead was
+        // measured ~16 us slower for the host to see per command: profiles/r03/c2_probe_publish16_v1.txt)
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __hip_atomic_store(&mail[0], ((c.seq & 0xffffffffull) << 32) | lo, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
       }
     }
     last = c.seq;
