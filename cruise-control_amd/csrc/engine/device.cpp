@@ -27,7 +27,7 @@ hipError_t launchScanCross(const DevTables& T, const MutTables& M, const UpdateL
                            unsigned long long* result, unsigned int* done, unsigned long long* mail,
                            unsigned long long seq, hipStream_t st);
 hipError_t launchScanSwap(const DevTables& T, const DevProgram& prog, const int32_t* srcs, int S, const int32_t* cbOff,
-                          const int32_t* cbRep, int M, unsigned long long* result, int32_t* rowVisited,
+                          const int32_t* cbRep, int M, const SwapLimit& lim, unsigned long long* result, int32_t* rowVisited,
                           unsigned long long* mail, unsigned long long seq, hipStream_t st, hipEvent_t ev0,
                           hipEvent_t ev1);
 hipError_t launchScanPairs(const DevTables& T, const MutTables& M, const UpdateList& U, const DevProgram& prog,
@@ -804,7 +804,7 @@ int64_t Device::scanCross(const DevProgram& prog, const int32_t* reps, int K, co
 }
 
 int64_t Device::scanSwap(const DevProgram& prog, const int32_t* srcs, int S, const int32_t* cbOff, int M,
-                         const int32_t* cbRep, int nCand, int64_t* visited) {
+                         const int32_t* cbRep, int nCand, const SwapLimit& lim, int64_t* visited) {
   DeviceGuard dg(ordinal_);
   stopServer();
   *visited = 0;
@@ -825,7 +825,7 @@ int64_t Device::scanSwap(const DevProgram& prog, const int32_t* srcs, int S, con
   launchPrepFor(g, req, true);
   ++seq_;
   hipCheck(launchScanSwap(tables(), prog, (const int32_t*)dReq_, S, (const int32_t*)(dReq_ + oOff),
-                          (const int32_t*)(dReq_ + oRep), M, dResult_, rowVisited_, hResultDev_, seq_, ST,
+                          (const int32_t*)(dReq_ + oRep), M, lim, dResult_, rowVisited_, hResultDev_, seq_, ST,
                           timing ? EV0 : nullptr, timing ? EV1 : nullptr),
            "scan_swap");
   perf.scanLaunches++;

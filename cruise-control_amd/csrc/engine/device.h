@@ -133,7 +133,7 @@ class Device {
   // Pairs: pairs [p0,p1) of (pr, pb), key = pair index. Keys are global, so shards MIN-combine them.
   int64_t scanCross(const DevProgram& prog, const int32_t* reps, int K, const int32_t* cands, int N, int c0, int c1);
   int64_t scanSwap(const DevProgram& prog, const int32_t* srcs, int S, const int32_t* cbOff, int M,
-                   const int32_t* cbRep, int nCand, int64_t* visited);
+                   const int32_t* cbRep, int nCand, const SwapLimit& lim, int64_t* visited);
   int64_t scanPairs(const DevProgram& prog, const int32_t* pr, const int32_t* pb, int p0, int p1);
   // A cross scan whose rows are snapshot segments: segment i contributes (*v)[skip, end) (replicas on broker cb, the
   // snapshot current for cb). Each snapshot is uploaded once into a device-resident pool and the scan sends only

@@ -83,6 +83,14 @@ struct DevGoal {
 
 // goals[0] is the goal being optimized (selfSatisfied); goals[1..n) are the optimized goals in the order
 // AnalyzerUtils.isProposalAcceptableForOptimizedGoals visits them.
+// A swap scan's candidate-row limit filter (sortedCandidateReplicas' selectReplicasBelowLimit / AboveLimit,
+// ResourceDistributionGoal.java:543-569), applied on the device to limit-free candidate lists: res < 0 = none.
+struct SwapLimit {
+  int32_t res = -1;
+  int32_t above = 0;  // 1: keep utilization > limit; 0: keep utilization < limit
+  double limit = 0;
+};
+
 struct DevProgram {
   int32_t nGoals;
   int32_t action;

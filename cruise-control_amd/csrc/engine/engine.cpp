@@ -322,7 +322,7 @@ int64_t Engine::pairScan(GoalImpl& self, const std::vector<int32_t>& pr, const s
 }
 
 int64_t Engine::swapScan(GoalImpl& self, const std::vector<int32_t>& srcs, const std::vector<int32_t>& cbOff,
-                         const std::vector<int32_t>& cbRep) {
+                         const std::vector<int32_t>& cbRep, const SwapLimit& lim) {
   if (srcs.empty() || cbRep.empty()) return -1;
   PhaseScope ps(PH_DEV_SCAN);
   m.flushToDevice();
@@ -333,6 +333,7 @@ int64_t Engine::swapScan(GoalImpl& self, const std::vector<int32_t>& srcs, const
   // throws unless an earlier row accepts a swap
   int64_t throwRow = -1;
   if (prog.newOnly) {
+    if (lim.res >= 0) throw std::logic_error("swapScan: a limit-free candidate list with new brokers");
     const int S = (int)srcs.size();
     for (int g = 0; g + 1 < (int)cbOff.size() && throwRow < 0; ++g) {
       if (cbOff[g] == cbOff[g + 1]) continue;
@@ -350,7 +351,7 @@ int64_t Engine::swapScan(GoalImpl& self, const std::vector<int32_t>& srcs, const
     }
   }
   const int64_t key = dev->scanSwap(prog, srcs.data(), (int)srcs.size(), cbOff.data(), (int)cbOff.size() - 1,
-                                    cbRep.data(), (int)cbRep.size(), &visited);
+                                    cbRep.data(), (int)cbRep.size(), lim, &visited);
   if (throwRow >= 0 && (key < 0 || (key >> 24) > throwRow))
     throw Unsupported("UnsupportedOperationException: removeIf on an unmodifiable sorted replica view");
   checkTerminal(key);
@@ -1715,23 +1716,38 @@ class ResourceDistribution : public GoalImpl {
     baseSpec.selBelowRes = noLimit.selBelowRes;
     baseSpec.belowLimit = noLimit.belowLimit;
     std::vector<int32_t> srcs, cbOff, cbRep, polled;
+    // Without new brokers the limit test runs on the device (SwapLimit) over the limit-free lists; with new brokers
+    // the host filters (eligibleReplicasForSwap's CASE#2 depends on which filtered lists are empty).
+    SwapLimit lim;
+    const bool devLimit = m.numNew == 0;
+    if (devLimit) {
+      lim.res = candSpec.selBelowRes >= 0 ? candSpec.selBelowRes : candSpec.selAboveRes;
+      lim.above = candSpec.selBelowRes >= 0 ? 0 : 1;
+      lim.limit = candSpec.selBelowRes >= 0 ? candSpec.belowLimit : candSpec.aboveLimit;
+    }
     size_t target = 4;
     while (!pqEmpty()) {
-      polled.clear();
-      cbOff.assign(1, 0);
-      cbRep.clear();
-      while (!pqEmpty() && (polled.empty() || polled.size() < target)) {
-        const int cb = pqPoll();
-        polled.push_back(cb);
-        const auto v = m.snapshot(cb, baseSpec);
-        for (int r : *v)  // baseSpec's other selections already hold: only the limit test remains
-          if ((candSpec.selAboveRes < 0 || m.ru(r, candSpec.selAboveRes) > candSpec.aboveLimit) &&
-              (candSpec.selBelowRes < 0 || m.ru(r, candSpec.selBelowRes) < candSpec.belowLimit))
-            cbRep.push_back(r);
-        cbOff.push_back((int32_t)cbRep.size());
+      {  // the polled brokers' candidate rows (limit filter) and the source rows
+        PhaseScope pc(PH_CAND_BUILD);
+        polled.clear();
+        cbOff.assign(1, 0);
+        cbRep.clear();
+        while (!pqEmpty() && (polled.empty() || polled.size() < target)) {
+          const int cb = pqPoll();
+          polled.push_back(cb);
+          const auto v = m.snapshot(cb, baseSpec);
+          if (devLimit)
+            cbRep.insert(cbRep.end(), v->begin(), v->end());
+          else
+            for (int r : *v)  // baseSpec's other selections already hold: only the limit test remains
+              if ((candSpec.selAboveRes < 0 || m.ru(r, candSpec.selAboveRes) > candSpec.aboveLimit) &&
+                  (candSpec.selBelowRes < 0 || m.ru(r, candSpec.selBelowRes) < candSpec.belowLimit))
+                cbRep.push_back(r);
+          cbOff.push_back((int32_t)cbRep.size());
+        }
+        srcs = *m.snapshot(b, srcSpec);
       }
-      srcs = *m.snapshot(b, srcSpec);
-      const int64_t key = e.swapScan(*this, srcs, cbOff, cbRep);
+      const int64_t key = e.swapScan(*this, srcs, cbOff, cbRep, lim);
       if (key < 0) {
         target = std::min<size_t>(target * 2, 1024);
         continue;  // every polled broker exhausted without a swap

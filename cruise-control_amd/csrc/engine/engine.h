@@ -132,7 +132,7 @@ class Engine {
   int64_t pairScan(GoalImpl& self, const std::vector<int32_t>& pr, const std::vector<int32_t>& pb,
                    int action = DA_LEADERSHIP, bool count = true);
   int64_t swapScan(GoalImpl& self, const std::vector<int32_t>& srcs, const std::vector<int32_t>& cbOff,
-                   const std::vector<int32_t>& cbRep);
+                   const std::vector<int32_t>& cbRep, const SwapLimit& lim = SwapLimit());
   void eligible(const std::vector<int32_t>& in, int action, std::vector<int32_t>& out) const;
   // Reference-visited candidates of replica r over cands[0, n) (eligible lists): the entries the replica-dependent
   // filters of GoalUtils.eligibleBrokers keep (blocked), skipping brokers that host r's partition when

@@ -1075,9 +1075,11 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, kServ
 }
 
 // One wavefront per row (m, s). rowsPerBlock = kBlock / 64.
+// With a SwapLimit the candidate lists are limit-free: rows failing the limit are not candidates (not evaluated,
+// not counted), exactly as if the host had filtered them; keys still index the unfiltered list.
 __global__ __launch_bounds__(kBlock) void scan_swap(DevTables T, DevProgram prog, const int32_t* __restrict__ srcs, int S,
                                                     const int32_t* __restrict__ cbOff, const int32_t* __restrict__ cbRep,
-                                                    int M, unsigned long long* __restrict__ result,
+                                                    int M, SwapLimit lim, unsigned long long* __restrict__ result,
                                                     int32_t* __restrict__ rowVisited) {
   const DevView v{T};
   const int lane = threadIdx.x & 63;
@@ -1100,20 +1102,27 @@ __global__ __launch_bounds__(kBlock) void scan_swap(DevTables T, DevProgram prog
       if (lane == 0) rowVisited[row] = 0;
       continue;
     }
-    int visited = c1 - c0;
+    int visited = 0;
     for (int base = c0; base < c1; base += 64) {
       const int idx = base + lane;
+      bool in = idx < c1;
+      if (in && lim.res >= 0) {
+        const double u = v.ru(cbRep[idx], lim.res);
+        in = lim.above ? u > lim.limit : u < lim.limit;
+      }
       int outcome = 0;
-      if (idx < c1) outcome = swapCandidateOutcome(prog, v, sr, cbRep[idx], db);
+      if (in) outcome = swapCandidateOutcome(prog, v, sr, cbRep[idx], db);
+      const unsigned long long passing = __ballot(in);
       const unsigned long long term = __ballot(outcome != 0);
       if (term) {
         const int first = __ffsll((long long)term) - 1;
         const int firstOutcome = __shfl(outcome, first, 64);
         if (firstOutcome == 1 && lane == 0)
           atomicMin(result, ((unsigned long long)row << 24) | (unsigned long long)(base + first - c0));
-        visited = base + first - c0 + 1;
+        visited += __popcll(passing & (first == 63 ? ~0ull : ((2ull << first) - 1)));
         break;
       }
+      visited += __popcll(passing);
     }
     if (lane == 0) rowVisited[row] = visited;
   }
@@ -1463,13 +1472,13 @@ hipError_t launchScanCross(const DevTables& T, const MutTables& M, const UpdateL
 }
 
 hipError_t launchScanSwap(const DevTables& T, const DevProgram& prog, const int32_t* srcs, int S, const int32_t* cbOff,
-                          const int32_t* cbRep, int M, unsigned long long* result, int32_t* rowVisited,
+                          const int32_t* cbRep, int M, const SwapLimit& lim, unsigned long long* result, int32_t* rowVisited,
                           unsigned long long* mail, unsigned long long seq, hipStream_t st, hipEvent_t ev0,
                           hipEvent_t ev1) {
   const uint64_t rows = (uint64_t)M * (uint64_t)S;
   const unsigned blocks = gridFor(rows, kBlock / 64);
   if (ev0) (void)hipEventRecord(ev0, st);
-  hipLaunchKernelGGL(scan_swap, dim3(blocks), dim3(kBlock), 0, st, T, prog, srcs, S, cbOff, cbRep, M, result,
+  hipLaunchKernelGGL(scan_swap, dim3(blocks), dim3(kBlock), 0, st, T, prog, srcs, S, cbOff, cbRep, M, lim, result,
                      rowVisited);
   if (ev1) (void)hipEventRecord(ev1, st);
   hipLaunchKernelGGL(swap_visited_sum, dim3(1), dim3(1024), 0, st, rowVisited, (long long)rows, result, mail, seq);

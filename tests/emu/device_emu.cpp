@@ -255,7 +255,7 @@ int64_t Device::scanPairs(const DevProgram& prog, const int32_t* pr, const int32
 }
 
 int64_t Device::scanSwap(const DevProgram& prog, const int32_t* srcs, int S, const int32_t* cbOff, int M,
-                         const int32_t* cbRep, int nCand, int64_t* visited) {
+                         const int32_t* cbRep, int nCand, const SwapLimit& lim, int64_t* visited) {
   flushOnly();
   View v{E(st_)};
   perf.scanLaunches++;
@@ -268,6 +268,10 @@ int64_t Device::scanSwap(const DevProgram& prog, const int32_t* srcs, int S, con
       const int db = E(st_).rBroker[cbRep[c0]];
       if (swapRowExcluded(prog, v, srcs[s], db)) continue;
       for (int j = c0; j < c1; ++j) {
+        if (lim.res >= 0) {  // the scan_swap limit filter: rows failing it are no candidates
+          const double u = v.ru(cbRep[j], lim.res);
+          if (!(lim.above ? u > lim.limit : u < lim.limit)) continue;
+        }
         const int o = swapCandidateOutcome(prog, v, srcs[s], cbRep[j], db);
         (*visited)++;
         if (o == 1) return ((int64_t)((int64_t)m * S + s) << 24) | (j - c0);
