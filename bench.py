@@ -253,6 +253,22 @@ def pmc_traffic(workload: str, kernels=SCAN_KERNELS):
     return (b / n if n else None), os.path.relpath(paths[-1], REPO)
 
 
+def pmc_server_traffic(workload: str, perf):
+    """HBM bytes per scan-server command: scan_server's counter bytes per launch in the newest committed PMC summary
+    (one proposal of this workload, so its launches serve the same commands per launch as this run) divided by this
+    run's commands per server launch. The counters also see the idle workgroups polling the command word."""
+    import glob
+    paths = sorted(glob.glob(os.path.join(REPO, "profiles", "r*", f"{workload}_pmc_summary.json")))
+    if not paths:
+        return None, None
+    with open(paths[-1]) as f:
+        k = json.load(f)["kernels"].get("scan_server")
+    if not k or perf.server_launches <= 0:
+        return None, None
+    per_launch = perf.server_scans / perf.server_launches
+    return k["hbm_bytes_per_launch"] / per_launch, os.path.relpath(paths[-1], REPO)
+
+
 def scan_cross_line(perf, workload: str):
     """scan_cross alone: its algorithmic bytes per launch (required candidates x BYTES_PER_CANDIDATE) next to its
     calibrated HBM counter bytes per launch from the committed PMC summary (tools/pmc_calib: FETCH_SIZE x2 holds for
@@ -407,6 +423,11 @@ def main() -> None:
     first = results[0]
     parity = check_parity(args.workload, sessions[0][0], first)
     traffic, traffic_src = pmc_traffic(args.workload, INTRA_KERNELS if intra else SCAN_KERNELS)
+    traffic_unit = "HBM bytes per scan launch"
+    if server:
+        st, ss = pmc_server_traffic(args.workload, perf)
+        if st is not None:
+            traffic, traffic_src, traffic_unit = st, ss, "HBM bytes per server command"
     line = {
         "metric": "candidate moves evaluated/s + proposal wall time, 10K brokers/1M replicas",
         "value": cands / elapsed,
@@ -435,7 +456,7 @@ def main() -> None:
         "proposals_per_step": len(first.proposals),
         "per_goal_gpu_s": {g.name: round(g.seconds, 4) for g in first.goal_results},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_unit": "HBM bytes per scan launch",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_unit": traffic_unit,
                      "traffic_source": traffic_src,
                      "kernel": ("K6 intra_brokers (one thread per broker; algorithmic bytes = 17 B per disk + 29 B per "
                                 "replica entry read once)" if intra else
@@ -451,6 +472,8 @@ def main() -> None:
                      "device_evaluated_candidates_per_s": perf.scan_required / (elapsed / args.steps),
                      "chain_launches_per_step": perf.chain_launches,
                      "algorithmic_bytes_per_launch": required_bytes_per_launch,
+                     "traffic_over_algorithmic": (traffic / required_bytes_per_launch
+                                                  if traffic and required_bytes_per_launch else None),
                      "required_candidates_per_step": perf.scan_required,
                      "reference_equivalent_candidates_per_step": inst_cands,
                      "stats_avg_launch_us": perf.stats_kernel_ms * 1e3 / max(1, perf.stats_launches),

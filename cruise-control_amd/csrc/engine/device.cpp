@@ -198,9 +198,11 @@ Device::~Device() {
   }
   void* ps[] = {brokers_, replicas_, parts_, allowedAlive_, topicCount_, topicNrep_, topicScratch_, statsOut_,
                 statsPart_, dReq_, rowVisited_, dResult_, dDone_, tUpper_, tLower_, dRLoad_, dBLoad_, dBLnw_, dBPot_, dPOff_, dPSlots_,
-                dPLeader_, dChainLog_, dChainOut_, pIneligOff_, pIneligB_, topicLead_, tMinLead_, tLeadLim_};
+                dPLeader_, pIneligOff_, pIneligB_, topicLead_, tMinLead_, tLeadLim_};
   for (void* p : ps)
     if (p) (void)hipFree(p);
+  if (hChainLog_) (void)hipHostFree(hChainLog_);
+  if (hChainOut_) (void)hipHostFree(hChainOut_);
   for (void* p : intraAllocs_)
     if (p) (void)hipFree(p);
   if (fg_) (void)hipFree(fg_);
@@ -1000,7 +1002,11 @@ void Device::uploadLoads(int W, const LoadVec* rLoad, const LoadVec* bLoad, cons
   dalloc(&dPOff_, (size_t)P_ + 1);
   dalloc(&dPSlots_, (size_t)R_);
   dalloc(&dPLeader_, (size_t)P_);
-  dalloc(&dChainOut_, 1);
+  if (!hChainOut_) {
+    hipCheck(hipHostMalloc((void**)&hChainOut_, sizeof(ChainResultDev), hipHostMallocMapped | hipHostMallocCoherent),
+             "hipHostMalloc chain result");
+    hipCheck(hipHostGetDevicePointer((void**)&hChainOutDev_, hChainOut_, 0), "hipHostGetDevicePointer");
+  }
   hipCheck(hipMemcpy(dRLoad_, rLoad, sizeof(LoadVec) * R_, hipMemcpyHostToDevice), "upload replica loads");
   hipCheck(hipMemcpy(dBLoad_, bLoad, sizeof(LoadVec) * B_, hipMemcpyHostToDevice), "upload broker loads");
   hipCheck(hipMemcpy(dBLnw_, bLnw, sizeof(LoadVec) * B_, hipMemcpyHostToDevice), "upload leadership loads");
@@ -1053,6 +1059,16 @@ size_t Device::stageChainCopy(size_t reqBytes, Staged& g, size_t& oReq, F fill) 
   return g.end + oR;
 }
 
+void Device::ensureChainLog(size_t n) {
+  if (n <= chainLogCap_) return;
+  if (hChainLog_) (void)hipHostFree(hChainLog_);
+  hChainLog_ = hChainLogDev_ = nullptr;
+  chainLogCap_ = std::max<size_t>(n * 2, 4096);
+  hipCheck(hipHostMalloc((void**)&hChainLog_, chainLogCap_ * sizeof(int32_t), hipHostMallocMapped | hipHostMallocCoherent),
+           "hipHostMalloc chain log");
+  hipCheck(hipHostGetDevicePointer((void**)&hChainLogDev_, hChainLog_, 0), "hipHostGetDevicePointer");
+}
+
 Device::ChainResult Device::chainPairs(const DevProgram& prog, const int32_t* pr, const int32_t* pb,
                                        const int32_t* next, int n, int maxAccepts, std::vector<int32_t>& log) {
   DeviceGuard dg(ordinal_);
@@ -1072,19 +1088,15 @@ Device::ChainResult Device::chainPairs(const DevProgram& prog, const int32_t* pr
     std::memcpy(base + oN, next, (size_t)n * 4);
   });
   (void)at;
-  if ((size_t)n > chainLogCap_) {
-    if (dChainLog_) (void)hipFree(dChainLog_);
-    chainLogCap_ = (size_t)n * 2;
-    dalloc(&dChainLog_, chainLogCap_);
-  }
+  ensureChainLog((size_t)n);
   if (timing) (void)hipEventRecord(EV0, ST);
   hipCheck(launchChainPairs(tables(), chainTables(), prog, (const int32_t*)dReq_, (const int32_t*)(dReq_ + oB),
-                            (const int32_t*)(dReq_ + oN), n, maxAccepts, dChainLog_, dChainOut_, ST),
+                            (const int32_t*)(dReq_ + oN), n, maxAccepts, hChainLogDev_, hChainOutDev_, ST),
            "chain_pairs");
   if (timing) (void)hipEventRecord(EV1, ST);
-  ChainResultDev out;
-  hipCheck(hipMemcpyAsync(&out, dChainOut_, sizeof(out), hipMemcpyDeviceToHost, ST), "chain result");
   hipCheck(hipStreamSynchronize(ST), "chain");
+  const volatile ChainResultDev* vo = hChainOut_;
+  const ChainResultDev out{vo->accepts, vo->visited, vo->failRow};
   perf.syncs++;
   perf.scanLaunches++;
   perf.chainLaunches++;
@@ -1099,7 +1111,7 @@ Device::ChainResult Device::chainPairs(const DevProgram& prog, const int32_t* pr
   res.visited = (int64_t)out.visited;
   log.resize((size_t)res.accepts);
   if (res.accepts)
-    hipCheck(hipMemcpy(log.data(), dChainLog_, sizeof(int32_t) * res.accepts, hipMemcpyDeviceToHost), "chain log");
+    std::memcpy(log.data(), hChainLog_, sizeof(int32_t) * res.accepts);
   return res;
 }
 
@@ -1120,19 +1132,15 @@ Device::ChainResult Device::chainRackRows(const DevProgram& prog, const int32_t*
     std::memcpy(base, rows, (size_t)n * 4);
     std::memcpy(base + oC, cands, (size_t)N * 4);
   });
-  if ((size_t)2 * n > chainLogCap_) {
-    if (dChainLog_) (void)hipFree(dChainLog_);
-    chainLogCap_ = (size_t)4 * n;
-    dalloc(&dChainLog_, chainLogCap_);
-  }
+  ensureChainLog((size_t)2 * n);
   if (timing) (void)hipEventRecord(EV0, ST);
   hipCheck(launchChainRackRows(tables(), chainTables(), prog, (const int32_t*)dReq_, n, (const int32_t*)(dReq_ + oC), N,
-                               dChainLog_, dChainOut_, ST),
+                               hChainLogDev_, hChainOutDev_, ST),
            "chain_rack_rows");
   if (timing) (void)hipEventRecord(EV1, ST);
-  ChainResultDev out;
-  hipCheck(hipMemcpyAsync(&out, dChainOut_, sizeof(out), hipMemcpyDeviceToHost, ST), "chain result");
   hipCheck(hipStreamSynchronize(ST), "chain");
+  const volatile ChainResultDev* vo = hChainOut_;
+  const ChainResultDev out{vo->accepts, vo->visited, vo->failRow};
   perf.syncs++;
   perf.scanLaunches++;
   perf.chainLaunches++;
@@ -1145,7 +1153,7 @@ Device::ChainResult Device::chainRackRows(const DevProgram& prog, const int32_t*
   res.failRow = (int64_t)out.failRow;
   log.resize((size_t)res.accepts * 2);
   if (res.accepts)
-    hipCheck(hipMemcpy(log.data(), dChainLog_, sizeof(int32_t) * 2 * res.accepts, hipMemcpyDeviceToHost), "chain log");
+    std::memcpy(log.data(), hChainLog_, sizeof(int32_t) * 2 * res.accepts);
   int64_t evaluated = res.failRow ? N : 0;
   for (size_t i = 1; i < log.size(); i += 2) evaluated += log[i] + 1;
   perf.scanPairs += evaluated;

@@ -266,9 +266,14 @@ class Device {
   int W_ = 1;
   LoadVec *dRLoad_ = nullptr, *dBLoad_ = nullptr, *dBLnw_ = nullptr, *dBPot_ = nullptr;
   int32_t *dPOff_ = nullptr, *dPSlots_ = nullptr, *dPLeader_ = nullptr;
-  int32_t* dChainLog_ = nullptr;
+  // chain results in host-coherent mapped memory: the kernels write them, the host reads them after the stream sync
+  // (no device-to-host copies per chain)
+  int32_t* hChainLog_ = nullptr;
+  int32_t* hChainLogDev_ = nullptr;
   size_t chainLogCap_ = 0;
-  ChainResultDev* dChainOut_ = nullptr;
+  ChainResultDev* hChainOut_ = nullptr;
+  ChainResultDev* hChainOutDev_ = nullptr;
+  void ensureChainLog(size_t n);
   ChainTables chainTables() const;
   template <class F>
   size_t stageChainCopy(size_t reqBytes, Staged& g, size_t& oReq, F fill);
