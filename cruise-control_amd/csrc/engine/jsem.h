@@ -103,6 +103,24 @@ class RbTreeSet {
     seqKey_.clear();
   }
   int size() const { return size_; }
+  // diagnostics / tests: a fingerprint of the structure (keys with their links and colours, walked from the root)
+  uint64_t shapeHash() const {
+    uint64_t h = 1469598103934665603ull;
+    auto mix = [&h](int64_t v) { h = (h ^ (uint64_t)v) * 1099511628211ull; };
+    std::vector<int> st;
+    if (root_ >= 0) st.push_back(root_);
+    while (!st.empty()) {
+      const int p = st.back();
+      st.pop_back();
+      mix(n_[p].key);
+      mix(n_[p].red);
+      mix(n_[p].left >= 0 ? n_[n_[p].left].key : -1);
+      mix(n_[p].right >= 0 ? n_[n_[p].right].key : -1);
+      if (n_[p].right >= 0) st.push_back(n_[p].right);
+      if (n_[p].left >= 0) st.push_back(n_[p].left);
+    }
+    return h;
+  }
   bool add(int k) {
     int t = root_;
     if (t < 0) {
@@ -352,46 +370,53 @@ class RbTreeSet {
     L.right = p;
     P.parent = l;
   }
-  // TreeMap.fixAfterInsertion
+  // TreeMap.fixAfterInsertion (a red parent is never the root, so the grandparent exists; after the rotation case
+  // the parent of x is black and the JDK loop ends)
   void insertFix(int x) {
-    n_[x].red = 1;
-    while (x >= 0 && x != root_ && n_[n_[x].parent].red) {
-      int g = par(par(x));
-      if (par(x) == lft(g)) {
-        int y = rgt(g);
-        if (isRed(y)) {
-          paint(par(x), false);
-          paint(y, false);
-          paint(g, true);
+    Node* N = n_.data();
+    N[x].red = 1;
+    while (x != root_) {
+      int p = N[x].parent;
+      if (!N[p].red) break;
+      const int g = N[p].parent;
+      if (p == N[g].left) {
+        const int y = N[g].right;
+        if (y >= 0 && N[y].red) {
+          N[p].red = 0;
+          N[y].red = 0;
+          N[g].red = 1;
           x = g;
-        } else {
-          if (x == rgt(par(x))) {
-            x = par(x);
-            rotL(x);
-          }
-          paint(par(x), false);
-          paint(par(par(x)), true);
-          rotR(par(par(x)));
+          continue;
         }
+        if (x == N[p].right) {
+          x = p;
+          rotL(x);
+          p = N[x].parent;
+        }
+        N[p].red = 0;
+        N[g].red = 1;
+        rotR(g);
       } else {
-        int y = lft(g);
-        if (isRed(y)) {
-          paint(par(x), false);
-          paint(y, false);
-          paint(g, true);
+        const int y = N[g].left;
+        if (y >= 0 && N[y].red) {
+          N[p].red = 0;
+          N[y].red = 0;
+          N[g].red = 1;
           x = g;
-        } else {
-          if (x == lft(par(x))) {
-            x = par(x);
-            rotR(x);
-          }
-          paint(par(x), false);
-          paint(par(par(x)), true);
-          rotL(par(par(x)));
+          continue;
         }
+        if (x == N[p].left) {
+          x = p;
+          rotR(x);
+          p = N[x].parent;
+        }
+        N[p].red = 0;
+        N[g].red = 1;
+        rotL(g);
       }
+      break;
     }
-    n_[root_].red = 0;
+    N[root_].red = 0;
   }
   // TreeMap.deleteEntry (successor key copied into the doomed node) + fixAfterDeletion
   void erase(int p) {
