@@ -109,6 +109,7 @@ Device::Device(int ordinal, int B, int R, int P, int T, int maxGoalSlots)
   if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
     throw std::runtime_error(std::string("libccmi is built for gfx950, device is ") + prop.gcnArchName);
   hipCheck(hipStreamCreateWithFlags((hipStream_t*)&st_, hipStreamNonBlocking), "hipStreamCreate");
+  hipCheck(hipStreamCreateWithFlags((hipStream_t*)&st2_, hipStreamNonBlocking), "hipStreamCreate");
   dalloc(&brokers_, (size_t)B);
   dalloc(&replicas_, (size_t)R);
   dalloc(&parts_, (size_t)P);
@@ -213,6 +214,10 @@ Device::~Device() {
   if (ev0_) (void)hipEventDestroy(EV0);
   if (ev1_) (void)hipEventDestroy(EV1);
   if (ST) (void)hipStreamDestroy(ST);
+  if (st2_) {
+    (void)hipStreamSynchronize((hipStream_t)st2_);
+    (void)hipStreamDestroy((hipStream_t)st2_);
+  }
 }
 
 // Staging is only rewritten after the previous request completed (every request waits for its mailbox), so
@@ -632,6 +637,15 @@ void Device::unpackUpdates(const Staged& g) {
 
 // One `prep` launch: apply the staged rows, copy `reqBytes` of request (staged at g.end) into HBM, and (for a
 // scan) reset the result words and the arrival counter.
+// prep on `stream` without stopping the server (the staging kernels of a chain that runs beside it)
+void Device::launchPrepOn(const Staged& g, size_t reqBytes, void* stream) {
+  const int nReq4 = (int)(align16(reqBytes) / 16);
+  if (nReq4) ensureReq((size_t)nReq4 * 16);
+  hipCheck(launchPrep(mutTables(), stagedList(g), (const int4*)(hStageDev_ + g.end), (int4*)dReq_, nReq4, nullptr,
+                      nullptr, (hipStream_t)stream),
+           "prep");
+}
+
 void Device::launchPrepFor(const Staged& g, size_t reqBytes, bool scan) {
   stopServer();
   const int nReq4 = (int)(align16(reqBytes) / 16);
@@ -1038,7 +1052,7 @@ ChainTables Device::chainTables() const {
 // [row updates | load rows | slot rows | request]; launches sync_loads and prep (rows applied, request copied into
 // HBM at dReq_). `fill` writes the request into the staging area.
 template <class F>
-size_t Device::stageChainCopy(size_t reqBytes, Staged& g, size_t& oReq, F fill) {
+size_t Device::stageChainCopy(size_t reqBytes, Staged& g, size_t& oReq, F fill, void* stream) {
   if (!dRLoad_) throw std::runtime_error("device chain state not uploaded");
   const size_t nl = lrows.size(), ns = srows.size();
   const size_t oL = 0, oS = align16(nl * sizeof(LoadRow)), oR = oS + align16(ns * sizeof(SlotRow));
@@ -1047,14 +1061,15 @@ size_t Device::stageChainCopy(size_t reqBytes, Staged& g, size_t& oReq, F fill) 
   std::memcpy(hStage_ + g.end + oS, srows.data(), ns * sizeof(SlotRow));
   fill(hStage_ + g.end + oR);
   hipCheck(launchSyncLoads(chainTables(), (const LoadRow*)(hStageDev_ + g.end + oL), (int)nl,
-                           (const SlotRow*)(hStageDev_ + g.end + oS), (int)ns, ST),
+                           (const SlotRow*)(hStageDev_ + g.end + oS), (int)ns, (hipStream_t)stream),
            "sync_loads");
   lrows.clear();
   srows.clear();
   // prep copies [g.end + oR, + reqBytes) into dReq_ when given the request at that offset
   Staged h = g;
   h.end = g.end + oR;
-  launchPrepFor(h, reqBytes, false);
+  if (stream == st_) launchPrepFor(h, reqBytes, false);
+  else launchPrepOn(h, reqBytes, stream);
   oReq = 0;
   return g.end + oR;
 }
@@ -1072,7 +1087,10 @@ void Device::ensureChainLog(size_t n) {
 Device::ChainResult Device::chainPairs(const DevProgram& prog, const int32_t* pr, const int32_t* pb,
                                        const int32_t* next, int n, int maxAccepts, std::vector<int32_t>& log) {
   DeviceGuard dg(ordinal_);
-  stopServer();
+  static const bool stops = std::getenv("CCMI_CHAIN_STOPS_SERVER") != nullptr;
+  const bool beside = serverOn_ && !stops;
+  if (!beside) stopServer();
+  hipStream_t CS = beside ? (hipStream_t)st2_ : ST;
   ChainResult res;
   log.clear();
   if (n <= 0) {
@@ -1086,15 +1104,18 @@ Device::ChainResult Device::chainPairs(const DevProgram& prog, const int32_t* pr
     std::memcpy(base, pr, (size_t)n * 4);
     std::memcpy(base + oB, pb, (size_t)n * 4);
     std::memcpy(base + oN, next, (size_t)n * 4);
-  });
+  }, CS);
   (void)at;
   ensureChainLog((size_t)n);
-  if (timing) (void)hipEventRecord(EV0, ST);
+  if (timing) (void)hipEventRecord(EV0, CS);
   hipCheck(launchChainPairs(tables(), chainTables(), prog, (const int32_t*)dReq_, (const int32_t*)(dReq_ + oB),
-                            (const int32_t*)(dReq_ + oN), n, maxAccepts, hChainLogDev_, hChainOutDev_, ST),
+                            (const int32_t*)(dReq_ + oN), n, maxAccepts, hChainLogDev_, hChainOutDev_, CS),
            "chain_pairs");
-  if (timing) (void)hipEventRecord(EV1, ST);
-  hipCheck(hipStreamSynchronize(ST), "chain");
+  if (timing) (void)hipEventRecord(EV1, CS);
+  hipCheck(hipStreamSynchronize(CS), "chain");
+  // the chain's record writes (and its staging kernels') become visible to the server's next command through the
+  // agent acquire its workgroups take on a new rows epoch
+  if (beside) ++rowsEpoch_;
   const volatile ChainResultDev* vo = hChainOut_;
   const ChainResultDev out{vo->accepts, vo->visited, vo->failRow};
   perf.syncs++;
@@ -1118,7 +1139,10 @@ Device::ChainResult Device::chainPairs(const DevProgram& prog, const int32_t* pr
 Device::ChainResult Device::chainRackRows(const DevProgram& prog, const int32_t* rows, int n, const int32_t* cands,
                                           int N, std::vector<int32_t>& log) {
   DeviceGuard dg(ordinal_);
-  stopServer();
+  static const bool stops = std::getenv("CCMI_CHAIN_STOPS_SERVER") != nullptr;
+  const bool beside = serverOn_ && !stops;
+  if (!beside) stopServer();
+  hipStream_t CS = beside ? (hipStream_t)st2_ : ST;
   ChainResult res;
   log.clear();
   if (n <= 0) {
@@ -1131,14 +1155,17 @@ Device::ChainResult Device::chainRackRows(const DevProgram& prog, const int32_t*
   (void)stageChainCopy(req, g, oReq, [&](char* base) {
     std::memcpy(base, rows, (size_t)n * 4);
     std::memcpy(base + oC, cands, (size_t)N * 4);
-  });
+  }, CS);
   ensureChainLog((size_t)2 * n);
-  if (timing) (void)hipEventRecord(EV0, ST);
+  if (timing) (void)hipEventRecord(EV0, CS);
   hipCheck(launchChainRackRows(tables(), chainTables(), prog, (const int32_t*)dReq_, n, (const int32_t*)(dReq_ + oC), N,
-                               hChainLogDev_, hChainOutDev_, ST),
+                               hChainLogDev_, hChainOutDev_, CS),
            "chain_rack_rows");
-  if (timing) (void)hipEventRecord(EV1, ST);
-  hipCheck(hipStreamSynchronize(ST), "chain");
+  if (timing) (void)hipEventRecord(EV1, CS);
+  hipCheck(hipStreamSynchronize(CS), "chain");
+  // the chain's record writes (and its staging kernels') become visible to the server's next command through the
+  // agent acquire its workgroups take on a new rows epoch
+  if (beside) ++rowsEpoch_;
   const volatile ChainResultDev* vo = hChainOut_;
   const ChainResultDev out{vo->accepts, vo->visited, vo->failRow};
   perf.syncs++;

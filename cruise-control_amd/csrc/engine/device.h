@@ -187,6 +187,10 @@ class Device {
  private:
   int ordinal_, B_, R_, P_, T_, ldB_, G_;
   void* st_ = nullptr;  // hipStream_t
+  // K7 chains (and their staging kernels) run on this second stream beside a running scan server (its workgroups use
+  // 200 VGPRs per wave and 16 KB LDS, so a chain workgroup fits on a CU next to one), instead of stopping and
+  // relaunching the server around every chain. CCMI_CHAIN_STOPS_SERVER=1 restores stop-and-relaunch.
+  void* st2_ = nullptr;
   // tables (records, devtypes.h) and the host copies used to assemble them
   BrokerRec* brokers_ = nullptr;
   ReplicaRec* replicas_ = nullptr;
@@ -225,6 +229,7 @@ class Device {
   void ensureStage(size_t bytes);
   void ensureReq(size_t bytes);
   void launchPrepFor(const Staged& g, size_t reqBytes, bool scan);
+  void launchPrepOn(const Staged& g, size_t reqBytes, void* stream);
   UpdateList stagedList(const Staged& g) const;
   UpdateList overlayFor(const Staged& g) const;
   MutTables mutTables() const;
@@ -276,7 +281,7 @@ class Device {
   void ensureChainLog(size_t n);
   ChainTables chainTables() const;
   template <class F>
-  size_t stageChainCopy(size_t reqBytes, Staged& g, size_t& oReq, F fill);
+  size_t stageChainCopy(size_t reqBytes, Staged& g, size_t& oReq, F fill, void* stream);
   // disk state (K6)
   int D_ = 0;
   int32_t *dBDiskOff_ = nullptr, *dBDisks_ = nullptr, *dROrigDisk_ = nullptr, *dRTie_ = nullptr;
