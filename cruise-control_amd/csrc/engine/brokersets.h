@@ -111,7 +111,11 @@ struct BrokerSets {
     policy = c->broker_set_policy;
     if (policy != CCMI_BROKER_SET_TOPIC_NAME_HASH && policy != CCMI_BROKER_SET_ORIGINAL_BROKER)
       throw std::invalid_argument("unknown replica-to-broker-set mapping policy");
-    std::map<std::string, std::vector<int32_t>> byName;  // broker set id -> Kafka broker ids
+    // broker set id -> the session's broker ids. The session's ids are dense (ccmi_cluster_desc.broker_id[b] == b;
+    // the builder numbers brokers in ascending Kafka-id order, ccmi_builder_broker_ids), so the caller maps its Kafka
+    // ids through that table and passes -1 for an id the model does not hold; such a member (any id outside [0, B))
+    // resolves to no broker, as a broker-set entry naming a broker absent from the cluster does in the reference.
+    std::map<std::string, std::vector<int32_t>> byName;
     for (int s = 0; s < c->num_broker_sets; ++s) {
       auto& v = byName[c->broker_set_names[s]];
       for (int k = c->broker_set_offset[s]; k < c->broker_set_offset[s + 1]; ++k) v.push_back(c->broker_set_members[k]);

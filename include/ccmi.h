@@ -215,7 +215,9 @@ typedef struct ccmi_balancing_constraint {
   int32_t broker_set_policy;              /* ccmi_broker_set_policy */
   const char* const* broker_set_names;    /* [num_broker_sets] brokerSetId */
   const int32_t* broker_set_offset;       /* [num_broker_sets + 1] CSR into broker_set_members */
-  const int32_t* broker_set_members;      /* Kafka broker ids */
+  const int32_t* broker_set_members;      /* broker indices of the session, in [0, B): a Kafka id's position in
+                                           * ccmi_builder_broker_ids (ascending Kafka ids); -1 (any id outside
+                                           * [0, B)) = a broker the model does not hold, ignored */
   /* MinTopicLeadersPerBrokerGoal (ABI v5): the topics topics.with.min.leaders.per.broker matches — the caller's
    * Utils.getTopicNamesMatchedWithPattern(BalancingConstraint.topicsWithMinLeadersPerBrokerPattern(), topics)
    * (common/Utils.java:26-36, BalancingConstraint.java:92,275-277), as topic indices of the session's desc (0 topics =

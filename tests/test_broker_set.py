@@ -215,6 +215,16 @@ def test_emu_random_unmapped_broker_fails_like_oracle(emu_lib, oracle_lib):
     assert res is None  # both raised the same OptimizationFailureException
 
 
+def test_emu_broker_set_member_outside_session_ignored(emu_lib, oracle_lib):
+    """Members are the session's dense broker indices (ccmi_builder_broker_ids order); -1 or an id outside [0, B) (a
+    Kafka id the model does not hold) resolves to no broker, as an absent broker does in the reference: "west" naming
+    1001 and -1 instead of broker 23 leaves 23 unmapped, exactly the unmapped case, with the same failure."""
+    buf, bc = random_case(40, unmapped=True)
+    bc.broker_sets["west"] = bc.broker_sets["west"] + [1001, -1]
+    _, res, _ = check_desc_against_oracle(emu_lib, buf.desc, buf, [BSA], bc)
+    assert res is None
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("goals", [[BSA], [BSA, "ReplicaCapacityGoal", "DiskCapacityGoal", "ReplicaDistributionGoal",
                                           "CpuUsageDistributionGoal", "LeaderReplicaDistributionGoal"]],
