@@ -458,7 +458,7 @@ def main() -> None:
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_unit": traffic_unit,
                      "traffic_source": traffic_src,
-                     "kernel": ("K6 intra_brokers (one thread per broker; algorithmic bytes = 17 B per disk + 29 B per "
+                     "kernel": ("K6 intra_brokers (one wavefront per broker; algorithmic bytes = 17 B per disk + 29 B per "
                                 "replica entry read once)" if intra else
                                 "K8 scan_server (persistent; per command: in-kernel busy time, the command's required "
                                 "candidates x 96 B)" if server else

@@ -1087,8 +1087,10 @@ void Device::ensureChainLog(size_t n) {
 Device::ChainResult Device::chainPairs(const DevProgram& prog, const int32_t* pr, const int32_t* pb,
                                        const int32_t* next, int n, int maxAccepts, std::vector<int32_t>& log) {
   DeviceGuard dg(ordinal_);
-  static const bool stops = std::getenv("CCMI_CHAIN_STOPS_SERVER") != nullptr;
-  const bool beside = serverOn_ && !stops;
+  // opt-in (CCMI_CHAIN_BESIDE_SERVER=1): the chain on a second stream beside the running server hung the C2 default
+  // chain in the full GPU suite (test_gpu_matches_headline_golden[c2_default], r03); by default the server is stopped
+  static const bool besideOk = std::getenv("CCMI_CHAIN_BESIDE_SERVER") != nullptr;
+  const bool beside = serverOn_ && besideOk;
   if (!beside) stopServer();
   hipStream_t CS = beside ? (hipStream_t)st2_ : ST;
   ChainResult res;
@@ -1139,8 +1141,10 @@ Device::ChainResult Device::chainPairs(const DevProgram& prog, const int32_t* pr
 Device::ChainResult Device::chainRackRows(const DevProgram& prog, const int32_t* rows, int n, const int32_t* cands,
                                           int N, std::vector<int32_t>& log) {
   DeviceGuard dg(ordinal_);
-  static const bool stops = std::getenv("CCMI_CHAIN_STOPS_SERVER") != nullptr;
-  const bool beside = serverOn_ && !stops;
+  // opt-in (CCMI_CHAIN_BESIDE_SERVER=1): the chain on a second stream beside the running server hung the C2 default
+  // chain in the full GPU suite (test_gpu_matches_headline_golden[c2_default], r03); by default the server is stopped
+  static const bool besideOk = std::getenv("CCMI_CHAIN_BESIDE_SERVER") != nullptr;
+  const bool beside = serverOn_ && besideOk;
   if (!beside) stopServer();
   hipStream_t CS = beside ? (hipStream_t)st2_ : ST;
   ChainResult res;

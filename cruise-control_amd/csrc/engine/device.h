@@ -189,7 +189,7 @@ class Device {
   void* st_ = nullptr;  // hipStream_t
   // K7 chains (and their staging kernels) run on this second stream beside a running scan server (its workgroups use
   // 200 VGPRs per wave and 16 KB LDS, so a chain workgroup fits on a CU next to one), instead of stopping and
-  // relaunching the server around every chain. CCMI_CHAIN_STOPS_SERVER=1 restores stop-and-relaunch.
+  // relaunching the server around every chain: opt-in only (CCMI_CHAIN_BESIDE_SERVER=1; it hung the C2 chain in r03).
   void* st2_ = nullptr;
   // tables (records, devtypes.h) and the host copies used to assemble them
   BrokerRec* brokers_ = nullptr;

@@ -1,4 +1,4 @@
-// K6: the intra-broker (JBOD) goals, one broker per device thread. Disks belong to one broker and the intra-broker
+// K6: the intra-broker (JBOD) goals, one broker per device wavefront. Disks belong to one broker and the intra-broker
 // goals never move a replica between brokers, so every broker's rebalance is independent of every other broker's:
 // the reference's sequential broker loop (AbstractGoal.optimize :98-101) runs as B independent programs and the host
 // concatenates their action logs in broker-id order. Written once for the gfx950 kernel (kernels/intra.hip) and the
@@ -112,8 +112,13 @@ CCMI_LD uint64_t intraSortKey(float score, int32_t tie, bool reverse) {
 
 class IntraBroker {
  public:
-  CCMI_LD IntraBroker(const IntraArgs& a, int broker) : A(a), b(broker) {
+  // snapA / snapB: the two snapshot buffers (nullptr = the broker's CSR range of A.snapA / A.snapB); the kernel passes
+  // LDS buffers when the broker's selected entries fit
+  CCMI_LD IntraBroker(const IntraArgs& a, int broker, int32_t* snapA = nullptr, int32_t* snapB = nullptr)
+      : A(a), b(broker) {
     e0 = A.eOff[b];
+    sa = snapA ? snapA : A.snapA + e0;
+    sb = snapB ? snapB : A.snapB + e0;
     e1 = A.eOff[b + 1];
     d0 = A.bDiskOff[b];
     d1 = A.bDiskOff[b + 1];
@@ -145,6 +150,8 @@ class IntraBroker {
   int64_t cand = 0;
   double up = 0, lo = 0;  // this goal's thresholds (IG_USAGE)
   int nSel = 0;           // selected entries (ordRev / ordFwd length)
+  int32_t* sa;            // snapshot buffers
+  int32_t* sb;
 
   CCMI_LD double pct(int d) const { return A.dCap[d] > 0 ? A.dUtil[d] / A.dCap[d] : 1.0; }
   CCMI_LD double avgPct() const {
@@ -161,8 +168,33 @@ class IntraBroker {
   CCMI_LD double du(int i) const { return A.rDu[A.eRep[i]]; }
 
   // the disk's tracked sorted replicas (a clone), as entry indices into out[0..n): prioritizeDiskImmigrants puts the
-  // replicas whose original disk is not d first, each group in the static order
-  CCMI_LD int snapshot(int d, bool reverse, int32_t* out) const {
+  // replicas whose original disk is not d first, each group in the static order. On the device the broker's wavefront
+  // runs the program redundantly on every lane (uniform control flow, identical stores) and only this filter is split
+  // over the lanes: 64 entries per step, the kept ones compacted in order by a ballot prefix count.
+#if defined(__HIP_DEVICE_COMPILE__)
+  __device__ int snapshot(int d, bool reverse, int32_t* out) const {
+    const int32_t* ord = (reverse ? A.ordRev : A.ordFwd) + e0;
+    const int lane = threadIdx.x & 63;
+    const uint64_t below = (1ull << lane) - 1;
+    int n = 0;
+    for (int pass = 0; pass < 2; ++pass)
+      for (int k0 = 0; k0 < nSel; k0 += 64) {
+        const int k = k0 + lane;
+        bool keep = false;
+        int i = 0;
+        if (k < nSel) {
+          i = ord[k];
+          keep = A.eDisk[i] == d && ((A.rOrigDisk[A.eRep[i]] != d) == (pass == 0));
+        }
+        const uint64_t m = __ballot(keep);
+        if (keep) out[n + __popcll(m & below)] = i;
+        n += __popcll(m);
+      }
+    __syncthreads();  // the block is this one wavefront: every lane sees the compacted list (LDS or global)
+    return n;
+  }
+#else
+  int snapshot(int d, bool reverse, int32_t* out) const {
     const int32_t* ord = (reverse ? A.ordRev : A.ordFwd) + e0;
     int n = 0;
     for (int pass = 0; pass < 2; ++pass)
@@ -172,6 +204,7 @@ class IntraBroker {
       }
     return n;
   }
+#endif
 
   CCMI_LD void record(int r, int src, int dst) {
     if (nLog >= logCap) {
@@ -285,9 +318,9 @@ class IntraBroker {
     timSortSmall(cands, nC);
     for (int k = 0; k < nOver; ++k) {
       const int d = overD[k];
-      const int n = snapshot(d, true, A.snapA + e0);
+      const int n = snapshot(d, true, sa);
       for (int q = 0; q < n; ++q) {
-        maybeMove(A.snapA[e0 + q], cands, nC);
+        maybeMove(sa[q], cands, nC);
         if (!over(d)) break;
       }
     }
@@ -407,9 +440,9 @@ class IntraBroker {
     const int32_t one[1] = {disk};
     while (n > 0) {
       const int cd = pqPoll(q, n, true);
-      const int m = snapshot(cd, true, A.snapA + e0);
+      const int m = snapshot(cd, true, sa);
       for (int s = 0; s < m; ++s) {
-        if (maybeMove(A.snapA[e0 + s], one, 1) >= 0) {
+        if (maybeMove(sa[s], one, 1) >= 0) {
           if (pct(disk) > lo) return false;
           if (n > 0 && pct(cd) < pct(q[0])) {
             pqAdd(q, n, cd, true);
@@ -431,9 +464,9 @@ class IntraBroker {
     while (n > 0) {
       const int cd = pqPoll(q, n, false);
       const int32_t one[1] = {cd};
-      const int m = snapshot(disk, true, A.snapA + e0);
+      const int m = snapshot(disk, true, sa);
       for (int s = 0; s < m; ++s) {
-        if (maybeMove(A.snapA[e0 + s], one, 1) >= 0) {
+        if (maybeMove(sa[s], one, 1) >= 0) {
           if (pct(disk) < up) return false;
           if (n > 0 && pct(cd) > pct(q[0])) {
             pqAdd(q, n, cd, false);
@@ -457,10 +490,10 @@ class IntraBroker {
     while (n > 0) {
       const int cd = pqPoll(q, n, in);
       bool swapped = false;
-      const int m = snapshot(disk, !in, A.snapA + e0);
-      const int c = snapshot(cd, in, A.snapB + e0);  // the candidate view cannot change before a swap
+      const int m = snapshot(disk, !in, sa);
+      const int c = snapshot(cd, in, sb);  // the candidate view cannot change before a swap
       for (int s = 0; s < m; ++s) {
-        if (maybeSwap(A.snapA[e0 + s], A.snapB + e0, c)) {
+        if (maybeSwap(sa[s], sb, c)) {
           if (in ? pct(disk) > lo : pct(disk) < up) return;
           swapped = true;
           break;

@@ -3,9 +3,11 @@
 //
 // intra_sort    : one wavefront per broker: its replicas' fixed sort orders (reverse / forward DISK score, then
 //                 Replica.compareTo) by rank counting over LDS tiles.
-// intra_brokers : one thread per broker. A broker's rebalance touches only its own disks and replicas, so the B
+// intra_brokers : one wavefront per broker. A broker's rebalance touches only its own disks and replicas, so the B
 //                 programs of a goal are independent; each reads its replicas' records (contiguous CSR range) and its
-//                 disks, and writes its ordered action records into its own log range.
+//                 disks, and writes its ordered action records into its own log range. The decisions are sequential
+//                 (first fit, Java order), so every lane runs them redundantly; the O(entries) disk snapshots, which
+//                 dominate, are filtered 64 entries per step into LDS (global scratch for brokers over kIntraLdsSnap).
 // intra_compact : packs the per-broker log ranges into one array in broker-id order (the reference's action order).
 // stats_disks   : per alive broker (one thread each, up to kDiskStatsBlocks workgroups) the average disk utilization
 //                 percentage and its disks' deviations; unbalanced-disk count and variance sum folded per workgroup,
@@ -66,10 +68,12 @@ __global__ __launch_bounds__(64) void intra_sort(IntraArgs A) {
   if (lane == 0) A.nSel[b] = selCount;
 }
 
+constexpr int kIntraLdsSnap = 2048;
 __global__ __launch_bounds__(64) void intra_brokers(IntraArgs A) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= A.nBrokers) return;
-  IntraBroker ib(A, A.brokers[i]);
+  __shared__ int32_t sA[kIntraLdsSnap], sB[kIntraLdsSnap];
+  const int b = A.brokers[blockIdx.x];
+  const bool lds = A.nSel[b] <= kIntraLdsSnap;  // a snapshot holds at most the broker's selected entries
+  IntraBroker ib(A, b, lds ? sA : nullptr, lds ? sB : nullptr);
   ib.run();
 }
 
@@ -187,7 +191,7 @@ hipError_t launchIntraSort(const IntraArgs& A, hipStream_t st) {
 
 hipError_t launchIntra(const IntraArgs& A, hipStream_t st) {
   if (A.nBrokers <= 0) return hipSuccess;
-  hipLaunchKernelGGL(intra_brokers, dim3((A.nBrokers + 63) / 64), dim3(64), 0, st, A);
+  hipLaunchKernelGGL(intra_brokers, dim3(A.nBrokers), dim3(64), 0, st, A);
   return hipGetLastError();
 }
 
