@@ -19,7 +19,7 @@ from __future__ import annotations
 import ctypes as C
 import os
 from dataclasses import dataclass, field
-from typing import Dict, List, Optional, Sequence
+from typing import Dict, Iterable, List, Optional, Sequence
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 DEFAULT_LIB = os.path.join(_HERE, "libccmi.so")
@@ -212,7 +212,7 @@ class DeviceError(CruiseControlError):
 _STATUS = {1: IllegalArgumentException, 2: DeviceError, 3: OptimizationFailureException, 4: IllegalStateException,
            5: UnsupportedOperationException}
 
-ABI_VERSION = 7  # CCMI_ABI_VERSION of include/ccmi.h
+ABI_VERSION = 8  # CCMI_ABI_VERSION of include/ccmi.h
 EXPORTED_SYMBOLS = (
     "ccmi_last_error", "ccmi_abi_version", "ccmi_device_count", "ccmi_default_constraint", "ccmi_default_random_cluster_props",
     "ccmi_random_cluster", "ccmi_cluster_buffers_desc", "ccmi_cluster_buffers_free", "ccmi_session_create",
@@ -253,7 +253,8 @@ class Library:
         L.ccmi_session_destroy.argtypes = [C.c_void_p]
         L.ccmi_optimizations.argtypes = [C.c_void_p, C.POINTER(C.c_int32), C.c_int32, C.POINTER(ConstraintStruct),
                                          C.POINTER(OptionsStruct), C.POINTER(GoalResultStruct)]
-        L.ccmi_goal_optimize.argtypes = [C.c_void_p, C.c_int32, C.POINTER(ConstraintStruct), C.POINTER(OptionsStruct),
+        L.ccmi_goal_optimize.argtypes = [C.c_void_p, C.c_int32, C.POINTER(C.c_int32), C.c_int32,
+                                         C.POINTER(ConstraintStruct), C.POINTER(OptionsStruct),
                                          C.POINTER(GoalResultStruct)]
         L.ccmi_action_acceptance.argtypes = [C.c_void_p, C.c_int32, C.POINTER(ActionStruct), C.POINTER(C.c_int32)]
         L.ccmi_action_acceptance_by_kind.argtypes = [C.c_void_p, C.c_int32, C.POINTER(ActionStruct),
@@ -361,7 +362,11 @@ class BalancingConstraint:
             raise IllegalArgumentException("topics.with.min.leaders.per.broker needs the cluster's topic names")
         return [t for t, n in enumerate(topic_names) if pat.fullmatch(n)]
 
-    def to_struct(self, topic_names: Optional[Sequence[str]] = None) -> ConstraintStruct:
+    def to_struct(self, topic_names: Optional[Sequence[str]] = None,
+                  broker_ids: Optional[Sequence[int]] = None) -> ConstraintStruct:
+        """broker_ids: the session's Kafka broker id of every broker index (ClusterModel.broker_ids); the broker ids
+        of `broker_sets` are mapped through it to the session's dense indices (ccmi_balancing_constraint
+        broker_set_members), an id the model does not hold to -1. None: ids are the indices."""
         s = ConstraintStruct()
         s.resource_balance_percentage[:] = list(self.resource_balance_percentage)
         s.capacity_threshold[:] = list(self.capacity_threshold)
@@ -382,7 +387,9 @@ class BalancingConstraint:
         s.topic_leader_replica_balance_margin = self.topic_leader_replica_balance_margin
         if self.broker_sets:
             names = list(self.broker_sets)
-            members = [int(b) for n in names for b in self.broker_sets[n]]
+            index_of = None if broker_ids is None else {int(k): i for i, k in enumerate(broker_ids)}
+            members = [int(b) if index_of is None else index_of.get(int(b), -1)
+                       for n in names for b in self.broker_sets[n]]
             offs = [0]
             for n in names:
                 offs.append(offs[-1] + len(self.broker_sets[n]))
@@ -471,9 +478,15 @@ class Goal:
     def is_hard_goal(self) -> bool:
         return self._name in self.HARD_GOALS
 
-    def optimize(self, cluster: "ClusterModel", options: Optional[OptimizationOptions] = None) -> bool:
-        """Goal.optimize: the session remembers this goal as optimized afterwards."""
-        res = cluster._goal_optimize(self, options)
+    def optimize(self, cluster: "ClusterModel", optimized_goals: Iterable["Goal"] = (),
+                 options: Optional[OptimizationOptions] = None) -> bool:
+        """Goal.optimize(clusterModel, optimizedGoals, optimizationOptions) (Goal.java:60-68). Only the goals in
+        `optimized_goals` constrain this goal's moves through their actionAcceptance; each must have been optimized
+        on this session (else UnsupportedOperationException: the JVM would run the goal). The session
+        keeps this goal, with its frozen state, for later optimized_goals sets."""
+        if isinstance(optimized_goals, OptimizationOptions):
+            raise IllegalArgumentException("Goal.optimize(cluster, optimized_goals, options): optimized_goals first")
+        res = cluster._goal_optimize(self, optimized_goals, options)
         return bool(res.succeeded)
 
     def __repr__(self) -> str:
@@ -1052,6 +1065,13 @@ class ClusterModel:
     def topic_names(self) -> List[str]:
         return [self.desc.topic_names[t].decode() for t in range(self.desc.num_topics)]
 
+    def broker_ids(self) -> List[int]:
+        """Kafka broker id of every broker index: the LoadMonitorModel's id table when the desc came from one
+        (ccmi_builder_broker_ids), else the desc's broker_id."""
+        if hasattr(self._keep, "broker_ids"):
+            return list(self._keep.broker_ids())
+        return [self.desc.broker_id[b] for b in range(self.desc.num_brokers)]
+
     @staticmethod
     def from_buffers(buf: ClusterBuffers, device: int = 0) -> "ClusterModel":
         return ClusterModel(buf.desc, device=device, lib=buf.lib, keepalive=buf)
@@ -1067,11 +1087,15 @@ class ClusterModel:
         except Exception:
             pass
 
-    def _goal_optimize(self, goal: Goal, options: Optional[OptimizationOptions]) -> GoalResultStruct:
+    def _goal_optimize(self, goal: Goal, optimized_goals: Iterable[Goal],
+                       options: Optional[OptimizationOptions]) -> GoalResultStruct:
         res = GoalResultStruct()
         o, keep = (options or OptimizationOptions()).to_struct()
-        c = (goal.constraint or BalancingConstraint()).to_struct(self.topic_names())
-        self._checked(self.lib.lib.ccmi_goal_optimize(self.handle, goal.kind, C.byref(c), C.byref(o), C.byref(res)))
+        c = (goal.constraint or BalancingConstraint()).to_struct(self.topic_names(), self.broker_ids())
+        prior = [g.kind if isinstance(g, Goal) else int(g) for g in optimized_goals]
+        kinds = (C.c_int32 * max(1, len(prior)))(*prior)
+        self._checked(self.lib.lib.ccmi_goal_optimize(self.handle, goal.kind, kinds, len(prior), C.byref(c),
+                                                      C.byref(o), C.byref(res)))
         goal.provision = ProvisionResponse.from_struct(res.provision, goal.name())
         return res
 
@@ -1123,7 +1147,7 @@ class ClusterModel:
                       options: Optional[OptimizationOptions] = None) -> Dict[str, object]:
         s = StatsStruct()
         o, keep = (options or OptimizationOptions()).to_struct()
-        c = (constraint or BalancingConstraint()).to_struct(self.topic_names())
+        c = (constraint or BalancingConstraint()).to_struct(self.topic_names(), self.broker_ids())
         self.lib.check(self.lib.lib.ccmi_compute_cluster_stats(self.handle, C.byref(c), C.byref(o), C.byref(s)))
         return stats_to_dict(s)
 
@@ -1231,7 +1255,7 @@ class GoalOptimizer:
         kinds = (C.c_int32 * len(goals_by_priority))(*[g.kind for g in goals_by_priority])
         results = (GoalResultStruct * len(goals_by_priority))()
         o, keep = (options or OptimizationOptions()).to_struct()
-        c = self.constraint.to_struct(cluster.topic_names())
+        c = self.constraint.to_struct(cluster.topic_names(), cluster.broker_ids())
         import time
         t0 = time.perf_counter()
         cluster._checked(cluster.lib.lib.ccmi_optimizations(cluster.handle, kinds, len(goals_by_priority),
@@ -1306,7 +1330,7 @@ class GoalViolationDetector:
             cm = ClusterModel(desc, device=self.devices[i % len(self.devices)], lib=self.lib, keepalive=keepalive)
             goal = goals_from_names([name], self.constraint)[0]
             try:
-                goal.optimize(cm, opts)
+                goal.optimize(cm, set(), opts)
             except OptimizationFailureException as e:
                 return name, "unfixable", e.provision
             diff = cm.proposals()

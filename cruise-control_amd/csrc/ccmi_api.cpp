@@ -189,11 +189,11 @@ struct Placement {
 // A chain is either broker-granularity or disk-granularity: each kind's actionAcceptance rejects the other's actions
 // with IllegalArgumentException (e.g. ResourceDistributionGoal.actionAcceptance default branch,
 // IntraBrokerDiskCapacityGoal.actionAcceptance :120-124), so a mixed chain is refused up front.
-void validateChain(const ccmi_session* s, const int32_t* kinds, int n) {
+void validateChain(const ccmi_session* s, const int32_t* kinds, int n, const std::vector<ccmi::GoalImpl*>& priors = {}) {
   int intra = 0;
   for (int i = 0; i < n; ++i) intra += ccmi::isIntraGoalKind(kinds[i]) ? 1 : 0;
-  for (auto& g : s->engine->optimized) intra += ccmi::isIntraGoalKind(g->kind) ? 1 : 0;
-  const int total = n + (int)s->engine->optimized.size();
+  for (const ccmi::GoalImpl* g : priors) intra += ccmi::isIntraGoalKind(g->kind) ? 1 : 0;
+  const int total = n + (int)priors.size();
   if (intra != 0 && intra != total)
     throw std::invalid_argument("intra-broker goals cannot be optimized together with inter-broker goals");
   // host resources (Resource.isHostResource: CPU, NW_IN, NW_OUT) are checked against the host's load and capacity by
@@ -314,7 +314,7 @@ ccmi_status ccmi_session_create(int32_t device_ordinal, const ccmi_cluster_desc*
     auto s = std::make_unique<ccmi_session>();
     s->model.build(*desc);
     ccmi::Model& m = s->model;
-    s->device = std::make_unique<ccmi::Device>(device_ordinal, m.B, m.R, m.P, m.T, ccmi::kMaxGoals);
+    s->device = std::make_unique<ccmi::Device>(device_ordinal, m.B, m.R, m.P, m.T, ccmi::kMaxSlots);
     s->device->setRowSource(m.rBroker.data(), m.rPart.data(), m.pTopic.data());
     s->deviceOrdinal = device_ordinal;
     // device layout: resource-major broker/replica columns
@@ -414,18 +414,31 @@ ccmi_status ccmi_session_destroy(ccmi_session* s) {
   });
 }
 
-ccmi_status ccmi_goal_optimize(ccmi_session* s, int32_t goal_kind, const ccmi_balancing_constraint* c,
+ccmi_status ccmi_goal_optimize(ccmi_session* s, int32_t goal_kind, const int32_t* optimized_goal_kinds,
+                               int32_t num_optimized_goals, const ccmi_balancing_constraint* c,
                                const ccmi_opt_options* o, ccmi_goal_result* result) {
   return guarded([&] {
     if (!s) throw std::invalid_argument("null session");
+    if (num_optimized_goals < 0 || (num_optimized_goals > 0 && !optimized_goal_kinds))
+      throw std::invalid_argument("null optimized_goal_kinds");
+    // Set<Goal> optimizedGoals: each kind resolves to the session's own optimization of it (its frozen state); a goal
+    // the session does not hold (run in the JVM, or a JVM-only goal class) cannot join the device conjunction
+    std::vector<ccmi::GoalImpl*> priors;
+    for (int i = 0; i < num_optimized_goals; ++i) {
+      ccmi::GoalImpl* g = s->engine->optimizedOfKind(optimized_goal_kinds[i]);
+      if (!g)
+        throw ccmi::Unsupported("optimized goal kind " + std::to_string(optimized_goal_kinds[i]) +
+                                " has not been optimized by this session: its actionAcceptance is not available here");
+      if (std::find(priors.begin(), priors.end(), g) == priors.end()) priors.push_back(g);
+    }
+    auto g = ccmi::makeGoal(goal_kind);
     StopServerOnExit stop{s};
     setOptions(s, c, o);
-    validateChain(s, &goal_kind, 1);
-    auto g = ccmi::makeGoal(goal_kind);
+    validateChain(s, &goal_kind, 1, priors);
     ccmi_goal_result tmp;
     std::memset(&tmp, 0, sizeof(tmp));
     const Placement pre(s->model);
-    s->engine->optimizeGoal(std::move(g), &tmp);
+    s->engine->optimizeGoal(std::move(g), priors, &tmp);
     tmp.has_diff = Placement(s->model) != pre ? 1 : 0;
     if (result) *result = tmp;
     buildProposals(s);
@@ -442,11 +455,16 @@ ccmi_status ccmi_optimizations(ccmi_session* s, const int32_t* goal_kinds, int32
     setOptions(s, c, o);
     validateChain(s, goal_kinds, n_goals);
     for (int i = 0; i < n_goals; ++i) (void)ccmi::makeGoal(goal_kinds[i]);  // fail fast on unsupported kinds
+    // optimizedGoals starts empty for every call (GoalOptimizer.java:449) and collects this call's goals (:471)
+    std::vector<int32_t> done;
     for (int i = 0; i < n_goals; ++i) {
       ccmi_goal_result tmp;
       std::memset(&tmp, 0, sizeof(tmp));
       const Placement pre(s->model);
-      s->engine->optimizeGoal(ccmi::makeGoal(goal_kinds[i]), &tmp);
+      std::vector<ccmi::GoalImpl*> priors;
+      for (int32_t k : done) priors.push_back(s->engine->optimizedOfKind(k));
+      s->engine->optimizeGoal(ccmi::makeGoal(goal_kinds[i]), priors, &tmp);
+      if (std::find(done.begin(), done.end(), goal_kinds[i]) == done.end()) done.push_back(goal_kinds[i]);
       tmp.has_diff = Placement(s->model) != pre ? 1 : 0;
       if (results) results[i] = tmp;
     }
@@ -488,83 +506,94 @@ ccmi_status ccmi_action_acceptance_by_kind(ccmi_session* s, int32_t kind, const 
 ccmi_status ccmi_session_apply(ccmi_session* s, const ccmi_action* actions, int64_t n, int64_t* applied) {
   if (applied) *applied = 0;
   // the proposals are the diff against the initial placement after every action applied, also when a later one fails
-  struct Rebuild {
+  bool rebuildFailed = false;
+  struct Rebuild {  // a destructor is noexcept: a failed rebuild is reported through the status below
     ccmi_session* s;
+    bool& failed;
     ~Rebuild() {
-      if (s) buildProposals(s);
-    }
-  } rebuild{s};
-  return guarded([&] {
-    if (!s || (n > 0 && !actions) || n < 0) throw std::invalid_argument("null argument");
-    ccmi::Model& m = s->model;
-    auto partition = [&](int p) {
-      if (p < 0 || p >= m.P) throw std::invalid_argument("partition out of range");
-    };
-    auto broker = [&](int b) {
-      if (b < 0 || b >= m.B) throw std::invalid_argument("broker out of range");
-    };
-    auto movable = [&](int p, int src, int dst) {  // ClusterModel.relocateReplica preconditions
-      partition(p);
-      broker(src);
-      broker(dst);
-      if (m.replicaOn(p, src) < 0) throw std::invalid_argument("source broker does not host the partition");
-      if (m.replicaOn(p, dst) >= 0) throw std::invalid_argument("destination broker already hosts the partition");
-    };
-    auto diskMove = [&](int p, int b, int sd, int dd) {
-      partition(p);
-      broker(b);
-      const int r = m.replicaOn(p, b);
-      if (r < 0) throw std::invalid_argument("broker does not host the partition");
-      if (sd < 0 || sd >= m.D || dd < 0 || dd >= m.D || m.dBroker[sd] != b || m.dBroker[dd] != b)
-        throw std::invalid_argument("disk out of range or not on the broker");
-      if (m.rDisk[r] != sd) throw std::invalid_argument("replica is not on the source disk");
-      m.relocateReplicaToDisk(p, b, dd);
-    };
-    for (int64_t i = 0; i < n; ++i) {
-      const ccmi_action& a = actions[i];
-      switch (a.type) {
-        case CCMI_INTER_BROKER_REPLICA_MOVEMENT:
-          movable(a.partition, a.source_broker, a.destination_broker);
-          m.relocateReplica(a.partition, a.source_broker, a.destination_broker);
-          break;
-        case CCMI_LEADERSHIP_MOVEMENT: {
-          partition(a.partition);
-          broker(a.source_broker);
-          broker(a.destination_broker);
-          const int sr = m.replicaOn(a.partition, a.source_broker), dr = m.replicaOn(a.partition, a.destination_broker);
-          if (sr < 0 || !m.rLeader[sr]) throw std::invalid_argument("source replica is not the leader");
-          if (dr < 0 || m.rLeader[dr]) throw std::invalid_argument("destination broker hosts no follower of the partition");
-          m.relocateLeadership(a.partition, a.source_broker, a.destination_broker);
-          break;
-        }
-        case CCMI_INTER_BROKER_REPLICA_SWAP:
-          movable(a.partition, a.source_broker, a.destination_broker);
-          partition(a.destination_partition);
-          if (m.replicaOn(a.destination_partition, a.destination_broker) < 0 ||
-              m.replicaOn(a.destination_partition, a.source_broker) >= 0)
-            throw std::invalid_argument("swap destination replica cannot move to the source broker");
-          m.relocateReplica(a.partition, a.source_broker, a.destination_broker);
-          m.relocateReplica(a.destination_partition, a.destination_broker, a.source_broker);
-          break;
-        case CCMI_INTRA_BROKER_REPLICA_MOVEMENT:
-          diskMove(a.partition, a.source_broker, a.source_disk, a.destination_disk);
-          break;
-        case CCMI_INTRA_BROKER_REPLICA_SWAP: {
-          partition(a.destination_partition);
-          const int r2 = m.replicaOn(a.destination_partition, a.source_broker);
-          if (r2 < 0 || m.rDisk[r2] != a.destination_disk)
-            throw std::invalid_argument("swap destination replica is not on the destination disk");
-          diskMove(a.partition, a.source_broker, a.source_disk, a.destination_disk);
-          diskMove(a.destination_partition, a.source_broker, a.destination_disk, a.source_disk);
-          break;
-        }
-        default:
-          throw std::invalid_argument("unknown action type");
+      try {
+        if (s) buildProposals(s);
+      } catch (std::exception& e) {
+        failed = true;
+        fail(CCMI_E_INVALID, std::string("rebuilding the proposals failed: ") + e.what());
       }
-      if (applied) *applied = i + 1;
     }
-    return CCMI_OK;
-  });
+  };
+  const ccmi_status st = [&] {
+    Rebuild rebuild{s, rebuildFailed};
+    return guarded([&] {
+      if (!s || (n > 0 && !actions) || n < 0) throw std::invalid_argument("null argument");
+      ccmi::Model& m = s->model;
+      auto partition = [&](int p) {
+        if (p < 0 || p >= m.P) throw std::invalid_argument("partition out of range");
+      };
+      auto broker = [&](int b) {
+        if (b < 0 || b >= m.B) throw std::invalid_argument("broker out of range");
+      };
+      auto movable = [&](int p, int src, int dst) {  // ClusterModel.relocateReplica preconditions
+        partition(p);
+        broker(src);
+        broker(dst);
+        if (m.replicaOn(p, src) < 0) throw std::invalid_argument("source broker does not host the partition");
+        if (m.replicaOn(p, dst) >= 0) throw std::invalid_argument("destination broker already hosts the partition");
+      };
+      auto diskMove = [&](int p, int b, int sd, int dd) {
+        partition(p);
+        broker(b);
+        const int r = m.replicaOn(p, b);
+        if (r < 0) throw std::invalid_argument("broker does not host the partition");
+        if (sd < 0 || sd >= m.D || dd < 0 || dd >= m.D || m.dBroker[sd] != b || m.dBroker[dd] != b)
+          throw std::invalid_argument("disk out of range or not on the broker");
+        if (m.rDisk[r] != sd) throw std::invalid_argument("replica is not on the source disk");
+        m.relocateReplicaToDisk(p, b, dd);
+      };
+      for (int64_t i = 0; i < n; ++i) {
+        const ccmi_action& a = actions[i];
+        switch (a.type) {
+          case CCMI_INTER_BROKER_REPLICA_MOVEMENT:
+            movable(a.partition, a.source_broker, a.destination_broker);
+            m.relocateReplica(a.partition, a.source_broker, a.destination_broker);
+            break;
+          case CCMI_LEADERSHIP_MOVEMENT: {
+            partition(a.partition);
+            broker(a.source_broker);
+            broker(a.destination_broker);
+            const int sr = m.replicaOn(a.partition, a.source_broker), dr = m.replicaOn(a.partition, a.destination_broker);
+            if (sr < 0 || !m.rLeader[sr]) throw std::invalid_argument("source replica is not the leader");
+            if (dr < 0 || m.rLeader[dr]) throw std::invalid_argument("destination broker hosts no follower of the partition");
+            m.relocateLeadership(a.partition, a.source_broker, a.destination_broker);
+            break;
+          }
+          case CCMI_INTER_BROKER_REPLICA_SWAP:
+            movable(a.partition, a.source_broker, a.destination_broker);
+            partition(a.destination_partition);
+            if (m.replicaOn(a.destination_partition, a.destination_broker) < 0 ||
+                m.replicaOn(a.destination_partition, a.source_broker) >= 0)
+              throw std::invalid_argument("swap destination replica cannot move to the source broker");
+            m.relocateReplica(a.partition, a.source_broker, a.destination_broker);
+            m.relocateReplica(a.destination_partition, a.destination_broker, a.source_broker);
+            break;
+          case CCMI_INTRA_BROKER_REPLICA_MOVEMENT:
+            diskMove(a.partition, a.source_broker, a.source_disk, a.destination_disk);
+            break;
+          case CCMI_INTRA_BROKER_REPLICA_SWAP: {
+            partition(a.destination_partition);
+            const int r2 = m.replicaOn(a.destination_partition, a.source_broker);
+            if (r2 < 0 || m.rDisk[r2] != a.destination_disk)
+              throw std::invalid_argument("swap destination replica is not on the destination disk");
+            diskMove(a.partition, a.source_broker, a.source_disk, a.destination_disk);
+            diskMove(a.destination_partition, a.source_broker, a.destination_disk, a.source_disk);
+            break;
+          }
+          default:
+            throw std::invalid_argument("unknown action type");
+        }
+        if (applied) *applied = i + 1;
+      }
+      return CCMI_OK;
+    });
+  }();
+  return st == CCMI_OK && rebuildFailed ? CCMI_E_INVALID : st;
 }
 
 ccmi_status ccmi_compute_cluster_stats(ccmi_session* s, const ccmi_balancing_constraint* c, const ccmi_opt_options* o,

@@ -20,11 +20,13 @@
 
 namespace ccmi {
 
-constexpr int kMaxGoals = 20;
+constexpr int kMaxGoals = 20;     // goals in one program: the goal being optimized + its optimized goals
 constexpr int kExclLeadBit = 31;  // allowedBits bit of a broker excluded for leadership (above every goal slot)
 constexpr int kExclMoveBit = 30;  // allowedBits bit of a broker excluded for replica moves
 constexpr int kNewBit = 29;       // allowedBits bit of a NEW broker (Broker.State.NEW)
-static_assert(kMaxGoals <= kNewBit, "goal slots overlap the broker flag bits");
+// allowedBits goal slots [0, kMaxSlots): one per goal the session holds (one per goal kind) plus the running one
+constexpr int kMaxSlots = 29;
+static_assert(kMaxSlots <= kNewBit && kMaxGoals <= kMaxSlots, "goal slots overlap the broker flag bits");
 constexpr int kMaxRf = 8;
 // Dirty rows of each kind a cross/pair scan stages into its LDS overlay itself (kernels/scan.hip OverlayLds); a
 // launch with more pending rows of any kind runs `prep` first (device.cpp stageScan). Shared by host and kernel.

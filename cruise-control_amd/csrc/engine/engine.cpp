@@ -131,11 +131,11 @@ DevProgram Engine::program(const GoalImpl& self, int action) const {
   p.action = action;
   // the conjunction of AnalyzerUtils.isProposalAcceptableForOptimizedGoals ends at a terminal goal (it throws)
   size_t nOpt = 0;
-  while (nOpt < optimized.size() && !(nOpt > 0 && optimized[nOpt - 1]->terminal)) ++nOpt;
+  while (nOpt < priors.size() && !(nOpt > 0 && priors[nOpt - 1]->terminal)) ++nOpt;
   p.nGoals = 1 + (int)nOpt;
   if (p.nGoals > kMaxGoals) throw Unsupported("too many goals in one chain");
   p.goals[0] = self.dg;
-  for (size_t i = 0; i < nOpt; ++i) p.goals[i + 1] = optimized[i]->dg;
+  for (size_t i = 0; i < nOpt; ++i) p.goals[i + 1] = priors[i]->dg;
   p.needs = 0;
   for (int i = 0; i < p.nGoals; ++i) p.needs |= needsOf(p.goals[i]);
   p.filter = FILTER_NONE;
@@ -365,14 +365,20 @@ bool Engine::chainsOn() const {
 }
 
 bool Engine::terminalOptimized() const {
-  for (const auto& g : optimized)
+  for (const GoalImpl* g : priors)
     if (g->terminal) return true;
   return false;
 }
 void Engine::checkTerminal(int64_t key) const {
   if (key < 0) return;
-  for (const auto& g : optimized)
+  for (const GoalImpl* g : priors)
     if (g->terminal) throw StateError("No goal should be executed after " + g->name);
+}
+
+GoalImpl* Engine::optimizedOfKind(int kind) const {
+  for (const auto& g : optimized)
+    if (g->kind == kind) return g.get();
+  return nullptr;
 }
 
 int64_t Engine::chainPairs(GoalImpl& self, int action, const std::vector<int32_t>& pr, const std::vector<int32_t>& pb,
@@ -423,8 +429,8 @@ int Engine::acceptance(int gi, const ccmi_action& a) {
       throw std::invalid_argument("Unsupported balancing action " + std::to_string(a.type) + " is provided.");
   }
   if (optimized.at(gi)->terminal) throw StateError("No goal should be executed after " + optimized.at(gi)->name);
-  std::vector<const std::vector<uint8_t>*> allowedBySlot;
-  for (auto& g : optimized) allowedBySlot.push_back(&g->allowed);
+  std::vector<const std::vector<uint8_t>*> allowedBySlot(kMaxSlots, nullptr);
+  for (auto& g : optimized) allowedBySlot[g->dg.allowedSlot] = &g->allowed;
   HostView v{m, allowedBySlot, topicUpper, topicLower, brokerSetOf, replicaSetOf, minLeadOf, topicLeadLim};
   const GoalImpl& g = *optimized.at(gi);
   const int sr = m.replicaOn(a.partition, a.source_broker);
@@ -530,7 +536,7 @@ ccmi_cluster_stats Engine::stats() {
 }
 
 // AbstractGoal.optimize (AbstractGoal.java:81-135) + the per-goal bookkeeping of GoalOptimizer.optimizations
-bool Engine::optimizeGoal(std::unique_ptr<GoalImpl> g, ccmi_goal_result* res) {
+bool Engine::optimizeGoal(std::unique_ptr<GoalImpl> g, const std::vector<GoalImpl*>& priorSet, ccmi_goal_result* res) {
   using clk = std::chrono::steady_clock;
   const auto t0 = clk::now();
   const int64_t c0 = candidates;
@@ -544,6 +550,20 @@ bool Engine::optimizeGoal(std::unique_ptr<GoalImpl> g, ccmi_goal_result* res) {
     }
   } guard{m};
   prof().candCounter = &candidates;
+  // optimizedGoals in the session's order; a goal's slot is free unless an entry of `optimized` holds it
+  priors.clear();
+  for (const auto& h : optimized)
+    if (std::find(priorSet.begin(), priorSet.end(), h.get()) != priorSet.end()) priors.push_back(h.get());
+  if (priors.size() != priorSet.size()) throw std::invalid_argument("optimized goal not held by the session");
+  uint32_t used = 0;
+  for (const auto& h : optimized) used |= 1u << h->dg.allowedSlot;
+  newSlot = 0;
+  while (newSlot < kMaxSlots && (used >> newSlot) & 1u) ++newSlot;
+  if (newSlot >= kMaxSlots) throw Unsupported("no free goal slot");
+  struct ClearPriors {
+    std::vector<GoalImpl*>& p;
+    ~ClearPriors() { p.clear(); }
+  } clearPriors{priors};
   g->succeeded = true;
   g->prov = provisionResponse(CCMI_PROVISION_UNDECIDED);  // AbstractGoal.java:87
   try {
@@ -578,8 +598,9 @@ bool Engine::optimizeGoalImpl(std::unique_ptr<GoalImpl>& g, ccmi_goal_result* re
   using clk = std::chrono::steady_clock;
   const ccmi_cluster_stats before = stats();
   g->finished = false;
-  g->dg.allowedSlot = (int)optimized.size();
+  g->dg.allowedSlot = newSlot;
   g->init(*this);
+  g->dg.allowedSlot = newSlot;
   dev->setAllowed(g->dg.allowedSlot, g->allowed.data());
   if (opt.anyExclLead || opt.anyExclMove || m.numNew > 0 || exclOnDevice) {
     const std::vector<uint8_t> none(m.B, 0);
@@ -621,6 +642,12 @@ bool Engine::optimizeGoalImpl(std::unique_ptr<GoalImpl>& g, ccmi_goal_result* re
     fresh.candCounter = prof().candCounter;
     prof() = fresh;
   }
+  // GoalOptimizer keeps one instance per goal class: a re-optimized kind replaces its older entry
+  for (size_t i = 0; i < optimized.size(); ++i)
+    if (optimized[i]->kind == g->kind) {
+      optimized.erase(optimized.begin() + (long)i);
+      break;
+    }
   optimized.push_back(std::move(g));
   if (res) {
     res->stats = stats();  // GoalOptimizer.statsByGoalPriority
@@ -694,7 +721,7 @@ class ReplicaDistribution : public GoalImpl {
     dg.upper = upper;
     dg.lower = lower;
     dg.fixOffline = 0;
-    dg.allowedSlot = (int)e.optimized.size();
+    dg.allowedSlot = e.newSlot;
     const bool selfHealing = m.numSelfHealing > 0;
     for (int b = 0; b < m.B; ++b) {
       Model::Spec s;
@@ -1076,7 +1103,7 @@ class ResourceDistribution : public GoalImpl {
     dg.upperThr = upperThr;
     dg.lowerThr = lowerThr;
     dg.fixOffline = 0;
-    dg.allowedSlot = (int)e.optimized.size();
+    dg.allowedSlot = e.newSlot;
   }
 
   // updateGoalState (:301-349)

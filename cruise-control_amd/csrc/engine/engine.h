@@ -97,7 +97,14 @@ class Engine {
   Options opt;
   Constraint bc{};
   Shard shard;
-  std::vector<std::unique_ptr<GoalImpl>> optimized;  // optimized goals, priority order
+  // The goals this session has optimized, one per goal kind (GoalOptimizer holds one instance per goal class, so a
+  // re-optimized kind replaces its older entry), in the order each was last optimized. A goal's frozen acceptance
+  // state (DevGoal, allowed-broker slot) lives here for as long as it may appear in a later optimizedGoals set.
+  std::vector<std::unique_ptr<GoalImpl>> optimized;
+  // Goal.optimize's optimizedGoals (Goal.java:60-68) for the running optimization: entries of `optimized`, in its
+  // order (AnalyzerUtils.isProposalAcceptableForOptimizedGoals, AnalyzerUtils.java:169-179). Only these goals'
+  // actionAcceptance joins the candidate conjunction.
+  std::vector<GoalImpl*> priors;
   int64_t candidates = 0;
   ccmi_provision_response lastFailure{};  // provisionResponse of the goal whose OptimizationFailure ended the last call
   std::vector<uint8_t> scratchB, scratchB2;  // per-broker scratch flags for the goal drivers
@@ -107,8 +114,13 @@ class Engine {
   std::vector<int32_t> minLeadOf;  // MinTopicLeadersPerBrokerGoal's minimum per topic, -1 = not its topic (setMinLeaders)
   std::vector<int32_t> topicLeadLim;  // TopicLeaderReplicaDistributionGoal (upper, lower) per topic (setTopicLeadLimits)
 
-  // one Goal.optimize; throws OptimizationFailure / StateError
-  bool optimizeGoal(std::unique_ptr<GoalImpl> g, ccmi_goal_result* res);
+  // one Goal.optimize(clusterModel, optimizedGoals = priorSet, options); throws OptimizationFailure / StateError.
+  // priorSet: entries of `optimized`. On success the goal joins `optimized` (replacing an entry of its kind).
+  bool optimizeGoal(std::unique_ptr<GoalImpl> g, const std::vector<GoalImpl*>& priorSet, ccmi_goal_result* res);
+  // The entry of `optimized` of a goal kind, or null
+  GoalImpl* optimizedOfKind(int kind) const;
+  // allowedBits slot of the goal being optimized (set before GoalImpl::init; DevGoal.allowedSlot)
+  int newSlot = 0;
   bool optimizeGoalImpl(std::unique_ptr<GoalImpl>& g, ccmi_goal_result* res, std::chrono::steady_clock::time_point t0,
                         int64_t c0, size_t a0, int64_t l0, int64_t p0);
   ccmi_cluster_stats stats();

@@ -148,7 +148,7 @@ class RackAware : public GoalImpl {
     alive = aliveById(m);
     dg = DevGoal{};
     dg.kind = DG_RACK_AWARE;
-    dg.allowedSlot = (int)e.optimized.size();
+    dg.allowedSlot = e.newSlot;
   }
 
   // shouldKeepInTheCurrentBroker (:214-225)
@@ -333,7 +333,7 @@ class RackAwareDist : public GoalImpl {
     alive = aliveById(m);
     dg = DevGoal{};
     dg.kind = DG_RACK_AWARE_DISTRIBUTION;
-    dg.allowedSlot = (int)e.optimized.size();
+    dg.allowedSlot = e.newSlot;
   }
 
   // numPartitionReplicasByRackId (:113-119) as (rack, count) pairs
@@ -484,7 +484,7 @@ class MinTopicLeaders : public GoalImpl {
     const int nAllowed = allowedForReplicaMove(e, allowed);
     dg = DevGoal{};
     dg.kind = DG_ACCEPT_ALL;
-    dg.allowedSlot = (int)e.optimized.size();
+    dg.allowedSlot = e.newSlot;
     mustOrder.clear();
     minOf.assign(m.T, -1);
     if (e.bc.minLeaderTopics.empty()) return;
@@ -672,7 +672,7 @@ class ReplicaCapacity : public GoalImpl {
     dg = DevGoal{};
     dg.kind = DG_REPLICA_CAPACITY;
     dg.maxReplicas = maxR;
-    dg.allowedSlot = (int)e.optimized.size();
+    dg.allowedSlot = e.newSlot;
   }
 
   // rebalanceForBroker (:221-263): rows that share one eligibleBrokers list (it only changes after a move) are
@@ -805,7 +805,7 @@ class Capacity : public GoalImpl {
     dg.kind = DG_CAPACITY;
     dg.resource = res;
     dg.capThr = thr;
-    dg.allowedSlot = (int)e.optimized.size();
+    dg.allowedSlot = e.newSlot;
   }
 
   // isUtilizationOverLimit (:410-428); the host is the broker
@@ -914,7 +914,7 @@ class PotentialNwOut : public GoalImpl {
     dg = DevGoal{};
     dg.kind = DG_POTENTIAL_NW_OUT;
     dg.capThr = thr;
-    dg.allowedSlot = (int)e.optimized.size();
+    dg.allowedSlot = e.newSlot;
   }
   // brokersToBalance (:140-150): the broken brokers if any, else all
   std::vector<int> brokersToBalance(Engine& e) override {
@@ -1068,7 +1068,7 @@ class TopicReplicaDistribution : public GoalImpl {
     e.dev->setTopicLimits(upper.data(), lower.data());
     dg = DevGoal{};
     dg.kind = DG_TOPIC_REPLICA_DISTRIBUTION;
-    dg.allowedSlot = (int)e.optimized.size();
+    dg.allowedSlot = e.newSlot;
   }
 
   // updateGoalState (:318-345)
@@ -1327,7 +1327,7 @@ class TopicLeaderReplicaDistribution : public GoalImpl {
     e.dev->setTopicLeadLimits(e.topicLeadLim.data());
     dg = DevGoal{};
     dg.kind = DG_TOPIC_LEADER_DISTRIBUTION;
-    dg.allowedSlot = (int)e.optimized.size();
+    dg.allowedSlot = e.newSlot;
   }
 
   // updateGoalState (:382-424)
@@ -1699,7 +1699,7 @@ class LeaderReplicaDistribution : public GoalImpl {
     dg.kind = DG_LEADER_REPLICA_DISTRIBUTION;
     dg.upper = upper;
     dg.lower = lower;
-    dg.allowedSlot = (int)e.optimized.size();
+    dg.allowedSlot = e.newSlot;
   }
   // updateGoalState (ReplicaDistributionAbstractGoal.java:183-223)
   void update(Engine& e) override {
@@ -2068,7 +2068,7 @@ class LeaderBytesIn : public GoalImpl {
     dg.kind = DG_LEADER_BYTES_IN;
     dg.lbiBalance = balance;
     dg.lbiLowUtil = lowUtil;
-    dg.allowedSlot = (int)e.optimized.size();
+    dg.allowedSlot = e.newSlot;
   }
   // brokersToBalance (:142-152)
   std::vector<int> brokersToBalance(Engine& e) override {
@@ -2152,7 +2152,7 @@ class PreferredLeaderElection : public GoalImpl {
     allowedForReplicaMove(e, allowed);
     dg = DevGoal{};
     dg.kind = DG_ACCEPT_ALL;  // actionAcceptance: ACCEPT
-    dg.allowedSlot = (int)e.optimized.size();
+    dg.allowedSlot = e.newSlot;
   }
   bool rebalanceAll(Engine& e) override {
     PhaseScope ps(PH_OTHER_GOALS);
@@ -2263,12 +2263,12 @@ class KafkaAssignerEvenRackAware : public GoalImpl {
   }
   void init(Engine& e) override {
     kaSanityCheck(e);
-    if (!e.optimized.empty())
-      throw std::invalid_argument("Goals " + std::to_string(e.optimized.size()) + " cannot be optimized before " + name + ".");
+    if (!e.priors.empty())  // optimizedGoals non-empty (KafkaAssignerEvenRackAwareGoal.java:125-128)
+      throw std::invalid_argument("Goals " + std::to_string(e.priors.size()) + " cannot be optimized before " + name + ".");
     allowed.assign(e.m.B, 1);
     dg = DevGoal{};
     dg.kind = DG_RACK_AWARE;  // actionAcceptance (:385-408): the rack-awareness test of RackAwareGoal
-    dg.allowedSlot = (int)e.optimized.size();
+    dg.allowedSlot = e.newSlot;
   }
   // Replica.toString (Replica.java:338-343); racks are named by their index
   static std::string replicaString(const Model& m, int r) {
@@ -2412,7 +2412,7 @@ class KafkaAssignerDiskUsageDistribution : public GoalImpl {
     allowed.assign(e.m.B, 1);
     dg = DevGoal{};
     dg.kind = DG_ACCEPT_ALL;
-    dg.allowedSlot = (int)e.optimized.size();
+    dg.allowedSlot = e.newSlot;
   }
 
   // optimize (:107-144) with checkAndOptimize (:197-252), swapReplicas (:268-383), isOptimized (:156-181)
@@ -2622,7 +2622,7 @@ class BrokerSetAware : public GoalImpl {
     alive = aliveById(m);
     dg = DevGoal{};
     dg.kind = DG_BROKER_SET_AWARE;
-    dg.allowedSlot = (int)e.optimized.size();
+    dg.allowedSlot = e.newSlot;
   }
 
   // rebalanceForBroker (:159-188): each misplaced replica goes to the first acceptable alive broker of its set in

@@ -49,7 +49,7 @@ class IntraGoalImpl : public GoalImpl {
     if (m.D == 0) throw std::invalid_argument(name + " needs the replica placement over disks (JBOD)");
     if (m.diskGhosts)
       throw Unsupported(name + " after inter-broker moves of a JBOD session (replicas left on their source disks)");
-    for (auto& g : e.optimized)
+    for (const GoalImpl* g : e.priors)
       if (!isIntraGoalKind(g->kind))
         throw std::invalid_argument("intra-broker goals cannot be optimized together with inter-broker goals");
     if (ig == IG_CAPACITY) {  // IntraBrokerDiskCapacityGoal.initGoalState
@@ -175,8 +175,8 @@ bool IntraGoalImpl::rebalanceAll(Engine& e) {
   q.capThr = e.bc.capThreshold[R_DISK];
   q.margin = (e.bc.resBalance[R_DISK] - 1) * 0.9;  // BALANCE_MARGIN
   q.slot = dg.allowedSlot;
-  for (auto& g : e.optimized) {
-    const auto* p = static_cast<const IntraGoalImpl*>(g.get());
+  for (const GoalImpl* g : e.priors) {
+    const auto* p = static_cast<const IntraGoalImpl*>(g);
     if (q.nPrior >= kIntraMaxPrior) throw std::invalid_argument("too many optimized intra-broker goals");
     q.priorKind[q.nPrior] = p->ig;
     q.priorSlot[q.nPrior] = p->dg.allowedSlot;

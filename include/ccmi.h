@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define CCMI_ABI_VERSION 7
+#define CCMI_ABI_VERSION 8
 
 typedef enum ccmi_status {
   CCMI_OK = 0,
@@ -407,14 +407,29 @@ ccmi_status ccmi_builder_broker_ids(const ccmi_model_builder* b, int32_t* out);
 ccmi_status ccmi_session_create(int32_t device_ordinal, const ccmi_cluster_desc* desc, ccmi_session** out);
 ccmi_status ccmi_session_destroy(ccmi_session* s);
 
-/* Run a whole goal chain (GoalOptimizer.optimizations). results: caller array of n_goals entries. */
+/* Run a whole goal chain (GoalOptimizer.optimizations). results: caller array of n_goals entries. Every goal's
+ * optimizedGoals are the goals before it in this call (GoalOptimizer.java:449,467-471), not earlier calls' goals. */
 ccmi_status ccmi_optimizations(ccmi_session* s, const int32_t* goal_kinds, int32_t n_goals,
                                const ccmi_balancing_constraint* constraint, const ccmi_opt_options* options,
                                ccmi_goal_result* results);
-/* Optimize one goal; the session remembers it (with its frozen state) as an optimized goal for later calls. */
-ccmi_status ccmi_goal_optimize(ccmi_session* s, int32_t goal_kind, const ccmi_balancing_constraint* constraint,
+/*
+ * Goal.optimize(ClusterModel, Set<Goal> optimizedGoals, OptimizationOptions) (analyzer/goals/Goal.java:60-68,
+ * AbstractGoal.java:81-135). The session keeps every goal it has optimized — one per goal kind, as GoalOptimizer keeps
+ * one instance per goal class, a re-optimized kind replacing its older entry — with the frozen state its
+ * actionAcceptance reads. optimized_goal_kinds[0, num_optimized_goals) is the caller's optimizedGoals set (ABI v8): only
+ * those goals' actionAcceptance joins the candidate conjunction (AnalyzerUtils.isProposalAcceptableForOptimizedGoals,
+ * AnalyzerUtils.java:169-179), whatever else the session has run. GoalOptimizer passes the goals optimized earlier in the
+ * same optimizations() call; GoalViolationDetector passes the empty set on a model it reuses across goals
+ * (GoalViolationDetector.java:193-211,314). Duplicate kinds count once; order does not matter.
+ * A kind the session has not optimized — a goal whose optimize ran in the JVM, or a goal class that exists only in the
+ * JVM (pass any kind outside ccmi_goal_kind, e.g. -1) — returns CCMI_E_UNSUPPORTED before anything changes: its
+ * actionAcceptance is not available to the device, so the caller runs this goal in the JVM instead.
+ */
+ccmi_status ccmi_goal_optimize(ccmi_session* s, int32_t goal_kind, const int32_t* optimized_goal_kinds,
+                               int32_t num_optimized_goals, const ccmi_balancing_constraint* constraint,
                                const ccmi_opt_options* options, ccmi_goal_result* result);
-/* Acceptance of an action by the i-th goal this session has optimized. */
+/* Acceptance of an action by the i-th goal the session holds (the goals it has optimized, one per kind, in the order
+ * each was last optimized: after one ccmi_optimizations call on a fresh session, the chain position). */
 ccmi_status ccmi_action_acceptance(ccmi_session* s, int32_t optimized_goal_index, const ccmi_action* action,
                                    int32_t* acceptance);
 /* Goal.actionAcceptance keyed by the goal plugin (ccmi_goal_kind) instead of the chain position: the most recently

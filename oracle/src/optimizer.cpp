@@ -146,4 +146,37 @@ OptimizerResult optimizations(ClusterModel& cm, const std::vector<int>& goalKind
   return res;
 }
 
+GoalResult goalOptimize(ClusterModel& cm, Goal& g, const GoalList& optimizedGoals, const BalancingConstraint& bc,
+                        const OptimizationOptions& o) {
+  using clk = std::chrono::steady_clock;
+  cm.excludedTopicsSel = o.excludedTopics;
+  const std::vector<int> preDist = cm.replicaDistributionFlat(), preDisks = cm.replicaDiskFlat();
+  const std::vector<int> preLeaders = cm.leaderDistribution();
+  auto leaderDisks = [&]() {
+    std::vector<int> out;
+    for (const Partition& p : cm.partitions) out.push_back(cm.replicas[p.leader].disk);
+    return out;
+  };
+  const std::vector<int> preLeaderDisks = leaderDisks();
+  const auto gs = clk::now();
+  const int64_t c0 = cm.candidatesEvaluated;
+  const size_t a0 = cm.actionLog.size();
+  GoalResult gr;
+  try {
+    gr.succeeded = g.optimize(cm, optimizedGoals, o);
+  } catch (OptimizationFailure&) {
+    g_lastFailure = g.provision();
+    throw;
+  }
+  gr.name = g.name();
+  gr.stats = computeStats(cm, bc, o);
+  gr.seconds = std::chrono::duration<double>(clk::now() - gs).count();
+  gr.candidates = cm.candidatesEvaluated - c0;
+  gr.actions = (int64_t)(cm.actionLog.size() - a0);
+  gr.provision = g.provision();
+  gr.hasDiff = cm.replicaDistributionFlat() != preDist || cm.replicaDiskFlat() != preDisks ||
+               cm.leaderDistribution() != preLeaders || leaderDisks() != preLeaderDisks;
+  return gr;
+}
+
 }  // namespace oracle

@@ -46,4 +46,10 @@ bool isIntraBrokerGoal(int kind);
 OptimizerResult optimizations(ClusterModel& cm, const std::vector<int>& goalKinds, const BalancingConstraint& bc,
                               const OptimizationOptions& o);
 
+// One Goal.optimize(clusterModel, optimizedGoals, optimizationOptions) (Goal.java:60-68) with the caller's
+// optimizedGoals set, as GoalViolationDetector.optimizeForGoal calls it (GoalViolationDetector.java:314) and as a
+// goal-by-goal caller would; the result carries the goal's stats afterwards and AnalyzerUtils.hasDiff.
+GoalResult goalOptimize(ClusterModel& cm, Goal& g, const GoalList& optimizedGoals, const BalancingConstraint& bc,
+                        const OptimizationOptions& o);
+
 }  // namespace oracle

@@ -1,5 +1,6 @@
 // ORACLE — test infrastructure only (see jsem.h header). C entry points (liboracle_cc.so) used by
 // tests/ (ctypes) and bench.py's cpu_baseline leg. Shares only the data layout of include/ccmi.h.
+#include <algorithm>
 #include <chrono>
 #include <cstring>
 #include <memory>
@@ -17,6 +18,22 @@ struct Handle {
   ClusterModel cm;
   OptimizerResult last;
   std::string err;
+  // Goal instances that have optimized this model, one per goal kind (GoalOptimizer's one instance per goal class),
+  // for the optimizedGoals sets of oc_goal_optimize
+  std::vector<std::pair<int, std::shared_ptr<Goal>>> held;
+  void hold(int kind, std::shared_ptr<Goal> g) {
+    for (auto& e : held)
+      if (e.first == kind) {
+        e.second = std::move(g);
+        return;
+      }
+    held.emplace_back(kind, std::move(g));
+  }
+  Goal* heldOf(int kind) const {
+    for (auto& e : held)
+      if (e.first == kind) return e.second.get();
+    return nullptr;
+  }
 };
 
 BalancingConstraint toBc(const ccmi_balancing_constraint* c) {
@@ -293,6 +310,7 @@ int oc_optimize(void* hv, const int32_t* goals, int n, const ccmi_balancing_cons
   try {
     std::vector<int> kinds(goals, goals + n);
     h->last = optimizations(h->cm, kinds, toBc(c), toOpts(o));
+    for (int i = 0; i < n; ++i) h->hold(goals[i], h->last.optimizedGoals[i]);
     for (int i = 0; i < n; ++i) {
       const GoalResult& g = h->last.goals[i];
       ccmi_goal_result& r = results[i];
@@ -325,6 +343,76 @@ int oc_optimize(void* hv, const int32_t* goals, int n, const ccmi_balancing_cons
   } catch (std::exception& e) {
     h->err = e.what();
     return CCMI_E_INVALID;
+  }
+}
+// Goal.optimize(cm, optimizedGoals, options) for one goal kind; optimizedGoals = the held goals of set_kinds
+// (CCMI_E_UNSUPPORTED when one is not held). The goal is held afterwards.
+int oc_goal_optimize(void* hv, int32_t kind, const int32_t* set_kinds, int32_t n_set, const ccmi_balancing_constraint* c,
+                     const ccmi_opt_options* o, ccmi_goal_result* result) {
+  auto* h = (Handle*)hv;
+  try {
+    GoalList set;
+    for (int i = 0; i < n_set; ++i) {
+      Goal* g = h->heldOf(set_kinds[i]);
+      if (!g) throw UnsupportedOperation("optimized goal kind " + std::to_string(set_kinds[i]) + " is not held");
+      if (std::find(set.begin(), set.end(), g) == set.end()) set.push_back(g);
+    }
+    if (isIntraBrokerGoal(kind) && h->cm.disks.empty())
+      throw std::invalid_argument("intra-broker goals need replica placement over disks");
+    for (Goal* g : set)
+      for (auto& e : h->held)
+        if (e.second.get() == g && isIntraBrokerGoal(e.first) != isIntraBrokerGoal(kind))
+          throw std::invalid_argument("intra-broker goals cannot be optimized together with inter-broker goals");
+    const BalancingConstraint bc = toBc(c);
+    std::shared_ptr<Goal> g = makeGoal(kind, bc);
+    const GoalResult gr = goalOptimize(h->cm, *g, set, bc, toOpts(o));
+    h->hold(kind, g);
+    ccmi_goal_result& r = *result;
+    std::memset(&r, 0, sizeof(r));
+    r.goal_kind = kind;
+    r.succeeded = gr.succeeded;
+    r.has_diff = gr.hasDiff;
+    r.seconds = gr.seconds;
+    r.candidates = gr.candidates;
+    r.actions = gr.actions;
+    toCStats(gr.stats, &r.stats);
+    toCProvision(gr.provision, &r.provision);
+    return 0;
+  } catch (OptimizationFailure& e) {
+    h->err = e.what();
+    return CCMI_E_OPT_FAILURE;
+  } catch (UnsupportedOperation& e) {
+    h->err = e.what();
+    return CCMI_E_UNSUPPORTED;
+  } catch (std::invalid_argument& e) {
+    h->err = e.what();
+    return CCMI_E_INVALID;
+  } catch (std::logic_error& e) {
+    h->err = e.what();
+    return CCMI_E_STATE;
+  } catch (std::exception& e) {
+    h->err = e.what();
+    return CCMI_E_INVALID;
+  }
+}
+// Goal.actionAcceptance of the held goal of a kind: 0/1/2, or -1 with the message in oc_error
+int32_t oc_action_acceptance_by_kind(void* hv, int32_t kind, const ccmi_action* a) {
+  auto* h = (Handle*)hv;
+  try {
+    Goal* g = h->heldOf(kind);
+    if (!g) throw std::invalid_argument("goal kind not held");
+    BalancingAction ba;
+    ba.type = (ActionType)a->type;
+    ba.partition = a->partition;
+    ba.sourceBroker = a->source_broker;
+    ba.destinationBroker = a->destination_broker;
+    ba.destPartition = a->destination_partition;
+    ba.sourceDisk = a->source_disk;
+    ba.destinationDisk = a->destination_disk;
+    return (int32_t)g->actionAcceptance(ba, h->cm);
+  } catch (std::exception& e) {
+    h->err = e.what();
+    return -1;
   }
 }
 const char* oc_error(void* hv) { return ((Handle*)hv)->err.c_str(); }

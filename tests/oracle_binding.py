@@ -47,6 +47,12 @@ class Oracle:
             L.oc_optimize.restype = C.c_int
             L.oc_optimize.argtypes = [C.c_void_p, C.POINTER(C.c_int32), C.c_int, C.POINTER(ccmi.ConstraintStruct),
                                       C.POINTER(ccmi.OptionsStruct), C.POINTER(ccmi.GoalResultStruct)]
+            L.oc_goal_optimize.restype = C.c_int
+            L.oc_goal_optimize.argtypes = [C.c_void_p, C.c_int32, C.POINTER(C.c_int32), C.c_int32,
+                                           C.POINTER(ccmi.ConstraintStruct), C.POINTER(ccmi.OptionsStruct),
+                                           C.POINTER(ccmi.GoalResultStruct)]
+            L.oc_action_acceptance_by_kind.restype = C.c_int32
+            L.oc_action_acceptance_by_kind.argtypes = [C.c_void_p, C.c_int32, C.POINTER(ccmi.ActionStruct)]
             L.oc_error.restype = C.c_char_p
             L.oc_error.argtypes = [C.c_void_p]
             L.oc_last_seconds.restype = C.c_double
@@ -173,6 +179,39 @@ class OracleCluster:
                                                                                 ccmi.GOAL_NAMES[r.goal_kind]))
                              for r in res]
         return self.last_results
+
+    def _raise(self, st: int):
+        err = ccmi._STATUS.get(st, RuntimeError)(self.L.oc_error(self.h).decode())
+        if isinstance(err, ccmi.OptimizationFailureException):
+            p = ccmi.ProvisionRespStruct()
+            self.L.oc_last_failure_provision(self.h, C.byref(p))
+            err.provision = ccmi.ProvisionResponse.from_struct(p, ccmi._goal_of_message(str(err)))
+        raise err
+
+    def goal_optimize(self, goal_name: str, optimized_goals=(), constraint: Optional[ccmi.BalancingConstraint] = None,
+                      options: Optional[ccmi.OptimizationOptions] = None) -> ccmi.GoalResult:
+        """Goal.optimize(clusterModel, optimizedGoals, options) for one goal: optimized_goals are names of goals this
+        model has optimized (the instance of their latest optimization)."""
+        prior = [ccmi.GOAL_KINDS[n] if isinstance(n, str) else int(n) for n in optimized_goals]
+        kinds = (C.c_int32 * max(1, len(prior)))(*prior)
+        r = ccmi.GoalResultStruct()
+        o, keep = (options or ccmi.OptimizationOptions()).to_struct()
+        c = (constraint or ccmi.BalancingConstraint()).to_struct(self.topic_names())
+        st = self.L.oc_goal_optimize(self.h, ccmi.GOAL_KINDS[goal_name], kinds, len(prior), C.byref(c), C.byref(o),
+                                     C.byref(r))
+        if st != 0:
+            self._raise(st)
+        return ccmi.GoalResult(goal_name, bool(r.succeeded), bool(r.has_diff), r.seconds, r.candidates, 0, 0,
+                               r.actions, ccmi.stats_to_dict(r.stats),
+                               ccmi.ProvisionResponse.from_struct(r.provision, goal_name))
+
+    def action_acceptance_by_goal(self, goal_name: str, action_type: int, partition: int, source: int,
+                                  destination: int, destination_partition: int = -1) -> str:
+        a = ccmi.ActionStruct(action_type, partition, source, destination, destination_partition, -1, -1)
+        v = self.L.oc_action_acceptance_by_kind(self.h, ccmi.GOAL_KINDS[goal_name], C.byref(a))
+        if v < 0:
+            raise ValueError(self.L.oc_error(self.h).decode())
+        return ccmi.ACCEPTANCE[v]
 
     def seconds(self) -> float:
         return self.L.oc_last_seconds(self.h)

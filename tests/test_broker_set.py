@@ -270,3 +270,49 @@ def test_emu_broker_set_acceptance_matches_oracle(emu_lib, oracle_lib):
 def test_gpu_broker_set_acceptance_matches_oracle(gpu_lib, oracle_lib):
     pairs = _acceptance_pairs(gpu_lib)
     assert all(g == w for g, w in pairs)
+
+
+# ------------------------------------------------------------------------------------------ non-dense Kafka ids
+def _builder_model_with_kafka_ids(lib):
+    """A LoadMonitor-built model whose Kafka broker ids are 1000 + 7 i (not the dense session indices)."""
+    import ctypes as C
+    rng = random.Random(5)
+    m = ccmi.LoadMonitorModel(num_windows=1, lib=lib)
+    kafka = [1000 + 7 * i for i in range(24)]
+    cap = {"CPU": 100.0, "NW_IN": 100000.0, "NW_OUT": 100000.0, "DISK": 500000.0}
+    for i, k in enumerate(kafka):
+        m.create_broker(f"rack{i % 4}", f"h{k}", k, cap)
+    for t in range(40):
+        for p in range(10):
+            reps = rng.sample(kafka, 3)
+            met = {mm: [C.c_float(rng.uniform(1, 50)).value] for mm in ccmi.LoadMonitorModel.METRICS}
+            met["CPU_USAGE"] = [C.c_float(rng.uniform(0, 0.02)).value]
+            m.populate_partition(f"topic{t}", p, reps, reps[0], met)
+    return m, kafka
+
+
+def _kafka_id_sets(lib):
+    """broker_sets name Kafka ids; BalancingConstraint.to_struct maps them through the session's broker_ids() to the
+    dense indices of ccmi_balancing_constraint (an id the model does not hold, 99, maps to -1 = no broker). The oracle
+    gets the same sets written as indices: both must agree bit for bit."""
+    m, kafka = _builder_model_with_kafka_ids(lib)
+    cm = ccmi.ClusterModel(m.desc(), device=0, lib=lib, keepalive=m)
+    assert cm.broker_ids() == sorted(kafka)
+    by_kafka = ccmi.BalancingConstraint()
+    by_kafka.broker_sets = {"east": kafka[:12] + [99], "west": kafka[12:]}
+    by_index = ccmi.BalancingConstraint()
+    by_index.broker_sets = {"east": list(range(12)) + [-1], "west": list(range(12, 24))}
+    res = ccmi.GoalOptimizer(by_kafka).optimizations(cm, ccmi.goals_from_names([BSA]))
+    oc = OracleCluster.from_desc(m.desc())
+    ores = oc.optimize([BSA], by_index)
+    assert cm.actions() == oc.actions() and res.goal_results[0].actions == ores[0].actions > 0
+    assert cm.replica_distribution() == oc.replica_distribution()
+
+
+def test_emu_broker_sets_by_kafka_id(emu_lib, oracle_lib):
+    _kafka_id_sets(emu_lib)
+
+
+@pytest.mark.gpu
+def test_gpu_broker_sets_by_kafka_id(gpu_lib, oracle_lib):
+    _kafka_id_sets(gpu_lib)

@@ -168,7 +168,7 @@ def product_runner(lib):
     def run(flat, goal, opts, bc):
         cm = ccmi.ClusterModel(flat.desc, device=0, lib=lib, keepalive=flat)
         g = getattr(ccmi, goal)(constraint=bc)
-        ok = g.optimize(cm, opts)
+        ok = g.optimize(cm, set(), opts)
         return ok, cm.proposals(), g.provision
     return run
 

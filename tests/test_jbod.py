@@ -141,7 +141,11 @@ def test_emu_intra_action_acceptance(emu_lib, oracle_lib):
     with pytest.raises(ccmi.IllegalArgumentException):
         cm.action_acceptance(0, 0, 0, 0, 1)  # an inter-broker action has no logdirs
     with pytest.raises(ccmi.IllegalArgumentException):  # a chain may not mix the two granularities
-        ccmi.GoalOptimizer(_zero_balance()).optimizations(cm, ccmi.goals_from_names(["DiskUsageDistributionGoal"]))
+        ccmi.GoalOptimizer(_zero_balance()).optimizations(
+            cm, ccmi.goals_from_names(["IntraBrokerDiskCapacityGoal", "DiskUsageDistributionGoal"]))
+    with pytest.raises(ccmi.IllegalArgumentException):  # nor may a goal's optimizedGoals set
+        ccmi.DiskUsageDistributionGoal(constraint=_zero_balance()).optimize(
+            cm, [ccmi.IntraBrokerDiskUsageDistributionGoal()], ccmi.OptimizationOptions())
 
 
 @pytest.mark.gpu
