@@ -706,6 +706,8 @@ ccmi_status ccmi_perf(const ccmi_session* s, ccmi_perf_counters* out) {
     out->server_required = p.serverRequired;
     out->server_busy_ms = p.serverBusyMs;
     out->server_payload_bytes = p.serverPayloadBytes;
+    out->server_chains = p.serverChains;
+    out->server_idle_exits = p.serverIdleExits;
     return CCMI_OK;
   });
 }

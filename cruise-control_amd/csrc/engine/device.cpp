@@ -36,8 +36,8 @@ hipError_t launchScanPairs(const DevTables& T, const MutTables& M, const UpdateL
 hipError_t launchPrep(const MutTables& M, const UpdateList& U, const int4* req, int4* dReq, int nReq4,
                       unsigned long long* result, unsigned int* done, hipStream_t st);
 uint32_t scanXcdSliceMinCols();
-hipError_t launchScanServer(const DevTables& T, const MutTables& M, const ServerCmd* cmd, const char* pay,
-                            const RowRef* pool, unsigned long long* result, unsigned int* done,
+hipError_t launchScanServer(const DevTables& T, const MutTables& M, const ChainTables& C, const ServerCmd* cmd,
+                            const char* pay, const RowRef* pool, unsigned long long* result, unsigned int* done,
                             unsigned long long* mail, unsigned long long* t0, unsigned long long startSeq, int blocks,
                             hipStream_t st);
 hipError_t launchChainPairs(const DevTables& T, const ChainTables& C, const DevProgram& prog, const int32_t* pr,
@@ -109,7 +109,6 @@ Device::Device(int ordinal, int B, int R, int P, int T, int maxGoalSlots)
   if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
     throw std::runtime_error(std::string("libccmi is built for gfx950, device is ") + prop.gcnArchName);
   hipCheck(hipStreamCreateWithFlags((hipStream_t*)&st_, hipStreamNonBlocking), "hipStreamCreate");
-  hipCheck(hipStreamCreateWithFlags((hipStream_t*)&st2_, hipStreamNonBlocking), "hipStreamCreate");
   dalloc(&brokers_, (size_t)B);
   dalloc(&replicas_, (size_t)R);
   dalloc(&parts_, (size_t)P);
@@ -198,7 +197,7 @@ Device::~Device() {
     (void)hipFree(stamps_);
   }
   void* ps[] = {brokers_, replicas_, parts_, allowedAlive_, topicCount_, topicNrep_, topicScratch_, statsOut_,
-                statsPart_, dReq_, rowVisited_, dResult_, dDone_, tUpper_, tLower_, dRLoad_, dBLoad_, dBLnw_, dBPot_, dPOff_, dPSlots_,
+                statsPart_, dReq_, rowVisited_, dResult_, dDone_, dChainReq_, tUpper_, tLower_, dRLoad_, dBLoad_, dBLnw_, dBPot_, dPOff_, dPSlots_,
                 dPLeader_, pIneligOff_, pIneligB_, topicLead_, tMinLead_, tLeadLim_};
   for (void* p : ps)
     if (p) (void)hipFree(p);
@@ -214,10 +213,6 @@ Device::~Device() {
   if (ev0_) (void)hipEventDestroy(EV0);
   if (ev1_) (void)hipEventDestroy(EV1);
   if (ST) (void)hipStreamDestroy(ST);
-  if (st2_) {
-    (void)hipStreamSynchronize((hipStream_t)st2_);
-    (void)hipStreamDestroy((hipStream_t)st2_);
-  }
 }
 
 // Staging is only rewritten after the previous request completed (every request waits for its mailbox), so
@@ -260,6 +255,8 @@ double nowSeconds() {
   return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
 inline void hostStoreFence() { __builtin_ia32_sfence(); }
+// a launched chain longer than this is reported as stuck (C2's longest chain takes milliseconds)
+constexpr double kChainWaitSeconds = 120.0;
 }  // namespace
 
 void Device::ensureFg(size_t bytes) {
@@ -311,6 +308,68 @@ bool Device::serveScan(const DevProgram& prog, const Staged& g, bool readsTopicC
   return true;
 }
 
+// Start the server unless it runs (restarting one the host left idle for a while, far from the device's 2 s
+// watchdog); false when the device already has its budget of servers (the caller launches instead).
+bool Device::ensureServer() {
+  if (serverOn_ && nowSeconds() - lastServerUse_ > 0.25) stopServer();
+  if (serverOn_) return true;
+  progSent_ = false;
+  {
+    std::lock_guard<std::mutex> lk(g_serverMu);
+    if (g_serverWgs[ordinal_ & 63] + serverBlocks_ > kServerBudget) return false;
+    g_serverWgs[ordinal_ & 63] += serverBlocks_;
+  }
+  // the arrival counter and the result word start clean for every server launch, whatever an earlier launch left
+  hipCheck(hipMemsetAsync(dDone_, 0, sizeof(unsigned int), ST), "reset server arrivals");
+  hipCheck(hipMemsetAsync(dResult_, 0xff, sizeof(unsigned long long), ST), "reset server result");
+  hipCheck(launchScanServer(tables(), mutTables(), chainTables(), (const ServerCmd*)fg_, fg_ + kCmdBytes, segPool_,
+                            dResult_, dDone_, hResultDev_, dServerT0_, lastCmdSeq_, serverBlocks_, ST),
+           "scan_server");
+  serverOn_ = true;
+  perf.serverLaunches++;
+  perf.scanLaunches++;
+  return true;
+}
+
+// The program into the payload's program slot when it changed (or the server is new); its version
+int Device::serverProgram(const DevProgram& prog, char* pay) {
+  if (progSent_ && std::memcmp(&prog, &lastProg_, sizeof(DevProgram)) == 0) return progVer_;
+  std::memcpy(pay, &prog, sizeof(DevProgram));
+  lastProg_ = prog;
+  progSent_ = true;
+  perf.serverPayloadBytes += (int64_t)sizeof(DevProgram);
+  prof().addPayload((int64_t)sizeof(DevProgram));
+  return ++progVer_;
+}
+
+// Publish a command (seqlock: the sequence word marked busy, every other field, then behind store fences the new
+// sequence word) and wait for its result. false: the server's idle watchdog ended it before it saw the command —
+// nothing of the command ran, and the caller takes its launch path.
+bool Device::postCommand(ServerCmd& c, bool rowsSent) {
+  c.rowsEpoch = rowsEpoch_;
+  *(volatile unsigned long long*)fg_ = (seq_ + 1) | kSeqBusy;
+  hostStoreFence();
+  std::memcpy(fg_ + sizeof(unsigned long long), (const char*)&c + sizeof(unsigned long long),
+              sizeof(ServerCmd) - sizeof(unsigned long long));
+  hostStoreFence();
+  lastCmdSeq_ = ++seq_;
+  *(volatile unsigned long long*)fg_ = lastCmdSeq_;
+  hostStoreFence();
+  if (!waitMail(seq_, true)) {
+    serverOn_ = false;
+    {
+      std::lock_guard<std::mutex> lk(g_serverMu);
+      g_serverWgs[ordinal_ & 63] -= serverBlocks_;
+    }
+    perf.serverIdleExits++;
+    return false;
+  }
+  if (rowsSent) ++rowsEpoch_;
+  lastServerUse_ = nowSeconds();
+  perf.serverBusyMs += (double)hResult_[1] * 1e-5;  // 100 MHz ticks
+  return true;
+}
+
 // params: CROSS {K, Nr, N, c0, sliced, -}; PAIRS {n, keyBase, -, -, -, -}
 int64_t Device::serverRun(const DevProgram& prog, const Staged& g, int op, const void* A, size_t nA,
                           const int32_t* C, size_t nC, const int32_t params[6]) {
@@ -321,35 +380,11 @@ int64_t Device::serverRun(const DevProgram& prog, const Staged& g, int op, const
   const size_t aBytes = op == SOP_SEGS ? nA * sizeof(SegEntry) : nA * sizeof(RowRef);
   const size_t oA = oRows + rows, oC = oA + align16(aBytes), end = oC + align16(nC * 4);
   ensureFg(kCmdBytes + end);
-  const double now = nowSeconds();
-  if (serverOn_ && now - lastServerUse_ > 0.25) stopServer();  // far from the device watchdog (2 s idle)
-  if (!serverOn_) {
-    progSent_ = false;
-    bool ok;
-    {
-      std::lock_guard<std::mutex> lk(g_serverMu);
-      ok = g_serverWgs[ordinal_ & 63] + serverBlocks_ <= kServerBudget;
-      if (ok) g_serverWgs[ordinal_ & 63] += serverBlocks_;
-    }
-    if (!ok) return INT64_MIN;  // the device has its budget of servers: the caller launches instead
-    hipCheck(launchScanServer(tables(), mutTables(), (const ServerCmd*)fg_, fg_ + kCmdBytes, segPool_, dResult_,
-                              dDone_, hResultDev_, dServerT0_, lastCmdSeq_, serverBlocks_, ST),
-             "scan_server");
-    serverOn_ = true;
-    perf.serverLaunches++;
-    perf.scanLaunches++;
-  }
-  const bool sendProg = !progSent_ || std::memcmp(&prog, &lastProg_, sizeof(DevProgram)) != 0;
+  if (!ensureServer()) return INT64_MIN;
   char* pay = fg_ + kCmdBytes;
-  int ver = progVer_;
-  if (sendProg) {
-    std::memcpy(pay + oProg, &prog, sizeof(DevProgram));
-    lastProg_ = prog;
-    progSent_ = true;
-    ver = ++progVer_;
-  }
-  perf.serverPayloadBytes += (int64_t)((sendProg ? sizeof(DevProgram) : 0) + rows + aBytes + nC * 4);
-  prof().addPayload((int64_t)((sendProg ? sizeof(DevProgram) : 0) + rows + aBytes + nC * 4));
+  const int ver = serverProgram(prog, pay + oProg);
+  perf.serverPayloadBytes += (int64_t)(rows + aBytes + nC * 4);
+  prof().addPayload((int64_t)(rows + aBytes + nC * 4));
   prof().count(11, "srv.bytes.rows", (int64_t)rows);
   prof().count(12, "srv.bytes.A", (int64_t)aBytes);
   prof().count(13, "srv.bytes.C", (int64_t)nC * 4);
@@ -389,34 +424,100 @@ int64_t Device::serverRun(const DevProgram& prog, const Staged& g, int op, const
   c.oT = (uint32_t)(oRows + g.otd);
   c.oA = (uint32_t)oA;
   c.oC = (uint32_t)oC;
-  const bool rowsSent = (g.nb | g.nr | g.np | g.nt) != 0;
-  c.rowsEpoch = rowsEpoch_;
-  // seqlock: the sequence word marked busy, every other field, then (behind store fences) the sequence word
-  *(volatile unsigned long long*)fg_ = (seq_ + 1) | kSeqBusy;
-  hostStoreFence();
-  std::memcpy(fg_ + sizeof(unsigned long long), (const char*)&c + sizeof(unsigned long long),
-              sizeof(ServerCmd) - sizeof(unsigned long long));
-  hostStoreFence();
-  lastCmdSeq_ = ++seq_;
-  *(volatile unsigned long long*)fg_ = lastCmdSeq_;
-  hostStoreFence();
-  if (!waitMail(seq_, true)) {
-    // The server's idle watchdog ended it just before it could see this command (a session host that stayed away
-    // for seconds): nothing of the command ran, so it goes through a launch like any scan the server declines.
-    serverOn_ = false;
-    {
-      std::lock_guard<std::mutex> lk(g_serverMu);
-      g_serverWgs[ordinal_ & 63] -= serverBlocks_;
-    }
-    perf.serverIdleExits++;
-    return INT64_MIN;
-  }
-  if (rowsSent) ++rowsEpoch_;
-  lastServerUse_ = nowSeconds();
+  if (!postCommand(c, (g.nb | g.nr | g.np | g.nt) != 0)) return INT64_MIN;
   perf.serverScans++;
-  perf.serverBusyMs += (double)hResult_[1] * 1e-5;  // 100 MHz ticks
   const unsigned long long lo = hResult_[0] & 0xffffffffull;
   return lo == 0 ? -1 : (int64_t)(lo - 1);
+}
+
+// A K7 chain as a server command (SOP_CHAIN): payload [program | rows | load rows | slot rows | request]. false: the
+// server cannot take it (not usable here, over budget, or ended by its watchdog before it saw the command) — the
+// pending rows are back in their lists and the caller launches the chain kernel instead.
+bool Device::serverChain(const DevProgram& prog, int mode, const int32_t* a0, int n0, const int32_t* a1, int n1,
+                         const int32_t* a2, int n2, int n, int m, int maxAccepts) {
+  if (!serverUsable_ || !serverAllowed_ || !dRLoad_) return false;
+  const size_t nl = lrows.size(), ns = srows.size();
+  const size_t words = (size_t)n0 + n1 + n2;
+  const size_t oRows = align16(sizeof(DevProgram));
+  const Staged g = packUpdates(0);
+  const size_t oL = oRows + g.end, oS = oL + align16(nl * sizeof(LoadRow)), oA = oS + align16(ns * sizeof(SlotRow));
+  const size_t end = oA + align16(words * 4);
+  ensureFg(kCmdBytes + end);
+  if (!ensureServer()) {
+    unpackUpdates(g);
+    return false;
+  }
+  if (words * 4 > chainReqCap_) {
+    if (dChainReq_) hipCheck(hipFree(dChainReq_), "hipFree chain request");
+    dChainReq_ = nullptr;
+    chainReqCap_ = std::max<size_t>(words * 8, 1 << 16);
+    hipCheck(hipMalloc((void**)&dChainReq_, chainReqCap_), "hipMalloc chain request");
+  }
+  char* pay = fg_ + kCmdBytes;
+  const int ver = serverProgram(prog, pay);
+  if (g.end) std::memcpy(pay + oRows, hStage_, g.end);
+  if (nl) std::memcpy(pay + oL, lrows.data(), nl * sizeof(LoadRow));
+  if (ns) std::memcpy(pay + oS, srows.data(), ns * sizeof(SlotRow));
+  std::memcpy(pay + oA, a0, (size_t)n0 * 4);
+  if (n1) std::memcpy(pay + oA + (size_t)n0 * 4, a1, (size_t)n1 * 4);
+  if (n2) std::memcpy(pay + oA + (size_t)(n0 + n1) * 4, a2, (size_t)n2 * 4);
+  perf.serverPayloadBytes += (int64_t)(end - oRows);
+  prof().addPayload((int64_t)(end - oRows));
+  ServerCmd c;
+  std::memset(&c, 0, sizeof(c));
+  c.op = SOP_CHAIN;
+  c.progVer = ver;
+  c.nActive = 1;
+  c.nb = g.nb;
+  c.nr = g.nr;
+  c.np = g.np;
+  c.nt = g.nt;
+  c.oProg = 0;
+  c.oB = (uint32_t)(oRows + g.obr);
+  c.oR = (uint32_t)(oRows + g.orr);
+  c.oP = (uint32_t)(oRows + g.opr);
+  c.oT = (uint32_t)(oRows + g.otd);
+  c.oA = (uint32_t)oA;
+  c.chainMode = mode;
+  c.chainN = n;
+  c.chainM = m;
+  c.maxAccepts = maxAccepts;
+  c.nl = (int32_t)nl;
+  c.ns = (int32_t)ns;
+  c.oL = (uint32_t)oL;
+  c.oS = (uint32_t)oS;
+  c.chainReq = (unsigned long long)(uintptr_t)dChainReq_;
+  c.chainLog = (unsigned long long)(uintptr_t)hChainLogDev_;
+  c.chainOut = (unsigned long long)(uintptr_t)hChainOutDev_;
+  // a chain writes the tables: every later command's workgroups acquire before reading them
+  if (!postCommand(c, true)) {
+    unpackUpdates(g);
+    return false;
+  }
+  lrows.clear();
+  srows.clear();
+  perf.serverChains++;
+  return true;
+}
+
+// A launched kernel's completion on the session stream, bounded: past `seconds` the wait reports what it waited for and
+// the mailbox / server state instead of blocking forever.
+void Device::streamWait(const char* what, double seconds) {
+  const double t0 = nowSeconds();
+  for (uint64_t spins = 0;; ++spins) {
+    const hipError_t q = hipStreamQuery(ST);
+    if (q == hipSuccess) return;
+    if (q != hipErrorNotReady) hipCheck(q, what);
+    if (nowSeconds() - t0 > seconds) {
+      char msg[256];
+      std::snprintf(msg, sizeof(msg), "%s did not complete within %.0f s (server %s, mail %016llx, server exit %016llx)",
+                    what, seconds, serverOn_ ? "on" : "off", (unsigned long long)hResult_[0],
+                    (unsigned long long)hResult_[3]);
+      throw std::runtime_error(msg);
+    }
+    if (spins < 4096) __builtin_ia32_pause();
+    else sched_yield();
+  }
 }
 
 void Device::writeRowRefs(char* dst, const int32_t* reps, size_t n) const {
@@ -637,15 +738,6 @@ void Device::unpackUpdates(const Staged& g) {
 
 // One `prep` launch: apply the staged rows, copy `reqBytes` of request (staged at g.end) into HBM, and (for a
 // scan) reset the result words and the arrival counter.
-// prep on `stream` without stopping the server (the staging kernels of a chain that runs beside it)
-void Device::launchPrepOn(const Staged& g, size_t reqBytes, void* stream) {
-  const int nReq4 = (int)(align16(reqBytes) / 16);
-  if (nReq4) ensureReq((size_t)nReq4 * 16);
-  hipCheck(launchPrep(mutTables(), stagedList(g), (const int4*)(hStageDev_ + g.end), (int4*)dReq_, nReq4, nullptr,
-                      nullptr, (hipStream_t)stream),
-           "prep");
-}
-
 void Device::launchPrepFor(const Staged& g, size_t reqBytes, bool scan) {
   stopServer();
   const int nReq4 = (int)(align16(reqBytes) / 16);
@@ -1068,8 +1160,8 @@ size_t Device::stageChainCopy(size_t reqBytes, Staged& g, size_t& oReq, F fill, 
   // prep copies [g.end + oR, + reqBytes) into dReq_ when given the request at that offset
   Staged h = g;
   h.end = g.end + oR;
-  if (stream == st_) launchPrepFor(h, reqBytes, false);
-  else launchPrepOn(h, reqBytes, stream);
+  launchPrepFor(h, reqBytes, false);
+  (void)stream;
   oReq = 0;
   return g.end + oR;
 }
@@ -1087,104 +1179,92 @@ void Device::ensureChainLog(size_t n) {
 Device::ChainResult Device::chainPairs(const DevProgram& prog, const int32_t* pr, const int32_t* pb,
                                        const int32_t* next, int n, int maxAccepts, std::vector<int32_t>& log) {
   DeviceGuard dg(ordinal_);
-  // opt-in (CCMI_CHAIN_BESIDE_SERVER=1): the chain on a second stream beside the running server hung the C2 default
-  // chain in the full GPU suite (test_gpu_matches_headline_golden[c2_default], r03); by default the server is stopped
-  static const bool besideOk = std::getenv("CCMI_CHAIN_BESIDE_SERVER") != nullptr;
-  const bool beside = serverOn_ && besideOk;
-  if (!beside) stopServer();
-  hipStream_t CS = beside ? (hipStream_t)st2_ : ST;
   ChainResult res;
   log.clear();
   if (n <= 0) {
     flushPending();
     return res;
   }
-  const size_t oB = align16((size_t)n * 4), oN = oB + align16((size_t)n * 4), req = oN + align16((size_t)n * 4);
-  Staged g;
-  size_t oReq = 0;
-  const size_t at = stageChainCopy(req, g, oReq, [&](char* base) {
-    std::memcpy(base, pr, (size_t)n * 4);
-    std::memcpy(base + oB, pb, (size_t)n * 4);
-    std::memcpy(base + oN, next, (size_t)n * 4);
-  }, CS);
-  (void)at;
   ensureChainLog((size_t)n);
-  if (timing) (void)hipEventRecord(EV0, CS);
-  hipCheck(launchChainPairs(tables(), chainTables(), prog, (const int32_t*)dReq_, (const int32_t*)(dReq_ + oB),
-                            (const int32_t*)(dReq_ + oN), n, maxAccepts, hChainLogDev_, hChainOutDev_, CS),
-           "chain_pairs");
-  if (timing) (void)hipEventRecord(EV1, CS);
-  hipCheck(hipStreamSynchronize(CS), "chain");
-  // the chain's record writes (and its staging kernels') become visible to the server's next command through the
-  // agent acquire its workgroups take on a new rows epoch
-  if (beside) ++rowsEpoch_;
+  // the running server takes the chain as a command (no stop and relaunch around it); otherwise one launch
+  const bool served = serverChain(prog, CM_PAIRS, pr, n, pb, n, next, n, n, 0, maxAccepts);
+  if (!served) {
+    stopServer();
+    const size_t oB = align16((size_t)n * 4), oN = oB + align16((size_t)n * 4), req = oN + align16((size_t)n * 4);
+    Staged g;
+    size_t oReq = 0;
+    (void)stageChainCopy(req, g, oReq, [&](char* base) {
+      std::memcpy(base, pr, (size_t)n * 4);
+      std::memcpy(base + oB, pb, (size_t)n * 4);
+      std::memcpy(base + oN, next, (size_t)n * 4);
+    }, st_);
+    if (timing) (void)hipEventRecord(EV0, ST);
+    hipCheck(launchChainPairs(tables(), chainTables(), prog, (const int32_t*)dReq_, (const int32_t*)(dReq_ + oB),
+                              (const int32_t*)(dReq_ + oN), n, maxAccepts, hChainLogDev_, hChainOutDev_, ST),
+             "chain_pairs");
+    if (timing) (void)hipEventRecord(EV1, ST);
+    streamWait("chain_pairs", kChainWaitSeconds);
+    perf.scanLaunches++;
+    perf.chainLaunches++;
+    if (timing) {
+      float ms = 0.f;
+      hipCheck(hipEventElapsedTime(&ms, EV0, EV1), "hipEventElapsedTime");
+      perf.scanKernelMs += ms;
+    }
+  }
   const volatile ChainResultDev* vo = hChainOut_;
   const ChainResultDev out{vo->accepts, vo->visited, vo->failRow};
   perf.syncs++;
-  perf.scanLaunches++;
-  perf.chainLaunches++;
   perf.scanPairs += (int64_t)out.visited;
   perf.scanRequired += (int64_t)out.visited;
-  if (timing) {
-    float ms = 0.f;
-    hipCheck(hipEventElapsedTime(&ms, EV0, EV1), "hipEventElapsedTime");
-    perf.scanKernelMs += ms;
-  }
   res.accepts = (int64_t)out.accepts;
   res.visited = (int64_t)out.visited;
   log.resize((size_t)res.accepts);
-  if (res.accepts)
-    std::memcpy(log.data(), hChainLog_, sizeof(int32_t) * res.accepts);
+  if (res.accepts) std::memcpy(log.data(), hChainLog_, sizeof(int32_t) * res.accepts);
   return res;
 }
 
 Device::ChainResult Device::chainRackRows(const DevProgram& prog, const int32_t* rows, int n, const int32_t* cands,
                                           int N, std::vector<int32_t>& log) {
   DeviceGuard dg(ordinal_);
-  // opt-in (CCMI_CHAIN_BESIDE_SERVER=1): the chain on a second stream beside the running server hung the C2 default
-  // chain in the full GPU suite (test_gpu_matches_headline_golden[c2_default], r03); by default the server is stopped
-  static const bool besideOk = std::getenv("CCMI_CHAIN_BESIDE_SERVER") != nullptr;
-  const bool beside = serverOn_ && besideOk;
-  if (!beside) stopServer();
-  hipStream_t CS = beside ? (hipStream_t)st2_ : ST;
   ChainResult res;
   log.clear();
   if (n <= 0) {
     flushPending();
     return res;
   }
-  const size_t oC = align16((size_t)n * 4), req = oC + align16((size_t)N * 4);
-  Staged g;
-  size_t oReq = 0;
-  (void)stageChainCopy(req, g, oReq, [&](char* base) {
-    std::memcpy(base, rows, (size_t)n * 4);
-    std::memcpy(base + oC, cands, (size_t)N * 4);
-  }, CS);
   ensureChainLog((size_t)2 * n);
-  if (timing) (void)hipEventRecord(EV0, CS);
-  hipCheck(launchChainRackRows(tables(), chainTables(), prog, (const int32_t*)dReq_, n, (const int32_t*)(dReq_ + oC), N,
-                               hChainLogDev_, hChainOutDev_, CS),
-           "chain_rack_rows");
-  if (timing) (void)hipEventRecord(EV1, CS);
-  hipCheck(hipStreamSynchronize(CS), "chain");
-  // the chain's record writes (and its staging kernels') become visible to the server's next command through the
-  // agent acquire its workgroups take on a new rows epoch
-  if (beside) ++rowsEpoch_;
+  const bool served = serverChain(prog, CM_RACK_ROWS, rows, n, cands, N, nullptr, 0, n, N, 0);
+  if (!served) {
+    stopServer();
+    const size_t oC = align16((size_t)n * 4), req = oC + align16((size_t)N * 4);
+    Staged g;
+    size_t oReq = 0;
+    (void)stageChainCopy(req, g, oReq, [&](char* base) {
+      std::memcpy(base, rows, (size_t)n * 4);
+      std::memcpy(base + oC, cands, (size_t)N * 4);
+    }, st_);
+    if (timing) (void)hipEventRecord(EV0, ST);
+    hipCheck(launchChainRackRows(tables(), chainTables(), prog, (const int32_t*)dReq_, n,
+                                 (const int32_t*)(dReq_ + oC), N, hChainLogDev_, hChainOutDev_, ST),
+             "chain_rack_rows");
+    if (timing) (void)hipEventRecord(EV1, ST);
+    streamWait("chain_rack_rows", kChainWaitSeconds);
+    perf.scanLaunches++;
+    perf.chainLaunches++;
+    if (timing) {
+      float ms = 0.f;
+      hipCheck(hipEventElapsedTime(&ms, EV0, EV1), "hipEventElapsedTime");
+      perf.scanKernelMs += ms;
+    }
+  }
   const volatile ChainResultDev* vo = hChainOut_;
   const ChainResultDev out{vo->accepts, vo->visited, vo->failRow};
   perf.syncs++;
-  perf.scanLaunches++;
-  perf.chainLaunches++;
-  if (timing) {
-    float ms = 0.f;
-    hipCheck(hipEventElapsedTime(&ms, EV0, EV1), "hipEventElapsedTime");
-    perf.scanKernelMs += ms;
-  }
   res.accepts = (int64_t)out.accepts;
   res.failRow = (int64_t)out.failRow;
   log.resize((size_t)res.accepts * 2);
-  if (res.accepts)
-    std::memcpy(log.data(), hChainLog_, sizeof(int32_t) * 2 * res.accepts);
+  if (res.accepts) std::memcpy(log.data(), hChainLog_, sizeof(int32_t) * 2 * res.accepts);
   int64_t evaluated = res.failRow ? N : 0;
   for (size_t i = 1; i < log.size(); i += 2) evaluated += log[i] + 1;
   perf.scanPairs += evaluated;

@@ -53,6 +53,7 @@ struct DevicePerf {
   double serverBusyMs = 0;     // their device busy time (s_memrealtime, command seen -> result published)
   int64_t serverPayloadBytes = 0;  // command payload written through the BAR (program, rows, request arrays)
   int64_t serverRequired = 0;  // candidates those scans had to evaluate
+  int64_t serverChains = 0;    // K7 chains the running server took as commands (no launch, no server restart)
 };
 
 // K6 (kernels/intra.hip, intra.h): one intra-broker goal over every broker in one launch.
@@ -187,10 +188,6 @@ class Device {
  private:
   int ordinal_, B_, R_, P_, T_, ldB_, G_;
   void* st_ = nullptr;  // hipStream_t
-  // K7 chains (and their staging kernels) run on this second stream beside a running scan server (its workgroups use
-  // 200 VGPRs per wave and 16 KB LDS, so a chain workgroup fits on a CU next to one), instead of stopping and
-  // relaunching the server around every chain: opt-in only (CCMI_CHAIN_BESIDE_SERVER=1; it hung the C2 chain in r03).
-  void* st2_ = nullptr;
   // tables (records, devtypes.h) and the host copies used to assemble them
   BrokerRec* brokers_ = nullptr;
   ReplicaRec* replicas_ = nullptr;
@@ -229,7 +226,6 @@ class Device {
   void ensureStage(size_t bytes);
   void ensureReq(size_t bytes);
   void launchPrepFor(const Staged& g, size_t reqBytes, bool scan);
-  void launchPrepOn(const Staged& g, size_t reqBytes, void* stream);
   UpdateList stagedList(const Staged& g) const;
   UpdateList overlayFor(const Staged& g) const;
   MutTables mutTables() const;
@@ -252,6 +248,15 @@ class Device {
   int32_t rowsEpoch_ = 0;              // server commands with rows so far (ServerCmd.rowsEpoch)
   double lastServerUse_ = 0;  // steady-clock seconds of the last served scan (the host restarts an idle server)
   bool serveScan(const DevProgram& prog, const Staged& g, bool readsTopicCounts);
+  bool ensureServer();
+  int serverProgram(const DevProgram& prog, char* pay);
+  bool postCommand(ServerCmd& c, bool rowsSent);
+  // a K7 chain as a server command over the request arrays a0 | a1 | a2 (SOP_CHAIN); false = launch it instead
+  bool serverChain(const DevProgram& prog, int mode, const int32_t* a0, int n0, const int32_t* a1, int n1,
+                   const int32_t* a2, int n2, int n, int m, int maxAccepts);
+  void streamWait(const char* what, double seconds);
+  int32_t* dChainReq_ = nullptr;  // SOP_CHAIN request copy in HBM (the chain rereads it per decision)
+  size_t chainReqCap_ = 0;
   const int32_t *rowBroker_ = nullptr, *rowPart_ = nullptr, *partTopic_ = nullptr;
   void writeRowRefs(char* dst, const int32_t* reps, size_t n) const;
   // A: replica ids sent as RowRefs (nA entries), or for SOP_SEGS the segment table (nA entries of SegEntry)

@@ -224,7 +224,11 @@ struct ScanHeader {
 
 // Scan-server command (kernels/scan.hip scan_server), at the start of the fine-grained VRAM block the host writes;
 // `seq` is written last, behind a store fence. Offsets are bytes from the payload base.
-enum ServerOp : int32_t { SOP_CROSS = 0, SOP_PAIRS = 1, SOP_EXIT = 2, SOP_SEGS = 3 };
+// SOP_CHAIN: a K7 chain (ChainMode) run by workgroup 0 of the server (nActive = 1) on the tables themselves: the
+// command's rows, load rows (oL, nl) and slot rows (oS, ns) are applied first, the request is copied into chainReq,
+// the decisions are logged to chainLog / chainOut (host-mapped), and the writes are released at system scope before
+// the publish — no stop and relaunch of the server around a chain.
+enum ServerOp : int32_t { SOP_CROSS = 0, SOP_PAIRS = 1, SOP_EXIT = 2, SOP_SEGS = 3, SOP_CHAIN = 4 };
 // SOP_SEGS: a cross scan whose rows are the concatenation of nSegs segments of the device-resident snapshot pool
 // (Device::scanSegs); the segment table at oA holds {first pool entry, first row} per segment plus {0, K} at the end.
 constexpr int kMaxSegs = 1024;
@@ -246,6 +250,13 @@ struct alignas(16) ServerCmd {
   // commands with rows before this one since the session started: a workgroup takes an agent acquire before it reads
   // the tables whenever this differs from the value it last acquired at (rows of commands it skipped included)
   int32_t rowsEpoch;
+  // SOP_CHAIN: mode (ChainMode), n (pairs / rows), N (RACK_ROWS candidates), maxAccepts (PAIRS), load / slot rows
+  int32_t chainMode, chainN, chainM, maxAccepts;
+  int32_t nl, ns;
+  uint32_t oL, oS;
+  unsigned long long chainReq;  // device addresses: HBM scratch for the request, host-mapped log and result
+  unsigned long long chainLog;
+  unsigned long long chainOut;
 };
 // The sequence word is a seqlock: the host stores (next | kSeqBusy) before it rewrites the other fields and `next`
 // after; a workgroup accepts a header only when the word it read before and after its copy is the same, not busy.

@@ -818,7 +818,67 @@ __device__ __forceinline__ void copySysOneThread(X* dst, const X* src) {  // all
 }
 constexpr unsigned long long kServerIdleTicks = 200000000ull;  // 2 s of s_memrealtime (100 MHz)
 
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, kServerWaves))) void scan_server(DevTables T, MutTables Mt, const ServerCmd* __restrict__ cmd,
+// thread 0's record writes become visible to the whole workgroup (one CU: workgroup scope; the next launch sees them
+// through the kernel boundary)
+__device__ __forceinline__ void chainSync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  __syncthreads();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+
+// K7 chain bodies (defined with the chain kernels below; SOP_CHAIN runs them inside the server)
+__device__ __forceinline__ void chainPairsRun(const DevTables& T, const ChainTables& C, const DevProgram& prog, const OverlayLds& ov,
+                              LoadVec* sc, const int32_t* __restrict__ pr, const int32_t* __restrict__ pb,
+                              const int32_t* __restrict__ next, int n, int maxAccepts, int32_t* __restrict__ log,
+                              ChainResultDev* __restrict__ out);
+__device__ __forceinline__ void chainRackRowsRun(const DevTables& T, const ChainTables& C, const DevProgram& prog,
+                                 const OverlayLds& ov, LoadVec* sc, const int32_t* __restrict__ rows, int n,
+                                 const int32_t* __restrict__ cands, int N, int32_t* __restrict__ log,
+                                 ChainResultDev* __restrict__ out);
+
+// SOP_CHAIN on workgroup 0: the command's rows and the host's load / slot rows into the tables, the request into HBM
+// (the chain rereads it per decision), then the chain itself on an empty overlay. Every write of the chain is a plain
+// store of this workgroup; the caller releases them (system scope: the log is host-mapped) before the publish.
+__device__ __forceinline__ void serverChain(const DevTables& T, const ChainTables& C, const MutTables& Mt,
+                                            const DevProgram& prog, const ServerCmd& c, const char* __restrict__ pay,
+                                            const UpdateList& U, OverlayLds& ov, LoadVec* sc) {
+  applyRowsCoherent(Mt, ov.b, ov.nb, ov.r, ov.nr, ov.p, ov.np, threadIdx.x, blockDim.x);
+  for (int i = threadIdx.x; i < U.nt; i += blockDim.x) {
+    TopicCountDelta d;
+    copySysOneThread(&d, &U.tdel[i]);
+    atomicAdd(&(d.kind ? Mt.topicLead : Mt.topicCount)[(size_t)d.topic * Mt.ldB + d.broker], d.delta);
+  }
+  const LoadRow* lrows = (const LoadRow*)(pay + c.oL);
+  for (int i = threadIdx.x; i < c.nl; i += blockDim.x) {
+    LoadRow x;
+    copySysOneThread(&x, &lrows[i]);
+    LoadVec* dst = x.kind == LR_REPLICA ? C.rLoad
+                   : (x.kind == LR_BROKER ? C.bLoad : (x.kind == LR_LEADERSHIP_NW ? C.bLnw : C.bPot));
+    dst[x.id] = x.v;
+  }
+  const SlotRow* srows = (const SlotRow*)(pay + c.oS);
+  for (int i = threadIdx.x; i < c.ns; i += blockDim.x) {
+    SlotRow x;
+    copySysOneThread(&x, &srows[i]);
+    const int o = C.pOff[x.p], n = C.pOff[x.p + 1] - o;
+    for (int k = 0; k < n; ++k) C.pSlots[o + k] = x.slots[k];
+    C.pLeader[x.p] = x.leader;
+  }
+  int32_t* req = reinterpret_cast<int32_t*>(c.chainReq);
+  const int words = c.chainMode == CM_PAIRS ? 3 * c.chainN : c.chainN + c.chainM;
+  for (int w = threadIdx.x; w < words; w += blockDim.x) req[w] = ldSys(reinterpret_cast<const int32_t*>(pay + c.oA) + w);
+  if (threadIdx.x == 0) ov.nb = ov.nr = ov.np = 0;  // the tables hold the rows now
+  __builtin_amdgcn_s_waitcnt(0);
+  chainSync();
+  int32_t* log = reinterpret_cast<int32_t*>(c.chainLog);
+  ChainResultDev* out = reinterpret_cast<ChainResultDev*>(c.chainOut);
+  if (c.chainMode == CM_PAIRS)
+    chainPairsRun(T, C, prog, ov, sc, req, req + c.chainN, req + 2 * c.chainN, c.chainN, c.maxAccepts, log, out);
+  else
+    chainRackRowsRun(T, C, prog, ov, sc, req, c.chainN, req + c.chainN, c.chainM, log, out);
+}
+
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, kServerWaves))) void scan_server(DevTables T, MutTables Mt, ChainTables Ch, const ServerCmd* __restrict__ cmd,
                                                       const char* __restrict__ pay, const RowRef* __restrict__ pool,
                                                       unsigned long long* __restrict__ result,
                                                       unsigned int* __restrict__ done,
@@ -830,6 +890,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, kServ
   __shared__ ServerCmd c;
   __shared__ int sExit;
   __shared__ SegEntry sSeg[kMaxSegs + 1];
+  __shared__ alignas(8) unsigned char scRaw[2 * sizeof(LoadVec)];  // a chain's leadership hand-over (LoadVec has a
+                                                                     // member initializer)
   unsigned long long last = startSeq;
   int progVer = -1;
   int acqEpoch = -1;  // ServerCmd.rowsEpoch of this workgroup's last acquire (-1: none since the launch)
@@ -933,7 +995,18 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, kServ
     bool firstTile = true;
     const int32_t* A = (const int32_t*)(pay + c.oA);
     const int32_t* C = (const int32_t*)(pay + c.oC);
-    if (c.op == SOP_CROSS || c.op == SOP_SEGS) {
+    if (c.op == SOP_CHAIN) {
+      stage();
+      serverChain(T, Ch, Mt, prog, c, pay, U, ov, reinterpret_cast<LoadVec*>(scRaw));
+      // every wave's stores complete, then one system-scope release: the records and loads for the other XCDs' next
+      // acquire, the log and result for the host (MI355X_MICROARCH.md, inter-workgroup visibility)
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (threadIdx.x == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+    } else if (c.op == SOP_CROSS || c.op == SOP_SEGS) {
       const bool segs = c.op == SOP_SEGS;
       bool segsLoaded = false;
       const int nSegs = c.nSegs;
@@ -1033,7 +1106,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, kServ
     // The writer workgroup writes the command's rows into the tables for the next commands (no workgroup reads them
     // from the tables in this one: the LDS overlay has them) after its tiles, with write-through device-scope stores,
     // and applies the topic-count deltas with device-scope atomics.
-    if (writer && rows) {
+    if (writer && rows && c.op != SOP_CHAIN) {
       if (!staged) stage();
       applyRowsCoherent(Mt, ov.b, ov.nb, ov.r, ov.nr, ov.p, ov.np, threadIdx.x, blockDim.x);
       for (int i = threadIdx.x; i < U.nt; i += blockDim.x) {
@@ -1231,13 +1304,6 @@ struct DevApply {
   }
 };
 
-// thread 0's record writes become visible to the whole workgroup (one CU: workgroup scope; the next launch sees them
-// through the kernel boundary)
-__device__ __forceinline__ void chainSync() {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-  __syncthreads();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-}
 
 // Apply one move with the whole workgroup (apply.h lanes on threads 0..5, one step at a time); every thread calls it.
 template <int WC>
@@ -1294,15 +1360,12 @@ __device__ __forceinline__ unsigned long long chainFirstPair(const DevTables& T,
 
 // PAIRS: pairs (pr[q], pb[q]) in reference order; after accepting q the loop resumes at next[q]; at most
 // maxAccepts moves (the callers' stop counts). visited = reference-equivalent candidates of the sequence of scans.
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, kServerWaves))) void chain_pairs(DevTables T, ChainTables C, DevProgram prog,
-                                                      const int32_t* __restrict__ pr, const int32_t* __restrict__ pb,
-                                                      const int32_t* __restrict__ next, int n, int maxAccepts,
-                                                      int32_t* __restrict__ log, ChainResultDev* __restrict__ out) {
-  __shared__ OverlayLds ov;
-  __shared__ alignas(8) unsigned char scRaw[2 * sizeof(LoadVec)];  // LoadVec has a member initializer
-  LoadVec* sc = reinterpret_cast<LoadVec*>(scRaw);
-  if (threadIdx.x == 0) ov.nb = ov.nr = ov.np = 0;
-  __syncthreads();
+// The body runs in its own launch (chain_pairs) or inside the scan server (SOP_CHAIN); `ov` is an empty overlay.
+__device__ __forceinline__ void chainPairsRun(const DevTables& T, const ChainTables& C, const DevProgram& prog,
+                                              const OverlayLds& ov, LoadVec* sc, const int32_t* __restrict__ pr,
+                                              const int32_t* __restrict__ pb, const int32_t* __restrict__ next, int n,
+                                              int maxAccepts, int32_t* __restrict__ log,
+                                              ChainResultDev* __restrict__ out) {
   int start = 0, acc = 0;
   unsigned long long visited = 0;
   // CCMI_STAMPS: thread 0 sums the time in candidate evaluation and in applying moves (stamps[8200 .. 8203])
@@ -1347,19 +1410,25 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, kServ
   }
 }
 
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, kServerWaves))) void chain_pairs(DevTables T, ChainTables C, DevProgram prog,
+                                                      const int32_t* __restrict__ pr, const int32_t* __restrict__ pb,
+                                                      const int32_t* __restrict__ next, int n, int maxAccepts,
+                                                      int32_t* __restrict__ log, ChainResultDev* __restrict__ out) {
+  __shared__ OverlayLds ov;
+  __shared__ alignas(8) unsigned char scRaw[2 * sizeof(LoadVec)];  // LoadVec has a member initializer
+  if (threadIdx.x == 0) ov.nb = ov.nr = ov.np = 0;
+  __syncthreads();
+  chainPairsRun(T, C, prog, ov, reinterpret_cast<LoadVec*>(scRaw), pr, pb, next, n, maxAccepts, log, out);
+}
+
 // RACK_ROWS: AbstractRackAwareGoal.rebalanceForBroker (AbstractRackAwareGoal.java:144-170) over the rows of every
 // broker in order. A row is skipped when its broker is alive, the replica online and shouldKeepInTheCurrentBroker
 // holds on the CURRENT partition state (RackAwareGoal.java:214-225); otherwise the first candidate in cands[0, N)
 // that rackAwareEligibleBrokers keeps and the predicate conjunction accepts wins. No winner: failRow = row + 1.
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, kServerWaves))) void chain_rack_rows(DevTables T, ChainTables C, DevProgram prog,
-                                                          const int32_t* __restrict__ rows, int n,
-                                                          const int32_t* __restrict__ cands, int N,
-                                                          int32_t* __restrict__ log, ChainResultDev* __restrict__ out) {
-  __shared__ OverlayLds ov;
-  __shared__ alignas(8) unsigned char scRaw[2 * sizeof(LoadVec)];  // LoadVec has a member initializer
-  LoadVec* sc = reinterpret_cast<LoadVec*>(scRaw);
-  if (threadIdx.x == 0) ov.nb = ov.nr = ov.np = 0;
-  __syncthreads();
+__device__ __forceinline__ void chainRackRowsRun(const DevTables& T, const ChainTables& C, const DevProgram& prog,
+                                                 const OverlayLds& ov, LoadVec* sc, const int32_t* __restrict__ rows,
+                                                 int n, const int32_t* __restrict__ cands, int N,
+                                                 int32_t* __restrict__ log, ChainResultDev* __restrict__ out) {
   int acc = 0;
   unsigned long long fail = 0;
   for (int k = 0; k < n; ++k) {
@@ -1404,6 +1473,17 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, kServ
     out->visited = 0;
     out->failRow = fail;
   }
+}
+
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, kServerWaves))) void chain_rack_rows(DevTables T, ChainTables C, DevProgram prog,
+                                                          const int32_t* __restrict__ rows, int n,
+                                                          const int32_t* __restrict__ cands, int N,
+                                                          int32_t* __restrict__ log, ChainResultDev* __restrict__ out) {
+  __shared__ OverlayLds ov;
+  __shared__ alignas(8) unsigned char scRaw[2 * sizeof(LoadVec)];  // LoadVec has a member initializer
+  if (threadIdx.x == 0) ov.nb = ov.nr = ov.np = 0;
+  __syncthreads();
+  chainRackRowsRun(T, C, prog, ov, reinterpret_cast<LoadVec*>(scRaw), rows, n, cands, N, log, out);
 }
 
 // Host-side load changes since the last chain (LoadRow / SlotRow lists staged in host-mapped memory).
@@ -1498,12 +1578,12 @@ hipError_t launchScanPairs(const DevTables& T, const MutTables& M, const UpdateL
 }
 
 // One workgroup per CU slot: `blocks` workgroups of kBlock threads, all resident (the launcher caps it at 2 per CU).
-hipError_t launchScanServer(const DevTables& T, const MutTables& M, const ServerCmd* cmd, const char* pay,
-                            const RowRef* pool, unsigned long long* result, unsigned int* done,
+hipError_t launchScanServer(const DevTables& T, const MutTables& M, const ChainTables& C, const ServerCmd* cmd,
+                            const char* pay, const RowRef* pool, unsigned long long* result, unsigned int* done,
                             unsigned long long* mail, unsigned long long* t0, unsigned long long startSeq, int blocks,
                             hipStream_t st) {
   if (blocks < (int)kXcds || blocks % (int)kXcds != 0 || blocks > 512) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(scan_server, dim3(blocks), dim3(kBlock), 0, st, T, M, cmd, pay, pool, result, done, mail, t0,
+  hipLaunchKernelGGL(scan_server, dim3(blocks), dim3(kBlock), 0, st, T, M, C, cmd, pay, pool, result, done, mail, t0,
                      startSeq);
   return hipGetLastError();
 }

@@ -510,6 +510,11 @@ typedef struct ccmi_perf_counters {
   int64_t server_required;
   double server_busy_ms;
   int64_t server_payload_bytes; /* command payload the host wrote into device memory for the server */
+  /* ABI v8: K7 chains the running server took as commands (SOP_CHAIN: no launch, no server stop and relaunch; the
+   * chain_launches above count only chains that ran as their own launch), and commands the server's idle watchdog
+   * ended before it saw them (each then ran as a launch) */
+  int64_t server_chains;
+  int64_t server_idle_exits;
 } ccmi_perf_counters;
 ccmi_status ccmi_perf(const ccmi_session* s, ccmi_perf_counters* out);
 void ccmi_perf_reset(ccmi_session* s);
