@@ -196,21 +196,6 @@ void validateChain(const ccmi_session* s, const int32_t* kinds, int n, const std
   const int total = n + (int)priors.size();
   if (intra != 0 && intra != total)
     throw std::invalid_argument("intra-broker goals cannot be optimized together with inter-broker goals");
-  // host resources (Resource.isHostResource: CPU, NW_IN, NW_OUT) are checked against the host's load and capacity by
-  // these goals; with two brokers on one host that differs from the per-broker evaluation of this build (ccmi.h)
-  if (s->model.sharedHosts)
-    for (int i = 0; i < n; ++i)
-      switch (kinds[i]) {
-        case CCMI_GOAL_CPU_CAPACITY:
-        case CCMI_GOAL_NW_IN_CAPACITY:
-        case CCMI_GOAL_NW_OUT_CAPACITY:
-        case CCMI_GOAL_CPU_USAGE_DISTRIBUTION:
-        case CCMI_GOAL_NW_IN_USAGE_DISTRIBUTION:
-        case CCMI_GOAL_NW_OUT_USAGE_DISTRIBUTION:
-          throw ccmi::Unsupported("goal kind " + std::to_string(kinds[i]) +
-                                  " reads host-level load, and this model has brokers sharing a host");
-        default: break;
-      }
 }
 
 // AnalyzerUtils.getDiff (AnalyzerUtils.java:63-93) against the session's initial placement
@@ -359,6 +344,15 @@ ccmi_status ccmi_session_create(int32_t device_ordinal, const ccmi_cluster_desc*
                              m.rOrigDisk.data(), rDu.data(), rScore.data(), m.rStatic.data());
       s->device->setDiskUtil(m.dUtil.data());
       m.diskDirty = false;
+    }
+    if (m.sharedHosts) {  // every broker's host utilization and capacity of the host resources
+      std::vector<double> hu((size_t)3 * m.B), hc((size_t)3 * m.B);
+      for (int b = 0; b < m.B; ++b)
+        for (int k = 0; k < 3; ++k) {
+          hu[3 * (size_t)b + k] = m.hu(b, k);
+          hc[3 * (size_t)b + k] = m.hcap(b, k);
+        }
+      s->device->uploadHosts(hu.data(), hc.data());
     }
     m.dev = s->device.get();
     s->engine = std::make_unique<ccmi::Engine>(m, s->device.get());

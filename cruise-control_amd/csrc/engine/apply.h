@@ -63,8 +63,9 @@ CCMI_LD void applyReplicaLane(S& s, int lane, int r, int src, int dst, int lr, b
   ldAddSignedAll(x, o, s.W, !(lane & 1));
   ldCopy(t, x, s.W);
   BrokerRec& rec = s.brk(b);
-  if (lane < 2) {
+  if (lane < 2) {  // (chains run only when every host holds one broker: the host values are the broker's)
     for (int k = 0; k < 4; ++k) rec.util[k] = ldUtil(x, k, s.W);
+    for (int k = 0; k < 3; ++k) rec.hutil[k] = rec.util[k];
   } else if (lane < 4) {
     rec.pot = ldUtil(x, R_NW_OUT, s.W);
   } else {
@@ -143,6 +144,7 @@ CCMI_LD void applyLeadershipLane(S& s, int step, int lane, int sr, int dr, int s
     if (lane < 2) {
       BrokerRec& rec = s.brk(lane == 0 ? src : dst);
       for (int k = 0; k < 4; ++k) rec.util[k] = ldUtil(x, k, s.W);
+      for (int k = 0; k < 3; ++k) rec.hutil[k] = rec.util[k];
     } else {
       ReplicaRec& rec = s.rep(dr);
       rec.flags |= (int32_t)RF_LEADER;

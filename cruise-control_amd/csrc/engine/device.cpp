@@ -198,7 +198,7 @@ Device::~Device() {
   }
   void* ps[] = {brokers_, replicas_, parts_, allowedAlive_, topicCount_, topicNrep_, topicScratch_, statsOut_,
                 statsPart_, dReq_, rowVisited_, dResult_, dDone_, dChainReq_, tUpper_, tLower_, dRLoad_, dBLoad_, dBLnw_, dBPot_, dPOff_, dPSlots_,
-                dPLeader_, pIneligOff_, pIneligB_, topicLead_, tMinLead_, tLeadLim_};
+                dPLeader_, pIneligOff_, pIneligB_, topicLead_, tMinLead_, tLeadLim_, hostCap_};
   for (void* p : ps)
     if (p) (void)hipFree(p);
   if (hChainLog_) (void)hipHostFree(hChainLog_);
@@ -547,6 +547,7 @@ DevTables Device::tables() const {
   t.topicLead = topicLead_;
   t.tMinLead = tMinLead_;
   t.tLeadLim = tLeadLim_;
+  t.hostCap = hostCap_;
   t.B = B_;
   t.R = R_;
   t.P = P_;
@@ -601,6 +602,7 @@ void Device::uploadDynamic(const double* bUtilRM, const int32_t* bNrep, const in
     x.lbi = bLeadNwIn[b];
     x.alive = bAlive[b];
     x.allowedBits = allowedHost_[b];
+    for (int k = 0; k < 3; ++k) x.hutil[k] = x.util[k];  // a host of its own (uploadHosts otherwise)
   }
   std::vector<ReplicaRec> reps(R_);
   for (int r = 0; r < R_; ++r) {
@@ -628,6 +630,16 @@ void Device::uploadDynamic(const double* bUtilRM, const int32_t* bNrep, const in
            "upload topicCount");
   hRPart_.clear();
   hROrig_.clear();
+}
+
+void Device::uploadHosts(const double* hutil, const double* hcap) {
+  DeviceGuard dg(ordinal_);
+  stopServer();
+  for (int b = 0; b < B_; ++b)
+    for (int k = 0; k < 3; ++k) hBrokers_[b].hutil[k] = hutil[3 * (size_t)b + k];
+  hipCheck(hipMemcpy(brokers_, hBrokers_.data(), sizeof(BrokerRec) * B_, hipMemcpyHostToDevice), "upload brokers");
+  if (!hostCap_) hipCheck(hipMalloc((void**)&hostCap_, sizeof(double) * 3 * (size_t)B_), "hipMalloc hostCap");
+  hipCheck(hipMemcpy(hostCap_, hcap, sizeof(double) * 3 * (size_t)B_, hipMemcpyHostToDevice), "upload hostCap");
 }
 
 void Device::setAllowed(int slot, const uint8_t* allowedB) {
@@ -1075,7 +1087,9 @@ void Device::stats(const StatsParams& P, const uint8_t* allowedAliveHost, StatsO
   std::memcpy(hStage_ + g.end, allowedAliveHost, (size_t)ldB_);
   launchPrepFor(g, req, false);
   hipCheck(hipMemcpyAsync(allowedAlive_, dReq_, (size_t)ldB_, hipMemcpyDeviceToDevice, ST), "allowedAlive");
-  hipCheck(launchStats(P, topicCount_, topicNrep_, brokers_, allowedAlive_, (TopicPartial*)topicScratch_,
+  StatsParams Ph = P;
+  Ph.hostCap = hostCap_;
+  hipCheck(launchStats(Ph, topicCount_, topicNrep_, brokers_, allowedAlive_, (TopicPartial*)topicScratch_,
                        statsPart_, (StatsOut*)statsOut_, ldB_, ST, timing ? EV0 : nullptr, timing ? EV1 : nullptr),
            "stats");
   hipCheck(hipMemcpyAsync(statsHost_, statsOut_, sizeof(StatsOut), hipMemcpyDeviceToHost, ST), "D2H stats");

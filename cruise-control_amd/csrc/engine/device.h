@@ -102,6 +102,9 @@ class Device {
                      const uint8_t* rFlags, const int32_t* pBrokers, const double* pLeadNwOut,
                      const int32_t* topicCountDense /* [T][ldB] */);
   void setAllowed(int slot, const uint8_t* allowedB);
+  // Brokers sharing hosts (Model::sharedHosts): every broker's host utilization [B][3] (CPU, NW_IN, NW_OUT) and its
+  // host's capacity [B][3] (Host.capacityFor); from then on the predicates and stats read host values for those
+  void uploadHosts(const double* hutil, const double* hcap);
   // The host model's replica -> broker, replica -> partition and partition -> topic arrays (stable for the session):
   // cross / pair scans send each row with its broker, partition and topic (RowRef).
   void setRowSource(const int32_t* rBroker, const int32_t* rPart, const int32_t* pTopic) {
@@ -195,6 +198,7 @@ class Device {
   int32_t *topicCount_ = nullptr, *topicNrep_ = nullptr, *tUpper_ = nullptr, *tLower_ = nullptr;
   int32_t *pIneligOff_ = nullptr, *pIneligB_ = nullptr;
   int32_t *topicLead_ = nullptr, *tMinLead_ = nullptr, *tLeadLim_ = nullptr;
+  double* hostCap_ = nullptr;  // [B][3] Host.capacityFor of each broker's host (null: no shared hosts)
   uint8_t* allowedAlive_ = nullptr;
   std::vector<BrokerRec> hBrokers_;
   std::vector<PartitionRec> hParts_;

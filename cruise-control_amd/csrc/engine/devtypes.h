@@ -57,6 +57,9 @@ enum DevNeed : uint32_t {
   NEED_RACK = 1, NEED_POT = 2, NEED_LEAD = 4, NEED_LBI = 8, NEED_TOPIC = 16, NEED_TLEAD = 32,
   NEED_TLLIM = 64  // TopicLeaderReplicaDistributionGoal's per-topic leader limits (with NEED_TLEAD)
 };
+// Resource.isHostResource / isBrokerResource (Resource.java:18-25): CPU both, NW_IN / NW_OUT host only, DISK broker only
+constexpr bool isHostRes(int res) { return res != 3; }
+constexpr bool isBrokerRes(int res) { return res == 0 || res == 3; }
 // Candidate filters applied inside a CROSS scan before the predicate conjunction (the reference builds these
 // candidate lists per replica; the kernel skips the excluded destinations instead).
 enum DevFilter : int32_t {
@@ -119,7 +122,9 @@ struct alignas(64) BrokerRec {
   uint32_t allowedBits;   // bit g: in goal slot g's _brokersAllowedReplicaMove; bit 31: excluded for leadership
   int32_t alive;
   int32_t bset;           // broker set index (BrokerSetAwareGoal; static while a goal chain runs), -1 = none
-  int32_t pad[6];
+  // Broker.host().load().expectedUtilizationFor(CPU, NW_IN, NW_OUT) — the host resources (Resource.isHostResource).
+  // Equal to util[0..2] unless brokers share a host; read only when DevTables.hostCap is set.
+  double hutil[3];
 };
 struct alignas(64) ReplicaRec {
   double util[4];
@@ -154,6 +159,9 @@ struct DevTables {
   // TopicLeaderReplicaDistributionGoal's _balanceUpperLimitByTopic / _balanceLowerLimitByTopic as [T][2] (upper,
   // lower) pairs, one 8-byte load per row; null until the goal runs
   const int32_t* tLeadLim;
+  // Host.capacityFor(CPU, NW_IN, NW_OUT) of every broker's host [B][3] (static: -1 for a host without alive brokers);
+  // null unless brokers share a host — then every host value is the broker's own and the predicates read those
+  const double* hostCap;
   int32_t B, R, P, ldB;
 };
 
@@ -163,6 +171,7 @@ struct BrokerRow {
   double util[4];
   double potNwOut;
   double leadNwIn;
+  double hutil[3];  // BrokerRec.hutil (a host's load changes mark every broker of the host dirty)
 };
 struct ReplicaRow {
   int32_t r, broker, flags, pad;
@@ -313,6 +322,9 @@ struct StatsParams {
   double nwOutCapThreshold;
   double potSum;                 // sum of potential NW_OUT over alive allowed brokers (ClusterModelStats.java:334-340)
   int64_t repTotal, leadTotal;   // replicas / leaders over all brokers (populateReplicaStats totals)
+  // brokers share hosts: the host resources' utilization and capacity are the host's (ClusterModelStats.java:297-303):
+  // BrokerRec.hutil and this [B][3] table; null = the broker's own
+  const double* hostCap;
 };
 // stats_partials record layout: double fields [0,4) hot, [4,8) cold, [8,12) variance sums per resource, then the
 // named ones; int fields [0,4) balanced counts per resource, then the named ones.

@@ -46,6 +46,8 @@ struct HostView {
   const std::vector<int32_t>& tLim;  // TopicLeaderReplicaDistributionGoal limits [T][2] (empty: none)
   double bu(int b, int res) const { return m.bu(b, res); }
   double bcap(int b, int res) const { return m.cap(b, res); }
+  double hu(int b, int res) const { return m.hu(b, res); }
+  double hcap(int b, int res) const { return m.hcap(b, res); }
   int nrep(int b) const { return m.nrep(b); }
   bool alive(int b) const { return m.alive(b); }
   bool allowed(int slot, int b) const { return (*allowedBySlot[slot])[b] != 0; }
@@ -361,7 +363,8 @@ int64_t Engine::swapScan(GoalImpl& self, const std::vector<int32_t>& srcs, const
 
 bool Engine::chainsOn() const {
   static const bool off = std::getenv("CCMI_NO_CHAINS") != nullptr;
-  return !off && shard.count <= 1 && !terminalOptimized();  // a chain would apply the move a terminal goal refuses
+  // a chain would apply the move a terminal goal refuses; chain kernels keep no host loads (shared hosts)
+  return !off && shard.count <= 1 && !terminalOptimized() && !m.sharedHosts;
 }
 
 bool Engine::terminalOptimized() const {
@@ -1034,9 +1037,28 @@ class ResourceDistribution : public GoalImpl {
   int nameId(bool reverse, bool leader) const { return nameBase() + (reverse ? 1 : 0) + (leader ? 2 : 0); }
   bool excluded(int b) const { return !allowed[b]; }
 
-  // isLoadAboveBalanceLowerLimit / isLoadUnderBalanceUpperLimit with a null load
-  bool aboveLower(const Model& m, int b) const { return m.bu(b, res) + 0 >= m.cap(b, res) * lowerThr; }
-  bool underUpper(const Model& m, int b, double thr) const { return m.bu(b, res) - 0 <= m.cap(b, res) * thr; }
+  // isLoadAboveBalanceLowerLimit / isLoadUnderBalanceUpperLimit with a null load (:880-927): for a host resource the
+  // host or the broker within the limit
+  bool aboveLower(const Model& m, int b) const {
+    const bool broker = m.bu(b, res) + 0 >= m.cap(b, res) * lowerThr;
+    return isHostRes(res) && m.sharedHosts ? (m.hu(b, res) + 0 >= m.hcap(b, res) * lowerThr) || broker : broker;
+  }
+  bool underUpper(const Model& m, int b, double thr) const {
+    const bool broker = m.bu(b, res) - 0 <= m.cap(b, res) * thr;
+    return isHostRes(res) && m.sharedHosts ? (m.hu(b, res) - 0 <= m.hcap(b, res) * thr) || broker : broker;
+  }
+  // ClusterModel.aliveBrokersUnderThreshold / aliveBrokersOverThreshold membership (ClusterModel.java:1080-1126) of
+  // an alive broker: the broker check for a broker resource, the host check for a host resource
+  bool underThreshold(const Model& m, int x, double thr) const {
+    if (isBrokerRes(res) && m.bu(x, res) >= m.cap(x, res) * thr) return false;
+    return !(isHostRes(res) && m.hu(x, res) >= m.hcap(x, res) * thr);
+  }
+  bool overThreshold(const Model& m, int x, double thr) const {
+    if (isBrokerRes(res) && m.bu(x, res) <= m.cap(x, res) * thr) return false;
+    return !(isHostRes(res) && m.hu(x, res) <= m.hcap(x, res) * thr);
+  }
+  // host and broker decide membership differently (brokers sharing a host): no (pct, id)-prefix shortcuts
+  bool hostMembership(const Model& m) const { return m.sharedHosts && isHostRes(res); }
   int cmpBroker(const Model& m, int x, int y) const {
     const int c = jcmpDouble(m.pct(x, res), m.pct(y, res));
     return c ? c : jcmpInt(m.bId[x], m.bId[y]);
@@ -1228,8 +1250,8 @@ class ResourceDistribution : public GoalImpl {
     {
       PhaseScope pi(PH_PQ_INIT);
       const auto& ord = m.brokersByPct(res);
-      auto under = [&](int x) { return fix || m.bu(x, res) < m.cap(x, res) * upperThr; };  // aliveBrokersUnderThreshold
-      if (m.numDead == 0 && posCap && !ord.empty() && upperThr > 0) {
+      auto under = [&](int x) { return fix || underThreshold(m, x, upperThr); };  // aliveBrokersUnderThreshold
+      if (m.numDead == 0 && posCap && !ord.empty() && upperThr > 0 && !hostMembership(m)) {
         // every broker alive with a positive capacity: membership is a prefix of the (pct, id) order except within a
         // relative 1e-9 band around the threshold, where the exact product test decides each broker
         size_t lo = (size_t)(std::partition_point(ord.begin(), ord.end(),
@@ -1703,8 +1725,8 @@ class ResourceDistribution : public GoalImpl {
       // insertion order does not matter to a PriorityQueue); in = alive brokers above the lower limit
       auto member = [&](int x) {
         if (!m.alive(x)) return false;
-        if (out) return !(m.bu(x, res) >= m.cap(x, res) * upperThr) && m.nrep(x) > 0;
-        return !(m.bu(x, res) <= m.cap(x, res) * lowerThr);
+        if (out) return underThreshold(m, x, upperThr) && m.nrep(x) > 0;
+        return overThreshold(m, x, lowerThr);
       };
       // swaps change only b and the polled broker; the ordered form is exact unless b itself is queued
       const bool ordered = !member(b);

@@ -808,13 +808,23 @@ class Capacity : public GoalImpl {
     dg.allowedSlot = e.newSlot;
   }
 
-  // isUtilizationOverLimit (:410-428); the host is the broker
-  bool over(const Model& m, int b) const { return m.nrep(b) > 0 && m.bu(b, res) > m.cap(b, res) * thr; }
+  // isUtilizationOverLimit (:389-408) with rebalanceForBroker's limits, computed once per broker (:282-284)
+  struct Limits {
+    double broker, host;
+  };
+  Limits limits(const Model& m, int b) const { return {m.cap(b, res) * thr, m.hcap(b, res) * thr}; }
+  bool over(const Model& m, int b, const Limits& L) const {
+    if (!m.hostEmpty(b) && isHostRes(res) && m.hu(b, res) > L.host) return true;
+    if (m.nrep(b) > 0 && isBrokerRes(res)) return m.bu(b, res) > L.broker;
+    return false;
+  }
 
   // rebalanceForBroker (:274-349)
   void rebalance(Engine& e, int b) override {
     PhaseScope ps(PH_OTHER_GOALS);
     Model& m = e.m;
+    const Limits L = limits(m, b);
+    auto over = [&](const Model& mm, int x) { return this->over(mm, x, L); };
     bool isOver = over(m, b);
     if (!isOver && !hasOffline(m, b)) return;
     if (res == R_NW_OUT || res == R_CPU) {
@@ -850,11 +860,20 @@ class Capacity : public GoalImpl {
       }
     }
     if (isOver || hasOffline(m, b)) {
-      // sortedAliveBrokersUnderThreshold (ClusterModel.java:1049-1095): a snapshot list
+      // sortedAliveBrokersUnderThreshold (ClusterModel.java:1049-1095): a snapshot list; aliveBrokersUnderThreshold
+      // checks the broker for a broker resource and the host for a host resource, and the sort compares host
+      // utilization first for a host resource
       std::vector<int32_t> under, cands;
-      for (int x = 0; x < m.B; ++x)
-        if (m.alive(x) && !(m.bu(x, res) >= m.cap(x, res) * thr)) under.push_back(x);
-      stableSortBy(under, [&](int x, int y) { return jcmpDouble(m.bu(x, res), m.bu(y, res)); });
+      for (int x = 0; x < m.B; ++x) {
+        if (!m.alive(x)) continue;
+        if (isBrokerRes(res) && m.bu(x, res) >= m.cap(x, res) * thr) continue;
+        if (isHostRes(res) && m.hu(x, res) >= m.hcap(x, res) * thr) continue;
+        under.push_back(x);
+      }
+      stableSortBy(under, [&](int x, int y) {
+        const int hc = isHostRes(res) ? jcmpDouble(m.hu(x, res), m.hu(y, res)) : 0;
+        return hc == 0 ? jcmpDouble(m.bu(x, res), m.bu(y, res)) : hc;
+      });
       e.eligible(under, DA_MOVE, cands);
       const std::vector<int32_t> list = m.sorted(b, sortId(kind, true, false));
       size_t i = 0;
@@ -881,11 +900,13 @@ class Capacity : public GoalImpl {
   // updateGoalState (:180-190) + ensureUtilizationUnderCapacity (:192-225)
   void update(Engine& e) override {
     Model& m = e.m;
-    for (int b = 0; b < m.B; ++b)
-      if (m.nrep(b) > 0 && m.bu(b, res) > m.cap(b, res) * thr)  // one broker per host: the host check comes first
-        throw OptimizationFailure("[" + name + "] utilization for " + (res != R_DISK ? "host" : "broker") +
-                                      " is above capacity limit.",
+    for (int b = 0; b < m.B; ++b) {  // the host check first (a host resource), then the broker check (a broker resource)
+      if (isHostRes(res) && !m.hostEmpty(b) && m.hu(b, res) > m.hcap(b, res) * thr)
+        throw OptimizationFailure("[" + name + "] utilization for host is above capacity limit.", underBrokers(1, res));
+      if (isBrokerRes(res) && m.nrep(b) > 0 && m.bu(b, res) > m.cap(b, res) * thr)
+        throw OptimizationFailure("[" + name + "] utilization for broker is above capacity limit.",
                                   underBrokers(1, res));
+    }
     ensureNoOfflineReplicas(m, name);
     finished = true;
   }

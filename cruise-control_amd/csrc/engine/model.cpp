@@ -44,6 +44,44 @@ void Model::build(const ccmi_cluster_desc& d) {
     if (bId[b] != b) throw std::invalid_argument("ABI v1 requires broker_id[b] == b");
   }
   bCap.assign(d.broker_capacity, d.broker_capacity + 4 * (size_t)B);
+  // hosts: Rack._hosts.computeIfAbsent(name) with the brokers created in index order; Host.createBroker adds each
+  // broker's capacity and counts it alive (Host.java)
+  sharedHosts = false;
+  bHost.assign(B, 0);
+  {
+    std::vector<int32_t> dense(d.broker_host ? (size_t)B : 0, -1), hostRack;
+    H = 0;
+    for (int b = 0; b < B; ++b) {
+      int h;
+      if (d.broker_host) {
+        const int x = d.broker_host[b];
+        if (x < 0 || x >= B) throw std::invalid_argument("broker_host out of range");
+        if (dense[x] < 0) {
+          dense[x] = H++;
+          hostRack.push_back(bRack[b]);
+        } else {
+          if (hostRack[dense[x]] != bRack[b]) throw std::invalid_argument("brokers of one host in different racks");
+          sharedHosts = true;
+        }
+        h = dense[x];
+      } else {
+        h = H++;
+      }
+      bHost[b] = h;
+    }
+    hBrokers.assign(H, {});
+    hCap.assign((size_t)4 * H, 0.0);
+    hAlive.assign(H, 0);
+    hNrep.assign(H, 0);
+    for (int b = 0; b < B; ++b) {
+      const int h = bHost[b];
+      hBrokers[h].push_back(b);
+      hAlive[h]++;
+      for (int k = 0; k < 4; ++k) hCap[4 * (size_t)h + k] += bCap[4 * (size_t)b + k];
+    }
+    hLoad.assign(sharedHosts ? H : 0, LoadVec());
+    hUtilC.assign(sharedHosts ? (size_t)4 * H : 0, 0.0);
+  }
   bRepl.assign(B, {});
   bNlead.assign(B, 0);
   bNimm.assign(B, 0);
@@ -119,6 +157,7 @@ void Model::build(const ccmi_cluster_desc& d) {
     ops.addAll(rLoad[r], amv);
     if (rLeader[r]) ops.addAll(bLnw[b], amv);
     ops.addAll(bLoad[b], amv);
+    if (sharedHosts) ops.addAll(hLoad[bHost[b]], amv);  // Host.setReplicaLoad: _load.addMetricValues
     ops.addAll(cLoad, amv);
     if (pLeader[p] >= 0 && rBroker[pLeader[p]] == b)
       for (int x : created[p]) ops.addAll(bPot[rBroker[x]], amv);
@@ -161,6 +200,11 @@ void Model::build(const ccmi_cluster_desc& d) {
       std::vector<int32_t> order;
       bReplicaSet[b].order(order);
       for (int r : order) bOfflineSet[b].add(r, replicaHash(r));
+      {  // Host.setBrokerState: a dying broker's capacity leaves its host before Broker.setState sets it to -1
+        const int h = bHost[b];
+        for (int k = 0; k < 4; ++k) hCap[4 * (size_t)h + k] -= bCap[4 * b + k];
+        hAlive[h]--;
+      }
       for (int k = 0; k < 4; ++k) bCap[4 * b + k] = -1.0;
     }
     if (s == BState::NEW) numNew++;
@@ -191,20 +235,6 @@ void Model::build(const ccmi_cluster_desc& d) {
       if (alive(b)) c += bCap[4 * b + k];
     clusterCap[k] = c;
   }
-  sharedHosts = false;
-  if (d.broker_host) {  // Rack._hosts: a host index names one host of one rack
-    std::vector<int32_t> hostRack;
-    for (int b = 0; b < B; ++b) {
-      const int h = d.broker_host[b];
-      if (h < 0 || h >= B) throw std::invalid_argument("broker_host out of range");
-      if ((int)hostRack.size() <= h) hostRack.resize(h + 1, -1);
-      if (hostRack[h] >= 0) {
-        if (hostRack[h] != bRack[b]) throw std::invalid_argument("brokers of one host in different racks");
-        sharedHosts = true;
-      }
-      hostRack[h] = bRack[b];
-    }
-  }
   bVer.assign(B, 0);
   bDelta.assign(B, {});
   sortedCache.assign(B, {});
@@ -216,6 +246,9 @@ void Model::build(const ccmi_cluster_desc& d) {
   rUtilC.assign((size_t)4 * R, 0.0);
   rScoreC.assign((size_t)4 * R, 0.f);
   for (int b = 0; b < B; ++b) refreshBroker(b);
+  if (sharedHosts)
+    for (int h = 0; h < H; ++h)
+      for (int k = 0; k < 4; ++k) hUtilC[4 * (size_t)h + k] = ops.util(hLoad[h], k);
   for (int r = 0; r < R; ++r) refreshReplica(r);
   buildDisks(d);
   {
@@ -407,6 +440,14 @@ void Model::refreshBroker(int b) {
   }
 }
 
+void Model::refreshHost(int b) {
+  if (!sharedHosts) return;
+  const int h = bHost[b];
+  for (int k = 0; k < 4; ++k) hUtilC[4 * (size_t)h + k] = ops.util(hLoad[h], k);
+  if (dev)  // the device keeps each broker's host utilization in its record (BrokerRec.hutil)
+    for (int x : hBrokers[h]) markB(x);
+}
+
 const std::vector<int32_t>& Model::brokersByPct(int res) {
   PhaseScope ps(PH_ORDER);
   auto less = [this, res](int x, int y) { return cmpBrokerPct(res, x, y) < 0; };
@@ -489,6 +530,8 @@ void Model::brokerAdd(int b, int r) {
     bLeaderSet[b].add(r, h);
   }
   ops.addAll(bLoad[b], rLoad[r]);
+  hNrep[bHost[b]]++;  // Host.addReplica: _replicas.add, _load.addLoad(replica.load())
+  if (sharedHosts) ops.addAll(hLoad[bHost[b]], rLoad[r]);
   sortedInsert(b, r);
 }
 
@@ -505,6 +548,8 @@ int Model::brokerRemove(int b, int p) {
   bReplicaSet[b].remove(r, h);
   bOfflineSet[b].remove(r, h);
   ops.subAll(bLoad[b], rLoad[r]);
+  hNrep[bHost[b]]--;
+  if (sharedHosts) ops.subAll(hLoad[bHost[b]], rLoad[r]);  // Host.removeReplica: _load.subtractLoad(replica.load())
   if (rLeader[r]) {
     ops.subAll(bLnw[b], rLoad[r]);
     bNlead[b]--;
@@ -540,6 +585,8 @@ void Model::relocateReplica(int p, int src, int dst) {
   ops.addAll(bPot[dst], rLoad[pLeader[p]]);
   refreshBroker(src);
   refreshBroker(dst);
+  refreshHost(src);
+  refreshHost(dst);
   log.push_back({CCMI_INTER_BROKER_REPLICA_MOVEMENT, p, src, dst, -1});
   if (!topicCountDense.empty()) {
     topicCountDense[(size_t)pTopic[p] * ldB + src]--;
@@ -622,6 +669,7 @@ bool Model::relocateLeadership(int p, int src, int dst) {
   rLeader[sr] = 0;
   refreshReplica(sr);
   if (bLoad[src].mask) ops.subAll(bLoad[src], delta);
+  if (sharedHosts && hLoad[bHost[src]].mask) ops.subAll(hLoad[bHost[src]], delta);  // Host.makeFollower
   bNlead[src]--;
   bLeaderSet[src].remove(sr, replicaHash(sr));
   sortedInsert(src, sr);
@@ -632,6 +680,7 @@ bool Model::relocateLeadership(int p, int src, int dst) {
   refreshReplica(dr);
   ops.addAll(bLnw[dst], rLoad[dr]);
   if (bLoad[dst].mask) ops.addAll(bLoad[dst], delta);
+  if (sharedHosts && hLoad[bHost[dst]].mask) ops.addAll(hLoad[bHost[dst]], delta);  // Host.makeLeader
   bNlead[dst]++;
   bLeaderSet[dst].add(dr, replicaHash(dr));
   sortedInsert(dst, dr);
@@ -642,6 +691,8 @@ bool Model::relocateLeadership(int p, int src, int dst) {
   pLeader[p] = dr;
   refreshBroker(src);
   refreshBroker(dst);
+  refreshHost(src);
+  refreshHost(dst);
   log.push_back({CCMI_LEADERSHIP_MOVEMENT, p, src, dst, -1});
   if (!topicLeadDense.empty()) {
     topicLeadDense[(size_t)pTopic[p] * ldB + src]--;
@@ -677,6 +728,7 @@ void Model::flushToDevice() {
     for (int k = 0; k < 4; ++k) row.util[k] = bUtilC[4 * b + k];
     row.potNwOut = potNwOut(b);
     row.leadNwIn = leadNwIn(b);
+    for (int k = 0; k < 3; ++k) row.hutil[k] = hu(b, k);
     dev->brows.push_back(row);
     bDirty[b] = 0;
   }

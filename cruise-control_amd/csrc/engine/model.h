@@ -160,8 +160,24 @@ class Model {
   std::vector<uint8_t> selfHealing;         // per replica: in _selfHealingEligibleReplicas
   int64_t numSelfHealing = 0;
   int numDead = 0, numNew = 0, numBadDisk = 0;
-  // hosts (ccmi.h broker_host): true when some host holds two or more brokers (host-level capacity not modelled)
+  // hosts (ccmi.h broker_host; Rack._hosts, model/Host.java). sharedHosts: some host holds two or more brokers. Only
+  // then is host state kept: the load of its brokers' replicas with every add / subtract in the reference's order,
+  // the capacity of its alive brokers (Host.capacityFor: -1 without one) and its replica count. Otherwise every host
+  // value is its broker's own, bit for bit.
   bool sharedHosts = false;
+  int H = 0;
+  std::vector<int32_t> bHost;                  // [B] dense host index
+  std::vector<std::vector<int32_t>> hBrokers;  // [H] brokers of each host
+  std::vector<LoadVec> hLoad;                  // [H] Host._load
+  std::vector<double> hCap, hUtilC;            // [H][4] Host._hostCapacity, cached expectedUtilizationFor
+  std::vector<int32_t> hAlive, hNrep;          // [H] Host._aliveBrokers, Host._replicas.size()
+  double hu(int b, int res) const { return sharedHosts ? hUtilC[4 * (size_t)bHost[b] + res] : bu(b, res); }
+  double hcap(int b, int res) const {
+    if (!sharedHosts) return cap(b, res);
+    const int h = bHost[b];
+    return hAlive[h] > 0 ? hCap[4 * (size_t)h + res] : -1.0;
+  }
+  bool hostEmpty(int b) const { return sharedHosts ? hNrep[bHost[b]] == 0 : nrep(b) == 0; }
   // Partition._ineligibleBrokers: a BAD_DISKS broker holding an offline replica of the partition may not receive
   // one of its replicas (ClusterModel.setBrokerState :325-331); CSR over partitions, static
   std::vector<int32_t> pIneligOff, pIneligB;
@@ -367,6 +383,7 @@ class Model {
   void brokerAdd(int b, int r);
   int brokerRemove(int b, int p);
   void refreshBroker(int b);
+  void refreshHost(int b);  // the host of broker b: cached utilization, and every broker of it dirty (BrokerRow.hutil)
   std::vector<int32_t> ordPct_[4], ordDirtyList_[4], ordScratch_;
   std::vector<uint8_t> ordDirty_[4];
   bool ordBuilt_[4] = {false, false, false, false};

@@ -18,8 +18,9 @@
 //   LeaderReplicaDistributionGoal                 LeaderReplicaDistributionGoal.java:91-123
 //   LeaderBytesInDistributionGoal                 LeaderBytesInDistributionGoal.java:69-127,264-271
 //   TopicLeaderReplicaDistributionGoal            TopicLeaderReplicaDistributionGoal.java:181-256,359-374
-// One broker per host (RandomCluster names hosts after brokers), so the host-resource branch equals the
-// broker branch bit for bit and is folded into it.
+// Host resources (CPU, NW_IN, NW_OUT; Resource.java:18-25) are checked against the broker's host as the reference
+// does (V::hu / V::hcap: Broker.host().load() / Host.capacityFor); when every host holds one broker those equal the
+// broker's own values bit for bit.
 #pragma once
 #include <stdint.h>
 
@@ -34,7 +35,7 @@
 
 namespace ccmi {
 
-// V must provide: bu(b,res) bcap(b,res) nrep(b) alive(b) allowed(slot,b) ru(r,res) flags(r) rbroker(r)
+// V must provide: bu(b,res) bcap(b,res) hu(b,res) hcap(b,res) nrep(b) alive(b) allowed(slot,b) ru(r,res) flags(r) rbroker(r)
 // rorig(r) origOff(r) rpart(r) hosts(p,b), and for the goals that read them: rack(b) otherOnRack(p,self,rack)
 // slotRack(p,b) (rack of partition p's replica on b) rackCount(p,rack) nlead(b)
 // pot(b) lnwin(b) pLeadNwOut(p) ptopic(p) tcount(t,b) tUpper(t) tLower(t) bset(b) rbset(r) (broker sets)
@@ -73,17 +74,31 @@ CCMI_HD bool rdAccept(const DevGoal& g, const V& v, int action, int src, int dst
 }
 
 // ---------------------------------------------------------------- ResourceDistributionGoal
+// isLoadAboveBalanceLowerLimitAfterChange / isLoadUnderBalanceUpperLimitAfterChange (:880-927): a host resource is
+// within the limit when the host or the broker is
 template <class V>
 CCMI_HD bool resAboveLowerAfter(const DevGoal& g, const V& v, int b, double delta, bool add) {
-  const double lim = v.bcap(b, g.resource) * g.lowerThr;
-  const double u = v.bu(b, g.resource);
-  return add ? (u + delta >= lim) : (u - delta >= lim);
+  const int res = g.resource;
+  const double lim = v.bcap(b, res) * g.lowerThr;
+  const double u = v.bu(b, res);
+  const bool brokerAbove = add ? (u + delta >= lim) : (u - delta >= lim);
+  if (!isHostRes(res)) return brokerAbove;
+  const double hlim = v.hcap(b, res) * g.lowerThr;
+  const double hu = v.hu(b, res);
+  const bool hostAbove = add ? (hu + delta >= hlim) : (hu - delta >= hlim);
+  return hostAbove || brokerAbove;
 }
 template <class V>
 CCMI_HD bool resUnderUpperAfter(const DevGoal& g, const V& v, int b, double delta, bool add, double thr) {
-  const double lim = v.bcap(b, g.resource) * thr;
-  const double u = v.bu(b, g.resource);
-  return add ? (u + delta <= lim) : (u - delta <= lim);
+  const int res = g.resource;
+  const double lim = v.bcap(b, res) * thr;
+  const double u = v.bu(b, res);
+  const bool brokerUnder = add ? (u + delta <= lim) : (u - delta <= lim);
+  if (!isHostRes(res)) return brokerUnder;
+  const double hlim = v.hcap(b, res) * thr;
+  const double hu = v.hu(b, res);
+  const bool hostUnder = add ? (hu + delta <= hlim) : (hu - delta <= hlim);
+  return hostUnder || brokerUnder;
 }
 template <class V>
 CCMI_HD bool resGettingMoreBalanced(const DevGoal& g, const V& v, int sb, double delta, int db) {
@@ -93,19 +108,27 @@ CCMI_HD bool resGettingMoreBalanced(const DevGoal& g, const V& v, int sb, double
   const double nextDiff = prevDiff + (delta / sc) + (delta / dc);
   return __builtin_fabs(nextDiff) < __builtin_fabs(prevDiff);
 }
-// isSwapViolatingContainerLimit for the broker container (host container identical)
+// isSwapViolatingContainerLimit (:1005-1037) for the broker container, or with `host` the brokers' hosts
 template <class V>
-CCMI_HD bool resSwapViolating(const DevGoal& g, const V& v, double delta, int sb, int db) {
+CCMI_HD bool resSwapContainerViolating(const DevGoal& g, const V& v, double delta, int sb, int db, bool host) {
   const int res = g.resource;
-  const double su = v.bu(sb, res), du = v.bu(db, res);
+  const double su = host ? v.hu(sb, res) : v.bu(sb, res), du = host ? v.hu(db, res) : v.bu(db, res);
+  const double sc = host ? v.hcap(sb, res) : v.bcap(sb, res), dc = host ? v.hcap(db, res) : v.bcap(db, res);
   bool underUpper;
-  if (delta > 0) underUpper = su + delta <= v.bcap(sb, res) * g.upperThr;
-  else underUpper = du - delta <= v.bcap(db, res) * g.upperThr;
+  if (delta > 0) underUpper = su + delta <= sc * g.upperThr;
+  else underUpper = du - delta <= dc * g.upperThr;
   if (!underUpper) return true;
   bool aboveLower;
-  if (delta < 0) aboveLower = su + delta >= v.bcap(sb, res) * g.lowerThr;
-  else aboveLower = du - delta >= v.bcap(db, res) * g.lowerThr;
+  if (delta < 0) aboveLower = su + delta >= sc * g.lowerThr;
+  else aboveLower = du - delta >= dc * g.lowerThr;
   return !aboveLower;
+}
+// isSwapViolatingLimit (:982-1003): the broker check, then for a host resource the host check
+template <class V>
+CCMI_HD bool resSwapViolating(const DevGoal& g, const V& v, double delta, int sb, int db) {
+  const bool broker = resSwapContainerViolating(g, v, delta, sb, db, false);
+  if (!broker || !isHostRes(g.resource)) return broker;
+  return resSwapContainerViolating(g, v, delta, sb, db, true);
 }
 
 template <class V>
@@ -203,10 +226,14 @@ CCMI_HD int minLeadAcceptSwap(const V& v, int sr, int sb, int dr, int db) {
 }
 
 // ---------------------------------------------------------------- CapacityGoal
-// isUtilizationUnderLimitAfterAddingLoad (host == broker: the host check is the broker check negated)
+// isUtilizationUnderLimitAfterAddingLoad (CapacityGoal.java:455-475): the host check for a host resource, the broker
+// check for a broker resource
 template <class V>
 CCMI_HD bool capUnderAfterAdding(const DevGoal& g, const V& v, int b, double u) {
-  return v.bu(b, g.resource) + u < v.bcap(b, g.resource) * g.capThr;
+  const int res = g.resource;
+  if (isHostRes(res) && v.hu(b, res) + u >= v.hcap(b, res) * g.capThr) return false;
+  if (isBrokerRes(res)) return v.bu(b, res) + u < v.bcap(b, res) * g.capThr;
+  return true;
 }
 
 // ---------------------------------------------------------------- PotentialNwOutGoal

@@ -33,6 +33,10 @@ struct DevView {
   DevTables t;
   __device__ __forceinline__ double bu(int b, int res) const { return t.brokers[b].util[res]; }
   __device__ __forceinline__ double bcap(int b, int res) const { return t.brokers[b].cap[res]; }
+  __device__ __forceinline__ double hu(int b, int res) const { return t.hostCap ? t.brokers[b].hutil[res] : bu(b, res); }
+  __device__ __forceinline__ double hcap(int b, int res) const {
+    return t.hostCap ? t.hostCap[3 * (size_t)b + res] : bcap(b, res);
+  }
   __device__ __forceinline__ int nrep(int b) const { return t.brokers[b].nrep; }
   __device__ __forceinline__ bool alive(int b) const { return t.brokers[b].alive != 0; }
   __device__ __forceinline__ bool allowed(int slot, int b) const { return (t.brokers[b].allowedBits >> slot) & 1u; }
@@ -136,6 +140,8 @@ __device__ __forceinline__ void applyRowsBlock(const MutTables& M, const BrokerR
     d.pot = x.potNwOut;
     d.lbi = x.leadNwIn;
     d.alive = x.alive;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) d.hutil[k] = x.hutil[k];
   }
   for (int i = first; i < nr; i += stride) {
     const ReplicaRow& x = rrows[i];
@@ -184,6 +190,8 @@ __device__ __forceinline__ void applyRowsCoherent(const MutTables& M, const Brok
     stDev(&d.pot, x.potNwOut);
     stDev(&d.lbi, x.leadNwIn);
     stDev(&d.alive, x.alive);
+#pragma unroll
+    for (int k = 0; k < 3; ++k) stDev(&d.hutil[k], x.hutil[k]);
   }
   for (int i = first; i < nr; i += stride) {
     const ReplicaRow& x = rrows[i];
@@ -259,6 +267,9 @@ struct PreView {
   int stl, dtl, tmn;  // leaders of the row's topic on the source / destination, MinTopicLeaders' minimum of it
   int tlu, tll;       // TopicLeaderReplicaDistributionGoal's leader limits of the row's topic
   bool inelig;  // dst is one of the row's partition's ineligible brokers
+  // host resources of the source's / destination's hosts (only when brokers share hosts: DevTables.hostCap set)
+  bool hmode;
+  double shu0, shu1, shu2, dhu0, dhu1, dhu2, shc0, shc1, shc2, dhc0, dhc1, dhc2;
 
   static __device__ __forceinline__ double sel(int k, double a, double b, double c, double d) {
     return k == 0 ? a : (k == 1 ? b : (k == 2 ? c : d));
@@ -325,6 +336,7 @@ struct PreView {
     scap3 = sb.cap[3];
     srcAllowed = sb.allowedBits;
     sbs = sb.bset;
+    loadSrcHost(t, sb, ov);
     const int pi = ov.partition(p);
     if (pi >= 0) {
       const PartitionRow& x = ov.p[pi];
@@ -422,6 +434,7 @@ struct PreView {
     scap3 = sb.cap[3];
     srcAllowed = sb.allowedBits;
     sbs = sb.bset;
+    loadSrcHost(t, sb, ov);
     if (prog.needs & NEED_TOPIC) {
       tup = t.tUpper[topic];
       tlo = t.tLower[topic];
@@ -478,6 +491,23 @@ struct PreView {
     }
     aliveBits = (aliveBits & 4u) | (aSrc ? 1u : 0u);
   }
+  // The source broker's host values (src is set; a dirty source row in the overlay wins)
+  __device__ __forceinline__ void loadSrcHost(const DevTables& t, const BrokerRec& sb, const OverlayLds& ov) {
+    hmode = t.hostCap != nullptr;
+    if (!hmode) return;  // uniform per launch
+    shu0 = sb.hutil[0];
+    shu1 = sb.hutil[1];
+    shu2 = sb.hutil[2];
+    shc0 = t.hostCap[3 * (size_t)src];
+    shc1 = t.hostCap[3 * (size_t)src + 1];
+    shc2 = t.hostCap[3 * (size_t)src + 2];
+    const int si = ov.broker(src);
+    if (si >= 0) {
+      shu0 = ov.b[si].hutil[0];
+      shu1 = ov.b[si].hutil[1];
+      shu2 = ov.b[si].hutil[2];
+    }
+  }
   // The destination side, loaded BEFORE the row (it depends only on the destination id); the destination's
   // topic count needs the row's topic and is read in loadRow.
   __device__ __forceinline__ void loadDst(const DevTables& t, int d, const OverlayLds& ov) {
@@ -513,12 +543,29 @@ struct PreView {
       dlbi = x.leadNwIn;
     }
     aliveBits = aDst ? 4u : 0u;
+    hmode = t.hostCap != nullptr;
+    if (hmode) {  // uniform per launch
+      dhu0 = di >= 0 ? ov.b[di].hutil[0] : db.hutil[0];
+      dhu1 = di >= 0 ? ov.b[di].hutil[1] : db.hutil[1];
+      dhu2 = di >= 0 ? ov.b[di].hutil[2] : db.hutil[2];
+      dhc0 = t.hostCap[3 * (size_t)d];
+      dhc1 = t.hostCap[3 * (size_t)d + 1];
+      dhc2 = t.hostCap[3 * (size_t)d + 2];
+    }
   }
   __device__ __forceinline__ double bu(int b, int k) const {
     return b == dst ? sel(k, dbu0, dbu1, dbu2, dbu3) : sel(k, sbu0, sbu1, sbu2, sbu3);
   }
   __device__ __forceinline__ double bcap(int b, int k) const {
     return b == dst ? sel(k, dcap0, dcap1, dcap2, dcap3) : sel(k, scap0, scap1, scap2, scap3);
+  }
+  __device__ __forceinline__ double hu(int b, int k) const {  // k < 3 (host resources)
+    if (!hmode) return bu(b, k);
+    return b == dst ? sel(k, dhu0, dhu1, dhu2, dhu2) : sel(k, shu0, shu1, shu2, shu2);
+  }
+  __device__ __forceinline__ double hcap(int b, int k) const {
+    if (!hmode) return bcap(b, k);
+    return b == dst ? sel(k, dhc0, dhc1, dhc2, dhc2) : sel(k, shc0, shc1, shc2, shc2);
   }
   __device__ __forceinline__ int nrep(int b) const { return b == dst ? dnrep : snrep; }
   // asked for src and dst only (the original broker's liveness is folded into origOff)

@@ -145,13 +145,15 @@ __global__ __launch_bounds__(kTB) void stats_partials(StatsParams P, const Broke
     iv[kSiLeadMx] = max(iv[kSiLeadMx], x.nlead);
     iv[kSiLeadMn] = min(iv[kSiLeadMn], x.nlead);
     if (!x.alive) continue;
+    // host resources are the host's when brokers share hosts (ClusterModelStats.java:297-303)
+    const bool hostVals = P.hostCap != nullptr;
 #pragma unroll
     for (int res = 0; res < 4; ++res) {
-      const double u = x.util[res];
+      const double u = hostVals && res < 3 ? x.hutil[res] : x.util[res];
       d[res] = u > d[res] ? u : d[res];
       d[4 + res] = u < d[4 + res] ? u : d[4 + res];
       if (allowed) {
-        const double cap = x.cap[res];
+        const double cap = hostVals && res < 3 ? P.hostCap[3 * (size_t)b + res] : x.cap[res];
         const double pct = u / cap;
         if (pct >= P.lowerThr[res] && pct <= P.upperThr[res]) iv[res]++;
         const double dv = u - P.avgPct[res] * cap;

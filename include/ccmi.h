@@ -178,13 +178,16 @@ typedef struct ccmi_cluster_desc {
    * ClusterModel.setReplicaLoad: its Load stays empty (model/Load.java isEmpty), as in hand-built fixtures such as
    * DeterministicCluster.minLeaderReplicaPerBrokerSatisfiable (DeterministicCluster.java:321-361). */
   int32_t num_replica_loads;
-  /* ABI v6: the host of every broker ([B] host index, or NULL = each broker on a host of its own). Hosts belong to
-   * a rack and are keyed by name within it (Rack._hosts.computeIfAbsent, model/Rack.java:256-262; LoadMonitor passes
-   * node.host(), LoadMonitor.java:602), so brokers sharing an index must share a rack. Host-level capacity
-   * (Resource.isHostResource: CPU, NW_IN, NW_OUT; CapacityGoal.java:230-239,395-399,457-466 and
-   * ResourceDistributionGoal.java:890-923) equals the broker's when the host has one broker, which is what this
-   * build evaluates: a chain with a CPU / NW_IN / NW_OUT capacity or usage-distribution goal on a model where two
-   * brokers share a host fails with CCMI_E_UNSUPPORTED instead of diverging from the reference. */
+  /* ABI v6: the host of every broker ([B] host index in [0, B), or NULL = each broker on a host of its own). Hosts
+   * belong to a rack and are keyed by name within it (Rack._hosts.computeIfAbsent, model/Rack.java:256-262;
+   * LoadMonitor passes node.host(), LoadMonitor.java:602), so brokers sharing an index must share a rack. ABI v8: a
+   * host keeps the reference's aggregates (model/Host.java): the load of its brokers' replicas, updated with every
+   * replica and leadership move in the reference's order; its capacity, the sum of its brokers' capacities in broker
+   * index order minus those of dead brokers (Host.capacityFor: -1 without an alive broker); its replica count. The
+   * host resources (Resource.isHostResource: CPU, NW_IN, NW_OUT) are checked against them where the reference does:
+   * CapacityGoal.java:230-239,284-366,389-408,455-475, ResourceDistributionGoal.java:880-927,982-1037,
+   * ClusterModel.aliveBrokers{Under,Over}Threshold / sortedAliveBrokersUnderThreshold (:1049-1126) and
+   * ClusterModelStats.java:297-303. */
   const int32_t* broker_host;
   /* ABI v6: [D] 1 = the disk is Disk.State.DEMOTED (DemoteBrokerRunnable.java:144-148), or NULL. Only
    * PreferredLeaderElectionGoal reads it (PreferredLeaderElectionGoal.java:114-124). */

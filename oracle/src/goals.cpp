@@ -491,20 +491,23 @@ bool ResourceDistributionGoal::isGettingMoreBalanced(ClusterModel& cm, int sb, d
 // :982-1037
 bool ResourceDistributionGoal::isSwapViolatingLimit(ClusterModel& cm, int sr, int dr) {
   double delta = cm.replicaUtil(dr, resource_) - cm.replicaUtil(sr, resource_);
-  bool v = isSwapViolatingContainerLimit(cm, delta, sr, dr);
+  bool v = isSwapViolatingContainerLimit(cm, delta, sr, dr, false);
   if (!v || !isHostResource(resource_)) return v;
-  return isSwapViolatingContainerLimit(cm, delta, sr, dr);  // host == broker
+  return isSwapViolatingContainerLimit(cm, delta, sr, dr, true);
 }
-bool ResourceDistributionGoal::isSwapViolatingContainerLimit(ClusterModel& cm, double delta, int sr, int dr) {
+// the container is the broker, or with `host` the broker's host (r -> r.broker().host().load() / capacityFor)
+bool ResourceDistributionGoal::isSwapViolatingContainerLimit(ClusterModel& cm, double delta, int sr, int dr, bool host) {
   int sb = cm.replicas[sr].broker, db = cm.replicas[dr].broker;
-  double su = cm.brokerUtil(sb, resource_), du = cm.brokerUtil(db, resource_);
+  auto util = [&](int b) { return host ? cm.hostUtil(b, resource_) : cm.brokerUtil(b, resource_); };
+  auto cap = [&](int b) { return host ? cm.hostCapacity(b, resource_) : cm.brokers[b].capacity[resource_]; };
+  double su = util(sb), du = util(db);
   bool underUpper;
-  if (delta > 0) underUpper = su + delta <= cm.brokers[sb].capacity[resource_] * upperThr_;
-  else underUpper = du - delta <= cm.brokers[db].capacity[resource_] * upperThr_;
+  if (delta > 0) underUpper = su + delta <= cap(sb) * upperThr_;
+  else underUpper = du - delta <= cap(db) * upperThr_;
   if (!underUpper) return true;
   bool aboveLower;
-  if (delta < 0) aboveLower = su + delta >= cm.brokers[sb].capacity[resource_] * lowerThr_;
-  else aboveLower = du - delta >= cm.brokers[db].capacity[resource_] * lowerThr_;
+  if (delta < 0) aboveLower = su + delta >= cap(sb) * lowerThr_;
+  else aboveLower = du - delta >= cap(db) * lowerThr_;
   return !aboveLower;
 }
 

@@ -191,7 +191,7 @@ class ResourceDistributionGoal : public AbstractGoal {
   bool isSelfSatisfiedAfterSwap(ClusterModel& cm, int srcReplica, int destReplica);
   bool isGettingMoreBalanced(ClusterModel& cm, int srcBroker, double delta, int destBroker);
   bool isSwapViolatingLimit(ClusterModel& cm, int srcReplica, int destReplica);
-  bool isSwapViolatingContainerLimit(ClusterModel& cm, double delta, int srcReplica, int destReplica);
+  bool isSwapViolatingContainerLimit(ClusterModel& cm, double delta, int srcReplica, int destReplica, bool host);
   int cmpBroker(ClusterModel& cm, int a, int b) const {
     int c = dcompare(cm.utilizationPct(a, resource_), cm.utilizationPct(b, resource_));
     return c != 0 ? c : icompare(cm.brokers[a].id, cm.brokers[b].id);

@@ -771,7 +771,8 @@ void CapacityGoal::updateGoalState(ClusterModel& cm, const OptimizationOptions&)
   const double thr = bc_.capacityThreshold[resource_];
   for (size_t b = 0; b < cm.brokers.size(); ++b) {
     const bool hasReplicas = !cm.brokers[b].replicas.empty();
-    if (isHostResource(resource_) && hasReplicas && cm.hostUtil((int)b, resource_) > cm.hostCapacity((int)b, resource_) * thr)
+    if (isHostResource(resource_) && !cm.hostReplicasEmpty((int)b) &&
+        cm.hostUtil((int)b, resource_) > cm.hostCapacity((int)b, resource_) * thr)
       throw OptimizationFailure("[" + name() + "] utilization for host is above capacity limit.", underBrokers(1, resource_));
     if (isBrokerResource(resource_) && hasReplicas &&
         cm.brokerUtil((int)b, resource_) > cm.brokers[b].capacity[resource_] * thr)
@@ -785,7 +786,7 @@ void CapacityGoal::updateGoalState(ClusterModel& cm, const OptimizationOptions&)
 // CapacityGoal.isUtilizationOverLimit (:410-428)
 bool CapacityGoal::utilizationOverLimit(ClusterModel& cm, int b, double brokerLimit, double hostLimit) const {
   const bool hasReplicas = !cm.brokers[b].replicas.empty();
-  if (hasReplicas && isHostResource(resource_) && cm.hostUtil(b, resource_) > hostLimit) return true;
+  if (!cm.hostReplicasEmpty(b) && isHostResource(resource_) && cm.hostUtil(b, resource_) > hostLimit) return true;
   if (hasReplicas && isBrokerResource(resource_)) return cm.brokerUtil(b, resource_) > brokerLimit;
   return false;
 }

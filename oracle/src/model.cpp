@@ -189,8 +189,17 @@ int ClusterModel::createRack(const std::string& id) {
   racks.push_back({id, {}});
   return (int)racks.size() - 1;
 }
-int ClusterModel::createBroker(int rackIdx, int brokerId, const double cap[NUM_RESOURCES]) {
+int ClusterModel::createBroker(int rackIdx, int brokerId, const double cap[NUM_RESOURCES], int host) {
   if (brokerId != (int)brokers.size()) throw std::runtime_error("oracle requires dense broker ids 0..B-1");
+  // Rack.createBroker -> Rack._hosts.computeIfAbsent(hostName) -> Host.createBroker (Host.java: _aliveBrokers++,
+  // _hostCapacity += the broker's capacity)
+  if (host < 0) host = (int)hosts.size();
+  if ((int)hosts.size() <= host) hosts.resize(host + 1);
+  Host& h = hosts[host];
+  h.brokers.push_back(brokerId);
+  h.aliveBrokers++;
+  for (int r = 0; r < NUM_RESOURCES; ++r) h.capacity[r] += cap[r];
+  brokerHost.push_back(host);
   Broker b;
   b.id = brokerId;
   b.rack = rackIdx;
@@ -270,7 +279,7 @@ void ClusterModel::setReplicaLoad(int r, const Load& amv) {
   amvAdd(rep.load, amv, W);  // Load.initializeMetricValues
   if (rep.isLeader) amvAdd(brokers[b].leadershipLoadForNwResources, amv, W);
   amvAdd(brokers[b].load, amv, W);
-  // (host and rack loads receive identical operations; host == broker here, rack load unused)
+  amvAdd(hosts[brokerHost[b]].load, amv, W);  // Host.setReplicaLoad: _load.addMetricValues (rack load unused)
   amvAdd(load, amv, W);  // cluster
   if (rep.disk >= 0) disks[rep.disk].utilization += replicaUtil(r, DISK);  // Disk.addReplicaLoad
   const Partition& part = partitions[rep.partition];
@@ -290,6 +299,16 @@ void ClusterModel::refreshCapacity() {
 
 void ClusterModel::setBrokerState(int b, BrokerState s) {
   Broker& br = brokers[b];
+  {  // Host.setBrokerState: the capacity of a broker that dies leaves the host's, before Broker.setState
+    Host& h = hosts[brokerHost[b]];
+    if (br.isAlive() && s == BrokerState::DEAD) {
+      for (int k = 0; k < NUM_RESOURCES; ++k) h.capacity[k] -= br.capacity[k];
+      h.aliveBrokers--;
+    } else if (!br.isAlive() && s != BrokerState::DEAD) {
+      for (int k = 0; k < NUM_RESOURCES; ++k) h.capacity[k] += br.capacity[k];
+      h.aliveBrokers++;
+    }
+  }
   br.state = s;
   if (!br.isAlive()) {  // Broker.setState: _currentOfflineReplicas.addAll(replicas())
     for (int r : br.replicaSet.order()) br.offlineSet.add(r, replicaHash(r));
@@ -433,6 +452,11 @@ void ClusterModel::brokerAddReplica(int b, int r) {
     br.leaderSet.add(r, replicaHash(r));
   }
   loadAddLoad(br.load, rep.load, W);
+  {  // Host.addReplica: _replicas.add, _load.addLoad(replica.load())
+    Host& h = hosts[brokerHost[b]];
+    h.numReplicas++;
+    loadAddLoad(h.load, rep.load, W);
+  }
   sortedAdd(b, r);
   if (rep.disk >= 0) {  // _diskByLogdir.get(replica.disk().logDir()).addReplica(replica)
     const int dd = diskOf(b, disks[rep.disk].logdir);
@@ -457,6 +481,11 @@ int ClusterModel::brokerRemoveReplica(int b, int partition) {
   br.replicaSet.remove(r, replicaHash(r));
   br.offlineSet.remove(r, replicaHash(r));
   loadSubLoad(br.load, rep.load, W);
+  {  // Host.removeReplica: _replicas.remove, _load.subtractLoad(replica.load())
+    Host& h = hosts[brokerHost[b]];
+    h.numReplicas--;
+    loadSubLoad(h.load, rep.load, W);
+  }
   br.topicReplicaCount[partitions[partition].topic] -= 1;
   if (rep.isLeader) {
     br.topicLeaderCount[partitions[partition].topic] -= 1;
@@ -519,6 +548,7 @@ Load ClusterModel::brokerMakeFollower(int b, int partition) {
   Load delta = replicaMakeFollower(r);
   br.topicLeaderCount[partitions[partition].topic] -= 1;
   loadSubDelta(br.load, delta, W);
+  loadSubDelta(hosts[brokerHost[b]].load, delta, W);  // Host.makeFollower: _load.subtractLoad(leadershipLoadDelta)
   if (replicas[r].inBrokerLeaders) {
     replicas[r].inBrokerLeaders = false;
     br.numLeaders--;
@@ -537,6 +567,7 @@ void ClusterModel::brokerMakeLeader(int b, int partition, const Load& delta) {
   loadAddDelta(replicas[r].load, delta, W);
   loadAddLoad(br.leadershipLoadForNwResources, replicas[r].load, W);
   loadAddDelta(br.load, delta, W);
+  loadAddDelta(hosts[brokerHost[b]].load, delta, W);  // Host.makeLeader: _load.addLoad(leadershipLoadDelta)
   if (!replicas[r].inBrokerLeaders) {
     replicas[r].inBrokerLeaders = true;
     br.numLeaders++;
@@ -662,6 +693,7 @@ void ClusterModel::markReplicaOriginalOffline(int r) {
 }
 void ClusterModel::markDiskDead(int b, int d) {
   Broker& br = brokers[b];
+  hosts[brokerHost[b]].capacity[DISK] -= disks[d].capacity;  // Host.markDiskDead
   br.capacity[DISK] -= disks[d].capacity;
   disks[d].alive = false;
   disks[d].capacity = -1.0;

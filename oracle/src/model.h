@@ -11,8 +11,9 @@
 //   SortedReplicas(+Helper, ReplicaSortFunctionFactory)  .../model/SortedReplicas.java,
 //                       SortedReplicasHelper.java, ReplicaSortFunctionFactory.java
 //   Disk                .../model/Disk.java (JBOD: Broker._diskByLogdir TreeMap, Broker.java:56,80-83,336-366,519-543)
-// Modelling assumption (asserted): one broker per host (RandomCluster names each host after its
-// broker, RandomCluster.java:80,87), so Host load/capacity are bit-identical to the broker's.
+//   Host                .../model/Host.java (load, capacity of the alive brokers, replica set; Rack._hosts keyed by
+//                       name within a rack, Rack.java:256-262)
+// RandomCluster names every host after its broker (RandomCluster.java:80,87); a desc's broker_host shares hosts.
 #pragma once
 #include <cstdint>
 #include <map>
@@ -239,6 +240,14 @@ struct Rack {
   std::vector<int> brokers;
 };
 
+struct Host {  // model/Host.java
+  std::vector<int> brokers;
+  Load load;                               // Host._load: every add/subtract of its brokers' replica loads
+  double capacity[NUM_RESOURCES] = {0, 0, 0, 0};  // Host._hostCapacity
+  int aliveBrokers = 0;
+  int numReplicas = 0;                     // Host._replicas.size()
+};
+
 struct BalancingAction {
   int partition;         // tp
   int sourceBroker;      // broker index
@@ -272,6 +281,8 @@ class ClusterModel {
   int W = 1;
   std::vector<Broker> brokers;  // index == broker id
   std::vector<Rack> racks;
+  std::vector<Host> hosts;
+  std::vector<int> brokerHost;  // Broker.host()
   std::vector<std::string> topicNames;
   std::vector<int32_t> topicHash;  // String.hashCode of each topic name
   std::vector<int> topicRank;  // rank of topic name in String.compareTo order
@@ -303,7 +314,8 @@ class ClusterModel {
 
   // --- construction (ClusterModel.createRack/createBroker/createReplica/setReplicaLoad)
   int createRack(const std::string& id);
-  int createBroker(int rackIdx, int brokerId, const double cap[NUM_RESOURCES]);
+  // host < 0: a host of its own (RandomCluster: host named after the broker)
+  int createBroker(int rackIdx, int brokerId, const double cap[NUM_RESOURCES], int host = -1);
   int ensureTopic(const std::string& name);
   int createPartition(int topic, int number);
   int createReplica(int brokerIdx, int partition, int index, bool isLeader, bool isOffline, int disk = -1);
@@ -344,8 +356,14 @@ class ClusterModel {
   bool isImmigrant(int r) const { return replicas[r].origBroker != replicas[r].broker; }
   double replicaUtil(int r, int res) const { return expectedUtil(replicas[r].load, res, W); }
   double brokerUtil(int b, int res) const { return expectedUtil(brokers[b].load, res, W); }
-  double hostUtil(int b, int res) const { return brokerUtil(b, res); }
-  double hostCapacity(int b, int res) const { return brokers[b].capacity[res]; }
+  // Broker.host().load().expectedUtilizationFor / Host.capacityFor (Host.java: -1 without alive brokers) /
+  // Host.replicas().isEmpty()
+  double hostUtil(int b, int res) const { return expectedUtil(hosts[brokerHost[b]].load, res, W); }
+  double hostCapacity(int b, int res) const {
+    const Host& h = hosts[brokerHost[b]];
+    return h.aliveBrokers > 0 ? h.capacity[res] : -1.0;
+  }
+  bool hostReplicasEmpty(int b) const { return hosts[brokerHost[b]].numReplicas == 0; }
   // GoalUtils.utilization
   double utilizationPct(int b, int res) const {
     double c = brokers[b].capacity[res];

@@ -173,7 +173,10 @@ void* oc_from_desc(const ccmi_cluster_desc* d) {
   try {
     cm.W = d->num_windows;
     for (int i = 0; i < d->num_racks; ++i) cm.createRack(std::to_string(i));
-    for (int b = 0; b < d->num_brokers; ++b) cm.createBroker(d->broker_rack[b], d->broker_id[b], &d->broker_capacity[4 * b]);
+    // broker_host: dense host indices (Rack._hosts by name); NULL = a host per broker
+    for (int b = 0; b < d->num_brokers; ++b)
+      cm.createBroker(d->broker_rack[b], d->broker_id[b], &d->broker_capacity[4 * b],
+                      d->broker_host ? d->broker_host[b] : -1);
     for (int t = 0; t < d->num_topics; ++t) {
       cm.topicNames.push_back(d->topic_names[t]);
       cm.topicHash.push_back(jStringHash(cm.topicNames.back()));
@@ -539,6 +542,8 @@ void oc_proposal_disks(void* hv, int max_rf, int32_t* old_out, int32_t* new_out)
 }
 // Replica utilization of broker b / resource (for host-side checks in tests).
 double oc_broker_util(void* hv, int b, int res) { return ((Handle*)hv)->cm.brokerUtil(b, res); }
+// Utilization of broker b's host (Broker.host().load().expectedUtilizationFor)
+double oc_host_util(void* hv, int b, int res) { return ((Handle*)hv)->cm.hostUtil(b, res); }
 // Exact RB-tree / PQ / Random probes for the known-answer tests.
 int64_t oc_java_random_probe(int64_t seed, int bound, int n, int32_t* ints, double* doubles) {
   JRandom r(seed), r2(seed);

@@ -30,6 +30,7 @@ namespace {
 struct Emu {
   int B, R, P, T, ldB, G;
   std::vector<double> bUtil, bCap, bPot, rUtil, bLeadNwIn, pLeadNwOut;
+  std::vector<double> hUtil, hCap;  // [B][3] host values of each broker (empty: every host holds one broker)
   std::vector<int32_t> bNrep, bNlead, rPart, rBroker, rOrig, pOff, pBrokers, topicCount, topicNrep;
   std::vector<int32_t> bRack, pTopic, tUpper, tLower, bSet, rSet;
   std::vector<int32_t> pIneligOff, pIneligB;  // Partition._ineligibleBrokers (empty: none)
@@ -53,6 +54,8 @@ struct View {
   const Emu& e;
   double bu(int b, int res) const { return e.bUtil[(size_t)res * e.B + b]; }
   double bcap(int b, int res) const { return e.bCap[(size_t)res * e.B + b]; }
+  double hu(int b, int res) const { return e.hCap.empty() ? bu(b, res) : e.hUtil[3 * (size_t)b + res]; }
+  double hcap(int b, int res) const { return e.hCap.empty() ? bcap(b, res) : e.hCap[3 * (size_t)b + res]; }
   int nrep(int b) const { return e.bNrep[b]; }
   bool alive(int b) const { return e.bAlive[b] != 0; }
   bool allowed(int slot, int b) const { return (e.allowed[b] >> slot) & 1u; }
@@ -199,6 +202,12 @@ void Device::setBrokerSets(const int32_t* brokerSet, const int32_t* replicaSet) 
   E(st_).rSet.assign(replicaSet, replicaSet + R_);
 }
 
+void Device::uploadHosts(const double* hutil, const double* hcap) {
+  Emu& e = E(st_);
+  e.hUtil.assign(hutil, hutil + 3 * (size_t)B_);
+  e.hCap.assign(hcap, hcap + 3 * (size_t)B_);
+}
+
 void Device::flushPending() { flushOnly(); }
 
 void Device::flushOnly() {
@@ -210,6 +219,8 @@ void Device::flushOnly() {
     e.bPot[x.b] = x.potNwOut;
     e.bLeadNwIn[x.b] = x.leadNwIn;
     e.bAlive[x.b] = (uint8_t)x.alive;
+    if (!e.hCap.empty())
+      for (int k = 0; k < 3; ++k) e.hUtil[3 * (size_t)x.b + k] = x.hutil[k];
   }
   for (const ReplicaRow& x : rrows) {
     for (int k = 0; k < 4; ++k) e.rUtil[(size_t)k * R_ + x.r] = x.util[k];
@@ -484,13 +495,14 @@ void Device::stats(const StatsParams& P, const uint8_t* aa, StatsOut* out) {
   for (int res = 0; res < 4; ++res) {
     double hot = 0, cold = 1.7976931348623157e308, var = 0;
     int bal = 0;
+    const bool host = res < 3 && !e.hCap.empty();  // ClusterModelStats.java:297-303
     for (int b = 0; b < B; ++b) {
       if (!e.bAlive[b]) continue;
-      const double u = e.bUtil[(size_t)res * B + b];
+      const double u = host ? e.hUtil[3 * (size_t)b + res] : e.bUtil[(size_t)res * B + b];
       hot = u > hot ? u : hot;
       cold = u < cold ? u : cold;
       if (aa[b]) {
-        const double cap = e.bCap[(size_t)res * B + b];
+        const double cap = host ? e.hCap[3 * (size_t)b + res] : e.bCap[(size_t)res * B + b];
         const double pct = u / cap;
         if (pct >= P.lowerThr[res] && pct <= P.upperThr[res]) bal++;
         const double d = u - P.avgPct[res] * cap;

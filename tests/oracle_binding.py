@@ -53,6 +53,10 @@ class Oracle:
                                            C.POINTER(ccmi.GoalResultStruct)]
             L.oc_action_acceptance_by_kind.restype = C.c_int32
             L.oc_action_acceptance_by_kind.argtypes = [C.c_void_p, C.c_int32, C.POINTER(ccmi.ActionStruct)]
+            L.oc_broker_util.restype = C.c_double
+            L.oc_broker_util.argtypes = [C.c_void_p, C.c_int, C.c_int]
+            L.oc_host_util.restype = C.c_double
+            L.oc_host_util.argtypes = [C.c_void_p, C.c_int, C.c_int]
             L.oc_error.restype = C.c_char_p
             L.oc_error.argtypes = [C.c_void_p]
             L.oc_last_seconds.restype = C.c_double
@@ -215,6 +219,13 @@ class OracleCluster:
 
     def seconds(self) -> float:
         return self.L.oc_last_seconds(self.h)
+
+    def broker_util(self, b: int, res: int) -> float:
+        return self.L.oc_broker_util(self.h, b, res)
+
+    def host_util(self, b: int, res: int) -> float:
+        """Utilization of broker b's host (Broker.host().load().expectedUtilizationFor)."""
+        return self.L.oc_host_util(self.h, b, res)
 
     def optimize_until(self, goal_names: List[str], seconds: float, constraint=None, options=None):
         """CPU-baseline sample: run the chain until `seconds` of wall time have passed (or it completes).
