@@ -47,6 +47,9 @@ hipError_t launchChainRackRows(const DevTables& T, const ChainTables& C, const D
                                int n, const int32_t* cands, int N, int32_t* log, ChainResultDev* out, hipStream_t st);
 hipError_t launchSyncLoads(const ChainTables& C, const LoadRow* lrows, int nl, const SlotRow* srows, int ns,
                            hipStream_t st);
+hipError_t launchRackRowsGroups(const DevTables& T, const DevProgram& prog, const int32_t* rows, const int32_t* order,
+                                const int32_t* gOff, int G, const int32_t* cands, int N, int32_t* res,
+                                unsigned long long* evaluated, hipStream_t st);
 hipError_t launchStats(const StatsParams& P, const int32_t* tc, const int32_t* topicNrep, const BrokerRec* brokers,
                        const uint8_t* allowedAlive, TopicPartial* scratch, void* partials, StatsOut* out, int ldB,
                        hipStream_t st,
@@ -197,7 +200,7 @@ Device::~Device() {
     (void)hipFree(stamps_);
   }
   void* ps[] = {brokers_, replicas_, parts_, allowedAlive_, topicCount_, topicNrep_, topicScratch_, statsOut_,
-                statsPart_, dReq_, rowVisited_, dResult_, dDone_, dChainReq_, tUpper_, tLower_, dRLoad_, dBLoad_, dBLnw_, dBPot_, dPOff_, dPSlots_,
+                statsPart_, dReq_, rowVisited_, dResult_, dDone_, dChainReq_, dRackRes_, tUpper_, tLower_, dRLoad_, dBLoad_, dBLnw_, dBPot_, dPOff_, dPSlots_,
                 dPLeader_, pIneligOff_, pIneligB_, topicLead_, tMinLead_, tLeadLim_, hostCap_};
   for (void* p : ps)
     if (p) (void)hipFree(p);
@@ -1236,6 +1239,52 @@ Device::ChainResult Device::chainPairs(const DevProgram& prog, const int32_t* pr
   log.resize((size_t)res.accepts);
   if (res.accepts) std::memcpy(log.data(), hChainLog_, sizeof(int32_t) * res.accepts);
   return res;
+}
+
+int64_t Device::rackRowsGroups(const DevProgram& prog, const int32_t* rows, int n, const int32_t* order,
+                               const int32_t* gOff, int G, const int32_t* cands, int N, int32_t* res) {
+  DeviceGuard dg(ordinal_);
+  stopServer();
+  if (n <= 0 || G <= 0) {
+    flushPending();
+    return 0;
+  }
+  // request [rows | order | gOff | cands] into HBM with the pending rows (prep), then one lane per partition group
+  const size_t oO = align16((size_t)n * 4), oG = oO + align16((size_t)n * 4), oC = oG + align16((size_t)(G + 1) * 4);
+  const size_t req = oC + align16((size_t)N * 4);
+  const Staged g = packUpdates(req);
+  std::memcpy(hStage_ + g.end, rows, (size_t)n * 4);
+  std::memcpy(hStage_ + g.end + oO, order, (size_t)n * 4);
+  std::memcpy(hStage_ + g.end + oG, gOff, (size_t)(G + 1) * 4);
+  std::memcpy(hStage_ + g.end + oC, cands, (size_t)N * 4);
+  launchPrepFor(g, req, false);
+  if ((size_t)n > rackResCap_) {
+    if (dRackRes_) hipCheck(hipFree(dRackRes_), "hipFree");
+    rackResCap_ = (size_t)n * 2;
+    hipCheck(hipMalloc((void**)&dRackRes_, rackResCap_ * 4 + 16), "hipMalloc rack rows");
+  }
+  unsigned long long* dEval = reinterpret_cast<unsigned long long*>(dRackRes_ + rackResCap_);
+  hipCheck(hipMemsetAsync(dEval, 0, sizeof(unsigned long long), ST), "memset");
+  if (timing) (void)hipEventRecord(EV0, ST);
+  hipCheck(launchRackRowsGroups(tables(), prog, (const int32_t*)dReq_, (const int32_t*)(dReq_ + oO),
+                                (const int32_t*)(dReq_ + oG), G, (const int32_t*)(dReq_ + oC), N, dRackRes_, dEval, ST),
+           "rack_rows_groups");
+  if (timing) (void)hipEventRecord(EV1, ST);
+  unsigned long long evaluated = 0;
+  hipCheck(hipMemcpyAsync(res, dRackRes_, (size_t)n * 4, hipMemcpyDeviceToHost, ST), "D2H rack rows");
+  hipCheck(hipMemcpyAsync(&evaluated, dEval, sizeof(evaluated), hipMemcpyDeviceToHost, ST), "D2H rack rows");
+  streamWait("rack_rows_groups", kChainWaitSeconds);
+  perf.syncs++;
+  perf.scanLaunches++;
+  perf.scanPairs += (int64_t)evaluated;
+  perf.scanRequired += (int64_t)evaluated;
+  perf.scanBytes += (int64_t)evaluated * kBytesPerCandidate;
+  if (timing) {
+    float ms = 0.f;
+    hipCheck(hipEventElapsedTime(&ms, EV0, EV1), "hipEventElapsedTime");
+    perf.scanKernelMs += ms;
+  }
+  return (int64_t)evaluated;
 }
 
 Device::ChainResult Device::chainRackRows(const DevProgram& prog, const int32_t* rows, int n, const int32_t* cands,

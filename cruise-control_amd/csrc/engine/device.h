@@ -169,6 +169,11 @@ class Device {
   // RACK_ROWS chain; log receives (row, candidate index) per accepted row
   ChainResult chainRackRows(const DevProgram& prog, const int32_t* rows, int n, const int32_t* cands, int N,
                             std::vector<int32_t>& log);
+  // RackAwareGoal's rows decided per partition group with no optimized goals (rackrows.h): rows[0, n) in loop order,
+  // order[gOff[g], gOff[g + 1]) the row indices of group g in row order; res[k] receives the accepted candidate
+  // index, kRackKeep or kRackFail. Nothing is applied on the device. Returns the candidates evaluated.
+  int64_t rackRowsGroups(const DevProgram& prog, const int32_t* rows, int n, const int32_t* order, const int32_t* gOff,
+                         int G, const int32_t* cands, int N, int32_t* res);
   void flushOnly();
   void flushPending();
 
@@ -259,6 +264,8 @@ class Device {
   bool serverChain(const DevProgram& prog, int mode, const int32_t* a0, int n0, const int32_t* a1, int n1,
                    const int32_t* a2, int n2, int n, int m, int maxAccepts);
   void streamWait(const char* what, double seconds);
+  int32_t* dRackRes_ = nullptr;  // rackRowsGroups results (+ the evaluated-candidate counter after them)
+  size_t rackResCap_ = 0;
   int32_t* dChainReq_ = nullptr;  // SOP_CHAIN request copy in HBM (the chain rereads it per decision)
   size_t chainReqCap_ = 0;
   const int32_t *rowBroker_ = nullptr, *rowPart_ = nullptr, *partTopic_ = nullptr;

@@ -14,6 +14,7 @@
 
 #include "device.h"
 #include "predicates.h"
+#include "rackrows.h"
 #include "prof.h"
 
 namespace ccmi {
@@ -422,6 +423,28 @@ int64_t Engine::chainRackRows(GoalImpl& self, const std::vector<int32_t>& rows, 
   const Device::ChainResult r = dev->chainRackRows(prog, rows.data(), (int)rows.size(), cands.data(),
                                                    (int)cands.size(), log);
   return r.failRow;
+}
+
+void Engine::rackRowsGroups(GoalImpl& self, const std::vector<int32_t>& rows, const std::vector<int32_t>& cands,
+                            std::vector<int32_t>& res) {
+  PhaseScope ps(PH_DEV_SCAN);
+  m.flushToDevice();
+  DevProgram prog = program(self, DA_MOVE);
+  prog.filter = FILTER_RACK_AWARE;
+  if (prog.nGoals != 1) throw std::logic_error("rackRowsGroups needs a program without optimized goals");
+  // the rows of each partition, in row order (a counting sort by partition)
+  const int n = (int)rows.size();
+  std::vector<int32_t> cnt((size_t)m.P + 1, 0), order(n), gOff;
+  for (int r : rows) cnt[(size_t)m.rPart[r] + 1]++;
+  for (int p = 0; p < m.P; ++p) cnt[(size_t)p + 1] += cnt[p];
+  std::vector<int32_t> at(cnt.begin(), cnt.end() - 1);
+  for (int k = 0; k < n; ++k) order[at[m.rPart[rows[k]]]++] = k;
+  gOff.push_back(0);
+  for (int p = 0; p < m.P; ++p)
+    if (cnt[(size_t)p + 1] > cnt[p]) gOff.push_back(cnt[(size_t)p + 1]);
+  res.assign(n, kRackKeep);
+  dev->rackRowsGroups(prog, rows.data(), n, order.data(), gOff.data(), (int)gOff.size() - 1, cands.data(),
+                      (int)cands.size(), res.data());
 }
 
 int Engine::acceptance(int gi, const ccmi_action& a) {

@@ -161,6 +161,10 @@ class Engine {
                      const std::vector<int32_t>& next, int maxAccepts, std::vector<int32_t>& log);
   int64_t chainRackRows(GoalImpl& self, const std::vector<int32_t>& rows, const std::vector<int32_t>& cands,
                         std::vector<int32_t>& log);
+  // RackAwareGoal's rows with no optimized goals, decided per partition on the device (Device::rackRowsGroups, nothing
+  // applied there): res[k] = accepted candidate index, kRackKeep or kRackFail
+  void rackRowsGroups(GoalImpl& self, const std::vector<int32_t>& rows, const std::vector<int32_t>& cands,
+                      std::vector<int32_t>& res);
 
  private:
   DevProgram program(const GoalImpl& self, int action) const;

@@ -29,6 +29,7 @@
 #include "device.h"
 #include "engine.h"
 #include "predicates.h"
+#include "rackrows.h"
 #include "prof.h"
 
 namespace ccmi {
@@ -192,8 +193,13 @@ class RackAware : public GoalImpl {
   // replicas moved onto later brokers are rack-aware there, so the device re-checks each row's
   // shouldKeepInTheCurrentBroker when it reaches it and skips it if it now holds; everything else it decides and
   // applies in order. The host replays the logged moves and counts the reference-equivalent candidates.
+  //
+  // With no optimized goals a row's decision reads only its own partition, so the rows are decided per partition on
+  // the device in one launch (rackrows.h, Engine::rackRowsGroups) and the host applies the accepted moves in row order:
+  // no device-side apply, no sequential decision chain.
   bool rebalanceAll(Engine& e) override {
-    if (!e.chainsOn()) return false;
+    const bool groups = e.priors.empty() && !std::getenv("CCMI_RACK_CHAIN");
+    if (!groups && !e.chainsOn()) return false;
     PhaseScope ps(PH_OTHER_GOALS);
     Model& m = e.m;
     const std::vector<int> order = brokersToBalance(e);
@@ -215,8 +221,22 @@ class RackAware : public GoalImpl {
       rows.insert(rows.end(), v.begin(), v.end());
     }
     e.eligible(alive, DA_MOVE, cands);
-    const int64_t failRow = e.chainRackRows(*this, rows, cands, log);
-    {
+    int64_t failRow = 0;
+    if (groups) {
+      std::vector<int32_t> res;
+      e.rackRowsGroups(*this, rows, cands, res);
+      for (size_t k = 0; k < rows.size(); ++k) {
+        if (res[k] == kRackFail) {
+          failRow = (int64_t)k + 1;
+          break;
+        }
+        if (res[k] == kRackKeep) continue;
+        const int r = rows[k], j = res[k];
+        e.candidates += eligibleCount(e, r, cands, (size_t)j + 1);
+        m.relocateReplica(m.rPart[r], m.rBroker[r], cands[j]);
+      }
+    } else {
+      failRow = e.chainRackRows(*this, rows, cands, log);
       Model::Replay rp(m);
       for (size_t i = 0; i + 1 < log.size(); i += 2) {
         const int r = rows[log[i]], j = log[i + 1];

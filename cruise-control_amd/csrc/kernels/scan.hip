@@ -26,6 +26,7 @@
 #include "../engine/apply.h"
 #include "../engine/devtypes.h"
 #include "../engine/predicates.h"
+#include "../engine/rackrows.h"
 
 namespace ccmi {
 
@@ -1533,6 +1534,39 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, kServ
   chainRackRowsRun(T, C, prog, ov, reinterpret_cast<LoadVec*>(scRaw), rows, n, cands, N, log, out);
 }
 
+// RackAwareGoal's rows with no optimized goals (rackrows.h): one lane per partition group, every group at once.
+struct RackRowsView {
+  DevTables t;
+  __device__ __forceinline__ int rack(int b) const { return t.brokers[b].rack; }
+  __device__ __forceinline__ bool alive(int b) const { return t.brokers[b].alive != 0; }
+  __device__ __forceinline__ uint32_t bits(int b) const { return t.brokers[b].allowedBits; }
+  __device__ __forceinline__ int flags(int r) const { return t.replicas[r].flags; }
+  __device__ __forceinline__ int rorig(int r) const { return t.replicas[r].orig; }
+  __device__ __forceinline__ int rbroker(int r) const { return t.replicas[r].broker; }
+  __device__ __forceinline__ int rpart(int r) const { return t.replicas[r].part; }
+  __device__ __forceinline__ int pn(int p) const { return t.parts[p].n; }
+  __device__ __forceinline__ int pbroker(int p, int i) const { return t.parts[p].brokers[i]; }
+  __device__ __forceinline__ bool ineligible(int p, int b) const {
+    if (!t.pIneligOff) return false;
+    bool in = false;
+    for (int k = t.pIneligOff[p]; k < t.pIneligOff[p + 1]; ++k) in |= t.pIneligB[k] == b;
+    return in;
+  }
+};
+__global__ __launch_bounds__(256) void rack_rows_groups(DevTables T, DevProgram prog, const int32_t* __restrict__ rows,
+                                                        const int32_t* __restrict__ order,
+                                                        const int32_t* __restrict__ gOff, int G,
+                                                        const int32_t* __restrict__ cands, int N,
+                                                        int32_t* __restrict__ res,
+                                                        unsigned long long* __restrict__ evaluated) {
+  const int g = blockIdx.x * blockDim.x + threadIdx.x;
+  unsigned long long ev = 0;
+  if (g < G) ev = (unsigned long long)rackRowsGroup(RackRowsView{T}, prog, rows, order, gOff[g], gOff[g + 1], cands, N, res);
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) ev += __shfl_xor(ev, off, 64);
+  if ((threadIdx.x & 63) == 0 && ev) atomicAdd(evaluated, ev);
+}
+
 // Host-side load changes since the last chain (LoadRow / SlotRow lists staged in host-mapped memory).
 __global__ __launch_bounds__(256) void sync_loads(ChainTables C, const LoadRow* __restrict__ lrows, int nl,
                                                   const SlotRow* __restrict__ srows, int ns) {
@@ -1645,6 +1679,15 @@ hipError_t launchChainPairs(const DevTables& T, const ChainTables& C, const DevP
 hipError_t launchChainRackRows(const DevTables& T, const ChainTables& C, const DevProgram& prog, const int32_t* rows,
                                int n, const int32_t* cands, int N, int32_t* log, ChainResultDev* out, hipStream_t st) {
   hipLaunchKernelGGL(chain_rack_rows, dim3(1), dim3(kBlock), 0, st, T, C, prog, rows, n, cands, N, log, out);
+  return hipGetLastError();
+}
+
+hipError_t launchRackRowsGroups(const DevTables& T, const DevProgram& prog, const int32_t* rows, const int32_t* order,
+                                const int32_t* gOff, int G, const int32_t* cands, int N, int32_t* res,
+                                unsigned long long* evaluated, hipStream_t st) {
+  if (G <= 0) return hipSuccess;
+  hipLaunchKernelGGL(rack_rows_groups, dim3((unsigned)((G + 255) / 256)), dim3(256), 0, st, T, prog, rows, order, gOff,
+                     G, cands, N, res, evaluated);
   return hipGetLastError();
 }
 

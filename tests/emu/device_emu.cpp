@@ -15,6 +15,7 @@
 #include "device.h"
 #include "intra.h"
 #include "predicates.h"
+#include "rackrows.h"
 #include "shard_rccl.h"
 
 namespace ccmi {
@@ -450,6 +451,35 @@ Device::ChainResult Device::chainPairs(const DevProgram& prog, const int32_t* pr
   }
   perf.scanPairs += res.visited;
   return res;
+}
+
+namespace {
+struct EmuRackView {  // rackrows.h view over the emulated tables
+  const Emu& e;
+  int rack(int b) const { return e.bRack[b]; }
+  bool alive(int b) const { return e.bAlive[b] != 0; }
+  uint32_t bits(int b) const { return e.allowed[b]; }
+  int flags(int r) const { return e.rFlags[r] | (e.bAlive[e.rOrig[r]] ? 0 : RF_ORIG_DEAD); }
+  int rorig(int r) const { return e.rOrig[r]; }
+  int rbroker(int r) const { return e.rBroker[r]; }
+  int rpart(int r) const { return e.rPart[r]; }
+  int pn(int p) const { return e.pOff[p + 1] - e.pOff[p]; }
+  int pbroker(int p, int i) const { return e.pBrokers[e.pOff[p] + i]; }
+  bool ineligible(int p, int b) const { return View{e}.ineligible(p, b); }
+};
+}  // namespace
+
+int64_t Device::rackRowsGroups(const DevProgram& prog, const int32_t* rows, int n, const int32_t* order,
+                               const int32_t* gOff, int G, const int32_t* cands, int N, int32_t* res) {
+  flushOnly();
+  if (n <= 0 || G <= 0) return 0;
+  Emu& e = E(st_);
+  perf.scanLaunches++;
+  int64_t evaluated = 0;
+  for (int g = 0; g < G; ++g)
+    evaluated += rackRowsGroup(EmuRackView{e}, prog, rows, order, gOff[g], gOff[g + 1], cands, N, res);
+  perf.scanPairs += evaluated;
+  return evaluated;
 }
 
 Device::ChainResult Device::chainRackRows(const DevProgram& prog, const int32_t* rows, int n, const int32_t* cands,
