@@ -1363,6 +1363,7 @@ class ResourceDistribution : public GoalImpl {
           if (entryIn[x]) ids.push_back(x);
         cand.buildByRank(ids, rank);
       }
+      if (action == DA_LEADERSHIP) cand.untrackSequence();  // the leadership form only searches the set
       for (const Step& h : hist) {
         for (auto& o : ovr) {
           if (o.first == h.dst) o.second = h.keyAfter;

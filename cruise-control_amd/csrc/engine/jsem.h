@@ -71,8 +71,12 @@ struct JavaRandom {
 // java.util.TreeMap<Integer-like key> with an external live comparator. Cmp: int(int a, int b).
 // Nodes are one 20-byte record each (key, links, colour) so a search step is one cache line.
 struct RbNode {
-  int key, left, right, parent;
-  int32_t red;
+  uint32_t kc;  // key (a non-negative int) with the colour in bit 31
+  int left, right, parent;
+  int key() const { return (int)(kc & 0x7fffffffu); }
+  bool red() const { return (kc >> 31) != 0; }
+  void setRed(bool r) { kc = (kc & 0x7fffffffu) | ((uint32_t)r << 31); }
+  void setKey(int k) { kc = (kc & 0x80000000u) | (uint32_t)k; }
 };
 template <class Cmp>
 class RbTreeSet {
@@ -112,10 +116,10 @@ class RbTreeSet {
     while (!st.empty()) {
       const int p = st.back();
       st.pop_back();
-      mix(n_[p].key);
-      mix(n_[p].red);
-      mix(n_[p].left >= 0 ? n_[n_[p].left].key : -1);
-      mix(n_[p].right >= 0 ? n_[n_[p].right].key : -1);
+      mix(n_[p].key());
+      mix(n_[p].red());
+      mix(n_[p].left >= 0 ? n_[n_[p].left].key() : -1);
+      mix(n_[p].right >= 0 ? n_[n_[p].right].key() : -1);
       if (n_[p].right >= 0) st.push_back(n_[p].right);
       if (n_[p].left >= 0) st.push_back(n_[p].left);
     }
@@ -135,7 +139,7 @@ class RbTreeSet {
     int parent = -1, c = 0;
     while (t >= 0) {
       parent = t;
-      c = cmp_(k, n_[t].key);
+      c = cmp_(k, n_[t].key());
       if (c < 0) t = n_[t].left;
       else if (c > 0) t = n_[t].right;
       else return false;
@@ -158,7 +162,12 @@ class RbTreeSet {
   // `cancel` (optional) stops the build early (the tree is then incomplete and must be discarded).
   void buildByRank(const std::vector<int>& ids, const std::vector<int32_t>& rank,
                    const std::atomic<bool>* cancel = nullptr) {
-    n_.reserve(ids.size());
+    // an empty tree: node i is the i-th put (no free list), written in place
+    n_.clear();
+    free_.clear();
+    root_ = -1;
+    size_ = 0;
+    n_.resize(ids.size());
     int32_t nr = 0;
     for (int k : ids) nr = std::max(nr, rank[k] + 1);
     const int nw = (nr + 63) >> 6, ns = (nw + 63) >> 6;
@@ -190,27 +199,28 @@ class RbTreeSet {
       wi = (si << 6) | __builtin_ctzll(sm);
       return (wi << 6) | __builtin_ctzll(w[wi]);
     };
-    size_t done = 0;
-    for (int k : ids) {
-      if (cancel && (++done & 511) == 0 && cancel->load(std::memory_order_relaxed)) return;
+    Node* N = n_.data();
+    for (int e = 0; e < (int)ids.size(); ++e) {
+      if (cancel && (e & 511) == 511 && cancel->load(std::memory_order_relaxed)) return;
+      const int k = ids[e];
       const int32_t rk = rank[k];
-      int e;
-      if (root_ < 0) {
-        e = root_ = alloc(k, -1);
+      if (e == 0) {
+        N[0] = Node{(uint32_t)k, -1, -1, -1};
+        root_ = 0;
         size_ = 1;
       } else {
         const int32_t pr = pred(rk);
         int parent;
         bool goLeft;
-        if (pr >= 0 && n_[nodeOf[pr]].right < 0) {
+        if (pr >= 0 && N[nodeOf[pr]].right < 0) {
           parent = nodeOf[pr];
           goLeft = false;
         } else {
           parent = nodeOf[succ(rk)];
           goLeft = true;
         }
-        e = alloc(k, parent);
-        (goLeft ? n_[parent].left : n_[parent].right) = e;
+        N[e] = Node{(uint32_t)k, -1, -1, parent};
+        (goLeft ? N[parent].left : N[parent].right) = e;
         insertFix(e);
         ++size_;
       }
@@ -223,8 +233,14 @@ class RbTreeSet {
     for (int32_t r = 0; r < nr; ++r)
       if (nodeOf[r] >= 0) seqId_.push_back(nodeOf[r]);
     seqKey_.resize(seqId_.size());
-    for (size_t i = 0; i < seqId_.size(); ++i) seqKey_[i] = n_[seqId_[i]].key;
+    for (size_t i = 0; i < seqId_.size(); ++i) seqKey_[i] = n_[seqId_[i]].key();
     seqOn_ = true;
+  }
+  // Stop maintaining the in-order sequence (trees that are only searched: add/remove then skip its O(n) updates)
+  void untrackSequence() {
+    seqOn_ = false;
+    seqId_.clear();
+    seqKey_.clear();
   }
   // Maintain the in-order sequence next to the tree from now on (a tree built by add(): one traversal), so
   // inorder() is a copy instead of a walk over every node.
@@ -237,7 +253,7 @@ class RbTreeSet {
       for (; p >= 0; p = succ(p)) seqId_.push_back(p);
     }
     seqKey_.resize(seqId_.size());
-    for (size_t i = 0; i < seqId_.size(); ++i) seqKey_[i] = n_[seqId_[i]].key;
+    for (size_t i = 0; i < seqId_.size(); ++i) seqKey_[i] = n_[seqId_[i]].key();
     seqOn_ = true;
   }
   bool remove(int k) {
@@ -269,7 +285,7 @@ class RbTreeSet {
     while (n_[p].left >= 0) p = n_[p].left;
     while (p >= 0) {
       int next = succ(p);
-      if (pred(n_[p].key)) {
+      if (pred(n_[p].key())) {
         if (n_[p].left >= 0 && n_[p].right >= 0) next = p;
         erase(p);
         removed = true;
@@ -287,7 +303,7 @@ class RbTreeSet {
     int p = root_;
     if (p < 0) return;
     while (n_[p].left >= 0) p = n_[p].left;
-    for (; p >= 0; p = succ(p)) out.push_back(n_[p].key);
+    for (; p >= 0; p = succ(p)) out.push_back(n_[p].key());
   }
 
  private:
@@ -306,17 +322,17 @@ class RbTreeSet {
     if (!free_.empty()) {
       id = free_.back();
       free_.pop_back();
-      n_[id] = Node{k, -1, -1, parent, 0};
+      n_[id] = Node{(uint32_t)k, -1, -1, parent};
     } else {
       id = (int)n_.size();
-      n_.push_back(Node{k, -1, -1, parent, 0});
+      n_.push_back(Node{(uint32_t)k, -1, -1, parent});
     }
     return id;
   }
   int find(int k) const {
     int p = root_;
     while (p >= 0) {
-      int c = cmp_(k, n_[p].key);
+      int c = cmp_(k, n_[p].key());
       if (c == 0) return p;
       p = c < 0 ? n_[p].left : n_[p].right;
     }
@@ -335,12 +351,12 @@ class RbTreeSet {
     }
     return p;
   }
-  bool isRed(int p) const { return p >= 0 && n_[p].red; }
+  bool isRed(int p) const { return p >= 0 && n_[p].red(); }
   int par(int p) const { return p < 0 ? -1 : n_[p].parent; }
   int lft(int p) const { return p < 0 ? -1 : n_[p].left; }
   int rgt(int p) const { return p < 0 ? -1 : n_[p].right; }
   void paint(int p, bool red) {
-    if (p >= 0) n_[p].red = red;
+    if (p >= 0) n_[p].setRed(red);
   }
   void rotL(int p) {
     if (p < 0) return;
@@ -374,17 +390,17 @@ class RbTreeSet {
   // the parent of x is black and the JDK loop ends)
   void insertFix(int x) {
     Node* N = n_.data();
-    N[x].red = 1;
+    N[x].setRed(1);
     while (x != root_) {
       int p = N[x].parent;
-      if (!N[p].red) break;
+      if (!N[p].red()) break;
       const int g = N[p].parent;
       if (p == N[g].left) {
         const int y = N[g].right;
-        if (y >= 0 && N[y].red) {
-          N[p].red = 0;
-          N[y].red = 0;
-          N[g].red = 1;
+        if (y >= 0 && N[y].red()) {
+          N[p].setRed(0);
+          N[y].setRed(0);
+          N[g].setRed(1);
           x = g;
           continue;
         }
@@ -393,15 +409,15 @@ class RbTreeSet {
           rotL(x);
           p = N[x].parent;
         }
-        N[p].red = 0;
-        N[g].red = 1;
+        N[p].setRed(0);
+        N[g].setRed(1);
         rotR(g);
       } else {
         const int y = N[g].left;
-        if (y >= 0 && N[y].red) {
-          N[p].red = 0;
-          N[y].red = 0;
-          N[g].red = 1;
+        if (y >= 0 && N[y].red()) {
+          N[p].setRed(0);
+          N[y].setRed(0);
+          N[g].setRed(1);
           x = g;
           continue;
         }
@@ -410,13 +426,13 @@ class RbTreeSet {
           rotR(x);
           p = N[x].parent;
         }
-        N[p].red = 0;
-        N[g].red = 1;
+        N[p].setRed(0);
+        N[g].setRed(1);
         rotL(g);
       }
       break;
     }
-    N[root_].red = 0;
+    N[root_].setRed(0);
   }
   // TreeMap.deleteEntry (successor key copied into the doomed node) + fixAfterDeletion
   void erase(int p) {
@@ -434,7 +450,7 @@ class RbTreeSet {
     }
     if (n_[p].left >= 0 && n_[p].right >= 0) {
       int s = succ(p);
-      n_[p].key = n_[s].key;
+      n_[p].setKey(n_[s].key());
       p = s;
     }
     int rep = n_[p].left >= 0 ? n_[p].left : n_[p].right;
@@ -445,11 +461,11 @@ class RbTreeSet {
       else if (p == n_[pp].left) n_[pp].left = rep;
       else n_[pp].right = rep;
       n_[p].left = n_[p].right = n_[p].parent = -1;
-      if (!n_[p].red) deleteFix(rep);
+      if (!n_[p].red()) deleteFix(rep);
     } else if (n_[p].parent < 0) {
       root_ = -1;
     } else {
-      if (!n_[p].red) deleteFix(p);
+      if (!n_[p].red()) deleteFix(p);
       int pp = n_[p].parent;
       if (pp >= 0) {
         if (p == n_[pp].left) n_[pp].left = -1;

@@ -268,9 +268,13 @@ struct PreView {
   int stl, dtl, tmn;  // leaders of the row's topic on the source / destination, MinTopicLeaders' minimum of it
   int tlu, tll;       // TopicLeaderReplicaDistributionGoal's leader limits of the row's topic
   bool inelig;  // dst is one of the row's partition's ineligible brokers
-  // host resources of the source's / destination's hosts (only when brokers share hosts: DevTables.hostCap set)
+  // host resources of the source's / destination's hosts (only when brokers share hosts: DevTables.hostCap set). The
+  // view keeps where they are (the broker's record or its dirty overlay row, and the host capacity table) and the
+  // predicates load them on use: no registers held for them on the common one-broker-per-host path.
   bool hmode;
-  double shu0, shu1, shu2, dhu0, dhu1, dhu2, shc0, shc1, shc2, dhc0, dhc1, dhc2;
+  const double* shu;  // source's host utilization [3] (HBM record or LDS overlay row)
+  const double* dhu;  // destination's
+  const double* hcapT;  // DevTables.hostCap
 
   static __device__ __forceinline__ double sel(int k, double a, double b, double c, double d) {
     return k == 0 ? a : (k == 1 ? b : (k == 2 ? c : d));
@@ -496,18 +500,8 @@ struct PreView {
   __device__ __forceinline__ void loadSrcHost(const DevTables& t, const BrokerRec& sb, const OverlayLds& ov) {
     hmode = t.hostCap != nullptr;
     if (!hmode) return;  // uniform per launch
-    shu0 = sb.hutil[0];
-    shu1 = sb.hutil[1];
-    shu2 = sb.hutil[2];
-    shc0 = t.hostCap[3 * (size_t)src];
-    shc1 = t.hostCap[3 * (size_t)src + 1];
-    shc2 = t.hostCap[3 * (size_t)src + 2];
     const int si = ov.broker(src);
-    if (si >= 0) {
-      shu0 = ov.b[si].hutil[0];
-      shu1 = ov.b[si].hutil[1];
-      shu2 = ov.b[si].hutil[2];
-    }
+    shu = si >= 0 ? ov.b[si].hutil : sb.hutil;
   }
   // The destination side, loaded BEFORE the row (it depends only on the destination id); the destination's
   // topic count needs the row's topic and is read in loadRow.
@@ -546,12 +540,8 @@ struct PreView {
     aliveBits = aDst ? 4u : 0u;
     hmode = t.hostCap != nullptr;
     if (hmode) {  // uniform per launch
-      dhu0 = di >= 0 ? ov.b[di].hutil[0] : db.hutil[0];
-      dhu1 = di >= 0 ? ov.b[di].hutil[1] : db.hutil[1];
-      dhu2 = di >= 0 ? ov.b[di].hutil[2] : db.hutil[2];
-      dhc0 = t.hostCap[3 * (size_t)d];
-      dhc1 = t.hostCap[3 * (size_t)d + 1];
-      dhc2 = t.hostCap[3 * (size_t)d + 2];
+      dhu = di >= 0 ? ov.b[di].hutil : db.hutil;
+      hcapT = t.hostCap;
     }
   }
   __device__ __forceinline__ double bu(int b, int k) const {
@@ -562,11 +552,11 @@ struct PreView {
   }
   __device__ __forceinline__ double hu(int b, int k) const {  // k < 3 (host resources)
     if (!hmode) return bu(b, k);
-    return b == dst ? sel(k, dhu0, dhu1, dhu2, dhu2) : sel(k, shu0, shu1, shu2, shu2);
+    return (b == dst ? dhu : shu)[k];
   }
   __device__ __forceinline__ double hcap(int b, int k) const {
     if (!hmode) return bcap(b, k);
-    return b == dst ? sel(k, dhc0, dhc1, dhc2, dhc2) : sel(k, shc0, shc1, shc2, shc2);
+    return hcapT[3 * (size_t)(b == dst ? dst : src) + k];
   }
   __device__ __forceinline__ int nrep(int b) const { return b == dst ? dnrep : snrep; }
   // asked for src and dst only (the original broker's liveness is folded into origOff)

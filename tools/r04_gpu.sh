@@ -1,7 +1,8 @@
 #!/bin/bash
 # Round-4 GPU pass (one gpurun call): smoke, the -m gpu suite, the default C2 bench line. Every GPU step runs under
 # its own time limit; anything but success stops the script (no GPU step after a fault, abort or timeout).
-#   env: TAG (log names), PYTEST_K (a -k filter), SKIP_TESTS=1, SKIP_BENCH=1, BENCH_ARGS, ENVS (exported for every step)
+#   env: TAG (log names), PYTEST_K (a -k filter), SKIP_TESTS=1, SKIP_BENCH=1, BENCH_ARGS, ENVS (exported for every step),
+#        PROBE=1 (CCMI_PROFILE=goal probe; PROBE_PROFILE, STAMPS=1 for CCMI_STAMPS), ROCPROF=1 (rocprofv3 kernel trace + stats of one bench step)
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out
 T=${TAG:-r04}
@@ -29,4 +30,13 @@ if [ -z "$SKIP_BENCH" ]; then
   tail -3 "gpurun_out/bench_$T.err"
   [ $rc -eq 0 ] || { echo "stopping: bench exited $rc"; exit $rc; }
   python3 -c "import json; d=json.loads(open('gpurun_out/bench_$T.json').read().strip().splitlines()[-1]); print(d['value'], d['ms_per_step'], d.get('parity'))"
+fi
+if [ -n "$PROBE" ]; then  # per-goal phase profile of one C2 optimization
+  ( export CCMI_PROFILE=${PROBE_PROFILE:-goal}; [ -n "$STAMPS" ] && export CCMI_STAMPS=1
+    step probe 600 python -u tools/probe.py --workload ${WORKLOAD:-c2} ) || exit $?
+  grep -E "^total|^perf|stamps\]" "gpurun_out/probe_$T.log"
+fi
+if [ -n "$ROCPROF" ]; then  # kernel trace + stats of one bench step
+  step rocprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_$T -o bench -- \
+    python3 -u bench.py --steps 1 --warmup 1 --no-cpu-baseline ${BENCH_ARGS:-}
 fi
