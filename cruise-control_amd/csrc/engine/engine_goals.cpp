@@ -1066,6 +1066,10 @@ class TopicReplicaDistribution : public GoalImpl {
   bool fix = false, anyAbove = false, anyUnder = false;
   std::vector<uint8_t> rebalanceTopic;
   std::vector<int32_t> upper, lower;
+  std::vector<int32_t> topicsScratch, perOff;
+  std::vector<uint32_t> perStamp;
+  std::vector<uint8_t> perImm;
+  uint32_t stamp = 0;
   int sid() const { return sortId(kind, false, false); }
   bool excluded(int b) const { return !allowed[b]; }
 
@@ -1137,35 +1141,33 @@ class TopicReplicaDistribution : public GoalImpl {
   void rebalance(Engine& e, int b) override {
     PhaseScope ps(PH_OTHER_GOALS);
     Model& m = e.m;
-    std::vector<int32_t> topics;
+    std::vector<int32_t>& topics = topicsScratch;
     m.bTopicKeys[b].order(topics);  // Broker.topics(): HashMap key order
-    // per-topic (offline count, has immigrant) of this broker's replicas, one pass (recounted after moves)
-    std::vector<std::pair<int, std::pair<int, int>>> per;
+    // per-topic (offline count, has immigrant) of this broker's replicas, one pass (recounted after moves); the
+    // per-topic slots are valid for the current stamp only
+    if (perStamp.size() != (size_t)m.T) {
+      perStamp.assign(m.T, 0);
+      perOff.assign(m.T, 0);
+      perImm.assign(m.T, 0);
+    }
     auto recount = [&]() {
-      per.clear();
+      ++stamp;
       for (int r : m.bRepl[b]) {
         const int t = m.pTopic[m.rPart[r]];
-        bool found = false;
-        for (auto& x : per)
-          if (x.first == t) {
-            x.second.first += m.rInOff[r];
-            x.second.second |= m.rInImm[r];
-            found = true;
-            break;
-          }
-        if (!found) per.push_back({t, {m.rInOff[r], m.rInImm[r]}});
+        if (perStamp[t] != stamp) {
+          perStamp[t] = stamp;
+          perOff[t] = 0;
+          perImm[t] = 0;
+        }
+        perOff[t] += m.rInOff[r];
+        perImm[t] |= m.rInImm[r];
       }
     };
     recount();
     for (int t : topics) {
       if (!rebalanceTopic[t]) continue;
-      int nOff = 0, hasImm = 0;
-      for (auto& x : per)
-        if (x.first == t) {
-          nOff = x.second.first;
-          hasImm = x.second.second;
-          break;
-        }
+      const bool seen = perStamp[t] == stamp;
+      const int nOff = seen ? perOff[t] : 0, hasImm = seen ? perImm[t] : 0;
       const int n = m.tcount(t, b);
       const bool excl = excluded(b);
       const bool requireLess = nOff > 0 || n > upper[t] || excl;
