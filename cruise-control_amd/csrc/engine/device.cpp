@@ -180,22 +180,30 @@ Device::~Device() {
                              "%.2f us, rest to arrival %.2f us (workgroup 0)\n",
                      h[8192], h[8193] * 0.01 / h[8192], h[8194] * 0.01 / h[8192], h[8195] * 0.01 / h[8192],
                      h[8196] * 0.01 / h[8192]);
+      if (h[8198])
+        std::fprintf(stderr, "[ccmi server stamps] %llu cross/segment commands: request + staging + view loads %.2f us "
+                             "of the first tile\n",
+                     h[8198], h[8197] * 0.01 / h[8198]);
       if (h[8200])
         std::fprintf(stderr, "[ccmi chain stamps] %llu chain_pairs launches, %llu accepts: %.2f us per launch in "
                              "evaluation, %.2f us applying, %.2f us in total (thread 0)\n",
                      h[8200], h[8201], h[8202] * 0.01 / h[8200], h[8203] * 0.01 / h[8200], h[8204] * 0.01 / h[8200]);
-      double acc[5] = {0, 0, 0, 0, 0};
-      int n = 0;
+      double acc[5] = {0, 0, 0, 0, 0}, loads = 0;
+      int n = 0, nl = 0;
       for (int i = 0; i < 1024; ++i) {
         const unsigned long long* t = &h[i * 8];
         if (!t[0] || !t[1] || !t[2] || !t[3] || !t[4] || !t[5] || t[5] < t[0]) continue;
         for (int k = 0; k < 5; ++k) acc[k] += (double)(t[k + 1] - t[k]) * 0.01;  // 100 MHz -> us
         n++;
+        if (t[6] > t[1] && t[6] <= t[2]) {  // scan_cross: the view's loads landed at t[6]
+          loads += (double)(t[6] - t[1]) * 0.01;
+          nl++;
+        }
       }
       if (n)
-        std::fprintf(stderr, "[ccmi stamps] %d launches: stage %.2f us, loads+predicate %.2f us, blockMin %.2f us, "
-                             "tail %.2f us, publish %.2f us\n",
-                     n, acc[0] / n, acc[1] / n, acc[2] / n, acc[3] / n, acc[4] / n);
+        std::fprintf(stderr, "[ccmi stamps] %d launches: stage %.2f us, loads+predicate %.2f us (loads %.2f us over %d), "
+                             "blockMin %.2f us, tail %.2f us, publish %.2f us\n",
+                     n, acc[0] / n, acc[1] / n, nl ? loads / nl : 0.0, nl, acc[2] / n, acc[3] / n, acc[4] / n);
     }
     (void)hipFree(stamps_);
   }

@@ -1363,7 +1363,10 @@ class ResourceDistribution : public GoalImpl {
           if (entryIn[x]) ids.push_back(x);
         cand.buildByRank(ids, rank);
       }
-      if (action == DA_LEADERSHIP) cand.untrackSequence();  // the leadership form only searches the set
+      // the replay keeps no in-order sequence (each step would shift it); the replica-move form, which walks the set
+      // in order for every candidate list, takes it once afterwards; the leadership form only searches the set
+      cand.untrackSequence();
+      prof().count(15, "tree.replay.steps", (int64_t)hist.size());
       for (const Step& h : hist) {
         for (auto& o : ovr) {
           if (o.first == h.dst) o.second = h.keyAfter;
@@ -1372,6 +1375,7 @@ class ResourceDistribution : public GoalImpl {
         cand.remove(h.dst);
         if (h.add) cand.add(h.dst);
       }
+      if (action != DA_LEADERSHIP) cand.trackSequence();
       ovr.clear();
       built = true;
     };

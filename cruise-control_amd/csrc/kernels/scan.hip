@@ -783,6 +783,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, kScan
       PreView v;
       v.loadDst(T, dq, ov);
       v.loadRowRef(T, prog, rq, ov);
+      CCMI_STAMP(T, seq, 6);  // the view's loads landed (diagnostics split loads from predicate time)
       const bool inList = (prog.filter != FILTER_RACK_AWARE || v.rackEligible()) && !v.exclLeadBlocked(prog);
       if (inList && moveCandidateAccepted(prog, v, v.r, v.dst)) local = (unsigned long long)k * N + c0 + j;
     }
@@ -934,7 +935,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, kServ
   int progVer = -1;
   int acqEpoch = -1;  // ServerCmd.rowsEpoch of this workgroup's last acquire (-1: none since the launch)
   unsigned long long idleSince = __builtin_amdgcn_s_memrealtime();
-  unsigned long long srvT[5] = {0, 0, 0, 0, 0};
+  unsigned long long srvT[6] = {0, 0, 0, 0, 0, 0};
   for (;;) {
     if (threadIdx.x == 0) {
       int ex = 0;
@@ -1096,6 +1097,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, kServ
           PreView v;
           v.loadDst(T, dq, ov);
           v.loadRowRef(T, prog, rq, ov);
+          if (firstTile) SRV_STAMP(T, 5);  // the first tile's view loads landed
           const bool inList = (prog.filter != FILTER_RACK_AWARE || v.rackEligible()) && !v.exclLeadBlocked(prog);
           if (inList && moveCandidateAccepted(prog, v, v.r, v.dst)) local = (unsigned long long)k * N + c0 + j;
         }
@@ -1163,6 +1165,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, kServ
         srvT[4] = __builtin_amdgcn_s_memrealtime();
         atomicAdd(&T.stamps[8192 + 0], 1ull);
         for (int i = 0; i < 4; ++i) atomicAdd(&T.stamps[8192 + 1 + i], srvT[i + 1] - srvT[i]);
+        if (srvT[5] > srvT[2] && srvT[5] <= srvT[3]) {  // cross / segment commands: ready -> view loads landed
+          atomicAdd(&T.stamps[8197], srvT[5] - srvT[2]);
+          atomicAdd(&T.stamps[8198], 1ull);
+        }
       }
       if (prev == nAct - 1) {
         const unsigned long long v = __hip_atomic_load(&result[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
