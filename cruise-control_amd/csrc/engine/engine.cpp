@@ -47,6 +47,7 @@ struct HostView {
   const std::vector<int32_t>& tLim;  // TopicLeaderReplicaDistributionGoal limits [T][2] (empty: none)
   double bu(int b, int res) const { return m.bu(b, res); }
   double bcap(int b, int res) const { return m.cap(b, res); }
+  bool hostMode() const { return m.hostMode(); }
   double hu(int b, int res) const { return m.hu(b, res); }
   double hcap(int b, int res) const { return m.hcap(b, res); }
   int nrep(int b) const { return m.nrep(b); }

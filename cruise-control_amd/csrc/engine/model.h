@@ -171,6 +171,7 @@ class Model {
   std::vector<LoadVec> hLoad;                  // [H] Host._load
   std::vector<double> hCap, hUtilC;            // [H][4] Host._hostCapacity, cached expectedUtilizationFor
   std::vector<int32_t> hAlive, hNrep;          // [H] Host._aliveBrokers, Host._replicas.size()
+  bool hostMode() const { return sharedHosts; }  // hu / hcap differ from bu / bcap only when brokers share hosts
   double hu(int b, int res) const { return sharedHosts ? hUtilC[4 * (size_t)bHost[b] + res] : bu(b, res); }
   double hcap(int b, int res) const {
     if (!sharedHosts) return cap(b, res);

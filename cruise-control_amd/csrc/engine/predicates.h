@@ -20,7 +20,8 @@
 //   TopicLeaderReplicaDistributionGoal            TopicLeaderReplicaDistributionGoal.java:181-256,359-374
 // Host resources (CPU, NW_IN, NW_OUT; Resource.java:18-25) are checked against the broker's host as the reference
 // does (V::hu / V::hcap: Broker.host().load() / Host.capacityFor); when every host holds one broker those equal the
-// broker's own values bit for bit.
+// broker's own values bit for bit, and V::hostMode() is false: the host checks are then the broker checks and are skipped
+// (the same booleans, without evaluating both).
 #pragma once
 #include <stdint.h>
 
@@ -35,7 +36,7 @@
 
 namespace ccmi {
 
-// V must provide: bu(b,res) bcap(b,res) hu(b,res) hcap(b,res) nrep(b) alive(b) allowed(slot,b) ru(r,res) flags(r) rbroker(r)
+// V must provide: bu(b,res) bcap(b,res) hostMode() hu(b,res) hcap(b,res) nrep(b) alive(b) allowed(slot,b) ru(r,res) flags(r) rbroker(r)
 // rorig(r) origOff(r) rpart(r) hosts(p,b), and for the goals that read them: rack(b) otherOnRack(p,self,rack)
 // slotRack(p,b) (rack of partition p's replica on b) rackCount(p,rack) nlead(b)
 // pot(b) lnwin(b) pLeadNwOut(p) ptopic(p) tcount(t,b) tUpper(t) tLower(t) bset(b) rbset(r) (broker sets)
@@ -82,7 +83,7 @@ CCMI_HD bool resAboveLowerAfter(const DevGoal& g, const V& v, int b, double delt
   const double lim = v.bcap(b, res) * g.lowerThr;
   const double u = v.bu(b, res);
   const bool brokerAbove = add ? (u + delta >= lim) : (u - delta >= lim);
-  if (!isHostRes(res)) return brokerAbove;
+  if (!isHostRes(res) || !v.hostMode()) return brokerAbove;
   const double hlim = v.hcap(b, res) * g.lowerThr;
   const double hu = v.hu(b, res);
   const bool hostAbove = add ? (hu + delta >= hlim) : (hu - delta >= hlim);
@@ -94,7 +95,7 @@ CCMI_HD bool resUnderUpperAfter(const DevGoal& g, const V& v, int b, double delt
   const double lim = v.bcap(b, res) * thr;
   const double u = v.bu(b, res);
   const bool brokerUnder = add ? (u + delta <= lim) : (u - delta <= lim);
-  if (!isHostRes(res)) return brokerUnder;
+  if (!isHostRes(res) || !v.hostMode()) return brokerUnder;
   const double hlim = v.hcap(b, res) * thr;
   const double hu = v.hu(b, res);
   const bool hostUnder = add ? (hu + delta <= hlim) : (hu - delta <= hlim);
@@ -127,7 +128,7 @@ CCMI_HD bool resSwapContainerViolating(const DevGoal& g, const V& v, double delt
 template <class V>
 CCMI_HD bool resSwapViolating(const DevGoal& g, const V& v, double delta, int sb, int db) {
   const bool broker = resSwapContainerViolating(g, v, delta, sb, db, false);
-  if (!broker || !isHostRes(g.resource)) return broker;
+  if (!broker || !isHostRes(g.resource) || !v.hostMode()) return broker;
   return resSwapContainerViolating(g, v, delta, sb, db, true);
 }
 
@@ -231,6 +232,10 @@ CCMI_HD int minLeadAcceptSwap(const V& v, int sr, int sb, int dr, int db) {
 template <class V>
 CCMI_HD bool capUnderAfterAdding(const DevGoal& g, const V& v, int b, double u) {
   const int res = g.resource;
+  if (!v.hostMode()) {  // one check: the host check of a host-only resource keeps its NaN behaviour
+    const double x = v.bu(b, res) + u, lim = v.bcap(b, res) * g.capThr;
+    return isBrokerRes(res) ? x < lim : !(x >= lim);
+  }
   if (isHostRes(res) && v.hu(b, res) + u >= v.hcap(b, res) * g.capThr) return false;
   if (isBrokerRes(res)) return v.bu(b, res) + u < v.bcap(b, res) * g.capThr;
   return true;

@@ -34,6 +34,7 @@ struct DevView {
   DevTables t;
   __device__ __forceinline__ double bu(int b, int res) const { return t.brokers[b].util[res]; }
   __device__ __forceinline__ double bcap(int b, int res) const { return t.brokers[b].cap[res]; }
+  __device__ __forceinline__ bool hostMode() const { return t.hostCap != nullptr; }
   __device__ __forceinline__ double hu(int b, int res) const { return t.hostCap ? t.brokers[b].hutil[res] : bu(b, res); }
   __device__ __forceinline__ double hcap(int b, int res) const {
     return t.hostCap ? t.hostCap[3 * (size_t)b + res] : bcap(b, res);
@@ -550,6 +551,7 @@ struct PreView {
   __device__ __forceinline__ double bcap(int b, int k) const {
     return b == dst ? sel(k, dcap0, dcap1, dcap2, dcap3) : sel(k, scap0, scap1, scap2, scap3);
   }
+  __device__ __forceinline__ bool hostMode() const { return hmode; }
   __device__ __forceinline__ double hu(int b, int k) const {  // k < 3 (host resources)
     if (!hmode) return bu(b, k);
     return (b == dst ? dhu : shu)[k];

@@ -55,6 +55,7 @@ struct View {
   const Emu& e;
   double bu(int b, int res) const { return e.bUtil[(size_t)res * e.B + b]; }
   double bcap(int b, int res) const { return e.bCap[(size_t)res * e.B + b]; }
+  bool hostMode() const { return !e.hCap.empty(); }
   double hu(int b, int res) const { return e.hCap.empty() ? bu(b, res) : e.hUtil[3 * (size_t)b + res]; }
   double hcap(int b, int res) const { return e.hCap.empty() ? bcap(b, res) : e.hCap[3 * (size_t)b + res]; }
   int nrep(int b) const { return e.bNrep[b]; }
