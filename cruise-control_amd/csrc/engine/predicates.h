@@ -36,6 +36,17 @@
 
 namespace ccmi {
 
+// A value every lane holds alike (program and goal fields): on gfx950 it goes to a scalar register, so the goal
+// dispatch below branches on a scalar (the scan server keeps the program in LDS, where the compiler cannot prove the
+// value uniform and would otherwise build the switch from per-lane compares).
+CCMI_HD int uniform(int x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_amdgcn_readfirstlane(x);
+#else
+  return x;
+#endif
+}
+
 // V must provide: bu(b,res) bcap(b,res) hostMode() hu(b,res) hcap(b,res) nrep(b) alive(b) allowed(slot,b) ru(r,res) flags(r) rbroker(r)
 // rorig(r) origOff(r) rpart(r) hosts(p,b), and for the goals that read them: rack(b) otherOnRack(p,self,rack)
 // slotRack(p,b) (rack of partition p's replica on b) rackCount(p,rack) nlead(b)
@@ -79,7 +90,7 @@ CCMI_HD bool rdAccept(const DevGoal& g, const V& v, int action, int src, int dst
 // within the limit when the host or the broker is
 template <class V>
 CCMI_HD bool resAboveLowerAfter(const DevGoal& g, const V& v, int b, double delta, bool add) {
-  const int res = g.resource;
+  const int res = uniform(g.resource);
   const double lim = v.bcap(b, res) * g.lowerThr;
   const double u = v.bu(b, res);
   const bool brokerAbove = add ? (u + delta >= lim) : (u - delta >= lim);
@@ -91,7 +102,7 @@ CCMI_HD bool resAboveLowerAfter(const DevGoal& g, const V& v, int b, double delt
 }
 template <class V>
 CCMI_HD bool resUnderUpperAfter(const DevGoal& g, const V& v, int b, double delta, bool add, double thr) {
-  const int res = g.resource;
+  const int res = uniform(g.resource);
   const double lim = v.bcap(b, res) * thr;
   const double u = v.bu(b, res);
   const bool brokerUnder = add ? (u + delta <= lim) : (u - delta <= lim);
@@ -103,7 +114,7 @@ CCMI_HD bool resUnderUpperAfter(const DevGoal& g, const V& v, int b, double delt
 }
 template <class V>
 CCMI_HD bool resGettingMoreBalanced(const DevGoal& g, const V& v, int sb, double delta, int db) {
-  const int res = g.resource;
+  const int res = uniform(g.resource);
   const double sc = v.bcap(sb, res), dc = v.bcap(db, res);
   const double prevDiff = (v.bu(sb, res) / sc) - (v.bu(db, res) / dc);
   const double nextDiff = prevDiff + (delta / sc) + (delta / dc);
@@ -112,7 +123,7 @@ CCMI_HD bool resGettingMoreBalanced(const DevGoal& g, const V& v, int sb, double
 // isSwapViolatingContainerLimit (:1005-1037) for the broker container, or with `host` the brokers' hosts
 template <class V>
 CCMI_HD bool resSwapContainerViolating(const DevGoal& g, const V& v, double delta, int sb, int db, bool host) {
-  const int res = g.resource;
+  const int res = uniform(g.resource);
   const double su = host ? v.hu(sb, res) : v.bu(sb, res), du = host ? v.hu(db, res) : v.bu(db, res);
   const double sc = host ? v.hcap(sb, res) : v.bcap(sb, res), dc = host ? v.hcap(db, res) : v.bcap(db, res);
   bool underUpper;
@@ -128,14 +139,14 @@ CCMI_HD bool resSwapContainerViolating(const DevGoal& g, const V& v, double delt
 template <class V>
 CCMI_HD bool resSwapViolating(const DevGoal& g, const V& v, double delta, int sb, int db) {
   const bool broker = resSwapContainerViolating(g, v, delta, sb, db, false);
-  if (!broker || !isHostRes(g.resource) || !v.hostMode()) return broker;
+  if (!broker || !isHostRes(uniform(g.resource)) || !v.hostMode()) return broker;
   return resSwapContainerViolating(g, v, delta, sb, db, true);
 }
 
 template <class V>
 CCMI_HD bool resAcceptMove(const DevGoal& g, const V& v, int action, int r, int src, int dst) {
-  if (action == DA_LEADERSHIP && (g.resource == 3 /*DISK*/ || g.resource == 1 /*NW_IN*/)) return true;
-  const double ru = v.ru(r, g.resource);
+  if (action == DA_LEADERSHIP && (uniform(g.resource) == 3 /*DISK*/ || uniform(g.resource) == 1 /*NW_IN*/)) return true;
+  const double ru = v.ru(r, uniform(g.resource));
   const bool srcExcluded = !v.allowed(g.allowedSlot, src);
   const bool srcAboveLower = resAboveLowerAfter(g, v, src, 0.0, true);
   const bool dstUnderUpper = resUnderUpperAfter(g, v, dst, 0.0, false, g.upperThr);
@@ -151,7 +162,7 @@ CCMI_HD bool resAcceptMove(const DevGoal& g, const V& v, int action, int r, int 
 // swap: source replica sr on sb, destination replica dr on db. Returns ccmi_acceptance (0 accept, 1 replica reject).
 template <class V>
 CCMI_HD int resAcceptSwap(const DevGoal& g, const V& v, int sr, int sb, int dr, int db) {
-  const double delta = v.ru(dr, g.resource) - v.ru(sr, g.resource);
+  const double delta = v.ru(dr, uniform(g.resource)) - v.ru(sr, uniform(g.resource));
   if (delta == 0) return 0;
   const bool both = delta > 0
                         ? (resAboveLowerAfter(g, v, db, 0.0, true) && resUnderUpperAfter(g, v, sb, 0.0, false, g.upperThr))
@@ -231,7 +242,7 @@ CCMI_HD int minLeadAcceptSwap(const V& v, int sr, int sb, int dr, int db) {
 // check for a broker resource
 template <class V>
 CCMI_HD bool capUnderAfterAdding(const DevGoal& g, const V& v, int b, double u) {
-  const int res = g.resource;
+  const int res = uniform(g.resource);
   if (!v.hostMode()) {  // one check: the host check of a host-only resource keeps its NaN behaviour
     const double x = v.bu(b, res) + u, lim = v.bcap(b, res) * g.capThr;
     return isBrokerRes(res) ? x < lim : !(x >= lim);
@@ -329,7 +340,7 @@ CCMI_HD bool lbiAcceptMove(const DevGoal& g, const V& v, int action, int r, int 
 // ---------------------------------------------------------------- dispatch
 template <class V>
 CCMI_HD bool goalAcceptMove(const DevGoal& g, const V& v, int action, int r, int src, int dst) {
-  switch (g.kind) {
+  switch (uniform(g.kind)) {
     case DG_REPLICA_DISTRIBUTION: return rdAccept(g, v, action, src, dst);
     case DG_RESOURCE_DISTRIBUTION: return resAcceptMove(g, v, action, r, src, dst);
     case DG_RACK_AWARE: return action == DA_LEADERSHIP || !rackViolates(v, r, dst);
@@ -338,8 +349,8 @@ CCMI_HD bool goalAcceptMove(const DevGoal& g, const V& v, int action, int r, int
     case DG_MIN_TOPIC_LEADERS: return minLeadAcceptMove(v, r, src);
     case DG_REPLICA_CAPACITY: return action == DA_LEADERSHIP || (int64_t)v.nrep(dst) < g.maxReplicas;
     case DG_CAPACITY:
-      if (action == DA_LEADERSHIP && (g.resource == 3 /*DISK*/ || g.resource == 1 /*NW_IN*/)) return true;
-      return capUnderAfterAdding(g, v, dst, v.ru(r, g.resource));
+      if (action == DA_LEADERSHIP && (uniform(g.resource) == 3 /*DISK*/ || uniform(g.resource) == 1 /*NW_IN*/)) return true;
+      return capUnderAfterAdding(g, v, dst, v.ru(r, uniform(g.resource)));
     case DG_POTENTIAL_NW_OUT: return potAcceptMove(g, v, action, r, src, dst);
     case DG_TOPIC_REPLICA_DISTRIBUTION: return topicAcceptMove(g, v, action, r, src, dst);
     case DG_LEADER_REPLICA_DISTRIBUTION: return leadAcceptMove(g, v, action, r, src, dst);
@@ -350,7 +361,7 @@ CCMI_HD bool goalAcceptMove(const DevGoal& g, const V& v, int action, int r, int
 }
 template <class V>
 CCMI_HD bool goalSelfSatisfiedMove(const DevGoal& g, const V& v, int action, int r, int src, int dst) {
-  switch (g.kind) {
+  switch (uniform(g.kind)) {
     case DG_REPLICA_DISTRIBUTION:
       if (g.fixOffline && currentOffline(v, r)) return true;
       return rdAccept(g, v, action, src, dst);
@@ -365,7 +376,7 @@ CCMI_HD bool goalSelfSatisfiedMove(const DevGoal& g, const V& v, int action, int
       return v.tlead(t, src) > v.tMinLead(t);
     }
     case DG_REPLICA_CAPACITY: return (int64_t)v.nrep(dst) < g.maxReplicas;
-    case DG_CAPACITY: return capUnderAfterAdding(g, v, dst, v.ru(r, g.resource));
+    case DG_CAPACITY: return capUnderAfterAdding(g, v, dst, v.ru(r, uniform(g.resource)));
     case DG_POTENTIAL_NW_OUT: return potSelfSatisfiedMove(g, v, action, r, dst);
     case DG_TOPIC_REPLICA_DISTRIBUTION:
       if (g.fixOffline && currentOffline(v, r)) return action == DA_MOVE;
@@ -380,13 +391,13 @@ CCMI_HD bool goalSelfSatisfiedMove(const DevGoal& g, const V& v, int action, int
     default: return true;
   }
   if (g.fixOffline && currentOffline(v, r)) return action == DA_MOVE;
-  const double ru = v.ru(r, g.resource);
+  const double ru = v.ru(r, uniform(g.resource));
   return resUnderUpperAfter(g, v, dst, ru, true, g.upperThr) && resAboveLowerAfter(g, v, src, ru, false);
 }
 // returns 0 ACCEPT, 1 REPLICA_REJECT, 2 BROKER_REJECT
 template <class V>
 CCMI_HD int goalAcceptSwap(const DevGoal& g, const V& v, int sr, int sb, int dr, int db) {
-  switch (g.kind) {
+  switch (uniform(g.kind)) {
     case DG_RESOURCE_DISTRIBUTION: return resAcceptSwap(g, v, sr, sb, dr, db);
     case DG_RACK_AWARE:
       if (rackViolates(v, sr, db)) return 2;
@@ -397,7 +408,7 @@ CCMI_HD int goalAcceptSwap(const DevGoal& g, const V& v, int sr, int sb, int dr,
     case DG_BROKER_SET_AWARE: return bsetAcceptSwap(v, sr, sb, dr, db);
     case DG_MIN_TOPIC_LEADERS: return minLeadAcceptSwap(v, sr, sb, dr, db);
     case DG_CAPACITY: {
-      const double su = v.ru(sr, g.resource), du = v.ru(dr, g.resource);
+      const double su = v.ru(sr, uniform(g.resource)), du = v.ru(dr, uniform(g.resource));
       const double delta = du - su;
       return (delta > 0 ? capUnderAfterAdding(g, v, sb, delta) : capUnderAfterAdding(g, v, db, -delta)) ? 0 : 1;
     }
@@ -445,12 +456,12 @@ CCMI_HD int goalAcceptSwap(const DevGoal& g, const V& v, int sr, int sb, int dr,
 }
 template <class V>
 CCMI_HD bool goalSelfSatisfiedSwap(const DevGoal& g, const V& v, int sr, int sb, int dr, int db) {
-  if (g.kind == DG_REPLICA_DISTRIBUTION) {
+  if (uniform(g.kind) == DG_REPLICA_DISTRIBUTION) {
     if (g.fixOffline && currentOffline(v, sr)) return true;
     return true;  // rdAccept(SWAP) == ACCEPT
   }
   if (g.fixOffline && currentOffline(v, sr)) return false;  // action != INTER_BROKER_REPLICA_MOVEMENT
-  const double delta = v.ru(dr, g.resource) - v.ru(sr, g.resource);
+  const double delta = v.ru(dr, uniform(g.resource)) - v.ru(sr, uniform(g.resource));
   return delta != 0 && !resSwapViolating(g, v, delta, sb, db);
 }
 
@@ -458,11 +469,12 @@ CCMI_HD bool goalSelfSatisfiedSwap(const DevGoal& g, const V& v, int sr, int sb,
 // legit && selfSatisfied && every optimized goal ACCEPTs.
 template <class V>
 CCMI_HD bool moveCandidateAccepted(const DevProgram& prog, const V& v, int r, int dst) {
-  const int action = prog.action;
+  const int action = uniform(prog.action);
   const int src = v.rbroker(r);
   if (!legitMove(v, r, dst, action)) return false;
   if (!goalSelfSatisfiedMove(prog.goals[0], v, action, r, src, dst)) return false;
-  for (int i = 1; i < prog.nGoals; ++i)
+  const int nGoals = uniform(prog.nGoals);
+  for (int i = 1; i < nGoals; ++i)
     if (!goalAcceptMove(prog.goals[i], v, action, r, src, dst)) return false;
   return true;
 }
@@ -503,7 +515,8 @@ CCMI_HD int swapCandidateOutcome(const DevProgram& prog, const V& v, int sr, int
   if (!legitMove(v, sr, db, DA_MOVE)) return 2;
   if (!legitMove(v, dr, sb, DA_MOVE)) return 0;
   if (!goalSelfSatisfiedSwap(prog.goals[0], v, sr, sb, dr, db)) return 2;
-  for (int i = 1; i < prog.nGoals; ++i) {
+  const int nGoals = uniform(prog.nGoals);
+  for (int i = 1; i < nGoals; ++i) {
     const int acc = goalAcceptSwap(prog.goals[i], v, sr, sb, dr, db);
     if (acc == 1) return 0;
     if (acc == 2) return 2;

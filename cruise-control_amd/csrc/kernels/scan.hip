@@ -877,12 +877,26 @@ __device__ __forceinline__ void chainRackRowsRun(const DevTables& T, const Chain
                                  const int32_t* __restrict__ cands, int N, int32_t* __restrict__ log,
                                  ChainResultDev* __restrict__ out);
 
+// The scan server's LDS objects at namespace scope: the kernel and its out-of-line chain body name the same objects
+// directly, so no LDS address is passed across the call.
+__shared__ OverlayLds gSrvOv;
+__shared__ DevProgram gSrvProg;
+alignas(8) __shared__ unsigned char gSrvScRaw[2 * sizeof(LoadVec)];  // a chain's leadership hand-over (LoadVec has a
+                                                                      // member initializer)
+
 // SOP_CHAIN on workgroup 0: the command's rows and the host's load / slot rows into the tables, the request into HBM
 // (the chain rereads it per decision), then the chain itself on an empty overlay. Every write of the chain is a plain
 // store of this workgroup; the caller releases them (system scope: the log is host-mapped) before the publish.
-__device__ __forceinline__ void serverChain(const DevTables& T, const ChainTables& C, const MutTables& Mt,
-                                            const DevProgram& prog, const ServerCmd& c, const char* __restrict__ pay,
-                                            const UpdateList& U, OverlayLds& ov, LoadVec* sc) {
+// Out of line (noinline): the chain bodies (K7 evaluation + apply) are several times the size of the scan paths, and
+// inlined they made the server's code ~3.5x larger and its scan commands ~50 % slower on gfx950 (same-box A/B).
+__device__ __attribute__((noinline)) void serverChain(const DevTables T, const ChainTables C, const MutTables Mt,
+                                                      const ServerCmd c, const char* __restrict__ pay) {
+  OverlayLds& ov = gSrvOv;
+  const DevProgram& prog = gSrvProg;
+  LoadVec* sc = reinterpret_cast<LoadVec*>(gSrvScRaw);
+  UpdateList U;
+  U.tdel = (const TopicCountDelta*)(pay + c.oT);
+  U.nt = c.nt;
   applyRowsCoherent(Mt, ov.b, ov.nb, ov.r, ov.nr, ov.p, ov.np, threadIdx.x, blockDim.x);
   for (int i = threadIdx.x; i < U.nt; i += blockDim.x) {
     TopicCountDelta d;
@@ -926,13 +940,11 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, kServ
                                                       unsigned long long* __restrict__ mail,
                                                       unsigned long long* __restrict__ t0,
                                                       unsigned long long startSeq) {
-  __shared__ OverlayLds ov;
-  __shared__ DevProgram prog;
+  OverlayLds& ov = gSrvOv;
+  DevProgram& prog = gSrvProg;
   __shared__ ServerCmd c;
   __shared__ int sExit;
   __shared__ SegEntry sSeg[kMaxSegs + 1];
-  __shared__ alignas(8) unsigned char scRaw[2 * sizeof(LoadVec)];  // a chain's leadership hand-over (LoadVec has a
-                                                                     // member initializer)
   unsigned long long last = startSeq;
   int progVer = -1;
   int acqEpoch = -1;  // ServerCmd.rowsEpoch of this workgroup's last acquire (-1: none since the launch)
@@ -1038,7 +1050,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, kServ
     const int32_t* C = (const int32_t*)(pay + c.oC);
     if (c.op == SOP_CHAIN) {
       stage();
-      serverChain(T, Ch, Mt, prog, c, pay, U, ov, reinterpret_cast<LoadVec*>(scRaw));
+      serverChain(T, Ch, Mt, c, pay);
       // every wave's stores complete, then one system-scope release: the records and loads for the other XCDs' next
       // acquire, the log and result for the host (MI355X_MICROARCH.md, inter-workgroup visibility)
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
