@@ -22,7 +22,9 @@ action log, final assignment and leaders, per-goal results, every goal's stats w
 
 Multi-GPU (torchrun, one process per GPU): by default every rank runs its own independent what-if proposal
 request (weak scaling, no data-path collective); timing is max over ranks. --sharded instead shards ONE proposal's
-candidate space by destination broker over the ranks (one RCCL MIN allreduce per scan, strong scaling).
+candidate space by destination broker over the ranks (strong scaling): every scan's per-rank first-fit keys are
+MIN-combined in host shared memory (--combiner shm, the default on one node: no GPU work per combine, so every rank
+keeps its scan server) or by an RCCL MIN allreduce (--combiner rccl).
 
 Roofline: the dominant kernels are the candidate scans (scan_cross / scan_pairs / scan_swap / chain_pairs /
 chain_rack_rows). Their HIP-event duration is measured during the warmup proposal(s) (events on the engine stream,
@@ -296,8 +298,10 @@ def main() -> None:
     ap.add_argument("--requests-per-gpu", type=int, default=1,
                     help="S concurrent what-if proposals per GPU in every step (one host thread + HIP stream per "
                          "session; the precompute pool of GoalOptimizer.java:117-119). Default 1: one proposal per step")
+    ap.add_argument("--combiner", choices=("shm", "rccl"), default="shm",
+                    help="--sharded: the per-scan MIN combiner (host shared memory on one node, or RCCL)")
     ap.add_argument("--sharded", action="store_true",
-                    help="N>1: one proposal sharded by destination broker over all ranks (RCCL MIN per scan) "
+                    help="N>1: one proposal sharded by destination broker over all ranks (a MIN combine per scan) "
                          "instead of one independent what-if proposal per rank")
     args = ap.parse_args()
 
@@ -316,7 +320,7 @@ def main() -> None:
     if world > 1:
         dist.init_process_group("gloo" if over_gloo else "nccl", init_method="env://")
     if over_gloo and args.sharded:
-        raise SystemExit("--sharded needs one GPU per rank (the RCCL combiner)")
+        raise SystemExit("--sharded needs one GPU per rank (each rank's scan server / RCCL combiner holds its GPU)")
 
     lib = ccmi.Library.get()
     props, goal_names, workload_name = WORKLOADS[args.workload]
@@ -326,15 +330,21 @@ def main() -> None:
     opt = ccmi.GoalOptimizer(workload_constraint(args.workload))
     sharded = args.sharded and world > 1
     uid = None
-    if sharded:  # rank 0's RCCL id reaches the other ranks over the default process group
-        obj = [ccmi.rccl_unique_id(lib) if rank == 0 else None]
+    if sharded:  # rank 0's RCCL id / shared-memory name reaches the other ranks over the default process group
+        obj = [(ccmi.rccl_unique_id(lib) if args.combiner == "rccl" else f"/ccmi_bench_{os.getpid()}_{int(time.time())}")
+               if rank == 0 else None]
         dist.broadcast_object_list(obj, src=0)
         uid = obj[0]
 
+    shm_sessions = [0]
+
     def session():
         s = ccmi.ClusterModel.from_buffers(buf, device=device)
-        if sharded:
+        if sharded and args.combiner == "rccl":
             s.attach_rccl(rank, world, uid)
+        elif sharded:  # one block per session (every rank creates its sessions in the same order)
+            shm_sessions[0] += 1
+            s.attach_shm(rank, world, f"{uid}_{shm_sessions[0]}")
         return s
 
     # Warmup proposals double as the instrumented pass: HIP events around every launched scan kernel and the scan
@@ -444,7 +454,7 @@ def main() -> None:
         "config": {"workload": workload_name,
                    "brokers": buf.desc.num_brokers, "replicas": buf.desc.num_replicas,
                    "partitions": buf.desc.num_partitions, "topics": buf.desc.num_topics,
-                   "goals": goal_names, "parallelism": (f"destination-sharded x{world} (RCCL MIN allreduce per scan)" if sharded
+                   "goals": goal_names, "parallelism": (f"destination-sharded x{world} ({args.combiner} MIN combine per scan)" if sharded
                                    else f"independent what-if per GPU x{world}")},
         "parity": parity,
         "requests_per_gpu": S,

@@ -213,7 +213,7 @@ class DeviceError(CruiseControlError):
 _STATUS = {1: IllegalArgumentException, 2: DeviceError, 3: OptimizationFailureException, 4: IllegalStateException,
            5: UnsupportedOperationException}
 
-ABI_VERSION = 8  # CCMI_ABI_VERSION of include/ccmi.h
+ABI_VERSION = 9  # CCMI_ABI_VERSION of include/ccmi.h
 EXPORTED_SYMBOLS = (
     "ccmi_last_error", "ccmi_abi_version", "ccmi_device_count", "ccmi_default_constraint", "ccmi_default_random_cluster_props",
     "ccmi_random_cluster", "ccmi_cluster_buffers_desc", "ccmi_cluster_buffers_free", "ccmi_session_create",
@@ -223,6 +223,7 @@ EXPORTED_SYMBOLS = (
     "ccmi_leader_distribution", "ccmi_replica_disks", "ccmi_proposal_count", "ccmi_proposals",
     "ccmi_proposal_disks", "ccmi_perf", "ccmi_perf_reset",
     "ccmi_set_kernel_timing", "ccmi_session_set_shard", "ccmi_rccl_unique_id", "ccmi_session_attach_rccl",
+    "ccmi_session_attach_shm",
     "ccmi_topic_broker_set",
     "ccmi_builder_create", "ccmi_builder_destroy", "ccmi_builder_create_broker", "ccmi_builder_add_disk",
     "ccmi_builder_populate_partition", "ccmi_builder_set_broker_state", "ccmi_builder_set_disk_state",
@@ -293,6 +294,7 @@ class Library:
         L.ccmi_session_set_shard.argtypes = [C.c_void_p, C.c_int32, C.c_int32, AllreduceMinFn, C.c_void_p]
         L.ccmi_rccl_unique_id.argtypes = [C.POINTER(C.c_uint8)]
         L.ccmi_session_attach_rccl.argtypes = [C.c_void_p, C.c_int32, C.c_int32, C.POINTER(C.c_uint8)]
+        L.ccmi_session_attach_shm.argtypes = [C.c_void_p, C.c_int32, C.c_int32, C.c_char_p]
         L.ccmi_default_constraint.argtypes = [C.POINTER(ConstraintStruct)]
         L.ccmi_topic_broker_set.restype = C.c_int32
         L.ccmi_topic_broker_set.argtypes = [C.c_char_p, C.c_int32]
@@ -1228,6 +1230,11 @@ class ClusterModel:
         """Destination-sharded mode over the built-in RCCL combiner (one int64 MIN allreduce per scan)."""
         buf = (C.c_uint8 * 128).from_buffer_copy(unique_id)
         self.lib.check(self.lib.lib.ccmi_session_attach_rccl(self.handle, rank, count, buf))
+
+    def attach_shm(self, rank: int, count: int, name: str) -> None:
+        """Destination-sharded mode over the built-in host shared-memory combiner (ranks on one node): one int64 MIN
+        per scan in a POSIX shared-memory block; the scan server stays on."""
+        self.lib.check(self.lib.lib.ccmi_session_attach_shm(self.handle, rank, count, name.encode()))
 
 
 def rccl_unique_id(lib: Optional["Library"] = None) -> bytes:

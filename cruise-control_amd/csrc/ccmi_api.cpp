@@ -13,17 +13,22 @@
 #include "engine/model.h"
 #include "engine/prof.h"
 #include "engine/shard_rccl.h"
+#include "engine/shard_shm.h"
 
 namespace ccmi {
 ccmi_cluster_buffers* generateRandomCluster(const ccmi_random_cluster_props& p);
 }
 
 struct ccmi_session {
-  ~ccmi_session() { ccmi::rcclDestroy(rccl); }
+  ~ccmi_session() {
+    ccmi::rcclDestroy(rccl);
+    ccmi::shmDestroy(shm);
+  }
   ccmi::Model model;
   std::unique_ptr<ccmi::Device> device;
   std::unique_ptr<ccmi::Engine> engine;
   ccmi::RcclShard* rccl = nullptr;
+  ccmi::ShmShard* shm = nullptr;
   int deviceOrdinal = 0;
   std::vector<int32_t> initDist, initLeaders;  // for ExecutionProposal diffs
   std::vector<int32_t> initDisks, initLeaderDisks;  // the logdir half of ReplicaPlacementInfo (JBOD)
@@ -395,6 +400,19 @@ ccmi_status ccmi_session_attach_rccl(ccmi_session* s, int32_t rank, int32_t coun
     s->rccl = ccmi::rcclCreate(s->deviceOrdinal, rank, count, unique_id);
     s->engine->shard = ccmi::Shard{rank, count, &ccmi::rcclMin, s->rccl};
     s->device->setServerAllowed(false);  // the collective kernels must not queue behind a resident server
+    return CCMI_OK;
+  });
+}
+
+ccmi_status ccmi_session_attach_shm(ccmi_session* s, int32_t rank, int32_t count, const char* name) {
+  return guarded([&] {
+    if (!s || !name) throw std::invalid_argument("null argument");
+    if (count < 1 || rank < 0 || rank >= count) throw std::invalid_argument("shard rank out of range");
+    ccmi::shmDestroy(s->shm);
+    s->shm = nullptr;
+    s->shm = ccmi::shmCreate(name, rank, count);
+    s->engine->shard = ccmi::Shard{rank, count, &ccmi::shmMin, s->shm};
+    s->device->setServerAllowed(true);  // the combine is host memory only: the scan server stays resident
     return CCMI_OK;
   });
 }

@@ -176,7 +176,7 @@ Device::~Device() {
     std::vector<unsigned long long> h(1024 * 8 + 16);
     if (hipMemcpy(h.data(), stamps_, h.size() * 8, hipMemcpyDeviceToHost) == hipSuccess) {
       if (h[8192])
-        std::fprintf(stderr, "[ccmi server stamps] %llu commands: copy+acquire %.2f us, stage %.2f us, first tile "
+        std::fprintf(stderr, "[ccmi server stamps] %llu scan commands: copy+acquire %.2f us, stage %.2f us, first tile "
                              "%.2f us, rest to arrival %.2f us (workgroup 0)\n",
                      h[8192], h[8193] * 0.01 / h[8192], h[8194] * 0.01 / h[8192], h[8195] * 0.01 / h[8192],
                      h[8196] * 0.01 / h[8192]);
@@ -563,6 +563,8 @@ DevTables Device::tables() const {
   t.R = R_;
   t.P = P_;
   t.ldB = ldB_;
+  static const int pollMode = std::getenv("CCMI_SERVER_POLL") ? std::atoi(std::getenv("CCMI_SERVER_POLL")) : 0;
+  t.pollMode = pollMode;
   return t;
 }
 

@@ -163,6 +163,8 @@ struct DevTables {
   // null unless brokers share a host — then every host value is the broker's own and the predicates read those
   const double* hostCap;
   int32_t B, R, P, ldB;
+  // scan server idle poll (CCMI_SERVER_POLL): 0 = back off (s_sleep 4, then 16 after 256 polls), 1 = spin, 2 = s_sleep 1
+  int32_t pollMode;
 };
 
 // Row updates the host flushes to the device before a scan (only rows touched since the last flush).

@@ -980,7 +980,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, kServ
         }
         // back off once the host has been away for a while (its own phases between commands): fewer polls of the
         // command word from every workgroup, at most ~0.4 us more latency for the command that ends the wait
-        if (spin < 256) __builtin_amdgcn_s_sleep(4);
+        if (T.pollMode == 1) continue;
+        if (T.pollMode == 2) __builtin_amdgcn_s_sleep(1);
+        else if (spin < 256) __builtin_amdgcn_s_sleep(4);
         else __builtin_amdgcn_s_sleep(16);
       }
       SRV_STAMP(T, 0);
@@ -1175,7 +1177,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, kServ
     if (threadIdx.x == 0) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       const unsigned int prev = __hip_atomic_fetch_add(done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (T.stamps && blockIdx.x == 0) {
+      if (T.stamps && blockIdx.x == 0 && c.op != SOP_CHAIN) {  // scan commands (chains have their own stamps)
         srvT[4] = __builtin_amdgcn_s_memrealtime();
         atomicAdd(&T.stamps[8192 + 0], 1ull);
         for (int i = 0; i < 4; ++i) atomicAdd(&T.stamps[8192 + 1 + i], srvT[i + 1] - srvT[i]);

@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define CCMI_ABI_VERSION 8
+#define CCMI_ABI_VERSION 9
 
 typedef enum ccmi_status {
   CCMI_OK = 0,
@@ -483,6 +483,10 @@ typedef int (*ccmi_allreduce_min_fn)(void* ctx, int64_t* key);
 ccmi_status ccmi_session_set_shard(ccmi_session* s, int32_t rank, int32_t count, ccmi_allreduce_min_fn fn, void* ctx);
 ccmi_status ccmi_rccl_unique_id(uint8_t out[128]);
 ccmi_status ccmi_session_attach_rccl(ccmi_session* s, int32_t rank, int32_t count, const uint8_t unique_id[128]);
+/* ABI v9. ccmi_session_attach_shm: the built-in combiner for ranks on one node — a MIN over one int64 per rank in a
+ * POSIX shared-memory block `name` ("/name"; rank 0 creates it, the others open it, and every rank waits until all
+ * `count` ranks are attached, at most 120 s). No GPU work per combine, so the session keeps its scan server. */
+ccmi_status ccmi_session_attach_shm(ccmi_session* s, int32_t rank, int32_t count, const char* name);
 
 /* Measurement hooks used by bench.py: device time of the last optimization's scan kernels (HIP events
  * on the engine stream) and their algorithmic bytes. */

@@ -49,6 +49,56 @@ def test_sharded_scans_match_unsharded_and_oracle(emu_lib, oracle_lib, tmp_path,
     assert [tuple(g) for g in outs[0]["goals"]] == [(r.name, r.succeeded, r.candidates, r.actions) for r in ores]
 
 
+@pytest.mark.parametrize("world", [2, 3])
+def test_shm_combiner_matches_oracle(emu_lib, oracle_lib, tmp_path, world):
+    """The built-in host shared-memory combiner (ccmi_session_attach_shm, shard_shm.cpp): every rank makes the
+    oracle's decisions with the same reference-equivalent candidate counts."""
+    import shard_worker
+
+    props = dict(num_racks=5, num_brokers=20, num_replicas=6000, num_topics=300)
+    goals = list(ccmi.DEFAULT_GOALS)
+    mp.start_processes(shard_worker.run, args=(world, _free_port(), props, goals, 1.05, str(tmp_path), emu_lib.path,
+                                               "shm"), nprocs=world, join=True, start_method="spawn")
+    outs = [json.load(open(tmp_path / f"rank{r}.json")) for r in range(world)]
+    buf = ccmi.RandomCluster.generate(emu_lib, **props)
+    oc = OracleCluster.from_desc(buf.desc)
+    ores = oc.optimize(goals, constraint(1.05))
+    for o in outs:
+        assert o["error"] is None and o["combines"] > 0
+        assert [tuple(a) for a in o["actions"]] == oc.actions()
+        assert [tuple(g) for g in o["goals"]] == [(r.name, r.succeeded, r.candidates, r.actions) for r in ores]
+
+
+def test_shm_combiner_rejects_bad_arguments(emu_lib):
+    buf = ccmi.RandomCluster.generate(emu_lib, num_racks=3, num_brokers=6, num_replicas=60, num_topics=5)
+    cm = ccmi.ClusterModel.from_buffers(buf, device=0)
+    with pytest.raises(ccmi.IllegalArgumentException):
+        cm.attach_shm(2, 2, "/ccmi_bad_rank")
+    with pytest.raises(ccmi.IllegalArgumentException):
+        cm.attach_shm(0, 1, "no_leading_slash")
+
+
+@pytest.mark.gpu
+def test_gpu_shm_combiner_keeps_scan_server(gpu_lib, oracle_lib, tmp_path):
+    """Two shard processes on the gfx950 device over the shared-memory combiner: both keep their scan server (64
+    workgroups each, so both are resident on one card) and make the oracle's decisions."""
+    import shard_worker
+
+    props = dict(num_racks=5, num_brokers=20, num_replicas=6000, num_topics=300)
+    goals = list(ccmi.DEFAULT_GOALS)
+    mp.start_processes(shard_worker.run, args=(2, _free_port(), props, goals, 1.05, str(tmp_path), gpu_lib.path,
+                                               "shm", {"CCMI_SERVER_BLOCKS": "64"}),
+                       nprocs=2, join=True, start_method="spawn")
+    outs = [json.load(open(tmp_path / f"rank{r}.json")) for r in range(2)]
+    buf = ccmi.RandomCluster.generate(gpu_lib, **props)
+    oc = OracleCluster.from_desc(buf.desc)
+    ores = oc.optimize(goals, constraint(1.05))
+    for o in outs:
+        assert o["error"] is None and o["combines"] > 0 and o["server_launches"] > 0
+        assert [tuple(a) for a in o["actions"]] == oc.actions()
+        assert [tuple(g) for g in o["goals"]] == [(r.name, r.succeeded, r.candidates, r.actions) for r in ores]
+
+
 @pytest.mark.gpu
 def test_gpu_sharded_scans_match_oracle(gpu_lib, oracle_lib, tmp_path):
     """Two shard processes on the gfx950 device (gloo combiner): the kernels' column / pair slices with global

@@ -2,7 +2,6 @@
 # The C2 probe under several environments on one box (A/B on the same host): AB_ENVS="NAME:VAR=x,VAR2=y NAME2:..."
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out
-make -C cruise-control_amd -j16 > gpurun_out/make.log 2>&1 || exit 1
 for spec in ${AB_ENVS:-base:CCMI_PROFILE=1}; do
   name=${spec%%:*}; envs=${spec#*:}
   echo "== $name ($envs) $(date +%T)"
