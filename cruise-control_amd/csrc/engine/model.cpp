@@ -1,9 +1,6 @@
 // Host model: build from the flattened desc, exact mutations, sorted-replica tracking, dirty rows.
 #include "model.h"
 
-#include <atomic>
-#include <thread>
-
 #include <algorithm>
 #include <cstring>
 #include <stdexcept>
@@ -851,7 +848,6 @@ void Model::untrack(int b, int nameId) {
 }
 void Model::clearTracked() {
   for (int b = 0; b < B; ++b) tracked[b].clear();
-  prefetched_.clear();
 }
 void Model::clearTracked(int b) { tracked[b].clear(); }
 
@@ -938,54 +934,6 @@ bool Model::snapshotFromPrevious(int b, const Spec& s, std::vector<SortedCacheEn
   return true;
 }
 
-void Model::sortSnapshot(int b, const Spec& s, std::vector<std::pair<uint64_t, int32_t>>& keyed,
-                         std::vector<int32_t>& out) const {
-  keyed.clear();
-  for (int r : bRepl[b])
-    if (selects(s, r)) keyed.push_back({replicaKey(s, r), r});
-  std::sort(keyed.begin(), keyed.end());
-  out.clear();
-  out.reserve(keyed.size());
-  for (const auto& kr : keyed) out.push_back(kr.second);
-}
-
-void Model::prefetchSnapshots(const Spec& s) {
-  const char* e = std::getenv("CCMI_HOST_THREADS");  // read per call (a few per goal)
-  const int hw = (int)std::max(1u, std::thread::hardware_concurrency());
-  const int threads = std::max(1, std::min(e ? std::atoi(e) : 8, hw));
-  if (threads <= 1 || B < 256) return;
-  PhaseScope ps(PH_SORTED_INIT);
-  // brokers the cache serves neither directly nor by derivation from an earlier version
-  std::vector<int32_t> todo;
-  for (int b = 0; b < B; ++b) {
-    const auto& cache = sortedCache[b];
-    bool have = false;
-    for (const auto& c : cache)
-      if (c.spec == s && c.v && (c.ver == bVer[b] || (c.ver < bVer[b] && bVer[b] - c.ver <= kDeltaLog))) have = true;
-    if (!have) todo.push_back(b);
-  }
-  if (todo.size() < 64) return;
-  std::vector<std::shared_ptr<std::vector<int32_t>>> out(todo.size());
-  std::atomic<size_t> next{0};
-  auto work = [&]() {
-    std::vector<std::pair<uint64_t, int32_t>> keyed;
-    for (;;) {
-      const size_t i0 = next.fetch_add(64, std::memory_order_relaxed);
-      if (i0 >= todo.size()) return;
-      for (size_t i = i0; i < std::min(todo.size(), i0 + 64); ++i) {
-        auto v = std::make_shared<std::vector<int32_t>>();
-        sortSnapshot(todo[i], s, keyed, *v);
-        out[i] = std::move(v);
-      }
-    }
-  };
-  std::vector<std::thread> pool;
-  for (int t = 1; t < threads; ++t) pool.emplace_back(work);
-  work();
-  for (auto& t : pool) t.join();
-  for (size_t i = 0; i < todo.size(); ++i) cachePut(sortedCache[todo[i]], bVer[todo[i]], s, std::move(out[i]));
-}
-
 std::shared_ptr<const std::vector<int32_t>> Model::snapshot(int b, const Spec& s) {
   const bool limited = s.selAboveRes >= 0 || s.selBelowRes >= 0;
   auto& cache = limited ? filteredCache[b] : sortedCache[b];
@@ -1005,15 +953,16 @@ std::shared_ptr<const std::vector<int32_t>> Model::snapshot(int b, const Spec& s
   } else {
     const bool derived = snapshotFromPrevious(b, s, cache, *v);
     static const bool check = std::getenv("CCMI_SNAPSHOT_CHECK") != nullptr;  // tests: derived == re-sorted
-    if (!derived && !check && std::find(prefetched_.begin(), prefetched_.end(), s) == prefetched_.end()) {
-      prefetched_.push_back(s);
-      prefetchSnapshots(s);
-      if (auto* hit = cacheFind(cache, bVer[b], s)) return *hit;
-    }
     if (!derived || check) {
       PhaseScope ps(PH_SORTED_INIT);
+      std::vector<std::pair<uint64_t, int32_t>>& keyed = snapKeys_;
+      keyed.clear();
+      for (int r : bRepl[b])
+        if (selects(s, r)) keyed.push_back({replicaKey(s, r), r});
+      std::sort(keyed.begin(), keyed.end());
       std::vector<int32_t> full;
-      sortSnapshot(b, s, snapKeys_, full);
+      full.reserve(keyed.size());
+      for (const auto& kr : keyed) full.push_back(kr.second);
       if (derived && full != *v) throw std::logic_error("snapshot derived from the previous version differs");
       *v = std::move(full);
     }

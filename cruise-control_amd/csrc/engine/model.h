@@ -347,13 +347,6 @@ class Model {
   // the live view of a set tracked earlier, because every key change re-inserts the replica.
   std::shared_ptr<const std::vector<int32_t>> snapshot(int b, const Spec& s);
   bool snapshotFromPrevious(int b, const Spec& s, std::vector<SortedCacheEntry>& cache, std::vector<int32_t>& out);
-  // The first full sort of a limit-free Spec since the last clearTracked() sorts that Spec for every broker the cache
-  // cannot serve, on CCMI_HOST_THREADS helper threads (default 8; 1 = off): each broker's sort is a pure function of
-  // its current state (memory-latency bound, ~100 replica gathers), and the results enter the cache at the broker's
-  // current version exactly as a lazy sort would have put them.
-  std::vector<Spec> prefetched_;
-  void prefetchSnapshots(const Spec& s);
-  void sortSnapshot(int b, const Spec& s, std::vector<std::pair<uint64_t, int32_t>>& keyed, std::vector<int32_t>& out) const;
   // One Spec's snapshots of every broker, looked up by broker id and version (no per-call cache search or
   // reference counting): the drivers that poll many brokers per scan (moveIn, swap) keep one per Spec.
   struct SnapTable {

@@ -126,13 +126,3 @@ BAD_DISK_CASES = [
 @pytest.mark.parametrize("props,goals", BAD_DISK_CASES)
 def test_emu_bad_disk_brokers_match_oracle(emu_lib, oracle_lib, props, goals):
     check_product_against_oracle(emu_lib, props, goals, 1.05, max_replicas=3000)
-
-
-@pytest.mark.parametrize("threads", ["1", "8"])
-def test_emu_snapshot_prefetch_matches_oracle(emu_lib, oracle_lib, monkeypatch, threads):
-    """Model::prefetchSnapshots (the first full sort of a Spec in a goal sorts every broker on helper threads) on a
-    cluster large enough to trigger it (>= 256 brokers): the same decisions as the oracle with and without it."""
-    monkeypatch.setenv("CCMI_HOST_THREADS", threads)
-    check_product_against_oracle(emu_lib, dict(num_racks=10, num_brokers=300, num_replicas=24000, num_topics=400),
-                                 ["ReplicaDistributionGoal", "DiskUsageDistributionGoal", "CpuUsageDistributionGoal",
-                                  "LeaderReplicaDistributionGoal"], 1.05)
