@@ -1321,6 +1321,14 @@ class ResourceDistribution : public GoalImpl {
     std::vector<int32_t> rank;
     auto materialise = [&]() {
       PhaseScope pi(PH_TREE_BUILD);
+      // CCMI_PROFILE: nanoseconds in the order construction (16), the put sequence (17) and the replay (18)
+      const bool tp = prof().on;
+      auto tnow = [] { return std::chrono::steady_clock::now(); };
+      auto ns = [](std::chrono::steady_clock::time_point a, std::chrono::steady_clock::time_point b) {
+        return (int64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(b - a).count();
+      };
+      auto t0 = tp ? tnow() : std::chrono::steady_clock::time_point();
+      auto t1 = t0;
       ovr = entryKey;
       if (useWorker) {
         cand.adopt(treeWorker->take());
@@ -1362,8 +1370,10 @@ class ResourceDistribution : public GoalImpl {
         ids.reserve(order.size());
         for (int x = 0; x < m.B; ++x)
           if (entryIn[x]) ids.push_back(x);
+        if (tp) t1 = tnow();
         cand.buildByRank(ids, rank);
       }
+      auto t2 = tp ? tnow() : t0;
       // the replay keeps no in-order sequence (each step would shift it); the replica-move form, which walks the set
       // in order for every candidate list, takes it once afterwards; the leadership form only searches the set
       cand.untrackSequence();
@@ -1377,6 +1387,11 @@ class ResourceDistribution : public GoalImpl {
         if (h.add) cand.add(h.dst);
       }
       if (action != DA_LEADERSHIP) cand.trackSequence();
+      if (tp) {
+        prof().count(16, "tree.ns.order", ns(t0, t1));
+        prof().count(17, "tree.ns.build", ns(t1, t2));
+        prof().count(18, "tree.ns.replay", ns(t2, tnow()));
+      }
       ovr.clear();
       built = true;
     };
