@@ -263,45 +263,94 @@ class IntraBroker {
     return true;
   }
 
-  // AbstractGoal.maybeMoveReplicaBetweenDisks
-  CCMI_LD int maybeMove(int i, const int32_t* cands, int n) {
-    for (int k = 0; k < n; ++k) {
-      const int t = cands[k];
-      ++cand;
-      if (!A.dAlive[t]) continue;  // legitMoveBetweenDisks (same broker by construction)
-      bool self;
-      if (A.goal == IG_CAPACITY) {
-        self = du(i) > 0 && underCap(t, du(i));
-      } else {
-        const double delta = -du(i);
-        self = delta != 0 && usageAccept(up, lo, A.eDisk[i], t, delta);
-      }
-      if (!self || !priorsAcceptMove(i, t)) continue;
-      relocate(i, t);
-      return t;
+  // One candidate of AbstractGoal.maybeMoveReplicaBetweenDisks: entry i to disk t accepted on the current state
+  CCMI_LD bool moveOk(int i, int t) const {
+    if (!A.dAlive[t]) return false;  // legitMoveBetweenDisks (same broker by construction)
+    bool self;
+    if (A.goal == IG_CAPACITY) {
+      self = du(i) > 0 && underCap(t, du(i));
+    } else {
+      const double delta = -du(i);
+      self = delta != 0 && usageAccept(up, lo, A.eDisk[i], t, delta);
     }
-    return -1;
+    return self && priorsAcceptMove(i, t);
+  }
+  // One candidate of AbstractGoal.maybeSwapReplicaBetweenDisks (usage goal): 0 continue, 1 swap, 2 return false
+  CCMI_LD int swapOutcome(int i, int j) const {
+    if (!A.dAlive[A.eDisk[j]]) return 2;
+    if (!A.dAlive[A.eDisk[i]]) return 0;
+    const double delta = du(j) - du(i);
+    if (!(delta != 0 && usageAccept(up, lo, A.eDisk[i], A.eDisk[j], delta))) return 2;
+    return priorsAcceptSwap(i, j) ? 1 : 0;
+  }
+  // The first q in [q0, n) whose candidate decides (moves: accepted; swaps: any outcome but 0), evaluated on the
+  // current state, or n; `out` = that outcome. On the device the broker's wavefront evaluates 64 candidates per step
+  // and a ballot picks the first (every lane then holds the same answer); on the host one at a time. Nothing changes
+  // state, so either way it is the candidate the sequential loop would stop at.
+#if defined(__HIP_DEVICE_COMPILE__)
+  template <class F>
+  __device__ int firstDeciding(int q0, int n, F outcome, int& out) const {
+    const int lane = threadIdx.x & 63;
+    for (int k0 = q0; k0 < n; k0 += 64) {
+      const int k = k0 + lane;
+      const int o = k < n ? outcome(k) : 0;
+      const uint64_t any = __ballot(o != 0);
+      if (any) {
+        const int first = __builtin_ctzll(any);
+        out = (__ballot(o == 1) >> first) & 1ull ? 1 : 2;
+        return k0 + first;
+      }
+    }
+    out = 0;
+    return n;
+  }
+#else
+  template <class F>
+  int firstDeciding(int q0, int n, F outcome, int& out) const {
+    for (int k = q0; k < n; ++k) {
+      const int o = outcome(k);
+      if (o != 0) {
+        out = o;
+        return k;
+      }
+    }
+    out = 0;
+    return n;
+  }
+#endif
+  // AbstractGoal.maybeMoveReplicaBetweenDisks: the first accepted candidate disk in cands[0, n)
+  CCMI_LD int maybeMove(int i, const int32_t* cands, int n) {
+    int o;
+    const int k = firstDeciding(0, n, [&](int q) { return moveOk(i, cands[q]) ? 1 : 0; }, o);
+    cand += k < n ? k + 1 : n;
+    if (k == n) return -1;
+    relocate(i, cands[k]);
+    return cands[k];
+  }
+  // The rows rows[s0, m) each tried against the single disk t (moveLoadIn / moveLoadOut): the first accepted row,
+  // moved, or m; one candidate per row visited
+  CCMI_LD int moveFirstRow(const int32_t* rows, int s0, int m, int t) {
+    int o;
+    const int s = firstDeciding(s0, m, [&](int q) { return moveOk(rows[q], t) ? 1 : 0; }, o);
+    cand += s < m ? s - s0 + 1 : m - s0;
+    if (s < m) relocate(rows[s], t);
+    return s;
   }
   // AbstractGoal.maybeSwapReplicaBetweenDisks (usage goal only)
   CCMI_LD bool maybeSwap(int i, const int32_t* cands, int n) {
-    for (int k = 0; k < n; ++k) {
-      const int j = cands[k];
-      ++cand;
-      if (!A.dAlive[A.eDisk[j]]) return false;
-      if (!A.dAlive[A.eDisk[i]]) continue;
-      const double delta = du(j) - du(i);
-      if (!(delta != 0 && usageAccept(up, lo, A.eDisk[i], A.eDisk[j], delta))) return false;
-      if (!priorsAcceptSwap(i, j)) continue;
-      const int t = A.eDisk[j];
-      relocate(i, t);
-      // the destination replica goes to sourceReplica.disk(), read after the first relocation: its own disk
-      const double u = du(j);
-      A.dUtil[t] -= u;
-      A.dUtil[t] += u;
-      record(A.eRep[j], t, t);
-      return true;
-    }
-    return false;
+    int o;
+    const int k = firstDeciding(0, n, [&](int q) { return swapOutcome(i, cands[q]); }, o);
+    cand += k < n ? k + 1 : n;
+    if (o != 1) return false;
+    const int j = cands[k];
+    const int t = A.eDisk[j];
+    relocate(i, t);
+    // the destination replica goes to sourceReplica.disk(), read after the first relocation: its own disk
+    const double u = du(j);
+    A.dUtil[t] -= u;
+    A.dUtil[t] += u;
+    record(A.eRep[j], t, t);
+    return true;
   }
 
   // ---------------------------------------------------------------- IntraBrokerDiskCapacityGoal
@@ -437,17 +486,14 @@ class IntraBroker {
       const int cd = A.bDisks[k];
       if (A.dAlive[cd] && pct(cd) > brokerUtil) pqAdd(q, n, cd, true);
     }
-    const int32_t one[1] = {disk};
     while (n > 0) {
       const int cd = pqPoll(q, n, true);
       const int m = snapshot(cd, true, sa);
-      for (int s = 0; s < m; ++s) {
-        if (maybeMove(sa[s], one, 1) >= 0) {
-          if (pct(disk) > lo) return false;
-          if (n > 0 && pct(cd) < pct(q[0])) {
-            pqAdd(q, n, cd, true);
-            break;
-          }
+      for (int s = moveFirstRow(sa, 0, m, disk); s < m; s = moveFirstRow(sa, s + 1, m, disk)) {
+        if (pct(disk) > lo) return false;
+        if (n > 0 && pct(cd) < pct(q[0])) {
+          pqAdd(q, n, cd, true);
+          break;
         }
       }
     }
@@ -463,15 +509,12 @@ class IntraBroker {
     }
     while (n > 0) {
       const int cd = pqPoll(q, n, false);
-      const int32_t one[1] = {cd};
       const int m = snapshot(disk, true, sa);
-      for (int s = 0; s < m; ++s) {
-        if (maybeMove(sa[s], one, 1) >= 0) {
-          if (pct(disk) < up) return false;
-          if (n > 0 && pct(cd) > pct(q[0])) {
-            pqAdd(q, n, cd, false);
-            break;
-          }
+      for (int s = moveFirstRow(sa, 0, m, cd); s < m; s = moveFirstRow(sa, s + 1, m, cd)) {
+        if (pct(disk) < up) return false;
+        if (n > 0 && pct(cd) > pct(q[0])) {
+          pqAdd(q, n, cd, false);
+          break;
         }
       }
     }
