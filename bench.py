@@ -478,6 +478,17 @@ def main() -> None:
                      "launches_per_step": perf.intra_launches if intra else perf.scan_launches,
                      "server_launches_per_step": perf.server_launches,
                      "server_commands_per_step": perf.server_scans,
+                     # the rocprof-derivable view of the same kernel: algorithmic bytes per scan_server launch over its
+                     # residency per launch (HIP events from launch to exit, idle polling included) — what a
+                     # rocprofv3 kernel trace's average scan_server duration gives
+                     "resident": None if not server or perf.server_resident_ms <= 0 else {
+                         "avg_launch_us": perf.server_resident_ms * 1e3 / max(1, perf.server_launches),
+                         "algorithmic_bytes_per_launch": perf.server_required * BYTES_PER_CANDIDATE
+                         / max(1, perf.server_launches),
+                         "achieved": perf.server_required * BYTES_PER_CANDIDATE / (perf.server_resident_ms * 1e-3) / 1e9,
+                         "frac": perf.server_required * BYTES_PER_CANDIDATE / (perf.server_resident_ms * 1e-3) / 1e9
+                         / HBM_PEAK_GBS,
+                         "busy_share": perf.server_busy_ms / perf.server_resident_ms},
                      "server_payload_bytes_per_step": perf.server_payload_bytes,
                      "device_evaluated_candidates_per_s": perf.scan_required / (elapsed / args.steps),
                      "chain_launches_per_step": perf.chain_launches,

@@ -182,7 +182,7 @@ class PerfStruct(C.Structure):
                 ("combines", C.c_int64), ("server_launches", C.c_int64), ("server_scans", C.c_int64),
                 ("server_required", C.c_int64), ("server_busy_ms", C.c_double),
                 ("server_payload_bytes", C.c_int64), ("server_chains", C.c_int64),
-                ("server_idle_exits", C.c_int64)]
+                ("server_idle_exits", C.c_int64), ("server_resident_ms", C.c_double)]
 
 
 # ----------------------------------------------------------------------------------------------- errors

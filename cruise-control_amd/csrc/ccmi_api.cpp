@@ -720,6 +720,7 @@ ccmi_status ccmi_perf(const ccmi_session* s, ccmi_perf_counters* out) {
     out->server_payload_bytes = p.serverPayloadBytes;
     out->server_chains = p.serverChains;
     out->server_idle_exits = p.serverIdleExits;
+    out->server_resident_ms = p.serverResidentMs;
     return CCMI_OK;
   });
 }

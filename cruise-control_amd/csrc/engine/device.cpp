@@ -142,6 +142,8 @@ Device::Device(int ordinal, int B, int R, int P, int T, int maxGoalSlots)
   }
   hipCheck(hipEventCreate((hipEvent_t*)&ev0_), "hipEventCreate");
   hipCheck(hipEventCreate((hipEvent_t*)&ev1_), "hipEventCreate");
+  hipCheck(hipEventCreate((hipEvent_t*)&evS0_), "hipEventCreate");
+  hipCheck(hipEventCreate((hipEvent_t*)&evS1_), "hipEventCreate");
   {  // scan server: on unless CCMI_SERVER=0; CCMI_SERVER_BLOCKS sets its workgroups (multiple of 8, <= 512)
     const char* e = std::getenv("CCMI_SERVER");
     serverUsable_ = !(e && e[0] == '0');
@@ -223,6 +225,8 @@ Device::~Device() {
   if (hResult_) (void)hipHostFree(hResult_);
   if (ev0_) (void)hipEventDestroy(EV0);
   if (ev1_) (void)hipEventDestroy(EV1);
+  if (evS0_) (void)hipEventDestroy((hipEvent_t)evS0_);
+  if (evS1_) (void)hipEventDestroy((hipEvent_t)evS1_);
   if (ST) (void)hipStreamDestroy(ST);
 }
 
@@ -306,7 +310,13 @@ void Device::stopServer() {
     std::lock_guard<std::mutex> lk(g_serverMu);
     g_serverWgs[ordinal_ & 63] -= serverBlocks_;
   }
+  if (serverTimed_) (void)hipEventRecord((hipEvent_t)evS1_, ST);
   hipCheck(hipStreamSynchronize(ST), "scan server exit");
+  if (serverTimed_) {
+    float ms = 0.f;
+    if (hipEventElapsedTime(&ms, (hipEvent_t)evS0_, (hipEvent_t)evS1_) == hipSuccess) perf.serverResidentMs += ms;
+    serverTimed_ = false;
+  }
 }
 
 // A cross / pair scan the running (or a newly started) server can take: its rows fit the LDS overlay and, when the
@@ -333,6 +343,8 @@ bool Device::ensureServer() {
   // the arrival counter and the result word start clean for every server launch, whatever an earlier launch left
   hipCheck(hipMemsetAsync(dDone_, 0, sizeof(unsigned int), ST), "reset server arrivals");
   hipCheck(hipMemsetAsync(dResult_, 0xff, sizeof(unsigned long long), ST), "reset server result");
+  serverTimed_ = timing;
+  if (serverTimed_) (void)hipEventRecord((hipEvent_t)evS0_, ST);
   hipCheck(launchScanServer(tables(), mutTables(), chainTables(), (const ServerCmd*)fg_, fg_ + kCmdBytes, segPool_,
                             dResult_, dDone_, hResultDev_, dServerT0_, lastCmdSeq_, serverBlocks_, ST),
            "scan_server");

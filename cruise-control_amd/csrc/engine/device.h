@@ -54,6 +54,7 @@ struct DevicePerf {
   int64_t serverPayloadBytes = 0;  // command payload written through the BAR (program, rows, request arrays)
   int64_t serverRequired = 0;  // candidates those scans had to evaluate
   int64_t serverChains = 0;    // K7 chains the running server took as commands (no launch, no server restart)
+  double serverResidentMs = 0;  // HIP-event time from each server launch to its exit (kernel timing on)
 };
 
 // K6 (kernels/intra.hip, intra.h): one intra-broker goal over every broker in one launch.
@@ -224,6 +225,8 @@ class Device {
   unsigned long long seq_ = 0;
   alignas(16) unsigned char statsHost_[sizeof(StatsOut)];
   void *ev0_ = nullptr, *ev1_ = nullptr;  // hipEvent_t
+  bool serverTimed_ = false;  // the running server launch has its start event recorded
+  void *evS0_ = nullptr, *evS1_ = nullptr;  // hipEvent_t: a scan-server launch's residency (kernel timing on)
   struct Staged {
     int nb = 0, nr = 0, np = 0, nt = 0;
     size_t obr = 0, orr = 0, opr = 0, otd = 0, end = 0;

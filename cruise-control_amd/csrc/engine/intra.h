@@ -507,10 +507,16 @@ class IntraBroker {
       const int cd = A.bDisks[k];
       if (A.dAlive[cd] && pct(cd) < brokerUtil) pqAdd(q, n, cd, false);
     }
+    // the disk's snapshot is re-taken only after a move left it (between polls without a move it is unchanged:
+    // entry disks, original disks and the static order are all it reads)
+    int m = 0;
+    bool fresh = false;
     while (n > 0) {
       const int cd = pqPoll(q, n, false);
-      const int m = snapshot(disk, true, sa);
+      if (!fresh) m = snapshot(disk, true, sa);
+      fresh = true;
       for (int s = moveFirstRow(sa, 0, m, cd); s < m; s = moveFirstRow(sa, s + 1, m, cd)) {
+        fresh = false;
         if (pct(disk) < up) return false;
         if (n > 0 && pct(cd) > pct(q[0])) {
           pqAdd(q, n, cd, false);
@@ -530,15 +536,19 @@ class IntraBroker {
       if (A.dAlive[cd] && (in ? pct(cd) > lo : pct(cd) < up)) pqAdd(q, n, cd, in);
     }
     int nHist = 0;
+    int m = 0;
+    bool fresh = false;  // sa holds the disk's snapshot of the current state (re-taken only after a swap)
     while (n > 0) {
       const int cd = pqPoll(q, n, in);
       bool swapped = false;
-      const int m = snapshot(disk, !in, sa);
+      if (!fresh) m = snapshot(disk, !in, sa);
+      fresh = true;
       const int c = snapshot(cd, in, sb);  // the candidate view cannot change before a swap
       for (int s = 0; s < m; ++s) {
         if (maybeSwap(sa[s], sb, c)) {
           if (in ? pct(disk) > lo : pct(disk) < up) return;
           swapped = true;
+          fresh = false;
           break;
         }
       }

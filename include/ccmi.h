@@ -522,6 +522,9 @@ typedef struct ccmi_perf_counters {
    * ended before it saw them (each then ran as a launch) */
   int64_t server_chains;
   int64_t server_idle_exits;
+  /* ABI v9: HIP-event time from each scan-server launch to its exit, summed (with ccmi_set_kernel_timing on): the
+   * residency a rocprofv3 kernel trace reports for scan_server, idle polling included */
+  double server_resident_ms;
 } ccmi_perf_counters;
 ccmi_status ccmi_perf(const ccmi_session* s, ccmi_perf_counters* out);
 void ccmi_perf_reset(ccmi_session* s);

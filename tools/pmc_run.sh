@@ -33,3 +33,13 @@ for c in FETCH_SIZE WRITE_SIZE; do
 done
 python3 tools/pmc_summary.py --calib "$DST/calib_summary.json" $(find "$W/c2_FETCH_SIZE" "$W/c2_WRITE_SIZE" \
   -name "*counter_collection.csv") > "$DST/c2_pmc_summary.json"
+# C4 (JBOD intra-broker goals, K6): the same three passes
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$W/c4_trace" -o c4 -- \
+  python3 bench.py --workload c4 --no-cpu-baseline --steps 1 --warmup 0 > "$DST/c4_bench_prof.json"
+collect c4_trace "*stats.csv"
+for c in FETCH_SIZE WRITE_SIZE; do
+  timeout -s KILL 300 rocprofv3 --pmc $c --output-format csv -d "$W/c4_$c" -o c4 -- \
+    python3 bench.py --workload c4 --no-cpu-baseline --steps 1 --warmup 0 > /dev/null
+done
+python3 tools/pmc_summary.py --calib "$DST/calib_summary.json" $(find "$W/c4_FETCH_SIZE" "$W/c4_WRITE_SIZE" \
+  -name "*counter_collection.csv") > "$DST/c4_pmc_summary.json"
