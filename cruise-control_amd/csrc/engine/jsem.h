@@ -162,17 +162,17 @@ class RbTreeSet {
   // `cancel` (optional) stops the build early (the tree is then incomplete and must be discarded).
   void buildByRank(const std::vector<int>& ids, const std::vector<int32_t>& rank,
                    const std::atomic<bool>* cancel = nullptr) {
-    // an empty tree: node i is the i-th put (no free list), written in place
+    // an empty tree whose node of a key is its rank: a put's parent is its in-order neighbour, so the puts and the
+    // fix-ups walk nearby nodes (the structure is the same as with any node numbering)
     n_.clear();
     free_.clear();
     root_ = -1;
     size_ = 0;
-    n_.resize(ids.size());
     int32_t nr = 0;
     for (int k : ids) nr = std::max(nr, rank[k] + 1);
+    n_.resize(nr);  // ranks no id takes stay unused slots
     const int nw = (nr + 63) >> 6, ns = (nw + 63) >> 6;
     std::vector<uint64_t> w(nw, 0), sw(ns, 0);
-    std::vector<int32_t> nodeOf(nr, -1);
     auto pred = [&](int32_t r) -> int32_t {  // largest set rank < r, or -1
       int wi = r >> 6;
       uint64_t m = w[wi] & ((1ull << (r & 63)) - 1);
@@ -200,38 +200,37 @@ class RbTreeSet {
       return (wi << 6) | __builtin_ctzll(w[wi]);
     };
     Node* N = n_.data();
-    for (int e = 0; e < (int)ids.size(); ++e) {
+    for (size_t e = 0; e < ids.size(); ++e) {
       if (cancel && (e & 511) == 511 && cancel->load(std::memory_order_relaxed)) return;
       const int k = ids[e];
       const int32_t rk = rank[k];
       if (e == 0) {
-        N[0] = Node{(uint32_t)k, -1, -1, -1};
-        root_ = 0;
+        N[rk] = Node{(uint32_t)k, -1, -1, -1};
+        root_ = rk;
         size_ = 1;
       } else {
         const int32_t pr = pred(rk);
         int parent;
         bool goLeft;
-        if (pr >= 0 && N[nodeOf[pr]].right < 0) {
-          parent = nodeOf[pr];
+        if (pr >= 0 && N[pr].right < 0) {
+          parent = pr;
           goLeft = false;
         } else {
-          parent = nodeOf[succ(rk)];
+          parent = succ(rk);
           goLeft = true;
         }
-        N[e] = Node{(uint32_t)k, -1, -1, parent};
-        (goLeft ? N[parent].left : N[parent].right) = e;
-        insertFix(e);
+        N[rk] = Node{(uint32_t)k, -1, -1, parent};
+        (goLeft ? N[parent].left : N[parent].right) = rk;
+        insertFix(rk);
         ++size_;
       }
-      nodeOf[rk] = e;
       w[rk >> 6] |= 1ull << (rk & 63);
       sw[rk >> 12] |= 1ull << ((rk >> 6) & 63);
     }
     // from here on the in-order sequence is maintained next to the tree (rotations do not change it)
     seqId_.clear();
-    for (int32_t r = 0; r < nr; ++r)
-      if (nodeOf[r] >= 0) seqId_.push_back(nodeOf[r]);
+    for (int wi = 0; wi < nw; ++wi)
+      for (uint64_t m = w[wi]; m; m &= m - 1) seqId_.push_back((wi << 6) | __builtin_ctzll(m));
     seqKey_.resize(seqId_.size());
     for (size_t i = 0; i < seqId_.size(); ++i) seqKey_[i] = n_[seqId_[i]].key();
     seqOn_ = true;
