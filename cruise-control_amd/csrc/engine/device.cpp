@@ -38,8 +38,8 @@ hipError_t launchPrep(const MutTables& M, const UpdateList& U, const int4* req, 
 uint32_t scanXcdSliceMinCols();
 hipError_t launchScanServer(const DevTables& T, const MutTables& M, const ChainTables& C, const ServerCmd* cmd,
                             const char* pay, const RowRef* pool, unsigned long long* result, unsigned int* done,
-                            unsigned long long* mail, unsigned long long* t0, unsigned long long startSeq, int blocks,
-                            hipStream_t st);
+                            unsigned long long* mail, unsigned long long* t0, unsigned long long* bell,
+                            unsigned long long startSeq, int blocks, hipStream_t st);
 hipError_t launchChainPairs(const DevTables& T, const ChainTables& C, const DevProgram& prog, const int32_t* pr,
                             const int32_t* pb, const int32_t* next, int n, int maxAccepts, int32_t* log,
                             ChainResultDev* out, hipStream_t st);
@@ -153,7 +153,7 @@ Device::Device(int ordinal, int B, int R, int P, int T, int maxGoalSlots)
     serverBlocks_ = std::min(serverBlocks_, prop.multiProcessorCount / 8 * 8);
     if (serverBlocks_ < 8) serverUsable_ = false;
     if (serverUsable_) {
-      dalloc(&dServerT0_, 1);
+      dalloc(&dServerT0_, 16);  // [0] busy-time stamp, [8] the doorbell (a line of its own)
       try {
         ensureFg(1 << 20);
         // snapshot pool: 4M rows (64 MB), host-written like the command block
@@ -343,10 +343,11 @@ bool Device::ensureServer() {
   // the arrival counter and the result word start clean for every server launch, whatever an earlier launch left
   hipCheck(hipMemsetAsync(dDone_, 0, sizeof(unsigned int), ST), "reset server arrivals");
   hipCheck(hipMemsetAsync(dResult_, 0xff, sizeof(unsigned long long), ST), "reset server result");
+  hipCheck(hipMemsetAsync(dServerT0_ + 8, 0, sizeof(unsigned long long), ST), "reset server doorbell");
   serverTimed_ = timing;
   if (serverTimed_) (void)hipEventRecord((hipEvent_t)evS0_, ST);
   hipCheck(launchScanServer(tables(), mutTables(), chainTables(), (const ServerCmd*)fg_, fg_ + kCmdBytes, segPool_,
-                            dResult_, dDone_, hResultDev_, dServerT0_, lastCmdSeq_, serverBlocks_, ST),
+                            dResult_, dDone_, hResultDev_, dServerT0_, dServerT0_ + 8, lastCmdSeq_, serverBlocks_, ST),
            "scan_server");
   serverOn_ = true;
   perf.serverLaunches++;

@@ -858,6 +858,9 @@ __device__ __forceinline__ void copySysOneThread(X* dst, const X* src) {  // all
   for (int w = 0; w < n; ++w) reinterpret_cast<int32_t*>(dst)[w] = v[w];
 }
 constexpr unsigned long long kServerIdleTicks = 200000000ull;  // 2 s of s_memrealtime (100 MHz)
+constexpr unsigned long long kServerStuckTicks = 1000000000ull;  // 10 s: a command unpublished that long is stuck
+// scan-server doorbell word: valid and exit flags, nActive (bits 32-61), the command sequence's low 32 bits
+constexpr unsigned long long kBellValid = 1ull << 63, kBellExit = 1ull << 62;
 
 // thread 0's record writes become visible to the whole workgroup (one CU: workgroup scope; the next launch sees them
 // through the kernel boundary)
@@ -939,6 +942,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, kServ
                                                       unsigned int* __restrict__ done,
                                                       unsigned long long* __restrict__ mail,
                                                       unsigned long long* __restrict__ t0,
+                                                      unsigned long long* __restrict__ bell,
                                                       unsigned long long startSeq) {
   OverlayLds& ov = gSrvOv;
   DevProgram& prog = gSrvProg;
@@ -956,15 +960,40 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, kServ
       // The idle clock starts once this workgroup sees its last command published: until then a workgroup that was
       // dispatched late (the GPU busy with other sessions' kernels) is still working on it and the host is waiting.
       bool published = last == startSeq;
+      // Workgroup 0 alone polls the host-written command word (fine-grained VRAM: every poll is a memory read) and
+      // rings a doorbell in device memory with the command's {valid, exit, nActive, seq}; the others poll the doorbell
+      // with agent-scope loads, which the XCD's L2 serves until it changes (MI355X_MICROARCH.md hand-off table: one
+      // lane's sc1 store, sc1 load polls). Only the command's participants then copy its header.
       for (int spin = 0;; ++spin) {
-        const unsigned long long s =
-            __hip_atomic_load(&cmd->seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        if (s != last && !(s & kSeqBusy)) {
-          // a workgroup that did not take part in the last command may read the next header while the host writes
-          // it: the copy counts only when the sequence word did not change across it
-          copySysOneThread(&c, cmd);
-          if (__hip_atomic_load(&cmd->seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == s) break;
-          continue;
+        if (blockIdx.x == 0) {
+          const unsigned long long s = __hip_atomic_load(&cmd->seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          if (s != last && !(s & kSeqBusy)) {
+            // the copy counts only when the sequence word did not change across it (seqlock, devtypes.h)
+            copySysOneThread(&c, cmd);
+            if (__hip_atomic_load(&cmd->seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == s) {
+              const unsigned long long ring = kBellValid | (c.op == SOP_EXIT ? kBellExit : 0ull) |
+                                              ((unsigned long long)(uint32_t)c.nActive << 32) | (s & 0xffffffffull);
+              __hip_atomic_store(bell, ring, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+              break;
+            }
+            continue;
+          }
+        } else {
+          const unsigned long long b = __hip_atomic_load(bell, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if ((b & kBellValid) && (b & 0xffffffffull) != (last & 0xffffffffull)) {
+            const uint32_t nAct = (uint32_t)(b >> 32) & 0x3fffffffu;
+            if ((b & kBellExit) || (uint32_t)blockIdx.x >= nAct) {
+              // not taking part (or the exit command): the doorbell says all this workgroup needs
+              c.op = (b & kBellExit) ? SOP_EXIT : SOP_CROSS;
+              c.nActive = (int32_t)nAct;
+              c.seq = b & 0xffffffffull;
+              break;
+            }
+            // a participant: the host rewrites the header only after this command's result, which waits for this
+            // workgroup, so one copy is stable
+            copySysOneThread(&c, cmd);
+            break;
+          }
         }
         if ((spin & 63) == 63) {
           if (!published) {
@@ -972,6 +1001,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, kServ
             if ((mw >> 32) == (last & 0xffffffffull)) {
               published = true;
               idleSince = __builtin_amdgcn_s_memrealtime();
+            } else if (__builtin_amdgcn_s_memrealtime() - idleSince > kServerStuckTicks) {
+              ex = 3;  // a command never completed (a participant never arrived): leave instead of spinning forever
+              break;
             }
           } else if (__builtin_amdgcn_s_memrealtime() - idleSince > kServerIdleTicks) {
             ex = 1;
@@ -999,9 +1031,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, kServ
     }
     __syncthreads();
     if (sExit || c.op == SOP_EXIT) {
-      // exit record for the host's diagnostics: mail[3] = {reason (1 watchdog, 2 exit command) : 32 | last seq : 32}
+      // exit record for the host's diagnostics: mail[3] = {reason (1 watchdog, 2 exit command, 3 stuck command) : 32 |
+      // last seq : 32}
       if (blockIdx.x == 0 && threadIdx.x == 0)
-        __hip_atomic_store(&mail[3], ((unsigned long long)(sExit ? 1 : 2) << 32) | (last & 0xffffffffull),
+        __hip_atomic_store(&mail[3], ((unsigned long long)(sExit ? sExit : 2) << 32) | (last & 0xffffffffull),
                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       break;
     }
@@ -1673,11 +1706,11 @@ hipError_t launchScanPairs(const DevTables& T, const MutTables& M, const UpdateL
 // One workgroup per CU slot: `blocks` workgroups of kBlock threads, all resident (the launcher caps it at 2 per CU).
 hipError_t launchScanServer(const DevTables& T, const MutTables& M, const ChainTables& C, const ServerCmd* cmd,
                             const char* pay, const RowRef* pool, unsigned long long* result, unsigned int* done,
-                            unsigned long long* mail, unsigned long long* t0, unsigned long long startSeq, int blocks,
-                            hipStream_t st) {
+                            unsigned long long* mail, unsigned long long* t0, unsigned long long* bell,
+                            unsigned long long startSeq, int blocks, hipStream_t st) {
   if (blocks < (int)kXcds || blocks % (int)kXcds != 0 || blocks > 512) return hipErrorInvalidValue;
   hipLaunchKernelGGL(scan_server, dim3(blocks), dim3(kBlock), 0, st, T, M, C, cmd, pay, pool, result, done, mail, t0,
-                     startSeq);
+                     bell, startSeq);
   return hipGetLastError();
 }
 
