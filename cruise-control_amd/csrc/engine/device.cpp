@@ -793,7 +793,12 @@ bool Device::waitMail(unsigned long long seq, bool serverCmd) {
   volatile unsigned long long* mail = hResult_;
   const unsigned long long want = seq & 0xffffffffull;
   uint64_t spins = 0;
+  bool idle = (bool)idleWork;
   while ((__atomic_load_n(&mail[0], __ATOMIC_ACQUIRE) >> 32) != want) {
+    if (idle) {  // the engine's speculative host work, one unit per poll
+      idle = idleWork();
+      continue;
+    }
     if ((++spins & 1023) == 0) {
       const hipError_t q = hipStreamQuery(ST);
       if (q == hipSuccess) {

@@ -8,6 +8,7 @@
 //   the last workgroup writes one {seq, key} word into a host-mapped mailbox; the host spins on it
 // Everything runs on one HIP stream per session, so HIP events on that stream time the kernels.
 #pragma once
+#include <functional>
 #include <cstdint>
 #include <string>
 #include <unordered_map>
@@ -92,6 +93,15 @@ class Device {
   ~Device();
   Device(const Device&) = delete;
   Device& operator=(const Device&) = delete;
+
+  // Host work the engine hands over for the time a scan is in flight: called between polls of the result until it
+  // returns false (each call a few microseconds of host-only work that touches no device state). Set around one
+  // scan by its caller.
+  std::function<bool()> idleWork;
+  struct IdleScope {  // clears idleWork when the scan returns or throws
+    Device* d;
+    ~IdleScope() { d->idleWork = nullptr; }
+  };
 
   // initial upload (host arrays in device layout)
   void uploadStatic(const double* bCapRM, const int32_t* rPart, const int32_t* rOrig, const int32_t* pOff,

@@ -33,6 +33,8 @@ size_t envSize(const char* name, size_t dflt) {
   return x ? x : dflt;
 }
 const size_t kFirstBatchRows = envSize("CCMI_FIRST_BATCH", 2048), kBatchGrowth = envSize("CCMI_BATCH_GROWTH", 8);
+// snapshots of upcoming queue polls computed while a move-in scan is in flight (Device::idleWork); 0 = off
+const size_t kIdleSnapshots = envSize("CCMI_IDLE_SNAPSHOTS", 8);
 constexpr size_t kMaxBatchRows = (size_t)1 << 18;
 
 // Host view of the model for predicates.h (same expressions the kernels evaluate).
@@ -703,6 +705,8 @@ class LiveQueue {
     if (ordered_) oq_.add(x);
     else pq_.add(x);
   }
+  // a likely future poll (-1: none known)
+  int upcoming(size_t k) const { return ordered_ ? oq_.upcoming(k) : -1; }
   // speculatively polled entries whose keys did not change, in reverse poll order
   void unpoll(int x) {
     if (ordered_) oq_.unpoll(x);
@@ -1608,7 +1612,19 @@ class ResourceDistribution : public GoalImpl {
         }
       }
       if (segs.empty()) break;
+      // while the scan is in flight, the snapshots of the next brokers the queue will poll (cached per broker version,
+      // so an unused one costs only host time that would otherwise be spent waiting)
+      size_t ahead = 0;
+      const Device::IdleScope idleScope{e.dev};
+      e.dev->idleWork = [&]() {
+        const int cb = pq.upcoming(ahead);
+        if (cb < 0 || ahead >= kIdleSnapshots) return false;
+        ++ahead;
+        (void)m.snapshotInShared(snapTab, cb, spec);
+        return true;
+      };
       const int64_t key = cands.empty() ? -1 : e.crossScanSegs(*this, action, segs, cands);
+      e.dev->idleWork = nullptr;  // (idleScope also clears it on a throw)
       if (key < 0) {
         target = std::min<size_t>(target * kBatchGrowth, kMaxBatchRows);
         continue;

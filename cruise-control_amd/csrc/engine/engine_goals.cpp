@@ -2035,7 +2035,17 @@ class LeaderReplicaDistribution : public GoalImpl {
         segs.push_back({m.snapshotInShared(snapTab, src, s), src, 0});
         rows += segLen(segs.back());
       }
+      size_t ahead = 0;  // snapshots of the next sources, computed while the scan is in flight (Device::idleWork)
+      const Device::IdleScope idleScope{e.dev};
+      e.dev->idleWork = [&]() {
+        const int src = pq.upcoming(ahead);
+        if (src < 0 || ahead >= 8) return false;
+        ++ahead;
+        (void)m.snapshotInShared(snapTab, src, s);
+        return true;
+      };
       const int64_t key = cands.empty() ? -1 : e.crossScanSegs(*this, DA_MOVE, segs, cands);
+      e.dev->idleWork = nullptr;
       if (key < 0) {
         target = std::min<size_t>(target * 8, (size_t)1 << 18);
         continue;  // every polled source exhausted; none is re-enqueued

@@ -595,6 +595,9 @@ class OrderedQueue {
     return s_[pos_++];
   }
   void add(int x) { heap_.add(x); }
+  // The k-th element of the sorted run after the poll position (-1 past its end): a likely future poll (elements
+  // re-added through the heap are not included)
+  int upcoming(size_t k) const { return pos_ + k < s_.size() ? s_[pos_ + k] : -1; }
   // Put back the most recently polled element (un-polls come in reverse poll order). An element that came from
   // the sorted run and whose key did not change since returns to its slot in the run (O(1)); anything else goes
   // through the heap. Either way the queue holds the same set, so the poll order is unchanged.

@@ -783,6 +783,9 @@ void Device::stopServer() {}  // the emulation has no scan server: every scan is
 // no snapshot pool either (segsUsable() is false, so the engine flattens first; kept for the link)
 int64_t Device::scanSegs(const DevProgram& prog, const std::vector<SegIn>& segs, const int32_t* cands, int N, int c0,
                          int c1) {
+  if (idleWork)  // the engine's speculative host work runs while a real scan is in flight
+    while (idleWork()) {
+    }
   segFlat_.clear();
   for (const SegIn& sg : segs)
     if (sg.v->size() > sg.skip) segFlat_.insert(segFlat_.end(), sg.v->begin() + sg.skip, sg.v->end());
