@@ -32,9 +32,15 @@ size_t envSize(const char* name, size_t dflt) {
   const size_t x = v ? (size_t)std::strtoull(v, nullptr, 10) : 0;
   return x ? x : dflt;
 }
+size_t envCount(const char* name, size_t dflt) {  // unset: dflt; "0" turns the feature off
+  const char* v = std::getenv(name);
+  return v ? (size_t)std::strtoull(v, nullptr, 10) : dflt;
+}
 const size_t kFirstBatchRows = envSize("CCMI_FIRST_BATCH", 2048), kBatchGrowth = envSize("CCMI_BATCH_GROWTH", 8);
 // snapshots of upcoming queue polls computed while a move-in scan is in flight (Device::idleWork); 0 = off
-const size_t kIdleSnapshots = envSize("CCMI_IDLE_SNAPSHOTS", 8);
+const size_t kIdleSnapshots = envCount("CCMI_IDLE_SNAPSHOTS", 8);
+// puts of the speculative entry tree per poll of an in-flight move-out scan; 0 = off (read per call: tests vary it)
+size_t idleTreePuts() { return envCount("CCMI_IDLE_TREE_PUTS", 512); }
 constexpr size_t kMaxBatchRows = (size_t)1 << 18;
 
 // Host view of the model for predicates.h (same expressions the kernels evaluate).
@@ -1323,6 +1329,8 @@ class ResourceDistribution : public GoalImpl {
       entryKey.push_back({x, m.pct(x, res)});
     };
     std::vector<int32_t> rank;
+    int specState = 0;  // the speculative entry-tree build: 0 not started, 1 puts in progress, 2 complete
+    std::vector<int32_t> entryOrder;
     auto materialise = [&]() {
       PhaseScope pi(PH_TREE_BUILD);
       // CCMI_PROFILE: nanoseconds in the order construction (16), the put sequence (17) and the replay (18)
@@ -1336,6 +1344,10 @@ class ResourceDistribution : public GoalImpl {
       ovr = entryKey;
       if (useWorker) {
         cand.adopt(treeWorker->take());
+      } else if (specState > 0) {  // the entry tree was started while scans were in flight: finish its puts
+        if (tp) t1 = tnow();
+        cand.buildStep((size_t)-1);
+        prof().count(19, "tree.spec.finished", 1);
       } else {
         // Entry-time (key, id) order of the members: the maintained live order with the few brokers whose key
         // moved since entry put back at their entry keys; the tree is then built by the same put sequence (ids in
@@ -1404,6 +1416,29 @@ class ResourceDistribution : public GoalImpl {
     // (checked after each move); the leadership form, which keeps no order, builds the tree.
     entryIn = inSet;
     if (inSet[b] && action == DA_LEADERSHIP) materialise();
+    // While this call's scans are in flight (Device::idleWork) the entry tree's put sequence is started from the entry
+    // order, a bounded number of puts per poll, so a later materialise() has fewer puts left (or none).
+    const Device::IdleScope idleScope{e.dev};
+    const size_t treePuts = idleTreePuts();
+    if (!built && !useWorker && treePuts > 0) {
+      entryOrder.assign(inorder.begin(), inorder.end());
+      e.dev->idleWork = [&]() {
+        if (built || specState == 2) return false;
+        if (specState == 0) {
+          std::vector<int32_t> rk(m.B, 0);
+          for (size_t i = 0; i < entryOrder.size(); ++i) rk[entryOrder[i]] = (int32_t)i;
+          std::vector<int> ids;
+          ids.reserve(entryOrder.size());
+          for (int x = 0; x < m.B; ++x)
+            if (entryIn[x]) ids.push_back(x);
+          cand.buildStart(std::move(ids), std::move(rk));
+          specState = 1;
+          return true;
+        }
+        if (cand.buildStep(treePuts)) specState = 2;
+        return specState == 1;
+      };
+    }
     auto memberBetween = [&](int dst, double k0, double k1) {
       // is a member other than dst strictly between (k0, id(dst)) and (k1, id(dst)) in (pct, id) order?
       const double lo = jcmpDouble(k0, k1) <= 0 ? k0 : k1, hi = jcmpDouble(k0, k1) <= 0 ? k1 : k0;

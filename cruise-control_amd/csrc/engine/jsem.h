@@ -96,8 +96,10 @@ class RbTreeSet {
     std::swap(seqOn_, o.seqOn_);
     seqId_.swap(o.seqId_);
     seqKey_.swap(o.seqKey_);
+    building_ = o.building_ = false;
   }
   void clear() {
+    building_ = false;
     n_.clear();
     free_.clear();
     root_ = -1;
@@ -158,65 +160,59 @@ class RbTreeSet {
   // Insert `ids` in order into an EMPTY tree whose comparator agrees with `rank` (distinct ranks in [0, n)) on
   // these elements: the same sequence of TreeMap.put calls and therefore the same structure. The search is not
   // walked: a put lands on the one empty link between the new key's in-order neighbours (the predecessor's right
-  // link when that is empty, else the successor's left link), found in a two-level bitmap over the ranks.
+  // link when that is empty, else the successor's left link), found in a two-level bitmap over the ranks. The node of
+  // a key is its rank, so a put's parent is its in-order neighbour and the puts walk nearby nodes.
   // `cancel` (optional) stops the build early (the tree is then incomplete and must be discarded).
   void buildByRank(const std::vector<int>& ids, const std::vector<int32_t>& rank,
                    const std::atomic<bool>* cancel = nullptr) {
-    // an empty tree whose node of a key is its rank: a put's parent is its in-order neighbour, so the puts and the
-    // fix-ups walk nearby nodes (the structure is the same as with any node numbering)
+    std::vector<int> i2(ids);
+    std::vector<int32_t> r2(rank);
+    buildByRank(std::move(i2), std::move(r2), cancel);
+  }
+  void buildByRank(std::vector<int>&& ids, std::vector<int32_t>&& rank, const std::atomic<bool>* cancel = nullptr) {
+    buildStart(std::move(ids), std::move(rank));
+    while (!buildStep(512))
+      if (cancel && cancel->load(std::memory_order_relaxed)) return;
+  }
+  // The same build a bounded number of puts at a time (buildStep returns true once every put is done, then the
+  // tree is complete); the tree must not be used before.
+  void buildStart(std::vector<int>&& ids, std::vector<int32_t>&& rank) {
     n_.clear();
     free_.clear();
     root_ = -1;
     size_ = 0;
+    bIds_ = std::move(ids);
+    bRank_ = std::move(rank);
+    bNext_ = 0;
     int32_t nr = 0;
-    for (int k : ids) nr = std::max(nr, rank[k] + 1);
+    for (int k : bIds_) nr = std::max(nr, bRank_[k] + 1);
+    bNr_ = nr;
     n_.resize(nr);  // ranks no id takes stay unused slots
-    const int nw = (nr + 63) >> 6, ns = (nw + 63) >> 6;
-    std::vector<uint64_t> w(nw, 0), sw(ns, 0);
-    auto pred = [&](int32_t r) -> int32_t {  // largest set rank < r, or -1
-      int wi = r >> 6;
-      uint64_t m = w[wi] & ((1ull << (r & 63)) - 1);
-      if (m) return (wi << 6) | (63 - __builtin_clzll(m));
-      int si = wi >> 6;
-      uint64_t sm = sw[si] & ((1ull << (wi & 63)) - 1);
-      while (!sm) {
-        if (--si < 0) return -1;
-        sm = sw[si];
-      }
-      wi = (si << 6) | (63 - __builtin_clzll(sm));
-      return (wi << 6) | (63 - __builtin_clzll(w[wi]));
-    };
-    auto succ = [&](int32_t r) -> int32_t {  // smallest set rank > r, or -1
-      int wi = r >> 6;
-      uint64_t m = (r & 63) == 63 ? 0 : w[wi] & (~0ull << ((r & 63) + 1));
-      if (m) return (wi << 6) | __builtin_ctzll(m);
-      int si = wi >> 6;
-      uint64_t sm = (wi & 63) == 63 ? 0 : sw[si] & (~0ull << ((wi & 63) + 1));
-      while (!sm) {
-        if (++si >= ns) return -1;
-        sm = sw[si];
-      }
-      wi = (si << 6) | __builtin_ctzll(sm);
-      return (wi << 6) | __builtin_ctzll(w[wi]);
-    };
+    bW_.assign((nr + 63) >> 6, 0);
+    bSw_.assign((bW_.size() + 63) >> 6, 0);
+    seqOn_ = false;
+    building_ = true;
+  }
+  bool buildStep(size_t maxPuts) {
+    if (!building_) return true;
     Node* N = n_.data();
-    for (size_t e = 0; e < ids.size(); ++e) {
-      if (cancel && (e & 511) == 511 && cancel->load(std::memory_order_relaxed)) return;
-      const int k = ids[e];
-      const int32_t rk = rank[k];
+    const size_t end = maxPuts >= bIds_.size() - bNext_ ? bIds_.size() : bNext_ + maxPuts;
+    for (size_t e = bNext_; e < end; ++e) {
+      const int k = bIds_[e];
+      const int32_t rk = bRank_[k];
       if (e == 0) {
         N[rk] = Node{(uint32_t)k, -1, -1, -1};
         root_ = rk;
         size_ = 1;
       } else {
-        const int32_t pr = pred(rk);
+        const int32_t pr = bPred(rk);
         int parent;
         bool goLeft;
         if (pr >= 0 && N[pr].right < 0) {
           parent = pr;
           goLeft = false;
         } else {
-          parent = succ(rk);
+          parent = bSucc(rk);
           goLeft = true;
         }
         N[rk] = Node{(uint32_t)k, -1, -1, parent};
@@ -224,17 +220,22 @@ class RbTreeSet {
         insertFix(rk);
         ++size_;
       }
-      w[rk >> 6] |= 1ull << (rk & 63);
-      sw[rk >> 12] |= 1ull << ((rk >> 6) & 63);
+      bW_[rk >> 6] |= 1ull << (rk & 63);
+      bSw_[rk >> 12] |= 1ull << ((rk >> 6) & 63);
     }
+    bNext_ = end;
+    if (bNext_ < bIds_.size()) return false;
     // from here on the in-order sequence is maintained next to the tree (rotations do not change it)
     seqId_.clear();
-    for (int wi = 0; wi < nw; ++wi)
-      for (uint64_t m = w[wi]; m; m &= m - 1) seqId_.push_back((wi << 6) | __builtin_ctzll(m));
+    for (size_t wi = 0; wi < bW_.size(); ++wi)
+      for (uint64_t m = bW_[wi]; m; m &= m - 1) seqId_.push_back((int)((wi << 6) | __builtin_ctzll(m)));
     seqKey_.resize(seqId_.size());
     for (size_t i = 0; i < seqId_.size(); ++i) seqKey_[i] = n_[seqId_[i]].key();
     seqOn_ = true;
+    building_ = false;
+    return true;
   }
+  bool building() const { return building_; }
   // Stop maintaining the in-order sequence (trees that are only searched: add/remove then skip its O(n) updates)
   void untrackSequence() {
     seqOn_ = false;
@@ -313,6 +314,40 @@ class RbTreeSet {
   int root_ = -1, size_ = 0;
   bool seqOn_ = false;
   std::vector<int> seqId_, seqKey_;  // node ids / keys in order (after buildByRank)
+  // a build in progress (buildStart / buildStep): the put sequence, the next put, the two-level bitmap of put ranks
+  bool building_ = false;
+  std::vector<int> bIds_;
+  std::vector<int32_t> bRank_;
+  size_t bNext_ = 0;
+  int32_t bNr_ = 0;
+  std::vector<uint64_t> bW_, bSw_;
+  int32_t bPred(int32_t r) const {  // largest put rank < r, or -1
+    int wi = r >> 6;
+    uint64_t m = bW_[wi] & ((1ull << (r & 63)) - 1);
+    if (m) return (wi << 6) | (63 - __builtin_clzll(m));
+    int si = wi >> 6;
+    uint64_t sm = bSw_[si] & ((1ull << (wi & 63)) - 1);
+    while (!sm) {
+      if (--si < 0) return -1;
+      sm = bSw_[si];
+    }
+    wi = (si << 6) | (63 - __builtin_clzll(sm));
+    return (wi << 6) | (63 - __builtin_clzll(bW_[wi]));
+  }
+  int32_t bSucc(int32_t r) const {  // smallest put rank > r, or -1
+    const int ns = (int)bSw_.size();
+    int wi = r >> 6;
+    uint64_t m = (r & 63) == 63 ? 0 : bW_[wi] & (~0ull << ((r & 63) + 1));
+    if (m) return (wi << 6) | __builtin_ctzll(m);
+    int si = wi >> 6;
+    uint64_t sm = (wi & 63) == 63 ? 0 : bSw_[si] & (~0ull << ((wi & 63) + 1));
+    while (!sm) {
+      if (++si >= ns) return -1;
+      sm = bSw_[si];
+    }
+    wi = (si << 6) | __builtin_ctzll(sm);
+    return (wi << 6) | __builtin_ctzll(bW_[wi]);
+  }
 
   size_t seqPos(int node) const { return (size_t)(std::find(seqId_.begin(), seqId_.end(), node) - seqId_.begin()); }
 

@@ -126,3 +126,13 @@ BAD_DISK_CASES = [
 @pytest.mark.parametrize("props,goals", BAD_DISK_CASES)
 def test_emu_bad_disk_brokers_match_oracle(emu_lib, oracle_lib, props, goals):
     check_product_against_oracle(emu_lib, props, goals, 1.05, max_replicas=3000)
+
+
+@pytest.mark.parametrize("calls,puts", [("0", "512"), ("2", "7"), ("-1", "1")])
+def test_emu_speculative_host_work_matches_oracle(emu_lib, oracle_lib, monkeypatch, calls, puts):
+    """Device::idleWork (host work while a scan is in flight): the move-out entry tree started a few puts at a time
+    and finished by materialise(), and the move-in snapshots of upcoming polls, left undone, partly done or done —
+    the decisions are the oracle's either way."""
+    monkeypatch.setenv("CCMI_EMU_IDLE_CALLS", calls)
+    monkeypatch.setenv("CCMI_IDLE_TREE_PUTS", puts)
+    check_product_against_oracle(emu_lib, dict(num_brokers=80), DEFAULT_GOALS, 1.05, max_replicas=1500)
