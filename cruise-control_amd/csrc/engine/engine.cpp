@@ -40,7 +40,7 @@ const size_t kFirstBatchRows = envSize("CCMI_FIRST_BATCH", 2048), kBatchGrowth =
 // snapshots of upcoming queue polls computed while a move-in scan is in flight (Device::idleWork); 0 = off
 const size_t kIdleSnapshots = envCount("CCMI_IDLE_SNAPSHOTS", 8);
 // puts of the speculative entry tree per poll of an in-flight move-out scan; 0 = off (read per call: tests vary it)
-size_t idleTreePuts() { return envCount("CCMI_IDLE_TREE_PUTS", 512); }
+size_t idleTreePuts() { return envCount("CCMI_IDLE_TREE_PUTS", 64); }
 constexpr size_t kMaxBatchRows = (size_t)1 << 18;
 
 // Host view of the model for predicates.h (same expressions the kernels evaluate).
