@@ -1491,23 +1491,25 @@ class ResourceDistribution : public GoalImpl {
         hitIdx = i + (size_t)(key / N);
         dst = cands[key % N];
       } else {
-        PhaseScope pc(PH_CAND_BUILD);
-        pr.clear();
-        pb.clear();
-        pairOwner.clear();
-        for (size_t q = i; q < list.size(); ++q) {
-          const int r = list[q];
-          m.onlineFollowerBrokers(m.rPart[r], fol);
-          inorder.clear();
-          for (int fb : fol)
-            if (built ? cand.contains(fb) : inSet[fb] != 0) inorder.push_back(fb);
-          std::sort(inorder.begin(), inorder.end(), [&](int x, int y) { return cmpBroker(m, x, y) < 0; });
-          inorder.erase(std::unique(inorder.begin(), inorder.end()), inorder.end());
-          e.eligible(inorder, DA_LEADERSHIP, elig);
-          for (int fb : elig) {
-            pr.push_back(r);
-            pb.push_back(fb);
-            pairOwner.push_back((int)q);
+        {
+          PhaseScope pc(PH_CAND_BUILD);
+          pr.clear();
+          pb.clear();
+          pairOwner.clear();
+          for (size_t q = i; q < list.size(); ++q) {
+            const int r = list[q];
+            m.onlineFollowerBrokers(m.rPart[r], fol);
+            inorder.clear();
+            for (int fb : fol)
+              if (built ? cand.contains(fb) : inSet[fb] != 0) inorder.push_back(fb);
+            std::sort(inorder.begin(), inorder.end(), [&](int x, int y) { return cmpBroker(m, x, y) < 0; });
+            inorder.erase(std::unique(inorder.begin(), inorder.end()), inorder.end());
+            e.eligible(inorder, DA_LEADERSHIP, elig);
+            for (int fb : elig) {
+              pr.push_back(r);
+              pb.push_back(fb);
+              pairOwner.push_back((int)q);
+            }
           }
         }
         const int64_t key = e.pairScan(*this, pr, pb);
