@@ -1472,8 +1472,18 @@ class ResourceDistribution : public GoalImpl {
     while (z < list.size() && (m.curOffline(list[z]) || m.ru(list[z], res) != 0.0)) ++z;
     list.resize(z);
     const double upperSrc = excluded(b) ? 0 : upperThr;
-    std::vector<int32_t> cands, pr, pb, fol, elig;
+    std::vector<int32_t> cands, pr, pb, fol;
     std::vector<int32_t> pairOwner;
+    // Leadership form: each row's candidate brokers (its online followers that are members, eligible, in live (key, id)
+    // order) are kept between scans. Before the set is materialised only dst's membership and key change per accept
+    // (b leads every row), so only rows with dst among their followers are rebuilt; after it, every row is (a search in
+    // the stale-key tree may change for any broker).
+    std::vector<std::vector<int32_t>> rowCands;
+    std::vector<uint8_t> rowValid;
+    if (lead) {
+      rowCands.resize(list.size());
+      rowValid.assign(list.size(), 0);
+    }
     size_t i = 0;
     while (i < list.size()) {
       int dst = -1;
@@ -1498,14 +1508,18 @@ class ResourceDistribution : public GoalImpl {
           pairOwner.clear();
           for (size_t q = i; q < list.size(); ++q) {
             const int r = list[q];
-            m.onlineFollowerBrokers(m.rPart[r], fol);
-            inorder.clear();
-            for (int fb : fol)
-              if (built ? cand.contains(fb) : inSet[fb] != 0) inorder.push_back(fb);
-            std::sort(inorder.begin(), inorder.end(), [&](int x, int y) { return cmpBroker(m, x, y) < 0; });
-            inorder.erase(std::unique(inorder.begin(), inorder.end()), inorder.end());
-            e.eligible(inorder, DA_LEADERSHIP, elig);
-            for (int fb : elig) {
+            std::vector<int32_t>& rc = rowCands[q];
+            if (built || !rowValid[q]) {
+              m.onlineFollowerBrokers(m.rPart[r], fol);
+              inorder.clear();
+              for (int fb : fol)
+                if (built ? cand.contains(fb) : inSet[fb] != 0) inorder.push_back(fb);
+              std::sort(inorder.begin(), inorder.end(), [&](int x, int y) { return cmpBroker(m, x, y) < 0; });
+              inorder.erase(std::unique(inorder.begin(), inorder.end()), inorder.end());
+              e.eligible(inorder, DA_LEADERSHIP, rc);
+              rowValid[q] = 1;
+            }
+            for (int fb : rc) {
               pr.push_back(r);
               pb.push_back(fb);
               pairOwner.push_back((int)q);
@@ -1566,6 +1580,9 @@ class ResourceDistribution : public GoalImpl {
             PhaseScope pc(PH_CAND_BUILD);
             inorder.erase(inorder.begin() + (ptrdiff_t)at);
             if (add) inorder.insert(std::lower_bound(inorder.begin(), inorder.end(), dst, less), dst);
+          } else {
+            for (size_t q = hitIdx + 1; q < list.size(); ++q)
+              if (rowValid[q] && m.replicaOn(m.rPart[list[q]], dst) >= 0) rowValid[q] = 0;
           }
           i = hitIdx + 1;
           continue;

@@ -849,7 +849,11 @@ class Capacity : public GoalImpl {
     if (!isOver && !hasOffline(m, b)) return;
     if (res == R_NW_OUT || res == R_CPU) {
       const std::vector<int32_t> leaders = m.sorted(b, sortId(kind, true, true));
-      std::vector<int32_t> pr, pb, owner, fol, elig;
+      std::vector<int32_t> pr, pb, owner, fol;
+      // each row's sorted eligible followers, kept between scans: a move changes the utilization of b (the leader of
+      // every row) and dst only, so only rows with dst among their followers are re-sorted
+      std::vector<std::vector<int32_t>> rowCands(leaders.size());
+      std::vector<uint8_t> rowValid(leaders.size(), 0);
       size_t i = 0;
       while (i < leaders.size()) {
         // every remaining leader with its online followers' brokers by (utilization, id)
@@ -858,12 +862,16 @@ class Capacity : public GoalImpl {
         owner.clear();
         for (size_t q = i; q < leaders.size(); ++q) {
           const int r = leaders[q];
-          m.onlineFollowerBrokers(m.rPart[r], fol);
-          std::sort(fol.begin(), fol.end(), [&](int x, int y) {
-            const int c = jcmpDouble(m.bu(x, res), m.bu(y, res));
-            return c ? c < 0 : x < y;
-          });
-          e.eligible(fol, DA_LEADERSHIP, elig);
+          std::vector<int32_t>& elig = rowCands[q];
+          if (!rowValid[q]) {
+            m.onlineFollowerBrokers(m.rPart[r], fol);
+            std::sort(fol.begin(), fol.end(), [&](int x, int y) {
+              const int c = jcmpDouble(m.bu(x, res), m.bu(y, res));
+              return c ? c < 0 : x < y;
+            });
+            e.eligible(fol, DA_LEADERSHIP, elig);
+            rowValid[q] = 1;
+          }
           for (int x : elig) {
             pr.push_back(r);
             pb.push_back(x);
@@ -873,10 +881,13 @@ class Capacity : public GoalImpl {
         const int64_t key = e.pairScan(*this, pr, pb);
         if (key < 0) break;
         const size_t k = (size_t)owner[key];
-        m.relocateLeadership(m.rPart[leaders[k]], b, pb[key]);
+        const int dst = pb[key];
+        m.relocateLeadership(m.rPart[leaders[k]], b, dst);
         isOver = over(m, b);
         if (!isOver) break;
         i = k + 1;
+        for (size_t q = i; q < leaders.size(); ++q)
+          if (rowValid[q] && m.replicaOn(m.rPart[leaders[q]], dst) >= 0) rowValid[q] = 0;
       }
     }
     if (isOver || hasOffline(m, b)) {
@@ -2139,7 +2150,11 @@ class LeaderBytesIn : public GoalImpl {
     if (m.leadNwIn(b) < thr) return;
     bool over = true;
     const std::vector<int32_t> leaders = m.sorted(b, sortId(kind, true, true));
-    std::vector<int32_t> pr, pb, owner, fol, elig;
+    std::vector<int32_t> pr, pb, owner, fol;
+    // each row's sorted eligible followers, kept between scans: a move changes the bytes-in of b (the leader of every
+    // row) and dst, so only rows with dst among their followers are re-sorted
+    std::vector<std::vector<int32_t>> rowCands(leaders.size());
+    std::vector<uint8_t> rowValid(leaders.size(), 0);
     size_t i = 0;
     while (over && i < leaders.size()) {
       pr.clear();
@@ -2147,9 +2162,13 @@ class LeaderBytesIn : public GoalImpl {
       owner.clear();
       for (size_t q = i; q < leaders.size(); ++q) {
         const int r = leaders[q];
-        m.onlineFollowerBrokers(m.rPart[r], fol);
-        stableSortBy(fol, [&](int x, int y) { return jcmpDouble(m.leadNwIn(x), m.leadNwIn(y)); });
-        e.eligible(fol, DA_LEADERSHIP, elig);
+        std::vector<int32_t>& elig = rowCands[q];
+        if (!rowValid[q]) {
+          m.onlineFollowerBrokers(m.rPart[r], fol);
+          stableSortBy(fol, [&](int x, int y) { return jcmpDouble(m.leadNwIn(x), m.leadNwIn(y)); });
+          e.eligible(fol, DA_LEADERSHIP, elig);
+          rowValid[q] = 1;
+        }
         for (int x : elig) {
           pr.push_back(r);
           pb.push_back(x);
@@ -2159,9 +2178,12 @@ class LeaderBytesIn : public GoalImpl {
       const int64_t key = e.pairScan(*this, pr, pb);
       if (key < 0) break;
       const size_t k = (size_t)owner[key];
-      m.relocateLeadership(m.rPart[leaders[k]], b, pb[key]);
+      const int dst = pb[key];
+      m.relocateLeadership(m.rPart[leaders[k]], b, dst);
       over = m.leadNwIn(b) > thr;
       i = k + 1;
+      for (size_t q = i; q < leaders.size(); ++q)
+        if (rowValid[q] && m.replicaOn(m.rPart[leaders[q]], dst) >= 0) rowValid[q] = 0;
     }
     if (over) overLimit = true;
   }
