@@ -120,6 +120,8 @@ uint32_t needsOf(const DevGoal& g) {
 
 }  // namespace
 
+size_t idleTreePutsPerPoll() { return idleTreePuts(); }
+
 std::vector<int> GoalImpl::brokersToBalance(Engine& e) {
   std::vector<int> v(e.m.B);
   for (int b = 0; b < e.m.B; ++b) v[b] = b;

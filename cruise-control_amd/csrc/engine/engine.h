@@ -55,6 +55,10 @@ struct Constraint {  // BalancingConstraint
 
 class Engine;
 
+// Puts of a speculative candidate-tree build per poll of an in-flight scan (Device::idleWork; CCMI_IDLE_TREE_PUTS,
+// 0 = off). Read per call.
+size_t idleTreePutsPerPoll();
+
 // Destination-sharded scans: every shard runs the same host drivers on an identical replica of
 // the model and scans only its slice of each candidate list; `combine` MIN-reduces the shards' first-fit keys
 // (keys are global list positions, so the minimum is the reference's first accepted candidate).

@@ -1908,6 +1908,12 @@ class LeaderReplicaDistribution : public GoalImpl {
       return c ? c : jcmpInt(m.bId[x], m.bId[y]);
     };
     RbTreeSet<decltype(cmp)> cand(cmp);
+    // Non-fix form: the set's in-order sequence at entry is the members' (leader count, id) order, which is all the
+    // first scan needs; the tree itself (its put sequence decides where stale keys send later searches) is needed only
+    // from the first accepted move on. Its puts start now and run while the first scan is in flight; a call whose
+    // first scan accepts nothing never completes them.
+    std::vector<int32_t> entryOrder;
+    bool treeReady = true;
     {
       PhaseScope pi(PH_PQ_INIT);
       if (fix) {
@@ -1933,10 +1939,22 @@ class LeaderReplicaDistribution : public GoalImpl {
           std::sort(byKey.begin(), byKey.end(), [&](int x, int y) { return cmp(x, y) < 0; });
         }
         for (size_t i = 0; i < byKey.size(); ++i) rank[byKey[i]] = (int32_t)i;
-        cand.buildByRank(order, rank);
+        entryOrder = std::move(byKey);
+        cand.buildStart(std::move(order), std::move(rank));
+        treeReady = false;
       }
     }
-    cand.trackSequence();
+    auto finishTree = [&]() {
+      if (treeReady) return;
+      PhaseScope pi(PH_PQ_INIT);
+      cand.buildStep((size_t)-1);
+      cand.trackSequence();
+      treeReady = true;
+    };
+    if (treeReady) cand.trackSequence();
+    const Device::IdleScope idleScope{e.dev};
+    const size_t treePuts = idleTreePutsPerPoll();
+    if (!treeReady && treePuts > 0) e.dev->idleWork = [&]() { return !cand.buildStep(treePuts); };
     const int upperLimit = fix ? 0 : upper;
     const int id = sortId(kind, false, !fix);
     Model::Spec s;
@@ -1950,9 +1968,11 @@ class LeaderReplicaDistribution : public GoalImpl {
     std::vector<int32_t> inorder, cands;
     size_t i = 0;
     while (i < list.size()) {
-      cand.inorder(inorder);
+      if (treeReady) cand.inorder(inorder);
+      else inorder.assign(entryOrder.begin(), entryOrder.end());
       e.eligible(inorder, DA_MOVE, cands);
       const int64_t key = e.crossScan(*this, DA_MOVE, list, i, cands);
+      e.dev->idleWork = nullptr;  // the remaining puts, if the tree is needed, are finished below
       if (key < 0) break;
       const size_t N = cands.size();
       const size_t k = i + (size_t)(key / (int64_t)N);
@@ -1962,6 +1982,7 @@ class LeaderReplicaDistribution : public GoalImpl {
         m.untrack(b, id);
         return false;
       }
+      finishTree();
       cand.remove(dst);
       if (m.bNlead[dst] < upper || fix) cand.add(dst);
       i = k + 1;
