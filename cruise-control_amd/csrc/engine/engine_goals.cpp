@@ -1077,7 +1077,7 @@ class TopicReplicaDistribution : public GoalImpl {
   bool fix = false, anyAbove = false, anyUnder = false;
   std::vector<uint8_t> rebalanceTopic;
   std::vector<int32_t> upper, lower;
-  std::vector<int32_t> topicsScratch, perOff;
+  std::vector<int32_t> topicsScratch, perOff, perN;
   std::vector<uint32_t> perStamp;
   std::vector<uint8_t> perImm;
   uint32_t stamp = 0;
@@ -1153,12 +1153,12 @@ class TopicReplicaDistribution : public GoalImpl {
     PhaseScope ps(PH_OTHER_GOALS);
     Model& m = e.m;
     std::vector<int32_t>& topics = topicsScratch;
-    m.bTopicKeys[b].order(topics);  // Broker.topics(): HashMap key order
     // per-topic (offline count, has immigrant) of this broker's replicas, one pass (recounted after moves); the
     // per-topic slots are valid for the current stamp only
     if (perStamp.size() != (size_t)m.T) {
       perStamp.assign(m.T, 0);
       perOff.assign(m.T, 0);
+      perN.assign(m.T, 0);
       perImm.assign(m.T, 0);
     }
     auto recount = [&]() {
@@ -1168,18 +1168,22 @@ class TopicReplicaDistribution : public GoalImpl {
         if (perStamp[t] != stamp) {
           perStamp[t] = stamp;
           perOff[t] = 0;
+          perN[t] = 0;
           perImm[t] = 0;
         }
         perOff[t] += m.rInOff[r];
+        perN[t] += 1;
         perImm[t] |= m.rInImm[r];
       }
     };
     recount();
+    m.bTopicKeys[b].order(topics);  // Broker.topics(): HashMap key order (keys stay after a topic's last replica left)
     for (int t : topics) {
       if (!rebalanceTopic[t]) continue;
       const bool seen = perStamp[t] == stamp;
-      const int nOff = seen ? perOff[t] : 0, hasImm = seen ? perImm[t] : 0;
-      const int n = m.tcount(t, b);
+      // b's replica count of t from the same pass (Broker.numReplicasOfTopicInBroker) instead of the [T][B] count
+      // table, whose row-per-topic layout makes every lookup here a cache miss
+      const int nOff = seen ? perOff[t] : 0, hasImm = seen ? perImm[t] : 0, n = seen ? perN[t] : 0;
       const bool excl = excluded(b);
       const bool requireLess = nOff > 0 || n > upper[t] || excl;
       const bool requireMore = !excl && m.alive(b) && n - nOff < lower[t];
