@@ -696,6 +696,7 @@ ccmi_status ccmi_proposals(const ccmi_session* s, int32_t max_rf, int32_t* parti
 ccmi_status ccmi_perf(const ccmi_session* s, ccmi_perf_counters* out) {
   return guarded([&] {
     if (!s || !out) throw std::invalid_argument("null argument");
+    s->device->collectServerBusy();
     const auto& p = s->device->perf;
     out->scan_launches = p.scanLaunches;
     out->scan_kernel_ms = p.scanKernelMs;
@@ -726,7 +727,10 @@ ccmi_status ccmi_perf(const ccmi_session* s, ccmi_perf_counters* out) {
 }
 
 void ccmi_perf_reset(ccmi_session* s) {
-  if (s) s->device->perf = ccmi::DevicePerf();
+  if (s) {
+    s->device->collectServerBusy();
+    s->device->perf = ccmi::DevicePerf();
+  }
 }
 
 void ccmi_set_kernel_timing(ccmi_session* s, int32_t enabled) {

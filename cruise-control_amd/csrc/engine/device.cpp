@@ -151,6 +151,8 @@ Device::Device(int ordinal, int B, int R, int P, int T, int maxGoalSlots)
     if (nb) serverBlocks_ = std::max(8, std::min(512, (int)std::strtol(nb, nullptr, 10) / 8 * 8));
     // one workgroup per CU at most, so every workgroup of the server is resident with room for other kernels
     serverBlocks_ = std::min(serverBlocks_, prop.multiProcessorCount / 8 * 8);
+    if (const char* gs = std::getenv("CCMI_GOAL_SPLIT")) goalSplitMax_ = (int)std::strtol(gs, nullptr, 10);
+    if (const char* gw = std::getenv("CCMI_GOAL_SPLIT_WGS")) goalSplitWgs_ = (int)std::strtol(gw, nullptr, 10);
     if (serverBlocks_ < 8) serverUsable_ = false;
     if (serverUsable_) {
       dalloc(&dServerT0_, 16);  // [0] busy-time stamp, [8] the doorbell (a line of its own)
@@ -370,6 +372,7 @@ int Device::serverProgram(const DevProgram& prog, char* pay) {
 // sequence word) and wait for its result. false: the server's idle watchdog ended it before it saw the command —
 // nothing of the command ran, and the caller takes its launch path.
 bool Device::postCommand(ServerCmd& c, bool rowsSent) {
+  collectServerBusy();
   c.rowsEpoch = rowsEpoch_;
   *(volatile unsigned long long*)fg_ = (seq_ + 1) | kSeqBusy;
   hostStoreFence();
@@ -390,8 +393,27 @@ bool Device::postCommand(ServerCmd& c, bool rowsSent) {
   }
   if (rowsSent) ++rowsEpoch_;
   lastServerUse_ = nowSeconds();
-  perf.serverBusyMs += (double)hResult_[1] * 1e-5;  // 100 MHz ticks
+  busyPending_ = true;  // its busy time lands in mail[5] just after the word (collected before the next command)
+  busySeq_ = seq_;
   return true;
+}
+
+// The last server command's busy time (mail[5], tagged with its sequence; scan.hip scan_server's publish)
+void Device::collectServerBusy() {
+  if (!busyPending_) return;
+  busyPending_ = false;
+  const unsigned long long want = busySeq_ & 0xffffffull;
+  volatile unsigned long long* mail = (volatile unsigned long long*)hResult_;
+  const double t0 = nowSeconds();
+  for (uint64_t spin = 0;; ++spin) {
+    const unsigned long long w = __atomic_load_n(&mail[5], __ATOMIC_ACQUIRE);
+    if ((w >> 40) == want) {
+      perf.serverBusyMs += (double)(w & ((1ull << 40) - 1)) * 1e-5;  // 100 MHz ticks
+      return;
+    }
+    // the store left the device right behind the result word: a miss here is a lost diagnostic, never a wait on work
+    if ((spin & 1023) == 1023 && nowSeconds() - t0 > 0.1) return;
+  }
 }
 
 // params: CROSS {K, Nr, N, c0, sliced, -}; PAIRS {n, keyBase, -, -, -, -}
@@ -433,9 +455,22 @@ int64_t Device::serverRun(const DevProgram& prog, const Staged& g, int op, const
   c.progVer = ver;
   {  // every tile of the first sweep gets its own workgroup; a smaller scan leaves the others out of the command
     const uint64_t total = op == SOP_PAIRS ? (uint64_t)params[0] : (uint64_t)params[0] * (uint64_t)params[1];
-    uint64_t need = (total + 255) / 256;
-    need = std::max<uint64_t>(8, (need + 7) / 8 * 8);
-    c.nActive = (int32_t)std::min<uint64_t>(need, (uint64_t)serverBlocks_);
+    auto wgsFor = [&](int parts) {
+      const uint64_t tile = 256 / (uint64_t)parts;
+      const uint64_t need = (total + tile - 1) / tile;
+      return std::max<uint64_t>(8, (need + 7) / 8 * 8);
+    };
+    // Goal-parallel tiles: when the scan's first sweep fits the server at 2 or 4 waves per candidate, each wave
+    // evaluates a share of the goals (the conjunction's latency over the prior goals is most of a small command's
+    // in-kernel time, and the workgroups a small command leaves idle take the other shares).
+    int parts = 1;
+    for (int p : {4, 2})
+      if (p <= goalSplitMax_ && p <= prog.nGoals && wgsFor(p) <= (uint64_t)std::min(goalSplitWgs_, serverBlocks_)) {
+        parts = p;
+        break;
+      }
+    c.goalParts = parts;
+    c.nActive = (int32_t)std::min<uint64_t>(wgsFor(parts), (uint64_t)serverBlocks_);
   }
   c.nb = g.nb;
   c.nr = g.nr;

@@ -98,6 +98,9 @@ class Device {
   // returns false (each call a few microseconds of host-only work that touches no device state). Set around one
   // scan by its caller.
   std::function<bool()> idleWork;
+  // Adds the last server command's busy time to perf (the kernel publishes it just after the result word); called
+  // before every command and before perf is read.
+  void collectServerBusy();
   struct IdleScope {  // clears idleWork when the scan returns or throws
     Device* d;
     ~IdleScope() { d->idleWork = nullptr; }
@@ -262,6 +265,10 @@ class Device {
   bool serverUsable_ = false;  // set in the constructor (gfx950, CCMI_SERVER, fine-grained VRAM host-writable)
   bool serverAllowed_ = true;   // setServerAllowed
   int serverBlocks_ = 256;
+  // goal-parallel server tiles (ServerCmd.goalParts): at most this many waves per candidate (CCMI_GOAL_SPLIT: 1, 2 or
+  // 4) and only for scans whose split first sweep needs at most CCMI_GOAL_SPLIT_WGS workgroups
+  int goalSplitMax_ = 4;
+  int goalSplitWgs_ = 256;
   int progVer_ = 0;
   bool progSent_ = false;
   DevProgram lastProg_{};
@@ -273,6 +280,8 @@ class Device {
   bool ensureServer();
   int serverProgram(const DevProgram& prog, char* pay);
   bool postCommand(ServerCmd& c, bool rowsSent);
+  bool busyPending_ = false;      // a completed command's busy time not yet collected
+  unsigned long long busySeq_ = 0;
   // a K7 chain as a server command over the request arrays a0 | a1 | a2 (SOP_CHAIN); false = launch it instead
   bool serverChain(const DevProgram& prog, int mode, const int32_t* a0, int n0, const int32_t* a1, int n1,
                    const int32_t* a2, int n2, int n, int m, int maxAccepts);

@@ -265,6 +265,9 @@ struct alignas(16) ServerCmd {
   int32_t chainMode, chainN, chainM, maxAccepts;
   int32_t nl, ns;
   uint32_t oL, oS;
+  // SOP_CROSS / SOP_SEGS / SOP_PAIRS: wavefronts per candidate (1, 2 or 4), each evaluating a share of the goals
+  // (moveCandidateAcceptedPart); a tile is then kBlock / goalParts candidates
+  int32_t goalParts;
   unsigned long long chainReq;  // device addresses: HBM scratch for the request, host-mapped log and result
   unsigned long long chainLog;
   unsigned long long chainOut;

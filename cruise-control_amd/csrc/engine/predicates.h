@@ -478,6 +478,24 @@ CCMI_HD bool moveCandidateAccepted(const DevProgram& prog, const V& v, int r, in
     if (!goalAcceptMove(prog.goals[i], v, action, r, src, dst)) return false;
   return true;
 }
+// moveCandidateAccepted split over `parts` evaluators of the same candidate (the scan server's goal-parallel tiles,
+// one wavefront per part): part 0 takes the legitimacy check and the optimizing goal, the prior goals go round robin
+// (goal i to part i % parts). The candidate is accepted iff every part accepts it — the same conjunction, since every
+// check is a pure function of the view; only the order of evaluation (and the early exit) differs.
+template <class V>
+CCMI_HD bool moveCandidateAcceptedPart(const DevProgram& prog, const V& v, int r, int dst, int part, int parts) {
+  const int action = uniform(prog.action);
+  const int src = v.rbroker(r);
+  part = uniform(part);
+  if (part == 0) {
+    if (!legitMove(v, r, dst, action)) return false;
+    if (!goalSelfSatisfiedMove(prog.goals[0], v, action, r, src, dst)) return false;
+  }
+  const int nGoals = uniform(prog.nGoals);
+  for (int i = part == 0 ? parts : part; i < nGoals; i += parts)
+    if (!goalAcceptMove(prog.goals[i], v, action, r, src, dst)) return false;
+  return true;
+}
 
 // GoalUtils.eligibleReplicasForSwap (GoalUtils.java:258-274): a swap row is empty when the destination broker is
 // excluded for leadership and the (originally online) source replica is a leader, or the destination is excluded

@@ -713,6 +713,28 @@ __device__ __forceinline__ unsigned long long blockBest(const unsigned long long
   return b;
 }
 
+// First accepted candidate slot of a scan-server tile, or -1. The block's waves form kBlock / 64 / parts groups of
+// `parts` waves; group g evaluates slots [64 g, 64 g + 64), each of its waves a share of the goals, and a slot is
+// accepted when every wave of its group accepted it (parts = 1: every wave is its own group). Slots are in key order.
+__device__ __forceinline__ int tileFirst(bool ok, int parts) {
+  __shared__ unsigned long long sBal[kBlock / 64];
+  const unsigned long long bal = __ballot(ok);
+  if ((threadIdx.x & 63) == 0) sBal[threadIdx.x >> 6] = bal;
+  __syncthreads();
+  int first = -1;
+  const int groups = (kBlock / 64) / parts;
+  for (int g = 0; g < groups; ++g) {
+    unsigned long long pass = ~0ull;
+    for (int p = 0; p < parts; ++p) pass &= sBal[g * parts + p];
+    if (pass) {
+      first = g * 64 + __builtin_ctzll(pass);
+      break;
+    }
+  }
+  __syncthreads();
+  return first;
+}
+
 // Last-arriver publish: every workgroup arrives once (after its final atomicMin); the last one reads the
 // winning key and writes ONE 64-bit word {seq:32 | key+1:32} (0 in the low half = no winner) to the host
 // mailbox — a single aligned 8-byte store, so the host never sees a sequence number without its key and
@@ -1108,14 +1130,20 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, kServ
         wg = blockIdx.x / kXcds;
         wgs = nAct / kXcds;
       }
+      // goal-parallel tiles: `parts` waves per candidate, tile = kBlock / parts candidates (slot = group * 64 + lane)
+      const int parts = (c.goalParts == 2 || c.goalParts == 4) ? c.goalParts : 1;
+      const uint32_t tile = (uint32_t)(kBlock / parts);
+      const int wave = (int)(threadIdx.x >> 6);
+      const int part = wave % parts;
+      const uint32_t slot = (uint32_t)(wave / parts) * 64u + (threadIdx.x & 63u);
       const uint32_t total = (uint32_t)K * Ws;
-      for (uint32_t base = wg * kBlock; base < total; base += wgs * kBlock) {
+      for (uint32_t base = wg * tile; base < total; base += wgs * tile) {
         const uint32_t kb = base / Ws;
         const unsigned long long keyBase = (unsigned long long)kb * N + c0 + colStart + (base - kb * Ws);
         // (the first tile skips the early-exit check: a winner can hardly exist yet, and its round trip would delay
         // the tile's request loads; a superfluous tile only loses to the smaller key in atomicMin)
         if (!firstTile && blockBest(result) <= keyBase) break;
-        const uint32_t q = base + threadIdx.x;
+        const uint32_t q = base + slot;
         const uint32_t k = q / Ws;
         const uint32_t j = colStart + (q - k * Ws);
         RowRef rq{0, 0, 0, 0};
@@ -1141,30 +1169,38 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, kServ
           dq = ldSys(C + j);
         }
         if (!staged) stage();
-        unsigned long long local = kNone;
+        bool ok = false;
         if (q < total) {
           PreView v;
           v.loadDst(T, dq, ov);
           v.loadRowRef(T, prog, rq, ov);
           if (firstTile) SRV_STAMP(T, 5);  // the first tile's view loads landed
           const bool inList = (prog.filter != FILTER_RACK_AWARE || v.rackEligible()) && !v.exclLeadBlocked(prog);
-          if (inList && moveCandidateAccepted(prog, v, v.r, v.dst)) local = (unsigned long long)k * N + c0 + j;
+          ok = inList && moveCandidateAcceptedPart(prog, v, v.r, v.dst, part, parts);
         }
-        const unsigned long long m = blockMin(local);
+        const int f = tileFirst(ok, parts);
         if (firstTile) {
           SRV_STAMP(T, 3);
           firstTile = false;
         }
-        if (m != kNone) {
-          if (threadIdx.x == 0) atomicMin(result, m);
+        if (f >= 0) {  // keys grow with q inside a workgroup's range (row-major over its columns)
+          if (threadIdx.x == 0) {
+            const uint32_t qf = base + (uint32_t)f, kf = qf / Ws;
+            atomicMin(result, (unsigned long long)kf * N + c0 + colStart + (qf - kf * Ws));
+          }
           break;
         }
       }
     } else {  // SOP_PAIRS
       const int n = c.n, keyBase = c.keyBase;
-      for (int base = blockIdx.x * kBlock; base < n; base += (int)nAct * kBlock) {
+      const int parts = (c.goalParts == 2 || c.goalParts == 4) ? c.goalParts : 1;
+      const int tile = kBlock / parts;
+      const int wave = (int)(threadIdx.x >> 6);
+      const int part = wave % parts;
+      const int slot = (wave / parts) * 64 + (int)(threadIdx.x & 63);
+      for (int base = blockIdx.x * tile; base < n; base += (int)nAct * tile) {
         if (!firstTile && blockBest(result) <= (unsigned long long)(keyBase + base)) break;
-        const int q = base + threadIdx.x;
+        const int q = base + slot;
         RowRef rq{0, 0, 0, 0};
         int dq = 0;
         if (q < n) {
@@ -1172,21 +1208,20 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, kServ
           dq = ldSys(C + q);
         }
         if (!staged) stage();
-        unsigned long long local = kNone;
+        bool ok = false;
         if (q < n) {
           PreView v;
           v.loadDst(T, dq, ov);
           v.loadRowRef(T, prog, rq, ov);
-          if (!v.exclLeadBlocked(prog) && moveCandidateAccepted(prog, v, v.r, v.dst))
-            local = (unsigned long long)(keyBase + q);
+          ok = !v.exclLeadBlocked(prog) && moveCandidateAcceptedPart(prog, v, v.r, v.dst, part, parts);
         }
-        const unsigned long long m = blockMin(local);
+        const int f = tileFirst(ok, parts);
         if (firstTile) {
           SRV_STAMP(T, 3);
           firstTile = false;
         }
-        if (m != kNone) {
-          if (threadIdx.x == 0) atomicMin(result, m);
+        if (f >= 0) {
+          if (threadIdx.x == 0) atomicMin(result, (unsigned long long)(keyBase + base + f));
           break;
         }
       }
@@ -1220,20 +1255,20 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, kServ
         }
       }
       if (prev == nAct - 1) {
+        // the result and workgroup 0's start stamp in one batch of loads
         const unsigned long long v = __hip_atomic_load(&result[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const unsigned long long tStart = __hip_atomic_load(t0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         const unsigned long long lo = v == kNone ? 0ull : (v + 1) & 0xffffffffull;
         __hip_atomic_store(&result[0], kNone, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        // mail[1]: the command's busy time (100 MHz ticks from workgroup 0 seeing it to this publish), then the word
-        __hip_atomic_store(&mail[1],
-                           __builtin_amdgcn_s_memrealtime() -
-                               __hip_atomic_load(t0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
-                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        // the busy time lands before the sequence word (one 16-byte system-scope store of both words instead was
-        // measured ~16 us slower for the host to see per command: profiles/r03/c2_probe_publish16_v1.txt)
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const unsigned long long busy = __builtin_amdgcn_s_memrealtime() - tStart;
         __hip_atomic_store(&mail[0], ((c.seq & 0xffffffffull) << 32) | lo, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
+        // mail[5]: the command's busy time (100 MHz ticks from workgroup 0 seeing it to the publish, low 40 bits)
+        // tagged with the sequence's low 24 bits, stored after the word with no wait in between: the host collects it
+        // before its next command (Device::collectServerBusy) instead of the publish waiting for a second PCIe write
+        __hip_atomic_store(&mail[5], ((c.seq & 0xffffffull) << 40) | (busy & ((1ull << 40) - 1)), __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_SYSTEM);
       }
     }
@@ -1432,21 +1467,29 @@ __device__ __forceinline__ void chainApplyAny(const ChainTables& C, LoadVec* sc,
   }
 }
 
-// First accepted pair q in [start, n) on the current state (kNone if none), block-uniform.
+// First accepted pair q in [start, n) on the current state (kNone if none), block-uniform. When the rest of the list
+// fits a tile of 64 or 128 pairs, 4 or 2 waves share each pair's goals (goal-parallel tiles, tileFirst): the same
+// single tile, with the conjunction's latency split over the SIMDs.
 __device__ __forceinline__ unsigned long long chainFirstPair(const DevTables& T, const DevProgram& prog,
                                                              const OverlayLds& ov, const int32_t* pr,
                                                              const int32_t* pb, int start, int n) {
-  for (int base = start; base < n; base += kBlock) {
-    const int q = base + threadIdx.x;
-    unsigned long long local = kNone;
+  const int nGoals = prog.nGoals;
+  for (int base = start; base < n;) {
+    const int rest = n - base;
+    const int parts = (rest <= 64 && nGoals >= 4) ? 4 : ((rest <= 128 && nGoals >= 2) ? 2 : 1);  // block-uniform
+    const int wave = (int)(threadIdx.x >> 6);
+    const int part = wave % parts;
+    const int q = base + (wave / parts) * 64 + (int)(threadIdx.x & 63);
+    bool ok = false;
     if (q < n) {
       PreView v;
       v.loadDst(T, pb[q], ov);
       v.loadRow(T, prog, pr[q], ov);
-      if (!v.exclLeadBlocked(prog) && moveCandidateAccepted(prog, v, v.r, v.dst)) local = (unsigned long long)q;
+      ok = !v.exclLeadBlocked(prog) && moveCandidateAcceptedPart(prog, v, v.r, v.dst, part, parts);
     }
-    const unsigned long long m = blockMin(local);
-    if (m != kNone) return m;
+    const int f = tileFirst(ok, parts);
+    if (f >= 0) return (unsigned long long)(base + f);
+    base += kBlock / parts;
   }
   return kNone;
 }

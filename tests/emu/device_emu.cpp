@@ -140,6 +140,8 @@ Device::Device(int ordinal, int B, int R, int P, int T, int maxGoalSlots)
 }
 Device::~Device() { delete static_cast<Emu*>(st_); }
 
+void Device::collectServerBusy() {}  // no scan server in the emulator
+
 void Device::uploadIneligible(const int32_t* off, const int32_t* brokers, int n) {
   if (n <= 0) return;
   Emu& e = E(st_);

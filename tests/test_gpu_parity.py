@@ -75,6 +75,18 @@ def test_gpu_goal_subsets(gpu_lib, oracle_lib, goals):
                                  goals, 1.05)
 
 
+@pytest.mark.parametrize("split,wgs", [("1", "256"), ("2", "256"), ("4", "256"), ("4", "24")])
+def test_gpu_goal_parallel_tiles_match_oracle(gpu_lib, oracle_lib, monkeypatch, split, wgs):
+    """Scan-server commands with 1, 2 or 4 wavefronts per candidate (ServerCmd.goalParts, each wave a share of the
+    goals) decide exactly as the oracle; with a 24-workgroup split budget larger scans fall back to fewer parts."""
+    monkeypatch.setenv("CCMI_GOAL_SPLIT", split)
+    monkeypatch.setenv("CCMI_GOAL_SPLIT_WGS", wgs)
+    check_product_against_oracle(gpu_lib, dict(num_racks=5, num_brokers=20, num_replicas=6000, num_topics=300),
+                                 DEFAULT_GOALS, 1.05)
+    check_product_against_oracle(gpu_lib, dict(num_racks=8, num_brokers=300, num_replicas=30000, num_topics=1000),
+                                 C1_GOALS, 1.05)
+
+
 @pytest.mark.parametrize("props", [dict(), dict(num_racks=20, num_brokers=1000, num_replicas=99999, num_topics=3000),
                                    dict(num_racks=3, num_brokers=10, num_replicas=3000, num_topics=100,
                                         num_dead_brokers=2)])
