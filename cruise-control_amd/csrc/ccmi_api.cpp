@@ -301,6 +301,7 @@ void ccmi_cluster_buffers_free(ccmi_cluster_buffers* buf) { delete buf; }
 ccmi_status ccmi_session_create(int32_t device_ordinal, const ccmi_cluster_desc* desc, ccmi_session** out) {
   return guarded([&] {
     if (!desc || !out) throw std::invalid_argument("null argument");
+    ccmi::Device::pinHostThread(device_ordinal);  // before the session's host memory is first touched
     auto s = std::make_unique<ccmi_session>();
     s->model.build(*desc);
     ccmi::Model& m = s->model;

@@ -14,7 +14,12 @@
 #include <chrono>
 #include <mutex>
 
+#include <pthread.h>
 #include <sched.h>
+
+#include <cctype>
+#include <fstream>
+#include <string>
 
 namespace ccmi {
 
@@ -89,6 +94,39 @@ struct DeviceGuard {
     if (prev >= 0) (void)hipSetDevice(prev);
   }
 };
+
+void Device::pinHostThread(int ordinal) {
+  const char* e = std::getenv("CCMI_NUMA_PIN");
+  if (e && e[0] == '0') return;
+  char bus[64] = {0};
+  if (hipDeviceGetPCIBusId(bus, (int)sizeof(bus), ordinal) != hipSuccess) return;
+  for (char* p = bus; *p; ++p) *p = (char)std::tolower((unsigned char)*p);
+  std::ifstream f(std::string("/sys/bus/pci/devices/") + bus + "/local_cpulist");
+  std::string list;
+  if (!std::getline(f, list)) return;
+  cpu_set_t local;
+  CPU_ZERO(&local);
+  size_t i = 0;
+  while (i < list.size()) {  // "a-b,c,..."
+    char* end = nullptr;
+    const long a = std::strtol(list.c_str() + i, &end, 10);
+    if (end == list.c_str() + i) return;
+    long b = a;
+    i = (size_t)(end - list.c_str());
+    if (i < list.size() && list[i] == '-') {
+      b = std::strtol(list.c_str() + i + 1, &end, 10);
+      i = (size_t)(end - list.c_str());
+    }
+    for (long c = a; c <= b && c < CPU_SETSIZE; ++c) CPU_SET((int)c, &local);
+    if (i < list.size() && list[i] == ',') ++i;
+    else break;
+  }
+  cpu_set_t cur, both;
+  if (pthread_getaffinity_np(pthread_self(), sizeof(cur), &cur) != 0) return;
+  CPU_AND(&both, &cur, &local);
+  if (CPU_COUNT(&both) == 0 || CPU_EQUAL(&both, &cur)) return;
+  (void)pthread_setaffinity_np(pthread_self(), sizeof(both), &both);
+}
 
 int Device::countGfx950() {
   int n = 0;

@@ -90,6 +90,12 @@ class Device {
  public:
   Device(int ordinal, int B, int R, int P, int T, int maxGoalSlots);
   static int countGfx950();  // visible gfx950 devices
+  // Narrows the calling thread's CPU affinity to the CPUs of the device's NUMA node (PCI sysfs local_cpulist,
+  // intersected with the current mask; unchanged when that is empty or already local; CCMI_NUMA_PIN=0: never). Every
+  // scan is a round trip through host memory (the command through the BAR, the result into a host-mapped mailbox the
+  // thread spins on); from the other socket it measured 30 us instead of 20 us (profiles/r04/numa_ab.txt). Called
+  // before a session allocates anything, so its host buffers are first touched on that node.
+  static void pinHostThread(int ordinal);
   ~Device();
   Device(const Device&) = delete;
   Device& operator=(const Device&) = delete;

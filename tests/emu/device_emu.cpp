@@ -125,6 +125,7 @@ Emu& E(void* st) { return *static_cast<Emu*>(st); }
 }  // namespace
 
 int Device::countGfx950() { return 1; }  // one emulated device
+void Device::pinHostThread(int) {}
 
 Device::Device(int ordinal, int B, int R, int P, int T, int maxGoalSlots)
     : ordinal_(ordinal), B_(B), R_(R), P_(P), T_(T), ldB_((B + 3) & ~3), G_(maxGoalSlots) {
