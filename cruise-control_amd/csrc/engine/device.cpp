@@ -190,6 +190,7 @@ Device::Device(int ordinal, int B, int R, int P, int T, int maxGoalSlots)
     // one workgroup per CU at most, so every workgroup of the server is resident with room for other kernels
     serverBlocks_ = std::min(serverBlocks_, prop.multiProcessorCount / 8 * 8);
     if (const char* gs = std::getenv("CCMI_GOAL_SPLIT")) goalSplitMax_ = (int)std::strtol(gs, nullptr, 10);
+    if (const char* sa = std::getenv("CCMI_SERVER_APPLY")) applyViaServer_ = sa[0] != '0';
     if (const char* gw = std::getenv("CCMI_GOAL_SPLIT_WGS")) goalSplitWgs_ = (int)std::strtol(gw, nullptr, 10);
     if (serverBlocks_ < 8) serverUsable_ = false;
     if (serverUsable_) {
@@ -361,6 +362,25 @@ void Device::stopServer() {
 
 // A cross / pair scan the running (or a newly started) server can take: its rows fit the LDS overlay and, when the
 // program reads topic counts, no topic delta is pending (those are applied by `prep` before any workgroup reads).
+// The pending rows for a served scan. A scan whose program reads topic counts cannot be served while topic-count
+// deltas are pending (the LDS overlay shadows records, not counts), so those go to the tables first in an apply-only
+// server command — a SOP_CHAIN with no pairs: workgroup 0 applies the rows and deltas and releases them — two server
+// round trips instead of stopping the server for a prep + scan launch and restarting it (CCMI_SERVER_APPLY=0: off).
+Device::Staged Device::packForServer(const DevProgram& prog, bool readsTc, bool& serve) {
+  Staged g = packUpdates(0);
+  serve = serveScan(prog, g, readsTc);
+  if (serve || !readsTc || g.nt == 0 || !applyViaServer_ || !serverUsable_ || !serverAllowed_ || !dRLoad_) return g;
+  unpackUpdates(g);
+  static const int32_t none = 0;
+  if (serverChain(prog, CM_PAIRS, &none, 0, &none, 0, &none, 0, 0, 0, 0)) {
+    perf.serverChains--;  // not a chain
+    perf.serverApplies++;
+  }
+  g = packUpdates(0);
+  serve = serveScan(prog, g, readsTc);
+  return g;
+}
+
 bool Device::serveScan(const DevProgram& prog, const Staged& g, bool readsTopicCounts) {
   (void)prog;
   if (!serverUsable_ || !serverAllowed_) return false;
@@ -537,6 +557,10 @@ bool Device::serverChain(const DevProgram& prog, int mode, const int32_t* a0, in
   const size_t words = (size_t)n0 + n1 + n2;
   const size_t oRows = align16(sizeof(DevProgram));
   const Staged g = packUpdates(0);
+  if (g.nb > kOverlayRows || g.nr > kOverlayRows || g.np > kOverlayRows) {  // the server stages rows in its LDS overlay
+    unpackUpdates(g);
+    return false;
+  }
   const size_t oL = oRows + g.end, oS = oL + align16(nl * sizeof(LoadRow)), oA = oS + align16(ns * sizeof(SlotRow));
   const size_t end = oA + align16(words * 4);
   ensureFg(kCmdBytes + end);
@@ -981,8 +1005,9 @@ int64_t Device::scanCross(const DevProgram& prog, const int32_t* reps, int K, co
   const size_t req = oCand + align16((size_t)Nr * 4);
   const bool readsTc = (prog.needs & (NEED_TOPIC | NEED_TLEAD)) != 0;
   {
-    const Staged g = packUpdates(0);
-    if (serveScan(prog, g, readsTc)) {
+    bool serve = false;
+    const Staged g = packForServer(prog, readsTc, serve);
+    if (serve) {
       const int32_t params[6] = {K, Nr, N, c0, Nr >= (int)scanXcdSliceMinCols() ? 1 : 0, 0};
       const int64_t key = serverRun(prog, g, SOP_CROSS, reps, (size_t)K, cands + c0, (size_t)Nr, params);
       if (key != INT64_MIN) {
@@ -1073,8 +1098,9 @@ int64_t Device::scanPairs(const DevProgram& prog, const int32_t* pr, const int32
   const size_t req = oB + align16((size_t)n * 4);
   const bool readsTc = (prog.needs & (NEED_TOPIC | NEED_TLEAD)) != 0;
   {
-    const Staged g0 = packUpdates(0);
-    if (serveScan(prog, g0, readsTc)) {
+    bool serve = false;
+    const Staged g0 = packForServer(prog, readsTc, serve);
+    if (serve) {
       const int32_t params[6] = {n, p0, 0, 0, 0, 0};
       const int64_t key = serverRun(prog, g0, SOP_PAIRS, pr + p0, (size_t)n, pb + p0, (size_t)n, params);
       if (key != INT64_MIN) {
@@ -1160,8 +1186,9 @@ int64_t Device::scanSegs(const DevProgram& prog, const std::vector<SegIn>& segs,
     segTab_.push_back(SegEntry{0, start});
   }
   if (served) {
-    const Staged g = packUpdates(0);
-    if (serveScan(prog, g, readsTc)) {
+    bool serve = false;
+    const Staged g = packForServer(prog, readsTc, serve);
+    if (serve) {
       const int S = (int)segs.size();
       const int32_t params[6] = {(int32_t)K, Nr, N, c0, Nr >= (int)scanXcdSliceMinCols() ? 1 : 0, S};
       const int64_t key = serverRun(prog, g, SOP_SEGS, segTab_.data(), (size_t)S + 1, cands + c0, (size_t)Nr, params);

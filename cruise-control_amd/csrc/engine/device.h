@@ -55,6 +55,7 @@ struct DevicePerf {
   int64_t serverPayloadBytes = 0;  // command payload written through the BAR (program, rows, request arrays)
   int64_t serverRequired = 0;  // candidates those scans had to evaluate
   int64_t serverChains = 0;    // K7 chains the running server took as commands (no launch, no server restart)
+  int64_t serverApplies = 0;   // apply-only server commands (topic-count deltas before a served scan that reads them)
   double serverResidentMs = 0;  // HIP-event time from each server launch to its exit (kernel timing on)
 };
 
@@ -274,6 +275,7 @@ class Device {
   // goal-parallel server tiles (ServerCmd.goalParts): at most this many waves per candidate (CCMI_GOAL_SPLIT: 1, 2 or
   // 4) and only for scans whose split first sweep needs at most CCMI_GOAL_SPLIT_WGS workgroups
   int goalSplitMax_ = 4;
+  bool applyViaServer_ = true;  // packForServer
   int goalSplitWgs_ = 256;
   int progVer_ = 0;
   bool progSent_ = false;
@@ -286,6 +288,7 @@ class Device {
   bool ensureServer();
   int serverProgram(const DevProgram& prog, char* pay);
   bool postCommand(ServerCmd& c, bool rowsSent);
+  Staged packForServer(const DevProgram& prog, bool readsTc, bool& serve);
   bool busyPending_ = false;      // a completed command's busy time not yet collected
   unsigned long long busySeq_ = 0;
   // a K7 chain as a server command over the request arrays a0 | a1 | a2 (SOP_CHAIN); false = launch it instead
