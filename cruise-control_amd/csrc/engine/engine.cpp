@@ -1309,9 +1309,12 @@ class ResourceDistribution : public GoalImpl {
         }
       }
     }
-    static const bool worker = std::getenv("CCMI_TREE_WORKER") != nullptr;
+    // The entry tree is built on a helper thread from the call's entry on (it runs beside this call's host work and
+    // scans; materialise() adopts it), for clusters of at least CCMI_TREE_WORKER_MIN brokers (2048); CCMI_TREE_WORKER=0
+    // builds on this thread instead, a few puts per poll of the in-flight scans (Device::idleWork). Read per call.
+    const char* wEnv = std::getenv("CCMI_TREE_WORKER");
     const char* minEnv = std::getenv("CCMI_TREE_WORKER_MIN");
-    const bool useWorker = worker && m.B >= (minEnv ? std::atoi(minEnv) : 2048);
+    const bool useWorker = !(wEnv && wEnv[0] == '0') && m.B >= (minEnv ? std::atoi(minEnv) : 2048);
     if (useWorker) {
       if (!treeWorker) treeWorker = std::make_unique<TreeWorker>();
       treeWorker->submit(inorder, m.B);  // `inorder` is the members' entry (key, id) order

@@ -136,3 +136,13 @@ def test_emu_speculative_host_work_matches_oracle(emu_lib, oracle_lib, monkeypat
     monkeypatch.setenv("CCMI_EMU_IDLE_CALLS", calls)
     monkeypatch.setenv("CCMI_IDLE_TREE_PUTS", puts)
     check_product_against_oracle(emu_lib, dict(num_brokers=80), DEFAULT_GOALS, 1.05, max_replicas=1500)
+
+
+@pytest.mark.parametrize("props", [dict(num_brokers=80), dict(num_racks=5, num_brokers=20, num_replicas=6000,
+                                                               num_topics=300)])
+def test_emu_tree_worker_matches_oracle(emu_lib, oracle_lib, monkeypatch, props):
+    """The move-out entry tree built on the helper thread (TreeWorker, on by default from 2048 brokers; forced here for
+    small clusters): adopted by materialise(), or superseded by the next call's submission when no step needs it."""
+    monkeypatch.setenv("CCMI_TREE_WORKER", "1")
+    monkeypatch.setenv("CCMI_TREE_WORKER_MIN", "1")
+    check_product_against_oracle(emu_lib, props, DEFAULT_GOALS, 1.05, max_replicas=1500)
