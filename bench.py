@@ -257,8 +257,8 @@ def pmc_traffic(workload: str, kernels=SCAN_KERNELS):
 
 def pmc_server_traffic(workload: str, perf):
     """HBM bytes per scan-server command: scan_server's counter bytes per launch in the newest committed PMC summary
-    (one proposal of this workload, so its launches serve the same commands per launch as this run) divided by this
-    run's commands per server launch. The counters also see the idle workgroups polling the command word."""
+    divided by the commands per server launch of the profiled run itself (its bench line, <workload>_bench_prof*.json
+    beside the summary; this run's ratio when that is missing). The counters also see the idle workgroups polling."""
     import glob
     paths = sorted(glob.glob(os.path.join(REPO, "profiles", "r*", f"{workload}_pmc_summary.json")))
     if not paths:
@@ -268,6 +268,15 @@ def pmc_server_traffic(workload: str, perf):
     if not k or perf.server_launches <= 0:
         return None, None
     per_launch = perf.server_scans / perf.server_launches
+    prof = sorted(glob.glob(os.path.join(os.path.dirname(paths[-1]), f"{workload}_bench_prof*.json")))
+    if prof:
+        try:
+            with open(prof[-1]) as f:
+                r = json.loads(f.read().strip().splitlines()[-1])["roofline"]
+            if r.get("server_launches_per_step"):
+                per_launch = r["server_commands_per_step"] / r["server_launches_per_step"]
+        except (OSError, ValueError, KeyError, IndexError):
+            pass
     return k["hbm_bytes_per_launch"] / per_launch, os.path.relpath(paths[-1], REPO)
 
 
