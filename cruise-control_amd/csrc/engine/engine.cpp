@@ -1494,17 +1494,18 @@ class ResourceDistribution : public GoalImpl {
       int dst = -1;
       size_t hitIdx = 0;
       if (!lead) {
+        const std::vector<int32_t>* cl;
         {
           PhaseScope pc(PH_CAND_BUILD);
           if (built) cand.inorder(inorder);
           // (the lazy order is kept up to date after every accept below)
-          e.eligible(inorder, DA_MOVE, cands);
+          cl = &e.eligibleView(inorder, DA_MOVE, cands);
         }
-        const int64_t key = e.crossScan(*this, DA_MOVE, list, i, cands);
+        const int64_t key = e.crossScan(*this, DA_MOVE, list, i, *cl);
         if (key < 0) break;
-        const int N = (int)cands.size();
+        const int N = (int)cl->size();
         hitIdx = i + (size_t)(key / N);
-        dst = cands[key % N];
+        dst = (*cl)[key % N];
       } else {
         {
           PhaseScope pc(PH_CAND_BUILD);

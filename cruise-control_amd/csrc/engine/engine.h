@@ -150,6 +150,14 @@ class Engine {
   int64_t swapScan(GoalImpl& self, const std::vector<int32_t>& srcs, const std::vector<int32_t>& cbOff,
                    const std::vector<int32_t>& cbRep, const SwapLimit& lim = SwapLimit());
   void eligible(const std::vector<int32_t>& in, int action, std::vector<int32_t>& out) const;
+  // eligible() without the copy when no exclusion applies to the action (the result is `in` itself, else `scratch`)
+  const std::vector<int32_t>& eligibleView(const std::vector<int32_t>& in, int action,
+                                           std::vector<int32_t>& scratch) const {
+    const bool keepsAll = action == DA_LEADERSHIP ? !opt.anyExclLead : (!opt.anyRequested && !opt.anyExclMove);
+    if (keepsAll) return in;
+    eligible(in, action, scratch);
+    return scratch;
+  }
   // Reference-visited candidates of replica r over cands[0, n) (eligible lists): the entries the replica-dependent
   // filters of GoalUtils.eligibleBrokers keep (blocked), skipping brokers that host r's partition when
   // `skipHosts` (candidate lists the device scans whole while the reference's list leaves the hosts out).
