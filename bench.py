@@ -435,6 +435,20 @@ def main() -> None:
         required_bytes_per_launch = perf.scan_required * BYTES_PER_CANDIDATE / launches
     achieved = required_bytes_per_launch / (scan_avg_ms * 1e-3) / 1e9 if scan_avg_ms > 0 else 0.0
     server = perf.server_scans > 0 and not intra
+    per_command = None
+    if server:
+        # The per-command view (in-kernel busy time per command) is kept as a secondary figure; the headline is the
+        # rocprof-reproducible one: algorithmic bytes per scan_server LAUNCH over its average launch duration (HIP events
+        # from launch to exit on the session stream, the same interval rocprofv3's kernel trace reports, idle polling
+        # between the host's commands included).
+        per_command = {"avg_us": scan_avg_ms * 1e3, "algorithmic_bytes": required_bytes_per_launch,
+                       "achieved": achieved, "frac": achieved / HBM_PEAK_GBS,
+                       "note": "in-kernel busy time per command (s_memrealtime, command seen -> result published)"}
+        if perf.server_resident_ms > 0:
+            launches = max(1, perf.server_launches)
+            scan_avg_ms = perf.server_resident_ms / launches
+            required_bytes_per_launch = perf.server_required * BYTES_PER_CANDIDATE / launches
+            achieved = required_bytes_per_launch / (scan_avg_ms * 1e-3) / 1e9
 
     if rank != 0:
         dist.destroy_process_group()
@@ -445,8 +459,11 @@ def main() -> None:
     traffic_unit = "HBM bytes per scan launch"
     if server:
         st, ss = pmc_server_traffic(args.workload, perf)
-        if st is not None:
-            traffic, traffic_src, traffic_unit = st, ss, "HBM bytes per server command"
+        if per_command is not None:
+            per_command["traffic"] = st
+            per_command["traffic_over_algorithmic"] = st / per_command["algorithmic_bytes"] if st else None
+        traffic, traffic_src = pmc_traffic(args.workload, ("scan_server",))
+        traffic_unit = "HBM bytes per scan_server launch"
     line = {
         "metric": "candidate moves evaluated/s + proposal wall time, 10K brokers/1M replicas",
         "value": cands / elapsed,
@@ -479,11 +496,12 @@ def main() -> None:
                      "traffic_source": traffic_src,
                      "kernel": ("K6 intra_brokers (one wavefront per broker; algorithmic bytes = 17 B per disk + 29 B per "
                                 "replica entry read once)" if intra else
-                                "K8 scan_server (persistent; per command: in-kernel busy time, the command's required "
-                                "candidates x 96 B)" if server else
+                                "K8 scan_server (persistent; per launch: the required candidates of its commands x 96 B "
+                                "over the launch's residency, HIP events on the session stream)" if server else
                                 "candidate scans (scan_cross/scan_pairs/scan_swap/chain_pairs/chain_rack_rows)"),
                      "avg_launch_us": scan_avg_ms * 1e3,
-                     "avg_unit": "per server command" if server else "per launch",
+                     "avg_unit": "per launch",
+                     "per_command": per_command,
                      "launches_per_step": perf.intra_launches if intra else perf.scan_launches,
                      "server_launches_per_step": perf.server_launches,
                      "server_commands_per_step": perf.server_scans,

@@ -14,6 +14,7 @@
 #include "engine/prof.h"
 #include "engine/shard_rccl.h"
 #include "engine/shard_shm.h"
+#include "engine/threadpin.h"
 
 namespace ccmi {
 ccmi_cluster_buffers* generateRandomCluster(const ccmi_random_cluster_props& p);
@@ -301,7 +302,7 @@ void ccmi_cluster_buffers_free(ccmi_cluster_buffers* buf) { delete buf; }
 ccmi_status ccmi_session_create(int32_t device_ordinal, const ccmi_cluster_desc* desc, ccmi_session** out) {
   return guarded([&] {
     if (!desc || !out) throw std::invalid_argument("null argument");
-    ccmi::Device::pinHostThread(device_ordinal);  // before the session's host memory is first touched
+    const ccmi::ThreadPin pin(device_ordinal);  // the session's host memory is first touched on the GPU's node
     auto s = std::make_unique<ccmi_session>();
     s->model.build(*desc);
     ccmi::Model& m = s->model;
@@ -445,6 +446,7 @@ ccmi_status ccmi_goal_optimize(ccmi_session* s, int32_t goal_kind, const int32_t
       if (std::find(priors.begin(), priors.end(), g) == priors.end()) priors.push_back(g);
     }
     auto g = ccmi::makeGoal(goal_kind);
+    const ccmi::ThreadPin pin(s->deviceOrdinal);  // restored when the call returns
     StopServerOnExit stop{s};
     setOptions(s, c, o);
     validateChain(s, &goal_kind, 1, priors);
@@ -464,6 +466,7 @@ ccmi_status ccmi_optimizations(ccmi_session* s, const int32_t* goal_kinds, int32
   return guarded([&] {
     if (!s || (!goal_kinds && n_goals > 0)) throw std::invalid_argument("null argument");
     if (n_goals <= 0) throw std::invalid_argument("At least one goal must be provided to get an optimization result.");
+    const ccmi::ThreadPin pin(s->deviceOrdinal);  // restored when the call returns
     StopServerOnExit stop{s};
     setOptions(s, c, o);
     validateChain(s, goal_kinds, n_goals);
@@ -519,21 +522,7 @@ ccmi_status ccmi_action_acceptance_by_kind(ccmi_session* s, int32_t kind, const 
 ccmi_status ccmi_session_apply(ccmi_session* s, const ccmi_action* actions, int64_t n, int64_t* applied) {
   if (applied) *applied = 0;
   // the proposals are the diff against the initial placement after every action applied, also when a later one fails
-  bool rebuildFailed = false;
-  struct Rebuild {  // a destructor is noexcept: a failed rebuild is reported through the status below
-    ccmi_session* s;
-    bool& failed;
-    ~Rebuild() {
-      try {
-        if (s) buildProposals(s);
-      } catch (std::exception& e) {
-        failed = true;
-        fail(CCMI_E_INVALID, std::string("rebuilding the proposals failed: ") + e.what());
-      }
-    }
-  };
   const ccmi_status st = [&] {
-    Rebuild rebuild{s, rebuildFailed};
     return guarded([&] {
       if (!s || (n > 0 && !actions) || n < 0) throw std::invalid_argument("null argument");
       ccmi::Model& m = s->model;
@@ -606,7 +595,14 @@ ccmi_status ccmi_session_apply(ccmi_session* s, const ccmi_action* actions, int6
       return CCMI_OK;
     });
   }();
-  return st == CCMI_OK && rebuildFailed ? CCMI_E_INVALID : st;
+  try {
+    if (s) buildProposals(s);
+  } catch (std::exception& e) {
+    // a rejected action's message (the last error when st != OK) stays first
+    const std::string msg = std::string("rebuilding the proposals failed: ") + e.what();
+    return fail(st == CCMI_OK ? CCMI_E_INVALID : st, st == CCMI_OK ? msg : g_err + "; " + msg);
+  }
+  return st;
 }
 
 ccmi_status ccmi_compute_cluster_stats(ccmi_session* s, const ccmi_balancing_constraint* c, const ccmi_opt_options* o,

@@ -2,6 +2,7 @@
 #include "device.h"
 #include "intra.h"
 #include "prof.h"
+#include "threadpin.h"
 
 #include <hip/hip_runtime.h>
 
@@ -95,37 +96,12 @@ struct DeviceGuard {
   }
 };
 
-void Device::pinHostThread(int ordinal) {
-  const char* e = std::getenv("CCMI_NUMA_PIN");
-  if (e && e[0] == '0') return;
+bool deviceLocalCpuList(int ordinal, std::string& out) {
   char bus[64] = {0};
-  if (hipDeviceGetPCIBusId(bus, (int)sizeof(bus), ordinal) != hipSuccess) return;
+  if (hipDeviceGetPCIBusId(bus, (int)sizeof(bus), ordinal) != hipSuccess) return false;
   for (char* p = bus; *p; ++p) *p = (char)std::tolower((unsigned char)*p);
   std::ifstream f(std::string("/sys/bus/pci/devices/") + bus + "/local_cpulist");
-  std::string list;
-  if (!std::getline(f, list)) return;
-  cpu_set_t local;
-  CPU_ZERO(&local);
-  size_t i = 0;
-  while (i < list.size()) {  // "a-b,c,..."
-    char* end = nullptr;
-    const long a = std::strtol(list.c_str() + i, &end, 10);
-    if (end == list.c_str() + i) return;
-    long b = a;
-    i = (size_t)(end - list.c_str());
-    if (i < list.size() && list[i] == '-') {
-      b = std::strtol(list.c_str() + i + 1, &end, 10);
-      i = (size_t)(end - list.c_str());
-    }
-    for (long c = a; c <= b && c < CPU_SETSIZE; ++c) CPU_SET((int)c, &local);
-    if (i < list.size() && list[i] == ',') ++i;
-    else break;
-  }
-  cpu_set_t cur, both;
-  if (pthread_getaffinity_np(pthread_self(), sizeof(cur), &cur) != 0) return;
-  CPU_AND(&both, &cur, &local);
-  if (CPU_COUNT(&both) == 0 || CPU_EQUAL(&both, &cur)) return;
-  (void)pthread_setaffinity_np(pthread_self(), sizeof(both), &both);
+  return (bool)std::getline(f, out);
 }
 
 int Device::countGfx950() {
@@ -1569,6 +1545,10 @@ void Device::intraRun(const IntraRequest& q, IntraResult& out) {
     dallocTracked(&dSnapB_, c, o);
     dallocTracked(&dOrdRev_, c, o);
     dallocTracked(&dOrdFwd_, c, o);
+    dallocTracked(&dEDu_, c, o);
+    dallocTracked(&dEOrig_, c, o);
+    dallocTracked(&dEKeyRev_, c, o);
+    dallocTracked(&dEKeyFwd_, c, o);
     entCap_ = c;
   }
   hipCheck(hipMemcpyAsync(dEOff_, q.eOff, sizeof(int32_t) * (B_ + 1), hipMemcpyHostToDevice, ST), "eOff");
@@ -1622,6 +1602,10 @@ void Device::intraRun(const IntraRequest& q, IntraResult& out) {
   A.snapB = dSnapB_;
   A.ordRev = dOrdRev_;
   A.ordFwd = dOrdFwd_;
+  A.eDu = dEDu_;
+  A.eOrig = dEOrig_;
+  A.eKeyRev = dEKeyRev_;
+  A.eKeyFwd = dEKeyFwd_;
   A.nSel = dNSel_;
   A.hist = dHist_;
   A.upperOut = dUpper_ + (size_t)q.slot * B_;

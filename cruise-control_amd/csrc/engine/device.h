@@ -91,12 +91,6 @@ class Device {
  public:
   Device(int ordinal, int B, int R, int P, int T, int maxGoalSlots);
   static int countGfx950();  // visible gfx950 devices
-  // Narrows the calling thread's CPU affinity to the CPUs of the device's NUMA node (PCI sysfs local_cpulist,
-  // intersected with the current mask; unchanged when that is empty or already local; CCMI_NUMA_PIN=0: never). Every
-  // scan is a round trip through host memory (the command through the BAR, the result into a host-mapped mailbox the
-  // thread spins on); from the other socket it measured 30 us instead of 20 us (profiles/r04/numa_ab.txt). Called
-  // before a session allocates anything, so its host buffers are first touched on that node.
-  static void pinHostThread(int ordinal);
   ~Device();
   Device(const Device&) = delete;
   Device& operator=(const Device&) = delete;
@@ -341,6 +335,9 @@ class Device {
           *dStatus_ = nullptr, *dLogRep_ = nullptr, *dLogSrc_ = nullptr, *dLogDst_ = nullptr, *dCRep_ = nullptr,
           *dCSrc_ = nullptr, *dCDst_ = nullptr;
   int64_t *dLogOff_ = nullptr, *dCand_ = nullptr, *dCOff_ = nullptr;
+  double* dEDu_ = nullptr;  // K6 entry-indexed gathers (IntraArgs.eDu / eOrig / eKeyRev / eKeyFwd)
+  int32_t* dEOrig_ = nullptr;
+  uint64_t *dEKeyRev_ = nullptr, *dEKeyFwd_ = nullptr;
   size_t entCap_ = 0, logCap_ = 0, compactCap_ = 0;
   DiskStatsOut* dDiskStats_ = nullptr;
   std::vector<void*> intraAllocs_;

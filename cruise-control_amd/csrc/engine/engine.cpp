@@ -968,10 +968,12 @@ class ReplicaDistribution : public GoalImpl {
 // Builds ResourceDistributionGoal.moveOut's entry-state candidate TreeSet on a helper thread while the driver scans:
 // the same put sequence (members in ascending id, placed by their entry (key, id) rank) the driver would otherwise run
 // when its lazy candidate order stops being exact. Most calls never need the tree: a newer submission cancels the
-// build in flight and the driver never waits except in take(). Used for clusters of at least CCMI_TREE_WORKER_MIN
-// brokers (default 2048; smaller trees are cheaper to build on the driver thread) when CCMI_TREE_WORKER=1. Off by
-// default: on the GPU box the second busy host thread made whole C2 proposals 1.3-2.5 s slower in some runs (the
-// scan-wait and in-kernel server times grew with it) for a best-case gain of 0.3 s (profiles/r03/c2_ab_worker_v2.txt).
+// build in flight, and the driver waits (on a condition variable) only in take(). On by default for clusters of at
+// least CCMI_TREE_WORKER_MIN brokers (2048; smaller trees are cheaper to build on the driver thread), CCMI_TREE_WORKER=0
+// turns it off. profiles/r04/tree_worker_ab_*.txt: tree.build 1.12 -> 0.79 s and whole C2 proposals 7.36-7.43 ->
+// 6.15-6.71 s on one box (round 3's version, which spun on the driver side, had cost 1.3-2.5 s on some boxes).
+// Workers are leased per move-out call from one process-wide pool (TreeWorkerPool) of at most CCMI_TREE_WORKERS
+// threads (default 4): concurrent sessions share them, and a call that finds none free builds on its own thread.
 class TreeWorker {
  public:
   struct RankOnly {  // buildByRank never compares
@@ -999,15 +1001,19 @@ class TreeWorker {
     }
     cv_.notify_one();
   }
+  // the build in flight (if any) is no longer wanted (the lease ends)
+  void cancel() { cancel_.store(true, std::memory_order_relaxed); }
   // the latest submission's tree (waits for it); its structure is handed over with RbTreeSet::adopt
   Tree& take() {
-    const uint64_t want = gen_;  // only the driver thread submits
-    while (done_.load(std::memory_order_acquire) != want) std::this_thread::yield();
+    std::unique_lock<std::mutex> l(mu_);
+    const uint64_t want = gen_;
+    cvDone_.wait(l, [&] { return done_ == want; });
     return tree_;
   }
 
  private:
   void loop() {
+    pthread_setname_np(pthread_self(), "ccmi-tree");
     uint64_t started = 0;
     for (;;) {
       uint64_t gen;
@@ -1031,7 +1037,13 @@ class TreeWorker {
       for (int x = 0; x < B_; ++x)
         if (mark_[x]) ids_.push_back(x);
       tree_.buildByRank(ids_, rank_, &cancel_);
-      if (!cancel_.load(std::memory_order_relaxed)) done_.store(gen, std::memory_order_release);
+      if (!cancel_.load(std::memory_order_relaxed)) {
+        {
+          std::lock_guard<std::mutex> l(mu_);
+          done_ = gen;
+        }
+        cvDone_.notify_one();
+      }
     }
   }
   Tree tree_;
@@ -1039,13 +1051,52 @@ class TreeWorker {
   std::vector<int> ids_;
   std::vector<uint8_t> mark_;
   int nextB_ = 0, B_ = 0;
-  uint64_t gen_ = 0;             // submissions (guarded by mu_; read unguarded by the driver thread, its only writer)
-  std::atomic<uint64_t> done_{0};  // the submission whose tree is complete in tree_
+  uint64_t gen_ = 0;   // submissions (guarded by mu_)
+  uint64_t done_ = 0;  // the submission whose tree is complete in tree_ (guarded by mu_)
   std::atomic<bool> cancel_{false};
   std::mutex mu_;
-  std::condition_variable cv_;
+  std::condition_variable cv_, cvDone_;
   bool stop_ = false;
   std::thread th_;
+};
+
+// The process-wide helper pool: threads are created on demand up to the cap and kept for reuse.
+class TreeWorkerPool {
+ public:
+  static TreeWorkerPool& get() {
+    static TreeWorkerPool* p = new TreeWorkerPool();  // never destroyed: idle workers are parked on a condition variable
+    return *p;
+  }
+  std::unique_ptr<TreeWorker> lease() {
+    std::lock_guard<std::mutex> l(mu_);
+    if (!free_.empty()) {
+      auto w = std::move(free_.back());
+      free_.pop_back();
+      return w;
+    }
+    if (live_ >= cap_) return nullptr;
+    ++live_;
+    return std::make_unique<TreeWorker>();
+  }
+  void give(std::unique_ptr<TreeWorker> w) {
+    if (!w) return;
+    w->cancel();
+    std::lock_guard<std::mutex> l(mu_);
+    free_.push_back(std::move(w));
+  }
+
+ private:
+  TreeWorkerPool() {
+    const char* e = std::getenv("CCMI_TREE_WORKERS");
+    cap_ = e ? std::max(0, std::atoi(e)) : 4;
+  }
+  std::mutex mu_;
+  std::vector<std::unique_ptr<TreeWorker>> free_;
+  int live_ = 0, cap_ = 4;
+};
+struct TreeLease {  // one move-out call's worker (or none)
+  std::unique_ptr<TreeWorker> w;
+  ~TreeLease() { TreeWorkerPool::get().give(std::move(w)); }
 };
 
 class ResourceDistribution : public GoalImpl {
@@ -1068,7 +1119,6 @@ class ResourceDistribution : public GoalImpl {
   ccmi_provision_recommendation overRec{};  // _overProvisionedRecommendation
   Model::SnapTable snapTab;  // moveIn's candidate-broker snapshots (one Spec per phase)
   std::vector<uint8_t> queued;  // moveIn: broker is in the candidate queue
-  std::unique_ptr<TreeWorker> treeWorker;  // moveOut's entry-state trees
   int nameBase() const { return 4 * kind; }
   int nameId(bool reverse, bool leader) const { return nameBase() + (reverse ? 1 : 0) + (leader ? 2 : 0); }
   bool excluded(int b) const { return !allowed[b]; }
@@ -1314,11 +1364,10 @@ class ResourceDistribution : public GoalImpl {
     // builds on this thread instead, a few puts per poll of the in-flight scans (Device::idleWork). Read per call.
     const char* wEnv = std::getenv("CCMI_TREE_WORKER");
     const char* minEnv = std::getenv("CCMI_TREE_WORKER_MIN");
-    const bool useWorker = !(wEnv && wEnv[0] == '0') && m.B >= (minEnv ? std::atoi(minEnv) : 2048);
-    if (useWorker) {
-      if (!treeWorker) treeWorker = std::make_unique<TreeWorker>();
-      treeWorker->submit(inorder, m.B);  // `inorder` is the members' entry (key, id) order
-    }
+    TreeLease lease;
+    if (!(wEnv && wEnv[0] == '0') && m.B >= (minEnv ? std::atoi(minEnv) : 2048)) lease.w = TreeWorkerPool::get().lease();
+    const bool useWorker = lease.w != nullptr;
+    if (useWorker) lease.w->submit(inorder, m.B);  // `inorder` is the members' entry (key, id) order
     struct Step {
       int dst;
       double keyAfter;
@@ -1348,7 +1397,7 @@ class ResourceDistribution : public GoalImpl {
       auto t1 = t0;
       ovr = entryKey;
       if (useWorker) {
-        cand.adopt(treeWorker->take());
+        cand.adopt(lease.w->take());
       } else if (specState > 0) {  // the entry tree was started while scans were in flight: finish its puts
         if (tp) t1 = tnow();
         cand.buildStep((size_t)-1);

@@ -58,6 +58,13 @@ struct IntraArgs {
   const int32_t* rTie;     // [R] Replica.compareTo rank among online replicas
   const int32_t* rOrigDisk;  // [R] Replica._originalDisk (-1 = null)
   const uint8_t* rSel;     // [R] selectOnlineReplicas && selectReplicasBasedOnExcludedTopics
+  // entry-indexed copies of the replica fields the program reads per entry (filled by intra_sort / the emulation
+  // once per launch): a broker's entries are one contiguous range, so its snapshots and candidate checks read a few
+  // lines instead of one 128-B replica-table line per entry per pass
+  double* eDu;             // [entries] rDu[eRep[i]]
+  int32_t* eOrig;          // [entries] rOrigDisk[eRep[i]]
+  uint64_t* eKeyRev;       // [entries] intraSortKey(.., reverse) of selected entries, ~0 for the others
+  uint64_t* eKeyFwd;       // [entries] intraSortKey(.., forward), ~0 for the others
   int32_t* snapA;          // [entries] scratch (the broker's CSR range)
   int32_t* snapB;
   int32_t* ordRev;         // [entries] the broker's selected entries in reverse-score order (intraSortKeys)
@@ -165,7 +172,7 @@ class IntraBroker {
     }
     return cap > 0 ? util / cap : 1.0;
   }
-  CCMI_LD double du(int i) const { return A.rDu[A.eRep[i]]; }
+  CCMI_LD double du(int i) const { return A.eDu[i]; }
 
   // the disk's tracked sorted replicas (a clone), as entry indices into out[0..n): prioritizeDiskImmigrants puts the
   // replicas whose original disk is not d first, each group in the static order. On the device the broker's wavefront
@@ -184,7 +191,7 @@ class IntraBroker {
         int i = 0;
         if (k < nSel) {
           i = ord[k];
-          keep = A.eDisk[i] == d && ((A.rOrigDisk[A.eRep[i]] != d) == (pass == 0));
+          keep = A.eDisk[i] == d && ((A.eOrig[i] != d) == (pass == 0));
         }
         const uint64_t m = __ballot(keep);
         if (keep) out[n + __popcll(m & below)] = i;
@@ -200,7 +207,7 @@ class IntraBroker {
     for (int pass = 0; pass < 2; ++pass)
       for (int k = 0; k < nSel; ++k) {
         const int i = ord[k];
-        if (A.eDisk[i] == d && ((A.rOrigDisk[A.eRep[i]] != d) == (pass == 0))) out[n++] = i;
+        if (A.eDisk[i] == d && ((A.eOrig[i] != d) == (pass == 0))) out[n++] = i;
       }
     return n;
   }

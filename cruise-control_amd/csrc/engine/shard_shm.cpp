@@ -33,7 +33,8 @@ struct Slot {
   Line32 departed;
 };
 struct Block {
-  Line64 magic;  // written last by rank 0 (release): the block is initialised
+  Line64 magic;    // written last by rank 0 (release): the block is initialised
+  Line64 created;  // CLOCK_REALTIME ns when rank 0 initialised it (before the magic)
   Line32 count;
   Line32 attached;
   Slot slot[2];
@@ -42,6 +43,10 @@ static_assert(std::atomic<int64_t>::is_always_lock_free && std::atomic<uint32_t>
               "lock-free atomics in shared memory");
 
 double now() { return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count(); }
+int64_t wallNs() {
+  return (int64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
+             std::chrono::system_clock::now().time_since_epoch()).count();
+}
 inline void relax(uint64_t spins) {
   if (spins > (1u << 16)) sched_yield();  // past ~1 ms another rank is far behind: give the core away between polls
   else __builtin_ia32_pause();
@@ -53,6 +58,7 @@ struct ShmShard {
   int rank = 0, count = 1;
   uint64_t calls = 0;
   double timeout = 120.0;
+  bool broken = false;  // a combine timed out: its slot counters are inconsistent, every later call fails fast
 };
 
 ShmShard* shmCreate(const char* name, int rank, int count, double timeoutSeconds) {
@@ -60,37 +66,28 @@ ShmShard* shmCreate(const char* name, int rank, int count, double timeoutSeconds
   if (count < 1 || rank < 0 || rank >= count) throw std::invalid_argument("shard rank out of range");
   int fd = -1;
   const double t0 = now();
-  if (rank == 0) {
-    shm_unlink(name);  // a block left by an earlier run of the same job name
-    fd = shm_open(name, O_CREAT | O_EXCL | O_RDWR, 0600);
-    if (fd < 0) throw std::runtime_error(std::string("shm_open(create) failed: ") + std::strerror(errno));
-    if (ftruncate(fd, sizeof(Block)) != 0) {
-      close(fd);
-      throw std::runtime_error(std::string("ftruncate failed: ") + std::strerror(errno));
-    }
-  } else {
-    for (;;) {
-      fd = shm_open(name, O_RDWR, 0600);
-      if (fd >= 0) {
-        struct stat st;
-        if (fstat(fd, &st) == 0 && (size_t)st.st_size >= sizeof(Block)) break;
-        close(fd);
-        fd = -1;
-      }
-      if (now() - t0 > timeoutSeconds) throw std::runtime_error("shm combiner: rank 0's block never appeared");
-      usleep(1000);
-    }
-  }
-  void* p = mmap(nullptr, sizeof(Block), PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
-  close(fd);
-  if (p == MAP_FAILED) throw std::runtime_error(std::string("mmap failed: ") + std::strerror(errno));
+  const int64_t joinNs = wallNs();
   auto* s = new ShmShard();
-  s->blk = static_cast<Block*>(p);
   s->rank = rank;
   s->count = count;
   s->timeout = timeoutSeconds;
-  Block& b = *s->blk;
   if (rank == 0) {
+    shm_unlink(name);  // a block left by an earlier run of the same job name
+    fd = shm_open(name, O_CREAT | O_EXCL | O_RDWR, 0600);
+    if (fd < 0 || ftruncate(fd, sizeof(Block)) != 0) {
+      const std::string err = std::strerror(errno);
+      if (fd >= 0) close(fd);
+      delete s;
+      throw std::runtime_error("shm_open(create) / ftruncate failed: " + err);
+    }
+    void* p = mmap(nullptr, sizeof(Block), PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+    close(fd);
+    if (p == MAP_FAILED) {
+      delete s;
+      throw std::runtime_error(std::string("mmap failed: ") + std::strerror(errno));
+    }
+    s->blk = static_cast<Block*>(p);
+    Block& b = *s->blk;
     for (Slot& x : b.slot) {
       x.minKey.v.store(INT64_MAX, std::memory_order_relaxed);
       x.arrived.v.store(0, std::memory_order_relaxed);
@@ -98,20 +95,50 @@ ShmShard* shmCreate(const char* name, int rank, int count, double timeoutSeconds
     }
     b.count.v.store((uint32_t)count, std::memory_order_relaxed);
     b.attached.v.store(0, std::memory_order_relaxed);
+    b.created.v.store(wallNs(), std::memory_order_relaxed);
     b.magic.v.store((int64_t)kMagic, std::memory_order_release);
   } else {
-    for (uint64_t spins = 0; b.magic.v.load(std::memory_order_acquire) != (int64_t)kMagic; ++spins) {
+    // A block a crashed run left under the same name can be opened before rank 0 replaces it. Its creation stamp
+    // gives it away: rank 0 of a block waits at most `timeoutSeconds` for its ranks, so a block created longer than
+    // that before this rank arrived has no rank 0 left; it is dropped and the name polled again.
+    for (uint64_t spins = 0;; ++spins) {
       if (now() - t0 > timeoutSeconds) {
         shmDestroy(s);
-        throw std::runtime_error("shm combiner: the block was never initialised");
+        throw std::runtime_error("shm combiner: rank 0's block never appeared (or was never initialised)");
       }
-      relax(spins);
+      fd = shm_open(name, O_RDWR, 0600);
+      if (fd >= 0) {
+        struct stat st;
+        if (fstat(fd, &st) == 0 && (size_t)st.st_size >= sizeof(Block)) {
+          void* p = mmap(nullptr, sizeof(Block), PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+          close(fd);
+          fd = -1;
+          if (p == MAP_FAILED) {
+            shmDestroy(s);
+            throw std::runtime_error(std::string("mmap failed: ") + std::strerror(errno));
+          }
+          Block* b = static_cast<Block*>(p);
+          if (b->magic.v.load(std::memory_order_acquire) == (int64_t)kMagic) {
+            const int64_t created = b->created.v.load(std::memory_order_relaxed);
+            if (created + (int64_t)(timeoutSeconds * 1e9) >= joinNs) {
+              s->blk = b;
+              break;
+            }
+          }
+          munmap(p, sizeof(Block));  // not initialised yet, or stale: look again
+        } else {
+          close(fd);
+          fd = -1;
+        }
+      }
+      usleep(1000);
     }
-    if (b.count.v.load(std::memory_order_relaxed) != (uint32_t)count) {
+    if (s->blk->count.v.load(std::memory_order_relaxed) != (uint32_t)count) {
       shmDestroy(s);
       throw std::invalid_argument("shm combiner: ranks disagree on the shard count");
     }
   }
+  Block& b = *s->blk;
   b.attached.v.fetch_add(1, std::memory_order_acq_rel);
   for (uint64_t spins = 0; b.attached.v.load(std::memory_order_acquire) < (uint32_t)count; ++spins) {
     if (now() - t0 > timeoutSeconds) {
@@ -132,6 +159,7 @@ void shmDestroy(ShmShard* s) {
 
 int shmMin(void* ctx, int64_t* key) {
   auto* s = static_cast<ShmShard*>(ctx);
+  if (s->broken) return 1;
   Slot& x = s->blk->slot[s->calls & 1];
   ++s->calls;
   int64_t cur = x.minKey.v.load(std::memory_order_relaxed);
@@ -140,7 +168,10 @@ int shmMin(void* ctx, int64_t* key) {
   x.arrived.v.fetch_add(1, std::memory_order_acq_rel);
   const double t0 = now();
   for (uint64_t spins = 0; x.arrived.v.load(std::memory_order_acquire) < (uint32_t)s->count; ++spins) {
-    if ((spins & 4095) == 4095 && now() - t0 > s->timeout) return 1;
+    if ((spins & 4095) == 4095 && now() - t0 > s->timeout) {
+      s->broken = true;  // this slot's arrival count now disagrees with the other ranks': never combine again
+      return 1;
+    }
     relax(spins);
   }
   *key = x.minKey.v.load(std::memory_order_acquire);

@@ -21,40 +21,50 @@
 
 namespace ccmi {
 
-// One wavefront per broker: rank of every selected entry under both orders (ranks are a permutation: keys are
-// unique), the key tiles staged through LDS; ordRev / ordFwd[e0 + rank] = entry.
+// One wavefront per broker. Pass 1 gathers each entry's replica fields ONCE (one replica-table line per entry) into
+// the entry-indexed arrays the program reads (eDu, eOrig) and the two sort keys (eKeyRev / eKeyFwd, ~0 = not
+// selected); pass 2 ranks every selected entry under both orders (ranks are a permutation: keys are unique) over key
+// tiles staged from those contiguous arrays through LDS; ordRev / ordFwd[e0 + rank] = entry.
 constexpr int kSortTile = 512;
 __global__ __launch_bounds__(64) void intra_sort(IntraArgs A) {
   __shared__ uint64_t kRev[kSortTile], kFwd[kSortTile];
-  __shared__ uint8_t kSel[kSortTile];
   const int b = A.brokers[blockIdx.x];
   const int e0 = A.eOff[b], n = A.eOff[b + 1] - e0;
   const int lane = threadIdx.x;
   int selCount = 0;
+  for (int i = lane; i < n; i += 64) {
+    const int r = A.eRep[e0 + i];
+    const bool sel = A.rSel[r] != 0;
+    const float sc = A.rScore[r];
+    const int32_t tie = A.rTie[r];
+    A.eDu[e0 + i] = A.rDu[r];
+    A.eOrig[e0 + i] = A.rOrigDisk[r];
+    A.eKeyRev[e0 + i] = sel ? intraSortKey(sc, tie, true) : ~0ull;
+    A.eKeyFwd[e0 + i] = sel ? intraSortKey(sc, tie, false) : ~0ull;
+    selCount += __popcll(__ballot(sel));
+  }
+  __syncthreads();  // this wavefront's own stores (one wavefront per workgroup) before its loads below
   for (int ic = 0; ic < n; ic += 64) {
     const int i = ic + lane;
-    bool mine = false;
-    uint64_t rev = 0, fwd = 0;
+    uint64_t rev = ~0ull, fwd = ~0ull;
     if (i < n) {
-      const int r = A.eRep[e0 + i];
-      mine = A.rSel[r] != 0;
-      rev = intraSortKey(A.rScore[r], A.rTie[r], true);
-      fwd = intraSortKey(A.rScore[r], A.rTie[r], false);
+      rev = A.eKeyRev[e0 + i];
+      fwd = A.eKeyFwd[e0 + i];
     }
+    const bool mine = rev != ~0ull;
     int rankRev = 0, rankFwd = 0;
     for (int jt = 0; jt < n; jt += kSortTile) {
       const int m = n - jt < kSortTile ? n - jt : kSortTile;
-      __syncthreads();
-      for (int j = lane; j < m; j += 64) {
-        const int r = A.eRep[e0 + jt + j];
-        kSel[j] = A.rSel[r];
-        kRev[j] = intraSortKey(A.rScore[r], A.rTie[r], true);
-        kFwd[j] = intraSortKey(A.rScore[r], A.rTie[r], false);
+      if (ic == 0 || n > kSortTile) {  // a broker of at most kSortTile entries stages its keys once
+        __syncthreads();
+        for (int j = lane; j < m; j += 64) {
+          kRev[j] = A.eKeyRev[e0 + jt + j];
+          kFwd[j] = A.eKeyFwd[e0 + jt + j];
+        }
+        __syncthreads();
       }
-      __syncthreads();
       if (mine)
-        for (int j = 0; j < m; ++j) {
-          if (!kSel[j]) continue;
+        for (int j = 0; j < m; ++j) {  // unselected entries carry ~0: never below a selected key
           rankRev += kRev[j] < rev ? 1 : 0;
           rankFwd += kFwd[j] < fwd ? 1 : 0;
         }
@@ -63,7 +73,6 @@ __global__ __launch_bounds__(64) void intra_sort(IntraArgs A) {
       A.ordRev[e0 + rankRev] = e0 + i;
       A.ordFwd[e0 + rankFwd] = e0 + i;
     }
-    selCount += __popcll(__ballot(mine));
   }
   if (lane == 0) A.nSel[b] = selCount;
 }

@@ -975,6 +975,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, kServ
   int progVer = -1;
   int acqEpoch = -1;  // ServerCmd.rowsEpoch of this workgroup's last acquire (-1: none since the launch)
   unsigned long long idleSince = __builtin_amdgcn_s_memrealtime();
+  bool participated = false;  // this workgroup took part in its last command (thread 0's view)
   unsigned long long srvT[6] = {0, 0, 0, 0, 0, 0};
   for (;;) {
     if (threadIdx.x == 0) {
@@ -1023,9 +1024,21 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, kServ
             if ((mw >> 32) == (last & 0xffffffffull)) {
               published = true;
               idleSince = __builtin_amdgcn_s_memrealtime();
-            } else if (__builtin_amdgcn_s_memrealtime() - idleSince > kServerStuckTicks) {
-              ex = 3;  // a command never completed (a participant never arrived): leave instead of spinning forever
-              break;
+            } else if (participated) {
+              // a command this workgroup took part in never completed (a participant never arrived), 10 s after this
+              // workgroup took it: leave instead of spinning forever
+              if (__builtin_amdgcn_s_memrealtime() - idleSince > kServerStuckTicks) {
+                ex = 3;
+                break;
+              }
+            } else {
+              // not a participant: the command may run as long as it needs (a K7 chain on workgroup 0); this workgroup
+              // leaves only with workgroup 0's stuck exit record for that command
+              const unsigned long long xr = __hip_atomic_load(&mail[3], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+              if ((xr >> 32) == 3ull && (xr & 0xffffffffull) == (last & 0xffffffffull)) {
+                ex = 3;
+                break;
+              }
             }
           } else if (__builtin_amdgcn_s_memrealtime() - idleSince > kServerIdleTicks) {
             ex = 1;
@@ -1040,6 +1053,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, kServ
         else __builtin_amdgcn_s_sleep(16);
       }
       SRV_STAMP(T, 0);
+      participated = !ex && c.op != SOP_EXIT && (uint32_t)blockIdx.x < (uint32_t)c.nActive;
+      idleSince = __builtin_amdgcn_s_memrealtime();  // a stuck command is timed from when this workgroup took it
       // the rows workgroup 0 wrote for earlier commands (released before its arrivals) become visible with an agent
       // acquire; a command no earlier one wrote rows before needs none
       if (!ex && c.rowsEpoch != acqEpoch && (uint32_t)blockIdx.x < (uint32_t)c.nActive) {

@@ -16,6 +16,7 @@
 #include "intra.h"
 #include "predicates.h"
 #include "rackrows.h"
+#include "threadpin.h"
 #include "shard_rccl.h"
 
 namespace ccmi {
@@ -125,7 +126,7 @@ Emu& E(void* st) { return *static_cast<Emu*>(st); }
 }  // namespace
 
 int Device::countGfx950() { return 1; }  // one emulated device
-void Device::pinHostThread(int) {}
+bool deviceLocalCpuList(int, std::string&) { return false; }  // no PCI device
 
 Device::Device(int ordinal, int B, int R, int P, int T, int maxGoalSlots)
     : ordinal_(ordinal), B_(B), R_(R), P_(P), T_(T), ldB_((B + 3) & ~3), G_(maxGoalSlots) {
@@ -713,6 +714,14 @@ void Device::intraRun(const IntraRequest& q, IntraResult& out) {
   A.ordFwd = ordFwd.data();
   std::vector<int32_t> nSel(B_, 0);
   A.nSel = nSel.data();
+  std::vector<double> eDu(E_ + 1);  // intra_sort's entry-indexed gathers
+  std::vector<int32_t> eOrig(E_ + 1);
+  for (int k = 0; k < E_; ++k) {
+    eDu[k] = e.rDu[q.eRep[k]];
+    eOrig[k] = e.rOrigDisk[q.eRep[k]];
+  }
+  A.eDu = eDu.data();
+  A.eOrig = eOrig.data();
   for (int i = 0; i < q.nBrokers; ++i) {  // kernels/intra.hip intra_sort: selected entries by their unique keys
     const int b = q.brokers[i];
     for (int pass = 0; pass < 2; ++pass) {
