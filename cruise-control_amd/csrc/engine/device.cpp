@@ -151,8 +151,8 @@ Device::Device(int ordinal, int B, int R, int P, int T, int maxGoalSlots)
   ensureStage(1 << 20);
   ensureReq(1 << 20);
   if (std::getenv("CCMI_STAMPS")) {
-    dalloc(&stamps_, 1024 * 8 + 16);  // + the scan server's phase sums at [8192, 8208)
-    hipCheck(hipMemset(stamps_, 0, (1024 * 8 + 16) * sizeof(unsigned long long)), "hipMemset");
+    dalloc(&stamps_, 1024 * 8 + 32);  // + the scan server's phase sums at [8192, 8224)
+    hipCheck(hipMemset(stamps_, 0, (1024 * 8 + 32) * sizeof(unsigned long long)), "hipMemset");
   }
   hipCheck(hipEventCreate((hipEvent_t*)&ev0_), "hipEventCreate");
   hipCheck(hipEventCreate((hipEvent_t*)&ev1_), "hipEventCreate");
@@ -192,7 +192,7 @@ Device::~Device() {
   }
   if (ST) (void)hipStreamSynchronize(ST);
   if (stamps_) {  // average in-launch phase times of the last 1024 cross/pair scans (workgroup 0)
-    std::vector<unsigned long long> h(1024 * 8 + 16);
+    std::vector<unsigned long long> h(1024 * 8 + 32);
     if (hipMemcpy(h.data(), stamps_, h.size() * 8, hipMemcpyDeviceToHost) == hipSuccess) {
       if (h[8192])
         std::fprintf(stderr, "[ccmi server stamps] %llu scan commands: copy+acquire %.2f us, stage %.2f us, first tile "
@@ -203,6 +203,11 @@ Device::~Device() {
         std::fprintf(stderr, "[ccmi server stamps] %llu cross/segment commands: request + staging + view loads %.2f us "
                              "of the first tile\n",
                      h[8198], h[8197] * 0.01 / h[8198]);
+      if (h[8210])
+        std::fprintf(stderr, "[ccmi queue stamps] %llu queue commands: seen -> ready %.2f us, directory batch %.2f us, "
+                             "first tile %.2f us, rest to arrival %.2f us, %.2f tiles (workgroup 0)\n",
+                     h[8210], h[8211] * 0.01 / h[8210], h[8212] * 0.01 / h[8210], h[8213] * 0.01 / h[8210],
+                     h[8214] * 0.01 / h[8210], (double)h[8215] / h[8210]);
       if (h[8200])
         std::fprintf(stderr, "[ccmi chain stamps] %llu chain_pairs launches, %llu accepts: %.2f us per launch in "
                              "evaluation, %.2f us applying, %.2f us in total (thread 0)\n",
@@ -237,6 +242,7 @@ Device::~Device() {
     if (p) (void)hipFree(p);
   if (fg_) (void)hipFree(fg_);
   if (segPool_) (void)hipFree(segPool_);
+  if (qdir_) (void)hipFree(qdir_);
   if (dServerT0_) (void)hipFree(dServerT0_);
   if (hStage_) (void)hipHostFree(hStage_);
   if (hResult_) (void)hipHostFree(hResult_);
@@ -1122,6 +1128,7 @@ int64_t Device::segUpload(const SegIn& sg) {
     stopServer();
     segCache_.clear();
     segHead_ = 0;
+    ++poolEpoch_;  // every queue-directory entry now points at rows that will be overwritten
   }
   if (n) {
     for (int r : *sg.v)
@@ -1135,6 +1142,135 @@ int64_t Device::segUpload(const SegIn& sg) {
   segHead_ += span;
   segCache_.emplace(key, std::make_pair(sg.v, off));
   return off;
+}
+
+bool Device::queueUsable() const { return serverUsable_ && serverAllowed_; }
+
+void Device::qdirBind(uint64_t key) {
+  if (key == qdirKey_ && qdir_) return;
+  qdirKey_ = key;
+  qdirSpan_ = 1;
+  qdirSnap_.assign(B_, nullptr);
+  if (!qdir_) {
+    DeviceGuard dg(ordinal_);
+    hipCheck(hipExtMallocWithFlags((void**)&qdir_, sizeof(QueueDirEntry) * (size_t)B_, hipDeviceMallocFinegrained),
+             "hipExtMallocWithFlags queue directory");
+  }
+}
+
+bool Device::qdirSet(int b, std::shared_ptr<const std::vector<int32_t>> v) {
+  if (!qdir_ || b < 0 || b >= B_) throw std::logic_error("qdirSet before qdirBind");
+  if (v->size() >= (1u << 20)) return false;
+  const int64_t off = segUpload(SegIn{v, b, 0});
+  if (off < 0) return false;
+  // a plain 8-byte store through the BAR; the command that reads it is published behind a store fence
+  QueueDirEntry e{(uint32_t)off, (int32_t)v->size()};
+  *reinterpret_cast<volatile unsigned long long*>(&qdir_[b]) = *reinterpret_cast<const unsigned long long*>(&e);
+  qdirSpan_ = std::max(qdirSpan_, (int)v->size());
+  qdirSnap_[b] = std::move(v);
+  return true;
+}
+
+int64_t Device::scanQueue(const DevProgram& prog, int head, int skip0, const int32_t* tail, int nTail,
+                          const int32_t* cands, int N) {
+  DeviceGuard dg(ordinal_);
+  const int hasHead = head >= 0 ? 1 : 0;
+  const int n = hasHead + nTail;
+  if (n <= 0 || N <= 0) return -1;
+  auto entry = [&](int i) { return i < hasHead ? head : tail[i - hasHead]; };
+  const int span = qdirSpan_;
+  const uint64_t space = (uint64_t)n * (uint64_t)span * (uint64_t)N;
+  if (queueUsable() && space < (1ull << 31)) {
+    bool serve = false;
+    const bool readsTc = (prog.needs & (NEED_TOPIC | NEED_TLEAD)) != 0;
+    const Staged g = packForServer(prog, readsTc, serve);
+    if (serve) {
+      const size_t oRows = align16(sizeof(DevProgram));
+      const size_t oA = oRows + g.end, oC = oA + align16((size_t)n * 4), end = oC + align16((size_t)N * 4);
+      ensureFg(kCmdBytes + end);
+      if (ensureServer()) {
+        char* pay = fg_ + kCmdBytes;
+        const int ver = serverProgram(prog, pay);
+        if (g.end) std::memcpy(pay + oRows, hStage_, g.end);
+        if (hasHead) std::memcpy(pay + oA, &head, 4);
+        std::memcpy(pay + oA + 4 * (size_t)hasHead, tail, (size_t)nTail * 4);
+        std::memcpy(pay + oC, cands, (size_t)N * 4);
+        perf.serverPayloadBytes += (int64_t)(g.end + (size_t)n * 4 + (size_t)N * 4);
+        prof().addPayload((int64_t)(g.end + (size_t)n * 4 + (size_t)N * 4));
+        prof().count(12, "srv.bytes.A", (int64_t)n * 4);
+        ServerCmd c;
+        std::memset(&c, 0, sizeof(c));
+        c.op = SOP_QUEUE;
+        c.n = n;
+        c.K = span;
+        c.N = N;
+        c.c0 = skip0;
+        c.progVer = ver;
+        // one wave per candidate (a tile of kBlock slots): the queue is usually hundreds of brokers deep, so the scan
+        // is a few sweeps of every workgroup and the sweeps, not a single tile's conjunction, are its latency
+        c.goalParts = 1;
+        c.nActive = std::min(serverBlocks_, std::max(8, (n + 7) / 8 * 8));
+        c.nb = g.nb;
+        c.nr = g.nr;
+        c.np = g.np;
+        c.nt = g.nt;
+        c.oProg = 0;
+        c.oB = (uint32_t)(oRows + g.obr);
+        c.oR = (uint32_t)(oRows + g.orr);
+        c.oP = (uint32_t)(oRows + g.opr);
+        c.oT = (uint32_t)(oRows + g.otd);
+        c.oA = (uint32_t)oA;
+        c.oC = (uint32_t)oC;
+        c.queueDir = (unsigned long long)(uintptr_t)qdir_;
+        const auto tq = std::chrono::steady_clock::now();
+        if (postCommand(c, (g.nb | g.nr | g.np | g.nt) != 0)) {
+          perf.serverScans++;
+          const unsigned long long lo = hResult_[0] & 0xffffffffull;
+          const int64_t key = lo == 0 ? -1 : (int64_t)(lo - 1);
+          if (prof().on) {  // CCMI_PROFILE: queue commands' round trips and depths
+            prof().count(21, "queue.wait.ns",
+                         (int64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - tq)
+                             .count());
+            prof().count(22, "queue.scans", 1);
+            prof().count(23, "queue.entries.before.winner", key < 0 ? n : key / N / span);
+          }
+          // required candidates: every row before the winner's, then the winner's columns up to it (device-side
+          // accounting only: the scan's evaluated pair space is not walked here)
+          int64_t required = 0, K = 0;
+          const int wi = key < 0 ? n : (int)(key / N / span);
+          for (int i = 0; i < wi; ++i) {
+            const int len = qdirLen(entry(i)), s0 = i == 0 ? skip0 : 0;
+            required += len > s0 ? (int64_t)(len - s0) * N : 0;
+          }
+          if (key >= 0) required += ((key / N) % span - (wi == 0 ? skip0 : 0)) * N + key % N + 1;
+          K = required;  // pairs the device had to evaluate (speculative tiles past the winner not counted)
+          perf.scanPairs += K;
+          perf.scanBytes += K * kBytesPerCandidate;
+          perf.scanRequired += required;
+          perf.serverRequired += required;
+          perf.crossRequired += required;
+          return key;
+        }
+      }
+    }
+    unpackUpdates(g);
+  }
+  // no server (or too many keys): the rows flattened for a plain cross scan, its key mapped back
+  segFlat_.clear();
+  std::vector<int32_t> entryOf, rowOf;
+  for (int i = 0; i < n; ++i) {
+    const auto& v = *qdirSnap_[entry(i)];
+    for (size_t r = i == 0 ? (size_t)skip0 : 0; r < v.size(); ++r) {
+      segFlat_.push_back(v[r]);
+      entryOf.push_back(i);
+      rowOf.push_back((int32_t)r);
+    }
+  }
+  if (segFlat_.empty()) return -1;
+  const int64_t k = scanCross(prog, segFlat_.data(), (int)segFlat_.size(), cands, N, 0, N);
+  if (k < 0) return -1;
+  const int64_t fr = k / N;
+  return ((int64_t)entryOf[fr] * span + rowOf[fr]) * N + k % N;
 }
 
 int64_t Device::scanSegs(const DevProgram& prog, const std::vector<SegIn>& segs, const int32_t* cands, int N, int c0,

@@ -161,6 +161,27 @@ class Device {
   int64_t scanSegs(const DevProgram& prog, const std::vector<SegIn>& segs, const int32_t* cands, int N, int c0,
                    int c1);
   bool segsUsable() const { return serverUsable_ && serverAllowed_; }
+
+  // Queue scans (SOP_QUEUE, devtypes.h): the rows of a whole broker queue in one command. Each broker's rows are its
+  // snapshot under ONE Spec, uploaded once per broker version into the snapshot pool and found through the snapshot
+  // directory (QueueDirEntry[B] in fine-grained VRAM, written by the host only when a broker's snapshot changes). The
+  // engine keeps the directory current (qdirSet after every version bump it has not yet seen); the device only reads.
+  bool queueUsable() const;
+  // entries belong to `key` (the engine's Spec + selection identity); another key drops every entry
+  void qdirBind(uint64_t key);
+  uint64_t qdirKey() const { return qdirKey_; }
+  // bumped when the pool wraps: every directory entry then refers to overwritten rows and must be set again
+  uint32_t poolEpoch() const { return poolEpoch_; }
+  // upload broker b's snapshot and point its directory entry at it (false: larger than the pool)
+  bool qdirSet(int b, std::shared_ptr<const std::vector<int32_t>> v);
+  const std::vector<int32_t>& qdirRows(int b) const { return *qdirSnap_[b]; }
+  int qdirLen(int b) const { return qdirSnap_[b] ? (int)qdirSnap_[b]->size() : 0; }
+  // first accepted (row, column) over the queue entries [head (if >= 0)] ++ tail[0, nTail) (entry 0 from row skip0) x
+  // cands[0, N); key = (i * span + row) * N + column with span = queueSpan(); -1 when none. Every entry must be set for
+  // the bound key.
+  int64_t scanQueue(const DevProgram& prog, int head, int skip0, const int32_t* tail, int nTail, const int32_t* cands,
+                    int N);
+  int queueSpan() const { return qdirSpan_; }
   // the session's scans may (not) use the resident scan server (sessions whose scans wait on other ranks may not)
   void setServerAllowed(bool on) {
     if (!on) stopServer();
@@ -305,6 +326,11 @@ class Device {
   std::vector<int32_t> segFlat_;
   std::vector<SegEntry> segTab_;
   int64_t segUpload(const SegIn& s);  // pool index of the snapshot's first entry, or -1 (does not fit)
+  uint32_t poolEpoch_ = 0;
+  uint64_t qdirKey_ = 0;
+  int qdirSpan_ = 1;  // >= every set entry's length since the last bind
+  QueueDirEntry* qdir_ = nullptr;  // fine-grained VRAM [B] (host-written through the BAR)
+  std::vector<std::shared_ptr<const std::vector<int32_t>>> qdirSnap_;  // [B] the snapshot each entry points at
   void ensureFg(size_t bytes);
   int32_t* rowVisited_ = nullptr;
   size_t rowVisitedCap_ = 0;

@@ -239,7 +239,16 @@ struct ScanHeader {
 // command's rows, load rows (oL, nl) and slot rows (oS, ns) are applied first, the request is copied into chainReq,
 // the decisions are logged to chainLog / chainOut (host-mapped), and the writes are released at system scope before
 // the publish — no stop and relaunch of the server around a chain.
-enum ServerOp : int32_t { SOP_CROSS = 0, SOP_PAIRS = 1, SOP_EXIT = 2, SOP_SEGS = 3, SOP_CHAIN = 4 };
+enum ServerOp : int32_t { SOP_CROSS = 0, SOP_PAIRS = 1, SOP_EXIT = 2, SOP_SEGS = 3, SOP_CHAIN = 4, SOP_QUEUE = 5 };
+// SOP_QUEUE: a cross scan whose rows are the snapshots of a queue of brokers (ResourceDistributionGoal's move-in
+// candidate queue, polled in order): queue entry i (broker id at oA) contributes rows [skip, len) of its snapshot in the
+// device-resident snapshot pool, where {pool offset, len} is the broker's entry in the snapshot directory (fine-grained
+// VRAM the host keeps current, ServerCmd.queueDir); skip = c0 for entry 0, 0 for the others. Columns are the N
+// candidates at oC. Key = (i * span + row) * N + column (span = K >= every entry's len), so keys follow the poll order.
+struct QueueDirEntry {
+  uint32_t off;  // pool index of the broker's first snapshot row
+  int32_t len;   // its snapshot length
+};
 // SOP_SEGS: a cross scan whose rows are the concatenation of nSegs segments of the device-resident snapshot pool
 // (Device::scanSegs); the segment table at oA holds {first pool entry, first row} per segment plus {0, K} at the end.
 constexpr int kMaxSegs = 1024;
@@ -271,6 +280,7 @@ struct alignas(16) ServerCmd {
   unsigned long long chainReq;  // device addresses: HBM scratch for the request, host-mapped log and result
   unsigned long long chainLog;
   unsigned long long chainOut;
+  unsigned long long queueDir;  // SOP_QUEUE: the snapshot directory (QueueDirEntry[B], fine-grained VRAM)
 };
 // The sequence word is a seqlock: the host stores (next | kSeqBusy) before it rewrites the other fields and `next`
 // after; a workgroup accepts a header only when the word it read before and after its copy is the same, not busy.

@@ -300,6 +300,102 @@ int64_t Engine::crossScanSegs(GoalImpl& self, int action, const std::vector<Snap
   return key;
 }
 
+bool Engine::queueOn(const GoalImpl& self, int action) const {
+  static const bool off = std::getenv("CCMI_QUEUE_SCAN") && std::getenv("CCMI_QUEUE_SCAN")[0] == '0';
+  if (off || shard.count > 1 || !dev->queueUsable()) return false;
+  const DevProgram prog = program(self, action);
+  return !prog.exclLeadMove && !prog.newOnly;
+}
+
+namespace {
+uint64_t specKey(const Model::Spec& s, uint32_t selEpoch) {  // identity of the directory's contents
+  uint64_t h = 1469598103934665603ull;
+  auto mix = [&h](uint64_t v) { h = (h ^ v) * 1099511628211ull; };
+  mix(s.selLeaders);
+  mix(s.selFollowers);
+  mix(s.selImmigrants);
+  mix(s.selImmOrOffline);
+  mix(s.selOffline);
+  mix(s.selExclTopics);
+  mix(s.selExclMust);
+  mix(s.selMustTopics);
+  mix((uint64_t)(int64_t)s.selAboveRes);
+  mix((uint64_t)(int64_t)s.selBelowRes);
+  uint64_t u;
+  std::memcpy(&u, &s.aboveLimit, 8);
+  mix(u);
+  std::memcpy(&u, &s.belowLimit, 8);
+  mix(u);
+  mix(s.prioOffline);
+  mix(s.prioImmigrants);
+  mix((uint64_t)(int64_t)s.scoreRes);
+  mix(s.scoreReverse);
+  mix(selEpoch);
+  return h | 1ull;  // never 0 (an unbound directory)
+}
+}  // namespace
+
+// Every broker's directory entry current for `spec`: all of them when the directory was filled for another Spec (or
+// the pool wrapped under it), otherwise only the brokers relocations touched since the last sync (Model::verLog).
+void Engine::queueSync(const Model::Spec& spec) {
+  PhaseScope ps(PH_FLATTEN);
+  const uint64_t key = specKey(spec, m.selEpoch);
+  QueueSync& q = qsync_;
+  if (q.stamp.size() != (size_t)m.B) q.stamp.assign(m.B, 0);
+  bool full = !q.bound || q.key != key || dev->qdirKey() != key || q.epoch != dev->poolEpoch();
+  auto set = [&](int b) {
+    if (!dev->qdirSet(b, m.snapshot(b, spec))) throw Unsupported("a broker's snapshot exceeds the snapshot pool");
+  };
+  for (int attempt = 0; attempt < 3; ++attempt) {
+    if (full) {
+      dev->qdirBind(key);
+      q.bound = true;
+      q.key = key;
+      q.epoch = dev->poolEpoch();
+      q.logPos = m.verLog.size();
+      for (int b = 0; b < m.B; ++b) set(b);
+      prof().count(20, "queue.dir.full", 1);
+    } else {
+      ++q.round;
+      const size_t end = m.verLog.size();
+      for (size_t k = q.logPos; k < end; ++k) {
+        const int b = m.verLog[k];
+        if (q.stamp[b] == q.round) continue;
+        q.stamp[b] = q.round;
+        set(b);
+      }
+      q.logPos = end;
+    }
+    if (q.epoch == dev->poolEpoch()) return;  // no pool wrap while setting: every entry points at live rows
+    full = true;
+  }
+  throw std::logic_error("queue directory: the snapshot pool keeps wrapping");
+}
+
+int64_t Engine::queueScan(GoalImpl& self, int action, const Model::Spec& spec, int head, int skip0,
+                          const int32_t* tail, int nTail, const std::vector<int32_t>& cands) {
+  const int hasHead = head >= 0 ? 1 : 0;
+  const int n = hasHead + nTail, N = (int)cands.size();
+  if (n == 0 || N == 0) return -1;
+  PhaseScope ps(PH_DEV_SCAN);
+  queueSync(spec);
+  m.flushToDevice();
+  const DevProgram prog = program(self, action);
+  const int64_t key = dev->scanQueue(prog, head, skip0, tail, nTail, cands.data(), N);
+  checkTerminal(key);
+  // reference-equivalent candidates: every row of the entries before the winner's, then its rows up to the winner
+  const int span = dev->queueSpan();
+  const int wi = key < 0 ? n : (int)(key / N / span);
+  int64_t rows = 0;
+  for (int i = 0; i < wi; ++i) {
+    const int len = dev->qdirLen(i < hasHead ? head : tail[i - hasHead]), s0 = i == 0 ? skip0 : 0;
+    rows += len > s0 ? len - s0 : 0;
+  }
+  if (key < 0) candidates += rows * N;
+  else candidates += (rows + (key / N) % span - (wi == 0 ? skip0 : 0)) * N + key % N + 1;
+  return key;
+}
+
 // CCMI_FORCE_COMBINE=1 sends single-shard keys through the combiner too (diagnostics: exercises the RCCL path of a
 // one-rank communicator on a one-GPU box)
 static bool forceCombine() {
@@ -715,6 +811,11 @@ class LiveQueue {
   }
   // a likely future poll (-1: none known)
   int upcoming(size_t k) const { return ordered_ ? oq_.upcoming(k) : -1; }
+  // ordered form with nothing re-added: the remaining poll order is a contiguous run (OrderedQueue::runData)
+  bool runOnly() const { return ordered_ && oq_.heapEmpty(); }
+  const int* runData() const { return oq_.runData(); }
+  size_t runLeft() const { return oq_.runLeft(); }
+  void skipRun(size_t k) { oq_.skipRun(k); }
   // speculatively polled entries whose keys did not change, in reverse poll order
   void unpoll(int x) {
     if (ordered_) oq_.unpoll(x);
@@ -1695,6 +1796,7 @@ class ResourceDistribution : public GoalImpl {
     // candidate list, nothing moves and nothing is counted — the loop's outcome without walking every broker
     if (cands.empty()) return true;
     if (action == DA_LEADERSHIP && pq.ordered() && e.shard.count <= 1) return moveInLeadership(e, b, pq, spec);
+    if (action == DA_MOVE && pq.ordered() && e.queueOn(*this, action)) return moveInQueue(e, b, pq, spec, cands);
     // rows: the current broker's remaining view, then the polled brokers' snapshots (device-resident segments)
     using Seg = SnapSeg;
     auto segLen = [](const Seg& x) { return x.v->size() > x.skip ? x.v->size() - x.skip : 0; };
@@ -1761,6 +1863,59 @@ class ResourceDistribution : public GoalImpl {
         prof().count(action == DA_MOVE ? 2 : 5, action == DA_MOVE ? "in.move.continue" : "in.lead.continue");
         cur = {nullptr, hit.cb, idx};
         haveCur = true;
+      }
+    }
+    return true;
+  }
+
+  // rebalanceByMovingLoadIn for INTER_BROKER_REPLICA_MOVEMENT (:437-526) with an ordered candidate queue, one device
+  // command per accepted move: the reference polls candidate brokers in (utilization %, id) descending order and walks
+  // each one's live sorted-replica view (restarting it after an accept, :484-522) until a replica is accepted into b.
+  // The rows of EVERY queued broker go to the device in one queue scan (Engine::queueScan), in poll order, so the
+  // scan's first fit is the reference's next accept however deep in the queue it lies; brokers before the winner's
+  // are consumed (polled, as the reference polled them), the ones after it are un-polled.
+  template <class Q>
+  bool moveInQueue(Engine& e, int b, Q& pq, const Model::Spec& spec, const std::vector<int32_t>& cands) {
+    Model& m = e.m;
+    std::vector<int32_t> merged;
+    int curCb = -1, curSkip = 0;
+    const int N = (int)cands.size();
+    while (curCb >= 0 || !pq.empty()) {
+      // the queue's poll order: its remaining sorted run as it is, or (after a re-add) every element polled in order
+      const bool run = pq.runOnly();
+      if (!run) {
+        PhaseScope pf(PH_FLATTEN);
+        merged.clear();
+        while (!pq.empty()) merged.push_back(pq.poll());
+      }
+      const int32_t* tail = run ? pq.runData() : merged.data();
+      const int nTail = (int)(run ? pq.runLeft() : merged.size());
+      const int head = curCb, hasHead = head >= 0 ? 1 : 0;
+      const int64_t key = e.queueScan(*this, DA_MOVE, spec, head, hasHead ? curSkip : 0, tail, nTail, cands);
+      if (key < 0) return true;  // every queued broker polled, nothing accepted
+      const int span = e.dev->queueSpan();
+      const int64_t row = key / N;
+      const int i = (int)(row / span), idx = (int)(row % span);
+      const int cb = i < hasHead ? head : tail[i - hasHead];
+      const int r = e.dev->qdirRows(cb)[idx];  // cb's live view == the snapshot the scan read
+      // the brokers up to the winner's are polled (the reference polled them); the ones after it stay queued
+      const int polled = i < hasHead ? 0 : i - hasHead + 1;
+      if (run) pq.skipRun((size_t)polled);
+      else
+        for (int t = nTail; t-- > polled;) pq.unpoll(merged[t]);
+      m.relocateReplica(m.rPart[r], cb, b);
+      if (aboveLower(m, b)) {
+        prof().count(0, "in.move.done");
+        return false;
+      }
+      if (!pq.empty() && m.pct(cb, res) < m.pct(pq.peek(), res)) {
+        prof().count(1, "in.move.readd");
+        pq.add(cb);
+        curCb = -1;
+      } else {
+        prof().count(2, "in.move.continue");
+        curCb = cb;
+        curSkip = idx;  // the reference's iteration resumes at the same index of the view without r
       }
     }
     return true;

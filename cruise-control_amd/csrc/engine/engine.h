@@ -139,6 +139,14 @@ class Engine {
   // crossScan over the concatenation of snapshot segments (Device::scanSegs: the rows stay device-resident)
   int64_t crossScanSegs(GoalImpl& self, int action, const std::vector<SnapSeg>& segs,
                         const std::vector<int32_t>& cands);
+  // Queue scans (Device::scanQueue): the rows of every broker of [head (if >= 0)] ++ tail[0, nTail) (poll order; entry 0
+  // from row skip0) x cands in
+  // ONE device command, each broker's rows its snapshot under `spec` from the device-resident snapshot directory.
+  // Returns the key (Device::scanQueue) or -1 and adds the reference-equivalent candidates. queueOn: the path applies
+  // (one shard, a usable server, no replica-dependent candidate filters; CCMI_QUEUE_SCAN=0 turns it off).
+  bool queueOn(const GoalImpl& self, int action) const;
+  int64_t queueScan(GoalImpl& self, int action, const Model::Spec& spec, int head, int skip0, const int32_t* tail,
+                    int nTail, const std::vector<int32_t>& cands);
   int64_t exclLeadCount(const DevProgram& prog, const int32_t* reps, int K, const std::vector<int32_t>& cands,
                         int64_t key) const;
   bool blocked(const DevProgram& prog, int r, int b) const;
@@ -179,6 +187,18 @@ class Engine {
                       std::vector<int32_t>& res);
 
  private:
+  // the snapshot directory's catch-up state: the Spec + selection it was filled for, the pool epoch it refers to and
+  // the position in Model::verLog up to which every changed broker's entry was set again
+  struct QueueSync {
+    bool bound = false;
+    uint64_t key = 0;
+    uint32_t epoch = 0;
+    size_t logPos = 0;
+    std::vector<uint32_t> stamp;  // [B] the round a broker was last set in (dedupes the log)
+    uint32_t round = 0;
+  };
+  QueueSync qsync_;
+  void queueSync(const Model::Spec& spec);
   DevProgram program(const GoalImpl& self, int action) const;
   int64_t combine(int64_t localKey) const;
   void refreshAllowed(GoalImpl& g);

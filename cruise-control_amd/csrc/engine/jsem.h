@@ -633,6 +633,12 @@ class OrderedQueue {
   // The k-th element of the sorted run after the poll position (-1 past its end): a likely future poll (elements
   // re-added through the heap are not included)
   int upcoming(size_t k) const { return pos_ + k < s_.size() ? s_[pos_ + k] : -1; }
+  // The sorted run's elements not yet polled (in poll order while the heap is empty), and skipping k of them: the
+  // same as k polls when the heap is empty
+  bool heapEmpty() const { return heap_.empty(); }
+  const int* runData() const { return s_.data() + pos_; }
+  size_t runLeft() const { return pos_ < s_.size() ? s_.size() - pos_ : 0; }
+  void skipRun(size_t k) { pos_ += k; }
   // Put back the most recently polled element (un-polls come in reverse poll order). An element that came from
   // the sorted run and whose key did not change since returns to its slot in the run (O(1)); anything else goes
   // through the heap. Either way the queue holds the same set, so the poll order is unchanged.

@@ -566,6 +566,8 @@ void Model::relocateReplica(int p, int src, int dst) {
   PhaseScope ps(PH_RELOCATE);
   bVer[src]++;
   bVer[dst]++;
+  verLog.push_back(src);
+  verLog.push_back(dst);
   const int r = brokerRemove(src, p);
   if (r < 0) throw std::runtime_error("Replica is not in the cluster.");
   noteDelta(src, r);
@@ -658,6 +660,8 @@ bool Model::relocateLeadership(int p, int src, int dst) {
                                 std::to_string(bId[dst]) + " because the destination replica is a leader.");
   bVer[src]++;
   bVer[dst]++;
+  verLog.push_back(src);
+  verLog.push_back(dst);
   noteDelta(src, sr);
   noteDelta(dst, dr);
   // Broker.makeFollower(src)
@@ -882,6 +886,7 @@ static void cachePut(std::vector<Model::SortedCacheEntry>& cache, uint32_t ver, 
 void Model::setMustTopicSelection(const std::vector<uint8_t>& t) {
   if (t == mustTopicSel) return;
   mustTopicSel = t;
+  ++selEpoch;
   for (auto& c : sortedCache) c.clear();
   for (auto& c : filteredCache) c.clear();
 }
@@ -889,6 +894,7 @@ void Model::setMustTopicSelection(const std::vector<uint8_t>& t) {
 void Model::setExcludedTopicSelection(const std::vector<uint8_t>& t) {
   if (t == exclTopicSel) return;
   exclTopicSel = t;
+  ++selEpoch;
   for (auto& c : sortedCache) c.clear();
   for (auto& c : filteredCache) c.clear();
 }

@@ -319,6 +319,11 @@ class Model {
     std::shared_ptr<const std::vector<int32_t>> v;
   };
   std::vector<uint32_t> bVer;
+  // Every version bump in order (src and dst of each relocation): readers that keep per-broker state derived from
+  // snapshots (the queue scans' snapshot directory) catch up from their position instead of re-checking every broker.
+  std::vector<int32_t> verLog;
+  // bumped whenever the selection sets the Specs do not carry change (excluded / must topics)
+  uint32_t selEpoch = 0;
   // The replica whose membership or sort key changed at each of a broker's last kDeltaLog version bumps (-1: none),
   // so a snapshot can be derived from the previous version's instead of re-sorting the broker.
   static constexpr size_t kDeltaLog = 8;

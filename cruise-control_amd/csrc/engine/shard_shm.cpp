@@ -101,7 +101,7 @@ ShmShard* shmCreate(const char* name, int rank, int count, double timeoutSeconds
     // A block a crashed run left under the same name can be opened before rank 0 replaces it. Its creation stamp
     // gives it away: rank 0 of a block waits at most `timeoutSeconds` for its ranks, so a block created longer than
     // that before this rank arrived has no rank 0 left; it is dropped and the name polled again.
-    for (uint64_t spins = 0;; ++spins) {
+    for (;;) {
       if (now() - t0 > timeoutSeconds) {
         shmDestroy(s);
         throw std::runtime_error("shm combiner: rank 0's block never appeared (or was never initialised)");

@@ -977,6 +977,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, kServ
   unsigned long long idleSince = __builtin_amdgcn_s_memrealtime();
   bool participated = false;  // this workgroup took part in its last command (thread 0's view)
   unsigned long long srvT[6] = {0, 0, 0, 0, 0, 0};
+  unsigned long long qBatch = 0, qTiles = 0;  // CCMI_STAMPS, SOP_QUEUE: workgroup 0's batch-loaded stamp and tiles
   for (;;) {
     if (threadIdx.x == 0) {
       int ex = 0;
@@ -1206,6 +1207,134 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, kServ
           break;
         }
       }
+    } else if (c.op == SOP_QUEUE) {
+      // Brokers in queue order over the workgroups (entry i on workgroup i % nAct). A workgroup loads the directory
+      // entries of all its brokers up front (two fine-grained round trips for the command, not per broker) and walks
+      // their rows as ONE range — its brokers' (row, column) pairs back to back, a prefix sum in LDS — in tiles of
+      // kBlock / parts slots, so a tile spans several short snapshots. Keys grow with (entry, row, column) along that
+      // range, so the early exits keep the first fit exact.
+      const int n = c.n, N = c.N, span = c.K, skip0 = c.c0;
+      const int parts = (c.goalParts == 2 || c.goalParts == 4) ? c.goalParts : 1;
+      const uint32_t tile = (uint32_t)(kBlock / parts);
+      const int wave = (int)(threadIdx.x >> 6);
+      const int part = wave % parts;
+      const uint32_t slot = (uint32_t)(wave / parts) * 64u + (threadIdx.x & 63u);
+      const int32_t* Q = (const int32_t*)(pay + c.oA);
+      const QueueDirEntry* dir = reinterpret_cast<const QueueDirEntry*>(c.queueDir);
+      __shared__ uint32_t sOff[kBlock];        // pool offset of each batch entry's first scanned row
+      __shared__ uint32_t sPre[kBlock + 1];    // pair prefix over the batch's entries
+      __shared__ int32_t sCand[kBlock];
+      const bool candsLds = N <= kBlock;
+      if (candsLds && (int)threadIdx.x < N) sCand[threadIdx.x] = ldSys(C + threadIdx.x);
+      const int wgI = (int)blockIdx.x;
+      const int mine = wgI < n ? (n - wgI + (int)nAct - 1) / (int)nAct : 0;  // entries wgI, wgI + nAct, ...
+      bool found = false;
+      for (int kb = 0; kb < mine && !found; kb += kBlock) {
+        const int nb = mine - kb < kBlock ? mine - kb : kBlock;
+        uint32_t cnt = 0;
+        if ((int)threadIdx.x < nb) {
+          const int i = wgI + (kb + (int)threadIdx.x) * (int)nAct;
+          const int b = ldSys(Q + i);
+          const unsigned long long e = __hip_atomic_load(reinterpret_cast<const unsigned long long*>(dir + b),
+                                                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          const int len = (int)(uint32_t)(e >> 32), r0 = i == 0 ? skip0 : 0;
+          cnt = len > r0 ? (uint32_t)(len - r0) * (uint32_t)N : 0u;
+          sOff[threadIdx.x] = (uint32_t)(e & 0xffffffffull) + (uint32_t)r0;
+        }
+        // exclusive prefix of cnt over the block (wave scans, then the wave totals)
+        {
+          __shared__ uint32_t sWave[kBlock / 64];
+          uint32_t x = cnt;
+          const int lane = (int)(threadIdx.x & 63u);
+#pragma unroll
+          for (int d = 1; d < 64; d <<= 1) {
+            const uint32_t y = __shfl_up(x, (unsigned)d, 64);
+            if (lane >= d) x += y;
+          }
+          if (lane == 63) sWave[threadIdx.x >> 6] = x;
+          __syncthreads();
+          uint32_t add = 0;
+          for (int w = 0; w < (int)(threadIdx.x >> 6); ++w) add += sWave[w];
+          sPre[threadIdx.x + 1] = x + add;
+          if (threadIdx.x == 0) sPre[0] = 0;
+          __syncthreads();
+        }
+        const uint32_t total = sPre[nb];
+        if (T.stamps && blockIdx.x == 0 && threadIdx.x == 0 && kb == 0) qBatch = __builtin_amdgcn_s_memrealtime();
+        // this slot's pair of the NEXT tile, loaded while the current one is evaluated (software pipelining of the
+        // fine-grained pool reads: a tile's critical path is then its record loads and the conjunction)
+        RowRef nextRq{0, 0, 0, 0};
+        int nextK = 0;
+        bool haveNext = false;
+        auto rowAt = [&](uint32_t v, int& k) {  // the pool row of pair v (k: its entry, advanced from the caller's)
+          while (k + 1 < nb && sPre[k + 1] <= v) ++k;
+          return pool[sOff[k] + (v - sPre[k]) / (uint32_t)N];  // written before any command read it (a ring)
+        };
+        for (uint32_t base = 0; base < total; base += tile) {
+          // the tile's first pair: its key bounds every key of the tile from below
+          int kf = 0;
+          {
+            int lo = 0, hi = nb - 1;  // last entry whose range starts at or before `base`
+            while (lo < hi) {
+              const int mid = (lo + hi + 1) >> 1;
+              if (sPre[mid] <= base) lo = mid;
+              else hi = mid - 1;
+            }
+            kf = lo;
+          }
+          auto keyOf = [&](int k, uint32_t v) {  // key of pair v of the range, inside batch entry k
+            const int i = wgI + (kb + k) * (int)nAct;
+            const uint32_t w = v - sPre[k];
+            const uint32_t row = (uint32_t)(i == 0 ? skip0 : 0) + w / (uint32_t)N;
+            return ((unsigned long long)i * (unsigned long long)span + row) * (unsigned long long)N + w % (uint32_t)N;
+          };
+          if (!firstTile && blockBest(result) <= keyOf(kf, base)) {
+            found = true;  // a smaller key exists: nothing later in this workgroup's range can win
+            break;
+          }
+          const uint32_t v = base + slot;
+          RowRef rq{0, 0, 0, 0};
+          int dq = 0;
+          int k = kf;
+          if (v < total) {
+            if (haveNext) {
+              rq = nextRq;
+              k = nextK;
+            } else {
+              rq = rowAt(v, k);
+            }
+            const uint32_t w = v - sPre[k];
+            dq = candsLds ? sCand[w % (uint32_t)N] : ldSys(C + w % (uint32_t)N);
+          }
+          haveNext = false;
+          if (v + tile < total) {  // the next tile's row of this slot (a tile spans a few entries)
+            nextK = k;
+            nextRq = rowAt(v + tile, nextK);
+            haveNext = true;
+          }
+          if (!staged) stage();
+          bool ok = false;
+          if (v < total) {
+            PreView pv;
+            pv.loadDst(T, dq, ov);
+            pv.loadRowRef(T, prog, rq, ov);
+            if (firstTile) SRV_STAMP(T, 5);
+            ok = !pv.exclLeadBlocked(prog) && moveCandidateAcceptedPart(prog, pv, pv.r, pv.dst, part, parts);
+          }
+          const int f = tileFirst(ok, parts);
+          if (firstTile) {
+            SRV_STAMP(T, 3);
+            firstTile = false;
+          }
+          ++qTiles;
+          if (f >= 0) {
+            if (threadIdx.x == (unsigned)(f % 64) + (unsigned)((f / 64) * parts * 64)) atomicMin(result, keyOf(k, v));
+            found = true;
+            break;
+          }
+        }
+        __syncthreads();  // the batch arrays are rewritten by the next batch
+      }
     } else {  // SOP_PAIRS
       const int n = c.n, keyBase = c.keyBase;
       const int parts = (c.goalParts == 2 || c.goalParts == 4) ? c.goalParts : 1;
@@ -1260,6 +1389,18 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, kServ
     if (threadIdx.x == 0) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       const unsigned int prev = __hip_atomic_fetch_add(done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (T.stamps && blockIdx.x == 0 && c.op == SOP_QUEUE) {  // queue commands: [8210..8215]
+        const unsigned long long tA = __builtin_amdgcn_s_memrealtime();
+        const unsigned long long tb = qBatch ? qBatch : srvT[2];
+        atomicAdd(&T.stamps[8210], 1ull);
+        atomicAdd(&T.stamps[8211], srvT[2] - srvT[0]);
+        atomicAdd(&T.stamps[8212], tb - srvT[2]);
+        atomicAdd(&T.stamps[8213], srvT[3] > tb ? srvT[3] - tb : 0ull);
+        atomicAdd(&T.stamps[8214], tA - (srvT[3] > tb ? srvT[3] : tb));
+        atomicAdd(&T.stamps[8215], qTiles);
+        qBatch = 0;
+        qTiles = 0;
+      }
       if (T.stamps && blockIdx.x == 0 && c.op != SOP_CHAIN) {  // scan commands (chains have their own stamps)
         srvT[4] = __builtin_amdgcn_s_memrealtime();
         atomicAdd(&T.stamps[8192 + 0], 1ull);

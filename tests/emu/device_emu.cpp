@@ -804,6 +804,42 @@ void Device::statsDisks(double balance, DiskStatsOut* out) {
 namespace ccmi {
 void Device::stopServer() {}  // the emulation has no scan server: every scan is evaluated in place
 
+// Queue scans: the directory is host bookkeeping here (no pool); the rows are evaluated in key order, which is the
+// order the server's first fit reports.
+bool Device::queueUsable() const { return true; }
+void Device::qdirBind(uint64_t key) {
+  if (key == qdirKey_ && !qdirSnap_.empty()) return;
+  qdirKey_ = key;
+  qdirSpan_ = 1;
+  qdirSnap_.assign(B_, nullptr);
+}
+bool Device::qdirSet(int b, std::shared_ptr<const std::vector<int32_t>> v) {
+  if (qdirSnap_.empty() || b < 0 || b >= B_) throw std::logic_error("qdirSet before qdirBind");
+  for (int r : *v)
+    if (rowBroker_ && rowBroker_[r] != b) throw std::logic_error("snapshot segment is not current for its broker");
+  qdirSpan_ = std::max(qdirSpan_, (int)v->size());
+  qdirSnap_[b] = std::move(v);
+  return true;
+}
+int64_t Device::scanQueue(const DevProgram& prog, int head, int skip0, const int32_t* tail, int nTail,
+                          const int32_t* cands, int N) {
+  runIdleWork(idleWork);
+  flushOnly();
+  View v{E(st_)};
+  perf.scanLaunches++;
+  const int span = qdirSpan_, hasHead = head >= 0 ? 1 : 0;
+  for (int i = 0; i < hasHead + nTail; ++i) {
+    const auto& rows = *qdirSnap_.at(i < hasHead ? head : tail[i - hasHead]);
+    for (size_t r = i == 0 ? (size_t)skip0 : 0; r < rows.size(); ++r)
+      for (int j = 0; j < N; ++j) {
+        perf.scanPairs++;
+        if (candidateBlocked(prog, v, rows[r], cands[j])) continue;
+        if (moveCandidateAccepted(prog, v, rows[r], cands[j])) return ((int64_t)i * span + (int64_t)r) * N + j;
+      }
+  }
+  return -1;
+}
+
 // no snapshot pool either (segsUsable() is false, so the engine flattens first; kept for the link)
 int64_t Device::scanSegs(const DevProgram& prog, const std::vector<SegIn>& segs, const int32_t* cands, int N, int c0,
                          int c1) {
