@@ -1941,26 +1941,63 @@ class ResourceDistribution : public GoalImpl {
     int curCb = -1;
     size_t curSkip = 0;
     auto cond = [&]() { return m.bNlead[b] != m.nrep(b); };
-    auto size = [&](int c) { return m.snapshotIn(snapTab, c, spec).size(); };
+    // The candidate brokers' live views: the queue scans' snapshot directory when it can be kept current for `spec`
+    // (the same Spec as this goal's replica move-in), else the goal's snapshot table.
+    const bool dir = e.queueOn(*this, DA_LEADERSHIP);
+    if (dir) e.queueSyncSpec(spec);
+    auto snap = [&](int c) -> const std::vector<int32_t>& {
+      return dir ? e.dev->qdirRows(c) : m.snapshotIn(snapTab, c, spec);
+    };
+    auto size = [&](int c) { return snap(c).size(); };
     auto indexOf = [&](int c, int r) {
-      const auto& v = m.snapshotIn(snapTab, c, spec);
+      const auto& v = snap(c);
       const uint64_t k = m.replicaKey(spec, r);
       return (size_t)(std::lower_bound(v.begin(), v.end(), k, [&](int x, uint64_t kk) { return m.replicaKey(spec, x) < kk; }) -
                       v.begin());
     };
+    // b's follower replicas grouped by the broker leading their partition (leaders move only by this loop's accepts,
+    // which make b the leader): a group's rows change only when its broker's view changes (version) or b leads one of
+    // its partitions, so the rows' view indices are cached per group and recomputed only then
+    struct Group {
+      int c;
+      std::vector<int32_t> rbs;
+      std::vector<int64_t> idx;  // view index of each rb's partition leader (-1: not selected / no row)
+      uint32_t ver = ~0u;
+    };
+    std::vector<Group> groups;
+    {
+      PhaseScope pf(PH_FLATTEN);
+      std::vector<std::pair<int, int>> lb;
+      for (int rb : m.bRepl[b])
+        if (!m.rLeader[rb]) lb.push_back({m.rBroker[m.pLeader[m.rPart[rb]]], rb});
+      std::sort(lb.begin(), lb.end());
+      for (const auto& x : lb) {
+        if (groups.empty() || groups.back().c != x.first) groups.push_back(Group{x.first, {}, {}, ~0u});
+        groups.back().rbs.push_back(x.second);
+      }
+    }
     while (curCb >= 0 || (!pq.empty() && cond())) {
       {
         PhaseScope pf(PH_FLATTEN);
         rows.clear();
-        for (int rb : m.bRepl[b]) {
-          if (m.rLeader[rb]) continue;  // b leads that partition: no leader row elsewhere
-          const int lr = m.pLeader[m.rPart[rb]];
-          const int cb = m.rBroker[lr];
-          if (cb != curCb && !queued[cb]) continue;
-          if (!m.selects(spec, lr)) continue;
-          const size_t idx = indexOf(cb, lr);
-          if (cb == curCb && idx < curSkip) continue;
-          rows.push_back({cb, idx, lr});
+        for (Group& g : groups) {
+          if (g.c != curCb && !queued[g.c]) continue;
+          if (g.ver != m.bVer[g.c]) {
+            g.idx.assign(g.rbs.size(), -1);
+            for (size_t k = 0; k < g.rbs.size(); ++k) {
+              const int rb = g.rbs[k];
+              if (m.rLeader[rb]) continue;  // b leads that partition now: no leader row elsewhere
+              const int lr = m.pLeader[m.rPart[rb]];
+              if (m.rBroker[lr] != g.c || !m.selects(spec, lr)) continue;
+              g.idx[k] = (int64_t)indexOf(g.c, lr);
+            }
+            g.ver = m.bVer[g.c];
+          }
+          for (size_t k = 0; k < g.rbs.size(); ++k) {
+            if (g.idx[k] < 0 || m.rLeader[g.rbs[k]]) continue;
+            if (g.c == curCb && (size_t)g.idx[k] < curSkip) continue;
+            rows.push_back({g.c, (size_t)g.idx[k], m.pLeader[m.rPart[g.rbs[k]]]});
+          }
         }
         std::sort(rows.begin(), rows.end(), [&](const Row& x, const Row& y) {
           if (x.cb != y.cb) {
@@ -2005,6 +2042,7 @@ class ResourceDistribution : public GoalImpl {
       const int cb = hit->cb;
       const size_t idx = hit->idx;
       m.relocateLeadership(m.rPart[hit->r], cb, b);
+      if (dir) e.queueSyncSpec(spec);  // cb's and b's views changed
       if (aboveLower(m, b)) return false;
       if (!pq.empty() && m.pct(cb, res) < m.pct(pq.peek(), res)) {
         pq.add(cb);

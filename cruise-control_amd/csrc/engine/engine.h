@@ -145,6 +145,8 @@ class Engine {
   // Returns the key (Device::scanQueue) or -1 and adds the reference-equivalent candidates. queueOn: the path applies
   // (one shard, a usable server, no replica-dependent candidate filters; CCMI_QUEUE_SCAN=0 turns it off).
   bool queueOn(const GoalImpl& self, int action) const;
+  // the snapshot directory current for `spec` (Device::qdirRows / qdirLen then give every broker's live view)
+  void queueSyncSpec(const Model::Spec& spec) { queueSync(spec); }
   int64_t queueScan(GoalImpl& self, int action, const Model::Spec& spec, int head, int skip0, const int32_t* tail,
                     int nTail, const std::vector<int32_t>& cands);
   int64_t exclLeadCount(const DevProgram& prog, const int32_t* reps, int K, const std::vector<int32_t>& cands,
