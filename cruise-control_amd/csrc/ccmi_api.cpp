@@ -352,6 +352,14 @@ ccmi_status ccmi_session_create(int32_t device_ordinal, const ccmi_cluster_desc*
       s->device->setDiskUtil(m.dUtil.data());
       m.diskDirty = false;
     }
+    if (m.sharedHosts) {  // Host._load for the chain kernels' moves, with each host's brokers (CSR)
+      std::vector<int32_t> hOff(1, 0), hBrk;
+      for (int h = 0; h < m.H; ++h) {
+        hBrk.insert(hBrk.end(), m.hBrokers[h].begin(), m.hBrokers[h].end());
+        hOff.push_back((int32_t)hBrk.size());
+      }
+      s->device->uploadHostLoads(m.H, m.hLoad.data(), m.bHost.data(), hOff.data(), hBrk.data());
+    }
     if (m.sharedHosts) {  // every broker's host utilization and capacity of the host resources
       std::vector<double> hu((size_t)3 * m.B), hc((size_t)3 * m.B);
       for (int b = 0; b < m.B; ++b)

@@ -45,7 +45,14 @@ CCMI_LD void ldAddSignedAll(LoadVec& d, const LoadVec& s, int W, bool neg) {
 
 // S provides: W; LoadVec& rLoad(r), bLoad(b), bLnw(b), bPot(b), scratch(i) (i = 0, 1: step-to-step values);
 // ReplicaRec& rep(r); BrokerRec& brk(b); PartitionRec& part(p); int& slot(p, i) (replica id of partition slot i);
-// int& leader(p); void topicAdd(t, b, d); void topicLeadAdd(t, b, d) (a no-op unless leader counts are kept).
+// int& leader(p); void topicAdd(t, b, d); void topicLeadAdd(t, b, d) (a no-op unless leader counts are kept);
+// bool hostsOn() (brokers share hosts), int host(b), LoadVec& hLoad(h), int hostBegin(h), hostEnd(h), hostBroker(i).
+//
+// Hosts (Model::sharedHosts): Host.addReplica / removeReplica add / subtract the replica's load (model/Host.java), and
+// Host.makeFollower / makeLeader the leadership CPU / NW_OUT delta when the host has metrics. Each host aggregate gets
+// one operation per broker of the move, in the reference's order (the source's first): two hosts take one lane each,
+// one host shared by source and destination takes both operations on one lane. Every broker of a touched host then
+// reads its host utilization (BrokerRec.hutil) again; without shared hosts hutil is the broker's own util.
 
 // ---- relocateReplica(tp, src, dst) of replica r: lanes 0..5, then applyReplicaFinish
 //   lane 0/1 Broker.load() of src (-= r) / dst (+= r)         -> util[4]
@@ -63,9 +70,10 @@ CCMI_LD void applyReplicaLane(S& s, int lane, int r, int src, int dst, int lr, b
   ldAddSignedAll(x, o, s.W, !(lane & 1));
   ldCopy(t, x, s.W);
   BrokerRec& rec = s.brk(b);
-  if (lane < 2) {  // (chains run only when every host holds one broker: the host values are the broker's)
+  if (lane < 2) {
     for (int k = 0; k < 4; ++k) rec.util[k] = ldUtil(x, k, s.W);
-    for (int k = 0; k < 3; ++k) rec.hutil[k] = rec.util[k];
+    if (!s.hostsOn())  // one broker per host: the host values are the broker's
+      for (int k = 0; k < 3; ++k) rec.hutil[k] = rec.util[k];
   } else if (lane < 4) {
     rec.pot = ldUtil(x, R_NW_OUT, s.W);
   } else {
@@ -144,7 +152,8 @@ CCMI_LD void applyLeadershipLane(S& s, int step, int lane, int sr, int dr, int s
     if (lane < 2) {
       BrokerRec& rec = s.brk(lane == 0 ? src : dst);
       for (int k = 0; k < 4; ++k) rec.util[k] = ldUtil(x, k, s.W);
-      for (int k = 0; k < 3; ++k) rec.hutil[k] = rec.util[k];
+      if (!s.hostsOn())
+        for (int k = 0; k < 3; ++k) rec.hutil[k] = rec.util[k];
     } else {
       ReplicaRec& rec = s.rep(dr);
       rec.flags |= (int32_t)RF_LEADER;
@@ -193,20 +202,75 @@ CCMI_LD void leadershipReplicas(S& s, int p, int src, int dst, int& sr, int& dr,
   }
 }
 
+// ---- host aggregates (S::hostsOn()): lane 0 the source's host, lane 1 the destination's when it is another host
+//   replica move: Host.removeReplica (src host -= r), Host.addReplica (dst host += r)
+constexpr int kHostLanes = 2;
+template <class S>
+CCMI_LD void applyHostReplicaLane(S& s, int lane, int r, int src, int dst) {
+  if (!s.hostsOn() || lane >= kHostLanes) return;
+  const int hs = s.host(src), hd = s.host(dst);
+  if (lane == 1 && hs == hd) return;
+  LoadVec& t = s.hLoad(lane == 0 ? hs : hd);
+  LoadVec x, o;
+  ldCopy(x, t, s.W);
+  ldCopy(o, s.rLoad(r), s.W);
+  ldAddSignedAll(x, o, s.W, lane == 0);
+  if (lane == 0 && hs == hd) ldAddSignedAll(x, o, s.W, false);
+  ldCopy(t, x, s.W);
+}
+//   leadership (step 1, delta = scratch(0)): Host.makeFollower (src host -= delta), Host.makeLeader (dst host += delta),
+//   each only when the host has metrics
+template <class S>
+CCMI_LD void applyHostLeadershipLane(S& s, int lane, int src, int dst) {
+  if (!s.hostsOn() || lane >= kHostLanes) return;
+  const int hs = s.host(src), hd = s.host(dst);
+  if (lane == 1 && hs == hd) return;
+  LoadVec& t = s.hLoad(lane == 0 ? hs : hd);
+  LoadVec x, o;
+  ldCopy(x, t, s.W);
+  if (!x.mask) return;
+  ldCopy(o, s.scratch(0), s.W);
+  ldAddSignedAll(x, o, s.W, lane == 0);
+  if (lane == 0 && hs == hd) ldAddSignedAll(x, o, s.W, false);
+  ldCopy(t, x, s.W);
+}
+// every broker of the move's host(s): BrokerRec.hutil from the host load (ClusterModel.host(...).load()); lanes
+// [lane0, ...) stepping by `step` share the brokers
+template <class S>
+CCMI_LD void applyHostUtil(S& s, int src, int dst, int lane, int step) {
+  if (!s.hostsOn()) return;
+  const int hs = s.host(src), hd = s.host(dst);
+  for (int pass = 0; pass < 2; ++pass) {
+    const int h = pass == 0 ? hs : hd;
+    if (pass == 1 && hd == hs) break;
+    const LoadVec& L = s.hLoad(h);
+    for (int i = s.hostBegin(h) + lane; i < s.hostEnd(h); i += step) {
+      BrokerRec& rec = s.brk(s.hostBroker(i));
+      for (int k = 0; k < 3; ++k) rec.hutil[k] = ldUtil(L, k, s.W);
+    }
+  }
+}
+
 // Sequential form (emulation): every lane of every step in order.
 template <class S>
 inline void applyRelocateReplica(S& s, int r, int dst) {
   const int src = s.rep(r).broker, lr = s.leader(s.rep(r).part);
   const bool lead = (s.rep(r).flags & RF_LEADER) != 0;
   for (int l = 0; l < kReplicaLanes; ++l) applyReplicaLane(s, l, r, src, dst, lr, lead);
+  for (int l = 0; l < kHostLanes; ++l) applyHostReplicaLane(s, l, r, src, dst);
+  applyHostUtil(s, src, dst, 0, 1);
   applyReplicaFinish(s, r, src, dst, lead);
 }
 template <class S>
 inline void applyRelocateLeadership(S& s, int p, int src, int dst) {
   int sr, dr, dpos;
   leadershipReplicas(s, p, src, dst, sr, dr, dpos);
-  for (int st = 0; st < kLeadershipSteps; ++st)
+  for (int st = 0; st < kLeadershipSteps; ++st) {
     for (int l = 0; l < 4; ++l) applyLeadershipLane(s, st, l, sr, dr, src, dst);
+    if (st == 1)
+      for (int l = 0; l < kHostLanes; ++l) applyHostLeadershipLane(s, l, src, dst);
+  }
+  applyHostUtil(s, src, dst, 0, 1);
   applyLeadershipFinish(s, p, dr, dpos, src, dst);
 }
 

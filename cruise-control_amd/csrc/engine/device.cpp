@@ -233,7 +233,8 @@ Device::~Device() {
   }
   void* ps[] = {brokers_, replicas_, parts_, allowedAlive_, topicCount_, topicNrep_, topicScratch_, statsOut_,
                 statsPart_, dReq_, rowVisited_, dResult_, dDone_, dChainReq_, dRackRes_, tUpper_, tLower_, dRLoad_, dBLoad_, dBLnw_, dBPot_, dPOff_, dPSlots_,
-                dPLeader_, pIneligOff_, pIneligB_, topicLead_, tMinLead_, tLeadLim_, hostCap_};
+                dPLeader_, pIneligOff_, pIneligB_, topicLead_, tMinLead_, tLeadLim_, hostCap_, dHLoad_, dBHost_,
+                dHOff_, dHBrk_};
   for (void* p : ps)
     if (p) (void)hipFree(p);
   if (hChainLog_) (void)hipHostFree(hChainLog_);
@@ -1379,6 +1380,20 @@ void Device::uploadLoads(int W, const LoadVec* rLoad, const LoadVec* bLoad, cons
   hipCheck(hipMemcpy(dPLeader_, pLeader, sizeof(int32_t) * P_, hipMemcpyHostToDevice), "upload pLeader");
 }
 
+void Device::uploadHostLoads(int H, const LoadVec* hLoad, const int32_t* bHost, const int32_t* hOff,
+                             const int32_t* hBrk) {
+  DeviceGuard dg(ordinal_);
+  stopServer();
+  dalloc(&dHLoad_, (size_t)H);
+  dalloc(&dBHost_, (size_t)B_);
+  dalloc(&dHOff_, (size_t)H + 1);
+  dalloc(&dHBrk_, (size_t)B_);
+  hipCheck(hipMemcpy(dHLoad_, hLoad, sizeof(LoadVec) * H, hipMemcpyHostToDevice), "upload host loads");
+  hipCheck(hipMemcpy(dBHost_, bHost, sizeof(int32_t) * B_, hipMemcpyHostToDevice), "upload broker hosts");
+  hipCheck(hipMemcpy(dHOff_, hOff, sizeof(int32_t) * (H + 1), hipMemcpyHostToDevice), "upload host offsets");
+  hipCheck(hipMemcpy(dHBrk_, hBrk, sizeof(int32_t) * hOff[H], hipMemcpyHostToDevice), "upload host brokers");
+}
+
 ChainTables Device::chainTables() const {
   ChainTables c;
   c.brokers = brokers_;
@@ -1395,6 +1410,10 @@ ChainTables Device::chainTables() const {
   c.pOff = dPOff_;
   c.pSlots = dPSlots_;
   c.pLeader = dPLeader_;
+  c.hLoad = dHLoad_;
+  c.bHost = dBHost_;
+  c.hOff = dHOff_;
+  c.hBrk = dHBrk_;
   return c;
 }
 

@@ -194,6 +194,8 @@ class Device {
   // without the device since the last chain and are sent first.
   void uploadLoads(int W, const LoadVec* rLoad, const LoadVec* bLoad, const LoadVec* bLnw, const LoadVec* bPot,
                    const int32_t* pSlots, const int32_t* pLeader);
+  // brokers sharing hosts: Host._load per host, each broker's host and the hosts' brokers (CSR), once per session
+  void uploadHostLoads(int H, const LoadVec* hLoad, const int32_t* bHost, const int32_t* hOff, const int32_t* hBrk);
   std::vector<LoadRow> lrows;
   std::vector<SlotRow> srows;
   struct ChainResult {
@@ -336,7 +338,8 @@ class Device {
   size_t rowVisitedCap_ = 0;
   // chain state
   int W_ = 1;
-  LoadVec *dRLoad_ = nullptr, *dBLoad_ = nullptr, *dBLnw_ = nullptr, *dBPot_ = nullptr;
+  LoadVec *dRLoad_ = nullptr, *dBLoad_ = nullptr, *dBLnw_ = nullptr, *dBPot_ = nullptr, *dHLoad_ = nullptr;
+  int32_t *dBHost_ = nullptr, *dHOff_ = nullptr, *dHBrk_ = nullptr;
   int32_t *dPOff_ = nullptr, *dPSlots_ = nullptr, *dPLeader_ = nullptr;
   // chain results in host-coherent mapped memory: the kernels write them, the host reads them after the stream sync
   // (no device-to-host copies per chain)

@@ -303,9 +303,15 @@ struct ChainTables {
   const int32_t* pOff;  // [P+1]
   int32_t* pSlots;   // [R]  replica ids in Partition._replicas order (leader first)
   int32_t* pLeader;  // [P]
+  // brokers sharing hosts (Model::sharedHosts; hLoad null otherwise): Host._load per host, each broker's host and every
+  // host's brokers (CSR), so a chain move updates the host aggregates and every broker's BrokerRec.hutil of the host
+  LoadVec* hLoad;         // [H]
+  const int32_t* bHost;   // [B]
+  const int32_t* hOff;    // [H+1]
+  const int32_t* hBrk;    // [B]
 };
 // Host-side changes to those loads since the last chain launch (moves the host applied without the device).
-enum LoadRowKind : int32_t { LR_REPLICA = 0, LR_BROKER = 1, LR_LEADERSHIP_NW = 2, LR_POTENTIAL = 3 };
+enum LoadRowKind : int32_t { LR_REPLICA = 0, LR_BROKER = 1, LR_LEADERSHIP_NW = 2, LR_POTENTIAL = 3, LR_HOST = 4 };
 struct LoadRow {
   int32_t kind, id;
   LoadVec v;

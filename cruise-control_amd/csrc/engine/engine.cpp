@@ -302,7 +302,8 @@ int64_t Engine::crossScanSegs(GoalImpl& self, int action, const std::vector<Snap
 
 bool Engine::queueOn(const GoalImpl& self, int action) const {
   static const bool off = std::getenv("CCMI_QUEUE_SCAN") && std::getenv("CCMI_QUEUE_SCAN")[0] == '0';
-  if (off || shard.count > 1 || !dev->queueUsable()) return false;
+  // (a destination-sharded session scans the whole queue on every rank: identical models, identical first fit)
+  if (off || !dev->queueUsable()) return false;
   const DevProgram prog = program(self, action);
   return !prog.exclLeadMove && !prog.newOnly;
 }
@@ -471,8 +472,10 @@ int64_t Engine::swapScan(GoalImpl& self, const std::vector<int32_t>& srcs, const
 
 bool Engine::chainsOn() const {
   static const bool off = std::getenv("CCMI_NO_CHAINS") != nullptr;
-  // a chain would apply the move a terminal goal refuses; chain kernels keep no host loads (shared hosts)
-  return !off && shard.count <= 1 && !terminalOptimized() && !m.sharedHosts;
+  // a chain would apply the move a terminal goal refuses; chains keep the host loads of brokers sharing hosts too
+  // (apply.h host lanes). A destination-sharded session runs every chain whole on each rank: the ranks hold identical
+  // models, so they make the same decisions without a combine.
+  return !off && !terminalOptimized();
 }
 
 bool Engine::terminalOptimized() const {

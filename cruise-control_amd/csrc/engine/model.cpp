@@ -276,6 +276,7 @@ void Model::build(const ccmi_cluster_desc& d) {
   cDirtyB.assign(B, 0);
   cDirtyR.assign(R, 0);
   cDirtyP.assign(P, 0);
+  cDirtyH.assign(sharedHosts ? H : 0, 0);
 }
 
 // Disks (ccmi.h desc fields): created with their broker, logdir order per broker, replica_disk given to
@@ -602,6 +603,10 @@ void Model::relocateReplica(int p, int src, int dst) {
   if (dev && !replaying) {
     markChain(cDirtyB, cDirtyBList, src);
     markChain(cDirtyB, cDirtyBList, dst);
+    if (sharedHosts) {
+      markChain(cDirtyH, cDirtyHList, bHost[src]);
+      markChain(cDirtyH, cDirtyHList, bHost[dst]);
+    }
     markB(src);
     markB(dst);
     markR(r);
@@ -709,6 +714,10 @@ bool Model::relocateLeadership(int p, int src, int dst) {
     }
     markChain(cDirtyB, cDirtyBList, src);
     markChain(cDirtyB, cDirtyBList, dst);
+    if (sharedHosts) {
+      markChain(cDirtyH, cDirtyHList, bHost[src]);
+      markChain(cDirtyH, cDirtyHList, bHost[dst]);
+    }
     markChain(cDirtyR, cDirtyRList, sr);
     markChain(cDirtyR, cDirtyRList, dr);
     markChain(cDirtyP, cDirtyPList, p);
@@ -786,6 +795,11 @@ void Model::flushChainLoads() {
     cDirtyP[p] = 0;
   }
   cDirtyPList.clear();
+  for (int h : cDirtyHList) {
+    dev->lrows.push_back({LR_HOST, h, hLoad[h]});
+    cDirtyH[h] = 0;
+  }
+  cDirtyHList.clear();
 }
 
 // ------------------------------------------------------------------------------- sorted replicas

@@ -219,8 +219,8 @@ class Model {
   // Device::lrows / srows before the next one. While `replaying` the host re-applies moves the device already made:
   // nothing is marked.
   bool replaying = false;
-  std::vector<uint8_t> cDirtyB, cDirtyR, cDirtyP;
-  std::vector<int32_t> cDirtyBList, cDirtyRList, cDirtyPList;
+  std::vector<uint8_t> cDirtyB, cDirtyR, cDirtyP, cDirtyH;
+  std::vector<int32_t> cDirtyBList, cDirtyRList, cDirtyPList, cDirtyHList;
   void markChain(std::vector<uint8_t>& f, std::vector<int32_t>& l, int x) {
     if (!f[x]) {
       f[x] = 1;

@@ -933,7 +933,8 @@ __device__ __attribute__((noinline)) void serverChain(const DevTables T, const C
     LoadRow x;
     copySysOneThread(&x, &lrows[i]);
     LoadVec* dst = x.kind == LR_REPLICA ? C.rLoad
-                   : (x.kind == LR_BROKER ? C.bLoad : (x.kind == LR_LEADERSHIP_NW ? C.bLnw : C.bPot));
+                   : (x.kind == LR_BROKER       ? C.bLoad
+                      : (x.kind == LR_LEADERSHIP_NW ? C.bLnw : (x.kind == LR_HOST ? C.hLoad : C.bPot)));
     dst[x.id] = x.v;
   }
   const SlotRow* srows = (const SlotRow*)(pay + c.oS);
@@ -1586,6 +1587,12 @@ struct DevApply {
   __device__ __forceinline__ void topicLeadAdd(int t, int b, int d) {
     if (c.topicLead) c.topicLead[(size_t)t * c.ldB + b] += d;
   }
+  __device__ __forceinline__ bool hostsOn() const { return c.hLoad != nullptr; }
+  __device__ __forceinline__ int host(int b) const { return c.bHost[b]; }
+  __device__ __forceinline__ LoadVec& hLoad(int h) { return c.hLoad[h]; }
+  __device__ __forceinline__ int hostBegin(int h) const { return c.hOff[h]; }
+  __device__ __forceinline__ int hostEnd(int h) const { return c.hOff[h + 1]; }
+  __device__ __forceinline__ int hostBroker(int i) const { return c.hBrk[i]; }
 };
 
 
@@ -1601,6 +1608,11 @@ __device__ void chainApply(const ChainTables& C, LoadVec* sc, int action, int r,
     leadershipReplicas(S, p, src, dst, sr, dr, dpos);
     for (int st = 0; st < kLeadershipSteps; ++st) {
       if (t < 4) applyLeadershipLane(S, st, t, sr, dr, src, dst);
+      else if (st == 1 && t < 4 + kHostLanes) applyHostLeadershipLane(S, t - 4, src, dst);
+      chainSync();
+    }
+    if (S.hostsOn()) {  // (block-uniform) every broker of the touched hosts reads its host utilization again
+      applyHostUtil(S, src, dst, t, (int)blockDim.x);
       chainSync();
     }
     if (t == 0) applyLeadershipFinish(S, p, dr, dpos, src, dst);
@@ -1608,7 +1620,12 @@ __device__ void chainApply(const ChainTables& C, LoadVec* sc, int action, int r,
     const bool lead = (rr.flags & RF_LEADER) != 0;
     const int lr = C.pLeader[p];
     if (t < kReplicaLanes) applyReplicaLane(S, t, r, src, dst, lr, lead);
+    else if (t < kReplicaLanes + kHostLanes) applyHostReplicaLane(S, t - kReplicaLanes, r, src, dst);
     chainSync();
+    if (S.hostsOn()) {
+      applyHostUtil(S, src, dst, t, (int)blockDim.x);
+      chainSync();
+    }
     if (t == 0) applyReplicaFinish(S, r, src, dst, lead);
   }
   chainSync();
@@ -1817,7 +1834,9 @@ __global__ __launch_bounds__(256) void sync_loads(ChainTables C, const LoadRow* 
   const int stride = gridDim.x * blockDim.x;
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < nl; i += stride) {
     const LoadRow& x = lrows[i];
-    LoadVec* dst = x.kind == LR_REPLICA ? C.rLoad : (x.kind == LR_BROKER ? C.bLoad : (x.kind == LR_LEADERSHIP_NW ? C.bLnw : C.bPot));
+    LoadVec* dst = x.kind == LR_REPLICA ? C.rLoad
+                   : (x.kind == LR_BROKER       ? C.bLoad
+                      : (x.kind == LR_LEADERSHIP_NW ? C.bLnw : (x.kind == LR_HOST ? C.hLoad : C.bPot)));
     dst[x.id] = x.v;
   }
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < ns; i += stride) {

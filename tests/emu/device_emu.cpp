@@ -43,6 +43,8 @@ struct Emu {
   // chain state (device.h uploadLoads)
   int W = 1;
   std::vector<LoadVec> lRep, lBrk, lLnw, lPot;
+  std::vector<LoadVec> lHost;  // Host._load (brokers sharing hosts; empty otherwise)
+  std::vector<int32_t> bHostOf, hOffE, hBrkE;
   std::vector<int32_t> pSlots, pLeader;
   // disk state (device.h uploadDisks)
   int D = 0;
@@ -334,6 +336,7 @@ struct EmuApply {
       x.rack = e.bRack[b];
       x.allowedBits = e.allowed[b];
       x.alive = e.bAlive[b];
+      for (int k = 0; k < 3; ++k) x.hutil[k] = e.hUtil.empty() ? x.util[k] : e.hUtil[3 * (size_t)b + k];
     }
     replicas.assign(e.R, ReplicaRec{});
     for (int r = 0; r < e.R; ++r) {
@@ -362,6 +365,12 @@ struct EmuApply {
   LoadVec& bLoad(int b) { return e.lBrk[b]; }
   LoadVec& bLnw(int b) { return e.lLnw[b]; }
   LoadVec& bPot(int b) { return e.lPot[b]; }
+  bool hostsOn() const { return !e.lHost.empty(); }
+  int host(int b) const { return e.bHostOf[b]; }
+  LoadVec& hLoad(int h) { return e.lHost[h]; }
+  int hostBegin(int h) const { return e.hOffE[h]; }
+  int hostEnd(int h) const { return e.hOffE[h + 1]; }
+  int hostBroker(int i) const { return e.hBrkE[i]; }
   ReplicaRec& rep(int r) { return replicas[r]; }
   BrokerRec& brk(int b) { return brokers[b]; }
   PartitionRec& part(int p) { return parts[p]; }
@@ -379,6 +388,11 @@ struct EmuApply {
     e.bLeadNwIn[b] = x.lbi;
     e.bNrep[b] = x.nrep;
     e.bNlead[b] = x.nlead;
+    if (hostsOn())  // the host utilization of every broker of b's host (applyHostUtil wrote them all)
+      for (int i = hostBegin(host(b)); i < hostEnd(host(b)); ++i) {
+        const int y = hostBroker(i);
+        for (int k = 0; k < 3; ++k) e.hUtil[3 * (size_t)y + k] = brokers[y].hutil[k];
+      }
   }
   void writeReplica(int r) {
     const ReplicaRec& x = replicas[r];
@@ -411,6 +425,15 @@ struct EmuApply {
 };
 }  // namespace
 
+void Device::uploadHostLoads(int H, const LoadVec* hLoad, const int32_t* bHost, const int32_t* hOff,
+                             const int32_t* hBrk) {
+  Emu& e = E(st_);
+  e.lHost.assign(hLoad, hLoad + H);
+  e.bHostOf.assign(bHost, bHost + B_);
+  e.hOffE.assign(hOff, hOff + H + 1);
+  e.hBrkE.assign(hBrk, hBrk + hOff[H]);
+}
+
 void Device::uploadLoads(int W, const LoadVec* rLoad, const LoadVec* bLoad, const LoadVec* bLnw, const LoadVec* bPot,
                          const int32_t* pSlots, const int32_t* pLeader) {
   Emu& e = E(st_);
@@ -425,7 +448,9 @@ void Device::uploadLoads(int W, const LoadVec* rLoad, const LoadVec* bLoad, cons
 
 static void emuSyncLoads(Emu& e, std::vector<LoadRow>& lrows, std::vector<SlotRow>& srows) {
   for (const LoadRow& x : lrows) {
-    std::vector<LoadVec>& v = x.kind == LR_REPLICA ? e.lRep : (x.kind == LR_BROKER ? e.lBrk : (x.kind == LR_LEADERSHIP_NW ? e.lLnw : e.lPot));
+    std::vector<LoadVec>& v = x.kind == LR_REPLICA ? e.lRep
+                              : (x.kind == LR_BROKER       ? e.lBrk
+                                 : (x.kind == LR_LEADERSHIP_NW ? e.lLnw : (x.kind == LR_HOST ? e.lHost : e.lPot)));
     v[x.id] = x.v;
   }
   for (const SlotRow& x : srows) {

@@ -42,13 +42,38 @@ def golden_options(g):
     return ccmi.OptimizationOptions(**g["options"]) if g.get("options") else None
 
 
+def assign_shared_hosts(buf, per_host):
+    """Brokers of a RandomCluster sharing hosts: within every rack (ascending rack index), consecutive brokers by id fill
+    hosts of `per_host` brokers (Rack._hosts keys a host by name within its rack, model/Rack.java:256-262). Sets
+    desc.broker_host and returns the host array (keep it alive with the buffers). No reference fixture shares a host
+    (RandomCluster names every host after its broker, RandomCluster.java:80,87): parity on these models is pinned by
+    the oracle's Host restatement and ClusterModel.sanityCheck's host sums (tests/test_hosts.py)."""
+    import ctypes as C
+    d = buf.desc
+    by_rack = {}
+    for b in range(d.num_brokers):
+        by_rack.setdefault(d.broker_rack[b], []).append(b)
+    host = [0] * d.num_brokers
+    nxt = 0
+    for rack in sorted(by_rack):
+        for i, b in enumerate(by_rack[rack]):
+            if i % per_host == 0:
+                nxt += 1
+            host[b] = nxt - 1
+    arr = (C.c_int32 * d.num_brokers)(*host)
+    d.broker_host = C.cast(arr, C.POINTER(C.c_int32))
+    return arr
+
+
 def check_product_against_golden(lib, name, per_goal_stats=False):
     """The product on a golden case: action log, assignment, leaders, per-goal (name, succeeded, candidates,
     actions) and final stats; with per_goal_stats every goal's ClusterModelStats (goldens that store them)."""
     g = golden(name)
     bc = constraint(g["resource_balance_percentage"], g.get("max_replicas_per_broker"), g.get("capacity_threshold"))
     buf = ccmi.RandomCluster.generate(lib, **g["props"])
-    cm = ccmi.ClusterModel.from_buffers(buf)
+    hosts = assign_shared_hosts(buf, g["brokers_per_host"]) if g.get("brokers_per_host") else None
+    cm = ccmi.ClusterModel(buf.desc, device=0, lib=lib, keepalive=(buf, hosts)) if hosts is not None \
+        else ccmi.ClusterModel.from_buffers(buf)
     pre = cm.cluster_stats(bc)
     res = ccmi.GoalOptimizer(bc).optimizations(cm, ccmi.goals_from_names(g["goals"]), golden_options(g))
     check_against_golden(g, cm.actions(), cm.replica_distribution(), cm.leader_distribution(), res.goal_results,

@@ -19,7 +19,7 @@ import pytest
 
 import ccmi
 from oracle_binding import OracleCluster
-from parity import check_desc_against_oracle, constraint
+from parity import assign_shared_hosts, check_desc_against_oracle, constraint
 
 CAP = {"CPU": 100.0, "DISK": 300000.0, "NW_IN": 300000.0, "NW_OUT": 200000.0}
 HOST_GOALS = ["CpuCapacityGoal", "NetworkInboundCapacityGoal", "NetworkOutboundCapacityGoal",
@@ -51,24 +51,10 @@ OWN = [f"h{b}" for b in range(6)]
 
 
 def _shared_random(lib, per_host=2, **props):
-    """A RandomCluster whose brokers share hosts: within every rack, consecutive brokers (by id) fill hosts of
-    `per_host` brokers. Returns (buffers, host array kept alive with them)."""
+    """A RandomCluster whose brokers share hosts (parity.assign_shared_hosts). Returns (buffers, host array kept alive
+    with them)."""
     buf = ccmi.RandomCluster.generate(lib, **props)
-    d = buf.desc
-    by_rack = {}
-    for b in range(d.num_brokers):
-        by_rack.setdefault(d.broker_rack[b], []).append(b)
-    host = [0] * d.num_brokers
-    nxt = 0
-    for rack in sorted(by_rack):
-        members = by_rack[rack]
-        for i, b in enumerate(members):
-            if i % per_host == 0:
-                nxt += 1
-            host[b] = nxt - 1
-    arr = (C.c_int32 * d.num_brokers)(*host)
-    d.broker_host = C.cast(arr, C.POINTER(C.c_int32))
-    return buf, arr
+    return buf, assign_shared_hosts(buf, per_host)
 
 
 RANDOM = dict(num_racks=5, num_brokers=24, num_replicas=6000, num_topics=300)
@@ -196,3 +182,20 @@ def test_gpu_load_monitor_shared_host_matches_oracle(gpu_lib, oracle_lib):
     m = _load_monitor_shared(gpu_lib)
     check_desc_against_oracle(gpu_lib, m.desc(), m, ["ReplicaDistributionGoal"] + HOST_GOALS,
                               ccmi.BalancingConstraint())
+
+
+# ------------------------------------------------------------------------------------------------ C1 with shared hosts
+# tests/golden/c1_shared_hosts_default.json: C1's cluster, two brokers of a rack per host, the 16 default goals — the
+# K7 chains (LeaderReplicaDistribution, RackAware with optimized goals) apply moves with the host loads on the device
+# (apply.h host lanes). Pinned by the oracle's Host restatement only (no reference fixture shares a host).
+def test_emu_c1_shared_hosts_matches_golden(emu_lib, oracle_lib):
+    from parity import check_product_against_golden
+    cm, _ = check_product_against_golden(emu_lib, "c1_shared_hosts_default")
+    assert cm.perf().chain_launches > 0  # the chains ran with shared hosts
+
+
+@pytest.mark.gpu
+def test_gpu_c1_shared_hosts_matches_golden(gpu_lib, oracle_lib):
+    from parity import check_product_against_golden
+    cm, res = check_product_against_golden(gpu_lib, "c1_shared_hosts_default", per_goal_stats=True)
+    assert cm.perf().chain_launches + cm.perf().server_chains > 0
