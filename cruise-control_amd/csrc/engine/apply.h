@@ -80,30 +80,46 @@ CCMI_LD void applyReplicaLane(S& s, int lane, int r, int src, int dst, int lr, b
     rec.lbi = ldUtil(x, R_NW_IN, s.W);
   }
 }
-// counts, the replica's broker, its partition slot and the topic counts (one thread, after the lanes)
+// counts, the replica's broker, its partition slot and the topic counts, after the lanes: independent fields, one
+// finish lane each (kReplicaFinishLanes, in parallel on the device)
+constexpr int kReplicaFinishLanes = 8;
+template <class S>
+CCMI_LD void applyReplicaFinishLane(S& s, int lane, int r, int p, int src, int dst, bool lead) {
+  switch (lane) {
+    case 0:
+      s.brk(src).nrep -= 1;
+      if (lead) s.brk(src).nlead -= 1;
+      break;
+    case 1:
+      s.brk(dst).nrep += 1;
+      if (lead) s.brk(dst).nlead += 1;
+      break;
+    case 2: s.rep(r).broker = dst; break;
+    case 3: {
+      PartitionRec& pr = s.part(p);
+      const int16_t rk = (int16_t)s.brk(dst).rack;
+      for (int i = 0; i < kMaxRf; ++i)
+        if (i < pr.n && s.slot(p, i) == r) {
+          pr.brokers[i] = dst;
+          pr.racks[i] = rk;
+        }
+      break;
+    }
+    case 4: s.topicAdd(s.part(p).topic, src, -1); break;
+    case 5: s.topicAdd(s.part(p).topic, dst, +1); break;
+    case 6:
+      if (lead) s.topicLeadAdd(s.part(p).topic, src, -1);
+      break;
+    case 7:
+      if (lead) s.topicLeadAdd(s.part(p).topic, dst, +1);
+      break;
+    default: break;
+  }
+}
 template <class S>
 CCMI_LD void applyReplicaFinish(S& s, int r, int src, int dst, bool lead) {
-  s.brk(src).nrep -= 1;
-  s.brk(dst).nrep += 1;
-  if (lead) {
-    s.brk(src).nlead -= 1;
-    s.brk(dst).nlead += 1;
-  }
   const int p = s.rep(r).part;
-  s.rep(r).broker = dst;
-  PartitionRec& pr = s.part(p);
-  const int16_t rk = (int16_t)s.brk(dst).rack;
-  for (int i = 0; i < kMaxRf; ++i)
-    if (i < pr.n && s.slot(p, i) == r) {
-      pr.brokers[i] = dst;
-      pr.racks[i] = rk;
-    }
-  s.topicAdd(pr.topic, src, -1);
-  s.topicAdd(pr.topic, dst, +1);
-  if (lead) {
-    s.topicLeadAdd(pr.topic, src, -1);
-    s.topicLeadAdd(pr.topic, dst, +1);
-  }
+  for (int l = 0; l < kReplicaFinishLanes; ++l) applyReplicaFinishLane(s, l, r, p, src, dst, lead);
 }
 
 // ---- relocateLeadership(tp, src, dst) of the leader sr (on src) to the follower dr (on dst)
@@ -167,24 +183,40 @@ CCMI_LD void applyLeadershipLane(S& s, int step, int lane, int sr, int dr, int s
     s.brk(dst).lbi = ldUtil(x, R_NW_IN, s.W);
   }
 }
+// leader counts, Partition.relocateLeadership (slots and leader), the partition record and the topic leader counts:
+// independent fields, one finish lane each (kLeadershipFinishLanes, in parallel on the device)
+constexpr int kLeadershipFinishLanes = 6;
+template <class S>
+CCMI_LD void applyLeadershipFinishLane(S& s, int lane, int p, int dr, int dpos, int src, int dst) {
+  switch (lane) {
+    case 0: s.brk(src).nlead -= 1; break;
+    case 1: s.brk(dst).nlead += 1; break;
+    case 2: {
+      const int first = s.slot(p, 0);
+      s.slot(p, 0) = dr;
+      s.slot(p, dpos) = first;
+      s.leader(p) = dr;
+      break;
+    }
+    case 3: {
+      PartitionRec& pr = s.part(p);
+      const int b0 = pr.brokers[0];
+      pr.brokers[0] = pr.brokers[dpos];
+      pr.brokers[dpos] = b0;
+      const int16_t k0 = pr.racks[0];
+      pr.racks[0] = pr.racks[dpos];
+      pr.racks[dpos] = k0;
+      pr.leadNwOut = s.rep(dr).util[R_NW_OUT];
+      break;
+    }
+    case 4: s.topicLeadAdd(s.part(p).topic, src, -1); break;
+    case 5: s.topicLeadAdd(s.part(p).topic, dst, +1); break;
+    default: break;
+  }
+}
 template <class S>
 CCMI_LD void applyLeadershipFinish(S& s, int p, int dr, int dpos, int src, int dst) {
-  s.brk(src).nlead -= 1;
-  s.brk(dst).nlead += 1;
-  const int first = s.slot(p, 0);
-  s.slot(p, 0) = dr;
-  s.slot(p, dpos) = first;
-  s.leader(p) = dr;
-  PartitionRec& pr = s.part(p);
-  const int b0 = pr.brokers[0];
-  pr.brokers[0] = pr.brokers[dpos];
-  pr.brokers[dpos] = b0;
-  const int16_t k0 = pr.racks[0];
-  pr.racks[0] = pr.racks[dpos];
-  pr.racks[dpos] = k0;
-  pr.leadNwOut = s.rep(dr).util[R_NW_OUT];
-  s.topicLeadAdd(pr.topic, src, -1);
-  s.topicLeadAdd(pr.topic, dst, +1);
+  for (int l = 0; l < kLeadershipFinishLanes; ++l) applyLeadershipFinishLane(s, l, p, dr, dpos, src, dst);
 }
 // the two replicas of p on src and dst, and dr's slot
 template <class S>

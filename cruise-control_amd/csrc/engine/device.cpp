@@ -1675,6 +1675,12 @@ void Device::uploadDisks(int D, const int32_t* bDiskOff, const int32_t* bDisks, 
   hipCheck(hipMemcpy(dRDu_, rDu, sizeof(double) * R_, hipMemcpyHostToDevice), "upload rDu");
   hipCheck(hipMemcpy(dRScore_, rScore, sizeof(float) * R_, hipMemcpyHostToDevice), "upload rScore");
   hipCheck(hipMemcpy(dRTie_, rTie, sizeof(int32_t) * R_, hipMemcpyHostToDevice), "upload rTie");
+  {
+    std::vector<IntraRep> st((size_t)R_);
+    for (int r = 0; r < R_; ++r) st[r] = IntraRep{rDu[r], rScore[r], rTie[r], rOrigDisk[r], {0, 0, 0}};
+    dallocTracked(&dRStat_, (size_t)R_, o);
+    hipCheck(hipMemcpy(dRStat_, st.data(), sizeof(IntraRep) * R_, hipMemcpyHostToDevice), "upload replica records");
+  }
   hBDiskOff_.assign(bDiskOff, bDiskOff + B_ + 1);
 }
 
@@ -1752,6 +1758,7 @@ void Device::intraRun(const IntraRequest& q, IntraResult& out) {
   A.rScore = dRScore_;
   A.rTie = dRTie_;
   A.rOrigDisk = dROrigDisk_;
+  A.rStat = dRStat_;
   A.rSel = dRSel_;
   A.snapA = dSnapA_;
   A.snapB = dSnapB_;

@@ -16,6 +16,7 @@
 #include <vector>
 
 #include "devtypes.h"
+#include "intra.h"
 #include "snapseg.h"
 
 namespace ccmi {
@@ -364,6 +365,7 @@ class Device {
           *dStatus_ = nullptr, *dLogRep_ = nullptr, *dLogSrc_ = nullptr, *dLogDst_ = nullptr, *dCRep_ = nullptr,
           *dCSrc_ = nullptr, *dCDst_ = nullptr;
   int64_t *dLogOff_ = nullptr, *dCand_ = nullptr, *dCOff_ = nullptr;
+  IntraRep* dRStat_ = nullptr;  // K6 packed static replica fields
   double* dEDu_ = nullptr;  // K6 entry-indexed gathers (IntraArgs.eDu / eOrig / eKeyRev / eKeyFwd)
   int32_t* dEOrig_ = nullptr;
   uint64_t *dEKeyRev_ = nullptr, *dEKeyFwd_ = nullptr;

@@ -35,6 +35,16 @@ struct IntraPrior {  // an optimized intra-broker goal whose actionAcceptance ev
   const double* lower;
 };
 
+// A replica's static K6 fields in one 32-byte record (intra_sort gathers one line per entry instead of one per field)
+struct alignas(32) IntraRep {
+  double du;         // expectedUtilizationFor(DISK)
+  float score;       // valuesForGroup(DISK).avg()
+  int32_t tie;       // Replica.compareTo rank among online replicas
+  int32_t origDisk;  // Replica._originalDisk (-1 = null)
+  int32_t pad[3];
+};
+static_assert(sizeof(IntraRep) == 32, "one aligned 32-byte record per replica");
+
 struct IntraArgs {
   int32_t goal;    // IntraGoal being optimized
   double capThr;   // BalancingConstraint.capacityThreshold(DISK)
@@ -58,6 +68,7 @@ struct IntraArgs {
   const int32_t* rTie;     // [R] Replica.compareTo rank among online replicas
   const int32_t* rOrigDisk;  // [R] Replica._originalDisk (-1 = null)
   const uint8_t* rSel;     // [R] selectOnlineReplicas && selectReplicasBasedOnExcludedTopics
+  const IntraRep* rStat;   // [R] rDu / rScore / rTie / rOrigDisk packed (device; the emulation reads the arrays)
   // entry-indexed copies of the replica fields the program reads per entry (filled by intra_sort / the emulation
   // once per launch): a broker's entries are one contiguous range, so its snapshots and candidate checks read a few
   // lines instead of one 128-B replica-table line per entry per pass

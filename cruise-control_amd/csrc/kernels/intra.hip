@@ -35,12 +35,11 @@ __global__ __launch_bounds__(64) void intra_sort(IntraArgs A) {
   for (int i = lane; i < n; i += 64) {
     const int r = A.eRep[e0 + i];
     const bool sel = A.rSel[r] != 0;
-    const float sc = A.rScore[r];
-    const int32_t tie = A.rTie[r];
-    A.eDu[e0 + i] = A.rDu[r];
-    A.eOrig[e0 + i] = A.rOrigDisk[r];
-    A.eKeyRev[e0 + i] = sel ? intraSortKey(sc, tie, true) : ~0ull;
-    A.eKeyFwd[e0 + i] = sel ? intraSortKey(sc, tie, false) : ~0ull;
+    const IntraRep x = A.rStat[r];
+    A.eDu[e0 + i] = x.du;
+    A.eOrig[e0 + i] = x.origDisk;
+    A.eKeyRev[e0 + i] = sel ? intraSortKey(x.score, x.tie, true) : ~0ull;
+    A.eKeyFwd[e0 + i] = sel ? intraSortKey(x.score, x.tie, false) : ~0ull;
     selCount += __popcll(__ballot(sel));
   }
   __syncthreads();  // this wavefront's own stores (one wavefront per workgroup) before its loads below

@@ -1596,37 +1596,122 @@ struct DevApply {
 };
 
 
-// Apply one move with the whole workgroup (apply.h lanes on threads 0..5, one step at a time); every thread calls it.
+// The finish fields of a move (apply.h finish lanes) spread over waves 1..3 — a wave runs only lanes that take the same
+// code path (the source and destination sides by address), so no wave serializes divergent paths of loads:
+//   wave 1 lanes 0/1: broker counts of src / dst; lanes 2/3: topic leader counts of src / dst
+//   wave 2 lane 0: Partition slots (and leader);   wave 3 lane 0: the partition record
+template <class S>
+__device__ __forceinline__ void leadershipFinishWaves(S& s, int t, int p, int dr, int dpos, int src, int dst) {
+  const int w = t >> 6, l = t & 63;
+  if (w == 1 && l < 2) s.brk(l == 0 ? src : dst).nlead += l == 0 ? -1 : 1;
+  else if (w == 1 && l < 4) s.topicLeadAdd(s.part(p).topic, l == 2 ? src : dst, l == 2 ? -1 : 1);
+  else if (w == 2 && l == 0) applyLeadershipFinishLane(s, 2, p, dr, dpos, src, dst);
+  else if (w == 3 && l == 0) applyLeadershipFinishLane(s, 3, p, dr, dpos, src, dst);
+}
+template <class S>
+__device__ __forceinline__ void replicaFinishWaves(S& s, int t, int r, int p, int src, int dst, bool lead) {
+  const int w = t >> 6, l = t & 63;
+  if (w == 1 && l < 2) {
+    BrokerRec& b = s.brk(l == 0 ? src : dst);
+    b.nrep += l == 0 ? -1 : 1;
+    if (lead) b.nlead += l == 0 ? -1 : 1;
+  } else if (w == 1 && l < 4) {
+    s.topicAdd(s.part(p).topic, l == 2 ? src : dst, l == 2 ? -1 : 1);
+  } else if (w == 1 && l < 6) {
+    if (lead) s.topicLeadAdd(s.part(p).topic, l == 4 ? src : dst, l == 4 ? -1 : 1);
+  } else if (w == 2 && l == 0) {
+    applyReplicaFinishLane(s, 2, r, p, src, dst, lead);  // the replica's broker
+  } else if (w == 3 && l == 0) {
+    applyReplicaFinishLane(s, 3, r, p, src, dst, lead);  // its partition slot
+  }
+}
+
+// Apply one move with the whole workgroup; every thread calls it. Replica move: the apply.h lanes on threads 0..5
+// (broker, potential and leadership-NW loads) and the host lanes on 6..7, one step; then the finish lanes (counts,
+// replica, partition slots, topic counts) in parallel, with the host utilizations. Leadership: every aggregate of the
+// move has its own lane, which loads it into registers at the first step (one memory round trip for all of them):
+//   lane 0 leadership NW load of src (-= sr's old load)        lane 1 sr's load (makeFollower -> delta, new load)
+//   lane 2 Broker.load() of src (-= delta)                     lane 3 Broker.load() of dst (+= delta)
+//   lane 4 dr's load (+= delta, -> scratch for lane 5)         lane 5 leadership NW load of dst (+= dr's new load)
+//   lanes 6, 7 the hosts (Host.makeFollower / makeLeader)
+// the same operations on the same values, in the order apply.h's sequential form (the emulation) runs them.
 template <int WC>
 __device__ void chainApply(const ChainTables& C, LoadVec* sc, int action, int r, int dst) {
   DevApply<WC> S{C, sc};
   const ReplicaRec rr = C.replicas[r];
   const int src = rr.broker, p = rr.part;
   const int t = threadIdx.x;
+  constexpr int W = WC;
   if (action == DA_LEADERSHIP) {
     int sr, dr, dpos;
     leadershipReplicas(S, p, src, dst, sr, dr, dpos);
-    for (int st = 0; st < kLeadershipSteps; ++st) {
-      if (t < 4) applyLeadershipLane(S, st, t, sr, dr, src, dst);
-      else if (st == 1 && t < 4 + kHostLanes) applyHostLeadershipLane(S, t - 4, src, dst);
-      chainSync();
+    // lane -> its aggregate, chosen by address (one load / store instruction stream for all lanes, no divergence)
+    const bool hosts = S.hostsOn();
+    const int hs = hosts ? S.host(src) : 0, hd = hosts ? S.host(dst) : 0;
+    const bool hostLane = t >= 6 && t < 6 + kHostLanes && hosts && !(t == 7 && hs == hd);
+    const bool active = t < 6 || hostLane;
+    LoadVec* agg = t == 0   ? &S.bLnw(src)
+                   : t == 1 ? &S.rLoad(sr)
+                   : t == 2 ? &S.bLoad(src)
+                   : t == 3 ? &S.bLoad(dst)
+                   : t == 4 ? &S.rLoad(dr)
+                   : t == 5 ? &S.bLnw(dst)
+                            : (hosts ? &S.hLoad(t == 6 ? hs : hd) : &S.bLnw(src));
+    LoadVec x, o;
+    // step 0: every lane's aggregate into registers (lane 0 also sr's load); lanes 0 and 1 compute
+    if (active) ldCopy(x, *agg, W);
+    if (t == 0) ldCopy(o, S.rLoad(sr), W);
+    if (t == 0) {
+      ldAddSignedAll(x, o, W, true);
+      ldCopy(*agg, x, W);
+      S.brk(src).lbi = ldUtil(x, R_NW_IN, W);
+    } else if (t == 1) {
+      ldMakeFollower(x, o, W);
+      ldCopy(S.scratch(0), o, W);  // delta
     }
-    if (S.hostsOn()) {  // (block-uniform) every broker of the touched hosts reads its host utilization again
-      applyHostUtil(S, src, dst, t, (int)blockDim.x);
-      chainSync();
+    chainSync();
+    // step 1: the delta everywhere it goes (lanes 2, 3, 4 and the hosts: one add or subtract each)
+    const bool takesDelta = (t >= 2 && t <= 4) || hostLane;
+    if (takesDelta && x.mask) {
+      ldCopy(o, S.scratch(0), W);
+      ldAddSignedAll(x, o, W, t == 2 || t == 6);
+      if (t == 6 && hs == hd) ldAddSignedAll(x, o, W, false);  // Host.makeFollower then makeLeader on one host
     }
-    if (t == 0) applyLeadershipFinish(S, p, dr, dpos, src, dst);
+    if (active && t >= 1 && t != 5) ldCopy(*agg, x, W);  // lane 1: sr's new load (makeFollower's result)
+    if (t == 1 || t == 4) {
+      ReplicaRec& rec = S.rep(t == 1 ? sr : dr);
+      if (t == 1) rec.flags &= ~(int32_t)RF_LEADER;
+      else rec.flags |= (int32_t)RF_LEADER;
+      for (int k = 0; k < 4; ++k) rec.util[k] = ldUtil(x, k, W);
+      if (t == 4) ldCopy(S.scratch(1), x, W);  // dr's new load, for lane 5
+    } else if (t == 2 || t == 3) {
+      BrokerRec& rec = S.brk(t == 2 ? src : dst);
+      for (int k = 0; k < 4; ++k) rec.util[k] = ldUtil(x, k, W);
+      if (!hosts)
+        for (int k = 0; k < 3; ++k) rec.hutil[k] = rec.util[k];
+    }
+    chainSync();
+    // step 2: dst's leadership NW load; the finish lanes (another wave); the host utilizations
+    if (t == 5) {
+      ldCopy(o, S.scratch(1), W);
+      ldAddSignedAll(x, o, W, false);
+      ldCopy(*agg, x, W);
+      S.brk(dst).lbi = ldUtil(x, R_NW_IN, W);
+    } else {
+      leadershipFinishWaves(S, t, p, dr, dpos, src, dst);
+    }
+    if (hosts) applyHostUtil(S, src, dst, t, (int)blockDim.x);
   } else {
     const bool lead = (rr.flags & RF_LEADER) != 0;
     const int lr = C.pLeader[p];
     if (t < kReplicaLanes) applyReplicaLane(S, t, r, src, dst, lr, lead);
     else if (t < kReplicaLanes + kHostLanes) applyHostReplicaLane(S, t - kReplicaLanes, r, src, dst);
-    chainSync();
+    else
+      replicaFinishWaves(S, t, r, p, src, dst, lead);  // independent of the load lanes (counts, slots, topic counts)
     if (S.hostsOn()) {
-      applyHostUtil(S, src, dst, t, (int)blockDim.x);
       chainSync();
+      applyHostUtil(S, src, dst, t, (int)blockDim.x);
     }
-    if (t == 0) applyReplicaFinish(S, r, src, dst, lead);
   }
   chainSync();
 }
