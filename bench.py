@@ -527,6 +527,10 @@ def main() -> None:
                      "stats_avg_launch_us": perf.stats_kernel_ms * 1e3 / max(1, perf.stats_launches),
                      "stats_bytes_per_launch": perf.stats_bytes / max(1, perf.stats_launches),
                      "host_syncs_per_step": perf.host_syncs,
+                     "intra_sort": None if not intra else {
+                         "launches_per_step": perf.intra_sort_launches,
+                         "avg_launch_us": perf.intra_sort_ms * 1e3 / max(1, perf.intra_sort_launches),
+                         "note": "K6's per-call entry sort, timed apart from intra_brokers (HIP events)"},
                      "scan_cross": scan_cross_line(launch_perf or perf, args.workload),
                      "launch_path": None if launch_perf is None else {
                          "scan_launches": launch_perf.scan_launches,

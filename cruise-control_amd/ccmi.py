@@ -182,7 +182,8 @@ class PerfStruct(C.Structure):
                 ("combines", C.c_int64), ("server_launches", C.c_int64), ("server_scans", C.c_int64),
                 ("server_required", C.c_int64), ("server_busy_ms", C.c_double),
                 ("server_payload_bytes", C.c_int64), ("server_chains", C.c_int64),
-                ("server_idle_exits", C.c_int64), ("server_resident_ms", C.c_double)]
+                ("server_idle_exits", C.c_int64), ("server_resident_ms", C.c_double),
+                ("intra_sort_launches", C.c_int64), ("intra_sort_ms", C.c_double)]
 
 
 # ----------------------------------------------------------------------------------------------- errors
@@ -213,7 +214,7 @@ class DeviceError(CruiseControlError):
 _STATUS = {1: IllegalArgumentException, 2: DeviceError, 3: OptimizationFailureException, 4: IllegalStateException,
            5: UnsupportedOperationException}
 
-ABI_VERSION = 9  # CCMI_ABI_VERSION of include/ccmi.h
+ABI_VERSION = 10  # CCMI_ABI_VERSION of include/ccmi.h
 EXPORTED_SYMBOLS = (
     "ccmi_last_error", "ccmi_abi_version", "ccmi_device_count", "ccmi_default_constraint", "ccmi_default_random_cluster_props",
     "ccmi_random_cluster", "ccmi_cluster_buffers_desc", "ccmi_cluster_buffers_free", "ccmi_session_create",

@@ -714,6 +714,8 @@ ccmi_status ccmi_perf(const ccmi_session* s, ccmi_perf_counters* out) {
     out->chain_launches = p.chainLaunches;
     out->intra_launches = p.intraLaunches;
     out->intra_kernel_ms = p.intraKernelMs;
+    out->intra_sort_launches = p.intraSorts;
+    out->intra_sort_ms = p.intraSortMs;
     out->intra_bytes = p.intraBytes;
     out->cross_launches = p.crossLaunches;
     out->cross_required = p.crossRequired;

@@ -27,6 +27,7 @@ namespace ccmi {
 #define ST ((hipStream_t)st_)
 #define EV0 ((hipEvent_t)ev0_)
 #define EV1 ((hipEvent_t)ev1_)
+#define EV2 ((hipEvent_t)ev2_)
 
 hipError_t launchScanCross(const DevTables& T, const MutTables& M, const UpdateList& U, const DevProgram& prog,
                            const RowRef* reps, const int32_t* cands, int K, int Nr, int N, int c0,
@@ -151,11 +152,12 @@ Device::Device(int ordinal, int B, int R, int P, int T, int maxGoalSlots)
   ensureStage(1 << 20);
   ensureReq(1 << 20);
   if (std::getenv("CCMI_STAMPS")) {
-    dalloc(&stamps_, 1024 * 8 + 32);  // + the scan server's phase sums at [8192, 8224)
-    hipCheck(hipMemset(stamps_, 0, (1024 * 8 + 32) * sizeof(unsigned long long)), "hipMemset");
+    dalloc(&stamps_, 1024 * 8 + 64);  // + the scan server's phase sums at [8192, 8256)
+    hipCheck(hipMemset(stamps_, 0, (1024 * 8 + 64) * sizeof(unsigned long long)), "hipMemset");
   }
   hipCheck(hipEventCreate((hipEvent_t*)&ev0_), "hipEventCreate");
   hipCheck(hipEventCreate((hipEvent_t*)&ev1_), "hipEventCreate");
+  hipCheck(hipEventCreate((hipEvent_t*)&ev2_), "hipEventCreate");
   hipCheck(hipEventCreate((hipEvent_t*)&evS0_), "hipEventCreate");
   hipCheck(hipEventCreate((hipEvent_t*)&evS1_), "hipEventCreate");
   {  // scan server: on unless CCMI_SERVER=0; CCMI_SERVER_BLOCKS sets its workgroups (multiple of 8, <= 512)
@@ -168,6 +170,7 @@ Device::Device(int ordinal, int B, int R, int P, int T, int maxGoalSlots)
     if (const char* gs = std::getenv("CCMI_GOAL_SPLIT")) goalSplitMax_ = (int)std::strtol(gs, nullptr, 10);
     if (const char* sa = std::getenv("CCMI_SERVER_APPLY")) applyViaServer_ = sa[0] != '0';
     if (const char* gw = std::getenv("CCMI_GOAL_SPLIT_WGS")) goalSplitWgs_ = (int)std::strtol(gw, nullptr, 10);
+    if (const char* sw = std::getenv("CCMI_SCAN_WIDTH")) adaptiveWidth_ = std::strcmp(sw, "adaptive") == 0;
     if (serverBlocks_ < 8) serverUsable_ = false;
     if (serverUsable_) {
       dalloc(&dServerT0_, 16);  // [0] busy-time stamp, [8] the doorbell (a line of its own)
@@ -192,7 +195,7 @@ Device::~Device() {
   }
   if (ST) (void)hipStreamSynchronize(ST);
   if (stamps_) {  // average in-launch phase times of the last 1024 cross/pair scans (workgroup 0)
-    std::vector<unsigned long long> h(1024 * 8 + 32);
+    std::vector<unsigned long long> h(1024 * 8 + 64);
     if (hipMemcpy(h.data(), stamps_, h.size() * 8, hipMemcpyDeviceToHost) == hipSuccess) {
       if (h[8192])
         std::fprintf(stderr, "[ccmi server stamps] %llu scan commands: copy+acquire %.2f us, stage %.2f us, first tile "
@@ -208,6 +211,12 @@ Device::~Device() {
                              "first tile %.2f us, rest to arrival %.2f us, %.2f tiles (workgroup 0)\n",
                      h[8210], h[8211] * 0.01 / h[8210], h[8212] * 0.01 / h[8210], h[8213] * 0.01 / h[8210],
                      h[8214] * 0.01 / h[8210], (double)h[8215] / h[8210]);
+      {
+        static const char* ops[6] = {"cross", "pairs", "-", "segs", "-", "queue"};
+        for (int o = 0; o < 6; ++o)
+          if (h[8220 + o])
+            std::fprintf(stderr, "[ccmi evaluated] %s: %llu pairs evaluated by the server's tiles\n", ops[o], h[8220 + o]);
+      }
       if (h[8200])
         std::fprintf(stderr, "[ccmi chain stamps] %llu chain_pairs launches, %llu accepts: %.2f us per launch in "
                              "evaluation, %.2f us applying, %.2f us in total (thread 0)\n",
@@ -249,6 +258,7 @@ Device::~Device() {
   if (hResult_) (void)hipHostFree(hResult_);
   if (ev0_) (void)hipEventDestroy(EV0);
   if (ev1_) (void)hipEventDestroy(EV1);
+  if (ev2_) (void)hipEventDestroy(EV2);
   if (evS0_) (void)hipEventDestroy((hipEvent_t)evS0_);
   if (evS1_) (void)hipEventDestroy((hipEvent_t)evS1_);
   if (ST) (void)hipStreamDestroy(ST);
@@ -494,8 +504,24 @@ int64_t Device::serverRun(const DevProgram& prog, const Staged& g, int op, const
     c.keyBase = params[1];
   }
   c.progVer = ver;
+  // the scan's site (op, action, goal count, filter: one driver loop of one goal) for its speculative width; sliced
+  // scans split columns over the XCDs and keep the full width
+  const bool sliced = op != SOP_PAIRS && params[4] != 0;
+  const uint64_t site = (uint64_t)op | ((uint64_t)(uint32_t)prog.action << 3) | ((uint64_t)(uint32_t)prog.nGoals << 8) |
+                        ((uint64_t)(uint32_t)prog.filter << 16) | ((uint64_t)sliced << 24);
   {  // every tile of the first sweep gets its own workgroup; a smaller scan leaves the others out of the command
-    const uint64_t total = op == SOP_PAIRS ? (uint64_t)params[0] : (uint64_t)params[0] * (uint64_t)params[1];
+    uint64_t total = op == SOP_PAIRS ? (uint64_t)params[0] : (uint64_t)params[0] * (uint64_t)params[1];
+    if (adaptiveWidth_) {
+      // Speculative width: the first sweep covers twice the depth of this site's last winner (plus eight tiles), or
+      // everything after a scan without one. Tiles past the winner are evaluated for nothing (their reads are the
+      // excess HBM traffic of first-fit scans); a winner beyond the sweep is found by the strided next sweeps, so
+      // the first fit is the same either way. A column-sliced scan (every XCD sweeps its own columns of each row)
+      // counts its depth in rows: the first sweep covers twice the winner's row plus one of every slice.
+      const auto it = lastDepth_.find(site);
+      if (it != lastDepth_.end() && it->second >= 0)
+        total = std::min<uint64_t>(total, sliced ? (2 * (uint64_t)it->second + 1) * (uint64_t)params[1]
+                                                 : 2 * (uint64_t)it->second + 8 * 256);
+    }
     auto wgsFor = [&](int parts) {
       const uint64_t tile = 256 / (uint64_t)parts;
       const uint64_t need = (total + tile - 1) / tile;
@@ -527,7 +553,16 @@ int64_t Device::serverRun(const DevProgram& prog, const Staged& g, int op, const
   if (!postCommand(c, (g.nb | g.nr | g.np | g.nt) != 0)) return INT64_MIN;
   perf.serverScans++;
   const unsigned long long lo = hResult_[0] & 0xffffffffull;
-  return lo == 0 ? -1 : (int64_t)(lo - 1);
+  const int64_t key = lo == 0 ? -1 : (int64_t)(lo - 1);
+  if (adaptiveWidth_) {  // the winner's position in the first-sweep order (sliced: its row; -1: none)
+    int64_t depth = -1;
+    if (key >= 0)
+      depth = op == SOP_PAIRS ? key - params[1]
+              : sliced        ? key / params[2]
+                              : (key / params[2]) * params[1] + (key % params[2] - params[3]);
+    lastDepth_[site] = depth;
+  }
+  return key;
 }
 
 // A K7 chain as a server command (SOP_CHAIN): payload [program | rows | load rows | slot rows | request]. false: the
@@ -1000,6 +1035,7 @@ int64_t Device::scanCross(const DevProgram& prog, const int32_t* reps, int K, co
         perf.scanRequired += required;
         perf.serverRequired += required;
         perf.crossRequired += required;
+        prof().count(24, "req.cross", required);
         return key;
       }
     }
@@ -1092,6 +1128,7 @@ int64_t Device::scanPairs(const DevProgram& prog, const int32_t* pr, const int32
         const int64_t required = key < 0 ? (int64_t)n : key - p0 + 1;
         perf.scanRequired += required;
         perf.serverRequired += required;
+        prof().count(25, "req.pairs", required);
         return key;
       }
     }
@@ -1210,7 +1247,10 @@ int64_t Device::scanQueue(const DevProgram& prog, int head, int skip0, const int
         // one wave per candidate (a tile of kBlock slots): the queue is usually hundreds of brokers deep, so the scan
         // is a few sweeps of every workgroup and the sweeps, not a single tile's conjunction, are its latency
         c.goalParts = 1;
-        c.nActive = std::min(serverBlocks_, std::max(8, (n + 7) / 8 * 8));
+        // (adaptive width: as serverRun, the workgroups of the first sweep sized from the last queue winner's entry)
+        int want = n;
+        if (adaptiveWidth_ && lastQueueDepth_ >= 0) want = std::min<int64_t>(n, 2 * lastQueueDepth_ + 8);
+        c.nActive = std::min(serverBlocks_, std::max(8, (want + 7) / 8 * 8));
         c.nb = g.nb;
         c.nr = g.nr;
         c.np = g.np;
@@ -1228,6 +1268,7 @@ int64_t Device::scanQueue(const DevProgram& prog, int head, int skip0, const int
           perf.serverScans++;
           const unsigned long long lo = hResult_[0] & 0xffffffffull;
           const int64_t key = lo == 0 ? -1 : (int64_t)(lo - 1);
+          lastQueueDepth_ = key < 0 ? -1 : key / N / span;
           if (prof().on) {  // CCMI_PROFILE: queue commands' round trips and depths
             prof().count(21, "queue.wait.ns",
                          (int64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - tq)
@@ -1250,6 +1291,7 @@ int64_t Device::scanQueue(const DevProgram& prog, int head, int skip0, const int
           perf.scanRequired += required;
           perf.serverRequired += required;
           perf.crossRequired += required;
+          prof().count(27, "req.queue", required);
           return key;
         }
       }
@@ -1312,6 +1354,7 @@ int64_t Device::scanSegs(const DevProgram& prog, const std::vector<SegIn>& segs,
         perf.scanRequired += required;
         perf.serverRequired += required;
         perf.crossRequired += required;
+        prof().count(26, "req.segs", required);
         return key;
       }
     }
@@ -1785,9 +1828,13 @@ void Device::intraRun(const IntraRequest& q, IntraResult& out) {
   auto launch = [&](const IntraArgs& a) {
     hipCheck(hipMemcpyAsync(dLogOff_, logOff.data(), sizeof(int64_t) * B_, hipMemcpyHostToDevice, ST), "logOff");
     hipCheck(hipMemcpyAsync(dLogCap_, cap.data(), sizeof(int32_t) * B_, hipMemcpyHostToDevice, ST), "logCap");
-    if (timing) hipCheck(hipEventRecord(EV0, ST), "event");
-    if (!sorted) hipCheck(launchIntraSort(a, ST), "intra_sort");
+    // kernel timing: intra_sort (once per call) and intra_brokers bracketed separately, so the K6 headline is
+    // intra_brokers alone (the kernel its algorithmic bytes count; rocprofv3 reports the two apart)
+    const bool sortNow = !sorted;
+    if (timing) hipCheck(hipEventRecord(EV2, ST), "event");
+    if (sortNow) hipCheck(launchIntraSort(a, ST), "intra_sort");
     sorted = true;
+    if (timing) hipCheck(hipEventRecord(EV0, ST), "event");
     hipCheck(launchIntra(a, ST), "intra_brokers");
     if (timing) hipCheck(hipEventRecord(EV1, ST), "event");
     out.status.resize(B_);
@@ -1799,6 +1846,11 @@ void Device::intraRun(const IntraRequest& q, IntraResult& out) {
       float ms = 0.f;
       hipCheck(hipEventElapsedTime(&ms, EV0, EV1), "hipEventElapsedTime");
       msTotal += ms;
+      if (sortNow) {
+        hipCheck(hipEventElapsedTime(&ms, EV2, EV0), "hipEventElapsedTime");
+        perf.intraSortMs += ms;
+        perf.intraSorts++;
+      }
     }
   };
   launch(A);

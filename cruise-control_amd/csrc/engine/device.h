@@ -43,7 +43,9 @@ struct DevicePerf {
   int64_t chainLaunches = 0; // K7 chains (several decisions per launch)
   int64_t scanRequired = 0;  // candidates the launches had to evaluate: each first-fit list up to its winner
   int64_t intraLaunches = 0;  // K6 intra-broker launches
-  double intraKernelMs = 0;
+  double intraKernelMs = 0;  // intra_brokers launches (HIP events, kernel timing on)
+  double intraSortMs = 0;    // intra_sort launches (one per K6 call)
+  int64_t intraSorts = 0;
   int64_t intraBytes = 0;     // algorithmic bytes of K6 (per broker record + per replica entry)
   int64_t combines = 0;       // shard-combiner calls (MIN allreduce of a scan's first-fit key)
   int64_t crossLaunches = 0;  // the scan_cross share of the scan counters
@@ -262,7 +264,7 @@ class Device {
   unsigned long long* hResultDev_ = nullptr;
   unsigned long long seq_ = 0;
   alignas(16) unsigned char statsHost_[sizeof(StatsOut)];
-  void *ev0_ = nullptr, *ev1_ = nullptr;  // hipEvent_t
+  void *ev0_ = nullptr, *ev1_ = nullptr, *ev2_ = nullptr;  // hipEvent_t
   bool serverTimed_ = false;  // the running server launch has its start event recorded
   void *evS0_ = nullptr, *evS1_ = nullptr;  // hipEvent_t: a scan-server launch's residency (kernel timing on)
   struct Staged {
@@ -295,6 +297,10 @@ class Device {
   int goalSplitMax_ = 4;
   bool applyViaServer_ = true;  // packForServer
   int goalSplitWgs_ = 256;
+  // CCMI_SCAN_WIDTH=adaptive: a server scan's first sweep sized from its site's last winner depth (serverRun)
+  bool adaptiveWidth_ = false;
+  std::unordered_map<uint64_t, int64_t> lastDepth_;
+  int64_t lastQueueDepth_ = -1;  // the last queue scan winner's entry (-1: none)
   int progVer_ = 0;
   bool progSent_ = false;
   DevProgram lastProg_{};

@@ -1200,6 +1200,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, kServ
           SRV_STAMP(T, 3);
           firstTile = false;
         }
+        if (T.stamps && threadIdx.x == 0)  // CCMI_STAMPS: pairs evaluated per op ([8220 + op])
+          atomicAdd(&T.stamps[8220 + c.op], (unsigned long long)min(tile, total - base));
         if (f >= 0) {  // keys grow with q inside a workgroup's range (row-major over its columns)
           if (threadIdx.x == 0) {
             const uint32_t qf = base + (uint32_t)f, kf = qf / Ws;
@@ -1328,6 +1330,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, kServ
             firstTile = false;
           }
           ++qTiles;
+          if (T.stamps && threadIdx.x == 0)
+            atomicAdd(&T.stamps[8220 + SOP_QUEUE], (unsigned long long)min(tile, total - base));
           if (f >= 0) {
             if (threadIdx.x == (unsigned)(f % 64) + (unsigned)((f / 64) * parts * 64)) atomicMin(result, keyOf(k, v));
             found = true;
@@ -1365,6 +1369,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, kServ
           SRV_STAMP(T, 3);
           firstTile = false;
         }
+        if (T.stamps && threadIdx.x == 0)
+          atomicAdd(&T.stamps[8220 + SOP_PAIRS], (unsigned long long)min(tile, n - base));
         if (f >= 0) {
           if (threadIdx.x == 0) atomicMin(result, (unsigned long long)(keyBase + base + f));
           break;

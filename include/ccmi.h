@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define CCMI_ABI_VERSION 9
+#define CCMI_ABI_VERSION 10
 
 typedef enum ccmi_status {
   CCMI_OK = 0,
@@ -503,7 +503,7 @@ typedef struct ccmi_perf_counters {
                                   cannot be accepted, e.g. non-legit leadership rows) */
   int64_t chain_launches;      /* K7 chain launches (several decisions applied on the device per launch) */
   int64_t intra_launches;      /* K6 intra-broker launches (one per intra-broker goal, plus overflow re-runs) */
-  double intra_kernel_ms;      /* HIP-event duration of the K6 launches */
+  double intra_kernel_ms;      /* HIP-event duration of the K6 intra_brokers launches */
   int64_t intra_bytes;         /* algorithmic bytes of K6 */
   int64_t cross_launches;      /* the scan_cross share of scan_launches / scan_required / scan_kernel_ms (the kernel */
   int64_t cross_required;      /* tools/pmc_summary.py prices against its own FETCH_SIZE / WRITE_SIZE counters) */
@@ -525,6 +525,10 @@ typedef struct ccmi_perf_counters {
   /* ABI v9: HIP-event time from each scan-server launch to its exit, summed (with ccmi_set_kernel_timing on): the
    * residency a rocprofv3 kernel trace reports for scan_server, idle polling included */
   double server_resident_ms;
+  /* ABI v10: K6's per-call sort (intra_sort, one launch per intra-broker call) timed apart from intra_brokers, whose
+   * HIP-event time intra_kernel_ms now holds alone */
+  int64_t intra_sort_launches;
+  double intra_sort_ms;
 } ccmi_perf_counters;
 ccmi_status ccmi_perf(const ccmi_session* s, ccmi_perf_counters* out);
 void ccmi_perf_reset(ccmi_session* s);

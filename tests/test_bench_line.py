@@ -3,6 +3,8 @@ import json
 import os
 import sys
 
+import pytest
+
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)
 
@@ -35,3 +37,46 @@ def test_server_traffic_uses_the_profiled_runs_commands_per_launch():
 def test_scan_traffic_summary_is_committed():
     traffic, src = bench.pmc_traffic("c2")
     assert traffic and traffic > 0 and src.startswith("profiles/")
+
+
+def _profiled_runs(workload):
+    """(round dir, tag) of every committed rocprofv3 run of `workload`: its bench line <workload>_bench_prof_<tag>.json
+    next to the kernel-trace stats of the same command, <workload>_kernel_stats_<tag>.csv."""
+    import glob
+    runs = []
+    for line in sorted(glob.glob(os.path.join(REPO, "profiles", "r*", f"{workload}_bench_prof_*.json"))):
+        tag = os.path.basename(line)[len(f"{workload}_bench_prof_"):-len(".json")]
+        csv = os.path.join(os.path.dirname(line), f"{workload}_kernel_stats_{tag}.csv")
+        if os.path.exists(csv):
+            runs.append((line, csv))
+    return runs
+
+
+def _avg_ns(csv_path, kernel):
+    import csv
+    with open(csv_path) as f:
+        rows = [r for r in csv.DictReader(f) if r["Name"].split("(")[0] == f"ccmi::{kernel}"]
+    assert len(rows) == 1, (csv_path, kernel)
+    return float(rows[0]["AverageNs"]), int(rows[0]["Calls"])
+
+
+@pytest.mark.parametrize("workload,kernel", [("c2", "scan_server"), ("c4", "intra_brokers")])
+def test_headline_frac_follows_committed_kernel_stats(workload, kernel):
+    """The bench line's headline roofline.frac = algorithmic bytes per launch of the dominant kernel over its average
+    launch duration / peak; the same figure recomputed from the rocprofv3 kernel-trace average of the same command
+    (committed beside the line) agrees within 10 %."""
+    runs = _profiled_runs(workload)
+    assert runs, f"no committed {workload} bench line + kernel stats pair under profiles/"
+    line_path, csv_path = runs[-1]
+    with open(line_path) as f:
+        r = json.loads(f.read().strip().splitlines()[-1])["roofline"]
+    avg_ns, calls = _avg_ns(csv_path, kernel)
+    assert calls > 0
+    alg = r["algorithmic_bytes_per_launch"]
+    frac = alg / (avg_ns * 1e-9) / 1e9 / r["peak"]
+    assert abs(frac - r["frac"]) <= 0.10 * r["frac"], (line_path, frac, r["frac"])
+    assert abs(r["avg_launch_us"] * 1e3 - avg_ns) <= 0.10 * avg_ns
+    assert r["frac"] == pytest.approx(r["achieved"] / r["peak"])
+    if kernel == "scan_server":  # the headline is the launch (residency) view, the per-command one secondary
+        assert r["resident"]["frac"] == pytest.approx(r["frac"])
+        assert r["per_command"]["frac"] > r["frac"]
