@@ -170,7 +170,7 @@ Device::Device(int ordinal, int B, int R, int P, int T, int maxGoalSlots)
     if (const char* gs = std::getenv("CCMI_GOAL_SPLIT")) goalSplitMax_ = (int)std::strtol(gs, nullptr, 10);
     if (const char* sa = std::getenv("CCMI_SERVER_APPLY")) applyViaServer_ = sa[0] != '0';
     if (const char* gw = std::getenv("CCMI_GOAL_SPLIT_WGS")) goalSplitWgs_ = (int)std::strtol(gw, nullptr, 10);
-    if (const char* sw = std::getenv("CCMI_SCAN_WIDTH")) adaptiveWidth_ = std::strcmp(sw, "adaptive") == 0;
+    if (const char* sw = std::getenv("CCMI_SCAN_WIDTH")) adaptiveWidth_ = std::strcmp(sw, "full") != 0;
     if (serverBlocks_ < 8) serverUsable_ = false;
     if (serverUsable_) {
       dalloc(&dServerT0_, 16);  // [0] busy-time stamp, [8] the doorbell (a line of its own)
@@ -217,6 +217,11 @@ Device::~Device() {
           if (h[8220 + o])
             std::fprintf(stderr, "[ccmi evaluated] %s: %llu pairs evaluated by the server's tiles\n", ops[o], h[8220 + o]);
       }
+      if (h[8230])
+        std::fprintf(stderr, "[ccmi chain command stamps] %llu chain commands: seen -> chain start %.2f us (ready -> "
+                             "start %.2f us), chain %.2f us, release %.2f us (workgroup 0)\n",
+                     h[8230], h[8234] * 0.01 / h[8230], h[8231] * 0.01 / h[8230], h[8232] * 0.01 / h[8230],
+                     h[8233] * 0.01 / h[8230]);
       if (h[8200])
         std::fprintf(stderr, "[ccmi chain stamps] %llu chain_pairs launches, %llu accepts: %.2f us per launch in "
                              "evaluation, %.2f us applying, %.2f us in total (thread 0)\n",
@@ -1247,10 +1252,10 @@ int64_t Device::scanQueue(const DevProgram& prog, int head, int skip0, const int
         // one wave per candidate (a tile of kBlock slots): the queue is usually hundreds of brokers deep, so the scan
         // is a few sweeps of every workgroup and the sweeps, not a single tile's conjunction, are its latency
         c.goalParts = 1;
-        // (adaptive width: as serverRun, the workgroups of the first sweep sized from the last queue winner's entry)
-        int want = n;
-        if (adaptiveWidth_ && lastQueueDepth_ >= 0) want = std::min<int64_t>(n, 2 * lastQueueDepth_ + 8);
-        c.nActive = std::min(serverBlocks_, std::max(8, (want + 7) / 8 * 8));
+        // (no adaptive width here: queue winners' depths vary too much from one command to the next — sized from the
+        // deepest of the last 8 winners, the extra sweeps cost 26 us per queue command on C2 against 0.25 GB less
+        // traffic, profiles/r05/README.md)
+        c.nActive = std::min(serverBlocks_, std::max(8, (n + 7) / 8 * 8));
         c.nb = g.nb;
         c.nr = g.nr;
         c.np = g.np;
@@ -1268,7 +1273,6 @@ int64_t Device::scanQueue(const DevProgram& prog, int head, int skip0, const int
           perf.serverScans++;
           const unsigned long long lo = hResult_[0] & 0xffffffffull;
           const int64_t key = lo == 0 ? -1 : (int64_t)(lo - 1);
-          lastQueueDepth_ = key < 0 ? -1 : key / N / span;
           if (prof().on) {  // CCMI_PROFILE: queue commands' round trips and depths
             prof().count(21, "queue.wait.ns",
                          (int64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - tq)

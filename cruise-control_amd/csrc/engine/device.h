@@ -297,10 +297,9 @@ class Device {
   int goalSplitMax_ = 4;
   bool applyViaServer_ = true;  // packForServer
   int goalSplitWgs_ = 256;
-  // CCMI_SCAN_WIDTH=adaptive: a server scan's first sweep sized from its site's last winner depth (serverRun)
-  bool adaptiveWidth_ = false;
+  // a server scan's first sweep sized from its site's last winner depth (serverRun; CCMI_SCAN_WIDTH=full: off)
+  bool adaptiveWidth_ = true;
   std::unordered_map<uint64_t, int64_t> lastDepth_;
-  int64_t lastQueueDepth_ = -1;  // the last queue scan winner's entry (-1: none)
   int progVer_ = 0;
   bool progSent_ = false;
   DevProgram lastProg_{};

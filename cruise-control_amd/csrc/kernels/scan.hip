@@ -922,32 +922,60 @@ __device__ __attribute__((noinline)) void serverChain(const DevTables T, const C
   UpdateList U;
   U.tdel = (const TopicCountDelta*)(pay + c.oT);
   U.nt = c.nt;
-  applyRowsCoherent(Mt, ov.b, ov.nb, ov.r, ov.nr, ov.p, ov.np, threadIdx.x, blockDim.x);
-  for (int i = threadIdx.x; i < U.nt; i += blockDim.x) {
-    TopicCountDelta d;
-    copySysOneThread(&d, &U.tdel[i]);
-    atomicAdd(&(d.kind ? Mt.topicLead : Mt.topicCount)[(size_t)d.topic * Mt.ldB + d.broker], d.delta);
-  }
   const LoadRow* lrows = (const LoadRow*)(pay + c.oL);
-  for (int i = threadIdx.x; i < c.nl; i += blockDim.x) {
-    LoadRow x;
-    copySysOneThread(&x, &lrows[i]);
+  const SlotRow* srows = (const SlotRow*)(pay + c.oS);
+  int32_t* req = reinterpret_cast<int32_t*>(c.chainReq);
+  const int32_t* reqIn = reinterpret_cast<const int32_t*>(pay + c.oA);
+  const int words = c.chainMode == CM_PAIRS ? 3 * c.chainN : c.chainN + c.chainM;
+  auto putLoad = [&](const LoadRow& x) {
     LoadVec* dst = x.kind == LR_REPLICA ? C.rLoad
                    : (x.kind == LR_BROKER       ? C.bLoad
                       : (x.kind == LR_LEADERSHIP_NW ? C.bLnw : (x.kind == LR_HOST ? C.hLoad : C.bPot)));
     dst[x.id] = x.v;
-  }
-  const SlotRow* srows = (const SlotRow*)(pay + c.oS);
-  for (int i = threadIdx.x; i < c.ns; i += blockDim.x) {
-    SlotRow x;
-    copySysOneThread(&x, &srows[i]);
+  };
+  auto putSlots = [&](const SlotRow& x) {
     const int o = C.pOff[x.p], n = C.pOff[x.p + 1] - o;
     for (int k = 0; k < n; ++k) C.pSlots[o + k] = x.slots[k];
     C.pLeader[x.p] = x.leader;
+  };
+  // First pass: each thread's first topic delta, load row, slot row and request words are loaded together (one
+  // fine-grained round trip for the lot instead of one per kind), then written; the rare remainders follow.
+  {
+    const int t = (int)threadIdx.x, nt = (int)blockDim.x;
+    TopicCountDelta d;
+    LoadRow xl;
+    SlotRow xs;
+    int32_t w4[4];
+    if (t < U.nt) copySysOneThread(&d, &U.tdel[t]);
+    if (t < c.nl) copySysOneThread(&xl, &lrows[t]);
+    if (t < c.ns) copySysOneThread(&xs, &srows[t]);
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      if (t + k * nt < words) w4[k] = ldSys(reqIn + t + k * nt);
+    applyRowsCoherent(Mt, ov.b, ov.nb, ov.r, ov.nr, ov.p, ov.np, threadIdx.x, blockDim.x);
+    if (t < U.nt) atomicAdd(&(d.kind ? Mt.topicLead : Mt.topicCount)[(size_t)d.topic * Mt.ldB + d.broker], d.delta);
+    if (t < c.nl) putLoad(xl);
+    if (t < c.ns) putSlots(xs);
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      if (t + k * nt < words) req[t + k * nt] = w4[k];
   }
-  int32_t* req = reinterpret_cast<int32_t*>(c.chainReq);
-  const int words = c.chainMode == CM_PAIRS ? 3 * c.chainN : c.chainN + c.chainM;
-  for (int w = threadIdx.x; w < words; w += blockDim.x) req[w] = ldSys(reinterpret_cast<const int32_t*>(pay + c.oA) + w);
+  for (int i = threadIdx.x + blockDim.x; i < U.nt; i += blockDim.x) {
+    TopicCountDelta d;
+    copySysOneThread(&d, &U.tdel[i]);
+    atomicAdd(&(d.kind ? Mt.topicLead : Mt.topicCount)[(size_t)d.topic * Mt.ldB + d.broker], d.delta);
+  }
+  for (int i = threadIdx.x + blockDim.x; i < c.nl; i += blockDim.x) {
+    LoadRow x;
+    copySysOneThread(&x, &lrows[i]);
+    putLoad(x);
+  }
+  for (int i = threadIdx.x + blockDim.x; i < c.ns; i += blockDim.x) {
+    SlotRow x;
+    copySysOneThread(&x, &srows[i]);
+    putSlots(x);
+  }
+  for (int w = threadIdx.x + 4 * blockDim.x; w < words; w += blockDim.x) req[w] = ldSys(reqIn + w);
   if (threadIdx.x == 0) ov.nb = ov.nr = ov.np = 0;  // the tables hold the rows now
   __builtin_amdgcn_s_waitcnt(0);
   chainSync();
@@ -1123,8 +1151,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, kServ
     const int32_t* A = (const int32_t*)(pay + c.oA);
     const int32_t* C = (const int32_t*)(pay + c.oC);
     if (c.op == SOP_CHAIN) {
+      const unsigned long long tc0 = T.stamps ? __builtin_amdgcn_s_memrealtime() : 0;
       stage();
       serverChain(T, Ch, Mt, c, pay);
+      const unsigned long long tc1 = T.stamps ? __builtin_amdgcn_s_memrealtime() : 0;
       // every wave's stores complete, then one system-scope release: the records and loads for the other XCDs' next
       // acquire, the log and result for the host (MI355X_MICROARCH.md, inter-workgroup visibility)
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1132,6 +1162,15 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, kServ
       if (threadIdx.x == 0) {
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (T.stamps) {  // CCMI_STAMPS, chain commands: [8230] count, [8231] ready -> chain start (rows, request),
+                         // [8232] the chain (rows into the tables + decisions), [8233] the release
+          const unsigned long long tc2 = __builtin_amdgcn_s_memrealtime();
+          atomicAdd(&T.stamps[8230], 1ull);
+          atomicAdd(&T.stamps[8231], tc0 - srvT[2]);
+          atomicAdd(&T.stamps[8232], tc1 - tc0);
+          atomicAdd(&T.stamps[8233], tc2 - tc1);
+          atomicAdd(&T.stamps[8234], tc0 - srvT[0]);
+        }
       }
     } else if (c.op == SOP_CROSS || c.op == SOP_SEGS) {
       const bool segs = c.op == SOP_SEGS;

@@ -87,6 +87,18 @@ def test_gpu_goal_parallel_tiles_match_oracle(gpu_lib, oracle_lib, monkeypatch, 
                                  C1_GOALS, 1.05)
 
 
+@pytest.mark.parametrize("width", ["full", "adaptive"])
+def test_gpu_scan_width_matches_oracle(gpu_lib, oracle_lib, monkeypatch, width):
+    """Server scans with every tile of the first sweep on its own workgroup (CCMI_SCAN_WIDTH=full) and with the first
+    sweep sized from the site's last winner (the default): the strided later sweeps find any winner past a short first
+    sweep, so both decide exactly as the oracle."""
+    monkeypatch.setenv("CCMI_SCAN_WIDTH", width)
+    check_product_against_oracle(gpu_lib, dict(num_racks=8, num_brokers=300, num_replicas=30000, num_topics=1000),
+                                 C1_GOALS, 1.05)
+    check_product_against_oracle(gpu_lib, dict(num_racks=5, num_brokers=20, num_replicas=6000, num_topics=300),
+                                 DEFAULT_GOALS, 1.05)
+
+
 @pytest.mark.parametrize("props", [dict(), dict(num_racks=20, num_brokers=1000, num_replicas=99999, num_topics=3000),
                                    dict(num_racks=3, num_brokers=10, num_replicas=3000, num_topics=100,
                                         num_dead_brokers=2)])
