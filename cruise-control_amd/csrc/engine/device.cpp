@@ -1,6 +1,7 @@
 // Device tables, staging and launch protocol (see device.h).
 #include "device.h"
 #include "intra.h"
+#include "hostpool.h"
 #include "prof.h"
 #include "threadpin.h"
 
@@ -9,6 +10,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <atomic>
 #include <stdexcept>
 
 #include <atomic>
@@ -1211,6 +1213,69 @@ bool Device::qdirSet(int b, std::shared_ptr<const std::vector<int32_t>> v) {
   *reinterpret_cast<volatile unsigned long long*>(&qdir_[b]) = *reinterpret_cast<const unsigned long long*>(&e);
   qdirSpan_ = std::max(qdirSpan_, (int)v->size());
   qdirSnap_[b] = std::move(v);
+  return true;
+}
+
+bool Device::qdirSetMany(const std::vector<int32_t>& bs,
+                         const std::vector<std::shared_ptr<const std::vector<int32_t>>>& snaps) {
+  const int n = (int)bs.size();
+  if (!qdir_ || (int)snaps.size() != n) throw std::logic_error("qdirSetMany before qdirBind");
+  if (n < 8) {
+    for (int i = 0; i < n; ++i)
+      if (!qdirSet(bs[i], snaps[i])) return false;
+    return true;
+  }
+  auto spanOf = [](size_t k) { return (k + 7) & ~(size_t)7; };  // whole 128-byte lines, as segUpload
+  std::vector<int64_t> off(n, -1);
+  std::vector<uint8_t> fresh(n, 0);
+  auto assign = [&]() {
+    size_t need = 0;
+    for (int i = 0; i < n; ++i) {
+      const auto it = segCache_.find(snaps[i].get());
+      fresh[i] = it == segCache_.end();
+      off[i] = fresh[i] ? -1 : (int64_t)it->second.second;
+      if (fresh[i]) need += spanOf(snaps[i]->size());
+    }
+    return need;
+  };
+  for (const auto& v : snaps)
+    if (v->size() >= (1u << 20)) return false;
+  size_t need = assign();
+  if (need > segCap_) return false;
+  if (segHead_ + need > segCap_) {  // wrap first (as segUpload): the listed entries are rewritten from the pool start
+    stopServer();
+    segCache_.clear();
+    segHead_ = 0;
+    ++poolEpoch_;
+    need = assign();
+  }
+  for (int i = 0; i < n; ++i)
+    if (fresh[i]) {
+      off[i] = (int64_t)segHead_;
+      segHead_ += spanOf(snaps[i]->size());
+    }
+  std::atomic<int> stale{-1};
+  HostPool::get().parallelFor(n, [&](int i) {
+    if (!fresh[i] || snaps[i]->empty()) return;
+    for (int r : *snaps[i])
+      if (rowBroker_[r] != bs[i]) stale.store(bs[i]);
+    writeRowRefs((char*)(segPool_ + off[i]), snaps[i]->data(), snaps[i]->size());
+  });
+  if (stale.load() >= 0) throw std::logic_error("snapshot segment is not current for its broker");
+  for (int i = 0; i < n; ++i) {
+    const int b = bs[i];
+    const auto& v = snaps[i];
+    if (fresh[i]) {
+      segCache_.emplace(v.get(), std::make_pair(v, (uint32_t)off[i]));
+      perf.serverPayloadBytes += (int64_t)(v->size() * sizeof(RowRef));
+      prof().addPayload((int64_t)(v->size() * sizeof(RowRef)));
+      prof().count(14, "srv.bytes.pool", (int64_t)(v->size() * sizeof(RowRef)));
+    }
+    QueueDirEntry e{(uint32_t)off[i], (int32_t)v->size()};
+    *reinterpret_cast<volatile unsigned long long*>(&qdir_[b]) = *reinterpret_cast<const unsigned long long*>(&e);
+    qdirSpan_ = std::max(qdirSpan_, (int)v->size());
+    qdirSnap_[b] = v;
+  }
   return true;
 }
 

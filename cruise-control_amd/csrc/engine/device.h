@@ -177,6 +177,10 @@ class Device {
   uint32_t poolEpoch() const { return poolEpoch_; }
   // upload broker b's snapshot and point its directory entry at it (false: larger than the pool)
   bool qdirSet(int b, std::shared_ptr<const std::vector<int32_t>> v);
+  // qdirSet(bs[i], snaps[i]) for many brokers at once: the pool offsets are assigned here, the rows are written
+  // through the BAR on the host pool (each row's RowRef gathers its partition and topic: random reads of the model,
+  // most of a directory sync's time). false: a snapshot does not fit the pool.
+  bool qdirSetMany(const std::vector<int32_t>& bs, const std::vector<std::shared_ptr<const std::vector<int32_t>>>& snaps);
   const std::vector<int32_t>& qdirRows(int b) const { return *qdirSnap_[b]; }
   int qdirLen(int b) const { return qdirSnap_[b] ? (int)qdirSnap_[b]->size() : 0; }
   // first accepted (row, column) over the queue entries [head (if >= 0)] ++ tail[0, nTail) (entry 0 from row skip0) x

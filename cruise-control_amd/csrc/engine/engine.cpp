@@ -344,18 +344,28 @@ void Engine::queueSync(const Model::Spec& spec) {
   QueueSync& q = qsync_;
   if (q.stamp.size() != (size_t)m.B) q.stamp.assign(m.B, 0);
   bool full = !q.bound || q.key != key || dev->qdirKey() != key || q.epoch != dev->poolEpoch();
-  auto set = [&](int b) {
-    if (!dev->qdirSet(b, m.snapshot(b, spec))) throw Unsupported("a broker's snapshot exceeds the snapshot pool");
+  // the listed brokers' snapshots and their rows' upload, on the host pool (hostpool.h) when there are many
+  auto setMany = [&](const std::vector<int32_t>& bs) {
+    m.snapshotMany(spec, bs, q.snaps);
+    if (!dev->qdirSetMany(bs, q.snaps)) throw Unsupported("a broker's snapshot exceeds the snapshot pool");
+    q.snaps.clear();
   };
   for (int attempt = 0; attempt < 3; ++attempt) {
+    const auto t0 = prof().on ? std::chrono::steady_clock::now() : std::chrono::steady_clock::time_point();
+    auto ns = [&] {
+      return (int64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count();
+    };
+    q.todo.clear();
     if (full) {
       dev->qdirBind(key);
       q.bound = true;
       q.key = key;
       q.epoch = dev->poolEpoch();
       q.logPos = m.verLog.size();
-      for (int b = 0; b < m.B; ++b) set(b);
+      for (int b = 0; b < m.B; ++b) q.todo.push_back(b);
+      setMany(q.todo);
       prof().count(20, "queue.dir.full", 1);
+      if (prof().on) prof().count(28, "queue.full.ns", ns());
     } else {
       ++q.round;
       const size_t end = m.verLog.size();
@@ -363,9 +373,12 @@ void Engine::queueSync(const Model::Spec& spec) {
         const int b = m.verLog[k];
         if (q.stamp[b] == q.round) continue;
         q.stamp[b] = q.round;
-        set(b);
+        q.todo.push_back(b);
       }
+      setMany(q.todo);
       q.logPos = end;
+      prof().count(29, "queue.sync.brokers", (int64_t)q.todo.size());
+      if (prof().on) prof().count(30, "queue.inc.ns", ns());
     }
     if (q.epoch == dev->poolEpoch()) return;  // no pool wrap while setting: every entry points at live rows
     full = true;
@@ -1944,9 +1957,11 @@ class ResourceDistribution : public GoalImpl {
     int curCb = -1;
     size_t curSkip = 0;
     auto cond = [&]() { return m.bNlead[b] != m.nrep(b); };
-    // The candidate brokers' live views: the queue scans' snapshot directory when it can be kept current for `spec`
-    // (the same Spec as this goal's replica move-in), else the goal's snapshot table.
-    const bool dir = e.queueOn(*this, DA_LEADERSHIP);
+    // The candidate brokers' live views: the goal's snapshot table (host only; a view is re-derived when its broker's
+    // version changes), or with CCMI_LEAD_DIR=1 the queue scans' snapshot directory, kept current for `spec` after
+    // every accept — which uploads the changed brokers' rows each time instead of once before the next queue scan.
+    static const bool leadDir = std::getenv("CCMI_LEAD_DIR") && std::getenv("CCMI_LEAD_DIR")[0] == '1';
+    const bool dir = leadDir && e.queueOn(*this, DA_LEADERSHIP);
     if (dir) e.queueSyncSpec(spec);
     auto snap = [&](int c) -> const std::vector<int32_t>& {
       return dir ? e.dev->qdirRows(c) : m.snapshotIn(snapTab, c, spec);

@@ -198,6 +198,8 @@ class Engine {
     size_t logPos = 0;
     std::vector<uint32_t> stamp;  // [B] the round a broker was last set in (dedupes the log)
     uint32_t round = 0;
+    std::vector<std::shared_ptr<const std::vector<int32_t>>> snaps;  // a sync's snapshots (scratch)
+    std::vector<int32_t> todo;                                       // a sync's brokers (scratch)
   };
   QueueSync qsync_;
   void queueSync(const Model::Spec& spec);

@@ -6,6 +6,7 @@
 #include <stdexcept>
 
 #include "device.h"
+#include "hostpool.h"
 #include "prof.h"
 
 namespace ccmi {
@@ -989,6 +990,74 @@ std::shared_ptr<const std::vector<int32_t>> Model::snapshot(int b, const Spec& s
   }
   cachePut(cache, bVer[b], s, v);
   return v;
+}
+
+void Model::snapshotMany(const Spec& s, const std::vector<int32_t>& bs,
+                         std::vector<std::shared_ptr<const std::vector<int32_t>>>& out) {
+  const int n = (int)bs.size();
+  out.assign(n, nullptr);
+  static const bool check = std::getenv("CCMI_SNAPSHOT_CHECK") != nullptr;
+  HostPool& pool = HostPool::get();
+  if (check || pool.threads() <= 1 || n < 8) {
+    for (int i = 0; i < n; ++i) out[i] = snapshot(bs[i], s);
+    return;
+  }
+  // A utilization limit only filters the limit-free snapshot (as snapshot() does): the base Spec is sorted, the
+  // limited one filtered from it.
+  const bool limited = s.selAboveRes >= 0 || s.selBelowRes >= 0;
+  Spec base = s;
+  base.selAboveRes = base.selBelowRes = -1;
+  base.aboveLimit = base.belowLimit = 0;
+  // read-only phase: cache hits, versions derived from a cached predecessor, full sorts of the rest
+  std::vector<std::shared_ptr<const std::vector<int32_t>>> freshBase(limited ? n : 0);
+  std::vector<uint8_t> fresh(n, 0);
+  auto baseOf = [&](int b, bool& isFresh) {
+    auto& cache = sortedCache[b];
+    if (auto* hit = cacheFind(cache, bVer[b], base)) {
+      isFresh = false;
+      return *hit;
+    }
+    auto v = std::make_shared<std::vector<int32_t>>();
+    if (!snapshotFromPrevious(b, base, cache, *v)) {
+      std::vector<std::pair<uint64_t, int32_t>> keyed;
+      for (int r : bRepl[b])
+        if (selects(base, r)) keyed.push_back({replicaKey(base, r), r});
+      std::sort(keyed.begin(), keyed.end());
+      v->reserve(keyed.size());
+      for (const auto& kr : keyed) v->push_back(kr.second);
+    }
+    isFresh = true;
+    return std::shared_ptr<const std::vector<int32_t>>(std::move(v));
+  };
+  pool.parallelFor(n, [&](int i) {
+    const int b = bs[i];
+    if (!limited) {
+      bool f = false;
+      out[i] = baseOf(b, f);
+      fresh[i] = f;
+      return;
+    }
+    if (auto* hit = cacheFind(filteredCache[b], bVer[b], s)) {
+      out[i] = *hit;
+      return;
+    }
+    bool f = false;
+    const auto v0 = baseOf(b, f);
+    if (f) freshBase[i] = v0;
+    auto v = std::make_shared<std::vector<int32_t>>();
+    v->reserve(v0->size());
+    for (int r : *v0)
+      if ((s.selAboveRes < 0 || ru(r, s.selAboveRes) > s.aboveLimit) &&
+          (s.selBelowRes < 0 || ru(r, s.selBelowRes) < s.belowLimit))
+        v->push_back(r);
+    out[i] = std::move(v);
+    fresh[i] = 1;
+  });
+  for (int i = 0; i < n; ++i) {
+    const int b = bs[i];
+    if (limited && freshBase[i]) cachePut(sortedCache[b], bVer[b], base, freshBase[i]);
+    if (fresh[i]) cachePut(limited ? filteredCache[b] : sortedCache[b], bVer[b], s, out[i]);
+  }
 }
 
 const std::vector<int32_t>& Model::sorted(int b, int nameId) {

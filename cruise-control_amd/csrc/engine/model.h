@@ -352,6 +352,11 @@ class Model {
   // the live view of a set tracked earlier, because every key change re-inserts the replica.
   std::shared_ptr<const std::vector<int32_t>> snapshot(int b, const Spec& s);
   bool snapshotFromPrevious(int b, const Spec& s, std::vector<SortedCacheEntry>& cache, std::vector<int32_t>& out);
+  // snapshot(bs[i], s) into out[i] for every listed broker, the misses computed on the host pool (hostpool.h; the
+  // model is only read while they run, the caches are filled afterwards on this thread). The contents snapshot()
+  // returns.
+  void snapshotMany(const Spec& s, const std::vector<int32_t>& bs,
+                    std::vector<std::shared_ptr<const std::vector<int32_t>>>& out);
   // One Spec's snapshots of every broker, looked up by broker id and version (no per-call cache search or
   // reference counting): the drivers that poll many brokers per scan (moveIn, swap) keep one per Spec.
   struct SnapTable {

@@ -838,6 +838,13 @@ void Device::qdirBind(uint64_t key) {
   qdirSpan_ = 1;
   qdirSnap_.assign(B_, nullptr);
 }
+bool Device::qdirSetMany(const std::vector<int32_t>& bs,
+                         const std::vector<std::shared_ptr<const std::vector<int32_t>>>& snaps) {
+  for (size_t i = 0; i < bs.size(); ++i)
+    if (!qdirSet(bs[i], snaps[i])) return false;
+  return true;
+}
+
 bool Device::qdirSet(int b, std::shared_ptr<const std::vector<int32_t>> v) {
   if (qdirSnap_.empty() || b < 0 || b >= B_) throw std::logic_error("qdirSet before qdirBind");
   for (int r : *v)
