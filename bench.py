@@ -294,6 +294,26 @@ def scan_cross_line(perf, workload: str):
             "traffic_source": src}
 
 
+class GroupSession:
+    """The sessions of one shard group (bench --sharded --combiner group): optimized together, one host thread per
+    rank; rank 0 stands for the proposal (every rank makes the same decisions)."""
+
+    def __init__(self, ranks):
+        from concurrent.futures import ThreadPoolExecutor
+        self.ranks = ranks
+        self.pool = ThreadPoolExecutor(len(ranks))
+
+    def optimize(self, opt, goals, options):
+        return list(self.pool.map(lambda s: opt.optimizations(s, goals, options), self.ranks))[0]
+
+    def __getattr__(self, name):  # perf(), set_kernel_timing(), reset_perf(), ... of rank 0
+        return getattr(self.ranks[0], name)
+
+
+def optimize(opt, s, goals, options):
+    return s.optimize(opt, goals, options) if isinstance(s, GroupSession) else opt.optimizations(s, goals, options)
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -307,8 +327,10 @@ def main() -> None:
     ap.add_argument("--requests-per-gpu", type=int, default=1,
                     help="S concurrent what-if proposals per GPU in every step (one host thread + HIP stream per "
                          "session; the precompute pool of GoalOptimizer.java:117-119). Default 1: one proposal per step")
-    ap.add_argument("--combiner", choices=("shm", "rccl"), default="shm",
-                    help="--sharded: the per-scan MIN combiner (host shared memory on one node, or RCCL)")
+    ap.add_argument("--combiner", choices=("shm", "rccl", "group"), default="shm",
+                    help="--sharded: the per-scan MIN combiner (host shared memory on one node, RCCL, or 'group': ONE "
+                         "process drives --gpus N sessions, one per GPU on its own thread, and the scan servers "
+                         "combine on the device through a shard group; run without torchrun)")
     ap.add_argument("--sharded", action="store_true",
                     help="N>1: one proposal sharded by destination broker over all ranks (a MIN combine per scan) "
                          "instead of one independent what-if proposal per rank")
@@ -337,7 +359,11 @@ def main() -> None:
     goals = ccmi.goals_from_names(goal_names)
     options = WORKLOAD_OPTIONS[args.workload]() if args.workload in WORKLOAD_OPTIONS else None
     opt = ccmi.GoalOptimizer(workload_constraint(args.workload))
-    sharded = args.sharded and world > 1
+    group_mode = args.sharded and args.combiner == "group"
+    if group_mode and world > 1:
+        raise SystemExit("--combiner group drives every shard from one process: run it without torchrun")
+    n_group = max(1, args.gpus) if group_mode else 1
+    sharded = (args.sharded and world > 1) or (group_mode and n_group > 1)
     uid = None
     if sharded:  # rank 0's RCCL id / shared-memory name reaches the other ranks over the default process group
         obj = [(ccmi.rccl_unique_id(lib) if args.combiner == "rccl" else f"/ccmi_bench_{os.getpid()}_{int(time.time())}")
@@ -348,6 +374,14 @@ def main() -> None:
     shm_sessions = [0]
 
     def session():
+        if group_mode and n_group > 1:  # the group's sessions, rank r on GPU r (round-robin on a smaller box)
+            g = ccmi.ShardGroup(n_group, lib)
+            ranks = []
+            for r in range(n_group):
+                x = ccmi.ClusterModel.from_buffers(buf, device=r % ndev)
+                x.attach_group(g, r)
+                ranks.append(x)
+            return GroupSession(ranks)
         s = ccmi.ClusterModel.from_buffers(buf, device=device)
         if sharded and args.combiner == "rccl":
             s.attach_rccl(rank, world, uid)
@@ -363,13 +397,13 @@ def main() -> None:
         ws = session()
         ws.set_kernel_timing(True)
         ws.reset_perf()
-        r = opt.optimizations(ws, goals, options)
+        r = optimize(opt, ws, goals, options)
         inst_perf, inst_cands = ws.perf(), r.candidates
         del ws
     # One more instrumented proposal with the scan server off (a launch per scan): the per-launch kernel times the
     # rocprofv3 trace of the same path can be checked against (rank 0, single GPU, outside the timed region).
     launch_perf = None
-    if world == 1 and not args.no_launch_pass and args.workload != "c4":
+    if world == 1 and not args.no_launch_pass and args.workload != "c4" and not group_mode:
         os.environ["CCMI_SERVER"] = "0"
         try:
             ls = session()
@@ -398,9 +432,9 @@ def main() -> None:
     results = []
     for step_sessions in sessions:
         if pool is None:
-            results.extend(opt.optimizations(s, goals, options) for s in step_sessions)
+            results.extend(optimize(opt, s, goals, options) for s in step_sessions)
         else:
-            results.extend(pool.map(lambda s: opt.optimizations(s, goals, options), step_sessions))
+            results.extend(pool.map(lambda s: optimize(opt, s, goals, options), step_sessions))
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -468,7 +502,7 @@ def main() -> None:
         "metric": "candidate moves evaluated/s + proposal wall time, 10K brokers/1M replicas",
         "value": cands / elapsed,
         "unit": "candidate moves evaluated/s",
-        "n_gpus": world,
+        "n_gpus": n_group if group_mode else world,
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": elapsed * 1e3 / args.steps,
@@ -480,7 +514,9 @@ def main() -> None:
         "config": {"workload": workload_name,
                    "brokers": buf.desc.num_brokers, "replicas": buf.desc.num_replicas,
                    "partitions": buf.desc.num_partitions, "topics": buf.desc.num_topics,
-                   "goals": goal_names, "parallelism": (f"destination-sharded x{world} ({args.combiner} MIN combine per scan)" if sharded
+                   "goals": goal_names, "parallelism": (f"destination-sharded x{n_group} (one process, shard group: the scan servers MIN-combine "
+                                   f"each scan on the device)" if group_mode and sharded else
+                                   f"destination-sharded x{world} ({args.combiner} MIN combine per scan)" if sharded
                                    else f"independent what-if per GPU x{world}")},
         "parity": parity,
         "requests_per_gpu": S,

@@ -214,7 +214,7 @@ class DeviceError(CruiseControlError):
 _STATUS = {1: IllegalArgumentException, 2: DeviceError, 3: OptimizationFailureException, 4: IllegalStateException,
            5: UnsupportedOperationException}
 
-ABI_VERSION = 10  # CCMI_ABI_VERSION of include/ccmi.h
+ABI_VERSION = 11  # CCMI_ABI_VERSION of include/ccmi.h
 EXPORTED_SYMBOLS = (
     "ccmi_last_error", "ccmi_abi_version", "ccmi_device_count", "ccmi_default_constraint", "ccmi_default_random_cluster_props",
     "ccmi_random_cluster", "ccmi_cluster_buffers_desc", "ccmi_cluster_buffers_free", "ccmi_session_create",
@@ -224,7 +224,7 @@ EXPORTED_SYMBOLS = (
     "ccmi_leader_distribution", "ccmi_replica_disks", "ccmi_proposal_count", "ccmi_proposals",
     "ccmi_proposal_disks", "ccmi_perf", "ccmi_perf_reset",
     "ccmi_set_kernel_timing", "ccmi_session_set_shard", "ccmi_rccl_unique_id", "ccmi_session_attach_rccl",
-    "ccmi_session_attach_shm",
+    "ccmi_session_attach_shm", "ccmi_shard_group_create", "ccmi_shard_group_destroy", "ccmi_session_attach_group",
     "ccmi_topic_broker_set",
     "ccmi_builder_create", "ccmi_builder_destroy", "ccmi_builder_create_broker", "ccmi_builder_add_disk",
     "ccmi_builder_populate_partition", "ccmi_builder_set_broker_state", "ccmi_builder_set_disk_state",
@@ -296,6 +296,9 @@ class Library:
         L.ccmi_rccl_unique_id.argtypes = [C.POINTER(C.c_uint8)]
         L.ccmi_session_attach_rccl.argtypes = [C.c_void_p, C.c_int32, C.c_int32, C.POINTER(C.c_uint8)]
         L.ccmi_session_attach_shm.argtypes = [C.c_void_p, C.c_int32, C.c_int32, C.c_char_p]
+        L.ccmi_shard_group_create.argtypes = [C.c_int32, C.POINTER(C.c_void_p)]
+        L.ccmi_shard_group_destroy.argtypes = [C.c_void_p]
+        L.ccmi_session_attach_group.argtypes = [C.c_void_p, C.c_void_p, C.c_int32]
         L.ccmi_default_constraint.argtypes = [C.POINTER(ConstraintStruct)]
         L.ccmi_topic_broker_set.restype = C.c_int32
         L.ccmi_topic_broker_set.argtypes = [C.c_char_p, C.c_int32]
@@ -1236,6 +1239,31 @@ class ClusterModel:
         """Destination-sharded mode over the built-in host shared-memory combiner (ranks on one node): one int64 MIN
         per scan in a POSIX shared-memory block; the scan server stays on."""
         self.lib.check(self.lib.lib.ccmi_session_attach_shm(self.handle, rank, count, name.encode()))
+
+    def attach_group(self, group: "ShardGroup", rank: int) -> None:
+        """Rank `rank` of a one-process shard group (ShardGroup): the scan server combines the ranks' keys on the
+        device; this session's optimizations must run on a thread of its own, concurrently with the other ranks'."""
+        self.lib.check(self.lib.lib.ccmi_session_attach_group(self.handle, group.handle, rank))
+        self._group = group  # the group outlives the session
+
+
+class ShardGroup:
+    """The ranks of one destination-sharded proposal driven from ONE process (ccmi_shard_group_*, ABI v11): one
+    session per rank (typically one per GPU), each optimized on its own host thread; a scan the session's scan server
+    ran is MIN-combined with the other ranks' on the device, through pinned host memory every GPU maps. Keep the group
+    alive while its sessions are."""
+
+    def __init__(self, count: int, lib: Optional["Library"] = None):
+        self.lib = lib or Library.get()
+        h = C.c_void_p()
+        self.lib.check(self.lib.lib.ccmi_shard_group_create(count, C.byref(h)))
+        self.handle = h
+        self.count = count
+
+    def __del__(self):
+        if getattr(self, "handle", None):
+            self.lib.lib.ccmi_shard_group_destroy(self.handle)
+            self.handle = None
 
 
 def rccl_unique_id(lib: Optional["Library"] = None) -> bytes:

@@ -427,6 +427,56 @@ ccmi_status ccmi_session_attach_shm(ccmi_session* s, int32_t rank, int32_t count
   });
 }
 
+struct ccmi_shard_group {
+  ccmi::CombineBlock* blk = nullptr;
+  int32_t count = 0;
+};
+
+namespace {
+// the shard-group combiner for scans the scan server did not combine (shard_group.h): the host side of the protocol
+int groupMin(void* ctx, int64_t* key) {
+  try {
+    auto* dev = static_cast<ccmi::Device*>(ctx);
+    const int64_t g = dev->groupCombineHost(*key == INT64_MAX ? -1 : *key);
+    *key = g < 0 ? INT64_MAX : g;
+    return 0;
+  } catch (std::exception&) {
+    return 1;
+  }
+}
+}  // namespace
+
+ccmi_status ccmi_shard_group_create(int32_t count, ccmi_shard_group** out) {
+  return guarded([&] {
+    if (!out) throw std::invalid_argument("null argument");
+    if (count < 1) throw std::invalid_argument("shard count out of range");
+    auto g = std::make_unique<ccmi_shard_group>();
+    g->blk = ccmi::Device::allocCombineBlock();
+    g->count = count;
+    *out = g.release();
+    return CCMI_OK;
+  });
+}
+
+ccmi_status ccmi_shard_group_destroy(ccmi_shard_group* g) {
+  return guarded([&] {
+    if (g) ccmi::Device::freeCombineBlock(g->blk);
+    delete g;
+    return CCMI_OK;
+  });
+}
+
+ccmi_status ccmi_session_attach_group(ccmi_session* s, ccmi_shard_group* g, int32_t rank) {
+  return guarded([&] {
+    if (!s || !g) throw std::invalid_argument("null argument");
+    if (rank < 0 || rank >= g->count) throw std::invalid_argument("shard rank out of range");
+    s->device->attachGroup(g->blk, g->count);
+    s->engine->shard = ccmi::Shard{rank, g->count, &groupMin, s->device.get()};
+    s->device->setServerAllowed(true);  // the server combines on the device: it stays resident
+    return CCMI_OK;
+  });
+}
+
 ccmi_status ccmi_session_destroy(ccmi_session* s) {
   return guarded([&] {
     ccmi::prof().print("session");

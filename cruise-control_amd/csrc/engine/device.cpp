@@ -546,6 +546,11 @@ int64_t Device::serverRun(const DevProgram& prog, const Staged& g, int op, const
     c.goalParts = parts;
     c.nActive = (int32_t)std::min<uint64_t>(wgsFor(parts), (uint64_t)serverBlocks_);
   }
+  const bool grouped = grpHost_ && (op == SOP_CROSS || op == SOP_SEGS || op == SOP_PAIRS);
+  if (grouped) {  // the server folds this scan's key into the group's slot and publishes the group minimum
+    c.combineSlot = grpDev_ + (grpCalls_ & 1) * sizeof(CombineSlot);
+    c.combineCount = grpCount_;
+  }
   c.nb = g.nb;
   c.nr = g.nr;
   c.np = g.np;
@@ -561,6 +566,13 @@ int64_t Device::serverRun(const DevProgram& prog, const Staged& g, int op, const
   perf.serverScans++;
   const unsigned long long lo = hResult_[0] & 0xffffffffull;
   const int64_t key = lo == 0 ? -1 : (int64_t)(lo - 1);
+  if (grouped) {
+    ++grpCalls_;
+    devCombined_ = true;
+    const unsigned long long ex = __atomic_load_n(&hResult_[3], __ATOMIC_ACQUIRE);
+    if ((ex >> 32) == 4ull && (ex & 0xffffffffull) == (seq_ & 0xffffffffull))
+      throw std::runtime_error("shard group combine: not every rank arrived (scan server, 10 s)");
+  }
   if (adaptiveWidth_) {  // the winner's position in the first-sweep order (sliced: its row; -1: none)
     int64_t depth = -1;
     if (key >= 0)
@@ -1159,6 +1171,33 @@ int64_t Device::scanPairs(const DevProgram& prog, const int32_t* pr, const int32
   const int64_t key = finishScan();
   perf.scanRequired += key < 0 ? (int64_t)n : key - p0 + 1;
   return key;
+}
+
+CombineBlock* Device::allocCombineBlock() {
+  CombineBlock* b = nullptr;
+  hipCheck(hipHostMalloc((void**)&b, sizeof(CombineBlock),
+                         hipHostMallocPortable | hipHostMallocMapped | hipHostMallocCoherent),
+           "hipHostMalloc shard group");
+  initCombineBlock(b);
+  return b;
+}
+void Device::freeCombineBlock(CombineBlock* b) {
+  if (b) (void)hipHostFree(b);
+}
+void Device::attachGroup(CombineBlock* blk, int count) {
+  DeviceGuard dg(ordinal_);
+  void* d = nullptr;
+  hipCheck(hipHostGetDevicePointer(&d, blk, 0), "hipHostGetDevicePointer shard group");
+  grpHost_ = blk;
+  grpDev_ = (unsigned long long)(uintptr_t)d;
+  grpCount_ = count;
+  grpCalls_ = 0;
+  devCombined_ = false;
+}
+int64_t Device::groupCombineHost(int64_t key) {
+  CombineSlot* s = &grpHost_->slot[grpCalls_ & 1];
+  ++grpCalls_;
+  return groupHostMin(s, grpCount_, key, 120.0);
 }
 
 int64_t Device::segUpload(const SegIn& sg) {

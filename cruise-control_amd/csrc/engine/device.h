@@ -17,6 +17,7 @@
 
 #include "devtypes.h"
 #include "intra.h"
+#include "shard_group.h"
 #include "snapseg.h"
 
 namespace ccmi {
@@ -189,6 +190,18 @@ class Device {
   int64_t scanQueue(const DevProgram& prog, int head, int skip0, const int32_t* tail, int nTail, const int32_t* cands,
                     int N);
   int queueSpan() const { return qdirSpan_; }
+  // Shard groups (shard_group.h): the block every rank of the group maps, and the group's rank count. A served cross /
+  // segment / pair scan is then combined by the server (takeDeviceCombined() reports it once); any other combine goes
+  // through groupCombineHost on the same slot sequence.
+  void attachGroup(CombineBlock* blk, int count);
+  bool takeDeviceCombined() {
+    const bool x = devCombined_;
+    devCombined_ = false;
+    return x;
+  }
+  int64_t groupCombineHost(int64_t key);  // -1 = none, both ways
+  static CombineBlock* allocCombineBlock();
+  static void freeCombineBlock(CombineBlock* b);
   // the session's scans may (not) use the resident scan server (sessions whose scans wait on other ranks may not)
   void setServerAllowed(bool on) {
     if (!on) stopServer();
@@ -295,6 +308,11 @@ class Device {
   bool serverOn_ = false;
   bool serverUsable_ = false;  // set in the constructor (gfx950, CCMI_SERVER, fine-grained VRAM host-writable)
   bool serverAllowed_ = true;   // setServerAllowed
+  CombineBlock* grpHost_ = nullptr;  // attachGroup: host pointer, this device's mapping, ranks, combines so far
+  unsigned long long grpDev_ = 0;
+  int grpCount_ = 0;
+  uint64_t grpCalls_ = 0;
+  bool devCombined_ = false;
   int serverBlocks_ = 256;
   // goal-parallel server tiles (ServerCmd.goalParts): at most this many waves per candidate (CCMI_GOAL_SPLIT: 1, 2 or
   // 4) and only for scans whose split first sweep needs at most CCMI_GOAL_SPLIT_WGS workgroups

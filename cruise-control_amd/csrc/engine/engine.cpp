@@ -420,6 +420,7 @@ static bool forceCombine() {
 int64_t Engine::combine(int64_t localKey) const {
   if (shard.count <= 1 && !(shard.fn && forceCombine())) return localKey;
   dev->perf.combines++;
+  if (dev->takeDeviceCombined()) return localKey;  // a shard group's scan server published the group minimum
   int64_t k = localKey < 0 ? INT64_MAX : localKey;
   if (!shard.fn || shard.fn(shard.ctx, &k) != 0) throw std::runtime_error("shard combine (MIN allreduce) failed");
   return k == INT64_MAX ? -1 : k;
@@ -2145,6 +2146,7 @@ class ResourceDistribution : public GoalImpl {
     baseSpec.selBelowRes = noLimit.selBelowRes;
     baseSpec.belowLimit = noLimit.belowLimit;
     std::vector<int32_t> srcs, cbOff, cbRep, polled;
+    std::vector<std::shared_ptr<const std::vector<int32_t>>> polledSnaps;
     // Without new brokers the limit test runs on the device (SwapLimit) over the limit-free lists; with new brokers
     // the host filters (eligibleReplicasForSwap's CASE#2 depends on which filtered lists are empty).
     SwapLimit lim;
@@ -2161,10 +2163,10 @@ class ResourceDistribution : public GoalImpl {
         polled.clear();
         cbOff.assign(1, 0);
         cbRep.clear();
-        while (!pqEmpty() && (polled.empty() || polled.size() < target)) {
-          const int cb = pqPoll();
-          polled.push_back(cb);
-          const auto v = m.snapshot(cb, baseSpec);
+        while (!pqEmpty() && (polled.empty() || polled.size() < target)) polled.push_back(pqPoll());
+        m.snapshotMany(baseSpec, polled, polledSnaps);  // (many polled brokers: their sorts on the host pool)
+        for (size_t pi = 0; pi < polled.size(); ++pi) {
+          const auto& v = polledSnaps[pi];
           if (devLimit)
             cbRep.insert(cbRep.end(), v->begin(), v->end());
           else

@@ -27,6 +27,7 @@
 #include "../engine/devtypes.h"
 #include "../engine/predicates.h"
 #include "../engine/rackrows.h"
+#include "../engine/shard_group.h"
 
 namespace ccmi {
 
@@ -987,6 +988,39 @@ __device__ __attribute__((noinline)) void serverChain(const DevTables T, const C
     chainRackRowsRun(T, C, prog, ov, sc, req, c.chainN, req + c.chainN, c.chainM, log, out);
 }
 
+// Shard groups (engine/shard_group.h): this rank's first-fit key into the combine slot with system-scope atomics (the
+// slot is pinned host memory every device of the process maps), a wait for the group's other ranks — their servers or
+// their host threads run the same protocol on the same slot — and the group minimum back. A group that does not
+// complete within kServerStuckTicks leaves {4, seq} in mail[3] (the host throws) and no winner.
+__device__ __attribute__((noinline)) unsigned long long groupCombine(unsigned long long slotAddr, int count,
+                                                                     unsigned long long v,
+                                                                     unsigned long long* __restrict__ mail,
+                                                                     unsigned long long seq) {
+  CombineSlot* s = reinterpret_cast<CombineSlot*>(slotAddr);
+  unsigned long long cur = __hip_atomic_load(&s->minKey, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  while (v < cur && !__hip_atomic_compare_exchange_weak(&s->minKey, &cur, v, __ATOMIC_ACQ_REL, __ATOMIC_RELAXED,
+                                                        __HIP_MEMORY_SCOPE_SYSTEM)) {
+  }
+  __hip_atomic_fetch_add(&s->arrived, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_SYSTEM);
+  const unsigned long long t = __builtin_amdgcn_s_memrealtime();
+  while (__hip_atomic_load(&s->arrived, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < (unsigned)count) {
+    if (__builtin_amdgcn_s_memrealtime() - t > kServerStuckTicks) {
+      __hip_atomic_store(&mail[3], (4ull << 32) | (seq & 0xffffffffull), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // the record before the publish that wakes the host
+      return kNone;
+    }
+    __builtin_amdgcn_s_sleep(2);
+  }
+  const unsigned long long g = __hip_atomic_load(&s->minKey, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+  // the last rank out resets the slot (no rank uses it again before every rank arrived at the other slot)
+  if (__hip_atomic_fetch_add(&s->departed, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_SYSTEM) == (unsigned)count - 1) {
+    __hip_atomic_store(&s->minKey, kNone, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(&s->arrived, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(&s->departed, 0u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+  return g;
+}
+
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, kServerWaves))) void scan_server(DevTables T, MutTables Mt, ChainTables Ch, const ServerCmd* __restrict__ cmd,
                                                       const char* __restrict__ pay, const RowRef* __restrict__ pool,
                                                       unsigned long long* __restrict__ result,
@@ -1458,11 +1492,12 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, kServ
       }
       if (prev == nAct - 1) {
         // the result and workgroup 0's start stamp in one batch of loads
-        const unsigned long long v = __hip_atomic_load(&result[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        unsigned long long v = __hip_atomic_load(&result[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         const unsigned long long tStart = __hip_atomic_load(t0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const unsigned long long lo = v == kNone ? 0ull : (v + 1) & 0xffffffffull;
         __hip_atomic_store(&result[0], kNone, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (c.combineSlot) v = groupCombine(c.combineSlot, c.combineCount, v, mail, c.seq);  // a shard group's scan
+        const unsigned long long lo = v == kNone ? 0ull : (v + 1) & 0xffffffffull;
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         const unsigned long long busy = __builtin_amdgcn_s_memrealtime() - tStart;
         __hip_atomic_store(&mail[0], ((c.seq & 0xffffffffull) << 32) | lo, __ATOMIC_RELAXED,

@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define CCMI_ABI_VERSION 10
+#define CCMI_ABI_VERSION 11
 
 typedef enum ccmi_status {
   CCMI_OK = 0,
@@ -487,6 +487,17 @@ ccmi_status ccmi_session_attach_rccl(ccmi_session* s, int32_t rank, int32_t coun
  * POSIX shared-memory block `name` ("/name"; rank 0 creates it, the others open it, and every rank waits until all
  * `count` ranks are attached, at most 120 s). No GPU work per combine, so the session keeps its scan server. */
 ccmi_status ccmi_session_attach_shm(ccmi_session* s, int32_t rank, int32_t count, const char* name);
+/* ABI v11. Shard groups: the ranks of one sharded proposal driven from ONE process, one host thread per session
+ * (typically one session per GPU of the node, each thread calling ccmi_optimizations on its own session). The ranks'
+ * first-fit keys are MIN-combined in a block of pinned host memory every device maps: a scan the session's resident
+ * scan server ran is combined by the server itself (its last workgroup folds the key in with system-scope atomics, waits
+ * for the other ranks and publishes the group minimum), any other scan by the host thread on the same slots. The group
+ * must outlive its sessions. Replaces the per-scan host MIN of GoalOptimizer's single-threaded loop with nothing on the
+ * host between the ranks' scans. */
+typedef struct ccmi_shard_group ccmi_shard_group;
+ccmi_status ccmi_shard_group_create(int32_t count, ccmi_shard_group** out);
+ccmi_status ccmi_shard_group_destroy(ccmi_shard_group* g);
+ccmi_status ccmi_session_attach_group(ccmi_session* s, ccmi_shard_group* g, int32_t rank);
 
 /* Measurement hooks used by bench.py: device time of the last optimization's scan kernels (HIP events
  * on the engine stream) and their algorithmic bytes. */

@@ -838,6 +838,26 @@ void Device::qdirBind(uint64_t key) {
   qdirSpan_ = 1;
   qdirSnap_.assign(B_, nullptr);
 }
+// Shard groups: the emulation has no scan server, so every combine is the host side of the protocol (shard_group.h).
+CombineBlock* Device::allocCombineBlock() {
+  auto* b = new CombineBlock();
+  initCombineBlock(b);
+  return b;
+}
+void Device::freeCombineBlock(CombineBlock* b) { delete b; }
+void Device::attachGroup(CombineBlock* blk, int count) {
+  grpHost_ = blk;
+  grpDev_ = 0;
+  grpCount_ = count;
+  grpCalls_ = 0;
+  devCombined_ = false;
+}
+int64_t Device::groupCombineHost(int64_t key) {
+  CombineSlot* s = &grpHost_->slot[grpCalls_ & 1];
+  ++grpCalls_;
+  return groupHostMin(s, grpCount_, key, 120.0);
+}
+
 bool Device::qdirSetMany(const std::vector<int32_t>& bs,
                          const std::vector<std::shared_ptr<const std::vector<int32_t>>>& snaps) {
   for (size_t i = 0; i < bs.size(); ++i)

@@ -138,3 +138,69 @@ def test_gpu_rccl_combiner_one_rank(gpu_lib, oracle_lib, monkeypatch):
     assert cm.actions() == oc.actions()
     assert [(r.name, r.succeeded, r.candidates, r.actions) for r in res.goal_results] == \
         [(r.name, r.succeeded, r.candidates, r.actions) for r in ores]
+
+
+def _group_run(lib, props, goals, world, device_of=lambda r: 0):
+    """One process, `world` sessions of one sharded proposal in a shard group (ccmi_shard_group_*), each optimized on
+    its own thread; returns the sessions and their results."""
+    from concurrent.futures import ThreadPoolExecutor
+    buf = ccmi.RandomCluster.generate(lib, **props)
+    group = ccmi.ShardGroup(world, lib)
+    sessions = []
+    for r in range(world):
+        cm = ccmi.ClusterModel(buf.desc, device=device_of(r), lib=lib, keepalive=buf)
+        cm.attach_group(group, r)
+        cm.reset_perf()
+        sessions.append(cm)
+    opt = ccmi.GoalOptimizer(constraint(1.05))
+    with ThreadPoolExecutor(world) as pool:
+        results = list(pool.map(lambda cm: opt.optimizations(cm, ccmi.goals_from_names(goals)), sessions))
+    return buf, sessions, results
+
+
+def _check_group_against_oracle(buf, sessions, results, goals):
+    oc = OracleCluster.from_desc(buf.desc)
+    ores = oc.optimize(goals, constraint(1.05))
+    for cm, res in zip(sessions, results):
+        assert cm.perf().combines > 0
+        assert cm.actions() == oc.actions()
+        assert [(r.name, r.succeeded, r.candidates, r.actions) for r in res.goal_results] == \
+            [(r.name, r.succeeded, r.candidates, r.actions) for r in ores]
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_shard_group_one_process_matches_oracle(emu_lib, oracle_lib, world):
+    """A shard group in one process (the emulation combines on the host side of the group protocol): every rank makes
+    the oracle's decisions with the reference-equivalent candidate counts."""
+    props = dict(num_racks=5, num_brokers=20, num_replicas=6000, num_topics=300)
+    goals = list(ccmi.DEFAULT_GOALS)
+    _check_group_against_oracle(*_group_run(emu_lib, props, goals, world), goals)
+
+
+def test_shard_group_rejects_bad_rank(emu_lib):
+    buf = ccmi.RandomCluster.generate(emu_lib, num_racks=3, num_brokers=6, num_replicas=60, num_topics=5)
+    cm = ccmi.ClusterModel.from_buffers(buf, device=0)
+    group = ccmi.ShardGroup(2, emu_lib)
+    with pytest.raises(ccmi.IllegalArgumentException):
+        cm.attach_group(group, 2)
+    with pytest.raises(ccmi.IllegalArgumentException):
+        ccmi.ShardGroup(0, emu_lib)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("blocks", ["64", "256"])
+def test_gpu_shard_group_same_gpu_twice(gpu_lib, oracle_lib, monkeypatch, blocks):
+    """One process, two sessions on device ordinal 0 as the two ranks of a shard group. With 64-workgroup servers both
+    sessions keep a resident scan server and every served scan is combined ON THE DEVICE (each server's last workgroup
+    folds its key into the group's pinned-host slot and waits for the other rank); with 256 only one session gets a
+    server and the other's launched scans combine on its host thread against the server's device side of the same
+    protocol. Both decide exactly as the oracle."""
+    monkeypatch.setenv("CCMI_SERVER_BLOCKS", blocks)
+    props = dict(num_racks=5, num_brokers=40, num_replicas=12000, num_topics=400)
+    goals = list(ccmi.DEFAULT_GOALS)
+    buf, sessions, results = _group_run(gpu_lib, props, goals, 2)
+    _check_group_against_oracle(buf, sessions, results, goals)
+    served = [cm.perf().server_scans for cm in sessions]
+    assert max(served) > 0
+    if blocks == "64":
+        assert min(served) > 0
