@@ -173,6 +173,10 @@ Device::Device(int ordinal, int B, int R, int P, int T, int maxGoalSlots)
     if (const char* sa = std::getenv("CCMI_SERVER_APPLY")) applyViaServer_ = sa[0] != '0';
     if (const char* gw = std::getenv("CCMI_GOAL_SPLIT_WGS")) goalSplitWgs_ = (int)std::strtol(gw, nullptr, 10);
     if (const char* sw = std::getenv("CCMI_SCAN_WIDTH")) adaptiveWidth_ = std::strcmp(sw, "full") != 0;
+    if (const char* sm = std::getenv("CCMI_SERVER_STUCK_MS"))
+      stuckTicks_ = (unsigned long long)std::max(1.0, std::atof(sm)) * 100000ull;  // 100 MHz s_memrealtime
+    if (const char* cd = std::getenv("CCMI_CHAIN_DELAY_US"))
+      chainDelayTicks_ = (unsigned long long)std::max(0.0, std::atof(cd)) * 100ull;
     if (serverBlocks_ < 8) serverUsable_ = false;
     if (serverUsable_) {
       dalloc(&dServerT0_, 16);  // [0] busy-time stamp, [8] the doorbell (a line of its own)
@@ -712,6 +716,8 @@ DevTables Device::tables() const {
   t.ldB = ldB_;
   static const int pollMode = std::getenv("CCMI_SERVER_POLL") ? std::atoi(std::getenv("CCMI_SERVER_POLL")) : 0;
   t.pollMode = pollMode;
+  t.stuckTicks = stuckTicks_;
+  t.chainDelayTicks = chainDelayTicks_;
   return t;
 }
 

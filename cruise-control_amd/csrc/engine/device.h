@@ -321,6 +321,8 @@ class Device {
   int goalSplitWgs_ = 256;
   // a server scan's first sweep sized from its site's last winner depth (serverRun; CCMI_SCAN_WIDTH=full: off)
   bool adaptiveWidth_ = true;
+  unsigned long long stuckTicks_ = 1000000000ull;  // 10 s of s_memrealtime: a command unpublished that long is stuck
+  unsigned long long chainDelayTicks_ = 0;
   std::unordered_map<uint64_t, int64_t> lastDepth_;
   int progVer_ = 0;
   bool progSent_ = false;

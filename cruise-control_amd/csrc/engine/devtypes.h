@@ -165,6 +165,10 @@ struct DevTables {
   int32_t B, R, P, ldB;
   // scan server idle poll (CCMI_SERVER_POLL): 0 = back off (s_sleep 4, then 16 after 256 polls), 1 = spin, 2 = s_sleep 1
   int32_t pollMode;
+  // the scan server's stuck-command bound in s_memrealtime ticks (CCMI_SERVER_STUCK_MS, default 10 s) and a test-only
+  // delay added to every chain command (CCMI_CHAIN_DELAY_US, default 0: a chain that outlasts a short bound)
+  unsigned long long stuckTicks;
+  unsigned long long chainDelayTicks;
 };
 
 // Row updates the host flushes to the device before a scan (only rows touched since the last flush).

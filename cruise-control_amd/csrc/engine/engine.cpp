@@ -1980,10 +1980,16 @@ class ResourceDistribution : public GoalImpl {
     struct Group {
       int c;
       std::vector<int32_t> rbs;
-      std::vector<int64_t> idx;  // view index of each rb's partition leader (-1: not selected / no row)
+      std::vector<std::pair<int64_t, int32_t>> byIdx;  // (view index of rbs[k]'s partition leader, k), sorted
       uint32_t ver = ~0u;
     };
     std::vector<Group> groups;
+    // The groups in poll order (the queue's reversed broker comparator). Only cb's key changes between scans (leadership
+    // moves cb -> b; b leads none of these partitions' leaders), so after an accept cb's group alone is re-placed and
+    // the rows are the groups' sorted rows walked in this order: the order a sort of all rows by (poll order, view
+    // index) gives, without the sort.
+    std::vector<int> order;
+    auto before = [&](int gx, int gy) { return cmpBroker(m, groups[gy].c, groups[gx].c) < 0; };
     {
       PhaseScope pf(PH_FLATTEN);
       std::vector<std::pair<int, int>> lb;
@@ -1994,37 +2000,40 @@ class ResourceDistribution : public GoalImpl {
         if (groups.empty() || groups.back().c != x.first) groups.push_back(Group{x.first, {}, {}, ~0u});
         groups.back().rbs.push_back(x.second);
       }
+      order.resize(groups.size());
+      for (size_t i = 0; i < groups.size(); ++i) order[i] = (int)i;
+      std::sort(order.begin(), order.end(), before);
     }
+    auto emit = [&](Group& g) {  // the group's rows in view order (its view indices recomputed on a new version)
+      if (g.ver != m.bVer[g.c]) {
+        g.byIdx.clear();
+        for (size_t k = 0; k < g.rbs.size(); ++k) {
+          const int rb = g.rbs[k];
+          if (m.rLeader[rb]) continue;  // b leads that partition now: no leader row elsewhere
+          const int lr = m.pLeader[m.rPart[rb]];
+          if (m.rBroker[lr] != g.c || !m.selects(spec, lr)) continue;
+          g.byIdx.push_back({(int64_t)indexOf(g.c, lr), (int32_t)k});
+        }
+        std::sort(g.byIdx.begin(), g.byIdx.end());
+        g.ver = m.bVer[g.c];
+      }
+      for (const auto& e : g.byIdx) {
+        if (m.rLeader[g.rbs[e.second]]) continue;
+        if (g.c == curCb && (size_t)e.first < curSkip) continue;
+        rows.push_back({g.c, (size_t)e.first, m.pLeader[m.rPart[g.rbs[e.second]]]});
+      }
+    };
     while (curCb >= 0 || (!pq.empty() && cond())) {
       {
         PhaseScope pf(PH_FLATTEN);
         rows.clear();
-        for (Group& g : groups) {
-          if (g.c != curCb && !queued[g.c]) continue;
-          if (g.ver != m.bVer[g.c]) {
-            g.idx.assign(g.rbs.size(), -1);
-            for (size_t k = 0; k < g.rbs.size(); ++k) {
-              const int rb = g.rbs[k];
-              if (m.rLeader[rb]) continue;  // b leads that partition now: no leader row elsewhere
-              const int lr = m.pLeader[m.rPart[rb]];
-              if (m.rBroker[lr] != g.c || !m.selects(spec, lr)) continue;
-              g.idx[k] = (int64_t)indexOf(g.c, lr);
-            }
-            g.ver = m.bVer[g.c];
-          }
-          for (size_t k = 0; k < g.rbs.size(); ++k) {
-            if (g.idx[k] < 0 || m.rLeader[g.rbs[k]]) continue;
-            if (g.c == curCb && (size_t)g.idx[k] < curSkip) continue;
-            rows.push_back({g.c, (size_t)g.idx[k], m.pLeader[m.rPart[g.rbs[k]]]});
-          }
+        if (curCb >= 0)  // the current broker's remaining view first
+          for (Group& g : groups)
+            if (g.c == curCb) emit(g);
+        for (int gi : order) {
+          Group& g = groups[gi];
+          if (g.c != curCb && queued[g.c]) emit(g);
         }
-        std::sort(rows.begin(), rows.end(), [&](const Row& x, const Row& y) {
-          if (x.cb != y.cb) {
-            if (x.cb == curCb || y.cb == curCb) return x.cb == curCb;
-            return cmpBroker(m, y.cb, x.cb) < 0;  // poll order: the queue's reversed broker comparator
-          }
-          return x.idx < y.idx;
-        });
         pr.clear();
         pb.clear();
         for (const Row& x : rows) {
@@ -2062,6 +2071,15 @@ class ResourceDistribution : public GoalImpl {
       const size_t idx = hit->idx;
       m.relocateLeadership(m.rPart[hit->r], cb, b);
       if (dir) e.queueSyncSpec(spec);  // cb's and b's views changed
+      for (size_t i = 0; i < order.size(); ++i)  // cb's key moved: re-place its group in the poll order
+        if (groups[order[i]].c == cb) {
+          const int gi = order[i];
+          order.erase(order.begin() + (ptrdiff_t)i);
+          size_t j = 0;
+          while (j < order.size() && !before(gi, order[j])) ++j;
+          order.insert(order.begin() + (ptrdiff_t)j, gi);
+          break;
+        }
       if (aboveLower(m, b)) return false;
       if (!pq.empty() && m.pct(cb, res) < m.pct(pq.peek(), res)) {
         pq.add(cb);

@@ -881,7 +881,6 @@ __device__ __forceinline__ void copySysOneThread(X* dst, const X* src) {  // all
   for (int w = 0; w < n; ++w) reinterpret_cast<int32_t*>(dst)[w] = v[w];
 }
 constexpr unsigned long long kServerIdleTicks = 200000000ull;  // 2 s of s_memrealtime (100 MHz)
-constexpr unsigned long long kServerStuckTicks = 1000000000ull;  // 10 s: a command unpublished that long is stuck
 // scan-server doorbell word: valid and exit flags, nActive (bits 32-61), the command sequence's low 32 bits
 constexpr unsigned long long kBellValid = 1ull << 63, kBellExit = 1ull << 62;
 
@@ -991,11 +990,12 @@ __device__ __attribute__((noinline)) void serverChain(const DevTables T, const C
 // Shard groups (engine/shard_group.h): this rank's first-fit key into the combine slot with system-scope atomics (the
 // slot is pinned host memory every device of the process maps), a wait for the group's other ranks — their servers or
 // their host threads run the same protocol on the same slot — and the group minimum back. A group that does not
-// complete within kServerStuckTicks leaves {4, seq} in mail[3] (the host throws) and no winner.
+// complete within the stuck bound (DevTables.stuckTicks) leaves {4, seq} in mail[3] (the host throws) and no winner.
 __device__ __attribute__((noinline)) unsigned long long groupCombine(unsigned long long slotAddr, int count,
                                                                      unsigned long long v,
                                                                      unsigned long long* __restrict__ mail,
-                                                                     unsigned long long seq) {
+                                                                     unsigned long long seq,
+                                                                     unsigned long long bound) {
   CombineSlot* s = reinterpret_cast<CombineSlot*>(slotAddr);
   unsigned long long cur = __hip_atomic_load(&s->minKey, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   while (v < cur && !__hip_atomic_compare_exchange_weak(&s->minKey, &cur, v, __ATOMIC_ACQ_REL, __ATOMIC_RELAXED,
@@ -1004,7 +1004,7 @@ __device__ __attribute__((noinline)) unsigned long long groupCombine(unsigned lo
   __hip_atomic_fetch_add(&s->arrived, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_SYSTEM);
   const unsigned long long t = __builtin_amdgcn_s_memrealtime();
   while (__hip_atomic_load(&s->arrived, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < (unsigned)count) {
-    if (__builtin_amdgcn_s_memrealtime() - t > kServerStuckTicks) {
+    if (__builtin_amdgcn_s_memrealtime() - t > bound) {
       __hip_atomic_store(&mail[3], (4ull << 32) | (seq & 0xffffffffull), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // the record before the publish that wakes the host
       return kNone;
@@ -1091,7 +1091,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, kServ
             } else if (participated) {
               // a command this workgroup took part in never completed (a participant never arrived), 10 s after this
               // workgroup took it: leave instead of spinning forever
-              if (__builtin_amdgcn_s_memrealtime() - idleSince > kServerStuckTicks) {
+              if (__builtin_amdgcn_s_memrealtime() - idleSince > T.stuckTicks) {
                 ex = 3;
                 break;
               }
@@ -1188,6 +1188,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, kServ
       const unsigned long long tc0 = T.stamps ? __builtin_amdgcn_s_memrealtime() : 0;
       stage();
       serverChain(T, Ch, Mt, c, pay);
+      if (T.chainDelayTicks) {  // tests: a chain that outlasts a short stuck bound (the other workgroups must wait)
+        const unsigned long long t = __builtin_amdgcn_s_memrealtime();
+        while (__builtin_amdgcn_s_memrealtime() - t < T.chainDelayTicks) __builtin_amdgcn_s_sleep(8);
+      }
       const unsigned long long tc1 = T.stamps ? __builtin_amdgcn_s_memrealtime() : 0;
       // every wave's stores complete, then one system-scope release: the records and loads for the other XCDs' next
       // acquire, the log and result for the host (MI355X_MICROARCH.md, inter-workgroup visibility)
@@ -1496,7 +1500,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, kServ
         const unsigned long long tStart = __hip_atomic_load(t0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(&result[0], kNone, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (c.combineSlot) v = groupCombine(c.combineSlot, c.combineCount, v, mail, c.seq);  // a shard group's scan
+        if (c.combineSlot) v = groupCombine(c.combineSlot, c.combineCount, v, mail, c.seq, T.stuckTicks);  // shard group
         const unsigned long long lo = v == kNone ? 0ull : (v + 1) & 0xffffffffull;
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         const unsigned long long busy = __builtin_amdgcn_s_memrealtime() - tStart;

@@ -232,3 +232,24 @@ def test_gpu_xcd_sliced_scans_match_oracle(gpu_lib, oracle_lib, tmp_path, monkey
 def test_gpu_bad_disk_brokers_match_oracle(gpu_lib, oracle_lib, props, goals):
     """Partition._ineligibleBrokers on the device (DevTables.pIneligOff/pIneligB in legitMove)."""
     check_product_against_oracle(gpu_lib, props, goals, 1.05, max_replicas=3000)
+
+
+def test_gpu_chain_outlasting_stuck_bound(gpu_lib, oracle_lib, monkeypatch):
+    """A K7 chain runs on workgroup 0 of the scan server alone; the other workgroups must wait for it however long it
+    takes instead of applying the stuck-command bound to a command they are not part of. With the bound at 2 ms and
+    every chain padded to 5 ms (test-only CCMI_CHAIN_DELAY_US), a proposal with chains still completes on the server
+    and decides exactly as the oracle."""
+    monkeypatch.setenv("CCMI_SERVER_STUCK_MS", "2")
+    monkeypatch.setenv("CCMI_CHAIN_DELAY_US", "5000")
+    props = dict(num_racks=5, num_brokers=20, num_replicas=6000, num_topics=300)
+    buf = ccmi.RandomCluster.generate(gpu_lib, **props)
+    cm = ccmi.ClusterModel.from_buffers(buf, device=0)
+    cm.reset_perf()
+    res = ccmi.GoalOptimizer(constraint(1.05)).optimizations(cm, ccmi.goals_from_names(DEFAULT_GOALS))
+    p = cm.perf()
+    assert p.server_chains > 0 and p.server_scans > 0
+    oc = OracleCluster.from_desc(buf.desc)
+    ores = oc.optimize(DEFAULT_GOALS, constraint(1.05))
+    assert cm.actions() == oc.actions()
+    assert [(r.name, r.succeeded, r.candidates, r.actions) for r in res.goal_results] == \
+        [(r.name, r.succeeded, r.candidates, r.actions) for r in ores]
