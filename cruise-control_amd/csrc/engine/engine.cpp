@@ -979,18 +979,23 @@ class ReplicaDistribution : public GoalImpl {
       size_t e2 = i;
       while (e2 < list.size() && m.curOffline(list[e2]) == runOffline) ++e2;
       batch.assign(list.begin() + i, list.begin() + e2);
-      cand.inorder(inorder);
-      e.eligible(inorder, DA_MOVE, cands);
-      const int64_t key = e.crossScan(*this, DA_MOVE, batch, 0, cands);
+      // the tree's maintained sequence itself (no copy) when no eligibility filter applies
+      const std::vector<int32_t>* seq = cand.sequence();
+      if (!seq) {
+        cand.inorder(inorder);
+        seq = &inorder;
+      }
+      const std::vector<int32_t>& cl = e.eligibleView(*seq, DA_MOVE, cands);
+      const int64_t key = e.crossScan(*this, DA_MOVE, batch, 0, cl);
       if (key < 0) {
         if (runOffline) wasUnable = true;
         i = e2;
         continue;
       }
-      const int N = (int)cands.size();
+      const int N = (int)cl.size();
       const int k = (int)(key / N), j = (int)(key % N);
       if (runOffline && k > 0) wasUnable = true;
-      const int r = batch[k], dst = cands[j];
+      const int r = batch[k], dst = cl[j];  // (read before the tree changes below)
       m.relocateReplica(m.rPart[r], b, dst);
       if (m.nrep(b) <= (m.bNoff[b] == 0 ? upperSrc : 0)) return false;
       cand.remove(dst);
@@ -1664,9 +1669,13 @@ class ResourceDistribution : public GoalImpl {
         const std::vector<int32_t>* cl;
         {
           PhaseScope pc(PH_CAND_BUILD);
-          if (built) cand.inorder(inorder);
-          // (the lazy order is kept up to date after every accept below)
-          cl = &e.eligibleView(inorder, DA_MOVE, cands);
+          // built: the tree's maintained sequence itself (no copy); else the lazy order, kept up to date below
+          const std::vector<int32_t>* seq = built ? cand.sequence() : &inorder;
+          if (!seq) {
+            cand.inorder(inorder);
+            seq = &inorder;
+          }
+          cl = &e.eligibleView(*seq, DA_MOVE, cands);
         }
         const int64_t key = e.crossScan(*this, DA_MOVE, list, i, *cl);
         if (key < 0) break;

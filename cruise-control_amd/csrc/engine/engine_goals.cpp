@@ -1249,18 +1249,22 @@ class TopicReplicaDistribution : public GoalImpl {
       const bool runOffline = m.curOffline(list[i]);
       size_t end = i;
       while (end < list.size() && m.curOffline(list[end]) == runOffline) ++end;
-      cand.inorder(inorder);
-      e.eligible(inorder, DA_MOVE, cands);
-      const int64_t key = e.crossScan(*this, DA_MOVE, list, i, cands, FILTER_NONE, true, end);
+      const std::vector<int32_t>* seq = cand.sequence();  // the maintained sequence itself (no copy)
+      if (!seq) {
+        cand.inorder(inorder);
+        seq = &inorder;
+      }
+      const std::vector<int32_t>& cl = e.eligibleView(*seq, DA_MOVE, cands);
+      const int64_t key = e.crossScan(*this, DA_MOVE, list, i, cl, FILTER_NONE, true, end);
       if (key < 0) {
         if (runOffline) wasUnable = true;
         i = end;
         continue;
       }
-      const size_t N = cands.size();
+      const size_t N = cl.size();
       const size_t k = i + (size_t)(key / (int64_t)N);
       if (runOffline && k > i) wasUnable = true;
-      const int r = list[k], dst = cands[key % (int64_t)N];
+      const int r = list[k], dst = cl[key % (int64_t)N];  // (read before the tree changes below)
       const bool wasOffline = m.curOffline(r);
       m.relocateReplica(m.rPart[r], b, dst);
       if (wasOffline) nOff--;
@@ -1972,15 +1976,19 @@ class LeaderReplicaDistribution : public GoalImpl {
     std::vector<int32_t> inorder, cands;
     size_t i = 0;
     while (i < list.size()) {
-      if (treeReady) cand.inorder(inorder);
-      else inorder.assign(entryOrder.begin(), entryOrder.end());
-      e.eligible(inorder, DA_MOVE, cands);
-      const int64_t key = e.crossScan(*this, DA_MOVE, list, i, cands);
+      // the tree's maintained sequence (or, before the tree is needed, the entry order) itself: no copy
+      const std::vector<int32_t>* seq = treeReady ? cand.sequence() : &entryOrder;
+      if (!seq) {
+        cand.inorder(inorder);
+        seq = &inorder;
+      }
+      const std::vector<int32_t>& cl = e.eligibleView(*seq, DA_MOVE, cands);
+      const int64_t key = e.crossScan(*this, DA_MOVE, list, i, cl);
       e.dev->idleWork = nullptr;  // the remaining puts, if the tree is needed, are finished below
       if (key < 0) break;
-      const size_t N = cands.size();
+      const size_t N = cl.size();
       const size_t k = i + (size_t)(key / (int64_t)N);
-      const int dst = cands[key % (int64_t)N];
+      const int dst = cl[key % (int64_t)N];  // (read before the tree changes below)
       m.relocateReplica(m.rPart[list[k]], b, dst);
       if (--n <= upperLimit) {
         m.untrack(b, id);

@@ -294,6 +294,8 @@ class RbTreeSet {
     }
     return removed;
   }
+  // the maintained in-order key sequence (no copy), or null when it is not maintained; valid until the next change
+  const std::vector<int>* sequence() const { return seqOn_ ? &seqKey_ : nullptr; }
   void inorder(std::vector<int>& out) const {
     if (seqOn_) {
       out.assign(seqKey_.begin(), seqKey_.end());
