@@ -550,7 +550,7 @@ int64_t Device::serverRun(const DevProgram& prog, const Staged& g, int op, const
     c.goalParts = parts;
     c.nActive = (int32_t)std::min<uint64_t>(wgsFor(parts), (uint64_t)serverBlocks_);
   }
-  const bool grouped = grpHost_ && (op == SOP_CROSS || op == SOP_SEGS || op == SOP_PAIRS);
+  const bool grouped = grpHost_ && combineArmed_ && (op == SOP_CROSS || op == SOP_SEGS || op == SOP_PAIRS);
   if (grouped) {  // the server folds this scan's key into the group's slot and publishes the group minimum
     c.combineSlot = grpDev_ + (grpCalls_ & 1) * sizeof(CombineSlot);
     c.combineCount = grpCount_;
@@ -573,6 +573,7 @@ int64_t Device::serverRun(const DevProgram& prog, const Staged& g, int op, const
   if (grouped) {
     ++grpCalls_;
     devCombined_ = true;
+    combineArmed_ = false;
     const unsigned long long ex = __atomic_load_n(&hResult_[3], __ATOMIC_ACQUIRE);
     if ((ex >> 32) == 4ull && (ex & 0xffffffffull) == (seq_ & 0xffffffffull))
       throw std::runtime_error("shard group combine: not every rank arrived (scan server, 10 s)");

@@ -194,9 +194,13 @@ class Device {
   // segment / pair scan is then combined by the server (takeDeviceCombined() reports it once); any other combine goes
   // through groupCombineHost on the same slot sequence.
   void attachGroup(CombineBlock* blk, int count);
+  // armGroupCombine before the scan call Engine::combine wraps: the first served cross / segment / pair command after it
+  // combines on the device (a scan the engine does not combine — a queue scan's flattened fallback — is never tagged)
+  void armGroupCombine() { combineArmed_ = grpHost_ != nullptr; }
   bool takeDeviceCombined() {
     const bool x = devCombined_;
     devCombined_ = false;
+    combineArmed_ = false;
     return x;
   }
   int64_t groupCombineHost(int64_t key);  // -1 = none, both ways
@@ -313,6 +317,7 @@ class Device {
   int grpCount_ = 0;
   uint64_t grpCalls_ = 0;
   bool devCombined_ = false;
+  bool combineArmed_ = false;
   int serverBlocks_ = 256;
   // goal-parallel server tiles (ServerCmd.goalParts): at most this many waves per candidate (CCMI_GOAL_SPLIT: 1, 2 or
   // 4) and only for scans whose split first sweep needs at most CCMI_GOAL_SPLIT_WGS workgroups

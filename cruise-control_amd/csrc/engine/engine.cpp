@@ -246,6 +246,7 @@ int64_t Engine::crossScan(GoalImpl& self, int action, const std::vector<int32_t>
   constexpr int kRowWindow = 32, kProbeCols = 1024;
   auto scanRows = [&](int k0, int nk, int cEnd) -> int64_t {  // rows [k0, k0 + nk) x columns [0, cEnd) of N
     const int s0 = (int)((int64_t)cEnd * shard.rank / shard.count), s1 = (int)((int64_t)cEnd * (shard.rank + 1) / shard.count);
+    dev->armGroupCombine();
     const int64_t k = combine(dev->scanCross(prog, reps.data() + r0 + k0, nk, cands.data(), N, s0, s1));
     return k < 0 ? -1 : k + (int64_t)k0 * N;
   };
@@ -294,6 +295,7 @@ int64_t Engine::crossScanSegs(GoalImpl& self, int action, const std::vector<Snap
   PhaseScope ps(PH_DEV_SCAN);
   m.flushToDevice();
   prog.filter = FILTER_NONE;
+  dev->armGroupCombine();
   const int64_t key = combine(dev->scanSegs(prog, segs, cands.data(), N, 0, N));
   checkTerminal(key);
   candidates += key >= 0 ? key + 1 : K * N;
@@ -418,9 +420,10 @@ static bool forceCombine() {
 }
 
 int64_t Engine::combine(int64_t localKey) const {
+  const bool onDevice = dev->takeDeviceCombined();  // (also disarms the group combine)
   if (shard.count <= 1 && !(shard.fn && forceCombine())) return localKey;
   dev->perf.combines++;
-  if (dev->takeDeviceCombined()) return localKey;  // a shard group's scan server published the group minimum
+  if (onDevice) return localKey;  // a shard group's scan server published the group minimum
   int64_t k = localKey < 0 ? INT64_MAX : localKey;
   if (!shard.fn || shard.fn(shard.ctx, &k) != 0) throw std::runtime_error("shard combine (MIN allreduce) failed");
   return k == INT64_MAX ? -1 : k;
@@ -434,6 +437,7 @@ int64_t Engine::pairScan(GoalImpl& self, const std::vector<int32_t>& pr, const s
   const int n = (int)pr.size();
   const int p0 = (int)((int64_t)n * shard.rank / shard.count), p1 = (int)((int64_t)n * (shard.rank + 1) / shard.count);
   const DevProgram prog = program(self, action);
+  dev->armGroupCombine();
   const int64_t key = combine(dev->scanPairs(prog, pr.data(), pb.data(), p0, p1));
   checkTerminal(key);
   if (!count) return key;
