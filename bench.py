@@ -365,7 +365,7 @@ def main() -> None:
     n_group = max(1, args.gpus) if group_mode else 1
     sharded = (args.sharded and world > 1) or (group_mode and n_group > 1)
     uid = None
-    if sharded:  # rank 0's RCCL id / shared-memory name reaches the other ranks over the default process group
+    if sharded and not group_mode:  # rank 0's RCCL id / shared-memory name reaches the other ranks over the process group
         obj = [(ccmi.rccl_unique_id(lib) if args.combiner == "rccl" else f"/ccmi_bench_{os.getpid()}_{int(time.time())}")
                if rank == 0 else None]
         dist.broadcast_object_list(obj, src=0)

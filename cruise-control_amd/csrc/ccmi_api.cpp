@@ -1,10 +1,12 @@
 // C ABI of libccmi.so (include/ccmi.h). Exceptions never cross the boundary: every entry point maps them to a
 // ccmi_status and keeps the message for ccmi_last_error() (thread-local).
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <mutex>
 #include <string>
+#include <vector>
 
 #include "ccmi.h"
 #include "engine/buffers.h"
@@ -430,6 +432,7 @@ ccmi_status ccmi_session_attach_shm(ccmi_session* s, int32_t rank, int32_t count
 struct ccmi_shard_group {
   ccmi::CombineBlock* blk = nullptr;
   int32_t count = 0;
+  std::vector<ccmi_session*> ranks;  // attached sessions by rank
 };
 
 namespace {
@@ -449,7 +452,7 @@ int groupMin(void* ctx, int64_t* key) {
 ccmi_status ccmi_shard_group_create(int32_t count, ccmi_shard_group** out) {
   return guarded([&] {
     if (!out) throw std::invalid_argument("null argument");
-    if (count < 1) throw std::invalid_argument("shard count out of range");
+    if (count < 1 || count > ccmi::kGroupMaxRanks) throw std::invalid_argument("shard count out of range");
     auto g = std::make_unique<ccmi_shard_group>();
     g->blk = ccmi::Device::allocCombineBlock();
     g->count = count;
@@ -470,9 +473,25 @@ ccmi_status ccmi_session_attach_group(ccmi_session* s, ccmi_shard_group* g, int3
   return guarded([&] {
     if (!s || !g) throw std::invalid_argument("null argument");
     if (rank < 0 || rank >= g->count) throw std::invalid_argument("shard rank out of range");
-    s->device->attachGroup(g->blk, g->count);
+    s->device->attachGroup(g->blk, g->count, rank);
     s->engine->shard = ccmi::Shard{rank, g->count, &groupMin, s->device.get()};
     s->device->setServerAllowed(true);  // the server combines on the device: it stays resident
+    // Ranks sharing a GPU: a kernel one rank launches can wait behind another rank's persistent server (hardware queues
+    // and CU slots are per device), while that server's command waits for the launching rank's arrival. Such ranks
+    // launch per scan and combine on their host threads; CCMI_GROUP_SHARED_SERVERS=1 instead gives each of them a
+    // server with an equal share of the device's workgroup budget (tests of the device-side combine on one GPU).
+    g->ranks.resize((size_t)g->count, nullptr);
+    g->ranks[(size_t)rank] = s;
+    std::vector<ccmi_session*> same;
+    for (ccmi_session* x : g->ranks)
+      if (x && x->deviceOrdinal == s->deviceOrdinal) same.push_back(x);
+    if (same.size() > 1) {
+      const bool shared = std::getenv("CCMI_GROUP_SHARED_SERVERS") && std::getenv("CCMI_GROUP_SHARED_SERVERS")[0] == '1';
+      for (ccmi_session* x : same) {
+        if (shared) x->device->limitServerBlocks((int)(256 / same.size()) / 8 * 8);
+        else x->device->setServerAllowed(false);
+      }
+    }
     return CCMI_OK;
   });
 }

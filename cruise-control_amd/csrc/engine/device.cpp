@@ -148,7 +148,9 @@ Device::Device(int ordinal, int B, int R, int P, int T, int maxGoalSlots)
   hipCheck(hipMemset(dDone_, 0, 4 * sizeof(unsigned int)), "hipMemset");
   hipCheck(hipMemset(dResult_, 0xff, 2 * sizeof(unsigned long long)), "hipMemset");
   // host-coherent (fine-grained) mapped memory: kernels read the staging area and write the mailbox directly
-  hipCheck(hipHostMalloc((void**)&hResult_, 1024, hipHostMallocMapped | hipHostMallocCoherent), "hipHostMalloc");
+  // portable: in a shard group another device's scan server may publish into this mailbox (shard_group.h)
+  hipCheck(hipHostMalloc((void**)&hResult_, 1024, hipHostMallocMapped | hipHostMallocCoherent | hipHostMallocPortable),
+           "hipHostMalloc");
   hipCheck(hipHostGetDevicePointer((void**)&hResultDev_, hResult_, 0), "hipHostGetDevicePointer");
   std::memset(hResult_, 0, 1024);
   ensureStage(1 << 20);
@@ -395,6 +397,11 @@ bool Device::serveScan(const DevProgram& prog, const Staged& g, bool readsTopicC
 
 // Start the server unless it runs (restarting one the host left idle for a while, far from the device's 2 s
 // watchdog); false when the device already has its budget of servers (the caller launches instead).
+void Device::limitServerBlocks(int blocks) {
+  stopServer();
+  serverBlocks_ = std::max(8, std::min(serverBlocks_, blocks / 8 * 8));
+}
+
 bool Device::ensureServer() {
   if (serverOn_ && nowSeconds() - lastServerUse_ > 0.25) stopServer();
   if (serverOn_) return true;
@@ -551,8 +558,10 @@ int64_t Device::serverRun(const DevProgram& prog, const Staged& g, int op, const
     c.nActive = (int32_t)std::min<uint64_t>(wgsFor(parts), (uint64_t)serverBlocks_);
   }
   const bool grouped = grpHost_ && combineArmed_ && (op == SOP_CROSS || op == SOP_SEGS || op == SOP_PAIRS);
-  if (grouped) {  // the server folds this scan's key into the group's slot and publishes the group minimum
-    c.combineSlot = grpDev_ + (grpCalls_ & 1) * sizeof(CombineSlot);
+  if (grouped) {  // the server folds this scan's key into the group's slot; the group's last rank publishes the minimum
+    c.combineBlock = grpDev_;
+    c.combineSlot = (int32_t)(grpCalls_ & 1);
+    c.combineRank = grpRank_;
     c.combineCount = grpCount_;
   }
   c.nb = g.nb;
@@ -574,9 +583,6 @@ int64_t Device::serverRun(const DevProgram& prog, const Staged& g, int op, const
     ++grpCalls_;
     devCombined_ = true;
     combineArmed_ = false;
-    const unsigned long long ex = __atomic_load_n(&hResult_[3], __ATOMIC_ACQUIRE);
-    if ((ex >> 32) == 4ull && (ex & 0xffffffffull) == (seq_ & 0xffffffffull))
-      throw std::runtime_error("shard group combine: not every rank arrived (scan server, 10 s)");
   }
   if (adaptiveWidth_) {  // the winner's position in the first-sweep order (sliced: its row; -1: none)
     int64_t depth = -1;
@@ -1191,20 +1197,27 @@ CombineBlock* Device::allocCombineBlock() {
 void Device::freeCombineBlock(CombineBlock* b) {
   if (b) (void)hipHostFree(b);
 }
-void Device::attachGroup(CombineBlock* blk, int count) {
+void Device::attachGroup(CombineBlock* blk, int count, int rank) {
   DeviceGuard dg(ordinal_);
   void* d = nullptr;
   hipCheck(hipHostGetDevicePointer(&d, blk, 0), "hipHostGetDevicePointer shard group");
+  // every rank (its server or its host thread) may publish into this rank's mailbox: one address for all of them
+  if (d != (void*)blk || hResultDev_ != (unsigned long long*)hResult_)
+    throw std::runtime_error("shard groups need pinned host memory at one address on host and devices");
   grpHost_ = blk;
   grpDev_ = (unsigned long long)(uintptr_t)d;
   grpCount_ = count;
+  grpRank_ = rank;
   grpCalls_ = 0;
+  grpHostSeq_ = 0;
   devCombined_ = false;
+  __atomic_store_n(&hResult_[6], 0ull, __ATOMIC_RELAXED);
+  __atomic_store_n(&blk->mail[rank], (unsigned long long)(uintptr_t)hResult_, __ATOMIC_RELEASE);
 }
 int64_t Device::groupCombineHost(int64_t key) {
-  CombineSlot* s = &grpHost_->slot[grpCalls_ & 1];
+  const int slot = (int)(grpCalls_ & 1);
   ++grpCalls_;
-  return groupHostMin(s, grpCount_, key, 120.0);
+  return groupHostMin(grpHost_, slot, grpRank_, grpCount_, key, ++grpHostSeq_, 120.0);
 }
 
 int64_t Device::segUpload(const SegIn& sg) {

@@ -193,7 +193,7 @@ class Device {
   // Shard groups (shard_group.h): the block every rank of the group maps, and the group's rank count. A served cross /
   // segment / pair scan is then combined by the server (takeDeviceCombined() reports it once); any other combine goes
   // through groupCombineHost on the same slot sequence.
-  void attachGroup(CombineBlock* blk, int count);
+  void attachGroup(CombineBlock* blk, int count, int rank);
   // armGroupCombine before the scan call Engine::combine wraps: the first served cross / segment / pair command after it
   // combines on the device (a scan the engine does not combine — a queue scan's flattened fallback — is never tagged)
   void armGroupCombine() { combineArmed_ = grpHost_ != nullptr; }
@@ -207,6 +207,8 @@ class Device {
   static CombineBlock* allocCombineBlock();
   static void freeCombineBlock(CombineBlock* b);
   // the session's scans may (not) use the resident scan server (sessions whose scans wait on other ranks may not)
+  // at most `blocks` server workgroups from the next server launch on (a multiple of 8, at least 8)
+  void limitServerBlocks(int blocks);
   void setServerAllowed(bool on) {
     if (!on) stopServer();
     serverAllowed_ = on;
@@ -314,10 +316,12 @@ class Device {
   bool serverAllowed_ = true;   // setServerAllowed
   CombineBlock* grpHost_ = nullptr;  // attachGroup: host pointer, this device's mapping, ranks, combines so far
   unsigned long long grpDev_ = 0;
-  int grpCount_ = 0;
+  int grpCount_ = 0, grpRank_ = 0;
   uint64_t grpCalls_ = 0;
+  uint32_t grpHostSeq_ = 0;  // host combines so far (their results arrive in mail[6] under this count)
   bool devCombined_ = false;
   bool combineArmed_ = false;
+  std::vector<unsigned long long> groupMail_;  // the test emulation's shard-group mailbox (the product uses hResult_)
   int serverBlocks_ = 256;
   // goal-parallel server tiles (ServerCmd.goalParts): at most this many waves per candidate (CCMI_GOAL_SPLIT: 1, 2 or
   // 4) and only for scans whose split first sweep needs at most CCMI_GOAL_SPLIT_WGS workgroups

@@ -285,12 +285,11 @@ struct alignas(16) ServerCmd {
   unsigned long long chainLog;
   unsigned long long chainOut;
   unsigned long long queueDir;  // SOP_QUEUE: the snapshot directory (QueueDirEntry[B], fine-grained VRAM)
-  // SOP_CROSS / SOP_SEGS / SOP_PAIRS of a session in a shard group (shard_group.h): the device address of this combine's
-  // slot (0: no combine) and the group's rank count; the last workgroup folds the scan's key in and publishes the group
-  // minimum
-  unsigned long long combineSlot;
-  int32_t combineCount;
-  int32_t combinePad;
+  // SOP_CROSS / SOP_SEGS / SOP_PAIRS of a session in a shard group (shard_group.h): the group's combine block (0: no
+  // combine), this combine's slot, the rank and the rank count; the last workgroup folds the scan's key into the slot
+  // instead of publishing it, and the group's last rank to arrive publishes the minimum to every rank
+  unsigned long long combineBlock;
+  int32_t combineSlot, combineRank, combineCount, combinePad;
 };
 // The sequence word is a seqlock: the host stores (next | kSeqBusy) before it rewrites the other fields and `next`
 // after; a workgroup accepts a header only when the word it read before and after its copy is the same, not busy.

@@ -988,37 +988,30 @@ __device__ __attribute__((noinline)) void serverChain(const DevTables T, const C
 }
 
 // Shard groups (engine/shard_group.h): this rank's first-fit key into the combine slot with system-scope atomics (the
-// slot is pinned host memory every device of the process maps), a wait for the group's other ranks — their servers or
-// their host threads run the same protocol on the same slot — and the group minimum back. A group that does not
-// complete within the stuck bound (DevTables.stuckTicks) leaves {4, seq} in mail[3] (the host throws) and no winner.
-__device__ __attribute__((noinline)) unsigned long long groupCombine(unsigned long long slotAddr, int count,
-                                                                     unsigned long long v,
-                                                                     unsigned long long* __restrict__ mail,
-                                                                     unsigned long long seq,
-                                                                     unsigned long long bound) {
-  CombineSlot* s = reinterpret_cast<CombineSlot*>(slotAddr);
+// block is pinned host memory every device of the process maps), its result tag (the command's sequence, mail[0]),
+// and its arrival. No wait: the group's LAST rank to arrive — this workgroup, another rank's server or a rank's host
+// thread — publishes the minimum into every rank's mailbox and resets the slot.
+__device__ __attribute__((noinline)) void groupArrive(unsigned long long blockAddr, int slot, int rank, int count,
+                                                      unsigned long long v, unsigned long long seq) {
+  CombineBlock* b = reinterpret_cast<CombineBlock*>(blockAddr);
+  CombineSlot* s = &b->slot[slot];
+  __hip_atomic_store(&s->tag[rank], kTagServer | (seq & 0xffffffffull), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   unsigned long long cur = __hip_atomic_load(&s->minKey, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   while (v < cur && !__hip_atomic_compare_exchange_weak(&s->minKey, &cur, v, __ATOMIC_ACQ_REL, __ATOMIC_RELAXED,
                                                         __HIP_MEMORY_SCOPE_SYSTEM)) {
   }
-  __hip_atomic_fetch_add(&s->arrived, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_SYSTEM);
-  const unsigned long long t = __builtin_amdgcn_s_memrealtime();
-  while (__hip_atomic_load(&s->arrived, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < (unsigned)count) {
-    if (__builtin_amdgcn_s_memrealtime() - t > bound) {
-      __hip_atomic_store(&mail[3], (4ull << 32) | (seq & 0xffffffffull), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // the record before the publish that wakes the host
-      return kNone;
-    }
-    __builtin_amdgcn_s_sleep(2);
-  }
+  if (__hip_atomic_fetch_add(&s->arrived, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_SYSTEM) != (unsigned)count - 1) return;
   const unsigned long long g = __hip_atomic_load(&s->minKey, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
-  // the last rank out resets the slot (no rank uses it again before every rank arrived at the other slot)
-  if (__hip_atomic_fetch_add(&s->departed, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_SYSTEM) == (unsigned)count - 1) {
-    __hip_atomic_store(&s->minKey, kNone, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    __hip_atomic_store(&s->arrived, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    __hip_atomic_store(&s->departed, 0u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  const unsigned long long lo = g == kCombineNone ? 0ull : (g + 1) & 0xffffffffull;
+  for (int r = 0; r < count; ++r) {
+    const unsigned long long t = __hip_atomic_load(&s->tag[r], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+    unsigned long long* mail =
+        reinterpret_cast<unsigned long long*>(__hip_atomic_load(&b->mail[r], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
+    __hip_atomic_store(&mail[(t >> 62) == 1 ? 0 : 6], ((t & 0xffffffffull) << 32) | lo, __ATOMIC_RELEASE,
+                       __HIP_MEMORY_SCOPE_SYSTEM);
   }
-  return g;
+  __hip_atomic_store(&s->minKey, kCombineNone, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  __hip_atomic_store(&s->arrived, 0u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, kServerWaves))) void scan_server(DevTables T, MutTables Mt, ChainTables Ch, const ServerCmd* __restrict__ cmd,
@@ -1496,16 +1489,18 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, kServ
       }
       if (prev == nAct - 1) {
         // the result and workgroup 0's start stamp in one batch of loads
-        unsigned long long v = __hip_atomic_load(&result[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const unsigned long long v = __hip_atomic_load(&result[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         const unsigned long long tStart = __hip_atomic_load(t0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(&result[0], kNone, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (c.combineSlot) v = groupCombine(c.combineSlot, c.combineCount, v, mail, c.seq, T.stuckTicks);  // shard group
         const unsigned long long lo = v == kNone ? 0ull : (v + 1) & 0xffffffffull;
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         const unsigned long long busy = __builtin_amdgcn_s_memrealtime() - tStart;
-        __hip_atomic_store(&mail[0], ((c.seq & 0xffffffffull) << 32) | lo, __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_SYSTEM);
+        if (c.combineBlock)  // a shard group's scan: the group's last rank publishes mail[0] (shard_group.h)
+          groupArrive(c.combineBlock, c.combineSlot, c.combineRank, c.combineCount, v, c.seq);
+        else
+          __hip_atomic_store(&mail[0], ((c.seq & 0xffffffffull) << 32) | lo, __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_SYSTEM);
         // mail[5]: the command's busy time (100 MHz ticks from workgroup 0 seeing it to the publish, low 40 bits)
         // tagged with the sequence's low 24 bits, stored after the word with no wait in between: the host collects it
         // before its next command (Device::collectServerBusy) instead of the publish waiting for a second PCIe write

@@ -838,6 +838,8 @@ void Device::qdirBind(uint64_t key) {
   qdirSpan_ = 1;
   qdirSnap_.assign(B_, nullptr);
 }
+void Device::limitServerBlocks(int) {}
+
 // Shard groups: the emulation has no scan server, so every combine is the host side of the protocol (shard_group.h).
 CombineBlock* Device::allocCombineBlock() {
   auto* b = new CombineBlock();
@@ -845,17 +847,21 @@ CombineBlock* Device::allocCombineBlock() {
   return b;
 }
 void Device::freeCombineBlock(CombineBlock* b) { delete b; }
-void Device::attachGroup(CombineBlock* blk, int count) {
+void Device::attachGroup(CombineBlock* blk, int count, int rank) {
   grpHost_ = blk;
   grpDev_ = 0;
   grpCount_ = count;
+  grpRank_ = rank;
   grpCalls_ = 0;
+  grpHostSeq_ = 0;
   devCombined_ = false;
+  groupMail_.assign(8, 0ull);
+  __atomic_store_n(&blk->mail[rank], (unsigned long long)(uintptr_t)groupMail_.data(), __ATOMIC_RELEASE);
 }
 int64_t Device::groupCombineHost(int64_t key) {
-  CombineSlot* s = &grpHost_->slot[grpCalls_ & 1];
+  const int slot = (int)(grpCalls_ & 1);
   ++grpCalls_;
-  return groupHostMin(s, grpCount_, key, 120.0);
+  return groupHostMin(grpHost_, slot, grpRank_, grpCount_, key, ++grpHostSeq_, 120.0);
 }
 
 bool Device::qdirSetMany(const std::vector<int32_t>& bs,

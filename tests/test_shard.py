@@ -188,19 +188,21 @@ def test_shard_group_rejects_bad_rank(emu_lib):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("blocks", ["64", "256"])
-def test_gpu_shard_group_same_gpu_twice(gpu_lib, oracle_lib, monkeypatch, blocks):
-    """One process, two sessions on device ordinal 0 as the two ranks of a shard group. With 64-workgroup servers both
-    sessions keep a resident scan server and every served scan is combined ON THE DEVICE (each server's last workgroup
-    folds its key into the group's pinned-host slot and waits for the other rank); with 256 only one session gets a
-    server and the other's launched scans combine on its host thread against the server's device side of the same
-    protocol. Both decide exactly as the oracle."""
-    monkeypatch.setenv("CCMI_SERVER_BLOCKS", blocks)
+@pytest.mark.parametrize("shared_servers", ["1", "0"])
+def test_gpu_shard_group_same_gpu_twice(gpu_lib, oracle_lib, monkeypatch, shared_servers):
+    """One process, two sessions on device ordinal 0 as the two ranks of a shard group. With
+    CCMI_GROUP_SHARED_SERVERS=1 each rank gets a scan server with half the device's workgroup budget and every served
+    scan is combined ON THE DEVICE (the server's last workgroup folds the rank's key into the group's pinned-host slot,
+    and the group's last rank publishes the minimum into both mailboxes); by default ranks sharing a GPU launch per scan
+    and combine on their host threads (a launch could wait behind the other rank's persistent server). Both decide
+    exactly as the oracle."""
+    monkeypatch.setenv("CCMI_GROUP_SHARED_SERVERS", shared_servers)
     props = dict(num_racks=5, num_brokers=40, num_replicas=12000, num_topics=400)
     goals = list(ccmi.DEFAULT_GOALS)
     buf, sessions, results = _group_run(gpu_lib, props, goals, 2)
     _check_group_against_oracle(buf, sessions, results, goals)
     served = [cm.perf().server_scans for cm in sessions]
-    assert max(served) > 0
-    if blocks == "64":
+    if shared_servers == "1":
         assert min(served) > 0
+    else:
+        assert max(served) == 0
