@@ -177,6 +177,8 @@ Device::Device(int ordinal, int B, int R, int P, int T, int maxGoalSlots)
     if (const char* sw = std::getenv("CCMI_SCAN_WIDTH")) adaptiveWidth_ = std::strcmp(sw, "full") != 0;
     if (const char* sm = std::getenv("CCMI_SERVER_STUCK_MS"))
       stuckTicks_ = (unsigned long long)std::max(1.0, std::atof(sm)) * 100000ull;  // 100 MHz s_memrealtime
+    if (const char* pk = std::getenv("CCMI_GROUP_PARK_US"))
+      parkTicks_ = (unsigned long long)std::max(1.0, std::atof(pk)) * 100ull;
     if (const char* cd = std::getenv("CCMI_CHAIN_DELAY_US"))
       chainDelayTicks_ = (unsigned long long)std::max(0.0, std::atof(cd)) * 100ull;
     if (serverBlocks_ < 8) serverUsable_ = false;
@@ -340,9 +342,40 @@ void Device::ensureFg(size_t bytes) {
   progSent_ = false;
 }
 
+// A shard-group session's server parks (ends its launch) when a group scan waits too long for the other ranks
+// (kernels/scan.hip, shard_group.h): its workgroups follow workgroup 0's exit record out, so the stream drains by
+// itself; the budget and the timing are settled as for a stop.
+void Device::retireParkedServer() {
+  if (serverTimed_) (void)hipEventRecord((hipEvent_t)evS1_, ST);
+  hipCheck(hipStreamSynchronize(ST), "parked scan server");
+  serverOn_ = false;
+  {
+    std::lock_guard<std::mutex> lk(g_serverMu);
+    g_serverWgs[ordinal_ & 63] -= serverBlocks_;
+  }
+  if (serverTimed_) {
+    float ms = 0.f;
+    if (hipEventElapsedTime(&ms, (hipEvent_t)evS0_, (hipEvent_t)evS1_) == hipSuccess) perf.serverResidentMs += ms;
+    serverTimed_ = false;
+  }
+  prof().count(31, "server.parks", 1);
+}
+
+// A group session moves mail[7] (the last posted command) forward before each command; false: the server parked
+// after its last command instead (it is retired here, nothing of the new command ran).
+bool Device::claimServer() {
+  if (!grpHost_) return true;
+  unsigned long long expect = lastCmdSeq_;
+  if (__atomic_compare_exchange_n(&hResult_[7], &expect, seq_ + 1, false, __ATOMIC_ACQ_REL, __ATOMIC_ACQUIRE))
+    return true;
+  retireParkedServer();
+  return false;
+}
+
 void Device::stopServer() {
   if (!serverOn_) return;
   DeviceGuard dg(ordinal_);
+  if (!claimServer()) return;  // parked: already ended
   ServerCmd* c = (ServerCmd*)fg_;
   *(volatile unsigned long long*)&c->seq = (seq_ + 1) | kSeqBusy;  // seqlock (devtypes.h kSeqBusy)
   hostStoreFence();
@@ -415,6 +448,7 @@ bool Device::ensureServer() {
   hipCheck(hipMemsetAsync(dDone_, 0, sizeof(unsigned int), ST), "reset server arrivals");
   hipCheck(hipMemsetAsync(dResult_, 0xff, sizeof(unsigned long long), ST), "reset server result");
   hipCheck(hipMemsetAsync(dServerT0_ + 8, 0, sizeof(unsigned long long), ST), "reset server doorbell");
+  __atomic_store_n(&hResult_[7], lastCmdSeq_, __ATOMIC_RELEASE);  // the new launch's last command (parking, groups)
   serverTimed_ = timing;
   if (serverTimed_) (void)hipEventRecord((hipEvent_t)evS0_, ST);
   hipCheck(launchScanServer(tables(), mutTables(), chainTables(), (const ServerCmd*)fg_, fg_ + kCmdBytes, segPool_,
@@ -442,6 +476,7 @@ int Device::serverProgram(const DevProgram& prog, char* pay) {
 // nothing of the command ran, and the caller takes its launch path.
 bool Device::postCommand(ServerCmd& c, bool rowsSent) {
   collectServerBusy();
+  if (!claimServer()) return false;  // parked after its last command: the caller takes its launch path
   c.rowsEpoch = rowsEpoch_;
   *(volatile unsigned long long*)fg_ = (seq_ + 1) | kSeqBusy;
   hostStoreFence();
@@ -451,7 +486,12 @@ bool Device::postCommand(ServerCmd& c, bool rowsSent) {
   lastCmdSeq_ = ++seq_;
   *(volatile unsigned long long*)fg_ = lastCmdSeq_;
   hostStoreFence();
-  if (!waitMail(seq_, true)) {
+  const bool seen = waitMail(seq_, true);
+  if (parkedPending_) {  // the result came after the server parked (a slow shard group): retire the ended launch
+    parkedPending_ = false;
+    retireParkedServer();
+  }
+  if (!seen) {
     serverOn_ = false;
     {
       std::lock_guard<std::mutex> lk(g_serverMu);
@@ -724,6 +764,7 @@ DevTables Device::tables() const {
   static const int pollMode = std::getenv("CCMI_SERVER_POLL") ? std::atoi(std::getenv("CCMI_SERVER_POLL")) : 0;
   t.pollMode = pollMode;
   t.stuckTicks = stuckTicks_;
+  t.parkTicks = parkTicks_;
   t.chainDelayTicks = chainDelayTicks_;
   return t;
 }
@@ -952,6 +993,18 @@ bool Device::waitMail(unsigned long long seq, bool serverCmd) {
         if ((__atomic_load_n(&mail[0], __ATOMIC_ACQUIRE) >> 32) == want) break;
         const unsigned long long ex = __atomic_load_n(&mail[3], __ATOMIC_ACQUIRE);
         if (serverCmd && (ex >> 32) == 1 && (ex & 0xffffffffull) == ((seq - 1) & 0xffffffffull)) return false;
+        if (serverCmd && (ex >> 32) == 5 && (ex & 0xffffffffull) == want) {
+          // the server parked with this command waiting for a shard group: its result still arrives in mail[0]
+          parkedPending_ = true;
+          const double t0 = nowSeconds();
+          for (uint64_t k = 0; (__atomic_load_n(&mail[0], __ATOMIC_ACQUIRE) >> 32) != want; ++k) {
+            if ((k & 4095) == 4095 && nowSeconds() - t0 > 120.0)
+              throw std::runtime_error("shard group combine: not every rank arrived (120 s)");
+            if (k > (1u << 16)) sched_yield();
+            else __builtin_ia32_pause();
+          }
+          break;
+        }
         char msg[256];
         std::snprintf(msg, sizeof(msg),
                       "scan finished without publishing its result (seq %llu, mail %016llx, server %s, server exit "

@@ -332,6 +332,10 @@ class Device {
   bool adaptiveWidth_ = true;
   unsigned long long stuckTicks_ = 1000000000ull;  // 10 s of s_memrealtime: a command unpublished that long is stuck
   unsigned long long chainDelayTicks_ = 0;
+  unsigned long long parkTicks_ = 100000ull;  // 1 ms: a shard-group scan waiting longer parks the server
+  bool parkedPending_ = false;                // waitMail saw the server park with the awaited command
+  void retireParkedServer();
+  bool claimServer();
   std::unordered_map<uint64_t, int64_t> lastDepth_;
   int progVer_ = 0;
   bool progSent_ = false;

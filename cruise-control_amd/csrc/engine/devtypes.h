@@ -169,6 +169,8 @@ struct DevTables {
   // delay added to every chain command (CCMI_CHAIN_DELAY_US, default 0: a chain that outlasts a short bound)
   unsigned long long stuckTicks;
   unsigned long long chainDelayTicks;
+  // a shard-group scan unpublished this long parks the server (CCMI_GROUP_PARK_US, default 1 ms; shard_group.h)
+  unsigned long long parkTicks;
 };
 
 // Row updates the host flushes to the device before a scan (only rows touched since the last flush).

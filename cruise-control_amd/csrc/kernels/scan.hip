@@ -883,6 +883,7 @@ __device__ __forceinline__ void copySysOneThread(X* dst, const X* src) {  // all
 constexpr unsigned long long kServerIdleTicks = 200000000ull;  // 2 s of s_memrealtime (100 MHz)
 // scan-server doorbell word: valid and exit flags, nActive (bits 32-61), the command sequence's low 32 bits
 constexpr unsigned long long kBellValid = 1ull << 63, kBellExit = 1ull << 62;
+constexpr unsigned long long kParkBit = 1ull << 62;  // mail[7]: the server parked after this command (shard groups)
 
 // thread 0's record writes become visible to the whole workgroup (one CU: workgroup scope; the next launch sees them
 // through the kernel boundary)
@@ -1032,6 +1033,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, kServ
   int acqEpoch = -1;  // ServerCmd.rowsEpoch of this workgroup's last acquire (-1: none since the launch)
   unsigned long long idleSince = __builtin_amdgcn_s_memrealtime();
   bool participated = false;  // this workgroup took part in its last command (thread 0's view)
+  bool lastGrouped = false;   // ... and that command was a shard group's scan
   unsigned long long srvT[6] = {0, 0, 0, 0, 0, 0};
   unsigned long long qBatch = 0, qTiles = 0;  // CCMI_STAMPS, SOP_QUEUE: workgroup 0's batch-loaded stamp and tiles
   for (;;) {
@@ -1081,19 +1083,32 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, kServ
             if ((mw >> 32) == (last & 0xffffffffull)) {
               published = true;
               idleSince = __builtin_amdgcn_s_memrealtime();
-            } else if (participated) {
+            } else {
+              const unsigned long long waited = __builtin_amdgcn_s_memrealtime() - idleSince;
+              // A shard group's scan waits for the other ranks' arrivals (shard_group.h). Past T.parkTicks workgroup 0
+              // parks the server — it ends the launch so nothing of this device waits behind it (a rank sharing the
+              // GPU may need it for a launch of its own) — unless the host has posted a newer command meanwhile: the
+              // compare-and-swap on mail[7] (the last posted sequence, which the host moves forward with its own
+              // compare-and-swap before every command) decides between the two. The result still arrives in mail[0].
+              if (blockIdx.x == 0 && lastGrouped && waited > T.parkTicks) {
+                unsigned long long expect = last;
+                if (__hip_atomic_compare_exchange_strong(&mail[7], &expect, last | kParkBit, __ATOMIC_ACQ_REL,
+                                                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) {
+                  ex = 5;
+                  break;
+                }
+              }
               // a command this workgroup took part in never completed (a participant never arrived), 10 s after this
               // workgroup took it: leave instead of spinning forever
-              if (__builtin_amdgcn_s_memrealtime() - idleSince > T.stuckTicks) {
+              if (participated && waited > T.stuckTicks) {
                 ex = 3;
                 break;
               }
-            } else {
-              // not a participant: the command may run as long as it needs (a K7 chain on workgroup 0); this workgroup
-              // leaves only with workgroup 0's stuck exit record for that command
+              // a non-participant (the command may run as long as it needs: a K7 chain on workgroup 0) or a participant
+              // of a parked group scan leaves with workgroup 0's exit record for that command
               const unsigned long long xr = __hip_atomic_load(&mail[3], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-              if ((xr >> 32) == 3ull && (xr & 0xffffffffull) == (last & 0xffffffffull)) {
-                ex = 3;
+              if (((xr >> 32) == 3ull || (xr >> 32) == 5ull) && (xr & 0xffffffffull) == (last & 0xffffffffull)) {
+                ex = (int)(xr >> 32);
                 break;
               }
             }
@@ -1111,6 +1126,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, kServ
       }
       SRV_STAMP(T, 0);
       participated = !ex && c.op != SOP_EXIT && (uint32_t)blockIdx.x < (uint32_t)c.nActive;
+      lastGrouped = participated && c.combineBlock != 0;
       idleSince = __builtin_amdgcn_s_memrealtime();  // a stuck command is timed from when this workgroup took it
       // the rows workgroup 0 wrote for earlier commands (released before its arrivals) become visible with an agent
       // acquire; a command no earlier one wrote rows before needs none
@@ -1125,8 +1141,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, kServ
     }
     __syncthreads();
     if (sExit || c.op == SOP_EXIT) {
-      // exit record for the host's diagnostics: mail[3] = {reason (1 watchdog, 2 exit command, 3 stuck command) : 32 |
-      // last seq : 32}
+      // exit record for the host's diagnostics: mail[3] = {reason (1 watchdog, 2 exit command, 3 stuck command, 5 parked
+      // waiting for a shard group) : 32 | last seq : 32}
       if (blockIdx.x == 0 && threadIdx.x == 0)
         __hip_atomic_store(&mail[3], ((unsigned long long)(sExit ? sExit : 2) << 32) | (last & 0xffffffffull),
                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
