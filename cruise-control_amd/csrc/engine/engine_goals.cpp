@@ -1736,6 +1736,10 @@ inline bool pairChainsOn(const Engine& e) {
   static const bool off = std::getenv("CCMI_NO_PAIR_CHAINS") != nullptr;
   return !off && e.chainsOn();
 }
+template <class Q>
+bool LeaderReplicaDistribution_moveInQueue(Engine& e, GoalImpl& self, int b, Q& pq, const Model::Spec& spec,
+                                           const std::vector<int32_t>& cands, int nl, int lower);
+
 class LeaderReplicaDistribution : public GoalImpl {
  public:
   LeaderReplicaDistribution() {
@@ -2058,6 +2062,7 @@ class LeaderReplicaDistribution : public GoalImpl {
     std::vector<int32_t> single{b}, cands;
     e.eligible(single, DA_MOVE, cands);
     if (cands.empty()) return true;  // every source replica visits an empty candidate list: nothing moves
+    if (e.queueOn(*this, DA_MOVE)) return LeaderReplicaDistribution_moveInQueue(e, *this, b, pq, s, cands, nl, lower);
     // rows: the sources' sorted leaders (snapshots held by snapTab until the next model change; device-resident
     // segments of the snapshot pool)
     auto segLen = [](const SnapSeg& x) { return x.v->size() > x.skip ? x.v->size() - x.skip : 0; };
@@ -2118,6 +2123,55 @@ class LeaderReplicaDistribution : public GoalImpl {
     return true;
   }
 };
+
+// rebalanceByMovingLeaderReplicasIn over the whole source queue in one command per accepted move (Engine::queueScan,
+// SOP_QUEUE; ResourceDistribution::moveInQueue is the same loop for the resource goals): the rows of every queued
+// source — its sorted leaders, the snapshot directory's view for `spec` — in poll order, so the scan's first fit is the
+// reference's next accept however deep in the queue it lies; sources polled before the winner's are consumed, the ones
+// after it stay queued. After an accept the source is re-added (fewer leaders than the queue's head), or iterated on at
+// the same index of its view without the moved replica, or dropped when that was its last row (:302-352).
+template <class Q>
+bool LeaderReplicaDistribution_moveInQueue(Engine& e, GoalImpl& self, int b, Q& pq, const Model::Spec& spec,
+                                           const std::vector<int32_t>& cands, int nl, int lower) {
+  Model& m = e.m;
+  std::vector<int32_t> merged;
+  int curCb = -1, curSkip = 0;
+  const int N = (int)cands.size();
+  while (curCb >= 0 || !pq.empty()) {
+    const bool run = pq.heapEmpty();
+    if (!run) {
+      merged.clear();
+      while (!pq.empty()) merged.push_back(pq.poll());
+    }
+    const int32_t* tail = run ? pq.runData() : merged.data();
+    const int nTail = (int)(run ? pq.runLeft() : merged.size());
+    const int head = curCb, hasHead = head >= 0 ? 1 : 0;
+    const int64_t key = e.queueScan(self, DA_MOVE, spec, head, hasHead ? curSkip : 0, tail, nTail, cands);
+    if (key < 0) return true;  // every queued source exhausted; none is re-enqueued
+    const int span = e.dev->queueSpan();
+    const int64_t row = key / N;
+    const int i = (int)(row / span), idx = (int)(row % span);
+    const int cb = i < hasHead ? head : tail[i - hasHead];
+    const int r = e.dev->qdirRows(cb)[idx];
+    const int hitSize = e.dev->qdirLen(cb);
+    const int polled = i < hasHead ? 0 : i - hasHead + 1;
+    if (run) pq.skipRun((size_t)polled);
+    else
+      for (int t = nTail; t-- > polled;) pq.unpoll(merged[t]);
+    m.relocateReplica(m.rPart[r], cb, b);
+    if (++nl >= lower) return false;
+    if (!pq.empty() && m.bNlead[cb] < m.bNlead[pq.peek()]) {
+      pq.add(cb);
+      curCb = -1;
+    } else if (idx + 1 < hitSize) {
+      curCb = cb;  // the view without the moved replica, from the same index
+      curSkip = idx;
+    } else {
+      curCb = -1;
+    }
+  }
+  return true;
+}
 
 // ======================================================================================= LeaderBytesInDistributionGoal
 class LeaderBytesIn : public GoalImpl {
