@@ -641,7 +641,10 @@ int64_t Device::serverRun(const DevProgram& prog, const Staged& g, int op, const
 bool Device::serverChain(const DevProgram& prog, int mode, const int32_t* a0, int n0, const int32_t* a1, int n1,
                          const int32_t* a2, int n2, int n, int m, int maxAccepts) {
   if (!serverUsable_ || !serverAllowed_ || !dRLoad_) return false;
+  const auto tS = prof().on ? std::chrono::steady_clock::now() : std::chrono::steady_clock::time_point();
   const size_t nl = lrows.size(), ns = srows.size();
+  lrowsSent_ = nl;
+  srowsSent_ = ns;
   const size_t words = (size_t)n0 + n1 + n2;
   const size_t oRows = align16(sizeof(DevProgram));
   const Staged g = packUpdates(0);
@@ -699,6 +702,8 @@ bool Device::serverChain(const DevProgram& prog, int mode, const int32_t* a0, in
   c.chainLog = (unsigned long long)(uintptr_t)hChainLogDev_;
   c.chainOut = (unsigned long long)(uintptr_t)hChainOutDev_;
   // a chain writes the tables: every later command's workgroups acquire before reading them
+  const auto tP = prof().on ? std::chrono::steady_clock::now() : std::chrono::steady_clock::time_point();
+  if (prof().on) prof().count(39, "chain.ns.stage", (int64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(tP - tS).count());
   if (!postCommand(c, true)) {
     unpackUpdates(g);
     return false;
@@ -1687,7 +1692,15 @@ Device::ChainResult Device::chainPairs(const DevProgram& prog, const int32_t* pr
   }
   ensureChainLog((size_t)n);
   // the running server takes the chain as a command (no stop and relaunch around it); otherwise one launch
+  const auto tw = prof().on ? std::chrono::steady_clock::now() : std::chrono::steady_clock::time_point();
   const bool served = serverChain(prog, CM_PAIRS, pr, n, pb, n, next, n, n, 0, maxAccepts);
+  if (prof().on) {
+    prof().count(36, "chain.ns.command",
+                 (int64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - tw)
+                     .count());
+    prof().count(37, "chain.lrows", (int64_t)lrowsSent_);
+    prof().count(38, "chain.srows", (int64_t)srowsSent_);
+  }
   if (!served) {
     stopServer();
     const size_t oB = align16((size_t)n * 4), oN = oB + align16((size_t)n * 4), req = oN + align16((size_t)n * 4);

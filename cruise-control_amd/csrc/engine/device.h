@@ -334,6 +334,7 @@ class Device {
   unsigned long long chainDelayTicks_ = 0;
   unsigned long long parkTicks_ = 100000ull;  // 1 ms: a shard-group scan waiting longer parks the server
   bool parkedPending_ = false;                // waitMail saw the server park with the awaited command
+  size_t lrowsSent_ = 0, srowsSent_ = 0;      // CCMI_PROFILE: the last chain command's load / slot rows
   void retireParkedServer();
   bool claimServer();
   std::unordered_map<uint64_t, int64_t> lastDepth_;

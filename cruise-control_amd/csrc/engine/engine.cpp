@@ -516,11 +516,26 @@ GoalImpl* Engine::optimizedOfKind(int kind) const {
 int64_t Engine::chainPairs(GoalImpl& self, int action, const std::vector<int32_t>& pr, const std::vector<int32_t>& pb,
                            const std::vector<int32_t>& next, int maxAccepts, std::vector<int32_t>& log) {
   PhaseScope ps(PH_DEV_SCAN);
+  const bool tp = prof().on;  // CCMI_PROFILE: ns in the row flushes, the program, the device round trip
+  auto tnow = [] { return std::chrono::steady_clock::now(); };
+  auto ns = [](std::chrono::steady_clock::time_point a, std::chrono::steady_clock::time_point b) {
+    return (int64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(b - a).count();
+  };
+  const auto c0 = tp ? tnow() : std::chrono::steady_clock::time_point();
   m.flushToDevice();
   m.flushChainLoads();
+  const auto c1 = tp ? tnow() : c0;
   const DevProgram prog = program(self, action);
+  const auto c2 = tp ? tnow() : c0;
   const Device::ChainResult r =
       dev->chainPairs(prog, pr.data(), pb.data(), next.data(), (int)pr.size(), maxAccepts, log);
+  if (tp) {
+    const auto c3 = tnow();
+    prof().count(32, "chain.ns.flush", ns(c0, c1));
+    prof().count(33, "chain.ns.program", ns(c1, c2));
+    prof().count(34, "chain.ns.device", ns(c2, c3));
+    prof().count(35, "chain.calls", 1);
+  }
   if (prog.exclLeadMove || prog.newOnly) {
     // the device counts every pair it passes; the reference never visits the blocked ones (the filters are static
     // over a leadership chain: original brokers, NEW states and exclusions do not change)
