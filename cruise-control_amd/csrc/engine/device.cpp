@@ -475,7 +475,12 @@ int Device::serverProgram(const DevProgram& prog, char* pay) {
 // sequence word) and wait for its result. false: the server's idle watchdog ended it before it saw the command —
 // nothing of the command ran, and the caller takes its launch path.
 bool Device::postCommand(ServerCmd& c, bool rowsSent) {
+  const bool tp = prof().on && c.op == SOP_CHAIN;  // CCMI_PROFILE: a chain command's busy-record wait and round trip
+  const auto tA = tp ? std::chrono::steady_clock::now() : std::chrono::steady_clock::time_point();
   collectServerBusy();
+  if (tp)
+    prof().count(40, "chain.ns.busywait",
+                 (int64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - tA).count());
   if (!claimServer()) return false;  // parked after its last command: the caller takes its launch path
   c.rowsEpoch = rowsEpoch_;
   *(volatile unsigned long long*)fg_ = (seq_ + 1) | kSeqBusy;
@@ -486,7 +491,11 @@ bool Device::postCommand(ServerCmd& c, bool rowsSent) {
   lastCmdSeq_ = ++seq_;
   *(volatile unsigned long long*)fg_ = lastCmdSeq_;
   hostStoreFence();
+  const auto tW = tp ? std::chrono::steady_clock::now() : std::chrono::steady_clock::time_point();
   const bool seen = waitMail(seq_, true);
+  if (tp)
+    prof().count(41, "chain.ns.roundtrip",
+                 (int64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - tW).count());
   if (parkedPending_) {  // the result came after the server parked (a slow shard group): retire the ended launch
     parkedPending_ = false;
     retireParkedServer();
