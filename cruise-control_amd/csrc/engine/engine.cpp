@@ -2008,7 +2008,10 @@ class ResourceDistribution : public GoalImpl {
     struct Group {
       int c;
       std::vector<int32_t> rbs;
-      std::vector<std::pair<int64_t, int32_t>> byIdx;  // (view index of rbs[k]'s partition leader, k), sorted
+      // (view index, leader replica) of each rbs[k]'s partition leader on c, sorted: recomputed whenever c's version
+      // changes — which every accept from c does (the moved partition's leader is then b, excluded at the refresh),
+      // and leaders move only by this loop's accepts — so between refreshes the rows need no model lookups
+      std::vector<std::pair<int64_t, int32_t>> byIdx;
       uint32_t ver = ~0u;
     };
     std::vector<Group> groups;
@@ -2040,15 +2043,14 @@ class ResourceDistribution : public GoalImpl {
           if (m.rLeader[rb]) continue;  // b leads that partition now: no leader row elsewhere
           const int lr = m.pLeader[m.rPart[rb]];
           if (m.rBroker[lr] != g.c || !m.selects(spec, lr)) continue;
-          g.byIdx.push_back({(int64_t)indexOf(g.c, lr), (int32_t)k});
+          g.byIdx.push_back({(int64_t)indexOf(g.c, lr), (int32_t)lr});
         }
         std::sort(g.byIdx.begin(), g.byIdx.end());
         g.ver = m.bVer[g.c];
       }
       for (const auto& e : g.byIdx) {
-        if (m.rLeader[g.rbs[e.second]]) continue;
         if (g.c == curCb && (size_t)e.first < curSkip) continue;
-        rows.push_back({g.c, (size_t)e.first, m.pLeader[m.rPart[g.rbs[e.second]]]});
+        rows.push_back({g.c, (size_t)e.first, e.second});
       }
     };
     while (curCb >= 0 || (!pq.empty() && cond())) {
