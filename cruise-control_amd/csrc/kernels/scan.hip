@@ -1691,18 +1691,10 @@ struct DevApply {
 };
 
 
-// The finish fields of a move (apply.h finish lanes) spread over waves 1..3 — a wave runs only lanes that take the same
-// code path (the source and destination sides by address), so no wave serializes divergent paths of loads:
-//   wave 1 lanes 0/1: broker counts of src / dst; lanes 2/3: topic leader counts of src / dst
-//   wave 2 lane 0: Partition slots (and leader);   wave 3 lane 0: the partition record
-template <class S>
-__device__ __forceinline__ void leadershipFinishWaves(S& s, int t, int p, int dr, int dpos, int src, int dst) {
-  const int w = t >> 6, l = t & 63;
-  if (w == 1 && l < 2) s.brk(l == 0 ? src : dst).nlead += l == 0 ? -1 : 1;
-  else if (w == 1 && l < 4) s.topicLeadAdd(s.part(p).topic, l == 2 ? src : dst, l == 2 ? -1 : 1);
-  else if (w == 2 && l == 0) applyLeadershipFinishLane(s, 2, p, dr, dpos, src, dst);
-  else if (w == 3 && l == 0) applyLeadershipFinishLane(s, 3, p, dr, dpos, src, dst);
-}
+// The finish fields of a replica move (apply.h finish lanes) spread over waves 1..3 — a wave runs only lanes that take
+// the same code path (the source and destination sides by address), so no wave serializes divergent paths of loads:
+//   wave 1 lanes 0/1: broker counts of src / dst; 2/3: topic counts; 4/5: topic leader counts
+//   wave 2 lane 0: the replica's broker;   wave 3 lane 0: its partition slot
 template <class S>
 __device__ __forceinline__ void replicaFinishWaves(S& s, int t, int r, int p, int src, int dst, bool lead) {
   const int w = t >> 6, l = t & 63;
@@ -1722,9 +1714,11 @@ __device__ __forceinline__ void replicaFinishWaves(S& s, int t, int r, int p, in
 }
 
 // Apply one move with the whole workgroup; every thread calls it. Replica move: the apply.h lanes on threads 0..5
-// (broker, potential and leadership-NW loads) and the host lanes on 6..7, one step; then the finish lanes (counts,
-// replica, partition slots, topic counts) in parallel, with the host utilizations. Leadership: every aggregate of the
-// move has its own lane, which loads it into registers at the first step (one memory round trip for all of them):
+// (broker, potential and leadership-NW loads) and the host lanes on 6..7, one step, beside the finish lanes (counts,
+// replica, partition slots, topic counts) on waves 1-3; then the host utilizations. Leadership: the finish fields no
+// step touches (leader / topic leader counts, slots) run on waves 1-2 from the start, the partition record on wave 3
+// after step 1; every aggregate of the move has its own lane, which loads it into registers at the first step (one
+// memory round trip for all of them):
 //   lane 0 leadership NW load of src (-= sr's old load)        lane 1 sr's load (makeFollower -> delta, new load)
 //   lane 2 Broker.load() of src (-= delta)                     lane 3 Broker.load() of dst (+= delta)
 //   lane 4 dr's load (+= delta, -> scratch for lane 5)         lane 5 leadership NW load of dst (+= dr's new load)
@@ -1752,10 +1746,30 @@ __device__ void chainApply(const ChainTables& C, LoadVec* sc, int action, int r,
                    : t == 4 ? &S.rLoad(dr)
                    : t == 5 ? &S.bLnw(dst)
                             : (hosts ? &S.hLoad(t == 6 ? hs : hd) : &S.bLnw(src));
+    // The finish fields that no step reads or writes run from the start on waves 1 and 2, beside the steps: the leader
+    // and topic leader counts of src and dst (wave 1, one lane per side) and the partition's slots and leader (wave 2).
+    // Wave 3 loads the partition record's broker and rack pairs now and writes the swap after step 1, with the leader
+    // NW_OUT the record keeps: dr's new load (scratch(1), the value lane 4 stores into dr's record).
+    const int w = t >> 6, l = t & 63;
+    if (w == 1 && l < 2) S.brk(l == 0 ? src : dst).nlead += l == 0 ? -1 : 1;
+    else if (w == 1 && l < 4) S.topicLeadAdd(S.part(p).topic, l == 2 ? src : dst, l == 2 ? -1 : 1);
+    else if (w == 2 && l == 0) applyLeadershipFinishLane(S, 2, p, dr, dpos, src, dst);
+    const bool recLane = w == 3 && l == 0;
+    int b0 = 0, bd = 0;
+    int16_t k0 = 0, kd = 0;
+    if (recLane) {
+      const PartitionRec& prc = S.part(p);
+      b0 = prc.brokers[0];
+      bd = prc.brokers[dpos];
+      k0 = prc.racks[0];
+      kd = prc.racks[dpos];
+    }
     LoadVec x, o;
-    // step 0: every lane's aggregate into registers (lane 0 also sr's load); lanes 0 and 1 compute
+    // step 0: every lane's aggregate into registers (lane 0 also sr's load, lanes 1 and 4 their replica's flags);
+    // lanes 0 and 1 compute
     if (active) ldCopy(x, *agg, W);
     if (t == 0) ldCopy(o, S.rLoad(sr), W);
+    const int32_t flags0 = (t == 1 || t == 4) ? S.rep(t == 1 ? sr : dr).flags : 0;
     if (t == 0) {
       ldAddSignedAll(x, o, W, true);
       ldCopy(*agg, x, W);
@@ -1775,8 +1789,7 @@ __device__ void chainApply(const ChainTables& C, LoadVec* sc, int action, int r,
     if (active && t >= 1 && t != 5) ldCopy(*agg, x, W);  // lane 1: sr's new load (makeFollower's result)
     if (t == 1 || t == 4) {
       ReplicaRec& rec = S.rep(t == 1 ? sr : dr);
-      if (t == 1) rec.flags &= ~(int32_t)RF_LEADER;
-      else rec.flags |= (int32_t)RF_LEADER;
+      rec.flags = t == 1 ? (flags0 & ~(int32_t)RF_LEADER) : (flags0 | (int32_t)RF_LEADER);
       for (int k = 0; k < 4; ++k) rec.util[k] = ldUtil(x, k, W);
       if (t == 4) ldCopy(S.scratch(1), x, W);  // dr's new load, for lane 5
     } else if (t == 2 || t == 3) {
@@ -1786,14 +1799,20 @@ __device__ void chainApply(const ChainTables& C, LoadVec* sc, int action, int r,
         for (int k = 0; k < 3; ++k) rec.hutil[k] = rec.util[k];
     }
     chainSync();
-    // step 2: dst's leadership NW load; the finish lanes (another wave); the host utilizations
+    // step 2: dst's leadership NW load; the partition record (wave 3); the host utilizations
     if (t == 5) {
       ldCopy(o, S.scratch(1), W);
       ldAddSignedAll(x, o, W, false);
       ldCopy(*agg, x, W);
       S.brk(dst).lbi = ldUtil(x, R_NW_IN, W);
-    } else {
-      leadershipFinishWaves(S, t, p, dr, dpos, src, dst);
+    } else if (recLane) {
+      PartitionRec& prc = S.part(p);
+      prc.brokers[0] = bd;
+      prc.brokers[dpos] = b0;
+      prc.racks[0] = kd;
+      prc.racks[dpos] = k0;
+      ldCopy(o, S.scratch(1), W);
+      prc.leadNwOut = ldUtil(o, R_NW_OUT, W);
     }
     if (hosts) applyHostUtil(S, src, dst, t, (int)blockDim.x);
   } else {
