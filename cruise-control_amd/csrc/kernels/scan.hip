@@ -893,11 +893,18 @@ __device__ __forceinline__ void chainSync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
 }
 
+// The accepted pair of a chain decision as its evaluating lane saw it (LDS): the apply starts from these instead of
+// re-reading the request, the replica record and the partition record (three dependent loads on its critical path).
+struct ChainWin {
+  int r, dst, src, p, flags;
+  int spos, dpos;  // src's and dst's positions in the partition's broker list (-1: not in it)
+};
+
 // K7 chain bodies (defined with the chain kernels below; SOP_CHAIN runs them inside the server)
 __device__ __forceinline__ void chainPairsRun(const DevTables& T, const ChainTables& C, const DevProgram& prog, const OverlayLds& ov,
                               LoadVec* sc, const int32_t* __restrict__ pr, const int32_t* __restrict__ pb,
                               const int32_t* __restrict__ next, int n, int maxAccepts, int32_t* __restrict__ log,
-                              ChainResultDev* __restrict__ out);
+                              ChainResultDev* __restrict__ out, ChainWin* win);
 __device__ __forceinline__ void chainRackRowsRun(const DevTables& T, const ChainTables& C, const DevProgram& prog,
                                  const OverlayLds& ov, LoadVec* sc, const int32_t* __restrict__ rows, int n,
                                  const int32_t* __restrict__ cands, int N, int32_t* __restrict__ log,
@@ -907,6 +914,7 @@ __device__ __forceinline__ void chainRackRowsRun(const DevTables& T, const Chain
 // directly, so no LDS address is passed across the call.
 __shared__ OverlayLds gSrvOv;
 __shared__ DevProgram gSrvProg;
+__shared__ ChainWin gSrvWin;  // a chain decision's winner, from its evaluating lane to the apply
 alignas(8) __shared__ unsigned char gSrvScRaw[2 * sizeof(LoadVec)];  // a chain's leadership hand-over (LoadVec has a
                                                                       // member initializer)
 
@@ -983,7 +991,8 @@ __device__ __attribute__((noinline)) void serverChain(const DevTables T, const C
   int32_t* log = reinterpret_cast<int32_t*>(c.chainLog);
   ChainResultDev* out = reinterpret_cast<ChainResultDev*>(c.chainOut);
   if (c.chainMode == CM_PAIRS)
-    chainPairsRun(T, C, prog, ov, sc, req, req + c.chainN, req + 2 * c.chainN, c.chainN, c.maxAccepts, log, out);
+    chainPairsRun(T, C, prog, ov, sc, req, req + c.chainN, req + 2 * c.chainN, c.chainN, c.maxAccepts, log, out,
+                  &gSrvWin);
   else
     chainRackRowsRun(T, C, prog, ov, sc, req, c.chainN, req + c.chainN, c.chainM, log, out);
 }
@@ -1725,15 +1734,31 @@ __device__ __forceinline__ void replicaFinishWaves(S& s, int t, int r, int p, in
 //   lanes 6, 7 the hosts (Host.makeFollower / makeLeader)
 // the same operations on the same values, in the order apply.h's sequential form (the emulation) runs them.
 template <int WC>
-__device__ void chainApply(const ChainTables& C, LoadVec* sc, int action, int r, int dst) {
+__device__ void chainApply(const ChainTables& C, LoadVec* sc, int action, int r, int dst, const ChainWin* win) {
   DevApply<WC> S{C, sc};
-  const ReplicaRec rr = C.replicas[r];
-  const int src = rr.broker, p = rr.part;
+  int src, p, rflags;
+  if (win) {  // the evaluating lane's view of the winner (same records, read in this decision's evaluation)
+    src = win->src;
+    p = win->p;
+    rflags = win->flags;
+  } else {
+    const ReplicaRec rr = C.replicas[r];
+    src = rr.broker;
+    p = rr.part;
+    rflags = rr.flags;
+  }
   const int t = threadIdx.x;
   constexpr int W = WC;
   if (action == DA_LEADERSHIP) {
     int sr, dr, dpos;
-    leadershipReplicas(S, p, src, dst, sr, dr, dpos);
+    if (win && win->spos >= 0 && win->dpos >= 0) {  // the two slots directly (leadershipReplicas' result)
+      const int o = C.pOff[p];
+      sr = C.pSlots[o + win->spos];
+      dr = C.pSlots[o + win->dpos];
+      dpos = win->dpos;
+    } else {
+      leadershipReplicas(S, p, src, dst, sr, dr, dpos);
+    }
     // lane -> its aggregate, chosen by address (one load / store instruction stream for all lanes, no divergence)
     const bool hosts = S.hostsOn();
     const int hs = hosts ? S.host(src) : 0, hd = hosts ? S.host(dst) : 0;
@@ -1816,7 +1841,7 @@ __device__ void chainApply(const ChainTables& C, LoadVec* sc, int action, int r,
     }
     if (hosts) applyHostUtil(S, src, dst, t, (int)blockDim.x);
   } else {
-    const bool lead = (rr.flags & RF_LEADER) != 0;
+    const bool lead = (rflags & RF_LEADER) != 0;
     const int lr = C.pLeader[p];
     if (t < kReplicaLanes) applyReplicaLane(S, t, r, src, dst, lr, lead);
     else if (t < kReplicaLanes + kHostLanes) applyHostReplicaLane(S, t - kReplicaLanes, r, src, dst);
@@ -1829,13 +1854,14 @@ __device__ void chainApply(const ChainTables& C, LoadVec* sc, int action, int r,
   }
   chainSync();
 }
-__device__ __forceinline__ void chainApplyAny(const ChainTables& C, LoadVec* sc, int action, int r, int dst) {
+__device__ __forceinline__ void chainApplyAny(const ChainTables& C, LoadVec* sc, int action, int r, int dst,
+                                              const ChainWin* win = nullptr) {
   switch (C.W) {  // block-uniform
-    case 1: chainApply<1>(C, sc, action, r, dst); break;
-    case 2: chainApply<2>(C, sc, action, r, dst); break;
-    case 3: chainApply<3>(C, sc, action, r, dst); break;
-    case 4: chainApply<4>(C, sc, action, r, dst); break;
-    default: chainApply<5>(C, sc, action, r, dst); break;
+    case 1: chainApply<1>(C, sc, action, r, dst, win); break;
+    case 2: chainApply<2>(C, sc, action, r, dst, win); break;
+    case 3: chainApply<3>(C, sc, action, r, dst, win); break;
+    case 4: chainApply<4>(C, sc, action, r, dst, win); break;
+    default: chainApply<5>(C, sc, action, r, dst, win); break;
   }
 }
 
@@ -1844,23 +1870,38 @@ __device__ __forceinline__ void chainApplyAny(const ChainTables& C, LoadVec* sc,
 // single tile, with the conjunction's latency split over the SIMDs.
 __device__ __forceinline__ unsigned long long chainFirstPair(const DevTables& T, const DevProgram& prog,
                                                              const OverlayLds& ov, const int32_t* pr,
-                                                             const int32_t* pb, int start, int n) {
+                                                             const int32_t* pb, int start, int n, ChainWin* win) {
   const int nGoals = prog.nGoals;
   for (int base = start; base < n;) {
     const int rest = n - base;
     const int parts = (rest <= 64 && nGoals >= 4) ? 4 : ((rest <= 128 && nGoals >= 2) ? 2 : 1);  // block-uniform
     const int wave = (int)(threadIdx.x >> 6);
     const int part = wave % parts;
-    const int q = base + (wave / parts) * 64 + (int)(threadIdx.x & 63);
+    const int slot = (wave / parts) * 64 + (int)(threadIdx.x & 63);
+    const int q = base + slot;
     bool ok = false;
+    PreView v;
     if (q < n) {
-      PreView v;
       v.loadDst(T, pb[q], ov);
       v.loadRow(T, prog, pr[q], ov);
       ok = !v.exclLeadBlocked(prog) && moveCandidateAcceptedPart(prog, v, v.r, v.dst, part, parts);
     }
     const int f = tileFirst(ok, parts);
-    if (f >= 0) return (unsigned long long)(base + f);
+    if (f >= 0) {
+      if (slot == f && part == 0) {  // the winner's lane hands its view of the pair to the apply
+        int sp = -1, dp = -1;
+        const int bs[8] = {v.pb0, v.pb1, v.pb2, v.pb3, v.pb4, v.pb5, v.pb6, v.pb7};
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+          if (i < v.pn) {
+            if (bs[i] == v.src) sp = i;
+            if (bs[i] == v.dst) dp = i;
+          }
+        *win = ChainWin{v.r, v.dst, v.src, v.p, v.rflags, sp, dp};
+      }
+      __syncthreads();
+      return (unsigned long long)(base + f);
+    }
     base += kBlock / parts;
   }
   return kNone;
@@ -1873,7 +1914,7 @@ __device__ __forceinline__ void chainPairsRun(const DevTables& T, const ChainTab
                                               const OverlayLds& ov, LoadVec* sc, const int32_t* __restrict__ pr,
                                               const int32_t* __restrict__ pb, const int32_t* __restrict__ next, int n,
                                               int maxAccepts, int32_t* __restrict__ log,
-                                              ChainResultDev* __restrict__ out) {
+                                              ChainResultDev* __restrict__ out, ChainWin* win) {
   int start = 0, acc = 0;
   unsigned long long visited = 0;
   // CCMI_STAMPS: thread 0 sums the time in candidate evaluation and in applying moves (stamps[8200 .. 8203])
@@ -1881,7 +1922,7 @@ __device__ __forceinline__ void chainPairsRun(const DevTables& T, const ChainTab
   unsigned long long tEval = 0, tApply = 0, t = st ? __builtin_amdgcn_s_memrealtime() : 0;
   const unsigned long long tStart = t;
   while (start < n && acc < maxAccepts) {
-    const unsigned long long best = chainFirstPair(T, prog, ov, pr, pb, start, n);
+    const unsigned long long best = chainFirstPair(T, prog, ov, pr, pb, start, n, win);
     if (st) {
       const unsigned long long u = __builtin_amdgcn_s_memrealtime();
       tEval += u - t;
@@ -1894,7 +1935,7 @@ __device__ __forceinline__ void chainPairsRun(const DevTables& T, const ChainTab
     visited += best - (unsigned long long)start + 1;
     const int q = (int)best;
     if (threadIdx.x == 0) log[acc] = q;
-    chainApplyAny(C, sc, prog.action, pr[q], pb[q]);
+    chainApplyAny(C, sc, prog.action, win->r, win->dst, win);
     if (st) {
       __builtin_amdgcn_s_waitcnt(0);
       const unsigned long long u = __builtin_amdgcn_s_memrealtime();
@@ -1924,9 +1965,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, kServ
                                                       int32_t* __restrict__ log, ChainResultDev* __restrict__ out) {
   __shared__ OverlayLds ov;
   __shared__ alignas(8) unsigned char scRaw[2 * sizeof(LoadVec)];  // LoadVec has a member initializer
+  __shared__ ChainWin win;
   if (threadIdx.x == 0) ov.nb = ov.nr = ov.np = 0;
   __syncthreads();
-  chainPairsRun(T, C, prog, ov, reinterpret_cast<LoadVec*>(scRaw), pr, pb, next, n, maxAccepts, log, out);
+  chainPairsRun(T, C, prog, ov, reinterpret_cast<LoadVec*>(scRaw), pr, pb, next, n, maxAccepts, log, out, &win);
 }
 
 // RACK_ROWS: AbstractRackAwareGoal.rebalanceForBroker (AbstractRackAwareGoal.java:144-170) over the rows of every
