@@ -1995,7 +1995,7 @@ class ResourceDistribution : public GoalImpl {
     auto snap = [&](int c) -> const std::vector<int32_t>& {
       return dir ? e.dev->qdirRows(c) : m.snapshotIn(snapTab, c, spec);
     };
-    auto size = [&](int c) { return snap(c).size(); };
+    auto size = [&](int c) { return dir ? e.dev->qdirRows(c).size() : m.viewSize(snapTab, c, spec); };
     auto indexOf = [&](int c, int r) {
       const auto& v = snap(c);
       const uint64_t k = m.replicaKey(spec, r);
@@ -2004,16 +2004,19 @@ class ResourceDistribution : public GoalImpl {
     };
     // b's follower replicas grouped by the broker leading their partition (leaders move only by this loop's accepts,
     // which make b the leader): a group's rows change only when its broker's view changes (version) or b leads one of
-    // its partitions, so the rows' view indices are cached per group and recomputed only then
+    // its partitions, so the rows' view order is cached per group and recomputed only then
     struct Group {
       int c;
       std::vector<int32_t> rbs;
-      // (view index, leader replica) of each rbs[k]'s partition leader on c, sorted: recomputed whenever c's version
-      // changes — which every accept from c does (the moved partition's leader is then b, excluded at the refresh),
-      // and leaders move only by this loop's accepts — so between refreshes the rows need no model lookups
-      std::vector<std::pair<int64_t, int32_t>> byIdx;
+      // (sort key, leader replica) of each rbs[k]'s partition leader on c, sorted — c's view order, the view being
+      // sorted by the unique Model::replicaKey — recomputed whenever c's version changes (which every accept from c
+      // does: the moved partition's leader is then b, excluded at the refresh; leaders move only by this loop's
+      // accepts), so between refreshes the rows need no model lookups. A row's view index itself is looked up only
+      // for the current broker's rows and the winner's.
+      std::vector<std::pair<uint64_t, int32_t>> byKey;
       uint32_t ver = ~0u;
     };
+    constexpr size_t kNoIdx = ~(size_t)0;
     std::vector<Group> groups;
     // The groups in poll order (the queue's reversed broker comparator). Only cb's key changes between scans (leadership
     // moves cb -> b; b leads none of these partitions' leaders), so after an accept cb's group alone is re-placed and
@@ -2023,6 +2026,7 @@ class ResourceDistribution : public GoalImpl {
     auto before = [&](int gx, int gy) { return cmpBroker(m, groups[gy].c, groups[gx].c) < 0; };
     {
       PhaseScope pf(PH_FLATTEN);
+      NsScope ns(42, "lead.in.ns.setup");
       std::vector<std::pair<int, int>> lb;
       for (int rb : m.bRepl[b])
         if (!m.rLeader[rb]) lb.push_back({m.rBroker[m.pLeader[m.rPart[rb]]], rb});
@@ -2035,27 +2039,34 @@ class ResourceDistribution : public GoalImpl {
       for (size_t i = 0; i < groups.size(); ++i) order[i] = (int)i;
       std::sort(order.begin(), order.end(), before);
     }
-    auto emit = [&](Group& g) {  // the group's rows in view order (its view indices recomputed on a new version)
+    auto emit = [&](Group& g) {  // the group's rows in view order (recomputed on a new version)
       if (g.ver != m.bVer[g.c]) {
-        g.byIdx.clear();
+        NsScope ns(43, "lead.in.ns.refresh");
+        prof().count(44, "lead.in.refreshes");
+        g.byKey.clear();
         for (size_t k = 0; k < g.rbs.size(); ++k) {
           const int rb = g.rbs[k];
           if (m.rLeader[rb]) continue;  // b leads that partition now: no leader row elsewhere
           const int lr = m.pLeader[m.rPart[rb]];
           if (m.rBroker[lr] != g.c || !m.selects(spec, lr)) continue;
-          g.byIdx.push_back({(int64_t)indexOf(g.c, lr), (int32_t)lr});
+          g.byKey.push_back({m.replicaKey(spec, lr), (int32_t)lr});
         }
-        std::sort(g.byIdx.begin(), g.byIdx.end());
+        std::sort(g.byKey.begin(), g.byKey.end());
         g.ver = m.bVer[g.c];
       }
-      for (const auto& e : g.byIdx) {
-        if (g.c == curCb && (size_t)e.first < curSkip) continue;
-        rows.push_back({g.c, (size_t)e.first, e.second});
+      if (g.c == curCb) {  // the current broker's view resumes at index curSkip (reference iteratedIndices)
+        for (const auto& e : g.byKey) {
+          const size_t idx = indexOf(g.c, e.second);
+          if (idx >= curSkip) rows.push_back({g.c, idx, e.second});
+        }
+        return;
       }
+      for (const auto& e : g.byKey) rows.push_back({g.c, kNoIdx, e.second});
     };
     while (curCb >= 0 || (!pq.empty() && cond())) {
       {
         PhaseScope pf(PH_FLATTEN);
+        NsScope ns(47, "lead.in.ns.rows");
         rows.clear();
         if (curCb >= 0)  // the current broker's remaining view first
           for (Group& g : groups)
@@ -2074,7 +2085,15 @@ class ResourceDistribution : public GoalImpl {
       const int64_t key = rows.empty() ? -1 : e.pairScan(*this, pr, pb, DA_LEADERSHIP, false);
       // reference-equivalent rows visited up to the accepted row (or everything left when nothing is accepted)
       int64_t visited = 0;
-      const Row* hit = key >= 0 ? &rows[(size_t)key] : nullptr;
+      Row hitRow{-1, 0, -1};
+      const Row* hit = nullptr;
+      if (key >= 0) {
+        hitRow = rows[(size_t)key];
+        if (hitRow.idx == kNoIdx) hitRow.idx = indexOf(hitRow.cb, hitRow.r);  // (the model is as the scan saw it)
+        hit = &hitRow;
+      }
+      {
+      NsScope ns(45, "lead.in.ns.polls");
       if (curCb >= 0) {
         if (hit && hit->cb == curCb) {
           visited += (int64_t)(hit->idx - curSkip + 1);
@@ -2086,7 +2105,36 @@ class ResourceDistribution : public GoalImpl {
       }
       if (!(hit && hit->cb == curCb)) {
         while (!pq.empty() && (hit || cond())) {
+          if (pq.runOnly() && !dir) {
+            // nothing re-added: the polls are the run's next brokers up to the hit's (cond() does not change while
+            // polling), summed in one pass
+            const int* run = pq.runData();
+            const size_t left = pq.runLeft();
+            size_t k = 0;
+            if (hit)
+              while (k < left && run[k] != hit->cb) ++k;
+            else
+              k = left;
+            if (k == left && hit) throw std::logic_error("moveInLeadership: the winner's broker is not queued");
+            m.bindSnapTable(snapTab, spec);
+            int64_t sum = 0;
+            for (size_t q = 0; q < k; ++q) {
+              queued[run[q]] = 0;
+              sum += (int64_t)m.viewSizeBound(snapTab, run[q]);
+            }
+            prof().count(46, "lead.in.polls", (int64_t)k + (hit ? 1 : 0));
+            visited += sum;
+            if (hit) {
+              queued[hit->cb] = 0;
+              visited += (int64_t)hit->idx + 1;
+              pq.skipRun(k + 1);
+            } else {
+              pq.skipRun(k);
+            }
+            break;
+          }
           const int c = pq.poll();
+          prof().count(46, "lead.in.polls");
           queued[c] = 0;
           if (hit && c == hit->cb) {
             visited += (int64_t)hit->idx + 1;
@@ -2094,6 +2142,7 @@ class ResourceDistribution : public GoalImpl {
           }
           visited += (int64_t)size(c);
         }
+      }
       }
       e.candidates += visited;
       if (!hit) break;
@@ -2110,12 +2159,17 @@ class ResourceDistribution : public GoalImpl {
           order.insert(order.begin() + (ptrdiff_t)j, gi);
           break;
         }
-      if (aboveLower(m, b)) return false;
+      if (aboveLower(m, b)) {
+        prof().count(3, "in.lead.done");
+        return false;
+      }
       if (!pq.empty() && m.pct(cb, res) < m.pct(pq.peek(), res)) {
+        prof().count(4, "in.lead.readd");
         pq.add(cb);
         queued[cb] = 1;
         curCb = -1;
       } else {
+        prof().count(5, "in.lead.continue");
         curCb = cb;
         curSkip = idx;
       }

@@ -363,23 +363,48 @@ class Model {
     Spec spec;
     const void* owner = nullptr;  // the Model the table was filled from
     bool bound = false;
+    uint32_t epoch = 0;         // selEpoch when bound
     std::vector<uint32_t> ver;  // bVer[b] + 1 of the stored snapshot, 0 = none
     std::vector<std::shared_ptr<const std::vector<int32_t>>> v;
+    // (bVer[b] + 1) << 32 | the snapshot's size, 0 = none: viewSize() without a snapshot
+    std::vector<uint64_t> size;
   };
-  const std::vector<int32_t>& snapshotIn(SnapTable& t, int b, const Spec& s) { return *snapshotInShared(t, b, s); }
-  const std::shared_ptr<const std::vector<int32_t>>& snapshotInShared(SnapTable& t, int b, const Spec& s) {
-    if (!t.bound || t.owner != this || !(t.spec == s)) {
+  void bindSnapTable(SnapTable& t, const Spec& s) {
+    if (!t.bound || t.owner != this || !(t.spec == s) || t.epoch != selEpoch) {
       t.spec = s;
       t.owner = this;
       t.bound = true;
+      t.epoch = selEpoch;
       t.ver.assign(B, 0);
       t.v.assign(B, nullptr);
+      t.size.assign(B, 0);
     }
+  }
+  const std::vector<int32_t>& snapshotIn(SnapTable& t, int b, const Spec& s) { return *snapshotInShared(t, b, s); }
+  const std::shared_ptr<const std::vector<int32_t>>& snapshotInShared(SnapTable& t, int b, const Spec& s) {
+    bindSnapTable(t, s);
     if (t.ver[b] != bVer[b] + 1u) {
       t.v[b] = snapshot(b, s);
       t.ver[b] = bVer[b] + 1u;
+      t.size[b] = ((uint64_t)t.ver[b] << 32) | (uint32_t)t.v[b]->size();
     }
     return t.v[b];
+  }
+  // snapshotIn(t, b, s).size() — the replicas of b that s selects — counted instead of sorted when the table holds no
+  // current snapshot of b (a polled broker's size is all a driver's visited count needs from it)
+  size_t viewSize(SnapTable& t, int b, const Spec& s) {
+    bindSnapTable(t, s);
+    return viewSizeBound(t, b);
+  }
+  // viewSize on a table bindSnapTable(t, s) bound to the same Spec since the last selection change
+  size_t viewSizeBound(SnapTable& t, int b) {
+    const uint32_t v = bVer[b] + 1u;
+    const uint64_t x = t.size[b];
+    if ((uint32_t)(x >> 32) == v) return (size_t)(uint32_t)x;
+    uint32_t n = 0;
+    for (int r : bRepl[b]) n += selects(t.spec, r) ? 1u : 0u;
+    t.size[b] = ((uint64_t)v << 32) | n;
+    return n;
   }
   bool selects(const Spec& s, int r) const;
   uint64_t replicaKey(const Spec& s, int r) const;

@@ -64,6 +64,23 @@ inline PhaseProf& prof() {
   return p;
 }
 
+// Adds the scope's nanoseconds to named counter i (CCMI_PROFILE only)
+struct NsScope {
+  int i;
+  const char* name;
+  bool on;
+  std::chrono::steady_clock::time_point t0;
+  NsScope(int idx, const char* n) : i(idx), name(n), on(prof().on) {
+    if (on) t0 = std::chrono::steady_clock::now();
+  }
+  ~NsScope() {
+    if (on)
+      prof().count(i, name,
+                   (int64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0)
+                       .count());
+  }
+};
+
 inline bool isDriverPhase(int p) {
   return p == PH_RDG_OUT || p == PH_RDG_IN || p == PH_RES_OUT || p == PH_RES_IN || p == PH_SWAP || p == PH_OTHER_GOALS ||
          p == PH_LEAD_OUT || p == PH_LEAD_IN || p == PH_REP_OUT || p == PH_REP_IN;
