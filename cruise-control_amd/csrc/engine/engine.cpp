@@ -1133,11 +1133,13 @@ class TreeWorker {
     th_.join();
   }
   // members in entry (key, id) order, over B brokers
-  void submit(const std::vector<int32_t>& order, int B) {
+  void submit(const std::vector<int32_t>& order, int B, bool withSequence) {
     {
       std::lock_guard<std::mutex> l(mu_);
       next_.assign(order.begin(), order.end());
       nextB_ = B;
+      nextSeq_ = withSequence;
+      tSubmit_ = std::chrono::steady_clock::now();
       ++gen_;
       cancel_.store(true, std::memory_order_relaxed);  // the build in flight (if any) is stale
     }
@@ -1147,9 +1149,18 @@ class TreeWorker {
   void cancel() { cancel_.store(true, std::memory_order_relaxed); }
   // the latest submission's tree (waits for it); its structure is handed over with RbTreeSet::adopt
   Tree& take() {
+    const auto tTake = std::chrono::steady_clock::now();
     std::unique_lock<std::mutex> l(mu_);
     const uint64_t want = gen_;
     cvDone_.wait(l, [&] { return done_ == want; });
+    if (prof().on) {  // CCMI_PROFILE: submit -> worker start, the build, submit -> take (ns)
+      auto ns = [](std::chrono::steady_clock::time_point a, std::chrono::steady_clock::time_point b) {
+        return (int64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(b - a).count();
+      };
+      prof().count(48, "tree.ns.wake", ns(tSubmit_, tStart_));
+      prof().count(49, "tree.ns.work", ns(tStart_, tDone_));
+      prof().count(50, "tree.ns.needed", ns(tSubmit_, tTake));
+    }
     return tree_;
   }
 
@@ -1164,8 +1175,10 @@ class TreeWorker {
         cv_.wait(l, [&] { return stop_ || gen_ != started; });
         if (stop_) return;
         gen = started = gen_;
+        tStart_ = std::chrono::steady_clock::now();
         order_.swap(next_);
         B_ = nextB_;
+        seq_ = nextSeq_;
         cancel_.store(false, std::memory_order_relaxed);
       }
       tree_.clear();
@@ -1178,10 +1191,11 @@ class TreeWorker {
       ids_.clear();
       for (int x = 0; x < B_; ++x)
         if (mark_[x]) ids_.push_back(x);
-      tree_.buildByRank(ids_, rank_, &cancel_);
+      tree_.buildByRank(std::move(ids_), std::move(rank_), &cancel_, seq_);
       if (!cancel_.load(std::memory_order_relaxed)) {
         {
           std::lock_guard<std::mutex> l(mu_);
+          tDone_ = std::chrono::steady_clock::now();
           done_ = gen;
         }
         cvDone_.notify_one();
@@ -1193,9 +1207,11 @@ class TreeWorker {
   std::vector<int> ids_;
   std::vector<uint8_t> mark_;
   int nextB_ = 0, B_ = 0;
+  bool nextSeq_ = true, seq_ = true;  // the tree's in-order sequence is wanted (RbTreeSet::buildByRank)
   uint64_t gen_ = 0;   // submissions (guarded by mu_)
   uint64_t done_ = 0;  // the submission whose tree is complete in tree_ (guarded by mu_)
   std::atomic<bool> cancel_{false};
+  std::chrono::steady_clock::time_point tSubmit_, tStart_, tDone_;  // (guarded by mu_)
   std::mutex mu_;
   std::condition_variable cv_, cvDone_;
   bool stop_ = false;
@@ -1509,7 +1525,8 @@ class ResourceDistribution : public GoalImpl {
     TreeLease lease;
     if (!(wEnv && wEnv[0] == '0') && m.B >= (minEnv ? std::atoi(minEnv) : 2048)) lease.w = TreeWorkerPool::get().lease();
     const bool useWorker = lease.w != nullptr;
-    if (useWorker) lease.w->submit(inorder, m.B);  // `inorder` is the members' entry (key, id) order
+    // `inorder` is the members' entry (key, id) order; the leadership form only searches the tree
+    if (useWorker) lease.w->submit(inorder, m.B, action != DA_LEADERSHIP);
     struct Step {
       int dst;
       double keyAfter;
@@ -1586,9 +1603,10 @@ class ResourceDistribution : public GoalImpl {
         cand.buildByRank(ids, rank);
       }
       auto t2 = tp ? tnow() : t0;
-      // the replay keeps no in-order sequence (each step would shift it); the replica-move form, which walks the set
-      // in order for every candidate list, takes it once afterwards; the leadership form only searches the set
-      cand.untrackSequence();
+      // The leadership form only searches the set: no in-order sequence. The replica-move form walks the set in order
+      // for every candidate list: the build's sequence is kept through a short replay (each step shifts it once),
+      // a long replay runs without it and the sequence is taken once afterwards (a walk over every node).
+      if (action == DA_LEADERSHIP || hist.size() > 4) cand.untrackSequence();
       prof().count(15, "tree.replay.steps", (int64_t)hist.size());
       for (const Step& h : hist) {
         for (auto& o : ovr) {

@@ -169,14 +169,17 @@ class RbTreeSet {
     std::vector<int32_t> r2(rank);
     buildByRank(std::move(i2), std::move(r2), cancel);
   }
-  void buildByRank(std::vector<int>&& ids, std::vector<int32_t>&& rank, const std::atomic<bool>* cancel = nullptr) {
-    buildStart(std::move(ids), std::move(rank));
+  // withSequence = false: the in-order sequence is not taken at the end (a tree that will only be searched)
+  void buildByRank(std::vector<int>&& ids, std::vector<int32_t>&& rank, const std::atomic<bool>* cancel = nullptr,
+                   bool withSequence = true) {
+    buildStart(std::move(ids), std::move(rank), withSequence);
     while (!buildStep(512))
       if (cancel && cancel->load(std::memory_order_relaxed)) return;
   }
   // The same build a bounded number of puts at a time (buildStep returns true once every put is done, then the
   // tree is complete); the tree must not be used before.
-  void buildStart(std::vector<int>&& ids, std::vector<int32_t>&& rank) {
+  void buildStart(std::vector<int>&& ids, std::vector<int32_t>&& rank, bool withSequence = true) {
+    bSeq_ = withSequence;
     n_.clear();
     free_.clear();
     root_ = -1;
@@ -225,6 +228,13 @@ class RbTreeSet {
     }
     bNext_ = end;
     if (bNext_ < bIds_.size()) return false;
+    building_ = false;
+    if (!bSeq_) {
+      seqOn_ = false;
+      seqId_.clear();
+      seqKey_.clear();
+      return true;
+    }
     // from here on the in-order sequence is maintained next to the tree (rotations do not change it)
     seqId_.clear();
     for (size_t wi = 0; wi < bW_.size(); ++wi)
@@ -317,7 +327,7 @@ class RbTreeSet {
   bool seqOn_ = false;
   std::vector<int> seqId_, seqKey_;  // node ids / keys in order (after buildByRank)
   // a build in progress (buildStart / buildStep): the put sequence, the next put, the two-level bitmap of put ranks
-  bool building_ = false;
+  bool building_ = false, bSeq_ = true;
   std::vector<int> bIds_;
   std::vector<int32_t> bRank_;
   size_t bNext_ = 0;

@@ -29,7 +29,7 @@ struct PhaseProf {
   }
   bool on = std::getenv("CCMI_PROFILE") != nullptr;
   // named event counters (diagnostics of the drivers' control flow)
-  static constexpr int kCounters = 48;
+  static constexpr int kCounters = 64;
   const char* counterName[kCounters] = {};
   int64_t counter[kCounters] = {};
   void count(int i, const char* name, int64_t d = 1) {
