@@ -849,6 +849,11 @@ class LiveQueue {
   int upcoming(size_t k) const { return ordered_ ? oq_.upcoming(k) : -1; }
   // ordered form with nothing re-added: the remaining poll order is a contiguous run (OrderedQueue::runData)
   bool runOnly() const { return ordered_ && oq_.heapEmpty(); }
+  // ordered form: the re-added heap's next element, its poll, and the run's elements that poll before x
+  bool heapEmpty() const { return oq_.heapEmpty(); }
+  int heapPeek() const { return oq_.heapPeek(); }
+  int heapPoll() { return oq_.heapPoll(); }
+  size_t runBefore(int x) const { return oq_.runBefore(x); }
   const int* runData() const { return oq_.runData(); }
   size_t runLeft() const { return oq_.runLeft(); }
   void skipRun(size_t k) { oq_.skipRun(k); }
@@ -2121,36 +2126,57 @@ class ResourceDistribution : public GoalImpl {
           curCb = -1;
         }
       }
-      if (!(hit && hit->cb == curCb)) {
-        while (!pq.empty() && (hit || cond())) {
-          if (pq.runOnly() && !dir) {
-            // nothing re-added: the polls are the run's next brokers up to the hit's (cond() does not change while
-            // polling), summed in one pass
-            const int* run = pq.runData();
-            const size_t left = pq.runLeft();
-            size_t k = 0;
-            if (hit)
-              while (k < left && run[k] != hit->cb) ++k;
-            else
-              k = left;
-            if (k == left && hit) throw std::logic_error("moveInLeadership: the winner's broker is not queued");
-            m.bindSnapTable(snapTab, spec);
-            int64_t sum = 0;
-            for (size_t q = 0; q < k; ++q) {
-              queued[run[q]] = 0;
-              sum += (int64_t)m.viewSizeBound(snapTab, run[q]);
+      if (!(hit && hit->cb == curCb) && pq.ordered() && !dir && (hit || cond())) {
+        // The polls up to the hit's broker (or all of them; cond() does not change while polling) in runs: the sorted
+        // run's brokers before the re-added heap's next one in one pass, then that one.
+        m.bindSnapTable(snapTab, spec);
+        int64_t sum = 0, polls = 0;
+        bool found = false;
+        auto takeRun = [&](size_t k) {
+          const int* run = pq.runData();
+          for (size_t q = 0; q < k; ++q) {
+            queued[run[q]] = 0;
+            sum += (int64_t)m.viewSizeBound(snapTab, run[q]);
+          }
+          pq.skipRun(k);
+          polls += (int64_t)k;
+        };
+        auto hitIn = [&](size_t k) {  // the hit's broker among the run's next k: its position, else k
+          const int* run = pq.runData();
+          size_t j = 0;
+          while (j < k && run[j] != hit->cb) ++j;
+          return j;
+        };
+        while (!pq.empty()) {
+          const bool heapEmpty = pq.heapEmpty();
+          const size_t k = heapEmpty ? pq.runLeft() : pq.runBefore(pq.heapPeek());
+          if (hit) {
+            const size_t j = hitIn(k);
+            if (j < k) {
+              takeRun(j);
+              pq.skipRun(1);
+              ++polls;
+              found = true;
+              break;
             }
-            prof().count(46, "lead.in.polls", (int64_t)k + (hit ? 1 : 0));
-            visited += sum;
-            if (hit) {
-              queued[hit->cb] = 0;
-              visited += (int64_t)hit->idx + 1;
-              pq.skipRun(k + 1);
-            } else {
-              pq.skipRun(k);
-            }
+          }
+          takeRun(k);
+          if (heapEmpty) break;
+          const int c = pq.heapPoll();
+          queued[c] = 0;
+          ++polls;
+          if (hit && c == hit->cb) {
+            found = true;
             break;
           }
+          sum += (int64_t)m.viewSizeBound(snapTab, c);
+        }
+        if (hit && !found) throw std::logic_error("moveInLeadership: the winner's broker is not queued");
+        prof().count(46, "lead.in.polls", polls);
+        visited += sum + (hit ? (int64_t)hit->idx + 1 : 0);
+        if (hit) queued[hit->cb] = 0;
+      } else if (!(hit && hit->cb == curCb)) {
+        while (!pq.empty() && (hit || cond())) {
           const int c = pq.poll();
           prof().count(46, "lead.in.polls");
           queued[c] = 0;

@@ -648,6 +648,13 @@ class OrderedQueue {
   // The sorted run's elements not yet polled (in poll order while the heap is empty), and skipping k of them: the
   // same as k polls when the heap is empty
   bool heapEmpty() const { return heap_.empty(); }
+  // the heap's next element and its poll; the sorted run's elements (from the poll position) that poll before x
+  int heapPeek() const { return heap_.peek(); }
+  int heapPoll() { return heap_.poll(); }
+  size_t runBefore(int x) const {
+    const auto b = s_.begin() + (ptrdiff_t)std::min(pos_, s_.size());
+    return (size_t)(std::partition_point(b, s_.end(), [&](int y) { return cmp_(x, y) >= 0; }) - b);
+  }
   const int* runData() const { return s_.data() + pos_; }
   size_t runLeft() const { return pos_ < s_.size() ? s_.size() - pos_ : 0; }
   void skipRun(size_t k) { pos_ += k; }
