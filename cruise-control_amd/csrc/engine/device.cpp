@@ -186,8 +186,12 @@ Device::Device(int ordinal, int B, int R, int P, int T, int maxGoalSlots)
       dalloc(&dServerT0_, 16);  // [0] busy-time stamp, [8] the doorbell (a line of its own)
       try {
         ensureFg(1 << 20);
-        // snapshot pool: 4M rows (64 MB), host-written like the command block
-        segCap_ = (size_t)4 << 20;
+        // snapshot pool: 16M rows (256 MB), host-written like the command block. A C2 proposal uploads ~10.6M rows
+        // of snapshots; every wrap restarts the server and re-sets the whole queue directory (4M rows wrapped 2-3
+        // times per proposal). CCMI_SNAPSHOT_POOL_ROWS sizes it (tests: a small pool wraps often).
+        segCap_ = (size_t)16 << 20;
+        if (const char* pr = std::getenv("CCMI_SNAPSHOT_POOL_ROWS"))
+          segCap_ = (size_t)std::max(1024ll, std::atoll(pr)) & ~(size_t)7;
         hipCheck(hipExtMallocWithFlags((void**)&segPool_, segCap_ * sizeof(RowRef), hipDeviceMallocFinegrained),
                  "hipExtMallocWithFlags snapshot pool");
       } catch (std::exception&) {

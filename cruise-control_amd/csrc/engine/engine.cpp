@@ -348,7 +348,11 @@ void Engine::queueSync(const Model::Spec& spec) {
   bool full = !q.bound || q.key != key || dev->qdirKey() != key || q.epoch != dev->poolEpoch();
   // the listed brokers' snapshots and their rows' upload, on the host pool (hostpool.h) when there are many
   auto setMany = [&](const std::vector<int32_t>& bs) {
-    m.snapshotMany(spec, bs, q.snaps);
+    {
+      NsScope ns(52, "queue.ns.snapshots");
+      m.snapshotMany(spec, bs, q.snaps);
+    }
+    NsScope ns(53, "queue.ns.uploads");
     if (!dev->qdirSetMany(bs, q.snaps)) throw Unsupported("a broker's snapshot exceeds the snapshot pool");
     q.snaps.clear();
   };

@@ -99,6 +99,14 @@ def test_gpu_scan_width_matches_oracle(gpu_lib, oracle_lib, monkeypatch, width):
                                  DEFAULT_GOALS, 1.05)
 
 
+def test_gpu_snapshot_pool_wraps_match_oracle(gpu_lib, oracle_lib, monkeypatch):
+    """A snapshot pool of 64K rows wraps many times per proposal (each wrap restarts the scan server and re-sets the
+    whole queue directory): the queue scans still read only current snapshots and decide exactly as the oracle."""
+    monkeypatch.setenv("CCMI_SNAPSHOT_POOL_ROWS", "65536")
+    check_product_against_oracle(gpu_lib, dict(num_racks=8, num_brokers=300, num_replicas=30000, num_topics=1000),
+                                 C1_GOALS, 1.05)
+
+
 @pytest.mark.parametrize("props", [dict(), dict(num_racks=20, num_brokers=1000, num_replicas=99999, num_topics=3000),
                                    dict(num_racks=3, num_brokers=10, num_replicas=3000, num_topics=100,
                                         num_dead_brokers=2)])
