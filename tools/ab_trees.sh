@@ -1,6 +1,7 @@
 #!/bin/bash
 # Same-box A/B over built trees (directories holding cruise-control_amd/ + tools/probe.py): one C2 proposal each with
-# server stamps, in the order given, twice. One gpurun call; stops at the first failure.
+# server stamps, in the order given, twice. One gpurun call; stops at the first failure. A tree such as ab_prev (a
+# `git worktree` of an older commit, built in place) must not be listed in .gpurunignore while it is compared.
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out
 for i in 1 2; do
