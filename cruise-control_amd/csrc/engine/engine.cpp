@@ -1285,6 +1285,7 @@ class ResourceDistribution : public GoalImpl {
   bool lowUtil = false;                   // _isLowUtilization
   ccmi_provision_recommendation overRec{};  // _overProvisionedRecommendation
   Model::SnapTable snapTab;  // moveIn's candidate-broker snapshots (one Spec per phase)
+  Model::SnapTable swapTab;  // the swap phase's polled brokers' limit-free snapshots
   std::vector<uint8_t> queued;  // moveIn: broker is in the candidate queue
   int nameBase() const { return 4 * kind; }
   int nameId(bool reverse, bool leader) const { return nameBase() + (reverse ? 1 : 0) + (leader ? 2 : 0); }
@@ -2252,6 +2253,7 @@ class ResourceDistribution : public GoalImpl {
     };
     {
       PhaseScope pi(PH_PQ_INIT);
+      NsScope ns(54, "swap.ns.pqinit");
       // candidates: out = alive brokers under the upper limit hosting replicas (a Collectors.toSet() whose
       // insertion order does not matter to a PriorityQueue); in = alive brokers above the lower limit
       auto member = [&](int x) {
@@ -2314,7 +2316,12 @@ class ResourceDistribution : public GoalImpl {
         cbOff.assign(1, 0);
         cbRep.clear();
         while (!pqEmpty() && (polled.empty() || polled.size() < target)) polled.push_back(pqPoll());
-        m.snapshotMany(baseSpec, polled, polledSnaps);  // (many polled brokers: their sorts on the host pool)
+        prof().count(57, "swap.polled", (int64_t)polled.size());
+        {
+          NsScope ns(55, "swap.ns.snapshots");
+          m.snapshotManyIn(swapTab, baseSpec, polled, polledSnaps);  // (many misses: their sorts on the host pool)
+        }
+        NsScope ns(56, "swap.ns.rows");
         for (size_t pi = 0; pi < polled.size(); ++pi) {
           const auto& v = polledSnaps[pi];
           if (devLimit)

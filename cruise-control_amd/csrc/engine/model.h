@@ -390,6 +390,27 @@ class Model {
     }
     return t.v[b];
   }
+  // snapshotInShared for every listed broker into out[i]: the table's current entries as they are, the rest computed
+  // together (snapshotMany: on the host pool when there are many) and stored in the table
+  void snapshotManyIn(SnapTable& t, const Spec& s, const std::vector<int32_t>& bs,
+                      std::vector<std::shared_ptr<const std::vector<int32_t>>>& out) {
+    bindSnapTable(t, s);
+    missB_.clear();
+    for (int b : bs)
+      if (t.ver[b] != bVer[b] + 1u) missB_.push_back(b);
+    if (!missB_.empty()) {
+      snapshotMany(s, missB_, missV_);
+      for (size_t i = 0; i < missB_.size(); ++i) {
+        const int b = missB_[i];
+        t.v[b] = std::move(missV_[i]);
+        t.ver[b] = bVer[b] + 1u;
+        t.size[b] = ((uint64_t)t.ver[b] << 32) | (uint32_t)t.v[b]->size();
+      }
+      missV_.clear();
+    }
+    out.resize(bs.size());
+    for (size_t i = 0; i < bs.size(); ++i) out[i] = t.v[bs[i]];
+  }
   // snapshotIn(t, b, s).size() — the replicas of b that s selects — counted instead of sorted when the table holds no
   // current snapshot of b (a polled broker's size is all a driver's visited count needs from it)
   size_t viewSize(SnapTable& t, int b, const Spec& s) {
@@ -421,6 +442,8 @@ class Model {
   void refreshBroker(int b);
   void refreshHost(int b);  // the host of broker b: cached utilization, and every broker of it dirty (BrokerRow.hutil)
   std::vector<int32_t> ordPct_[4], ordDirtyList_[4], ordScratch_;
+  std::vector<int32_t> missB_;  // snapshotManyIn scratch
+  std::vector<std::shared_ptr<const std::vector<int32_t>>> missV_;
   std::vector<uint8_t> ordDirty_[4];
   bool ordBuilt_[4] = {false, false, false, false};
   void refreshReplica(int r);
