@@ -20,8 +20,11 @@ per-proposal latency.
 Parity: the first timed proposal is checked against the committed oracle golden of the workload (tests/golden/:
 action log, final assignment and leaders, per-goal results, every goal's stats within 1e-9) -> "parity".
 
-Multi-GPU (torchrun, one process per GPU): by default every rank runs its own independent what-if proposal
-request (weak scaling, no data-path collective); timing is max over ranks. --sharded instead shards ONE proposal's
+Multi-GPU: under torchrun (one process per GPU) every rank runs its own independent what-if proposal request by
+default (weak scaling, no data-path collective); timing is max over ranks. A plain `python3 bench.py --gpus N` (no
+WORLD_SIZE) runs the same N independent proposals per step in one process, one session per device 0..N-1 on its own
+host thread, timed from a common start until the slowest device finishes; n_gpus = N and `devices` lists the ordinals
+used (fewer devices than N: sessions share them round-robin, flagged in `devices_note`). --sharded instead shards ONE proposal's
 candidate space by destination broker over the ranks (strong scaling): every scan's per-rank first-fit keys are
 MIN-combined in host shared memory (--combiner shm, the default on one node: no GPU work per combine, so every rank
 keeps its scan server) or by an RCCL MIN allreduce (--combiner rccl).
@@ -316,7 +319,9 @@ def optimize(opt, s, goals, options):
 
 def main() -> None:
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=1,
+                    help="N GPUs. Under torchrun (WORLD_SIZE set) one rank per GPU; from a plain launch, N sessions on "
+                         "devices 0..N-1 of this process, one host thread each (independent what-if proposals)")
     ap.add_argument("--steps", type=int, default=2)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -334,6 +339,7 @@ def main() -> None:
     ap.add_argument("--sharded", action="store_true",
                     help="N>1: one proposal sharded by destination broker over all ranks (a MIN combine per scan) "
                          "instead of one independent what-if proposal per rank")
+    ap.add_argument("--lib", default=None, help=argparse.SUPPRESS)  # tests: the CPU emulation build (tests/emu)
     args = ap.parse_args()
 
     import torch
@@ -342,18 +348,20 @@ def main() -> None:
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    ndev = max(1, torch.cuda.device_count())
+    lib = ccmi.Library.get(args.lib) if args.lib else ccmi.Library.get()
+    cuda = torch.cuda.is_available() and not args.lib
+    ndev = max(1, lib.device_count())
     # one rank per GPU with the bookkeeping collectives over RCCL; more ranks than GPUs (a rehearsal of the N-rank
     # path on a smaller box) share the cards round-robin and time over gloo (RCCL refuses two ranks on one GPU)
-    over_gloo = world > ndev
+    over_gloo = world > ndev or not cuda
     device = local_rank % ndev if world > 1 else 0
-    torch.cuda.set_device(device)
+    if cuda:
+        torch.cuda.set_device(device)
     if world > 1:
         dist.init_process_group("gloo" if over_gloo else "nccl", init_method="env://")
-    if over_gloo and args.sharded:
+    if over_gloo and args.sharded and world > 1:
         raise SystemExit("--sharded needs one GPU per rank (each rank's scan server / RCCL combiner holds its GPU)")
 
-    lib = ccmi.Library.get()
     props, goal_names, workload_name = WORKLOADS[args.workload]
     buf = ccmi.RandomCluster.generate(lib, **props)
     goals = ccmi.goals_from_names(goal_names)
@@ -364,16 +372,22 @@ def main() -> None:
         raise SystemExit("--combiner group drives every shard from one process: run it without torchrun")
     n_group = max(1, args.gpus) if group_mode else 1
     sharded = (args.sharded and world > 1) or (group_mode and n_group > 1)
+    if args.sharded and world == 1 and not group_mode and args.gpus > 1:
+        raise SystemExit("--sharded --combiner shm/rccl needs one process per GPU (torchrun); use --combiner group")
+    # A plain launch with --gpus N > 1 (no torchrun): N independent what-if proposals per step in THIS process, one
+    # per device 0..N-1 (round-robin when the box has fewer), each on its own host thread (ctypes drops the GIL)
+    local_devices = ([r % ndev for r in range(args.gpus)] if world == 1 and not group_mode and args.gpus > 1
+                     else [device])
     uid = None
-    if sharded and not group_mode:  # rank 0's RCCL id / shared-memory name reaches the other ranks over the process group
-        obj = [(ccmi.rccl_unique_id(lib) if args.combiner == "rccl" else f"/ccmi_bench_{os.getpid()}_{int(time.time())}")
-               if rank == 0 else None]
+    if sharded and not group_mode:  # rank 0's RCCL id / shared-memory name + job nonce reach the other ranks
+        obj = [(ccmi.rccl_unique_id(lib) if args.combiner == "rccl" else
+                (f"/ccmi_bench_{os.getpid()}_{int(time.time())}", time.time_ns() | 1)) if rank == 0 else None]
         dist.broadcast_object_list(obj, src=0)
         uid = obj[0]
 
     shm_sessions = [0]
 
-    def session():
+    def session(dev=device):
         if group_mode and n_group > 1:  # the group's sessions, rank r on GPU r (round-robin on a smaller box)
             g = ccmi.ShardGroup(n_group, lib)
             ranks = []
@@ -382,28 +396,39 @@ def main() -> None:
                 x.attach_group(g, r)
                 ranks.append(x)
             return GroupSession(ranks)
-        s = ccmi.ClusterModel.from_buffers(buf, device=device)
+        s = ccmi.ClusterModel.from_buffers(buf, device=dev)
         if sharded and args.combiner == "rccl":
             s.attach_rccl(rank, world, uid)
         elif sharded:  # one block per session (every rank creates its sessions in the same order)
             shm_sessions[0] += 1
-            s.attach_shm(rank, world, f"{uid}_{shm_sessions[0]}")
+            s.attach_shm(rank, world, f"{uid[0]}_{shm_sessions[0]}", job_nonce=uid[1] + shm_sessions[0])
         return s
 
+    def sync_all():
+        if cuda:
+            for d in sorted(set(local_devices)):
+                torch.cuda.synchronize(d)
+
+    from concurrent.futures import ThreadPoolExecutor
     # Warmup proposals double as the instrumented pass: HIP events around every launched scan kernel and the scan
-    # server's in-kernel busy time per command (outside the timed region).
+    # server's in-kernel busy time per command (outside the timed region). Every local device warms up (its first
+    # launches load the code object); device 0's session is the instrumented one.
     inst_perf = inst_cands = None
     for w in range(max(1, args.warmup)):
-        ws = session()
-        ws.set_kernel_timing(True)
-        ws.reset_perf()
-        r = optimize(opt, ws, goals, options)
-        inst_perf, inst_cands = ws.perf(), r.candidates
-        del ws
+        wss = [session(d) for d in local_devices]
+        wss[0].set_kernel_timing(True)
+        wss[0].reset_perf()
+        if len(wss) == 1:
+            rs = [optimize(opt, wss[0], goals, options)]
+        else:
+            with ThreadPoolExecutor(len(wss)) as wp:
+                rs = list(wp.map(lambda s: optimize(opt, s, goals, options), wss))
+        inst_perf, inst_cands = wss[0].perf(), rs[0].candidates
+        del wss
     # One more instrumented proposal with the scan server off (a launch per scan): the per-launch kernel times the
     # rocprofv3 trace of the same path can be checked against (rank 0, single GPU, outside the timed region).
     launch_perf = None
-    if world == 1 and not args.no_launch_pass and args.workload != "c4" and not group_mode:
+    if world == 1 and len(local_devices) == 1 and not args.no_launch_pass and args.workload != "c4" and not group_mode:
         os.environ["CCMI_SERVER"] = "0"
         try:
             ls = session()
@@ -416,30 +441,43 @@ def main() -> None:
         del ls
 
     S = max(1, args.requests_per_gpu) if not sharded else 1
-    # cluster resident in HBM before timing starts: one session per proposal
+    # cluster resident in HBM before timing starts: one session per proposal, [device][step][request]
     t_up = time.perf_counter()
-    sessions = [[session() for _ in range(S)] for _ in range(args.steps)]
-    upload_s = (time.perf_counter() - t_up) / max(1, args.steps * S)
-    pool = None
-    if S > 1:
-        from concurrent.futures import ThreadPoolExecutor  # ctypes drops the GIL inside ccmi_optimizations
-        pool = ThreadPoolExecutor(S)
-    torch.cuda.synchronize()
+    sessions = [[[session(d) for _ in range(S)] for _ in range(args.steps)] for d in local_devices]
+    upload_s = (time.perf_counter() - t_up) / max(1, len(local_devices) * args.steps * S)
+
+    def run_device(steps):  # one device's K steps in order, S concurrent proposals per step
+        out = []
+        pool = ThreadPoolExecutor(S) if S > 1 else None
+        try:
+            for step_sessions in steps:
+                if pool is None:
+                    out.extend(optimize(opt, s, goals, options) for s in step_sessions)
+                else:
+                    out.extend(pool.map(lambda s: optimize(opt, s, goals, options), step_sessions))
+        finally:
+            if pool is not None:
+                pool.shutdown()
+        return out
+
+    dev_pool = ThreadPoolExecutor(len(local_devices)) if len(local_devices) > 1 else None
+    sync_all()
     if world > 1:
         dist.barrier()
-    torch.cuda.synchronize()
+    sync_all()
     t0 = time.perf_counter()
-    results = []
-    for step_sessions in sessions:
-        if pool is None:
-            results.extend(optimize(opt, s, goals, options) for s in step_sessions)
-        else:
-            results.extend(pool.map(lambda s: optimize(opt, s, goals, options), step_sessions))
-    torch.cuda.synchronize()
+    if dev_pool is None:
+        per_device = [run_device(sessions[0])]
+    else:  # every device's thread starts together; the region ends when the slowest finishes (max over devices)
+        per_device = list(dev_pool.map(run_device, sessions))
+    sync_all()
     if world > 1:
         dist.barrier()
-    torch.cuda.synchronize()
+    sync_all()
     elapsed = time.perf_counter() - t0
+    if dev_pool is not None:
+        dev_pool.shutdown()
+    results = [r for rs in per_device for r in rs]
 
     cands = sum(r.candidates for r in results)
     if world > 1:
@@ -488,7 +526,7 @@ def main() -> None:
         dist.destroy_process_group()
         return
     first = results[0]
-    parity = check_parity(args.workload, sessions[0][0], first)
+    parity = check_parity(args.workload, sessions[0][0][0], first)
     traffic, traffic_src = pmc_traffic(args.workload, INTRA_KERNELS if intra else SCAN_KERNELS)
     traffic_unit = "HBM bytes per scan launch"
     if server:
@@ -502,7 +540,7 @@ def main() -> None:
         "metric": "candidate moves evaluated/s + proposal wall time, 10K brokers/1M replicas",
         "value": cands / elapsed,
         "unit": "candidate moves evaluated/s",
-        "n_gpus": n_group if group_mode else world,
+        "n_gpus": n_group if group_mode else world if world > 1 else len(local_devices),
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": elapsed * 1e3 / args.steps,
@@ -517,9 +555,15 @@ def main() -> None:
                    "goals": goal_names, "parallelism": (f"destination-sharded x{n_group} (one process, shard group: the scan servers MIN-combine "
                                    f"each scan on the device)" if group_mode and sharded else
                                    f"destination-sharded x{world} ({args.combiner} MIN combine per scan)" if sharded
-                                   else f"independent what-if per GPU x{world}")},
+                                   else f"independent what-if per GPU x{max(world, len(local_devices))}"
+                                   + ("" if world > 1 or len(local_devices) == 1 else
+                                      " (one process, one host thread per device)"))},
         "parity": parity,
         "requests_per_gpu": S,
+        "devices": (sorted(set(local_devices)) if world == 1 and not group_mode else None),
+        "devices_note": (None if world > 1 or group_mode or len(set(local_devices)) == len(local_devices) else
+                         f"{len(local_devices)} sessions on {len(set(local_devices))} device(s): fewer GPUs than "
+                         f"--gpus on this box, so sessions share devices round-robin (a rehearsal, not a scaling point)"),
         "proposal_wall_s": sum(r.seconds for r in results) / len(results),
         "session_upload_s": upload_s,
         "timed_region": "GoalOptimizer.optimizations on sessions already resident in HBM (upload excluded)",
@@ -576,12 +620,14 @@ def main() -> None:
                          "note": "the same proposal with CCMI_SERVER=0 (one launch per scan), HIP events per launch"}},
         "cpu_baseline": None,
     }
-    if world == 1 and not args.no_cpu_baseline:
+    if world == 1 and len(local_devices) == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(lib, buf, args.workload, goal_names, options, first, device,
                                             args.cpu_sample_seconds, args.what_if_procs)
     print(json.dumps(line))
     if world > 1:
         dist.destroy_process_group()
+
+
 
 
 if __name__ == "__main__":

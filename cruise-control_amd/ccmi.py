@@ -214,7 +214,7 @@ class DeviceError(CruiseControlError):
 _STATUS = {1: IllegalArgumentException, 2: DeviceError, 3: OptimizationFailureException, 4: IllegalStateException,
            5: UnsupportedOperationException}
 
-ABI_VERSION = 11  # CCMI_ABI_VERSION of include/ccmi.h
+ABI_VERSION = 12  # CCMI_ABI_VERSION of include/ccmi.h
 EXPORTED_SYMBOLS = (
     "ccmi_last_error", "ccmi_abi_version", "ccmi_device_count", "ccmi_default_constraint", "ccmi_default_random_cluster_props",
     "ccmi_random_cluster", "ccmi_cluster_buffers_desc", "ccmi_cluster_buffers_free", "ccmi_session_create",
@@ -224,7 +224,7 @@ EXPORTED_SYMBOLS = (
     "ccmi_leader_distribution", "ccmi_replica_disks", "ccmi_proposal_count", "ccmi_proposals",
     "ccmi_proposal_disks", "ccmi_perf", "ccmi_perf_reset",
     "ccmi_set_kernel_timing", "ccmi_session_set_shard", "ccmi_rccl_unique_id", "ccmi_session_attach_rccl",
-    "ccmi_session_attach_shm", "ccmi_shard_group_create", "ccmi_shard_group_destroy", "ccmi_session_attach_group",
+    "ccmi_session_attach_shm", "ccmi_session_attach_shm_job", "ccmi_shard_group_create", "ccmi_shard_group_destroy", "ccmi_session_attach_group",
     "ccmi_topic_broker_set",
     "ccmi_builder_create", "ccmi_builder_destroy", "ccmi_builder_create_broker", "ccmi_builder_add_disk",
     "ccmi_builder_populate_partition", "ccmi_builder_set_broker_state", "ccmi_builder_set_disk_state",
@@ -296,6 +296,7 @@ class Library:
         L.ccmi_rccl_unique_id.argtypes = [C.POINTER(C.c_uint8)]
         L.ccmi_session_attach_rccl.argtypes = [C.c_void_p, C.c_int32, C.c_int32, C.POINTER(C.c_uint8)]
         L.ccmi_session_attach_shm.argtypes = [C.c_void_p, C.c_int32, C.c_int32, C.c_char_p]
+        L.ccmi_session_attach_shm_job.argtypes = [C.c_void_p, C.c_int32, C.c_int32, C.c_char_p, C.c_uint64, C.c_double]
         L.ccmi_shard_group_create.argtypes = [C.c_int32, C.POINTER(C.c_void_p)]
         L.ccmi_shard_group_destroy.argtypes = [C.c_void_p]
         L.ccmi_session_attach_group.argtypes = [C.c_void_p, C.c_void_p, C.c_int32]
@@ -1235,10 +1236,16 @@ class ClusterModel:
         buf = (C.c_uint8 * 128).from_buffer_copy(unique_id)
         self.lib.check(self.lib.lib.ccmi_session_attach_rccl(self.handle, rank, count, buf))
 
-    def attach_shm(self, rank: int, count: int, name: str) -> None:
+    def attach_shm(self, rank: int, count: int, name: str, job_nonce: int = 0, timeout_s: float = 0.0) -> None:
         """Destination-sharded mode over the built-in host shared-memory combiner (ranks on one node): one int64 MIN
-        per scan in a POSIX shared-memory block; the scan server stays on."""
-        self.lib.check(self.lib.lib.ccmi_session_attach_shm(self.handle, rank, count, name.encode()))
+        per scan in a POSIX shared-memory block; the scan server stays on. `job_nonce` (the same nonzero value on
+        every rank, ccmi_session_attach_shm_job, ABI v12): the other ranks refuse a block rank 0 of this job did not
+        stamp with it, however recent; `timeout_s` bounds the waits (0 = 120 s)."""
+        if job_nonce or timeout_s:
+            self.lib.check(self.lib.lib.ccmi_session_attach_shm_job(self.handle, rank, count, name.encode(),
+                                                                    job_nonce & (2 ** 64 - 1), float(timeout_s)))
+        else:
+            self.lib.check(self.lib.lib.ccmi_session_attach_shm(self.handle, rank, count, name.encode()))
 
     def attach_group(self, group: "ShardGroup", rank: int) -> None:
         """Rank `rank` of a one-process shard group (ShardGroup): the scan server combines the ranks' keys on the

@@ -22,8 +22,19 @@ namespace ccmi {
 ccmi_cluster_buffers* generateRandomCluster(const ccmi_random_cluster_props& p);
 }
 
+struct ccmi_session;
+struct ccmi_shard_group {
+  ccmi::CombineBlock* blk = nullptr;
+  int32_t count = 0;
+  // attached sessions by rank; a destroyed session clears its slot and a destroyed group its sessions' back pointers,
+  // so neither side is ever read after it is freed
+  std::vector<ccmi_session*> ranks;
+};
+static void groupDetach(ccmi_session* s);
+
 struct ccmi_session {
   ~ccmi_session() {
+    groupDetach(this);
     ccmi::rcclDestroy(rccl);
     ccmi::shmDestroy(shm);
   }
@@ -32,6 +43,8 @@ struct ccmi_session {
   std::unique_ptr<ccmi::Engine> engine;
   ccmi::RcclShard* rccl = nullptr;
   ccmi::ShmShard* shm = nullptr;
+  ccmi_shard_group* group = nullptr;  // the shard group this session is a rank of (ccmi_session_attach_group)
+  int32_t groupRank = -1;
   int deviceOrdinal = 0;
   std::vector<int32_t> initDist, initLeaders;  // for ExecutionProposal diffs
   std::vector<int32_t> initDisks, initLeaderDisks;  // the logdir half of ReplicaPlacementInfo (JBOD)
@@ -41,6 +54,14 @@ struct ccmi_session {
   };
   std::vector<Prop> proposals;
 };
+
+static void groupDetach(ccmi_session* s) {
+  if (!s->group) return;
+  auto& ranks = s->group->ranks;
+  if ((size_t)s->groupRank < ranks.size() && ranks[(size_t)s->groupRank] == s) ranks[(size_t)s->groupRank] = nullptr;
+  s->group = nullptr;
+  s->groupRank = -1;
+}
 
 namespace {
 thread_local std::string g_err;
@@ -417,25 +438,36 @@ ccmi_status ccmi_session_attach_rccl(ccmi_session* s, int32_t rank, int32_t coun
 }
 
 ccmi_status ccmi_session_attach_shm(ccmi_session* s, int32_t rank, int32_t count, const char* name) {
+  return ccmi_session_attach_shm_job(s, rank, count, name, 0, 0.0);
+}
+
+ccmi_status ccmi_session_attach_shm_job(ccmi_session* s, int32_t rank, int32_t count, const char* name,
+                                        uint64_t job_nonce, double timeout_s) {
   return guarded([&] {
     if (!s || !name) throw std::invalid_argument("null argument");
     if (count < 1 || rank < 0 || rank >= count) throw std::invalid_argument("shard rank out of range");
+    if (!(timeout_s >= 0.0)) throw std::invalid_argument("negative timeout");
     ccmi::shmDestroy(s->shm);
     s->shm = nullptr;
-    s->shm = ccmi::shmCreate(name, rank, count);
+    s->shm = ccmi::shmCreate(name, rank, count, timeout_s > 0.0 ? timeout_s : 120.0, job_nonce);
     s->engine->shard = ccmi::Shard{rank, count, &ccmi::shmMin, s->shm};
     s->device->setServerAllowed(true);  // the combine is host memory only: the scan server stays resident
     return CCMI_OK;
   });
 }
 
-struct ccmi_shard_group {
-  ccmi::CombineBlock* blk = nullptr;
-  int32_t count = 0;
-  std::vector<ccmi_session*> ranks;  // attached sessions by rank
-};
-
 namespace {
+
+// The queue-scan path is decided group-wide: every rank must run the same scans so that the combines (made by the
+// queue path's fallbacks, never by a queue scan itself) pair up. It is allowed only when every rank is attached and
+// every rank's device can serve queue scans; recomputed for all attached ranks at each attach.
+void groupQueueDecision(ccmi_shard_group* g) {
+  bool all = true;
+  for (ccmi_session* x : g->ranks) all = all && x && x->device->queueUsable();
+  for (ccmi_session* x : g->ranks)
+    if (x) x->engine->shardQueueAllowed = all;
+}
+
 // the shard-group combiner for scans the scan server did not combine (shard_group.h): the host side of the protocol
 int groupMin(void* ctx, int64_t* key) {
   try {
@@ -463,7 +495,14 @@ ccmi_status ccmi_shard_group_create(int32_t count, ccmi_shard_group** out) {
 
 ccmi_status ccmi_shard_group_destroy(ccmi_shard_group* g) {
   return guarded([&] {
-    if (g) ccmi::Device::freeCombineBlock(g->blk);
+    if (g) {
+      for (ccmi_session* x : g->ranks)
+        if (x) {
+          x->group = nullptr;
+          x->groupRank = -1;
+        }
+      ccmi::Device::freeCombineBlock(g->blk);
+    }
     delete g;
     return CCMI_OK;
   });
@@ -480,8 +519,12 @@ ccmi_status ccmi_session_attach_group(ccmi_session* s, ccmi_shard_group* g, int3
     // and CU slots are per device), while that server's command waits for the launching rank's arrival. Such ranks
     // launch per scan and combine on their host threads; CCMI_GROUP_SHARED_SERVERS=1 instead gives each of them a
     // server with an equal share of the device's workgroup budget (tests of the device-side combine on one GPU).
-    g->ranks.resize((size_t)g->count, nullptr);
+    if (g->ranks.size() != (size_t)g->count) g->ranks.resize((size_t)g->count, nullptr);
+    if (g->ranks[(size_t)rank] && g->ranks[(size_t)rank] != s) throw std::invalid_argument("shard rank already attached");
+    groupDetach(s);
     g->ranks[(size_t)rank] = s;
+    s->group = g;
+    s->groupRank = rank;
     std::vector<ccmi_session*> same;
     for (ccmi_session* x : g->ranks)
       if (x && x->deviceOrdinal == s->deviceOrdinal) same.push_back(x);
@@ -492,6 +535,7 @@ ccmi_status ccmi_session_attach_group(ccmi_session* s, ccmi_shard_group* g, int3
         else x->device->setServerAllowed(false);
       }
     }
+    groupQueueDecision(g);
     return CCMI_OK;
   });
 }

@@ -1377,7 +1377,9 @@ bool Device::qdirSetMany(const std::vector<int32_t>& bs,
     segCache_.clear();
     segHead_ = 0;
     ++poolEpoch_;
+    // every snapshot is fresh after the wrap: the whole directory may not fit even though its uncached part did
     need = assign();
+    if (need > segCap_) return false;
   }
   for (int i = 0; i < n; ++i)
     if (fresh[i]) {
@@ -1524,7 +1526,11 @@ int64_t Device::scanSegs(const DevProgram& prog, const std::vector<SegIn>& segs,
   const bool readsTc = (prog.needs & (NEED_TOPIC | NEED_TLEAD)) != 0;
   bool served = serverUsable_ && serverAllowed_ && K > 0 && Nr > 0 && segs.size() <= (size_t)kMaxSegs &&
                 (uint64_t)K * (uint64_t)N < (1ull << 31);
-  if (served) {
+  // A pool wrap while uploading segment j rewrites the pool from its start, so the offsets of segments 0..j-1 may
+  // name overwritten rows: the table is rebuilt once from the emptied pool, and a second wrap means the segments do
+  // not fit the pool together (the flat path below).
+  for (int attempt = 0; served && attempt < 2; ++attempt) {
+    const auto epoch = poolEpoch_;
     segTab_.clear();
     int32_t start = 0;
     for (const SegIn& sg : segs) {
@@ -1538,6 +1544,8 @@ int64_t Device::scanSegs(const DevProgram& prog, const std::vector<SegIn>& segs,
       start += (int32_t)len;
     }
     segTab_.push_back(SegEntry{0, start});
+    if (!served || poolEpoch_ == epoch) break;
+    if (attempt == 1) served = false;
   }
   if (served) {
     bool serve = false;

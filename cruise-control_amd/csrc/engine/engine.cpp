@@ -16,6 +16,7 @@
 #include "predicates.h"
 #include "rackrows.h"
 #include "prof.h"
+#include "threadpin.h"
 
 namespace ccmi {
 
@@ -305,7 +306,7 @@ int64_t Engine::crossScanSegs(GoalImpl& self, int action, const std::vector<Snap
 bool Engine::queueOn(const GoalImpl& self, int action) const {
   static const bool off = std::getenv("CCMI_QUEUE_SCAN") && std::getenv("CCMI_QUEUE_SCAN")[0] == '0';
   // (a destination-sharded session scans the whole queue on every rank: identical models, identical first fit)
-  if (off || !dev->queueUsable()) return false;
+  if (off || !dev->queueUsable() || !shardQueueAllowed) return false;
   const DevProgram prog = program(self, action);
   return !prog.exclLeadMove && !prog.newOnly;
 }
@@ -338,9 +339,21 @@ uint64_t specKey(const Model::Spec& s, uint32_t selEpoch) {  // identity of the 
 }
 }  // namespace
 
+bool Engine::queueReady(const GoalImpl& self, int action, const Model::Spec& spec) {
+  if (!queueOn(self, action)) return false;
+  PhaseScope ps(PH_DEV_SCAN);
+  return queueSyncTry(spec);
+}
+
+void Engine::queueSync(const Model::Spec& spec) {
+  if (!queueSyncTry(spec))
+    throw Unsupported("the snapshot directory outgrew the snapshot pool (CCMI_SNAPSHOT_POOL_ROWS) during a move-in loop");
+}
+
 // Every broker's directory entry current for `spec`: all of them when the directory was filled for another Spec (or
 // the pool wrapped under it), otherwise only the brokers relocations touched since the last sync (Model::verLog).
-void Engine::queueSync(const Model::Spec& spec) {
+// False when the directory's snapshots do not fit the pool together; the directory is then left unbound.
+bool Engine::queueSyncTry(const Model::Spec& spec) {
   PhaseScope ps(PH_FLATTEN);
   const uint64_t key = specKey(spec, m.selEpoch);
   QueueSync& q = qsync_;
@@ -353,8 +366,13 @@ void Engine::queueSync(const Model::Spec& spec) {
       m.snapshotMany(spec, bs, q.snaps);
     }
     NsScope ns(53, "queue.ns.uploads");
-    if (!dev->qdirSetMany(bs, q.snaps)) throw Unsupported("a broker's snapshot exceeds the snapshot pool");
+    const bool ok = dev->qdirSetMany(bs, q.snaps);
     q.snaps.clear();
+    return ok;
+  };
+  auto unbind = [&]() {
+    q.bound = false;
+    return false;
   };
   for (int attempt = 0; attempt < 3; ++attempt) {
     const auto t0 = prof().on ? std::chrono::steady_clock::now() : std::chrono::steady_clock::time_point();
@@ -369,7 +387,7 @@ void Engine::queueSync(const Model::Spec& spec) {
       q.epoch = dev->poolEpoch();
       q.logPos = m.verLog.size();
       for (int b = 0; b < m.B; ++b) q.todo.push_back(b);
-      setMany(q.todo);
+      if (!setMany(q.todo)) return unbind();
       prof().count(20, "queue.dir.full", 1);
       if (prof().on) prof().count(28, "queue.full.ns", ns());
     } else {
@@ -381,15 +399,15 @@ void Engine::queueSync(const Model::Spec& spec) {
         q.stamp[b] = q.round;
         q.todo.push_back(b);
       }
-      setMany(q.todo);
+      if (!setMany(q.todo)) return unbind();
       q.logPos = end;
       prof().count(29, "queue.sync.brokers", (int64_t)q.todo.size());
       if (prof().on) prof().count(30, "queue.inc.ns", ns());
     }
-    if (q.epoch == dev->poolEpoch()) return;  // no pool wrap while setting: every entry points at live rows
+    if (q.epoch == dev->poolEpoch()) return true;  // no pool wrap while setting: every entry points at live rows
     full = true;
   }
-  throw std::logic_error("queue directory: the snapshot pool keeps wrapping");
+  return unbind();  // the pool keeps wrapping: the directory does not fit it
 }
 
 int64_t Engine::queueScan(GoalImpl& self, int action, const Model::Spec& spec, int head, int skip0,
@@ -1148,6 +1166,7 @@ class TreeWorker {
       next_.assign(order.begin(), order.end());
       nextB_ = B;
       nextSeq_ = withSequence;
+      nextMask_ = CpuMask::current();  // built on the submitting thread's CPUs (its session's pin, if any)
       tSubmit_ = std::chrono::steady_clock::now();
       ++gen_;
       cancel_.store(true, std::memory_order_relaxed);  // the build in flight (if any) is stale
@@ -1177,6 +1196,7 @@ class TreeWorker {
   void loop() {
     pthread_setname_np(pthread_self(), "ccmi-tree");
     uint64_t started = 0;
+    CpuMask mine = CpuMask::current(), want;
     for (;;) {
       uint64_t gen;
       {
@@ -1188,8 +1208,10 @@ class TreeWorker {
         order_.swap(next_);
         B_ = nextB_;
         seq_ = nextSeq_;
+        want = nextMask_;
         cancel_.store(false, std::memory_order_relaxed);
       }
+      mine.follow(want);
       tree_.clear();
       rank_.assign(B_, 0);
       mark_.assign(B_, 0);
@@ -1217,6 +1239,7 @@ class TreeWorker {
   std::vector<uint8_t> mark_;
   int nextB_ = 0, B_ = 0;
   bool nextSeq_ = true, seq_ = true;  // the tree's in-order sequence is wanted (RbTreeSet::buildByRank)
+  CpuMask nextMask_;                  // the submitter's CPU mask (guarded by mu_)
   uint64_t gen_ = 0;   // submissions (guarded by mu_)
   uint64_t done_ = 0;  // the submission whose tree is complete in tree_ (guarded by mu_)
   std::atomic<bool> cancel_{false};
@@ -1869,7 +1892,7 @@ class ResourceDistribution : public GoalImpl {
     // candidate list, nothing moves and nothing is counted — the loop's outcome without walking every broker
     if (cands.empty()) return true;
     if (action == DA_LEADERSHIP && pq.ordered() && e.shard.count <= 1) return moveInLeadership(e, b, pq, spec);
-    if (action == DA_MOVE && pq.ordered() && e.queueOn(*this, action)) return moveInQueue(e, b, pq, spec, cands);
+    if (action == DA_MOVE && pq.ordered() && e.queueReady(*this, action, spec)) return moveInQueue(e, b, pq, spec, cands);
     // rows: the current broker's remaining view, then the polled brokers' snapshots (device-resident segments)
     using Seg = SnapSeg;
     auto segLen = [](const Seg& x) { return x.v->size() > x.skip ? x.v->size() - x.skip : 0; };

@@ -145,6 +145,12 @@ class Engine {
   // Returns the key (Device::scanQueue) or -1 and adds the reference-equivalent candidates. queueOn: the path applies
   // (one shard, a usable server, no replica-dependent candidate filters; CCMI_QUEUE_SCAN=0 turns it off).
   bool queueOn(const GoalImpl& self, int action) const;
+  // queueOn, and the snapshot directory set for `spec`: false when the directory does not fit the snapshot pool (the
+  // caller then takes the segment path, which uploads only the polled brokers' snapshots). Called before a move-in
+  // loop changes any state, so the fallback starts from the same state.
+  bool queueReady(const GoalImpl& self, int action, const Model::Spec& spec);
+  // Shard groups: the queue path is allowed only when every rank can take it (set at attach, ccmi_api.cpp)
+  bool shardQueueAllowed = true;
   // the snapshot directory current for `spec` (Device::qdirRows / qdirLen then give every broker's live view)
   void queueSyncSpec(const Model::Spec& spec) { queueSync(spec); }
   int64_t queueScan(GoalImpl& self, int action, const Model::Spec& spec, int head, int skip0, const int32_t* tail,
@@ -203,6 +209,7 @@ class Engine {
   };
   QueueSync qsync_;
   void queueSync(const Model::Spec& spec);
+  bool queueSyncTry(const Model::Spec& spec);  // queueSync, false (directory unbound) when it does not fit the pool
   DevProgram program(const GoalImpl& self, int action) const;
   int64_t combine(int64_t localKey) const;
   void refreshAllowed(GoalImpl& g);

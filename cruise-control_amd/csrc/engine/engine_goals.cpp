@@ -2062,7 +2062,7 @@ class LeaderReplicaDistribution : public GoalImpl {
     std::vector<int32_t> single{b}, cands;
     e.eligible(single, DA_MOVE, cands);
     if (cands.empty()) return true;  // every source replica visits an empty candidate list: nothing moves
-    if (e.queueOn(*this, DA_MOVE)) return LeaderReplicaDistribution_moveInQueue(e, *this, b, pq, s, cands, nl, lower);
+    if (e.queueReady(*this, DA_MOVE, s)) return LeaderReplicaDistribution_moveInQueue(e, *this, b, pq, s, cands, nl, lower);
     // rows: the sources' sorted leaders (snapshots held by snapTab until the next model change; device-resident
     // segments of the snapshot pool)
     auto segLen = [](const SnapSeg& x) { return x.v->size() > x.skip ? x.v->size() - x.skip : 0; };

@@ -3,7 +3,8 @@
 // as every index is done; helpers wake on a condition variable and share the remaining indices, so a short loop runs
 // on the caller alone without waiting for a wake-up. Jobs are reference-counted: a helper that wakes after the loop
 // finished finds nothing left and drops its reference. One loop at a time per process; a caller that finds the pool
-// busy (another session's loop) runs its loop alone. CCMI_SYNC_THREADS (default 8) counts the caller.
+// busy (another session's loop) runs its loop alone. CCMI_SYNC_THREADS (default 8) counts the caller. A helper runs
+// each job on the CPU mask of the job's caller (CpuMask::follow): the pool belongs to no session's NUMA node.
 #pragma once
 #include <atomic>
 #include <condition_variable>
@@ -16,6 +17,8 @@
 
 #include <immintrin.h>
 #include <pthread.h>
+
+#include "threadpin.h"
 
 namespace ccmi {
 
@@ -35,6 +38,7 @@ class HostPool {
       return;
     }
     auto job = std::make_shared<Job>(n, f);
+    job->mask = CpuMask::current();  // the helpers run this job on the caller's CPUs
     {
       std::lock_guard<std::mutex> l(mu_);
       job_ = job;
@@ -52,6 +56,7 @@ class HostPool {
     Job(int n_, const std::function<void(int)>& f_) : n(n_), f(f_) {}
     const int n;
     std::function<void(int)> f;
+    CpuMask mask;
     std::atomic<int> next{0}, done{0};
   };
   static void run(Job& j) {
@@ -68,6 +73,7 @@ class HostPool {
   void loop() {
     pthread_setname_np(pthread_self(), "ccmi-sync");
     uint64_t seen = 0;
+    CpuMask mine = CpuMask::current();
     for (;;) {
       std::shared_ptr<Job> j;
       {
@@ -76,7 +82,10 @@ class HostPool {
         seen = gen_;
         j = job_;
       }
-      if (j) run(*j);
+      if (j) {
+        mine.follow(j->mask);
+        run(*j);
+      }
     }
   }
   int threads_ = 1;

@@ -35,6 +35,7 @@ struct Slot {
 struct Block {
   Line64 magic;    // written last by rank 0 (release): the block is initialised
   Line64 created;  // CLOCK_REALTIME ns when rank 0 initialised it (before the magic)
+  Line64 nonce;    // the job's nonce (shmCreate), written before the magic
   Line32 count;
   Line32 attached;
   Slot slot[2];
@@ -61,7 +62,7 @@ struct ShmShard {
   bool broken = false;  // a combine timed out: its slot counters are inconsistent, every later call fails fast
 };
 
-ShmShard* shmCreate(const char* name, int rank, int count, double timeoutSeconds) {
+ShmShard* shmCreate(const char* name, int rank, int count, double timeoutSeconds, uint64_t nonce) {
   if (!name || name[0] != '/' || std::strchr(name + 1, '/')) throw std::invalid_argument("shm name must be \"/name\"");
   if (count < 1 || rank < 0 || rank >= count) throw std::invalid_argument("shard rank out of range");
   int fd = -1;
@@ -96,11 +97,13 @@ ShmShard* shmCreate(const char* name, int rank, int count, double timeoutSeconds
     b.count.v.store((uint32_t)count, std::memory_order_relaxed);
     b.attached.v.store(0, std::memory_order_relaxed);
     b.created.v.store(wallNs(), std::memory_order_relaxed);
+    b.nonce.v.store((int64_t)nonce, std::memory_order_relaxed);
     b.magic.v.store((int64_t)kMagic, std::memory_order_release);
   } else {
-    // A block a crashed run left under the same name can be opened before rank 0 replaces it. Its creation stamp
-    // gives it away: rank 0 of a block waits at most `timeoutSeconds` for its ranks, so a block created longer than
-    // that before this rank arrived has no rank 0 left; it is dropped and the name polled again.
+    // A block a crashed run left under the same name can be opened before rank 0 replaces it. With a job nonce it is
+    // told apart by the nonce, whatever its age. Without one (nonce 0) its creation stamp gives it away: rank 0 of a
+    // block waits at most `timeoutSeconds` for its ranks, so a block created longer than that before this rank arrived
+    // has no rank 0 left. Either way it is dropped and the name polled again.
     for (;;) {
       if (now() - t0 > timeoutSeconds) {
         shmDestroy(s);
@@ -120,7 +123,9 @@ ShmShard* shmCreate(const char* name, int rank, int count, double timeoutSeconds
           Block* b = static_cast<Block*>(p);
           if (b->magic.v.load(std::memory_order_acquire) == (int64_t)kMagic) {
             const int64_t created = b->created.v.load(std::memory_order_relaxed);
-            if (created + (int64_t)(timeoutSeconds * 1e9) >= joinNs) {
+            const bool current = nonce != 0 ? (uint64_t)b->nonce.v.load(std::memory_order_relaxed) == nonce
+                                            : created + (int64_t)(timeoutSeconds * 1e9) >= joinNs;
+            if (current) {
               s->blk = b;
               break;
             }

@@ -2,7 +2,8 @@
 // CPUs of the GPU's NUMA node on entry and restored on exit, so the library leaves no lasting side effect on a caller's
 // thread (a JVM pool thread that later runs unrelated work). Every scan is a round trip through host memory (the command
 // through the BAR, the result into a host-mapped mailbox the thread spins on): 20 us from the GPU's socket, 30 us from
-// the other one (profiles/r04/numa_ab.txt). Threads the library owns (the tree helpers) inherit the pinned mask.
+// the other one (profiles/r04/numa_ab.txt). Threads the library owns (the sync and tree helpers) take the mask of the
+// caller whose job they run (CpuMask::follow), so they never keep another session's pin.
 //
 //   CCMI_NUMA_PIN=0       never pin
 //   CCMI_NUMA_CPULIST=L   use the cpulist L ("0-3,8") instead of the device's PCI local_cpulist (tests)
@@ -37,6 +38,24 @@ inline bool parseCpuList(const std::string& list, cpu_set_t* set) {
   }
   return CPU_COUNT(set) > 0;
 }
+
+// A thread's CPU mask, for helper threads that follow the thread they work for: a pool helper takes the mask of the
+// caller whose job it runs (so a session's helpers run on its GPU's node while the call is pinned, and on the caller's
+// own mask otherwise), instead of keeping the mask of whichever call created it.
+struct CpuMask {
+  cpu_set_t set;
+  bool valid = false;
+  static CpuMask current() {
+    CpuMask m;
+    m.valid = pthread_getaffinity_np(pthread_self(), sizeof(m.set), &m.set) == 0;
+    return m;
+  }
+  // make this thread's mask `want` (no syscall when it already is)
+  void follow(const CpuMask& want) {
+    if (!want.valid || (valid && CPU_EQUAL(&set, &want.set))) return;
+    if (pthread_setaffinity_np(pthread_self(), sizeof(want.set), &want.set) == 0) *this = want;
+  }
+};
 
 class ThreadPin {
  public:

@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define CCMI_ABI_VERSION 11
+#define CCMI_ABI_VERSION 12
 
 typedef enum ccmi_status {
   CCMI_OK = 0,
@@ -487,12 +487,20 @@ ccmi_status ccmi_session_attach_rccl(ccmi_session* s, int32_t rank, int32_t coun
  * POSIX shared-memory block `name` ("/name"; rank 0 creates it, the others open it, and every rank waits until all
  * `count` ranks are attached, at most 120 s). No GPU work per combine, so the session keeps its scan server. */
 ccmi_status ccmi_session_attach_shm(ccmi_session* s, int32_t rank, int32_t count, const char* name);
+/* ABI v12. ccmi_session_attach_shm with a job nonce: every rank passes the same nonzero `job_nonce` (e.g. rank 0's
+ * start time broadcast over the job's process group); rank 0 stamps it into the block and the other ranks attach only
+ * to a block carrying it, so a block a crashed run left under the same name is refused however recent (nonce 0: the
+ * v9 rule, a block older than the timeout is stale). `timeout_s` bounds every wait (0 = 120 s). */
+ccmi_status ccmi_session_attach_shm_job(ccmi_session* s, int32_t rank, int32_t count, const char* name,
+                                        uint64_t job_nonce, double timeout_s);
 /* ABI v11. Shard groups: the ranks of one sharded proposal driven from ONE process, one host thread per session
  * (typically one session per GPU of the node, each thread calling ccmi_optimizations on its own session). The ranks'
  * first-fit keys are MIN-combined in a block of pinned host memory every device maps: a scan the session's resident
- * scan server ran is combined by the server itself (its last workgroup folds the key in with system-scope atomics, waits
- * for the other ranks and publishes the group minimum), any other scan by the host thread on the same slots. The group
- * must outlive its sessions. Replaces the per-scan host MIN of GoalOptimizer's single-threaded loop with nothing on the
+ * scan server ran is combined by the server itself (its last workgroup folds the key in with system-scope atomics and
+ * counts the rank in; no kernel waits for another rank), any other scan by the host thread on the same slots; whichever
+ * rank arrives last (a server's workgroup or a host thread) publishes the group minimum into every rank's mailbox. A
+ * destroyed session leaves its rank's slot empty and a destroyed group detaches its sessions. The queue-scan path is
+ * taken only when every rank can take it (decided at each attach), so all ranks run the same scans and combines. Replaces the per-scan host MIN of GoalOptimizer's single-threaded loop with nothing on the
  * host between the ranks' scans. */
 typedef struct ccmi_shard_group ccmi_shard_group;
 ccmi_status ccmi_shard_group_create(int32_t count, ccmi_shard_group** out);

@@ -7,6 +7,7 @@
 // The product library always uses the HIP implementation (device.cpp) and fails loudly without a gfx950.
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <stdexcept>
 #include <vector>
@@ -127,7 +128,10 @@ struct View {
 Emu& E(void* st) { return *static_cast<Emu*>(st); }
 }  // namespace
 
-int Device::countGfx950() { return 1; }  // one emulated device
+int Device::countGfx950() {  // one emulated device, or CCMI_EMU_DEVICES (tests of the multi-device host paths)
+  const char* e = std::getenv("CCMI_EMU_DEVICES");
+  return e ? std::max(1, std::atoi(e)) : 1;
+}
 bool deviceLocalCpuList(int, std::string&) { return false; }  // no PCI device
 
 Device::Device(int ordinal, int B, int R, int P, int T, int maxGoalSlots)
@@ -831,7 +835,7 @@ void Device::stopServer() {}  // the emulation has no scan server: every scan is
 
 // Queue scans: the directory is host bookkeeping here (no pool); the rows are evaluated in key order, which is the
 // order the server's first fit reports.
-bool Device::queueUsable() const { return true; }
+bool Device::queueUsable() const { return serverAllowed_; }
 void Device::qdirBind(uint64_t key) {
   if (key == qdirKey_ && !qdirSnap_.empty()) return;
   qdirKey_ = key;
@@ -866,6 +870,17 @@ int64_t Device::groupCombineHost(int64_t key) {
 
 bool Device::qdirSetMany(const std::vector<int32_t>& bs,
                          const std::vector<std::shared_ptr<const std::vector<int32_t>>>& snaps) {
+  // CCMI_SNAPSHOT_POOL_ROWS: the pool the real directory lives in, in rows of whole 128-byte lines: a directory whose
+  // snapshots do not fit it together is refused, as Device::qdirSetMany refuses it
+  if (const char* pr = std::getenv("CCMI_SNAPSHOT_POOL_ROWS")) {
+    const size_t cap = (size_t)std::max(1024ll, std::atoll(pr)) & ~(size_t)7;
+    std::vector<size_t> len(B_, 0);
+    for (int b = 0; b < B_; ++b) len[b] = qdirSnap_[b] ? qdirSnap_[b]->size() : 0;
+    for (size_t i = 0; i < bs.size(); ++i) len[bs[i]] = snaps[i]->size();
+    size_t need = 0;
+    for (size_t n : len) need += (n + 7) & ~(size_t)7;
+    if (need > cap) return false;
+  }
   for (size_t i = 0; i < bs.size(); ++i)
     if (!qdirSet(bs[i], snaps[i])) return false;
   return true;

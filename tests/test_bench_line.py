@@ -80,3 +80,32 @@ def test_headline_frac_follows_committed_kernel_stats(workload, kernel):
     if kernel == "scan_server":  # the headline is the launch (residency) view, the per-command one secondary
         assert r["resident"]["frac"] == pytest.approx(r["frac"])
         assert r["per_command"]["frac"] > r["frac"]
+
+
+def _bench_emu(emu_lib, gpus, devices, extra=()):
+    import subprocess
+    env = dict(os.environ, CCMI_EMU_DEVICES=str(devices))
+    cmd = [sys.executable, os.path.join(REPO, "bench.py"), "--lib", emu_lib.path, "--workload", "c0", "--gpus",
+           str(gpus), "--steps", "1", "--warmup", "1", "--no-cpu-baseline", *extra]
+    r = subprocess.run(cmd, capture_output=True, text=True, env=env, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    return json.loads(r.stdout.strip().splitlines()[-1])
+
+
+def test_bench_plain_launch_runs_one_session_per_device(emu_lib):
+    """`python3 bench.py --gpus 2` without torchrun (the driver's plain form) runs two independent what-if proposals
+    per step in one process, one on each of device ordinals 0 and 1 (CPU emulation with two devices), and reports the
+    whole job: n_gpus 2, both proposals' candidates."""
+    one = _bench_emu(emu_lib, 1, 2)
+    two = _bench_emu(emu_lib, 2, 2)
+    assert one["n_gpus"] == 1 and one["devices"] == [0]
+    assert two["n_gpus"] == 2 and two["devices"] == [0, 1] and two["devices_note"] is None
+    # weak scaling: the same proposal on every device, so twice the candidates per step
+    assert two["value"] * two["ms_per_step"] == pytest.approx(2 * one["value"] * one["ms_per_step"], rel=1e-9)
+    assert two["scaling"] == "weak" and "x2" in two["config"]["parallelism"]
+
+
+def test_bench_plain_launch_with_fewer_devices_says_so(emu_lib):
+    """--gpus 2 on a one-device box: both sessions on ordinal 0, reported as a rehearsal."""
+    two = _bench_emu(emu_lib, 2, 1)
+    assert two["n_gpus"] == 2 and two["devices"] == [0] and "rehearsal" in two["devices_note"]

@@ -146,3 +146,13 @@ def test_emu_tree_worker_matches_oracle(emu_lib, oracle_lib, monkeypatch, props)
     monkeypatch.setenv("CCMI_TREE_WORKER", "1")
     monkeypatch.setenv("CCMI_TREE_WORKER_MIN", "1")
     check_product_against_oracle(emu_lib, props, DEFAULT_GOALS, 1.05, max_replicas=1500)
+
+
+@pytest.mark.parametrize("pool_rows", ["1024", "4096", "12000"])
+def test_emu_queue_directory_larger_than_pool_falls_back(emu_lib, oracle_lib, monkeypatch, pool_rows):
+    """A snapshot directory that does not fit the snapshot pool (CCMI_SNAPSHOT_POOL_ROWS) is refused before the move-in
+    loop changes any state, and the loop takes the segment path instead of failing: same decisions as the
+    oracle."""
+    monkeypatch.setenv("CCMI_SNAPSHOT_POOL_ROWS", pool_rows)
+    check_product_against_oracle(emu_lib, dict(num_racks=5, num_brokers=20, num_replicas=6000, num_topics=300),
+                                 DEFAULT_GOALS, 1.05)

@@ -206,3 +206,60 @@ def test_gpu_shard_group_same_gpu_twice(gpu_lib, oracle_lib, monkeypatch, shared
         assert min(served) > 0
     else:
         assert max(served) == 0
+
+
+def test_shard_group_mixed_device_layout(emu_lib, oracle_lib):
+    """Three ranks, two of them sharing a device (those launch per scan: their queue scans are off) and one on a device
+    of its own: the queue-scan path is decided group-wide, so every rank runs the same scans, pairs its combines with
+    the others' and makes the oracle's decisions (a per-rank decision mismatched the slot pairing)."""
+    props = dict(num_racks=5, num_brokers=20, num_replicas=6000, num_topics=300)
+    goals = list(ccmi.DEFAULT_GOALS)
+    buf, sessions, results = _group_run(emu_lib, props, goals, 3, device_of=lambda r: [0, 0, 1][r])
+    _check_group_against_oracle(buf, sessions, results, goals)
+    assert len({cm.perf().combines for cm in sessions}) == 1
+
+
+def test_shard_group_survives_destroyed_session(emu_lib, oracle_lib):
+    """A session destroyed while attached leaves its rank's slot empty: attaching another session to that rank later
+    reads no freed memory, and the group then optimizes as usual."""
+    import gc
+    props = dict(num_racks=5, num_brokers=20, num_replicas=6000, num_topics=300)
+    buf = ccmi.RandomCluster.generate(emu_lib, **props)
+    group = ccmi.ShardGroup(2, emu_lib)
+    gone = ccmi.ClusterModel(buf.desc, device=0, lib=emu_lib, keepalive=buf)
+    gone.attach_group(group, 1)
+    del gone
+    gc.collect()
+    sessions = []
+    for r in range(2):
+        cm = ccmi.ClusterModel(buf.desc, device=r, lib=emu_lib, keepalive=buf)
+        cm.attach_group(group, r)
+        cm.reset_perf()
+        sessions.append(cm)
+    from concurrent.futures import ThreadPoolExecutor
+    goals = list(ccmi.C1_GOALS)
+    opt = ccmi.GoalOptimizer(constraint(1.05))
+    with ThreadPoolExecutor(2) as pool:
+        results = list(pool.map(lambda cm: opt.optimizations(cm, ccmi.goals_from_names(goals)), sessions))
+    _check_group_against_oracle(buf, sessions, results, goals)
+
+
+def test_shm_combiner_refuses_stale_block(emu_lib):
+    """A block a crashed run left under the job's name seconds ago (rank 0 created it, then gave up waiting) is refused
+    by a rank of a new job whose nonce differs — the v9 age window alone would have accepted it — and accepted by a
+    rank carrying the nonce rank 0 stamped (ccmi_session_attach_shm_job, ABI v12)."""
+    name = f"/ccmi_stale_{os.getpid()}"
+    buf = ccmi.RandomCluster.generate(emu_lib, num_racks=3, num_brokers=6, num_replicas=60, num_topics=5)
+    crashed = ccmi.ClusterModel.from_buffers(buf, device=0)
+    try:
+        with pytest.raises(ccmi.CruiseControlError):  # rank 0 of the crashed job: rank 1 never came
+            crashed.attach_shm(0, 2, name, job_nonce=1111, timeout_s=0.5)
+        assert os.path.exists(f"/dev/shm{name}")  # the stale block stays behind, well inside 120 s
+        late = ccmi.ClusterModel.from_buffers(buf, device=0)
+        with pytest.raises(ccmi.CruiseControlError):  # a new job's rank 1 waits for its own rank 0, never attaching the stale one
+            late.attach_shm(1, 2, name, job_nonce=2222, timeout_s=1.0)
+        same = ccmi.ClusterModel.from_buffers(buf, device=0)
+        same.attach_shm(1, 2, name, job_nonce=1111, timeout_s=1.0)  # the nonce matches: it is that job's block
+    finally:
+        if os.path.exists(f"/dev/shm{name}"):
+            os.unlink(f"/dev/shm{name}")
