@@ -107,6 +107,19 @@ def test_gpu_snapshot_pool_wraps_match_oracle(gpu_lib, oracle_lib, monkeypatch):
                                  C1_GOALS, 1.05)
 
 
+@pytest.mark.parametrize("pool_rows", ["4096", "12288", "16384", "20480", "24576"])
+def test_gpu_snapshot_directory_larger_than_pool_matches_oracle(gpu_lib, oracle_lib, monkeypatch, pool_rows):
+    """Snapshot pools around the size of a queue directory (≈10 000 leader rows, ≈30 000 replica rows on this cluster):
+    a directory that does not fit — before a wrap, or only after one when the segment path had cached part of it — is
+    refused and the move-in loop takes the segment path (the wrap branch once wrote past the pool); the
+    segment path's own wraps rebuild its table. Same decisions as the oracle."""
+    monkeypatch.setenv("CCMI_SNAPSHOT_POOL_ROWS", pool_rows)
+    check_product_against_oracle(gpu_lib, dict(num_racks=8, num_brokers=300, num_replicas=30000, num_topics=1000),
+                                 C1_GOALS, 1.05)
+    check_product_against_oracle(gpu_lib, dict(num_racks=8, num_brokers=300, num_replicas=30000, num_topics=1000),
+                                 DEFAULT_GOALS, 1.05)
+
+
 @pytest.mark.parametrize("props", [dict(), dict(num_racks=20, num_brokers=1000, num_replicas=99999, num_topics=3000),
                                    dict(num_racks=3, num_brokers=10, num_replicas=3000, num_topics=100,
                                         num_dead_brokers=2)])
