@@ -49,7 +49,7 @@ hipError_t launchScanServer(const DevTables& T, const MutTables& M, const ChainT
                             const char* pay, const RowRef* pool, unsigned long long* result, unsigned int* done,
                             unsigned long long* mail, unsigned long long* t0, unsigned long long* bell,
                             unsigned long long startSeq, int blocks, hipStream_t st);
-hipError_t launchChainPairs(const DevTables& T, const ChainTables& C, const DevProgram& prog, const int32_t* pr,
+hipError_t launchChainPairs(const DevTables& T, const ChainTables& C, const DevProgram& prog, const RowRef* pr,
                             const int32_t* pb, const int32_t* next, int n, int maxAccepts, int32_t* log,
                             ChainResultDev* out, hipStream_t st);
 hipError_t launchChainRackRows(const DevTables& T, const ChainTables& C, const DevProgram& prog, const int32_t* rows,
@@ -240,6 +240,16 @@ Device::~Device() {
         std::fprintf(stderr, "[ccmi chain stamps] %llu chain_pairs launches, %llu accepts: %.2f us per launch in "
                              "evaluation, %.2f us applying, %.2f us in total (thread 0)\n",
                      h[8200], h[8201], h[8202] * 0.01 / h[8200], h[8203] * 0.01 / h[8200], h[8204] * 0.01 / h[8200]);
+      if (h[8240])
+        std::fprintf(stderr, "[ccmi apply stamps] %llu applies: leadership loads %.2f us, step 0 %.2f us, step 1 %.2f us, "
+                             "step 2 + end %.2f us; replica lanes %.2f us, end %.2f us (thread 0, summed over all applies "
+                             "/ applies)\n",
+                     h[8240], h[8241] * 0.01 / h[8240], h[8242] * 0.01 / h[8240], h[8243] * 0.01 / h[8240],
+                     h[8244] * 0.01 / h[8240], h[8245] * 0.01 / h[8240], h[8246] * 0.01 / h[8240]);
+      if (h[8250])
+        std::fprintf(stderr, "[ccmi chain eval stamps] %llu tiles: view loads %.2f us, conjunction %.2f us, tile "
+                             "reduction %.2f us (thread 0)\n",
+                     h[8250], h[8251] * 0.01 / h[8250], h[8252] * 0.01 / h[8250], h[8253] * 0.01 / h[8250]);
       double acc[5] = {0, 0, 0, 0, 0}, loads = 0;
       int n = 0, nl = 0;
       for (int i = 0; i < 1024; ++i) {
@@ -658,7 +668,9 @@ bool Device::serverChain(const DevProgram& prog, int mode, const int32_t* a0, in
   const size_t nl = lrows.size(), ns = srows.size();
   lrowsSent_ = nl;
   srowsSent_ = ns;
-  const size_t words = (size_t)n0 + n1 + n2;
+  // CM_PAIRS: a0 (the pairs' replicas) goes out as RowRefs (scan.hip serverChain's request layout)
+  const bool refs = mode == CM_PAIRS;
+  const size_t words = (size_t)n0 * (refs ? 4 : 1) + n1 + n2;
   const size_t oRows = align16(sizeof(DevProgram));
   const Staged g = packUpdates(0);
   if (g.nb > kOverlayRows || g.nr > kOverlayRows || g.np > kOverlayRows) {  // the server stages rows in its LDS overlay
@@ -683,9 +695,11 @@ bool Device::serverChain(const DevProgram& prog, int mode, const int32_t* a0, in
   if (g.end) std::memcpy(pay + oRows, hStage_, g.end);
   if (nl) std::memcpy(pay + oL, lrows.data(), nl * sizeof(LoadRow));
   if (ns) std::memcpy(pay + oS, srows.data(), ns * sizeof(SlotRow));
-  std::memcpy(pay + oA, a0, (size_t)n0 * 4);
-  if (n1) std::memcpy(pay + oA + (size_t)n0 * 4, a1, (size_t)n1 * 4);
-  if (n2) std::memcpy(pay + oA + (size_t)(n0 + n1) * 4, a2, (size_t)n2 * 4);
+  const size_t a0Bytes = (size_t)n0 * (refs ? sizeof(RowRef) : 4);
+  if (refs) writeRowRefs(pay + oA, a0, (size_t)n0);
+  else std::memcpy(pay + oA, a0, a0Bytes);
+  if (n1) std::memcpy(pay + oA + a0Bytes, a1, (size_t)n1 * 4);
+  if (n2) std::memcpy(pay + oA + a0Bytes + (size_t)n1 * 4, a2, (size_t)n2 * 4);
   perf.serverPayloadBytes += (int64_t)(end - oRows);
   prof().addPayload((int64_t)(end - oRows));
   ServerCmd c;
@@ -1724,16 +1738,17 @@ Device::ChainResult Device::chainPairs(const DevProgram& prog, const int32_t* pr
   }
   if (!served) {
     stopServer();
-    const size_t oB = align16((size_t)n * 4), oN = oB + align16((size_t)n * 4), req = oN + align16((size_t)n * 4);
+    const size_t oB = align16((size_t)n * sizeof(RowRef)), oN = oB + align16((size_t)n * 4),
+                 req = oN + align16((size_t)n * 4);
     Staged g;
     size_t oReq = 0;
     (void)stageChainCopy(req, g, oReq, [&](char* base) {
-      std::memcpy(base, pr, (size_t)n * 4);
+      writeRowRefs(base, pr, (size_t)n);
       std::memcpy(base + oB, pb, (size_t)n * 4);
       std::memcpy(base + oN, next, (size_t)n * 4);
     }, st_);
     if (timing) (void)hipEventRecord(EV0, ST);
-    hipCheck(launchChainPairs(tables(), chainTables(), prog, (const int32_t*)dReq_, (const int32_t*)(dReq_ + oB),
+    hipCheck(launchChainPairs(tables(), chainTables(), prog, (const RowRef*)dReq_, (const int32_t*)(dReq_ + oB),
                               (const int32_t*)(dReq_ + oN), n, maxAccepts, hChainLogDev_, hChainOutDev_, ST),
              "chain_pairs");
     if (timing) (void)hipEventRecord(EV1, ST);

@@ -1309,7 +1309,7 @@ class ResourceDistribution : public GoalImpl {
   ccmi_provision_recommendation overRec{};  // _overProvisionedRecommendation
   Model::SnapTable snapTab;  // moveIn's candidate-broker snapshots (one Spec per phase)
   Model::SnapTable swapTab;  // the swap phase's polled brokers' limit-free snapshots
-  std::vector<uint8_t> queued;  // moveIn: broker is in the candidate queue
+  std::vector<uint8_t> queued;  // moveInLeadership: a group's broker is in the candidate queue (other entries: stale)
   int nameBase() const { return 4 * kind; }
   int nameId(bool reverse, bool leader) const { return nameBase() + (reverse ? 1 : 0) + (leader ? 2 : 0); }
   bool excluded(int b) const { return !allowed[b]; }
@@ -1848,6 +1848,12 @@ class ResourceDistribution : public GoalImpl {
     return m.nrep(b) != 0;
   }
 
+  // a candidate broker of rebalanceByMovingLoadIn's queue (:450-462): alive, utilization above the lower threshold
+  // (above 0 for a broker excluded for replica moves)
+  bool moveInMember(const Model& m, int c) const {
+    return m.alive(c) && m.pct(c, res) > (excluded(c) ? 0.0 : lowerThr);
+  }
+
   // rebalanceByMovingLoadIn (:437-526): speculative multi-candidate-broker batches over the live views
   bool moveIn(Engine& e, int b, int action, bool immOnly) {
     PhaseScope ps(PH_RES_IN);
@@ -1863,24 +1869,17 @@ class ResourceDistribution : public GoalImpl {
     {
       PhaseScope pi(PH_PQ_INIT);
       const auto& ord = m.brokersByPct(res);
-      auto member = [&](int c) { return m.alive(c) && m.pct(c, res) > (excluded(c) ? 0.0 : lowerThr); };
+      auto member = [&](int c) { return moveInMember(m, c); };
       // only b's key changes while brokers are queued (moves go cb -> b, cb polled): exact unless b is queued
       pq.init(m.B, !member(b));
-      const bool lead = action == DA_LEADERSHIP;  // `queued` is read by the leadership driver only
-      if (lead) queued.assign(m.B, 0);
       if (pq.ordered() && m.numDead == 0 && !exclAlive && !ord.empty() && m.pct(ord.back(), res) == m.pct(ord.back(), res)) {
         // every broker is alive and allowed, and no key is NaN: the members are exactly the suffix of the (pct, id)
         // order above the lower threshold, queued in reverse
         const auto first = std::partition_point(ord.begin(), ord.end(), [&](int c) { return !(m.pct(c, res) > lowerThr); });
         pq.sortedRun().assign(ord.rbegin(), std::make_reverse_iterator(first));
-        if (lead)
-          for (int c : pq.sortedRun()) queued[c] = 1;
       } else {
         for (auto it = ord.rbegin(); it != ord.rend(); ++it)
-          if (member(*it)) {
-            pq.push_sorted(*it);
-            if (lead) queued[*it] = 1;
-          }
+          if (member(*it)) pq.push_sorted(*it);
       }
       if (!pq.ordered())
         for (int c = 0; c < m.B; ++c)
@@ -1891,7 +1890,7 @@ class ResourceDistribution : public GoalImpl {
     // b outside the eligible set (e.g. not a requested destination): every polled replica visits an empty
     // candidate list, nothing moves and nothing is counted — the loop's outcome without walking every broker
     if (cands.empty()) return true;
-    if (action == DA_LEADERSHIP && pq.ordered() && e.shard.count <= 1) return moveInLeadership(e, b, pq, spec);
+    if (action == DA_LEADERSHIP && pq.ordered()) return moveInLeadership(e, b, pq, spec);
     if (action == DA_MOVE && pq.ordered() && e.queueReady(*this, action, spec)) return moveInQueue(e, b, pq, spec, cands);
     // rows: the current broker's remaining view, then the polled brokers' snapshots (device-resident segments)
     using Seg = SnapSeg;
@@ -2089,6 +2088,10 @@ class ResourceDistribution : public GoalImpl {
       order.resize(groups.size());
       for (size_t i = 0; i < groups.size(); ++i) order[i] = (int)i;
       std::sort(order.begin(), order.end(), before);
+      // `queued` is read for the groups' brokers only: they start queued when they are members (the ordered queue
+      // holds exactly the members); polls and re-adds keep them current below
+      if (queued.size() != (size_t)m.B) queued.assign(m.B, 0);
+      for (const Group& g : groups) queued[g.c] = moveInMember(m, g.c) ? 1 : 0;
     }
     auto emit = [&](Group& g) {  // the group's rows in view order (recomputed on a new version)
       if (g.ver != m.bVer[g.c]) {

@@ -902,7 +902,7 @@ struct ChainWin {
 
 // K7 chain bodies (defined with the chain kernels below; SOP_CHAIN runs them inside the server)
 __device__ __forceinline__ void chainPairsRun(const DevTables& T, const ChainTables& C, const DevProgram& prog, const OverlayLds& ov,
-                              LoadVec* sc, const int32_t* __restrict__ pr, const int32_t* __restrict__ pb,
+                              LoadVec* sc, const RowRef* __restrict__ pr, const int32_t* __restrict__ pb,
                               const int32_t* __restrict__ next, int n, int maxAccepts, int32_t* __restrict__ log,
                               ChainResultDev* __restrict__ out, ChainWin* win);
 __device__ __forceinline__ void chainRackRowsRun(const DevTables& T, const ChainTables& C, const DevProgram& prog,
@@ -935,7 +935,9 @@ __device__ __attribute__((noinline)) void serverChain(const DevTables T, const C
   const SlotRow* srows = (const SlotRow*)(pay + c.oS);
   int32_t* req = reinterpret_cast<int32_t*>(c.chainReq);
   const int32_t* reqIn = reinterpret_cast<const int32_t*>(pay + c.oA);
-  const int words = c.chainMode == CM_PAIRS ? 3 * c.chainN : c.chainN + c.chainM;
+  // CM_PAIRS request: [RowRef pr[n] | pb[n] | next[n]] (the rows' broker, partition and topic as the host knows them:
+  // a leadership chain moves no replica, so they stay valid through the chain); RACK_ROWS: [rows[n] | cands[N]]
+  const int words = c.chainMode == CM_PAIRS ? 6 * c.chainN : c.chainN + c.chainM;
   auto putLoad = [&](const LoadRow& x) {
     LoadVec* dst = x.kind == LR_REPLICA ? C.rLoad
                    : (x.kind == LR_BROKER       ? C.bLoad
@@ -991,7 +993,8 @@ __device__ __attribute__((noinline)) void serverChain(const DevTables T, const C
   int32_t* log = reinterpret_cast<int32_t*>(c.chainLog);
   ChainResultDev* out = reinterpret_cast<ChainResultDev*>(c.chainOut);
   if (c.chainMode == CM_PAIRS)
-    chainPairsRun(T, C, prog, ov, sc, req, req + c.chainN, req + 2 * c.chainN, c.chainN, c.maxAccepts, log, out,
+    chainPairsRun(T, C, prog, ov, sc, reinterpret_cast<const RowRef*>(req), req + 4 * c.chainN, req + 5 * c.chainN,
+                  c.chainN, c.maxAccepts, log, out,
                   &gSrvWin);
   else
     chainRackRowsRun(T, C, prog, ov, sc, req, c.chainN, req + c.chainN, c.chainM, log, out);
@@ -1733,8 +1736,20 @@ __device__ __forceinline__ void replicaFinishWaves(S& s, int t, int r, int p, in
 //   lane 4 dr's load (+= delta, -> scratch for lane 5)         lane 5 leadership NW load of dst (+= dr's new load)
 //   lanes 6, 7 the hosts (Host.makeFollower / makeLeader)
 // the same operations on the same values, in the order apply.h's sequential form (the emulation) runs them.
+// CCMI_STAMPS: thread 0's time points inside an apply ([8240] applies, [8241..8244] leadership: loads landed, step 0
+// done, step 1 done, end; [8245..8246] replica move: lanes done, end), each summed from the previous point
+__device__ __forceinline__ void applyStamp(unsigned long long* st, unsigned long long& t, int slot, bool drain) {
+  if (!st || threadIdx.x != 0) return;
+  if (drain) __builtin_amdgcn_s_waitcnt(0);
+  const unsigned long long u = __builtin_amdgcn_s_memrealtime();
+  atomicAdd(&st[slot], u - t);
+  t = u;
+}
 template <int WC>
-__device__ void chainApply(const ChainTables& C, LoadVec* sc, int action, int r, int dst, const ChainWin* win) {
+__device__ void chainApply(const ChainTables& C, LoadVec* sc, int action, int r, int dst, const ChainWin* win,
+                           unsigned long long* st) {
+  unsigned long long tS = st ? __builtin_amdgcn_s_memrealtime() : 0;
+  if (st && threadIdx.x == 0) atomicAdd(&st[8240], 1ull);
   DevApply<WC> S{C, sc};
   int src, p, rflags;
   if (win) {  // the evaluating lane's view of the winner (same records, read in this decision's evaluation)
@@ -1795,6 +1810,7 @@ __device__ void chainApply(const ChainTables& C, LoadVec* sc, int action, int r,
     if (active) ldCopy(x, *agg, W);
     if (t == 0) ldCopy(o, S.rLoad(sr), W);
     const int32_t flags0 = (t == 1 || t == 4) ? S.rep(t == 1 ? sr : dr).flags : 0;
+    applyStamp(st, tS, 8241, true);
     if (t == 0) {
       ldAddSignedAll(x, o, W, true);
       ldCopy(*agg, x, W);
@@ -1804,6 +1820,7 @@ __device__ void chainApply(const ChainTables& C, LoadVec* sc, int action, int r,
       ldCopy(S.scratch(0), o, W);  // delta
     }
     chainSync();
+    applyStamp(st, tS, 8242, false);
     // step 1: the delta everywhere it goes (lanes 2, 3, 4 and the hosts: one add or subtract each)
     const bool takesDelta = (t >= 2 && t <= 4) || hostLane;
     if (takesDelta && x.mask) {
@@ -1824,6 +1841,7 @@ __device__ void chainApply(const ChainTables& C, LoadVec* sc, int action, int r,
         for (int k = 0; k < 3; ++k) rec.hutil[k] = rec.util[k];
     }
     chainSync();
+    applyStamp(st, tS, 8243, false);
     // step 2: dst's leadership NW load; the partition record (wave 3); the host utilizations
     if (t == 5) {
       ldCopy(o, S.scratch(1), W);
@@ -1840,6 +1858,8 @@ __device__ void chainApply(const ChainTables& C, LoadVec* sc, int action, int r,
       prc.leadNwOut = ldUtil(o, R_NW_OUT, W);
     }
     if (hosts) applyHostUtil(S, src, dst, t, (int)blockDim.x);
+    chainSync();
+    applyStamp(st, tS, 8244, false);
   } else {
     const bool lead = (rflags & RF_LEADER) != 0;
     const int lr = C.pLeader[p];
@@ -1847,21 +1867,23 @@ __device__ void chainApply(const ChainTables& C, LoadVec* sc, int action, int r,
     else if (t < kReplicaLanes + kHostLanes) applyHostReplicaLane(S, t - kReplicaLanes, r, src, dst);
     else
       replicaFinishWaves(S, t, r, p, src, dst, lead);  // independent of the load lanes (counts, slots, topic counts)
+    applyStamp(st, tS, 8245, true);
     if (S.hostsOn()) {
       chainSync();
       applyHostUtil(S, src, dst, t, (int)blockDim.x);
     }
+    chainSync();
+    applyStamp(st, tS, 8246, false);
   }
-  chainSync();
 }
 __device__ __forceinline__ void chainApplyAny(const ChainTables& C, LoadVec* sc, int action, int r, int dst,
-                                              const ChainWin* win = nullptr) {
+                                              const ChainWin* win = nullptr, unsigned long long* st = nullptr) {
   switch (C.W) {  // block-uniform
-    case 1: chainApply<1>(C, sc, action, r, dst, win); break;
-    case 2: chainApply<2>(C, sc, action, r, dst, win); break;
-    case 3: chainApply<3>(C, sc, action, r, dst, win); break;
-    case 4: chainApply<4>(C, sc, action, r, dst, win); break;
-    default: chainApply<5>(C, sc, action, r, dst, win); break;
+    case 1: chainApply<1>(C, sc, action, r, dst, win, st); break;
+    case 2: chainApply<2>(C, sc, action, r, dst, win, st); break;
+    case 3: chainApply<3>(C, sc, action, r, dst, win, st); break;
+    case 4: chainApply<4>(C, sc, action, r, dst, win, st); break;
+    default: chainApply<5>(C, sc, action, r, dst, win, st); break;
   }
 }
 
@@ -1869,7 +1891,7 @@ __device__ __forceinline__ void chainApplyAny(const ChainTables& C, LoadVec* sc,
 // fits a tile of 64 or 128 pairs, 4 or 2 waves share each pair's goals (goal-parallel tiles, tileFirst): the same
 // single tile, with the conjunction's latency split over the SIMDs.
 __device__ __forceinline__ unsigned long long chainFirstPair(const DevTables& T, const DevProgram& prog,
-                                                             const OverlayLds& ov, const int32_t* pr,
+                                                             const OverlayLds& ov, const RowRef* pr,
                                                              const int32_t* pb, int start, int n, ChainWin* win) {
   const int nGoals = prog.nGoals;
   for (int base = start; base < n;) {
@@ -1881,12 +1903,18 @@ __device__ __forceinline__ unsigned long long chainFirstPair(const DevTables& T,
     const int q = base + slot;
     bool ok = false;
     PreView v;
+    // CCMI_STAMPS: [8250] tiles, thread 0's view loads [8251], conjunction [8252], tile reduction [8253]
+    unsigned long long tE = T.stamps ? __builtin_amdgcn_s_memrealtime() : 0;
+    if (T.stamps && threadIdx.x == 0) atomicAdd(&T.stamps[8250], 1ull);
     if (q < n) {
       v.loadDst(T, pb[q], ov);
-      v.loadRow(T, prog, pr[q], ov);
+      v.loadRowRef(T, prog, pr[q], ov);  // one dependent level: the row's records and the destination's together
+      applyStamp(T.stamps, tE, 8251, true);
       ok = !v.exclLeadBlocked(prog) && moveCandidateAcceptedPart(prog, v, v.r, v.dst, part, parts);
+      applyStamp(T.stamps, tE, 8252, true);
     }
     const int f = tileFirst(ok, parts);
+    applyStamp(T.stamps, tE, 8253, false);
     if (f >= 0) {
       if (slot == f && part == 0) {  // the winner's lane hands its view of the pair to the apply
         int sp = -1, dp = -1;
@@ -1911,7 +1939,7 @@ __device__ __forceinline__ unsigned long long chainFirstPair(const DevTables& T,
 // maxAccepts moves (the callers' stop counts). visited = reference-equivalent candidates of the sequence of scans.
 // The body runs in its own launch (chain_pairs) or inside the scan server (SOP_CHAIN); `ov` is an empty overlay.
 __device__ __forceinline__ void chainPairsRun(const DevTables& T, const ChainTables& C, const DevProgram& prog,
-                                              const OverlayLds& ov, LoadVec* sc, const int32_t* __restrict__ pr,
+                                              const OverlayLds& ov, LoadVec* sc, const RowRef* __restrict__ pr,
                                               const int32_t* __restrict__ pb, const int32_t* __restrict__ next, int n,
                                               int maxAccepts, int32_t* __restrict__ log,
                                               ChainResultDev* __restrict__ out, ChainWin* win) {
@@ -1935,7 +1963,7 @@ __device__ __forceinline__ void chainPairsRun(const DevTables& T, const ChainTab
     visited += best - (unsigned long long)start + 1;
     const int q = (int)best;
     if (threadIdx.x == 0) log[acc] = q;
-    chainApplyAny(C, sc, prog.action, win->r, win->dst, win);
+    chainApplyAny(C, sc, prog.action, win->r, win->dst, win, T.stamps);
     if (st) {
       __builtin_amdgcn_s_waitcnt(0);
       const unsigned long long u = __builtin_amdgcn_s_memrealtime();
@@ -1960,7 +1988,7 @@ __device__ __forceinline__ void chainPairsRun(const DevTables& T, const ChainTab
 }
 
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, kServerWaves))) void chain_pairs(DevTables T, ChainTables C, DevProgram prog,
-                                                      const int32_t* __restrict__ pr, const int32_t* __restrict__ pb,
+                                                      const RowRef* __restrict__ pr, const int32_t* __restrict__ pb,
                                                       const int32_t* __restrict__ next, int n, int maxAccepts,
                                                       int32_t* __restrict__ log, ChainResultDev* __restrict__ out) {
   __shared__ OverlayLds ov;
@@ -2173,7 +2201,7 @@ hipError_t launchScanServer(const DevTables& T, const MutTables& M, const ChainT
   return hipGetLastError();
 }
 
-hipError_t launchChainPairs(const DevTables& T, const ChainTables& C, const DevProgram& prog, const int32_t* pr,
+hipError_t launchChainPairs(const DevTables& T, const ChainTables& C, const DevProgram& prog, const RowRef* pr,
                             const int32_t* pb, const int32_t* next, int n, int maxAccepts, int32_t* log,
                             ChainResultDev* out, hipStream_t st) {
   hipLaunchKernelGGL(chain_pairs, dim3(1), dim3(kBlock), 0, st, T, C, prog, pr, pb, next, n, maxAccepts, log, out);
