@@ -189,6 +189,15 @@ struct StopServerOnExit {
     }
   }
 };
+// An optimization call in progress on the session's device: concurrent calls share the device's scan-server budget
+// (Device::ensureServer). Declared before StopServerOnExit, so the server is stopped before the call stops counting.
+struct ActiveCall {
+  ccmi_session* s;
+  explicit ActiveCall(ccmi_session* x) : s(x) { s->device->callBegin(); }
+  ~ActiveCall() { s->device->callEnd(); }
+  ActiveCall(const ActiveCall&) = delete;
+  ActiveCall& operator=(const ActiveCall&) = delete;
+};
 
 std::vector<int32_t> replicaDist(const ccmi::Model& m) {
   std::vector<int32_t> v(m.R);
@@ -568,6 +577,7 @@ ccmi_status ccmi_goal_optimize(ccmi_session* s, int32_t goal_kind, const int32_t
     }
     auto g = ccmi::makeGoal(goal_kind);
     const ccmi::ThreadPin pin(s->deviceOrdinal);  // restored when the call returns
+    const ActiveCall active(s);
     StopServerOnExit stop{s};
     setOptions(s, c, o);
     validateChain(s, &goal_kind, 1, priors);
@@ -588,6 +598,7 @@ ccmi_status ccmi_optimizations(ccmi_session* s, const int32_t* goal_kinds, int32
     if (!s || (!goal_kinds && n_goals > 0)) throw std::invalid_argument("null argument");
     if (n_goals <= 0) throw std::invalid_argument("At least one goal must be provided to get an optimization result.");
     const ccmi::ThreadPin pin(s->deviceOrdinal);  // restored when the call returns
+    const ActiveCall active(s);
     StopServerOnExit stop{s};
     setOptions(s, c, o);
     validateChain(s, goal_kinds, n_goals);

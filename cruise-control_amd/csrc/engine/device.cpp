@@ -168,9 +168,10 @@ Device::Device(int ordinal, int B, int R, int P, int T, int maxGoalSlots)
     const char* e = std::getenv("CCMI_SERVER");
     serverUsable_ = !(e && e[0] == '0');
     const char* nb = std::getenv("CCMI_SERVER_BLOCKS");
-    if (nb) serverBlocks_ = std::max(8, std::min(512, (int)std::strtol(nb, nullptr, 10) / 8 * 8));
+    if (nb) serverBlocksCap_ = std::max(8, std::min(512, (int)std::strtol(nb, nullptr, 10) / 8 * 8));
     // one workgroup per CU at most, so every workgroup of the server is resident with room for other kernels
-    serverBlocks_ = std::min(serverBlocks_, prop.multiProcessorCount / 8 * 8);
+    serverBlocksCap_ = std::min(serverBlocksCap_, prop.multiProcessorCount / 8 * 8);
+    serverBlocks_ = serverBlocksCap_;
     if (const char* gs = std::getenv("CCMI_GOAL_SPLIT")) goalSplitMax_ = (int)std::strtol(gs, nullptr, 10);
     if (const char* sa = std::getenv("CCMI_SERVER_APPLY")) applyViaServer_ = sa[0] != '0';
     if (const char* gw = std::getenv("CCMI_GOAL_SPLIT_WGS")) goalSplitWgs_ = (int)std::strtol(gw, nullptr, 10);
@@ -324,11 +325,16 @@ namespace {
 constexpr size_t kCmdBytes = 256;  // the ServerCmd block; the payload follows
 static_assert(sizeof(ServerCmd) <= kCmdBytes, "ServerCmd fits its block");
 // Persistent scan servers of this process per device and their workgroups: a session starts one only while the
-// device's total stays within kServerBudget workgroups — one server per device, so no other persistent launch holds
-// the CU slots a server's late-dispatched workgroups wait for; concurrent sessions beyond it launch per scan.
+// device's total stays within kServerBudget workgroups (one workgroup per CU), so no persistent launch holds the CU
+// slots another server's workgroups wait for; a session that finds no room launches per scan. Concurrent calls on a
+// device share the budget: a server started while A sessions of the process are inside an optimization call on the
+// device gets kServerBudget / A workgroups (servers restart at every goal's statistics, so the shares follow the
+// calls), and the sessions' servers run side by side on disjoint CUs instead of one session launching per scan
+// behind another's resident server.
 constexpr int kServerBudget = 256;
 std::mutex g_serverMu;
 int g_serverWgs[64] = {};
+int g_activeCalls[64] = {};
 double nowSeconds() {
   return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
@@ -446,7 +452,17 @@ bool Device::serveScan(const DevProgram& prog, const Staged& g, bool readsTopicC
 // watchdog); false when the device already has its budget of servers (the caller launches instead).
 void Device::limitServerBlocks(int blocks) {
   stopServer();
-  serverBlocks_ = std::max(8, std::min(serverBlocks_, blocks / 8 * 8));
+  serverBlocksCap_ = std::max(8, std::min(serverBlocksCap_, blocks / 8 * 8));
+  serverBlocks_ = serverBlocksCap_;
+}
+
+void Device::callBegin() {
+  std::lock_guard<std::mutex> lk(g_serverMu);
+  ++g_activeCalls[ordinal_ & 63];
+}
+void Device::callEnd() {
+  std::lock_guard<std::mutex> lk(g_serverMu);
+  --g_activeCalls[ordinal_ & 63];
 }
 
 bool Device::ensureServer() {
@@ -455,8 +471,11 @@ bool Device::ensureServer() {
   progSent_ = false;
   {
     std::lock_guard<std::mutex> lk(g_serverMu);
-    if (g_serverWgs[ordinal_ & 63] + serverBlocks_ > kServerBudget) return false;
-    g_serverWgs[ordinal_ & 63] += serverBlocks_;
+    const int active = std::max(1, g_activeCalls[ordinal_ & 63]);
+    const int want = std::min(serverBlocksCap_, std::max(8, kServerBudget / active / 8 * 8));
+    if (g_serverWgs[ordinal_ & 63] + want > kServerBudget) return false;
+    g_serverWgs[ordinal_ & 63] += want;
+    serverBlocks_ = want;  // this launch's workgroups (the stop returns them)
   }
   // the arrival counter and the result word start clean for every server launch, whatever an earlier launch left
   hipCheck(hipMemsetAsync(dDone_, 0, sizeof(unsigned int), ST), "reset server arrivals");

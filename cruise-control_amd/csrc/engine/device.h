@@ -209,6 +209,10 @@ class Device {
   // the session's scans may (not) use the resident scan server (sessions whose scans wait on other ranks may not)
   // at most `blocks` server workgroups from the next server launch on (a multiple of 8, at least 8)
   void limitServerBlocks(int blocks);
+  // an API call that may scan on this device begins / ends (the device's server budget is shared among its active
+  // calls, ensureServer)
+  void callBegin();
+  void callEnd();
   void setServerAllowed(bool on) {
     if (!on) stopServer();
     serverAllowed_ = on;
@@ -322,7 +326,8 @@ class Device {
   bool devCombined_ = false;
   bool combineArmed_ = false;
   std::vector<unsigned long long> groupMail_;  // the test emulation's shard-group mailbox (the product uses hResult_)
-  int serverBlocks_ = 256;
+  int serverBlocks_ = 256;     // the running (or last) server launch's workgroups
+  int serverBlocksCap_ = 256;  // at most this many (CU count, CCMI_SERVER_BLOCKS, limitServerBlocks)
   // goal-parallel server tiles (ServerCmd.goalParts): at most this many waves per candidate (CCMI_GOAL_SPLIT: 1, 2 or
   // 4) and only for scans whose split first sweep needs at most CCMI_GOAL_SPLIT_WGS workgroups
   int goalSplitMax_ = 4;

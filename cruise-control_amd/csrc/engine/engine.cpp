@@ -787,6 +787,11 @@ ccmi_provision_response validateProvision(const ccmi_provision_response& p, cons
 bool Engine::optimizeGoalImpl(std::unique_ptr<GoalImpl>& g, ccmi_goal_result* res, std::chrono::steady_clock::time_point t0,
                               int64_t c0, size_t a0, int64_t l0, int64_t p0) {
   using clk = std::chrono::steady_clock;
+  {  // the leadership loops' K7 chains are opt-in (CCMI_PAIR_CHAINS=1, read per goal): one pair scan per decision with
+     // the move applied on the host is faster (profiles/r06/README.md, chain A/B)
+    const char* pc = std::getenv("CCMI_PAIR_CHAINS");
+    pairChains = pc && pc[0] == '1' && !std::getenv("CCMI_NO_PAIR_CHAINS");
+  }
   const ccmi_cluster_stats before = stats();
   g->finished = false;
   g->dg.allowedSlot = newSlot;

@@ -185,6 +185,7 @@ class Engine {
   // decisions in one launch, applying each move before the next; the engine replays the logged moves into the host
   // model (Model::replaying). Not used for destination-sharded sessions. CCMI_NO_CHAINS=1 turns them off.
   bool chainsOn() const;
+  bool pairChains = false;  // the leadership loops run as K7 chains (CCMI_PAIR_CHAINS=1, set per goal; chainsOn too)
   int64_t chainPairs(GoalImpl& self, int action, const std::vector<int32_t>& pr, const std::vector<int32_t>& pb,
                      const std::vector<int32_t>& next, int maxAccepts, std::vector<int32_t>& log);
   int64_t chainRackRows(GoalImpl& self, const std::vector<int32_t>& rows, const std::vector<int32_t>& cands,

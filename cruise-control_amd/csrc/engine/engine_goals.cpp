@@ -1731,11 +1731,9 @@ class TopicLeaderReplicaDistribution : public GoalImpl {
 };
 
 // ======================================================================================= LeaderReplicaDistributionGoal
-// CCMI_NO_PAIR_CHAINS=1: the leadership loops use one pair scan per decision instead of a K7 chain (A/B switch)
-inline bool pairChainsOn(const Engine& e) {
-  static const bool off = std::getenv("CCMI_NO_PAIR_CHAINS") != nullptr;
-  return !off && e.chainsOn();
-}
+// The leadership loops use one pair scan per decision, the move applied on the host; CCMI_PAIR_CHAINS=1 runs each
+// call as one K7 chain instead (device-side applies: slower at C2, profiles/r06/README.md)
+inline bool pairChainsOn(const Engine& e) { return e.pairChains && e.chainsOn(); }
 template <class Q>
 bool LeaderReplicaDistribution_moveInQueue(Engine& e, GoalImpl& self, int b, Q& pq, const Model::Spec& spec,
                                            const std::vector<int32_t>& cands, int nl, int lower);

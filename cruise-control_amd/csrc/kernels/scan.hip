@@ -1935,6 +1935,20 @@ __device__ __forceinline__ unsigned long long chainFirstPair(const DevTables& T,
   return kNone;
 }
 
+// A chain's decision log is kept in LDS while the chain runs and copied to the host-mapped log once at the end: a store
+// to host memory completes only after its PCIe round trip, and a wave's later loads wait for its older stores (vmcnt
+// counts both in issue order), so a per-decision store there stalled the next apply's loads by several microseconds.
+constexpr int kChainLogLds = 1024;
+__shared__ int32_t gChainLog[kChainLogLds];
+__device__ __forceinline__ void chainLogPut(int32_t* __restrict__ log, int i, int32_t v) {  // thread 0
+  if (i < kChainLogLds) gChainLog[i] = v;
+  else log[i] = v;  // (a longer log than the LDS copy holds goes out directly)
+}
+__device__ __forceinline__ void chainLogFlush(int32_t* __restrict__ log, int n) {  // every thread
+  __syncthreads();
+  for (int i = (int)threadIdx.x; i < n && i < kChainLogLds; i += (int)blockDim.x) log[i] = gChainLog[i];
+}
+
 // PAIRS: pairs (pr[q], pb[q]) in reference order; after accepting q the loop resumes at next[q]; at most
 // maxAccepts moves (the callers' stop counts). visited = reference-equivalent candidates of the sequence of scans.
 // The body runs in its own launch (chain_pairs) or inside the scan server (SOP_CHAIN); `ov` is an empty overlay.
@@ -1962,7 +1976,7 @@ __device__ __forceinline__ void chainPairsRun(const DevTables& T, const ChainTab
     }
     visited += best - (unsigned long long)start + 1;
     const int q = (int)best;
-    if (threadIdx.x == 0) log[acc] = q;
+    if (threadIdx.x == 0) chainLogPut(log, acc, q);
     chainApplyAny(C, sc, prog.action, win->r, win->dst, win, T.stamps);
     if (st) {
       __builtin_amdgcn_s_waitcnt(0);
@@ -1980,6 +1994,7 @@ __device__ __forceinline__ void chainPairsRun(const DevTables& T, const ChainTab
     atomicAdd(&T.stamps[8203], tApply);
     atomicAdd(&T.stamps[8204], __builtin_amdgcn_s_memrealtime() - tStart);
   }
+  chainLogFlush(log, acc);
   if (threadIdx.x == 0) {
     out->accepts = (unsigned long long)acc;
     out->visited = visited;
@@ -2040,12 +2055,13 @@ __device__ __forceinline__ void chainRackRowsRun(const DevTables& T, const Chain
       break;
     }
     if (threadIdx.x == 0) {
-      log[2 * acc] = k;
-      log[2 * acc + 1] = (int)best;
+      chainLogPut(log, 2 * acc, k);
+      chainLogPut(log, 2 * acc + 1, (int)best);
     }
     chainApplyAny(C, sc, DA_MOVE, r, cands[best]);
     ++acc;
   }
+  chainLogFlush(log, 2 * acc);
   if (threadIdx.x == 0) {
     out->accepts = (unsigned long long)acc;
     out->visited = 0;

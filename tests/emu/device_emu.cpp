@@ -843,6 +843,8 @@ void Device::qdirBind(uint64_t key) {
   qdirSnap_.assign(B_, nullptr);
 }
 void Device::limitServerBlocks(int) {}
+void Device::callBegin() {}
+void Device::callEnd() {}
 
 // Shard groups: the emulation has no scan server, so every combine is the host side of the protocol (shard_group.h).
 CombineBlock* Device::allocCombineBlock() {

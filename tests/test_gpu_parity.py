@@ -255,6 +255,18 @@ def test_gpu_bad_disk_brokers_match_oracle(gpu_lib, oracle_lib, props, goals):
     check_product_against_oracle(gpu_lib, props, goals, 1.05, max_replicas=3000)
 
 
+@pytest.mark.parametrize("pair_chains", ["0", "1"])
+def test_gpu_leadership_pair_chains_match_oracle(gpu_lib, oracle_lib, monkeypatch, pair_chains):
+    """LeaderReplicaDistributionGoal's leadership loops as one pair scan per decision (the default) and as K7 chains
+    (CCMI_PAIR_CHAINS=1, moves applied on the device): both decide exactly as the oracle."""
+    monkeypatch.setenv("CCMI_PAIR_CHAINS", pair_chains)
+    check_product_against_oracle(gpu_lib, dict(num_racks=5, num_brokers=20, num_replicas=6000, num_topics=300),
+                                 DEFAULT_GOALS, 1.05)
+    check_product_against_oracle(gpu_lib, dict(num_racks=8, num_brokers=300, num_replicas=30000, num_topics=1000),
+                                 ["LeaderReplicaDistributionGoal", "CpuUsageDistributionGoal",
+                                  "LeaderReplicaDistributionGoal"], 1.05)
+
+
 def test_gpu_chain_outlasting_stuck_bound(gpu_lib, oracle_lib, monkeypatch):
     """A K7 chain runs on workgroup 0 of the scan server alone; the other workgroups must wait for it however long it
     takes instead of applying the stuck-command bound to a command they are not part of. With the bound at 2 ms and
@@ -262,6 +274,7 @@ def test_gpu_chain_outlasting_stuck_bound(gpu_lib, oracle_lib, monkeypatch):
     and decides exactly as the oracle."""
     monkeypatch.setenv("CCMI_SERVER_STUCK_MS", "2")
     monkeypatch.setenv("CCMI_CHAIN_DELAY_US", "5000")
+    monkeypatch.setenv("CCMI_PAIR_CHAINS", "1")
     props = dict(num_racks=5, num_brokers=20, num_replicas=6000, num_topics=300)
     buf = ccmi.RandomCluster.generate(gpu_lib, **props)
     cm = ccmi.ClusterModel.from_buffers(buf, device=0)

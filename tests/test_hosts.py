@@ -188,14 +188,20 @@ def test_gpu_load_monitor_shared_host_matches_oracle(gpu_lib, oracle_lib):
 # tests/golden/c1_shared_hosts_default.json: C1's cluster, two brokers of a rack per host, the 16 default goals — the
 # K7 chains (LeaderReplicaDistribution, RackAware with optimized goals) apply moves with the host loads on the device
 # (apply.h host lanes). Pinned by the oracle's Host restatement only (no reference fixture shares a host).
-def test_emu_c1_shared_hosts_matches_golden(emu_lib, oracle_lib):
+@pytest.mark.parametrize("pair_chains", ["0", "1"])
+def test_emu_c1_shared_hosts_matches_golden(emu_lib, oracle_lib, monkeypatch, pair_chains):
     from parity import check_product_against_golden
+    monkeypatch.setenv("CCMI_PAIR_CHAINS", pair_chains)
     cm, _ = check_product_against_golden(emu_lib, "c1_shared_hosts_default")
-    assert cm.perf().chain_launches > 0  # the chains ran with shared hosts
+    if pair_chains == "1":
+        assert cm.perf().chain_launches > 0  # the chains ran with shared hosts
 
 
 @pytest.mark.gpu
-def test_gpu_c1_shared_hosts_matches_golden(gpu_lib, oracle_lib):
+@pytest.mark.parametrize("pair_chains", ["0", "1"])
+def test_gpu_c1_shared_hosts_matches_golden(gpu_lib, oracle_lib, monkeypatch, pair_chains):
     from parity import check_product_against_golden
+    monkeypatch.setenv("CCMI_PAIR_CHAINS", pair_chains)
     cm, res = check_product_against_golden(gpu_lib, "c1_shared_hosts_default", per_goal_stats=True)
-    assert cm.perf().chain_launches + cm.perf().server_chains > 0
+    if pair_chains == "1":
+        assert cm.perf().chain_launches + cm.perf().server_chains > 0

@@ -2,7 +2,7 @@
 # Round-5 GPU pass (one gpurun call): smoke, the -m gpu suite, the default C2 bench line. Every GPU step runs under
 # its own time limit; anything but success stops the script (no GPU step after a fault, abort or timeout).
 #   env: TAG (log names), PYTEST_K (a -k filter), SKIP_TESTS=1, SKIP_BENCH=1, BENCH_ARGS, ENVS (exported for every step),
-#        REHEARSE2=1 (bench --gpus 2 from a plain launch), PROBE=1 (CCMI_PROFILE=goal probe; PROBE_PROFILE, STAMPS=1 for CCMI_STAMPS), ROCPROF=1 (rocprofv3 kernel trace + stats of one bench step)
+#        REQ2=1 (bench --requests-per-gpu 2), REHEARSE2=1 (bench --gpus 2 from a plain launch), PROBE=1 (CCMI_PROFILE=goal probe; PROBE_PROFILE, STAMPS=1 for CCMI_STAMPS), ROCPROF=1 (rocprofv3 kernel trace + stats of one bench step)
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out
 T=${TAG:-r05}
@@ -30,6 +30,10 @@ if [ -z "$SKIP_BENCH" ]; then
   tail -3 "gpurun_out/bench_$T.err"
   [ $rc -eq 0 ] || { echo "stopping: bench exited $rc"; exit $rc; }
   python3 -c "import json; d=json.loads(open('gpurun_out/bench_$T.json').read().strip().splitlines()[-1]); print(d['value'], d['ms_per_step'], d.get('parity'))"
+fi
+if [ -n "$REQ2" ]; then  # two concurrent what-if proposals per step on the one GPU (sessions share its server budget)
+  step req2 900 python -u bench.py --requests-per-gpu 2 --steps 2 --warmup 1 --no-cpu-baseline --no-launch-pass ${BENCH_ARGS:-}
+  tail -1 "gpurun_out/req2_$T.log" | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('req2', d['value'], d['ms_per_step'], d['proposal_wall_s'], d['parity']['status'])"
 fi
 if [ -n "$REHEARSE2" ]; then  # the driver's plain multi-GPU form on the one-GPU box: two sessions share the card
   step gpus2 900 python -u bench.py --gpus 2 --steps 2 --warmup 1 --no-cpu-baseline ${BENCH_ARGS:-}
