@@ -241,6 +241,11 @@ Device::~Device() {
         std::fprintf(stderr, "[ccmi chain stamps] %llu chain_pairs launches, %llu accepts: %.2f us per launch in "
                              "evaluation, %.2f us applying, %.2f us in total (thread 0)\n",
                      h[8200], h[8201], h[8202] * 0.01 / h[8200], h[8203] * 0.01 / h[8200], h[8204] * 0.01 / h[8200]);
+      if (h[8236] || h[8238])
+        std::fprintf(stderr, "[ccmi row stamps] %llu scans with rows: busy %.2f us (the row writer arrived last in "
+                             "%llu); %llu scans without rows: busy %.2f us\n",
+                     h[8236], h[8236] ? h[8237] * 0.01 / h[8236] : 0.0, h[8235], h[8238],
+                     h[8238] ? h[8239] * 0.01 / h[8238] : 0.0);
       if (h[8240])
         std::fprintf(stderr, "[ccmi apply stamps] %llu applies: leadership loads %.2f us, step 0 %.2f us, step 1 %.2f us, "
                              "step 2 + end %.2f us; replica lanes %.2f us, end %.2f us (thread 0, summed over all applies "

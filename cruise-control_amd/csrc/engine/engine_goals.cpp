@@ -700,6 +700,9 @@ class ReplicaCapacity : public GoalImpl {
   void rebalance(Engine& e, int b) override {
     PhaseScope ps(PH_OTHER_GOALS);
     Model& m = e.m;
+    // the loop's break on its first replica (within the limit, and the first replica — offline ones sort first — not
+    // offline) without sorting the broker's replicas: bNoff counts b's current offline replicas
+    if ((int64_t)m.nrep(b) <= maxR && m.bNoff[b] == 0) return;
     const std::vector<int32_t> list = m.sorted(b, sortId(kind, false, false));
     std::vector<int32_t> order, cands;
     auto fail = [&](int r) {

@@ -1524,6 +1524,11 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, kServ
         const unsigned long long lo = v == kNone ? 0ull : (v + 1) & 0xffffffffull;
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         const unsigned long long busy = __builtin_amdgcn_s_memrealtime() - tStart;
+        if (T.stamps && c.op != SOP_CHAIN) {  // CCMI_STAMPS: busy time of scans with / without rows, the writer last
+          atomicAdd(&T.stamps[rows ? 8236 : 8238], 1ull);
+          atomicAdd(&T.stamps[rows ? 8237 : 8239], busy);
+          if (rows && writer) atomicAdd(&T.stamps[8235], 1ull);
+        }
         if (c.combineBlock)  // a shard group's scan: the group's last rank publishes mail[0] (shard_group.h)
           groupArrive(c.combineBlock, c.combineSlot, c.combineRank, c.combineCount, v, c.seq);
         else
