@@ -1315,6 +1315,10 @@ class ResourceDistribution : public GoalImpl {
   Model::SnapTable snapTab;  // moveIn's candidate-broker snapshots (one Spec per phase)
   Model::SnapTable swapTab;  // the swap phase's polled brokers' limit-free snapshots
   std::vector<uint8_t> queued;  // moveInLeadership: a group's broker is in the candidate queue (other entries: stale)
+  // leadership move-out on a materialised tree: contains() per broker memoised for one scan's rows
+  std::vector<uint32_t> containsStamp_;
+  std::vector<uint8_t> containsVal_;
+  uint32_t containsGen_ = 0;
   int nameBase() const { return 4 * kind; }
   int nameId(bool reverse, bool leader) const { return nameBase() + (reverse ? 1 : 0) + (leader ? 2 : 0); }
   bool excluded(int b) const { return !allowed[b]; }
@@ -1730,11 +1734,13 @@ class ResourceDistribution : public GoalImpl {
     // order) are kept between scans. Before the set is materialised only dst's membership and key change per accept
     // (b leads every row), so only rows with dst among their followers are rebuilt; after it, every row is (a search in
     // the stale-key tree may change for any broker).
-    std::vector<std::vector<int32_t>> rowCands;
-    std::vector<uint8_t> rowValid;
+    std::vector<std::vector<int32_t>> rowCands, rowFol;
+    std::vector<uint8_t> rowValid, rowFolSet;
     if (lead) {
       rowCands.resize(list.size());
       rowValid.assign(list.size(), 0);
+      rowFol.resize(list.size());
+      rowFolSet.assign(list.size(), 0);
     }
     size_t i = 0;
     while (i < list.size()) {
@@ -1763,14 +1769,35 @@ class ResourceDistribution : public GoalImpl {
           pr.clear();
           pb.clear();
           pairOwner.clear();
+          // the tree does not change within one scan's rows: each broker's search runs once per scan (generation-
+          // stamped memo, never cleared); a row's online followers do not change while b moves its leaders (a
+          // leadership move touches only its own partition), so they are taken once per row
+          if (built && ++containsGen_ == 0) {
+            containsStamp_.assign(m.B, 0);
+            containsGen_ = 1;
+          }
+          if (built && containsStamp_.size() != (size_t)m.B) containsStamp_.assign(m.B, 0);
+          if (built && containsVal_.size() != (size_t)m.B) containsVal_.assign(m.B, 0);
+          auto inCand = [&](int fb) {
+            if (!built) return inSet[fb] != 0;
+            if (containsStamp_[fb] != containsGen_) {
+              containsStamp_[fb] = containsGen_;
+              containsVal_[fb] = cand.contains(fb) ? 1 : 0;
+            }
+            return containsVal_[fb] != 0;
+          };
           for (size_t q = i; q < list.size(); ++q) {
             const int r = list[q];
             std::vector<int32_t>& rc = rowCands[q];
             if (built || !rowValid[q]) {
-              m.onlineFollowerBrokers(m.rPart[r], fol);
+              std::vector<int32_t>& rf = rowFol[q];
+              if (!rowFolSet[q]) {
+                m.onlineFollowerBrokers(m.rPart[r], rf);
+                rowFolSet[q] = 1;
+              }
               inorder.clear();
-              for (int fb : fol)
-                if (built ? cand.contains(fb) : inSet[fb] != 0) inorder.push_back(fb);
+              for (int fb : rf)
+                if (inCand(fb)) inorder.push_back(fb);
               std::sort(inorder.begin(), inorder.end(), [&](int x, int y) { return cmpBroker(m, x, y) < 0; });
               inorder.erase(std::unique(inorder.begin(), inorder.end()), inorder.end());
               e.eligible(inorder, DA_LEADERSHIP, rc);
