@@ -313,6 +313,11 @@ class GroupSession:
         return getattr(self.ranks[0], name)
 
 
+def progress(msg: str) -> None:
+    """A progress line on stderr (long runs print one per proposal; stdout carries only the result line)."""
+    print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
+
+
 def optimize(opt, s, goals, options):
     return s.optimize(opt, goals, options) if isinstance(s, GroupSession) else opt.optimizations(s, goals, options)
 
@@ -425,6 +430,7 @@ def main() -> None:
                 rs = list(wp.map(lambda s: optimize(opt, s, goals, options), wss))
         inst_perf, inst_cands = wss[0].perf(), rs[0].candidates
         del wss
+        progress(f"warmup {w + 1}/{max(1, args.warmup)}: {rs[0].seconds:.2f} s")
     # One more instrumented proposal with the scan server off (a launch per scan): the per-launch kernel times the
     # rocprofv3 trace of the same path can be checked against (rank 0, single GPU, outside the timed region).
     launch_perf = None
@@ -439,22 +445,25 @@ def main() -> None:
         opt.optimizations(ls, goals, options)
         launch_perf = ls.perf()
         del ls
+        progress("launch-path proposal done")
 
     S = max(1, args.requests_per_gpu) if not sharded else 1
     # cluster resident in HBM before timing starts: one session per proposal, [device][step][request]
     t_up = time.perf_counter()
     sessions = [[[session(d) for _ in range(S)] for _ in range(args.steps)] for d in local_devices]
     upload_s = (time.perf_counter() - t_up) / max(1, len(local_devices) * args.steps * S)
+    progress(f"{len(local_devices) * args.steps * S} sessions resident; timed region starts")
 
     def run_device(steps):  # one device's K steps in order, S concurrent proposals per step
         out = []
         pool = ThreadPoolExecutor(S) if S > 1 else None
         try:
-            for step_sessions in steps:
+            for k, step_sessions in enumerate(steps):
                 if pool is None:
                     out.extend(optimize(opt, s, goals, options) for s in step_sessions)
                 else:
                     out.extend(pool.map(lambda s: optimize(opt, s, goals, options), step_sessions))
+                progress(f"step {k + 1}/{len(steps)}: {out[-1].seconds:.2f} s")
         finally:
             if pool is not None:
                 pool.shutdown()
@@ -621,6 +630,7 @@ def main() -> None:
         "cpu_baseline": None,
     }
     if world == 1 and len(local_devices) == 1 and not args.no_cpu_baseline:
+        progress("cpu baseline")
         line["cpu_baseline"] = cpu_baseline(lib, buf, args.workload, goal_names, options, first, device,
                                             args.cpu_sample_seconds, args.what_if_procs)
     print(json.dumps(line))
