@@ -184,7 +184,7 @@ Device::Device(int ordinal, int B, int R, int P, int T, int maxGoalSlots)
       chainDelayTicks_ = (unsigned long long)std::max(0.0, std::atof(cd)) * 100ull;
     if (serverBlocks_ < 8) serverUsable_ = false;
     if (serverUsable_) {
-      dalloc(&dServerT0_, 16);  // [0] busy-time stamp, [8] the doorbell (a line of its own)
+      dalloc(&dServerT0_, 16);  // [0] busy-time stamp, [8] the doorbell (a line of its own), [12] the last published seq
       try {
         ensureFg(1 << 20);
         // snapshot pool: 16M rows (256 MB), host-written like the command block. A C2 proposal uploads ~10.6M rows
@@ -486,6 +486,7 @@ bool Device::ensureServer() {
   hipCheck(hipMemsetAsync(dDone_, 0, sizeof(unsigned int), ST), "reset server arrivals");
   hipCheck(hipMemsetAsync(dResult_, 0xff, sizeof(unsigned long long), ST), "reset server result");
   hipCheck(hipMemsetAsync(dServerT0_ + 8, 0, sizeof(unsigned long long), ST), "reset server doorbell");
+  hipCheck(hipMemsetAsync(dServerT0_ + 12, 0, sizeof(unsigned long long), ST), "reset server publication word");
   __atomic_store_n(&hResult_[7], lastCmdSeq_, __ATOMIC_RELEASE);  // the new launch's last command (parking, groups)
   serverTimed_ = timing;
   if (serverTimed_) (void)hipEventRecord((hipEvent_t)evS0_, ST);

@@ -791,8 +791,6 @@ bool Engine::optimizeGoalImpl(std::unique_ptr<GoalImpl>& g, ccmi_goal_result* re
      // the move applied on the host is faster (profiles/r06/README.md, chain A/B)
     const char* pc = std::getenv("CCMI_PAIR_CHAINS");
     pairChains = pc && pc[0] == '1' && !std::getenv("CCMI_NO_PAIR_CHAINS");
-    const char* ss = std::getenv("CCMI_SPEC_SCAN");  // A/B switch: 0 turns the speculative move-out scan off
-    specScans = !(ss && ss[0] == '0');
   }
   const ccmi_cluster_stats before = stats();
   g->finished = false;
@@ -1732,11 +1730,6 @@ class ResourceDistribution : public GoalImpl {
     const double upperSrc = excluded(b) ? 0 : upperThr;
     std::vector<int32_t> cands, pr, pb, fol;
     std::vector<int32_t> pairOwner;
-    // the scan speculated during a materialisation (replica form, helper-built trees, one shard, no terminal goal)
-    const bool specOn = useWorker && !lead && e.shard.count <= 1 && !e.terminalOptimized() && e.specScans;
-    bool specHave = false;
-    int64_t specKey = -1, specCount = 0;
-    std::vector<int32_t> specList, specCl;
     // Leadership form: each row's candidate brokers (its online followers that are members, eligible, in live (key, id)
     // order) are kept between scans. Before the set is materialised only dst's membership and key change per accept
     // (b leads every row), so only rows with dst among their followers are rebuilt; after it, every row is (a search in
@@ -1755,25 +1748,17 @@ class ResourceDistribution : public GoalImpl {
       size_t hitIdx = 0;
       if (!lead) {
         const std::vector<int32_t>* cl;
-        int64_t key;
-        if (specHave) {  // the speculative scan ran on exactly this candidate list (see the materialisation below)
-          specHave = false;
-          cl = &specCl;
-          key = specKey;
-          e.candidates += specCount;
-        } else {
-          {
-            PhaseScope pc(PH_CAND_BUILD);
-            // built: the tree's maintained sequence itself (no copy); else the lazy order, kept up to date below
-            const std::vector<int32_t>* seq = built ? cand.sequence() : &inorder;
-            if (!seq) {
-              cand.inorder(inorder);
-              seq = &inorder;
-            }
-            cl = &e.eligibleView(*seq, DA_MOVE, cands);
+        {
+          PhaseScope pc(PH_CAND_BUILD);
+          // built: the tree's maintained sequence itself (no copy); else the lazy order, kept up to date below
+          const std::vector<int32_t>* seq = built ? cand.sequence() : &inorder;
+          if (!seq) {
+            cand.inorder(inorder);
+            seq = &inorder;
           }
-          key = e.crossScan(*this, DA_MOVE, list, i, *cl);
+          cl = &e.eligibleView(*seq, DA_MOVE, cands);
         }
+        const int64_t key = e.crossScan(*this, DA_MOVE, list, i, *cl);
         if (key < 0) break;
         const int N = (int)cl->size();
         hitIdx = i + (size_t)(key / N);
@@ -1868,47 +1853,6 @@ class ResourceDistribution : public GoalImpl {
             const size_t bj = (size_t)(std::find(inorder.begin(), inorder.end(), b) - inorder.begin());
             clean = bj == n || fits(bj);
           }
-        }
-        if (!clean && !lead && specOn) {
-          // The next scan goes out on the order a clean update would give (dst re-placed by its live key) while the
-          // helper's tree is adopted and replayed during the scan's wait (Device::idleWork). The scan changes nothing:
-          // its result is used only when the tree's exact order equals the list it scanned, and thrown away (its
-          // candidates uncounted) otherwise, so the next scan is the reference's either way.
-          prof().count(9, "out.materialise");
-          specList.assign(inorder.begin(), inorder.end());
-          specList.erase(specList.begin() + (ptrdiff_t)at);
-          if (add) specList.insert(std::lower_bound(specList.begin(), specList.end(), dst, less), dst);
-          const std::vector<int32_t>& sl = e.eligibleView(specList, DA_MOVE, cands);
-          specCl.assign(sl.begin(), sl.end());
-          bool treeDone = false;
-          auto finishTree = [&]() {
-            if (treeDone) return false;
-            treeDone = true;
-            materialise();
-            cand.remove(dst);
-            if (add) cand.add(dst);
-            return false;
-          };
-          const int64_t c0 = e.candidates;
-          {
-            const Device::IdleScope idleSpec{e.dev};
-            e.dev->idleWork = finishTree;
-            specKey = e.crossScan(*this, DA_MOVE, list, hitIdx + 1, specCl);
-          }
-          specCount = e.candidates - c0;
-          e.candidates = c0;
-          finishTree();
-          i = hitIdx + 1;
-          const std::vector<int32_t>* seq = cand.sequence();
-          if (!seq) {
-            cand.inorder(inorder);
-            seq = &inorder;
-          }
-          const std::vector<int32_t>& exact = e.eligibleView(*seq, DA_MOVE, cands);
-          specHave = i < list.size() && exact == specCl;
-          if (specHave) prof().count(58, "out.spec.used");
-          else prof().count(59, "out.spec.dropped");
-          continue;
         }
         if (!clean) {
           prof().count(9, "out.materialise");

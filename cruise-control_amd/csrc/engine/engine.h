@@ -186,9 +186,6 @@ class Engine {
   // model (Model::replaying). Not used for destination-sharded sessions. CCMI_NO_CHAINS=1 turns them off.
   bool chainsOn() const;
   bool pairChains = false;  // the leadership loops run as K7 chains (CCMI_PAIR_CHAINS=1, set per goal; chainsOn too)
-  // a resource move-out call whose helper-built tree is materialised speculates its next scan meanwhile (CCMI_SPEC_SCAN,
-  // set per goal)
-  bool specScans = true;
   int64_t chainPairs(GoalImpl& self, int action, const std::vector<int32_t>& pr, const std::vector<int32_t>& pb,
                      const std::vector<int32_t>& next, int maxAccepts, std::vector<int32_t>& log);
   int64_t chainRackRows(GoalImpl& self, const std::vector<int32_t>& rows, const std::vector<int32_t>& cands,

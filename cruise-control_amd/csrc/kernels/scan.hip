@@ -1043,6 +1043,13 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, kServ
   unsigned long long last = startSeq;
   int progVer = -1;
   int acqEpoch = -1;  // ServerCmd.rowsEpoch of this workgroup's last acquire (-1: none since the launch)
+  // The acquire an epoch change needs is taken early when possible: once this workgroup's last command is published
+  // (the last arriver stores its sequence into pub, a device word beside the doorbell, after every participant's
+  // writes completed), the workgroup invalidates its L1 while it idles, so the next command's loads need no acquire
+  // of their own (an agent acquire is ~1.7 us of its first tile otherwise, MI355X_MICROARCH.md). acqFresh: no device
+  // write was published since that acquire.
+  unsigned long long* const pub = bell + 4;
+  bool acqFresh = false;
   unsigned long long idleSince = __builtin_amdgcn_s_memrealtime();
   bool participated = false;  // this workgroup took part in its last command (thread 0's view)
   bool lastGrouped = false;   // ... and that command was a shard group's scan
@@ -1059,6 +1066,12 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, kServ
       // with agent-scope loads, which the XCD's L2 serves until it changes (MI355X_MICROARCH.md hand-off table: one
       // lane's sc1 store, sc1 load polls). Only the command's participants then copy its header.
       for (int spin = 0;; ++spin) {
+        if (!acqFresh && last != startSeq &&
+            __hip_atomic_load(pub, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == last) {
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          acqFresh = true;
+        }
         if (blockIdx.x == 0) {
           const unsigned long long s = __hip_atomic_load(&cmd->seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
           if (s != last && !(s & kSeqBusy)) {
@@ -1142,10 +1155,15 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, kServ
       idleSince = __builtin_amdgcn_s_memrealtime();  // a stuck command is timed from when this workgroup took it
       // the rows workgroup 0 wrote for earlier commands (released before its arrivals) become visible with an agent
       // acquire; a command no earlier one wrote rows before needs none
-      if (!ex && c.rowsEpoch != acqEpoch && (uint32_t)blockIdx.x < (uint32_t)c.nActive) {
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        acqEpoch = c.rowsEpoch;
+      if (!ex && (uint32_t)blockIdx.x < (uint32_t)c.nActive) {
+        if (acqFresh) {
+          acqEpoch = c.rowsEpoch;  // acquired after the previous command's publication: nothing newer to see
+        } else if (c.rowsEpoch != acqEpoch) {
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+          acqEpoch = c.rowsEpoch;
+        }
       }
+      acqFresh = false;  // this command may write (its rows, a chain's moves) before the next one
       SRV_STAMP(T, 1);
       if (blockIdx.x == 0)  // busy-time stamp, read by the last workgroup to arrive
         __hip_atomic_store(t0, __builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1539,6 +1557,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, kServ
         // before its next command (Device::collectServerBusy) instead of the publish waiting for a second PCIe write
         __hip_atomic_store(&mail[5], ((c.seq & 0xffffffull) << 40) | (busy & ((1ull << 40) - 1)), __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_SYSTEM);
+        // every participant arrived after its writes completed: the idle workgroups may take their acquire now
+        __hip_atomic_store(pub, c.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
     }
     last = c.seq;

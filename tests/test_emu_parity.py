@@ -138,17 +138,13 @@ def test_emu_speculative_host_work_matches_oracle(emu_lib, oracle_lib, monkeypat
     check_product_against_oracle(emu_lib, dict(num_brokers=80), DEFAULT_GOALS, 1.05, max_replicas=1500)
 
 
-@pytest.mark.parametrize("spec", ["1", "0"])
 @pytest.mark.parametrize("props", [dict(num_brokers=80), dict(num_racks=5, num_brokers=20, num_replicas=6000,
                                                                num_topics=300)])
-def test_emu_tree_worker_matches_oracle(emu_lib, oracle_lib, monkeypatch, props, spec):
+def test_emu_tree_worker_matches_oracle(emu_lib, oracle_lib, monkeypatch, props):
     """The move-out entry tree built on the helper thread (TreeWorker, on by default from 2048 brokers; forced here for
-    small clusters): adopted by materialise(), or superseded by the next call's submission when no step needs it. With
-    the speculative scan (default; CCMI_SPEC_SCAN=0 off) the next scan runs on the clean-update order while the tree is
-    adopted during its wait, and is used only when the tree's exact order equals it."""
+    small clusters): adopted by materialise(), or superseded by the next call's submission when no step needs it."""
     monkeypatch.setenv("CCMI_TREE_WORKER", "1")
     monkeypatch.setenv("CCMI_TREE_WORKER_MIN", "1")
-    monkeypatch.setenv("CCMI_SPEC_SCAN", spec)
     check_product_against_oracle(emu_lib, props, DEFAULT_GOALS, 1.05, max_replicas=1500)
 
 

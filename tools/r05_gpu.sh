@@ -44,7 +44,8 @@ if [ -n "$PROBE" ]; then  # per-goal phase profile of one C2 optimization
     step probe 600 python -u tools/probe.py --workload ${WORKLOAD:-c2} ) || exit $?
   grep -E "^total|^perf|stamps\]" "gpurun_out/probe_$T.log"
 fi
-if [ -n "$ROCPROF" ]; then  # kernel trace + stats of one bench step
-  step rocprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_$T -o bench -- \
-    python3 -u bench.py --steps 1 --warmup 1 --no-cpu-baseline ${BENCH_ARGS:-}
+if [ -n "$ROCPROF" ]; then  # kernel trace + stats of one bench step (the per-dispatch trace stays in /tmp)
+  step rocprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d /tmp/prof_$T -o bench -- \
+    python3 -u bench.py --steps ${PROF_STEPS:-1} --warmup 1 --no-cpu-baseline
+  mkdir -p gpurun_out/prof_$T && find /tmp/prof_$T -name "*stats.csv" -exec cp {} gpurun_out/prof_$T/ \;
 fi
