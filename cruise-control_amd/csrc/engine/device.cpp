@@ -616,7 +616,8 @@ int64_t Device::serverRun(const DevProgram& prog, const Staged& g, int op, const
   const uint64_t site = (uint64_t)op | ((uint64_t)(uint32_t)prog.action << 3) | ((uint64_t)(uint32_t)prog.nGoals << 8) |
                         ((uint64_t)(uint32_t)prog.filter << 16) | ((uint64_t)sliced << 24);
   {  // every tile of the first sweep gets its own workgroup; a smaller scan leaves the others out of the command
-    uint64_t total = op == SOP_PAIRS ? (uint64_t)params[0] : (uint64_t)params[0] * (uint64_t)params[1];
+    const uint64_t whole = op == SOP_PAIRS ? (uint64_t)params[0] : (uint64_t)params[0] * (uint64_t)params[1];
+    uint64_t total = whole;
     if (adaptiveWidth_) {
       // Speculative width: the first sweep covers twice the depth of this site's last winner (plus eight tiles), or
       // everything after a scan without one. Tiles past the winner are evaluated for nothing (their reads are the
@@ -644,6 +645,9 @@ int64_t Device::serverRun(const DevProgram& prog, const Staged& g, int op, const
       }
     c.goalParts = parts;
     c.nActive = (int32_t)std::min<uint64_t>(wgsFor(parts), (uint64_t)serverBlocks_);
+    if (prof().on && op == SOP_PAIRS)  // CCMI_PROFILE: pair-scan sizes
+      prof().count(whole <= 64 ? 58 : whole <= 256 ? 59 : whole <= 2048 ? 60 : 61,
+                   whole <= 64 ? "pairs.n<=64" : whole <= 256 ? "pairs.n<=256" : whole <= 2048 ? "pairs.n<=2048" : "pairs.n>2048");
   }
   const bool grouped = grpHost_ && combineArmed_ && (op == SOP_CROSS || op == SOP_SEGS || op == SOP_PAIRS);
   if (grouped) {  // the server folds this scan's key into the group's slot; the group's last rank publishes the minimum
@@ -820,6 +824,8 @@ DevTables Device::tables() const {
   t.ldB = ldB_;
   static const int pollMode = std::getenv("CCMI_SERVER_POLL") ? std::atoi(std::getenv("CCMI_SERVER_POLL")) : 0;
   t.pollMode = pollMode;
+  static const int seqRecheck = std::getenv("CCMI_SEQ_RECHECK") ? std::atoi(std::getenv("CCMI_SEQ_RECHECK")) : 0;
+  t.seqRecheck = seqRecheck;
   t.stuckTicks = stuckTicks_;
   t.parkTicks = parkTicks_;
   t.chainDelayTicks = chainDelayTicks_;

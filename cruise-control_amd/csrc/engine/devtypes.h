@@ -165,6 +165,8 @@ struct DevTables {
   int32_t B, R, P, ldB;
   // scan server idle poll (CCMI_SERVER_POLL): 0 = back off (s_sleep 4, then 16 after 256 polls), 1 = spin, 2 = s_sleep 1
   int32_t pollMode;
+  // 1: workgroup 0 re-reads the sequence word after copying a header (CCMI_SEQ_RECHECK=1); 0 (default): one read
+  int32_t seqRecheck;
   // the scan server's stuck-command bound in s_memrealtime ticks (CCMI_SERVER_STUCK_MS, default 10 s) and a test-only
   // delay added to every chain command (CCMI_CHAIN_DELAY_US, default 0: a chain that outlasts a short bound)
   unsigned long long stuckTicks;
@@ -293,8 +295,10 @@ struct alignas(16) ServerCmd {
   unsigned long long combineBlock;
   int32_t combineSlot, combineRank, combineCount, combinePad;
 };
-// The sequence word is a seqlock: the host stores (next | kSeqBusy) before it rewrites the other fields and `next`
-// after; a workgroup accepts a header only when the word it read before and after its copy is the same, not busy.
+// The sequence word: the host stores (next | kSeqBusy) before it rewrites the other fields and `next` after them, each
+// behind a store fence; a workgroup copies the header once it reads a new sequence that is not busy (the fields landed
+// first, and the host rewrites them only after that command's result). DevTables.seqRecheck adds the seqlock's second
+// read of the word after the copy.
 constexpr unsigned long long kSeqBusy = 1ull << 63;
 static_assert(sizeof(ServerCmd) % 16 == 0, "ServerCmd words");
 

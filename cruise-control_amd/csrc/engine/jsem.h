@@ -72,7 +72,13 @@ struct JavaRandom {
 // Nodes are one 20-byte record each (key, links, colour) so a search step is one cache line.
 struct RbNode {
   uint32_t kc;  // key (a non-negative int) with the colour in bit 31
-  int left, right, parent;
+  union {
+    struct {
+      int left, right;
+    };
+    int ch[2];  // ch[0] = left, ch[1] = right: the build's fix-up picks a side by index instead of by branch
+  };
+  int parent;
   int key() const { return (int)(kc & 0x7fffffffu); }
   bool red() const { return (kc >> 31) != 0; }
   void setRed(bool r) { kc = (kc & 0x7fffffffu) | ((uint32_t)r << 31); }
@@ -180,7 +186,6 @@ class RbTreeSet {
   // tree is complete); the tree must not be used before.
   void buildStart(std::vector<int>&& ids, std::vector<int32_t>&& rank, bool withSequence = true) {
     bSeq_ = withSequence;
-    n_.clear();
     free_.clear();
     root_ = -1;
     size_ = 0;
@@ -190,7 +195,8 @@ class RbTreeSet {
     int32_t nr = 0;
     for (int k : bIds_) nr = std::max(nr, bRank_[k] + 1);
     bNr_ = nr;
-    n_.resize(nr);  // ranks no id takes stay unused slots
+    n_.resize(nr);  // every put writes its rank's node whole; ranks no id takes stay unused (never linked), so the
+                    // slots kept from an earlier build are not cleared
     bW_.assign((nr + 63) >> 6, 0);
     bSw_.assign((bW_.size() + 63) >> 6, 0);
     seqOn_ = false;
@@ -203,24 +209,30 @@ class RbTreeSet {
     for (size_t e = bNext_; e < end; ++e) {
       const int k = bIds_[e];
       const int32_t rk = bRank_[k];
+#ifndef CCMI_TREE_PF
+#define CCMI_TREE_PF 0
+#endif
+#if CCMI_TREE_PF > 0
+      if (e + CCMI_TREE_PF < bIds_.size()) {  // a later put's node and in-order neighbours into cache ahead of its turn
+        const int32_t r2 = bRank_[bIds_[e + CCMI_TREE_PF]];
+        __builtin_prefetch(&N[r2], 1, 3);
+        const int32_t p2 = bPred(r2), s2 = bSucc(r2);
+        if (p2 >= 0) __builtin_prefetch(&N[p2], 1, 3);
+        if (s2 >= 0) __builtin_prefetch(&N[s2], 1, 3);
+      }
+#endif
       if (e == 0) {
         N[rk] = Node{(uint32_t)k, -1, -1, -1};
         root_ = rk;
         size_ = 1;
       } else {
-        const int32_t pr = bPred(rk);
-        int parent;
-        bool goLeft;
-        if (pr >= 0 && N[pr].right < 0) {
-          parent = pr;
-          goLeft = false;
-        } else {
-          parent = bSucc(rk);
-          goLeft = true;
-        }
-        N[rk] = Node{(uint32_t)k, -1, -1, parent};
-        (goLeft ? N[parent].left : N[parent].right) = rk;
-        insertFix(rk);
+        // the empty link between the in-order neighbours: the predecessor's right one when free, else the successor's left
+        const int32_t pr = bPred(rk), sc = bSucc(rk);
+        const int side = pr >= 0 && N[pr].right < 0 ? 1 : 0;
+        const int parent = side ? pr : sc;
+        N[rk] = Node{(uint32_t)k, {{-1, -1}}, parent};
+        N[parent].ch[side] = rk;
+        insertFixDir(N, rk);
         ++size_;
       }
       bW_[rk >> 6] |= 1ull << (rk & 63);
@@ -476,6 +488,47 @@ class RbTreeSet {
         N[g].setRed(1);
         rotL(g);
       }
+      break;
+    }
+    N[root_].setRed(0);
+  }
+  // insertFix with the two mirrored cases folded by side index (d: the side of g that p hangs on), for the builds:
+  // the same recolourings and rotations in the same order, fewer data-dependent branches
+  void rotDir(Node* N, int p, int d) {  // rotate p down to side d: its child on side 1 - d takes its place
+    const int c = N[p].ch[1 - d];
+    const int cc = N[c].ch[d];
+    N[p].ch[1 - d] = cc;
+    if (cc >= 0) N[cc].parent = p;
+    const int pp = N[p].parent;
+    N[c].parent = pp;
+    if (pp < 0) root_ = c;
+    else N[pp].ch[N[pp].ch[1] == p ? 1 : 0] = c;
+    N[c].ch[d] = p;
+    N[p].parent = c;
+  }
+  void insertFixDir(Node* N, int x) {
+    N[x].setRed(1);
+    while (x != root_) {
+      int p = N[x].parent;
+      if (!N[p].red()) break;
+      const int g = N[p].parent;
+      const int d = N[g].ch[1] == p ? 1 : 0;
+      const int y = N[g].ch[1 - d];
+      if (y >= 0 && N[y].red()) {
+        N[p].setRed(0);
+        N[y].setRed(0);
+        N[g].setRed(1);
+        x = g;
+        continue;
+      }
+      if (x == N[p].ch[1 - d]) {  // the inner grandchild: p rotates down to side d first
+        x = p;
+        rotDir(N, x, d);
+        p = N[x].parent;
+      }
+      N[p].setRed(0);
+      N[g].setRed(1);
+      rotDir(N, g, 1 - d);
       break;
     }
     N[root_].setRed(0);

@@ -1075,9 +1075,11 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, kServ
         if (blockIdx.x == 0) {
           const unsigned long long s = __hip_atomic_load(&cmd->seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
           if (s != last && !(s & kSeqBusy)) {
-            // the copy counts only when the sequence word did not change across it (seqlock, devtypes.h)
+            // One read of the sequence word suffices: the host stores the header's other fields, a store fence, then
+            // the new sequence (Device::postCommand), so they landed before it did, and it rewrites them only after
+            // this command's result, which waits for this copy. (T.seqRecheck: the seqlock's second read as well.)
             copySysOneThread(&c, cmd);
-            if (__hip_atomic_load(&cmd->seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == s) {
+            if (!T.seqRecheck || __hip_atomic_load(&cmd->seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == s) {
               const unsigned long long ring = kBellValid | (c.op == SOP_EXIT ? kBellExit : 0ull) |
                                               ((unsigned long long)(uint32_t)c.nActive << 32) | (s & 0xffffffffull);
               __hip_atomic_store(bell, ring, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
