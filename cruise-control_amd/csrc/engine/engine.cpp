@@ -1147,7 +1147,8 @@ class ReplicaDistribution : public GoalImpl {
 // turns it off. profiles/r04/tree_worker_ab_*.txt: tree.build 1.12 -> 0.79 s and whole C2 proposals 7.36-7.43 ->
 // 6.15-6.71 s on one box (round 3's version, which spun on the driver side, had cost 1.3-2.5 s on some boxes).
 // Workers are leased per move-out call from one process-wide pool (TreeWorkerPool) of at most CCMI_TREE_WORKERS
-// threads (default 4): concurrent sessions share them, and a call that finds none free builds on its own thread.
+// threads (default 8, one per session of an 8-GPU node's plain multi-GPU bench): concurrent sessions share them, and a
+// call that finds none free builds on its own thread.
 class TreeWorker {
  public:
   struct RankOnly {  // buildByRank never compares
@@ -1283,11 +1284,11 @@ class TreeWorkerPool {
  private:
   TreeWorkerPool() {
     const char* e = std::getenv("CCMI_TREE_WORKERS");
-    cap_ = e ? std::max(0, std::atoi(e)) : 4;
+    cap_ = e ? std::max(0, std::atoi(e)) : 8;
   }
   std::mutex mu_;
   std::vector<std::unique_ptr<TreeWorker>> free_;
-  int live_ = 0, cap_ = 4;
+  int live_ = 0, cap_ = 8;
 };
 struct TreeLease {  // one move-out call's worker (or none)
   std::unique_ptr<TreeWorker> w;

@@ -2,9 +2,11 @@
 // every broker's sorted view and its rows' upload). The calling thread takes part in its own loop and returns as soon
 // as every index is done; helpers wake on a condition variable and share the remaining indices, so a short loop runs
 // on the caller alone without waiting for a wake-up. Jobs are reference-counted: a helper that wakes after the loop
-// finished finds nothing left and drops its reference. One loop at a time per process; a caller that finds the pool
-// busy (another session's loop) runs its loop alone. CCMI_SYNC_THREADS (default 8) counts the caller. A helper runs
-// each job on the CPU mask of the job's caller (CpuMask::follow): the pool belongs to no session's NUMA node.
+// finished finds nothing left and drops its reference. The helpers form crews of CCMI_SYNC_THREADS - 1 (the count
+// includes the caller; default 8); a crew runs one loop at a time, and concurrent sessions (one per GPU of a node, or
+// several what-if sessions) each take a free crew — a new one is started on demand up to CCMI_SYNC_CREWS (default 8);
+// a caller that finds every crew busy runs its loop alone. A helper runs each job on the CPU mask of the job's caller
+// (CpuMask::follow): the crews belong to no session's NUMA node.
 #pragma once
 #include <atomic>
 #include <condition_variable>
@@ -25,30 +27,33 @@ namespace ccmi {
 class HostPool {
  public:
   static HostPool& get() {
-    static HostPool* p = new HostPool();  // never destroyed: helpers stay parked on the condition variable
+    static HostPool* p = new HostPool();  // never destroyed: helpers stay parked on their crews' condition variables
     return *p;
   }
   int threads() const { return threads_; }
-  // f(i) for every i in [0, n), on the caller and the helpers; returns when all are done
+  // f(i) for every i in [0, n), on the caller and a crew's helpers; returns when all are done
   void parallelFor(int n, const std::function<void(int)>& f) {
     if (n <= 0) return;
-    std::unique_lock<std::mutex> busy(runMu_, std::try_to_lock);
-    if (threads_ <= 1 || n == 1 || !busy.owns_lock()) {
+    Crew* c = threads_ > 1 && n > 1 ? acquire() : nullptr;
+    if (!c) {
       for (int i = 0; i < n; ++i) f(i);
       return;
     }
     auto job = std::make_shared<Job>(n, f);
     job->mask = CpuMask::current();  // the helpers run this job on the caller's CPUs
     {
-      std::lock_guard<std::mutex> l(mu_);
-      job_ = job;
-      ++gen_;
+      std::lock_guard<std::mutex> l(c->mu);
+      c->job = job;
+      ++c->gen;
     }
-    cv_.notify_all();
+    c->cv.notify_all();
     run(*job);
     while (job->done.load(std::memory_order_acquire) < n) _mm_pause();
-    std::lock_guard<std::mutex> l(mu_);
-    if (job_ == job) job_.reset();
+    {
+      std::lock_guard<std::mutex> l(c->mu);
+      if (c->job == job) c->job.reset();
+    }
+    release(c);
   }
 
  private:
@@ -59,6 +64,13 @@ class HostPool {
     CpuMask mask;
     std::atomic<int> next{0}, done{0};
   };
+  struct Crew {  // threads_ - 1 helpers sharing one job slot
+    std::mutex mu;
+    std::condition_variable cv;
+    std::shared_ptr<Job> job;
+    uint64_t gen = 0;
+    bool busy = false;  // guarded by HostPool::crewMu_
+  };
   static void run(Job& j) {
     for (int i; (i = j.next.fetch_add(1, std::memory_order_relaxed)) < j.n;) {
       j.f(i);
@@ -68,19 +80,38 @@ class HostPool {
   HostPool() {
     const char* e = std::getenv("CCMI_SYNC_THREADS");
     threads_ = e ? std::max(1, std::atoi(e)) : 8;
-    for (int t = 1; t < threads_; ++t) std::thread([this] { loop(); }).detach();
+    const char* c = std::getenv("CCMI_SYNC_CREWS");
+    maxCrews_ = c ? std::max(1, std::atoi(c)) : 8;
   }
-  void loop() {
+  Crew* acquire() {
+    std::lock_guard<std::mutex> l(crewMu_);
+    for (auto& c : crews_)
+      if (!c->busy) {
+        c->busy = true;
+        return c.get();
+      }
+    if ((int)crews_.size() >= maxCrews_) return nullptr;
+    crews_.push_back(std::unique_ptr<Crew>(new Crew()));  // never destroyed: its helpers hold its address
+    Crew* c = crews_.back().get();
+    c->busy = true;
+    for (int t = 1; t < threads_; ++t) std::thread([this, c] { loop(c); }).detach();
+    return c;
+  }
+  void release(Crew* c) {
+    std::lock_guard<std::mutex> l(crewMu_);
+    c->busy = false;
+  }
+  void loop(Crew* c) {
     pthread_setname_np(pthread_self(), "ccmi-sync");
     uint64_t seen = 0;
     CpuMask mine = CpuMask::current();
     for (;;) {
       std::shared_ptr<Job> j;
       {
-        std::unique_lock<std::mutex> l(mu_);
-        cv_.wait(l, [&] { return gen_ != seen; });
-        seen = gen_;
-        j = job_;
+        std::unique_lock<std::mutex> l(c->mu);
+        c->cv.wait(l, [&] { return c->gen != seen; });
+        seen = c->gen;
+        j = c->job;
       }
       if (j) {
         mine.follow(j->mask);
@@ -88,11 +119,9 @@ class HostPool {
       }
     }
   }
-  int threads_ = 1;
-  std::mutex runMu_, mu_;
-  std::condition_variable cv_;
-  std::shared_ptr<Job> job_;
-  uint64_t gen_ = 0;
+  int threads_ = 1, maxCrews_ = 8;
+  std::mutex crewMu_;
+  std::vector<std::unique_ptr<Crew>> crews_;  // guarded by crewMu_
 };
 
 }  // namespace ccmi
