@@ -472,13 +472,30 @@ void Device::callEnd() {
 
 bool Device::ensureServer() {
   if (serverOn_ && nowSeconds() - lastServerUse_ > 0.25) stopServer();
-  if (serverOn_) return true;
+  if (serverOn_) {
+    // A running server is resized when the device's concurrent calls changed its share: shrunk when another call
+    // began (that call's server needs the workgroups this one holds, one workgroup per CU), grown when its share at
+    // least doubled. The stop retires the launch between two commands, and the relaunch below takes the new share.
+    int target;
+    {
+      std::lock_guard<std::mutex> lk(g_serverMu);
+      const int active = std::max(1, g_activeCalls[ordinal_ & 63]);
+      const int want = std::min(serverBlocksCap_, std::max(8, kServerBudget / active / 8 * 8));
+      const int room = kServerBudget - g_serverWgs[ordinal_ & 63] + serverBlocks_;  // with this server's returned
+      target = std::min(want, room / 8 * 8);
+    }
+    if (target == serverBlocks_ || (target > serverBlocks_ && target < 2 * serverBlocks_)) return true;
+    stopServer();
+  }
   progSent_ = false;
   {
     std::lock_guard<std::mutex> lk(g_serverMu);
     const int active = std::max(1, g_activeCalls[ordinal_ & 63]);
-    const int want = std::min(serverBlocksCap_, std::max(8, kServerBudget / active / 8 * 8));
-    if (g_serverWgs[ordinal_ & 63] + want > kServerBudget) return false;
+    // this call's share of the device's server budget, or what the other calls' servers leave of it (they shrink to
+    // their own shares at their next commands)
+    const int room = (kServerBudget - g_serverWgs[ordinal_ & 63]) / 8 * 8;
+    const int want = std::min({serverBlocksCap_, std::max(8, kServerBudget / active / 8 * 8), room});
+    if (want < 8) return false;
     g_serverWgs[ordinal_ & 63] += want;
     serverBlocks_ = want;  // this launch's workgroups (the stop returns them)
   }
