@@ -31,6 +31,7 @@ def helper_threads():
 
 def main():
     name, sessions = sys.argv[1], int(sys.argv[2])
+    stagger = float(sys.argv[3]) if len(sys.argv) > 3 else 0.0  # seconds between the sessions' starts
     lib = ccmi.Library.get(os.path.join(os.path.dirname(HERE), "cruise-control_amd", "libccmi.so"))
     g = golden(name)
     bc = constraint(g["resource_balance_percentage"], g.get("max_replicas_per_broker"), g.get("capacity_threshold"))
@@ -47,9 +48,12 @@ def main():
     th.start()
     opt = ccmi.GoalOptimizer(bc)
     t0 = time.perf_counter()
+    def one(i):
+        time.sleep(i * stagger)
+        return opt.optimizations(cms[i], ccmi.goals_from_names(g["goals"]), golden_options(g))
+
     with ThreadPoolExecutor(sessions) as pool:
-        results = list(pool.map(lambda cm: opt.optimizations(cm, ccmi.goals_from_names(g["goals"]), golden_options(g)),
-                                cms))
+        results = list(pool.map(one, range(sessions)))
     wall = time.perf_counter() - t0
     stop[0] = True
     th.join()
@@ -57,7 +61,9 @@ def main():
         check_against_golden(g, cm.actions(), cm.replica_distribution(), cm.leader_distribution(), res.goal_results,
                              res.goal_results[-1].stats, replica_disks=cm.replica_disks())
     print(json.dumps({"sessions": sessions, "peak_helper_threads": peak[0], "after": helper_threads(),
-                      "actions": len(cms[0].actions()), "wall_s": wall}))
+                      "actions": len(cms[0].actions()), "wall_s": wall,
+                      "server_scans": [cm.perf().server_scans for cm in cms],
+                      "scan_launches": [cm.perf().scan_launches for cm in cms]}))
 
 
 if __name__ == "__main__":
