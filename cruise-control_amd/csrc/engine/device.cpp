@@ -156,8 +156,8 @@ Device::Device(int ordinal, int B, int R, int P, int T, int maxGoalSlots)
   ensureStage(1 << 20);
   ensureReq(1 << 20);
   if (std::getenv("CCMI_STAMPS")) {
-    dalloc(&stamps_, 1024 * 8 + 64);  // + the scan server's phase sums at [8192, 8256)
-    hipCheck(hipMemset(stamps_, 0, (1024 * 8 + 64) * sizeof(unsigned long long)), "hipMemset");
+    dalloc(&stamps_, 1024 * 8 + 128);  // + the scan server's phase sums at [8192, 8320)
+    hipCheck(hipMemset(stamps_, 0, (1024 * 8 + 128) * sizeof(unsigned long long)), "hipMemset");
   }
   hipCheck(hipEventCreate((hipEvent_t*)&ev0_), "hipEventCreate");
   hipCheck(hipEventCreate((hipEvent_t*)&ev1_), "hipEventCreate");
@@ -210,7 +210,7 @@ Device::~Device() {
   }
   if (ST) (void)hipStreamSynchronize(ST);
   if (stamps_) {  // average in-launch phase times of the last 1024 cross/pair scans (workgroup 0)
-    std::vector<unsigned long long> h(1024 * 8 + 64);
+    std::vector<unsigned long long> h(1024 * 8 + 128);
     if (hipMemcpy(h.data(), stamps_, h.size() * 8, hipMemcpyDeviceToHost) == hipSuccess) {
       if (h[8192])
         std::fprintf(stderr, "[ccmi server stamps] %llu scan commands: copy+acquire %.2f us, stage %.2f us, first tile "
@@ -252,6 +252,12 @@ Device::~Device() {
                              "/ applies)\n",
                      h[8240], h[8241] * 0.01 / h[8240], h[8242] * 0.01 / h[8240], h[8243] * 0.01 / h[8240],
                      h[8244] * 0.01 / h[8240], h[8245] * 0.01 / h[8240], h[8246] * 0.01 / h[8240]);
+      for (int o : {8256, 8261})
+        if (h[o])
+          std::fprintf(stderr, "[ccmi tile stamps] %llu %s commands, first tile: request landed %.2f us, rows staged %.2f us, "
+                       "view loads %.2f us, conjunction to the first slot %.2f us (workgroup 0)\n",
+                       h[o], o == 8256 ? "pair" : "cross", h[o + 1] * 0.01 / h[o], h[o + 2] * 0.01 / h[o],
+                       h[o + 3] * 0.01 / h[o], h[o + 4] * 0.01 / h[o]);
       if (h[8250])
         std::fprintf(stderr, "[ccmi chain eval stamps] %llu tiles: view loads %.2f us, conjunction %.2f us, tile "
                              "reduction %.2f us (thread 0)\n",

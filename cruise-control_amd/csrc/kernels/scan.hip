@@ -1053,7 +1053,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, kServ
   unsigned long long idleSince = __builtin_amdgcn_s_memrealtime();
   bool participated = false;  // this workgroup took part in its last command (thread 0's view)
   bool lastGrouped = false;   // ... and that command was a shard group's scan
-  unsigned long long srvT[6] = {0, 0, 0, 0, 0, 0};
+  unsigned long long srvT[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // (6: the first tile's request landed, 7: rows staged)
   unsigned long long qBatch = 0, qTiles = 0;  // CCMI_STAMPS, SOP_QUEUE: workgroup 0's batch-loaded stamp and tiles
   for (;;) {
     if (threadIdx.x == 0) {
@@ -1303,7 +1303,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, kServ
           rq = ldSysRow(A + 4 * (size_t)k);
           dq = ldSys(C + j);
         }
+        if (firstTile) SRV_STAMP(T, 6);
         if (!staged) stage();
+        if (firstTile) SRV_STAMP(T, 7);
         bool ok = false;
         if (q < total) {
           PreView v;
@@ -1474,12 +1476,15 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, kServ
           rq = ldSysRow(A + 4 * (size_t)q);
           dq = ldSys(C + q);
         }
+        if (firstTile) SRV_STAMP(T, 6);
         if (!staged) stage();
+        if (firstTile) SRV_STAMP(T, 7);
         bool ok = false;
         if (q < n) {
           PreView v;
           v.loadDst(T, dq, ov);
           v.loadRowRef(T, prog, rq, ov);
+          if (firstTile) SRV_STAMP(T, 5);
           ok = !v.exclLeadBlocked(prog) && moveCandidateAcceptedPart(prog, v, v.r, v.dst, part, parts);
         }
         const int f = tileFirst(ok, parts);
@@ -1530,9 +1535,20 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, kServ
         srvT[4] = __builtin_amdgcn_s_memrealtime();
         atomicAdd(&T.stamps[8192 + 0], 1ull);
         for (int i = 0; i < 4; ++i) atomicAdd(&T.stamps[8192 + 1 + i], srvT[i + 1] - srvT[i]);
-        if (srvT[5] > srvT[2] && srvT[5] <= srvT[3]) {  // cross / segment commands: ready -> view loads landed
+        if (srvT[5] > srvT[2] && srvT[5] <= srvT[3] && c.op != SOP_PAIRS) {  // cross / segment: ready -> views landed
           atomicAdd(&T.stamps[8197], srvT[5] - srvT[2]);
           atomicAdd(&T.stamps[8198], 1ull);
+        }
+        // the first tile in four parts, pair commands at [8256..8260], cross commands at [8261..8265]: ready -> the
+        // request landed (6), -> rows staged (7), -> view loads landed (5), -> the tile's first slot (3)
+        if ((c.op == SOP_PAIRS || c.op == SOP_CROSS) && srvT[2] < srvT[6] && srvT[6] <= srvT[7] && srvT[7] <= srvT[5] &&
+            srvT[5] <= srvT[3]) {
+          const int o = c.op == SOP_PAIRS ? 8256 : 8261;
+          atomicAdd(&T.stamps[o], 1ull);
+          atomicAdd(&T.stamps[o + 1], srvT[6] - srvT[2]);
+          atomicAdd(&T.stamps[o + 2], srvT[7] - srvT[6]);
+          atomicAdd(&T.stamps[o + 3], srvT[5] - srvT[7]);
+          atomicAdd(&T.stamps[o + 4], srvT[3] - srvT[5]);
         }
       }
       if (prev == nAct - 1) {
