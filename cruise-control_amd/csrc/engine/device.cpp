@@ -176,6 +176,7 @@ Device::Device(int ordinal, int B, int R, int P, int T, int maxGoalSlots)
     if (const char* sa = std::getenv("CCMI_SERVER_APPLY")) applyViaServer_ = sa[0] != '0';
     if (const char* gw = std::getenv("CCMI_GOAL_SPLIT_WGS")) goalSplitWgs_ = (int)std::strtol(gw, nullptr, 10);
     if (const char* sw = std::getenv("CCMI_SCAN_WIDTH")) adaptiveWidth_ = std::strcmp(sw, "full") != 0;
+    if (const char* ws = std::getenv("CCMI_WG_GOAL_SPLIT")) wgGoalSplit_ = ws[0] != '0';
     if (const char* sm = std::getenv("CCMI_SERVER_STUCK_MS"))
       stuckTicks_ = (unsigned long long)std::max(1.0, std::atof(sm)) * 100000ull;  // 100 MHz s_memrealtime
     if (const char* pk = std::getenv("CCMI_GROUP_PARK_US"))
@@ -184,7 +185,8 @@ Device::Device(int ordinal, int B, int R, int P, int T, int maxGoalSlots)
       chainDelayTicks_ = (unsigned long long)std::max(0.0, std::atof(cd)) * 100ull;
     if (serverBlocks_ < 8) serverUsable_ = false;
     if (serverUsable_) {
-      dalloc(&dServerT0_, 16);  // [0] busy-time stamp, [8] the doorbell (a line of its own), [12] the last published seq
+      dalloc(&dServerT0_, 16);  // [0] busy-time stamp, [4] shared-goal pair mask, [8] the doorbell (a line of its own),
+                                // [12] the last published seq
       try {
         ensureFg(1 << 20);
         // snapshot pool: 16M rows (256 MB), host-written like the command block. A C2 proposal uploads ~10.6M rows
@@ -510,6 +512,7 @@ bool Device::ensureServer() {
   hipCheck(hipMemsetAsync(dResult_, 0xff, sizeof(unsigned long long), ST), "reset server result");
   hipCheck(hipMemsetAsync(dServerT0_ + 8, 0, sizeof(unsigned long long), ST), "reset server doorbell");
   hipCheck(hipMemsetAsync(dServerT0_ + 12, 0, sizeof(unsigned long long), ST), "reset server publication word");
+  hipCheck(hipMemsetAsync(dServerT0_ + 4, 0xff, sizeof(unsigned long long), ST), "reset server mask word");
   __atomic_store_n(&hResult_[7], lastCmdSeq_, __ATOMIC_RELEASE);  // the new launch's last command (parking, groups)
   serverTimed_ = timing;
   if (serverTimed_) (void)hipEventRecord((hipEvent_t)evS0_, ST);
@@ -668,6 +671,11 @@ int64_t Device::serverRun(const DevProgram& prog, const Staged& g, int op, const
       }
     c.goalParts = parts;
     c.nActive = (int32_t)std::min<uint64_t>(wgsFor(parts), (uint64_t)serverBlocks_);
+    // A pair command of at most one tile: its goals are shared by enough of the command's workgroups to leave about
+    // one goal per wave (scan.hip, c.wgParts: the conjunction is most of such a command's first tile)
+    c.wgParts = 1;
+    if (wgGoalSplit_ && op == SOP_PAIRS && parts == 4 && whole <= 64 && prog.nGoals > parts)
+      c.wgParts = std::min(c.nActive, std::min(8, (prog.nGoals + parts - 1) / parts));
     if (prof().on && op == SOP_PAIRS)  // CCMI_PROFILE: pair-scan sizes
       prof().count(whole <= 64 ? 58 : whole <= 256 ? 59 : whole <= 2048 ? 60 : 61,
                    whole <= 64 ? "pairs.n<=64" : whole <= 256 ? "pairs.n<=256" : whole <= 2048 ? "pairs.n<=2048" : "pairs.n>2048");
@@ -849,6 +857,11 @@ DevTables Device::tables() const {
   t.pollMode = pollMode;
   static const int seqRecheck = std::getenv("CCMI_SEQ_RECHECK") ? std::atoi(std::getenv("CCMI_SEQ_RECHECK")) : 0;
   t.seqRecheck = seqRecheck;
+  static const int conjRepeat = std::getenv("CCMI_CONJ_REPEAT") ? std::atoi(std::getenv("CCMI_CONJ_REPEAT")) : 0;
+  t.conjRepeat = conjRepeat;
+  static const int directPollers =
+      std::getenv("CCMI_DIRECT_POLLERS") ? std::max(1, std::min(8, std::atoi(std::getenv("CCMI_DIRECT_POLLERS")))) : 8;
+  t.directPollers = directPollers;
   t.stuckTicks = stuckTicks_;
   t.parkTicks = parkTicks_;
   t.chainDelayTicks = chainDelayTicks_;

@@ -335,6 +335,8 @@ class Device {
   int goalSplitWgs_ = 256;
   // a server scan's first sweep sized from its site's last winner depth (serverRun; CCMI_SCAN_WIDTH=full: off)
   bool adaptiveWidth_ = true;
+  // pair commands within one tile share their goals over several workgroups (serverRun; CCMI_WG_GOAL_SPLIT=0: off)
+  bool wgGoalSplit_ = true;
   unsigned long long stuckTicks_ = 1000000000ull;  // 10 s of s_memrealtime: a command unpublished that long is stuck
   unsigned long long chainDelayTicks_ = 0;
   unsigned long long parkTicks_ = 100000ull;  // 1 ms: a shard-group scan waiting longer parks the server

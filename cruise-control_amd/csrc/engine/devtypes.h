@@ -167,6 +167,12 @@ struct DevTables {
   int32_t pollMode;
   // 1: workgroup 0 re-reads the sequence word after copying a header (CCMI_SEQ_RECHECK=1); 0 (default): one read
   int32_t seqRecheck;
+  // diagnostics (CCMI_CONJ_REPEAT=1): pair scans evaluate each candidate's conjunction twice (same result), so the
+  // stamps show what the conjunction's arithmetic costs
+  int32_t conjRepeat;
+  // scan-server workgroups that poll the command word themselves (CCMI_DIRECT_POLLERS, default 8; 1: workgroup 0
+  // alone, the others wait for its doorbell)
+  int32_t directPollers;
   // the scan server's stuck-command bound in s_memrealtime ticks (CCMI_SERVER_STUCK_MS, default 10 s) and a test-only
   // delay added to every chain command (CCMI_CHAIN_DELAY_US, default 0: a chain that outlasts a short bound)
   unsigned long long stuckTicks;
@@ -293,7 +299,10 @@ struct alignas(16) ServerCmd {
   // combine), this combine's slot, the rank and the rank count; the last workgroup folds the scan's key into the slot
   // instead of publishing it, and the group's last rank to arrive publishes the minimum to every rank
   unsigned long long combineBlock;
-  int32_t combineSlot, combineRank, combineCount, combinePad;
+  int32_t combineSlot, combineRank, combineCount;
+  // SOP_PAIRS within one tile: this many workgroups (each goalParts waves) share the tile's goals — workgroup w takes
+  // parts w * goalParts + wave % goalParts of wgParts * goalParts — and AND their accept masks (1: one workgroup)
+  int32_t wgParts;
 };
 // The sequence word: the host stores (next | kSeqBusy) before it rewrites the other fields and `next` after them, each
 // behind a store fence; a workgroup copies the header once it reads a new sequence that is not busy (the fields landed

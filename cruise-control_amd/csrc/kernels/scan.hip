@@ -736,6 +736,18 @@ __device__ __forceinline__ int tileFirst(bool ok, int parts) {
   return first;
 }
 
+// The accept mask of a scan-server tile's first group (slots 0..63): the AND of its `parts` waves' ballots.
+__device__ __forceinline__ unsigned long long tileMask(bool ok, int parts) {
+  __shared__ unsigned long long sBalM[kBlock / 64];
+  const unsigned long long bal = __ballot(ok);
+  if ((threadIdx.x & 63) == 0) sBalM[threadIdx.x >> 6] = bal;
+  __syncthreads();
+  unsigned long long pass = ~0ull;
+  for (int p = 0; p < parts; ++p) pass &= sBalM[p];
+  __syncthreads();
+  return pass;
+}
+
 // Last-arriver publish: every workgroup arrives once (after its final atomicMin); the last one reads the
 // winning key and writes ONE 64-bit word {seq:32 | key+1:32} (0 in the low half = no winner) to the host
 // mailbox — a single aligned 8-byte store, so the host never sees a sequence number without its key and
@@ -1049,6 +1061,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, kServ
   // of their own (an agent acquire is ~1.7 us of its first tile otherwise, MI355X_MICROARCH.md). acqFresh: no device
   // write was published since that acquire.
   unsigned long long* const pub = bell + 4;
+  unsigned long long* const maskWord = t0 + 4;  // a shared-goal pair command's accept mask (all ones between commands)
   bool acqFresh = false;
   unsigned long long idleSince = __builtin_amdgcn_s_memrealtime();
   bool participated = false;  // this workgroup took part in its last command (thread 0's view)
@@ -1061,10 +1074,12 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, kServ
       // The idle clock starts once this workgroup sees its last command published: until then a workgroup that was
       // dispatched late (the GPU busy with other sessions' kernels) is still working on it and the host is waiting.
       bool published = last == startSeq;
-      // Workgroup 0 alone polls the host-written command word (fine-grained VRAM: every poll is a memory read) and
-      // rings a doorbell in device memory with the command's {valid, exit, nActive, seq}; the others poll the doorbell
-      // with agent-scope loads, which the XCD's L2 serves until it changes (MI355X_MICROARCH.md hand-off table: one
-      // lane's sc1 store, sc1 load polls). Only the command's participants then copy its header.
+      // Workgroups 0 .. T.directPollers - 1 (8) poll the host-written command word (fine-grained VRAM: every poll is a memory
+      // read) and copy the header themselves, so a small command's workgroups all start together; workgroup 0 then
+      // rings a doorbell in device memory with the command's {valid, exit, nActive, seq} for the others, which poll it
+      // with agent-scope loads the XCD's L2 serves until it changes (MI355X_MICROARCH.md hand-off table: one lane's sc1
+      // store, sc1 load polls) — 256 workgroups polling the command word would be most of the server's memory traffic.
+      // Only the command's participants copy its header.
       for (int spin = 0;; ++spin) {
         if (!acqFresh && last != startSeq &&
             __hip_atomic_load(pub, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == last) {
@@ -1072,7 +1087,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, kServ
           asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
           acqFresh = true;
         }
-        if (blockIdx.x == 0) {
+        if ((uint32_t)blockIdx.x < (uint32_t)T.directPollers) {
           const unsigned long long s = __hip_atomic_load(&cmd->seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
           if (s != last && !(s & kSeqBusy)) {
             // One read of the sequence word suffices: the host stores the header's other fields, a store fence, then
@@ -1080,9 +1095,11 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, kServ
             // this command's result, which waits for this copy. (T.seqRecheck: the seqlock's second read as well.)
             copySysOneThread(&c, cmd);
             if (!T.seqRecheck || __hip_atomic_load(&cmd->seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == s) {
-              const unsigned long long ring = kBellValid | (c.op == SOP_EXIT ? kBellExit : 0ull) |
-                                              ((unsigned long long)(uint32_t)c.nActive << 32) | (s & 0xffffffffull);
-              __hip_atomic_store(bell, ring, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+              if (blockIdx.x == 0) {  // the doorbell is for the workgroups past the direct pollers
+                const unsigned long long ring = kBellValid | (c.op == SOP_EXIT ? kBellExit : 0ull) |
+                                                ((unsigned long long)(uint32_t)c.nActive << 32) | (s & 0xffffffffull);
+                __hip_atomic_store(bell, ring, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+              }
               break;
             }
             continue;
@@ -1460,6 +1477,37 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, kServ
         }
         __syncthreads();  // the batch arrays are rewritten by the next batch
       }
+    } else if (c.wgParts > 1) {  // SOP_PAIRS within one tile, its goals shared by c.wgParts workgroups
+      // Every sharing workgroup evaluates the same candidates (slots 0..n-1, n <= 64: one group of `parts` waves) on
+      // its share of the goal conjunction and ANDs its accept mask into the command's mask word; the last workgroup to
+      // arrive takes the first set bit (moveCandidateAcceptedPart: the same conjunction whatever the split).
+      const int n = c.n;
+      const int parts = (c.goalParts == 2 || c.goalParts == 4) ? c.goalParts : 1;
+      const int wave = (int)(threadIdx.x >> 6);
+      const int q = (wave / parts) * 64 + (int)(threadIdx.x & 63);
+      if ((int)blockIdx.x < c.wgParts) {
+        RowRef rq{0, 0, 0, 0};
+        int dq = 0;
+        if (q < n) {
+          rq = ldSysRow(A + 4 * (size_t)q);
+          dq = ldSys(C + q);
+        }
+        if (!staged) stage();
+        bool ok = false;
+        if (q < n) {
+          PreView v;
+          v.loadDst(T, dq, ov);
+          v.loadRowRef(T, prog, rq, ov);
+          ok = !v.exclLeadBlocked(prog) &&
+               moveCandidateAcceptedPart(prog, v, v.r, v.dst, (int)blockIdx.x * parts + wave % parts, c.wgParts * parts);
+        }
+        const unsigned long long m = tileMask(ok, parts);
+        if (firstTile) {
+          SRV_STAMP(T, 3);
+          firstTile = false;
+        }
+        if (threadIdx.x == 0 && m != ~0ull) __hip_atomic_fetch_and(maskWord, m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
     } else {  // SOP_PAIRS
       const int n = c.n, keyBase = c.keyBase;
       const int parts = (c.goalParts == 2 || c.goalParts == 4) ? c.goalParts : 1;
@@ -1486,6 +1534,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, kServ
           v.loadRowRef(T, prog, rq, ov);
           if (firstTile) SRV_STAMP(T, 5);
           ok = !v.exclLeadBlocked(prog) && moveCandidateAcceptedPart(prog, v, v.r, v.dst, part, parts);
+          if (T.conjRepeat)  // diagnostics: the same conjunction again (the part index is opaque to the compiler)
+            ok = ok & moveCandidateAcceptedPart(prog, v, v.r, v.dst, part + T.conjRepeat - 1, parts);
         }
         const int f = tileFirst(ok, parts);
         if (firstTile) {
@@ -1552,9 +1602,15 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, kServ
         }
       }
       if (prev == nAct - 1) {
-        // the result and workgroup 0's start stamp in one batch of loads
-        const unsigned long long v = __hip_atomic_load(&result[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        // the result and workgroup 0's start stamp in one batch of loads (a pair command with shared goals: the first
+        // slot its mask word kept, the word reset to all ones)
+        unsigned long long v = __hip_atomic_load(&result[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         const unsigned long long tStart = __hip_atomic_load(t0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (c.op == SOP_PAIRS && c.wgParts > 1) {
+          const unsigned long long m = __hip_atomic_load(maskWord, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store(maskWord, ~0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          v = m ? (unsigned long long)c.keyBase + (unsigned long long)__builtin_ctzll(m) : kNone;
+        }
         __hip_atomic_store(&result[0], kNone, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         const unsigned long long lo = v == kNone ? 0ull : (v + 1) & 0xffffffffull;
