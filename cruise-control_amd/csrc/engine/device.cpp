@@ -185,7 +185,7 @@ Device::Device(int ordinal, int B, int R, int P, int T, int maxGoalSlots)
       chainDelayTicks_ = (unsigned long long)std::max(0.0, std::atof(cd)) * 100ull;
     if (serverBlocks_ < 8) serverUsable_ = false;
     if (serverUsable_) {
-      dalloc(&dServerT0_, 16);  // [0] busy-time stamp, [4] shared-goal pair mask, [8] the doorbell (a line of its own),
+      dalloc(&dServerT0_, 16);  // [0] busy-time stamp, [4, 8) shared-goal pair masks, [8] the doorbell (a line of its own),
                                 // [12] the last published seq
       try {
         ensureFg(1 << 20);
@@ -348,6 +348,12 @@ constexpr int kServerBudget = 256;
 std::mutex g_serverMu;
 int g_serverWgs[64] = {};
 int g_activeCalls[64] = {};
+// the scan server's direct pollers of the command word (DevTables.directPollers)
+int directPollers() {
+  static const int v =
+      std::getenv("CCMI_DIRECT_POLLERS") ? std::max(1, std::min(32, std::atoi(std::getenv("CCMI_DIRECT_POLLERS")))) : 8;
+  return v;
+}
 double nowSeconds() {
   return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
@@ -512,7 +518,7 @@ bool Device::ensureServer() {
   hipCheck(hipMemsetAsync(dResult_, 0xff, sizeof(unsigned long long), ST), "reset server result");
   hipCheck(hipMemsetAsync(dServerT0_ + 8, 0, sizeof(unsigned long long), ST), "reset server doorbell");
   hipCheck(hipMemsetAsync(dServerT0_ + 12, 0, sizeof(unsigned long long), ST), "reset server publication word");
-  hipCheck(hipMemsetAsync(dServerT0_ + 4, 0xff, sizeof(unsigned long long), ST), "reset server mask word");
+  hipCheck(hipMemsetAsync(dServerT0_ + 4, 0xff, 4 * sizeof(unsigned long long), ST), "reset server mask words");
   __atomic_store_n(&hResult_[7], lastCmdSeq_, __ATOMIC_RELEASE);  // the new launch's last command (parking, groups)
   serverTimed_ = timing;
   if (serverTimed_) (void)hipEventRecord((hipEvent_t)evS0_, ST);
@@ -554,7 +560,7 @@ bool Device::postCommand(ServerCmd& c, bool rowsSent) {
               sizeof(ServerCmd) - sizeof(unsigned long long));
   hostStoreFence();
   lastCmdSeq_ = ++seq_;
-  *(volatile unsigned long long*)fg_ = lastCmdSeq_;
+  *(volatile unsigned long long*)fg_ = lastCmdSeq_ | (c.nActive >= directPollers() ? kSeqAll : 0ull);
   hostStoreFence();
   const auto tW = tp ? std::chrono::steady_clock::now() : std::chrono::steady_clock::time_point();
   const bool seen = waitMail(seq_, true);
@@ -671,11 +677,19 @@ int64_t Device::serverRun(const DevProgram& prog, const Staged& g, int op, const
       }
     c.goalParts = parts;
     c.nActive = (int32_t)std::min<uint64_t>(wgsFor(parts), (uint64_t)serverBlocks_);
-    // A pair command of at most one tile: its goals are shared by enough of the command's workgroups to leave about
-    // one goal per wave (scan.hip, c.wgParts: the conjunction is most of such a command's first tile)
+    // A pair command of at most four tiles of 64: each tile's goals are shared by enough workgroups to leave about one
+    // goal per wave (scan.hip, c.wgParts: the conjunction is most of such a command's first tile), and one more
+    // workgroup without a tile writes the command's rows
     c.wgParts = 1;
-    if (wgGoalSplit_ && op == SOP_PAIRS && parts == 4 && whole <= 64 && prog.nGoals > parts)
-      c.wgParts = std::min(c.nActive, std::min(8, (prog.nGoals + parts - 1) / parts));
+    if (wgGoalSplit_ && op == SOP_PAIRS && parts == 4 && whole <= 4 * 64 && prog.nGoals > parts) {
+      const int tiles = (int)((whole + 63) / 64);
+      // the sharing workgroups and the writer within the direct pollers, which all see the command at once
+      const int share = std::min((prog.nGoals + parts - 1) / parts, (directPollers() - 1) / tiles);
+      if (share >= 2 && tiles * share + 1 <= serverBlocks_) {
+        c.wgParts = share;
+        c.nActive = std::max(c.nActive, tiles * share + 1);
+      }
+    }
     if (prof().on && op == SOP_PAIRS)  // CCMI_PROFILE: pair-scan sizes
       prof().count(whole <= 64 ? 58 : whole <= 256 ? 59 : whole <= 2048 ? 60 : 61,
                    whole <= 64 ? "pairs.n<=64" : whole <= 256 ? "pairs.n<=256" : whole <= 2048 ? "pairs.n<=2048" : "pairs.n>2048");
@@ -859,9 +873,7 @@ DevTables Device::tables() const {
   t.seqRecheck = seqRecheck;
   static const int conjRepeat = std::getenv("CCMI_CONJ_REPEAT") ? std::atoi(std::getenv("CCMI_CONJ_REPEAT")) : 0;
   t.conjRepeat = conjRepeat;
-  static const int directPollers =
-      std::getenv("CCMI_DIRECT_POLLERS") ? std::max(1, std::min(8, std::atoi(std::getenv("CCMI_DIRECT_POLLERS")))) : 8;
-  t.directPollers = directPollers;
+  t.directPollers = directPollers();
   t.stuckTicks = stuckTicks_;
   t.parkTicks = parkTicks_;
   t.chainDelayTicks = chainDelayTicks_;

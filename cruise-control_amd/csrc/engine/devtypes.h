@@ -170,8 +170,8 @@ struct DevTables {
   // diagnostics (CCMI_CONJ_REPEAT=1): pair scans evaluate each candidate's conjunction twice (same result), so the
   // stamps show what the conjunction's arithmetic costs
   int32_t conjRepeat;
-  // scan-server workgroups that poll the command word themselves (CCMI_DIRECT_POLLERS, default 8; 1: workgroup 0
-  // alone, the others wait for its doorbell)
+  // scan-server workgroups that poll the command word themselves (CCMI_DIRECT_POLLERS, default 8, the fewest workgroups
+  // a scan command has; 1: workgroup 0 alone, the others wait for its doorbell)
   int32_t directPollers;
   // the scan server's stuck-command bound in s_memrealtime ticks (CCMI_SERVER_STUCK_MS, default 10 s) and a test-only
   // delay added to every chain command (CCMI_CHAIN_DELAY_US, default 0: a chain that outlasts a short bound)
@@ -309,6 +309,9 @@ struct alignas(16) ServerCmd {
 // first, and the host rewrites them only after that command's result). DevTables.seqRecheck adds the seqlock's second
 // read of the word after the copy.
 constexpr unsigned long long kSeqBusy = 1ull << 63;
+// Set in the sequence word of a command every direct poller takes part in (ServerCmd.nActive >= DevTables.directPollers):
+// those workgroups then know from the word alone that their header copy cannot tear (scan.hip scan_server).
+constexpr unsigned long long kSeqAll = 1ull << 62;
 static_assert(sizeof(ServerCmd) % 16 == 0, "ServerCmd words");
 
 // Device-resident Java loads and partition slot order, so chain kernels can apply moves themselves (apply.h).

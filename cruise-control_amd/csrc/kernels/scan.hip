@@ -893,6 +893,7 @@ __device__ __forceinline__ void copySysOneThread(X* dst, const X* src) {  // all
   for (int w = 0; w < n; ++w) reinterpret_cast<int32_t*>(dst)[w] = v[w];
 }
 constexpr unsigned long long kServerIdleTicks = 200000000ull;  // 2 s of s_memrealtime (100 MHz)
+constexpr int kMaskTiles = 4;  // tiles of a shared-goal pair command (ServerCmd.wgParts; the server's mask words)
 // scan-server doorbell word: valid and exit flags, nActive (bits 32-61), the command sequence's low 32 bits
 constexpr unsigned long long kBellValid = 1ull << 63, kBellExit = 1ull << 62;
 constexpr unsigned long long kParkBit = 1ull << 62;  // mail[7]: the server parked after this command (shard groups)
@@ -1061,7 +1062,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, kServ
   // of their own (an agent acquire is ~1.7 us of its first tile otherwise, MI355X_MICROARCH.md). acqFresh: no device
   // write was published since that acquire.
   unsigned long long* const pub = bell + 4;
-  unsigned long long* const maskWord = t0 + 4;  // a shared-goal pair command's accept mask (all ones between commands)
+  unsigned long long* const maskWord = t0 + 4;  // a shared-goal pair command's tile accept masks [kMaskTiles] (all ones
+                                                // between commands)
   bool acqFresh = false;
   unsigned long long idleSince = __builtin_amdgcn_s_memrealtime();
   bool participated = false;  // this workgroup took part in its last command (thread 0's view)
@@ -1089,15 +1091,24 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, kServ
         }
         if ((uint32_t)blockIdx.x < (uint32_t)T.directPollers) {
           const unsigned long long s = __hip_atomic_load(&cmd->seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-          if (s != last && !(s & kSeqBusy)) {
-            // One read of the sequence word suffices: the host stores the header's other fields, a store fence, then
-            // the new sequence (Device::postCommand), so they landed before it did, and it rewrites them only after
-            // this command's result, which waits for this copy. (T.seqRecheck: the seqlock's second read as well.)
+          const unsigned long long sp = s & ~kSeqAll;
+          if (sp != last && !(s & kSeqBusy)) {
+            // The host stores the header's other fields, a store fence, then the new sequence (Device::postCommand),
+            // so they landed before it did, and it rewrites them only after this command's result — which waits for
+            // every participant, so a participant's copy cannot tear. Workgroup 0 always takes part, and so does every
+            // direct poller when the word carries kSeqAll: one read suffices. Otherwise (a chain, one participant)
+            // another poller may be no participant while the host already rewrites the header for the next command:
+            // its copy counts only when the word still reads `s` after it (the seqlock's second read), unless the copy
+            // says it does not take part (then it does not, whatever the rest of a torn copy says: a participant's copy
+            // cannot tear). T.seqRecheck: the second read always.
             copySysOneThread(&c, cmd);
-            if (!T.seqRecheck || __hip_atomic_load(&cmd->seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == s) {
+            c.seq = sp;
+            const bool recheck = T.seqRecheck || (blockIdx.x != 0 && !(s & kSeqAll) &&
+                                                  (uint32_t)blockIdx.x < (uint32_t)c.nActive);
+            if (!recheck || __hip_atomic_load(&cmd->seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == s) {
               if (blockIdx.x == 0) {  // the doorbell is for the workgroups past the direct pollers
                 const unsigned long long ring = kBellValid | (c.op == SOP_EXIT ? kBellExit : 0ull) |
-                                                ((unsigned long long)(uint32_t)c.nActive << 32) | (s & 0xffffffffull);
+                                                ((unsigned long long)(uint32_t)c.nActive << 32) | (sp & 0xffffffffull);
                 __hip_atomic_store(bell, ring, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
               }
               break;
@@ -1477,15 +1488,17 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, kServ
         }
         __syncthreads();  // the batch arrays are rewritten by the next batch
       }
-    } else if (c.wgParts > 1) {  // SOP_PAIRS within one tile, its goals shared by c.wgParts workgroups
-      // Every sharing workgroup evaluates the same candidates (slots 0..n-1, n <= 64: one group of `parts` waves) on
-      // its share of the goal conjunction and ANDs its accept mask into the command's mask word; the last workgroup to
-      // arrive takes the first set bit (moveCandidateAcceptedPart: the same conjunction whatever the split).
+    } else if (c.wgParts > 1) {  // SOP_PAIRS of at most kMaskTiles tiles of 64, each tile's goals shared by wgParts WGs
+      // Workgroup w takes tile w / wgParts (slots 64 t .. 64 t + 63 of the pairs, one group of `parts` waves) and share
+      // w % wgParts of its goal conjunction, and ANDs its accept mask into the tile's mask word; the last workgroup to
+      // arrive takes the first set bit of the first tile (moveCandidateAcceptedPart: the same conjunction whatever the
+      // split, and every tile is evaluated, so the first fit is exact).
       const int n = c.n;
       const int parts = (c.goalParts == 2 || c.goalParts == 4) ? c.goalParts : 1;
       const int wave = (int)(threadIdx.x >> 6);
-      const int q = (wave / parts) * 64 + (int)(threadIdx.x & 63);
-      if ((int)blockIdx.x < c.wgParts) {
+      const int tileI = (int)blockIdx.x / c.wgParts, share = (int)blockIdx.x % c.wgParts;
+      const int q = tileI * 64 + (wave / parts) * 64 + (int)(threadIdx.x & 63);
+      if (tileI * 64 < n && tileI < kMaskTiles) {
         RowRef rq{0, 0, 0, 0};
         int dq = 0;
         if (q < n) {
@@ -1499,14 +1512,15 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, kServ
           v.loadDst(T, dq, ov);
           v.loadRowRef(T, prog, rq, ov);
           ok = !v.exclLeadBlocked(prog) &&
-               moveCandidateAcceptedPart(prog, v, v.r, v.dst, (int)blockIdx.x * parts + wave % parts, c.wgParts * parts);
+               moveCandidateAcceptedPart(prog, v, v.r, v.dst, share * parts + wave % parts, c.wgParts * parts);
         }
         const unsigned long long m = tileMask(ok, parts);
         if (firstTile) {
           SRV_STAMP(T, 3);
           firstTile = false;
         }
-        if (threadIdx.x == 0 && m != ~0ull) __hip_atomic_fetch_and(maskWord, m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (threadIdx.x == 0 && m != ~0ull)
+          __hip_atomic_fetch_and(maskWord + tileI, m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
     } else {  // SOP_PAIRS
       const int n = c.n, keyBase = c.keyBase;
@@ -1607,9 +1621,18 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, kServ
         unsigned long long v = __hip_atomic_load(&result[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         const unsigned long long tStart = __hip_atomic_load(t0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (c.op == SOP_PAIRS && c.wgParts > 1) {
-          const unsigned long long m = __hip_atomic_load(maskWord, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          __hip_atomic_store(maskWord, ~0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          v = m ? (unsigned long long)c.keyBase + (unsigned long long)__builtin_ctzll(m) : kNone;
+          unsigned long long m[kMaskTiles];
+          const int tiles = min((c.n + 63) / 64, kMaskTiles);
+#pragma unroll
+          for (int t = 0; t < kMaskTiles; ++t)
+            m[t] = t < tiles ? __hip_atomic_load(maskWord + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0ull;
+          v = kNone;
+#pragma unroll
+          for (int t = kMaskTiles - 1; t >= 0; --t)
+            if (t < tiles) {
+              if (m[t]) v = (unsigned long long)c.keyBase + (unsigned long long)(t * 64 + __builtin_ctzll(m[t]));
+              __hip_atomic_store(maskWord + t, ~0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
         }
         __hip_atomic_store(&result[0], kNone, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
