@@ -177,6 +177,7 @@ Device::Device(int ordinal, int B, int R, int P, int T, int maxGoalSlots)
     if (const char* gw = std::getenv("CCMI_GOAL_SPLIT_WGS")) goalSplitWgs_ = (int)std::strtol(gw, nullptr, 10);
     if (const char* sw = std::getenv("CCMI_SCAN_WIDTH")) adaptiveWidth_ = std::strcmp(sw, "full") != 0;
     if (const char* ws = std::getenv("CCMI_WG_GOAL_SPLIT")) wgGoalSplit_ = ws[0] != '0';
+    if (const char* qs = std::getenv("CCMI_QUERY_SPINS")) spinsBeforeQuery_ = std::strtoull(qs, nullptr, 10);
     if (const char* sm = std::getenv("CCMI_SERVER_STUCK_MS"))
       stuckTicks_ = (unsigned long long)std::max(1.0, std::atof(sm)) * 100000ull;  // 100 MHz s_memrealtime
     if (const char* pk = std::getenv("CCMI_GROUP_PARK_US"))
@@ -1098,7 +1099,10 @@ bool Device::waitMail(unsigned long long seq, bool serverCmd) {
       idle = idleWork();
       continue;
     }
-    if ((++spins & 1023) == 0) {
+    // the stream is asked whether the kernel ended without publishing (a server's watchdog exit, a park, a fault) only
+    // after ~16 K polls (~0.2 ms, ten round trips) and then every 1 K: a runtime call in the middle of an ordinary wait
+    // would hold up noticing the result that lands meanwhile
+    if ((++spins & 1023) == 0 && spins >= spinsBeforeQuery_) {
       const hipError_t q = hipStreamQuery(ST);
       if (q == hipSuccess) {
         if ((__atomic_load_n(&mail[0], __ATOMIC_ACQUIRE) >> 32) == want) break;

@@ -337,6 +337,8 @@ class Device {
   bool adaptiveWidth_ = true;
   // pair commands within one tile share their goals over several workgroups (serverRun; CCMI_WG_GOAL_SPLIT=0: off)
   bool wgGoalSplit_ = true;
+  // Device::waitMail: polls of the result word before the first stream query (CCMI_QUERY_SPINS, default 16384)
+  uint64_t spinsBeforeQuery_ = 16384;
   unsigned long long stuckTicks_ = 1000000000ull;  // 10 s of s_memrealtime: a command unpublished that long is stuck
   unsigned long long chainDelayTicks_ = 0;
   unsigned long long parkTicks_ = 100000ull;  // 1 ms: a shard-group scan waiting longer parks the server
