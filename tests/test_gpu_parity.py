@@ -99,6 +99,20 @@ def test_gpu_scan_width_matches_oracle(gpu_lib, oracle_lib, monkeypatch, width):
                                  DEFAULT_GOALS, 1.05)
 
 
+@pytest.mark.parametrize("split", ["0", "1"])
+def test_gpu_shared_goal_pair_scans_match_oracle(gpu_lib, oracle_lib, monkeypatch, split):
+    """Pair scans of at most four tiles with each tile's goals shared by several scan-server workgroups that AND their
+    accept masks (CCMI_WG_GOAL_SPLIT=1, the default) and with every goal on one workgroup (0): the same conjunction, so
+    both decide exactly as the oracle — the leadership loops of LeaderReplicaDistribution / LeaderBytesIn and the
+    resource goals' leadership move-in are pair scans."""
+    monkeypatch.setenv("CCMI_WG_GOAL_SPLIT", split)
+    check_product_against_oracle(gpu_lib, dict(num_racks=8, num_brokers=300, num_replicas=30000, num_topics=1000),
+                                 ["LeaderReplicaDistributionGoal", "CpuUsageDistributionGoal",
+                                  "NetworkOutboundUsageDistributionGoal", "LeaderBytesInDistributionGoal"], 1.05)
+    check_product_against_oracle(gpu_lib, dict(num_racks=5, num_brokers=20, num_replicas=6000, num_topics=300),
+                                 DEFAULT_GOALS, 1.05)
+
+
 def test_gpu_snapshot_pool_wraps_match_oracle(gpu_lib, oracle_lib, monkeypatch):
     """A snapshot pool of 64K rows wraps many times per proposal (each wrap restarts the scan server and re-sets the
     whole queue directory): the queue scans still read only current snapshots and decide exactly as the oracle."""
