@@ -16,6 +16,7 @@
 #include <atomic>
 #include <chrono>
 #include <mutex>
+#include <optional>
 
 #include <pthread.h>
 #include <sched.h>
@@ -555,6 +556,8 @@ bool Device::postCommand(ServerCmd& c, bool rowsSent) {
                  (int64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - tA).count());
   if (!claimServer()) return false;  // parked after its last command: the caller takes its launch path
   c.rowsEpoch = rowsEpoch_;
+  std::optional<NsScope> nsHdr;
+  if (prof().on) nsHdr.emplace(7, "srv.ns.header");  // CCMI_PROFILE: the header's seqlock writes and fences
   *(volatile unsigned long long*)fg_ = (seq_ + 1) | kSeqBusy;
   hostStoreFence();
   std::memcpy(fg_ + sizeof(unsigned long long), (const char*)&c + sizeof(unsigned long long),
@@ -563,6 +566,7 @@ bool Device::postCommand(ServerCmd& c, bool rowsSent) {
   lastCmdSeq_ = ++seq_;
   *(volatile unsigned long long*)fg_ = lastCmdSeq_ | (c.nActive >= directPollers() ? kSeqAll : 0ull);
   hostStoreFence();
+  nsHdr.reset();
   const auto tW = tp ? std::chrono::steady_clock::now() : std::chrono::steady_clock::time_point();
   const bool seen = waitMail(seq_, true);
   if (tp)
@@ -617,6 +621,8 @@ int64_t Device::serverRun(const DevProgram& prog, const Staged& g, int op, const
   const size_t oA = oRows + rows, oC = oA + align16(aBytes), end = oC + align16(nC * 4);
   ensureFg(kCmdBytes + end);
   if (!ensureServer()) return INT64_MIN;
+  std::optional<NsScope> nsPay;
+  if (prof().on) nsPay.emplace(6, "srv.ns.payload");  // CCMI_PROFILE: the payload's writes through the BAR
   char* pay = fg_ + kCmdBytes;
   const int ver = serverProgram(prog, pay + oProg);
   perf.serverPayloadBytes += (int64_t)(rows + aBytes + nC * 4);
@@ -713,6 +719,7 @@ int64_t Device::serverRun(const DevProgram& prog, const Staged& g, int op, const
   c.oT = (uint32_t)(oRows + g.otd);
   c.oA = (uint32_t)oA;
   c.oC = (uint32_t)oC;
+  nsPay.reset();
   if (!postCommand(c, (g.nb | g.nr | g.np | g.nt) != 0)) return INT64_MIN;
   perf.serverScans++;
   const unsigned long long lo = hResult_[0] & 0xffffffffull;
