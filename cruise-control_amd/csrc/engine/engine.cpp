@@ -1219,15 +1219,11 @@ class TreeWorker {
       }
       mine.follow(want);
       tree_.clear();
-      rank_.assign(B_, 0);
-      mark_.assign(B_, 0);
-      for (size_t i = 0; i < order_.size(); ++i) {
-        rank_[order_[i]] = (int32_t)i;
-        mark_[order_[i]] = 1;
-      }
+      rank_.assign(B_, -1);  // -1: not a member
+      for (size_t i = 0; i < order_.size(); ++i) rank_[order_[i]] = (int32_t)i;
       ids_.clear();
       for (int x = 0; x < B_; ++x)
-        if (mark_[x]) ids_.push_back(x);
+        if (rank_[x] >= 0) ids_.push_back(x);
       tree_.buildByRank(std::move(ids_), std::move(rank_), &cancel_, seq_);
       if (!cancel_.load(std::memory_order_relaxed)) {
         {
@@ -1242,7 +1238,6 @@ class TreeWorker {
   Tree tree_;
   std::vector<int32_t> next_, order_, rank_;
   std::vector<int> ids_;
-  std::vector<uint8_t> mark_;
   int nextB_ = 0, B_ = 0;
   bool nextSeq_ = true, seq_ = true;  // the tree's in-order sequence is wanted (RbTreeSet::buildByRank)
   CpuMask nextMask_;                  // the submitter's CPU mask (guarded by mu_)
