@@ -1565,6 +1565,7 @@ class ResourceDistribution : public GoalImpl {
     const bool useWorker = lease.w != nullptr;
     // `inorder` is the members' entry (key, id) order; the leadership form only searches the tree
     if (useWorker) lease.w->submit(inorder, m.B, action != DA_LEADERSHIP);
+    const int64_t relocBeforeEntry = m.lastRelocNs;  // CCMI_PROFILE: how long the entry state had been final
     struct Step {
       int dst;
       double keyAfter;
@@ -1594,6 +1595,13 @@ class ResourceDistribution : public GoalImpl {
       auto t1 = t0;
       ovr = entryKey;
       if (useWorker) {
+        if (tp && relocBeforeEntry > 0) {  // the entry state was final this long before the tree was wanted
+          const int64_t lead =
+              (int64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(t0.time_since_epoch()).count() -
+              relocBeforeEntry;
+          prof().count(51, "out.tree.lead.ns", std::min<int64_t>(lead, 1000000));
+          if (lead >= 150000) prof().count(63, "out.tree.lead.ge150us", 1);
+        }
         cand.adopt(lease.w->take());
       } else if (specState > 0) {  // the entry tree was started while scans were in flight: finish its puts
         if (tp) t1 = tnow();

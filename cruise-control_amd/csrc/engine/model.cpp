@@ -564,7 +564,14 @@ int Model::brokerRemove(int b, int p) {
   return r;
 }
 
+static inline int64_t relocStampNs() {
+  return prof().on ? (int64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
+                         std::chrono::steady_clock::now().time_since_epoch()).count()
+                   : 0;
+}
+
 void Model::relocateReplica(int p, int src, int dst) {
+  lastRelocNs = relocStampNs();
   PhaseScope ps(PH_RELOCATE);
   bVer[src]++;
   bVer[dst]++;
@@ -655,6 +662,7 @@ void Model::moveReplicaToEnd(int r) {
 }
 
 bool Model::relocateLeadership(int p, int src, int dst) {
+  lastRelocNs = relocStampNs();
   PhaseScope ps(PH_RELOCATE);
   const int sr = replicaOn(p, src);
   if (sr < 0 || !rLeader[sr]) return false;

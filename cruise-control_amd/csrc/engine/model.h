@@ -322,6 +322,8 @@ class Model {
   // Every version bump in order (src and dst of each relocation): readers that keep per-broker state derived from
   // snapshots (the queue scans' snapshot directory) catch up from their position instead of re-checking every broker.
   std::vector<int32_t> verLog;
+  // CCMI_PROFILE: when the last relocation happened (steady_clock nanoseconds; 0 before the first)
+  int64_t lastRelocNs = 0;
   // bumped whenever the selection sets the Specs do not carry change (excluded / must topics)
   uint32_t selEpoch = 0;
   // The replica whose membership or sort key changed at each of a broker's last kDeltaLog version bumps (-1: none),
